@@ -1,0 +1,329 @@
+/* mocohip.h — C ABI of the MI355X-native Moco direct-collocation hot path.
+ *
+ * This is the drop-in boundary.  A host NLP solver
+ * (IPOPT's TNLP, or the Python MocoHipSolver mirror) drives it exactly the
+ * way tropter's IPOPTSolver::TNLP drives its problem:
+ *
+ *   reference callback                      replaced by
+ *   ------------------------------------    ---------------------------------
+ *   TNLP::get_nlp_info                      mh_get_nlp_info
+ *     (tropter/tropter/optimization/IPOPTSolver.cpp:302-335)
+ *   TNLP::get_bounds_info                   mh_get_bounds
+ *     (IPOPTSolver.cpp:337-383; bounds rules CasOCTranscription.cpp:173-250)
+ *   TNLP::get_starting_point                mh_get_initial_guess_from_bounds,
+ *                                           mh_get_random_iterate
+ *     (IPOPTSolver.cpp:385-399; CasOCTranscription.cpp:1123-1177)
+ *   TNLP::eval_f / eval_grad_f              mh_eval_f / mh_eval_grad_f
+ *     (IPOPTSolver.cpp:401-416)
+ *   TNLP::eval_g                            mh_eval_g
+ *     (IPOPTSolver.cpp:417-427; CasOCTranscription.cpp:253-446)
+ *   TNLP::eval_jac_g (values==nullptr)      mh_get_jac_structure
+ *   TNLP::eval_jac_g (values!=nullptr)      mh_eval_jac_g
+ *     (IPOPTSolver.cpp:428-447; ProblemDecorator_double.cpp:261-291)
+ *
+ * The per-grid-point callbacks of CasOC::Problem
+ * (Moco/Moco/MocoCasADiSolver/CasOCProblem.h:313-332) are not exported
+ * individually: they are the device kernels behind these entry points.
+ *
+ * Conventions
+ *  - All arithmetic is IEEE binary64.
+ *  - Indices are 0-based (IPOPT C_STYLE).
+ *  - Host-pointer entry points copy x to the device and results back; the
+ *    *_device variants take device pointers (e.g. torch tensor data_ptr())
+ *    and never touch host memory.  Both are asynchronous w.r.t. nothing:
+ *    they return after the results are complete.
+ *  - Every function returns MH_OK (0) or an error code; mh_last_error()
+ *    gives a thread-local message.  A context is used by one host thread at
+ *    a time; distinct contexts may run concurrently (one HIP stream each).
+ *  - There is NO CPU fallback: mh_create fails with MH_ERR_HIP when no
+ *    gfx950 device is usable.
+ */
+#ifndef MOCOHIP_H
+#define MOCOHIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MH_ABI_VERSION 1
+
+enum mh_status {
+    MH_OK = 0,
+    MH_ERR_INVALID = 1,     /* bad argument / malformed problem            */
+    MH_ERR_HIP = 2,         /* HIP runtime failure or no usable device      */
+    MH_ERR_UNSUPPORTED = 3, /* feature outside the implemented hot path     */
+    MH_ERR_ALLOC = 4
+};
+
+/* ------------------------------------------------------------------------ */
+/* Model description ("model tape").  Plain structs of int32/double so that  */
+/* ctypes, cgo or JNI can fill them.  Produced by the host-side model        */
+/* compiler (opensim-moco_amd/mocohip/model.py) from an OpenSim model.       */
+/* ------------------------------------------------------------------------ */
+
+/* Scalar function of (at most) one generalized coordinate: the subset of
+ * OpenSim::Function used by CustomJoint TransformAxis and MovingPathPoint
+ * (Constant, LinearFunction, SimmSpline, MultiplierFunction(SimmSpline)). */
+enum mh_function_kind {
+    MH_FN_CONSTANT = 0,   /* value = a                                   */
+    MH_FN_LINEAR = 1,     /* value = scale * (a * q + b)                  */
+    MH_FN_SIMMSPLINE = 2  /* value = scale * SimmSpline(knots)(q)         */
+};
+typedef struct mh_function {
+    int32_t kind;
+    int32_t coord;       /* generalized coordinate index; -1 if constant  */
+    int32_t knot_begin;  /* first knot in mh_model.knot_x / knot_y        */
+    int32_t knot_count;
+    double a;
+    double b;
+    double scale;
+    double reserved;
+} mh_function;
+
+/* One elementary joint axis (a SimTK FunctionBased mobility).  A joint is a
+ * list of axes: translations are along axes fixed in the joint's parent
+ * frame F; rotations are a body-fixed sequence about the joint's child
+ * frame origin (Simbody MobilizedBody::FunctionBased semantics). PinJoint,
+ * SliderJoint, PlanarJoint and CustomJoint all lower to this form. */
+enum mh_axis_type { MH_AXIS_ROTATION = 0, MH_AXIS_TRANSLATION = 1 };
+typedef struct mh_axis {
+    int32_t type;
+    int32_t func;        /* index into mh_model.functions                 */
+    double dir[3];       /* unit axis                                      */
+} mh_axis;
+
+/* A rigid body and the joint connecting it to its parent.  Bodies must be
+ * listed in topological order (parent index < own index). */
+typedef struct mh_body {
+    int32_t parent;      /* -1 = ground                                   */
+    int32_t axis_begin;
+    int32_t axis_count;  /* 0 = weld                                      */
+    int32_t reserved;
+    double mass;
+    double com[3];       /* in body frame                                  */
+    double inertia[6];   /* about COM, body frame: xx yy zz xy xz yz       */
+    double R_PF[9];      /* joint parent frame F in parent body (row-major)*/
+    double p_PF[3];
+    double R_BM[9];      /* joint child frame M in this body               */
+    double p_BM[3];
+} mh_body;
+
+/* Muscle path points (OpenSim PathPoint / ConditionalPathPoint /
+ * MovingPathPoint). */
+enum mh_path_point_kind { MH_PP_FIXED = 0, MH_PP_CONDITIONAL = 1, MH_PP_MOVING = 2 };
+typedef struct mh_path_point {
+    int32_t kind;
+    int32_t body;        /* -1 = ground                                   */
+    int32_t coord;       /* conditional: coordinate tested                 */
+    int32_t fx, fy, fz;  /* moving: location functions (-1 = use loc[i])   */
+    double loc[3];
+    double range[2];     /* conditional: active when range[0]<=q<=range[1]*/
+} mh_path_point;
+
+/* DeGrooteFregly2016Muscle properties
+ * (Moco/Moco/Components/DeGrooteFregly2016Muscle.{h,cpp}). */
+typedef struct mh_muscle {
+    int32_t point_begin;
+    int32_t point_count;
+    int32_t ignore_activation_dynamics;
+    int32_t ignore_tendon_compliance;
+    int32_t ignore_passive_fiber_force;
+    int32_t tendon_dynamics_implicit;   /* must be 0 (explicit) for now   */
+    double max_isometric_force;
+    double optimal_fiber_length;
+    double tendon_slack_length;
+    double pennation_angle_at_optimal;
+    double max_contraction_velocity;
+    double activation_time_constant;
+    double deactivation_time_constant;
+    double fiber_damping;
+    double passive_fiber_strain_at_one_norm_force;
+    double tendon_strain_at_one_norm_force;
+    double active_force_width_scale;
+} mh_muscle;
+
+/* Actuators, in model order; each contributes one control. */
+enum mh_actuator_kind { MH_ACT_MUSCLE = 0, MH_ACT_COORDINATE = 1 };
+typedef struct mh_actuator {
+    int32_t kind;
+    int32_t target;      /* muscle index or coordinate index               */
+    double optimal_force;/* CoordinateActuator: tau = control*optimal_force*/
+} mh_actuator;
+
+/* Piecewise-polynomial table of time (data splines: ExternalForce GRF,
+ * state-tracking references).  Segment s covers [breaks[s], breaks[s+1]);
+ * column c value = sum_k coefs[(s*ncol + c)*(degree+1) + k] * (t-breaks[s])^k.
+ * Times outside the breaks use the first/last segment polynomial. */
+typedef struct mh_table {
+    int32_t nseg;
+    int32_t degree;
+    int32_t ncol;
+    int32_t break_begin; /* into mh_model.table_breaks                     */
+    int32_t coef_begin;  /* into mh_model.table_coefs                      */
+    int32_t reserved;
+} mh_table;
+
+/* OpenSim ExternalForce with force and point expressed in ground. */
+typedef struct mh_external_force {
+    int32_t body;
+    int32_t table;
+    int32_t force_col;   /* first of 3 columns, -1 = none                  */
+    int32_t point_col;   /* first of 3 columns, -1 = body origin           */
+    int32_t torque_col;  /* first of 3 columns, -1 = none                  */
+    int32_t reserved;
+} mh_external_force;
+
+typedef struct mh_model {
+    int32_t nq;          /* coordinates (= speeds)                          */
+    int32_t nbodies;
+    int32_t naxes;
+    int32_t nfunctions;
+    int32_t nknots;
+    int32_t nmuscles;
+    int32_t npoints;
+    int32_t nactuators;
+    int32_t ntables;
+    int32_t nbreaks;
+    int32_t ncoefs;
+    int32_t nexternal;
+    double gravity[3];
+    const mh_body* bodies;
+    const mh_axis* axes;
+    const mh_function* functions;
+    const double* knot_x;
+    const double* knot_y;
+    const mh_muscle* muscles;
+    const mh_path_point* points;
+    const mh_actuator* actuators;
+    const mh_table* tables;
+    const double* table_breaks;
+    const double* table_coefs;
+    const mh_external_force* external;
+} mh_model;
+
+/* ------------------------------------------------------------------------ */
+/* Problem (what MocoProblemRep compiles to; MocoCasOCProblem.cpp:30-251).   */
+/* State order = Simbody Y order: q[0..nq), u[0..nq), then per muscle in     */
+/* model order: activation (if dynamic), normalized tendon force (if         */
+/* compliant).  Control order = actuator order.                              */
+/* ------------------------------------------------------------------------ */
+
+/* A NaN lower or upper means "not set" (CasOC::Bounds::isSet). */
+typedef struct mh_bounds { double lower, upper; } mh_bounds;
+typedef struct mh_variable_info {
+    mh_bounds bounds, initial, final;
+} mh_variable_info;
+
+enum mh_goal_kind {
+    MH_GOAL_CONTROL = 0,        /* MocoControlGoal                         */
+    MH_GOAL_STATE_TRACKING = 1, /* MocoStateTrackingGoal                   */
+    MH_GOAL_FINAL_TIME = 2,     /* MocoFinalTimeGoal                       */
+    MH_GOAL_SUM_SQUARED_STATE = 3 /* MocoSumSquaredStateGoal (no reference) */
+};
+typedef struct mh_goal {
+    int32_t kind;
+    int32_t table;       /* state tracking: reference table                */
+    int32_t term_begin;  /* into mh_problem.goal_index / goal_weight       */
+    int32_t term_count;  /* control: #controls weighted; tracking: #states */
+    int32_t exponent;    /* control goal exponent (>=2)                    */
+    int32_t reserved;
+    double weight;       /* MocoGoal weight                                */
+} mh_goal;
+
+typedef struct mh_problem {
+    mh_model model;
+    mh_bounds time_initial;      /* bounds on initial_time                  */
+    mh_bounds time_final;        /* bounds on final_time                    */
+    const mh_variable_info* state_infos;   /* NS entries                    */
+    const mh_variable_info* control_infos; /* NC entries                    */
+    int32_t ngoals;
+    int32_t nterms;
+    const mh_goal* goals;
+    const int32_t* goal_index;   /* control index / state index per term    */
+    const int32_t* goal_column;  /* tracking: table column per term         */
+    const double* goal_weight;   /* per-term weight                         */
+} mh_problem;
+
+enum mh_scheme { MH_HERMITE_SIMPSON = 0, MH_TRAPEZOIDAL = 1 };
+enum mh_fd { MH_FD_CENTRAL = 0, MH_FD_FORWARD = 1, MH_FD_BACKWARD = 2 };
+
+typedef struct mh_options {
+    int32_t num_mesh_intervals;          /* uniform mesh (CasOCSolver.h:38-42) */
+    int32_t transcription;               /* mh_scheme                        */
+    int32_t interpolate_control_midpoints;
+    int32_t finite_difference_scheme;    /* mh_fd                            */
+    double fd_step;                      /* absolute step h (<=0: 1e-8)      */
+    /* Mesh-interval shard owned by this context, [interval_begin,
+     * interval_end).  interval_end <= 0 means "all intervals".  A sharded
+     * context evaluates the g rows / Jacobian nonzeros of its intervals
+     * (CasOCTranscription.h:219-313 keeps them contiguous). */
+    int32_t interval_begin;
+    int32_t interval_end;
+    int32_t device;                      /* HIP device ordinal               */
+    int32_t reserved;
+} mh_options;
+
+typedef struct mh_ctx mh_ctx;
+
+/* Sizes of the full NLP and of this context's shard. */
+typedef struct mh_nlp_info {
+    int64_t n;           /* variables                                        */
+    int64_t m;           /* constraints                                      */
+    int64_t nnz_jac_g;   /* Jacobian nonzeros                                */
+    int64_t nnz_h_lag;   /* 0: limited-memory Hessian                        */
+    int64_t num_grid_points;
+    int64_t num_states, num_controls;
+    /* shard: rows [row_begin,row_end) and nonzeros [nnz_begin,nnz_end)     */
+    int64_t row_begin, row_end;
+    int64_t nnz_begin, nnz_end;
+} mh_nlp_info;
+
+int mh_abi_version(void);
+const char* mh_last_error(void);
+
+int mh_create(const mh_problem* problem, const mh_options* options,
+        mh_ctx** ctx);
+void mh_destroy(mh_ctx* ctx);
+
+int mh_get_nlp_info(const mh_ctx* ctx, mh_nlp_info* info);
+int mh_get_bounds(const mh_ctx* ctx, double* x_l, double* x_u, double* g_l,
+        double* g_u);
+int mh_get_initial_guess_from_bounds(const mh_ctx* ctx, double* x);
+/* createRandomIterateWithinBounds with caller-provided uniform(-1,1) draws
+ * (one per variable, in x order). */
+int mh_get_random_iterate(const mh_ctx* ctx, const double* rand, double* x);
+/* Full-problem structure (all rows), C_STYLE, row-major nonzero order. */
+int mh_get_jac_structure(const mh_ctx* ctx, int32_t* iRow, int32_t* jCol);
+
+/* Host-pointer evaluations.  g / values receive the FULL vectors when the
+ * context is unsharded, otherwise this shard's rows / nonzeros only. */
+int mh_eval_f(mh_ctx* ctx, const double* x, int new_x, double* f);
+int mh_eval_grad_f(mh_ctx* ctx, const double* x, int new_x, double* grad_f);
+int mh_eval_g(mh_ctx* ctx, const double* x, int new_x, double* g);
+int mh_eval_jac_g(mh_ctx* ctx, const double* x, int new_x, double* values);
+
+/* Device-pointer evaluations (x, g, values in device memory of the
+ * context's device; stream-ordered on the context stream and synchronized
+ * before returning). */
+int mh_eval_g_device(mh_ctx* ctx, const double* x_dev, double* g_dev);
+int mh_eval_jac_g_device(mh_ctx* ctx, const double* x_dev,
+        double* values_dev);
+
+/* Per-point DAE probe (CasOC::Problem::calcMultibodySystemExplicit,
+ * CasOCProblem.h:313-332) evaluated on the device for npoints inputs laid
+ * out as [time, states(NS), controls(NC)] per point; outputs
+ * [udot(NQ), zdot(NZ)] per point.  Used by parity tests. */
+int mh_eval_dae(mh_ctx* ctx, int32_t npoints, const double* inputs,
+        double* outputs);
+
+/* Timing of the last evaluation on the context stream (HIP events), in ms:
+ * [0] whole call, [1] DAE/FD kernel, [2] assembly kernel. */
+int mh_last_timings(const mh_ctx* ctx, double* ms3);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* MOCOHIP_H */

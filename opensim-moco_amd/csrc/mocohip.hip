@@ -1,0 +1,1204 @@
+// mocohip.hip — MI355X (gfx950) implementation of the C ABI in
+// include/mocohip.h: the direct-collocation NLP hot path of Moco's
+// MocoCasADiSolver (CasOCTranscription / CasOCHermiteSimpson /
+// CasOCTrapezoidal) with its per-grid-point DAE and finite-difference
+// Jacobian, re-designed for CDNA4:
+//
+//   k_base      one lane per grid point: DAE at the unperturbed point
+//               (feeds eval_g, the t0/tf Jacobian terms and forward FD).
+//   k_fd        one 64-lane wave per (grid point, 32 directions): lanes l and
+//               l^32 evaluate the +h / -h arms of the same direction and
+//               difference through a cross-lane shuffle (no HBM round trip
+//               of the arms); writes D[k][out][dir] with dir contiguous.
+//   k_defects   one workgroup per mesh interval: Hermite / Simpson /
+//               trapezoidal defects + control interpolation rows, written in
+//               CasOC flattenConstraints order (CasOCTranscription.h:219-313).
+//   k_assemble  one workgroup per mesh interval: streams the interval's
+//               nonzeros (row-major, a fixed per-interval template) and
+//               chains D through the defect formulas.  HBM-bound.
+//   k_integrand / k_grad_f / k_reduce_f : objective and its gradient.
+//
+// There is no CPU fallback anywhere in this file.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/mocohip.h"
+#include "dae_device.hpp"
+
+using namespace mh;
+
+// ------------------------------------------------------------------------
+// error handling
+// ------------------------------------------------------------------------
+static thread_local std::string g_err;
+static int set_err(int code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+#define HIPCHK(expr)                                                              \
+    do {                                                                          \
+        hipError_t e_ = (expr);                                                   \
+        if (e_ != hipSuccess)                                                     \
+            return set_err(MH_ERR_HIP, "%s failed: %s", #expr, hipGetErrorString(e_)); \
+    } while (0)
+
+extern "C" int mh_abi_version(void) { return MH_ABI_VERSION; }
+extern "C" const char* mh_last_error(void) { return g_err.c_str(); }
+
+// ------------------------------------------------------------------------
+// Jacobian template (per mesh interval; identical for every interval).
+// ------------------------------------------------------------------------
+enum TplKind : uint8_t {
+    T_HERM_T = 0, T_SIMP_T = 1, T_HERM_X = 2, T_SIMP_X = 3, T_INTERP = 4,
+    T_TRAP_T = 5, T_TRAP_X = 6
+};
+struct TplEntry {
+    int16_t row;   // row within the interval
+    uint8_t kind;
+    uint8_t pt;    // 0 = first point of interval, 1 = mid (HS), 2 = last (HS) / 1 last (trap)
+    int16_t dir;   // 0 = t0, 1 = tf, 2 + j = point input j
+    int16_t s;     // state index of the row (defects) / control index (interp)
+};
+
+// ------------------------------------------------------------------------
+// Size classes of the per-lane workspace.
+// ------------------------------------------------------------------------
+struct SzSmall { static constexpr int MB = 4, MQ = 4, MP = 4, MI = 24, MO = 12; };
+struct SzMedium { static constexpr int MB = 16, MQ = 16, MP = 8, MI = 128, MO = 64; };
+struct SzLarge { static constexpr int MB = 32, MQ = 40, MP = 12, MI = 384, MO = 192; };
+
+struct Layout {
+    int NS, NC, NQ, NO, NI;  // NI = NS + NC
+    int G;                   // grid points (full problem)
+    int k0;                  // first grid point of this shard
+    int nk;                  // grid points in this shard
+};
+
+__device__ __forceinline__ void gather_inputs(const double* __restrict__ x, const Layout& L,
+        int k, double* in, int NI) {
+    const double* xs = x + 2 + (long)k * L.NS;
+    const double* xc = x + 2 + (long)L.NS * L.G + (long)k * L.NC;
+    for (int s = 0; s < L.NS; ++s) in[s] = xs[s];
+    for (int j = 0; j < L.NC; ++j) in[L.NS + j] = xc[j];
+    (void)NI;
+}
+
+template <class Z>
+__global__ void __launch_bounds__(64) k_base(DevModel M, Layout L, const double* __restrict__ x,
+        const double* __restrict__ grid, double* __restrict__ times, double* __restrict__ Y) {
+    const int kl = blockIdx.x * blockDim.x + threadIdx.x;
+    if (kl >= L.nk) return;
+    const int k = L.k0 + kl;
+    const double t0 = x[0], tf = x[1];
+    const double t = (tf - t0) * grid[k] + t0;
+    times[kl] = t;
+    double in[Z::MI];
+    double out[Z::MO];
+    gather_inputs(x, L, k, in, L.NI);
+    Work<Z::MB, Z::MQ, Z::MP> w;
+    dae_eval<Z::MB, Z::MQ, Z::MP>(M, w, t, in, in + L.NS, out);
+    for (int o = 0; o < L.NO; ++o) Y[(long)kl * L.NO + o] = out[o];
+}
+
+// Central differences: lanes (l, l^32) are the (+h, -h) arms of direction
+// blockIdx.x*32 + (l&31) at grid point blockIdx.y.  Forward/backward: one
+// arm per lane, 64 directions per wave.
+template <class Z>
+__global__ void __launch_bounds__(64) k_fd(DevModel M, Layout L, int fd, double h,
+        const double* __restrict__ x, const double* __restrict__ grid,
+        const double* __restrict__ Ybase, double* __restrict__ D) {
+    const int ND = L.NI + 2;
+    const int lane = threadIdx.x;
+    const int kl = blockIdx.y;
+    const int k = L.k0 + kl;
+    int d, sign;
+    if (fd == MH_FD_CENTRAL) { d = blockIdx.x * 32 + (lane & 31); sign = lane >> 5; }
+    else { d = blockIdx.x * 64 + lane; sign = (fd == MH_FD_FORWARD) ? 0 : 1; }
+    const bool valid = d < ND;
+    const int dd = valid ? d : ND - 1;
+    const double g = grid[k];
+    const double t0 = x[0], tf = x[1];
+    double t = (tf - t0) * g + t0;
+    double in[Z::MI];
+    double out[Z::MO];
+    gather_inputs(x, L, k, in, L.NI);
+    const double step = sign == 0 ? h : -h;
+    if (dd == 0) t = t + step * (1.0 - g);
+    else if (dd == 1) t = t + step * g;
+    else in[dd - 2] = in[dd - 2] + step;
+    Work<Z::MB, Z::MQ, Z::MP> w;
+    dae_eval<Z::MB, Z::MQ, Z::MP>(M, w, t, in, in + L.NS, out);
+    double* Dk = D + (long)kl * L.NO * ND;
+    if (fd == MH_FD_CENTRAL) {
+        const double inv2h = 2.0 * h;
+        for (int o = 0; o < L.NO; ++o) {
+            const double other = __shfl_xor(out[o], 32);
+            if (sign == 0 && valid) Dk[(long)o * ND + d] = (out[o] - other) / inv2h;
+        }
+    } else {
+        const double* yb = Ybase + (long)kl * L.NO;
+        if (valid) {
+            for (int o = 0; o < L.NO; ++o) {
+                const double v = fd == MH_FD_FORWARD ? (out[o] - yb[o]) / h : (yb[o] - out[o]) / h;
+                Dk[(long)o * ND + d] = v;
+            }
+        }
+    }
+}
+
+struct Interval {
+    int scheme;      // MH_HERMITE_SIMPSON / MH_TRAPEZOIDAL
+    int interp;
+    int ib;          // first interval of shard
+    int rpi;         // rows per interval
+    int nnz_int;     // nonzeros per interval
+};
+
+__device__ __forceinline__ int grid_of(const Interval& I, int i, int pt) {
+    return I.scheme == MH_HERMITE_SIMPSON ? 2 * i + pt : i + pt;
+}
+
+// xdot[s] at local grid point kl (global k).
+__device__ __forceinline__ double xdot_at(const Layout& L, const double* __restrict__ x,
+        const double* __restrict__ Y, int k, int kl, int s) {
+    if (s < L.NQ) return x[2 + (long)k * L.NS + L.NQ + s];
+    return Y[(long)kl * L.NO + (s - L.NQ)];
+}
+
+__global__ void __launch_bounds__(256) k_defects(Layout L, Interval I, const double* __restrict__ x,
+        const double* __restrict__ times, const double* __restrict__ Y, double* __restrict__ g) {
+    const int il = blockIdx.x;
+    const int i = I.ib + il;
+    const int NS = L.NS;
+    double* gi = g + (long)il * I.rpi;
+    if (I.scheme == MH_HERMITE_SIMPSON) {
+        const int ki = 2 * i, km = ki + 1, kp = ki + 2;
+        const int kli = ki - L.k0, klm = km - L.k0, klp = kp - L.k0;
+        const double h = times[klp] - times[kli];
+        for (int r = threadIdx.x; r < I.rpi; r += blockDim.x) {
+            double v;
+            if (r < NS) {
+                const int s = r;
+                const double xi = x[2 + (long)ki * NS + s], xm = x[2 + (long)km * NS + s],
+                             xp = x[2 + (long)kp * NS + s];
+                const double fi = xdot_at(L, x, Y, ki, kli, s), fp = xdot_at(L, x, Y, kp, klp, s);
+                v = xm - 0.5 * (xp + xi) - (h / 8.0) * (fi - fp);
+            } else if (r < 2 * NS) {
+                const int s = r - NS;
+                const double xi = x[2 + (long)ki * NS + s], xp = x[2 + (long)kp * NS + s];
+                const double fi = xdot_at(L, x, Y, ki, kli, s), fm = xdot_at(L, x, Y, km, klm, s),
+                             fp = xdot_at(L, x, Y, kp, klp, s);
+                v = xp - xi - (h / 6.0) * (fp + 4.0 * fm + fi);
+            } else {
+                const int j = r - 2 * NS;
+                const double* xc = x + 2 + (long)NS * L.G;
+                v = xc[(long)km * L.NC + j] - 0.5 * (xc[(long)kp * L.NC + j] + xc[(long)ki * L.NC + j]);
+            }
+            gi[r] = v;
+        }
+    } else {
+        const int ki = i, kp = i + 1;
+        const int kli = ki - L.k0, klp = kp - L.k0;
+        const double h = times[klp] - times[kli];
+        for (int r = threadIdx.x; r < I.rpi; r += blockDim.x) {
+            const int s = r;
+            const double xi = x[2 + (long)ki * NS + s], xp = x[2 + (long)kp * NS + s];
+            const double fi = xdot_at(L, x, Y, ki, kli, s), fp = xdot_at(L, x, Y, kp, klp, s);
+            gi[r] = xp - (xi + 0.5 * h * (fp + fi));
+        }
+    }
+}
+
+// d xdot[s] / d dir at local grid point kl.
+__device__ __forceinline__ double dxdot(const Layout& L, const double* __restrict__ D, int kl,
+        int s, int dir) {
+    const int ND = L.NI + 2;
+    if (s < L.NQ) return dir == 2 + L.NQ + s ? 1.0 : 0.0;
+    return D[((long)kl * L.NO + (s - L.NQ)) * ND + dir];
+}
+
+__global__ void __launch_bounds__(256) k_assemble(Layout L, Interval I,
+        const TplEntry* __restrict__ tpl, const double* __restrict__ x,
+        const double* __restrict__ grid, const double* __restrict__ times,
+        const double* __restrict__ Y, const double* __restrict__ D, double* __restrict__ values) {
+    const int il = blockIdx.x;
+    const int i = I.ib + il;
+    const int k_first = grid_of(I, i, 0);
+    const int npts = I.scheme == MH_HERMITE_SIMPSON ? 3 : 2;
+    const int k_last = k_first + npts - 1;
+    const double h = times[k_last - L.k0] - times[k_first - L.k0];
+    const double dgap = grid[k_last] - grid[k_first];
+    double* vi = values + (long)il * I.nnz_int;
+    for (int e = threadIdx.x; e < I.nnz_int; e += blockDim.x) {
+        const TplEntry T = tpl[e];
+        const int s = T.s, dir = T.dir;
+        double v = 0.0;
+        switch (T.kind) {
+        case T_HERM_T: {
+            const int ki = k_first, kp = k_first + 2;
+            const double dh = dir == 0 ? -dgap : dgap;
+            const double fi = xdot_at(L, x, Y, ki, ki - L.k0, s), fp = xdot_at(L, x, Y, kp, kp - L.k0, s);
+            v = -(dh / 8.0) * (fi - fp) -
+                (h / 8.0) * (dxdot(L, D, ki - L.k0, s, dir) - dxdot(L, D, kp - L.k0, s, dir));
+            break;
+        }
+        case T_SIMP_T: {
+            const int ki = k_first, km = k_first + 1, kp = k_first + 2;
+            const double dh = dir == 0 ? -dgap : dgap;
+            const double fi = xdot_at(L, x, Y, ki, ki - L.k0, s), fm = xdot_at(L, x, Y, km, km - L.k0, s),
+                         fp = xdot_at(L, x, Y, kp, kp - L.k0, s);
+            v = -(dh / 6.0) * (fp + 4.0 * fm + fi) -
+                (h / 6.0) * (dxdot(L, D, kp - L.k0, s, dir) + 4.0 * dxdot(L, D, km - L.k0, s, dir) +
+                             dxdot(L, D, ki - L.k0, s, dir));
+            break;
+        }
+        case T_HERM_X: {
+            const int k = k_first + T.pt;
+            const bool ident = dir == 2 + s;
+            if (T.pt == 1) { v = ident ? 1.0 : 0.0; break; }
+            if (ident) v += -0.5;
+            const double dv = dxdot(L, D, k - L.k0, s, dir);
+            v += (T.pt == 0 ? -(h / 8.0) : (h / 8.0)) * dv;
+            break;
+        }
+        case T_SIMP_X: {
+            const int k = k_first + T.pt;
+            const bool ident = dir == 2 + s;
+            const double dv = dxdot(L, D, k - L.k0, s, dir);
+            if (T.pt == 2) { if (ident) v += 1.0; v += -(h / 6.0) * dv; }
+            else if (T.pt == 0) { if (ident) v += -1.0; v += -(h / 6.0) * dv; }
+            else v += -(h / 6.0) * 4.0 * dv;
+            break;
+        }
+        case T_INTERP:
+            v = T.pt == 1 ? 1.0 : -0.5;
+            break;
+        case T_TRAP_T: {
+            const int ki = k_first, kp = k_first + 1;
+            const double dh = dir == 0 ? -dgap : dgap;
+            const double fi = xdot_at(L, x, Y, ki, ki - L.k0, s), fp = xdot_at(L, x, Y, kp, kp - L.k0, s);
+            v = -0.5 * dh * (fp + fi) -
+                0.5 * h * (dxdot(L, D, kp - L.k0, s, dir) + dxdot(L, D, ki - L.k0, s, dir));
+            break;
+        }
+        case T_TRAP_X: {
+            const int k = k_first + T.pt;
+            const bool ident = dir == 2 + s;
+            const double dv = dxdot(L, D, k - L.k0, s, dir);
+            if (T.pt == 1) { if (ident) v += 1.0; v += -0.5 * h * dv; }
+            else { if (ident) v += -1.0; v += -0.5 * h * dv; }
+            break;
+        }
+        }
+        vi[e] = v;
+    }
+}
+
+// ---- objective -------------------------------------------------------------
+struct GoalSet {
+    int ngoals;
+    const mh_goal* goals;
+    const int* gidx;
+    const int* gcol;
+    const double* gw;
+};
+
+__device__ double goal_integrand(const DevModel& M, const GoalSet& GS, int g, double t,
+        const double* st, const double* ct) {
+    const mh_goal G = GS.goals[g];
+    double L = 0.0;
+    for (int k = G.term_begin; k < G.term_begin + G.term_count; ++k) {
+        const int idx = GS.gidx[k];
+        const double w = GS.gw[k];
+        if (G.kind == MH_GOAL_CONTROL) {
+            const double v = ct[idx];
+            L += w * (G.exponent == 2 ? v * v : pow(fabs(v), (double)G.exponent));
+        } else if (G.kind == MH_GOAL_STATE_TRACKING) {
+            const double d = st[idx] - table_eval(M, G.table, GS.gcol[k], t);
+            L += w * (d * d);
+        } else if (G.kind == MH_GOAL_SUM_SQUARED_STATE) {
+            const double v = st[idx];
+            L += w * (v * v);
+        }
+    }
+    return L;
+}
+
+// Per-point quad-weighted integrands: C[k*ngoals + g] = quad_k * L_g(k).
+template <class Z>
+__global__ void __launch_bounds__(64) k_integrand(DevModel M, Layout L, GoalSet GS,
+        const double* __restrict__ x, const double* __restrict__ grid,
+        const double* __restrict__ quad, double* __restrict__ C) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= L.G) return;
+    const double t = (x[1] - x[0]) * grid[k] + x[0];
+    double in[Z::MI];
+    gather_inputs(x, L, k, in, L.NI);
+    for (int g = 0; g < GS.ngoals; ++g) {
+        const bool integral = GS.goals[g].kind != MH_GOAL_FINAL_TIME;
+        C[(long)k * GS.ngoals + g] =
+                integral ? quad[k] * goal_integrand(M, GS, g, t, in, in + L.NS) : 0.0;
+    }
+}
+
+// Gradient of the integral terms: one lane per (grid point, direction).
+template <class Z>
+__global__ void __launch_bounds__(64) k_grad(DevModel M, Layout L, GoalSet GS, int fd, double h,
+        const double* __restrict__ x, const double* __restrict__ grid,
+        const double* __restrict__ quad, double* __restrict__ grad, double* __restrict__ tpart) {
+    const int ND = L.NI + 2;
+    const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (tid >= (long)L.G * ND) return;
+    const int k = (int)(tid / ND), d = (int)(tid % ND);
+    const double g = grid[k];
+    const double dur = x[1] - x[0];
+    const double t = dur * g + x[0];
+    double in[Z::MI];
+    gather_inputs(x, L, k, in, L.NI);
+    double acc = 0.0;
+    for (int gi = 0; gi < GS.ngoals; ++gi) {
+        const mh_goal G = GS.goals[gi];
+        if (G.kind == MH_GOAL_FINAL_TIME) continue;
+        const double seed = d == 0 ? 1.0 - g : (d == 1 ? g : 1.0);
+        double lp = 0.0, lm = 0.0, l0 = 0.0;
+        if (fd != MH_FD_CENTRAL) l0 = goal_integrand(M, GS, gi, t, in, in + L.NS);
+        if (fd != MH_FD_BACKWARD) {
+            if (d < 2) lp = goal_integrand(M, GS, gi, t + h * seed, in, in + L.NS);
+            else {
+                const double s = in[d - 2];
+                in[d - 2] = s + h;
+                lp = goal_integrand(M, GS, gi, t, in, in + L.NS);
+                in[d - 2] = s;
+            }
+        }
+        if (fd != MH_FD_FORWARD) {
+            if (d < 2) lm = goal_integrand(M, GS, gi, t - h * seed, in, in + L.NS);
+            else {
+                const double s = in[d - 2];
+                in[d - 2] = s - h;
+                lm = goal_integrand(M, GS, gi, t, in, in + L.NS);
+                in[d - 2] = s;
+            }
+        }
+        const double dL = fd == MH_FD_CENTRAL ? (lp - lm) / (2.0 * h)
+                        : (fd == MH_FD_FORWARD ? (lp - l0) / h : (l0 - lm) / h);
+        acc += G.weight * dur * quad[k] * dL;
+    }
+    if (d < 2) tpart[(long)k * 2 + d] = acc;
+    else if (d - 2 < L.NS) grad[2 + (long)k * L.NS + (d - 2)] = acc;
+    else grad[2 + (long)L.NS * L.G + (long)k * L.NC + (d - 2 - L.NS)] = acc;
+}
+
+// Single-workgroup deterministic reduction of the objective (mode 0) or of
+// the t0/tf gradient entries (mode 1).
+__global__ void __launch_bounds__(256) k_reduce_obj(Layout L, GoalSet GS, int mode,
+        const double* __restrict__ x, const double* __restrict__ C,
+        const double* __restrict__ tpart, double* __restrict__ out) {
+    __shared__ double red[256];
+    const int ng = GS.ngoals;
+    double total = 0.0, g0 = 0.0, g1 = 0.0;
+    for (int gi = 0; gi < ng; ++gi) {
+        double s = 0.0;
+        for (int k = threadIdx.x; k < L.G; k += blockDim.x) s += C[(long)k * ng + gi];
+        red[threadIdx.x] = s;
+        __syncthreads();
+        for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+            if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+            __syncthreads();
+        }
+        const double acc = red[0];
+        __syncthreads();
+        const mh_goal G = GS.goals[gi];
+        if (G.kind == MH_GOAL_FINAL_TIME) {
+            total += G.weight * x[1];
+            g1 += G.weight;
+        } else {
+            total += G.weight * ((x[1] - x[0]) * acc);
+            g0 += -G.weight * acc;
+            g1 += G.weight * acc;
+        }
+    }
+    if (mode == 0) {
+        if (threadIdx.x == 0) out[0] = total;
+        return;
+    }
+    for (int c = 0; c < 2; ++c) {
+        double s = 0.0;
+        for (int k = threadIdx.x; k < L.G; k += blockDim.x) s += tpart[(long)k * 2 + c];
+        red[threadIdx.x] = s;
+        __syncthreads();
+        for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+            if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) out[c] = red[0] + (c == 0 ? g0 : g1);
+        __syncthreads();
+    }
+}
+
+// DAE probe: one lane per input row [time, states, controls].
+template <class Z>
+__global__ void __launch_bounds__(64) k_dae_probe(DevModel M, Layout L, int npts,
+        const double* __restrict__ in, double* __restrict__ outp) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= npts) return;
+    const double* r = in + (long)p * (1 + L.NI);
+    double v[Z::MI];
+    double out[Z::MO];
+    for (int i = 0; i < L.NI; ++i) v[i] = r[1 + i];
+    Work<Z::MB, Z::MQ, Z::MP> w;
+    dae_eval<Z::MB, Z::MQ, Z::MP>(M, w, r[0], v, v + L.NS, out);
+    for (int o = 0; o < L.NO; ++o) outp[(long)p * L.NO + o] = out[o];
+}
+
+// ------------------------------------------------------------------------
+// Host side.
+// ------------------------------------------------------------------------
+namespace {
+
+// SimmSpline coefficients (Forsythe–Malcolm–Moler with third-derivative end
+// conditions; opensim-core SimmSpline::calcCoefficients, third-party).
+void simm_coefficients(int n, const double* x, const double* y, double* b, double* c, double* d) {
+    if (n < 2) { if (n == 1) b[0] = c[0] = d[0] = 0.0; return; }
+    if (n < 3) {
+        const double t = (y[1] - y[0]) / (x[1] - x[0]);
+        b[0] = b[1] = t; c[0] = c[1] = d[0] = d[1] = 0.0;
+        return;
+    }
+    const int nm1 = n - 1;
+    d[0] = x[1] - x[0];
+    c[1] = (y[1] - y[0]) / d[0];
+    for (int i = 1; i < nm1; ++i) {
+        d[i] = x[i + 1] - x[i];
+        b[i] = 2.0 * (d[i - 1] + d[i]);
+        c[i + 1] = (y[i + 1] - y[i]) / d[i];
+        c[i] = c[i + 1] - c[i];
+    }
+    b[0] = -d[0];
+    b[nm1] = -d[n - 2];
+    c[0] = 0.0;
+    c[nm1] = 0.0;
+    if (n > 3) {
+        const double d1 = c[2] / (x[3] - x[1]) - c[1] / (x[2] - x[0]);
+        const double d2 = c[nm1 - 1] / (x[nm1] - x[n - 3]) - c[n - 3] / (x[nm1 - 1] - x[n - 4]);
+        c[0] = d[0] * d1 / (x[3] - x[0]);
+        c[nm1] = -d[n - 2] * d2 / (x[nm1] - x[n - 4]);
+    }
+    for (int i = 1; i < n; ++i) {
+        const double t = d[i - 1] / b[i - 1];
+        b[i] -= t * d[i - 1];
+        c[i] -= t * c[i - 1];
+    }
+    c[nm1] /= b[nm1];
+    for (int j = 0; j < nm1; ++j) {
+        const int i = nm1 - j - 1;
+        c[i] = (c[i] - d[i] * c[i + 1]) / b[i];
+    }
+    b[nm1] = (y[nm1] - y[n - 2]) / d[n - 2] + d[n - 2] * (c[n - 2] + 2.0 * c[nm1]);
+    for (int i = 0; i < nm1; ++i) {
+        b[i] = (y[i + 1] - y[i]) / d[i] - d[i] * (c[i + 1] + 2.0 * c[i]);
+        d[i] = (c[i + 1] - c[i]) / d[i];
+        c[i] *= 3.0;
+    }
+    c[nm1] *= 3.0;
+    d[nm1] = d[n - 2];
+}
+
+// Device arena: one allocation per context, carved into aligned pieces.
+struct Arena {
+    char* base = nullptr;
+    size_t size = 0, used = 0;
+    std::vector<std::pair<size_t, std::vector<char>>> uploads;
+    size_t reserve(size_t bytes) {
+        size_t off = (used + 255) & ~size_t(255);
+        used = off + bytes;
+        return off;
+    }
+    template <class T>
+    size_t put(const T* p, size_t n) {
+        size_t off = reserve(sizeof(T) * std::max<size_t>(n, 1));
+        std::vector<char> blob(sizeof(T) * std::max<size_t>(n, 1), 0);
+        if (n) std::memcpy(blob.data(), p, sizeof(T) * n);
+        uploads.emplace_back(off, std::move(blob));
+        return off;
+    }
+};
+
+}  // namespace
+
+struct mh_ctx {
+    // problem
+    int NQ = 0, NZ = 0, NS = 0, NC = 0, NO = 0, NI = 0;
+    int scheme = 0, N = 0, G = 0, interp = 0, rpi = 0, nnz_int = 0;
+    int ib = 0, ie = 0, k0 = 0, nk = 0;
+    int fd = 0;
+    double h = 1e-8;
+    int size_class = 0;
+    int64_t n = 0, m = 0, nnz = 0;
+    std::vector<double> grid, quad;
+    std::vector<TplEntry> tpl;
+    std::vector<int> tpl_col_pt;   // template column: point (0..2) or -1 for t0/tf
+    std::vector<int64_t> tpl_col_off;  // template column offset within point block
+    std::vector<mh_variable_info> sinfo, cinfo;
+    mh_bounds t_init{}, t_final{};
+    int ngoals = 0;
+    // device
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[4] = {};
+    char* dmem = nullptr;
+    DevModel M{};
+    GoalSet GS{};
+    double *d_x = nullptr, *d_grid = nullptr, *d_quad = nullptr, *d_times = nullptr, *d_Y = nullptr,
+           *d_D = nullptr, *d_g = nullptr, *d_vals = nullptr, *d_C = nullptr, *d_grad = nullptr,
+           *d_tpart = nullptr, *d_f = nullptr;
+    TplEntry* d_tpl = nullptr;
+    float timings[3] = {0, 0, 0};
+};
+
+static int64_t col_state(const mh_ctx* c, int64_t k, int s) { return 2 + k * c->NS + s; }
+static int64_t col_control(const mh_ctx* c, int64_t k, int j) {
+    return 2 + (int64_t)c->NS * c->G + k * c->NC + j;
+}
+
+// Build the per-interval template in CasOC row order with columns sorted
+// ascending (the block-dense structural rule).
+static void build_template(mh_ctx* c) {
+    const int NS = c->NS, NQ = c->NQ, NC = c->NC;
+    struct Col { int pt; int dir; };  // dir: 0/1 time, 2+input
+    auto key = [&](const Col& col) -> int64_t {
+        // column index for interval 0
+        if (col.dir < 2) return col.dir;
+        const int j = col.dir - 2;
+        if (j < NS) return col_state(c, col.pt, j);
+        return col_control(c, col.pt, j - NS);
+    };
+    auto emit_row = [&](int row, uint8_t kind_t, uint8_t kind_x, int s, std::vector<Col> cols) {
+        std::sort(cols.begin(), cols.end(), [&](const Col& a, const Col& b) { return key(a) < key(b); });
+        for (const auto& col : cols) {
+            TplEntry e{};
+            e.row = (int16_t)row;
+            e.kind = col.dir < 2 ? kind_t : kind_x;
+            e.pt = (uint8_t)(col.dir < 2 ? 0 : col.pt);
+            e.dir = (int16_t)col.dir;
+            e.s = (int16_t)s;
+            c->tpl.push_back(e);
+            c->tpl_col_pt.push_back(col.dir < 2 ? -1 : col.pt);
+        }
+    };
+    auto point_all = [&](int pt, std::vector<Col>& v) {
+        for (int j = 0; j < NS + NC; ++j) v.push_back({pt, 2 + j});
+    };
+    int row = 0;
+    if (c->scheme == MH_HERMITE_SIMPSON) {
+        for (int s = 0; s < NS; ++s) {
+            std::vector<Col> v{{0, 0}, {0, 1}};
+            if (s < NQ) {
+                v.push_back({1, 2 + s}); v.push_back({0, 2 + s}); v.push_back({2, 2 + s});
+                v.push_back({0, 2 + NQ + s}); v.push_back({2, 2 + NQ + s});
+            } else {
+                v.push_back({1, 2 + s});
+                point_all(0, v); point_all(2, v);
+            }
+            emit_row(row++, T_HERM_T, T_HERM_X, s, v);
+        }
+        for (int s = 0; s < NS; ++s) {
+            std::vector<Col> v{{0, 0}, {0, 1}};
+            if (s < NQ) {
+                v.push_back({0, 2 + s}); v.push_back({2, 2 + s});
+                v.push_back({0, 2 + NQ + s}); v.push_back({1, 2 + NQ + s}); v.push_back({2, 2 + NQ + s});
+            } else {
+                point_all(0, v); point_all(1, v); point_all(2, v);
+            }
+            emit_row(row++, T_SIMP_T, T_SIMP_X, s, v);
+        }
+        if (c->interp) {
+            for (int j = 0; j < NC; ++j) {
+                std::vector<Col> v{{0, 2 + NS + j}, {1, 2 + NS + j}, {2, 2 + NS + j}};
+                emit_row(row++, T_INTERP, T_INTERP, j, v);
+            }
+        }
+    } else {
+        for (int s = 0; s < NS; ++s) {
+            std::vector<Col> v{{0, 0}, {0, 1}};
+            if (s < NQ) {
+                v.push_back({0, 2 + s}); v.push_back({1, 2 + s});
+                v.push_back({0, 2 + NQ + s}); v.push_back({1, 2 + NQ + s});
+            } else {
+                point_all(0, v); point_all(1, v);
+            }
+            emit_row(row++, T_TRAP_T, T_TRAP_X, s, v);
+        }
+    }
+    c->rpi = row;
+    c->nnz_int = (int)c->tpl.size();
+}
+
+static int validate_and_layout(mh_ctx* c, const mh_problem* p, const mh_options* o,
+        std::vector<int>& coord_body, std::vector<int>& act_state, std::vector<int>& ftn_state,
+        std::vector<int>& mus_control, double& tau_act, double& tau_deact) {
+    const mh_model& M = p->model;
+    if (M.nq < 0 || M.nbodies < 0 || M.nmuscles < 0 || M.nactuators < 0)
+        return set_err(MH_ERR_INVALID, "negative model counts");
+    if (o->num_mesh_intervals < 1) return set_err(MH_ERR_INVALID, "num_mesh_intervals must be >= 1");
+    if (o->transcription != MH_HERMITE_SIMPSON && o->transcription != MH_TRAPEZOIDAL)
+        return set_err(MH_ERR_INVALID, "unknown transcription scheme %d", o->transcription);
+    if (o->finite_difference_scheme < 0 || o->finite_difference_scheme > 2)
+        return set_err(MH_ERR_INVALID, "unknown finite difference scheme");
+    c->NQ = M.nq;
+    int z = 2 * M.nq;
+    tau_act = tau_deact = NAN;
+    act_state.resize(M.nmuscles);
+    ftn_state.resize(M.nmuscles);
+    mus_control.assign(M.nmuscles, -1);
+    for (int im = 0; im < M.nmuscles; ++im) {
+        const mh_muscle& mu = M.muscles[im];
+        if (mu.tendon_dynamics_implicit && !mu.ignore_tendon_compliance)
+            return set_err(MH_ERR_UNSUPPORTED, "implicit tendon compliance dynamics not supported");
+        if (mu.point_begin < 0 || mu.point_begin + mu.point_count > M.npoints)
+            return set_err(MH_ERR_INVALID, "muscle %d: bad path point range", im);
+        act_state[im] = mu.ignore_activation_dynamics ? -1 : z++;
+        ftn_state[im] = mu.ignore_tendon_compliance ? -1 : z++;
+        // DeGrooteFregly2016Muscle.cpp:194-195 static time constants.
+        if (!mu.ignore_activation_dynamics && std::isnan(tau_act)) {
+            tau_act = mu.activation_time_constant;
+            tau_deact = mu.deactivation_time_constant;
+        }
+    }
+    c->NS = z;
+    c->NZ = z - 2 * M.nq;
+    c->NC = M.nactuators;
+    c->NO = c->NQ + c->NZ;
+    c->NI = c->NS + c->NC;
+    for (int ia = 0; ia < M.nactuators; ++ia) {
+        const mh_actuator& a = M.actuators[ia];
+        if (a.kind == MH_ACT_MUSCLE) {
+            if (a.target < 0 || a.target >= M.nmuscles) return set_err(MH_ERR_INVALID, "actuator %d: bad muscle", ia);
+            mus_control[a.target] = ia;
+        } else if (a.kind == MH_ACT_COORDINATE) {
+            if (a.target < 0 || a.target >= M.nq) return set_err(MH_ERR_INVALID, "actuator %d: bad coordinate", ia);
+        } else {
+            return set_err(MH_ERR_INVALID, "actuator %d: bad kind", ia);
+        }
+    }
+    for (int im = 0; im < M.nmuscles; ++im)
+        if (mus_control[im] < 0) return set_err(MH_ERR_INVALID, "muscle %d has no actuator", im);
+    coord_body.assign(M.nq, -1);
+    for (int b = 0; b < M.nbodies; ++b) {
+        const mh_body& B = M.bodies[b];
+        if (B.parent >= b || B.parent < -1) return set_err(MH_ERR_INVALID, "body %d not topologically ordered", b);
+        if (B.axis_begin < 0 || B.axis_begin + B.axis_count > M.naxes) return set_err(MH_ERR_INVALID, "body %d: bad axes", b);
+        for (int a = B.axis_begin; a < B.axis_begin + B.axis_count; ++a) {
+            const int f = M.axes[a].func;
+            if (f < 0 || f >= M.nfunctions) return set_err(MH_ERR_INVALID, "axis %d: bad function", a);
+            const mh_function& F = M.functions[f];
+            if (F.kind == MH_FN_CONSTANT) continue;
+            if (F.coord < 0 || F.coord >= M.nq) return set_err(MH_ERR_INVALID, "axis %d: bad coordinate", a);
+            if (coord_body[F.coord] >= 0 && coord_body[F.coord] != b)
+                return set_err(MH_ERR_UNSUPPORTED, "coordinate %d drives axes of two bodies", F.coord);
+            coord_body[F.coord] = b;
+        }
+    }
+    for (int j = 0; j < M.nq; ++j)
+        if (coord_body[j] < 0) return set_err(MH_ERR_INVALID, "coordinate %d drives no axis", j);
+    for (int f = 0; f < M.nfunctions; ++f) {
+        const mh_function& F = M.functions[f];
+        if (F.kind == MH_FN_SIMMSPLINE &&
+                (F.knot_count < 1 || F.knot_begin < 0 || F.knot_begin + F.knot_count > M.nknots))
+            return set_err(MH_ERR_INVALID, "function %d: bad knots", f);
+        if (F.kind != MH_FN_CONSTANT && (F.coord < 0 || F.coord >= M.nq))
+            return set_err(MH_ERR_INVALID, "function %d: bad coordinate", f);
+    }
+    for (int i = 0; i < M.npoints; ++i) {
+        const mh_path_point& pt = M.points[i];
+        if (pt.body < -1 || pt.body >= M.nbodies) return set_err(MH_ERR_INVALID, "path point %d: bad body", i);
+        if (pt.kind == MH_PP_CONDITIONAL && (pt.coord < 0 || pt.coord >= M.nq))
+            return set_err(MH_ERR_INVALID, "path point %d: bad coordinate", i);
+    }
+    for (int g = 0; g < p->ngoals; ++g) {
+        const mh_goal& G = p->goals[g];
+        if (G.term_begin < 0 || G.term_begin + G.term_count > p->nterms)
+            return set_err(MH_ERR_INVALID, "goal %d: bad terms", g);
+        if (G.kind == MH_GOAL_STATE_TRACKING && (G.table < 0 || G.table >= M.ntables))
+            return set_err(MH_ERR_INVALID, "goal %d: bad table", g);
+    }
+    for (int e = 0; e < M.nexternal; ++e) {
+        const mh_external_force& E = M.external[e];
+        if (E.body < 0 || E.body >= M.nbodies || E.table < 0 || E.table >= M.ntables)
+            return set_err(MH_ERR_INVALID, "external force %d: bad body/table", e);
+    }
+    // transcription
+    c->scheme = o->transcription;
+    c->N = o->num_mesh_intervals;
+    c->interp = (o->interpolate_control_midpoints && c->NC > 0) ? 1 : 0;
+    c->G = c->scheme == MH_HERMITE_SIMPSON ? 2 * c->N + 1 : c->N + 1;
+    c->grid.assign(c->G, 0.0);
+    c->quad.assign(c->G, 0.0);
+    std::vector<double> mesh(c->N + 1);
+    for (int i = 0; i <= c->N; ++i) mesh[i] = i / (double)c->N;   // CasOCSolver.h:38-42
+    if (c->scheme == MH_HERMITE_SIMPSON) {
+        for (int k = 0; k < c->G; ++k)
+            c->grid[k] = (k % 2 == 0) ? mesh[k / 2] : .5 * (mesh[k / 2] + mesh[k / 2 + 1]);
+        for (int i = 0; i < c->N; ++i) {  // CasOCHermiteSimpson.cpp:36-43
+            const double dm = mesh[i + 1] - mesh[i];
+            c->quad[2 * i] += (1.0 / 6.0) * dm;
+            c->quad[2 * i + 1] += (2.0 / 3.0) * dm;
+            c->quad[2 * i + 2] += (1.0 / 6.0) * dm;
+        }
+    } else {
+        for (int k = 0; k < c->G; ++k) c->grid[k] = mesh[k];
+        for (int i = 0; i < c->N; ++i) {  // CasOCTrapezoidal.cpp:26-37
+            const double dm = mesh[i + 1] - mesh[i];
+            c->quad[i] += 0.5 * dm;
+            c->quad[i + 1] += 0.5 * dm;
+        }
+    }
+    c->n = 2 + (int64_t)(c->NS + c->NC) * c->G;
+    build_template(c);
+    c->m = (int64_t)c->rpi * c->N;
+    c->nnz = (int64_t)c->nnz_int * c->N;
+    c->ib = std::max(0, o->interval_begin);
+    c->ie = o->interval_end > 0 ? std::min(o->interval_end, c->N) : c->N;
+    if (c->ib >= c->ie) return set_err(MH_ERR_INVALID, "empty interval shard [%d, %d)", c->ib, c->ie);
+    c->k0 = c->scheme == MH_HERMITE_SIMPSON ? 2 * c->ib : c->ib;
+    const int klast = c->scheme == MH_HERMITE_SIMPSON ? 2 * c->ie : c->ie;
+    c->nk = klast - c->k0 + 1;
+    c->fd = o->finite_difference_scheme;
+    c->h = o->fd_step > 0 ? o->fd_step : 1e-8;
+    c->sinfo.assign(p->state_infos, p->state_infos + c->NS);
+    c->cinfo.assign(p->control_infos, p->control_infos + c->NC);
+    c->t_init = p->time_initial;
+    c->t_final = p->time_final;
+    c->ngoals = p->ngoals;
+    // size class
+    int maxpts = 0;
+    for (int im = 0; im < M.nmuscles; ++im) maxpts = std::max(maxpts, M.muscles[im].point_count);
+    auto fits = [&](int MB, int MQ, int MP, int MI, int MO) {
+        return M.nbodies <= MB && M.nq <= MQ && maxpts <= MP && c->NI <= MI && c->NO <= MO;
+    };
+    if (fits(SzSmall::MB, SzSmall::MQ, SzSmall::MP, SzSmall::MI, SzSmall::MO)) c->size_class = 0;
+    else if (fits(SzMedium::MB, SzMedium::MQ, SzMedium::MP, SzMedium::MI, SzMedium::MO)) c->size_class = 1;
+    else if (fits(SzLarge::MB, SzLarge::MQ, SzLarge::MP, SzLarge::MI, SzLarge::MO)) c->size_class = 2;
+    else return set_err(MH_ERR_UNSUPPORTED, "model exceeds the largest size class");
+    return MH_OK;
+}
+
+extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out) {
+    if (!p || !o || !out) return set_err(MH_ERR_INVALID, "null argument");
+    *out = nullptr;
+    std::unique_ptr<mh_ctx> c(new mh_ctx());
+    std::vector<int> coord_body, act_state, ftn_state, mus_control;
+    double tau_act, tau_deact;
+    int rc = validate_and_layout(c.get(), p, o, coord_body, act_state, ftn_state, mus_control,
+            tau_act, tau_deact);
+    if (rc) return rc;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return set_err(MH_ERR_HIP, "no HIP device available (the hot path has no CPU fallback)");
+    if (o->device < 0 || o->device >= ndev) return set_err(MH_ERR_HIP, "device %d out of range", o->device);
+    c->device = o->device;
+    HIPCHK(hipSetDevice(c->device));
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, c->device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return set_err(MH_ERR_HIP, "device %d is %s; this build targets gfx950 only", c->device,
+                prop.gcnArchName);
+
+    const mh_model& M = p->model;
+    // host-derived tables
+    std::vector<double> kb(M.nknots + 1, 0.0), kc(M.nknots + 1, 0.0), kd(M.nknots + 1, 0.0);
+    for (int f = 0; f < M.nfunctions; ++f) {
+        const mh_function& F = M.functions[f];
+        if (F.kind == MH_FN_SIMMSPLINE)
+            simm_coefficients(F.knot_count, M.knot_x + F.knot_begin, M.knot_y + F.knot_begin,
+                    kb.data() + F.knot_begin, kc.data() + F.knot_begin, kd.data() + F.knot_begin);
+    }
+    std::vector<double> mder((size_t)MUS_DERIVED * std::max(1, M.nmuscles), 0.0);
+    for (int im = 0; im < M.nmuscles; ++im) {
+        const mh_muscle& mu = M.muscles[im];
+        double* d = &mder[(size_t)im * MUS_DERIVED];
+        d[0] = mu.optimal_fiber_length * std::sin(mu.pennation_angle_at_optimal);
+        d[1] = d[0] * d[0];
+        d[2] = mu.max_contraction_velocity * mu.optimal_fiber_length;
+        d[3] = std::log((1.0 + 0.2) / 0.2) / (1.0 + mu.tendon_strain_at_one_norm_force - 1.0);
+        const double e0 = mu.passive_fiber_strain_at_one_norm_force;
+        d[4] = std::exp(4.0 * (0.2 - 1.0) / e0);
+        d[5] = std::exp(4.0) - d[4];
+    }
+
+    Arena A;
+    const size_t o_bodies = A.put(M.bodies, M.nbodies), o_axes = A.put(M.axes, M.naxes),
+                 o_funcs = A.put(M.functions, M.nfunctions), o_kx = A.put(M.knot_x, M.nknots),
+                 o_ky = A.put(M.knot_y, M.nknots), o_kb = A.put(kb.data(), kb.size()),
+                 o_kc = A.put(kc.data(), kc.size()), o_kd = A.put(kd.data(), kd.size()),
+                 o_mus = A.put(M.muscles, M.nmuscles), o_pts = A.put(M.points, M.npoints),
+                 o_acts = A.put(M.actuators, M.nactuators), o_tabs = A.put(M.tables, M.ntables),
+                 o_brk = A.put(M.table_breaks, M.nbreaks), o_coef = A.put(M.table_coefs, M.ncoefs),
+                 o_ext = A.put(M.external, M.nexternal),
+                 o_cb = A.put(coord_body.data(), coord_body.size()),
+                 o_as = A.put(act_state.data(), act_state.size()),
+                 o_fs = A.put(ftn_state.data(), ftn_state.size()),
+                 o_mc = A.put(mus_control.data(), mus_control.size()),
+                 o_md = A.put(mder.data(), mder.size()),
+                 o_goals = A.put(p->goals, p->ngoals), o_gidx = A.put(p->goal_index, p->nterms),
+                 o_gcol = A.put(p->goal_column, p->nterms), o_gw = A.put(p->goal_weight, p->nterms),
+                 o_grid = A.put(c->grid.data(), c->grid.size()),
+                 o_quad = A.put(c->quad.data(), c->quad.size()),
+                 o_tpl = A.put(c->tpl.data(), c->tpl.size());
+    const int nint = c->ie - c->ib;
+    const int ND = c->NI + 2;
+    const size_t o_x = A.reserve(sizeof(double) * c->n);
+    const size_t o_times = A.reserve(sizeof(double) * c->nk);
+    const size_t o_Y = A.reserve(sizeof(double) * (size_t)c->nk * std::max(1, c->NO));
+    const size_t o_D = A.reserve(sizeof(double) * (size_t)c->nk * std::max(1, c->NO) * ND);
+    const size_t o_g = A.reserve(sizeof(double) * (size_t)nint * c->rpi);
+    const size_t o_vals = A.reserve(sizeof(double) * (size_t)nint * c->nnz_int);
+    const size_t o_C = A.reserve(sizeof(double) * (size_t)c->G * std::max(1, p->ngoals));
+    const size_t o_grad = A.reserve(sizeof(double) * c->n);
+    const size_t o_tpart = A.reserve(sizeof(double) * 2 * (size_t)c->G);
+    const size_t o_f = A.reserve(sizeof(double) * 4);
+    A.size = A.used;
+    HIPCHK(hipMalloc(&c->dmem, A.size));
+    for (auto& up : A.uploads)
+        HIPCHK(hipMemcpy(c->dmem + up.first, up.second.data(), up.second.size(), hipMemcpyHostToDevice));
+    char* b = c->dmem;
+    DevModel& D = c->M;
+    D.nq = M.nq; D.nb = M.nbodies; D.nmus = M.nmuscles; D.nact = M.nactuators; D.next = M.nexternal;
+    D.ns = c->NS; D.nz = c->NZ; D.nc = c->NC; D.no = c->NO; D.np = c->NI;
+    for (int i = 0; i < 3; ++i) D.gravity[i] = M.gravity[i];
+    D.tau_act = tau_act; D.tau_deact = tau_deact;
+    D.bodies = (const mh_body*)(b + o_bodies); D.axes = (const mh_axis*)(b + o_axes);
+    D.funcs = (const mh_function*)(b + o_funcs);
+    D.kx = (const double*)(b + o_kx); D.ky = (const double*)(b + o_ky);
+    D.kb = (const double*)(b + o_kb); D.kc = (const double*)(b + o_kc); D.kd = (const double*)(b + o_kd);
+    D.mus = (const mh_muscle*)(b + o_mus); D.pts = (const mh_path_point*)(b + o_pts);
+    D.acts = (const mh_actuator*)(b + o_acts); D.tabs = (const mh_table*)(b + o_tabs);
+    D.brk = (const double*)(b + o_brk); D.coef = (const double*)(b + o_coef);
+    D.ext = (const mh_external_force*)(b + o_ext);
+    D.coord_body = (const int*)(b + o_cb); D.mus_act_state = (const int*)(b + o_as);
+    D.mus_ftn_state = (const int*)(b + o_fs); D.mus_control = (const int*)(b + o_mc);
+    D.mus_derived = (const double*)(b + o_md);
+    c->GS.ngoals = p->ngoals;
+    c->GS.goals = (const mh_goal*)(b + o_goals);
+    c->GS.gidx = (const int*)(b + o_gidx);
+    c->GS.gcol = (const int*)(b + o_gcol);
+    c->GS.gw = (const double*)(b + o_gw);
+    c->d_grid = (double*)(b + o_grid); c->d_quad = (double*)(b + o_quad);
+    c->d_tpl = (TplEntry*)(b + o_tpl);
+    c->d_x = (double*)(b + o_x); c->d_times = (double*)(b + o_times); c->d_Y = (double*)(b + o_Y);
+    c->d_D = (double*)(b + o_D); c->d_g = (double*)(b + o_g); c->d_vals = (double*)(b + o_vals);
+    c->d_C = (double*)(b + o_C); c->d_grad = (double*)(b + o_grad); c->d_tpart = (double*)(b + o_tpart);
+    c->d_f = (double*)(b + o_f);
+    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
+    *out = c.release();
+    return MH_OK;
+}
+
+extern "C" void mh_destroy(mh_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (auto& e : c->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->dmem) (void)hipFree(c->dmem);
+    delete c;
+}
+
+extern "C" int mh_get_nlp_info(const mh_ctx* c, mh_nlp_info* info) {
+    if (!c || !info) return set_err(MH_ERR_INVALID, "null argument");
+    std::memset(info, 0, sizeof *info);
+    info->n = c->n;
+    info->m = c->m;
+    info->nnz_jac_g = c->nnz;
+    info->nnz_h_lag = 0;
+    info->num_grid_points = c->G;
+    info->num_states = c->NS;
+    info->num_controls = c->NC;
+    info->row_begin = (int64_t)c->ib * c->rpi;
+    info->row_end = (int64_t)c->ie * c->rpi;
+    info->nnz_begin = (int64_t)c->ib * c->nnz_int;
+    info->nnz_end = (int64_t)c->ie * c->nnz_int;
+    return MH_OK;
+}
+
+// CasOC::Problem::clipEndpointBounds (CasOCProblem.h:603-606).
+static mh_bounds clip(mh_bounds b, mh_bounds e) {
+    mh_bounds r;
+    r.lower = std::max(b.lower, e.lower);
+    r.upper = std::min(b.upper, e.upper);
+    return r;
+}
+static void put_bounds(mh_bounds b, double& lo, double& up) {
+    if (!std::isnan(b.lower) && !std::isnan(b.upper)) { lo = b.lower; up = b.upper; }
+    else { lo = -INFINITY; up = INFINITY; }
+}
+
+extern "C" int mh_get_bounds(const mh_ctx* c, double* xl, double* xu, double* gl, double* gu) {
+    if (!c || !xl || !xu) return set_err(MH_ERR_INVALID, "null argument");
+    put_bounds(c->t_init, xl[0], xu[0]);
+    put_bounds(c->t_final, xl[1], xu[1]);
+    auto fill = [&](const mh_variable_info& vi, auto col) {
+        const mh_bounds ib = clip(vi.bounds, vi.initial), fb = clip(vi.bounds, vi.final);
+        for (int k = 1; k < c->G - 1; ++k) put_bounds(vi.bounds, xl[col(k)], xu[col(k)]);
+        put_bounds(ib, xl[col(0)], xu[col(0)]);
+        put_bounds(fb, xl[col(c->G - 1)], xu[col(c->G - 1)]);
+    };
+    for (int s = 0; s < c->NS; ++s) fill(c->sinfo[s], [&](int k) { return col_state(c, k, s); });
+    for (int j = 0; j < c->NC; ++j) fill(c->cinfo[j], [&](int k) { return col_control(c, k, j); });
+    if (gl && gu)
+        for (int64_t r = 0; r < c->m; ++r) { gl[r] = 0.0; gu[r] = 0.0; }
+    return MH_OK;
+}
+
+extern "C" int mh_get_initial_guess_from_bounds(const mh_ctx* c, double* x) {
+    if (!c || !x) return set_err(MH_ERR_INVALID, "null argument");
+    std::vector<double> lo(c->n), up(c->n);
+    mh_get_bounds(c, lo.data(), up.data(), nullptr, nullptr);
+    for (int64_t i = 0; i < c->n; ++i) {  // CasOCTranscription.cpp:1124-1139
+        const double l = lo[i], u = up[i];
+        if (!std::isinf(l) && !std::isinf(u)) x[i] = 0.5 * (u + l);
+        else if (!std::isinf(l)) x[i] = l;
+        else if (!std::isinf(u)) x[i] = u;
+        else x[i] = 0;
+    }
+    return MH_OK;
+}
+
+extern "C" int mh_get_random_iterate(const mh_ctx* c, const double* rnd, double* x) {
+    if (!c || !rnd || !x) return set_err(MH_ERR_INVALID, "null argument");
+    std::vector<double> lo(c->n), up(c->n);
+    mh_get_bounds(c, lo.data(), up.data(), nullptr, nullptr);
+    for (int64_t i = 0; i < c->n; ++i) {  // CasOCTranscription.cpp:1156-1166
+        const double l = lo[i], u = up[i], r = rnd[i];
+        double v = 0.5 * (r + 1.0) * (u - l) + l;
+        if (std::isnan(v)) v = r < l ? l : (r > u ? u : r);
+        x[i] = v;
+    }
+    return MH_OK;
+}
+
+extern "C" int mh_get_jac_structure(const mh_ctx* c, int32_t* iRow, int32_t* jCol) {
+    if (!c || !iRow || !jCol) return set_err(MH_ERR_INVALID, "null argument");
+    const int step = c->scheme == MH_HERMITE_SIMPSON ? 2 : 1;
+    int64_t e = 0;
+    for (int i = 0; i < c->N; ++i) {
+        for (size_t t = 0; t < c->tpl.size(); ++t) {
+            const TplEntry& T = c->tpl[t];
+            iRow[e] = (int32_t)((int64_t)i * c->rpi + T.row);
+            int64_t col;
+            if (T.dir < 2) col = T.dir;
+            else {
+                const int j = T.dir - 2;
+                const int64_t k = (int64_t)i * step + T.pt;
+                col = j < c->NS ? col_state(c, k, j) : col_control(c, k, j - c->NS);
+            }
+            jCol[e] = (int32_t)col;
+            ++e;
+        }
+    }
+    return MH_OK;
+}
+
+// ------------------------------------------------------------------------
+// Launchers.
+// ------------------------------------------------------------------------
+template <class Z>
+static void launch_base(mh_ctx* c, const double* x) {
+    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, c->k0, c->nk};
+    hipLaunchKernelGGL(k_base<Z>, dim3((c->nk + 63) / 64), dim3(64), 0, c->stream, c->M, L, x,
+            c->d_grid, c->d_times, c->d_Y);
+}
+template <class Z>
+static void launch_fd(mh_ctx* c, const double* x) {
+    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, c->k0, c->nk};
+    const int ND = c->NI + 2;
+    const int per = c->fd == MH_FD_CENTRAL ? 32 : 64;
+    hipLaunchKernelGGL(k_fd<Z>, dim3((ND + per - 1) / per, c->nk), dim3(64), 0, c->stream, c->M, L,
+            c->fd, c->h, x, c->d_grid, c->d_Y, c->d_D);
+}
+template <class Z>
+static void launch_integrand(mh_ctx* c, const double* x) {
+    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, 0, c->G};
+    hipLaunchKernelGGL(k_integrand<Z>, dim3((c->G + 63) / 64), dim3(64), 0, c->stream, c->M, L,
+            c->GS, x, c->d_grid, c->d_quad, c->d_C);
+}
+template <class Z>
+static void launch_grad(mh_ctx* c, const double* x) {
+    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, 0, c->G};
+    const long tot = (long)c->G * (c->NI + 2);
+    hipLaunchKernelGGL(k_grad<Z>, dim3((unsigned)((tot + 63) / 64)), dim3(64), 0, c->stream, c->M, L,
+            c->GS, c->fd, c->h, x, c->d_grid, c->d_quad, c->d_grad, c->d_tpart);
+}
+
+#define DISPATCH(fn, ...)                                                  \
+    do {                                                                   \
+        if (c->size_class == 0) fn<SzSmall>(__VA_ARGS__);                  \
+        else if (c->size_class == 1) fn<SzMedium>(__VA_ARGS__);            \
+        else fn<SzLarge>(__VA_ARGS__);                                     \
+    } while (0)
+
+static int run_g(mh_ctx* c, const double* x_dev, double* g_dev) {
+    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, c->k0, c->nk};
+    Interval I{c->scheme, c->interp, c->ib, c->rpi, c->nnz_int};
+    HIPCHK(hipEventRecord(c->ev[0], c->stream));
+    DISPATCH(launch_base, c, x_dev);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->ev[1], c->stream));
+    hipLaunchKernelGGL(k_defects, dim3(c->ie - c->ib), dim3(256), 0, c->stream, L, I, x_dev,
+            c->d_times, c->d_Y, g_dev);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->ev[2], c->stream));
+    return MH_OK;
+}
+
+static int run_jac(mh_ctx* c, const double* x_dev, double* v_dev) {
+    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, c->k0, c->nk};
+    Interval I{c->scheme, c->interp, c->ib, c->rpi, c->nnz_int};
+    HIPCHK(hipEventRecord(c->ev[0], c->stream));
+    DISPATCH(launch_base, c, x_dev);
+    DISPATCH(launch_fd, c, x_dev);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->ev[1], c->stream));
+    hipLaunchKernelGGL(k_assemble, dim3(c->ie - c->ib), dim3(256), 0, c->stream, L, I, c->d_tpl,
+            x_dev, c->d_grid, c->d_times, c->d_Y, c->d_D, v_dev);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->ev[2], c->stream));
+    return MH_OK;
+}
+
+static int finish(mh_ctx* c) {
+    HIPCHK(hipEventRecord(c->ev[3], c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    float a = 0, b = 0, d = 0;
+    (void)hipEventElapsedTime(&a, c->ev[0], c->ev[3]);
+    (void)hipEventElapsedTime(&b, c->ev[0], c->ev[1]);
+    (void)hipEventElapsedTime(&d, c->ev[1], c->ev[2]);
+    c->timings[0] = a; c->timings[1] = b; c->timings[2] = d;
+    return MH_OK;
+}
+
+extern "C" int mh_eval_g(mh_ctx* c, const double* x, int, double* g) {
+    if (!c || !x || !g) return set_err(MH_ERR_INVALID, "null argument");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemcpyAsync(c->d_x, x, sizeof(double) * c->n, hipMemcpyHostToDevice, c->stream));
+    int rc = run_g(c, c->d_x, c->d_g);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(g, c->d_g, sizeof(double) * (size_t)(c->ie - c->ib) * c->rpi,
+            hipMemcpyDeviceToHost, c->stream));
+    return finish(c);
+}
+
+extern "C" int mh_eval_jac_g(mh_ctx* c, const double* x, int, double* values) {
+    if (!c || !x || !values) return set_err(MH_ERR_INVALID, "null argument");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemcpyAsync(c->d_x, x, sizeof(double) * c->n, hipMemcpyHostToDevice, c->stream));
+    int rc = run_jac(c, c->d_x, c->d_vals);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(values, c->d_vals, sizeof(double) * (size_t)(c->ie - c->ib) * c->nnz_int,
+            hipMemcpyDeviceToHost, c->stream));
+    return finish(c);
+}
+
+extern "C" int mh_eval_g_device(mh_ctx* c, const double* x_dev, double* g_dev) {
+    if (!c || !x_dev || !g_dev) return set_err(MH_ERR_INVALID, "null argument");
+    HIPCHK(hipSetDevice(c->device));
+    int rc = run_g(c, x_dev, g_dev);
+    if (rc) return rc;
+    return finish(c);
+}
+
+extern "C" int mh_eval_jac_g_device(mh_ctx* c, const double* x_dev, double* v_dev) {
+    if (!c || !x_dev || !v_dev) return set_err(MH_ERR_INVALID, "null argument");
+    HIPCHK(hipSetDevice(c->device));
+    int rc = run_jac(c, x_dev, v_dev);
+    if (rc) return rc;
+    return finish(c);
+}
+
+extern "C" int mh_eval_f(mh_ctx* c, const double* x, int, double* f) {
+    if (!c || !x || !f) return set_err(MH_ERR_INVALID, "null argument");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemcpyAsync(c->d_x, x, sizeof(double) * c->n, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipEventRecord(c->ev[0], c->stream));
+    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, 0, c->G};
+    if (c->ngoals > 0) {
+        DISPATCH(launch_integrand, c, c->d_x);
+        HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipEventRecord(c->ev[1], c->stream));
+    hipLaunchKernelGGL(k_reduce_obj, dim3(1), dim3(256), 0, c->stream, L, c->GS, 0, c->d_x, c->d_C,
+            c->d_tpart, c->d_f);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->ev[2], c->stream));
+    HIPCHK(hipMemcpyAsync(f, c->d_f, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    return finish(c);
+}
+
+extern "C" int mh_eval_grad_f(mh_ctx* c, const double* x, int, double* grad) {
+    if (!c || !x || !grad) return set_err(MH_ERR_INVALID, "null argument");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemcpyAsync(c->d_x, x, sizeof(double) * c->n, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipEventRecord(c->ev[0], c->stream));
+    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, 0, c->G};
+    HIPCHK(hipMemsetAsync(c->d_grad, 0, sizeof(double) * c->n, c->stream));
+    HIPCHK(hipMemsetAsync(c->d_tpart, 0, sizeof(double) * 2 * c->G, c->stream));
+    HIPCHK(hipMemsetAsync(c->d_C, 0, sizeof(double) * c->G * std::max(1, c->ngoals), c->stream));
+    if (c->ngoals > 0) {
+        DISPATCH(launch_integrand, c, c->d_x);
+        DISPATCH(launch_grad, c, c->d_x);
+        HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipEventRecord(c->ev[1], c->stream));
+    hipLaunchKernelGGL(k_reduce_obj, dim3(1), dim3(256), 0, c->stream, L, c->GS, 1, c->d_x, c->d_C,
+            c->d_tpart, c->d_f);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->ev[2], c->stream));
+    HIPCHK(hipMemcpyAsync(c->d_grad, c->d_f, sizeof(double) * 2, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(grad, c->d_grad, sizeof(double) * c->n, hipMemcpyDeviceToHost, c->stream));
+    return finish(c);
+}
+
+template <class Z>
+static void launch_probe(mh_ctx* c, int np, const double* in, double* out) {
+    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, 0, 0};
+    hipLaunchKernelGGL(k_dae_probe<Z>, dim3((np + 63) / 64), dim3(64), 0, c->stream, c->M, L, np, in, out);
+}
+
+extern "C" int mh_eval_dae(mh_ctx* c, int32_t np, const double* inputs, double* outputs) {
+    if (!c || !inputs || !outputs || np < 0) return set_err(MH_ERR_INVALID, "bad argument");
+    if (np == 0) return MH_OK;
+    HIPCHK(hipSetDevice(c->device));
+    double *din = nullptr, *dout = nullptr;
+    const size_t nin = (size_t)np * (1 + c->NI), nout = (size_t)np * c->NO;
+    HIPCHK(hipMalloc(&din, sizeof(double) * nin));
+    HIPCHK(hipMalloc(&dout, sizeof(double) * std::max<size_t>(nout, 1)));
+    HIPCHK(hipMemcpyAsync(din, inputs, sizeof(double) * nin, hipMemcpyHostToDevice, c->stream));
+    DISPATCH(launch_probe, c, np, din, dout);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(outputs, dout, sizeof(double) * nout, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    (void)hipFree(din);
+    (void)hipFree(dout);
+    return MH_OK;
+}
+
+extern "C" int mh_last_timings(const mh_ctx* c, double* ms3) {
+    if (!c || !ms3) return set_err(MH_ERR_INVALID, "null argument");
+    for (int i = 0; i < 3; ++i) ms3[i] = c->timings[i];
+    return MH_OK;
+}

@@ -1,0 +1,228 @@
+"""ctypes mirror of include/mocohip.h (the C-ABI drop-in boundary).
+
+The structs here are byte-for-byte the ones declared in include/mocohip.h;
+``tests/test_abi.py`` checks sizes and field offsets against the header.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(_HERE)                     # opensim-moco_amd/
+REPO_ROOT = os.path.dirname(PKG_ROOT)
+
+MH_OK, MH_ERR_INVALID, MH_ERR_HIP, MH_ERR_UNSUPPORTED, MH_ERR_ALLOC = range(5)
+
+MH_FN_CONSTANT, MH_FN_LINEAR, MH_FN_SIMMSPLINE = 0, 1, 2
+MH_AXIS_ROTATION, MH_AXIS_TRANSLATION = 0, 1
+MH_PP_FIXED, MH_PP_CONDITIONAL, MH_PP_MOVING = 0, 1, 2
+MH_ACT_MUSCLE, MH_ACT_COORDINATE = 0, 1
+MH_GOAL_CONTROL, MH_GOAL_STATE_TRACKING, MH_GOAL_FINAL_TIME, \
+    MH_GOAL_SUM_SQUARED_STATE = 0, 1, 2, 3
+MH_HERMITE_SIMPSON, MH_TRAPEZOIDAL = 0, 1
+MH_FD_CENTRAL, MH_FD_FORWARD, MH_FD_BACKWARD = 0, 1, 2
+
+i32 = C.c_int32
+f64 = C.c_double
+P = C.POINTER
+
+
+class mh_function(C.Structure):
+    _fields_ = [("kind", i32), ("coord", i32), ("knot_begin", i32),
+                ("knot_count", i32), ("a", f64), ("b", f64), ("scale", f64),
+                ("reserved", f64)]
+
+
+class mh_axis(C.Structure):
+    _fields_ = [("type", i32), ("func", i32), ("dir", f64 * 3)]
+
+
+class mh_body(C.Structure):
+    _fields_ = [("parent", i32), ("axis_begin", i32), ("axis_count", i32),
+                ("reserved", i32), ("mass", f64), ("com", f64 * 3),
+                ("inertia", f64 * 6), ("R_PF", f64 * 9), ("p_PF", f64 * 3),
+                ("R_BM", f64 * 9), ("p_BM", f64 * 3)]
+
+
+class mh_path_point(C.Structure):
+    _fields_ = [("kind", i32), ("body", i32), ("coord", i32), ("fx", i32),
+                ("fy", i32), ("fz", i32), ("loc", f64 * 3),
+                ("range", f64 * 2)]
+
+
+class mh_muscle(C.Structure):
+    _fields_ = [("point_begin", i32), ("point_count", i32),
+                ("ignore_activation_dynamics", i32),
+                ("ignore_tendon_compliance", i32),
+                ("ignore_passive_fiber_force", i32),
+                ("tendon_dynamics_implicit", i32),
+                ("max_isometric_force", f64), ("optimal_fiber_length", f64),
+                ("tendon_slack_length", f64),
+                ("pennation_angle_at_optimal", f64),
+                ("max_contraction_velocity", f64),
+                ("activation_time_constant", f64),
+                ("deactivation_time_constant", f64), ("fiber_damping", f64),
+                ("passive_fiber_strain_at_one_norm_force", f64),
+                ("tendon_strain_at_one_norm_force", f64),
+                ("active_force_width_scale", f64)]
+
+
+class mh_actuator(C.Structure):
+    _fields_ = [("kind", i32), ("target", i32), ("optimal_force", f64)]
+
+
+class mh_table(C.Structure):
+    _fields_ = [("nseg", i32), ("degree", i32), ("ncol", i32),
+                ("break_begin", i32), ("coef_begin", i32), ("reserved", i32)]
+
+
+class mh_external_force(C.Structure):
+    _fields_ = [("body", i32), ("table", i32), ("force_col", i32),
+                ("point_col", i32), ("torque_col", i32), ("reserved", i32)]
+
+
+class mh_model(C.Structure):
+    _fields_ = [("nq", i32), ("nbodies", i32), ("naxes", i32),
+                ("nfunctions", i32), ("nknots", i32), ("nmuscles", i32),
+                ("npoints", i32), ("nactuators", i32), ("ntables", i32),
+                ("nbreaks", i32), ("ncoefs", i32), ("nexternal", i32),
+                ("gravity", f64 * 3),
+                ("bodies", P(mh_body)), ("axes", P(mh_axis)),
+                ("functions", P(mh_function)), ("knot_x", P(f64)),
+                ("knot_y", P(f64)), ("muscles", P(mh_muscle)),
+                ("points", P(mh_path_point)), ("actuators", P(mh_actuator)),
+                ("tables", P(mh_table)), ("table_breaks", P(f64)),
+                ("table_coefs", P(f64)),
+                ("external", P(mh_external_force))]
+
+
+class mh_bounds(C.Structure):
+    _fields_ = [("lower", f64), ("upper", f64)]
+
+
+class mh_variable_info(C.Structure):
+    _fields_ = [("bounds", mh_bounds), ("initial", mh_bounds),
+                ("final", mh_bounds)]
+
+
+class mh_goal(C.Structure):
+    _fields_ = [("kind", i32), ("table", i32), ("term_begin", i32),
+                ("term_count", i32), ("exponent", i32), ("reserved", i32),
+                ("weight", f64)]
+
+
+class mh_problem(C.Structure):
+    _fields_ = [("model", mh_model), ("time_initial", mh_bounds),
+                ("time_final", mh_bounds),
+                ("state_infos", P(mh_variable_info)),
+                ("control_infos", P(mh_variable_info)),
+                ("ngoals", i32), ("nterms", i32), ("goals", P(mh_goal)),
+                ("goal_index", P(i32)), ("goal_column", P(i32)),
+                ("goal_weight", P(f64))]
+
+
+class mh_options(C.Structure):
+    _fields_ = [("num_mesh_intervals", i32), ("transcription", i32),
+                ("interpolate_control_midpoints", i32),
+                ("finite_difference_scheme", i32), ("fd_step", f64),
+                ("interval_begin", i32), ("interval_end", i32),
+                ("device", i32), ("reserved", i32)]
+
+
+class mh_nlp_info(C.Structure):
+    _fields_ = [("n", C.c_int64), ("m", C.c_int64), ("nnz_jac_g", C.c_int64),
+                ("nnz_h_lag", C.c_int64), ("num_grid_points", C.c_int64),
+                ("num_states", C.c_int64), ("num_controls", C.c_int64),
+                ("row_begin", C.c_int64), ("row_end", C.c_int64),
+                ("nnz_begin", C.c_int64), ("nnz_end", C.c_int64)]
+
+
+# Exported entry points of libmocohip.so and their signatures; the
+# C-ABI test checks every one is exported (and matches include/mocohip.h).
+MOCOHIP_SYMBOLS = {
+    "mh_abi_version": (i32, []),
+    "mh_last_error": (C.c_char_p, []),
+    "mh_create": (i32, [P(mh_problem), P(mh_options), P(C.c_void_p)]),
+    "mh_destroy": (None, [C.c_void_p]),
+    "mh_get_nlp_info": (i32, [C.c_void_p, P(mh_nlp_info)]),
+    "mh_get_bounds": (i32, [C.c_void_p, P(f64), P(f64), P(f64), P(f64)]),
+    "mh_get_initial_guess_from_bounds": (i32, [C.c_void_p, P(f64)]),
+    "mh_get_random_iterate": (i32, [C.c_void_p, P(f64), P(f64)]),
+    "mh_get_jac_structure": (i32, [C.c_void_p, P(i32), P(i32)]),
+    "mh_eval_f": (i32, [C.c_void_p, P(f64), C.c_int, P(f64)]),
+    "mh_eval_grad_f": (i32, [C.c_void_p, P(f64), C.c_int, P(f64)]),
+    "mh_eval_g": (i32, [C.c_void_p, P(f64), C.c_int, P(f64)]),
+    "mh_eval_jac_g": (i32, [C.c_void_p, P(f64), C.c_int, P(f64)]),
+    "mh_eval_g_device": (i32, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "mh_eval_jac_g_device": (i32, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "mh_eval_dae": (i32, [C.c_void_p, i32, P(f64), P(f64)]),
+    "mh_last_timings": (i32, [C.c_void_p, P(f64)]),
+}
+
+ORACLE_SYMBOLS = {
+    "orc_last_error": (C.c_char_p, []),
+    "orc_create": (i32, [P(mh_problem), P(mh_options), P(C.c_void_p)]),
+    "orc_destroy": (None, [C.c_void_p]),
+    "orc_set_threads": (None, [C.c_void_p, C.c_int]),
+    "orc_get_nlp_info": (i32, [C.c_void_p, P(mh_nlp_info)]),
+    "orc_get_bounds": (i32, [C.c_void_p, P(f64), P(f64), P(f64), P(f64)]),
+    "orc_get_initial_guess_from_bounds": (i32, [C.c_void_p, P(f64)]),
+    "orc_get_random_iterate": (i32, [C.c_void_p, P(f64), P(f64)]),
+    "orc_get_jac_structure": (i32, [C.c_void_p, P(i32), P(i32)]),
+    "orc_eval_f": (i32, [C.c_void_p, P(f64), P(f64)]),
+    "orc_eval_grad_f": (i32, [C.c_void_p, P(f64), P(f64)]),
+    "orc_eval_g": (i32, [C.c_void_p, P(f64), P(f64)]),
+    "orc_eval_jac_g": (i32, [C.c_void_p, P(f64), P(f64)]),
+    "orc_eval_dae": (i32, [C.c_void_p, i32, P(f64), P(f64)]),
+    "orc_dgf_curve": (f64, [P(mh_muscle), C.c_int, f64]),
+    "orc_muscle_length_speed": (i32, [C.c_void_p, C.c_int, P(f64), P(f64),
+                                      P(f64)]),
+    "orc_eval_function": (i32, [C.c_void_p, C.c_int, f64, P(f64)]),
+}
+
+LIBMOCOHIP_PATH = os.path.join(PKG_ROOT, "csrc", "build", "libmocohip.so")
+LIBORACLE_PATH = os.path.join(REPO_ROOT, "oracle", "build", "liboracle.so")
+
+
+def _bind(lib, table):
+    for name, (res, args) in table.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+_libs: dict = {}
+
+
+def load_mocohip(path: str | None = None):
+    """Load the product library.  Raises if it is missing: there is no CPU
+    fallback for the hot path."""
+    path = path or LIBMOCOHIP_PATH
+    if path not in _libs:
+        if not os.path.exists(path):
+            raise RuntimeError(
+                f"libmocohip.so not built at {path}; run "
+                "`python -c 'import __graft_entry__ as g; g.build()'`")
+        _libs[path] = _bind(C.CDLL(path), MOCOHIP_SYMBOLS)
+    return _libs[path]
+
+
+def load_oracle(path: str | None = None):
+    """Load the CPU oracle (test infrastructure only)."""
+    path = path or LIBORACLE_PATH
+    if path not in _libs:
+        if not os.path.exists(path):
+            raise RuntimeError(f"liboracle.so not built at {path}")
+        _libs[path] = _bind(C.CDLL(path), ORACLE_SYMBOLS)
+    return _libs[path]
+
+
+def dptr(a):
+    """ctypes double* of a contiguous float64 numpy array."""
+    return a.ctypes.data_as(P(f64))
+
+
+def iptr(a):
+    return a.ctypes.data_as(P(i32))

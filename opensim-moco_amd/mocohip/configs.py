@@ -1,0 +1,132 @@
+"""The BASELINE.json configurations as MocoStudy builders.
+
+  sliding_mass        configs[0]: exampleSlidingMass (Moco/Examples/C++/
+                      exampleSlidingMass/exampleSlidingMass.cpp:35-90)
+  double_pendulum     configs[1]: ModelFactory::createNLinkPendulum(2)
+                      (Moco/Moco/Components/ModelFactory.cpp:33-89) with the
+                      bounds of testImplicit.cpp:63-75
+  gait10dof18musc     configs[2]: MocoTrack gait10dof18musc
+                      (Moco/Tests/testMocoTrack.cpp:46-68) with the muscles
+                      replaced by DeGrooteFregly2016Muscle
+                      (ModOpReplaceMusclesWithDeGrooteFregly2016) instead of
+                      removed, plus ModOpAddReserves(100) and the GRF
+                      ExternalLoads; MocoTrack settings from MocoTrack.cpp:54-132.
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+from typing import Optional
+
+import numpy as np
+
+from .model import (Body, Coordinate, CoordinateActuator, DataTable,
+                    ExternalForce, Joint, Model, model_from_dict)
+from .osim import add_reserves
+from .problem import (MocoControlGoal, MocoFinalTimeGoal, MocoProblem,
+                      MocoStateTrackingGoal)
+from .solver import MocoHipSolver, MocoStudy
+
+DATA = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data")
+
+
+def sliding_mass(num_mesh_intervals: int = 50) -> MocoStudy:
+    m = Model("sliding_mass", gravity=(0, 0, 0))
+    m.add_body(Body("body", 2.0, (0, 0, 0), (0, 0, 0, 0, 0, 0)))
+    pos = Coordinate("position", (-math.inf, math.inf), "translational", path="/slider/position")
+    m.add_joint(Joint.slider("slider", "ground", "body", pos))
+    m.add_coordinate_actuator(CoordinateActuator("actuator", "position", 1.0, path="/actuator"))
+    p = MocoProblem(m)
+    p.set_time_bounds(0.0, (0.0, 5.0))
+    p.set_state_info("/slider/position/value", (-5, 5), 0, 1)
+    p.set_state_info("/slider/position/speed", (-50, 50), 0, 0)
+    p.set_control_info("/actuator", (-50, 50))
+    p.add_goal(MocoFinalTimeGoal())
+    s = MocoHipSolver(num_mesh_intervals=num_mesh_intervals)
+    return MocoStudy(p, s)
+
+
+def n_link_pendulum(num_links: int) -> Model:
+    """ModelFactory::createNLinkPendulum."""
+    m = Model({1: "pendulum", 2: "double_pendulum"}.get(num_links, f"{num_links}_link_pendulum"))
+    prev = "ground"
+    for i in range(num_links):
+        m.add_body(Body(f"b{i}", 1.0, (0, 0, 0), (1, 1, 1, 0, 0, 0)))
+        q = Coordinate(f"q{i}", (-math.pi / 2, math.pi / 2))
+        m.add_joint(Joint.pin(f"j{i}", prev, f"b{i}", q, loc_in_child=(-1, 0, 0)))
+        prev = f"b{i}"
+    for i in range(num_links):
+        m.add_coordinate_actuator(CoordinateActuator(f"tau{i}", f"q{i}", 1.0, path=f"/tau{i}"))
+    return m
+
+
+def double_pendulum(num_mesh_intervals: int = 100, scheme: str = "hermite-simpson") -> MocoStudy:
+    m = n_link_pendulum(2)
+    p = MocoProblem(m)
+    p.set_time_bounds(0.0, (0.0, 5.0))
+    p.set_state_info("/jointset/j0/q0/value", (-10, 10), 0)
+    p.set_state_info("/jointset/j0/q0/speed", (-50, 50), 0, 0)
+    p.set_state_info("/jointset/j1/q1/value", (-10, 10), 0)
+    p.set_state_info("/jointset/j1/q1/speed", (-50, 50), 0, 0)
+    p.set_control_info("/tau0", (-100, 100))
+    p.set_control_info("/tau1", (-100, 100))
+    p.add_goal(MocoFinalTimeGoal(weight=0.001))
+    p.add_goal(MocoControlGoal(weight=1e-3))
+    s = MocoHipSolver(num_mesh_intervals=num_mesh_intervals, transcription_scheme=scheme)
+    return MocoStudy(p, s)
+
+
+def _load(name):
+    with open(os.path.join(DATA, name)) as fh:
+        return json.load(fh)
+
+
+def gait10dof18musc_model(muscles: bool = True, tendon_compliance: bool = False,
+                          reserves: float = 100.0, external_loads: bool = True) -> Model:
+    m = model_from_dict(_load("gait10dof18musc.json"))
+    if not muscles:
+        m.actuators = [a for a in m.actuators if not hasattr(a, "points")]
+        m.muscles = []
+    for mu in m.muscles:
+        mu.ignore_tendon_compliance = not tendon_compliance
+    if reserves:
+        add_reserves(m, reserves)
+    if external_loads:
+        grf = _load("walk_gait1018_subject01_grf.json")
+        cols = {k: np.asarray(v) for k, v in grf["columns"].items()}
+        m.add_table(DataTable("grf", np.asarray(grf["time"]), cols, degree=3))
+        for ef in grf["external_forces"]:
+            if ef["force_expressed_in_body"] != "ground" or ef["point_expressed_in_body"] != "ground":
+                raise NotImplementedError("ExternalForce must be expressed in ground")
+            m.add_external_force(ExternalForce(ef["name"], ef["body"], "grf",
+                                               ef["force_identifier"], ef["point_identifier"],
+                                               ef["torque_identifier"]))
+    return m
+
+
+def gait10dof18musc(num_mesh_intervals: int = 200, muscles: bool = True,
+                    tendon_compliance: bool = False,
+                    fd_scheme: str = "forward") -> MocoStudy:
+    """MocoTrack gait10dof18musc (config 3).  MocoTrack: states tracking goal
+    (weight 1, GCVSpline reference), control effort goal (0.001), time
+    [0.01, 1.3], explicit dynamics, forward FD (MocoTrack.cpp:54-132)."""
+    m = gait10dof18musc_model(muscles=muscles, tendon_compliance=tendon_compliance)
+    ref = _load("walk_gait1018_state_reference.json")
+    cols = {k: np.asarray(v) for k, v in ref["columns"].items()}
+    m.add_table(DataTable("state_reference", np.asarray(ref["time"]), cols, degree=5))
+    p = MocoProblem(m)
+    p.add_goal(MocoStateTrackingGoal("state_tracking", 1.0, DataTable(
+        "state_reference", np.asarray(ref["time"]), cols, degree=5)))
+    p.add_goal(MocoControlGoal("control_effort", 0.001))
+    p.set_time_bounds(0.01, 1.3)
+    s = MocoHipSolver(num_mesh_intervals=num_mesh_intervals,
+                      optim_finite_difference_scheme=fd_scheme)
+    return MocoStudy(p, s)
+
+
+CONFIGS = {
+    "sliding_mass": sliding_mass,
+    "double_pendulum": double_pendulum,
+    "gait10dof18musc": gait10dof18musc,
+}

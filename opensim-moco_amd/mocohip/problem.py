@@ -1,0 +1,243 @@
+"""MocoProblem / MocoProblemRep mirror: goals, bounds rules, and lowering of
+a problem to the C-ABI ``mh_problem`` struct.
+
+Default-bound rules restate MocoProblemRep::initialize
+(Moco/Moco/MocoProblemRep.cpp:306-427) and MocoPhase defaults
+(Moco/Moco/MocoProblem.cpp:30-43).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import abi
+from .model import CompiledModel, CoordinateActuator, DataTable, \
+    DeGrooteFregly2016Muscle, Model
+
+NAN = float("nan")
+
+
+@dataclass
+class MocoBounds:
+    lower: float = NAN
+    upper: float = NAN
+
+    @staticmethod
+    def of(b) -> "MocoBounds":
+        if b is None:
+            return MocoBounds()
+        if isinstance(b, MocoBounds):
+            return b
+        if isinstance(b, (int, float)):
+            return MocoBounds(float(b), float(b))
+        lo, hi = b
+        return MocoBounds(float(lo), float(hi))
+
+    def is_set(self) -> bool:
+        return not (math.isnan(self.lower) or math.isnan(self.upper))
+
+
+@dataclass
+class MocoVariableInfo:
+    bounds: MocoBounds = field(default_factory=MocoBounds)
+    initial: MocoBounds = field(default_factory=MocoBounds)
+    final: MocoBounds = field(default_factory=MocoBounds)
+
+
+# ---------------------------------------------------------------- goals ----
+@dataclass
+class MocoControlGoal:
+    """MocoControlGoal (Moco/Moco/MocoGoal/MocoControlGoal.cpp:54-131)."""
+    name: str = "control_effort"
+    weight: float = 1.0
+    exponent: int = 2
+    control_weights: Dict[str, float] = field(default_factory=dict)
+
+
+@dataclass
+class MocoStateTrackingGoal:
+    """MocoStateTrackingGoal (MocoStateTrackingGoal.cpp:27-117).  The
+    reference is a DataTable whose column labels are state paths."""
+    name: str = "state_tracking"
+    weight: float = 1.0
+    reference: Optional[DataTable] = None
+    state_weights: Dict[str, float] = field(default_factory=dict)
+
+
+@dataclass
+class MocoFinalTimeGoal:
+    name: str = "final_time"
+    weight: float = 1.0
+
+
+@dataclass
+class MocoSumSquaredStateGoal:
+    name: str = "sum_squared_state"
+    weight: float = 1.0
+    state_weights: Dict[str, float] = field(default_factory=dict)
+
+
+class MocoProblem:
+    """Single-phase MocoProblem (MocoProblem.h)."""
+
+    def __init__(self, model: Optional[Model] = None):
+        self.model = model
+        self.time_initial = MocoBounds()
+        self.time_final = MocoBounds()
+        self.state_infos: Dict[str, MocoVariableInfo] = {}
+        self.control_infos: Dict[str, MocoVariableInfo] = {}
+        self.goals: List[object] = []
+        self.default_speed_bounds = MocoBounds(-50.0, 50.0)
+        self.bound_activation_from_excitation = True
+
+    def set_model(self, model: Model):
+        self.model = model
+
+    def set_time_bounds(self, initial, final):
+        self.time_initial = MocoBounds.of(initial)
+        self.time_final = MocoBounds.of(final)
+
+    def set_state_info(self, name, bounds=None, initial=None, final=None):
+        self.state_infos[name] = MocoVariableInfo(
+            MocoBounds.of(bounds), MocoBounds.of(initial), MocoBounds.of(final))
+
+    def set_control_info(self, name, bounds=None, initial=None, final=None):
+        self.control_infos[name] = MocoVariableInfo(
+            MocoBounds.of(bounds), MocoBounds.of(initial), MocoBounds.of(final))
+
+    def add_goal(self, goal):
+        self.goals.append(goal)
+        return goal
+
+    def create_rep(self) -> "ProblemRep":
+        return ProblemRep(self)
+
+
+def _vi(info: MocoVariableInfo) -> abi.mh_variable_info:
+    v = abi.mh_variable_info()
+    for dst, src in ((v.bounds, info.bounds), (v.initial, info.initial),
+                     (v.final, info.final)):
+        dst.lower, dst.upper = src.lower, src.upper
+    return v
+
+
+class ProblemRep:
+    """MocoProblemRep: resolves default bounds and lowers to mh_problem."""
+
+    def __init__(self, problem: MocoProblem):
+        self.problem = problem
+        model = problem.model
+        self.compiled: CompiledModel = model.compile()
+        self.state_names = self.compiled.state_names
+        self.control_names = self.compiled.control_names
+        sinfo: Dict[str, MocoVariableInfo] = {}
+        cinfo: Dict[str, MocoVariableInfo] = {}
+        for k, v in problem.state_infos.items():
+            sinfo[k] = MocoVariableInfo(v.bounds, v.initial, v.final)
+        for k, v in problem.control_infos.items():
+            cinfo[k] = MocoVariableInfo(v.bounds, v.initial, v.final)
+        # statebounds_ outputs: DGF normalized tendon force in [0, 5]
+        # (DeGrooteFregly2016Muscle.h:131-132,304-305).
+        for m in model.muscles:
+            if not m.ignore_tendon_compliance:
+                nm = m.path + "/normalized_tendon_force"
+                info = sinfo.setdefault(nm, MocoVariableInfo())
+                if not info.bounds.is_set():
+                    info.bounds = MocoBounds(0.0, 5.0)
+        # coordinates: range; speeds: default speed bounds (:336-362)
+        for c in model.coordinates():
+            vn, sn = c.path + "/value", c.path + "/speed"
+            info = sinfo.setdefault(vn, MocoVariableInfo())
+            if not info.bounds.is_set():
+                info.bounds = MocoBounds(float(c.range[0]), float(c.range[1]))
+            info = sinfo.setdefault(sn, MocoVariableInfo())
+            if not info.bounds.is_set():
+                info.bounds = problem.default_speed_bounds
+        # controls from actuator min/max; activation from excitation (:394-427)
+        for a in model.actuators:
+            info = cinfo.setdefault(a.path, MocoVariableInfo())
+            if not info.bounds.is_set():
+                info.bounds = MocoBounds(float(a.min_control), float(a.max_control))
+            if (problem.bound_activation_from_excitation and
+                    isinstance(a, DeGrooteFregly2016Muscle) and
+                    not a.ignore_activation_dynamics):
+                an = a.path + "/activation"
+                ai = sinfo.setdefault(an, MocoVariableInfo())
+                if not ai.bounds.is_set():
+                    ai.bounds = info.bounds
+        self.state_infos = [sinfo.get(n, MocoVariableInfo()) for n in self.state_names]
+        self.control_infos = [cinfo.get(n, MocoVariableInfo()) for n in self.control_names]
+
+        # goals
+        goals, gidx, gcol, gw = [], [], [], []
+        sidx = {n: i for i, n in enumerate(self.state_names)}
+        cidx = {n: i for i, n in enumerate(self.control_names)}
+        self.extra_tables: List[DataTable] = []
+        for g in problem.goals:
+            gs = abi.mh_goal()
+            gs.weight = float(g.weight)
+            gs.term_begin = len(gidx)
+            gs.table = -1
+            gs.exponent = 2
+            if isinstance(g, MocoControlGoal):
+                gs.kind = abi.MH_GOAL_CONTROL
+                gs.exponent = int(g.exponent)
+                if gs.exponent < 2:
+                    raise ValueError("Exponent must be 2 or greater.")
+                for n in self.control_names:
+                    w = float(g.control_weights.get(n, 1.0))
+                    if w != 0.0:
+                        gidx.append(cidx[n]); gcol.append(-1); gw.append(w)
+            elif isinstance(g, MocoStateTrackingGoal):
+                gs.kind = abi.MH_GOAL_STATE_TRACKING
+                ref = g.reference
+                if ref.name not in self.compiled.table_index:
+                    raise ValueError(f"reference table {ref.name} not in model")
+                gs.table = self.compiled.table_index[ref.name]
+                cols = self.compiled.table_columns[ref.name]
+                for ci, n in enumerate(cols):
+                    if n not in sidx:
+                        raise ValueError(f"State reference '{n}' unrecognized.")
+                    gidx.append(sidx[n]); gcol.append(ci)
+                    gw.append(float(g.state_weights.get(n, 1.0)))
+            elif isinstance(g, MocoFinalTimeGoal):
+                gs.kind = abi.MH_GOAL_FINAL_TIME
+            elif isinstance(g, MocoSumSquaredStateGoal):
+                gs.kind = abi.MH_GOAL_SUM_SQUARED_STATE
+                for n in self.state_names:
+                    w = float(g.state_weights.get(n, 1.0))
+                    if w != 0.0:
+                        gidx.append(sidx[n]); gcol.append(-1); gw.append(w)
+            else:
+                raise TypeError(f"unsupported goal {type(g).__name__}")
+            gs.term_count = len(gidx) - gs.term_begin
+            goals.append(gs)
+
+        self._sinfo = (abi.mh_variable_info * max(1, len(self.state_infos)))(
+            *[_vi(i) for i in self.state_infos])
+        self._cinfo = (abi.mh_variable_info * max(1, len(self.control_infos)))(
+            *[_vi(i) for i in self.control_infos])
+        self._goals = (abi.mh_goal * max(1, len(goals)))(*goals)
+        self._gidx = np.ascontiguousarray(gidx + [0], np.int32)
+        self._gcol = np.ascontiguousarray(gcol + [0], np.int32)
+        self._gw = np.ascontiguousarray(gw + [0.0], float)
+        p = abi.mh_problem()
+        p.model = self.compiled.struct
+        p.time_initial.lower, p.time_initial.upper = problem.time_initial.lower, problem.time_initial.upper
+        p.time_final.lower, p.time_final.upper = problem.time_final.lower, problem.time_final.upper
+        p.state_infos = self._sinfo
+        p.control_infos = self._cinfo
+        p.ngoals = len(goals)
+        p.nterms = len(gidx)
+        p.goals = self._goals
+        p.goal_index = abi.iptr(self._gidx)
+        p.goal_column = abi.iptr(self._gcol)
+        p.goal_weight = abi.dptr(self._gw)
+        self.struct = p
+        self.num_states = len(self.state_names)
+        self.num_controls = len(self.control_names)
+        self.nq = self.compiled.nq

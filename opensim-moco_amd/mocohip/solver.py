@@ -1,0 +1,235 @@
+"""MocoSolver plugin mirror and NLP wrappers over the C ABI.
+
+``MocoHipSolver`` mirrors the property surface of MocoDirectCollocationSolver
+/ MocoCasADiSolver that the hot path consumes
+(Moco/Moco/MocoDirectCollocationSolver.h:90-153,
+ Moco/Moco/MocoCasADiSolver/MocoCasADiSolver.h:115-159; defaults at
+ MocoDirectCollocationSolver.cpp:23-43 and MocoCasADiSolver.cpp:37-49).
+
+``HipNLP`` is the IPOPT-facing NLP (the methods of tropter's
+IPOPTSolver::TNLP, IPOPTSolver.cpp:302-447) backed by libmocohip.so.
+``OracleNLP`` is the same interface backed by the CPU oracle; it exists for
+tests and for bench.py's cpu_baseline leg only.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+from . import abi
+from .problem import MocoProblem, ProblemRep
+
+_SCHEMES = {"hermite-simpson": abi.MH_HERMITE_SIMPSON,
+            "trapezoidal": abi.MH_TRAPEZOIDAL}
+_FD = {"central": abi.MH_FD_CENTRAL, "forward": abi.MH_FD_FORWARD,
+       "backward": abi.MH_FD_BACKWARD}
+
+
+@dataclass
+class MocoHipSolver:
+    num_mesh_intervals: int = 100
+    transcription_scheme: str = "hermite-simpson"
+    interpolate_control_midpoints: bool = True
+    multibody_dynamics_mode: str = "explicit"
+    optim_finite_difference_scheme: str = "central"
+    optim_sparsity_detection: str = "none"
+    fd_step: float = 1e-8
+    device: int = 0
+
+    def options(self, interval_begin: int = 0, interval_end: int = 0) -> abi.mh_options:
+        if self.transcription_scheme not in _SCHEMES:
+            raise ValueError(f"transcription_scheme {self.transcription_scheme!r} "
+                             "not in {'trapezoidal', 'hermite-simpson'}")
+        if self.optim_finite_difference_scheme not in _FD:
+            raise ValueError("optim_finite_difference_scheme must be one of "
+                             "central, forward, backward")
+        if self.multibody_dynamics_mode != "explicit":
+            raise NotImplementedError("implicit multibody dynamics: not yet on the HIP path")
+        if self.optim_sparsity_detection != "none":
+            raise NotImplementedError("sparsity detection: not yet on the HIP path")
+        o = abi.mh_options()
+        o.num_mesh_intervals = int(self.num_mesh_intervals)
+        o.transcription = _SCHEMES[self.transcription_scheme]
+        o.interpolate_control_midpoints = int(bool(self.interpolate_control_midpoints))
+        o.finite_difference_scheme = _FD[self.optim_finite_difference_scheme]
+        o.fd_step = float(self.fd_step)
+        o.interval_begin = int(interval_begin)
+        o.interval_end = int(interval_end)
+        o.device = int(self.device)
+        return o
+
+
+class _NLPBase:
+    prefix = ""
+
+    def __init__(self, rep: ProblemRep, opts: abi.mh_options):
+        self.rep = rep
+        self.opts = opts
+        self.ctx = C.c_void_p()
+        self._create()
+        info = abi.mh_nlp_info()
+        self._check(self._fn("get_nlp_info")(self.ctx, C.byref(info)))
+        self.info = info
+        self.n, self.m, self.nnz = int(info.n), int(info.m), int(info.nnz_jac_g)
+        self.G = int(info.num_grid_points)
+        self.NS, self.NC = int(info.num_states), int(info.num_controls)
+        self.NQ = rep.nq
+        self.row_begin, self.row_end = int(info.row_begin), int(info.row_end)
+        self.nnz_begin, self.nnz_end = int(info.nnz_begin), int(info.nnz_end)
+
+    # -- plumbing
+    def _fn(self, name):
+        return getattr(self.lib, self.prefix + name)
+
+    def _check(self, rc):
+        if rc != 0:
+            err = self._fn("last_error")()
+            raise RuntimeError(f"{self.prefix}: error {rc}: {err.decode() if err else ''}")
+
+    def _create(self):
+        self._check(self._fn("create")(C.byref(self.rep.struct), C.byref(self.opts),
+                                       C.byref(self.ctx)))
+
+    def close(self):
+        if self.ctx:
+            self._fn("destroy")(self.ctx)
+            self.ctx = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- TNLP surface
+    def bounds(self):
+        xl, xu = np.empty(self.n), np.empty(self.n)
+        gl, gu = np.empty(max(self.m, 1)), np.empty(max(self.m, 1))
+        self._check(self._fn("get_bounds")(self.ctx, abi.dptr(xl), abi.dptr(xu),
+                                           abi.dptr(gl), abi.dptr(gu)))
+        return xl, xu, gl[:self.m], gu[:self.m]
+
+    def initial_guess_from_bounds(self):
+        x = np.empty(self.n)
+        self._check(self._fn("get_initial_guess_from_bounds")(self.ctx, abi.dptr(x)))
+        return x
+
+    def random_iterate(self, rand: np.ndarray):
+        rand = np.ascontiguousarray(rand, float)
+        assert rand.shape == (self.n,)
+        x = np.empty(self.n)
+        self._check(self._fn("get_random_iterate")(self.ctx, abi.dptr(rand), abi.dptr(x)))
+        return x
+
+    def jac_structure(self):
+        ir = np.empty(max(self.nnz, 1), np.int32)
+        jc = np.empty(max(self.nnz, 1), np.int32)
+        self._check(self._fn("get_jac_structure")(self.ctx, abi.iptr(ir), abi.iptr(jc)))
+        return ir[:self.nnz], jc[:self.nnz]
+
+    def eval_dae(self, inputs: np.ndarray) -> np.ndarray:
+        inputs = np.ascontiguousarray(inputs, float)
+        npts = inputs.shape[0]
+        assert inputs.shape[1] == 1 + self.NS + self.NC
+        out = np.empty((npts, self.NS - self.NQ))
+        self._check(self._fn("eval_dae")(self.ctx, npts, abi.dptr(inputs), abi.dptr(out)))
+        return out
+
+
+class HipNLP(_NLPBase):
+    """NLP backed by libmocohip.so (the product path)."""
+    prefix = "mh_"
+
+    def __init__(self, rep: ProblemRep, opts: abi.mh_options, lib=None):
+        self.lib = lib or abi.load_mocohip()
+        super().__init__(rep, opts)
+
+    def eval_f(self, x, new_x=True):
+        x = np.ascontiguousarray(x, float)
+        f = np.zeros(1)
+        self._check(self.lib.mh_eval_f(self.ctx, abi.dptr(x), int(new_x), abi.dptr(f)))
+        return float(f[0])
+
+    def eval_grad_f(self, x, new_x=True):
+        x = np.ascontiguousarray(x, float)
+        g = np.empty(self.n)
+        self._check(self.lib.mh_eval_grad_f(self.ctx, abi.dptr(x), int(new_x), abi.dptr(g)))
+        return g
+
+    def eval_g(self, x, new_x=True):
+        x = np.ascontiguousarray(x, float)
+        g = np.empty(max(self.row_end - self.row_begin, 1))
+        self._check(self.lib.mh_eval_g(self.ctx, abi.dptr(x), int(new_x), abi.dptr(g)))
+        return g[:self.row_end - self.row_begin]
+
+    def eval_jac_g(self, x, new_x=True):
+        x = np.ascontiguousarray(x, float)
+        v = np.empty(max(self.nnz_end - self.nnz_begin, 1))
+        self._check(self.lib.mh_eval_jac_g(self.ctx, abi.dptr(x), int(new_x), abi.dptr(v)))
+        return v[:self.nnz_end - self.nnz_begin]
+
+    def eval_g_device(self, x_ptr: int, g_ptr: int):
+        self._check(self.lib.mh_eval_g_device(self.ctx, C.c_void_p(x_ptr), C.c_void_p(g_ptr)))
+
+    def eval_jac_g_device(self, x_ptr: int, v_ptr: int):
+        self._check(self.lib.mh_eval_jac_g_device(self.ctx, C.c_void_p(x_ptr), C.c_void_p(v_ptr)))
+
+    def last_timings(self):
+        t = np.zeros(3)
+        self._check(self.lib.mh_last_timings(self.ctx, abi.dptr(t)))
+        return t
+
+
+class OracleNLP(_NLPBase):
+    """NLP backed by the CPU oracle — TEST INFRASTRUCTURE / CPU BASELINE."""
+    prefix = "orc_"
+
+    def __init__(self, rep: ProblemRep, opts: abi.mh_options, threads: int = 1):
+        self.lib = abi.load_oracle()
+        super().__init__(rep, opts)
+        self.lib.orc_set_threads(self.ctx, int(threads))
+
+    def eval_f(self, x, new_x=True):
+        x = np.ascontiguousarray(x, float)
+        f = np.zeros(1)
+        self._check(self.lib.orc_eval_f(self.ctx, abi.dptr(x), abi.dptr(f)))
+        return float(f[0])
+
+    def eval_grad_f(self, x, new_x=True):
+        x = np.ascontiguousarray(x, float)
+        g = np.empty(self.n)
+        self._check(self.lib.orc_eval_grad_f(self.ctx, abi.dptr(x), abi.dptr(g)))
+        return g
+
+    def eval_g(self, x, new_x=True):
+        x = np.ascontiguousarray(x, float)
+        g = np.empty(max(self.m, 1))
+        self._check(self.lib.orc_eval_g(self.ctx, abi.dptr(x), abi.dptr(g)))
+        return g[:self.m]
+
+    def eval_jac_g(self, x, new_x=True):
+        x = np.ascontiguousarray(x, float)
+        v = np.empty(max(self.nnz, 1))
+        self._check(self.lib.orc_eval_jac_g(self.ctx, abi.dptr(x), abi.dptr(v)))
+        return v[:self.nnz]
+
+
+class MocoStudy:
+    """MocoStudy mirror: owns a problem and a solver; ``create_nlp`` builds
+    the transcription on the HIP path (MocoStudy.cpp:79-101)."""
+
+    def __init__(self, problem: Optional[MocoProblem] = None,
+                 solver: Optional[MocoHipSolver] = None):
+        self.problem = problem or MocoProblem()
+        self.solver = solver or MocoHipSolver()
+
+    def init_solver(self) -> MocoHipSolver:
+        self.solver = MocoHipSolver()
+        return self.solver
+
+    def create_nlp(self, interval_begin: int = 0, interval_end: int = 0) -> HipNLP:
+        rep = self.problem.create_rep()
+        return HipNLP(rep, self.solver.options(interval_begin, interval_end))

@@ -1,0 +1,1556 @@
+/* oracle.c — CPU restatement of the Moco direct-collocation hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY (see oracle.h).  Plain C99, serial reference
+ * arithmetic, optional OpenMP fan-out over grid points mirroring CasADi's
+ * map(N, "thread", T) (CasOCTranscription.cpp:1179-1184).
+ *
+ * Each function cites the reference file:line it restates.  Third-party
+ * arithmetic that is not in /root/reference (Simbody forward dynamics,
+ * OpenSim GeometryPath / SimmSpline, CasADi FiniteDiff) is restated from the
+ * published algorithms; see DESIGN.md §Oracle for the parity status of each.
+ */
+#include "oracle.h"
+
+#include <float.h>
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+static __thread char g_err[512];
+const char* orc_last_error(void) { return g_err; }
+static int fail(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof g_err, fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+/* ======================================================================== */
+/* Small 3-vector / 3x3 helpers (row-major matrices).                        */
+/* ======================================================================== */
+typedef struct { double w[3], v[3]; } sv6; /* spatial vector about ground origin */
+
+static void mat_mul(const double* A, const double* B, double* C) {
+    double T[9];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            T[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] +
+                           A[3 * i + 2] * B[6 + j];
+    memcpy(C, T, sizeof T);
+}
+static void mat_mul_bt(const double* A, const double* B, double* C) { /* A*B^T */
+    double T[9];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            T[3 * i + j] = A[3 * i] * B[3 * j] + A[3 * i + 1] * B[3 * j + 1] +
+                           A[3 * i + 2] * B[3 * j + 2];
+    memcpy(C, T, sizeof T);
+}
+static void mat_vec(const double* A, const double* x, double* y) {
+    double t0 = A[0] * x[0] + A[1] * x[1] + A[2] * x[2];
+    double t1 = A[3] * x[0] + A[4] * x[1] + A[5] * x[2];
+    double t2 = A[6] * x[0] + A[7] * x[1] + A[8] * x[2];
+    y[0] = t0; y[1] = t1; y[2] = t2;
+}
+static void cross(const double* a, const double* b, double* c) {
+    double t0 = a[1] * b[2] - a[2] * b[1];
+    double t1 = a[2] * b[0] - a[0] * b[2];
+    double t2 = a[0] * b[1] - a[1] * b[0];
+    c[0] = t0; c[1] = t1; c[2] = t2;
+}
+static double dot3(const double* a, const double* b) {
+    return a[0] * b[0] + a[1] * b[1] + a[2] * b[2];
+}
+/* Rodrigues rotation about unit axis a by angle t. */
+static void axis_rotation(const double* a, double t, double* R) {
+    double c = cos(t), s = sin(t), k = 1.0 - c;
+    R[0] = c + k * a[0] * a[0];
+    R[1] = k * a[0] * a[1] - s * a[2];
+    R[2] = k * a[0] * a[2] + s * a[1];
+    R[3] = k * a[1] * a[0] + s * a[2];
+    R[4] = c + k * a[1] * a[1];
+    R[5] = k * a[1] * a[2] - s * a[0];
+    R[6] = k * a[2] * a[0] - s * a[1];
+    R[7] = k * a[2] * a[1] + s * a[0];
+    R[8] = c + k * a[2] * a[2];
+}
+/* Spatial motion cross product (w,v) x_m (w2,v2). */
+static sv6 cross_m(sv6 a, sv6 b) {
+    sv6 r;
+    double t[3];
+    cross(a.w, b.w, r.w);
+    cross(a.w, b.v, r.v);
+    cross(a.v, b.w, t);
+    for (int i = 0; i < 3; ++i) r.v[i] += t[i];
+    return r;
+}
+/* Spatial force cross product (w,v) x_f (n,f). */
+static sv6 cross_f(sv6 a, sv6 f) {
+    sv6 r;
+    double t[3];
+    cross(a.w, f.w, r.w);
+    cross(a.v, f.v, t);
+    for (int i = 0; i < 3; ++i) r.w[i] += t[i];
+    cross(a.w, f.v, r.v);
+    return r;
+}
+static double sv_dot(sv6 m, sv6 f) { return dot3(m.w, f.w) + dot3(m.v, f.v); }
+
+/* Rigid-body inertia about the ground origin: mass, first moment h = m c,
+ * rotational inertia about the origin I_O (sym: xx yy zz xy xz yz). */
+typedef struct { double m, h[3], I[6]; } rbi;
+static sv6 rbi_apply(const rbi* I, sv6 x) {
+    /* (I_O w + h x u, m u - h x w) */
+    sv6 r;
+    double t[3];
+    r.w[0] = I->I[0] * x.w[0] + I->I[3] * x.w[1] + I->I[4] * x.w[2];
+    r.w[1] = I->I[3] * x.w[0] + I->I[1] * x.w[1] + I->I[5] * x.w[2];
+    r.w[2] = I->I[4] * x.w[0] + I->I[5] * x.w[1] + I->I[2] * x.w[2];
+    cross(I->h, x.v, t);
+    for (int i = 0; i < 3; ++i) r.w[i] += t[i];
+    cross(I->h, x.w, t);
+    for (int i = 0; i < 3; ++i) r.v[i] = I->m * x.v[i] - t[i];
+    return r;
+}
+
+/* ======================================================================== */
+/* Functions of a coordinate.                                                */
+/* ======================================================================== */
+/* SimmSpline coefficients: the Forsythe–Malcolm–Moler cubic spline with
+ * third-derivative end conditions, as in opensim-core SimmSpline
+ * (SimmSpline::calcCoefficients; third-party, absent from /root/reference).
+ * b,c,d have n entries each. */
+static void simm_coefficients(int n, const double* x, const double* y,
+        double* b, double* c, double* d) {
+    if (n < 2) {
+        if (n == 1) { b[0] = c[0] = d[0] = 0.0; }
+        return;
+    }
+    if (n < 3) {
+        double t = (y[1] - y[0]) / (x[1] - x[0]);
+        b[0] = b[1] = t;
+        c[0] = c[1] = 0.0;
+        d[0] = d[1] = 0.0;
+        return;
+    }
+    int nm1 = n - 1;
+    d[0] = x[1] - x[0];
+    c[1] = (y[1] - y[0]) / d[0];
+    for (int i = 1; i < nm1; ++i) {
+        d[i] = x[i + 1] - x[i];
+        b[i] = 2.0 * (d[i - 1] + d[i]);
+        c[i + 1] = (y[i + 1] - y[i]) / d[i];
+        c[i] = c[i + 1] - c[i];
+    }
+    b[0] = -d[0];
+    b[nm1] = -d[n - 2];
+    c[0] = 0.0;
+    c[nm1] = 0.0;
+    if (n > 3) {
+        double d1 = c[2] / (x[3] - x[1]) - c[1] / (x[2] - x[0]);
+        double d2 = c[nm1 - 1] / (x[nm1] - x[n - 3]) -
+                    c[n - 3] / (x[nm1 - 1] - x[n - 4]);
+        double d31 = x[3] - x[0];
+        double d32 = x[nm1] - x[n - 4];
+        c[0] = d[0] * d1 / d31;
+        c[nm1] = -d[n - 2] * d2 / d32;
+    }
+    for (int i = 1; i < n; ++i) {
+        double t = d[i - 1] / b[i - 1];
+        b[i] -= t * d[i - 1];
+        c[i] -= t * c[i - 1];
+    }
+    c[nm1] /= b[nm1];
+    for (int j = 0; j < nm1; ++j) {
+        int i = nm1 - j - 1;
+        c[i] = (c[i] - d[i] * c[i + 1]) / b[i];
+    }
+    b[nm1] = (y[nm1] - y[n - 2]) / d[n - 2] + d[n - 2] * (c[n - 2] + 2.0 * c[nm1]);
+    for (int i = 0; i < nm1; ++i) {
+        b[i] = (y[i + 1] - y[i]) / d[i] - d[i] * (c[i + 1] + 2.0 * c[i]);
+        d[i] = (c[i + 1] - c[i]) / d[i];
+        c[i] *= 3.0;
+    }
+    c[nm1] *= 3.0;
+    d[nm1] = d[n - 2];
+}
+
+/* SimmSpline::interpolate (value, first, second derivative), with linear
+ * extrapolation outside the knots. */
+static void simm_eval(int n, const double* x, const double* y, const double* b,
+        const double* c, const double* d, double t, double* out) {
+    if (n == 1) { out[0] = y[0]; out[1] = out[2] = 0.0; return; }
+    if (t < x[0]) {
+        out[0] = y[0] + (t - x[0]) * b[0]; out[1] = b[0]; out[2] = 0.0; return;
+    }
+    if (t > x[n - 1]) {
+        out[0] = y[n - 1] + (t - x[n - 1]) * b[n - 1];
+        out[1] = b[n - 1]; out[2] = 0.0; return;
+    }
+    int k;
+    const double tol = 2e-13; /* SIMM ROUNDOFF_ERROR */
+    if (fabs(t - x[0]) <= tol) k = 0;
+    else if (fabs(t - x[n - 1]) <= tol) k = n - 1;
+    else {
+        int i = 0, j = n;
+        for (;;) {
+            k = (i + j) / 2;
+            if (t < x[k]) j = k;
+            else if (t > x[k + 1]) i = k;
+            else break;
+        }
+    }
+    double dx = t - x[k];
+    out[0] = y[k] + dx * (b[k] + dx * (c[k] + dx * d[k]));
+    out[1] = b[k] + dx * (2.0 * c[k] + 3.0 * dx * d[k]);
+    out[2] = 2.0 * c[k] + 6.0 * dx * d[k];
+}
+
+/* ======================================================================== */
+/* Context.                                                                  */
+/* ======================================================================== */
+struct orc_ctx {
+    mh_problem P;      /* shallow copy; arrays are deep-copied below       */
+    mh_options O;
+    int nthreads;
+    /* model copies */
+    mh_body* bodies; mh_axis* axes; mh_function* funcs; double *kx, *ky;
+    double *kb, *kc, *kd;          /* spline coefficients (per knot)       */
+    mh_muscle* mus; mh_path_point* pts; mh_actuator* acts; mh_table* tabs;
+    double *brk, *coef; mh_external_force* ext;
+    mh_variable_info *sinfo, *cinfo; mh_goal* goals; int32_t *gidx, *gcol;
+    double* gw;
+    /* derived sizes */
+    int NQ, NZ, NS, NC, NP; /* NP = per-point inputs excluding time */
+    int* mus_act_state;     /* state index of activation (-1)          */
+    int* mus_ftn_state;     /* state index of normalized tendon force   */
+    int* mus_control;       /* control index of excitation (-1)        */
+    int* coord_body;        /* owning body of coordinate               */
+    double tau_act, tau_deact; /* DGF static time constants quirk      */
+    /* transcription */
+    int scheme, N, G, nmesh, interp;
+    double* grid;   /* G */
+    double* quad;   /* G quadrature coefficients */
+    int64_t n, m, nnz;
+    int32_t *iRow, *jCol;
+    int fd; double h;
+};
+
+static double* dup_d(const double* p, size_t n) {
+    if (!n) return NULL;
+    double* r = (double*)malloc(n * sizeof(double));
+    memcpy(r, p, n * sizeof(double));
+    return r;
+}
+#define DUP(T, p, n) ((n) ? (T*)memcpy(malloc((size_t)(n) * sizeof(T)), (p), (size_t)(n) * sizeof(T)) : NULL)
+
+void orc_set_threads(orc_ctx* c, int nthreads) { c->nthreads = nthreads < 1 ? 1 : nthreads; }
+
+/* ------------------------------------------------------------------------ */
+/* Jacobian structure (block-dense CasOC rule).         */
+/* Columns of x: [t0, tf, states(NS x G grid-major), controls(NC x G)].      */
+/* ------------------------------------------------------------------------ */
+static int64_t col_state(const orc_ctx* c, int k, int s) { return 2 + (int64_t)k * c->NS + s; }
+static int64_t col_control(const orc_ctx* c, int k, int j) {
+    return 2 + (int64_t)c->NS * c->G + (int64_t)k * c->NC + j;
+}
+
+/* Sorted columns of all point inputs at grid point k (excluding t0/tf). */
+static int point_cols(const orc_ctx* c, int k, int64_t* out) {
+    int n = 0;
+    for (int s = 0; s < c->NS; ++s) out[n++] = col_state(c, k, s);
+    for (int j = 0; j < c->NC; ++j) out[n++] = col_control(c, k, j);
+    return n;
+}
+
+static int cmp64(const void* a, const void* b) {
+    int64_t x = *(const int64_t*)a, y = *(const int64_t*)b;
+    return x < y ? -1 : x > y;
+}
+
+/* Emits the sorted column set of every row of interval i, in row order.
+ * emit(row_local, cols, ncols). Returns rows per interval. */
+typedef void (*row_fn)(void* ud, int64_t row, const int64_t* cols, int ncols);
+static void interval_rows(const orc_ctx* c, int i, int64_t row0, row_fn emit, void* ud) {
+    int NQ = c->NQ, NS = c->NS, NC = c->NC;
+    int64_t* cols = (int64_t*)malloc(sizeof(int64_t) * (size_t)(3 * (NS + NC) + 8));
+    int64_t row = row0;
+    if (c->scheme == MH_HERMITE_SIMPSON) {
+        int ki = 2 * i, km = 2 * i + 1, kp = 2 * i + 2;
+        /* Hermite rows, then Simpson rows (CasOCHermiteSimpson.cpp:79-84). */
+        for (int pass = 0; pass < 2; ++pass) {
+            for (int s = 0; s < NS; ++s) {
+                int n = 0;
+                cols[n++] = 0; cols[n++] = 1;
+                if (s < NQ) {
+                    /* qdot = u is not a callback output: exact dependence. */
+                    if (pass == 0) {
+                        cols[n++] = col_state(c, km, s);
+                        cols[n++] = col_state(c, ki, s); cols[n++] = col_state(c, kp, s);
+                        cols[n++] = col_state(c, ki, NQ + s); cols[n++] = col_state(c, kp, NQ + s);
+                    } else {
+                        cols[n++] = col_state(c, ki, s); cols[n++] = col_state(c, kp, s);
+                        cols[n++] = col_state(c, ki, NQ + s); cols[n++] = col_state(c, km, NQ + s);
+                        cols[n++] = col_state(c, kp, NQ + s);
+                    }
+                } else {
+                    if (pass == 0) {
+                        cols[n++] = col_state(c, km, s);
+                        n += point_cols(c, ki, cols + n);
+                        n += point_cols(c, kp, cols + n);
+                    } else {
+                        n += point_cols(c, ki, cols + n);
+                        n += point_cols(c, km, cols + n);
+                        n += point_cols(c, kp, cols + n);
+                    }
+                }
+                qsort(cols, (size_t)n, sizeof(int64_t), cmp64);
+                emit(ud, row++, cols, n);
+            }
+        }
+        if (c->interp) {
+            for (int j = 0; j < NC; ++j) {
+                cols[0] = col_control(c, ki, j); cols[1] = col_control(c, km, j);
+                cols[2] = col_control(c, kp, j);
+                emit(ud, row++, cols, 3);
+            }
+        }
+    } else { /* trapezoidal (CasOCTrapezoidal.cpp:43-59) */
+        int ki = i, kp = i + 1;
+        for (int s = 0; s < NS; ++s) {
+            int n = 0;
+            cols[n++] = 0; cols[n++] = 1;
+            if (s < NQ) {
+                cols[n++] = col_state(c, ki, s); cols[n++] = col_state(c, kp, s);
+                cols[n++] = col_state(c, ki, NQ + s); cols[n++] = col_state(c, kp, NQ + s);
+            } else {
+                n += point_cols(c, ki, cols + n);
+                n += point_cols(c, kp, cols + n);
+            }
+            qsort(cols, (size_t)n, sizeof(int64_t), cmp64);
+            emit(ud, row++, cols, n);
+        }
+    }
+    free(cols);
+}
+
+typedef struct { int64_t count; int32_t *ir, *jc; } emit_state;
+static void emit_count(void* ud, int64_t row, const int64_t* cols, int n) {
+    (void)row; (void)cols;
+    ((emit_state*)ud)->count += n;
+}
+static void emit_fill(void* ud, int64_t row, const int64_t* cols, int n) {
+    emit_state* e = (emit_state*)ud;
+    for (int k = 0; k < n; ++k) {
+        e->ir[e->count] = (int32_t)row;
+        e->jc[e->count] = (int32_t)cols[k];
+        ++e->count;
+    }
+}
+static int rows_per_interval(const orc_ctx* c) {
+    return 2 * c->NS * (c->scheme == MH_HERMITE_SIMPSON) + c->NS * (c->scheme == MH_TRAPEZOIDAL) +
+           (c->scheme == MH_HERMITE_SIMPSON && c->interp ? c->NC : 0);
+}
+
+int orc_create(const mh_problem* p, const mh_options* o, orc_ctx** out) {
+    if (!p || !o || !out) return fail(MH_ERR_INVALID, "null argument");
+    const mh_model* M = &p->model;
+    if (M->nq <= 0 && M->nmuscles <= 0) return fail(MH_ERR_INVALID, "empty model");
+    if (o->num_mesh_intervals < 1) return fail(MH_ERR_INVALID, "num_mesh_intervals must be >= 1");
+    orc_ctx* c = (orc_ctx*)calloc(1, sizeof(orc_ctx));
+    c->P = *p;
+    c->O = *o;
+    c->nthreads = 1;
+    c->bodies = DUP(mh_body, M->bodies, M->nbodies);
+    c->axes = DUP(mh_axis, M->axes, M->naxes);
+    c->funcs = DUP(mh_function, M->functions, M->nfunctions);
+    c->kx = dup_d(M->knot_x, (size_t)M->nknots);
+    c->ky = dup_d(M->knot_y, (size_t)M->nknots);
+    c->mus = DUP(mh_muscle, M->muscles, M->nmuscles);
+    c->pts = DUP(mh_path_point, M->points, M->npoints);
+    c->acts = DUP(mh_actuator, M->actuators, M->nactuators);
+    c->tabs = DUP(mh_table, M->tables, M->ntables);
+    c->brk = dup_d(M->table_breaks, (size_t)M->nbreaks);
+    c->coef = dup_d(M->table_coefs, (size_t)M->ncoefs);
+    c->ext = DUP(mh_external_force, M->external, M->nexternal);
+    c->goals = DUP(mh_goal, p->goals, p->ngoals);
+    c->gidx = DUP(int32_t, p->goal_index, p->nterms);
+    c->gcol = DUP(int32_t, p->goal_column, p->nterms);
+    c->gw = dup_d(p->goal_weight, (size_t)p->nterms);
+
+    /* spline coefficients */
+    c->kb = (double*)calloc((size_t)M->nknots + 1, sizeof(double));
+    c->kc = (double*)calloc((size_t)M->nknots + 1, sizeof(double));
+    c->kd = (double*)calloc((size_t)M->nknots + 1, sizeof(double));
+    for (int f = 0; f < M->nfunctions; ++f) {
+        const mh_function* F = &c->funcs[f];
+        if (F->kind == MH_FN_SIMMSPLINE) {
+            if (F->knot_count < 1 || F->knot_begin < 0 || F->knot_begin + F->knot_count > M->nknots) {
+                orc_destroy(c);
+                return fail(MH_ERR_INVALID, "function %d: bad knots", f);
+            }
+            int b0 = F->knot_begin;
+            simm_coefficients(F->knot_count, c->kx + b0, c->ky + b0, c->kb + b0, c->kc + b0, c->kd + b0);
+        }
+    }
+
+    /* state layout (Simbody Y order, MocoUtilities.cpp:495-528) */
+    c->NQ = M->nq;
+    c->mus_act_state = (int*)malloc(sizeof(int) * (size_t)(M->nmuscles + 1));
+    c->mus_ftn_state = (int*)malloc(sizeof(int) * (size_t)(M->nmuscles + 1));
+    c->mus_control = (int*)malloc(sizeof(int) * (size_t)(M->nmuscles + 1));
+    int z = 2 * c->NQ;
+    c->tau_act = c->tau_deact = NAN;
+    for (int im = 0; im < M->nmuscles; ++im) {
+        const mh_muscle* mu = &c->mus[im];
+        if (mu->tendon_dynamics_implicit && !mu->ignore_tendon_compliance) {
+            orc_destroy(c);
+            return fail(MH_ERR_UNSUPPORTED, "implicit tendon dynamics not supported");
+        }
+        c->mus_act_state[im] = mu->ignore_activation_dynamics ? -1 : z++;
+        c->mus_ftn_state[im] = mu->ignore_tendon_compliance ? -1 : z++;
+        c->mus_control[im] = -1;
+        /* DeGrooteFregly2016Muscle.cpp:194-195: the activation time constants
+         * are function-level statics, fixed by the first muscle evaluated. */
+        if (!mu->ignore_activation_dynamics && isnan(c->tau_act)) {
+            c->tau_act = mu->activation_time_constant;
+            c->tau_deact = mu->deactivation_time_constant;
+        }
+    }
+    c->NS = z;
+    c->NZ = z - 2 * c->NQ;
+    c->NC = M->nactuators;
+    c->NP = c->NS + c->NC;
+    for (int ia = 0; ia < M->nactuators; ++ia) {
+        if (c->acts[ia].kind == MH_ACT_MUSCLE) {
+            int t = c->acts[ia].target;
+            if (t < 0 || t >= M->nmuscles) { orc_destroy(c); return fail(MH_ERR_INVALID, "actuator %d: bad muscle", ia); }
+            c->mus_control[t] = ia;
+        }
+    }
+    for (int im = 0; im < M->nmuscles; ++im)
+        if (c->mus_control[im] < 0) { orc_destroy(c); return fail(MH_ERR_INVALID, "muscle %d has no actuator", im); }
+    /* coordinate -> body */
+    c->coord_body = (int*)malloc(sizeof(int) * (size_t)(c->NQ + 1));
+    for (int j = 0; j < c->NQ; ++j) c->coord_body[j] = -1;
+    for (int b = 0; b < M->nbodies; ++b) {
+        const mh_body* B = &c->bodies[b];
+        if (B->parent >= b) { orc_destroy(c); return fail(MH_ERR_INVALID, "body %d not topologically ordered", b); }
+        for (int a = B->axis_begin; a < B->axis_begin + B->axis_count; ++a) {
+            int f = c->axes[a].func;
+            if (f < 0 || f >= M->nfunctions) { orc_destroy(c); return fail(MH_ERR_INVALID, "axis %d: bad function", a); }
+            int q = c->funcs[f].coord;
+            if (c->funcs[f].kind == MH_FN_CONSTANT) continue;
+            if (q < 0 || q >= c->NQ) { orc_destroy(c); return fail(MH_ERR_INVALID, "axis %d: bad coordinate", a); }
+            if (c->coord_body[q] >= 0 && c->coord_body[q] != b) {
+                orc_destroy(c);
+                return fail(MH_ERR_UNSUPPORTED, "coordinate %d drives axes of two bodies", q);
+            }
+            c->coord_body[q] = b;
+        }
+    }
+    for (int j = 0; j < c->NQ; ++j)
+        if (c->coord_body[j] < 0) { orc_destroy(c); return fail(MH_ERR_INVALID, "coordinate %d drives no axis", j); }
+
+    c->sinfo = DUP(mh_variable_info, p->state_infos, c->NS);
+    c->cinfo = DUP(mh_variable_info, p->control_infos, c->NC);
+
+    /* transcription grid (CasOCHermiteSimpson.h:45-68, CasOCSolver.h:38-42) */
+    c->scheme = o->transcription;
+    c->N = o->num_mesh_intervals;
+    c->nmesh = c->N + 1;
+    c->interp = o->interpolate_control_midpoints && c->NC > 0;
+    c->G = c->scheme == MH_HERMITE_SIMPSON ? 2 * c->N + 1 : c->N + 1;
+    c->grid = (double*)malloc(sizeof(double) * (size_t)c->G);
+    c->quad = (double*)calloc((size_t)c->G, sizeof(double));
+    double* mesh = (double*)malloc(sizeof(double) * (size_t)c->nmesh);
+    for (int i = 0; i < c->nmesh; ++i) mesh[i] = i / (double)c->N;
+    if (c->scheme == MH_HERMITE_SIMPSON) {
+        for (int k = 0; k < c->G; ++k)
+            c->grid[k] = (k % 2 == 0) ? mesh[k / 2] : .5 * (mesh[k / 2] + mesh[k / 2 + 1]);
+        /* CasOCHermiteSimpson.cpp:26-45 */
+        for (int i = 0; i < c->N; ++i) {
+            double dm = mesh[i + 1] - mesh[i];
+            c->quad[2 * i] += (1.0 / 6.0) * dm;
+            c->quad[2 * i + 1] += (2.0 / 3.0) * dm;
+            c->quad[2 * i + 2] += (1.0 / 6.0) * dm;
+        }
+    } else {
+        for (int k = 0; k < c->G; ++k) c->grid[k] = mesh[k];
+        /* CasOCTrapezoidal.cpp:26-41 */
+        for (int i = 0; i < c->N; ++i) {
+            double dm = mesh[i + 1] - mesh[i];
+            c->quad[i] += 0.5 * dm;
+            c->quad[i + 1] += 0.5 * dm;
+        }
+    }
+    free(mesh);
+    c->n = 2 + (int64_t)(c->NS + c->NC) * c->G;
+    c->m = (int64_t)rows_per_interval(c) * c->N;
+    /* structure */
+    emit_state e = {0, NULL, NULL};
+    for (int i = 0; i < c->N; ++i) interval_rows(c, i, 0, emit_count, &e);
+    c->nnz = e.count;
+    c->iRow = (int32_t*)malloc(sizeof(int32_t) * (size_t)(c->nnz + 1));
+    c->jCol = (int32_t*)malloc(sizeof(int32_t) * (size_t)(c->nnz + 1));
+    e.count = 0; e.ir = c->iRow; e.jc = c->jCol;
+    int rpi = rows_per_interval(c);
+    for (int i = 0; i < c->N; ++i) interval_rows(c, i, (int64_t)i * rpi, emit_fill, &e);
+    c->fd = o->finite_difference_scheme;
+    c->h = o->fd_step > 0 ? o->fd_step : 1e-8;
+    *out = c;
+    return MH_OK;
+}
+
+void orc_destroy(orc_ctx* c) {
+    if (!c) return;
+    void* ptrs[] = {c->bodies, c->axes, c->funcs, c->kx, c->ky, c->kb, c->kc, c->kd,
+            c->mus, c->pts, c->acts, c->tabs, c->brk, c->coef, c->ext, c->sinfo, c->cinfo,
+            c->goals, c->gidx, c->gcol, c->gw, c->mus_act_state, c->mus_ftn_state,
+            c->mus_control, c->coord_body, c->grid, c->quad, c->iRow, c->jCol};
+    for (size_t i = 0; i < sizeof ptrs / sizeof ptrs[0]; ++i) free(ptrs[i]);
+    free(c);
+}
+
+int orc_get_nlp_info(const orc_ctx* c, mh_nlp_info* info) {
+    memset(info, 0, sizeof *info);
+    info->n = c->n; info->m = c->m; info->nnz_jac_g = c->nnz; info->nnz_h_lag = 0;
+    info->num_grid_points = c->G; info->num_states = c->NS; info->num_controls = c->NC;
+    info->row_begin = 0; info->row_end = c->m; info->nnz_begin = 0; info->nnz_end = c->nnz;
+    return MH_OK;
+}
+
+int orc_get_jac_structure(const orc_ctx* c, int32_t* iRow, int32_t* jCol) {
+    memcpy(iRow, c->iRow, sizeof(int32_t) * (size_t)c->nnz);
+    memcpy(jCol, c->jCol, sizeof(int32_t) * (size_t)c->nnz);
+    return MH_OK;
+}
+
+/* CasOC::Problem::clipEndpointBounds (CasOCProblem.h:603-606) with the
+ * exact std::max / std::min NaN semantics. */
+static mh_bounds clip_endpoint(mh_bounds b, mh_bounds e) {
+    mh_bounds r;
+    r.lower = (b.lower < e.lower) ? e.lower : b.lower;
+    r.upper = (e.upper < b.upper) ? e.upper : b.upper;
+    return r;
+}
+static void set_bounds(mh_bounds b, double* lo, double* up) {
+    /* Transcription::setVariableBounds (CasOCTranscription.h:82-95) */
+    if (!isnan(b.lower) && !isnan(b.upper)) { *lo = b.lower; *up = b.upper; }
+    else { *lo = -INFINITY; *up = INFINITY; }
+}
+
+int orc_get_bounds(const orc_ctx* c, double* xl, double* xu, double* gl, double* gu) {
+    /* CasOCTranscription.cpp:183-250 */
+    set_bounds(c->P.time_initial, &xl[0], &xu[0]);
+    set_bounds(c->P.time_final, &xl[1], &xu[1]);
+    for (int s = 0; s < c->NS; ++s) {
+        mh_variable_info vi = c->sinfo[s];
+        mh_bounds ib = clip_endpoint(vi.bounds, vi.initial);
+        mh_bounds fb = clip_endpoint(vi.bounds, vi.final);
+        for (int k = 1; k < c->G - 1; ++k) set_bounds(vi.bounds, &xl[col_state(c, k, s)], &xu[col_state(c, k, s)]);
+        set_bounds(ib, &xl[col_state(c, 0, s)], &xu[col_state(c, 0, s)]);
+        set_bounds(fb, &xl[col_state(c, c->G - 1, s)], &xu[col_state(c, c->G - 1, s)]);
+    }
+    for (int j = 0; j < c->NC; ++j) {
+        mh_variable_info vi = c->cinfo[j];
+        mh_bounds ib = clip_endpoint(vi.bounds, vi.initial);
+        mh_bounds fb = clip_endpoint(vi.bounds, vi.final);
+        for (int k = 1; k < c->G - 1; ++k) set_bounds(vi.bounds, &xl[col_control(c, k, j)], &xu[col_control(c, k, j)]);
+        set_bounds(ib, &xl[col_control(c, 0, j)], &xu[col_control(c, 0, j)]);
+        set_bounds(fb, &xl[col_control(c, c->G - 1, j)], &xu[col_control(c, c->G - 1, j)]);
+    }
+    /* defects and interpolating-control rows: equality to 0
+     * (CasOCTranscription.cpp:275-278, 440-443) */
+    if (gl) for (int64_t r = 0; r < c->m; ++r) { gl[r] = 0.0; gu[r] = 0.0; }
+    return MH_OK;
+}
+
+int orc_get_initial_guess_from_bounds(const orc_ctx* c, double* x) {
+    /* CasOCTranscription.cpp:1123-1149 */
+    double* lo = (double*)malloc(sizeof(double) * (size_t)c->n);
+    double* up = (double*)malloc(sizeof(double) * (size_t)c->n);
+    orc_get_bounds(c, lo, up, NULL, NULL);
+    for (int64_t i = 0; i < c->n; ++i) {
+        double l = lo[i], u = up[i];
+        if (!isinf(l) && !isinf(u)) x[i] = 0.5 * (u + l);
+        else if (!isinf(l)) x[i] = l;
+        else if (!isinf(u)) x[i] = u;
+        else x[i] = 0;
+    }
+    free(lo); free(up);
+    return MH_OK;
+}
+
+int orc_get_random_iterate(const orc_ctx* c, const double* rnd, double* x) {
+    /* CasOCTranscription.cpp:1151-1177 */
+    double* lo = (double*)malloc(sizeof(double) * (size_t)c->n);
+    double* up = (double*)malloc(sizeof(double) * (size_t)c->n);
+    orc_get_bounds(c, lo, up, NULL, NULL);
+    for (int64_t i = 0; i < c->n; ++i) {
+        double l = lo[i], u = up[i], r = rnd[i];
+        double v = 0.5 * (r + 1.0) * (u - l) + l;
+        if (isnan(v)) v = r < l ? l : (r > u ? u : r); /* SimTK::clamp */
+        x[i] = v;
+    }
+    free(lo); free(up);
+    return MH_OK;
+}
+
+/* ======================================================================== */
+/* Model evaluation.                                                         */
+/* ======================================================================== */
+static void eval_function(const orc_ctx* c, int f, const double* q, double* out) {
+    const mh_function* F = &c->funcs[f];
+    switch (F->kind) {
+    case MH_FN_CONSTANT: out[0] = F->a; out[1] = out[2] = 0.0; return;
+    case MH_FN_LINEAR: {
+        double s = F->scale;
+        out[0] = s * (F->a * q[F->coord] + F->b);
+        out[1] = s * F->a; out[2] = 0.0; return;
+    }
+    default: {
+        int b0 = F->knot_begin;
+        simm_eval(F->knot_count, c->kx + b0, c->ky + b0, c->kb + b0, c->kc + b0, c->kd + b0,
+                q[F->coord], out);
+        out[0] *= F->scale; out[1] *= F->scale; out[2] *= F->scale;
+    }
+    }
+}
+
+int orc_eval_function(orc_ctx* c, int f, double qv, double* out3) {
+    if (f < 0 || f >= c->P.model.nfunctions) return fail(MH_ERR_INVALID, "bad function");
+    double* q = (double*)calloc((size_t)c->NQ + 1, sizeof(double));
+    int crd = c->funcs[f].coord;
+    if (crd >= 0) q[crd] = qv;
+    eval_function(c, f, q, out3);
+    free(q);
+    return MH_OK;
+}
+
+/* Piecewise-polynomial data table (GCVSpline restated as its piecewise
+ * polynomial). Column value at t. */
+static double table_eval(const orc_ctx* c, int ti, int col, double t) {
+    const mh_table* T = &c->tabs[ti];
+    const double* br = c->brk + T->break_begin;
+    int s;
+    if (t <= br[0]) s = 0;
+    else if (t >= br[T->nseg]) s = T->nseg - 1;
+    else {
+        int lo = 0, hi = T->nseg; /* br[lo] <= t < br[hi] */
+        while (hi - lo > 1) {
+            int mid = (lo + hi) / 2;
+            if (t < br[mid]) hi = mid; else lo = mid;
+        }
+        s = lo;
+    }
+    const double* cf = c->coef + T->coef_begin + ((int64_t)s * T->ncol + col) * (T->degree + 1);
+    double dt = t - br[s];
+    double v = cf[T->degree];
+    for (int k = T->degree - 1; k >= 0; --k) v = v * dt + cf[k];
+    return v;
+}
+
+/* ---- DeGrooteFregly2016Muscle curves (DeGrooteFregly2016Muscle.h:332-476,
+ *      constants :769-817) ---- */
+static const double DGF_b11 = 0.8150671134243542, DGF_b21 = 1.055033428970575,
+                    DGF_b31 = 0.162384573599574, DGF_b41 = 0.063303448465465,
+                    DGF_b12 = 0.433004984392647, DGF_b22 = 0.716775413397760,
+                    DGF_b32 = -0.029947116970696, DGF_b42 = 0.200356847296188,
+                    DGF_b13 = 0.1, DGF_b23 = 1.0, DGF_b33 = 0.353553390593274,
+                    DGF_b43 = 0.0;
+static const double DGF_kPE = 4.0, DGF_c1 = 0.200, DGF_c2 = 1.0, DGF_c3 = 0.200;
+static const double DGF_d1 = -0.3211346127989808, DGF_d2 = -8.149, DGF_d3 = -0.374,
+                    DGF_d4 = 0.8825327733249912;
+static const double DGF_minNormFiberLength = 0.2;
+
+static double gaussian_like(double x, double b1, double b2, double b3, double b4) {
+    double num = (x - b2) * (x - b2);
+    double den = (b3 + b4 * x) * (b3 + b4 * x);
+    return b1 * exp(-0.5 * num / den);
+}
+static double dgf_fal(const mh_muscle* mu, double l) {
+    double scale = mu->active_force_width_scale;
+    double x = (l - 1.0) / scale + 1.0;
+    return gaussian_like(x, DGF_b11, DGF_b21, DGF_b31, DGF_b41) +
+           gaussian_like(x, DGF_b12, DGF_b22, DGF_b32, DGF_b42) +
+           gaussian_like(x, DGF_b13, DGF_b23, DGF_b33, DGF_b43);
+}
+static double dgf_fv(double v) {
+    double tv = DGF_d2 * v + DGF_d3;
+    double arg = tv + sqrt(tv * tv + 1.0);
+    return DGF_d1 * log(arg) + DGF_d4;
+}
+static double dgf_fv_inv(double fv) {
+    return (sinh(1.0 / DGF_d1 * (fv - DGF_d4)) - DGF_d3) / DGF_d2;
+}
+static double dgf_fpe(const mh_muscle* mu, double l) {
+    if (mu->ignore_passive_fiber_force) return 0.0;
+    double e0 = mu->passive_fiber_strain_at_one_norm_force;
+    double offset = exp(DGF_kPE * (DGF_minNormFiberLength - 1.0) / e0);
+    double denom = exp(DGF_kPE) - offset;
+    return (exp(DGF_kPE * (l - 1.0) / e0) - offset) / denom;
+}
+static double dgf_kT(const mh_muscle* mu) {
+    return log((1.0 + DGF_c3) / DGF_c1) / (1.0 + mu->tendon_strain_at_one_norm_force - DGF_c2);
+}
+static double dgf_ft(const mh_muscle* mu, double l) {
+    return DGF_c1 * exp(dgf_kT(mu) * (l - DGF_c2)) - DGF_c3;
+}
+static double dgf_ft_deriv(const mh_muscle* mu, double l) {
+    double kT = dgf_kT(mu);
+    return DGF_c1 * kT * exp(kT * (l - DGF_c2));
+}
+static double dgf_ft_inv(const mh_muscle* mu, double f) {
+    return log((1.0 / DGF_c1) * (f + DGF_c3)) / dgf_kT(mu) + DGF_c2;
+}
+
+double orc_dgf_curve(const mh_muscle* mu, int which, double x) {
+    switch (which) {
+    case 0: return dgf_fal(mu, x);
+    case 1: return dgf_fpe(mu, x);
+    case 2: return dgf_fv(x);
+    case 3: return dgf_fv_inv(x);
+    case 4: return dgf_ft(mu, x);
+    case 5: return dgf_ft_inv(mu, x);
+    case 6: return dgf_ft_deriv(mu, x);
+    default: return NAN;
+    }
+}
+
+/* Tendon force and auxiliary derivatives of one DGF muscle
+ * (DeGrooteFregly2016Muscle.cpp:186-233, 240-425). */
+static void dgf_muscle(const orc_ctx* c, const mh_muscle* mu, double LMT, double VMT,
+        double activation, double excitation, int has_act, double normTendonForce,
+        int compliant, double* tendonForce, double* adot, double* ftdot) {
+    /* calcMuscleLengthInfoHelper (:240-275) */
+    double normTendonLength = compliant ? dgf_ft_inv(mu, normTendonForce) : 1.0;
+    double tendonLength = mu->tendon_slack_length * normTendonLength;
+    double fiberWidth = mu->optimal_fiber_length * sin(mu->pennation_angle_at_optimal);
+    double squareFiberWidth = fiberWidth * fiberWidth;
+    double fiberLengthAlongTendon = LMT - tendonLength;
+    double fiberLength = sqrt(fiberLengthAlongTendon * fiberLengthAlongTendon + squareFiberWidth);
+    double normFiberLength = fiberLength / mu->optimal_fiber_length;
+    double cosPenn = fiberLengthAlongTendon / fiberLength;
+    double fPE = dgf_fpe(mu, normFiberLength);
+    double fAL = dgf_fal(mu, normFiberLength);
+    double vmax = mu->max_contraction_velocity * mu->optimal_fiber_length;
+    /* calcFiberVelocityInfoHelper (:277-323) */
+    double normFiberVelocity, fV, normTendonVelocity;
+    if (compliant) {
+        double normFiberForce = normTendonForce / cosPenn;
+        fV = (normFiberForce - fPE) / (activation * fAL);
+        normFiberVelocity = dgf_fv_inv(fV);
+        double fiberVelocity = normFiberVelocity * vmax;
+        double fiberVelocityAlongTendon = fiberVelocity / cosPenn;
+        double tendonVelocity = VMT - fiberVelocityAlongTendon;
+        normTendonVelocity = tendonVelocity / mu->tendon_slack_length;
+    } else {
+        normTendonVelocity = 0.0;
+        double tendonVelocity = mu->tendon_slack_length * normTendonVelocity;
+        double fiberVelocityAlongTendon = VMT - tendonVelocity;
+        double fiberVelocity = fiberVelocityAlongTendon * cosPenn;
+        normFiberVelocity = fiberVelocity / vmax;
+        fV = dgf_fv(normFiberVelocity);
+    }
+    /* calcMuscleDynamicsInfoHelper (:325-425) via calcFiberForce (.h:482-503) */
+    double Fmax = mu->max_isometric_force;
+    double activeFiberForce = Fmax * (activation * fAL * fV);
+    double conPassive = Fmax * fPE;
+    double nonConPassive = Fmax * mu->fiber_damping * normFiberVelocity;
+    double totalFiberForce = activeFiberForce + conPassive + nonConPassive;
+    if (compliant) *tendonForce = Fmax * normTendonForce;
+    else *tendonForce = totalFiberForce * cosPenn;
+    /* computeStateVariableDerivatives (:186-233) */
+    if (has_act) {
+        double timeConstFactor = 0.5 + 1.5 * activation;
+        double tempAct = 1.0 / (c->tau_act * timeConstFactor);
+        double tempDeact = timeConstFactor / c->tau_deact;
+        double f = 0.5 * tanh(0.1 * (excitation - activation));
+        double timeConst = tempAct * (f + 0.5) + tempDeact * (-f + 0.5);
+        *adot = timeConst * (excitation - activation);
+    }
+    if (compliant) *ftdot = normTendonVelocity * dgf_ft_deriv(mu, normTendonLength);
+}
+
+/* Workspace for one DAE evaluation. */
+typedef struct {
+    double *R, *p;    /* body pose (world): 9, 3 per body                  */
+    sv6 *V, *A, *F;   /* velocity, bias acceleration, net force per body   */
+    sv6* S;           /* motion subspace per coordinate                    */
+    rbi* I;           /* world inertia per body; then composite            */
+    double* M;        /* NQ x NQ mass matrix                               */
+    double* tau;      /* generalized forces                                */
+    double* ppos;     /* path point world positions (3 per point)          */
+    double* pvel;
+    int* pact;
+    double* fvals;    /* function value/d1/d2 per axis (3 per axis)        */
+} dae_ws;
+
+static void ws_alloc(const orc_ctx* c, dae_ws* w) {
+    const mh_model* M = &c->P.model;
+    int nb = M->nbodies + 1;
+    w->R = (double*)malloc(sizeof(double) * 9 * (size_t)nb);
+    w->p = (double*)malloc(sizeof(double) * 3 * (size_t)nb);
+    w->V = (sv6*)malloc(sizeof(sv6) * (size_t)nb);
+    w->A = (sv6*)malloc(sizeof(sv6) * (size_t)nb);
+    w->F = (sv6*)malloc(sizeof(sv6) * (size_t)nb);
+    w->S = (sv6*)malloc(sizeof(sv6) * (size_t)(c->NQ + 1));
+    w->I = (rbi*)malloc(sizeof(rbi) * (size_t)nb);
+    w->M = (double*)malloc(sizeof(double) * (size_t)(c->NQ * c->NQ + 1));
+    w->tau = (double*)malloc(sizeof(double) * (size_t)(c->NQ + 1));
+    w->ppos = (double*)malloc(sizeof(double) * 3 * (size_t)(M->npoints + 1));
+    w->pvel = (double*)malloc(sizeof(double) * 3 * (size_t)(M->npoints + 1));
+    w->pact = (int*)malloc(sizeof(int) * (size_t)(M->npoints + 1));
+    w->fvals = (double*)malloc(sizeof(double) * 3 * (size_t)(M->naxes + 1));
+}
+static void ws_free(dae_ws* w) {
+    free(w->R); free(w->p); free(w->V); free(w->A); free(w->F); free(w->S); free(w->I);
+    free(w->M); free(w->tau); free(w->ppos); free(w->pvel); free(w->pact); free(w->fvals);
+}
+
+/* Forward kinematics, velocities and velocity-product accelerations in the
+ * ground frame (Simbody realizePosition/Velocity for FunctionBased
+ * mobilizers; restated).  Body index b is stored at b+1; slot 0 = ground. */
+static void kinematics(const orc_ctx* c, const double* q, const double* u, dae_ws* w) {
+    const mh_model* Mo = &c->P.model;
+    static const double I3[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    memcpy(w->R, I3, sizeof I3);
+    w->p[0] = w->p[1] = w->p[2] = 0.0;
+    memset(&w->V[0], 0, sizeof(sv6));
+    memset(&w->A[0], 0, sizeof(sv6));
+    /* gravity via base acceleration -g */
+    for (int i = 0; i < 3; ++i) w->A[0].v[i] = -Mo->gravity[i];
+    for (int j = 0; j < c->NQ; ++j) memset(&w->S[j], 0, sizeof(sv6));
+    for (int b = 0; b < Mo->nbodies; ++b) {
+        const mh_body* B = &c->bodies[b];
+        int ps = B->parent + 1, bs = b + 1;
+        const double* Rp = w->R + 9 * ps;
+        const double* pp = w->p + 3 * ps;
+        double RGF[9], pGF[3], t[3];
+        mat_mul(Rp, B->R_PF, RGF);
+        mat_vec(Rp, B->p_PF, t);
+        for (int i = 0; i < 3; ++i) pGF[i] = pp[i] + t[i];
+        sv6 V = w->V[ps];
+        sv6 Vpar = w->V[ps];
+        sv6 A = w->A[ps];
+        /* translations (axes fixed in F) */
+        double pFM[3] = {0, 0, 0};
+        for (int a = B->axis_begin; a < B->axis_begin + B->axis_count; ++a) {
+            const mh_axis* X = &c->axes[a];
+            double* fv = w->fvals + 3 * a;
+            eval_function(c, X->func, q, fv);
+            if (X->type != MH_AXIS_TRANSLATION) continue;
+            for (int i = 0; i < 3; ++i) pFM[i] += fv[0] * X->dir[i];
+        }
+        double oM[3];
+        mat_vec(RGF, pFM, t);
+        for (int i = 0; i < 3; ++i) oM[i] = pGF[i] + t[i];
+        for (int a = B->axis_begin; a < B->axis_begin + B->axis_count; ++a) {
+            const mh_axis* X = &c->axes[a];
+            if (X->type != MH_AXIS_TRANSLATION) continue;
+            const mh_function* F = &c->funcs[X->func];
+            if (F->kind == MH_FN_CONSTANT) continue;
+            const double* fv = w->fvals + 3 * a;
+            double uj = u[F->coord];
+            sv6 s;
+            s.w[0] = s.w[1] = s.w[2] = 0.0;
+            mat_vec(RGF, X->dir, s.v);
+            sv6 sd = cross_m(Vpar, s);
+            double thd = fv[1] * uj, thdd = fv[2] * uj * uj;
+            for (int i = 0; i < 3; ++i) {
+                V.w[i] += s.w[i] * thd; V.v[i] += s.v[i] * thd;
+                A.w[i] += sd.w[i] * thd + s.w[i] * thdd;
+                A.v[i] += sd.v[i] * thd + s.v[i] * thdd;
+                w->S[F->coord].w[i] += fv[1] * s.w[i];
+                w->S[F->coord].v[i] += fv[1] * s.v[i];
+            }
+        }
+        /* rotations (body-fixed sequence about the M origin) */
+        double Rcur[9];
+        memcpy(Rcur, I3, sizeof I3);
+        for (int a = B->axis_begin; a < B->axis_begin + B->axis_count; ++a) {
+            const mh_axis* X = &c->axes[a];
+            if (X->type != MH_AXIS_ROTATION) continue;
+            const mh_function* F = &c->funcs[X->func];
+            const double* fv = w->fvals + 3 * a;
+            if (F->kind != MH_FN_CONSTANT) {
+                double RGc[9];
+                mat_mul(RGF, Rcur, RGc);
+                sv6 s;
+                mat_vec(RGc, X->dir, s.w);
+                cross(oM, s.w, s.v);
+                sv6 sd = cross_m(V, s);
+                double uj = u[F->coord];
+                double thd = fv[1] * uj, thdd = fv[2] * uj * uj;
+                for (int i = 0; i < 3; ++i) {
+                    V.w[i] += s.w[i] * thd; V.v[i] += s.v[i] * thd;
+                    A.w[i] += sd.w[i] * thd + s.w[i] * thdd;
+                    A.v[i] += sd.v[i] * thd + s.v[i] * thdd;
+                    w->S[F->coord].w[i] += fv[1] * s.w[i];
+                    w->S[F->coord].v[i] += fv[1] * s.v[i];
+                }
+            }
+            double Rk[9];
+            axis_rotation(X->dir, fv[0], Rk);
+            mat_mul(Rcur, Rk, Rcur);
+        }
+        double RGM[9];
+        mat_mul(RGF, Rcur, RGM);
+        double* RB = w->R + 9 * bs;
+        double* pB = w->p + 3 * bs;
+        mat_mul_bt(RGM, B->R_BM, RB);       /* R_GB = R_GM R_BM^T */
+        mat_vec(RB, B->p_BM, t);
+        for (int i = 0; i < 3; ++i) pB[i] = oM[i] - t[i];
+        w->V[bs] = V;
+        w->A[bs] = A;
+    }
+}
+
+/* Path point world positions and velocities (OpenSim GeometryPath current
+ * path: inactive ConditionalPathPoints are skipped). */
+static void path_points(const orc_ctx* c, const double* q, const double* u, dae_ws* w) {
+    const mh_model* Mo = &c->P.model;
+    for (int i = 0; i < Mo->npoints; ++i) {
+        const mh_path_point* pt = &c->pts[i];
+        double loc[3] = {pt->loc[0], pt->loc[1], pt->loc[2]};
+        double dloc[3] = {0, 0, 0};
+        w->pact[i] = 1;
+        if (pt->kind == MH_PP_CONDITIONAL) {
+            double qv = q[pt->coord];
+            w->pact[i] = (qv >= pt->range[0] && qv <= pt->range[1]);
+        } else if (pt->kind == MH_PP_MOVING) {
+            int fs[3] = {pt->fx, pt->fy, pt->fz};
+            for (int d = 0; d < 3; ++d) {
+                if (fs[d] < 0) continue;
+                double o[3];
+                eval_function(c, fs[d], q, o);
+                loc[d] = o[0];
+                const mh_function* F = &c->funcs[fs[d]];
+                if (F->kind != MH_FN_CONSTANT) dloc[d] = o[1] * u[F->coord];
+            }
+        }
+        int bs = pt->body + 1;
+        const double* R = w->R + 9 * bs;
+        const double* p = w->p + 3 * bs;
+        double* P = w->ppos + 3 * i;
+        double* Vp = w->pvel + 3 * i;
+        double t[3], t2[3];
+        mat_vec(R, loc, t);
+        for (int d = 0; d < 3; ++d) P[d] = p[d] + t[d];
+        /* v = v_O + w x P + R dloc */
+        cross(w->V[bs].w, P, t);
+        mat_vec(R, dloc, t2);
+        for (int d = 0; d < 3; ++d) Vp[d] = w->V[bs].v[d] + t[d] + t2[d];
+    }
+}
+
+static void muscle_length_speed(const orc_ctx* c, const dae_ws* w, int im, double* len, double* spd) {
+    const mh_muscle* mu = &c->mus[im];
+    double L = 0.0, S = 0.0;
+    int prev = -1;
+    for (int i = mu->point_begin; i < mu->point_begin + mu->point_count; ++i) {
+        if (!w->pact[i]) continue;
+        if (prev >= 0) {
+            const double* a = w->ppos + 3 * prev;
+            const double* b = w->ppos + 3 * i;
+            double d[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]};
+            double l = sqrt(dot3(d, d));
+            L += l;
+            const double* va = w->pvel + 3 * prev;
+            const double* vb = w->pvel + 3 * i;
+            double dv[3] = {vb[0] - va[0], vb[1] - va[1], vb[2] - va[2]};
+            S += dot3(d, dv) / l;
+        }
+        prev = i;
+    }
+    *len = L;
+    *spd = S;
+}
+
+/* Apply point force Fp (world) at path point i to its body, including the
+ * MovingPathPoint generalized-force term tau_j += Fp . (R dloc/dq_j). */
+static void apply_point_force(const orc_ctx* c, dae_ws* w, const double* q, int i, const double* Fp) {
+    const mh_path_point* pt = &c->pts[i];
+    int bs = pt->body + 1;
+    if (pt->body >= 0) {
+        double t[3];
+        cross(w->ppos + 3 * i, Fp, t);
+        for (int d = 0; d < 3; ++d) { w->F[bs].w[d] -= t[d]; w->F[bs].v[d] -= Fp[d]; }
+        /* F[] holds (I a + v x* I v - f_ext): external forces subtract. */
+    }
+    if (pt->kind == MH_PP_MOVING && pt->body >= 0) {
+        int fs[3] = {pt->fx, pt->fy, pt->fz};
+        const double* R = w->R + 9 * bs;
+        for (int d = 0; d < 3; ++d) {
+            if (fs[d] < 0) continue;
+            const mh_function* F = &c->funcs[fs[d]];
+            if (F->kind == MH_FN_CONSTANT) continue;
+            double o[3];
+            eval_function(c, fs[d], q, o);
+            /* R * (e_d * o[1]) dotted with Fp */
+            double g = (R[0 + d] * Fp[0] + R[3 + d] * Fp[1] + R[6 + d] * Fp[2]) * o[1];
+            w->tau[F->coord] += g;
+        }
+    }
+}
+
+/* The explicit per-point DAE (MocoCasOCProblem::calcMultibodySystemExplicit,
+ * MocoCasOCProblem.h:203-244): time, states, controls -> udot, zdot. */
+static void eval_dae_point(const orc_ctx* c, dae_ws* w, double time, const double* x,
+        const double* ctrl, double* out) {
+    const mh_model* Mo = &c->P.model;
+    int NQ = c->NQ;
+    const double* q = x;
+    const double* u = x + NQ;
+    kinematics(c, q, u, w);
+    path_points(c, q, u, w);
+    /* Body inertias in ground about the origin; RNEA body forces. */
+    for (int b = 0; b < Mo->nbodies; ++b) {
+        const mh_body* B = &c->bodies[b];
+        int bs = b + 1;
+        const double* R = w->R + 9 * bs;
+        const double* p = w->p + 3 * bs;
+        double cw[3], t[3];
+        mat_vec(R, B->com, t);
+        for (int i = 0; i < 3; ++i) cw[i] = p[i] + t[i];
+        /* I_c in ground: R Ib R^T */
+        double Ib[9] = {B->inertia[0], B->inertia[3], B->inertia[4],
+                        B->inertia[3], B->inertia[1], B->inertia[5],
+                        B->inertia[4], B->inertia[5], B->inertia[2]};
+        double T1[9], Ig[9];
+        mat_mul(R, Ib, T1);
+        mat_mul_bt(T1, R, Ig);
+        rbi* I = &w->I[bs];
+        double m = B->mass;
+        I->m = m;
+        for (int i = 0; i < 3; ++i) I->h[i] = m * cw[i];
+        double c2 = dot3(cw, cw);
+        I->I[0] = Ig[0] + m * (c2 - cw[0] * cw[0]);
+        I->I[1] = Ig[4] + m * (c2 - cw[1] * cw[1]);
+        I->I[2] = Ig[8] + m * (c2 - cw[2] * cw[2]);
+        I->I[3] = Ig[1] - m * cw[0] * cw[1];
+        I->I[4] = Ig[2] - m * cw[0] * cw[2];
+        I->I[5] = Ig[5] - m * cw[1] * cw[2];
+        sv6 Ia = rbi_apply(I, w->A[bs]);
+        sv6 h = rbi_apply(I, w->V[bs]);
+        sv6 vxh = cross_f(w->V[bs], h);
+        for (int i = 0; i < 3; ++i) {
+            w->F[bs].w[i] = Ia.w[i] + vxh.w[i];
+            w->F[bs].v[i] = Ia.v[i] + vxh.v[i];
+        }
+    }
+    for (int j = 0; j < NQ; ++j) w->tau[j] = 0.0;
+    /* Coordinate actuators and muscles (controls in actuator order). */
+    double* zdot = out + NQ;
+    for (int ia = 0; ia < Mo->nactuators; ++ia) {
+        const mh_actuator* A = &c->acts[ia];
+        if (A->kind == MH_ACT_COORDINATE) {
+            w->tau[A->target] += ctrl[ia] * A->optimal_force;
+        }
+    }
+    for (int im = 0; im < Mo->nmuscles; ++im) {
+        const mh_muscle* mu = &c->mus[im];
+        double L, V;
+        muscle_length_speed(c, w, im, &L, &V);
+        double e = ctrl[c->mus_control[im]];
+        int sa = c->mus_act_state[im], sf = c->mus_ftn_state[im];
+        double a = sa >= 0 ? x[sa] : e;
+        double ftn = sf >= 0 ? x[sf] : NAN;
+        double T, adot = 0, ftdot = 0;
+        dgf_muscle(c, mu, L, V, a, e, sa >= 0, ftn, sf >= 0, &T, &adot, &ftdot);
+        if (sa >= 0) zdot[sa - 2 * NQ] = adot;
+        if (sf >= 0) zdot[sf - 2 * NQ] = ftdot;
+        /* Tension along each segment of the current path. */
+        int prev = -1;
+        for (int i = mu->point_begin; i < mu->point_begin + mu->point_count; ++i) {
+            if (!w->pact[i]) continue;
+            if (prev >= 0) {
+                const double* pa = w->ppos + 3 * prev;
+                const double* pb = w->ppos + 3 * i;
+                double d[3] = {pb[0] - pa[0], pb[1] - pa[1], pb[2] - pa[2]};
+                double l = sqrt(dot3(d, d));
+                double Fa[3], Fb[3];
+                for (int k = 0; k < 3; ++k) { Fa[k] = T * d[k] / l; Fb[k] = -Fa[k]; }
+                apply_point_force(c, w, q, prev, Fa);
+                apply_point_force(c, w, q, i, Fb);
+            }
+            prev = i;
+        }
+    }
+    /* External forces (ExternalForce, ground-expressed force and point). */
+    for (int ie = 0; ie < Mo->nexternal; ++ie) {
+        const mh_external_force* E = &c->ext[ie];
+        double Fv[3] = {0, 0, 0}, P[3], Tq[3] = {0, 0, 0};
+        int bs = E->body + 1;
+        for (int d = 0; d < 3; ++d) {
+            if (E->force_col >= 0) Fv[d] = table_eval(c, E->table, E->force_col + d, time);
+            P[d] = E->point_col >= 0 ? table_eval(c, E->table, E->point_col + d, time) : w->p[3 * bs + d];
+            if (E->torque_col >= 0) Tq[d] = table_eval(c, E->table, E->torque_col + d, time);
+        }
+        double t[3];
+        cross(P, Fv, t);
+        for (int d = 0; d < 3; ++d) { w->F[bs].w[d] -= t[d] + Tq[d]; w->F[bs].v[d] -= Fv[d]; }
+    }
+    /* RNEA backward pass: tau_applied - bias. */
+    for (int b = Mo->nbodies - 1; b >= 0; --b) {
+        int bs = b + 1;
+        int ps = c->bodies[b].parent + 1;
+        if (ps > 0) {
+            for (int i = 0; i < 3; ++i) { w->F[ps].w[i] += w->F[bs].w[i]; w->F[ps].v[i] += w->F[bs].v[i]; }
+        }
+    }
+    for (int j = 0; j < NQ; ++j) w->tau[j] -= sv_dot(w->S[j], w->F[c->coord_body[j] + 1]);
+    /* CRBA mass matrix. */
+    for (int b = Mo->nbodies - 1; b >= 0; --b) {
+        int bs = b + 1, ps = c->bodies[b].parent + 1;
+        if (ps > 0) {
+            rbi* P = &w->I[ps];
+            rbi* C = &w->I[bs];
+            P->m += C->m;
+            for (int i = 0; i < 3; ++i) P->h[i] += C->h[i];
+            for (int i = 0; i < 6; ++i) P->I[i] += C->I[i];
+        }
+    }
+    for (int i = 0; i < NQ; ++i) {
+        int b = c->coord_body[i];
+        sv6 Fi = rbi_apply(&w->I[b + 1], w->S[i]);
+        for (int j = 0; j < NQ; ++j) {
+            /* dof j on body b or an ancestor of b */
+            int bj = c->coord_body[j];
+            int anc = b;
+            while (anc >= 0 && anc != bj) anc = c->bodies[anc].parent;
+            if (anc == bj) {
+                double v = sv_dot(w->S[j], Fi);
+                w->M[i * NQ + j] = v;
+                w->M[j * NQ + i] = v;
+            } else {
+                int anc2 = bj;
+                while (anc2 >= 0 && anc2 != b) anc2 = c->bodies[anc2].parent;
+                if (anc2 < 0) { w->M[i * NQ + j] = 0.0; w->M[j * NQ + i] = 0.0; }
+            }
+        }
+    }
+    /* Cholesky M = L L^T (in place, lower) and solve. */
+    double* L = w->M;
+    for (int j = 0; j < NQ; ++j) {
+        double s = L[j * NQ + j];
+        for (int k = 0; k < j; ++k) s -= L[j * NQ + k] * L[j * NQ + k];
+        double d = sqrt(s);
+        L[j * NQ + j] = d;
+        for (int i = j + 1; i < NQ; ++i) {
+            double t = L[i * NQ + j];
+            for (int k = 0; k < j; ++k) t -= L[i * NQ + k] * L[j * NQ + k];
+            L[i * NQ + j] = t / d;
+        }
+    }
+    double* y = out; /* udot */
+    for (int i = 0; i < NQ; ++i) {
+        double t = w->tau[i];
+        for (int k = 0; k < i; ++k) t -= L[i * NQ + k] * y[k];
+        y[i] = t / L[i * NQ + i];
+    }
+    for (int i = NQ - 1; i >= 0; --i) {
+        double t = y[i];
+        for (int k = i + 1; k < NQ; ++k) t -= L[k * NQ + i] * y[k];
+        y[i] = t / L[i * NQ + i];
+    }
+}
+
+int orc_muscle_length_speed(orc_ctx* c, int im, const double* q, const double* u, double* out) {
+    if (im < 0 || im >= c->P.model.nmuscles) return fail(MH_ERR_INVALID, "bad muscle");
+    dae_ws w;
+    ws_alloc(c, &w);
+    kinematics(c, q, u, &w);
+    path_points(c, q, u, &w);
+    muscle_length_speed(c, &w, im, &out[0], &out[1]);
+    ws_free(&w);
+    return MH_OK;
+}
+
+int orc_eval_dae(orc_ctx* c, int32_t np, const double* in, double* out) {
+    int NI = 1 + c->NS + c->NC, NO = c->NQ + c->NZ;
+#pragma omp parallel num_threads(c->nthreads)
+    {
+        dae_ws w;
+        ws_alloc(c, &w);
+#pragma omp for schedule(static)
+        for (int k = 0; k < np; ++k) {
+            const double* p = in + (int64_t)k * NI;
+            eval_dae_point(c, &w, p[0], p + 1, p + 1 + c->NS, out + (int64_t)k * NO);
+        }
+        ws_free(&w);
+    }
+    return MH_OK;
+}
+
+/* ======================================================================== */
+/* Transcription evaluation.                                                 */
+/* ======================================================================== */
+static void times_of(const orc_ctx* c, const double* x, double* t) {
+    /* Transcription::createTimes (CasOCTranscription.h:40-43) */
+    double t0 = x[0], tf = x[1];
+    for (int k = 0; k < c->G; ++k) t[k] = (tf - t0) * c->grid[k] + t0;
+}
+
+static void gather_point(const orc_ctx* c, const double* x, int k, double* st, double* ct) {
+    memcpy(st, x + col_state(c, k, 0), sizeof(double) * (size_t)c->NS);
+    if (c->NC) memcpy(ct, x + col_control(c, k, 0), sizeof(double) * (size_t)c->NC);
+}
+
+/* xdot at all grid points: qdot = u (CasOCTranscription.cpp:313-314) and
+ * callback outputs for the rest. xd: NS x G (grid-major). */
+static void all_xdot(orc_ctx* c, const double* x, const double* times, double* xd) {
+    int NS = c->NS, NC = c->NC, NQ = c->NQ;
+#pragma omp parallel num_threads(c->nthreads)
+    {
+        dae_ws w;
+        ws_alloc(c, &w);
+        double* st = (double*)malloc(sizeof(double) * (size_t)(NS + NC + 1));
+        double* ct = st + NS;
+#pragma omp for schedule(static)
+        for (int k = 0; k < c->G; ++k) {
+            gather_point(c, x, k, st, ct);
+            double* o = xd + (int64_t)k * NS;
+            for (int j = 0; j < NQ; ++j) o[j] = st[NQ + j];
+            eval_dae_point(c, &w, times[k], st, ct, o + NQ);
+        }
+        free(st);
+        ws_free(&w);
+    }
+}
+
+int orc_eval_g(orc_ctx* c, const double* x, double* g) {
+    int NS = c->NS, NC = c->NC;
+    double* times = (double*)malloc(sizeof(double) * (size_t)c->G);
+    double* xd = (double*)malloc(sizeof(double) * (size_t)c->G * (size_t)NS);
+    times_of(c, x, times);
+    all_xdot(c, x, times, xd);
+    int rpi = rows_per_interval(c);
+    for (int i = 0; i < c->N; ++i) {
+        double* gi = g + (int64_t)i * rpi;
+        if (c->scheme == MH_HERMITE_SIMPSON) {
+            int ki = 2 * i, km = 2 * i + 1, kp = 2 * i + 2;
+            double h = times[kp] - times[ki];
+            const double *xi = x + col_state(c, ki, 0), *xm = x + col_state(c, km, 0),
+                         *xp = x + col_state(c, kp, 0);
+            const double *fi = xd + (int64_t)ki * NS, *fm = xd + (int64_t)km * NS,
+                         *fp = xd + (int64_t)kp * NS;
+            /* CasOCHermiteSimpson.cpp:79-84 */
+            for (int s = 0; s < NS; ++s)
+                gi[s] = xm[s] - 0.5 * (xp[s] + xi[s]) - (h / 8.0) * (fi[s] - fp[s]);
+            for (int s = 0; s < NS; ++s)
+                gi[NS + s] = xp[s] - xi[s] - (h / 6.0) * (fp[s] + 4.0 * fm[s] + fi[s]);
+            if (c->interp) {
+                const double *ci = x + col_control(c, ki, 0), *cm = x + col_control(c, km, 0),
+                             *cp = x + col_control(c, kp, 0);
+                /* CasOCHermiteSimpson.cpp:102 */
+                for (int j = 0; j < NC; ++j) gi[2 * NS + j] = cm[j] - 0.5 * (cp[j] + ci[j]);
+            }
+        } else {
+            int ki = i, kp = i + 1;
+            double h = times[kp] - times[ki];
+            const double *xi = x + col_state(c, ki, 0), *xp = x + col_state(c, kp, 0);
+            const double *fi = xd + (int64_t)ki * NS, *fp = xd + (int64_t)kp * NS;
+            /* CasOCTrapezoidal.cpp:52-56 */
+            for (int s = 0; s < NS; ++s) gi[s] = xp[s] - (xi[s] + 0.5 * h * (fp[s] + fi[s]));
+        }
+    }
+    free(times);
+    free(xd);
+    return MH_OK;
+}
+
+/* FD derivative blocks of the DAE at every grid point.
+ * D[k][d][o]: derivative of callback output o (udot, zdot) along direction
+ * d in {t0, tf, input 0..NP-1}.  CasADi FiniteDiff with enable_fd
+ * (CasOCFunction.h:38-44); time seeds are d(time_k)/d(t0) = 1-grid_k and
+ * d(time_k)/d(tf) = grid_k (CasOCTranscription.cpp:126-127,1189). */
+static void fd_blocks(orc_ctx* c, const double* x, const double* times, double* D) {
+    int NS = c->NS, NP = c->NP, NO = c->NQ + c->NZ;
+    int ND = NP + 2;
+    double h = c->h;
+#pragma omp parallel num_threads(c->nthreads)
+    {
+        dae_ws w;
+        ws_alloc(c, &w);
+        double* in = (double*)malloc(sizeof(double) * (size_t)(NP + 1));
+        double* yp = (double*)malloc(sizeof(double) * (size_t)(3 * NO + 1));
+        double* ym = yp + NO;
+        double* y0 = ym + NO;
+#pragma omp for schedule(static)
+        for (int k = 0; k < c->G; ++k) {
+            gather_point(c, x, k, in, in + NS);
+            double t = times[k];
+            if (c->fd != MH_FD_CENTRAL) eval_dae_point(c, &w, t, in, in + NS, y0);
+            for (int d = 0; d < ND; ++d) {
+                double seed;
+                int idx = -1;
+                if (d == 0) seed = 1.0 - c->grid[k];
+                else if (d == 1) seed = c->grid[k];
+                else { seed = 1.0; idx = d - 2; }
+                double* Dk = D + ((int64_t)k * ND + d) * NO;
+                if (c->fd != MH_FD_BACKWARD) {
+                    if (idx < 0) eval_dae_point(c, &w, t + h * seed, in, in + NS, yp);
+                    else {
+                        double s = in[idx];
+                        in[idx] = s + h * seed;
+                        eval_dae_point(c, &w, t, in, in + NS, yp);
+                        in[idx] = s;
+                    }
+                }
+                if (c->fd != MH_FD_FORWARD) {
+                    if (idx < 0) eval_dae_point(c, &w, t - h * seed, in, in + NS, ym);
+                    else {
+                        double s = in[idx];
+                        in[idx] = s - h * seed;
+                        eval_dae_point(c, &w, t, in, in + NS, ym);
+                        in[idx] = s;
+                    }
+                }
+                for (int o = 0; o < NO; ++o) {
+                    if (c->fd == MH_FD_CENTRAL) Dk[o] = (yp[o] - ym[o]) / (2.0 * h);
+                    else if (c->fd == MH_FD_FORWARD) Dk[o] = (yp[o] - y0[o]) / h;
+                    else Dk[o] = (y0[o] - ym[o]) / h;
+                }
+            }
+        }
+        free(in);
+        free(yp);
+        ws_free(&w);
+    }
+}
+
+/* Derivative of xdot[s] at grid point k along direction d (0=t0, 1=tf,
+ * 2+j = input j).  For s < NQ, qdot = u exactly. */
+static double xdot_deriv(const orc_ctx* c, const double* D, int k, int s, int d) {
+    int NQ = c->NQ, NO = c->NQ + c->NZ, ND = c->NP + 2;
+    if (s < NQ) return (d == 2 + NQ + s) ? 1.0 : 0.0;
+    return D[((int64_t)k * ND + d) * NO + (s - NQ)];
+}
+
+/* Map a Jacobian column to (grid point, direction) for an interval row. */
+static int col_to_dir(const orc_ctx* c, int64_t col, int* k) {
+    if (col < 2) { *k = -1; return (int)col; }
+    int64_t sblock = (int64_t)c->NS * c->G;
+    if (col < 2 + sblock) {
+        int64_t r = col - 2;
+        *k = (int)(r / c->NS);
+        return 2 + (int)(r % c->NS);
+    }
+    int64_t r = col - 2 - sblock;
+    *k = (int)(r / c->NC);
+    return 2 + c->NS + (int)(r % c->NC);
+}
+
+int orc_eval_jac_g(orc_ctx* c, const double* x, double* values) {
+    int NS = c->NS, NQ = c->NQ;
+    int NO = c->NQ + c->NZ, ND = c->NP + 2;
+    double* times = (double*)malloc(sizeof(double) * (size_t)c->G);
+    double* xd = (double*)malloc(sizeof(double) * (size_t)c->G * (size_t)NS);
+    double* D = (double*)malloc(sizeof(double) * (size_t)c->G * (size_t)ND * (size_t)NO);
+    times_of(c, x, times);
+    all_xdot(c, x, times, xd);
+    fd_blocks(c, x, times, D);
+    int rpi = rows_per_interval(c);
+    double t0 = x[0], tf = x[1];
+    (void)t0; (void)tf;
+    for (int64_t e = 0; e < c->nnz; ++e) {
+        int64_t row = c->iRow[e], col = c->jCol[e];
+        int i = (int)(row / rpi);
+        int rl = (int)(row % rpi);
+        double v = 0.0;
+        int kc;
+        int dir = col_to_dir(c, col, &kc);
+        if (c->scheme == MH_HERMITE_SIMPSON) {
+            int ki = 2 * i, km = 2 * i + 1, kp = 2 * i + 2;
+            double gi = c->grid[ki], gp = c->grid[kp];
+            double h = times[kp] - times[ki];
+            /* dh/dt0 = -(g_p - g_i), dh/dtf = (g_p - g_i) */
+            double dh0 = -(gp - gi), dhf = (gp - gi);
+            if (rl < NS) { /* Hermite: x_mid - .5(x_p + x_i) - h/8 (f_i - f_p) */
+                int s = rl;
+                const double* fi = xd + (int64_t)ki * NS;
+                const double* fp = xd + (int64_t)kp * NS;
+                if (dir < 2) {
+                    double dh = dir == 0 ? dh0 : dhf;
+                    v = -(dh / 8.0) * (fi[s] - fp[s]) -
+                        (h / 8.0) * (xdot_deriv(c, D, ki, s, dir) - xdot_deriv(c, D, kp, s, dir));
+                } else {
+                    if (kc == km && dir == 2 + s) v += 1.0;
+                    if (kc == ki) {
+                        if (dir == 2 + s) v += -0.5;
+                        v += -(h / 8.0) * xdot_deriv(c, D, ki, s, dir);
+                    }
+                    if (kc == kp) {
+                        if (dir == 2 + s) v += -0.5;
+                        v += (h / 8.0) * xdot_deriv(c, D, kp, s, dir);
+                    }
+                }
+            } else if (rl < 2 * NS) { /* Simpson: x_p - x_i - h/6 (f_p + 4 f_m + f_i) */
+                int s = rl - NS;
+                const double* fi = xd + (int64_t)ki * NS;
+                const double* fm = xd + (int64_t)km * NS;
+                const double* fp = xd + (int64_t)kp * NS;
+                if (dir < 2) {
+                    double dh = dir == 0 ? dh0 : dhf;
+                    v = -(dh / 6.0) * (fp[s] + 4.0 * fm[s] + fi[s]) -
+                        (h / 6.0) * (xdot_deriv(c, D, kp, s, dir) + 4.0 * xdot_deriv(c, D, km, s, dir) +
+                                     xdot_deriv(c, D, ki, s, dir));
+                } else {
+                    if (kc == kp) {
+                        if (dir == 2 + s) v += 1.0;
+                        v += -(h / 6.0) * xdot_deriv(c, D, kp, s, dir);
+                    }
+                    if (kc == ki) {
+                        if (dir == 2 + s) v += -1.0;
+                        v += -(h / 6.0) * xdot_deriv(c, D, ki, s, dir);
+                    }
+                    if (kc == km) v += -(h / 6.0) * 4.0 * xdot_deriv(c, D, km, s, dir);
+                }
+            } else { /* interpolating controls */
+                v = (kc == km) ? 1.0 : -0.5;
+            }
+        } else {
+            int ki = i, kp = i + 1;
+            double gi = c->grid[ki], gp = c->grid[kp];
+            double h = times[kp] - times[ki];
+            double dh0 = -(gp - gi), dhf = (gp - gi);
+            int s = rl;
+            const double* fi = xd + (int64_t)ki * NS;
+            const double* fp = xd + (int64_t)kp * NS;
+            if (dir < 2) {
+                double dh = dir == 0 ? dh0 : dhf;
+                v = -0.5 * dh * (fp[s] + fi[s]) -
+                    0.5 * h * (xdot_deriv(c, D, kp, s, dir) + xdot_deriv(c, D, ki, s, dir));
+            } else {
+                if (kc == kp) {
+                    if (dir == 2 + s) v += 1.0;
+                    v += -0.5 * h * xdot_deriv(c, D, kp, s, dir);
+                }
+                if (kc == ki) {
+                    if (dir == 2 + s) v += -1.0;
+                    v += -0.5 * h * xdot_deriv(c, D, ki, s, dir);
+                }
+            }
+        }
+        values[e] = v;
+    }
+    (void)NQ;
+    free(times);
+    free(xd);
+    free(D);
+    return MH_OK;
+}
+
+/* ======================================================================== */
+/* Objective.                                                                */
+/* ======================================================================== */
+/* Integrand of goal g at one point (MocoControlGoal.cpp:120-131,
+ * MocoStateTrackingGoal.cpp:103-117). */
+static double goal_integrand(const orc_ctx* c, const mh_goal* G, double t, const double* st,
+        const double* ct) {
+    double L = 0.0;
+    for (int k = G->term_begin; k < G->term_begin + G->term_count; ++k) {
+        int idx = c->gidx[k];
+        double w = c->gw[k];
+        if (G->kind == MH_GOAL_CONTROL) {
+            double v = ct[idx];
+            /* MocoControlGoal.cpp:98-107: x*x for exponent 2 */
+            L += w * (G->exponent == 2 ? v * v : pow(fabs(v), G->exponent));
+        } else if (G->kind == MH_GOAL_STATE_TRACKING) {
+            double ref = table_eval(c, G->table, c->gcol[k], t);
+            double d = st[idx] - ref;
+            L += w * (d * d);
+        } else if (G->kind == MH_GOAL_SUM_SQUARED_STATE) {
+            double v = st[idx];
+            L += w * (v * v);
+        }
+    }
+    return L;
+}
+static int goal_has_integral(const mh_goal* G) { return G->kind != MH_GOAL_FINAL_TIME; }
+
+int orc_eval_f(orc_ctx* c, const double* x, double* f) {
+    double* times = (double*)malloc(sizeof(double) * (size_t)c->G);
+    double* st = (double*)malloc(sizeof(double) * (size_t)(c->NS + c->NC + 1));
+    double* ct = st + c->NS;
+    times_of(c, x, times);
+    double total = 0.0;
+    /* CasOCTranscription.cpp:478-511: cost = weight * (tf-t0) * dot(quad, L) */
+    for (int g = 0; g < c->P.ngoals; ++g) {
+        const mh_goal* G = &c->goals[g];
+        double cost;
+        if (goal_has_integral(G)) {
+            double acc = 0.0;
+            for (int k = 0; k < c->G; ++k) {
+                gather_point(c, x, k, st, ct);
+                acc += c->quad[k] * goal_integrand(c, G, times[k], st, ct);
+            }
+            double integral = (x[1] - x[0]) * acc;
+            cost = G->weight * integral;
+        } else {
+            cost = G->weight * x[1];
+        }
+        total += cost;
+    }
+    *f = total;
+    free(times);
+    free(st);
+    return MH_OK;
+}
+
+int orc_eval_grad_f(orc_ctx* c, const double* x, double* grad) {
+    int NS = c->NS, NP = c->NP;
+    double h = c->h;
+    double* times = (double*)malloc(sizeof(double) * (size_t)c->G);
+    double* in = (double*)malloc(sizeof(double) * (size_t)(NP + 1));
+    times_of(c, x, times);
+    for (int64_t i = 0; i < c->n; ++i) grad[i] = 0.0;
+    double dur = x[1] - x[0];
+    for (int g = 0; g < c->P.ngoals; ++g) {
+        const mh_goal* G = &c->goals[g];
+        if (!goal_has_integral(G)) { grad[1] += G->weight; continue; }
+        double acc = 0.0;
+        for (int k = 0; k < c->G; ++k) {
+            gather_point(c, x, k, in, in + NS);
+            double t = times[k];
+            double L0 = goal_integrand(c, G, t, in, in + NS);
+            acc += c->quad[k] * L0;
+            double wq = G->weight * dur * c->quad[k];
+            for (int d = 0; d < NP + 2; ++d) {
+                double seed = d == 0 ? 1.0 - c->grid[k] : (d == 1 ? c->grid[k] : 1.0);
+                double lp = 0, lm = 0;
+                int idx = d - 2;
+                if (c->fd != MH_FD_BACKWARD) {
+                    if (idx < 0) lp = goal_integrand(c, G, t + h * seed, in, in + NS);
+                    else { double s = in[idx]; in[idx] = s + h; lp = goal_integrand(c, G, t, in, in + NS); in[idx] = s; }
+                }
+                if (c->fd != MH_FD_FORWARD) {
+                    if (idx < 0) lm = goal_integrand(c, G, t - h * seed, in, in + NS);
+                    else { double s = in[idx]; in[idx] = s - h; lm = goal_integrand(c, G, t, in, in + NS); in[idx] = s; }
+                }
+                double dL = c->fd == MH_FD_CENTRAL ? (lp - lm) / (2.0 * h)
+                          : (c->fd == MH_FD_FORWARD ? (lp - L0) / h : (L0 - lm) / h);
+                int64_t col;
+                if (d == 0) col = 0;
+                else if (d == 1) col = 1;
+                else if (idx < NS) col = col_state(c, k, idx);
+                else col = col_control(c, k, idx - NS);
+                grad[col] += wq * dL;
+            }
+        }
+        /* d/dt0 and d/dtf of the duration factor */
+        grad[0] += -G->weight * acc;
+        grad[1] += G->weight * acc;
+    }
+    free(times);
+    free(in);
+    return MH_OK;
+}

@@ -1,0 +1,76 @@
+/* oracle.h — CPU restatement of the reference hot path (TEST INFRASTRUCTURE).
+ *
+ * This is the parity oracle for the MI355X path.  It is NOT part of the
+ * product: only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+ * leg may load it, and only as the checker / CPU baseline.  The product
+ * library (libmocohip.so) never links or calls it.
+ *
+ * It restates, in plain C99 and independently of the HIP kernels:
+ *   - CasOC transcription layout, bounds, defects, quadrature, constraint
+ *     flattening and block-dense Jacobian structure
+ *     (Moco/Moco/MocoCasADiSolver/CasOCTranscription.{h,cpp},
+ *      CasOCHermiteSimpson.cpp, CasOCTrapezoidal.cpp);
+ *   - the per-grid-point explicit DAE of MocoCasOCProblem
+ *     (MocoCasOCProblem.h:203-244) on a Simbody-equivalent multibody model;
+ *   - DeGrooteFregly2016Muscle (Moco/Moco/Components/DeGrooteFregly2016Muscle.*);
+ *   - goal integrands (MocoControlGoal.cpp:120-131,
+ *     MocoStateTrackingGoal.cpp:103-117, MocoGoal.h:387-400);
+ *   - finite-difference derivatives of the per-point callbacks
+ *     (CasOCFunction.h:38-44: enable_fd, fd_method central|forward|backward).
+ * Parity status of each piece is documented in DESIGN.md §Oracle.
+ */
+#ifndef MOCO_ORACLE_H
+#define MOCO_ORACLE_H
+
+#include "../include/mocohip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct orc_ctx orc_ctx;
+
+const char* orc_last_error(void);
+int orc_create(const mh_problem* problem, const mh_options* options,
+        orc_ctx** ctx);
+void orc_destroy(orc_ctx* ctx);
+/* Worker threads used for per-grid-point work (1 = serial). */
+void orc_set_threads(orc_ctx* ctx, int nthreads);
+
+int orc_get_nlp_info(const orc_ctx* ctx, mh_nlp_info* info);
+int orc_get_bounds(const orc_ctx* ctx, double* x_l, double* x_u, double* g_l,
+        double* g_u);
+int orc_get_initial_guess_from_bounds(const orc_ctx* ctx, double* x);
+int orc_get_random_iterate(const orc_ctx* ctx, const double* rand, double* x);
+int orc_get_jac_structure(const orc_ctx* ctx, int32_t* iRow, int32_t* jCol);
+
+int orc_eval_f(orc_ctx* ctx, const double* x, double* f);
+int orc_eval_grad_f(orc_ctx* ctx, const double* x, double* grad_f);
+int orc_eval_g(orc_ctx* ctx, const double* x, double* g);
+int orc_eval_jac_g(orc_ctx* ctx, const double* x, double* values);
+
+/* inputs per point: [time, states(NS), controls(NC)];
+ * outputs per point: [udot(NQ), zdot(NZ)]. */
+int orc_eval_dae(orc_ctx* ctx, int32_t npoints, const double* inputs,
+        double* outputs);
+
+/* Muscle-level probes for the DGF known-answer tests
+ * (Moco/Tests/testMocoActuators.cpp:199-220,1026-1039). which:
+ *  0 active force-length f_AL(x)      1 passive force-length f_PE(x)
+ *  2 force-velocity f_V(x)            3 force-velocity inverse
+ *  4 tendon force-length f_T(x)       5 tendon force-length inverse
+ *  6 tendon f_T'(x)                                                   */
+double orc_dgf_curve(const mh_muscle* muscle, int which, double x);
+
+/* Muscle-tendon length / lengthening speed and generalized-coordinate
+ * probes at a state (q,u): out = [length, speed] for muscle im. */
+int orc_muscle_length_speed(orc_ctx* ctx, int im, const double* q,
+        const double* u, double* out);
+/* Evaluate a model function (joint axis / moving point) and derivatives. */
+int orc_eval_function(orc_ctx* ctx, int ifn, double q, double* out3);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,87 @@
+#!/usr/bin/env python
+"""Convert the reference's gait10dof18musc model and data files into the
+committed data files under opensim-moco_amd/mocohip/data/ (run once, in the
+container that has /root/reference; the GPU box never reads the reference).
+
+Inputs (all under /root/reference, read as data):
+  Moco/Archive/Tests/testGait10dof18musc_subject01.osim   (model)
+  Moco/Tests/walk_gait1018_subject01_grf.mot               (GRF data)
+  Moco/Tests/walk_gait1018_subject01_grf.xml               (ExternalLoads)
+  Moco/Tests/walk_gait1018_state_reference.mot             (MocoTrack reference)
+  Moco/Tests/std_testMocoTrackGait10dof18musc_solution.sto (golden solution)
+"""
+import json
+import math
+import os
+import sys
+import xml.etree.ElementTree as ET
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+sys.path.insert(0, os.path.join(REPO, "opensim-moco_amd"))
+
+from mocohip.model import model_to_dict  # noqa: E402
+from mocohip.osim import read_osim, read_storage  # noqa: E402
+
+REF = "/root/reference"
+DATA = os.path.join(REPO, "opensim-moco_amd", "mocohip", "data")
+GOLDEN = os.path.join(REPO, "tests", "golden")
+
+
+def main():
+    os.makedirs(DATA, exist_ok=True)
+    os.makedirs(GOLDEN, exist_ok=True)
+    osim = os.path.join(REF, "Moco/Archive/Tests/testGait10dof18musc_subject01.osim")
+    model = read_osim(osim)
+    with open(os.path.join(DATA, "gait10dof18musc.json"), "w") as fh:
+        json.dump(model_to_dict(model), fh, indent=1)
+
+    # Ground reactions (ExternalLoads file: which columns go to which body).
+    labels, data, hdr = read_storage(os.path.join(REF, "Moco/Tests/walk_gait1018_subject01_grf.mot"))
+    xml = ET.parse(os.path.join(REF, "Moco/Tests/walk_gait1018_subject01_grf.xml")).getroot()
+    forces = []
+    for ef in xml.iter("ExternalForce"):
+        forces.append({
+            "name": ef.get("name"),
+            "body": ef.findtext("applied_to_body").strip(),
+            "force_expressed_in_body": ef.findtext("force_expressed_in_body").strip(),
+            "point_expressed_in_body": ef.findtext("point_expressed_in_body").strip(),
+            "force_identifier": ef.findtext("force_identifier").strip(),
+            "point_identifier": ef.findtext("point_identifier").strip(),
+            "torque_identifier": ef.findtext("torque_identifier").strip(),
+        })
+    grf = {"labels": labels, "time": data[:, 0].tolist(),
+           "columns": {l: data[:, i].tolist() for i, l in enumerate(labels) if i > 0},
+           "external_forces": forces}
+    with open(os.path.join(DATA, "walk_gait1018_subject01_grf.json"), "w") as fh:
+        json.dump(grf, fh)
+
+    # State reference (degrees -> radians for rotational coordinates, as
+    # TableProcessor does for inDegrees=yes tables).
+    labels, data, hdr = read_storage(os.path.join(REF, "Moco/Tests/walk_gait1018_state_reference.mot"))
+    rot = {c.path + "/value" for j in model.joints for c in j.coordinates
+           if c.motion_type == "rotational"}
+    in_deg = hdr.get("inDegrees", "no").lower() == "yes"
+    cols = {}
+    for i, l in enumerate(labels):
+        if i == 0:
+            continue
+        v = data[:, i]
+        if in_deg and l in rot:
+            v = v * math.pi / 180.0
+        cols[l] = v.tolist()
+    with open(os.path.join(DATA, "walk_gait1018_state_reference.json"), "w") as fh:
+        json.dump({"time": data[:, 0].tolist(), "columns": cols}, fh)
+
+    # Golden torque-driven MocoTrack solution (N=65 HS; 131 rows).
+    labels, data, hdr = read_storage(os.path.join(REF, "Moco/Tests/std_testMocoTrackGait10dof18musc_solution.sto"))
+    np.savez_compressed(os.path.join(GOLDEN, "std_testMocoTrackGait10dof18musc_solution.npz"),
+                        labels=np.array(labels), data=data,
+                        header=np.array([f"{k}={v}" for k, v in hdr.items()]))
+    print("wrote", DATA, GOLDEN)
+
+
+if __name__ == "__main__":
+    main()
