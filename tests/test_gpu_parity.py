@@ -1,0 +1,186 @@
+"""GPU (libmocohip.so on gfx950) vs the CPU oracle, through the C ABI.
+
+Tolerances (the oracle and the kernels use different libm implementations
+and FMA contraction, so bit equality is not expected for floating point):
+  * structure (iRow/jCol), bounds, initial guesses: bit-exact;
+  * DAE outputs and g: |d| <= 1e-10 * (row scale);
+  * Jacobian: |dJ| <= 1e-8 |J| + tau_row, with the finite-difference
+    cancellation bound tau_row = 256 eps * F_i * h_i / h_fd (F_i: largest
+    |xdot| on the interval's grid points, h_i: interval duration, h_fd the
+    FD step) — the noise any two FP implementations of the same FD differ by.
+"""
+import numpy as np
+import pytest
+
+from mocohip import configs
+from mocohip.solver import HipNLP, OracleNLP
+
+pytestmark = pytest.mark.gpu
+EPS = np.finfo(float).eps
+
+CASES = {
+    "sliding_mass": lambda: configs.sliding_mass(50),
+    "double_pendulum_hs": lambda: configs.double_pendulum(100),
+    "double_pendulum_trap": lambda: configs.double_pendulum(40, "trapezoidal"),
+    "double_pendulum_N1": lambda: configs.double_pendulum(1),
+    "gait_rigid_forward": lambda: configs.gait10dof18musc(12),
+    "gait_rigid_central": lambda: configs.gait10dof18musc(8, fd_scheme="central"),
+    "gait_rigid_backward": lambda: configs.gait10dof18musc(6, fd_scheme="backward"),
+    "gait_compliant_central": lambda: configs.gait10dof18musc(8, tendon_compliance=True,
+                                                               fd_scheme="central"),
+    "gait_torque_driven": lambda: configs.gait10dof18musc(10, muscles=False),
+}
+
+
+def _pair(name):
+    st = CASES[name]()
+    rep = st.problem.create_rep()
+    opts = st.solver.options()
+    return HipNLP(rep, opts), OracleNLP(rep, opts, threads=8), st
+
+
+def _points(nlp, x):
+    G, NS, NC = nlp.G, nlp.NS, nlp.NC
+    t = np.array([(x[1] - x[0]) * g + x[0] for g in _grid(nlp)])
+    S = x[2:2 + NS * G].reshape(G, NS)
+    U = x[2 + NS * G:].reshape(G, NC)
+    return np.concatenate([t[:, None], S, U], 1)
+
+
+def _grid(nlp):
+    N = nlp.opts.num_mesh_intervals
+    mesh = np.arange(N + 1) / N
+    if nlp.opts.transcription == 0:
+        return np.array([mesh[k // 2] if k % 2 == 0 else 0.5 * (mesh[k // 2] + mesh[k // 2 + 1])
+                         for k in range(nlp.G)])
+    return mesh
+
+
+def _iterates(nlp):
+    xr = nlp.random_iterate(np.random.default_rng(0).uniform(-1, 1, nlp.n))
+    xm = nlp.initial_guess_from_bounds()
+    return [("random", xr), ("midpoint", xm)]
+
+
+def _interval_scale(ref, x):
+    """(F_i, h_i) per mesh interval from the oracle's DAE at the grid."""
+    P = _points(ref, x)
+    Y = ref.eval_dae(P)
+    u = np.abs(P[:, 1 + ref.NQ:1 + 2 * ref.NQ]).max(1) if ref.NQ else 0
+    F = np.maximum(np.nan_to_num(np.abs(Y), nan=0).max(1), u)
+    hs = ref.opts.transcription == 0
+    N = ref.opts.num_mesh_intervals
+    step = 2 if hs else 1
+    Fi = np.array([F[i * step:i * step + step + 1].max() for i in range(N)])
+    hi = np.array([P[(i + 1) * step, 0] - P[i * step, 0] for i in range(N)])
+    return Fi, np.abs(hi)
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_structure_bounds_guess_bit_exact(name):
+    gpu, ref, _ = _pair(name)
+    assert (gpu.n, gpu.m, gpu.nnz) == (ref.n, ref.m, ref.nnz)
+    ir, jc = gpu.jac_structure()
+    ir0, jc0 = ref.jac_structure()
+    assert np.array_equal(ir, ir0) and np.array_equal(jc, jc0)
+    for a, b in zip(gpu.bounds(), ref.bounds()):
+        assert np.array_equal(a, b)
+    assert np.array_equal(gpu.initial_guess_from_bounds(), ref.initial_guess_from_bounds())
+    r = np.random.default_rng(5).uniform(-1, 1, gpu.n)
+    assert np.array_equal(gpu.random_iterate(r), ref.random_iterate(r))
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_dae_probe(name):
+    gpu, ref, _ = _pair(name)
+    for _, x in _iterates(gpu):
+        P = _points(gpu, x)
+        Y, Y0 = gpu.eval_dae(P), ref.eval_dae(P)
+        assert np.array_equal(np.isnan(Y), np.isnan(Y0))
+        ok = ~np.isnan(Y0)
+        scale = np.nan_to_num(np.abs(Y0), nan=0).max(1, keepdims=True) + 1.0
+        assert np.all(np.abs(Y - Y0)[ok] <= (1e-10 * np.broadcast_to(scale, Y.shape))[ok])
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_eval_g(name):
+    gpu, ref, _ = _pair(name)
+    rpi = gpu.m // gpu.opts.num_mesh_intervals
+    for _, x in _iterates(gpu):
+        g, g0 = gpu.eval_g(x), ref.eval_g(x)
+        assert np.array_equal(np.isnan(g), np.isnan(g0))
+        Fi, hi = _interval_scale(ref, x)
+        scale = np.repeat(Fi * hi + np.abs(x).max() + 1.0, rpi)
+        ok = ~np.isnan(g0)
+        assert np.all(np.abs(g - g0)[ok] <= 1e-10 * scale[ok])
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_eval_jac_g(name):
+    gpu, ref, st = _pair(name)
+    rpi = gpu.m // gpu.opts.num_mesh_intervals
+    ir, _ = gpu.jac_structure()
+    for _, x in _iterates(gpu):
+        J, J0 = gpu.eval_jac_g(x), ref.eval_jac_g(x)
+        assert np.array_equal(np.isnan(J), np.isnan(J0))
+        Fi, hi = _interval_scale(ref, x)
+        tau_int = 256 * EPS * (Fi + 1.0) * (hi + 1.0) / st.solver.fd_step
+        tau = tau_int[ir // rpi]
+        ok = ~np.isnan(J0)
+        err = np.abs(J - J0)[ok]
+        assert np.all(err <= 1e-8 * np.abs(J0[ok]) + tau[ok]), err.max()
+
+
+@pytest.mark.parametrize("name", ["sliding_mass", "double_pendulum_hs", "gait_rigid_forward",
+                                  "gait_compliant_central"])
+def test_objective_and_gradient(name):
+    gpu, ref, st = _pair(name)
+    for _, x in _iterates(gpu):
+        f, f0 = gpu.eval_f(x), ref.eval_f(x)
+        assert f == pytest.approx(f0, rel=1e-12, abs=1e-12)
+        gf, gf0 = gpu.eval_grad_f(x), ref.eval_grad_f(x)
+        tol = 1e-8 * np.abs(gf0) + 1e3 * EPS * max(abs(f0), 1.0) / st.solver.fd_step
+        assert np.all(np.abs(gf - gf0) <= tol)
+
+
+@pytest.mark.parametrize("name", ["double_pendulum_hs", "gait_rigid_forward"])
+def test_shards_reassemble_bit_exact(name):
+    """Mesh-interval shards (the multi-GPU partition) concatenate to exactly
+    the unsharded g and Jacobian values."""
+    st = CASES[name]()
+    rep = st.problem.create_rep()
+    N = st.solver.num_mesh_intervals
+    full = HipNLP(rep, st.solver.options())
+    x = full.random_iterate(np.random.default_rng(1).uniform(-1, 1, full.n))
+    g, J = full.eval_g(x), full.eval_jac_g(x)
+    cuts = [0, N // 3, (2 * N) // 3, N]
+    gs, Js = [], []
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        sh = HipNLP(rep, st.solver.options(a, b))
+        assert (sh.row_begin, sh.row_end) == (a * full.m // N, b * full.m // N)
+        gs.append(sh.eval_g(x))
+        Js.append(sh.eval_jac_g(x))
+    assert np.array_equal(np.concatenate(gs), g)
+    assert np.array_equal(np.concatenate(Js), J)
+
+
+def test_device_pointer_entry_points():
+    import torch
+    gpu, ref, _ = _pair("double_pendulum_hs")
+    x = gpu.random_iterate(np.random.default_rng(2).uniform(-1, 1, gpu.n))
+    xd = torch.tensor(x, dtype=torch.float64, device="cuda")
+    gd = torch.empty(gpu.m, dtype=torch.float64, device="cuda")
+    vd = torch.empty(gpu.nnz, dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
+    gpu.eval_g_device(xd.data_ptr(), gd.data_ptr())
+    gpu.eval_jac_g_device(xd.data_ptr(), vd.data_ptr())
+    assert np.array_equal(gd.cpu().numpy(), gpu.eval_g(x))
+    assert np.array_equal(vd.cpu().numpy(), gpu.eval_jac_g(x))
+
+
+def test_repeatable_bitwise():
+    gpu, _, _ = _pair("gait_rigid_forward")
+    x = gpu.random_iterate(np.random.default_rng(3).uniform(-1, 1, gpu.n))
+    a = gpu.eval_jac_g(x)
+    b = gpu.eval_jac_g(x)
+    assert np.array_equal(a, b)

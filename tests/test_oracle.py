@@ -1,0 +1,263 @@
+"""Pin the CPU oracle against the reference's own known answers and golden
+files.  CPU only."""
+import ctypes as C
+import math
+
+import numpy as np
+import pytest
+
+from mocohip import abi, configs
+from mocohip.problem import MocoControlGoal, MocoProblem
+from mocohip.solver import MocoHipSolver, OracleNLP
+from mocohip.splines import SimmSpline, gcv_interpolating_ppoly, ppoly_eval
+
+lib = abi.load_oracle()
+
+
+def dgf_muscle(**kw):
+    m = abi.mh_muscle()
+    m.active_force_width_scale = 1.0
+    m.passive_fiber_strain_at_one_norm_force = 0.6
+    m.tendon_strain_at_one_norm_force = 0.049
+    for k, v in kw.items():
+        setattr(m, k, v)
+    return m
+
+
+def curve(m, which, x):
+    return lib.orc_dgf_curve(C.byref(m), which, float(x))
+
+
+def test_dgf_curve_known_answers():
+    """Moco/Tests/testMocoActuators.cpp:199-220 ("Curve values")."""
+    m = dgf_muscle()
+    assert curve(m, 4, 1.0) == 0.0                                  # f_T(1) == 0
+    assert curve(m, 4, 1 + 0.049) == pytest.approx(1, rel=1e-10)    # f_T(1+eps_T)
+    assert curve(m, 1, 1.0) == pytest.approx(0.0182288, rel=1e-4)   # f_PE(1)
+    assert curve(m, 1, 0.2) == pytest.approx(0, abs=1e-4)           # f_PE(0.2)
+    assert curve(m, 1, 1 + 0.6) == pytest.approx(1, rel=1e-4)       # f_PE(1+e0)
+    assert curve(m, 0, 1.0) == pytest.approx(1)                     # f_AL(1)
+    assert curve(m, 2, -1.0) == 0.0 or abs(curve(m, 2, -1.0)) < 1e-15  # f_V(-1)
+    assert curve(m, 2, 0.0) == pytest.approx(1)                     # f_V(0)
+    assert curve(m, 2, 1.0) == pytest.approx(1.794, rel=1e-3)       # f_V(1)
+
+
+def test_dgf_force_velocity_inverse():
+    """testMocoActuators.cpp:1026-1039: FV inverse round trip."""
+    m = dgf_muscle()
+    for v in np.linspace(-1, 1, 100):
+        assert curve(m, 3, curve(m, 2, v)) == pytest.approx(v, abs=1e-12)
+
+
+def test_dgf_tendon_inverse_and_derivative():
+    m = dgf_muscle()
+    for lt in np.linspace(0.99, 1.06, 30):
+        f = curve(m, 4, lt)
+        assert curve(m, 5, f) == pytest.approx(lt, rel=1e-12)
+        h = 1e-6
+        fd = (curve(m, 4, lt + h) - curve(m, 4, lt - h)) / (2 * h)
+        assert curve(m, 6, lt) == pytest.approx(fd, rel=1e-7)
+
+
+def test_simmspline_restatement():
+    """SimmSpline (FMM cubic): interpolates the knots, C2 inside, linear
+    extrapolation outside; oracle and host restatement agree."""
+    x = [-2.0944, -1.74533, -1.39626, -1.0472, -0.698132, -0.349066, -0.174533,
+         0.197344, 0.337395, 0.490178, 1.52146, 2.0944]
+    y = [-0.0032, 0.00179, 0.00411, 0.0041, 0.00212, -0.001, -0.0031, -0.005227,
+         -0.005435, -0.005574, -0.005435, -0.00525]
+    s = SimmSpline(x, y)
+    for xi, yi in zip(x, y):
+        assert s(xi) == pytest.approx(yi, abs=1e-15)
+    for t in np.linspace(-1.9, 2.0, 37):
+        h = 1e-6
+        assert s(t, 1) == pytest.approx((s(t + h) - s(t - h)) / (2 * h), abs=1e-7)
+    assert s(3.0) == pytest.approx(y[-1] + (3.0 - x[-1]) * s.b[-1])
+    # oracle evaluation through a one-coordinate model
+    from mocohip.model import Body, Coordinate, Function, Joint, Model, Axis
+    m = Model("spline_probe")
+    m.add_body(Body("b", 1.0, (0, 0, 0), (1, 1, 1, 0, 0, 0)))
+    q = Coordinate("q")
+    m.add_joint(Joint("j", "ground", "b", [q], [
+        Axis(abi.MH_AXIS_ROTATION, (0, 0, 1), Function.linear("q")),
+        Axis(abi.MH_AXIS_TRANSLATION, (1, 0, 0), Function.simm_spline("q", x, y, 1.14724))]))
+    p = MocoProblem(m)
+    nlp = OracleNLP(p.create_rep(), MocoHipSolver(num_mesh_intervals=2).options())
+    out = np.zeros(3)
+    for t in np.linspace(-2.5, 2.5, 23):
+        lib.orc_eval_function(nlp.ctx, 1, float(t), abi.dptr(out))
+        assert out[0] == pytest.approx(1.14724 * s(t), abs=1e-15)
+        assert out[1] == pytest.approx(1.14724 * s(t, 1), abs=1e-13)
+
+
+def test_gcv_natural_spline_interpolates():
+    t = np.linspace(0, 1, 23)
+    y = np.sin(3 * t)[:, None]
+    for deg in (3, 5):
+        br, cf = gcv_interpolating_ppoly(t, y, deg)
+        assert np.allclose(ppoly_eval(br, cf, t, 0), y[:, 0], atol=1e-12)
+        assert np.abs(ppoly_eval(br, cf, 0.5, 0) - np.sin(1.5)) < 1e-5
+
+
+def _point_inputs(nlp, states, controls, t=0.3):
+    return np.concatenate([[t], states, controls])[None, :]
+
+
+def test_double_pendulum_closed_form():
+    """ModelFactory::createNLinkPendulum(2) dynamics vs the closed form of
+    tropter/tests/test_double_pendulum.cpp:45-74 (point masses) plus the unit
+    rotational inertia of each body (Inertia(1))."""
+    st = configs.double_pendulum(4)
+    nlp = OracleNLP(st.problem.create_rep(), st.solver.options())
+    rng = np.random.default_rng(3)
+    g = 9.80665
+    for _ in range(20):
+        q0, q1, u0, u1, t0, t1 = rng.uniform(-2, 2, 6)
+        out = nlp.eval_dae(_point_inputs(nlp, [q0, q1, u0, u1], [t0, t1]))[0]
+        L0 = L1 = m0 = m1 = 1.0
+        z0 = m1 * L0 * L1 * math.cos(q1)
+        M = np.array([[m0 * L0 ** 2 + m1 * (L0 ** 2 + L1 ** 2) + 2 * z0 + 2.0, m1 * L1 ** 2 + z0 + 1.0],
+                      [m1 * L1 ** 2 + z0 + 1.0, m1 * L1 ** 2 + 1.0]])
+        V = np.array([-u1 * (2 * u0 + u1), u0 * u0]) * m1 * L0 * L1 * math.sin(q1)
+        Gv = np.array([g * ((m0 + m1) * L0 * math.cos(q0) + m1 * L1 * math.cos(q0 + q1)),
+                       g * m1 * L1 * math.cos(q0 + q1)])
+        udot = np.linalg.solve(M, np.array([t0, t1]) - (V + Gv))
+        assert np.allclose(out, udot, rtol=1e-12, atol=1e-12)
+
+
+def test_sliding_mass_dynamics():
+    st = configs.sliding_mass(3)
+    nlp = OracleNLP(st.problem.create_rep(), st.solver.options())
+    out = nlp.eval_dae(np.array([[0.1, 0.3, -2.0, 7.0]]))
+    assert out[0, 0] == pytest.approx(7.0 / 2.0, rel=1e-15)
+
+
+@pytest.mark.parametrize("name,N,n,m,nnz", [
+    ("sliding_mass", 50, 305, 250, 1850),
+    ("double_pendulum", 100, 1208, 1000, 10400),
+])
+def test_layout_sizes(name, N, n, m, nnz):
+    """SURVEY.md §8 config size table."""
+    st = configs.CONFIGS[name](N)
+    nlp = OracleNLP(st.problem.create_rep(), st.solver.options())
+    assert (nlp.n, nlp.m, nlp.nnz) == (n, m, nnz)
+
+
+def test_gait_layout_sizes():
+    st = configs.gait10dof18musc(200)
+    nlp = OracleNLP(st.problem.create_rep(), st.solver.options())
+    assert (nlp.NS, nlp.NC) == (38, 28)
+    assert (nlp.n, nlp.m) == (26468, 20800)
+    assert nlp.nnz == 9604 * 200          # ≈1.92 M
+
+
+def test_sliding_mass_bounds():
+    """exampleSlidingMass bounds through CasOC's column rules
+    (CasOCTranscription.cpp:183-250)."""
+    st = configs.sliding_mass(5)
+    nlp = OracleNLP(st.problem.create_rep(), st.solver.options())
+    xl, xu, gl, gu = nlp.bounds()
+    G = nlp.G
+    assert (xl[0], xu[0], xl[1], xu[1]) == (0, 0, 0, 5)
+    pos = lambda k: 2 + k * 2
+    assert (xl[pos(0)], xu[pos(0)]) == (0, 0)
+    assert (xl[pos(G - 1)], xu[pos(G - 1)]) == (1, 1)
+    assert (xl[pos(3)], xu[pos(3)]) == (-5, 5)
+    assert (xl[pos(3) + 1], xu[pos(3) + 1]) == (-50, 50)
+    assert (xl[2 + 2 * G + 3], xu[2 + 2 * G + 3]) == (-50, 50)
+    assert np.all(gl == 0) and np.all(gu == 0)
+    x = nlp.initial_guess_from_bounds()
+    assert x[1] == 2.5 and x[pos(0)] == 0 and x[pos(G - 1)] == 1
+
+
+def test_structure_contains_true_dependencies():
+    """Perturbing any variable changes only rows where the structure has a
+    nonzero in that column."""
+    st = configs.double_pendulum(4)
+    nlp = OracleNLP(st.problem.create_rep(), st.solver.options())
+    ir, jc = nlp.jac_structure()
+    S = set(zip(ir.tolist(), jc.tolist()))
+    x = nlp.random_iterate(np.random.default_rng(1).uniform(-1, 1, nlp.n))
+    x[1] = 2.0
+    g0 = nlp.eval_g(x)
+    for j in range(nlp.n):
+        xp = x.copy()
+        xp[j] += 1e-3
+        rows = np.nonzero(nlp.eval_g(xp) != g0)[0]
+        for r in rows:
+            assert (int(r), j) in S
+
+
+def _numjac(fun, x, cols, h=1e-4):
+    out = []
+    for j in cols:
+        e = np.zeros_like(x)
+        e[j] = 1.0
+        f1, f2 = fun(x + h * e), fun(x - h * e)
+        f3, f4 = fun(x + 2 * h * e), fun(x - 2 * h * e)
+        out.append((8 * (f1 - f2) - (f3 - f4)) / (12 * h))
+    return np.array(out).T
+
+
+@pytest.mark.parametrize("scheme", ["hermite-simpson", "trapezoidal"])
+def test_jacobian_matches_numerical_derivative(scheme):
+    st = configs.double_pendulum(3, scheme)
+    nlp = OracleNLP(st.problem.create_rep(), st.solver.options())
+    x = nlp.random_iterate(np.random.default_rng(2).uniform(-1, 1, nlp.n))
+    x[1] = 1.5
+    ir, jc = nlp.jac_structure()
+    J = np.zeros((nlp.m, nlp.n))
+    J[ir, jc] = nlp.eval_jac_g(x)
+    Jn = _numjac(nlp.eval_g, x, range(nlp.n))
+    # central FD at h=1e-8 carries ~eps*|f|/h rounding noise
+    assert np.allclose(J, Jn, rtol=1e-5, atol=1e-6)
+
+
+def test_grad_f_matches_numerical_derivative():
+    st = configs.double_pendulum(3)
+    nlp = OracleNLP(st.problem.create_rep(), st.solver.options())
+    x = nlp.random_iterate(np.random.default_rng(4).uniform(-1, 1, nlp.n))
+    x[1] = 1.5
+    gn = _numjac(lambda z: np.array([nlp.eval_f(z)]), x, range(nlp.n))[0]
+    assert np.allclose(nlp.eval_grad_f(x), gn, rtol=1e-6, atol=1e-7)
+
+
+def _golden_iterate(nlp, rep):
+    d = np.load(__import__("os").path.join(__import__("os").path.dirname(__file__),
+                                           "golden", "std_testMocoTrackGait10dof18musc_solution.npz"))
+    labels, data = list(d["labels"]), d["data"]
+    col = {l: i for i, l in enumerate(labels)}
+    G, NS, NC = nlp.G, nlp.NS, nlp.NC
+    x = np.zeros(nlp.n)
+    x[0], x[1] = data[0, 0], data[-1, 0]
+    for k in range(G):
+        for s, n in enumerate(rep.state_names):
+            x[2 + k * NS + s] = data[k, col[n]]
+        for j, n in enumerate(rep.control_names):
+            x[2 + NS * G + k * NC + j] = data[k, col[n]]
+    return x, labels
+
+
+def test_golden_gait_solution_order_and_defects():
+    """Moco/Tests/std_testMocoTrackGait10dof18musc_solution.sto (MocoTrack
+    gait10dof18musc, reserves, GRF, HS N=65, converged with constraint
+    tolerance 1e-2, MocoTrack.cpp:107-109): state/control order must equal
+    the file's column order, and the reference's converged iterate must
+    satisfy our defects to that tolerance (pins multibody dynamics, the knee
+    CustomJoint splines, reserves and the ground reactions)."""
+    m = configs.gait10dof18musc_model(muscles=False)
+    p = MocoProblem(m)
+    p.set_time_bounds(0.01, 1.3)
+    p.add_goal(MocoControlGoal(weight=0.001))
+    rep = p.create_rep()
+    nlp = OracleNLP(rep, MocoHipSolver(num_mesh_intervals=65).options())
+    x, labels = _golden_iterate(nlp, rep)
+    assert labels[1:] == rep.state_names + rep.control_names
+    g = nlp.eval_g(x)
+    assert np.abs(g).max() < 1e-2
+    # and a 1% heavier femur or a 1% shorter knee spline is detected
+    m.bodies["femur_r"].mass *= 1.5
+    p2 = MocoProblem(m)
+    p2.set_time_bounds(0.01, 1.3)
+    nlp2 = OracleNLP(p2.create_rep(), MocoHipSolver(num_mesh_intervals=65).options())
+    assert np.abs(nlp2.eval_g(x)).max() > 1e-2
