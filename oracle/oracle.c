@@ -21,6 +21,14 @@
 #include <omp.h>
 #endif
 
+/* Scalar type of the model evaluation.  The FLOP-counting build
+ * (oracle/flopcount.cpp) compiles this file as C++ with a counting type. */
+#ifndef ORACLE_REAL
+typedef double real;
+#else
+typedef ORACLE_REAL real;
+#endif
+
 static __thread char g_err[512];
 const char* orc_last_error(void) { return g_err; }
 static int fail(int code, const char* fmt, ...) {
@@ -34,42 +42,42 @@ static int fail(int code, const char* fmt, ...) {
 /* ======================================================================== */
 /* Small 3-vector / 3x3 helpers (row-major matrices).                        */
 /* ======================================================================== */
-typedef struct { double w[3], v[3]; } sv6; /* spatial vector about ground origin */
+typedef struct { real w[3], v[3]; } sv6; /* spatial vector about ground origin */
 
-static void mat_mul(const double* A, const double* B, double* C) {
-    double T[9];
+static void mat_mul(const real* A, const real* B, real* C) {
+    real T[9];
     for (int i = 0; i < 3; ++i)
         for (int j = 0; j < 3; ++j)
             T[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] +
                            A[3 * i + 2] * B[6 + j];
     memcpy(C, T, sizeof T);
 }
-static void mat_mul_bt(const double* A, const double* B, double* C) { /* A*B^T */
-    double T[9];
+static void mat_mul_bt(const real* A, const real* B, real* C) { /* A*B^T */
+    real T[9];
     for (int i = 0; i < 3; ++i)
         for (int j = 0; j < 3; ++j)
             T[3 * i + j] = A[3 * i] * B[3 * j] + A[3 * i + 1] * B[3 * j + 1] +
                            A[3 * i + 2] * B[3 * j + 2];
     memcpy(C, T, sizeof T);
 }
-static void mat_vec(const double* A, const double* x, double* y) {
-    double t0 = A[0] * x[0] + A[1] * x[1] + A[2] * x[2];
-    double t1 = A[3] * x[0] + A[4] * x[1] + A[5] * x[2];
-    double t2 = A[6] * x[0] + A[7] * x[1] + A[8] * x[2];
+static void mat_vec(const real* A, const real* x, real* y) {
+    real t0 = A[0] * x[0] + A[1] * x[1] + A[2] * x[2];
+    real t1 = A[3] * x[0] + A[4] * x[1] + A[5] * x[2];
+    real t2 = A[6] * x[0] + A[7] * x[1] + A[8] * x[2];
     y[0] = t0; y[1] = t1; y[2] = t2;
 }
-static void cross(const double* a, const double* b, double* c) {
-    double t0 = a[1] * b[2] - a[2] * b[1];
-    double t1 = a[2] * b[0] - a[0] * b[2];
-    double t2 = a[0] * b[1] - a[1] * b[0];
+static void cross(const real* a, const real* b, real* c) {
+    real t0 = a[1] * b[2] - a[2] * b[1];
+    real t1 = a[2] * b[0] - a[0] * b[2];
+    real t2 = a[0] * b[1] - a[1] * b[0];
     c[0] = t0; c[1] = t1; c[2] = t2;
 }
-static double dot3(const double* a, const double* b) {
+static real dot3(const real* a, const real* b) {
     return a[0] * b[0] + a[1] * b[1] + a[2] * b[2];
 }
 /* Rodrigues rotation about unit axis a by angle t. */
-static void axis_rotation(const double* a, double t, double* R) {
-    double c = cos(t), s = sin(t), k = 1.0 - c;
+static void axis_rotation(const real* a, real t, real* R) {
+    real c = cos(t), s = sin(t), k = 1.0 - c;
     R[0] = c + k * a[0] * a[0];
     R[1] = k * a[0] * a[1] - s * a[2];
     R[2] = k * a[0] * a[2] + s * a[1];
@@ -83,7 +91,7 @@ static void axis_rotation(const double* a, double t, double* R) {
 /* Spatial motion cross product (w,v) x_m (w2,v2). */
 static sv6 cross_m(sv6 a, sv6 b) {
     sv6 r;
-    double t[3];
+    real t[3];
     cross(a.w, b.w, r.w);
     cross(a.w, b.v, r.v);
     cross(a.v, b.w, t);
@@ -93,22 +101,22 @@ static sv6 cross_m(sv6 a, sv6 b) {
 /* Spatial force cross product (w,v) x_f (n,f). */
 static sv6 cross_f(sv6 a, sv6 f) {
     sv6 r;
-    double t[3];
+    real t[3];
     cross(a.w, f.w, r.w);
     cross(a.v, f.v, t);
     for (int i = 0; i < 3; ++i) r.w[i] += t[i];
     cross(a.w, f.v, r.v);
     return r;
 }
-static double sv_dot(sv6 m, sv6 f) { return dot3(m.w, f.w) + dot3(m.v, f.v); }
+static real sv_dot(sv6 m, sv6 f) { return dot3(m.w, f.w) + dot3(m.v, f.v); }
 
 /* Rigid-body inertia about the ground origin: mass, first moment h = m c,
  * rotational inertia about the origin I_O (sym: xx yy zz xy xz yz). */
-typedef struct { double m, h[3], I[6]; } rbi;
+typedef struct { real m, h[3], I[6]; } rbi;
 static sv6 rbi_apply(const rbi* I, sv6 x) {
     /* (I_O w + h x u, m u - h x w) */
     sv6 r;
-    double t[3];
+    real t[3];
     r.w[0] = I->I[0] * x.w[0] + I->I[3] * x.w[1] + I->I[4] * x.w[2];
     r.w[1] = I->I[3] * x.w[0] + I->I[1] * x.w[1] + I->I[5] * x.w[2];
     r.w[2] = I->I[4] * x.w[0] + I->I[5] * x.w[1] + I->I[2] * x.w[2];
@@ -184,7 +192,7 @@ static void simm_coefficients(int n, const double* x, const double* y,
 /* SimmSpline::interpolate (value, first, second derivative), with linear
  * extrapolation outside the knots. */
 static void simm_eval(int n, const double* x, const double* y, const double* b,
-        const double* c, const double* d, double t, double* out) {
+        const double* c, const double* d, real t, real* out) {
     if (n == 1) { out[0] = y[0]; out[1] = out[2] = 0.0; return; }
     if (t < x[0]) {
         out[0] = y[0] + (t - x[0]) * b[0]; out[1] = b[0]; out[2] = 0.0; return;
@@ -206,7 +214,7 @@ static void simm_eval(int n, const double* x, const double* y, const double* b,
             else break;
         }
     }
-    double dx = t - x[k];
+    real dx = t - x[k];
     out[0] = y[k] + dx * (b[k] + dx * (c[k] + dx * d[k]));
     out[1] = b[k] + dx * (2.0 * c[k] + 3.0 * dx * d[k]);
     out[2] = 2.0 * c[k] + 6.0 * dx * d[k];
@@ -606,12 +614,12 @@ int orc_get_random_iterate(const orc_ctx* c, const double* rnd, double* x) {
 /* ======================================================================== */
 /* Model evaluation.                                                         */
 /* ======================================================================== */
-static void eval_function(const orc_ctx* c, int f, const double* q, double* out) {
+static void eval_function(const orc_ctx* c, int f, const real* q, real* out) {
     const mh_function* F = &c->funcs[f];
     switch (F->kind) {
     case MH_FN_CONSTANT: out[0] = F->a; out[1] = out[2] = 0.0; return;
     case MH_FN_LINEAR: {
-        double s = F->scale;
+        real s = F->scale;
         out[0] = s * (F->a * q[F->coord] + F->b);
         out[1] = s * F->a; out[2] = 0.0; return;
     }
@@ -624,19 +632,21 @@ static void eval_function(const orc_ctx* c, int f, const double* q, double* out)
     }
 }
 
+#ifndef ORACLE_COUNTING
 int orc_eval_function(orc_ctx* c, int f, double qv, double* out3) {
     if (f < 0 || f >= c->P.model.nfunctions) return fail(MH_ERR_INVALID, "bad function");
-    double* q = (double*)calloc((size_t)c->NQ + 1, sizeof(double));
+    real* q = (real*)calloc((size_t)c->NQ + 1, sizeof(real));
     int crd = c->funcs[f].coord;
     if (crd >= 0) q[crd] = qv;
     eval_function(c, f, q, out3);
     free(q);
     return MH_OK;
 }
+#endif
 
 /* Piecewise-polynomial data table (GCVSpline restated as its piecewise
  * polynomial). Column value at t. */
-static double table_eval(const orc_ctx* c, int ti, int col, double t) {
+static real table_eval(const orc_ctx* c, int ti, int col, real t) {
     const mh_table* T = &c->tabs[ti];
     const double* br = c->brk + T->break_begin;
     int s;
@@ -651,8 +661,8 @@ static double table_eval(const orc_ctx* c, int ti, int col, double t) {
         s = lo;
     }
     const double* cf = c->coef + T->coef_begin + ((int64_t)s * T->ncol + col) * (T->degree + 1);
-    double dt = t - br[s];
-    double v = cf[T->degree];
+    real dt = t - br[s];
+    real v = cf[T->degree];
     for (int k = T->degree - 1; k >= 0; --k) v = v * dt + cf[k];
     return v;
 }
@@ -670,47 +680,48 @@ static const double DGF_d1 = -0.3211346127989808, DGF_d2 = -8.149, DGF_d3 = -0.3
                     DGF_d4 = 0.8825327733249912;
 static const double DGF_minNormFiberLength = 0.2;
 
-static double gaussian_like(double x, double b1, double b2, double b3, double b4) {
-    double num = (x - b2) * (x - b2);
-    double den = (b3 + b4 * x) * (b3 + b4 * x);
+static real gaussian_like(real x, double b1, double b2, double b3, double b4) {
+    real num = (x - b2) * (x - b2);
+    real den = (b3 + b4 * x) * (b3 + b4 * x);
     return b1 * exp(-0.5 * num / den);
 }
-static double dgf_fal(const mh_muscle* mu, double l) {
-    double scale = mu->active_force_width_scale;
-    double x = (l - 1.0) / scale + 1.0;
+static real dgf_fal(const mh_muscle* mu, real l) {
+    real scale = mu->active_force_width_scale;
+    real x = (l - 1.0) / scale + 1.0;
     return gaussian_like(x, DGF_b11, DGF_b21, DGF_b31, DGF_b41) +
            gaussian_like(x, DGF_b12, DGF_b22, DGF_b32, DGF_b42) +
            gaussian_like(x, DGF_b13, DGF_b23, DGF_b33, DGF_b43);
 }
-static double dgf_fv(double v) {
-    double tv = DGF_d2 * v + DGF_d3;
-    double arg = tv + sqrt(tv * tv + 1.0);
+static real dgf_fv(real v) {
+    real tv = DGF_d2 * v + DGF_d3;
+    real arg = tv + sqrt(tv * tv + 1.0);
     return DGF_d1 * log(arg) + DGF_d4;
 }
-static double dgf_fv_inv(double fv) {
+static real dgf_fv_inv(real fv) {
     return (sinh(1.0 / DGF_d1 * (fv - DGF_d4)) - DGF_d3) / DGF_d2;
 }
-static double dgf_fpe(const mh_muscle* mu, double l) {
+static real dgf_fpe(const mh_muscle* mu, real l) {
     if (mu->ignore_passive_fiber_force) return 0.0;
-    double e0 = mu->passive_fiber_strain_at_one_norm_force;
-    double offset = exp(DGF_kPE * (DGF_minNormFiberLength - 1.0) / e0);
-    double denom = exp(DGF_kPE) - offset;
+    real e0 = mu->passive_fiber_strain_at_one_norm_force;
+    real offset = exp(DGF_kPE * (DGF_minNormFiberLength - 1.0) / e0);
+    real denom = exp(DGF_kPE) - offset;
     return (exp(DGF_kPE * (l - 1.0) / e0) - offset) / denom;
 }
 static double dgf_kT(const mh_muscle* mu) {
     return log((1.0 + DGF_c3) / DGF_c1) / (1.0 + mu->tendon_strain_at_one_norm_force - DGF_c2);
 }
-static double dgf_ft(const mh_muscle* mu, double l) {
+static real dgf_ft(const mh_muscle* mu, real l) {
     return DGF_c1 * exp(dgf_kT(mu) * (l - DGF_c2)) - DGF_c3;
 }
-static double dgf_ft_deriv(const mh_muscle* mu, double l) {
+static real dgf_ft_deriv(const mh_muscle* mu, real l) {
     double kT = dgf_kT(mu);
     return DGF_c1 * kT * exp(kT * (l - DGF_c2));
 }
-static double dgf_ft_inv(const mh_muscle* mu, double f) {
+static real dgf_ft_inv(const mh_muscle* mu, real f) {
     return log((1.0 / DGF_c1) * (f + DGF_c3)) / dgf_kT(mu) + DGF_c2;
 }
 
+#ifndef ORACLE_COUNTING
 double orc_dgf_curve(const mh_muscle* mu, int which, double x) {
     switch (which) {
     case 0: return dgf_fal(mu, x);
@@ -723,57 +734,58 @@ double orc_dgf_curve(const mh_muscle* mu, int which, double x) {
     default: return NAN;
     }
 }
+#endif
 
 /* Tendon force and auxiliary derivatives of one DGF muscle
  * (DeGrooteFregly2016Muscle.cpp:186-233, 240-425). */
-static void dgf_muscle(const orc_ctx* c, const mh_muscle* mu, double LMT, double VMT,
-        double activation, double excitation, int has_act, double normTendonForce,
-        int compliant, double* tendonForce, double* adot, double* ftdot) {
+static void dgf_muscle(const orc_ctx* c, const mh_muscle* mu, real LMT, real VMT,
+        real activation, real excitation, int has_act, real normTendonForce,
+        int compliant, real* tendonForce, real* adot, real* ftdot) {
     /* calcMuscleLengthInfoHelper (:240-275) */
-    double normTendonLength = compliant ? dgf_ft_inv(mu, normTendonForce) : 1.0;
-    double tendonLength = mu->tendon_slack_length * normTendonLength;
-    double fiberWidth = mu->optimal_fiber_length * sin(mu->pennation_angle_at_optimal);
-    double squareFiberWidth = fiberWidth * fiberWidth;
-    double fiberLengthAlongTendon = LMT - tendonLength;
-    double fiberLength = sqrt(fiberLengthAlongTendon * fiberLengthAlongTendon + squareFiberWidth);
-    double normFiberLength = fiberLength / mu->optimal_fiber_length;
-    double cosPenn = fiberLengthAlongTendon / fiberLength;
-    double fPE = dgf_fpe(mu, normFiberLength);
-    double fAL = dgf_fal(mu, normFiberLength);
-    double vmax = mu->max_contraction_velocity * mu->optimal_fiber_length;
+    real normTendonLength = compliant ? dgf_ft_inv(mu, normTendonForce) : 1.0;
+    real tendonLength = mu->tendon_slack_length * normTendonLength;
+    real fiberWidth = mu->optimal_fiber_length * sin(mu->pennation_angle_at_optimal);
+    real squareFiberWidth = fiberWidth * fiberWidth;
+    real fiberLengthAlongTendon = LMT - tendonLength;
+    real fiberLength = sqrt(fiberLengthAlongTendon * fiberLengthAlongTendon + squareFiberWidth);
+    real normFiberLength = fiberLength / mu->optimal_fiber_length;
+    real cosPenn = fiberLengthAlongTendon / fiberLength;
+    real fPE = dgf_fpe(mu, normFiberLength);
+    real fAL = dgf_fal(mu, normFiberLength);
+    real vmax = mu->max_contraction_velocity * mu->optimal_fiber_length;
     /* calcFiberVelocityInfoHelper (:277-323) */
-    double normFiberVelocity, fV, normTendonVelocity;
+    real normFiberVelocity, fV, normTendonVelocity;
     if (compliant) {
-        double normFiberForce = normTendonForce / cosPenn;
+        real normFiberForce = normTendonForce / cosPenn;
         fV = (normFiberForce - fPE) / (activation * fAL);
         normFiberVelocity = dgf_fv_inv(fV);
-        double fiberVelocity = normFiberVelocity * vmax;
-        double fiberVelocityAlongTendon = fiberVelocity / cosPenn;
-        double tendonVelocity = VMT - fiberVelocityAlongTendon;
+        real fiberVelocity = normFiberVelocity * vmax;
+        real fiberVelocityAlongTendon = fiberVelocity / cosPenn;
+        real tendonVelocity = VMT - fiberVelocityAlongTendon;
         normTendonVelocity = tendonVelocity / mu->tendon_slack_length;
     } else {
         normTendonVelocity = 0.0;
-        double tendonVelocity = mu->tendon_slack_length * normTendonVelocity;
-        double fiberVelocityAlongTendon = VMT - tendonVelocity;
-        double fiberVelocity = fiberVelocityAlongTendon * cosPenn;
+        real tendonVelocity = mu->tendon_slack_length * normTendonVelocity;
+        real fiberVelocityAlongTendon = VMT - tendonVelocity;
+        real fiberVelocity = fiberVelocityAlongTendon * cosPenn;
         normFiberVelocity = fiberVelocity / vmax;
         fV = dgf_fv(normFiberVelocity);
     }
     /* calcMuscleDynamicsInfoHelper (:325-425) via calcFiberForce (.h:482-503) */
-    double Fmax = mu->max_isometric_force;
-    double activeFiberForce = Fmax * (activation * fAL * fV);
-    double conPassive = Fmax * fPE;
-    double nonConPassive = Fmax * mu->fiber_damping * normFiberVelocity;
-    double totalFiberForce = activeFiberForce + conPassive + nonConPassive;
+    real Fmax = mu->max_isometric_force;
+    real activeFiberForce = Fmax * (activation * fAL * fV);
+    real conPassive = Fmax * fPE;
+    real nonConPassive = Fmax * mu->fiber_damping * normFiberVelocity;
+    real totalFiberForce = activeFiberForce + conPassive + nonConPassive;
     if (compliant) *tendonForce = Fmax * normTendonForce;
     else *tendonForce = totalFiberForce * cosPenn;
     /* computeStateVariableDerivatives (:186-233) */
     if (has_act) {
-        double timeConstFactor = 0.5 + 1.5 * activation;
-        double tempAct = 1.0 / (c->tau_act * timeConstFactor);
-        double tempDeact = timeConstFactor / c->tau_deact;
-        double f = 0.5 * tanh(0.1 * (excitation - activation));
-        double timeConst = tempAct * (f + 0.5) + tempDeact * (-f + 0.5);
+        real timeConstFactor = 0.5 + 1.5 * activation;
+        real tempAct = 1.0 / (c->tau_act * timeConstFactor);
+        real tempDeact = timeConstFactor / c->tau_deact;
+        real f = 0.5 * tanh(0.1 * (excitation - activation));
+        real timeConst = tempAct * (f + 0.5) + tempDeact * (-f + 0.5);
         *adot = timeConst * (excitation - activation);
     }
     if (compliant) *ftdot = normTendonVelocity * dgf_ft_deriv(mu, normTendonLength);
@@ -781,34 +793,34 @@ static void dgf_muscle(const orc_ctx* c, const mh_muscle* mu, double LMT, double
 
 /* Workspace for one DAE evaluation. */
 typedef struct {
-    double *R, *p;    /* body pose (world): 9, 3 per body                  */
+    real *R, *p;    /* body pose (world): 9, 3 per body                  */
     sv6 *V, *A, *F;   /* velocity, bias acceleration, net force per body   */
     sv6* S;           /* motion subspace per coordinate                    */
     rbi* I;           /* world inertia per body; then composite            */
-    double* M;        /* NQ x NQ mass matrix                               */
-    double* tau;      /* generalized forces                                */
-    double* ppos;     /* path point world positions (3 per point)          */
-    double* pvel;
+    real* M;        /* NQ x NQ mass matrix                               */
+    real* tau;      /* generalized forces                                */
+    real* ppos;     /* path point world positions (3 per point)          */
+    real* pvel;
     int* pact;
-    double* fvals;    /* function value/d1/d2 per axis (3 per axis)        */
+    real* fvals;    /* function value/d1/d2 per axis (3 per axis)        */
 } dae_ws;
 
 static void ws_alloc(const orc_ctx* c, dae_ws* w) {
     const mh_model* M = &c->P.model;
     int nb = M->nbodies + 1;
-    w->R = (double*)malloc(sizeof(double) * 9 * (size_t)nb);
-    w->p = (double*)malloc(sizeof(double) * 3 * (size_t)nb);
+    w->R = (real*)malloc(sizeof(real) * 9 * (size_t)nb);
+    w->p = (real*)malloc(sizeof(real) * 3 * (size_t)nb);
     w->V = (sv6*)malloc(sizeof(sv6) * (size_t)nb);
     w->A = (sv6*)malloc(sizeof(sv6) * (size_t)nb);
     w->F = (sv6*)malloc(sizeof(sv6) * (size_t)nb);
     w->S = (sv6*)malloc(sizeof(sv6) * (size_t)(c->NQ + 1));
     w->I = (rbi*)malloc(sizeof(rbi) * (size_t)nb);
-    w->M = (double*)malloc(sizeof(double) * (size_t)(c->NQ * c->NQ + 1));
-    w->tau = (double*)malloc(sizeof(double) * (size_t)(c->NQ + 1));
-    w->ppos = (double*)malloc(sizeof(double) * 3 * (size_t)(M->npoints + 1));
-    w->pvel = (double*)malloc(sizeof(double) * 3 * (size_t)(M->npoints + 1));
+    w->M = (real*)malloc(sizeof(real) * (size_t)(c->NQ * c->NQ + 1));
+    w->tau = (real*)malloc(sizeof(real) * (size_t)(c->NQ + 1));
+    w->ppos = (real*)malloc(sizeof(real) * 3 * (size_t)(M->npoints + 1));
+    w->pvel = (real*)malloc(sizeof(real) * 3 * (size_t)(M->npoints + 1));
     w->pact = (int*)malloc(sizeof(int) * (size_t)(M->npoints + 1));
-    w->fvals = (double*)malloc(sizeof(double) * 3 * (size_t)(M->naxes + 1));
+    w->fvals = (real*)malloc(sizeof(real) * 3 * (size_t)(M->naxes + 1));
 }
 static void ws_free(dae_ws* w) {
     free(w->R); free(w->p); free(w->V); free(w->A); free(w->F); free(w->S); free(w->I);
@@ -818,7 +830,7 @@ static void ws_free(dae_ws* w) {
 /* Forward kinematics, velocities and velocity-product accelerations in the
  * ground frame (Simbody realizePosition/Velocity for FunctionBased
  * mobilizers; restated).  Body index b is stored at b+1; slot 0 = ground. */
-static void kinematics(const orc_ctx* c, const double* q, const double* u, dae_ws* w) {
+static void kinematics(const orc_ctx* c, const real* q, const real* u, dae_ws* w) {
     const mh_model* Mo = &c->P.model;
     static const double I3[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
     memcpy(w->R, I3, sizeof I3);
@@ -831,25 +843,28 @@ static void kinematics(const orc_ctx* c, const double* q, const double* u, dae_w
     for (int b = 0; b < Mo->nbodies; ++b) {
         const mh_body* B = &c->bodies[b];
         int ps = B->parent + 1, bs = b + 1;
-        const double* Rp = w->R + 9 * ps;
-        const double* pp = w->p + 3 * ps;
-        double RGF[9], pGF[3], t[3];
-        mat_mul(Rp, B->R_PF, RGF);
-        mat_vec(Rp, B->p_PF, t);
+        const real* Rp = w->R + 9 * ps;
+        const real* pp = w->p + 3 * ps;
+        real RGF[9], pGF[3], t[3];
+        real RPF[9], pPF[3], RBM[9], pBM[3];
+        for (int i = 0; i < 9; ++i) { RPF[i] = B->R_PF[i]; RBM[i] = B->R_BM[i]; }
+        for (int i = 0; i < 3; ++i) { pPF[i] = B->p_PF[i]; pBM[i] = B->p_BM[i]; }
+        mat_mul(Rp, RPF, RGF);
+        mat_vec(Rp, pPF, t);
         for (int i = 0; i < 3; ++i) pGF[i] = pp[i] + t[i];
         sv6 V = w->V[ps];
         sv6 Vpar = w->V[ps];
         sv6 A = w->A[ps];
         /* translations (axes fixed in F) */
-        double pFM[3] = {0, 0, 0};
+        real pFM[3] = {0, 0, 0};
         for (int a = B->axis_begin; a < B->axis_begin + B->axis_count; ++a) {
             const mh_axis* X = &c->axes[a];
-            double* fv = w->fvals + 3 * a;
+            real* fv = w->fvals + 3 * a;
             eval_function(c, X->func, q, fv);
             if (X->type != MH_AXIS_TRANSLATION) continue;
             for (int i = 0; i < 3; ++i) pFM[i] += fv[0] * X->dir[i];
         }
-        double oM[3];
+        real oM[3];
         mat_vec(RGF, pFM, t);
         for (int i = 0; i < 3; ++i) oM[i] = pGF[i] + t[i];
         for (int a = B->axis_begin; a < B->axis_begin + B->axis_count; ++a) {
@@ -857,13 +872,14 @@ static void kinematics(const orc_ctx* c, const double* q, const double* u, dae_w
             if (X->type != MH_AXIS_TRANSLATION) continue;
             const mh_function* F = &c->funcs[X->func];
             if (F->kind == MH_FN_CONSTANT) continue;
-            const double* fv = w->fvals + 3 * a;
-            double uj = u[F->coord];
+            const real* fv = w->fvals + 3 * a;
+            real uj = u[F->coord];
             sv6 s;
             s.w[0] = s.w[1] = s.w[2] = 0.0;
-            mat_vec(RGF, X->dir, s.v);
+            real dir[3] = {X->dir[0], X->dir[1], X->dir[2]};
+            mat_vec(RGF, dir, s.v);
             sv6 sd = cross_m(Vpar, s);
-            double thd = fv[1] * uj, thdd = fv[2] * uj * uj;
+            real thd = fv[1] * uj, thdd = fv[2] * uj * uj;
             for (int i = 0; i < 3; ++i) {
                 V.w[i] += s.w[i] * thd; V.v[i] += s.v[i] * thd;
                 A.w[i] += sd.w[i] * thd + s.w[i] * thdd;
@@ -873,22 +889,23 @@ static void kinematics(const orc_ctx* c, const double* q, const double* u, dae_w
             }
         }
         /* rotations (body-fixed sequence about the M origin) */
-        double Rcur[9];
+        real Rcur[9];
         memcpy(Rcur, I3, sizeof I3);
         for (int a = B->axis_begin; a < B->axis_begin + B->axis_count; ++a) {
             const mh_axis* X = &c->axes[a];
             if (X->type != MH_AXIS_ROTATION) continue;
             const mh_function* F = &c->funcs[X->func];
-            const double* fv = w->fvals + 3 * a;
+            const real* fv = w->fvals + 3 * a;
             if (F->kind != MH_FN_CONSTANT) {
-                double RGc[9];
+                real RGc[9];
                 mat_mul(RGF, Rcur, RGc);
                 sv6 s;
-                mat_vec(RGc, X->dir, s.w);
+                real dir[3] = {X->dir[0], X->dir[1], X->dir[2]};
+                mat_vec(RGc, dir, s.w);
                 cross(oM, s.w, s.v);
                 sv6 sd = cross_m(V, s);
-                double uj = u[F->coord];
-                double thd = fv[1] * uj, thdd = fv[2] * uj * uj;
+                real uj = u[F->coord];
+                real thd = fv[1] * uj, thdd = fv[2] * uj * uj;
                 for (int i = 0; i < 3; ++i) {
                     V.w[i] += s.w[i] * thd; V.v[i] += s.v[i] * thd;
                     A.w[i] += sd.w[i] * thd + s.w[i] * thdd;
@@ -897,16 +914,17 @@ static void kinematics(const orc_ctx* c, const double* q, const double* u, dae_w
                     w->S[F->coord].v[i] += fv[1] * s.v[i];
                 }
             }
-            double Rk[9];
-            axis_rotation(X->dir, fv[0], Rk);
+            real Rk[9];
+            real adir[3] = {X->dir[0], X->dir[1], X->dir[2]};
+            axis_rotation(adir, fv[0], Rk);
             mat_mul(Rcur, Rk, Rcur);
         }
-        double RGM[9];
+        real RGM[9];
         mat_mul(RGF, Rcur, RGM);
-        double* RB = w->R + 9 * bs;
-        double* pB = w->p + 3 * bs;
-        mat_mul_bt(RGM, B->R_BM, RB);       /* R_GB = R_GM R_BM^T */
-        mat_vec(RB, B->p_BM, t);
+        real* RB = w->R + 9 * bs;
+        real* pB = w->p + 3 * bs;
+        mat_mul_bt(RGM, RBM, RB);       /* R_GB = R_GM R_BM^T */
+        mat_vec(RB, pBM, t);
         for (int i = 0; i < 3; ++i) pB[i] = oM[i] - t[i];
         w->V[bs] = V;
         w->A[bs] = A;
@@ -915,21 +933,21 @@ static void kinematics(const orc_ctx* c, const double* q, const double* u, dae_w
 
 /* Path point world positions and velocities (OpenSim GeometryPath current
  * path: inactive ConditionalPathPoints are skipped). */
-static void path_points(const orc_ctx* c, const double* q, const double* u, dae_ws* w) {
+static void path_points(const orc_ctx* c, const real* q, const real* u, dae_ws* w) {
     const mh_model* Mo = &c->P.model;
     for (int i = 0; i < Mo->npoints; ++i) {
         const mh_path_point* pt = &c->pts[i];
-        double loc[3] = {pt->loc[0], pt->loc[1], pt->loc[2]};
-        double dloc[3] = {0, 0, 0};
+        real loc[3] = {pt->loc[0], pt->loc[1], pt->loc[2]};
+        real dloc[3] = {0, 0, 0};
         w->pact[i] = 1;
         if (pt->kind == MH_PP_CONDITIONAL) {
-            double qv = q[pt->coord];
+            real qv = q[pt->coord];
             w->pact[i] = (qv >= pt->range[0] && qv <= pt->range[1]);
         } else if (pt->kind == MH_PP_MOVING) {
             int fs[3] = {pt->fx, pt->fy, pt->fz};
             for (int d = 0; d < 3; ++d) {
                 if (fs[d] < 0) continue;
-                double o[3];
+                real o[3];
                 eval_function(c, fs[d], q, o);
                 loc[d] = o[0];
                 const mh_function* F = &c->funcs[fs[d]];
@@ -937,11 +955,11 @@ static void path_points(const orc_ctx* c, const double* q, const double* u, dae_
             }
         }
         int bs = pt->body + 1;
-        const double* R = w->R + 9 * bs;
-        const double* p = w->p + 3 * bs;
-        double* P = w->ppos + 3 * i;
-        double* Vp = w->pvel + 3 * i;
-        double t[3], t2[3];
+        const real* R = w->R + 9 * bs;
+        const real* p = w->p + 3 * bs;
+        real* P = w->ppos + 3 * i;
+        real* Vp = w->pvel + 3 * i;
+        real t[3], t2[3];
         mat_vec(R, loc, t);
         for (int d = 0; d < 3; ++d) P[d] = p[d] + t[d];
         /* v = v_O + w x P + R dloc */
@@ -951,21 +969,21 @@ static void path_points(const orc_ctx* c, const double* q, const double* u, dae_
     }
 }
 
-static void muscle_length_speed(const orc_ctx* c, const dae_ws* w, int im, double* len, double* spd) {
+static void muscle_length_speed(const orc_ctx* c, const dae_ws* w, int im, real* len, real* spd) {
     const mh_muscle* mu = &c->mus[im];
-    double L = 0.0, S = 0.0;
+    real L = 0.0, S = 0.0;
     int prev = -1;
     for (int i = mu->point_begin; i < mu->point_begin + mu->point_count; ++i) {
         if (!w->pact[i]) continue;
         if (prev >= 0) {
-            const double* a = w->ppos + 3 * prev;
-            const double* b = w->ppos + 3 * i;
-            double d[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]};
-            double l = sqrt(dot3(d, d));
+            const real* a = w->ppos + 3 * prev;
+            const real* b = w->ppos + 3 * i;
+            real d[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]};
+            real l = sqrt(dot3(d, d));
             L += l;
-            const double* va = w->pvel + 3 * prev;
-            const double* vb = w->pvel + 3 * i;
-            double dv[3] = {vb[0] - va[0], vb[1] - va[1], vb[2] - va[2]};
+            const real* va = w->pvel + 3 * prev;
+            const real* vb = w->pvel + 3 * i;
+            real dv[3] = {vb[0] - va[0], vb[1] - va[1], vb[2] - va[2]};
             S += dot3(d, dv) / l;
         }
         prev = i;
@@ -976,26 +994,26 @@ static void muscle_length_speed(const orc_ctx* c, const dae_ws* w, int im, doubl
 
 /* Apply point force Fp (world) at path point i to its body, including the
  * MovingPathPoint generalized-force term tau_j += Fp . (R dloc/dq_j). */
-static void apply_point_force(const orc_ctx* c, dae_ws* w, const double* q, int i, const double* Fp) {
+static void apply_point_force(const orc_ctx* c, dae_ws* w, const real* q, int i, const real* Fp) {
     const mh_path_point* pt = &c->pts[i];
     int bs = pt->body + 1;
     if (pt->body >= 0) {
-        double t[3];
+        real t[3];
         cross(w->ppos + 3 * i, Fp, t);
         for (int d = 0; d < 3; ++d) { w->F[bs].w[d] -= t[d]; w->F[bs].v[d] -= Fp[d]; }
         /* F[] holds (I a + v x* I v - f_ext): external forces subtract. */
     }
     if (pt->kind == MH_PP_MOVING && pt->body >= 0) {
         int fs[3] = {pt->fx, pt->fy, pt->fz};
-        const double* R = w->R + 9 * bs;
+        const real* R = w->R + 9 * bs;
         for (int d = 0; d < 3; ++d) {
             if (fs[d] < 0) continue;
             const mh_function* F = &c->funcs[fs[d]];
             if (F->kind == MH_FN_CONSTANT) continue;
-            double o[3];
+            real o[3];
             eval_function(c, fs[d], q, o);
             /* R * (e_d * o[1]) dotted with Fp */
-            double g = (R[0 + d] * Fp[0] + R[3 + d] * Fp[1] + R[6 + d] * Fp[2]) * o[1];
+            real g = (R[0 + d] * Fp[0] + R[3 + d] * Fp[1] + R[6 + d] * Fp[2]) * o[1];
             w->tau[F->coord] += g;
         }
     }
@@ -1003,35 +1021,36 @@ static void apply_point_force(const orc_ctx* c, dae_ws* w, const double* q, int 
 
 /* The explicit per-point DAE (MocoCasOCProblem::calcMultibodySystemExplicit,
  * MocoCasOCProblem.h:203-244): time, states, controls -> udot, zdot. */
-static void eval_dae_point(const orc_ctx* c, dae_ws* w, double time, const double* x,
-        const double* ctrl, double* out) {
+static void eval_dae_point(const orc_ctx* c, dae_ws* w, real time, const real* x,
+        const real* ctrl, real* out) {
     const mh_model* Mo = &c->P.model;
     int NQ = c->NQ;
-    const double* q = x;
-    const double* u = x + NQ;
+    const real* q = x;
+    const real* u = x + NQ;
     kinematics(c, q, u, w);
     path_points(c, q, u, w);
     /* Body inertias in ground about the origin; RNEA body forces. */
     for (int b = 0; b < Mo->nbodies; ++b) {
         const mh_body* B = &c->bodies[b];
         int bs = b + 1;
-        const double* R = w->R + 9 * bs;
-        const double* p = w->p + 3 * bs;
-        double cw[3], t[3];
-        mat_vec(R, B->com, t);
+        const real* R = w->R + 9 * bs;
+        const real* p = w->p + 3 * bs;
+        real cw[3], t[3];
+        real com[3] = {B->com[0], B->com[1], B->com[2]};
+        mat_vec(R, com, t);
         for (int i = 0; i < 3; ++i) cw[i] = p[i] + t[i];
         /* I_c in ground: R Ib R^T */
-        double Ib[9] = {B->inertia[0], B->inertia[3], B->inertia[4],
+        real Ib[9] = {B->inertia[0], B->inertia[3], B->inertia[4],
                         B->inertia[3], B->inertia[1], B->inertia[5],
                         B->inertia[4], B->inertia[5], B->inertia[2]};
-        double T1[9], Ig[9];
+        real T1[9], Ig[9];
         mat_mul(R, Ib, T1);
         mat_mul_bt(T1, R, Ig);
         rbi* I = &w->I[bs];
-        double m = B->mass;
+        real m = B->mass;
         I->m = m;
         for (int i = 0; i < 3; ++i) I->h[i] = m * cw[i];
-        double c2 = dot3(cw, cw);
+        real c2 = dot3(cw, cw);
         I->I[0] = Ig[0] + m * (c2 - cw[0] * cw[0]);
         I->I[1] = Ig[4] + m * (c2 - cw[1] * cw[1]);
         I->I[2] = Ig[8] + m * (c2 - cw[2] * cw[2]);
@@ -1048,7 +1067,7 @@ static void eval_dae_point(const orc_ctx* c, dae_ws* w, double time, const doubl
     }
     for (int j = 0; j < NQ; ++j) w->tau[j] = 0.0;
     /* Coordinate actuators and muscles (controls in actuator order). */
-    double* zdot = out + NQ;
+    real* zdot = out + NQ;
     for (int ia = 0; ia < Mo->nactuators; ++ia) {
         const mh_actuator* A = &c->acts[ia];
         if (A->kind == MH_ACT_COORDINATE) {
@@ -1057,13 +1076,13 @@ static void eval_dae_point(const orc_ctx* c, dae_ws* w, double time, const doubl
     }
     for (int im = 0; im < Mo->nmuscles; ++im) {
         const mh_muscle* mu = &c->mus[im];
-        double L, V;
+        real L, V;
         muscle_length_speed(c, w, im, &L, &V);
-        double e = ctrl[c->mus_control[im]];
+        real e = ctrl[c->mus_control[im]];
         int sa = c->mus_act_state[im], sf = c->mus_ftn_state[im];
-        double a = sa >= 0 ? x[sa] : e;
-        double ftn = sf >= 0 ? x[sf] : NAN;
-        double T, adot = 0, ftdot = 0;
+        real a = sa >= 0 ? x[sa] : e;
+        real ftn = sf >= 0 ? x[sf] : NAN;
+        real T, adot = 0, ftdot = 0;
         dgf_muscle(c, mu, L, V, a, e, sa >= 0, ftn, sf >= 0, &T, &adot, &ftdot);
         if (sa >= 0) zdot[sa - 2 * NQ] = adot;
         if (sf >= 0) zdot[sf - 2 * NQ] = ftdot;
@@ -1072,11 +1091,11 @@ static void eval_dae_point(const orc_ctx* c, dae_ws* w, double time, const doubl
         for (int i = mu->point_begin; i < mu->point_begin + mu->point_count; ++i) {
             if (!w->pact[i]) continue;
             if (prev >= 0) {
-                const double* pa = w->ppos + 3 * prev;
-                const double* pb = w->ppos + 3 * i;
-                double d[3] = {pb[0] - pa[0], pb[1] - pa[1], pb[2] - pa[2]};
-                double l = sqrt(dot3(d, d));
-                double Fa[3], Fb[3];
+                const real* pa = w->ppos + 3 * prev;
+                const real* pb = w->ppos + 3 * i;
+                real d[3] = {pb[0] - pa[0], pb[1] - pa[1], pb[2] - pa[2]};
+                real l = sqrt(dot3(d, d));
+                real Fa[3], Fb[3];
                 for (int k = 0; k < 3; ++k) { Fa[k] = T * d[k] / l; Fb[k] = -Fa[k]; }
                 apply_point_force(c, w, q, prev, Fa);
                 apply_point_force(c, w, q, i, Fb);
@@ -1087,14 +1106,14 @@ static void eval_dae_point(const orc_ctx* c, dae_ws* w, double time, const doubl
     /* External forces (ExternalForce, ground-expressed force and point). */
     for (int ie = 0; ie < Mo->nexternal; ++ie) {
         const mh_external_force* E = &c->ext[ie];
-        double Fv[3] = {0, 0, 0}, P[3], Tq[3] = {0, 0, 0};
+        real Fv[3] = {0, 0, 0}, P[3], Tq[3] = {0, 0, 0};
         int bs = E->body + 1;
         for (int d = 0; d < 3; ++d) {
             if (E->force_col >= 0) Fv[d] = table_eval(c, E->table, E->force_col + d, time);
             P[d] = E->point_col >= 0 ? table_eval(c, E->table, E->point_col + d, time) : w->p[3 * bs + d];
             if (E->torque_col >= 0) Tq[d] = table_eval(c, E->table, E->torque_col + d, time);
         }
-        double t[3];
+        real t[3];
         cross(P, Fv, t);
         for (int d = 0; d < 3; ++d) { w->F[bs].w[d] -= t[d] + Tq[d]; w->F[bs].v[d] -= Fv[d]; }
     }
@@ -1127,7 +1146,7 @@ static void eval_dae_point(const orc_ctx* c, dae_ws* w, double time, const doubl
             int anc = b;
             while (anc >= 0 && anc != bj) anc = c->bodies[anc].parent;
             if (anc == bj) {
-                double v = sv_dot(w->S[j], Fi);
+                real v = sv_dot(w->S[j], Fi);
                 w->M[i * NQ + j] = v;
                 w->M[j * NQ + i] = v;
             } else {
@@ -1138,31 +1157,32 @@ static void eval_dae_point(const orc_ctx* c, dae_ws* w, double time, const doubl
         }
     }
     /* Cholesky M = L L^T (in place, lower) and solve. */
-    double* L = w->M;
+    real* L = w->M;
     for (int j = 0; j < NQ; ++j) {
-        double s = L[j * NQ + j];
+        real s = L[j * NQ + j];
         for (int k = 0; k < j; ++k) s -= L[j * NQ + k] * L[j * NQ + k];
-        double d = sqrt(s);
+        real d = sqrt(s);
         L[j * NQ + j] = d;
         for (int i = j + 1; i < NQ; ++i) {
-            double t = L[i * NQ + j];
+            real t = L[i * NQ + j];
             for (int k = 0; k < j; ++k) t -= L[i * NQ + k] * L[j * NQ + k];
             L[i * NQ + j] = t / d;
         }
     }
-    double* y = out; /* udot */
+    real* y = out; /* udot */
     for (int i = 0; i < NQ; ++i) {
-        double t = w->tau[i];
+        real t = w->tau[i];
         for (int k = 0; k < i; ++k) t -= L[i * NQ + k] * y[k];
         y[i] = t / L[i * NQ + i];
     }
     for (int i = NQ - 1; i >= 0; --i) {
-        double t = y[i];
+        real t = y[i];
         for (int k = i + 1; k < NQ; ++k) t -= L[k * NQ + i] * y[k];
         y[i] = t / L[i * NQ + i];
     }
 }
 
+#ifndef ORACLE_COUNTING
 int orc_muscle_length_speed(orc_ctx* c, int im, const double* q, const double* u, double* out) {
     if (im < 0 || im >= c->P.model.nmuscles) return fail(MH_ERR_INVALID, "bad muscle");
     dae_ws w;
@@ -1182,7 +1202,7 @@ int orc_eval_dae(orc_ctx* c, int32_t np, const double* in, double* out) {
         ws_alloc(c, &w);
 #pragma omp for schedule(static)
         for (int k = 0; k < np; ++k) {
-            const double* p = in + (int64_t)k * NI;
+            const real* p = in + (int64_t)k * NI;
             eval_dae_point(c, &w, p[0], p + 1, p + 1 + c->NS, out + (int64_t)k * NO);
         }
         ws_free(&w);
@@ -1554,3 +1574,4 @@ int orc_eval_grad_f(orc_ctx* c, const double* x, double* grad) {
     free(in);
     return MH_OK;
 }
+#endif /* ORACLE_COUNTING */
