@@ -318,6 +318,15 @@ int mh_eval_jac_g_device(mh_ctx* ctx, const double* x_dev,
 int mh_eval_dae(mh_ctx* ctx, int32_t npoints, const double* inputs,
         double* outputs);
 
+/* Identity of the device back end serving this context: the generic DAE
+ * interpreter or a model-specialized (generated) kernel, the FP64 operation
+ * count of one generated DAE evaluation (0 for generic), and the model hash
+ * used to select it. */
+int mh_get_backend(const mh_ctx* ctx, char* name, int32_t name_len,
+        double* flops_per_eval, uint64_t* model_hash);
+/* FNV-1a hash of everything the per-point DAE depends on (host only). */
+int mh_model_hash(const mh_model* model, uint64_t* hash);
+
 /* Timing of the last evaluation on the context stream (HIP events), in ms:
  * [0] whole call, [1] DAE/FD kernel, [2] assembly kernel. */
 int mh_last_timings(const mh_ctx* ctx, double* ms3);

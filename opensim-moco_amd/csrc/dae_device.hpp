@@ -631,3 +631,53 @@ __device__ void dae_eval(const DevModel& M, Work<MB, MQ, MP>& w, double time, co
 }
 
 }  // namespace mh
+
+namespace mh {
+// ---- helpers used by generated (model-specialized) DAE code ---------------
+// SimmSpline with a compile-time knot count: interval by an unrolled scan
+// (no data-dependent loop), SIMM end handling and linear extrapolation.
+template <int N>
+__device__ __forceinline__ void simm_eval_n(const DevModel& M, int kb, double t, double& v,
+        double& d1, double& d2) {
+    const double* __restrict__ x = M.kx + kb;
+    const double* __restrict__ y = M.ky + kb;
+    const double* __restrict__ b = M.kb + kb;
+    const double* __restrict__ c = M.kc + kb;
+    const double* __restrict__ d = M.kd + kb;
+    if (N == 1) { v = y[0]; d1 = 0.0; d2 = 0.0; return; }
+    int k = 0;
+#pragma unroll
+    for (int i = 1; i < N - 1; ++i) k += (t >= x[i]) ? 1 : 0;
+    if (fabs(t - x[0]) <= 2e-13) k = 0;
+    else if (fabs(t - x[N - 1]) <= 2e-13) k = N - 1;
+    const double dx = t - x[k];
+    const double bk = b[k], ck = c[k], dk = d[k];
+    v = y[k] + dx * (bk + dx * (ck + dx * dk));
+    d1 = bk + dx * (2.0 * ck + 3.0 * dx * dk);
+    d2 = 2.0 * ck + 6.0 * dx * dk;
+    if (t < x[0]) { v = y[0] + (t - x[0]) * b[0]; d1 = b[0]; d2 = 0.0; }
+    if (t > x[N - 1]) { v = y[N - 1] + (t - x[N - 1]) * b[N - 1]; d1 = b[N - 1]; d2 = 0.0; }
+}
+
+__device__ __forceinline__ int table_segment(const DevModel& M, int ti, double t) {
+    const mh_table T = M.tabs[ti];
+    const double* br = M.brk + T.break_begin;
+    if (t <= br[0]) return 0;
+    if (t >= br[T.nseg]) return T.nseg - 1;
+    int lo = 0, hi = T.nseg;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (t < br[mid]) hi = mid; else lo = mid;
+    }
+    return lo;
+}
+
+__device__ __forceinline__ double table_value(const DevModel& M, int ti, int s, int col, double t) {
+    const mh_table T = M.tabs[ti];
+    const double* cf = M.coef + T.coef_begin + ((long)s * T.ncol + col) * (T.degree + 1);
+    const double dt = t - M.brk[T.break_begin + s];
+    double v = cf[T.degree];
+    for (int k = T.degree - 1; k >= 0; --k) v = v * dt + cf[k];
+    return v;
+}
+}  // namespace mh

@@ -25,6 +25,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -74,11 +75,24 @@ struct TplEntry {
 };
 
 // ------------------------------------------------------------------------
-// Size classes of the per-lane workspace.
+// DAE back ends.  Generic: the interpreter of dae_device.hpp with size-class
+// bounded per-lane arrays.  Generated: a model-specialized straight-line
+// struct from mocohip/codegen.py (see generated/models.inc), selected by
+// model hash at mh_create.
 // ------------------------------------------------------------------------
 struct SzSmall { static constexpr int MB = 4, MQ = 4, MP = 4, MI = 24, MO = 12; };
 struct SzMedium { static constexpr int MB = 16, MQ = 16, MP = 8, MI = 128, MO = 64; };
 struct SzLarge { static constexpr int MB = 32, MQ = 40, MP = 12, MI = 384, MO = 192; };
+
+template <class Z>
+struct GenericDae {
+    static constexpr int MI = Z::MI, MO = Z::MO;
+    __device__ __forceinline__ static void eval(const DevModel& M, double t, const double* in,
+            double* out) {
+        Work<Z::MB, Z::MQ, Z::MP> w;
+        dae_eval<Z::MB, Z::MQ, Z::MP>(M, w, t, in, in + M.ns, out);
+    }
+};
 
 struct Layout {
     int NS, NC, NQ, NO, NI;  // NI = NS + NC
@@ -87,76 +101,66 @@ struct Layout {
     int nk;                  // grid points in this shard
 };
 
-__device__ __forceinline__ void gather_inputs(const double* __restrict__ x, const Layout& L,
-        int k, double* in, int NI) {
+// Per grid point the evaluation lanes are laid out as
+//   forward/backward: [dir 0 .. ND-1 perturbed, ND = unperturbed base]
+//   central:          [dir 0 .. ND-1 at +h, ND .. 2ND-1 at -h, 2ND = base]
+// (dir 0 = t0 seed, dir 1 = tf seed, dir 2+j = point input j) and raw DAE
+// outputs are stored Y[(kl*NO + o)*stride + lane]; eval_g uses stride 1
+// with the base lane only.
+struct Lanes {
+    int fd;       // MH_FD_*
+    int ND;       // directions
+    int stride;   // lanes per grid point
+    int base;     // index of the base lane
+    double h;     // FD step
+};
+
+template <class D>
+__device__ __forceinline__ void load_point(const double* __restrict__ x, const Layout& L, int k,
+        double (&in)[D::MI]) {
     const double* xs = x + 2 + (long)k * L.NS;
     const double* xc = x + 2 + (long)L.NS * L.G + (long)k * L.NC;
-    for (int s = 0; s < L.NS; ++s) in[s] = xs[s];
-    for (int j = 0; j < L.NC; ++j) in[L.NS + j] = xc[j];
-    (void)NI;
+#pragma unroll
+    for (int i = 0; i < D::MI; ++i) {
+        double v = 0.0;
+        if (i < L.NS) v = xs[i];
+        else if (i < L.NI) v = xc[i - L.NS];
+        in[i] = v;
+    }
 }
 
-template <class Z>
-__global__ void __launch_bounds__(64) k_base(DevModel M, Layout L, const double* __restrict__ x,
-        const double* __restrict__ grid, double* __restrict__ times, double* __restrict__ Y) {
-    const int kl = blockIdx.x * blockDim.x + threadIdx.x;
-    if (kl >= L.nk) return;
-    const int k = L.k0 + kl;
-    const double t0 = x[0], tf = x[1];
-    const double t = (tf - t0) * grid[k] + t0;
-    times[kl] = t;
-    double in[Z::MI];
-    double out[Z::MO];
-    gather_inputs(x, L, k, in, L.NI);
-    Work<Z::MB, Z::MQ, Z::MP> w;
-    dae_eval<Z::MB, Z::MQ, Z::MP>(M, w, t, in, in + L.NS, out);
-    for (int o = 0; o < L.NO; ++o) Y[(long)kl * L.NO + o] = out[o];
-}
-
-// Central differences: lanes (l, l^32) are the (+h, -h) arms of direction
-// blockIdx.x*32 + (l&31) at grid point blockIdx.y.  Forward/backward: one
-// arm per lane, 64 directions per wave.
-template <class Z>
-__global__ void __launch_bounds__(64) k_fd(DevModel M, Layout L, int fd, double h,
+// One lane = one DAE evaluation (grid point kl, lane role r).
+template <class D>
+__global__ void __launch_bounds__(64) k_eval(DevModel M, Layout L, Lanes Ln,
         const double* __restrict__ x, const double* __restrict__ grid,
-        const double* __restrict__ Ybase, double* __restrict__ D) {
-    const int ND = L.NI + 2;
-    const int lane = threadIdx.x;
-    const int kl = blockIdx.y;
+        double* __restrict__ times, double* __restrict__ Y) {
+    const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= (long)L.nk * Ln.stride) return;
+    const int kl = (int)(gid / Ln.stride);
+    const int r = (int)(gid - (long)kl * Ln.stride);
     const int k = L.k0 + kl;
-    int d, sign;
-    if (fd == MH_FD_CENTRAL) { d = blockIdx.x * 32 + (lane & 31); sign = lane >> 5; }
-    else { d = blockIdx.x * 64 + lane; sign = (fd == MH_FD_FORWARD) ? 0 : 1; }
-    const bool valid = d < ND;
-    const int dd = valid ? d : ND - 1;
     const double g = grid[k];
     const double t0 = x[0], tf = x[1];
     double t = (tf - t0) * g + t0;
-    double in[Z::MI];
-    double out[Z::MO];
-    gather_inputs(x, L, k, in, L.NI);
-    const double step = sign == 0 ? h : -h;
-    if (dd == 0) t = t + step * (1.0 - g);
-    else if (dd == 1) t = t + step * g;
-    else in[dd - 2] = in[dd - 2] + step;
-    Work<Z::MB, Z::MQ, Z::MP> w;
-    dae_eval<Z::MB, Z::MQ, Z::MP>(M, w, t, in, in + L.NS, out);
-    double* Dk = D + (long)kl * L.NO * ND;
-    if (fd == MH_FD_CENTRAL) {
-        const double inv2h = 2.0 * h;
-        for (int o = 0; o < L.NO; ++o) {
-            const double other = __shfl_xor(out[o], 32);
-            if (sign == 0 && valid) Dk[(long)o * ND + d] = (out[o] - other) / inv2h;
-        }
-    } else {
-        const double* yb = Ybase + (long)kl * L.NO;
-        if (valid) {
-            for (int o = 0; o < L.NO; ++o) {
-                const double v = fd == MH_FD_FORWARD ? (out[o] - yb[o]) / h : (yb[o] - out[o]) / h;
-                Dk[(long)o * ND + d] = v;
-            }
-        }
+    if (r == Ln.base) times[kl] = t;
+    double in[D::MI];
+    double out[D::MO];
+    load_point<D>(x, L, k, in);
+    if (r != Ln.base) {
+        int dir = r;
+        double step = Ln.fd == MH_FD_BACKWARD ? -Ln.h : Ln.h;
+        if (Ln.fd == MH_FD_CENTRAL && r >= Ln.ND) { dir = r - Ln.ND; step = -Ln.h; }
+        if (dir == 0) t = t + step * (1.0 - g);
+        else if (dir == 1) t = t + step * g;
+        const int pi = dir - 2;
+#pragma unroll
+        for (int i = 0; i < D::MI; ++i) in[i] = (i == pi) ? in[i] + step : in[i];
     }
+    D::eval(M, t, in, out);
+    double* Yk = Y + (long)kl * L.NO * Ln.stride + r;
+#pragma unroll
+    for (int o = 0; o < D::MO; ++o)
+        if (o < L.NO) Yk[(long)o * Ln.stride] = out[o];
 }
 
 struct Interval {
@@ -172,14 +176,15 @@ __device__ __forceinline__ int grid_of(const Interval& I, int i, int pt) {
 }
 
 // xdot[s] at local grid point kl (global k).
-__device__ __forceinline__ double xdot_at(const Layout& L, const double* __restrict__ x,
-        const double* __restrict__ Y, int k, int kl, int s) {
+__device__ __forceinline__ double xdot_at(const Layout& L, const Lanes& Ln,
+        const double* __restrict__ x, const double* __restrict__ Y, int k, int kl, int s) {
     if (s < L.NQ) return x[2 + (long)k * L.NS + L.NQ + s];
-    return Y[(long)kl * L.NO + (s - L.NQ)];
+    return Y[((long)kl * L.NO + (s - L.NQ)) * Ln.stride + Ln.base];
 }
 
-__global__ void __launch_bounds__(256) k_defects(Layout L, Interval I, const double* __restrict__ x,
-        const double* __restrict__ times, const double* __restrict__ Y, double* __restrict__ g) {
+__global__ void __launch_bounds__(256) k_defects(Layout L, Interval I, Lanes Ln,
+        const double* __restrict__ x, const double* __restrict__ times,
+        const double* __restrict__ Y, double* __restrict__ g) {
     const int il = blockIdx.x;
     const int i = I.ib + il;
     const int NS = L.NS;
@@ -194,13 +199,14 @@ __global__ void __launch_bounds__(256) k_defects(Layout L, Interval I, const dou
                 const int s = r;
                 const double xi = x[2 + (long)ki * NS + s], xm = x[2 + (long)km * NS + s],
                              xp = x[2 + (long)kp * NS + s];
-                const double fi = xdot_at(L, x, Y, ki, kli, s), fp = xdot_at(L, x, Y, kp, klp, s);
+                const double fi = xdot_at(L, Ln, x, Y, ki, kli, s), fp = xdot_at(L, Ln, x, Y, kp, klp, s);
                 v = xm - 0.5 * (xp + xi) - (h / 8.0) * (fi - fp);
             } else if (r < 2 * NS) {
                 const int s = r - NS;
                 const double xi = x[2 + (long)ki * NS + s], xp = x[2 + (long)kp * NS + s];
-                const double fi = xdot_at(L, x, Y, ki, kli, s), fm = xdot_at(L, x, Y, km, klm, s),
-                             fp = xdot_at(L, x, Y, kp, klp, s);
+                const double fi = xdot_at(L, Ln, x, Y, ki, kli, s),
+                             fm = xdot_at(L, Ln, x, Y, km, klm, s),
+                             fp = xdot_at(L, Ln, x, Y, kp, klp, s);
                 v = xp - xi - (h / 6.0) * (fp + 4.0 * fm + fi);
             } else {
                 const int j = r - 2 * NS;
@@ -216,24 +222,27 @@ __global__ void __launch_bounds__(256) k_defects(Layout L, Interval I, const dou
         for (int r = threadIdx.x; r < I.rpi; r += blockDim.x) {
             const int s = r;
             const double xi = x[2 + (long)ki * NS + s], xp = x[2 + (long)kp * NS + s];
-            const double fi = xdot_at(L, x, Y, ki, kli, s), fp = xdot_at(L, x, Y, kp, klp, s);
+            const double fi = xdot_at(L, Ln, x, Y, ki, kli, s), fp = xdot_at(L, Ln, x, Y, kp, klp, s);
             gi[r] = xp - (xi + 0.5 * h * (fp + fi));
         }
     }
 }
 
-// d xdot[s] / d dir at local grid point kl.
-__device__ __forceinline__ double dxdot(const Layout& L, const double* __restrict__ D, int kl,
-        int s, int dir) {
-    const int ND = L.NI + 2;
+// d xdot[s] / d dir at local grid point kl from the raw lane outputs
+// (CasADi FiniteDiff formulas: (f+ - f-)/2h, (f+ - f0)/h, (f0 - f-)/h).
+__device__ __forceinline__ double dxdot(const Layout& L, const Lanes& Ln,
+        const double* __restrict__ Y, int kl, int s, int dir) {
     if (s < L.NQ) return dir == 2 + L.NQ + s ? 1.0 : 0.0;
-    return D[((long)kl * L.NO + (s - L.NQ)) * ND + dir];
+    const double* y = Y + ((long)kl * L.NO + (s - L.NQ)) * Ln.stride;
+    if (Ln.fd == MH_FD_CENTRAL) return (y[dir] - y[Ln.ND + dir]) / (2.0 * Ln.h);
+    if (Ln.fd == MH_FD_FORWARD) return (y[dir] - y[Ln.base]) / Ln.h;
+    return (y[Ln.base] - y[dir]) / Ln.h;
 }
 
-__global__ void __launch_bounds__(256) k_assemble(Layout L, Interval I,
+__global__ void __launch_bounds__(256) k_assemble(Layout L, Interval I, Lanes Ln,
         const TplEntry* __restrict__ tpl, const double* __restrict__ x,
         const double* __restrict__ grid, const double* __restrict__ times,
-        const double* __restrict__ Y, const double* __restrict__ D, double* __restrict__ values) {
+        const double* __restrict__ Y, double* __restrict__ values) {
     const int il = blockIdx.x;
     const int i = I.ib + il;
     const int k_first = grid_of(I, i, 0);
@@ -250,19 +259,20 @@ __global__ void __launch_bounds__(256) k_assemble(Layout L, Interval I,
         case T_HERM_T: {
             const int ki = k_first, kp = k_first + 2;
             const double dh = dir == 0 ? -dgap : dgap;
-            const double fi = xdot_at(L, x, Y, ki, ki - L.k0, s), fp = xdot_at(L, x, Y, kp, kp - L.k0, s);
+            const double fi = xdot_at(L, Ln, x, Y, ki, ki - L.k0, s), fp = xdot_at(L, Ln, x, Y, kp, kp - L.k0, s);
             v = -(dh / 8.0) * (fi - fp) -
-                (h / 8.0) * (dxdot(L, D, ki - L.k0, s, dir) - dxdot(L, D, kp - L.k0, s, dir));
+                (h / 8.0) * (dxdot(L, Ln, Y, ki - L.k0, s, dir) - dxdot(L, Ln, Y, kp - L.k0, s, dir));
             break;
         }
         case T_SIMP_T: {
             const int ki = k_first, km = k_first + 1, kp = k_first + 2;
             const double dh = dir == 0 ? -dgap : dgap;
-            const double fi = xdot_at(L, x, Y, ki, ki - L.k0, s), fm = xdot_at(L, x, Y, km, km - L.k0, s),
-                         fp = xdot_at(L, x, Y, kp, kp - L.k0, s);
+            const double fi = xdot_at(L, Ln, x, Y, ki, ki - L.k0, s),
+                         fm = xdot_at(L, Ln, x, Y, km, km - L.k0, s),
+                         fp = xdot_at(L, Ln, x, Y, kp, kp - L.k0, s);
             v = -(dh / 6.0) * (fp + 4.0 * fm + fi) -
-                (h / 6.0) * (dxdot(L, D, kp - L.k0, s, dir) + 4.0 * dxdot(L, D, km - L.k0, s, dir) +
-                             dxdot(L, D, ki - L.k0, s, dir));
+                (h / 6.0) * (dxdot(L, Ln, Y, kp - L.k0, s, dir) + 4.0 * dxdot(L, Ln, Y, km - L.k0, s, dir) +
+                             dxdot(L, Ln, Y, ki - L.k0, s, dir));
             break;
         }
         case T_HERM_X: {
@@ -270,14 +280,14 @@ __global__ void __launch_bounds__(256) k_assemble(Layout L, Interval I,
             const bool ident = dir == 2 + s;
             if (T.pt == 1) { v = ident ? 1.0 : 0.0; break; }
             if (ident) v += -0.5;
-            const double dv = dxdot(L, D, k - L.k0, s, dir);
+            const double dv = dxdot(L, Ln, Y, k - L.k0, s, dir);
             v += (T.pt == 0 ? -(h / 8.0) : (h / 8.0)) * dv;
             break;
         }
         case T_SIMP_X: {
             const int k = k_first + T.pt;
             const bool ident = dir == 2 + s;
-            const double dv = dxdot(L, D, k - L.k0, s, dir);
+            const double dv = dxdot(L, Ln, Y, k - L.k0, s, dir);
             if (T.pt == 2) { if (ident) v += 1.0; v += -(h / 6.0) * dv; }
             else if (T.pt == 0) { if (ident) v += -1.0; v += -(h / 6.0) * dv; }
             else v += -(h / 6.0) * 4.0 * dv;
@@ -289,15 +299,15 @@ __global__ void __launch_bounds__(256) k_assemble(Layout L, Interval I,
         case T_TRAP_T: {
             const int ki = k_first, kp = k_first + 1;
             const double dh = dir == 0 ? -dgap : dgap;
-            const double fi = xdot_at(L, x, Y, ki, ki - L.k0, s), fp = xdot_at(L, x, Y, kp, kp - L.k0, s);
+            const double fi = xdot_at(L, Ln, x, Y, ki, ki - L.k0, s), fp = xdot_at(L, Ln, x, Y, kp, kp - L.k0, s);
             v = -0.5 * dh * (fp + fi) -
-                0.5 * h * (dxdot(L, D, kp - L.k0, s, dir) + dxdot(L, D, ki - L.k0, s, dir));
+                0.5 * h * (dxdot(L, Ln, Y, kp - L.k0, s, dir) + dxdot(L, Ln, Y, ki - L.k0, s, dir));
             break;
         }
         case T_TRAP_X: {
             const int k = k_first + T.pt;
             const bool ident = dir == 2 + s;
-            const double dv = dxdot(L, D, k - L.k0, s, dir);
+            const double dv = dxdot(L, Ln, Y, k - L.k0, s, dir);
             if (T.pt == 1) { if (ident) v += 1.0; v += -0.5 * h * dv; }
             else { if (ident) v += -1.0; v += -0.5 * h * dv; }
             break;
@@ -308,6 +318,15 @@ __global__ void __launch_bounds__(256) k_assemble(Layout L, Interval I,
 }
 
 // ---- objective -------------------------------------------------------------
+__device__ __forceinline__ void gather_inputs(const double* __restrict__ x, const Layout& L,
+        int k, double* in, int NI) {
+    const double* xs = x + 2 + (long)k * L.NS;
+    const double* xc = x + 2 + (long)L.NS * L.G + (long)k * L.NC;
+    for (int s = 0; s < L.NS; ++s) in[s] = xs[s];
+    for (int j = 0; j < L.NC; ++j) in[L.NS + j] = xc[j];
+    (void)NI;
+}
+
 struct GoalSet {
     int ngoals;
     const mh_goal* goals;
@@ -450,18 +469,20 @@ __global__ void __launch_bounds__(256) k_reduce_obj(Layout L, GoalSet GS, int mo
 }
 
 // DAE probe: one lane per input row [time, states, controls].
-template <class Z>
+template <class D>
 __global__ void __launch_bounds__(64) k_dae_probe(DevModel M, Layout L, int npts,
         const double* __restrict__ in, double* __restrict__ outp) {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= npts) return;
     const double* r = in + (long)p * (1 + L.NI);
-    double v[Z::MI];
-    double out[Z::MO];
-    for (int i = 0; i < L.NI; ++i) v[i] = r[1 + i];
-    Work<Z::MB, Z::MQ, Z::MP> w;
-    dae_eval<Z::MB, Z::MQ, Z::MP>(M, w, r[0], v, v + L.NS, out);
-    for (int o = 0; o < L.NO; ++o) outp[(long)p * L.NO + o] = out[o];
+    double v[D::MI];
+    double out[D::MO];
+#pragma unroll
+    for (int i = 0; i < D::MI; ++i) v[i] = i < L.NI ? r[1 + i] : 0.0;
+    D::eval(M, r[0], v, out);
+#pragma unroll
+    for (int o = 0; o < D::MO; ++o)
+        if (o < L.NO) outp[(long)p * L.NO + o] = out[o];
 }
 
 // ------------------------------------------------------------------------
@@ -539,6 +560,8 @@ struct Arena {
 
 }  // namespace
 
+struct Backend;
+
 struct mh_ctx {
     // problem
     int NQ = 0, NZ = 0, NS = 0, NC = 0, NO = 0, NI = 0;
@@ -547,6 +570,9 @@ struct mh_ctx {
     int fd = 0;
     double h = 1e-8;
     int size_class = 0;
+    const struct Backend* be = nullptr;
+    Lanes lanes_jac{}, lanes_g{};
+    uint64_t model_hash = 0;
     int64_t n = 0, m = 0, nnz = 0;
     std::vector<double> grid, quad;
     std::vector<TplEntry> tpl;
@@ -563,7 +589,7 @@ struct mh_ctx {
     DevModel M{};
     GoalSet GS{};
     double *d_x = nullptr, *d_grid = nullptr, *d_quad = nullptr, *d_times = nullptr, *d_Y = nullptr,
-           *d_D = nullptr, *d_g = nullptr, *d_vals = nullptr, *d_C = nullptr, *d_grad = nullptr,
+           *d_Yg = nullptr, *d_g = nullptr, *d_vals = nullptr, *d_C = nullptr, *d_grad = nullptr,
            *d_tpart = nullptr, *d_f = nullptr;
     TplEntry* d_tpl = nullptr;
     float timings[3] = {0, 0, 0};
@@ -796,6 +822,43 @@ static int validate_and_layout(mh_ctx* c, const mh_problem* p, const mh_options*
     return MH_OK;
 }
 
+// FNV-1a 64 over everything the per-point DAE depends on (table *values* are
+// excluded: they are read from HBM at run time).  Selects generated back ends.
+static uint64_t fnv1a(uint64_t h, const void* p, size_t n) {
+    const unsigned char* b = (const unsigned char*)p;
+    for (size_t i = 0; i < n; ++i) { h ^= b[i]; h *= 1099511628211ULL; }
+    return h;
+}
+static uint64_t model_hash(const mh_model* M) {
+    uint64_t h = 1469598103934665603ULL;
+    const int32_t counts[] = {M->nq, M->nbodies, M->naxes, M->nfunctions, M->nknots, M->nmuscles,
+            M->npoints, M->nactuators, M->ntables, M->nexternal};
+    h = fnv1a(h, counts, sizeof counts);
+    h = fnv1a(h, M->gravity, sizeof M->gravity);
+    h = fnv1a(h, M->bodies, sizeof(mh_body) * (size_t)M->nbodies);
+    h = fnv1a(h, M->axes, sizeof(mh_axis) * (size_t)M->naxes);
+    h = fnv1a(h, M->functions, sizeof(mh_function) * (size_t)M->nfunctions);
+    h = fnv1a(h, M->knot_x, sizeof(double) * (size_t)M->nknots);
+    h = fnv1a(h, M->knot_y, sizeof(double) * (size_t)M->nknots);
+    h = fnv1a(h, M->muscles, sizeof(mh_muscle) * (size_t)M->nmuscles);
+    h = fnv1a(h, M->points, sizeof(mh_path_point) * (size_t)M->npoints);
+    h = fnv1a(h, M->actuators, sizeof(mh_actuator) * (size_t)M->nactuators);
+    h = fnv1a(h, M->external, sizeof(mh_external_force) * (size_t)M->nexternal);
+    for (int t = 0; t < M->ntables; ++t) {
+        const int32_t shape[2] = {M->tables[t].degree, M->tables[t].ncol};
+        h = fnv1a(h, shape, sizeof shape);
+    }
+    return h;
+}
+
+extern "C" int mh_model_hash(const mh_model* M, uint64_t* hash) {
+    if (!M || !hash) return set_err(MH_ERR_INVALID, "null argument");
+    *hash = model_hash(M);
+    return MH_OK;
+}
+
+static const Backend* select_backend(mh_ctx* c, const mh_problem* p);
+
 extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out) {
     if (!p || !o || !out) return set_err(MH_ERR_INVALID, "null argument");
     *out = nullptr;
@@ -810,6 +873,7 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
         return set_err(MH_ERR_HIP, "no HIP device available (the hot path has no CPU fallback)");
     if (o->device < 0 || o->device >= ndev) return set_err(MH_ERR_HIP, "device %d out of range", o->device);
     c->device = o->device;
+    c->be = select_backend(c.get(), p);
     HIPCHK(hipSetDevice(c->device));
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, c->device));
@@ -862,8 +926,11 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     const int ND = c->NI + 2;
     const size_t o_x = A.reserve(sizeof(double) * c->n);
     const size_t o_times = A.reserve(sizeof(double) * c->nk);
-    const size_t o_Y = A.reserve(sizeof(double) * (size_t)c->nk * std::max(1, c->NO));
-    const size_t o_D = A.reserve(sizeof(double) * (size_t)c->nk * std::max(1, c->NO) * ND);
+    const int stride = c->fd == MH_FD_CENTRAL ? 2 * ND + 1 : ND + 1;
+    c->lanes_jac = Lanes{c->fd, ND, stride, stride - 1, c->h};
+    c->lanes_g = Lanes{c->fd, ND, 1, 0, c->h};
+    const size_t o_Y = A.reserve(sizeof(double) * (size_t)c->nk * std::max(1, c->NO) * stride);
+    const size_t o_Yg = A.reserve(sizeof(double) * (size_t)c->nk * std::max(1, c->NO));
     const size_t o_g = A.reserve(sizeof(double) * (size_t)nint * c->rpi);
     const size_t o_vals = A.reserve(sizeof(double) * (size_t)nint * c->nnz_int);
     const size_t o_C = A.reserve(sizeof(double) * (size_t)c->G * std::max(1, p->ngoals));
@@ -899,7 +966,7 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     c->d_grid = (double*)(b + o_grid); c->d_quad = (double*)(b + o_quad);
     c->d_tpl = (TplEntry*)(b + o_tpl);
     c->d_x = (double*)(b + o_x); c->d_times = (double*)(b + o_times); c->d_Y = (double*)(b + o_Y);
-    c->d_D = (double*)(b + o_D); c->d_g = (double*)(b + o_g); c->d_vals = (double*)(b + o_vals);
+    c->d_Yg = (double*)(b + o_Yg); c->d_g = (double*)(b + o_g); c->d_vals = (double*)(b + o_vals);
     c->d_C = (double*)(b + o_C); c->d_grad = (double*)(b + o_grad); c->d_tpart = (double*)(b + o_tpart);
     c->d_f = (double*)(b + o_f);
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
@@ -1015,52 +1082,71 @@ extern "C" int mh_get_jac_structure(const mh_ctx* c, int32_t* iRow, int32_t* jCo
 }
 
 // ------------------------------------------------------------------------
-// Launchers.
+// Back ends and launchers.
 // ------------------------------------------------------------------------
-template <class Z>
-static void launch_base(mh_ctx* c, const double* x) {
+struct Backend {
+    const char* name;
+    void (*eval)(mh_ctx*, const double* x, const Lanes& ln, double* Y);
+    void (*integrand)(mh_ctx*, const double* x);
+    void (*grad)(mh_ctx*, const double* x);
+    void (*probe)(mh_ctx*, int np, const double* in, double* out);
+    double flops_per_eval;   // generated back ends: emitted FP64 ops per DAE
+};
+
+template <class D>
+static void be_eval(mh_ctx* c, const double* x, const Lanes& ln, double* Y) {
     Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, c->k0, c->nk};
-    hipLaunchKernelGGL(k_base<Z>, dim3((c->nk + 63) / 64), dim3(64), 0, c->stream, c->M, L, x,
-            c->d_grid, c->d_times, c->d_Y);
+    const long lanes = (long)c->nk * ln.stride;
+    hipLaunchKernelGGL(k_eval<D>, dim3((unsigned)((lanes + 63) / 64)), dim3(64), 0, c->stream, c->M,
+            L, ln, x, c->d_grid, c->d_times, Y);
 }
-template <class Z>
-static void launch_fd(mh_ctx* c, const double* x) {
-    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, c->k0, c->nk};
-    const int ND = c->NI + 2;
-    const int per = c->fd == MH_FD_CENTRAL ? 32 : 64;
-    hipLaunchKernelGGL(k_fd<Z>, dim3((ND + per - 1) / per, c->nk), dim3(64), 0, c->stream, c->M, L,
-            c->fd, c->h, x, c->d_grid, c->d_Y, c->d_D);
-}
-template <class Z>
-static void launch_integrand(mh_ctx* c, const double* x) {
+template <class D>
+static void be_integrand(mh_ctx* c, const double* x) {
     Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, 0, c->G};
-    hipLaunchKernelGGL(k_integrand<Z>, dim3((c->G + 63) / 64), dim3(64), 0, c->stream, c->M, L,
+    hipLaunchKernelGGL(k_integrand<D>, dim3((c->G + 63) / 64), dim3(64), 0, c->stream, c->M, L,
             c->GS, x, c->d_grid, c->d_quad, c->d_C);
 }
-template <class Z>
-static void launch_grad(mh_ctx* c, const double* x) {
+template <class D>
+static void be_grad(mh_ctx* c, const double* x) {
     Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, 0, c->G};
     const long tot = (long)c->G * (c->NI + 2);
-    hipLaunchKernelGGL(k_grad<Z>, dim3((unsigned)((tot + 63) / 64)), dim3(64), 0, c->stream, c->M, L,
+    hipLaunchKernelGGL(k_grad<D>, dim3((unsigned)((tot + 63) / 64)), dim3(64), 0, c->stream, c->M, L,
             c->GS, c->fd, c->h, x, c->d_grid, c->d_quad, c->d_grad, c->d_tpart);
 }
+template <class D>
+static void be_probe(mh_ctx* c, int np, const double* in, double* out) {
+    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, 0, 0};
+    hipLaunchKernelGGL(k_dae_probe<D>, dim3((np + 63) / 64), dim3(64), 0, c->stream, c->M, L, np, in, out);
+}
+template <class D>
+static constexpr Backend make_backend(const char* name, double flops) {
+    return Backend{name, &be_eval<D>, &be_integrand<D>, &be_grad<D>, &be_probe<D>, flops};
+}
 
-#define DISPATCH(fn, ...)                                                  \
-    do {                                                                   \
-        if (c->size_class == 0) fn<SzSmall>(__VA_ARGS__);                  \
-        else if (c->size_class == 1) fn<SzMedium>(__VA_ARGS__);            \
-        else fn<SzLarge>(__VA_ARGS__);                                     \
-    } while (0)
+static const Backend kGeneric[3] = {
+    make_backend<GenericDae<SzSmall>>("generic-small", 0.0),
+    make_backend<GenericDae<SzMedium>>("generic-medium", 0.0),
+    make_backend<GenericDae<SzLarge>>("generic-large", 0.0),
+};
+
+// Model-specialized back ends produced by tools/gen_models.py.
+#include "generated/models_structs.inc"
+struct GenEntry { uint64_t hash; Backend be; };
+#define MH_GEN_MODEL(T, H, NAME) GenEntry{H, make_backend<T>(NAME, T::FLOPS_PER_EVAL)},
+static const GenEntry kGeneratedModels[] = {
+#include "generated/models_table.inc"
+    GenEntry{0, Backend{nullptr, nullptr, nullptr, nullptr, nullptr, 0.0}}};
+#undef MH_GEN_MODEL
 
 static int run_g(mh_ctx* c, const double* x_dev, double* g_dev) {
     Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, c->k0, c->nk};
     Interval I{c->scheme, c->interp, c->ib, c->rpi, c->nnz_int};
     HIPCHK(hipEventRecord(c->ev[0], c->stream));
-    DISPATCH(launch_base, c, x_dev);
+    c->be->eval(c, x_dev, c->lanes_g, c->d_Yg);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[1], c->stream));
-    hipLaunchKernelGGL(k_defects, dim3(c->ie - c->ib), dim3(256), 0, c->stream, L, I, x_dev,
-            c->d_times, c->d_Y, g_dev);
+    hipLaunchKernelGGL(k_defects, dim3(c->ie - c->ib), dim3(256), 0, c->stream, L, I, c->lanes_g,
+            x_dev, c->d_times, c->d_Yg, g_dev);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[2], c->stream));
     return MH_OK;
@@ -1070,12 +1156,11 @@ static int run_jac(mh_ctx* c, const double* x_dev, double* v_dev) {
     Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, c->k0, c->nk};
     Interval I{c->scheme, c->interp, c->ib, c->rpi, c->nnz_int};
     HIPCHK(hipEventRecord(c->ev[0], c->stream));
-    DISPATCH(launch_base, c, x_dev);
-    DISPATCH(launch_fd, c, x_dev);
+    c->be->eval(c, x_dev, c->lanes_jac, c->d_Y);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[1], c->stream));
-    hipLaunchKernelGGL(k_assemble, dim3(c->ie - c->ib), dim3(256), 0, c->stream, L, I, c->d_tpl,
-            x_dev, c->d_grid, c->d_times, c->d_Y, c->d_D, v_dev);
+    hipLaunchKernelGGL(k_assemble, dim3(c->ie - c->ib), dim3(256), 0, c->stream, L, I, c->lanes_jac,
+            c->d_tpl, x_dev, c->d_grid, c->d_times, c->d_Y, v_dev);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[2], c->stream));
     return MH_OK;
@@ -1137,7 +1222,7 @@ extern "C" int mh_eval_f(mh_ctx* c, const double* x, int, double* f) {
     HIPCHK(hipEventRecord(c->ev[0], c->stream));
     Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, 0, c->G};
     if (c->ngoals > 0) {
-        DISPATCH(launch_integrand, c, c->d_x);
+        c->be->integrand(c, c->d_x);
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(c->ev[1], c->stream));
@@ -1159,8 +1244,8 @@ extern "C" int mh_eval_grad_f(mh_ctx* c, const double* x, int, double* grad) {
     HIPCHK(hipMemsetAsync(c->d_tpart, 0, sizeof(double) * 2 * c->G, c->stream));
     HIPCHK(hipMemsetAsync(c->d_C, 0, sizeof(double) * c->G * std::max(1, c->ngoals), c->stream));
     if (c->ngoals > 0) {
-        DISPATCH(launch_integrand, c, c->d_x);
-        DISPATCH(launch_grad, c, c->d_x);
+        c->be->integrand(c, c->d_x);
+        c->be->grad(c, c->d_x);
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(c->ev[1], c->stream));
@@ -1173,12 +1258,6 @@ extern "C" int mh_eval_grad_f(mh_ctx* c, const double* x, int, double* grad) {
     return finish(c);
 }
 
-template <class Z>
-static void launch_probe(mh_ctx* c, int np, const double* in, double* out) {
-    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, 0, 0};
-    hipLaunchKernelGGL(k_dae_probe<Z>, dim3((np + 63) / 64), dim3(64), 0, c->stream, c->M, L, np, in, out);
-}
-
 extern "C" int mh_eval_dae(mh_ctx* c, int32_t np, const double* inputs, double* outputs) {
     if (!c || !inputs || !outputs || np < 0) return set_err(MH_ERR_INVALID, "bad argument");
     if (np == 0) return MH_OK;
@@ -1188,7 +1267,7 @@ extern "C" int mh_eval_dae(mh_ctx* c, int32_t np, const double* inputs, double* 
     HIPCHK(hipMalloc(&din, sizeof(double) * nin));
     HIPCHK(hipMalloc(&dout, sizeof(double) * std::max<size_t>(nout, 1)));
     HIPCHK(hipMemcpyAsync(din, inputs, sizeof(double) * nin, hipMemcpyHostToDevice, c->stream));
-    DISPATCH(launch_probe, c, np, din, dout);
+    c->be->probe(c, np, din, dout);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(outputs, dout, sizeof(double) * nout, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -1201,4 +1280,27 @@ extern "C" int mh_last_timings(const mh_ctx* c, double* ms3) {
     if (!c || !ms3) return set_err(MH_ERR_INVALID, "null argument");
     for (int i = 0; i < 3; ++i) ms3[i] = c->timings[i];
     return MH_OK;
+}
+
+extern "C" int mh_get_backend(const mh_ctx* c, char* name, int32_t name_len, double* flops_per_eval,
+        uint64_t* model_hash) {
+    if (!c) return set_err(MH_ERR_INVALID, "null argument");
+    if (name && name_len > 0) {
+        std::strncpy(name, c->be->name, (size_t)name_len - 1);
+        name[name_len - 1] = 0;
+    }
+    if (flops_per_eval) *flops_per_eval = c->be->flops_per_eval;
+    if (model_hash) *model_hash = c->model_hash;
+    return MH_OK;
+}
+
+static const Backend* select_backend(mh_ctx* c, const mh_problem* p) {
+    c->model_hash = model_hash(&p->model);
+    const char* force = std::getenv("MOCOHIP_BACKEND");
+    const bool generic = force && std::strcmp(force, "generic") == 0;
+    if (!generic) {
+        for (const GenEntry& e : kGeneratedModels)
+            if (e.be.name && e.hash == c->model_hash) return &e.be;
+    }
+    return &kGeneric[c->size_class];
 }

@@ -1,0 +1,689 @@
+"""Model-specialized DAE code generator (the "model compiler" back end).
+
+Given a compiled model tape (the same mh_model arrays the C ABI receives),
+emit straight-line HIP C++ for the explicit per-point DAE
+(MocoCasOCProblem::calcMultibodySystemExplicit semantics, same algorithm as
+csrc/dae_device.hpp) with every structural constant folded at generation
+time: joint axes, frame offsets, body inertias, path-point layout,
+conditional/moving point logic, actuator wiring.  Zero terms of the 3-D
+spatial algebra vanish (planar models lose most of them), all per-lane
+state is scalar temporaries (VGPRs instead of scratch), and the mass matrix
+is factored with Featherstone's fill-free L^T L scheme on the coordinate
+tree.
+
+The generated struct is compiled into libmocohip.so and selected at
+mh_create by the model hash (mh_model_hash); models without a generated
+kernel run the generic device interpreter.
+"""
+from __future__ import annotations
+
+import math
+import struct
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import abi
+
+
+def lit(v: float) -> str:
+    """Exact C++ literal of a double (Python repr round-trips exactly)."""
+    v = float(v)
+    if math.isinf(v):
+        return "(-INFINITY)" if v < 0 else "INFINITY"
+    if math.isnan(v):
+        return "NAN"
+    r = repr(v)
+    return r if ("e" in r or "." in r) else r + ".0"
+
+
+class S:
+    """A scalar: a folded constant (c) or a named temporary (n)."""
+    __slots__ = ("c", "n")
+
+    def __init__(self, c=None, n=None):
+        self.c = c
+        self.n = n
+
+    def is_c(self, v=None):
+        return self.c is not None and (v is None or self.c == v)
+
+    def __str__(self):
+        return lit(self.c) if self.c is not None else self.n
+
+
+class Gen:
+    def __init__(self):
+        self.lines: List[str] = []
+        self.k = 0
+        self.flops = {"add": 0, "mul": 0, "div": 0, "fn": 0}
+
+    # -- emission -----------------------------------------------------------
+    def tmp(self, expr: str, kind: Optional[str] = None) -> S:
+        self.k += 1
+        name = f"t{self.k}"
+        self.lines.append(f"    const double {name} = {expr};")
+        if kind:
+            self.flops[kind] += 1
+        return S(n=name)
+
+    def var(self, init: S) -> str:
+        """A mutable double (for accumulators updated in loops)."""
+        self.k += 1
+        name = f"v{self.k}"
+        self.lines.append(f"    double {name} = {init};")
+        return name
+
+    def raw(self, line: str):
+        self.lines.append("    " + line)
+
+    @staticmethod
+    def const(v: float) -> S:
+        return S(c=float(v))
+
+    # -- arithmetic with folding -----------------------------------------------
+    def add(self, a: S, b: S) -> S:
+        if a.is_c() and b.is_c():
+            return S(c=a.c + b.c)
+        if a.is_c(0.0):
+            return b
+        if b.is_c(0.0):
+            return a
+        return self.tmp(f"{a} + {b}", "add")
+
+    def sub(self, a: S, b: S) -> S:
+        if a.is_c() and b.is_c():
+            return S(c=a.c - b.c)
+        if b.is_c(0.0):
+            return a
+        if a.is_c(0.0):
+            return self.neg(b)
+        return self.tmp(f"{a} - {b}", "add")
+
+    def neg(self, a: S) -> S:
+        if a.is_c():
+            return S(c=-a.c)
+        return self.tmp(f"-{a}")
+
+    def mul(self, a: S, b: S) -> S:
+        if a.is_c() and b.is_c():
+            return S(c=a.c * b.c)
+        if a.is_c(0.0) or b.is_c(0.0):
+            return S(c=0.0)
+        if a.is_c(1.0):
+            return b
+        if b.is_c(1.0):
+            return a
+        if a.is_c(-1.0):
+            return self.neg(b)
+        if b.is_c(-1.0):
+            return self.neg(a)
+        return self.tmp(f"{a} * {b}", "mul")
+
+    def div(self, a: S, b: S) -> S:
+        if a.is_c() and b.is_c():
+            return S(c=a.c / b.c)
+        if a.is_c(0.0):
+            return S(c=0.0)
+        if b.is_c(1.0):
+            return a
+        return self.tmp(f"{a} / {b}", "div")
+
+    def fn(self, name: str, a: S) -> S:
+        if a.is_c():
+            return S(c=getattr(math, name)(a.c))
+        return self.tmp(f"{name}({a})", "fn")
+
+    def sel(self, cond: str, a: S, b: S) -> S:
+        return self.tmp(f"({cond}) ? {a} : {b}")
+
+    def dot(self, a: Sequence[S], b: Sequence[S]) -> S:
+        acc = S(c=0.0)
+        for x, y in zip(a, b):
+            acc = self.add(acc, self.mul(x, y))
+        return acc
+
+    # -- 3-vectors / 3x3 (row-major lists) ---------------------------------------
+    def mm(self, A, B):
+        return [self.dot([A[3 * i], A[3 * i + 1], A[3 * i + 2]], [B[j], B[3 + j], B[6 + j]])
+                for i in range(3) for j in range(3)]
+
+    def mmt(self, A, B):  # A B^T
+        return [self.dot([A[3 * i], A[3 * i + 1], A[3 * i + 2]],
+                         [B[3 * j], B[3 * j + 1], B[3 * j + 2]]) for i in range(3) for j in range(3)]
+
+    def mv(self, A, x):
+        return [self.dot([A[3 * i], A[3 * i + 1], A[3 * i + 2]], x) for i in range(3)]
+
+    def vadd(self, a, b):
+        return [self.add(x, y) for x, y in zip(a, b)]
+
+    def vsub(self, a, b):
+        return [self.sub(x, y) for x, y in zip(a, b)]
+
+    def vscale(self, a, s):
+        return [self.mul(x, s) for x in a]
+
+    def cross(self, a, b):
+        return [self.sub(self.mul(a[1], b[2]), self.mul(a[2], b[1])),
+                self.sub(self.mul(a[2], b[0]), self.mul(a[0], b[2])),
+                self.sub(self.mul(a[0], b[1]), self.mul(a[1], b[0]))]
+
+    # spatial (w, v) pairs of 3-lists
+    def crm(self, a, b):
+        w = self.cross(a[0], b[0])
+        v = self.vadd(self.cross(a[0], b[1]), self.cross(a[1], b[0]))
+        return (w, v)
+
+    def crf(self, a, f):
+        w = self.vadd(self.cross(a[0], f[0]), self.cross(a[1], f[1]))
+        v = self.cross(a[0], f[1])
+        return (w, v)
+
+    def svdot(self, m, f):
+        return self.add(self.dot(m[0], f[0]), self.dot(m[1], f[1]))
+
+    def svadd(self, a, b):
+        return (self.vadd(a[0], b[0]), self.vadd(a[1], b[1]))
+
+    def svscale(self, a, s):
+        return (self.vscale(a[0], s), self.vscale(a[1], s))
+
+    def rbi_mul(self, I, x):
+        m, h, II = I
+        w = [self.dot([II[0], II[3], II[4]], x[0]),
+             self.dot([II[3], II[1], II[5]], x[0]),
+             self.dot([II[4], II[5], II[2]], x[0])]
+        w = self.vadd(w, self.cross(h, x[1]))
+        v = self.vsub(self.vscale(x[1], m), self.cross(h, x[0]))
+        return (w, v)
+
+    def materialize(self, a: S) -> S:
+        """Force a named temporary (used for accumulators that are read many
+        times, to keep the generated expression graph shallow)."""
+        return a
+
+
+def _c(v):
+    return S(c=float(v))
+
+
+def _vec(vals):
+    return [_c(v) for v in vals]
+
+
+class ModelView:
+    """Read-only access to the tape arrays of a CompiledModel."""
+
+    def __init__(self, cm):
+        st = cm.struct
+        self.cm = cm
+        self.nq = st.nq
+        self.nb = st.nbodies
+        self.bodies = [cm._bodies[i] for i in range(st.nbodies)]
+        self.axes = [cm._axes[i] for i in range(st.naxes)]
+        self.funcs = [cm._funcs[i] for i in range(st.nfunctions)]
+        self.kx = cm._kx
+        self.ky = cm._ky
+        self.muscles = [cm._muscles[i] for i in range(st.nmuscles)]
+        self.points = [cm._points[i] for i in range(st.npoints)]
+        self.acts = [cm._acts[i] for i in range(st.nactuators)]
+        self.tables = [cm._tables[i] for i in range(st.ntables)]
+        self.ext = [cm._ext[i] for i in range(st.nexternal)]
+        self.gravity = list(st.gravity)
+
+
+def generate(cm, struct_name: str) -> Tuple[str, Dict]:
+    """Return (C++ source of `struct <struct_name>`, info dict with counts)."""
+    M = ModelView(cm)
+    g = Gen()
+    NQ = M.nq
+    # ---- state layout ----------------------------------------------------
+    z = 2 * NQ
+    act_state, ftn_state, mus_control = [], [], [-1] * len(M.muscles)
+    tau_act = tau_deact = None
+    for mu in M.muscles:
+        if mu.tendon_dynamics_implicit and not mu.ignore_tendon_compliance:
+            raise NotImplementedError("implicit tendon dynamics")
+        act_state.append(-1 if mu.ignore_activation_dynamics else z)
+        z += 0 if mu.ignore_activation_dynamics else 1
+        ftn_state.append(-1 if mu.ignore_tendon_compliance else z)
+        z += 0 if mu.ignore_tendon_compliance else 1
+        if not mu.ignore_activation_dynamics and tau_act is None:
+            tau_act, tau_deact = mu.activation_time_constant, mu.deactivation_time_constant
+    NS, NC = z, len(M.acts)
+    NZ, NO, NI = NS - 2 * NQ, NQ + NS - 2 * NQ, NS + NC
+    for ia, a in enumerate(M.acts):
+        if a.kind == abi.MH_ACT_MUSCLE:
+            mus_control[a.target] = ia
+    inp = [S(n=f"in[{i}]") for i in range(NI)]
+    q = inp[:NQ]
+    u = inp[NQ:2 * NQ]
+    ctrl = inp[NS:NS + NC]
+    time = S(n="t")
+
+    # ---- functions of one coordinate --------------------------------------
+    fcache: Dict[int, Tuple[S, S, S]] = {}
+
+    def fn_eval(fi: int):
+        if fi in fcache:
+            return fcache[fi]
+        F = M.funcs[fi]
+        if F.kind == abi.MH_FN_CONSTANT:
+            r = (_c(F.a), _c(0.0), _c(0.0))
+        elif F.kind == abi.MH_FN_LINEAR:
+            # value = scale * (a*q + b)
+            r = (g.mul(_c(F.scale), g.add(g.mul(_c(F.a), q[F.coord]), _c(F.b))),
+                 _c(F.scale * F.a), _c(0.0))
+        else:
+            g.k += 1
+            base = f"f{g.k}"
+            g.raw(f"double {base}v, {base}d1, {base}d2;")
+            g.raw(f"mh::simm_eval_n<{F.knot_count}>(M, {F.knot_begin}, {q[F.coord]}, "
+                  f"{base}v, {base}d1, {base}d2);")
+            g.flops["add"] += 6
+            g.flops["mul"] += 8
+            v, d1, d2 = S(n=f"{base}v"), S(n=f"{base}d1"), S(n=f"{base}d2")
+            if F.scale != 1.0:
+                v, d1, d2 = g.mul(_c(F.scale), v), g.mul(_c(F.scale), d1), g.mul(_c(F.scale), d2)
+            r = (v, d1, d2)
+        fcache[fi] = r
+        return r
+
+    # ---- kinematics + RNEA forward pass ----------------------------------
+    I3 = _vec([1, 0, 0, 0, 1, 0, 0, 0, 1])
+    Z3 = _vec([0, 0, 0])
+    R = {-1: I3}
+    P = {-1: Z3}
+    V = {-1: (Z3, Z3)}
+    A = {-1: (Z3, _vec([-M.gravity[0], -M.gravity[1], -M.gravity[2]]))}
+    Sj = [(Z3, Z3) for _ in range(NQ)]
+    coord_body = [-1] * NQ
+    Fb: Dict[int, Tuple] = {}
+    Ibody: Dict[int, Tuple] = {}
+    g.raw("// ---- kinematics, velocities, bias accelerations, RNEA forward ----")
+    for b, B in enumerate(M.bodies):
+        p = B.parent
+        RPF = _vec(B.R_PF)
+        RGF = g.mm(R[p], RPF)
+        pGF = g.vadd(P[p], g.mv(R[p], _vec(B.p_PF)))
+        Vb, Ab, Vpar = V[p], A[p], V[p]
+        axes = M.axes[B.axis_begin:B.axis_begin + B.axis_count]
+        fvals = [fn_eval(ax.func) for ax in axes]
+        pFM = Z3
+        for ax, fv in zip(axes, fvals):
+            if ax.type == abi.MH_AXIS_TRANSLATION:
+                pFM = g.vadd(pFM, g.vscale(_vec(ax.dir), fv[0]))
+        oM = g.vadd(pGF, g.mv(RGF, pFM))
+        for ax, fv in zip(axes, fvals):
+            F = M.funcs[ax.func]
+            if ax.type != abi.MH_AXIS_TRANSLATION or F.kind == abi.MH_FN_CONSTANT:
+                continue
+            j = F.coord
+            coord_body[j] = b
+            s = (Z3, g.mv(RGF, _vec(ax.dir)))
+            sd = g.crm(Vpar, s)
+            thd = g.mul(fv[1], u[j])
+            thdd = g.mul(fv[2], g.mul(u[j], u[j]))
+            Vb = g.svadd(Vb, g.svscale(s, thd))
+            Ab = g.svadd(Ab, g.svadd(g.svscale(sd, thd), g.svscale(s, thdd)))
+            Sj[j] = g.svadd(Sj[j], g.svscale(s, fv[1]))
+        Rcur = I3
+        for ax, fv in zip(axes, fvals):
+            if ax.type != abi.MH_AXIS_ROTATION:
+                continue
+            F = M.funcs[ax.func]
+            if F.kind != abi.MH_FN_CONSTANT:
+                j = F.coord
+                coord_body[j] = b
+                RGc = g.mm(RGF, Rcur)
+                w = g.mv(RGc, _vec(ax.dir))
+                s = (w, g.cross(oM, w))
+                sd = g.crm(Vb, s)
+                thd = g.mul(fv[1], u[j])
+                thdd = g.mul(fv[2], g.mul(u[j], u[j]))
+                Vb = g.svadd(Vb, g.svscale(s, thd))
+                Ab = g.svadd(Ab, g.svadd(g.svscale(sd, thd), g.svscale(s, thdd)))
+                Sj[j] = g.svadd(Sj[j], g.svscale(s, fv[1]))
+            # Rodrigues rotation about a constant unit axis
+            a0, a1, a2 = ax.dir
+            if fv[0].is_c():
+                th = fv[0].c
+                cth, sth = math.cos(th), math.sin(th)
+                cs, sn = _c(cth), _c(sth)
+            else:
+                g.k += 1
+                nm = f"sc{g.k}"
+                g.raw(f"double {nm}s, {nm}c; sincos({fv[0]}, &{nm}s, &{nm}c);")
+                g.flops["fn"] += 2
+                cs, sn = S(n=f"{nm}c"), S(n=f"{nm}s")
+            kk = g.sub(_c(1.0), cs)
+            Rk = [g.add(cs, g.mul(kk, _c(a0 * a0))), g.sub(g.mul(kk, _c(a0 * a1)), g.mul(sn, _c(a2))),
+                  g.add(g.mul(kk, _c(a0 * a2)), g.mul(sn, _c(a1))),
+                  g.add(g.mul(kk, _c(a1 * a0)), g.mul(sn, _c(a2))), g.add(cs, g.mul(kk, _c(a1 * a1))),
+                  g.sub(g.mul(kk, _c(a1 * a2)), g.mul(sn, _c(a0))),
+                  g.sub(g.mul(kk, _c(a2 * a0)), g.mul(sn, _c(a1))),
+                  g.add(g.mul(kk, _c(a2 * a1)), g.mul(sn, _c(a0))), g.add(cs, g.mul(kk, _c(a2 * a2)))]
+            Rcur = g.mm(Rcur, Rk)
+        RGM = g.mm(RGF, Rcur)
+        RB = g.mmt(RGM, _vec(B.R_BM))
+        pB = g.vsub(oM, g.mv(RB, _vec(B.p_BM)))
+        R[b], P[b], V[b], A[b] = RB, pB, Vb, Ab
+        # inertia about the origin in ground
+        cw = g.vadd(pB, g.mv(RB, _vec(B.com)))
+        In = B.inertia
+        Ib = _vec([In[0], In[3], In[4], In[3], In[1], In[5], In[4], In[5], In[2]])
+        Ig = g.mmt(g.mm(RB, Ib), RB)
+        m = _c(B.mass)
+        c2 = g.dot(cw, cw)
+        II = [g.add(Ig[0], g.mul(m, g.sub(c2, g.mul(cw[0], cw[0])))),
+              g.add(Ig[4], g.mul(m, g.sub(c2, g.mul(cw[1], cw[1])))),
+              g.add(Ig[8], g.mul(m, g.sub(c2, g.mul(cw[2], cw[2])))),
+              g.sub(Ig[1], g.mul(m, g.mul(cw[0], cw[1]))),
+              g.sub(Ig[2], g.mul(m, g.mul(cw[0], cw[2]))),
+              g.sub(Ig[5], g.mul(m, g.mul(cw[1], cw[2])))]
+        Ibody[b] = (m, g.vscale(cw, m), II)
+        Ia = g.rbi_mul(Ibody[b], Ab)
+        hV = g.rbi_mul(Ibody[b], Vb)
+        Fb[b] = g.svadd(Ia, g.crf(Vb, hV))
+
+    # body force accumulators (mutable, so muscles can add into them)
+    Facc: Dict[int, List[str]] = {}
+    for b in range(M.nb):
+        w, v = Fb[b]
+        Facc[b] = [g.var(x) for x in list(w) + list(v)]
+    tau = [g.var(_c(0.0)) for _ in range(NQ)]
+
+    def acc(name: str, val: S, sign: float = 1.0):
+        if val.is_c(0.0):
+            return
+        if sign > 0:
+            g.raw(f"{name} += {val};")
+        else:
+            g.raw(f"{name} -= {val};")
+        g.flops["add"] += 1
+
+    # ---- actuators -----------------------------------------------------------
+    g.raw("// ---- coordinate actuators ----")
+    for ia, a in enumerate(M.acts):
+        if a.kind == abi.MH_ACT_COORDINATE:
+            acc(tau[a.target], g.mul(ctrl[ia], _c(a.optimal_force)))
+
+    # ---- muscles ---------------------------------------------------------------
+    out_z = {}
+    g.raw("// ---- muscles ----")
+    for im, mu in enumerate(M.muscles):
+        g.raw(f"// muscle {im}")
+        pts = M.points[mu.point_begin:mu.point_begin + mu.point_count]
+        pos, vel, act, dl_funcs = [], [], [], []
+        for pt in pts:
+            loc = _vec(pt.loc)
+            dloc = [Z3[0], Z3[1], Z3[2]]
+            mov = []
+            if pt.kind == abi.MH_PP_CONDITIONAL:
+                qv = q[pt.coord]
+                act.append(f"({qv} >= {lit(pt.range[0])} && {qv} <= {lit(pt.range[1])})")
+            else:
+                act.append(None)
+            if pt.kind == abi.MH_PP_MOVING:
+                loc = list(loc)
+                for d, fi in enumerate((pt.fx, pt.fy, pt.fz)):
+                    if fi < 0:
+                        continue
+                    fv = fn_eval(fi)
+                    loc[d] = fv[0]
+                    F = M.funcs[fi]
+                    if F.kind != abi.MH_FN_CONSTANT:
+                        dloc[d] = g.mul(fv[1], u[F.coord])
+                        mov.append((d, F.coord, fv[1]))
+            b = pt.body
+            Pw = g.vadd(P[b], g.mv(R[b], loc))
+            Vw = g.vadd(g.vadd(V[b][1], g.cross(V[b][0], Pw)), g.mv(R[b], dloc))
+            pos.append(Pw)
+            vel.append(Vw)
+            dl_funcs.append(mov)
+        # candidate segments (j -> i): both active, all points between inactive
+        segs = []
+        n = len(pts)
+        for i in range(n):
+            for j in range(i - 1, -1, -1):
+                conds = []
+                if act[j]:
+                    conds.append(act[j])
+                if act[i]:
+                    conds.append(act[i])
+                for k in range(j + 1, i):
+                    conds.append(f"!{act[k]}")
+                segs.append((j, i, " && ".join(conds) if conds else None))
+                if act[j] is None:
+                    break
+        L, Sp = _c(0.0), _c(0.0)
+        seginfo = []
+        for (j, i, cond) in segs:
+            d = g.vsub(pos[i], pos[j])
+            l = g.fn("sqrt", g.dot(d, d))
+            dv = g.vsub(vel[i], vel[j])
+            sp = g.div(g.dot(d, dv), l)
+            if cond:
+                ind = g.sel(cond, _c(1.0), _c(0.0))
+                L = g.add(L, g.mul(ind, l))
+                Sp = g.add(Sp, g.mul(ind, sp))
+            else:
+                ind = None
+                L = g.add(L, l)
+                Sp = g.add(Sp, sp)
+            seginfo.append((j, i, d, l, ind))
+        exc = ctrl[mus_control[im]]
+        sa, sf = act_state[im], ftn_state[im]
+        a_ = inp[sa] if sa >= 0 else exc
+        ftn = inp[sf] if sf >= 0 else None
+        T, adot, ftdot = _dgf(g, mu, L, Sp, a_, exc, sa >= 0, ftn, sf >= 0, tau_act, tau_deact)
+        if sa >= 0:
+            out_z[sa - 2 * NQ] = adot
+        if sf >= 0:
+            out_z[sf - 2 * NQ] = ftdot
+        for (j, i, d, l, ind) in seginfo:
+            Tl = g.div(T, l) if ind is None else g.mul(ind, g.div(T, l))
+            Fv = g.vscale(d, Tl)
+            for kk, sgn in ((j, 1.0), (i, -1.0)):
+                pt = pts[kk]
+                if pt.body < 0:
+                    continue
+                f = Fv if sgn > 0 else [g.neg(x) for x in Fv]
+                nrm = g.cross(pos[kk], f)
+                fa = Facc[pt.body]
+                for c in range(3):
+                    acc(fa[c], nrm[c], -1.0)
+                    acc(fa[3 + c], f[c], -1.0)
+                for (dd, coord, d1) in dl_funcs[kk]:
+                    Rb = R[pt.body]
+                    gg = g.mul(g.dot([Rb[dd], Rb[3 + dd], Rb[6 + dd]], f), d1)
+                    acc(tau[coord], gg)
+
+    # ---- external forces ---------------------------------------------------------
+    g.raw("// ---- external forces ----")
+    for e in M.ext:
+        b = e.body
+        g.k += 1
+        seg = f"seg{g.k}"
+        g.raw(f"const int {seg} = mh::table_segment(M, {e.table}, t);")
+
+        def col(cidx):
+            return g.tmp(f"mh::table_value(M, {e.table}, {seg}, {cidx}, t)")
+        Fv = [col(e.force_col + d) for d in range(3)] if e.force_col >= 0 else Z3
+        Pp = [col(e.point_col + d) for d in range(3)] if e.point_col >= 0 else P[b]
+        Tq = [col(e.torque_col + d) for d in range(3)] if e.torque_col >= 0 else Z3
+        nrm = g.vadd(g.cross(Pp, Fv), Tq)
+        for c in range(3):
+            acc(Facc[b][c], nrm[c], -1.0)
+            acc(Facc[b][3 + c], Fv[c], -1.0)
+
+    # ---- RNEA backward ----------------------------------------------------------------
+    g.raw("// ---- RNEA backward pass ----")
+    for b in range(M.nb - 1, -1, -1):
+        p = M.bodies[b].parent
+        if p >= 0:
+            for c in range(6):
+                g.raw(f"{Facc[p][c]} += {Facc[b][c]};")
+                g.flops["add"] += 1
+    for j in range(NQ):
+        fa = Facc[coord_body[j]]
+        fsv = ([S(n=fa[0]), S(n=fa[1]), S(n=fa[2])], [S(n=fa[3]), S(n=fa[4]), S(n=fa[5])])
+        acc(tau[j], g.svdot(Sj[j], fsv), -1.0)
+
+    # ---- CRBA --------------------------------------------------------------------------
+    g.raw("// ---- composite inertias and mass matrix ----")
+    Ic = {b: Ibody[b] for b in range(M.nb)}
+    for b in range(M.nb - 1, -1, -1):
+        p = M.bodies[b].parent
+        if p >= 0:
+            mp, hp, Ip = Ic[p]
+            mb, hb, Ibb = Ic[b]
+            Ic[p] = (g.add(mp, mb), g.vadd(hp, hb), [g.add(x, y) for x, y in zip(Ip, Ibb)])
+    # coordinate tree parent lambda(k)
+    body_coords: Dict[int, List[int]] = {}
+    for j in range(NQ):
+        body_coords.setdefault(coord_body[j], []).append(j)
+
+    def anc_coord(b):
+        p = M.bodies[b].parent
+        while p >= 0:
+            if p in body_coords:
+                return body_coords[p][-1]
+            p = M.bodies[p].parent
+        return -1
+    lam = [-1] * NQ
+    for b, cs in body_coords.items():
+        for idx, j in enumerate(cs):
+            lam[j] = cs[idx - 1] if idx > 0 else anc_coord(b)
+    for j in range(NQ):
+        if lam[j] >= j:
+            raise ValueError("coordinates must be ordered parents-first")
+    H: Dict[Tuple[int, int], S] = {}
+    for i in range(NQ):
+        b = coord_body[i]
+        Fi = g.rbi_mul(Ic[b], Sj[i])
+        j = i
+        while j >= 0:
+            H[(i, j)] = g.svdot(Sj[j], Fi)
+            j = lam[j]
+    # Featherstone L^T L factorization (fill-free on the coordinate tree)
+    g.raw("// ---- L^T L factorization and solve ----")
+    for k in range(NQ - 1, -1, -1):
+        a = g.fn("sqrt", H[(k, k)])
+        H[(k, k)] = a
+        i = lam[k]
+        while i >= 0:
+            H[(k, i)] = g.div(H[(k, i)], a)
+            i = lam[i]
+        i = lam[k]
+        while i >= 0:
+            j = i
+            while j >= 0:
+                H[(i, j)] = g.sub(H[(i, j)], g.mul(H[(k, i)], H[(k, j)]))
+                j = lam[j]
+            i = lam[i]
+    bvec = [S(n=t) for t in tau]
+    xs = [None] * NQ
+    for i in range(NQ - 1, -1, -1):
+        xs[i] = g.div(bvec[i], H[(i, i)])
+        j = lam[i]
+        while j >= 0:
+            bvec[j] = g.sub(bvec[j], g.mul(H[(i, j)], xs[i]))
+            j = lam[j]
+    for i in range(NQ):
+        j = lam[i]
+        xi = xs[i]
+        while j >= 0:
+            xi = g.sub(xi, g.mul(H[(i, j)], xs[j]))
+            j = lam[j]
+        xs[i] = g.div(xi, H[(i, i)])
+    for i in range(NQ):
+        g.raw(f"out[{i}] = {xs[i]};")
+    for zi in range(NZ):
+        g.raw(f"out[{NQ + zi}] = {out_z.get(zi, _c(0.0))};")
+    flops = dict(g.flops)
+    flops["total"] = sum(flops.values())
+    body = "\n".join(g.lines)
+    src = f"""struct {struct_name} {{
+    static constexpr int NQ = {NQ}, NZ = {NZ}, NS = {NS}, NC = {NC}, NO = {NO}, NI = {NI};
+    static constexpr double FLOPS_PER_EVAL = {float(flops['total'])};
+    __device__ __forceinline__ static void eval(const mh::DevModel& M, const double t,
+            const double* __restrict__ in, double* __restrict__ out) {{
+{body}
+    }}
+}};
+"""
+    return src, {"NQ": NQ, "NS": NS, "NC": NC, "flops": flops, "lines": len(g.lines)}
+
+
+def _dgf(g: Gen, mu, LMT: S, VMT: S, act: S, exc: S, has_act: bool, ftn: Optional[S],
+         compliant: bool, tau_act, tau_deact):
+    """DeGrooteFregly2016Muscle (DeGrooteFregly2016Muscle.cpp:186-425)."""
+    c1, c2, c3 = 0.2, 1.0, 0.2
+    d1, d2, d3, d4 = -0.3211346127989808, -8.149, -0.374, 0.8825327733249912
+    lopt, lts, Fmax = mu.optimal_fiber_length, mu.tendon_slack_length, mu.max_isometric_force
+    fiberWidth = lopt * math.sin(mu.pennation_angle_at_optimal)
+    sqW = fiberWidth * fiberWidth
+    vmax = mu.max_contraction_velocity * lopt
+    kT = math.log((1.0 + c3) / c1) / (1.0 + mu.tendon_strain_at_one_norm_force - c2)
+    e0 = mu.passive_fiber_strain_at_one_norm_force
+    peOffset = math.exp(4.0 * (0.2 - 1.0) / e0)
+    peDenom = math.exp(4.0) - peOffset
+    C = _c
+    if compliant:
+        ntl = g.add(g.div(g.fn("log", g.mul(C(1.0 / c1), g.add(ftn, C(c3)))), C(kT)), C(c2))
+    else:
+        ntl = C(1.0)
+    tendonLength = g.mul(C(lts), ntl)
+    flat = g.sub(LMT, tendonLength)
+    fiberLength = g.fn("sqrt", g.add(g.mul(flat, flat), C(sqW)))
+    nfl = g.div(fiberLength, C(lopt))
+    cosP = g.div(flat, fiberLength)
+    if mu.ignore_passive_fiber_force:
+        fPE = C(0.0)
+    else:
+        fPE = g.div(g.sub(g.fn("exp", g.div(g.mul(C(4.0), g.sub(nfl, C(1.0))), C(e0))), C(peOffset)),
+                    C(peDenom))
+    x = g.add(g.div(g.sub(nfl, C(1.0)), C(mu.active_force_width_scale)), C(1.0))
+
+    def gl(b1, b2, b3, b4):
+        num = g.mul(g.sub(x, C(b2)), g.sub(x, C(b2)))
+        dd = g.add(C(b3), g.mul(C(b4), x))
+        den = g.mul(dd, dd)
+        return g.mul(C(b1), g.fn("exp", g.mul(C(-0.5), g.div(num, den))))
+    fAL = g.add(g.add(gl(0.8150671134243542, 1.055033428970575, 0.162384573599574, 0.063303448465465),
+                      gl(0.433004984392647, 0.716775413397760, -0.029947116970696, 0.200356847296188)),
+                gl(0.1, 1.0, 0.353553390593274, 0.0))
+    if compliant:
+        nff = g.div(ftn, cosP)
+        fV = g.div(g.sub(nff, fPE), g.mul(act, fAL))
+        nfv = g.div(g.sub(g.fn("sinh", g.mul(C(1.0 / d1), g.sub(fV, C(d4)))), C(d3)), C(d2))
+        fiberVelocity = g.mul(nfv, C(vmax))
+        fvat = g.div(fiberVelocity, cosP)
+        tendonVelocity = g.sub(VMT, fvat)
+        ntv = g.div(tendonVelocity, C(lts))
+    else:
+        ntv = C(0.0)
+        fvat = VMT
+        fiberVelocity = g.mul(fvat, cosP)
+        nfv = g.div(fiberVelocity, C(vmax))
+        tv = g.add(g.mul(C(d2), nfv), C(d3))
+        arg = g.add(tv, g.fn("sqrt", g.add(g.mul(tv, tv), C(1.0))))
+        fV = g.add(g.mul(C(d1), g.fn("log", arg)), C(d4))
+    activeF = g.mul(C(Fmax), g.mul(g.mul(act, fAL), fV))
+    conPass = g.mul(C(Fmax), fPE)
+    nonCon = g.mul(g.mul(C(Fmax), C(mu.fiber_damping)), nfv)
+    total = g.add(g.add(activeF, conPass), nonCon)
+    T = g.mul(C(Fmax), ftn) if compliant else g.mul(total, cosP)
+    adot = ftdot = C(0.0)
+    if has_act:
+        tcf = g.add(C(0.5), g.mul(C(1.5), act))
+        tempAct = g.div(C(1.0), g.mul(C(tau_act), tcf))
+        tempDeact = g.div(tcf, C(tau_deact))
+        f = g.mul(C(0.5), g.fn("tanh", g.mul(C(0.1), g.sub(exc, act))))
+        tc = g.add(g.mul(tempAct, g.add(f, C(0.5))), g.mul(tempDeact, g.add(g.neg(f), C(0.5))))
+        adot = g.mul(tc, g.sub(exc, act))
+    if compliant:
+        ftdot = g.mul(ntv, g.mul(C(c1 * kT), g.fn("exp", g.mul(C(kT), g.sub(ntl, C(c2))))))
+    return T, adot, ftdot

@@ -177,6 +177,14 @@ class HipNLP(_NLPBase):
     def eval_jac_g_device(self, x_ptr: int, v_ptr: int):
         self._check(self.lib.mh_eval_jac_g_device(self.ctx, C.c_void_p(x_ptr), C.c_void_p(v_ptr)))
 
+    def backend(self):
+        """(back-end name, FP64 ops per generated DAE eval, model hash)."""
+        buf = C.create_string_buffer(128)
+        fl = C.c_double()
+        h = C.c_uint64()
+        self._check(self.lib.mh_get_backend(self.ctx, buf, 128, C.byref(fl), C.byref(h)))
+        return buf.value.decode(), fl.value, h.value
+
     def last_timings(self):
         t = np.zeros(3)
         self._check(self.lib.mh_last_timings(self.ctx, abi.dptr(t)))
