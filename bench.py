@@ -36,6 +36,9 @@ def parse():
     ap.add_argument("--fd", default="forward")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--mode", choices=["separate", "fused"], default="separate",
+                    help="separate: eval_g then eval_jac_g C-ABI calls; fused: one "
+                         "mh_eval_g_jac_g call (IPOPT new_x=false pattern)")
     return ap.parse_args()
 
 
@@ -87,8 +90,11 @@ def main():
     fd_ms = []
 
     def step(record=False):
-        nlp.eval_g_device(xd.data_ptr(), gseg.data_ptr())
-        nlp.eval_jac_g_device(xd.data_ptr(), vseg.data_ptr())
+        if args.mode == "fused":
+            nlp.eval_g_jac_g_device(xd.data_ptr(), gseg.data_ptr(), vseg.data_ptr())
+        else:
+            nlp.eval_g_device(xd.data_ptr(), gseg.data_ptr())
+            nlp.eval_jac_g_device(xd.data_ptr(), vseg.data_ptr())
         if record:
             fd_ms.append(nlp.last_timings())
         if world > 1:
@@ -160,7 +166,7 @@ def main():
             "config": {"workload": "MocoTrack gait10dof18musc DGF rigid tendon (configs[2])",
                        "mesh_intervals": N, "grid_points": nlp.G, "n": nlp.n, "m": nlp.m,
                        "nnz_jac": nlp.nnz, "transcription": "hermite-simpson",
-                       "fd": args.fd, "parallelism": f"mesh-shard{world}",
+                       "fd": args.fd, "parallelism": f"mesh-shard{world}", "mode": args.mode,
                        "iterate": "bounds-midpoint states, uniform random controls (seed 0)"},
             "roofline": roof,
             "cpu_baseline": cpu,

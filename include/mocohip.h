@@ -311,6 +311,13 @@ int mh_eval_g_device(mh_ctx* ctx, const double* x_dev, double* g_dev);
 int mh_eval_jac_g_device(mh_ctx* ctx, const double* x_dev,
         double* values_dev);
 
+/* eval_g and eval_jac_g at the same iterate from one device evaluation pass
+ * (what an IPOPT adapter does for eval_g(new_x=true) followed by
+ * eval_jac_g(new_x=false)).  Results are identical to the separate calls. */
+int mh_eval_g_jac_g(mh_ctx* ctx, const double* x, double* g, double* values);
+int mh_eval_g_jac_g_device(mh_ctx* ctx, const double* x_dev, double* g_dev,
+        double* values_dev);
+
 /* Per-point DAE probe (CasOC::Problem::calcMultibodySystemExplicit,
  * CasOCProblem.h:313-332) evaluated on the device for npoints inputs laid
  * out as [time, states(NS), controls(NC)] per point; outputs

@@ -239,11 +239,13 @@ __device__ __forceinline__ double dxdot(const Layout& L, const Lanes& Ln,
     return (y[Ln.base] - y[dir]) / Ln.h;
 }
 
+constexpr int ASM_CHUNK = 1024;   // nonzeros per assembly workgroup
+
 __global__ void __launch_bounds__(256) k_assemble(Layout L, Interval I, Lanes Ln,
         const TplEntry* __restrict__ tpl, const double* __restrict__ x,
         const double* __restrict__ grid, const double* __restrict__ times,
         const double* __restrict__ Y, double* __restrict__ values) {
-    const int il = blockIdx.x;
+    const int il = blockIdx.y;
     const int i = I.ib + il;
     const int k_first = grid_of(I, i, 0);
     const int npts = I.scheme == MH_HERMITE_SIMPSON ? 3 : 2;
@@ -251,7 +253,8 @@ __global__ void __launch_bounds__(256) k_assemble(Layout L, Interval I, Lanes Ln
     const double h = times[k_last - L.k0] - times[k_first - L.k0];
     const double dgap = grid[k_last] - grid[k_first];
     double* vi = values + (long)il * I.nnz_int;
-    for (int e = threadIdx.x; e < I.nnz_int; e += blockDim.x) {
+    const int e_end = min(I.nnz_int, (int)(blockIdx.x + 1) * ASM_CHUNK);
+    for (int e = blockIdx.x * ASM_CHUNK + threadIdx.x; e < e_end; e += blockDim.x) {
         const TplEntry T = tpl[e];
         const int s = T.s, dir = T.dir;
         double v = 0.0;
@@ -1159,8 +1162,29 @@ static int run_jac(mh_ctx* c, const double* x_dev, double* v_dev) {
     c->be->eval(c, x_dev, c->lanes_jac, c->d_Y);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[1], c->stream));
-    hipLaunchKernelGGL(k_assemble, dim3(c->ie - c->ib), dim3(256), 0, c->stream, L, I, c->lanes_jac,
+    hipLaunchKernelGGL(k_assemble, dim3((c->nnz_int + ASM_CHUNK - 1) / ASM_CHUNK, c->ie - c->ib),
+            dim3(256), 0, c->stream, L, I, c->lanes_jac,
             c->d_tpl, x_dev, c->d_grid, c->d_times, c->d_Y, v_dev);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->ev[2], c->stream));
+    return MH_OK;
+}
+
+// eval_g and eval_jac_g at the same iterate from ONE evaluation launch: the
+// base lane of every grid point feeds the defects (the host-side adapter uses
+// it for IPOPT's eval_g(new_x=true) -> eval_jac_g(new_x=false) sequence).
+static int run_g_jac(mh_ctx* c, const double* x_dev, double* g_dev, double* v_dev) {
+    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, c->k0, c->nk};
+    Interval I{c->scheme, c->interp, c->ib, c->rpi, c->nnz_int};
+    HIPCHK(hipEventRecord(c->ev[0], c->stream));
+    c->be->eval(c, x_dev, c->lanes_jac, c->d_Y);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->ev[1], c->stream));
+    hipLaunchKernelGGL(k_defects, dim3(c->ie - c->ib), dim3(256), 0, c->stream, L, I, c->lanes_jac,
+            x_dev, c->d_times, c->d_Y, g_dev);
+    hipLaunchKernelGGL(k_assemble, dim3((c->nnz_int + ASM_CHUNK - 1) / ASM_CHUNK, c->ie - c->ib),
+            dim3(256), 0, c->stream, L, I, c->lanes_jac, c->d_tpl, x_dev, c->d_grid, c->d_times,
+            c->d_Y, v_dev);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[2], c->stream));
     return MH_OK;
@@ -1212,6 +1236,27 @@ extern "C" int mh_eval_jac_g_device(mh_ctx* c, const double* x_dev, double* v_de
     HIPCHK(hipSetDevice(c->device));
     int rc = run_jac(c, x_dev, v_dev);
     if (rc) return rc;
+    return finish(c);
+}
+
+extern "C" int mh_eval_g_jac_g_device(mh_ctx* c, const double* x_dev, double* g_dev, double* v_dev) {
+    if (!c || !x_dev || !g_dev || !v_dev) return set_err(MH_ERR_INVALID, "null argument");
+    HIPCHK(hipSetDevice(c->device));
+    int rc = run_g_jac(c, x_dev, g_dev, v_dev);
+    if (rc) return rc;
+    return finish(c);
+}
+
+extern "C" int mh_eval_g_jac_g(mh_ctx* c, const double* x, double* g, double* values) {
+    if (!c || !x || !g || !values) return set_err(MH_ERR_INVALID, "null argument");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemcpyAsync(c->d_x, x, sizeof(double) * c->n, hipMemcpyHostToDevice, c->stream));
+    int rc = run_g_jac(c, c->d_x, c->d_g, c->d_vals);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(g, c->d_g, sizeof(double) * (size_t)(c->ie - c->ib) * c->rpi,
+            hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(values, c->d_vals, sizeof(double) * (size_t)(c->ie - c->ib) * c->nnz_int,
+            hipMemcpyDeviceToHost, c->stream));
     return finish(c);
 }
 

@@ -171,6 +171,17 @@ class HipNLP(_NLPBase):
         self._check(self.lib.mh_eval_jac_g(self.ctx, abi.dptr(x), int(new_x), abi.dptr(v)))
         return v[:self.nnz_end - self.nnz_begin]
 
+    def eval_g_jac_g(self, x):
+        x = np.ascontiguousarray(x, float)
+        g = np.empty(max(self.row_end - self.row_begin, 1))
+        v = np.empty(max(self.nnz_end - self.nnz_begin, 1))
+        self._check(self.lib.mh_eval_g_jac_g(self.ctx, abi.dptr(x), abi.dptr(g), abi.dptr(v)))
+        return g[:self.row_end - self.row_begin], v[:self.nnz_end - self.nnz_begin]
+
+    def eval_g_jac_g_device(self, x_ptr: int, g_ptr: int, v_ptr: int):
+        self._check(self.lib.mh_eval_g_jac_g_device(self.ctx, C.c_void_p(x_ptr), C.c_void_p(g_ptr),
+                                                    C.c_void_p(v_ptr)))
+
     def eval_g_device(self, x_ptr: int, g_ptr: int):
         self._check(self.lib.mh_eval_g_device(self.ctx, C.c_void_p(x_ptr), C.c_void_p(g_ptr)))
 
