@@ -87,6 +87,7 @@ struct SzLarge { static constexpr int MB = 32, MQ = 40, MP = 12, MI = 384, MO = 
 template <class Z>
 struct GenericDae {
     static constexpr int MI = Z::MI, MO = Z::MO;
+    static constexpr bool SPLIT = false;
     __device__ __forceinline__ static void eval(const DevModel& M, double t, const double* in,
             double* out) {
         Work<Z::MB, Z::MQ, Z::MP> w;
@@ -129,22 +130,12 @@ __device__ __forceinline__ void load_point(const double* __restrict__ x, const L
     }
 }
 
-// One lane = one DAE evaluation (grid point kl, lane role r).
+// Time and inputs of evaluation lane r of grid point k (Lanes layout above).
 template <class D>
-__global__ void __launch_bounds__(64) k_eval(DevModel M, Layout L, Lanes Ln,
-        const double* __restrict__ x, const double* __restrict__ grid,
-        double* __restrict__ times, double* __restrict__ Y) {
-    const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (gid >= (long)L.nk * Ln.stride) return;
-    const int kl = (int)(gid / Ln.stride);
-    const int r = (int)(gid - (long)kl * Ln.stride);
-    const int k = L.k0 + kl;
-    const double g = grid[k];
+__device__ __forceinline__ double lane_inputs(const Layout& L, const Lanes& Ln,
+        const double* __restrict__ x, double g, int k, int r, double (&in)[D::MI]) {
     const double t0 = x[0], tf = x[1];
     double t = (tf - t0) * g + t0;
-    if (r == Ln.base) times[kl] = t;
-    double in[D::MI];
-    double out[D::MO];
     load_point<D>(x, L, k, in);
     if (r != Ln.base) {
         int dir = r;
@@ -156,11 +147,147 @@ __global__ void __launch_bounds__(64) k_eval(DevModel M, Layout L, Lanes Ln,
 #pragma unroll
         for (int i = 0; i < D::MI; ++i) in[i] = (i == pi) ? in[i] + step : in[i];
     }
+    return t;
+}
+
+// One lane = one DAE evaluation (grid point kl, lane role r).
+template <class D>
+__global__ void __launch_bounds__(64) k_eval(DevModel M, Layout L, Lanes Ln,
+        const double* __restrict__ x, const double* __restrict__ grid,
+        double* __restrict__ times, double* __restrict__ Y) {
+    const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= (long)L.nk * Ln.stride) return;
+    const int kl = (int)(gid / Ln.stride);
+    const int r = (int)(gid - (long)kl * Ln.stride);
+    const int k = L.k0 + kl;
+    double in[D::MI];
+    double out[D::MO];
+    const double t = lane_inputs<D>(L, Ln, x, grid[k], k, r, in);
+    if (r == Ln.base) times[kl] = t;
     D::eval(M, t, in, out);
     double* Yk = Y + (long)kl * L.NO * Ln.stride + r;
 #pragma unroll
     for (int o = 0; o < D::MO; ++o)
         if (o < L.NO) Yk[(long)o * Ln.stride] = out[o];
+}
+
+// Workgroup-split evaluation for muscle-driven generated models: a
+// workgroup owns 64 evaluation lanes; wave 0 runs the multibody chain
+// (kinematics, RNEA bias + external + coordinate-actuator forces, CRBA and
+// the L^T L factor of the mass matrix) while waves 1..NGROUPS each run one
+// muscle group (path kinematics, DeGroote-Fregly muscle, generalized forces
+// of the tendon point forces, activation / tendon-force derivatives straight
+// to Y).  The muscle waves meet wave 0 at one LDS barrier; wave 0 adds their
+// generalized forces and finishes the two triangular solves.  Shortens the
+// per-lane dependency chain ~3x and gives the SIMDs NGROUPS+1 independent
+// waves per 64 evaluations.
+// Inputs of one evaluation lane read where used (L1/L2-resident x) instead
+// of held in VGPRs: a lane's 60+ doubles would otherwise take half the
+// register budget of a 2-wave/SIMD launch.
+template <class D>
+struct LaneIn {
+    const double* __restrict__ xs;
+    const double* __restrict__ xc;
+    int pi;
+    double step;
+    __device__ __forceinline__ double operator[](int i) const {
+        const double v = i < D::NS ? xs[i] : xc[i - D::NS];
+        return i == pi ? v + step : v;
+    }
+};
+
+// The two roles are separate non-inlined functions so the compiler cannot
+// hoist the kinematics the roles share above the role branch (which doubles
+// the live registers of both and spills).
+template <class D>
+__device__ __attribute__((noinline)) void role_multibody(const DevModel& M, double t,
+        const LaneIn<D>& in, double* st) {
+    D::mb_factor(M, t, in, st);
+}
+template <class D>
+__device__ __attribute__((noinline)) void role_muscles(int w, const DevModel& M, double t,
+        const LaneIn<D>& in, double* tq, double* zo, long zs) {
+    D::muscles(w, M, t, in, tq, zo, zs);
+}
+
+// Body of the split evaluation for one 64-lane group: outputs to
+// Yk[o * ys] (o < NO).  Every wave of the workgroup must call it (barrier).
+template <class D>
+__device__ __forceinline__ void split_eval(const DevModel& M, double t, const LaneIn<D>& in,
+        int w, int lane, bool live, double* __restrict__ Yk, long ys,
+        double (&tau_lds)[D::NGROUPS][D::NQ][64]) {
+    if (w == 0) {
+        double st[D::NST];
+        role_multibody<D>(M, t, in, st);
+        __syncthreads();
+        double tm[D::NQ];
+#pragma unroll
+        for (int j = 0; j < D::NQ; ++j) {
+            double s = 0.0;
+#pragma unroll
+            for (int gi = 0; gi < D::NGROUPS; ++gi) s += tau_lds[gi][j][lane];
+            tm[j] = s;
+        }
+        double out[D::NQ];
+        D::mb_solve(st, tm, out);
+        if (live) {
+#pragma unroll
+            for (int o = 0; o < D::NQ; ++o) Yk[(long)o * ys] = out[o];
+        }
+    } else {
+        double tq[D::NQ];
+        double zo_dummy;
+        double* zo = live ? Yk + (long)D::NQ * ys : &zo_dummy;
+        role_muscles<D>(w - 1, M, t, in, tq, zo, live ? ys : 0);
+#pragma unroll
+        for (int j = 0; j < D::NQ; ++j) tau_lds[w - 1][j][lane] = tq[j];
+        __syncthreads();
+    }
+}
+
+template <class D>
+__global__ void __launch_bounds__((D::NGROUPS + 1) * 64) k_eval_split(DevModel M, Layout L,
+        Lanes Ln, const double* __restrict__ x, const double* __restrict__ grid,
+        double* __restrict__ times, double* __restrict__ Y) {
+    __shared__ double tau_lds[D::NGROUPS][D::NQ][64];
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const long gid = (long)blockIdx.x * 64 + lane;
+    const bool live = gid < (long)L.nk * Ln.stride;
+    const long gc = live ? gid : 0;
+    const int kl = (int)(gc / Ln.stride);
+    const int r = (int)(gc - (long)kl * Ln.stride);
+    const int k = L.k0 + kl;
+    const double g = grid[k];
+    const double t0 = x[0], tf = x[1];
+    double t = (tf - t0) * g + t0;
+    LaneIn<D> in{x + 2 + (long)k * D::NS, x + 2 + (long)D::NS * L.G + (long)k * D::NC, -1, 0.0};
+    if (r != Ln.base) {
+        int dir = r;
+        double step = Ln.fd == MH_FD_BACKWARD ? -Ln.h : Ln.h;
+        if (Ln.fd == MH_FD_CENTRAL && r >= Ln.ND) { dir = r - Ln.ND; step = -Ln.h; }
+        if (dir == 0) t = t + step * (1.0 - g);
+        else if (dir == 1) t = t + step * g;
+        in.pi = dir - 2;
+        in.step = step;
+    }
+    if (w == 0 && live && r == Ln.base) times[kl] = t;
+    split_eval<D>(M, t, in, w, lane, live, Y + (long)kl * L.NO * Ln.stride + r, Ln.stride,
+                  tau_lds);
+}
+
+// mh_eval_dae through the split path: point p = [t, states, controls].
+template <class D>
+__global__ void __launch_bounds__((D::NGROUPS + 1) * 64) k_probe_split(DevModel M, int npts,
+        const double* __restrict__ pts, double* __restrict__ outp) {
+    __shared__ double tau_lds[D::NGROUPS][D::NQ][64];
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int p = blockIdx.x * 64 + lane;
+    const bool live = p < npts;
+    const double* r = pts + (long)(live ? p : 0) * (1 + D::NI);
+    LaneIn<D> in{r + 1, r + 1 + D::NS, -1, 0.0};
+    split_eval<D>(M, r[0], in, w, lane, live, outp + (long)(live ? p : 0) * D::NO, 1, tau_lds);
 }
 
 struct Interval {
@@ -1100,8 +1227,13 @@ template <class D>
 static void be_eval(mh_ctx* c, const double* x, const Lanes& ln, double* Y) {
     Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, c->k0, c->nk};
     const long lanes = (long)c->nk * ln.stride;
-    hipLaunchKernelGGL(k_eval<D>, dim3((unsigned)((lanes + 63) / 64)), dim3(64), 0, c->stream, c->M,
-            L, ln, x, c->d_grid, c->d_times, Y);
+    const dim3 grid((unsigned)((lanes + 63) / 64));
+    if constexpr (D::SPLIT)
+        hipLaunchKernelGGL(k_eval_split<D>, grid, dim3((D::NGROUPS + 1) * 64), 0, c->stream, c->M, L,
+                ln, x, c->d_grid, c->d_times, Y);
+    else
+        hipLaunchKernelGGL(k_eval<D>, grid, dim3(64), 0, c->stream, c->M, L, ln, x, c->d_grid,
+                c->d_times, Y);
 }
 template <class D>
 static void be_integrand(mh_ctx* c, const double* x) {
@@ -1118,8 +1250,14 @@ static void be_grad(mh_ctx* c, const double* x) {
 }
 template <class D>
 static void be_probe(mh_ctx* c, int np, const double* in, double* out) {
-    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, 0, 0};
-    hipLaunchKernelGGL(k_dae_probe<D>, dim3((np + 63) / 64), dim3(64), 0, c->stream, c->M, L, np, in, out);
+    if constexpr (D::SPLIT) {
+        hipLaunchKernelGGL(k_probe_split<D>, dim3((np + 63) / 64), dim3((D::NGROUPS + 1) * 64), 0,
+                c->stream, c->M, np, in, out);
+    } else {
+        Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, 0, 0};
+        hipLaunchKernelGGL(k_dae_probe<D>, dim3((np + 63) / 64), dim3(64), 0, c->stream, c->M, L, np,
+                in, out);
+    }
 }
 template <class D>
 static constexpr Backend make_backend(const char* name, double flops) {

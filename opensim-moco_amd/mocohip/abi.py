@@ -205,6 +205,13 @@ def load_mocohip(path: str | None = None):
     fallback for the hot path."""
     path = path or LIBMOCOHIP_PATH
     if path not in _libs:
+        # One HIP runtime per process: if PyTorch is installed, load it first so
+        # libmocohip binds (by soname) to the same libamdhip64 as torch and
+        # torch-allocated device pointers can be passed to the *_device calls.
+        try:
+            import torch  # noqa: F401
+        except Exception:
+            pass
         if not os.path.exists(path):
             raise RuntimeError(
                 f"libmocohip.so not built at {path}; run "

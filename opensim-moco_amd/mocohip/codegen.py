@@ -233,53 +233,60 @@ class ModelView:
         self.gravity = list(st.gravity)
 
 
-def generate(cm, struct_name: str) -> Tuple[str, Dict]:
-    """Return (C++ source of `struct <struct_name>`, info dict with counts)."""
-    M = ModelView(cm)
-    g = Gen()
-    NQ = M.nq
-    # ---- state layout ----------------------------------------------------
-    z = 2 * NQ
-    act_state, ftn_state, mus_control = [], [], [-1] * len(M.muscles)
-    tau_act = tau_deact = None
-    for mu in M.muscles:
-        if mu.tendon_dynamics_implicit and not mu.ignore_tendon_compliance:
-            raise NotImplementedError("implicit tendon dynamics")
-        act_state.append(-1 if mu.ignore_activation_dynamics else z)
-        z += 0 if mu.ignore_activation_dynamics else 1
-        ftn_state.append(-1 if mu.ignore_tendon_compliance else z)
-        z += 0 if mu.ignore_tendon_compliance else 1
-        if not mu.ignore_activation_dynamics and tau_act is None:
-            tau_act, tau_deact = mu.activation_time_constant, mu.deactivation_time_constant
-    NS, NC = z, len(M.acts)
-    NZ, NO, NI = NS - 2 * NQ, NQ + NS - 2 * NQ, NS + NC
-    for ia, a in enumerate(M.acts):
-        if a.kind == abi.MH_ACT_MUSCLE:
-            mus_control[a.target] = ia
-    inp = [S(n=f"in[{i}]") for i in range(NI)]
-    q = inp[:NQ]
-    u = inp[NQ:2 * NQ]
-    ctrl = inp[NS:NS + NC]
-    time = S(n="t")
+class _Layout:
+    def __init__(self, M: ModelView):
+        NQ = M.nq
+        z = 2 * NQ
+        self.act_state, self.ftn_state = [], []
+        self.mus_control = [-1] * len(M.muscles)
+        self.tau_act = self.tau_deact = None
+        for mu in M.muscles:
+            if mu.tendon_dynamics_implicit and not mu.ignore_tendon_compliance:
+                raise NotImplementedError("implicit tendon dynamics")
+            self.act_state.append(-1 if mu.ignore_activation_dynamics else z)
+            z += 0 if mu.ignore_activation_dynamics else 1
+            self.ftn_state.append(-1 if mu.ignore_tendon_compliance else z)
+            z += 0 if mu.ignore_tendon_compliance else 1
+            if not mu.ignore_activation_dynamics and self.tau_act is None:
+                self.tau_act = mu.activation_time_constant
+                self.tau_deact = mu.deactivation_time_constant
+        self.NQ, self.NS, self.NC = NQ, z, len(M.acts)
+        self.NZ = z - 2 * NQ
+        self.NO = NQ + self.NZ
+        self.NI = self.NS + self.NC
+        for ia, a in enumerate(M.acts):
+            if a.kind == abi.MH_ACT_MUSCLE:
+                self.mus_control[a.target] = ia
 
-    # ---- functions of one coordinate --------------------------------------
-    fcache: Dict[int, Tuple[S, S, S]] = {}
 
-    def fn_eval(fi: int):
-        if fi in fcache:
-            return fcache[fi]
+class _Emitter:
+    """Emits one device function body (a fresh Gen) for a model."""
+
+    def __init__(self, M: ModelView, Lo: _Layout):
+        self.M, self.Lo = M, Lo
+        self.g = Gen()
+        self.inp = [S(n=f"in[{i}]") for i in range(Lo.NI)]
+        self.q = self.inp[:Lo.NQ]
+        self.u = self.inp[Lo.NQ:2 * Lo.NQ]
+        self.ctrl = self.inp[Lo.NS:Lo.NS + Lo.NC]
+        self.fcache: Dict[int, Tuple[S, S, S]] = {}
+
+    # functions of one coordinate
+    def fn_eval(self, fi: int):
+        g, M = self.g, self.M
+        if fi in self.fcache:
+            return self.fcache[fi]
         F = M.funcs[fi]
         if F.kind == abi.MH_FN_CONSTANT:
             r = (_c(F.a), _c(0.0), _c(0.0))
         elif F.kind == abi.MH_FN_LINEAR:
-            # value = scale * (a*q + b)
-            r = (g.mul(_c(F.scale), g.add(g.mul(_c(F.a), q[F.coord]), _c(F.b))),
+            r = (g.mul(_c(F.scale), g.add(g.mul(_c(F.a), self.q[F.coord]), _c(F.b))),
                  _c(F.scale * F.a), _c(0.0))
         else:
             g.k += 1
             base = f"f{g.k}"
             g.raw(f"double {base}v, {base}d1, {base}d2;")
-            g.raw(f"mh::simm_eval_n<{F.knot_count}>(M, {F.knot_begin}, {q[F.coord]}, "
+            g.raw(f"mh::simm_eval_n<{F.knot_count}>(M, {F.knot_begin}, {self.q[F.coord]}, "
                   f"{base}v, {base}d1, {base}d2);")
             g.flops["add"] += 6
             g.flops["mul"] += 8
@@ -287,93 +294,97 @@ def generate(cm, struct_name: str) -> Tuple[str, Dict]:
             if F.scale != 1.0:
                 v, d1, d2 = g.mul(_c(F.scale), v), g.mul(_c(F.scale), d1), g.mul(_c(F.scale), d2)
             r = (v, d1, d2)
-        fcache[fi] = r
+        self.fcache[fi] = r
         return r
 
-    # ---- kinematics + RNEA forward pass ----------------------------------
-    I3 = _vec([1, 0, 0, 0, 1, 0, 0, 0, 1])
-    Z3 = _vec([0, 0, 0])
-    R = {-1: I3}
-    P = {-1: Z3}
-    V = {-1: (Z3, Z3)}
-    A = {-1: (Z3, _vec([-M.gravity[0], -M.gravity[1], -M.gravity[2]]))}
-    Sj = [(Z3, Z3) for _ in range(NQ)]
-    coord_body = [-1] * NQ
-    Fb: Dict[int, Tuple] = {}
-    Ibody: Dict[int, Tuple] = {}
-    g.raw("// ---- kinematics, velocities, bias accelerations, RNEA forward ----")
-    for b, B in enumerate(M.bodies):
-        p = B.parent
-        RPF = _vec(B.R_PF)
-        RGF = g.mm(R[p], RPF)
-        pGF = g.vadd(P[p], g.mv(R[p], _vec(B.p_PF)))
-        Vb, Ab, Vpar = V[p], A[p], V[p]
-        axes = M.axes[B.axis_begin:B.axis_begin + B.axis_count]
-        fvals = [fn_eval(ax.func) for ax in axes]
-        pFM = Z3
-        for ax, fv in zip(axes, fvals):
-            if ax.type == abi.MH_AXIS_TRANSLATION:
-                pFM = g.vadd(pFM, g.vscale(_vec(ax.dir), fv[0]))
-        oM = g.vadd(pGF, g.mv(RGF, pFM))
-        for ax, fv in zip(axes, fvals):
-            F = M.funcs[ax.func]
-            if ax.type != abi.MH_AXIS_TRANSLATION or F.kind == abi.MH_FN_CONSTANT:
-                continue
-            j = F.coord
-            coord_body[j] = b
-            s = (Z3, g.mv(RGF, _vec(ax.dir)))
-            sd = g.crm(Vpar, s)
-            thd = g.mul(fv[1], u[j])
-            thdd = g.mul(fv[2], g.mul(u[j], u[j]))
-            Vb = g.svadd(Vb, g.svscale(s, thd))
-            Ab = g.svadd(Ab, g.svadd(g.svscale(sd, thd), g.svscale(s, thdd)))
-            Sj[j] = g.svadd(Sj[j], g.svscale(s, fv[1]))
-        Rcur = I3
-        for ax, fv in zip(axes, fvals):
-            if ax.type != abi.MH_AXIS_ROTATION:
-                continue
-            F = M.funcs[ax.func]
-            if F.kind != abi.MH_FN_CONSTANT:
-                j = F.coord
+    def closure(self, bodies):
+        """Bodies plus all their ancestors, in model (topological) order."""
+        need = set()
+        for b in bodies:
+            while b >= 0 and b not in need:
+                need.add(b)
+                b = self.M.bodies[b].parent
+        return sorted(need)
+
+    def kinematics(self, bodies: Sequence[int], accel: bool):
+        """Poses, spatial velocities, (bias accelerations) and motion
+        subspaces for the given bodies (must be ancestor-closed)."""
+        g, M, q, u = self.g, self.M, self.q, self.u
+        I3 = _vec([1, 0, 0, 0, 1, 0, 0, 0, 1])
+        Z3 = _vec([0, 0, 0])
+        R, P, V, A = {-1: I3}, {-1: Z3}, {-1: (Z3, Z3)}, {}
+        if accel:
+            A[-1] = (Z3, _vec([-M.gravity[0], -M.gravity[1], -M.gravity[2]]))
+        Sj = {}
+        coord_body = {}
+        for b in bodies:
+            B = M.bodies[b]
+            p = B.parent
+            RGF = g.mm(R[p], _vec(B.R_PF))
+            pGF = g.vadd(P[p], g.mv(R[p], _vec(B.p_PF)))
+            Vb, Vpar = V[p], V[p]
+            Ab = A[p] if accel else None
+            axes = M.axes[B.axis_begin:B.axis_begin + B.axis_count]
+            fvals = [self.fn_eval(ax.func) for ax in axes]
+            pFM = Z3
+            for ax, fv in zip(axes, fvals):
+                if ax.type == abi.MH_AXIS_TRANSLATION:
+                    pFM = g.vadd(pFM, g.vscale(_vec(ax.dir), fv[0]))
+            oM = g.vadd(pGF, g.mv(RGF, pFM))
+
+            def motion(s, Vframe, fv, j):
+                nonlocal Vb, Ab
                 coord_body[j] = b
-                RGc = g.mm(RGF, Rcur)
-                w = g.mv(RGc, _vec(ax.dir))
-                s = (w, g.cross(oM, w))
-                sd = g.crm(Vb, s)
                 thd = g.mul(fv[1], u[j])
-                thdd = g.mul(fv[2], g.mul(u[j], u[j]))
                 Vb = g.svadd(Vb, g.svscale(s, thd))
-                Ab = g.svadd(Ab, g.svadd(g.svscale(sd, thd), g.svscale(s, thdd)))
-                Sj[j] = g.svadd(Sj[j], g.svscale(s, fv[1]))
-            # Rodrigues rotation about a constant unit axis
-            a0, a1, a2 = ax.dir
-            if fv[0].is_c():
-                th = fv[0].c
-                cth, sth = math.cos(th), math.sin(th)
-                cs, sn = _c(cth), _c(sth)
-            else:
-                g.k += 1
-                nm = f"sc{g.k}"
-                g.raw(f"double {nm}s, {nm}c; sincos({fv[0]}, &{nm}s, &{nm}c);")
-                g.flops["fn"] += 2
-                cs, sn = S(n=f"{nm}c"), S(n=f"{nm}s")
-            kk = g.sub(_c(1.0), cs)
-            Rk = [g.add(cs, g.mul(kk, _c(a0 * a0))), g.sub(g.mul(kk, _c(a0 * a1)), g.mul(sn, _c(a2))),
-                  g.add(g.mul(kk, _c(a0 * a2)), g.mul(sn, _c(a1))),
-                  g.add(g.mul(kk, _c(a1 * a0)), g.mul(sn, _c(a2))), g.add(cs, g.mul(kk, _c(a1 * a1))),
-                  g.sub(g.mul(kk, _c(a1 * a2)), g.mul(sn, _c(a0))),
-                  g.sub(g.mul(kk, _c(a2 * a0)), g.mul(sn, _c(a1))),
-                  g.add(g.mul(kk, _c(a2 * a1)), g.mul(sn, _c(a0))), g.add(cs, g.mul(kk, _c(a2 * a2)))]
-            Rcur = g.mm(Rcur, Rk)
-        RGM = g.mm(RGF, Rcur)
-        RB = g.mmt(RGM, _vec(B.R_BM))
-        pB = g.vsub(oM, g.mv(RB, _vec(B.p_BM)))
-        R[b], P[b], V[b], A[b] = RB, pB, Vb, Ab
-        # inertia about the origin in ground
-        cw = g.vadd(pB, g.mv(RB, _vec(B.com)))
+                if accel:
+                    sd = g.crm(Vframe, s)
+                    thdd = g.mul(fv[2], g.mul(u[j], u[j]))
+                    Ab = g.svadd(Ab, g.svadd(g.svscale(sd, thd), g.svscale(s, thdd)))
+                Sj[j] = g.svadd(Sj.get(j, (Z3, Z3)), g.svscale(s, fv[1]))
+            for ax, fv in zip(axes, fvals):
+                F = M.funcs[ax.func]
+                if ax.type != abi.MH_AXIS_TRANSLATION or F.kind == abi.MH_FN_CONSTANT:
+                    continue
+                motion((Z3, g.mv(RGF, _vec(ax.dir))), Vpar, fv, F.coord)
+            Rcur = I3
+            for ax, fv in zip(axes, fvals):
+                if ax.type != abi.MH_AXIS_ROTATION:
+                    continue
+                F = M.funcs[ax.func]
+                if F.kind != abi.MH_FN_CONSTANT:
+                    w = g.mv(g.mm(RGF, Rcur), _vec(ax.dir))
+                    motion((w, g.cross(oM, w)), Vb, fv, F.coord)
+                a0, a1, a2 = ax.dir
+                if fv[0].is_c():
+                    cs, sn = _c(math.cos(fv[0].c)), _c(math.sin(fv[0].c))
+                else:
+                    g.k += 1
+                    nm = f"sc{g.k}"
+                    g.raw(f"double {nm}s, {nm}c; sincos({fv[0]}, &{nm}s, &{nm}c);")
+                    g.flops["fn"] += 2
+                    cs, sn = S(n=f"{nm}c"), S(n=f"{nm}s")
+                kk = g.sub(_c(1.0), cs)
+                Rk = [g.add(cs, g.mul(kk, _c(a0 * a0))), g.sub(g.mul(kk, _c(a0 * a1)), g.mul(sn, _c(a2))),
+                      g.add(g.mul(kk, _c(a0 * a2)), g.mul(sn, _c(a1))),
+                      g.add(g.mul(kk, _c(a1 * a0)), g.mul(sn, _c(a2))), g.add(cs, g.mul(kk, _c(a1 * a1))),
+                      g.sub(g.mul(kk, _c(a1 * a2)), g.mul(sn, _c(a0))),
+                      g.sub(g.mul(kk, _c(a2 * a0)), g.mul(sn, _c(a1))),
+                      g.add(g.mul(kk, _c(a2 * a1)), g.mul(sn, _c(a0))), g.add(cs, g.mul(kk, _c(a2 * a2)))]
+                Rcur = g.mm(Rcur, Rk)
+            RGM = g.mm(RGF, Rcur)
+            RB = g.mmt(RGM, _vec(B.R_BM))
+            R[b], P[b], V[b] = RB, g.vsub(oM, g.mv(RB, _vec(B.p_BM))), Vb
+            if accel:
+                A[b] = Ab
+        return R, P, V, A, Sj, coord_body
+
+    def inertia(self, b, R, P):
+        g, B = self.g, self.M.bodies[b]
+        cw = g.vadd(P[b], g.mv(R[b], _vec(B.com)))
         In = B.inertia
         Ib = _vec([In[0], In[3], In[4], In[3], In[1], In[5], In[4], In[5], In[2]])
-        Ig = g.mmt(g.mm(RB, Ib), RB)
+        Ig = g.mmt(g.mm(R[b], Ib), R[b])
         m = _c(B.mass)
         c2 = g.dot(cw, cw)
         II = [g.add(Ig[0], g.mul(m, g.sub(c2, g.mul(cw[0], cw[0])))),
@@ -382,43 +393,28 @@ def generate(cm, struct_name: str) -> Tuple[str, Dict]:
               g.sub(Ig[1], g.mul(m, g.mul(cw[0], cw[1]))),
               g.sub(Ig[2], g.mul(m, g.mul(cw[0], cw[2]))),
               g.sub(Ig[5], g.mul(m, g.mul(cw[1], cw[2])))]
-        Ibody[b] = (m, g.vscale(cw, m), II)
-        Ia = g.rbi_mul(Ibody[b], Ab)
-        hV = g.rbi_mul(Ibody[b], Vb)
-        Fb[b] = g.svadd(Ia, g.crf(Vb, hV))
+        return (m, g.vscale(cw, m), II)
 
-    # body force accumulators (mutable, so muscles can add into them)
-    Facc: Dict[int, List[str]] = {}
-    for b in range(M.nb):
-        w, v = Fb[b]
-        Facc[b] = [g.var(x) for x in list(w) + list(v)]
-    tau = [g.var(_c(0.0)) for _ in range(NQ)]
-
-    def acc(name: str, val: S, sign: float = 1.0):
+    def acc(self, name: str, val: S, sign: float = 1.0):
         if val.is_c(0.0):
             return
-        if sign > 0:
-            g.raw(f"{name} += {val};")
-        else:
-            g.raw(f"{name} -= {val};")
-        g.flops["add"] += 1
+        self.g.raw(f"{name} {'+=' if sign > 0 else '-='} {val};")
+        self.g.flops["add"] += 1
 
-    # ---- actuators -----------------------------------------------------------
-    g.raw("// ---- coordinate actuators ----")
-    for ia, a in enumerate(M.acts):
-        if a.kind == abi.MH_ACT_COORDINATE:
-            acc(tau[a.target], g.mul(ctrl[ia], _c(a.optimal_force)))
-
-    # ---- muscles ---------------------------------------------------------------
-    out_z = {}
-    g.raw("// ---- muscles ----")
-    for im, mu in enumerate(M.muscles):
+    def muscle(self, im, R, P, V, Facc, tau, zdot_sink):
+        """Path geometry, DGF and tension point forces of muscle im.  Point
+        forces are subtracted into the body accumulators Facc (RNEA sign
+        convention), MovingPathPoint terms added into tau; zdot values are
+        handed to zdot_sink(state_index, S)."""
+        g, M, Lo, u, q = self.g, self.M, self.Lo, self.u, self.q
+        Z3 = _vec([0, 0, 0])
+        mu = M.muscles[im]
         g.raw(f"// muscle {im}")
         pts = M.points[mu.point_begin:mu.point_begin + mu.point_count]
         pos, vel, act, dl_funcs = [], [], [], []
         for pt in pts:
             loc = _vec(pt.loc)
-            dloc = [Z3[0], Z3[1], Z3[2]]
+            dloc = list(Z3)
             mov = []
             if pt.kind == abi.MH_PP_CONDITIONAL:
                 qv = q[pt.coord]
@@ -430,7 +426,7 @@ def generate(cm, struct_name: str) -> Tuple[str, Dict]:
                 for d, fi in enumerate((pt.fx, pt.fy, pt.fz)):
                     if fi < 0:
                         continue
-                    fv = fn_eval(fi)
+                    fv = self.fn_eval(fi)
                     loc[d] = fv[0]
                     F = M.funcs[fi]
                     if F.kind != abi.MH_FN_CONSTANT:
@@ -442,18 +438,11 @@ def generate(cm, struct_name: str) -> Tuple[str, Dict]:
             pos.append(Pw)
             vel.append(Vw)
             dl_funcs.append(mov)
-        # candidate segments (j -> i): both active, all points between inactive
         segs = []
-        n = len(pts)
-        for i in range(n):
+        for i in range(len(pts)):
             for j in range(i - 1, -1, -1):
-                conds = []
-                if act[j]:
-                    conds.append(act[j])
-                if act[i]:
-                    conds.append(act[i])
-                for k in range(j + 1, i):
-                    conds.append(f"!{act[k]}")
+                conds = [c for c in (act[j], act[i]) if c]
+                conds += [f"!{act[k]}" for k in range(j + 1, i)]
                 segs.append((j, i, " && ".join(conds) if conds else None))
                 if act[j] is None:
                     break
@@ -462,26 +451,20 @@ def generate(cm, struct_name: str) -> Tuple[str, Dict]:
         for (j, i, cond) in segs:
             d = g.vsub(pos[i], pos[j])
             l = g.fn("sqrt", g.dot(d, d))
-            dv = g.vsub(vel[i], vel[j])
-            sp = g.div(g.dot(d, dv), l)
-            if cond:
-                ind = g.sel(cond, _c(1.0), _c(0.0))
-                L = g.add(L, g.mul(ind, l))
-                Sp = g.add(Sp, g.mul(ind, sp))
-            else:
-                ind = None
-                L = g.add(L, l)
-                Sp = g.add(Sp, sp)
+            sp = g.div(g.dot(d, g.vsub(vel[i], vel[j])), l)
+            ind = g.sel(cond, _c(1.0), _c(0.0)) if cond else None
+            L = g.add(L, l if ind is None else g.mul(ind, l))
+            Sp = g.add(Sp, sp if ind is None else g.mul(ind, sp))
             seginfo.append((j, i, d, l, ind))
-        exc = ctrl[mus_control[im]]
-        sa, sf = act_state[im], ftn_state[im]
-        a_ = inp[sa] if sa >= 0 else exc
-        ftn = inp[sf] if sf >= 0 else None
-        T, adot, ftdot = _dgf(g, mu, L, Sp, a_, exc, sa >= 0, ftn, sf >= 0, tau_act, tau_deact)
+        exc = self.ctrl[Lo.mus_control[im]]
+        sa, sf = Lo.act_state[im], Lo.ftn_state[im]
+        a_ = self.inp[sa] if sa >= 0 else exc
+        ftn = self.inp[sf] if sf >= 0 else None
+        T, adot, ftdot = _dgf(g, mu, L, Sp, a_, exc, sa >= 0, ftn, sf >= 0, Lo.tau_act, Lo.tau_deact)
         if sa >= 0:
-            out_z[sa - 2 * NQ] = adot
+            zdot_sink(sa, adot)
         if sf >= 0:
-            out_z[sf - 2 * NQ] = ftdot
+            zdot_sink(sf, ftdot)
         for (j, i, d, l, ind) in seginfo:
             Tl = g.div(T, l) if ind is None else g.mul(ind, g.div(T, l))
             Fv = g.vscale(d, Tl)
@@ -493,128 +476,274 @@ def generate(cm, struct_name: str) -> Tuple[str, Dict]:
                 nrm = g.cross(pos[kk], f)
                 fa = Facc[pt.body]
                 for c in range(3):
-                    acc(fa[c], nrm[c], -1.0)
-                    acc(fa[3 + c], f[c], -1.0)
+                    self.acc(fa[c], nrm[c], -1.0)
+                    self.acc(fa[3 + c], f[c], -1.0)
                 for (dd, coord, d1) in dl_funcs[kk]:
                     Rb = R[pt.body]
-                    gg = g.mul(g.dot([Rb[dd], Rb[3 + dd], Rb[6 + dd]], f), d1)
-                    acc(tau[coord], gg)
+                    self.acc(tau[coord], g.mul(g.dot([Rb[dd], Rb[3 + dd], Rb[6 + dd]], f), d1))
 
-    # ---- external forces ---------------------------------------------------------
-    g.raw("// ---- external forces ----")
-    for e in M.ext:
-        b = e.body
-        g.k += 1
-        seg = f"seg{g.k}"
-        g.raw(f"const int {seg} = mh::table_segment(M, {e.table}, t);")
+    def body_force_vars(self, bodies, init):
+        return {b: [self.g.var(x) for x in (init(b) if init else [_c(0.0)] * 6)] for b in bodies}
 
-        def col(cidx):
-            return g.tmp(f"mh::table_value(M, {e.table}, {seg}, {cidx}, t)")
-        Fv = [col(e.force_col + d) for d in range(3)] if e.force_col >= 0 else Z3
-        Pp = [col(e.point_col + d) for d in range(3)] if e.point_col >= 0 else P[b]
-        Tq = [col(e.torque_col + d) for d in range(3)] if e.torque_col >= 0 else Z3
-        nrm = g.vadd(g.cross(Pp, Fv), Tq)
-        for c in range(3):
-            acc(Facc[b][c], nrm[c], -1.0)
-            acc(Facc[b][3 + c], Fv[c], -1.0)
+    def backward(self, bodies, Facc, Sj, coord_body, tau):
+        """F_parent += F_child over `bodies` (descending), then
+        tau_j -= S_j . F_body(j)."""
+        g, M = self.g, self.M
+        bset = set(bodies)
+        for b in sorted(bodies, reverse=True):
+            p = M.bodies[b].parent
+            if p >= 0 and p in bset:
+                for c in range(6):
+                    g.raw(f"{Facc[p][c]} += {Facc[b][c]};")
+                    g.flops["add"] += 1
+        for j, b in sorted(coord_body.items()):
+            fa = Facc[b]
+            fsv = ([S(n=fa[0]), S(n=fa[1]), S(n=fa[2])], [S(n=fa[3]), S(n=fa[4]), S(n=fa[5])])
+            self.acc(tau[j], g.svdot(Sj[j], fsv), -1.0)
 
-    # ---- RNEA backward ----------------------------------------------------------------
-    g.raw("// ---- RNEA backward pass ----")
-    for b in range(M.nb - 1, -1, -1):
-        p = M.bodies[b].parent
-        if p >= 0:
-            for c in range(6):
-                g.raw(f"{Facc[p][c]} += {Facc[b][c]};")
-                g.flops["add"] += 1
-    for j in range(NQ):
-        fa = Facc[coord_body[j]]
-        fsv = ([S(n=fa[0]), S(n=fa[1]), S(n=fa[2])], [S(n=fa[3]), S(n=fa[4]), S(n=fa[5])])
-        acc(tau[j], g.svdot(Sj[j], fsv), -1.0)
+    def mass_matrix_factor(self, Ibody, Sj, coord_body):
+        """CRBA composite inertias + Featherstone L^T L on the coordinate
+        tree.  Returns (lam, H) with H the factor entries."""
+        g, M, NQ = self.g, self.M, self.Lo.NQ
+        Ic = dict(Ibody)
+        for b in range(M.nb - 1, -1, -1):
+            p = M.bodies[b].parent
+            if p >= 0:
+                mp, hp, Ip = Ic[p]
+                mb, hb, Ibb = Ic[b]
+                Ic[p] = (g.add(mp, mb), g.vadd(hp, hb), [g.add(x, y) for x, y in zip(Ip, Ibb)])
+        body_coords: Dict[int, List[int]] = {}
+        for j in range(NQ):
+            body_coords.setdefault(coord_body[j], []).append(j)
 
-    # ---- CRBA --------------------------------------------------------------------------
-    g.raw("// ---- composite inertias and mass matrix ----")
-    Ic = {b: Ibody[b] for b in range(M.nb)}
-    for b in range(M.nb - 1, -1, -1):
-        p = M.bodies[b].parent
-        if p >= 0:
-            mp, hp, Ip = Ic[p]
-            mb, hb, Ibb = Ic[b]
-            Ic[p] = (g.add(mp, mb), g.vadd(hp, hb), [g.add(x, y) for x, y in zip(Ip, Ibb)])
-    # coordinate tree parent lambda(k)
-    body_coords: Dict[int, List[int]] = {}
-    for j in range(NQ):
-        body_coords.setdefault(coord_body[j], []).append(j)
-
-    def anc_coord(b):
-        p = M.bodies[b].parent
-        while p >= 0:
-            if p in body_coords:
-                return body_coords[p][-1]
-            p = M.bodies[p].parent
-        return -1
-    lam = [-1] * NQ
-    for b, cs in body_coords.items():
-        for idx, j in enumerate(cs):
-            lam[j] = cs[idx - 1] if idx > 0 else anc_coord(b)
-    for j in range(NQ):
-        if lam[j] >= j:
-            raise ValueError("coordinates must be ordered parents-first")
-    H: Dict[Tuple[int, int], S] = {}
-    for i in range(NQ):
-        b = coord_body[i]
-        Fi = g.rbi_mul(Ic[b], Sj[i])
-        j = i
-        while j >= 0:
-            H[(i, j)] = g.svdot(Sj[j], Fi)
-            j = lam[j]
-    # Featherstone L^T L factorization (fill-free on the coordinate tree)
-    g.raw("// ---- L^T L factorization and solve ----")
-    for k in range(NQ - 1, -1, -1):
-        a = g.fn("sqrt", H[(k, k)])
-        H[(k, k)] = a
-        i = lam[k]
-        while i >= 0:
-            H[(k, i)] = g.div(H[(k, i)], a)
-            i = lam[i]
-        i = lam[k]
-        while i >= 0:
+        def anc_coord(b):
+            p = M.bodies[b].parent
+            while p >= 0:
+                if p in body_coords:
+                    return body_coords[p][-1]
+                p = M.bodies[p].parent
+            return -1
+        lam = [-1] * NQ
+        for b, cs in body_coords.items():
+            for idx, j in enumerate(cs):
+                lam[j] = cs[idx - 1] if idx > 0 else anc_coord(b)
+        for j in range(NQ):
+            if lam[j] >= j:
+                raise ValueError("coordinates must be ordered parents-first")
+        H: Dict[Tuple[int, int], S] = {}
+        for i in range(NQ):
+            Fi = g.rbi_mul(Ic[coord_body[i]], Sj[i])
             j = i
             while j >= 0:
-                H[(i, j)] = g.sub(H[(i, j)], g.mul(H[(k, i)], H[(k, j)]))
+                H[(i, j)] = g.svdot(Sj[j], Fi)
                 j = lam[j]
-            i = lam[i]
-    bvec = [S(n=t) for t in tau]
-    xs = [None] * NQ
-    for i in range(NQ - 1, -1, -1):
-        xs[i] = g.div(bvec[i], H[(i, i)])
-        j = lam[i]
-        while j >= 0:
-            bvec[j] = g.sub(bvec[j], g.mul(H[(i, j)], xs[i]))
-            j = lam[j]
+        for k in range(NQ - 1, -1, -1):
+            a = g.fn("sqrt", H[(k, k)])
+            H[(k, k)] = a
+            i = lam[k]
+            while i >= 0:
+                H[(k, i)] = g.div(H[(k, i)], a)
+                i = lam[i]
+            i = lam[k]
+            while i >= 0:
+                j = i
+                while j >= 0:
+                    H[(i, j)] = g.sub(H[(i, j)], g.mul(H[(k, i)], H[(k, j)]))
+                    j = lam[j]
+                i = lam[i]
+        return lam, H
+
+    def solve(self, lam, H, bvec):
+        g, NQ = self.g, self.Lo.NQ
+        bvec = list(bvec)
+        xs = [None] * NQ
+        for i in range(NQ - 1, -1, -1):
+            xs[i] = g.div(bvec[i], H[(i, i)])
+            j = lam[i]
+            while j >= 0:
+                bvec[j] = g.sub(bvec[j], g.mul(H[(i, j)], xs[i]))
+                j = lam[j]
+        for i in range(NQ):
+            j = lam[i]
+            xi = xs[i]
+            while j >= 0:
+                xi = g.sub(xi, g.mul(H[(i, j)], xs[j]))
+                j = lam[j]
+            xs[i] = g.div(xi, H[(i, i)])
+        return xs
+
+    def external_forces(self, P, Facc):
+        g, M = self.g, self.M
+        Z3 = _vec([0, 0, 0])
+        for e in M.ext:
+            b = e.body
+            g.k += 1
+            seg = f"seg{g.k}"
+            g.raw(f"const int {seg} = mh::table_segment(M, {e.table}, t);")
+
+            def col(cidx):
+                return g.tmp(f"mh::table_value(M, {e.table}, {seg}, {cidx}, t)")
+            Fv = [col(e.force_col + d) for d in range(3)] if e.force_col >= 0 else Z3
+            Pp = [col(e.point_col + d) for d in range(3)] if e.point_col >= 0 else P[b]
+            Tq = [col(e.torque_col + d) for d in range(3)] if e.torque_col >= 0 else Z3
+            nrm = g.vadd(g.cross(Pp, Fv), Tq)
+            for c in range(3):
+                self.acc(Facc[b][c], nrm[c], -1.0)
+                self.acc(Facc[b][3 + c], Fv[c], -1.0)
+
+    def actuators(self, tau):
+        for ia, a in enumerate(self.M.acts):
+            if a.kind == abi.MH_ACT_COORDINATE:
+                self.acc(tau[a.target], self.g.mul(self.ctrl[ia], _c(a.optimal_force)))
+
+
+def _multibody_front(E: _Emitter, with_muscles: bool):
+    """Kinematics, RNEA (bias + external + coordinate actuators [+ muscles]),
+    CRBA and the L^T L factor.  Returns (tau vars, lam, H)."""
+    g, M, Lo = E.g, E.M, E.Lo
+    allb = list(range(M.nb))
+    R, P, V, A, Sj, coord_body = E.kinematics(allb, accel=True)
+    Ibody = {b: E.inertia(b, R, P) for b in allb}
+
+    def init(b):
+        Ia = g.rbi_mul(Ibody[b], A[b])
+        hV = g.rbi_mul(Ibody[b], V[b])
+        w, v = g.svadd(Ia, g.crf(V[b], hV))
+        return list(w) + list(v)
+    Facc = E.body_force_vars(allb, init)
+    tau = [g.var(_c(0.0)) for _ in range(Lo.NQ)]
+    E.actuators(tau)
+    zd = {}
+    if with_muscles:
+        for im in range(len(M.muscles)):
+            E.muscle(im, R, P, V, Facc, tau, lambda s, v: zd.__setitem__(s, v))
+    E.external_forces(P, Facc)
+    E.backward(allb, Facc, Sj, coord_body, tau)
+    lam, H = E.mass_matrix_factor(Ibody, Sj, [coord_body[j] for j in range(Lo.NQ)])
+    return tau, lam, H, zd
+
+
+def _muscle_groups(M: ModelView, ngroups: int):
+    """Greedy longest-processing-time split of muscles over waves."""
+    cost = [(len(M.points[m.point_begin:m.point_begin + m.point_count]) + 4, i)
+            for i, m in enumerate(M.muscles)]
+    cost.sort(reverse=True)
+    groups = [[] for _ in range(ngroups)]
+    load = [0] * ngroups
+    for cst, i in cost:
+        w = min(range(ngroups), key=lambda k: load[k])
+        groups[w].append(i)
+        load[w] += cst
+    return [sorted(gr) for gr in groups if gr]
+
+
+def generate(cm, struct_name: str, muscle_waves: int = 7) -> Tuple[str, Dict]:
+    """Return (C++ source of `struct <struct_name>`, info dict).
+
+    The struct has eval() (whole DAE in one lane) and, for muscle models, the
+    workgroup-split pieces used by k_eval_split: mb_factor() (multibody wave:
+    everything but muscle forces, up to the L^T L factor), mb_solve()
+    (adds the muscle generalized forces and solves) and muscles() (one muscle
+    group per wave: path, DGF, generalized forces)."""
+    M = ModelView(cm)
+    Lo = _Layout(M)
+    NQ, NZ = Lo.NQ, Lo.NZ
+    parts = []
+    info = {"NQ": NQ, "NS": Lo.NS, "NC": Lo.NC}
+
+    # ---- single-lane eval ---------------------------------------------------
+    E = _Emitter(M, Lo)
+    tau, lam, H, zd = _multibody_front(E, with_muscles=True)
+    xs = E.solve(lam, H, [S(n=t) for t in tau])
     for i in range(NQ):
-        j = lam[i]
-        xi = xs[i]
-        while j >= 0:
-            xi = g.sub(xi, g.mul(H[(i, j)], xs[j]))
-            j = lam[j]
-        xs[i] = g.div(xi, H[(i, i)])
-    for i in range(NQ):
-        g.raw(f"out[{i}] = {xs[i]};")
+        E.g.raw(f"out[{i}] = {xs[i]};")
     for zi in range(NZ):
-        g.raw(f"out[{NQ + zi}] = {out_z.get(zi, _c(0.0))};")
-    flops = dict(g.flops)
-    flops["total"] = sum(flops.values())
-    body = "\n".join(g.lines)
+        E.g.raw(f"out[{NQ + zi}] = {zd.get(2 * NQ + zi, _c(0.0))};")
+    fl = dict(E.g.flops)
+    fl["total"] = sum(fl.values())
+    info["flops"] = fl
+    info["lines"] = len(E.g.lines)
+    parts.append(("eval", "const mh::DevModel& M, const double t, const double* __restrict__ in, "
+                          "double* __restrict__ out", E.g.lines))
+
+    split = len(M.muscles) > 0 and muscle_waves > 0
+    ngroups = 0
+    nst = 0
+    if split:
+        # ---- multibody wave: factor -------------------------------------------
+        E = _Emitter(M, Lo)
+        tau, lam, H, _ = _multibody_front(E, with_muscles=False)
+        keys = sorted(H.keys())
+        st = [S(n=t) for t in tau] + [H[k] for k in keys]
+        for i, v in enumerate(st):
+            E.g.raw(f"st[{i}] = {v};")
+        nst = len(st)
+        parts.append(("mb_factor", "const mh::DevModel& M, const double t, "
+                                   "const double* __restrict__ in, double* __restrict__ st", E.g.lines))
+        # ---- multibody wave: solve with muscle forces --------------------------
+        E2 = _Emitter(M, Lo)
+        Hs = {k: S(n=f"st[{NQ + i}]") for i, k in enumerate(keys)}
+        bvec = [E2.g.add(S(n=f"st[{j}]"), S(n=f"tm[{j}]")) for j in range(NQ)]
+        xs = E2.solve(lam, Hs, bvec)
+        for i in range(NQ):
+            E2.g.raw(f"out[{i}] = {xs[i]};")
+        parts.append(("mb_solve", "const double* __restrict__ st, const double* __restrict__ tm, "
+                                  "double* __restrict__ out", E2.g.lines))
+        # ---- muscle waves ---------------------------------------------------------
+        groups = _muscle_groups(M, muscle_waves)
+        ngroups = len(groups)
+        gl = []
+        for gi, grp in enumerate(groups):
+            E3 = _Emitter(M, Lo)
+            bodies = sorted({M.points[i].body for m in grp
+                             for i in range(M.muscles[m].point_begin,
+                                            M.muscles[m].point_begin + M.muscles[m].point_count)
+                             if M.points[i].body >= 0})
+            cl = E3.closure(bodies)
+            R, P, V, _, Sj, coord_body = E3.kinematics(cl, accel=False)
+            Facc = E3.body_force_vars(cl, None)
+            tvars = [E3.g.var(_c(0.0)) for _ in range(NQ)]
+            zsink = lambda s, v, E3=E3: E3.g.raw(f"zo[{s - 2 * NQ} * zs] = {v};")
+            for m in grp:
+                E3.muscle(m, R, P, V, Facc, tvars, zsink)
+            # generalized forces of the point forces: -(S . F_subtree), since
+            # Facc holds -f_ext
+            E3.backward(cl, Facc, Sj, coord_body, tvars)
+            for j in range(NQ):
+                E3.g.raw(f"tq[{j}] = {tvars[j]};")
+            gl.append((gi, E3.g.lines, grp))
+        body = []
+        body.append("        switch (w) {")
+        for gi, lines, grp in gl:
+            body.append(f"        case {gi}: {{  // muscles {grp}")
+            body.extend("    " + l for l in lines)
+            body.append("        } break;")
+        body.append("        default: break;")
+        body.append("        }")
+        parts.append(("muscles", "const int w, const mh::DevModel& M, const double t, "
+                                 "const double* __restrict__ in, double* __restrict__ tq, "
+                                 "double* __restrict__ zo, const long zs", body))
+        info["groups"] = [grp for _, _, grp in gl]
+
+    fns = []
+    for name, args, lines in parts:
+        tpl = ""
+        if name in ("mb_factor", "muscles"):
+            # inputs through an accessor (loaded where used, not held in VGPRs)
+            tpl = "template <class IN> "
+            args = args.replace("const double* __restrict__ in", "const IN& in")
+        fns.append(f"    {tpl}__device__ __forceinline__ static void {name}({args}) {{\n"
+                   + "\n".join(lines) + "\n    }")
     src = f"""struct {struct_name} {{
-    static constexpr int NQ = {NQ}, NZ = {NZ}, NS = {NS}, NC = {NC}, NO = {NO}, NI = {NI};
-    static constexpr double FLOPS_PER_EVAL = {float(flops['total'])};
-    __device__ __forceinline__ static void eval(const mh::DevModel& M, const double t,
-            const double* __restrict__ in, double* __restrict__ out) {{
-{body}
-    }}
+    static constexpr int NQ = {NQ}, NZ = {NZ}, NS = {Lo.NS}, NC = {Lo.NC}, NO = {Lo.NO}, NI = {Lo.NI};
+    static constexpr int MI = NI, MO = NO;
+    static constexpr bool SPLIT = {"true" if split else "false"};
+    static constexpr int NGROUPS = {ngroups}, NST = {max(nst, 1)};
+    static constexpr double FLOPS_PER_EVAL = {float(fl['total'])};
+{chr(10).join(fns)}
 }};
 """
-    return src, {"NQ": NQ, "NS": NS, "NC": NC, "flops": flops, "lines": len(g.lines)}
+    return src, info
 
 
 def _dgf(g: Gen, mu, LMT: S, VMT: S, act: S, exc: S, has_act: bool, ftn: Optional[S],
