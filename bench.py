@@ -34,7 +34,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--intervals", type=int, default=200)
     ap.add_argument("--fd", default="forward")
-    ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", choices=["separate", "fused"], default="separate",
                     help="separate: eval_g then eval_jac_g C-ABI calls; fused: one "
@@ -55,6 +55,7 @@ def main():
     import torch
     import torch.distributed as dist
     from mocohip import configs
+    from mocohip.distributed import ShardGather, interval_shard
     from mocohip.solver import HipNLP
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -70,7 +71,7 @@ def main():
     st = configs.gait10dof18musc(N, fd_scheme=args.fd)
     st.solver.device = local
     rep = st.problem.create_rep()
-    ib, ie = (N * rank) // world, (N * (rank + 1)) // world
+    ib, ie = interval_shard(N, rank, world)
     nlp = HipNLP(rep, st.solver.options(ib, ie))
     x = nlp.random_iterate(np.random.default_rng(0).uniform(-1, 1, nlp.n))
     # an iterate within bounds where the muscle model is regular: bounds
@@ -81,11 +82,8 @@ def main():
     xd = torch.tensor(x, dtype=torch.float64, device=dev)
     rpi = nlp.m // N
     nzi = nlp.nnz // N
-    seg_int = (N + world - 1) // world
-    gseg = torch.zeros(seg_int * rpi, dtype=torch.float64, device=dev)
-    vseg = torch.zeros(seg_int * nzi, dtype=torch.float64, device=dev)
-    gall = torch.zeros(world * seg_int * rpi, dtype=torch.float64, device=dev) if world > 1 else None
-    vall = torch.zeros(world * seg_int * nzi, dtype=torch.float64, device=dev) if world > 1 else None
+    sg = ShardGather(N, rpi, nzi, world, dev)
+    gseg, vseg = sg.gseg, sg.vseg
 
     fd_ms = []
 
@@ -98,8 +96,7 @@ def main():
         if record:
             fd_ms.append(nlp.last_timings())
         if world > 1:
-            dist.all_gather_into_tensor(gall, gseg)
-            dist.all_gather_into_tensor(vall, vseg)
+            sg.gather()
 
     for _ in range(args.warmup):
         step()
@@ -192,7 +189,7 @@ def cpu_baseline(rep, opts, x, budget_s):
         ref.eval_jac_g(x)
         calls += 1
         el = time.perf_counter() - t0
-        if el > budget_s or calls >= 50:
+        if el > budget_s or calls >= 5000:
             break
     ref.close()
     return {"value": round(calls / el, 4), "unit": "calls/s", "cores": threads, "kind": "port",

@@ -623,28 +623,21 @@ def _multibody_front(E: _Emitter, with_muscles: bool):
     return tau, lam, H, zd
 
 
-def _muscle_groups(M: ModelView, ngroups: int):
-    """Greedy longest-processing-time split of muscles over waves."""
-    cost = [(len(M.points[m.point_begin:m.point_begin + m.point_count]) + 4, i)
-            for i, m in enumerate(M.muscles)]
-    cost.sort(reverse=True)
-    groups = [[] for _ in range(ngroups)]
-    load = [0] * ngroups
-    for cst, i in cost:
-        w = min(range(ngroups), key=lambda k: load[k])
-        groups[w].append(i)
-        load[w] += cst
-    return [sorted(gr) for gr in groups if gr]
-
-
-def generate(cm, struct_name: str, muscle_waves: int = 7) -> Tuple[str, Dict]:
+def generate(cm, struct_name: str, waves: int = 8) -> Tuple[str, Dict]:
     """Return (C++ source of `struct <struct_name>`, info dict).
 
     The struct has eval() (whole DAE in one lane) and, for muscle models, the
-    workgroup-split pieces used by k_eval_split: mb_factor() (multibody wave:
-    everything but muscle forces, up to the L^T L factor), mb_solve()
-    (adds the muscle generalized forces and solves) and muscles() (one muscle
-    group per wave: path, DGF, generalized forces)."""
+    pieces of the workgroup-split evaluation used by k_eval_split (``waves``
+    waves per 64 evaluations):
+      mass_factor()  wave 0: position kinematics, CRBA mass matrix and its
+                     L^T L factor (kept in registers across the barrier);
+      forces(w)      waves 1..: force group w -> generalized forces tq and
+                     muscle state derivatives.  Group 0 is the RNEA bias
+                     (inertial + gravity), coordinate actuators and external
+                     loads; every group also owns a set of muscles (path,
+                     DeGroote-Fregly dynamics, tension point forces), assigned
+                     longest-first by emitted FP64 op count;
+      mass_solve()   wave 0 after the barrier: H udot = sum of the groups' tq."""
     M = ModelView(cm)
     Lo = _Layout(M)
     NQ, NZ = Lo.NQ, Lo.NZ
@@ -666,69 +659,103 @@ def generate(cm, struct_name: str, muscle_waves: int = 7) -> Tuple[str, Dict]:
     parts.append(("eval", "const mh::DevModel& M, const double t, const double* __restrict__ in, "
                           "double* __restrict__ out", E.g.lines))
 
-    split = len(M.muscles) > 0 and muscle_waves > 0
+    split = len(M.muscles) > 0 and waves > 2
     ngroups = 0
     nst = 0
     if split:
-        # ---- multibody wave: factor -------------------------------------------
+        # ---- wave 0: mass matrix (CRBA) and its L^T L factor --------------------
         E = _Emitter(M, Lo)
-        tau, lam, H, _ = _multibody_front(E, with_muscles=False)
+        allb = list(range(M.nb))
+        R, P, _, _, Sj, coord_body = E.kinematics(allb, accel=False)
+        Ibody = {b: E.inertia(b, R, P) for b in allb}
+        lam, H = E.mass_matrix_factor(Ibody, Sj, [coord_body[j] for j in range(NQ)])
         keys = sorted(H.keys())
-        st = [S(n=t) for t in tau] + [H[k] for k in keys]
-        for i, v in enumerate(st):
-            E.g.raw(f"st[{i}] = {v};")
-        nst = len(st)
-        parts.append(("mb_factor", "const mh::DevModel& M, const double t, "
-                                   "const double* __restrict__ in, double* __restrict__ st", E.g.lines))
-        # ---- multibody wave: solve with muscle forces --------------------------
+        for i, k in enumerate(keys):
+            E.g.raw(f"st[{i}] = {H[k]};")
+        nst = len(keys)
+        info["mass_flops"] = sum(E.g.flops.values())
+        parts.append(("mass_factor", "const mh::DevModel& M, const double t, "
+                                     "const double* __restrict__ in, double* __restrict__ st", E.g.lines))
+        # ---- wave 0 after the barrier: solve with the summed forces -------------
         E2 = _Emitter(M, Lo)
-        Hs = {k: S(n=f"st[{NQ + i}]") for i, k in enumerate(keys)}
-        bvec = [E2.g.add(S(n=f"st[{j}]"), S(n=f"tm[{j}]")) for j in range(NQ)]
-        xs = E2.solve(lam, Hs, bvec)
+        Hs = {k: S(n=f"st[{i}]") for i, k in enumerate(keys)}
+        xs = E2.solve(lam, Hs, [S(n=f"tm[{j}]") for j in range(NQ)])
         for i in range(NQ):
             E2.g.raw(f"out[{i}] = {xs[i]};")
-        parts.append(("mb_solve", "const double* __restrict__ st, const double* __restrict__ tm, "
-                                  "double* __restrict__ out", E2.g.lines))
-        # ---- muscle waves ---------------------------------------------------------
-        groups = _muscle_groups(M, muscle_waves)
-        ngroups = len(groups)
-        gl = []
-        for gi, grp in enumerate(groups):
-            E3 = _Emitter(M, Lo)
-            bodies = sorted({M.points[i].body for m in grp
-                             for i in range(M.muscles[m].point_begin,
-                                            M.muscles[m].point_begin + M.muscles[m].point_count)
-                             if M.points[i].body >= 0})
-            cl = E3.closure(bodies)
-            R, P, V, _, Sj, coord_body = E3.kinematics(cl, accel=False)
-            Facc = E3.body_force_vars(cl, None)
-            tvars = [E3.g.var(_c(0.0)) for _ in range(NQ)]
-            zsink = lambda s, v, E3=E3: E3.g.raw(f"zo[{s - 2 * NQ} * zs] = {v};")
-            for m in grp:
-                E3.muscle(m, R, P, V, Facc, tvars, zsink)
-            # generalized forces of the point forces: -(S . F_subtree), since
-            # Facc holds -f_ext
-            E3.backward(cl, Facc, Sj, coord_body, tvars)
+        info["solve_flops"] = sum(E2.g.flops.values())
+        parts.append(("mass_solve", "const double* __restrict__ st, const double* __restrict__ tm, "
+                                    "double* __restrict__ out", E2.g.lines))
+
+        # ---- waves 1..: force groups -------------------------------------------
+        def emit_group(bias, muscles):
+            Eg = _Emitter(M, Lo)
+            tv = [Eg.g.var(_c(0.0)) for _ in range(NQ)]
+            zsink = lambda s, v: Eg.g.raw(f"zo[{s - 2 * NQ} * zs] = {v};")
+            if bias:
+                # RNEA bias (inertial + gravity), coordinate actuators and
+                # external loads over the whole tree
+                R, P, V, A, Sj, cb = Eg.kinematics(allb, accel=True)
+                Ib = {b: Eg.inertia(b, R, P) for b in allb}
+
+                def init(b):
+                    Ia = Eg.g.rbi_mul(Ib[b], A[b])
+                    hV = Eg.g.rbi_mul(Ib[b], V[b])
+                    w, v = Eg.g.svadd(Ia, Eg.g.crf(V[b], hV))
+                    return list(w) + list(v)
+                cl = allb
+                Facc = Eg.body_force_vars(allb, init)
+                Eg.actuators(tv)
+                Eg.external_forces(P, Facc)
+            else:
+                bodies = sorted({M.points[i].body for m in muscles
+                                 for i in range(M.muscles[m].point_begin,
+                                                M.muscles[m].point_begin + M.muscles[m].point_count)
+                                 if M.points[i].body >= 0})
+                cl = Eg.closure(bodies)
+                R, P, V, _, Sj, cb = Eg.kinematics(cl, accel=False)
+                Facc = Eg.body_force_vars(cl, None)
+            for m in muscles:
+                Eg.muscle(m, R, P, V, Facc, tv, zsink)
+            # generalized forces: tau_j -= S_j . F_subtree (Facc holds the
+            # RNEA sign: inertial/bias minus applied)
+            Eg.backward(cl, Facc, Sj, cb, tv)
             for j in range(NQ):
-                E3.g.raw(f"tq[{j}] = {tvars[j]};")
-            gl.append((gi, E3.g.lines, grp))
-        body = []
-        body.append("        switch (w) {")
-        for gi, lines, grp in gl:
-            body.append(f"        case {gi}: {{  // muscles {grp}")
+                Eg.g.raw(f"tq[{j}] = {tv[j]};")
+            return Eg.g.lines, sum(Eg.g.flops.values())
+
+        nforce = waves - 1
+        _, bias_cost = emit_group(True, [])
+        cost = {m: emit_group(False, [m])[1] for m in range(len(M.muscles))}
+        bins = [[] for _ in range(nforce)]
+        load = [0.0] * nforce
+        load[0] = bias_cost
+        for m in sorted(cost, key=lambda m: -cost[m]):
+            w = min(range(nforce), key=lambda k: load[k])
+            bins[w].append(m)
+            load[w] += cost[m]
+        gl = []
+        for gi, grp in enumerate(bins):
+            if gi > 0 and not grp:
+                continue
+            lines, gfl = emit_group(gi == 0, sorted(grp))
+            gl.append((gi, lines, sorted(grp), gfl))
+        ngroups = len(gl)
+        info["group_flops"] = [c for *_, c in gl]
+        info["groups"] = [grp for _, _, grp, _ in gl]
+        body = ["        switch (w) {"]
+        for gi, (_, lines, grp, _) in enumerate(gl):
+            body.append(f"        case {gi}: {{  // {'bias + ' if gi == 0 else ''}muscles {grp}")
             body.extend("    " + l for l in lines)
             body.append("        } break;")
-        body.append("        default: break;")
-        body.append("        }")
-        parts.append(("muscles", "const int w, const mh::DevModel& M, const double t, "
-                                 "const double* __restrict__ in, double* __restrict__ tq, "
-                                 "double* __restrict__ zo, const long zs", body))
-        info["groups"] = [grp for _, _, grp in gl]
+        body += ["        default: break;", "        }"]
+        parts.append(("forces", "const int w, const mh::DevModel& M, const double t, "
+                                "const double* __restrict__ in, double* __restrict__ tq, "
+                                "double* __restrict__ zo, const long zs", body))
 
     fns = []
     for name, args, lines in parts:
         tpl = ""
-        if name in ("mb_factor", "muscles"):
+        if name in ("mass_factor", "forces"):
             # inputs through an accessor (loaded where used, not held in VGPRs)
             tpl = "template <class IN> "
             args = args.replace("const double* __restrict__ in", "const IN& in")
