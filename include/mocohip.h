@@ -334,6 +334,13 @@ int mh_get_backend(const mh_ctx* ctx, char* name, int32_t name_len,
 /* FNV-1a hash of everything the per-point DAE depends on (host only). */
 int mh_model_hash(const mh_model* model, uint64_t* hash);
 
+/* Work of one DAE stage on this context: [0] FP64 operations executed per
+ * eval_jac_g, [1] per eval_g, [2] group evaluations per eval_jac_g (task
+ * back ends; 0 otherwise), [3] DAE evaluations a full re-evaluation per
+ * finite-difference lane would need per eval_jac_g.  0 where unknown (the
+ * generic interpreter's op count is not tracked). */
+int mh_get_work(const mh_ctx* ctx, double* work4);
+
 /* Timing of the last evaluation on the context stream (HIP events), in ms:
  * [0] whole call, [1] DAE/FD kernel, [2] assembly kernel. */
 int mh_last_timings(const mh_ctx* ctx, double* ms3);

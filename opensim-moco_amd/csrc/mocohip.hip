@@ -171,20 +171,30 @@ __global__ void __launch_bounds__(64) k_eval(DevModel M, Layout L, Lanes Ln,
         if (o < L.NO) Yk[(long)o * Ln.stride] = out[o];
 }
 
-// Workgroup-split evaluation for muscle-driven generated models: a
-// workgroup owns 64 evaluation lanes.  Wave 0 builds the mass matrix (CRBA)
-// and its L^T L factor; waves 1..NGROUPS each evaluate one force group
-// (group 0: RNEA bias + gravity + coordinate actuators + external loads;
-// every group: a set of muscles -- path kinematics, DeGroote-Fregly
-// dynamics, generalized forces of the tendon point forces, activation /
-// tendon-force derivatives written straight to Y).  The groups hand their
-// generalized forces to wave 0 through LDS at one barrier; wave 0 sums them
-// and runs the two triangular solves.  Shortens the per-lane dependency
-// chain ~4x against the one-lane kernel and gives every SIMD independent
-// waves to interleave.
+// ------------------------------------------------------------------------
+// Task-decomposed evaluation for generated models.
+//
+// A DAE evaluation is split into independent groups (mocohip/codegen.py
+// _emit_groups): the mass-matrix factor, the RNEA bias forces, one group per
+// external load and one per muscle.  Each group reads a known subset of the
+// point inputs, so a finite-difference lane only re-evaluates the groups
+// that read its perturbed input and takes every other group's result from
+// the unperturbed (base) lane of the same grid point:
+//
+//   k_groups   one wave = one group for 64 (grid point, lane role) tasks;
+//              results to T (force groups) / H (mass factor) in HBM.
+//   k_combine  one lane = one (grid point, lane role): sums the generalized
+//              forces of all groups in a fixed order, adds the coordinate
+//              actuators, solves with the mass factor, evaluates activation
+//              dynamics, writes the raw outputs Y.
+//
+// The fixed summation order makes a reused group result bit-identical to
+// re-evaluating it, so the Jacobian equals that of full re-evaluation per
+// direction (tests/test_gpu_parity.py::test_pruned_tasks_bit_identical).
+// ------------------------------------------------------------------------
+
 // Inputs of one evaluation lane read where used (L1/L2-resident x) instead
-// of held in VGPRs: a lane's 60+ doubles would otherwise take half the
-// register budget of a 2-wave/SIMD launch.
+// of held in VGPRs.
 template <class D>
 struct LaneIn {
     const double* __restrict__ xs;
@@ -197,74 +207,28 @@ struct LaneIn {
     }
 };
 
-// Each role launders its input pointers through an empty asm so the
-// compiler cannot hoist the kinematics the roles share above the role branch
-// (which would double the live registers of both and spill).
-template <class D>
-__device__ __forceinline__ LaneIn<D> opaque(const LaneIn<D>& in) {
-    LaneIn<D> r = in;
-    asm volatile("" : "+v"(r.xs), "+v"(r.xc));
-    return r;
-}
-__device__ __forceinline__ DevModel opaque_model(const DevModel& M) {
-    DevModel r = M;
-    asm volatile("" : "+s"(r.kx), "+s"(r.ky), "+s"(r.kb), "+s"(r.kc), "+s"(r.kd), "+s"(r.brk),
-                 "+s"(r.coef));
-    return r;
-}
+// Where lane inputs come from: the NLP iterate x (grid times) or explicit
+// points [t, states, controls] (mh_eval_dae).
+struct Src {
+    const double* x;
+    const double* grid;
+    const double* pts;   // non-null: explicit points
+    int G, k0;
+};
 
-// Body of the split evaluation for one 64-lane group: outputs to
-// Yk[o * ys] (o < NO).  Every wave of the workgroup must call it (barrier).
 template <class D>
-__device__ __forceinline__ void split_eval(const DevModel& M, double t, const LaneIn<D>& in,
-        int w, int lane, bool live, double* __restrict__ Yk, long ys,
-        double (&tau_lds)[D::NGROUPS][D::NQ][64]) {
-    if (w == 0) {
-        double st[D::NST];
-        D::mass_factor(opaque_model(M), t, opaque(in), st);
-        __syncthreads();
-        double tm[D::NQ];
-#pragma unroll
-        for (int j = 0; j < D::NQ; ++j) {
-            double s = 0.0;
-#pragma unroll
-            for (int gi = 0; gi < D::NGROUPS; ++gi) s += tau_lds[gi][j][lane];
-            tm[j] = s;
-        }
-        double out[D::NQ];
-        D::mass_solve(st, tm, out);
-        if (live) {
-#pragma unroll
-            for (int o = 0; o < D::NQ; ++o) Yk[(long)o * ys] = out[o];
-        }
-    } else {
-        double tq[D::NQ];
-        double zo_dummy;
-        double* zo = live ? Yk + (long)D::NQ * ys : &zo_dummy;
-        D::forces(w - 1, opaque_model(M), t, opaque(in), tq, zo, live ? ys : 0);
-#pragma unroll
-        for (int j = 0; j < D::NQ; ++j) tau_lds[w - 1][j][lane] = tq[j];
-        __syncthreads();
+__device__ __forceinline__ LaneIn<D> lane_input(const Src& S, const Lanes& Ln, int kl, int r,
+        double& t) {
+    if (S.pts) {
+        const double* p = S.pts + (long)kl * (1 + D::NI);
+        t = p[0];
+        return LaneIn<D>{p + 1, p + 1 + D::NS, -1, 0.0};
     }
-}
-
-template <class D>
-__global__ void __launch_bounds__((D::NGROUPS + 1) * 64) k_eval_split(DevModel M, Layout L,
-        Lanes Ln, const double* __restrict__ x, const double* __restrict__ grid,
-        double* __restrict__ times, double* __restrict__ Y) {
-    __shared__ double tau_lds[D::NGROUPS][D::NQ][64];
-    const int lane = threadIdx.x & 63;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const long gid = (long)blockIdx.x * 64 + lane;
-    const bool live = gid < (long)L.nk * Ln.stride;
-    const long gc = live ? gid : 0;
-    const int kl = (int)(gc / Ln.stride);
-    const int r = (int)(gc - (long)kl * Ln.stride);
-    const int k = L.k0 + kl;
-    const double g = grid[k];
-    const double t0 = x[0], tf = x[1];
-    double t = (tf - t0) * g + t0;
-    LaneIn<D> in{x + 2 + (long)k * D::NS, x + 2 + (long)D::NS * L.G + (long)k * D::NC, -1, 0.0};
+    const int k = S.k0 + kl;
+    const double g = S.grid[k];
+    const double t0 = S.x[0], tf = S.x[1];
+    t = (tf - t0) * g + t0;
+    LaneIn<D> in{S.x + 2 + (long)k * D::NS, S.x + 2 + (long)D::NS * S.G + (long)k * D::NC, -1, 0.0};
     if (r != Ln.base) {
         int dir = r;
         double step = Ln.fd == MH_FD_BACKWARD ? -Ln.h : Ln.h;
@@ -274,23 +238,85 @@ __global__ void __launch_bounds__((D::NGROUPS + 1) * 64) k_eval_split(DevModel M
         in.pi = dir - 2;
         in.step = step;
     }
-    if (w == 0 && live && r == Ln.base) times[kl] = t;
-    split_eval<D>(M, t, in, w, lane, live, Y + (long)kl * L.NO * Ln.stride + r, Ln.stride,
-                  tau_lds);
+    return in;
 }
 
-// mh_eval_dae through the split path: point p = [t, states, controls].
+// Device task tables (built on the host per lane configuration).
+struct Tasks {
+    int ng, stride, nslot, nmass, nk;
+    const int* dlen;     // [ng] tasks per grid point of group g
+    const int* off;      // [ng] slot offset of force group g within a grid point
+    const int* roles;    // [ng][stride] j -> lane role
+    const int* jd;       // [ng][stride] lane role -> j (0 = base)
+    const int* blk;      // [nblocks][2] (group, first task)
+};
+
 template <class D>
-__global__ void __launch_bounds__((D::NGROUPS + 1) * 64) k_probe_split(DevModel M, int npts,
-        const double* __restrict__ pts, double* __restrict__ outp) {
-    __shared__ double tau_lds[D::NGROUPS][D::NQ][64];
-    const int lane = threadIdx.x & 63;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int p = blockIdx.x * 64 + lane;
-    const bool live = p < npts;
-    const double* r = pts + (long)(live ? p : 0) * (1 + D::NI);
-    LaneIn<D> in{r + 1, r + 1 + D::NS, -1, 0.0};
-    split_eval<D>(M, r[0], in, w, lane, live, outp + (long)(live ? p : 0) * D::NO, 1, tau_lds);
+__global__ void __launch_bounds__(64) k_groups(DevModel M, Src S, Lanes Ln, Tasks TK,
+        double* __restrict__ T, double* __restrict__ H) {
+    const int lane = threadIdx.x;
+    const int g = __builtin_amdgcn_readfirstlane(TK.blk[2 * blockIdx.x]);
+    const int first = __builtin_amdgcn_readfirstlane(TK.blk[2 * blockIdx.x + 1]);
+    const int n = __builtin_amdgcn_readfirstlane(TK.dlen[g]);
+    const int task = first + lane;
+    const bool live = task < TK.nk * n;
+    const int tc = live ? task : 0;
+    const int kl = tc / n;
+    const int j = tc - kl * n;
+    const int r = TK.roles[g * TK.stride + j];
+    double t;
+    const LaneIn<D> in = lane_input<D>(S, Ln, kl, r, t);
+    constexpr int NOUT = D::NST > D::NF ? D::NST : D::NF;
+    double out[NOUT];
+    D::group(g, M, t, in, out);
+    if (!live) return;
+    if (g == 0) {
+        double* dst = H + ((long)kl * TK.nmass + j) * D::NST;
+#pragma unroll
+        for (int f = 0; f < D::NST; ++f) dst[f] = out[f];
+    } else {
+        double* dst = T + ((long)kl * TK.nslot + TK.off[g] + j) * D::NF;
+#pragma unroll
+        for (int f = 0; f < D::NF; ++f) dst[f] = out[f];
+    }
+}
+
+template <class D>
+struct TaskLoad {
+    const double* __restrict__ T;
+    const double* __restrict__ H;
+    const int* __restrict__ jd;
+    const int* __restrict__ off;
+    int stride, nslot, nmass, kl, r;
+    __device__ __forceinline__ double operator()(int g, int f) const {
+        const int j = jd[g * stride + r];
+        return T[((long)kl * nslot + off[g] + j) * D::NF + f];
+    }
+    __device__ __forceinline__ double h(int f) const {
+        const int j = jd[r];
+        return H[((long)kl * nmass + j) * D::NST + f];
+    }
+};
+
+template <class D>
+__global__ void __launch_bounds__(64) k_combine(DevModel M, Src S, Lanes Ln, Tasks TK,
+        const double* __restrict__ T, const double* __restrict__ H, double* __restrict__ times,
+        double* __restrict__ Y, long ystride_pt) {
+    const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= (long)TK.nk * Ln.stride) return;
+    const int kl = (int)(gid / Ln.stride);
+    const int r = (int)(gid - (long)kl * Ln.stride);
+    double t;
+    const LaneIn<D> in = lane_input<D>(S, Ln, kl, r, t);
+    if (r == Ln.base && times) times[kl] = t;
+    const TaskLoad<D> TL{T, H, TK.jd, TK.off, TK.stride, TK.nslot, TK.nmass, kl, r};
+    double out[D::NO];
+    D::combine(M, t, in, TL, out);
+    // Y[(kl*NO + o)*stride + r]  (ystride_pt = NO*stride; explicit points:
+    // stride 1 -> out[p*NO + o])
+    double* Yk = Y + (long)kl * ystride_pt + r;
+#pragma unroll
+    for (int o = 0; o < D::NO; ++o) Yk[(long)o * Ln.stride] = out[o];
 }
 
 struct Interval {
@@ -691,6 +717,103 @@ struct Arena {
     }
 };
 
+// Static description of a task-decomposed generated model (codegen.py).
+struct TaskInfo {
+    int ng, nst, nf, rw;
+    const int* group_nf;
+    const unsigned long long* reads;   // [ng][rw] bit i = group reads point input i
+    const unsigned char* time;         // [ng] group reads the time
+    const double* gflops;              // [ng] FP64 ops per group evaluation
+    double combine_flops;
+};
+
+// Task tables for one lane configuration (host copy + device view).
+struct TaskSet {
+    Tasks dev{};
+    int nblocks = 0;
+    double flops = 0.0;     // FP64 ops per launch (groups + combine)
+    double ntasks = 0.0;    // group evaluations per launch
+    std::vector<int> dlen, off, roles, jd, blk;
+    size_t t_doubles = 0, h_doubles = 0;
+};
+
+// Which groups a lane role re-evaluates: the base lane all of them, a
+// perturbed lane those that read its perturbed input (or the time, for the
+// t0/tf directions).  MOCOHIP_TASKS=all disables the pruning (every group
+// for every lane; the reference for the bit-identity test).
+static void build_taskset(const TaskInfo& ti, const Lanes& ln, int nk, TaskSet& ts) {
+    const char* env = std::getenv("MOCOHIP_TASKS");
+    const bool all = env && std::strcmp(env, "all") == 0;
+    const int ng = ti.ng, S = ln.stride;
+    ts.dlen.assign(ng, 0);
+    ts.off.assign(ng, 0);
+    ts.roles.assign((size_t)ng * S, 0);
+    ts.jd.assign((size_t)ng * S, 0);
+    int nslot = 0;
+    for (int g = 0; g < ng; ++g) {
+        std::vector<int> D{ln.base};
+        for (int r = 0; r < S; ++r) {
+            if (r == ln.base) continue;
+            const int dir = (ln.fd == MH_FD_CENTRAL && r >= ln.ND) ? r - ln.ND : r;
+            bool hit;
+            if (dir < 2) hit = ti.time[g] != 0;
+            else {
+                const int i = dir - 2;
+                hit = (ti.reads[(size_t)g * ti.rw + i / 64] >> (i % 64)) & 1ULL;
+            }
+            if (hit || all) D.push_back(r);
+        }
+        ts.dlen[g] = (int)D.size();
+        for (size_t j = 0; j < D.size(); ++j) {
+            ts.roles[(size_t)g * S + j] = D[j];
+            ts.jd[(size_t)g * S + D[j]] = (int)j;
+        }
+        if (g > 0) { ts.off[g] = nslot; nslot += (int)D.size(); }
+    }
+    // expensive groups first so they start before the cheap ones fill in
+    std::vector<int> order(ng);
+    for (int g = 0; g < ng; ++g) order[g] = g;
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+        return ti.gflops[a] > ti.gflops[b];
+    });
+    ts.blk.clear();
+    ts.flops = 0.0;
+    ts.ntasks = 0.0;
+    for (int g : order) {
+        const long n = (long)nk * ts.dlen[g];
+        for (long f = 0; f < n; f += 64) { ts.blk.push_back(g); ts.blk.push_back((int)f); }
+        ts.flops += (double)n * ti.gflops[g];
+        ts.ntasks += (double)n;
+    }
+    ts.flops += (double)nk * S * ti.combine_flops;
+    ts.nblocks = (int)(ts.blk.size() / 2);
+    ts.dev.ng = ng;
+    ts.dev.stride = S;
+    ts.dev.nslot = nslot;
+    ts.dev.nmass = ts.dlen[0];
+    ts.dev.nk = nk;
+    ts.t_doubles = (size_t)nk * std::max(nslot, 1) * ti.nf;
+    ts.h_doubles = (size_t)nk * ts.dlen[0] * ti.nst;
+}
+
+struct TaskOffsets { size_t dlen, off, roles, jd, blk; };
+static TaskOffsets put_taskset(Arena& A, const TaskSet& ts) {
+    TaskOffsets o;
+    o.dlen = A.put(ts.dlen.data(), ts.dlen.size());
+    o.off = A.put(ts.off.data(), ts.off.size());
+    o.roles = A.put(ts.roles.data(), ts.roles.size());
+    o.jd = A.put(ts.jd.data(), ts.jd.size());
+    o.blk = A.put(ts.blk.data(), ts.blk.size());
+    return o;
+}
+static void bind_taskset(char* base, const TaskOffsets& o, TaskSet& ts) {
+    ts.dev.dlen = (const int*)(base + o.dlen);
+    ts.dev.off = (const int*)(base + o.off);
+    ts.dev.roles = (const int*)(base + o.roles);
+    ts.dev.jd = (const int*)(base + o.jd);
+    ts.dev.blk = (const int*)(base + o.blk);
+}
+
 }  // namespace
 
 struct Backend;
@@ -726,7 +849,35 @@ struct mh_ctx {
            *d_tpart = nullptr, *d_f = nullptr;
     TplEntry* d_tpl = nullptr;
     float timings[3] = {0, 0, 0};
+    // task-decomposed back ends
+    TaskSet ts_jac, ts_g, ts_probe;
+    double *d_T = nullptr, *d_H = nullptr;
+    char* probe_mem = nullptr;     // tables + T/H of the last mh_eval_dae size
+    double *d_pT = nullptr, *d_pH = nullptr;
+    int probe_np = -1;
 };
+
+// Task tables and T/H buffers for an mh_eval_dae call of np points (kept
+// until the next call with a different np).
+static int probe_tasks(mh_ctx* c, const TaskInfo& ti, const Lanes& ln, int np) {
+    if (np == c->probe_np) return MH_OK;
+    if (c->probe_mem) { (void)hipFree(c->probe_mem); c->probe_mem = nullptr; }
+    c->probe_np = -1;
+    build_taskset(ti, ln, np, c->ts_probe);
+    Arena A;
+    const TaskOffsets to = put_taskset(A, c->ts_probe);
+    const size_t oT = A.reserve(sizeof(double) * c->ts_probe.t_doubles);
+    const size_t oH = A.reserve(sizeof(double) * c->ts_probe.h_doubles);
+    HIPCHK(hipMalloc(&c->probe_mem, A.used));
+    for (auto& up : A.uploads)
+        HIPCHK(hipMemcpy(c->probe_mem + up.first, up.second.data(), up.second.size(),
+                hipMemcpyHostToDevice));
+    bind_taskset(c->probe_mem, to, c->ts_probe);
+    c->d_pT = (double*)(c->probe_mem + oT);
+    c->d_pH = (double*)(c->probe_mem + oH);
+    c->probe_np = np;
+    return MH_OK;
+}
 
 static int64_t col_state(const mh_ctx* c, int64_t k, int s) { return 2 + k * c->NS + s; }
 static int64_t col_control(const mh_ctx* c, int64_t k, int j) {
@@ -991,6 +1142,7 @@ extern "C" int mh_model_hash(const mh_model* M, uint64_t* hash) {
 }
 
 static const Backend* select_backend(mh_ctx* c, const mh_problem* p);
+static const TaskInfo* backend_tasks(const Backend* b);
 
 extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out) {
     if (!p || !o || !out) return set_err(MH_ERR_INVALID, "null argument");
@@ -1070,6 +1222,17 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     const size_t o_grad = A.reserve(sizeof(double) * c->n);
     const size_t o_tpart = A.reserve(sizeof(double) * 2 * (size_t)c->G);
     const size_t o_f = A.reserve(sizeof(double) * 4);
+    TaskOffsets to_jac{}, to_g{};
+    size_t o_T = 0, o_H = 0;
+    const TaskInfo* ti = backend_tasks(c->be);
+    if (ti) {
+        build_taskset(*ti, c->lanes_jac, c->nk, c->ts_jac);
+        build_taskset(*ti, c->lanes_g, c->nk, c->ts_g);
+        to_jac = put_taskset(A, c->ts_jac);
+        to_g = put_taskset(A, c->ts_g);
+        o_T = A.reserve(sizeof(double) * std::max(c->ts_jac.t_doubles, c->ts_g.t_doubles));
+        o_H = A.reserve(sizeof(double) * std::max(c->ts_jac.h_doubles, c->ts_g.h_doubles));
+    }
     A.size = A.used;
     HIPCHK(hipMalloc(&c->dmem, A.size));
     for (auto& up : A.uploads)
@@ -1102,6 +1265,12 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     c->d_Yg = (double*)(b + o_Yg); c->d_g = (double*)(b + o_g); c->d_vals = (double*)(b + o_vals);
     c->d_C = (double*)(b + o_C); c->d_grad = (double*)(b + o_grad); c->d_tpart = (double*)(b + o_tpart);
     c->d_f = (double*)(b + o_f);
+    if (ti) {
+        bind_taskset(b, to_jac, c->ts_jac);
+        bind_taskset(b, to_g, c->ts_g);
+        c->d_T = (double*)(b + o_T);
+        c->d_H = (double*)(b + o_H);
+    }
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
     *out = c.release();
@@ -1116,6 +1285,7 @@ extern "C" void mh_destroy(mh_ctx* c) {
         if (e) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->dmem) (void)hipFree(c->dmem);
+    if (c->probe_mem) (void)hipFree(c->probe_mem);
     delete c;
 }
 
@@ -1219,24 +1389,38 @@ extern "C" int mh_get_jac_structure(const mh_ctx* c, int32_t* iRow, int32_t* jCo
 // ------------------------------------------------------------------------
 struct Backend {
     const char* name;
-    void (*eval)(mh_ctx*, const double* x, const Lanes& ln, double* Y);
+    // one evaluation stage: raw DAE outputs of every lane of c->lanes_g
+    // (mode 0) or c->lanes_jac (mode 1) into Y, base-lane times into d_times
+    void (*eval)(mh_ctx*, const double* x, int mode, double* Y);
     void (*integrand)(mh_ctx*, const double* x);
     void (*grad)(mh_ctx*, const double* x);
     void (*probe)(mh_ctx*, int np, const double* in, double* out);
     double flops_per_eval;   // generated back ends: emitted FP64 ops per DAE
+    const TaskInfo* tasks;   // task-decomposed back ends (else one lane per DAE)
 };
 
 template <class D>
-static void be_eval(mh_ctx* c, const double* x, const Lanes& ln, double* Y) {
+static void be_eval_lane(mh_ctx* c, const double* x, int mode, double* Y) {
     Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, c->k0, c->nk};
+    const Lanes& ln = mode ? c->lanes_jac : c->lanes_g;
     const long lanes = (long)c->nk * ln.stride;
-    const dim3 grid((unsigned)((lanes + 63) / 64));
-    if constexpr (D::SPLIT)
-        hipLaunchKernelGGL(k_eval_split<D>, grid, dim3((D::NGROUPS + 1) * 64), 0, c->stream, c->M, L,
-                ln, x, c->d_grid, c->d_times, Y);
-    else
-        hipLaunchKernelGGL(k_eval<D>, grid, dim3(64), 0, c->stream, c->M, L, ln, x, c->d_grid,
-                c->d_times, Y);
+    hipLaunchKernelGGL(k_eval<D>, dim3((unsigned)((lanes + 63) / 64)), dim3(64), 0, c->stream, c->M, L,
+            ln, x, c->d_grid, c->d_times, Y);
+}
+template <class D>
+static void launch_tasks(mh_ctx* c, const Src& S, const Lanes& ln, const TaskSet& ts, double* T,
+        double* H, double* times, double* Y) {
+    hipLaunchKernelGGL(k_groups<D>, dim3((unsigned)ts.nblocks), dim3(64), 0, c->stream, c->M, S, ln,
+            ts.dev, T, H);
+    const long lanes = (long)ts.dev.nk * ln.stride;
+    hipLaunchKernelGGL(k_combine<D>, dim3((unsigned)((lanes + 63) / 64)), dim3(64), 0, c->stream, c->M,
+            S, ln, ts.dev, T, H, times, Y, (long)D::NO * ln.stride);
+}
+template <class D>
+static void be_eval_tasks(mh_ctx* c, const double* x, int mode, double* Y) {
+    const Src S{x, c->d_grid, nullptr, c->G, c->k0};
+    launch_tasks<D>(c, S, mode ? c->lanes_jac : c->lanes_g, mode ? c->ts_jac : c->ts_g, c->d_T, c->d_H,
+            c->d_times, Y);
 }
 template <class D>
 static void be_integrand(mh_ctx* c, const double* x) {
@@ -1252,41 +1436,60 @@ static void be_grad(mh_ctx* c, const double* x) {
             c->GS, c->fd, c->h, x, c->d_grid, c->d_quad, c->d_grad, c->d_tpart);
 }
 template <class D>
-static void be_probe(mh_ctx* c, int np, const double* in, double* out) {
-    if constexpr (D::SPLIT) {
-        hipLaunchKernelGGL(k_probe_split<D>, dim3((np + 63) / 64), dim3((D::NGROUPS + 1) * 64), 0,
-                c->stream, c->M, np, in, out);
-    } else {
-        Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, 0, 0};
-        hipLaunchKernelGGL(k_dae_probe<D>, dim3((np + 63) / 64), dim3(64), 0, c->stream, c->M, L, np,
-                in, out);
-    }
+static void be_probe_lane(mh_ctx* c, int np, const double* in, double* out) {
+    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, 0, 0};
+    hipLaunchKernelGGL(k_dae_probe<D>, dim3((np + 63) / 64), dim3(64), 0, c->stream, c->M, L, np, in,
+            out);
+}
+// mh_eval_dae through the task kernels: explicit points, base lanes only.
+template <class D>
+static void be_probe_tasks(mh_ctx* c, int np, const double* in, double* out) {
+    const Lanes ln{c->fd, c->NI + 2, 1, 0, c->h};
+    if (probe_tasks(c, *c->be->tasks, ln, np) != MH_OK) return;
+    const Src S{nullptr, nullptr, in, 0, 0};
+    launch_tasks<D>(c, S, ln, c->ts_probe, c->d_pT, c->d_pH, nullptr, out);
 }
 template <class D>
-static constexpr Backend make_backend(const char* name, double flops) {
-    return Backend{name, &be_eval<D>, &be_integrand<D>, &be_grad<D>, &be_probe<D>, flops};
+static constexpr Backend make_backend_lane(const char* name, double flops) {
+    return Backend{name, &be_eval_lane<D>, &be_integrand<D>, &be_grad<D>, &be_probe_lane<D>, flops,
+                   nullptr};
+}
+template <class D>
+struct TaskInfoOf {
+    static constexpr TaskInfo value{D::NG, D::NST, D::NF, D::RW, D::GROUP_NF, &D::GROUP_READS[0][0],
+                                    D::GROUP_TIME, D::GROUP_FLOPS, D::COMBINE_FLOPS};
+};
+template <class D>
+static constexpr Backend make_backend_tasks(const char* name, double flops) {
+    return Backend{name, &be_eval_tasks<D>, &be_integrand<D>, &be_grad<D>, &be_probe_tasks<D>, flops,
+                   &TaskInfoOf<D>::value};
 }
 
+static const TaskInfo* backend_tasks(const Backend* b) { return b->tasks; }
+
 static const Backend kGeneric[3] = {
-    make_backend<GenericDae<SzSmall>>("generic-small", 0.0),
-    make_backend<GenericDae<SzMedium>>("generic-medium", 0.0),
-    make_backend<GenericDae<SzLarge>>("generic-large", 0.0),
+    make_backend_lane<GenericDae<SzSmall>>("generic-small", 0.0),
+    make_backend_lane<GenericDae<SzMedium>>("generic-medium", 0.0),
+    make_backend_lane<GenericDae<SzLarge>>("generic-large", 0.0),
 };
 
-// Model-specialized back ends produced by tools/gen_models.py.
+// Model-specialized back ends produced by tools/gen_models.py: the task
+// kernels (default) and the one-lane-per-DAE kernel (MOCOHIP_BACKEND=lane).
 #include "generated/models_structs.inc"
-struct GenEntry { uint64_t hash; Backend be; };
-#define MH_GEN_MODEL(T, H, NAME) GenEntry{H, make_backend<T>(NAME, T::FLOPS_PER_EVAL)},
+struct GenEntry { uint64_t hash; Backend tasks, lane; };
+#define MH_GEN_MODEL(T, H, NAME)                                                       \
+    GenEntry{H, make_backend_tasks<T>("generated:" NAME, T::FLOPS_PER_EVAL),            \
+             make_backend_lane<T>("generated-lane:" NAME, T::FLOPS_PER_EVAL)},
 static const GenEntry kGeneratedModels[] = {
 #include "generated/models_table.inc"
-    GenEntry{0, Backend{nullptr, nullptr, nullptr, nullptr, nullptr, 0.0}}};
+};
 #undef MH_GEN_MODEL
 
 static int run_g(mh_ctx* c, const double* x_dev, double* g_dev) {
     Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, c->k0, c->nk};
     Interval I{c->scheme, c->interp, c->ib, c->rpi, c->nnz_int};
     HIPCHK(hipEventRecord(c->ev[0], c->stream));
-    c->be->eval(c, x_dev, c->lanes_g, c->d_Yg);
+    c->be->eval(c, x_dev, 0, c->d_Yg);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[1], c->stream));
     hipLaunchKernelGGL(k_defects, dim3(c->ie - c->ib), dim3(256), 0, c->stream, L, I, c->lanes_g,
@@ -1300,7 +1503,7 @@ static int run_jac(mh_ctx* c, const double* x_dev, double* v_dev) {
     Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, c->k0, c->nk};
     Interval I{c->scheme, c->interp, c->ib, c->rpi, c->nnz_int};
     HIPCHK(hipEventRecord(c->ev[0], c->stream));
-    c->be->eval(c, x_dev, c->lanes_jac, c->d_Y);
+    c->be->eval(c, x_dev, 1, c->d_Y);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[1], c->stream));
     hipLaunchKernelGGL(k_assemble, dim3((c->nnz_int + ASM_CHUNK - 1) / ASM_CHUNK, c->ie - c->ib),
@@ -1318,7 +1521,7 @@ static int run_g_jac(mh_ctx* c, const double* x_dev, double* g_dev, double* v_de
     Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, c->k0, c->nk};
     Interval I{c->scheme, c->interp, c->ib, c->rpi, c->nnz_int};
     HIPCHK(hipEventRecord(c->ev[0], c->stream));
-    c->be->eval(c, x_dev, c->lanes_jac, c->d_Y);
+    c->be->eval(c, x_dev, 1, c->d_Y);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[1], c->stream));
     hipLaunchKernelGGL(k_defects, dim3(c->ie - c->ib), dim3(256), 0, c->stream, L, I, c->lanes_jac,
@@ -1462,6 +1665,7 @@ extern "C" int mh_eval_dae(mh_ctx* c, int32_t np, const double* inputs, double* 
     return MH_OK;
 }
 
+
 extern "C" int mh_last_timings(const mh_ctx* c, double* ms3) {
     if (!c || !ms3) return set_err(MH_ERR_INVALID, "null argument");
     for (int i = 0; i < 3; ++i) ms3[i] = c->timings[i];
@@ -1480,13 +1684,30 @@ extern "C" int mh_get_backend(const mh_ctx* c, char* name, int32_t name_len, dou
     return MH_OK;
 }
 
+extern "C" int mh_get_work(const mh_ctx* c, double* work4) {
+    if (!c || !work4) return set_err(MH_ERR_INVALID, "null argument");
+    const double lanes_jac = (double)c->nk * c->lanes_jac.stride, lanes_g = (double)c->nk;
+    if (c->be->tasks) {
+        work4[0] = c->ts_jac.flops;
+        work4[1] = c->ts_g.flops;
+        work4[2] = c->ts_jac.ntasks;
+    } else {
+        work4[0] = lanes_jac * c->be->flops_per_eval;
+        work4[1] = lanes_g * c->be->flops_per_eval;
+        work4[2] = 0.0;
+    }
+    work4[3] = lanes_jac;
+    return MH_OK;
+}
+
 static const Backend* select_backend(mh_ctx* c, const mh_problem* p) {
     c->model_hash = model_hash(&p->model);
     const char* force = std::getenv("MOCOHIP_BACKEND");
     const bool generic = force && std::strcmp(force, "generic") == 0;
+    const bool lane = force && std::strcmp(force, "lane") == 0;
     if (!generic) {
         for (const GenEntry& e : kGeneratedModels)
-            if (e.be.name && e.hash == c->model_hash) return &e.be;
+            if (e.hash == c->model_hash) return lane ? &e.lane : &e.tasks;
     }
     return &kGeneric[c->size_class];
 }

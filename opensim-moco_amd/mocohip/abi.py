@@ -162,6 +162,7 @@ MOCOHIP_SYMBOLS = {
     "mh_last_timings": (i32, [C.c_void_p, P(f64)]),
     "mh_get_backend": (i32, [C.c_void_p, C.c_char_p, i32, P(f64), P(C.c_uint64)]),
     "mh_model_hash": (i32, [P(mh_model), P(C.c_uint64)]),
+    "mh_get_work": (i32, [C.c_void_p, P(f64)]),
 }
 
 ORACLE_SYMBOLS = {

@@ -18,6 +18,7 @@ kernel run the generic device interpreter.
 from __future__ import annotations
 
 import math
+import re
 import struct
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -270,6 +271,7 @@ class _Emitter:
         self.u = self.inp[Lo.NQ:2 * Lo.NQ]
         self.ctrl = self.inp[Lo.NS:Lo.NS + Lo.NC]
         self.fcache: Dict[int, Tuple[S, S, S]] = {}
+        self.touched = set()
 
     # functions of one coordinate
     def fn_eval(self, fi: int):
@@ -306,9 +308,10 @@ class _Emitter:
                 b = self.M.bodies[b].parent
         return sorted(need)
 
-    def kinematics(self, bodies: Sequence[int], accel: bool):
-        """Poses, spatial velocities, (bias accelerations) and motion
-        subspaces for the given bodies (must be ancestor-closed)."""
+    def kinematics(self, bodies: Sequence[int], accel: bool, vel: bool = True):
+        """Poses, spatial velocities (if vel), bias accelerations (if accel)
+        and motion subspaces for the given bodies (must be ancestor-closed)."""
+        accel = accel and vel
         g, M, q, u = self.g, self.M, self.q, self.u
         I3 = _vec([1, 0, 0, 0, 1, 0, 0, 0, 1])
         Z3 = _vec([0, 0, 0])
@@ -335,6 +338,9 @@ class _Emitter:
             def motion(s, Vframe, fv, j):
                 nonlocal Vb, Ab
                 coord_body[j] = b
+                if not vel:
+                    Sj[j] = g.svadd(Sj.get(j, (Z3, Z3)), g.svscale(s, fv[1]))
+                    return
                 thd = g.mul(fv[1], u[j])
                 Vb = g.svadd(Vb, g.svscale(s, thd))
                 if accel:
@@ -398,10 +404,11 @@ class _Emitter:
     def acc(self, name: str, val: S, sign: float = 1.0):
         if val.is_c(0.0):
             return
+        self.touched.add(name)
         self.g.raw(f"{name} {'+=' if sign > 0 else '-='} {val};")
         self.g.flops["add"] += 1
 
-    def muscle(self, im, R, P, V, Facc, tau, zdot_sink):
+    def muscle(self, im, R, P, V, Facc, tau, zdot_sink, with_adot: bool = True):
         """Path geometry, DGF and tension point forces of muscle im.  Point
         forces are subtracted into the body accumulators Facc (RNEA sign
         convention), MovingPathPoint terms added into tau; zdot values are
@@ -460,8 +467,9 @@ class _Emitter:
         sa, sf = Lo.act_state[im], Lo.ftn_state[im]
         a_ = self.inp[sa] if sa >= 0 else exc
         ftn = self.inp[sf] if sf >= 0 else None
-        T, adot, ftdot = _dgf(g, mu, L, Sp, a_, exc, sa >= 0, ftn, sf >= 0, Lo.tau_act, Lo.tau_deact)
-        if sa >= 0:
+        T, adot, ftdot = _dgf(g, mu, L, Sp, a_, exc, sa >= 0 and with_adot, ftn, sf >= 0,
+                              Lo.tau_act, Lo.tau_deact)
+        if sa >= 0 and with_adot:
             zdot_sink(sa, adot)
         if sf >= 0:
             zdot_sink(sf, ftdot)
@@ -483,23 +491,34 @@ class _Emitter:
                     self.acc(tau[coord], g.mul(g.dot([Rb[dd], Rb[3 + dd], Rb[6 + dd]], f), d1))
 
     def body_force_vars(self, bodies, init):
-        return {b: [self.g.var(x) for x in (init(b) if init else [_c(0.0)] * 6)] for b in bodies}
+        out = {}
+        for b in bodies:
+            vals = init(b) if init else [_c(0.0)] * 6
+            out[b] = [self.g.var(x) for x in vals]
+            for name, x in zip(out[b], vals):
+                if not x.is_c(0.0):
+                    self.touched.add(name)
+        return out
 
     def backward(self, bodies, Facc, Sj, coord_body, tau):
         """F_parent += F_child over `bodies` (descending), then
-        tau_j -= S_j . F_body(j)."""
+        tau_j -= S_j . F_body(j).  Accumulators never touched are structural
+        zeros and are skipped."""
         g, M = self.g, self.M
         bset = set(bodies)
         for b in sorted(bodies, reverse=True):
             p = M.bodies[b].parent
             if p >= 0 and p in bset:
                 for c in range(6):
-                    g.raw(f"{Facc[p][c]} += {Facc[b][c]};")
-                    g.flops["add"] += 1
+                    if Facc[b][c] in self.touched:
+                        g.raw(f"{Facc[p][c]} += {Facc[b][c]};")
+                        g.flops["add"] += 1
+                        self.touched.add(Facc[p][c])
         for j, b in sorted(coord_body.items()):
-            fa = Facc[b]
-            fsv = ([S(n=fa[0]), S(n=fa[1]), S(n=fa[2])], [S(n=fa[3]), S(n=fa[4]), S(n=fa[5])])
-            self.acc(tau[j], g.svdot(Sj[j], fsv), -1.0)
+            if b not in Facc:
+                continue
+            fa = [S(n=n) if n in self.touched else _c(0.0) for n in Facc[b]]
+            self.acc(tau[j], g.svdot(Sj[j], (fa[:3], fa[3:])), -1.0)
 
     def mass_matrix_factor(self, Ibody, Sj, coord_body):
         """CRBA composite inertias + Featherstone L^T L on the coordinate
@@ -572,10 +591,12 @@ class _Emitter:
             xs[i] = g.div(xi, H[(i, i)])
         return xs
 
-    def external_forces(self, P, Facc):
+    def external_forces(self, P, Facc, only=None):
         g, M = self.g, self.M
         Z3 = _vec([0, 0, 0])
-        for e in M.ext:
+        for ie, e in enumerate(M.ext):
+            if only is not None and ie not in only:
+                continue
             b = e.body
             g.k += 1
             seg = f"seg{g.k}"
@@ -623,21 +644,18 @@ def _multibody_front(E: _Emitter, with_muscles: bool):
     return tau, lam, H, zd
 
 
-def generate(cm, struct_name: str, waves: int = 8) -> Tuple[str, Dict]:
+def generate(cm, struct_name: str) -> Tuple[str, Dict]:
     """Return (C++ source of `struct <struct_name>`, info dict).
 
-    The struct has eval() (whole DAE in one lane) and, for muscle models, the
-    pieces of the workgroup-split evaluation used by k_eval_split (``waves``
-    waves per 64 evaluations):
-      mass_factor()  wave 0: position kinematics, CRBA mass matrix and its
-                     L^T L factor (kept in registers across the barrier);
-      forces(w)      waves 1..: force group w -> generalized forces tq and
-                     muscle state derivatives.  Group 0 is the RNEA bias
-                     (inertial + gravity), coordinate actuators and external
-                     loads; every group also owns a set of muscles (path,
-                     DeGroote-Fregly dynamics, tension point forces), assigned
-                     longest-first by emitted FP64 op count;
-      mass_solve()   wave 0 after the barrier: H udot = sum of the groups' tq."""
+    The struct has
+      eval()     the whole DAE in one lane (k_eval; also the FLOP reference);
+      group(g)   one independent piece of the DAE (see _emit_groups) for the
+                 task kernel k_groups, which evaluates only the groups a
+                 finite-difference direction perturbs;
+      combine()  the per-lane reduction of the group results into udot, zdot
+                 (k_combine),
+    plus the group metadata (fields, inputs read, time dependence, FP64 op
+    counts) the host uses to build the task tables."""
     M = ModelView(cm)
     Lo = _Layout(M)
     NQ, NZ = Lo.NQ, Lo.NZ
@@ -659,118 +677,218 @@ def generate(cm, struct_name: str, waves: int = 8) -> Tuple[str, Dict]:
     parts.append(("eval", "const mh::DevModel& M, const double t, const double* __restrict__ in, "
                           "double* __restrict__ out", E.g.lines))
 
-    split = len(M.muscles) > 0 and waves > 2
-    ngroups = 0
-    nst = 0
-    if split:
-        # ---- wave 0: mass matrix (CRBA) and its L^T L factor --------------------
-        E = _Emitter(M, Lo)
-        allb = list(range(M.nb))
-        R, P, _, _, Sj, coord_body = E.kinematics(allb, accel=False)
-        Ibody = {b: E.inertia(b, R, P) for b in allb}
-        lam, H = E.mass_matrix_factor(Ibody, Sj, [coord_body[j] for j in range(NQ)])
-        keys = sorted(H.keys())
-        for i, k in enumerate(keys):
-            E.g.raw(f"st[{i}] = {H[k]};")
-        nst = len(keys)
-        info["mass_flops"] = sum(E.g.flops.values())
-        parts.append(("mass_factor", "const mh::DevModel& M, const double t, "
-                                     "const double* __restrict__ in, double* __restrict__ st", E.g.lines))
-        # ---- wave 0 after the barrier: solve with the summed forces -------------
-        E2 = _Emitter(M, Lo)
-        Hs = {k: S(n=f"st[{i}]") for i, k in enumerate(keys)}
-        xs = E2.solve(lam, Hs, [S(n=f"tm[{j}]") for j in range(NQ)])
-        for i in range(NQ):
-            E2.g.raw(f"out[{i}] = {xs[i]};")
-        info["solve_flops"] = sum(E2.g.flops.values())
-        parts.append(("mass_solve", "const double* __restrict__ st, const double* __restrict__ tm, "
-                                    "double* __restrict__ out", E2.g.lines))
-
-        # ---- waves 1..: force groups -------------------------------------------
-        def emit_group(bias, muscles):
-            Eg = _Emitter(M, Lo)
-            tv = [Eg.g.var(_c(0.0)) for _ in range(NQ)]
-            zsink = lambda s, v: Eg.g.raw(f"zo[{s - 2 * NQ} * zs] = {v};")
-            if bias:
-                # RNEA bias (inertial + gravity), coordinate actuators and
-                # external loads over the whole tree
-                R, P, V, A, Sj, cb = Eg.kinematics(allb, accel=True)
-                Ib = {b: Eg.inertia(b, R, P) for b in allb}
-
-                def init(b):
-                    Ia = Eg.g.rbi_mul(Ib[b], A[b])
-                    hV = Eg.g.rbi_mul(Ib[b], V[b])
-                    w, v = Eg.g.svadd(Ia, Eg.g.crf(V[b], hV))
-                    return list(w) + list(v)
-                cl = allb
-                Facc = Eg.body_force_vars(allb, init)
-                Eg.actuators(tv)
-                Eg.external_forces(P, Facc)
-            else:
-                bodies = sorted({M.points[i].body for m in muscles
-                                 for i in range(M.muscles[m].point_begin,
-                                                M.muscles[m].point_begin + M.muscles[m].point_count)
-                                 if M.points[i].body >= 0})
-                cl = Eg.closure(bodies)
-                R, P, V, _, Sj, cb = Eg.kinematics(cl, accel=False)
-                Facc = Eg.body_force_vars(cl, None)
-            for m in muscles:
-                Eg.muscle(m, R, P, V, Facc, tv, zsink)
-            # generalized forces: tau_j -= S_j . F_subtree (Facc holds the
-            # RNEA sign: inertial/bias minus applied)
-            Eg.backward(cl, Facc, Sj, cb, tv)
-            for j in range(NQ):
-                Eg.g.raw(f"tq[{j}] = {tv[j]};")
-            return Eg.g.lines, sum(Eg.g.flops.values())
-
-        nforce = waves - 1
-        _, bias_cost = emit_group(True, [])
-        cost = {m: emit_group(False, [m])[1] for m in range(len(M.muscles))}
-        bins = [[] for _ in range(nforce)]
-        load = [0.0] * nforce
-        load[0] = bias_cost
-        for m in sorted(cost, key=lambda m: -cost[m]):
-            w = min(range(nforce), key=lambda k: load[k])
-            bins[w].append(m)
-            load[w] += cost[m]
-        gl = []
-        for gi, grp in enumerate(bins):
-            if gi > 0 and not grp:
-                continue
-            lines, gfl = emit_group(gi == 0, sorted(grp))
-            gl.append((gi, lines, sorted(grp), gfl))
-        ngroups = len(gl)
-        info["group_flops"] = [c for *_, c in gl]
-        info["groups"] = [grp for _, _, grp, _ in gl]
-        body = ["        switch (w) {"]
-        for gi, (_, lines, grp, _) in enumerate(gl):
-            body.append(f"        case {gi}: {{  // {'bias + ' if gi == 0 else ''}muscles {grp}")
-            body.extend("    " + l for l in lines)
-            body.append("        } break;")
-        body += ["        default: break;", "        }"]
-        parts.append(("forces", "const int w, const mh::DevModel& M, const double t, "
-                                "const double* __restrict__ in, double* __restrict__ tq, "
-                                "double* __restrict__ zo, const long zs", body))
+    # ---- task decomposition ------------------------------------------------
+    groups = _emit_groups(M, Lo)
+    comb, comb_flops = _emit_combine(M, Lo, groups)
+    info["groups"] = [(gr.name, gr.nf, sorted(gr.reads), gr.time, gr.flops) for gr in groups]
+    info["combine_flops"] = comb_flops
+    NG = len(groups)
+    NF = max([gr.nf for gr in groups[1:]] + [1])
+    NST = max(groups[0].nf, 1)
+    RW = (Lo.NI + 63) // 64
+    reads = []
+    for gr in groups:
+        words = [0] * RW
+        for i in gr.reads:
+            words[i // 64] |= 1 << (i % 64)
+        reads.append("{" + ", ".join(f"0x{w:x}ULL" for w in words) + "}")
+    body = ["        switch (g) {"]
+    for gi, gr in enumerate(groups):
+        body.append(f"        case {gi}: {{  // {gr.name}")
+        body.extend("    " + l for l in gr.lines)
+        body.append("        } break;")
+    body += ["        default: break;", "        }"]
+    parts.append(("group", "const int g, const mh::DevModel& M, const double t, "
+                           "const double* __restrict__ in, double* __restrict__ out", body))
+    parts.append(("combine", "const mh::DevModel& M, const double t, const double* __restrict__ in, "
+                             "const TL& T, double* __restrict__ out", comb))
 
     fns = []
     for name, args, lines in parts:
         tpl = ""
-        if name in ("mass_factor", "forces"):
+        if name in ("group", "combine"):
             # inputs through an accessor (loaded where used, not held in VGPRs)
-            tpl = "template <class IN> "
+            tpl = "template <class IN> " if name == "group" else "template <class IN, class TL> "
             args = args.replace("const double* __restrict__ in", "const IN& in")
         fns.append(f"    {tpl}__device__ __forceinline__ static void {name}({args}) {{\n"
                    + "\n".join(lines) + "\n    }")
+    lst = lambda v: "{" + ", ".join(str(x) for x in v) + "}"
     src = f"""struct {struct_name} {{
     static constexpr int NQ = {NQ}, NZ = {NZ}, NS = {Lo.NS}, NC = {Lo.NC}, NO = {Lo.NO}, NI = {Lo.NI};
     static constexpr int MI = NI, MO = NO;
-    static constexpr bool SPLIT = {"true" if split else "false"};
-    static constexpr int NGROUPS = {ngroups}, NST = {max(nst, 1)};
     static constexpr double FLOPS_PER_EVAL = {float(fl['total'])};
+    // task decomposition: group 0 = mass matrix factor (NST values), groups
+    // 1.. = force groups (NF values: nonzero generalized forces, z output)
+    static constexpr int NG = {NG}, NST = {NST}, NF = {NF}, RW = {RW};
+    static constexpr int GROUP_NF[NG] = {lst([gr.nf for gr in groups])};
+    static constexpr unsigned long long GROUP_READS[NG][RW] = {{{", ".join(reads)}}};
+    static constexpr unsigned char GROUP_TIME[NG] = {lst([int(gr.time) for gr in groups])};
+    static constexpr double GROUP_FLOPS[NG] = {lst([float(gr.flops) for gr in groups])};
+    static constexpr double COMBINE_FLOPS = {float(comb_flops)};
 {chr(10).join(fns)}
 }};
 """
     return src, info
+
+
+class _Group:
+    def __init__(self, name, lines, fields, reads, time, flops):
+        self.name, self.lines, self.fields = name, lines, fields
+        self.nf = len(fields)
+        self.reads, self.time, self.flops = reads, time, flops
+
+
+_IN_RE = re.compile(r"\bin\[(\d+)\]")
+
+
+def _reads_of(lines):
+    reads = set()
+    time = False
+    for l in lines:
+        reads.update(int(m) for m in _IN_RE.findall(l))
+        if "mh::table_" in l:
+            time = True
+    return reads, time
+
+
+def _emit_groups(M: ModelView, Lo: _Layout) -> List[_Group]:
+    """Independent pieces of one DAE evaluation.  Each reads a subset of the
+    point inputs (found from the emitted code) so a finite-difference
+    direction only re-evaluates the groups that read the perturbed input:
+      mass      position kinematics, CRBA mass matrix, L^T L factor (q only)
+      bias      RNEA inertial + gravity generalized forces (q, u)
+      ext_e     external load e (q along the body chain, time)
+      muscle_m  path, DeGroote-Fregly force, tendon point forces -> tau, and
+                the normalized tendon force derivative if compliant
+    Coordinate actuators and activation dynamics are evaluated per lane in
+    the combine step."""
+    NQ = Lo.NQ
+    allb = list(range(M.nb))
+    out = []
+
+    # mass
+    E = _Emitter(M, Lo)
+    R, P, _, _, Sj, cb = E.kinematics(allb, accel=False, vel=False)
+    Ib = {b: E.inertia(b, R, P) for b in allb}
+    lam, H = E.mass_matrix_factor(Ib, Sj, [cb[j] for j in range(NQ)])
+    keys = sorted(H.keys())
+    for f, k in enumerate(keys):
+        E.g.raw(f"out[{f}] = {H[k]};")
+    r, t = _reads_of(E.g.lines)
+    g0 = _Group("mass", E.g.lines, [("H", k) for k in keys], r, t, sum(E.g.flops.values()))
+    g0.lam = lam
+    out.append(g0)
+
+    def finish(Eg, name, tv, zf=None):
+        fields = []
+        for j in range(NQ):
+            if tv[j] in Eg.touched:
+                Eg.g.raw(f"out[{len(fields)}] = {tv[j]};")
+                fields.append(("tau", j))
+        if zf is not None:
+            Eg.g.raw(f"out[{len(fields)}] = {zf[1]};")
+            fields.append(("z", zf[0]))
+        r, t = _reads_of(Eg.g.lines)
+        out.append(_Group(name, Eg.g.lines, fields, r, t, sum(Eg.g.flops.values())))
+
+    # bias
+    E = _Emitter(M, Lo)
+    R, P, V, A, Sj, cb = E.kinematics(allb, accel=True)
+    Ib = {b: E.inertia(b, R, P) for b in allb}
+
+    def init(b):
+        Ia = E.g.rbi_mul(Ib[b], A[b])
+        hV = E.g.rbi_mul(Ib[b], V[b])
+        w, v = E.g.svadd(Ia, E.g.crf(V[b], hV))
+        return list(w) + list(v)
+    Facc = E.body_force_vars(allb, init)
+    tv = [E.g.var(_c(0.0)) for _ in range(NQ)]
+    E.backward(allb, Facc, Sj, cb, tv)
+    finish(E, "bias", tv)
+
+    # external loads
+    for ie, e in enumerate(M.ext):
+        E = _Emitter(M, Lo)
+        cl = E.closure([e.body])
+        R, P, _, _, Sj, cb = E.kinematics(cl, accel=False, vel=False)
+        Facc = E.body_force_vars(cl, None)
+        tv = [E.g.var(_c(0.0)) for _ in range(NQ)]
+        E.external_forces(P, Facc, only=[ie])
+        E.backward(cl, Facc, Sj, cb, tv)
+        finish(E, f"ext_{ie}", tv)
+
+    # muscles
+    for im, mu in enumerate(M.muscles):
+        E = _Emitter(M, Lo)
+        bodies = sorted({M.points[i].body for i in range(mu.point_begin, mu.point_begin + mu.point_count)
+                         if M.points[i].body >= 0})
+        cl = E.closure(bodies)
+        R, P, V, _, Sj, cb = E.kinematics(cl, accel=False)
+        Facc = E.body_force_vars(cl, None)
+        tv = [E.g.var(_c(0.0)) for _ in range(NQ)]
+        zs = {}
+        E.muscle(im, R, P, V, Facc, tv, lambda si, v: zs.__setitem__(si, v), with_adot=False)
+        E.backward(cl, Facc, Sj, cb, tv)
+        zf = None
+        if Lo.ftn_state[im] >= 0:
+            zf = (Lo.ftn_state[im] - 2 * NQ, zs[Lo.ftn_state[im]])
+        finish(E, f"muscle_{im}", tv, zf)
+    return out
+
+
+def _emit_combine(M: ModelView, Lo: _Layout, groups: List[_Group]):
+    """Per-lane combine: generalized forces summed over the groups in a fixed
+    order (so re-using a group's unperturbed result is bit-identical to
+    re-evaluating it), coordinate actuators, the two triangular solves with
+    the mass-matrix factor, activation dynamics and the compliant-tendon
+    derivatives."""
+    NQ = Lo.NQ
+    E = _Emitter(M, Lo)
+    g = E.g
+    terms = [[] for _ in range(NQ)]
+    for gi, gr in enumerate(groups[1:], start=1):
+        for f, (kind, j) in enumerate(gr.fields):
+            if kind == "tau":
+                terms[j].append(S(n=f"T({gi}, {f})"))
+    for ia, a in enumerate(M.acts):
+        if a.kind == abi.MH_ACT_COORDINATE:
+            terms[a.target].append(g.mul(E.ctrl[ia], _c(a.optimal_force)))
+
+    def tree(ts):
+        if not ts:
+            return _c(0.0)
+        while len(ts) > 1:
+            ts = [g.add(ts[i], ts[i + 1]) if i + 1 < len(ts) else ts[i] for i in range(0, len(ts), 2)]
+        return ts[0]
+    bvec = [tree(t) for t in terms]
+    keys = [k for _, k in groups[0].fields]
+    Hs = {k: S(n=f"T.h({f})") for f, k in enumerate(keys)}
+    xs = E.solve(groups[0].lam, Hs, bvec)
+    for i in range(NQ):
+        g.raw(f"out[{i}] = {xs[i]};")
+    for im in range(len(M.muscles)):
+        sa = Lo.act_state[im]
+        if sa >= 0:
+            adot = _activation_dot(g, E.inp[sa], E.ctrl[Lo.mus_control[im]], Lo.tau_act, Lo.tau_deact)
+            g.raw(f"out[{NQ + sa - 2 * NQ}] = {adot};")
+    for gi, gr in enumerate(groups[1:], start=1):
+        for f, (kind, zi) in enumerate(gr.fields):
+            if kind == "z":
+                g.raw(f"out[{NQ + zi}] = T({gi}, {f});")
+    return g.lines, sum(g.flops.values())
+
+
+def _activation_dot(g: Gen, act: S, exc: S, tau_act, tau_deact) -> S:
+    """DeGrooteFregly2016Muscle::calcActivationDerivative
+    (DeGrooteFregly2016Muscle.cpp:189-209; the time constants are the static
+    ones of the first muscle evaluated, :194-195)."""
+    C = _c
+    tcf = g.add(C(0.5), g.mul(C(1.5), act))
+    tempAct = g.div(C(1.0), g.mul(C(tau_act), tcf))
+    tempDeact = g.div(tcf, C(tau_deact))
+    f = g.mul(C(0.5), g.fn("tanh", g.mul(C(0.1), g.sub(exc, act))))
+    tc = g.add(g.mul(tempAct, g.add(f, C(0.5))), g.mul(tempDeact, g.add(g.neg(f), C(0.5))))
+    return g.mul(tc, g.sub(exc, act))
 
 
 def _dgf(g: Gen, mu, LMT: S, VMT: S, act: S, exc: S, has_act: bool, ftn: Optional[S],
@@ -834,12 +952,7 @@ def _dgf(g: Gen, mu, LMT: S, VMT: S, act: S, exc: S, has_act: bool, ftn: Optiona
     T = g.mul(C(Fmax), ftn) if compliant else g.mul(total, cosP)
     adot = ftdot = C(0.0)
     if has_act:
-        tcf = g.add(C(0.5), g.mul(C(1.5), act))
-        tempAct = g.div(C(1.0), g.mul(C(tau_act), tcf))
-        tempDeact = g.div(tcf, C(tau_deact))
-        f = g.mul(C(0.5), g.fn("tanh", g.mul(C(0.1), g.sub(exc, act))))
-        tc = g.add(g.mul(tempAct, g.add(f, C(0.5))), g.mul(tempDeact, g.add(g.neg(f), C(0.5))))
-        adot = g.mul(tc, g.sub(exc, act))
+        adot = _activation_dot(g, act, exc, tau_act, tau_deact)
     if compliant:
         ftdot = g.mul(ntv, g.mul(C(c1 * kT), g.fn("exp", g.mul(C(kT), g.sub(ntl, C(c2))))))
     return T, adot, ftdot

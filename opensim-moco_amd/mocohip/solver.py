@@ -196,6 +196,13 @@ class HipNLP(_NLPBase):
         self._check(self.lib.mh_get_backend(self.ctx, buf, 128, C.byref(fl), C.byref(h)))
         return buf.value.decode(), fl.value, h.value
 
+    def work(self):
+        """FP64 ops per eval_jac_g / eval_g DAE stage, group evaluations per
+        eval_jac_g, full-DAE-equivalent lanes per eval_jac_g (mh_get_work)."""
+        w = np.zeros(4)
+        self._check(self.lib.mh_get_work(self.ctx, abi.dptr(w)))
+        return w
+
     def last_timings(self):
         t = np.zeros(3)
         self._check(self.lib.mh_last_timings(self.ctx, abi.dptr(t)))

@@ -93,28 +93,36 @@ def _row_mask(ref, x):
     return mask.reshape(-1)
 
 
-BACKENDS = ["auto", "generic"]
+BACKENDS = ["auto", "lane", "generic"]
 
 
-def _pair(name, backend="auto"):
+def _pair(name, backend="auto", tasks=None):
     """(GPU NLP, oracle NLP, study).  backend "auto" lets mh_create pick the
-    generated model-specialized kernel when one matches the model hash;
-    "generic" forces the device interpreter (MOCOHIP_BACKEND=generic)."""
+    generated model-specialized task kernels when one matches the model hash;
+    "lane" the generated one-lane-per-DAE kernel; "generic" forces the device
+    interpreter (MOCOHIP_BACKEND).  tasks="all" disables the
+    finite-difference dependency pruning (MOCOHIP_TASKS=all)."""
     import os
     st = CASES[name]()
     rep = st.problem.create_rep()
     opts = st.solver.options()
-    old = os.environ.pop("MOCOHIP_BACKEND", None)
-    if backend == "generic":
-        os.environ["MOCOHIP_BACKEND"] = "generic"
+    saved = {k: os.environ.pop(k, None) for k in ("MOCOHIP_BACKEND", "MOCOHIP_TASKS")}
+    if backend != "auto":
+        os.environ["MOCOHIP_BACKEND"] = backend
+    if tasks:
+        os.environ["MOCOHIP_TASKS"] = tasks
     try:
         gpu = HipNLP(rep, opts)
     finally:
-        os.environ.pop("MOCOHIP_BACKEND", None)
-        if old is not None:
-            os.environ["MOCOHIP_BACKEND"] = old
+        for k, v in saved.items():
+            os.environ.pop(k, None)
+            if v is not None:
+                os.environ[k] = v
     name_ = gpu.backend()[0]
-    assert (name_.startswith("generic") if backend == "generic" else True), name_
+    if backend == "generic":
+        assert name_.startswith("generic"), name_
+    elif backend == "lane":
+        assert name_.startswith("generated-lane:"), name_
     return gpu, OracleNLP(rep, opts, threads=8), st
 
 
@@ -290,3 +298,27 @@ def test_fused_g_jac_identical_to_separate_calls(name):
     g, J = gpu.eval_g_jac_g(x)
     assert np.array_equal(g, gpu.eval_g(x))
     assert np.array_equal(J, gpu.eval_jac_g(x))
+
+
+@pytest.mark.parametrize("name", ["double_pendulum_hs", "gait_rigid_forward", "gait_rigid_central",
+                                  "gait_compliant_central", "gait_torque_driven"])
+def test_pruned_tasks_bit_identical(name):
+    """Re-evaluating only the groups a direction perturbs gives exactly the
+    Jacobian of re-evaluating every group for every direction: the reused
+    unperturbed group results are bit-identical and the combine sums in a
+    fixed order.  A missed input dependency would show up here."""
+    gpu, _, _ = _pair(name)
+    full, _, _ = _pair(name, tasks="all")
+    for _, x in _iterates(gpu):
+        assert np.array_equal(gpu.eval_g(x), full.eval_g(x), equal_nan=True)
+        assert np.array_equal(gpu.eval_jac_g(x), full.eval_jac_g(x), equal_nan=True)
+    w, wf = gpu.work(), full.work()
+    assert w[3] == wf[3] and w[2] < wf[2] and w[0] < wf[0]
+
+
+def test_work_accounting():
+    gpu, _, _ = _pair("gait_rigid_forward")
+    lane, _, _ = _pair("gait_rigid_forward", "lane")
+    w, wl = gpu.work(), lane.work()
+    assert w[3] == wl[3] == gpu.G * (gpu.NS + gpu.NC + 3)
+    assert 0 < w[0] < wl[0] and w[2] > 0 and wl[2] == 0
