@@ -681,3 +681,55 @@ __device__ __forceinline__ double table_value(const DevModel& M, int ti, int s, 
     return v;
 }
 }  // namespace mh
+
+namespace mh {
+// Segment of a table whose breakpoints are near-uniform (checked by the
+// generator: the uniform guess is within one segment for every t): direct
+// index, one correction step.  Same result as table_segment.
+template <int NSEG>
+__device__ __forceinline__ int table_segment_u(const double* __restrict__ br, double t, double b0,
+        double inv) {
+    if (t <= br[0]) return 0;
+    if (t >= br[NSEG]) return NSEG - 1;
+    if (t != t) return NSEG - 1;
+    int s = (int)((t - b0) * inv);
+    s = s < 0 ? 0 : (s > NSEG - 1 ? NSEG - 1 : s);
+    const double lo = br[s], hi = br[s + 1 <= NSEG ? s + 1 : NSEG];
+    if (t < lo) s -= 1;
+    else if (t >= hi && s < NSEG - 1) s += 1;
+    return s;
+}
+
+// Piecewise-polynomial value with compile-time degree and column count.
+template <int DEG, int NCOL>
+__device__ __forceinline__ double table_value_c(const double* __restrict__ coef,
+        const double* __restrict__ br, int s, int col, double t) {
+    const double* cf = coef + ((long)s * NCOL + col) * (DEG + 1);
+    const double dt = t - br[s];
+    double v = cf[DEG];
+#pragma unroll
+    for (int k = DEG - 1; k >= 0; --k) v = v * dt + cf[k];
+    return v;
+}
+}  // namespace mh
+
+namespace mh {
+// SimmSpline evaluation with the interval k already found (by the generated
+// code, from literal knots): every load below is independent of the others.
+template <int N>
+__device__ __forceinline__ void simm_eval_k(const DevModel& M, int kb, double t, int k, double x0,
+        double xn, double& v, double& d1, double& d2) {
+    const double* __restrict__ x = M.kx + kb;
+    const double* __restrict__ y = M.ky + kb;
+    const double* __restrict__ b = M.kb + kb;
+    const double* __restrict__ c = M.kc + kb;
+    const double* __restrict__ d = M.kd + kb;
+    const double dx = t - x[k];
+    const double bk = b[k], ck = c[k], dk = d[k];
+    v = y[k] + dx * (bk + dx * (ck + dx * dk));
+    d1 = bk + dx * (2.0 * ck + 3.0 * dx * dk);
+    d2 = 2.0 * ck + 6.0 * dx * dk;
+    if (t < x0) { v = y[0] + (t - x0) * b[0]; d1 = b[0]; d2 = 0.0; }
+    if (t > xn) { v = y[N - 1] + (t - xn) * b[N - 1]; d1 = b[N - 1]; d2 = 0.0; }
+}
+}  // namespace mh

@@ -2,21 +2,25 @@
 // include/mocohip.h: the direct-collocation NLP hot path of Moco's
 // MocoCasADiSolver (CasOCTranscription / CasOCHermiteSimpson /
 // CasOCTrapezoidal) with its per-grid-point DAE and finite-difference
-// Jacobian, re-designed for CDNA4:
+// Jacobian, re-designed for CDNA4.  One evaluation is two stages:
 //
-//   k_base      one lane per grid point: DAE at the unperturbed point
-//               (feeds eval_g, the t0/tf Jacobian terms and forward FD).
-//   k_fd        one 64-lane wave per (grid point, 32 directions): lanes l and
-//               l^32 evaluate the +h / -h arms of the same direction and
-//               difference through a cross-lane shuffle (no HBM round trip
-//               of the arms); writes D[k][out][dir] with dir contiguous.
-//   k_defects   one workgroup per mesh interval: Hermite / Simpson /
-//               trapezoidal defects + control interpolation rows, written in
-//               CasOC flattenConstraints order (CasOCTranscription.h:219-313).
-//   k_assemble  one workgroup per mesh interval: streams the interval's
-//               nonzeros (row-major, a fixed per-interval template) and
-//               chains D through the defect formulas.  HBM-bound.
-//   k_integrand / k_grad_f / k_reduce_f : objective and its gradient.
+//   DAE stage (model-specialized back ends from mocohip/codegen.py)
+//     k_groups    one wave = one independent piece of the DAE (mass matrix,
+//                 bias forces, an external load, a muscle, an activation) for
+//                 64 (grid point, lane role) tasks; a finite-difference lane
+//                 only re-evaluates the pieces that read its perturbed input.
+//     k_combine   one workgroup per grid point: stages the pieces in LDS, sums
+//                 the generalized forces in a fixed order, solves with the
+//                 mass-matrix factor -> raw outputs Y of every lane.
+//   (generic interpreter / one-lane kernels: k_eval, one lane per DAE.)
+//
+//   transcription stage
+//     k_transcribe  one workgroup per (mesh interval, nonzero chunk): the
+//                 Jacobian values of a fixed per-interval template, chained
+//                 through the Hermite-Simpson / trapezoidal defect formulas
+//                 and CasADi's finite-difference quotients; plus one block
+//                 per interval for the defect / interpolation rows of g.
+//   k_integrand / k_grad / k_reduce_obj : objective and its gradient.
 //
 // There is no CPU fallback anywhere in this file.
 #include <hip/hip_runtime.h>
@@ -247,27 +251,46 @@ struct Tasks {
     const int* dlen;     // [ng] tasks per grid point of group g
     const int* off;      // [ng] slot offset of force group g within a grid point
     const int* roles;    // [ng][stride] j -> lane role
-    const int* jd;       // [ng][stride] lane role -> j (0 = base)
-    const int* blk;      // [nblocks][2] (group, first task)
+    const int* jd;       // [stride][ng] lane role -> slot of group g within the grid
+                         // point (g = 0: index of the mass factor; base = first)
+    const int4* blk;     // [nblocks] (group, first task, tasks per grid point, 1/n as float bits)
 };
+
+#ifdef MH_TASK_TIMING
+// Diagnostic build only (make task-timing, tools/task_timing.py): per block
+// [group, wall clock at start, at end, shader clock at start, at end].
+constexpr int TIMING_SLOTS = 1 << 16;
+__device__ long long g_task_timing[TIMING_SLOTS][5];
+#endif
 
 template <class D>
 __global__ void __launch_bounds__(64) k_groups(DevModel M, Src S, Lanes Ln, Tasks TK,
         double* __restrict__ T, double* __restrict__ H) {
     const int lane = threadIdx.x;
-    const int g = __builtin_amdgcn_readfirstlane(TK.blk[2 * blockIdx.x]);
-    const int first = __builtin_amdgcn_readfirstlane(TK.blk[2 * blockIdx.x + 1]);
-    const int n = __builtin_amdgcn_readfirstlane(TK.dlen[g]);
+#ifdef MH_TASK_TIMING
+    const long long w0 = wall_clock64(), c0 = __builtin_amdgcn_s_memtime();
+#endif
+    const int4 rec = TK.blk[blockIdx.x];   // one scalar load: no dependent table chain
+    const int g = __builtin_amdgcn_readfirstlane(rec.x);
+    const int first = __builtin_amdgcn_readfirstlane(rec.y);
+    const int n = __builtin_amdgcn_readfirstlane(rec.z);
+    const float inv = __int_as_float(__builtin_amdgcn_readfirstlane(rec.w));
     const int task = first + lane;
     const bool live = task < TK.nk * n;
     const int tc = live ? task : 0;
-    const int kl = tc / n;
+    // tc / n through the float reciprocal, corrected to the exact quotient
+    int kl = (int)((float)tc * inv);
+    kl += (kl + 1) * n <= tc ? 1 : 0;
+    kl -= kl * n > tc ? 1 : 0;
     const int j = tc - kl * n;
     const int r = TK.roles[g * TK.stride + j];
     double t;
     const LaneIn<D> in = lane_input<D>(S, Ln, kl, r, t);
     constexpr int NOUT = D::NST > D::NF ? D::NST : D::NF;
     double out[NOUT];
+    // the mass-matrix and bias groups are the longest tasks: give them issue
+    // priority over the short muscle tasks sharing their SIMD
+    if (g < 2) __builtin_amdgcn_s_setprio(2);
     D::group(g, M, t, in, out);
     if (!live) return;
     if (g == 0) {
@@ -279,27 +302,52 @@ __global__ void __launch_bounds__(64) k_groups(DevModel M, Src S, Lanes Ln, Task
 #pragma unroll
         for (int f = 0; f < D::NF; ++f) dst[f] = out[f];
     }
+#ifdef MH_TASK_TIMING
+    if (lane == 0 && blockIdx.x < TIMING_SLOTS) {
+        __builtin_amdgcn_s_waitcnt(0);
+        long long* rec = g_task_timing[blockIdx.x];
+        rec[0] = g; rec[1] = w0; rec[2] = wall_clock64(); rec[3] = c0;
+        rec[4] = __builtin_amdgcn_s_memtime();
+    }
+#endif
 }
 
+// Combine: one workgroup per grid point.  The grid point's group results
+// (contiguous in T and H) are staged in LDS with coalesced loads; each lane
+// (one lane role) then reads the slots it needs from LDS.
 template <class D>
-struct TaskLoad {
-    const double* __restrict__ T;
-    const double* __restrict__ H;
-    const int* __restrict__ jd;
-    const int* __restrict__ off;
-    int stride, nslot, nmass, kl, r;
+struct TaskLoadLds {
+    const double* sT;
+    const double* sH;
+    const int* __restrict__ slot;   // [stride][ng]: slot of group g for this role
+    int r;
     __device__ __forceinline__ double operator()(int g, int f) const {
-        const int j = jd[g * stride + r];
-        return T[((long)kl * nslot + off[g] + j) * D::NF + f];
+        return sT[slot[r * D::NG + g] * D::NF + f];
     }
     __device__ __forceinline__ double h(int f) const {
-        const int j = jd[r];
-        return H[((long)kl * nmass + j) * D::NST + f];
+        return sH[slot[r * D::NG] * D::NST + f];
+    }
+};
+
+// Same arithmetic reading T/H straight from global memory: used when the
+// grid point's slots do not fit in LDS (e.g. MOCOHIP_TASKS=all with central
+// differences).
+template <class D>
+struct TaskLoadGlobal {
+    const double* __restrict__ sT;
+    const double* __restrict__ sH;
+    const int* __restrict__ slot;
+    int r;
+    __device__ __forceinline__ double operator()(int g, int f) const {
+        return sT[slot[r * D::NG + g] * D::NF + f];
+    }
+    __device__ __forceinline__ double h(int f) const {
+        return sH[slot[r * D::NG] * D::NST + f];
     }
 };
 
 template <class D>
-__global__ void __launch_bounds__(64) k_combine(DevModel M, Src S, Lanes Ln, Tasks TK,
+__global__ void __launch_bounds__(64) k_combine_global(DevModel M, Src S, Lanes Ln, Tasks TK,
         const double* __restrict__ T, const double* __restrict__ H, double* __restrict__ times,
         double* __restrict__ Y, long ystride_pt) {
     const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -309,7 +357,55 @@ __global__ void __launch_bounds__(64) k_combine(DevModel M, Src S, Lanes Ln, Tas
     double t;
     const LaneIn<D> in = lane_input<D>(S, Ln, kl, r, t);
     if (r == Ln.base && times) times[kl] = t;
-    const TaskLoad<D> TL{T, H, TK.jd, TK.off, TK.stride, TK.nslot, TK.nmass, kl, r};
+    const TaskLoadGlobal<D> TL{T + (long)kl * TK.nslot * D::NF, H + (long)kl * TK.nmass * D::NST,
+                               TK.jd, r};
+    double out[D::NO];
+    D::combine(M, t, in, TL, out);
+    double* Yk = Y + (long)kl * ystride_pt + r;
+#pragma unroll
+    for (int o = 0; o < D::NO; ++o) Yk[(long)o * Ln.stride] = out[o];
+}
+
+// Copy n doubles to LDS with U loads in flight per thread before the first
+// store (a plain strided loop serializes one memory round trip per pass).
+template <int U>
+__device__ __forceinline__ void stage_lds(double* __restrict__ dst, const double* __restrict__ src,
+        int n) {
+    for (int b = 0; b < n; b += U * (int)blockDim.x) {
+        double v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = b + u * (int)blockDim.x + (int)threadIdx.x;
+            v[u] = src[i < n ? i : n - 1];   // unconditional: no branch per load
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = b + u * (int)blockDim.x + (int)threadIdx.x;
+            if (i < n) dst[i] = v[u];
+        }
+    }
+}
+
+template <class D>
+__global__ void __launch_bounds__(1024) k_combine(DevModel M, Src S, Lanes Ln, Tasks TK,
+        const double* __restrict__ T, const double* __restrict__ H, double* __restrict__ times,
+        double* __restrict__ Y, long ystride_pt) {
+    extern __shared__ double smem[];
+    const int kl = blockIdx.x;
+    const int nt = TK.nslot * D::NF, nh = TK.nmass * D::NST;
+    double* sT = smem;
+    double* sH = smem + nt;
+    const double* Tk = T + (long)kl * nt;
+    const double* Hk = H + (long)kl * nh;
+    if (nt > 0) stage_lds<16>(sT, Tk, nt);
+    if (nh > 0) stage_lds<8>(sH, Hk, nh);
+    __syncthreads();
+    const int r = threadIdx.x;
+    if (r >= Ln.stride) return;
+    double t;
+    const LaneIn<D> in = lane_input<D>(S, Ln, kl, r, t);
+    if (r == Ln.base && times) times[kl] = t;
+    const TaskLoadLds<D> TL{sT, sH, TK.jd, r};
     double out[D::NO];
     D::combine(M, t, in, TL, out);
     // Y[(kl*NO + o)*stride + r]  (ystride_pt = NO*stride; explicit points:
@@ -338,10 +434,9 @@ __device__ __forceinline__ double xdot_at(const Layout& L, const Lanes& Ln,
     return Y[((long)kl * L.NO + (s - L.NQ)) * Ln.stride + Ln.base];
 }
 
-__global__ void __launch_bounds__(256) k_defects(Layout L, Interval I, Lanes Ln,
+__device__ __forceinline__ void defects_block(const Layout& L, const Interval& I, const Lanes& Ln,
         const double* __restrict__ x, const double* __restrict__ times,
-        const double* __restrict__ Y, double* __restrict__ g) {
-    const int il = blockIdx.x;
+        const double* __restrict__ Y, double* __restrict__ g, int il) {
     const int i = I.ib + il;
     const int NS = L.NS;
     double* gi = g + (long)il * I.rpi;
@@ -397,11 +492,10 @@ __device__ __forceinline__ double dxdot(const Layout& L, const Lanes& Ln,
 
 constexpr int ASM_CHUNK = 1024;   // nonzeros per assembly workgroup
 
-__global__ void __launch_bounds__(256) k_assemble(Layout L, Interval I, Lanes Ln,
+__device__ __forceinline__ void assemble_chunk(const Layout& L, const Interval& I, const Lanes& Ln,
         const TplEntry* __restrict__ tpl, const double* __restrict__ x,
         const double* __restrict__ grid, const double* __restrict__ times,
-        const double* __restrict__ Y, double* __restrict__ values) {
-    const int il = blockIdx.y;
+        const double* __restrict__ Y, double* __restrict__ values, int il, int chunk) {
     const int i = I.ib + il;
     const int k_first = grid_of(I, i, 0);
     const int npts = I.scheme == MH_HERMITE_SIMPSON ? 3 : 2;
@@ -409,8 +503,8 @@ __global__ void __launch_bounds__(256) k_assemble(Layout L, Interval I, Lanes Ln
     const double h = times[k_last - L.k0] - times[k_first - L.k0];
     const double dgap = grid[k_last] - grid[k_first];
     double* vi = values + (long)il * I.nnz_int;
-    const int e_end = min(I.nnz_int, (int)(blockIdx.x + 1) * ASM_CHUNK);
-    for (int e = blockIdx.x * ASM_CHUNK + threadIdx.x; e < e_end; e += blockDim.x) {
+    const int e_end = min(I.nnz_int, (chunk + 1) * ASM_CHUNK);
+    for (int e = chunk * ASM_CHUNK + threadIdx.x; e < e_end; e += blockDim.x) {
         const TplEntry T = tpl[e];
         const int s = T.s, dir = T.dir;
         double v = 0.0;
@@ -474,6 +568,19 @@ __global__ void __launch_bounds__(256) k_assemble(Layout L, Interval I, Lanes Ln
         }
         vi[e] = v;
     }
+}
+
+// Transcription stage, one launch: blockIdx.y = mesh interval; blockIdx.x <
+// nchunks streams Jacobian nonzeros (values != null), the last x-block (when
+// g != null) writes the interval's defect / interpolation rows.
+__global__ void __launch_bounds__(256) k_transcribe(Layout L, Interval I, Lanes Ln,
+        const TplEntry* __restrict__ tpl, const double* __restrict__ x,
+        const double* __restrict__ grid, const double* __restrict__ times,
+        const double* __restrict__ Y, double* __restrict__ g, double* __restrict__ values,
+        int nchunks) {
+    const int il = blockIdx.y;
+    if ((int)blockIdx.x < nchunks) assemble_chunk(L, I, Ln, tpl, x, grid, times, Y, values, il, blockIdx.x);
+    else defects_block(L, I, Ln, x, times, Y, g, il);
 }
 
 // ---- objective -------------------------------------------------------------
@@ -766,10 +873,13 @@ static void build_taskset(const TaskInfo& ti, const Lanes& ln, int nk, TaskSet& 
         ts.dlen[g] = (int)D.size();
         for (size_t j = 0; j < D.size(); ++j) {
             ts.roles[(size_t)g * S + j] = D[j];
-            ts.jd[(size_t)g * S + D[j]] = (int)j;
+            ts.jd[(size_t)D[j] * ng + g] = (int)j;
         }
         if (g > 0) { ts.off[g] = nslot; nslot += (int)D.size(); }
     }
+    // the combine reads slot = off[g] + j directly (g = 0: j of the mass factor)
+    for (int r = 0; r < S; ++r)
+        for (int g = 1; g < ng; ++g) ts.jd[(size_t)r * ng + g] += ts.off[g];
     // expensive groups first so they start before the cheap ones fill in
     std::vector<int> order(ng);
     for (int g = 0; g < ng; ++g) order[g] = g;
@@ -781,12 +891,18 @@ static void build_taskset(const TaskInfo& ti, const Lanes& ln, int nk, TaskSet& 
     ts.ntasks = 0.0;
     for (int g : order) {
         const long n = (long)nk * ts.dlen[g];
-        for (long f = 0; f < n; f += 64) { ts.blk.push_back(g); ts.blk.push_back((int)f); }
+        const float inv = 1.0f / (float)ts.dlen[g];
+        int inv_bits;
+        std::memcpy(&inv_bits, &inv, sizeof inv);
+        for (long f = 0; f < n; f += 64) {
+            ts.blk.push_back(g); ts.blk.push_back((int)f);
+            ts.blk.push_back(ts.dlen[g]); ts.blk.push_back(inv_bits);
+        }
         ts.flops += (double)n * ti.gflops[g];
         ts.ntasks += (double)n;
     }
     ts.flops += (double)nk * S * ti.combine_flops;
-    ts.nblocks = (int)(ts.blk.size() / 2);
+    ts.nblocks = (int)(ts.blk.size() / 4);
     ts.dev.ng = ng;
     ts.dev.stride = S;
     ts.dev.nslot = nslot;
@@ -811,7 +927,7 @@ static void bind_taskset(char* base, const TaskOffsets& o, TaskSet& ts) {
     ts.dev.off = (const int*)(base + o.off);
     ts.dev.roles = (const int*)(base + o.roles);
     ts.dev.jd = (const int*)(base + o.jd);
-    ts.dev.blk = (const int*)(base + o.blk);
+    ts.dev.blk = (const int4*)(base + o.blk);
 }
 
 }  // namespace
@@ -855,6 +971,11 @@ struct mh_ctx {
     char* probe_mem = nullptr;     // tables + T/H of the last mh_eval_dae size
     double *d_pT = nullptr, *d_pH = nullptr;
     int probe_np = -1;
+    // captured launch sequences, keyed by (kind, x, out pointers)
+    struct GraphEntry { int kind; const void *x, *a, *b; hipGraphExec_t exec; };
+    std::vector<GraphEntry> graphs;
+    bool use_graphs = false;
+    bool spin_wait = false;
 };
 
 // Task tables and T/H buffers for an mh_eval_dae call of np points (kept
@@ -1272,6 +1393,16 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
         c->d_H = (double*)(b + o_H);
     }
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    {
+        // hipGraph replay of the stages: measured slower than direct launches
+        // on ROCm 7.2 for this sequence (opt-in, MOCOHIP_GRAPHS=1)
+        const char* eg = std::getenv("MOCOHIP_GRAPHS");
+        c->use_graphs = eg && std::strcmp(eg, "1") == 0;
+        // poll for completion instead of a blocking wait (opt-in,
+        // MOCOHIP_SPIN=1; no measurable gain on the bench workload)
+        const char* es = std::getenv("MOCOHIP_SPIN");
+        c->spin_wait = es && std::strcmp(es, "1") == 0;
+    }
     for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
     *out = c.release();
     return MH_OK;
@@ -1286,6 +1417,7 @@ extern "C" void mh_destroy(mh_ctx* c) {
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->dmem) (void)hipFree(c->dmem);
     if (c->probe_mem) (void)hipFree(c->probe_mem);
+    for (auto& e : c->graphs) (void)hipGraphExecDestroy(e.exec);
     delete c;
 }
 
@@ -1387,6 +1519,8 @@ extern "C" int mh_get_jac_structure(const mh_ctx* c, int32_t* iRow, int32_t* jCo
 // ------------------------------------------------------------------------
 // Back ends and launchers.
 // ------------------------------------------------------------------------
+constexpr size_t kMaxLds = 160 * 1024;   // gfx950 LDS per workgroup
+
 struct Backend {
     const char* name;
     // one evaluation stage: raw DAE outputs of every lane of c->lanes_g
@@ -1412,9 +1546,19 @@ static void launch_tasks(mh_ctx* c, const Src& S, const Lanes& ln, const TaskSet
         double* H, double* times, double* Y) {
     hipLaunchKernelGGL(k_groups<D>, dim3((unsigned)ts.nblocks), dim3(64), 0, c->stream, c->M, S, ln,
             ts.dev, T, H);
-    const long lanes = (long)ts.dev.nk * ln.stride;
-    hipLaunchKernelGGL(k_combine<D>, dim3((unsigned)((lanes + 63) / 64)), dim3(64), 0, c->stream, c->M,
-            S, ln, ts.dev, T, H, times, Y, (long)D::NO * ln.stride);
+    const unsigned threads = (unsigned)((ln.stride + 63) / 64 * 64);
+    const size_t lds = sizeof(double) * ((size_t)ts.dev.nslot * D::NF + (size_t)ts.dev.nmass * D::NST);
+    if (threads <= 1024 && lds <= kMaxLds) {
+        if (lds > 65536)
+            (void)hipFuncSetAttribute((const void*)k_combine<D>,
+                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL(k_combine<D>, dim3((unsigned)ts.dev.nk), dim3(threads), lds, c->stream, c->M,
+                S, ln, ts.dev, T, H, times, Y, (long)D::NO * ln.stride);
+    } else {
+        const long lanes = (long)ts.dev.nk * ln.stride;
+        hipLaunchKernelGGL(k_combine_global<D>, dim3((unsigned)((lanes + 63) / 64)), dim3(64), 0,
+                c->stream, c->M, S, ln, ts.dev, T, H, times, Y, (long)D::NO * ln.stride);
+    }
 }
 template <class D>
 static void be_eval_tasks(mh_ctx* c, const double* x, int mode, double* Y) {
@@ -1485,58 +1629,85 @@ static const GenEntry kGeneratedModels[] = {
 };
 #undef MH_GEN_MODEL
 
-static int run_g(mh_ctx* c, const double* x_dev, double* g_dev) {
+// One evaluation = two stages on the context stream: the DAE stage (eval
+// kernels) and the transcription stage (defects and/or Jacobian assembly),
+// with timing events recorded between them.  kind 0: g, 1: Jacobian, 2: both
+// from one DAE pass (the base lane of every grid point feeds the defects;
+// IPOPT's eval_g(new_x=true) -> eval_jac_g(new_x=false) sequence).
+static int launch_stage(mh_ctx* c, int stage, int kind, const double* x, double* a, double* b) {
+    if (stage == 0) {
+        c->be->eval(c, x, kind == 0 ? 0 : 1, kind == 0 ? c->d_Yg : c->d_Y);
+        HIPCHK(hipGetLastError());
+        return MH_OK;
+    }
     Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, c->k0, c->nk};
     Interval I{c->scheme, c->interp, c->ib, c->rpi, c->nnz_int};
-    HIPCHK(hipEventRecord(c->ev[0], c->stream));
-    c->be->eval(c, x_dev, 0, c->d_Yg);
+    const Lanes& ln = kind == 0 ? c->lanes_g : c->lanes_jac;
+    const double* Y = kind == 0 ? c->d_Yg : c->d_Y;
+    const int nchunks = kind == 0 ? 0 : (c->nnz_int + ASM_CHUNK - 1) / ASM_CHUNK;
+    double* g = kind == 1 ? nullptr : a;
+    double* v = kind == 0 ? nullptr : (kind == 1 ? a : b);
+    hipLaunchKernelGGL(k_transcribe, dim3((unsigned)(nchunks + (g ? 1 : 0)), (unsigned)(c->ie - c->ib)),
+            dim3(256), 0, c->stream, L, I, ln, c->d_tpl, x, c->d_grid, c->d_times, Y, g, v, nchunks);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(c->ev[1], c->stream));
-    hipLaunchKernelGGL(k_defects, dim3(c->ie - c->ib), dim3(256), 0, c->stream, L, I, c->lanes_g,
-            x_dev, c->d_times, c->d_Yg, g_dev);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(c->ev[2], c->stream));
     return MH_OK;
 }
 
-static int run_jac(mh_ctx* c, const double* x_dev, double* v_dev) {
-    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, c->k0, c->nk};
-    Interval I{c->scheme, c->interp, c->ib, c->rpi, c->nnz_int};
-    HIPCHK(hipEventRecord(c->ev[0], c->stream));
-    c->be->eval(c, x_dev, 1, c->d_Y);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(c->ev[1], c->stream));
-    hipLaunchKernelGGL(k_assemble, dim3((c->nnz_int + ASM_CHUNK - 1) / ASM_CHUNK, c->ie - c->ib),
-            dim3(256), 0, c->stream, L, I, c->lanes_jac,
-            c->d_tpl, x_dev, c->d_grid, c->d_times, c->d_Y, v_dev);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(c->ev[2], c->stream));
+// A stage as one hipGraph launch, captured on first use for a given set of
+// device pointers (IPOPT and the device entry points reuse the same buffers
+// every call).  Opt-in: MOCOHIP_GRAPHS=1.
+static int run_stage(mh_ctx* c, int stage, int kind, const double* x, double* a, double* b) {
+    if (!c->use_graphs) return launch_stage(c, stage, kind, x, a, b);
+    const int key = stage * 4 + kind;
+    for (const auto& e : c->graphs)
+        if (e.kind == key && e.x == x && e.a == a && e.b == b) {
+            HIPCHK(hipGraphLaunch(e.exec, c->stream));
+            return MH_OK;
+        }
+    hipGraph_t graph = nullptr;
+    HIPCHK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+    const int rc = launch_stage(c, stage, kind, x, a, b);
+    const hipError_t ec = hipStreamEndCapture(c->stream, &graph);
+    if (rc) {
+        if (graph) (void)hipGraphDestroy(graph);
+        return rc;
+    }
+    HIPCHK(ec);
+    hipGraphExec_t exec = nullptr;
+    const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    HIPCHK(ei);
+    if (c->graphs.size() >= 16) {
+        (void)hipGraphExecDestroy(c->graphs.front().exec);
+        c->graphs.erase(c->graphs.begin());
+    }
+    c->graphs.push_back({key, x, a, b, exec});
+    HIPCHK(hipGraphLaunch(exec, c->stream));
     return MH_OK;
 }
 
-// eval_g and eval_jac_g at the same iterate from ONE evaluation launch: the
-// base lane of every grid point feeds the defects (the host-side adapter uses
-// it for IPOPT's eval_g(new_x=true) -> eval_jac_g(new_x=false) sequence).
-static int run_g_jac(mh_ctx* c, const double* x_dev, double* g_dev, double* v_dev) {
-    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, c->k0, c->nk};
-    Interval I{c->scheme, c->interp, c->ib, c->rpi, c->nnz_int};
+static int run_cached(mh_ctx* c, int kind, const double* x, double* a, double* b) {
     HIPCHK(hipEventRecord(c->ev[0], c->stream));
-    c->be->eval(c, x_dev, 1, c->d_Y);
-    HIPCHK(hipGetLastError());
+    int rc = run_stage(c, 0, kind, x, a, b);
+    if (rc) return rc;
     HIPCHK(hipEventRecord(c->ev[1], c->stream));
-    hipLaunchKernelGGL(k_defects, dim3(c->ie - c->ib), dim3(256), 0, c->stream, L, I, c->lanes_jac,
-            x_dev, c->d_times, c->d_Y, g_dev);
-    hipLaunchKernelGGL(k_assemble, dim3((c->nnz_int + ASM_CHUNK - 1) / ASM_CHUNK, c->ie - c->ib),
-            dim3(256), 0, c->stream, L, I, c->lanes_jac, c->d_tpl, x_dev, c->d_grid, c->d_times,
-            c->d_Y, v_dev);
-    HIPCHK(hipGetLastError());
+    rc = run_stage(c, 1, kind, x, a, b);
+    if (rc) return rc;
     HIPCHK(hipEventRecord(c->ev[2], c->stream));
     return MH_OK;
 }
 
 static int finish(mh_ctx* c) {
     HIPCHK(hipEventRecord(c->ev[3], c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    if (c->spin_wait) {
+        // poll instead of a blocking wait: the call is latency-bound and the
+        // wake-up of a blocking synchronize costs several microseconds
+        hipError_t q;
+        while ((q = hipEventQuery(c->ev[3])) == hipErrorNotReady) {}
+        HIPCHK(q);
+    } else {
+        HIPCHK(hipStreamSynchronize(c->stream));
+    }
     float a = 0, b = 0, d = 0;
     (void)hipEventElapsedTime(&a, c->ev[0], c->ev[3]);
     (void)hipEventElapsedTime(&b, c->ev[0], c->ev[1]);
@@ -1549,7 +1720,7 @@ extern "C" int mh_eval_g(mh_ctx* c, const double* x, int, double* g) {
     if (!c || !x || !g) return set_err(MH_ERR_INVALID, "null argument");
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipMemcpyAsync(c->d_x, x, sizeof(double) * c->n, hipMemcpyHostToDevice, c->stream));
-    int rc = run_g(c, c->d_x, c->d_g);
+    int rc = run_cached(c, 0, c->d_x, c->d_g, nullptr);
     if (rc) return rc;
     HIPCHK(hipMemcpyAsync(g, c->d_g, sizeof(double) * (size_t)(c->ie - c->ib) * c->rpi,
             hipMemcpyDeviceToHost, c->stream));
@@ -1560,7 +1731,7 @@ extern "C" int mh_eval_jac_g(mh_ctx* c, const double* x, int, double* values) {
     if (!c || !x || !values) return set_err(MH_ERR_INVALID, "null argument");
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipMemcpyAsync(c->d_x, x, sizeof(double) * c->n, hipMemcpyHostToDevice, c->stream));
-    int rc = run_jac(c, c->d_x, c->d_vals);
+    int rc = run_cached(c, 1, c->d_x, c->d_vals, nullptr);
     if (rc) return rc;
     HIPCHK(hipMemcpyAsync(values, c->d_vals, sizeof(double) * (size_t)(c->ie - c->ib) * c->nnz_int,
             hipMemcpyDeviceToHost, c->stream));
@@ -1570,7 +1741,7 @@ extern "C" int mh_eval_jac_g(mh_ctx* c, const double* x, int, double* values) {
 extern "C" int mh_eval_g_device(mh_ctx* c, const double* x_dev, double* g_dev) {
     if (!c || !x_dev || !g_dev) return set_err(MH_ERR_INVALID, "null argument");
     HIPCHK(hipSetDevice(c->device));
-    int rc = run_g(c, x_dev, g_dev);
+    int rc = run_cached(c, 0, x_dev, g_dev, nullptr);
     if (rc) return rc;
     return finish(c);
 }
@@ -1578,7 +1749,7 @@ extern "C" int mh_eval_g_device(mh_ctx* c, const double* x_dev, double* g_dev) {
 extern "C" int mh_eval_jac_g_device(mh_ctx* c, const double* x_dev, double* v_dev) {
     if (!c || !x_dev || !v_dev) return set_err(MH_ERR_INVALID, "null argument");
     HIPCHK(hipSetDevice(c->device));
-    int rc = run_jac(c, x_dev, v_dev);
+    int rc = run_cached(c, 1, x_dev, v_dev, nullptr);
     if (rc) return rc;
     return finish(c);
 }
@@ -1586,7 +1757,7 @@ extern "C" int mh_eval_jac_g_device(mh_ctx* c, const double* x_dev, double* v_de
 extern "C" int mh_eval_g_jac_g_device(mh_ctx* c, const double* x_dev, double* g_dev, double* v_dev) {
     if (!c || !x_dev || !g_dev || !v_dev) return set_err(MH_ERR_INVALID, "null argument");
     HIPCHK(hipSetDevice(c->device));
-    int rc = run_g_jac(c, x_dev, g_dev, v_dev);
+    int rc = run_cached(c, 2, x_dev, g_dev, v_dev);
     if (rc) return rc;
     return finish(c);
 }
@@ -1595,7 +1766,7 @@ extern "C" int mh_eval_g_jac_g(mh_ctx* c, const double* x, double* g, double* va
     if (!c || !x || !g || !values) return set_err(MH_ERR_INVALID, "null argument");
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipMemcpyAsync(c->d_x, x, sizeof(double) * c->n, hipMemcpyHostToDevice, c->stream));
-    int rc = run_g_jac(c, c->d_x, c->d_g, c->d_vals);
+    int rc = run_cached(c, 2, c->d_x, c->d_g, c->d_vals);
     if (rc) return rc;
     HIPCHK(hipMemcpyAsync(g, c->d_g, sizeof(double) * (size_t)(c->ie - c->ib) * c->rpi,
             hipMemcpyDeviceToHost, c->stream));
@@ -1607,6 +1778,7 @@ extern "C" int mh_eval_g_jac_g(mh_ctx* c, const double* x, double* g, double* va
 extern "C" int mh_eval_f(mh_ctx* c, const double* x, int, double* f) {
     if (!c || !x || !f) return set_err(MH_ERR_INVALID, "null argument");
     HIPCHK(hipSetDevice(c->device));
+    (void)hipGetLastError();   // report only this call's launch errors
     HIPCHK(hipMemcpyAsync(c->d_x, x, sizeof(double) * c->n, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipEventRecord(c->ev[0], c->stream));
     Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, 0, c->G};
@@ -1626,6 +1798,7 @@ extern "C" int mh_eval_f(mh_ctx* c, const double* x, int, double* f) {
 extern "C" int mh_eval_grad_f(mh_ctx* c, const double* x, int, double* grad) {
     if (!c || !x || !grad) return set_err(MH_ERR_INVALID, "null argument");
     HIPCHK(hipSetDevice(c->device));
+    (void)hipGetLastError();   // report only this call's launch errors
     HIPCHK(hipMemcpyAsync(c->d_x, x, sizeof(double) * c->n, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipEventRecord(c->ev[0], c->stream));
     Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, 0, c->G};
@@ -1656,6 +1829,7 @@ extern "C" int mh_eval_dae(mh_ctx* c, int32_t np, const double* inputs, double* 
     HIPCHK(hipMalloc(&din, sizeof(double) * nin));
     HIPCHK(hipMalloc(&dout, sizeof(double) * std::max<size_t>(nout, 1)));
     HIPCHK(hipMemcpyAsync(din, inputs, sizeof(double) * nin, hipMemcpyHostToDevice, c->stream));
+    (void)hipGetLastError();
     c->be->probe(c, np, din, dout);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(outputs, dout, sizeof(double) * nout, hipMemcpyDeviceToHost, c->stream));
@@ -1665,6 +1839,14 @@ extern "C" int mh_eval_dae(mh_ctx* c, int32_t np, const double* inputs, double* 
     return MH_OK;
 }
 
+
+#ifdef MH_TASK_TIMING
+extern "C" int mh_debug_task_timing(long long* out, int nslots) {
+    const int n = std::min(nslots, TIMING_SLOTS);
+    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_task_timing), sizeof(long long) * 5 * n));
+    return MH_OK;
+}
+#endif
 
 extern "C" int mh_last_timings(const mh_ctx* c, double* ms3) {
     if (!c || !ms3) return set_err(MH_ERR_INVALID, "null argument");

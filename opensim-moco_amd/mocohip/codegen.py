@@ -231,7 +231,26 @@ class ModelView:
         self.acts = [cm._acts[i] for i in range(st.nactuators)]
         self.tables = [cm._tables[i] for i in range(st.ntables)]
         self.ext = [cm._ext[i] for i in range(st.nexternal)]
+        self.breaks = [st.table_breaks[i] for i in range(st.nbreaks)]
         self.gravity = list(st.gravity)
+
+
+def _uniform_guess(br):
+    """1/spacing if floor((t - br[0]) / spacing) is within one segment of the
+    right one for every t in range (so a single +-1 correction step finds
+    it), else None."""
+    n = len(br) - 1
+    if n < 2:
+        return None
+    inv = n / (br[-1] - br[0])
+    if not math.isfinite(inv) or inv <= 0:
+        return None
+    for i in range(n):
+        lo = math.floor((br[i] - br[0]) * inv)
+        hi = math.floor((np.nextafter(br[i + 1], -np.inf) - br[0]) * inv)
+        if lo < i - 1 or hi > i + 1:
+            return None
+    return inv
 
 
 class _Layout:
@@ -288,8 +307,20 @@ class _Emitter:
             g.k += 1
             base = f"f{g.k}"
             g.raw(f"double {base}v, {base}d1, {base}d2;")
-            g.raw(f"mh::simm_eval_n<{F.knot_count}>(M, {F.knot_begin}, {self.q[F.coord]}, "
-                  f"{base}v, {base}d1, {base}d2);")
+            # interval from the literal knots (no load on the dependency
+            # chain), then one round trip for the coefficients
+            N = F.knot_count
+            xk = [float(M.kx[F.knot_begin + i]) for i in range(N)]
+            qv = self.q[F.coord]
+            if N > 1:
+                cnt = " + ".join(f"({qv} >= {lit(xk[i])})" for i in range(1, N - 1)) or "0"
+                g.raw(f"int {base}k = {cnt};")
+                g.raw(f"if (fabs({qv} - {lit(xk[0])}) <= 2e-13) {base}k = 0; "
+                      f"else if (fabs({qv} - {lit(xk[N - 1])}) <= 2e-13) {base}k = {N - 1};")
+                g.raw(f"mh::simm_eval_k<{N}>(M, {F.knot_begin}, {qv}, {base}k, {lit(xk[0])}, "
+                      f"{lit(xk[N - 1])}, {base}v, {base}d1, {base}d2);")
+            else:
+                g.raw(f"mh::simm_eval_n<1>(M, {F.knot_begin}, {qv}, {base}v, {base}d1, {base}d2);")
             g.flops["add"] += 6
             g.flops["mul"] += 8
             v, d1, d2 = S(n=f"{base}v"), S(n=f"{base}d1"), S(n=f"{base}d2")
@@ -557,11 +588,13 @@ class _Emitter:
                 H[(i, j)] = g.svdot(Sj[j], Fi)
                 j = lam[j]
         for k in range(NQ - 1, -1, -1):
-            a = g.fn("sqrt", H[(k, k)])
+            # the factor keeps 1/L_kk on the diagonal: one division per
+            # column here, multiplications in the factorization and solves
+            a = g.div(_c(1.0), g.fn("sqrt", H[(k, k)]))
             H[(k, k)] = a
             i = lam[k]
             while i >= 0:
-                H[(k, i)] = g.div(H[(k, i)], a)
+                H[(k, i)] = g.mul(H[(k, i)], a)
                 i = lam[i]
             i = lam[k]
             while i >= 0:
@@ -577,7 +610,7 @@ class _Emitter:
         bvec = list(bvec)
         xs = [None] * NQ
         for i in range(NQ - 1, -1, -1):
-            xs[i] = g.div(bvec[i], H[(i, i)])
+            xs[i] = g.mul(bvec[i], H[(i, i)])
             j = lam[i]
             while j >= 0:
                 bvec[j] = g.sub(bvec[j], g.mul(H[(i, j)], xs[i]))
@@ -588,7 +621,7 @@ class _Emitter:
             while j >= 0:
                 xi = g.sub(xi, g.mul(H[(i, j)], xs[j]))
                 j = lam[j]
-            xs[i] = g.div(xi, H[(i, i)])
+            xs[i] = g.mul(xi, H[(i, i)])
         return xs
 
     def external_forces(self, P, Facc, only=None):
@@ -600,10 +633,20 @@ class _Emitter:
             b = e.body
             g.k += 1
             seg = f"seg{g.k}"
-            g.raw(f"const int {seg} = mh::table_segment(M, {e.table}, t);")
+            T = M.tables[e.table]
+            br = M.breaks[T.break_begin:T.break_begin + T.nseg + 1]
+            guess = _uniform_guess(br)
+            if guess is not None:
+                # near-uniform breakpoints: direct index + one-step
+                # correction (two dependent loads instead of a binary search)
+                g.raw(f"const int {seg} = mh::table_segment_u<{T.nseg}>(M.brk + {T.break_begin}, t, "
+                      f"{lit(br[0])}, {lit(guess)});")
+            else:
+                g.raw(f"const int {seg} = mh::table_segment(M, {e.table}, t);")
 
             def col(cidx):
-                return g.tmp(f"mh::table_value(M, {e.table}, {seg}, {cidx}, t)")
+                return g.tmp(f"mh::table_value_c<{T.degree}, {T.ncol}>(M.coef + {T.coef_begin}, "
+                             f"M.brk + {T.break_begin}, {seg}, {cidx}, t)")
             Fv = [col(e.force_col + d) for d in range(3)] if e.force_col >= 0 else Z3
             Pp = [col(e.point_col + d) for d in range(3)] if e.point_col >= 0 else P[b]
             Tq = [col(e.torque_col + d) for d in range(3)] if e.torque_col >= 0 else Z3
@@ -760,8 +803,8 @@ def _emit_groups(M: ModelView, Lo: _Layout) -> List[_Group]:
       ext_e     external load e (q along the body chain, time)
       muscle_m  path, DeGroote-Fregly force, tendon point forces -> tau, and
                 the normalized tendon force derivative if compliant
-    Coordinate actuators and activation dynamics are evaluated per lane in
-    the combine step."""
+      activation_m  DeGroote-Fregly activation dynamics (a_m, e_m)
+    Coordinate actuators are evaluated per lane in the combine step."""
     NQ = Lo.NQ
     allb = list(range(M.nb))
     out = []
@@ -817,6 +860,18 @@ def _emit_groups(M: ModelView, Lo: _Layout) -> List[_Group]:
         E.backward(cl, Facc, Sj, cb, tv)
         finish(E, f"ext_{ie}", tv)
 
+    # activation dynamics (reads the muscle's activation and excitation only)
+    for im in range(len(M.muscles)):
+        sa = Lo.act_state[im]
+        if sa < 0:
+            continue
+        E = _Emitter(M, Lo)
+        adot = _activation_dot(E.g, E.inp[sa], E.ctrl[Lo.mus_control[im]], Lo.tau_act, Lo.tau_deact)
+        E.g.raw(f"out[0] = {adot};")
+        r, t = _reads_of(E.g.lines)
+        out.append(_Group(f"activation_{im}", E.g.lines, [("z", sa - 2 * NQ)], r, t,
+                          sum(E.g.flops.values())))
+
     # muscles
     for im, mu in enumerate(M.muscles):
         E = _Emitter(M, Lo)
@@ -840,8 +895,7 @@ def _emit_combine(M: ModelView, Lo: _Layout, groups: List[_Group]):
     """Per-lane combine: generalized forces summed over the groups in a fixed
     order (so re-using a group's unperturbed result is bit-identical to
     re-evaluating it), coordinate actuators, the two triangular solves with
-    the mass-matrix factor, activation dynamics and the compliant-tendon
-    derivatives."""
+    the mass-matrix factor, and the z outputs of the groups."""
     NQ = Lo.NQ
     E = _Emitter(M, Lo)
     g = E.g
@@ -866,11 +920,6 @@ def _emit_combine(M: ModelView, Lo: _Layout, groups: List[_Group]):
     xs = E.solve(groups[0].lam, Hs, bvec)
     for i in range(NQ):
         g.raw(f"out[{i}] = {xs[i]};")
-    for im in range(len(M.muscles)):
-        sa = Lo.act_state[im]
-        if sa >= 0:
-            adot = _activation_dot(g, E.inp[sa], E.ctrl[Lo.mus_control[im]], Lo.tau_act, Lo.tau_deact)
-            g.raw(f"out[{NQ + sa - 2 * NQ}] = {adot};")
     for gi, gr in enumerate(groups[1:], start=1):
         for f, (kind, zi) in enumerate(gr.fields):
             if kind == "z":
