@@ -1,0 +1,18 @@
+#!/bin/bash
+# Copy the judged parts of a GPU session (tools/gpu_session.sh <tag>) from
+# gpurun_out/ into profiles/<dest>/: rocprofv3 kernel stats, the per-kernel
+# PMC summary, the bench JSON lines and the host description.
+#   usage: tools/collect_profile.sh <tag> <dest>
+set -e
+TAG=$1
+DEST=profiles/$2
+mkdir -p "$DEST"
+P=gpurun_out/prof_$TAG
+for d in trace_fused trace_separate; do
+    [ -f "$P/$d/run_kernel_stats.csv" ] && cp "$P/$d/run_kernel_stats.csv" "$DEST/${d}_kernel_stats.csv"
+done
+python tools/kstats.py "$P" > "$DEST/summary.txt"
+grep -h '^{' "$P"/*.log > "$DEST/bench_lines_under_profiler.jsonl" || true
+[ -f "gpurun_out/$TAG/bench.json" ] && cp "gpurun_out/$TAG/bench.json" "$DEST/bench.json"
+[ -f "gpurun_out/$TAG/host.txt" ] && head -20 "gpurun_out/$TAG/host.txt" > "$DEST/host.txt"
+ls "$DEST"

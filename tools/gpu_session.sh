@@ -1,0 +1,25 @@
+#!/bin/bash
+# One GPU-box session (run through gpurun from the repo root): GPU parity
+# tests, smoke, the default bench line, then the round profile.  Every GPU
+# step has its own time limit and the steps stop at the first failure.
+#   usage: tools/gpu_session.sh <tag> [tests|bench|profile|all]
+set -e
+TAG=${1:-r01}
+WHAT=${2:-all}
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$ROOT/gpurun_out/$TAG
+mkdir -p "$OUT"
+cd "$ROOT"
+(nproc; lscpu | head -20; rocm-smi --showproductname 2>/dev/null | head -20) > "$OUT/host.txt" 2>&1 || true
+if [[ $WHAT == tests || $WHAT == all ]]; then
+    timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+        > "$OUT/pytest_gpu.log" 2>&1
+    timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
+fi
+if [[ $WHAT == bench || $WHAT == all ]]; then
+    timeout -k 10 300 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
+fi
+if [[ $WHAT == profile || $WHAT == all ]]; then
+    timeout -k 10 900 bash tools/profile_gpu.sh "$TAG"
+fi
+echo "session $TAG done"
