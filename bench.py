@@ -1,18 +1,31 @@
 #!/usr/bin/env python
 """Benchmark: NLP eval_g + eval_jac_g calls/sec on MocoTrack gait10dof18musc
 (DeGrooteFregly2016 muscles, rigid tendon, 18 excitations + 10 reserves,
-Hermite-Simpson, forward finite differences), BASELINE.json configs[2].
+GRF external loads, Hermite-Simpson, forward finite differences),
+BASELINE.json configs[2] (N=200 mesh intervals).
 
 One step = one eval_g and one eval_jac_g of the full NLP at an iterate
-resident in HBM (device-pointer C ABI), results left in HBM.  With
---gpus N > 1 the mesh intervals are sharded over the ranks (one process per
-GPU) and the g / Jacobian-value segments are all-gathered over RCCL so
-every rank holds the whole g and J (what a host IPOPT needs): strong
-scaling of the same NLP.
+resident in HBM (device-pointer C ABI), results left in HBM
+(--mode fused: the one-call form IPOPT's eval_g(new_x) -> eval_jac_g(!new_x)
+pair allows; identical results).
+
+Timed region: K steps without per-call instrumentation.  The roofline
+numbers come from a second, instrumented pass of the same K steps right
+after it (HIP events between the stages on the context stream; they cost
+microseconds per call, so they stay out of `value`).
+
+--gpus N > 1 (one process per GPU, torch.distributed.run):
+  --multi replicas (default): every rank evaluates its own copy of the NLP
+      (the configs[4] batch layout: independent NLPs, one per GPU, no
+      collective on the data path) -> "scaling": "weak".
+  --multi mesh: the mesh intervals of ONE NLP are sharded over the ranks and
+      the g / Jacobian segments all-gathered over RCCL every step (what a
+      single host IPOPT needs) -> "scaling": "strong".
 
 Prints one JSON line on rank 0.
 """
 import argparse
+import glob
 import json
 import os
 import sys
@@ -23,15 +36,15 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "opensim-moco_amd"))
 
-FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 (vector = matrix) dense peak, spec
-HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md
+FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector (= FP64 matrix) dense peak, spec
+HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md (spec; 6.29 TB/s measured copy)
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--intervals", type=int, default=200)
     ap.add_argument("--fd", default="forward")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
@@ -39,15 +52,18 @@ def parse():
     ap.add_argument("--mode", choices=["separate", "fused"], default="separate",
                     help="separate: eval_g then eval_jac_g C-ABI calls; fused: one "
                          "mh_eval_g_jac_g call (IPOPT new_x=false pattern)")
+    ap.add_argument("--multi", choices=["replicas", "mesh"], default="replicas")
     return ap.parse_args()
 
 
-def flops_per_dae():
-    path = os.path.join(ROOT, "tests", "golden", "flop_counts.json")
-    if not os.path.exists(path):
-        return None
-    with open(path) as fh:
-        return json.load(fh)
+def latest_pmc():
+    """Per-launch HBM bytes of the hot kernels from the newest committed
+    rocprofv3 PMC summary (profiles/*/pmc.json, tools/pmc_summary.py)."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc.json")), key=os.path.getmtime)
+    if not files:
+        return None, None
+    with open(files[-1]) as fh:
+        return json.load(fh), os.path.relpath(files[-1], ROOT)
 
 
 def main():
@@ -61,96 +77,118 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        world = max(world, 1)
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    mesh = world > 1 and args.multi == "mesh"
 
     N = args.intervals
     st = configs.gait10dof18musc(N, fd_scheme=args.fd)
     st.solver.device = local
     rep = st.problem.create_rep()
-    ib, ie = interval_shard(N, rank, world)
+    ib, ie = interval_shard(N, rank, world) if mesh else (0, N)
     nlp = HipNLP(rep, st.solver.options(ib, ie))
-    x = nlp.random_iterate(np.random.default_rng(0).uniform(-1, 1, nlp.n))
-    # an iterate within bounds where the muscle model is regular: bounds
-    # midpoint for states, random controls
+    # iterate: bounds midpoint for the states (where the muscle model is
+    # regular), uniform random controls within bounds (seed 0; replicas use
+    # seed = rank: independent trials)
+    x = nlp.random_iterate(np.random.default_rng(rank if not mesh else 0).uniform(-1, 1, nlp.n))
     xm = nlp.initial_guess_from_bounds()
     x[2:2 + nlp.NS * nlp.G] = xm[2:2 + nlp.NS * nlp.G]
     dev = torch.device("cuda", local)
     xd = torch.tensor(x, dtype=torch.float64, device=dev)
     rpi = nlp.m // N
     nzi = nlp.nnz // N
-    sg = ShardGather(N, rpi, nzi, world, dev)
+    sg = ShardGather(N, rpi, nzi, world if mesh else 1, dev)
     gseg, vseg = sg.gseg, sg.vseg
 
-    fd_ms = []
+    rec = {"g": [], "jac": []}
 
     def step(record=False):
         if args.mode == "fused":
             nlp.eval_g_jac_g_device(xd.data_ptr(), gseg.data_ptr(), vseg.data_ptr())
+            if record:
+                rec["jac"].append(nlp.last_timings())
         else:
             nlp.eval_g_device(xd.data_ptr(), gseg.data_ptr())
+            if record:
+                rec["g"].append(nlp.last_timings())
             nlp.eval_jac_g_device(xd.data_ptr(), vseg.data_ptr())
-        if record:
-            fd_ms.append(nlp.last_timings())
-        if world > 1:
+            if record:
+                rec["jac"].append(nlp.last_timings())
+        if mesh:
             sg.gather()
+
+    def timed(k, record):
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(k):
+            step(record)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(record=True)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = timed(args.steps, False)
+    # instrumented pass (roofline): same K steps with stage events
+    nlp.set_timing(True)
+    inst_elapsed = timed(args.steps, True)
+    nlp.set_timing(False)
+
     ms_per_step = 1e3 * elapsed / args.steps
-    value = args.steps / elapsed
+    value = (args.steps if mesh else args.steps * world) / elapsed
 
     if rank == 0:
-        T = np.array(fd_ms)            # [whole, dae+fd kernels, assembly] per jac call
-        fd_kernel_ms = float(T[:, 1].mean())
-        asm_ms = float(T[:, 2].mean())
-        G_local = nlp.G if world == 1 else (2 * (ie - ib) + 1)
-        ND = nlp.NS + nlp.NC + 2
+        J = np.array(rec["jac"])          # [whole, DAE stage, transcription, k_groups] ms
+        dae_ms = float(np.median(J[:, 1]))
+        groups_ms = float(np.median(J[:, 3]))
+        asm_ms = float(np.median(J[:, 2]))
+        G_local = nlp.G if not mesh else (2 * (ie - ib) + 1)
+        ND = nlp.NS + nlp.NC + 2              # FD directions incl. t0, tf
         n_dae = G_local * (ND + 1) if args.fd != "central" else G_local * (2 * ND + 1)
-        # (one lane per FD arm plus the unperturbed base lane per grid point)
-        be_name, gen_flops, mhash = nlp.backend()
-        fc = flops_per_dae() or {}
-        key = "gait10dof18musc_rigid"
-        # algorithmic FP64 ops per DAE evaluation of the algorithm the kernel
-        # runs: the generator's emitted-op count for a generated back end,
-        # the oracle's counted restatement for the generic interpreter.
-        f_dae = gen_flops if gen_flops > 0 else fc.get(key, {}).get("flops_per_dae")
-        if f_dae:
-            flops = n_dae * f_dae
-            achieved = flops / (fd_kernel_ms * 1e-3) / 1e12
-        else:
-            achieved = None
-        roof = {"bound": "mfma", "kernel": "k_eval (one lane per DAE evaluation; FP64 VALU; "
-                                           "MI355X FP64 vector peak = FP64 matrix peak)",
-                "achieved": None if achieved is None else round(achieved, 4),
-                "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": None if achieved is None else round(achieved / FP64_PEAK_TFLOPS, 5),
-                "traffic": None, "backend": be_name, "model_hash": f"0x{mhash:016x}",
-                "dae_evals_per_launch": n_dae, "flops_per_dae": f_dae,
-                "oracle_flops_per_dae": fc.get(key, {}).get("flops_per_dae"),
-                "kernel_ms": round(fd_kernel_ms, 5),
-                "assembly": {"kernel": "k_assemble", "ms": round(asm_ms, 5),
-                             "achieved_GBs": round(8 * (nlp.n + (ie - ib) * nzi) / (asm_ms * 1e-3) / 1e9, 2),
-                             "peak_GBs": HBM_PEAK_GBS}}
+        be_name, f_dae, mhash = nlp.backend()
+        work = nlp.work()                     # executed FP64 ops of the (pruned) task kernels
+        flops = n_dae * f_dae                 # algorithmic: one full DAE per FD lane
+        achieved = flops / (dae_ms * 1e-3) / 1e12
+        nnz_local = (ie - ib) * nzi
+        alg_bytes_jac = 8 * (nlp.n + nnz_local)
+        pmc, pmc_src = latest_pmc()
+        traffic = None
+        if pmc:
+            kb = pmc.get("kernels", {})
+            dae_b = [kb.get(k, {}).get("hbm_bytes") for k in ("k_groups", "k_combine")]
+            if all(b is not None for b in dae_b) and pmc.get("workload") == f"N={N},fd={args.fd}":
+                traffic = sum(dae_b)
+        roof = {"bound": "mfma", "achieved": round(achieved, 4), "peak": FP64_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 5),
+                "traffic": traffic,
+                "kernel": "DAE stage of eval_jac_g = k_groups + k_combine (FP64 VALU; MI355X FP64 "
+                          "vector peak = FP64 matrix peak); 'mfma' names the compute roof",
+                "kernel_ms": round(dae_ms, 5), "k_groups_ms": round(groups_ms, 5),
+                "k_combine_ms": round(dae_ms - groups_ms, 5),
+                "algorithmic_flops_per_launch": flops, "dae_evals_per_launch": n_dae,
+                "flops_per_dae": f_dae, "executed_flops_per_launch": float(work[0]),
+                "executed_TFLOPs": round(float(work[0]) / (dae_ms * 1e-3) / 1e12, 4),
+                "backend": be_name, "model_hash": f"0x{mhash:016x}",
+                "traffic_source": pmc_src if traffic is not None else None,
+                "assembly": {"kernel": "k_transcribe", "ms": round(asm_ms, 5),
+                             "algorithmic_bytes": alg_bytes_jac,
+                             "achieved_GBs": round(alg_bytes_jac / (asm_ms * 1e-3) / 1e9, 2),
+                             "peak_GBs": HBM_PEAK_GBS},
+                "instrumented_ms_per_step": round(1e3 * inst_elapsed / args.steps, 4)}
+        if rec["g"]:
+            Gt = np.array(rec["g"])
+            roof["eval_g_stage_ms"] = [round(float(np.median(Gt[:, i])), 5) for i in range(4)]
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(rep, st.solver.options(), x, args.cpu_baseline_seconds)
@@ -158,13 +196,16 @@ def main():
             "metric": "NLP eval_g+eval_jac_g calls/sec (gait10dof18musc)",
             "value": round(value, 3), "unit": "calls/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-            "scaling": "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "ms_per_step": round(ms_per_step, 5), "higher_is_better": True,
+            "scaling": "strong" if mesh else "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic",
             "config": {"workload": "MocoTrack gait10dof18musc DGF rigid tendon (configs[2])",
                        "mesh_intervals": N, "grid_points": nlp.G, "n": nlp.n, "m": nlp.m,
                        "nnz_jac": nlp.nnz, "transcription": "hermite-simpson",
-                       "fd": args.fd, "parallelism": f"mesh-shard{world}", "mode": args.mode,
-                       "iterate": "bounds-midpoint states, uniform random controls (seed 0)"},
+                       "fd": args.fd, "mode": args.mode,
+                       "parallelism": (f"mesh-shard{world}+rccl-allgather" if mesh
+                                       else f"replicas{world}" if world > 1 else "single"),
+                       "iterate": "bounds-midpoint states, uniform random controls"},
             "roofline": roof,
             "cpu_baseline": cpu,
         }
@@ -193,8 +234,8 @@ def cpu_baseline(rep, opts, x, budget_s):
             break
     ref.close()
     return {"value": round(calls / el, 4), "unit": "calls/s", "cores": threads, "kind": "port",
-            "sample": f"{calls} eval_g+eval_jac_g calls of the same workload in {el:.1f}s "
-                      f"(oracle/oracle.c, OpenMP over grid points)"}
+            "sample": f"{calls} eval_g+eval_jac_g calls of the same workload (N={opts.num_mesh_intervals}) "
+                      f"in {el:.1f}s (oracle/oracle.c, OpenMP over grid points, {threads} threads)"}
 
 
 if __name__ == "__main__":

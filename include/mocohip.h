@@ -341,9 +341,15 @@ int mh_model_hash(const mh_model* model, uint64_t* hash);
  * generic interpreter's op count is not tracked). */
 int mh_get_work(const mh_ctx* ctx, double* work4);
 
-/* Timing of the last evaluation on the context stream (HIP events), in ms:
- * [0] whole call, [1] DAE/FD kernel, [2] assembly kernel. */
-int mh_last_timings(const mh_ctx* ctx, double* ms3);
+/* Stage timing: when on, every evaluation records HIP events between its
+ * stages on the context stream and mh_last_timings reports them.  Off by
+ * default (each event packet adds microseconds to a latency-bound call). */
+int mh_set_timing(mh_ctx* ctx, int on);
+/* Timing of the last evaluation (requires mh_set_timing(ctx, 1)), in ms:
+ * [0] whole call, [1] DAE stage (k_groups + k_combine, or k_eval),
+ * [2] transcription stage (k_transcribe), [3] k_groups alone (= [1] when
+ * the DAE stage is one kernel). */
+int mh_last_timings(const mh_ctx* ctx, double* ms4);
 
 #ifdef __cplusplus
 } /* extern "C" */

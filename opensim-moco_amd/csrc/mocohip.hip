@@ -40,6 +40,8 @@
 
 using namespace mh;
 
+constexpr size_t kMaxLds = 160 * 1024;   // gfx950 LDS per workgroup
+
 // ------------------------------------------------------------------------
 // error handling
 // ------------------------------------------------------------------------
@@ -247,7 +249,7 @@ __device__ __forceinline__ LaneIn<D> lane_input(const Src& S, const Lanes& Ln, i
 
 // Device task tables (built on the host per lane configuration).
 struct Tasks {
-    int ng, stride, nslot, nmass, nk;
+    int ng, stride, tdoubles, nmass, nk;   // tdoubles: T doubles per grid point
     const int* dlen;     // [ng] tasks per grid point of group g
     const int* off;      // [ng] slot offset of force group g within a grid point
     const int* roles;    // [ng][stride] j -> lane role
@@ -298,9 +300,12 @@ __global__ void __launch_bounds__(64) k_groups(DevModel M, Src S, Lanes Ln, Task
 #pragma unroll
         for (int f = 0; f < D::NST; ++f) dst[f] = out[f];
     } else {
-        double* dst = T + ((long)kl * TK.nslot + TK.off[g] + j) * D::NF;
+        // compact slab: group g's slots hold exactly its GROUP_NF[g] fields
+        const int nf = D::GROUP_NF[g];
+        double* dst = T + (long)kl * TK.tdoubles + TK.off[g] + j * nf;
 #pragma unroll
-        for (int f = 0; f < D::NF; ++f) dst[f] = out[f];
+        for (int f = 0; f < D::NF; ++f)
+            if (f < nf) dst[f] = out[f];
     }
 #ifdef MH_TASK_TIMING
     if (lane == 0 && blockIdx.x < TIMING_SLOTS) {
@@ -322,7 +327,7 @@ struct TaskLoadLds {
     const int* __restrict__ slot;   // [stride][ng]: slot of group g for this role
     int r;
     __device__ __forceinline__ double operator()(int g, int f) const {
-        return sT[slot[r * D::NG + g] * D::NF + f];
+        return sT[slot[r * D::NG + g] + f];
     }
     __device__ __forceinline__ double h(int f) const {
         return sH[slot[r * D::NG] * D::NST + f];
@@ -339,7 +344,7 @@ struct TaskLoadGlobal {
     const int* __restrict__ slot;
     int r;
     __device__ __forceinline__ double operator()(int g, int f) const {
-        return sT[slot[r * D::NG + g] * D::NF + f];
+        return sT[slot[r * D::NG + g] + f];
     }
     __device__ __forceinline__ double h(int f) const {
         return sH[slot[r * D::NG] * D::NST + f];
@@ -357,7 +362,7 @@ __global__ void __launch_bounds__(64) k_combine_global(DevModel M, Src S, Lanes 
     double t;
     const LaneIn<D> in = lane_input<D>(S, Ln, kl, r, t);
     if (r == Ln.base && times) times[kl] = t;
-    const TaskLoadGlobal<D> TL{T + (long)kl * TK.nslot * D::NF, H + (long)kl * TK.nmass * D::NST,
+    const TaskLoadGlobal<D> TL{T + (long)kl * TK.tdoubles, H + (long)kl * TK.nmass * D::NST,
                                TK.jd, r};
     double out[D::NO];
     D::combine(M, t, in, TL, out);
@@ -386,13 +391,19 @@ __device__ __forceinline__ void stage_lds(double* __restrict__ dst, const double
     }
 }
 
+// With quot != 0 (Jacobian lanes) the kernel writes, per output o, the
+// finite-difference quotient of direction r into Y slot r instead of the raw
+// lane value (CasADi FiniteDiff formulas (f+ - f-)/2h, (f+ - f0)/h,
+// (f0 - f-)/h; the base slot keeps the raw base value): one division per
+// (grid point, output, direction) instead of one per Jacobian nonzero that
+// reads it.  The lanes exchange their raw values through LDS.
 template <class D>
 __global__ void __launch_bounds__(1024) k_combine(DevModel M, Src S, Lanes Ln, Tasks TK,
         const double* __restrict__ T, const double* __restrict__ H, double* __restrict__ times,
-        double* __restrict__ Y, long ystride_pt) {
+        double* __restrict__ Y, long ystride_pt, int quot) {
     extern __shared__ double smem[];
     const int kl = blockIdx.x;
-    const int nt = TK.nslot * D::NF, nh = TK.nmass * D::NST;
+    const int nt = TK.tdoubles, nh = TK.nmass * D::NST;
     double* sT = smem;
     double* sH = smem + nt;
     const double* Tk = T + (long)kl * nt;
@@ -401,18 +412,43 @@ __global__ void __launch_bounds__(1024) k_combine(DevModel M, Src S, Lanes Ln, T
     if (nh > 0) stage_lds<8>(sH, Hk, nh);
     __syncthreads();
     const int r = threadIdx.x;
-    if (r >= Ln.stride) return;
-    double t;
-    const LaneIn<D> in = lane_input<D>(S, Ln, kl, r, t);
-    if (r == Ln.base && times) times[kl] = t;
-    const TaskLoadLds<D> TL{sT, sH, TK.jd, r};
+    const bool act = r < Ln.stride;
     double out[D::NO];
-    D::combine(M, t, in, TL, out);
+    if (act) {
+        double t;
+        const LaneIn<D> in = lane_input<D>(S, Ln, kl, r, t);
+        if (r == Ln.base && times) times[kl] = t;
+        const TaskLoadLds<D> TL{sT, sH, TK.jd, r};
+        D::combine(M, t, in, TL, out);
+    }
     // Y[(kl*NO + o)*stride + r]  (ystride_pt = NO*stride; explicit points:
     // stride 1 -> out[p*NO + o])
     double* Yk = Y + (long)kl * ystride_pt + r;
+    if (!quot) {
+        if (act) {
 #pragma unroll
-    for (int o = 0; o < D::NO; ++o) Yk[(long)o * Ln.stride] = out[o];
+            for (int o = 0; o < D::NO; ++o) Yk[(long)o * Ln.stride] = out[o];
+        }
+        return;
+    }
+    __syncthreads();                 // every lane is done reading sT / sH
+    double* sY = smem;               // [NO][stride] raw lane values
+    if (act) {
+#pragma unroll
+        for (int o = 0; o < D::NO; ++o) sY[o * Ln.stride + r] = out[o];
+    }
+    __syncthreads();
+    if (!act) return;
+#pragma unroll
+    for (int o = 0; o < D::NO; ++o) {
+        const double* y = sY + o * Ln.stride;
+        double v;
+        if (r == Ln.base) v = out[o];
+        else if (Ln.fd == MH_FD_CENTRAL) v = r < Ln.ND ? (out[o] - y[Ln.ND + r]) / (2.0 * Ln.h) : 0.0;
+        else if (Ln.fd == MH_FD_FORWARD) v = (out[o] - y[Ln.base]) / Ln.h;
+        else v = (y[Ln.base] - out[o]) / Ln.h;
+        Yk[(long)o * Ln.stride] = v;
+    }
 }
 
 struct Interval {
@@ -427,64 +463,81 @@ __device__ __forceinline__ int grid_of(const Interval& I, int i, int pt) {
     return I.scheme == MH_HERMITE_SIMPSON ? 2 * i + pt : i + pt;
 }
 
-// xdot[s] at local grid point kl (global k).
+// Raw DAE outputs of a grid point's lanes and the grid point's time, as
+// read by the transcription arithmetic.  YG: Y and the base-lane times in
+// HBM (written by k_combine, indexed by local grid point k - k0).  YS: the
+// same values staged in LDS by k_interval for the interval's own points
+// (indexed by k - kf, kf = the interval's first grid point).
+struct YG {
+    const double* __restrict__ Y;
+    const double* __restrict__ times;
+    int NO, stride, k0;
+    int q;   // Y holds finite-difference quotients (k_combine quot mode)
+    __device__ __forceinline__ const double* row(int k, int o) const {
+        return Y + ((long)(k - k0) * NO + o) * stride;
+    }
+    __device__ __forceinline__ double t(int k) const { return times[k - k0]; }
+};
+struct YS {
+    const double* Y;
+    const double* times;
+    int NO, stride, kf;
+    int q;
+    __device__ __forceinline__ const double* row(int k, int o) const {
+        return Y + ((k - kf) * NO + o) * stride;
+    }
+    __device__ __forceinline__ double t(int k) const { return times[k - kf]; }
+};
+
+// xdot[s] at grid point k.
+template <class YV>
 __device__ __forceinline__ double xdot_at(const Layout& L, const Lanes& Ln,
-        const double* __restrict__ x, const double* __restrict__ Y, int k, int kl, int s) {
+        const double* __restrict__ x, const YV& Y, int k, int s) {
     if (s < L.NQ) return x[2 + (long)k * L.NS + L.NQ + s];
-    return Y[((long)kl * L.NO + (s - L.NQ)) * Ln.stride + Ln.base];
+    return Y.row(k, s - L.NQ)[Ln.base];
 }
 
-__device__ __forceinline__ void defects_block(const Layout& L, const Interval& I, const Lanes& Ln,
-        const double* __restrict__ x, const double* __restrict__ times,
-        const double* __restrict__ Y, double* __restrict__ g, int il) {
-    const int i = I.ib + il;
+template <class YV>
+__device__ __forceinline__ double defect_row(const Layout& L, const Interval& I, const Lanes& Ln,
+        const double* __restrict__ x, const YV& Y, int i, int r) {
     const int NS = L.NS;
-    double* gi = g + (long)il * I.rpi;
     if (I.scheme == MH_HERMITE_SIMPSON) {
         const int ki = 2 * i, km = ki + 1, kp = ki + 2;
-        const int kli = ki - L.k0, klm = km - L.k0, klp = kp - L.k0;
-        const double h = times[klp] - times[kli];
-        for (int r = threadIdx.x; r < I.rpi; r += blockDim.x) {
-            double v;
-            if (r < NS) {
-                const int s = r;
-                const double xi = x[2 + (long)ki * NS + s], xm = x[2 + (long)km * NS + s],
-                             xp = x[2 + (long)kp * NS + s];
-                const double fi = xdot_at(L, Ln, x, Y, ki, kli, s), fp = xdot_at(L, Ln, x, Y, kp, klp, s);
-                v = xm - 0.5 * (xp + xi) - (h / 8.0) * (fi - fp);
-            } else if (r < 2 * NS) {
-                const int s = r - NS;
-                const double xi = x[2 + (long)ki * NS + s], xp = x[2 + (long)kp * NS + s];
-                const double fi = xdot_at(L, Ln, x, Y, ki, kli, s),
-                             fm = xdot_at(L, Ln, x, Y, km, klm, s),
-                             fp = xdot_at(L, Ln, x, Y, kp, klp, s);
-                v = xp - xi - (h / 6.0) * (fp + 4.0 * fm + fi);
-            } else {
-                const int j = r - 2 * NS;
-                const double* xc = x + 2 + (long)NS * L.G;
-                v = xc[(long)km * L.NC + j] - 0.5 * (xc[(long)kp * L.NC + j] + xc[(long)ki * L.NC + j]);
-            }
-            gi[r] = v;
-        }
-    } else {
-        const int ki = i, kp = i + 1;
-        const int kli = ki - L.k0, klp = kp - L.k0;
-        const double h = times[klp] - times[kli];
-        for (int r = threadIdx.x; r < I.rpi; r += blockDim.x) {
+        const double h = Y.t(kp) - Y.t(ki);
+        if (r < NS) {
             const int s = r;
-            const double xi = x[2 + (long)ki * NS + s], xp = x[2 + (long)kp * NS + s];
-            const double fi = xdot_at(L, Ln, x, Y, ki, kli, s), fp = xdot_at(L, Ln, x, Y, kp, klp, s);
-            gi[r] = xp - (xi + 0.5 * h * (fp + fi));
+            const double xi = x[2 + (long)ki * NS + s], xm = x[2 + (long)km * NS + s],
+                         xp = x[2 + (long)kp * NS + s];
+            const double fi = xdot_at(L, Ln, x, Y, ki, s), fp = xdot_at(L, Ln, x, Y, kp, s);
+            return xm - 0.5 * (xp + xi) - (h / 8.0) * (fi - fp);
         }
+        if (r < 2 * NS) {
+            const int s = r - NS;
+            const double xi = x[2 + (long)ki * NS + s], xp = x[2 + (long)kp * NS + s];
+            const double fi = xdot_at(L, Ln, x, Y, ki, s), fm = xdot_at(L, Ln, x, Y, km, s),
+                         fp = xdot_at(L, Ln, x, Y, kp, s);
+            return xp - xi - (h / 6.0) * (fp + 4.0 * fm + fi);
+        }
+        const int j = r - 2 * NS;
+        const double* xc = x + 2 + (long)NS * L.G;
+        return xc[(long)km * L.NC + j] - 0.5 * (xc[(long)kp * L.NC + j] + xc[(long)ki * L.NC + j]);
     }
+    const int ki = i, kp = i + 1;
+    const double h = Y.t(kp) - Y.t(ki);
+    const int s = r;
+    const double xi = x[2 + (long)ki * NS + s], xp = x[2 + (long)kp * NS + s];
+    const double fi = xdot_at(L, Ln, x, Y, ki, s), fp = xdot_at(L, Ln, x, Y, kp, s);
+    return xp - (xi + 0.5 * h * (fp + fi));
 }
 
-// d xdot[s] / d dir at local grid point kl from the raw lane outputs
+// d xdot[s] / d dir at grid point k from the raw lane outputs
 // (CasADi FiniteDiff formulas: (f+ - f-)/2h, (f+ - f0)/h, (f0 - f-)/h).
-__device__ __forceinline__ double dxdot(const Layout& L, const Lanes& Ln,
-        const double* __restrict__ Y, int kl, int s, int dir) {
+template <class YV>
+__device__ __forceinline__ double dxdot(const Layout& L, const Lanes& Ln, const YV& Y, int k, int s,
+        int dir) {
     if (s < L.NQ) return dir == 2 + L.NQ + s ? 1.0 : 0.0;
-    const double* y = Y + ((long)kl * L.NO + (s - L.NQ)) * Ln.stride;
+    const double* y = Y.row(k, s - L.NQ);
+    if (Y.q) return y[dir];
     if (Ln.fd == MH_FD_CENTRAL) return (y[dir] - y[Ln.ND + dir]) / (2.0 * Ln.h);
     if (Ln.fd == MH_FD_FORWARD) return (y[dir] - y[Ln.base]) / Ln.h;
     return (y[Ln.base] - y[dir]) / Ln.h;
@@ -492,95 +545,215 @@ __device__ __forceinline__ double dxdot(const Layout& L, const Lanes& Ln,
 
 constexpr int ASM_CHUNK = 1024;   // nonzeros per assembly workgroup
 
-__device__ __forceinline__ void assemble_chunk(const Layout& L, const Interval& I, const Lanes& Ln,
-        const TplEntry* __restrict__ tpl, const double* __restrict__ x,
-        const double* __restrict__ grid, const double* __restrict__ times,
-        const double* __restrict__ Y, double* __restrict__ values, int il, int chunk) {
-    const int i = I.ib + il;
-    const int k_first = grid_of(I, i, 0);
-    const int npts = I.scheme == MH_HERMITE_SIMPSON ? 3 : 2;
-    const int k_last = k_first + npts - 1;
-    const double h = times[k_last - L.k0] - times[k_first - L.k0];
-    const double dgap = grid[k_last] - grid[k_first];
-    double* vi = values + (long)il * I.nnz_int;
-    const int e_end = min(I.nnz_int, (chunk + 1) * ASM_CHUNK);
-    for (int e = chunk * ASM_CHUNK + threadIdx.x; e < e_end; e += blockDim.x) {
-        const TplEntry T = tpl[e];
-        const int s = T.s, dir = T.dir;
-        double v = 0.0;
-        switch (T.kind) {
-        case T_HERM_T: {
-            const int ki = k_first, kp = k_first + 2;
-            const double dh = dir == 0 ? -dgap : dgap;
-            const double fi = xdot_at(L, Ln, x, Y, ki, ki - L.k0, s), fp = xdot_at(L, Ln, x, Y, kp, kp - L.k0, s);
-            v = -(dh / 8.0) * (fi - fp) -
-                (h / 8.0) * (dxdot(L, Ln, Y, ki - L.k0, s, dir) - dxdot(L, Ln, Y, kp - L.k0, s, dir));
-            break;
-        }
-        case T_SIMP_T: {
-            const int ki = k_first, km = k_first + 1, kp = k_first + 2;
-            const double dh = dir == 0 ? -dgap : dgap;
-            const double fi = xdot_at(L, Ln, x, Y, ki, ki - L.k0, s),
-                         fm = xdot_at(L, Ln, x, Y, km, km - L.k0, s),
-                         fp = xdot_at(L, Ln, x, Y, kp, kp - L.k0, s);
-            v = -(dh / 6.0) * (fp + 4.0 * fm + fi) -
-                (h / 6.0) * (dxdot(L, Ln, Y, kp - L.k0, s, dir) + 4.0 * dxdot(L, Ln, Y, km - L.k0, s, dir) +
-                             dxdot(L, Ln, Y, ki - L.k0, s, dir));
-            break;
-        }
-        case T_HERM_X: {
-            const int k = k_first + T.pt;
-            const bool ident = dir == 2 + s;
-            if (T.pt == 1) { v = ident ? 1.0 : 0.0; break; }
-            if (ident) v += -0.5;
-            const double dv = dxdot(L, Ln, Y, k - L.k0, s, dir);
-            v += (T.pt == 0 ? -(h / 8.0) : (h / 8.0)) * dv;
-            break;
-        }
-        case T_SIMP_X: {
-            const int k = k_first + T.pt;
-            const bool ident = dir == 2 + s;
-            const double dv = dxdot(L, Ln, Y, k - L.k0, s, dir);
-            if (T.pt == 2) { if (ident) v += 1.0; v += -(h / 6.0) * dv; }
-            else if (T.pt == 0) { if (ident) v += -1.0; v += -(h / 6.0) * dv; }
-            else v += -(h / 6.0) * 4.0 * dv;
-            break;
-        }
-        case T_INTERP:
-            v = T.pt == 1 ? 1.0 : -0.5;
-            break;
-        case T_TRAP_T: {
-            const int ki = k_first, kp = k_first + 1;
-            const double dh = dir == 0 ? -dgap : dgap;
-            const double fi = xdot_at(L, Ln, x, Y, ki, ki - L.k0, s), fp = xdot_at(L, Ln, x, Y, kp, kp - L.k0, s);
-            v = -0.5 * dh * (fp + fi) -
-                0.5 * h * (dxdot(L, Ln, Y, kp - L.k0, s, dir) + dxdot(L, Ln, Y, ki - L.k0, s, dir));
-            break;
-        }
-        case T_TRAP_X: {
-            const int k = k_first + T.pt;
-            const bool ident = dir == 2 + s;
-            const double dv = dxdot(L, Ln, Y, k - L.k0, s, dir);
-            if (T.pt == 1) { if (ident) v += 1.0; v += -0.5 * h * dv; }
-            else { if (ident) v += -1.0; v += -0.5 * h * dv; }
-            break;
-        }
-        }
-        vi[e] = v;
-    }
+// Per-interval constants of the Jacobian formulas (computed once per
+// interval; exactly the subexpressions the formulas would form per entry).
+struct IvC { double h8, h6, hh, g8, g6, gh; };
+__device__ __forceinline__ IvC iv_const(double h, double dgap) {
+    return IvC{h / 8.0, h / 6.0, 0.5 * h, dgap / 8.0, dgap / 6.0, 0.5 * dgap};
 }
 
-// Transcription stage, one launch: blockIdx.y = mesh interval; blockIdx.x <
-// nchunks streams Jacobian nonzeros (values != null), the last x-block (when
-// g != null) writes the interval's defect / interpolation rows.
+// Jacobian value of template entry T of the interval whose first grid point
+// is k_first (HS: d/d[t0,tf] of -(h/8)(f_i - f_p) with dh/dt0 = -dgap,
+// dh/dtf = dgap, etc.).
+template <class YV>
+__device__ __forceinline__ double jac_entry(const Layout& L, const Lanes& Ln,
+        const double* __restrict__ x, const YV& Y, const TplEntry T, int k_first, const IvC& C) {
+    const int s = T.s, dir = T.dir;
+    double v = 0.0;
+    switch (T.kind) {
+    case T_HERM_T: {
+        const int ki = k_first, kp = k_first + 2;
+        const double fi = xdot_at(L, Ln, x, Y, ki, s), fp = xdot_at(L, Ln, x, Y, kp, s);
+        v = (dir == 0 ? C.g8 : -C.g8) * (fi - fp) -
+            C.h8 * (dxdot(L, Ln, Y, ki, s, dir) - dxdot(L, Ln, Y, kp, s, dir));
+        break;
+    }
+    case T_SIMP_T: {
+        const int ki = k_first, km = k_first + 1, kp = k_first + 2;
+        const double fi = xdot_at(L, Ln, x, Y, ki, s), fm = xdot_at(L, Ln, x, Y, km, s),
+                     fp = xdot_at(L, Ln, x, Y, kp, s);
+        v = (dir == 0 ? C.g6 : -C.g6) * (fp + 4.0 * fm + fi) -
+            C.h6 * (dxdot(L, Ln, Y, kp, s, dir) + 4.0 * dxdot(L, Ln, Y, km, s, dir) +
+                    dxdot(L, Ln, Y, ki, s, dir));
+        break;
+    }
+    case T_HERM_X: {
+        const int k = k_first + T.pt;
+        const bool ident = dir == 2 + s;
+        if (T.pt == 1) { v = ident ? 1.0 : 0.0; break; }
+        if (ident) v += -0.5;
+        const double dv = dxdot(L, Ln, Y, k, s, dir);
+        v += (T.pt == 0 ? -C.h8 : C.h8) * dv;
+        break;
+    }
+    case T_SIMP_X: {
+        const int k = k_first + T.pt;
+        const bool ident = dir == 2 + s;
+        const double dv = dxdot(L, Ln, Y, k, s, dir);
+        if (T.pt == 2) { if (ident) v += 1.0; v += -C.h6 * dv; }
+        else if (T.pt == 0) { if (ident) v += -1.0; v += -C.h6 * dv; }
+        else v += -C.h6 * 4.0 * dv;
+        break;
+    }
+    case T_INTERP:
+        v = T.pt == 1 ? 1.0 : -0.5;
+        break;
+    case T_TRAP_T: {
+        const int ki = k_first, kp = k_first + 1;
+        const double fi = xdot_at(L, Ln, x, Y, ki, s), fp = xdot_at(L, Ln, x, Y, kp, s);
+        v = (dir == 0 ? C.gh : -C.gh) * (fp + fi) -
+            C.hh * (dxdot(L, Ln, Y, kp, s, dir) + dxdot(L, Ln, Y, ki, s, dir));
+        break;
+    }
+    case T_TRAP_X: {
+        const int k = k_first + T.pt;
+        const bool ident = dir == 2 + s;
+        const double dv = dxdot(L, Ln, Y, k, s, dir);
+        if (T.pt == 1) { if (ident) v += 1.0; v += -C.hh * dv; }
+        else { if (ident) v += -1.0; v += -C.hh * dv; }
+        break;
+    }
+    }
+    return v;
+}
+
+__device__ __forceinline__ void interval_span(const Interval& I, int i, int& k_first, int& k_last) {
+    k_first = grid_of(I, i, 0);
+    k_last = k_first + (I.scheme == MH_HERMITE_SIMPSON ? 2 : 1);
+}
+
+// Transcription stage of the split path, one launch: blockIdx.y = mesh
+// interval; blockIdx.x < nchunks streams Jacobian nonzeros (values != null),
+// the last x-block (when g != null) writes the interval's defect /
+// interpolation rows.
 __global__ void __launch_bounds__(256) k_transcribe(Layout L, Interval I, Lanes Ln,
         const TplEntry* __restrict__ tpl, const double* __restrict__ x,
         const double* __restrict__ grid, const double* __restrict__ times,
         const double* __restrict__ Y, double* __restrict__ g, double* __restrict__ values,
-        int nchunks) {
+        int nchunks, int yq) {
     const int il = blockIdx.y;
-    if ((int)blockIdx.x < nchunks) assemble_chunk(L, I, Ln, tpl, x, grid, times, Y, values, il, blockIdx.x);
-    else defects_block(L, I, Ln, x, times, Y, g, il);
+    const int i = I.ib + il;
+    const YG YV{Y, times, L.NO, Ln.stride, L.k0, yq};
+    if ((int)blockIdx.x < nchunks) {
+        int k_first, k_last;
+        interval_span(I, i, k_first, k_last);
+        const IvC C = iv_const(YV.t(k_last) - YV.t(k_first), grid[k_last] - grid[k_first]);
+        double* vi = values + (long)il * I.nnz_int;
+        const int e_end = min(I.nnz_int, ((int)blockIdx.x + 1) * ASM_CHUNK);
+        for (int e = (int)blockIdx.x * ASM_CHUNK + threadIdx.x; e < e_end; e += blockDim.x)
+            vi[e] = jac_entry(L, Ln, x, YV, tpl[e], k_first, C);
+    } else {
+        double* gi = g + (long)il * I.rpi;
+        for (int r = threadIdx.x; r < I.rpi; r += blockDim.x) gi[r] = defect_row(L, I, Ln, x, YV, i, r);
+    }
+}
+
+// Transcription stage of the split path as a grid-stride loop over the
+// shard's (interval, nonzero) and (interval, row) pairs: a few long-lived
+// waves per SIMD instead of thousands of short workgroups (whose dispatch,
+// not their memory traffic, bounded the chunked form).
+__device__ __forceinline__ int div_exact(int w, int n, double inv) {
+    int q = (int)((double)w * inv);
+    q += (q + 1) * n <= w ? 1 : 0;
+    q -= q * n > w ? 1 : 0;
+    return q;
+}
+__global__ void __launch_bounds__(256) k_transcribe_gs(Layout L, Interval I, Lanes Ln,
+        const TplEntry* __restrict__ tpl, const double* __restrict__ x,
+        const double* __restrict__ grid, const double* __restrict__ times,
+        const double* __restrict__ Y, double* __restrict__ g, double* __restrict__ values,
+        int nint, int yq) {
+    const YG YV{Y, times, L.NO, Ln.stride, L.k0, yq};
+    const int nthreads = gridDim.x * blockDim.x;
+    const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (values) {
+        const int total = nint * I.nnz_int;
+        const double inv = 1.0 / I.nnz_int;
+        for (int w = tid; w < total; w += nthreads) {
+            const int il = div_exact(w, I.nnz_int, inv);
+            const int e = w - il * I.nnz_int;
+            const int i = I.ib + il;
+            int k_first, k_last;
+            interval_span(I, i, k_first, k_last);
+            const IvC C = iv_const(YV.t(k_last) - YV.t(k_first), grid[k_last] - grid[k_first]);
+            values[w] = jac_entry(L, Ln, x, YV, tpl[e], k_first, C);
+        }
+    }
+    if (g) {
+        const int total = nint * I.rpi;
+        const double inv = 1.0 / I.rpi;
+        for (int w = tid; w < total; w += nthreads) {
+            const int il = div_exact(w, I.rpi, inv);
+            g[w] = defect_row(L, I, Ln, x, YV, I.ib + il, w - il * I.rpi);
+        }
+    }
+}
+
+// Fused combine + transcription: one workgroup per mesh interval.  The
+// group results (T, H) of the interval's 2-3 grid points are staged in LDS
+// together, every (grid point, lane role) is combined in parallel into
+// LDS-resident raw outputs, and the whole workgroup then writes the
+// interval's g rows and Jacobian values from LDS.  Same arithmetic as
+// k_combine + k_transcribe (bit-identical results) with Y never touching
+// HBM and one kernel less per evaluation.  Launched when the LDS budget
+// allows (interval_lds), otherwise the split path runs.
+constexpr int IV_UNROLL = 4;
+template <class D>
+__global__ void __launch_bounds__(1024) k_interval(DevModel M, Src S, Lanes Ln, Tasks TK, Layout L,
+        Interval I, const TplEntry* __restrict__ tpl, const double* __restrict__ T,
+        const double* __restrict__ H, double* __restrict__ g, double* __restrict__ values) {
+    extern __shared__ double smem[];
+    const int il = blockIdx.x;
+    const int i = I.ib + il;
+    int k_first, k_last;
+    interval_span(I, i, k_first, k_last);
+    const int npts = k_last - k_first + 1;
+    const int nt = TK.tdoubles, nh = TK.nmass * D::NST;
+    const int ny = D::NO * Ln.stride;
+    double* sY = smem;                       // [npts][NO][stride]
+    double* sTimes = sY + npts * ny;         // [npts]
+    double* sT = sTimes + 4;                 // [npts][nt]
+    double* sH = sT + npts * nt;             // [npts][nh]
+    // the interval's points are consecutive local grid points: their T (and
+    // H) slabs are one contiguous run each
+    const int kl0 = k_first - S.k0;
+    if (nt > 0) stage_lds<16>(sT, T + (long)kl0 * nt, npts * nt);
+    if (nh > 0) stage_lds<8>(sH, H + (long)kl0 * nh, npts * nh);
+    __syncthreads();
+    for (int w = threadIdx.x; w < npts * Ln.stride; w += blockDim.x) {
+        const int p = w / Ln.stride, r = w - p * Ln.stride;
+        double t;
+        const LaneIn<D> in = lane_input<D>(S, Ln, kl0 + p, r, t);
+        if (r == Ln.base) sTimes[p] = t;
+        const TaskLoadLds<D> TL{sT + p * nt, sH + p * nh, TK.jd, r};
+        double out[D::NO];
+        D::combine(M, t, in, TL, out);
+        double* Yp = sY + p * ny + r;
+#pragma unroll
+        for (int o = 0; o < D::NO; ++o) Yp[o * Ln.stride] = out[o];
+    }
+    __syncthreads();
+    const YS YV{sY, sTimes, D::NO, Ln.stride, k_first, 0};
+    if (g) {
+        double* gi = g + (long)il * I.rpi;
+        for (int r = threadIdx.x; r < I.rpi; r += blockDim.x) gi[r] = defect_row(L, I, Ln, S.x, YV, i, r);
+    }
+    if (values) {
+        const IvC C = iv_const(YV.t(k_last) - YV.t(k_first), S.grid[k_last] - S.grid[k_first]);
+        double* vi = values + (long)il * I.nnz_int;
+        const int B = blockDim.x;
+        int e = threadIdx.x;
+        // template entries for IV_UNROLL iterations are loaded before any is
+        // evaluated (independent loads in flight, then LDS reads + stores)
+        for (; e + (IV_UNROLL - 1) * B < I.nnz_int; e += IV_UNROLL * B) {
+            TplEntry te[IV_UNROLL];
+#pragma unroll
+            for (int u = 0; u < IV_UNROLL; ++u) te[u] = tpl[e + u * B];
+#pragma unroll
+            for (int u = 0; u < IV_UNROLL; ++u) vi[e + u * B] = jac_entry(L, Ln, S.x, YV, te[u], k_first, C);
+        }
+        for (; e < I.nnz_int; e += B) vi[e] = jac_entry(L, Ln, S.x, YV, tpl[e], k_first, C);
+    }
 }
 
 // ---- objective -------------------------------------------------------------
@@ -848,7 +1021,7 @@ struct TaskSet {
 // perturbed lane those that read its perturbed input (or the time, for the
 // t0/tf directions).  MOCOHIP_TASKS=all disables the pruning (every group
 // for every lane; the reference for the bit-identity test).
-static void build_taskset(const TaskInfo& ti, const Lanes& ln, int nk, TaskSet& ts) {
+static void build_taskset(const TaskInfo& ti, const Lanes& ln, int nk, int nsimd, TaskSet& ts) {
     const char* env = std::getenv("MOCOHIP_TASKS");
     const bool all = env && std::strcmp(env, "all") == 0;
     const int ng = ti.ng, S = ln.stride;
@@ -856,7 +1029,7 @@ static void build_taskset(const TaskInfo& ti, const Lanes& ln, int nk, TaskSet& 
     ts.off.assign(ng, 0);
     ts.roles.assign((size_t)ng * S, 0);
     ts.jd.assign((size_t)ng * S, 0);
-    int nslot = 0;
+    int tdoubles = 0;
     for (int g = 0; g < ng; ++g) {
         std::vector<int> D{ln.base};
         for (int r = 0; r < S; ++r) {
@@ -871,15 +1044,18 @@ static void build_taskset(const TaskInfo& ti, const Lanes& ln, int nk, TaskSet& 
             if (hit || all) D.push_back(r);
         }
         ts.dlen[g] = (int)D.size();
+        // g > 0: T slab offset (doubles) of the group's slot j; g = 0: j of
+        // the mass factor
+        const int nf = g > 0 ? ti.group_nf[g] : 1;
+        if (g > 0) ts.off[g] = tdoubles;
+        // roles that do not re-evaluate g read its base-lane slot (j = 0)
+        for (int r = 0; r < S; ++r) ts.jd[(size_t)r * ng + g] = g > 0 ? ts.off[g] : 0;
         for (size_t j = 0; j < D.size(); ++j) {
             ts.roles[(size_t)g * S + j] = D[j];
-            ts.jd[(size_t)D[j] * ng + g] = (int)j;
+            ts.jd[(size_t)D[j] * ng + g] = (g > 0 ? ts.off[g] : 0) + (int)j * nf;
         }
-        if (g > 0) { ts.off[g] = nslot; nslot += (int)D.size(); }
+        if (g > 0) tdoubles += (int)D.size() * nf;
     }
-    // the combine reads slot = off[g] + j directly (g = 0: j of the mass factor)
-    for (int r = 0; r < S; ++r)
-        for (int g = 1; g < ng; ++g) ts.jd[(size_t)r * ng + g] += ts.off[g];
     // expensive groups first so they start before the cheap ones fill in
     std::vector<int> order(ng);
     for (int g = 0; g < ng; ++g) order[g] = g;
@@ -903,12 +1079,22 @@ static void build_taskset(const TaskInfo& ti, const Lanes& ln, int nk, TaskSet& 
     }
     ts.flops += (double)nk * S * ti.combine_flops;
     ts.nblocks = (int)(ts.blk.size() / 4);
+    // When the launch fits in two waves per SIMD, blocks p and p + nsimd
+    // share a SIMD: order the second round ascending so the heaviest block
+    // shares its SIMD with the lightest (MOCOHIP_ORDER=desc keeps plain
+    // longest-first order).
+    const char* eo = std::getenv("MOCOHIP_ORDER");
+    const bool pair = !(eo && std::strcmp(eo, "desc") == 0);
+    if (pair && ts.nblocks > nsimd && ts.nblocks <= 2 * nsimd) {
+        for (int a = nsimd, b = ts.nblocks - 1; a < b; ++a, --b)
+            for (int w = 0; w < 4; ++w) std::swap(ts.blk[4 * (size_t)a + w], ts.blk[4 * (size_t)b + w]);
+    }
     ts.dev.ng = ng;
     ts.dev.stride = S;
-    ts.dev.nslot = nslot;
+    ts.dev.tdoubles = tdoubles;
     ts.dev.nmass = ts.dlen[0];
     ts.dev.nk = nk;
-    ts.t_doubles = (size_t)nk * std::max(nslot, 1) * ti.nf;
+    ts.t_doubles = (size_t)nk * std::max(tdoubles, 1);
     ts.h_doubles = (size_t)nk * ts.dlen[0] * ti.nst;
 }
 
@@ -956,7 +1142,7 @@ struct mh_ctx {
     // device
     int device = 0;
     hipStream_t stream = nullptr;
-    hipEvent_t ev[4] = {};
+    hipEvent_t ev[5] = {};         // stage boundaries (+ ev[4] after k_groups)
     char* dmem = nullptr;
     DevModel M{};
     GoalSet GS{};
@@ -964,7 +1150,7 @@ struct mh_ctx {
            *d_Yg = nullptr, *d_g = nullptr, *d_vals = nullptr, *d_C = nullptr, *d_grad = nullptr,
            *d_tpart = nullptr, *d_f = nullptr;
     TplEntry* d_tpl = nullptr;
-    float timings[3] = {0, 0, 0};
+    float timings[4] = {0, 0, 0, 0};
     // task-decomposed back ends
     TaskSet ts_jac, ts_g, ts_probe;
     double *d_T = nullptr, *d_H = nullptr;
@@ -976,6 +1162,15 @@ struct mh_ctx {
     std::vector<GraphEntry> graphs;
     bool use_graphs = false;
     bool spin_wait = false;
+    // per lane configuration (0: eval_g lanes, 1: Jacobian lanes): combine
+    // and transcription fused in k_interval (LDS-resident raw outputs)
+    bool use_interval[2] = {false, false};
+    int nsimd = 1024;              // SIMDs of the device (4 per CU)
+    bool asm_grid_stride = false;  // k_transcribe_gs (MOCOHIP_ASM=gs) instead of k_transcribe
+    bool quot = false;             // k_combine writes FD quotients (MOCOHIP_QUOT=1)
+    int yq[2] = {0, 0};            // per lane configuration: Y of the last evaluation holds quotients
+    bool timing = false;           // stage events for mh_last_timings (mh_set_timing)
+    bool groups_timed = false;     // the last evaluation recorded ev[4]
 };
 
 // Task tables and T/H buffers for an mh_eval_dae call of np points (kept
@@ -984,7 +1179,7 @@ static int probe_tasks(mh_ctx* c, const TaskInfo& ti, const Lanes& ln, int np) {
     if (np == c->probe_np) return MH_OK;
     if (c->probe_mem) { (void)hipFree(c->probe_mem); c->probe_mem = nullptr; }
     c->probe_np = -1;
-    build_taskset(ti, ln, np, c->ts_probe);
+    build_taskset(ti, ln, np, c->nsimd, c->ts_probe);
     Arena A;
     const TaskOffsets to = put_taskset(A, c->ts_probe);
     const size_t oT = A.reserve(sizeof(double) * c->ts_probe.t_doubles);
@@ -1264,6 +1459,7 @@ extern "C" int mh_model_hash(const mh_model* M, uint64_t* hash) {
 
 static const Backend* select_backend(mh_ctx* c, const mh_problem* p);
 static const TaskInfo* backend_tasks(const Backend* b);
+static bool interval_fits(const mh_ctx* c, int mode);
 
 extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out) {
     if (!p || !o || !out) return set_err(MH_ERR_INVALID, "null argument");
@@ -1286,6 +1482,7 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
         return set_err(MH_ERR_HIP, "device %d is %s; this build targets gfx950 only", c->device,
                 prop.gcnArchName);
+    c->nsimd = 4 * prop.multiProcessorCount;
 
     const mh_model& M = p->model;
     // host-derived tables
@@ -1347,8 +1544,8 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     size_t o_T = 0, o_H = 0;
     const TaskInfo* ti = backend_tasks(c->be);
     if (ti) {
-        build_taskset(*ti, c->lanes_jac, c->nk, c->ts_jac);
-        build_taskset(*ti, c->lanes_g, c->nk, c->ts_g);
+        build_taskset(*ti, c->lanes_jac, c->nk, c->nsimd, c->ts_jac);
+        build_taskset(*ti, c->lanes_g, c->nk, c->nsimd, c->ts_g);
         to_jac = put_taskset(A, c->ts_jac);
         to_g = put_taskset(A, c->ts_g);
         o_T = A.reserve(sizeof(double) * std::max(c->ts_jac.t_doubles, c->ts_g.t_doubles));
@@ -1402,6 +1599,18 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
         // MOCOHIP_SPIN=1; no measurable gain on the bench workload)
         const char* es = std::getenv("MOCOHIP_SPIN");
         c->spin_wait = es && std::strcmp(es, "1") == 0;
+        // fused combine + transcription per mesh interval unless the LDS
+        // budget is exceeded (MOCOHIP_INTERVAL=0 forces the split path)
+        const char* ei = std::getenv("MOCOHIP_INTERVAL");
+        const bool allow = !(ei && std::strcmp(ei, "0") == 0);
+        const char* ea = std::getenv("MOCOHIP_ASM");
+        c->asm_grid_stride = ea && std::strcmp(ea, "gs") == 0;
+        const char* ee = std::getenv("MOCOHIP_EVENTS");
+        c->timing = ee && std::strcmp(ee, "1") == 0;
+        const char* eq = std::getenv("MOCOHIP_QUOT");
+        c->quot = eq && std::strcmp(eq, "1") == 0;   // opt-in: measured slower
+        for (int mode = 0; mode < 2; ++mode)
+            c->use_interval[mode] = allow && interval_fits(c.get(), mode);
     }
     for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
     *out = c.release();
@@ -1519,7 +1728,6 @@ extern "C" int mh_get_jac_structure(const mh_ctx* c, int32_t* iRow, int32_t* jCo
 // ------------------------------------------------------------------------
 // Back ends and launchers.
 // ------------------------------------------------------------------------
-constexpr size_t kMaxLds = 160 * 1024;   // gfx950 LDS per workgroup
 
 struct Backend {
     const char* name;
@@ -1531,6 +1739,10 @@ struct Backend {
     void (*probe)(mh_ctx*, int np, const double* in, double* out);
     double flops_per_eval;   // generated back ends: emitted FP64 ops per DAE
     const TaskInfo* tasks;   // task-decomposed back ends (else one lane per DAE)
+    // task back ends: fused combine + transcription (k_interval) for lanes
+    // of mode 0/1 writing g and/or values; null for one-lane back ends
+    void (*interval)(mh_ctx*, const double* x, int mode, double* g, double* v);
+    size_t (*interval_bytes)(const mh_ctx*, int mode);   // its LDS need
 };
 
 template <class D>
@@ -1542,29 +1754,68 @@ static void be_eval_lane(mh_ctx* c, const double* x, int mode, double* Y) {
             ln, x, c->d_grid, c->d_times, Y);
 }
 template <class D>
-static void launch_tasks(mh_ctx* c, const Src& S, const Lanes& ln, const TaskSet& ts, double* T,
-        double* H, double* times, double* Y) {
+// Returns 1 when Y holds finite-difference quotients (k_combine quot mode,
+// Jacobian lanes staged in LDS), 0 when it holds raw lane values.
+static int launch_tasks(mh_ctx* c, const Src& S, const Lanes& ln, const TaskSet& ts, double* T,
+        double* H, double* times, double* Y, bool quot) {
     hipLaunchKernelGGL(k_groups<D>, dim3((unsigned)ts.nblocks), dim3(64), 0, c->stream, c->M, S, ln,
             ts.dev, T, H);
+    if (c->timing && times) (void)hipEventRecord(c->ev[4], c->stream);
     const unsigned threads = (unsigned)((ln.stride + 63) / 64 * 64);
-    const size_t lds = sizeof(double) * ((size_t)ts.dev.nslot * D::NF + (size_t)ts.dev.nmass * D::NST);
+    quot = quot && ln.stride > 1;
+    size_t lds = sizeof(double) * ((size_t)ts.dev.tdoubles + (size_t)ts.dev.nmass * D::NST);
+    if (quot) lds = std::max(lds, sizeof(double) * (size_t)D::NO * ln.stride);
     if (threads <= 1024 && lds <= kMaxLds) {
         if (lds > 65536)
             (void)hipFuncSetAttribute((const void*)k_combine<D>,
                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         hipLaunchKernelGGL(k_combine<D>, dim3((unsigned)ts.dev.nk), dim3(threads), lds, c->stream, c->M,
-                S, ln, ts.dev, T, H, times, Y, (long)D::NO * ln.stride);
+                S, ln, ts.dev, T, H, times, Y, (long)D::NO * ln.stride, quot ? 1 : 0);
+        return quot ? 1 : 0;
     } else {
         const long lanes = (long)ts.dev.nk * ln.stride;
         hipLaunchKernelGGL(k_combine_global<D>, dim3((unsigned)((lanes + 63) / 64)), dim3(64), 0,
                 c->stream, c->M, S, ln, ts.dev, T, H, times, Y, (long)D::NO * ln.stride);
     }
+    return 0;
 }
 template <class D>
 static void be_eval_tasks(mh_ctx* c, const double* x, int mode, double* Y) {
     const Src S{x, c->d_grid, nullptr, c->G, c->k0};
-    launch_tasks<D>(c, S, mode ? c->lanes_jac : c->lanes_g, mode ? c->ts_jac : c->ts_g, c->d_T, c->d_H,
-            c->d_times, Y);
+    const Lanes& ln = mode ? c->lanes_jac : c->lanes_g;
+    const TaskSet& ts = mode ? c->ts_jac : c->ts_g;
+    if (c->use_interval[mode]) {   // combine happens inside k_interval
+        hipLaunchKernelGGL(k_groups<D>, dim3((unsigned)ts.nblocks), dim3(64), 0, c->stream, c->M, S, ln,
+                ts.dev, c->d_T, c->d_H);
+        return;
+    }
+    c->yq[mode] = launch_tasks<D>(c, S, ln, ts, c->d_T, c->d_H, c->d_times, Y, mode == 1 && c->quot);
+}
+// LDS bytes of k_interval for one lane configuration (0: does not apply).
+template <class D>
+static size_t interval_lds(const mh_ctx* c, const Lanes& ln, const TaskSet& ts) {
+    const size_t npts = c->scheme == MH_HERMITE_SIMPSON ? 3 : 2;
+    return sizeof(double) * (npts * D::NO * ln.stride + 4 +
+                             npts * ((size_t)ts.dev.tdoubles + (size_t)ts.dev.nmass * D::NST));
+}
+template <class D>
+static size_t be_interval_bytes(const mh_ctx* c, int mode) {
+    return interval_lds<D>(c, mode ? c->lanes_jac : c->lanes_g, mode ? c->ts_jac : c->ts_g);
+}
+template <class D>
+static void be_interval(mh_ctx* c, const double* x, int mode, double* g, double* v) {
+    const Src S{x, c->d_grid, nullptr, c->G, c->k0};
+    const Lanes& ln = mode ? c->lanes_jac : c->lanes_g;
+    const TaskSet& ts = mode ? c->ts_jac : c->ts_g;
+    const size_t lds = interval_lds<D>(c, ln, ts);
+    if (lds > 65536)
+        (void)hipFuncSetAttribute((const void*)k_interval<D>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                (int)lds);
+    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, c->k0, c->nk};
+    Interval I{c->scheme, c->interp, c->ib, c->rpi, c->nnz_int};
+    const unsigned threads = v ? 1024u : 256u;
+    hipLaunchKernelGGL(k_interval<D>, dim3((unsigned)(c->ie - c->ib)), dim3(threads), lds, c->stream, c->M,
+            S, ln, ts.dev, L, I, c->d_tpl, c->d_T, c->d_H, g, v);
 }
 template <class D>
 static void be_integrand(mh_ctx* c, const double* x) {
@@ -1591,12 +1842,12 @@ static void be_probe_tasks(mh_ctx* c, int np, const double* in, double* out) {
     const Lanes ln{c->fd, c->NI + 2, 1, 0, c->h};
     if (probe_tasks(c, *c->be->tasks, ln, np) != MH_OK) return;
     const Src S{nullptr, nullptr, in, 0, 0};
-    launch_tasks<D>(c, S, ln, c->ts_probe, c->d_pT, c->d_pH, nullptr, out);
+    (void)launch_tasks<D>(c, S, ln, c->ts_probe, c->d_pT, c->d_pH, nullptr, out, false);
 }
 template <class D>
 static constexpr Backend make_backend_lane(const char* name, double flops) {
     return Backend{name, &be_eval_lane<D>, &be_integrand<D>, &be_grad<D>, &be_probe_lane<D>, flops,
-                   nullptr};
+                   nullptr, nullptr, nullptr};
 }
 template <class D>
 struct TaskInfoOf {
@@ -1606,10 +1857,13 @@ struct TaskInfoOf {
 template <class D>
 static constexpr Backend make_backend_tasks(const char* name, double flops) {
     return Backend{name, &be_eval_tasks<D>, &be_integrand<D>, &be_grad<D>, &be_probe_tasks<D>, flops,
-                   &TaskInfoOf<D>::value};
+                   &TaskInfoOf<D>::value, &be_interval<D>, &be_interval_bytes<D>};
 }
 
 static const TaskInfo* backend_tasks(const Backend* b) { return b->tasks; }
+static bool interval_fits(const mh_ctx* c, int mode) {
+    return c->be->interval && c->be->interval_bytes(c, mode) <= kMaxLds;
+}
 
 static const Backend kGeneric[3] = {
     make_backend_lane<GenericDae<SzSmall>>("generic-small", 0.0),
@@ -1647,8 +1901,22 @@ static int launch_stage(mh_ctx* c, int stage, int kind, const double* x, double*
     const int nchunks = kind == 0 ? 0 : (c->nnz_int + ASM_CHUNK - 1) / ASM_CHUNK;
     double* g = kind == 1 ? nullptr : a;
     double* v = kind == 0 ? nullptr : (kind == 1 ? a : b);
-    hipLaunchKernelGGL(k_transcribe, dim3((unsigned)(nchunks + (g ? 1 : 0)), (unsigned)(c->ie - c->ib)),
-            dim3(256), 0, c->stream, L, I, ln, c->d_tpl, x, c->d_grid, c->d_times, Y, g, v, nchunks);
+    if (c->use_interval[kind == 0 ? 0 : 1]) {
+        c->be->interval(c, x, kind == 0 ? 0 : 1, g, v);
+        HIPCHK(hipGetLastError());
+        return MH_OK;
+    }
+    const int nint = c->ie - c->ib;
+    if (c->asm_grid_stride) {
+        const long work = (long)nint * ((v ? c->nnz_int : 0) + (g ? c->rpi : 0));
+        const unsigned blocks = (unsigned)std::max(1L, std::min((long)c->nsimd, (work + 255) / 256));
+        hipLaunchKernelGGL(k_transcribe_gs, dim3(blocks), dim3(256), 0, c->stream, L, I, ln, c->d_tpl, x,
+                c->d_grid, c->d_times, Y, g, v, nint, c->yq[kind == 0 ? 0 : 1]);
+    } else {
+        hipLaunchKernelGGL(k_transcribe, dim3((unsigned)(nchunks + (g ? 1 : 0)), (unsigned)nint), dim3(256), 0,
+                c->stream, L, I, ln, c->d_tpl, x, c->d_grid, c->d_times, Y, g, v, nchunks,
+                c->yq[kind == 0 ? 0 : 1]);
+    }
     HIPCHK(hipGetLastError());
     return MH_OK;
 }
@@ -1686,18 +1954,28 @@ static int run_stage(mh_ctx* c, int stage, int kind, const double* x, double* a,
     return MH_OK;
 }
 
+// Stage timing (mh_set_timing / MOCOHIP_EVENTS=1): events recorded
+// between the stages on the context stream.  Off by default: each event
+// packet costs several microseconds on a call that is itself tens of
+// microseconds.
 static int run_cached(mh_ctx* c, int kind, const double* x, double* a, double* b) {
-    HIPCHK(hipEventRecord(c->ev[0], c->stream));
+    // ev[4] (after k_groups) is recorded only by the split task path
+    c->groups_timed = c->timing && c->be->tasks && !c->use_interval[kind == 0 ? 0 : 1];
+    if (c->timing) HIPCHK(hipEventRecord(c->ev[0], c->stream));
     int rc = run_stage(c, 0, kind, x, a, b);
     if (rc) return rc;
-    HIPCHK(hipEventRecord(c->ev[1], c->stream));
+    if (c->timing) HIPCHK(hipEventRecord(c->ev[1], c->stream));
     rc = run_stage(c, 1, kind, x, a, b);
     if (rc) return rc;
-    HIPCHK(hipEventRecord(c->ev[2], c->stream));
+    if (c->timing) HIPCHK(hipEventRecord(c->ev[2], c->stream));
     return MH_OK;
 }
 
 static int finish(mh_ctx* c) {
+    if (!c->timing) {
+        HIPCHK(hipStreamSynchronize(c->stream));
+        return MH_OK;
+    }
     HIPCHK(hipEventRecord(c->ev[3], c->stream));
     if (c->spin_wait) {
         // poll instead of a blocking wait: the call is latency-bound and the
@@ -1708,11 +1986,12 @@ static int finish(mh_ctx* c) {
     } else {
         HIPCHK(hipStreamSynchronize(c->stream));
     }
-    float a = 0, b = 0, d = 0;
+    float a = 0, b = 0, d = 0, e = 0;
     (void)hipEventElapsedTime(&a, c->ev[0], c->ev[3]);
     (void)hipEventElapsedTime(&b, c->ev[0], c->ev[1]);
     (void)hipEventElapsedTime(&d, c->ev[1], c->ev[2]);
-    c->timings[0] = a; c->timings[1] = b; c->timings[2] = d;
+    if (c->groups_timed) (void)hipEventElapsedTime(&e, c->ev[0], c->ev[4]);
+    c->timings[0] = a; c->timings[1] = b; c->timings[2] = d; c->timings[3] = c->groups_timed ? e : b;
     return MH_OK;
 }
 
@@ -1780,17 +2059,17 @@ extern "C" int mh_eval_f(mh_ctx* c, const double* x, int, double* f) {
     HIPCHK(hipSetDevice(c->device));
     (void)hipGetLastError();   // report only this call's launch errors
     HIPCHK(hipMemcpyAsync(c->d_x, x, sizeof(double) * c->n, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipEventRecord(c->ev[0], c->stream));
+    if (c->timing) HIPCHK(hipEventRecord(c->ev[0], c->stream));
     Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, 0, c->G};
     if (c->ngoals > 0) {
         c->be->integrand(c, c->d_x);
         HIPCHK(hipGetLastError());
     }
-    HIPCHK(hipEventRecord(c->ev[1], c->stream));
+    if (c->timing) HIPCHK(hipEventRecord(c->ev[1], c->stream));
     hipLaunchKernelGGL(k_reduce_obj, dim3(1), dim3(256), 0, c->stream, L, c->GS, 0, c->d_x, c->d_C,
             c->d_tpart, c->d_f);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(c->ev[2], c->stream));
+    if (c->timing) HIPCHK(hipEventRecord(c->ev[2], c->stream));
     HIPCHK(hipMemcpyAsync(f, c->d_f, sizeof(double), hipMemcpyDeviceToHost, c->stream));
     return finish(c);
 }
@@ -1800,7 +2079,7 @@ extern "C" int mh_eval_grad_f(mh_ctx* c, const double* x, int, double* grad) {
     HIPCHK(hipSetDevice(c->device));
     (void)hipGetLastError();   // report only this call's launch errors
     HIPCHK(hipMemcpyAsync(c->d_x, x, sizeof(double) * c->n, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipEventRecord(c->ev[0], c->stream));
+    if (c->timing) HIPCHK(hipEventRecord(c->ev[0], c->stream));
     Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, 0, c->G};
     HIPCHK(hipMemsetAsync(c->d_grad, 0, sizeof(double) * c->n, c->stream));
     HIPCHK(hipMemsetAsync(c->d_tpart, 0, sizeof(double) * 2 * c->G, c->stream));
@@ -1810,11 +2089,11 @@ extern "C" int mh_eval_grad_f(mh_ctx* c, const double* x, int, double* grad) {
         c->be->grad(c, c->d_x);
         HIPCHK(hipGetLastError());
     }
-    HIPCHK(hipEventRecord(c->ev[1], c->stream));
+    if (c->timing) HIPCHK(hipEventRecord(c->ev[1], c->stream));
     hipLaunchKernelGGL(k_reduce_obj, dim3(1), dim3(256), 0, c->stream, L, c->GS, 1, c->d_x, c->d_C,
             c->d_tpart, c->d_f);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(c->ev[2], c->stream));
+    if (c->timing) HIPCHK(hipEventRecord(c->ev[2], c->stream));
     HIPCHK(hipMemcpyAsync(c->d_grad, c->d_f, sizeof(double) * 2, hipMemcpyDeviceToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(grad, c->d_grad, sizeof(double) * c->n, hipMemcpyDeviceToHost, c->stream));
     return finish(c);
@@ -1848,9 +2127,15 @@ extern "C" int mh_debug_task_timing(long long* out, int nslots) {
 }
 #endif
 
-extern "C" int mh_last_timings(const mh_ctx* c, double* ms3) {
-    if (!c || !ms3) return set_err(MH_ERR_INVALID, "null argument");
-    for (int i = 0; i < 3; ++i) ms3[i] = c->timings[i];
+extern "C" int mh_set_timing(mh_ctx* c, int on) {
+    if (!c) return set_err(MH_ERR_INVALID, "null argument");
+    c->timing = on != 0;
+    return MH_OK;
+}
+
+extern "C" int mh_last_timings(const mh_ctx* c, double* ms4) {
+    if (!c || !ms4) return set_err(MH_ERR_INVALID, "null argument");
+    for (int i = 0; i < 4; ++i) ms4[i] = c->timings[i];
     return MH_OK;
 }
 

@@ -203,8 +203,14 @@ class HipNLP(_NLPBase):
         self._check(self.lib.mh_get_work(self.ctx, abi.dptr(w)))
         return w
 
+    def set_timing(self, on: bool):
+        """Record stage events on every evaluation (mh_set_timing)."""
+        self._check(self.lib.mh_set_timing(self.ctx, int(bool(on))))
+
     def last_timings(self):
-        t = np.zeros(3)
+        """[whole, DAE stage, transcription stage, k_groups] of the last
+        evaluation in ms (needs set_timing(True))."""
+        t = np.zeros(4)
         self._check(self.lib.mh_last_timings(self.ctx, abi.dptr(t)))
         return t
 

@@ -96,21 +96,27 @@ def _row_mask(ref, x):
 BACKENDS = ["auto", "lane", "generic"]
 
 
-def _pair(name, backend="auto", tasks=None):
+def _pair(name, backend="auto", tasks=None, env=None):
     """(GPU NLP, oracle NLP, study).  backend "auto" lets mh_create pick the
     generated model-specialized task kernels when one matches the model hash;
     "lane" the generated one-lane-per-DAE kernel; "generic" forces the device
     interpreter (MOCOHIP_BACKEND).  tasks="all" disables the
-    finite-difference dependency pruning (MOCOHIP_TASKS=all)."""
+    finite-difference dependency pruning (MOCOHIP_TASKS=all).  ``env``
+    selects kernel variants read at mh_create (MOCOHIP_INTERVAL=0: split
+    k_combine + k_transcribe instead of the fused per-interval kernel;
+    MOCOHIP_ASM=gs: grid-stride transcription; MOCOHIP_QUOT=1: k_combine
+    writes finite-difference quotients)."""
     import os
     st = CASES[name]()
     rep = st.problem.create_rep()
     opts = st.solver.options()
-    saved = {k: os.environ.pop(k, None) for k in ("MOCOHIP_BACKEND", "MOCOHIP_TASKS")}
+    saved = {k: os.environ.pop(k, None) for k in ("MOCOHIP_BACKEND", "MOCOHIP_TASKS", "MOCOHIP_INTERVAL",
+                                                  "MOCOHIP_ASM", "MOCOHIP_QUOT")}
     if backend != "auto":
         os.environ["MOCOHIP_BACKEND"] = backend
     if tasks:
         os.environ["MOCOHIP_TASKS"] = tasks
+    os.environ.update(env or {})
     try:
         gpu = HipNLP(rep, opts)
     finally:
@@ -314,6 +320,27 @@ def test_pruned_tasks_bit_identical(name):
         assert np.array_equal(gpu.eval_jac_g(x), full.eval_jac_g(x), equal_nan=True)
     w, wf = gpu.work(), full.work()
     assert w[3] == wf[3] and w[2] < wf[2] and w[0] < wf[0]
+
+
+@pytest.mark.parametrize("name", ["sliding_mass", "double_pendulum_hs", "double_pendulum_trap",
+                                  "gait_rigid_forward", "gait_rigid_central", "gait_rigid_backward",
+                                  "gait_compliant_central", "gait_torque_driven"])
+@pytest.mark.parametrize("variant", [{"MOCOHIP_INTERVAL": "0"},
+                                     {"MOCOHIP_INTERVAL": "0", "MOCOHIP_ASM": "gs"},
+                                     {"MOCOHIP_INTERVAL": "0", "MOCOHIP_QUOT": "1"}])
+def test_kernel_variants_bit_identical(name, variant):
+    """The default k_interval (combine + transcription per mesh interval,
+    raw outputs in LDS) writes exactly what the split path writes through
+    HBM: k_combine + k_transcribe (chunked or grid-stride), with raw lane
+    values or with finite-difference quotients in Y."""
+    gpu, _, _ = _pair(name)
+    split, _, _ = _pair(name, env=variant)
+    for _, x in _iterates(gpu):
+        assert np.array_equal(gpu.eval_g(x), split.eval_g(x), equal_nan=True)
+        assert np.array_equal(gpu.eval_jac_g(x), split.eval_jac_g(x), equal_nan=True)
+        ga, Ja = gpu.eval_g_jac_g(x)
+        gb, Jb = split.eval_g_jac_g(x)
+        assert np.array_equal(ga, gb, equal_nan=True) and np.array_equal(Ja, Jb, equal_nan=True)
 
 
 def test_work_accounting():

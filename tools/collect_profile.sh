@@ -14,5 +14,6 @@ done
 python tools/kstats.py "$P" > "$DEST/summary.txt"
 grep -h '^{' "$P"/*.log > "$DEST/bench_lines_under_profiler.jsonl" || true
 [ -f "gpurun_out/$TAG/bench.json" ] && cp "gpurun_out/$TAG/bench.json" "$DEST/bench.json"
+[ -f "$P/pmc.json" ] && cp "$P/pmc.json" "$DEST/pmc.json"
 [ -f "gpurun_out/$TAG/host.txt" ] && head -20 "gpurun_out/$TAG/host.txt" > "$DEST/host.txt"
 ls "$DEST"

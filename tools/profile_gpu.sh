@@ -1,8 +1,10 @@
 #!/bin/bash
 # Round profile on one MI355X (run through gpurun from the repo root):
-#   kernel trace + stats of the bench's fused step, then separate PMC passes
-#   (TCC FETCH_SIZE / WRITE_SIZE cannot share a pass; SQ counters alone).
-# Output: gpurun_out/prof_<tag>/...  Copy the summaries into profiles/.
+#   kernel trace + stats of the bench (fused and separate steps), then
+#   separate PMC passes (TCC FETCH_SIZE / WRITE_SIZE cannot share a pass; SQ
+#   counters alone), then the per-launch HBM traffic summary (pmc.json).
+# Output: gpurun_out/prof_<tag>/...  tools/collect_profile.sh copies the
+# summaries into profiles/.
 set -e
 TAG=${1:-r01}
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -20,4 +22,5 @@ timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_wr
     -- python3 $B --mode fused > "$OUT/pmc_write.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU --output-format csv -d "$OUT/pmc_sq" -o run \
     -- python3 $B --mode fused > "$OUT/pmc_sq.log" 2>&1
+python3 "$ROOT/tools/pmc_summary.py" "$OUT" "N=200,fd=forward" "$OUT/pmc.json" > "$OUT/pmc_summary.log" 2>&1
 echo "profile done: $OUT"
