@@ -25,7 +25,6 @@ microseconds per call, so they stay out of `value`).
 Prints one JSON line on rank 0.
 """
 import argparse
-import glob
 import json
 import os
 import sys
@@ -57,13 +56,15 @@ def parse():
 
 
 def latest_pmc():
-    """Per-launch HBM bytes of the hot kernels from the newest committed
-    rocprofv3 PMC summary (profiles/*/pmc.json, tools/pmc_summary.py)."""
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc.json")), key=os.path.getmtime)
-    if not files:
+    """Per-launch HBM bytes of the hot kernels from the committed rocprofv3
+    PMC summary of the current code (profiles/pmc_current.json, written by
+    tools/pmc_summary.py and copied by tools/collect_profile.sh)."""
+    path = os.path.join(ROOT, "profiles", "pmc_current.json")
+    if not os.path.exists(path):
         return None, None
-    with open(files[-1]) as fh:
-        return json.load(fh), os.path.relpath(files[-1], ROOT)
+    with open(path) as fh:
+        d = json.load(fh)
+    return d, d.get("source", "profiles/pmc_current.json")
 
 
 def main():
@@ -149,42 +150,44 @@ def main():
     value = (args.steps if mesh else args.steps * world) / elapsed
 
     if rank == 0:
-        J = np.array(rec["jac"])          # [whole, DAE stage, transcription, k_groups] ms
+        J = np.array(rec["jac"])          # [whole, DAE stage, transcription stage, k_groups] ms
         dae_ms = float(np.median(J[:, 1]))
-        groups_ms = float(np.median(J[:, 3]))
-        asm_ms = float(np.median(J[:, 2]))
+        tr_ms = float(np.median(J[:, 2]))
         G_local = nlp.G if not mesh else (2 * (ie - ib) + 1)
         ND = nlp.NS + nlp.NC + 2              # FD directions incl. t0, tf
         n_dae = G_local * (ND + 1) if args.fd != "central" else G_local * (2 * ND + 1)
         be_name, f_dae, mhash = nlp.backend()
         work = nlp.work()                     # executed FP64 ops of the (pruned) task kernels
         flops = n_dae * f_dae                 # algorithmic: one full DAE per FD lane
-        achieved = flops / (dae_ms * 1e-3) / 1e12
         nnz_local = (ie - ib) * nzi
-        alg_bytes_jac = 8 * (nlp.n + nnz_local)
+        alg_bytes_jac = 8 * (nlp.n + nnz_local)   # x in, Jacobian values out
+        fused_iv = nlp.uses_interval_kernel()
+        tr_kernel = "k_interval" if fused_iv else "k_transcribe"
         pmc, pmc_src = latest_pmc()
-        traffic = None
-        if pmc:
+        traffic = dae_traffic = None
+        if pmc and pmc.get("workload") == f"N={N},fd={args.fd}":
             kb = pmc.get("kernels", {})
-            dae_b = [kb.get(k, {}).get("hbm_bytes") for k in ("k_groups", "k_combine")]
-            if all(b is not None for b in dae_b) and pmc.get("workload") == f"N={N},fd={args.fd}":
-                traffic = sum(dae_b)
-        roof = {"bound": "mfma", "achieved": round(achieved, 4), "peak": FP64_PEAK_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 5),
-                "traffic": traffic,
-                "kernel": "DAE stage of eval_jac_g = k_groups + k_combine (FP64 VALU; MI355X FP64 "
-                          "vector peak = FP64 matrix peak); 'mfma' names the compute roof",
-                "kernel_ms": round(dae_ms, 5), "k_groups_ms": round(groups_ms, 5),
-                "k_combine_ms": round(dae_ms - groups_ms, 5),
-                "algorithmic_flops_per_launch": flops, "dae_evals_per_launch": n_dae,
-                "flops_per_dae": f_dae, "executed_flops_per_launch": float(work[0]),
-                "executed_TFLOPs": round(float(work[0]) / (dae_ms * 1e-3) / 1e12, 4),
-                "backend": be_name, "model_hash": f"0x{mhash:016x}",
+            traffic = kb.get(tr_kernel, {}).get("hbm_bytes")
+            dae_traffic = kb.get("k_groups", {}).get("hbm_bytes")
+        achieved = alg_bytes_jac / (tr_ms * 1e-3) / 1e9
+        dae_tf = flops / (dae_ms * 1e-3) / 1e12
+        roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                "kernel": (f"{tr_kernel}: finite-difference quotients + Jacobian assembly per mesh interval"
+                           + (" (group results combined in LDS)" if fused_iv else "")
+                           + "; the longest kernel of eval_jac_g"),
+                "kernel_ms": round(tr_ms, 5), "algorithmic_bytes": alg_bytes_jac,
                 "traffic_source": pmc_src if traffic is not None else None,
-                "assembly": {"kernel": "k_transcribe", "ms": round(asm_ms, 5),
-                             "algorithmic_bytes": alg_bytes_jac,
-                             "achieved_GBs": round(alg_bytes_jac / (asm_ms * 1e-3) / 1e9, 2),
-                             "peak_GBs": HBM_PEAK_GBS},
+                "dae_stage": {"kernel": "k_groups" if fused_iv else "k_groups + k_combine",
+                              "bound": "mfma", "unit": "TFLOP/s",
+                              "note": "FP64 VALU; MI355X FP64 vector peak = FP64 matrix peak",
+                              "achieved": round(dae_tf, 4), "peak": FP64_PEAK_TFLOPS,
+                              "frac": round(dae_tf / FP64_PEAK_TFLOPS, 5), "ms": round(dae_ms, 5),
+                              "algorithmic_flops_per_launch": flops, "dae_evals_per_launch": n_dae,
+                              "flops_per_dae": f_dae, "executed_flops_per_launch": float(work[0]),
+                              "executed_TFLOPs": round(float(work[0]) / (dae_ms * 1e-3) / 1e12, 4),
+                              "traffic": dae_traffic},
+                "backend": be_name, "model_hash": f"0x{mhash:016x}",
                 "instrumented_ms_per_step": round(1e3 * inst_elapsed / args.steps, 4)}
         if rec["g"]:
             Gt = np.array(rec["g"])

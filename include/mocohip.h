@@ -331,6 +331,10 @@ int mh_eval_dae(mh_ctx* ctx, int32_t npoints, const double* inputs,
  * used to select it. */
 int mh_get_backend(const mh_ctx* ctx, char* name, int32_t name_len,
         double* flops_per_eval, uint64_t* model_hash);
+/* Kernel variants this context launches, as a space-separated list
+ * ("tasks interval" = task kernels with the fused per-interval transcription
+ * for the Jacobian lanes; "lane", "generic", "split", ...). */
+int mh_get_backend_flags(const mh_ctx* ctx, char* flags, int32_t len);
 /* FNV-1a hash of everything the per-point DAE depends on (host only). */
 int mh_model_hash(const mh_model* model, uint64_t* hash);
 

@@ -42,6 +42,14 @@ using namespace mh;
 
 constexpr size_t kMaxLds = 160 * 1024;   // gfx950 LDS per workgroup
 
+// LDS-qualified views of dynamic shared memory.  Kept in address space 3 so
+// that a load that may come from LDS or from global memory (e.g. xdot_at) is
+// never merged into one flat load: flat loads wait on vmcnt, i.e. on every
+// outstanding global store of the thread.
+typedef __attribute__((address_space(3))) double lds_double;
+typedef __attribute__((address_space(3))) int lds_int;
+__device__ __forceinline__ lds_double* lds(double* p) { return (lds_double*)p; }
+
 // ------------------------------------------------------------------------
 // error handling
 // ------------------------------------------------------------------------
@@ -79,6 +87,21 @@ struct TplEntry {
     int16_t dir;   // 0 = t0, 1 = tf, 2 + j = point input j
     int16_t s;     // state index of the row (defects) / control index (interp)
 };
+// 4-byte form of a template entry (staged in LDS by k_interval):
+// kind | pt << 3 | dir << 5 | row << 16; s is implied by the row.
+__host__ __device__ __forceinline__ uint32_t tpl_pack(const TplEntry& e) {
+    return (uint32_t)e.kind | ((uint32_t)e.pt << 3) | ((uint32_t)e.dir << 5) | ((uint32_t)e.row << 16);
+}
+__host__ __device__ __forceinline__ TplEntry tpl_unpack(uint32_t u, int NS, bool hs) {
+    TplEntry e;
+    e.kind = (uint8_t)(u & 7u);
+    e.pt = (uint8_t)((u >> 3) & 3u);
+    e.dir = (int16_t)((u >> 5) & 2047u);
+    const int r = (int)(u >> 16);
+    e.row = (int16_t)r;
+    e.s = (int16_t)(hs ? (r < NS ? r : (r < 2 * NS ? r - NS : r - 2 * NS)) : r);
+    return e;
+}
 
 // ------------------------------------------------------------------------
 // DAE back ends.  Generic: the interpreter of dae_device.hpp with size-class
@@ -222,6 +245,38 @@ struct Src {
     int G, k0;
 };
 
+// Same, reading a grid point's inputs staged in LDS (k_interval).
+template <class D>
+struct LaneInL {
+    const lds_double* xs;
+    const lds_double* xc;
+    int pi;
+    double step;
+    __device__ __forceinline__ double operator[](int i) const {
+        const double v = i < D::NS ? xs[i] : xc[i - D::NS];
+        return i == pi ? v + step : v;
+    }
+};
+
+// Time, perturbed input and step of evaluation lane r at normalized grid
+// time g (Lanes layout above).  The single definition of the lane
+// arithmetic: every kernel that evaluates lanes goes through it.
+__device__ __forceinline__ double lane_time(const Lanes& Ln, double g, double t0, double tf, int r,
+        int& pi, double& step) {
+    double t = (tf - t0) * g + t0;
+    pi = -1;
+    step = 0.0;
+    if (r != Ln.base) {
+        int dir = r;
+        step = Ln.fd == MH_FD_BACKWARD ? -Ln.h : Ln.h;
+        if (Ln.fd == MH_FD_CENTRAL && r >= Ln.ND) { dir = r - Ln.ND; step = -Ln.h; }
+        if (dir == 0) t = t + step * (1.0 - g);
+        else if (dir == 1) t = t + step * g;
+        pi = dir - 2;
+    }
+    return t;
+}
+
 template <class D>
 __device__ __forceinline__ LaneIn<D> lane_input(const Src& S, const Lanes& Ln, int kl, int r,
         double& t) {
@@ -231,19 +286,8 @@ __device__ __forceinline__ LaneIn<D> lane_input(const Src& S, const Lanes& Ln, i
         return LaneIn<D>{p + 1, p + 1 + D::NS, -1, 0.0};
     }
     const int k = S.k0 + kl;
-    const double g = S.grid[k];
-    const double t0 = S.x[0], tf = S.x[1];
-    t = (tf - t0) * g + t0;
     LaneIn<D> in{S.x + 2 + (long)k * D::NS, S.x + 2 + (long)D::NS * S.G + (long)k * D::NC, -1, 0.0};
-    if (r != Ln.base) {
-        int dir = r;
-        double step = Ln.fd == MH_FD_BACKWARD ? -Ln.h : Ln.h;
-        if (Ln.fd == MH_FD_CENTRAL && r >= Ln.ND) { dir = r - Ln.ND; step = -Ln.h; }
-        if (dir == 0) t = t + step * (1.0 - g);
-        else if (dir == 1) t = t + step * g;
-        in.pi = dir - 2;
-        in.step = step;
-    }
+    t = lane_time(Ln, S.grid[k], S.x[0], S.x[1], r, in.pi, in.step);
     return in;
 }
 
@@ -263,6 +307,13 @@ struct Tasks {
 // [group, wall clock at start, at end, shader clock at start, at end].
 constexpr int TIMING_SLOTS = 1 << 16;
 __device__ long long g_task_timing[TIMING_SLOTS][5];
+// k_interval phases per block: start, staged, combined, end (wall clock)
+constexpr int IV_TIMING_SLOTS = 4096;
+__device__ long long g_iv_timing[IV_TIMING_SLOTS][4];
+#define MH_IV_STAMP(i) \
+    if (threadIdx.x == 0 && blockIdx.x < IV_TIMING_SLOTS) g_iv_timing[blockIdx.x][i] = wall_clock64();
+#else
+#define MH_IV_STAMP(i)
 #endif
 
 template <class D>
@@ -322,8 +373,8 @@ __global__ void __launch_bounds__(64) k_groups(DevModel M, Src S, Lanes Ln, Task
 // (one lane role) then reads the slots it needs from LDS.
 template <class D>
 struct TaskLoadLds {
-    const double* sT;
-    const double* sH;
+    const lds_double* sT;
+    const lds_double* sH;
     const int* __restrict__ slot;   // [stride][ng]: slot of group g for this role
     int r;
     __device__ __forceinline__ double operator()(int g, int f) const {
@@ -418,7 +469,7 @@ __global__ void __launch_bounds__(1024) k_combine(DevModel M, Src S, Lanes Ln, T
         double t;
         const LaneIn<D> in = lane_input<D>(S, Ln, kl, r, t);
         if (r == Ln.base && times) times[kl] = t;
-        const TaskLoadLds<D> TL{sT, sH, TK.jd, r};
+        const TaskLoadLds<D> TL{lds(sT), lds(sH), TK.jd, r};
         D::combine(M, t, in, TL, out);
     }
     // Y[(kl*NO + o)*stride + r]  (ystride_pt = NO*stride; explicit points:
@@ -473,17 +524,30 @@ struct YG {
     const double* __restrict__ times;
     int NO, stride, k0;
     int q;   // Y holds finite-difference quotients (k_combine quot mode)
+    const double* __restrict__ x;
+    int NS, NC, G;
+    // state s / control j of grid point k from the iterate
+    __device__ __forceinline__ double xs(int k, int s) const { return x[2 + (long)k * NS + s]; }
+    __device__ __forceinline__ double xc(int k, int j) const {
+        return x[2 + (long)NS * G + (long)k * NC + j];
+    }
     __device__ __forceinline__ const double* row(int k, int o) const {
         return Y + ((long)(k - k0) * NO + o) * stride;
     }
     __device__ __forceinline__ double t(int k) const { return times[k - k0]; }
 };
 struct YS {
-    const double* Y;
-    const double* times;
+    const lds_double* Y;
+    const lds_double* times;
     int NO, stride, kf;
     int q;
-    __device__ __forceinline__ const double* row(int k, int o) const {
+    // the interval's states / controls staged in LDS ([point][NS], [point][NC])
+    const lds_double* sxs;
+    const lds_double* sxc;
+    int NS, NC;
+    __device__ __forceinline__ double xs(int k, int s) const { return sxs[(k - kf) * NS + s]; }
+    __device__ __forceinline__ double xc(int k, int j) const { return sxc[(k - kf) * NC + j]; }
+    __device__ __forceinline__ const lds_double* row(int k, int o) const {
         return Y + ((k - kf) * NO + o) * stride;
     }
     __device__ __forceinline__ double t(int k) const { return times[k - kf]; }
@@ -493,7 +557,7 @@ struct YS {
 template <class YV>
 __device__ __forceinline__ double xdot_at(const Layout& L, const Lanes& Ln,
         const double* __restrict__ x, const YV& Y, int k, int s) {
-    if (s < L.NQ) return x[2 + (long)k * L.NS + L.NQ + s];
+    if (s < L.NQ) return Y.xs(k, L.NQ + s);
     return Y.row(k, s - L.NQ)[Ln.base];
 }
 
@@ -506,26 +570,24 @@ __device__ __forceinline__ double defect_row(const Layout& L, const Interval& I,
         const double h = Y.t(kp) - Y.t(ki);
         if (r < NS) {
             const int s = r;
-            const double xi = x[2 + (long)ki * NS + s], xm = x[2 + (long)km * NS + s],
-                         xp = x[2 + (long)kp * NS + s];
+            const double xi = Y.xs(ki, s), xm = Y.xs(km, s), xp = Y.xs(kp, s);
             const double fi = xdot_at(L, Ln, x, Y, ki, s), fp = xdot_at(L, Ln, x, Y, kp, s);
             return xm - 0.5 * (xp + xi) - (h / 8.0) * (fi - fp);
         }
         if (r < 2 * NS) {
             const int s = r - NS;
-            const double xi = x[2 + (long)ki * NS + s], xp = x[2 + (long)kp * NS + s];
+            const double xi = Y.xs(ki, s), xp = Y.xs(kp, s);
             const double fi = xdot_at(L, Ln, x, Y, ki, s), fm = xdot_at(L, Ln, x, Y, km, s),
                          fp = xdot_at(L, Ln, x, Y, kp, s);
             return xp - xi - (h / 6.0) * (fp + 4.0 * fm + fi);
         }
         const int j = r - 2 * NS;
-        const double* xc = x + 2 + (long)NS * L.G;
-        return xc[(long)km * L.NC + j] - 0.5 * (xc[(long)kp * L.NC + j] + xc[(long)ki * L.NC + j]);
+        return Y.xc(km, j) - 0.5 * (Y.xc(kp, j) + Y.xc(ki, j));
     }
     const int ki = i, kp = i + 1;
     const double h = Y.t(kp) - Y.t(ki);
     const int s = r;
-    const double xi = x[2 + (long)ki * NS + s], xp = x[2 + (long)kp * NS + s];
+    const double xi = Y.xs(ki, s), xp = Y.xs(kp, s);
     const double fi = xdot_at(L, Ln, x, Y, ki, s), fp = xdot_at(L, Ln, x, Y, kp, s);
     return xp - (xi + 0.5 * h * (fp + fi));
 }
@@ -536,7 +598,7 @@ template <class YV>
 __device__ __forceinline__ double dxdot(const Layout& L, const Lanes& Ln, const YV& Y, int k, int s,
         int dir) {
     if (s < L.NQ) return dir == 2 + L.NQ + s ? 1.0 : 0.0;
-    const double* y = Y.row(k, s - L.NQ);
+    const auto y = Y.row(k, s - L.NQ);
     if (Y.q) return y[dir];
     if (Ln.fd == MH_FD_CENTRAL) return (y[dir] - y[Ln.ND + dir]) / (2.0 * Ln.h);
     if (Ln.fd == MH_FD_FORWARD) return (y[dir] - y[Ln.base]) / Ln.h;
@@ -633,7 +695,7 @@ __global__ void __launch_bounds__(256) k_transcribe(Layout L, Interval I, Lanes 
         int nchunks, int yq) {
     const int il = blockIdx.y;
     const int i = I.ib + il;
-    const YG YV{Y, times, L.NO, Ln.stride, L.k0, yq};
+    const YG YV{Y, times, L.NO, Ln.stride, L.k0, yq, x, L.NS, L.NC, L.G};
     if ((int)blockIdx.x < nchunks) {
         int k_first, k_last;
         interval_span(I, i, k_first, k_last);
@@ -663,7 +725,7 @@ __global__ void __launch_bounds__(256) k_transcribe_gs(Layout L, Interval I, Lan
         const double* __restrict__ grid, const double* __restrict__ times,
         const double* __restrict__ Y, double* __restrict__ g, double* __restrict__ values,
         int nint, int yq) {
-    const YG YV{Y, times, L.NO, Ln.stride, L.k0, yq};
+    const YG YV{Y, times, L.NO, Ln.stride, L.k0, yq, x, L.NS, L.NC, L.G};
     const int nthreads = gridDim.x * blockDim.x;
     const int tid = blockIdx.x * blockDim.x + threadIdx.x;
     if (values) {
@@ -700,8 +762,9 @@ __global__ void __launch_bounds__(256) k_transcribe_gs(Layout L, Interval I, Lan
 constexpr int IV_UNROLL = 4;
 template <class D>
 __global__ void __launch_bounds__(1024) k_interval(DevModel M, Src S, Lanes Ln, Tasks TK, Layout L,
-        Interval I, const TplEntry* __restrict__ tpl, const double* __restrict__ T,
-        const double* __restrict__ H, double* __restrict__ g, double* __restrict__ values) {
+        Interval I, const TplEntry* __restrict__ tpl, const uint32_t* __restrict__ tplp, int tables_lds,
+        const double* __restrict__ T, const double* __restrict__ H, double* __restrict__ g,
+        double* __restrict__ values) {
     extern __shared__ double smem[];
     const int il = blockIdx.x;
     const int i = I.ib + il;
@@ -714,26 +777,58 @@ __global__ void __launch_bounds__(1024) k_interval(DevModel M, Src S, Lanes Ln, 
     double* sTimes = sY + npts * ny;         // [npts]
     double* sT = sTimes + 4;                 // [npts][nt]
     double* sH = sT + npts * nt;             // [npts][nh]
+    // tables_lds: the packed Jacobian template and the role -> slot table
+    // are staged too, so that the combine and the assembly issue no global
+    // loads after this one round trip
+    const int ntp = (I.nnz_int + 1) / 2;     // in doubles
+    double* sXs = sH + npts * nh;            // [npts][NS] states, [npts][NC] controls
+    double* sXc = sXs + npts * L.NS;
+    double* sTpl = sXc + npts * L.NC;
     // the interval's points are consecutive local grid points: their T (and
     // H) slabs are one contiguous run each
     const int kl0 = k_first - S.k0;
+    MH_IV_STAMP(0)
     if (nt > 0) stage_lds<16>(sT, T + (long)kl0 * nt, npts * nt);
     if (nh > 0) stage_lds<8>(sH, H + (long)kl0 * nh, npts * nh);
+    if (tables_lds && values) stage_lds<8>(sTpl, (const double*)tplp, ntp);
+    stage_lds<1>(sXs, S.x + 2 + (long)k_first * L.NS, npts * L.NS);
+    if (L.NC > 0) stage_lds<1>(sXc, S.x + 2 + (long)L.NS * L.G + (long)k_first * L.NC, npts * L.NC);
+    const __attribute__((address_space(3))) uint32_t* tp = (const __attribute__((address_space(3))) uint32_t*)sTpl;
+    const double t0 = S.x[0], tf = S.x[1];
     __syncthreads();
+    MH_IV_STAMP(1)
     for (int w = threadIdx.x; w < npts * Ln.stride; w += blockDim.x) {
         const int p = w / Ln.stride, r = w - p * Ln.stride;
-        double t;
-        const LaneIn<D> in = lane_input<D>(S, Ln, kl0 + p, r, t);
+        LaneInL<D> in{lds(sXs + p * L.NS), lds(sXc + p * L.NC), -1, 0.0};
+        const double t = lane_time(Ln, S.grid[k_first + p], t0, tf, r, in.pi, in.step);
         if (r == Ln.base) sTimes[p] = t;
-        const TaskLoadLds<D> TL{sT + p * nt, sH + p * nh, TK.jd, r};
+        const TaskLoadLds<D> TL{lds(sT + p * nt), lds(sH + p * nh), TK.jd, r};
         double out[D::NO];
         D::combine(M, t, in, TL, out);
-        double* Yp = sY + p * ny + r;
+        lds_double* Yp = lds(sY + p * ny + r);
 #pragma unroll
         for (int o = 0; o < D::NO; ++o) Yp[o * Ln.stride] = out[o];
     }
     __syncthreads();
-    const YS YV{sY, sTimes, D::NO, Ln.stride, k_first, 0};
+    // finite-difference quotients in place (CasADi FiniteDiff formulas), once
+    // per (point, output, direction) instead of once per Jacobian entry that
+    // reads them; the base slot keeps the raw value for the defect rows
+    const int quot = values && Ln.stride > 1;
+    if (quot) {
+        const int ndir = Ln.ND;
+        for (int w = threadIdx.x; w < npts * D::NO * ndir; w += blockDim.x) {
+            const int po = w / ndir, d = w - po * ndir;
+            lds_double* y = lds(sY + po * Ln.stride);
+            double q;
+            if (Ln.fd == MH_FD_CENTRAL) q = (y[d] - y[Ln.ND + d]) / (2.0 * Ln.h);
+            else if (Ln.fd == MH_FD_FORWARD) q = (y[d] - y[Ln.base]) / Ln.h;
+            else q = (y[Ln.base] - y[d]) / Ln.h;
+            y[d] = q;
+        }
+        __syncthreads();
+    }
+    MH_IV_STAMP(2)
+    const YS YV{lds(sY), lds(sTimes), D::NO, Ln.stride, k_first, quot, lds(sXs), lds(sXc), L.NS, L.NC};
     if (g) {
         double* gi = g + (long)il * I.rpi;
         for (int r = threadIdx.x; r < I.rpi; r += blockDim.x) gi[r] = defect_row(L, I, Ln, S.x, YV, i, r);
@@ -743,6 +838,12 @@ __global__ void __launch_bounds__(1024) k_interval(DevModel M, Src S, Lanes Ln, 
         double* vi = values + (long)il * I.nnz_int;
         const int B = blockDim.x;
         int e = threadIdx.x;
+        const bool hs = I.scheme == MH_HERMITE_SIMPSON;
+        if (tables_lds) {
+            for (; e < I.nnz_int; e += B)
+                vi[e] = jac_entry(L, Ln, S.x, YV, tpl_unpack(tp[e], L.NS, hs), k_first, C);
+            e = I.nnz_int;
+        }
         // template entries for IV_UNROLL iterations are loaded before any is
         // evaluated (independent loads in flight, then LDS reads + stores)
         for (; e + (IV_UNROLL - 1) * B < I.nnz_int; e += IV_UNROLL * B) {
@@ -754,6 +855,7 @@ __global__ void __launch_bounds__(1024) k_interval(DevModel M, Src S, Lanes Ln, 
         }
         for (; e < I.nnz_int; e += B) vi[e] = jac_entry(L, Ln, S.x, YV, tpl[e], k_first, C);
     }
+    MH_IV_STAMP(3)
 }
 
 // ---- objective -------------------------------------------------------------
@@ -1028,7 +1130,7 @@ static void build_taskset(const TaskInfo& ti, const Lanes& ln, int nk, int nsimd
     ts.dlen.assign(ng, 0);
     ts.off.assign(ng, 0);
     ts.roles.assign((size_t)ng * S, 0);
-    ts.jd.assign((size_t)ng * S, 0);
+    ts.jd.assign((size_t)ng * S + 1, 0);   // +1: whole doubles when staged to LDS
     int tdoubles = 0;
     for (int g = 0; g < ng; ++g) {
         std::vector<int> D{ln.base};
@@ -1150,6 +1252,8 @@ struct mh_ctx {
            *d_Yg = nullptr, *d_g = nullptr, *d_vals = nullptr, *d_C = nullptr, *d_grad = nullptr,
            *d_tpart = nullptr, *d_f = nullptr;
     TplEntry* d_tpl = nullptr;
+    uint32_t* d_tplp = nullptr;    // packed template (k_interval)
+    std::vector<uint32_t> tplp;
     float timings[4] = {0, 0, 0, 0};
     // task-decomposed back ends
     TaskSet ts_jac, ts_g, ts_probe;
@@ -1166,6 +1270,7 @@ struct mh_ctx {
     // and transcription fused in k_interval (LDS-resident raw outputs)
     bool use_interval[2] = {false, false};
     int nsimd = 1024;              // SIMDs of the device (4 per CU)
+    bool tables_lds = false;       // k_interval stages the packed template (MOCOHIP_TABLES=1)
     bool asm_grid_stride = false;  // k_transcribe_gs (MOCOHIP_ASM=gs) instead of k_transcribe
     bool quot = false;             // k_combine writes FD quotients (MOCOHIP_QUOT=1)
     int yq[2] = {0, 0};            // per lane configuration: Y of the last evaluation holds quotients
@@ -1525,6 +1630,17 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
                  o_grid = A.put(c->grid.data(), c->grid.size()),
                  o_quad = A.put(c->quad.data(), c->quad.size()),
                  o_tpl = A.put(c->tpl.data(), c->tpl.size());
+    // packed template, padded to whole doubles (staged in LDS as doubles)
+    c->tplp.clear();
+    for (const TplEntry& e : c->tpl) {
+        c->tplp.push_back(tpl_pack(e));
+        const TplEntry u = tpl_unpack(c->tplp.back(), c->NS, c->scheme == MH_HERMITE_SIMPSON);
+        if (u.row != e.row || u.kind != e.kind || u.pt != e.pt || u.dir != e.dir || u.s != e.s)
+            return set_err(MH_ERR_UNSUPPORTED, "Jacobian template entry does not pack into 32 bits");
+    }
+    if (c->tplp.size() % 2) c->tplp.push_back(0u);
+    const size_t o_tplp = A.put(c->tplp.data(), c->tplp.size());
+
     const int nint = c->ie - c->ib;
     const int ND = c->NI + 2;
     const size_t o_x = A.reserve(sizeof(double) * c->n);
@@ -1579,6 +1695,8 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     c->GS.gw = (const double*)(b + o_gw);
     c->d_grid = (double*)(b + o_grid); c->d_quad = (double*)(b + o_quad);
     c->d_tpl = (TplEntry*)(b + o_tpl);
+    c->d_tplp = (uint32_t*)(b + o_tplp);
+
     c->d_x = (double*)(b + o_x); c->d_times = (double*)(b + o_times); c->d_Y = (double*)(b + o_Y);
     c->d_Yg = (double*)(b + o_Yg); c->d_g = (double*)(b + o_g); c->d_vals = (double*)(b + o_vals);
     c->d_C = (double*)(b + o_C); c->d_grad = (double*)(b + o_grad); c->d_tpart = (double*)(b + o_tpart);
@@ -1603,6 +1721,8 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
         // budget is exceeded (MOCOHIP_INTERVAL=0 forces the split path)
         const char* ei = std::getenv("MOCOHIP_INTERVAL");
         const bool allow = !(ei && std::strcmp(ei, "0") == 0);
+        const char* et = std::getenv("MOCOHIP_TABLES");
+        c->tables_lds = et && std::strcmp(et, "1") == 0;   // opt-in: measured slower
         const char* ea = std::getenv("MOCOHIP_ASM");
         c->asm_grid_stride = ea && std::strcmp(ea, "gs") == 0;
         const char* ee = std::getenv("MOCOHIP_EVENTS");
@@ -1793,21 +1913,25 @@ static void be_eval_tasks(mh_ctx* c, const double* x, int mode, double* Y) {
 }
 // LDS bytes of k_interval for one lane configuration (0: does not apply).
 template <class D>
-static size_t interval_lds(const mh_ctx* c, const Lanes& ln, const TaskSet& ts) {
+static size_t interval_lds(const mh_ctx* c, const Lanes& ln, const TaskSet& ts, bool tables) {
     const size_t npts = c->scheme == MH_HERMITE_SIMPSON ? 3 : 2;
-    return sizeof(double) * (npts * D::NO * ln.stride + 4 +
-                             npts * ((size_t)ts.dev.tdoubles + (size_t)ts.dev.nmass * D::NST));
+    const size_t tab = tables ? (size_t)(c->nnz_int + 1) / 2 : 0;
+    return sizeof(double) * (npts * D::NO * ln.stride + 4 + npts * (size_t)(c->NS + c->NC) +
+                             npts * ((size_t)ts.dev.tdoubles + (size_t)ts.dev.nmass * D::NST) + tab);
 }
 template <class D>
 static size_t be_interval_bytes(const mh_ctx* c, int mode) {
-    return interval_lds<D>(c, mode ? c->lanes_jac : c->lanes_g, mode ? c->ts_jac : c->ts_g);
+    return interval_lds<D>(c, mode ? c->lanes_jac : c->lanes_g, mode ? c->ts_jac : c->ts_g, false);
 }
 template <class D>
 static void be_interval(mh_ctx* c, const double* x, int mode, double* g, double* v) {
     const Src S{x, c->d_grid, nullptr, c->G, c->k0};
     const Lanes& ln = mode ? c->lanes_jac : c->lanes_g;
     const TaskSet& ts = mode ? c->ts_jac : c->ts_g;
-    const size_t lds = interval_lds<D>(c, ln, ts);
+    // stage the packed template too when it fits and MOCOHIP_TABLES=1
+    const size_t lds_tab = interval_lds<D>(c, ln, ts, true);
+    const int tables = c->tables_lds && lds_tab <= kMaxLds ? 1 : 0;
+    const size_t lds = tables ? lds_tab : interval_lds<D>(c, ln, ts, false);
     if (lds > 65536)
         (void)hipFuncSetAttribute((const void*)k_interval<D>, hipFuncAttributeMaxDynamicSharedMemorySize,
                 (int)lds);
@@ -1815,7 +1939,7 @@ static void be_interval(mh_ctx* c, const double* x, int mode, double* g, double*
     Interval I{c->scheme, c->interp, c->ib, c->rpi, c->nnz_int};
     const unsigned threads = v ? 1024u : 256u;
     hipLaunchKernelGGL(k_interval<D>, dim3((unsigned)(c->ie - c->ib)), dim3(threads), lds, c->stream, c->M,
-            S, ln, ts.dev, L, I, c->d_tpl, c->d_T, c->d_H, g, v);
+            S, ln, ts.dev, L, I, c->d_tpl, c->d_tplp, tables, c->d_T, c->d_H, g, v);
 }
 template <class D>
 static void be_integrand(mh_ctx* c, const double* x) {
@@ -2125,6 +2249,11 @@ extern "C" int mh_debug_task_timing(long long* out, int nslots) {
     HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_task_timing), sizeof(long long) * 5 * n));
     return MH_OK;
 }
+extern "C" int mh_debug_interval_timing(long long* out, int nslots) {
+    const int n = std::min(nslots, IV_TIMING_SLOTS);
+    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_iv_timing), sizeof(long long) * 4 * n));
+    return MH_OK;
+}
 #endif
 
 extern "C" int mh_set_timing(mh_ctx* c, int on) {
@@ -2148,6 +2277,19 @@ extern "C" int mh_get_backend(const mh_ctx* c, char* name, int32_t name_len, dou
     }
     if (flops_per_eval) *flops_per_eval = c->be->flops_per_eval;
     if (model_hash) *model_hash = c->model_hash;
+    return MH_OK;
+}
+
+extern "C" int mh_get_backend_flags(const mh_ctx* c, char* flags, int32_t len) {
+    if (!c || !flags || len <= 0) return set_err(MH_ERR_INVALID, "bad argument");
+    std::string f = c->be->tasks ? "tasks" : (std::strncmp(c->be->name, "generic", 7) == 0 ? "generic" : "lane");
+    f += c->use_interval[1] ? " interval" : " split";
+    if (c->use_interval[0]) f += " interval-g";
+    if (c->tables_lds) f += " tables";
+    if (c->quot) f += " quot";
+    if (c->asm_grid_stride) f += " asm-gs";
+    std::strncpy(flags, f.c_str(), (size_t)len - 1);
+    flags[len - 1] = 0;
     return MH_OK;
 }
 

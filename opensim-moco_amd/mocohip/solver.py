@@ -203,6 +203,16 @@ class HipNLP(_NLPBase):
         self._check(self.lib.mh_get_work(self.ctx, abi.dptr(w)))
         return w
 
+    def uses_interval_kernel(self) -> bool:
+        """True when eval_jac_g runs the fused k_interval transcription
+        (group results combined in LDS) rather than k_combine + k_transcribe."""
+        return "interval" in self.backend_flags()
+
+    def backend_flags(self) -> str:
+        buf = C.create_string_buffer(256)
+        self._check(self.lib.mh_get_backend_flags(self.ctx, buf, 256))
+        return buf.value.decode()
+
     def set_timing(self, on: bool):
         """Record stage events on every evaluation (mh_set_timing)."""
         self._check(self.lib.mh_set_timing(self.ctx, int(bool(on))))

@@ -111,7 +111,7 @@ def _pair(name, backend="auto", tasks=None, env=None):
     rep = st.problem.create_rep()
     opts = st.solver.options()
     saved = {k: os.environ.pop(k, None) for k in ("MOCOHIP_BACKEND", "MOCOHIP_TASKS", "MOCOHIP_INTERVAL",
-                                                  "MOCOHIP_ASM", "MOCOHIP_QUOT")}
+                                                  "MOCOHIP_ASM", "MOCOHIP_QUOT", "MOCOHIP_TABLES")}
     if backend != "auto":
         os.environ["MOCOHIP_BACKEND"] = backend
     if tasks:
@@ -327,7 +327,8 @@ def test_pruned_tasks_bit_identical(name):
                                   "gait_compliant_central", "gait_torque_driven"])
 @pytest.mark.parametrize("variant", [{"MOCOHIP_INTERVAL": "0"},
                                      {"MOCOHIP_INTERVAL": "0", "MOCOHIP_ASM": "gs"},
-                                     {"MOCOHIP_INTERVAL": "0", "MOCOHIP_QUOT": "1"}])
+                                     {"MOCOHIP_INTERVAL": "0", "MOCOHIP_QUOT": "1"},
+                                     {"MOCOHIP_TABLES": "1"}])
 def test_kernel_variants_bit_identical(name, variant):
     """The default k_interval (combine + transcription per mesh interval,
     raw outputs in LDS) writes exactly what the split path writes through

@@ -14,6 +14,14 @@ done
 python tools/kstats.py "$P" > "$DEST/summary.txt"
 grep -h '^{' "$P"/*.log > "$DEST/bench_lines_under_profiler.jsonl" || true
 [ -f "gpurun_out/$TAG/bench.json" ] && cp "gpurun_out/$TAG/bench.json" "$DEST/bench.json"
-[ -f "$P/pmc.json" ] && cp "$P/pmc.json" "$DEST/pmc.json"
+if [ -f "$P/pmc.json" ]; then
+    cp "$P/pmc.json" "$DEST/pmc.json"
+    python - "$DEST/pmc.json" <<'PY'
+import json, sys
+d = json.load(open(sys.argv[1]))
+d["source"] = sys.argv[1]
+json.dump(d, open("profiles/pmc_current.json", "w"), indent=1)
+PY
+fi
 [ -f "gpurun_out/$TAG/host.txt" ] && head -20 "gpurun_out/$TAG/host.txt" > "$DEST/host.txt"
 ls "$DEST"

@@ -21,7 +21,7 @@ def main():
     Ns = [int(a) for a in sys.argv[1:]] or [200, 400]
     variants = [{}, {"MOCOHIP_INTERVAL": "0"}]
     for N, var in [(N, v) for N in Ns for v in variants]:
-        for k in ("MOCOHIP_ORDER", "MOCOHIP_INTERVAL", "MOCOHIP_ASM", "MOCOHIP_QUOT", "MOCOHIP_EVENTS"):
+        for k in ("MOCOHIP_ORDER", "MOCOHIP_INTERVAL", "MOCOHIP_ASM", "MOCOHIP_QUOT", "MOCOHIP_EVENTS", "MOCOHIP_TABLES", "MOCOHIP_ROWSEG"):
             os.environ.pop(k, None)
         os.environ.update(var)
         st = configs.gait10dof18musc(N, fd_scheme="forward")

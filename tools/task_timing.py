@@ -39,6 +39,20 @@ def main():
     a = a[a[:, 1] != 0]
     t0 = a[:, 1].min()
     print(f"{len(a)} blocks, span {(a[:, 2].max() - t0) / 100:.2f} us")
+    lib.mh_debug_interval_timing.restype = C.c_int
+    lib.mh_debug_interval_timing.argtypes = [C.POINTER(C.c_longlong), C.c_int]
+    nb = 4096
+    ib = (C.c_longlong * (4 * nb))()
+    assert lib.mh_debug_interval_timing(ib, nb) == 0
+    iv = np.frombuffer(ib, dtype=np.int64).reshape(nb, 4)
+    iv = iv[iv[:, 0] != 0]
+    if len(iv):
+        z = iv[:, 0].min()
+        d = np.diff(iv, axis=1) / 100.0
+        print(f"k_interval: {len(iv)} blocks, span {(iv[:, 3].max() - z) / 100:.2f} us; start spread "
+              f"{(iv[:, 0].max() - z) / 100:.2f} us; phase medians (us) stage {np.median(d[:, 0]):.2f} "
+              f"combine {np.median(d[:, 1]):.2f} assemble {np.median(d[:, 2]):.2f}; max "
+              f"{d[:, 0].max():.2f} {d[:, 1].max():.2f} {d[:, 2].max():.2f}")
     for g in np.unique(a[:, 0]):
         b = a[a[:, 0] == g]
         lat = b[:, 4] - b[:, 3]
