@@ -141,6 +141,14 @@ def main():
     for _ in range(args.warmup):
         step()
     elapsed = timed(args.steps, False)
+    # secondary: the same K steps as one fused call each (IPOPT's
+    # eval_g(new_x) -> eval_jac_g(!new_x) pair from one DAE pass)
+    other = "fused" if args.mode == "separate" else "separate"
+    mode0, args.mode = args.mode, other
+    for _ in range(args.warmup):
+        step()
+    other_elapsed = timed(args.steps, False)
+    args.mode = mode0
     # instrumented pass (roofline): same K steps with stage events
     nlp.set_timing(True)
     inst_elapsed = timed(args.steps, True)
@@ -212,6 +220,7 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
         }
+        line[f"value_{other}"] = round((args.steps if mesh else args.steps * world) / other_elapsed, 3)
         if cpu and cpu.get("value"):
             line["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 2)
         print(json.dumps(line), flush=True)

@@ -261,3 +261,68 @@ def test_golden_gait_solution_order_and_defects():
     p2.set_time_bounds(0.01, 1.3)
     nlp2 = OracleNLP(p2.create_rep(), MocoHipSolver(num_mesh_intervals=65).options())
     assert np.abs(nlp2.eval_g(x)).max() > 1e-2
+
+
+def test_muscle_geometry_matches_reference_gso_fiber_lengths():
+    """Muscle path geometry (PathPoint / ConditionalPathPoint /
+    MovingPathPoint with the knee SimmSplines) pinned by the
+    reference's GSO golden file
+    Moco/Archive/Tests/std_testGait10dof18musc_GSO_solution_norm_fiber_length.sto
+    (tests/golden/gso_norm_fiber_length.npz, tools/make_gso_fixture.py): the
+    rigid-tendon normalized fiber lengths of the 9 right-leg muscles
+    GlobalStaticOptimization computed from testGait10dof18musc_kinematics.mot.
+    Preprocessing restated: rows within [0.58-0.05, 1.8+0.05] s
+    (InverseMuscleSolverMotionData.cpp:49-59), 3rd-order Butterworth lowpass
+    at 6 Hz applied forward-backward (Storage::lowpassIIR; the setup's
+    lowpass_cutoff_frequency_for_kinematics), a cubic spline of the
+    muscle-tendon lengths in place of the GCV spline, and
+    DeGrooteFregly2016MuscleStandalone.h:207-231.  The remaining differences
+    (spline and filter-padding details) are ~1e-6 typical."""
+    err = _gso_errors(configs.gait10dof18musc_model())
+    rms = np.sqrt((err ** 2).mean(0))
+    assert np.median(err) < 1e-5, np.median(err)
+    assert rms.max() < 5e-5, rms
+    assert err.max() < 5e-4, err.max()
+    # sensitivity: one vasti_r path point moved by 5 mm is far outside this
+    m = configs.gait10dof18musc_model()
+    vi = [mu.name for mu in m.muscles].index("vasti_r")
+    p0 = m.muscles[vi].points[0]
+    p0.loc = tuple(np.asarray(p0.loc, float) + [0.005, 0.0, 0.0])
+    assert _gso_errors(m).max() > 1e-3
+
+
+def _gso_errors(m):
+    """|normalized fiber length - GSO golden| per (time, right-leg muscle)."""
+    from scipy.interpolate import CubicSpline
+    from scipy.signal import butter, filtfilt
+    import os
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "gso_norm_fiber_length.npz"))
+    kl, kin = list(z["kin_labels"]), z["kin"]
+    gl, gso = list(z["nfl_labels"]), z["nfl"]
+    rep = MocoProblem(m).create_rep()
+    nlp = OracleNLP(rep, MocoHipSolver(num_mesh_intervals=2).options())
+    qnames = [n.split("/")[-2] for n in rep.state_names[:rep.nq]]
+    t = kin[:, 0]
+    sel = (t >= 0.58 - 0.05) & (t <= 1.8 + 0.05)
+    t = t[sel]
+    Q = np.stack([np.deg2rad(kin[sel, kl.index(q)]) if q not in ("pelvis_tx", "pelvis_ty")
+                  else kin[sel, kl.index(q)] for q in qnames], 1)
+    b, a = butter(3, 6.0 / (0.5 / (t[1] - t[0])))
+    Q = filtfilt(b, a, Q, axis=0, padtype="odd", padlen=len(t) // 2)
+    names = [mu.name for mu in m.muscles]
+    cols = [names.index(l.split("/")[-1]) for l in gl[1:]]
+    L = np.zeros((len(t), len(cols)))
+    out = np.zeros(2)
+    for i, q in enumerate(Q):
+        q = np.ascontiguousarray(q)
+        for c, im in enumerate(cols):
+            assert lib.orc_muscle_length_speed(nlp.ctx, im, abi.dptr(q), abi.dptr(np.zeros(rep.nq)),
+                                               abi.dptr(out)) == 0
+            L[i, c] = out[0]
+    Lg = CubicSpline(t, L, axis=0)(gso[:, 0])
+    nfl = np.empty_like(Lg)
+    for c, im in enumerate(cols):
+        mu = m.muscles[im]
+        w = mu.optimal_fiber_length * math.sin(mu.pennation_angle_at_optimal)
+        nfl[:, c] = np.sqrt((Lg[:, c] - mu.tendon_slack_length) ** 2 + w * w) / mu.optimal_fiber_length
+    return np.abs(nfl - gso[:, 1:])
