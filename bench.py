@@ -52,6 +52,10 @@ def parse():
                     help="separate: eval_g then eval_jac_g C-ABI calls; fused: one "
                          "mh_eval_g_jac_g call (IPOPT new_x=false pattern)")
     ap.add_argument("--multi", choices=["replicas", "mesh"], default="replicas")
+    ap.add_argument("--batch", type=int, default=8,
+                    help="also measure B independent NLPs per GPU evaluated concurrently, one "
+                         "context (HIP stream) and host thread each (the configs[4] batch layout); "
+                         "reported beside the headline, 0 = skip")
     return ap.parse_args()
 
 
@@ -156,6 +160,9 @@ def main():
 
     ms_per_step = 1e3 * elapsed / args.steps
     value = (args.steps if mesh else args.steps * world) / elapsed
+    batch = None
+    if args.batch > 1 and not mesh:
+        batch = batch_throughput(args, rep, st, local, rank, world, dev, torch, dist)
 
     if rank == 0:
         J = np.array(rec["jac"])          # [whole, DAE stage, transcription stage, k_groups] ms
@@ -221,11 +228,62 @@ def main():
             "cpu_baseline": cpu,
         }
         line[f"value_{other}"] = round((args.steps if mesh else args.steps * world) / other_elapsed, 3)
+        if batch:
+            line["batch"] = batch
         if cpu and cpu.get("value"):
             line["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 2)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def batch_throughput(args, rep, st, local, rank, world, dev, torch, dist):
+    """B independent NLPs of the same workload per GPU (different iterates),
+    each on its own context / HIP stream and driven by its own host thread
+    (ctypes releases the GIL inside the C ABI calls): aggregate eval_g +
+    eval_jac_g calls/s over all NLPs and ranks."""
+    from concurrent.futures import ThreadPoolExecutor
+    from mocohip.solver import HipNLP
+    B = args.batch
+    items = []
+    for b in range(B):
+        nlp = HipNLP(rep, st.solver.options())
+        x = nlp.random_iterate(np.random.default_rng(1000 + rank * B + b).uniform(-1, 1, nlp.n))
+        xm = nlp.initial_guess_from_bounds()
+        x[2:2 + nlp.NS * nlp.G] = xm[2:2 + nlp.NS * nlp.G]
+        xd = torch.tensor(x, dtype=torch.float64, device=dev)
+        gd = torch.zeros(nlp.m, dtype=torch.float64, device=dev)
+        vd = torch.zeros(nlp.nnz, dtype=torch.float64, device=dev)
+        items.append((nlp, xd, gd, vd))
+
+    def run(item, k):
+        nlp, xd, gd, vd = item
+        for _ in range(k):
+            if args.mode == "fused":
+                nlp.eval_g_jac_g_device(xd.data_ptr(), gd.data_ptr(), vd.data_ptr())
+            else:
+                nlp.eval_g_device(xd.data_ptr(), gd.data_ptr())
+                nlp.eval_jac_g_device(xd.data_ptr(), vd.data_ptr())
+
+    with ThreadPoolExecutor(B) as pool:
+        list(pool.map(lambda it: run(it, args.warmup), items))
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        list(pool.map(lambda it: run(it, args.steps), items))
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    for nlp, *_ in items:
+        nlp.close()
+    return {"nlps_per_gpu": B, "value": round(B * world * args.steps / el, 3), "unit": "calls/s",
+            "mode": args.mode, "layout": "one context (HIP stream) + host thread per NLP"}
 
 
 def cpu_baseline(rep, opts, x, budget_s):
