@@ -262,8 +262,21 @@ typedef struct mh_options {
     int32_t interval_begin;
     int32_t interval_end;
     int32_t device;                      /* HIP device ordinal               */
-    int32_t reserved;
+    /* MocoDirectCollocationSolver multibody_dynamics_mode
+     * (MocoDirectCollocationSolver.h:96-153): MH_DYNAMICS_EXPLICIT, or
+     * MH_DYNAMICS_IMPLICIT = generalized accelerations are NLP variables
+     * ("derivatives", CasOCTranscription.cpp:134-135, bounds :222-226) and
+     * the multibody equations are residual constraints at every grid point
+     * (findMotionForces, MocoCasOCProblem.h:245-297;
+     * CasOCTranscription.cpp:335-378; rows placed by flattenConstraints,
+     * CasOCTranscription.h:219-313). */
+    int32_t multibody_dynamics_mode;
+    /* implicit_multibody_acceleration_bounds; {0, 0} = the reference default
+     * [-1000, 1000] (MocoDirectCollocationSolver.cpp:39-40). */
+    double implicit_accel_bounds[2];
 } mh_options;
+
+enum mh_dynamics_mode { MH_DYNAMICS_EXPLICIT = 0, MH_DYNAMICS_IMPLICIT = 1 };
 
 typedef struct mh_ctx mh_ctx;
 
@@ -275,7 +288,9 @@ typedef struct mh_nlp_info {
     int64_t nnz_h_lag;   /* 0: limited-memory Hessian                        */
     int64_t num_grid_points;
     int64_t num_states, num_controls;
-    /* shard: rows [row_begin,row_end) and nonzeros [nnz_begin,nnz_end)     */
+    /* shard: rows [row_begin,row_end) and nonzeros [nnz_begin,nnz_end).
+     * Implicit mode adds the residual rows of the final grid point after the
+     * last interval; the shard owning the last interval owns them too.     */
     int64_t row_begin, row_end;
     int64_t nnz_begin, nnz_end;
 } mh_nlp_info;
@@ -318,10 +333,12 @@ int mh_eval_g_jac_g(mh_ctx* ctx, const double* x, double* g, double* values);
 int mh_eval_g_jac_g_device(mh_ctx* ctx, const double* x_dev, double* g_dev,
         double* values_dev);
 
-/* Per-point DAE probe (CasOC::Problem::calcMultibodySystemExplicit,
- * CasOCProblem.h:313-332) evaluated on the device for npoints inputs laid
- * out as [time, states(NS), controls(NC)] per point; outputs
- * [udot(NQ), zdot(NZ)] per point.  Used by parity tests. */
+/* Per-point DAE probe (CasOC::Problem::calcMultibodySystemExplicit /
+ * calcMultibodySystemImplicit, CasOCProblem.h:313-332) evaluated on the
+ * device for npoints inputs laid out as [time, states(NS), controls(NC)]
+ * (+ [udot(NQ)] in implicit mode) per point; outputs [udot(NQ), zdot(NZ)]
+ * (implicit: [multibody residual(NQ), zdot(NZ)]) per point.  Used by
+ * parity tests. */
 int mh_eval_dae(mh_ctx* ctx, int32_t npoints, const double* inputs,
         double* outputs);
 

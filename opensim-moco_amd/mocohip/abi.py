@@ -21,6 +21,7 @@ MH_ACT_MUSCLE, MH_ACT_COORDINATE = 0, 1
 MH_GOAL_CONTROL, MH_GOAL_STATE_TRACKING, MH_GOAL_FINAL_TIME, \
     MH_GOAL_SUM_SQUARED_STATE = 0, 1, 2, 3
 MH_HERMITE_SIMPSON, MH_TRAPEZOIDAL = 0, 1
+MH_DYNAMICS_EXPLICIT, MH_DYNAMICS_IMPLICIT = 0, 1
 MH_FD_CENTRAL, MH_FD_FORWARD, MH_FD_BACKWARD = 0, 1, 2
 
 i32 = C.c_int32
@@ -127,7 +128,8 @@ class mh_options(C.Structure):
                 ("interpolate_control_midpoints", i32),
                 ("finite_difference_scheme", i32), ("fd_step", f64),
                 ("interval_begin", i32), ("interval_end", i32),
-                ("device", i32), ("reserved", i32)]
+                ("device", i32), ("multibody_dynamics_mode", i32),
+                ("implicit_accel_bounds", f64 * 2)]
 
 
 class mh_nlp_info(C.Structure):

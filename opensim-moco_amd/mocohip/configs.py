@@ -31,7 +31,7 @@ from .solver import MocoHipSolver, MocoStudy
 DATA = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data")
 
 
-def sliding_mass(num_mesh_intervals: int = 50) -> MocoStudy:
+def sliding_mass(num_mesh_intervals: int = 50, dynamics: str = "explicit") -> MocoStudy:
     m = Model("sliding_mass", gravity=(0, 0, 0))
     m.add_body(Body("body", 2.0, (0, 0, 0), (0, 0, 0, 0, 0, 0)))
     pos = Coordinate("position", (-math.inf, math.inf), "translational", path="/slider/position")
@@ -43,7 +43,7 @@ def sliding_mass(num_mesh_intervals: int = 50) -> MocoStudy:
     p.set_state_info("/slider/position/speed", (-50, 50), 0, 0)
     p.set_control_info("/actuator", (-50, 50))
     p.add_goal(MocoFinalTimeGoal())
-    s = MocoHipSolver(num_mesh_intervals=num_mesh_intervals)
+    s = MocoHipSolver(num_mesh_intervals=num_mesh_intervals, multibody_dynamics_mode=dynamics)
     return MocoStudy(p, s)
 
 
@@ -61,7 +61,9 @@ def n_link_pendulum(num_links: int) -> Model:
     return m
 
 
-def double_pendulum(num_mesh_intervals: int = 100, scheme: str = "hermite-simpson") -> MocoStudy:
+def double_pendulum(num_mesh_intervals: int = 100, scheme: str = "hermite-simpson",
+                    dynamics: str = "explicit") -> MocoStudy:
+    """testImplicit.cpp:63-75 solves this problem in both dynamics modes."""
     m = n_link_pendulum(2)
     p = MocoProblem(m)
     p.set_time_bounds(0.0, (0.0, 5.0))
@@ -73,7 +75,8 @@ def double_pendulum(num_mesh_intervals: int = 100, scheme: str = "hermite-simpso
     p.set_control_info("/tau1", (-100, 100))
     p.add_goal(MocoFinalTimeGoal(weight=0.001))
     p.add_goal(MocoControlGoal(weight=1e-3))
-    s = MocoHipSolver(num_mesh_intervals=num_mesh_intervals, transcription_scheme=scheme)
+    s = MocoHipSolver(num_mesh_intervals=num_mesh_intervals, transcription_scheme=scheme,
+                      multibody_dynamics_mode=dynamics)
     return MocoStudy(p, s)
 
 
@@ -107,7 +110,7 @@ def gait10dof18musc_model(muscles: bool = True, tendon_compliance: bool = False,
 
 def gait10dof18musc(num_mesh_intervals: int = 200, muscles: bool = True,
                     tendon_compliance: bool = False,
-                    fd_scheme: str = "forward") -> MocoStudy:
+                    fd_scheme: str = "forward", dynamics: str = "explicit") -> MocoStudy:
     """MocoTrack gait10dof18musc (config 3).  MocoTrack: states tracking goal
     (weight 1, GCVSpline reference), control effort goal (0.001), time
     [0.01, 1.3], explicit dynamics, forward FD (MocoTrack.cpp:54-132)."""
@@ -121,7 +124,7 @@ def gait10dof18musc(num_mesh_intervals: int = 200, muscles: bool = True,
     p.add_goal(MocoControlGoal("control_effort", 0.001))
     p.set_time_bounds(0.01, 1.3)
     s = MocoHipSolver(num_mesh_intervals=num_mesh_intervals,
-                      optim_finite_difference_scheme=fd_scheme)
+                      optim_finite_difference_scheme=fd_scheme, multibody_dynamics_mode=dynamics)
     return MocoStudy(p, s)
 
 

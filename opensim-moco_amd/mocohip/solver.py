@@ -38,6 +38,9 @@ class MocoHipSolver:
     optim_sparsity_detection: str = "none"
     fd_step: float = 1e-8
     device: int = 0
+    # MocoDirectCollocationSolver implicit_multibody_acceleration_bounds
+    # (default [-1000, 1000], MocoDirectCollocationSolver.cpp:39-40)
+    implicit_multibody_acceleration_bounds: tuple = (-1000.0, 1000.0)
 
     def options(self, interval_begin: int = 0, interval_end: int = 0) -> abi.mh_options:
         if self.transcription_scheme not in _SCHEMES:
@@ -46,8 +49,8 @@ class MocoHipSolver:
         if self.optim_finite_difference_scheme not in _FD:
             raise ValueError("optim_finite_difference_scheme must be one of "
                              "central, forward, backward")
-        if self.multibody_dynamics_mode != "explicit":
-            raise NotImplementedError("implicit multibody dynamics: not yet on the HIP path")
+        if self.multibody_dynamics_mode not in ("explicit", "implicit"):
+            raise ValueError("multibody_dynamics_mode must be 'explicit' or 'implicit'")
         if self.optim_sparsity_detection != "none":
             raise NotImplementedError("sparsity detection: not yet on the HIP path")
         o = abi.mh_options()
@@ -59,6 +62,11 @@ class MocoHipSolver:
         o.interval_begin = int(interval_begin)
         o.interval_end = int(interval_end)
         o.device = int(self.device)
+        o.multibody_dynamics_mode = (abi.MH_DYNAMICS_IMPLICIT if self.multibody_dynamics_mode == "implicit"
+                                     else abi.MH_DYNAMICS_EXPLICIT)
+        lo, hi = self.implicit_multibody_acceleration_bounds
+        o.implicit_accel_bounds[0] = float(lo)
+        o.implicit_accel_bounds[1] = float(hi)
         return o
 
 
@@ -130,10 +138,17 @@ class _NLPBase:
         self._check(self._fn("get_jac_structure")(self.ctx, abi.iptr(ir), abi.iptr(jc)))
         return ir[:self.nnz], jc[:self.nnz]
 
+    @property
+    def NDV(self) -> int:
+        """Derivative variables per grid point (implicit mode: NQ)."""
+        return self.NQ if self.opts.multibody_dynamics_mode == abi.MH_DYNAMICS_IMPLICIT else 0
+
     def eval_dae(self, inputs: np.ndarray) -> np.ndarray:
+        """Per-point DAE: rows [t, states, controls(, accelerations)] ->
+        [udot or multibody residual, zdot]."""
         inputs = np.ascontiguousarray(inputs, float)
         npts = inputs.shape[0]
-        assert inputs.shape[1] == 1 + self.NS + self.NC
+        assert inputs.shape[1] == 1 + self.NS + self.NC + self.NDV
         out = np.empty((npts, self.NS - self.NQ))
         self._check(self._fn("eval_dae")(self.ctx, npts, abi.dptr(inputs), abi.dptr(out)))
         return out

@@ -236,6 +236,9 @@ struct orc_ctx {
     double* gw;
     /* derived sizes */
     int NQ, NZ, NS, NC, NP; /* NP = per-point inputs excluding time */
+    int implicit;           /* MH_DYNAMICS_IMPLICIT                     */
+    int NDV;                /* derivative variables per grid point      */
+    double acc_lo, acc_hi;  /* implicit multibody acceleration bounds   */
     int* mus_act_state;     /* state index of activation (-1)          */
     int* mus_ftn_state;     /* state index of normalized tendon force   */
     int* mus_control;       /* control index of excitation (-1)        */
@@ -268,12 +271,20 @@ static int64_t col_state(const orc_ctx* c, int k, int s) { return 2 + (int64_t)k
 static int64_t col_control(const orc_ctx* c, int k, int j) {
     return 2 + (int64_t)c->NS * c->G + (int64_t)k * c->NC + j;
 }
+/* implicit mode: generalized accelerations ("derivatives" variables, sorted
+ * after controls and (empty) multipliers / slacks, CasOCIterate.h:27-44) */
+static int64_t col_deriv(const orc_ctx* c, int k, int j) {
+    return 2 + (int64_t)(c->NS + c->NC) * c->G + (int64_t)k * c->NDV + j;
+}
+/* multibody residual rows per grid point (implicit mode) */
+static int nres(const orc_ctx* c) { return c->implicit ? c->NQ : 0; }
 
 /* Sorted columns of all point inputs at grid point k (excluding t0/tf). */
 static int point_cols(const orc_ctx* c, int k, int64_t* out) {
     int n = 0;
     for (int s = 0; s < c->NS; ++s) out[n++] = col_state(c, k, s);
     for (int j = 0; j < c->NC; ++j) out[n++] = col_control(c, k, j);
+    for (int j = 0; j < c->NDV; ++j) out[n++] = col_deriv(c, k, j);
     return n;
 }
 
@@ -285,12 +296,33 @@ static int cmp64(const void* a, const void* b) {
 /* Emits the sorted column set of every row of interval i, in row order.
  * emit(row_local, cols, ncols). Returns rows per interval. */
 typedef void (*row_fn)(void* ud, int64_t row, const int64_t* cols, int ncols);
+/* Multibody residual rows of grid point k (implicit mode): the callback
+ * output depends on every input of the point and on the time. */
+static int64_t residual_rows(const orc_ctx* c, int k, int64_t row, row_fn emit, void* ud,
+        int64_t* cols) {
+    for (int o = 0; o < nres(c); ++o) {
+        int n = 0;
+        cols[n++] = 0; cols[n++] = 1;
+        n += point_cols(c, k, cols + n);
+        emit(ud, row++, cols, n);
+    }
+    return row;
+}
+/* Implicit mode: the speed rows (NQ <= s < 2NQ) have udot = the derivative
+ * variable, a direct MX expression (CasOCTranscription.cpp:339-341), so they
+ * depend on the point's own state s and derivative s - NQ only. */
+static int speed_row_sparse(const orc_ctx* c, int s) { return c->implicit && s >= c->NQ && s < 2 * c->NQ; }
+
 static void interval_rows(const orc_ctx* c, int i, int64_t row0, row_fn emit, void* ud) {
     int NQ = c->NQ, NS = c->NS, NC = c->NC;
-    int64_t* cols = (int64_t*)malloc(sizeof(int64_t) * (size_t)(3 * (NS + NC) + 8));
+    int64_t* cols = (int64_t*)malloc(sizeof(int64_t) * (size_t)(3 * (NS + NC + c->NDV) + 8));
     int64_t row = row0;
     if (c->scheme == MH_HERMITE_SIMPSON) {
         int ki = 2 * i, km = 2 * i + 1, kp = 2 * i + 2;
+        /* flattenConstraints: residuals of the interval's grid points before
+         * its defects (CasOCTranscription.h:290-300) */
+        row = residual_rows(c, ki, row, emit, ud, cols);
+        row = residual_rows(c, km, row, emit, ud, cols);
         /* Hermite rows, then Simpson rows (CasOCHermiteSimpson.cpp:79-84). */
         for (int pass = 0; pass < 2; ++pass) {
             for (int s = 0; s < NS; ++s) {
@@ -306,6 +338,17 @@ static void interval_rows(const orc_ctx* c, int i, int64_t row0, row_fn emit, vo
                         cols[n++] = col_state(c, ki, s); cols[n++] = col_state(c, kp, s);
                         cols[n++] = col_state(c, ki, NQ + s); cols[n++] = col_state(c, km, NQ + s);
                         cols[n++] = col_state(c, kp, NQ + s);
+                    }
+                } else if (speed_row_sparse(c, s)) {
+                    int j = s - NQ;
+                    if (pass == 0) {
+                        cols[n++] = col_state(c, km, s);
+                        cols[n++] = col_state(c, ki, s); cols[n++] = col_state(c, kp, s);
+                        cols[n++] = col_deriv(c, ki, j); cols[n++] = col_deriv(c, kp, j);
+                    } else {
+                        cols[n++] = col_state(c, ki, s); cols[n++] = col_state(c, kp, s);
+                        cols[n++] = col_deriv(c, ki, j); cols[n++] = col_deriv(c, km, j);
+                        cols[n++] = col_deriv(c, kp, j);
                     }
                 } else {
                     if (pass == 0) {
@@ -331,12 +374,16 @@ static void interval_rows(const orc_ctx* c, int i, int64_t row0, row_fn emit, vo
         }
     } else { /* trapezoidal (CasOCTrapezoidal.cpp:43-59) */
         int ki = i, kp = i + 1;
+        row = residual_rows(c, ki, row, emit, ud, cols);
         for (int s = 0; s < NS; ++s) {
             int n = 0;
             cols[n++] = 0; cols[n++] = 1;
             if (s < NQ) {
                 cols[n++] = col_state(c, ki, s); cols[n++] = col_state(c, kp, s);
                 cols[n++] = col_state(c, ki, NQ + s); cols[n++] = col_state(c, kp, NQ + s);
+            } else if (speed_row_sparse(c, s)) {
+                cols[n++] = col_state(c, ki, s); cols[n++] = col_state(c, kp, s);
+                cols[n++] = col_deriv(c, ki, s - NQ); cols[n++] = col_deriv(c, kp, s - NQ);
             } else {
                 n += point_cols(c, ki, cols + n);
                 n += point_cols(c, kp, cols + n);
@@ -363,7 +410,15 @@ static void emit_fill(void* ud, int64_t row, const int64_t* cols, int n) {
 }
 static int rows_per_interval(const orc_ctx* c) {
     return 2 * c->NS * (c->scheme == MH_HERMITE_SIMPSON) + c->NS * (c->scheme == MH_TRAPEZOIDAL) +
-           (c->scheme == MH_HERMITE_SIMPSON && c->interp ? c->NC : 0);
+           (c->scheme == MH_HERMITE_SIMPSON && c->interp ? c->NC : 0) +
+           nres(c) * (c->scheme == MH_HERMITE_SIMPSON ? 2 : 1);
+}
+/* residual rows of the final grid point, after all intervals
+ * (CasOCTranscription.h:306-308) */
+static void tail_rows(const orc_ctx* c, int64_t row0, row_fn emit, void* ud) {
+    int64_t* cols = (int64_t*)malloc(sizeof(int64_t) * (size_t)(c->NS + c->NC + c->NDV + 4));
+    residual_rows(c, c->G - 1, row0, emit, ud, cols);
+    free(cols);
 }
 
 int orc_create(const mh_problem* p, const mh_options* o, orc_ctx** out) {
@@ -434,7 +489,18 @@ int orc_create(const mh_problem* p, const mh_options* o, orc_ctx** out) {
     c->NS = z;
     c->NZ = z - 2 * c->NQ;
     c->NC = M->nactuators;
-    c->NP = c->NS + c->NC;
+    c->implicit = o->multibody_dynamics_mode == MH_DYNAMICS_IMPLICIT;
+    if (o->multibody_dynamics_mode != MH_DYNAMICS_EXPLICIT && !c->implicit) {
+        orc_destroy(c);
+        return fail(MH_ERR_INVALID, "unknown multibody dynamics mode %d", o->multibody_dynamics_mode);
+    }
+    c->NDV = c->implicit ? c->NQ : 0;
+    c->acc_lo = -1000.0; c->acc_hi = 1000.0;
+    if (o->implicit_accel_bounds[0] != 0.0 || o->implicit_accel_bounds[1] != 0.0) {
+        c->acc_lo = o->implicit_accel_bounds[0];
+        c->acc_hi = o->implicit_accel_bounds[1];
+    }
+    c->NP = c->NS + c->NC + c->NDV;
     for (int ia = 0; ia < M->nactuators; ++ia) {
         if (c->acts[ia].kind == MH_ACT_MUSCLE) {
             int t = c->acts[ia].target;
@@ -499,17 +565,19 @@ int orc_create(const mh_problem* p, const mh_options* o, orc_ctx** out) {
         }
     }
     free(mesh);
-    c->n = 2 + (int64_t)(c->NS + c->NC) * c->G;
-    c->m = (int64_t)rows_per_interval(c) * c->N;
+    c->n = 2 + (int64_t)(c->NS + c->NC + c->NDV) * c->G;
+    c->m = (int64_t)rows_per_interval(c) * c->N + nres(c);
     /* structure */
     emit_state e = {0, NULL, NULL};
     for (int i = 0; i < c->N; ++i) interval_rows(c, i, 0, emit_count, &e);
+    tail_rows(c, 0, emit_count, &e);
     c->nnz = e.count;
     c->iRow = (int32_t*)malloc(sizeof(int32_t) * (size_t)(c->nnz + 1));
     c->jCol = (int32_t*)malloc(sizeof(int32_t) * (size_t)(c->nnz + 1));
     e.count = 0; e.ir = c->iRow; e.jc = c->jCol;
     int rpi = rows_per_interval(c);
     for (int i = 0; i < c->N; ++i) interval_rows(c, i, (int64_t)i * rpi, emit_fill, &e);
+    tail_rows(c, (int64_t)c->N * rpi, emit_fill, &e);
     c->fd = o->finite_difference_scheme;
     c->h = o->fd_step > 0 ? o->fd_step : 1e-8;
     *out = c;
@@ -574,7 +642,10 @@ int orc_get_bounds(const orc_ctx* c, double* xl, double* xu, double* gl, double*
         set_bounds(ib, &xl[col_control(c, 0, j)], &xu[col_control(c, 0, j)]);
         set_bounds(fb, &xl[col_control(c, c->G - 1, j)], &xu[col_control(c, c->G - 1, j)]);
     }
-    /* defects and interpolating-control rows: equality to 0
+    /* implicit: accelerations at every grid point (CasOCTranscription.cpp:222-226) */
+    for (int j = 0; j < c->NDV; ++j)
+        for (int k = 0; k < c->G; ++k) { xl[col_deriv(c, k, j)] = c->acc_lo; xu[col_deriv(c, k, j)] = c->acc_hi; }
+    /* defects, residuals and interpolating-control rows: equality to 0
      * (CasOCTranscription.cpp:275-278, 440-443) */
     if (gl) for (int64_t r = 0; r < c->m; ++r) { gl[r] = 0.0; gu[r] = 0.0; }
     return MH_OK;
@@ -830,7 +901,8 @@ static void ws_free(dae_ws* w) {
 /* Forward kinematics, velocities and velocity-product accelerations in the
  * ground frame (Simbody realizePosition/Velocity for FunctionBased
  * mobilizers; restated).  Body index b is stored at b+1; slot 0 = ground. */
-static void kinematics(const orc_ctx* c, const real* q, const real* u, dae_ws* w) {
+/* wacc: generalized accelerations (implicit mode) or NULL (bias only). */
+static void kinematics(const orc_ctx* c, const real* q, const real* u, const real* wacc, dae_ws* w) {
     const mh_model* Mo = &c->P.model;
     static const double I3[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
     memcpy(w->R, I3, sizeof I3);
@@ -880,6 +952,7 @@ static void kinematics(const orc_ctx* c, const real* q, const real* u, dae_ws* w
             mat_vec(RGF, dir, s.v);
             sv6 sd = cross_m(Vpar, s);
             real thd = fv[1] * uj, thdd = fv[2] * uj * uj;
+            if (wacc) thdd += fv[1] * wacc[F->coord];
             for (int i = 0; i < 3; ++i) {
                 V.w[i] += s.w[i] * thd; V.v[i] += s.v[i] * thd;
                 A.w[i] += sd.w[i] * thd + s.w[i] * thdd;
@@ -906,6 +979,7 @@ static void kinematics(const orc_ctx* c, const real* q, const real* u, dae_ws* w
                 sv6 sd = cross_m(V, s);
                 real uj = u[F->coord];
                 real thd = fv[1] * uj, thdd = fv[2] * uj * uj;
+                if (wacc) thdd += fv[1] * wacc[F->coord];
                 for (int i = 0; i < 3; ++i) {
                     V.w[i] += s.w[i] * thd; V.v[i] += s.v[i] * thd;
                     A.w[i] += sd.w[i] * thd + s.w[i] * thdd;
@@ -1021,13 +1095,20 @@ static void apply_point_force(const orc_ctx* c, dae_ws* w, const real* q, int i,
 
 /* The explicit per-point DAE (MocoCasOCProblem::calcMultibodySystemExplicit,
  * MocoCasOCProblem.h:203-244): time, states, controls -> udot, zdot. */
+/* One grid point: inputs x (states), ctrl (controls) and, in implicit mode,
+ * the generalized accelerations ctrl + NC.  Outputs [udot, zdot] (explicit,
+ * MocoCasOCProblem.h:203-244) or [residual, zdot] (implicit,
+ * MocoCasOCProblem.h:245-297: residual = the mobility forces
+ * findMotionForces needs for udot = w, i.e. M w + C - f_applied, computed by
+ * RNEA with the accelerations included). */
 static void eval_dae_point(const orc_ctx* c, dae_ws* w, real time, const real* x,
         const real* ctrl, real* out) {
     const mh_model* Mo = &c->P.model;
     int NQ = c->NQ;
     const real* q = x;
     const real* u = x + NQ;
-    kinematics(c, q, u, w);
+    const real* wacc = c->implicit ? ctrl + c->NC : NULL;
+    kinematics(c, q, u, wacc, w);
     path_points(c, q, u, w);
     /* Body inertias in ground about the origin; RNEA body forces. */
     for (int b = 0; b < Mo->nbodies; ++b) {
@@ -1126,6 +1207,10 @@ static void eval_dae_point(const orc_ctx* c, dae_ws* w, real time, const real* x
         }
     }
     for (int j = 0; j < NQ; ++j) w->tau[j] -= sv_dot(w->S[j], w->F[c->coord_body[j] + 1]);
+    if (wacc) {
+        for (int j = 0; j < NQ; ++j) out[j] = -w->tau[j];
+        return;
+    }
     /* CRBA mass matrix. */
     for (int b = Mo->nbodies - 1; b >= 0; --b) {
         int bs = b + 1, ps = c->bodies[b].parent + 1;
@@ -1187,7 +1272,7 @@ int orc_muscle_length_speed(orc_ctx* c, int im, const double* q, const double* u
     if (im < 0 || im >= c->P.model.nmuscles) return fail(MH_ERR_INVALID, "bad muscle");
     dae_ws w;
     ws_alloc(c, &w);
-    kinematics(c, q, u, &w);
+    kinematics(c, q, u, NULL, &w);
     path_points(c, q, u, &w);
     muscle_length_speed(c, &w, im, &out[0], &out[1]);
     ws_free(&w);
@@ -1195,7 +1280,7 @@ int orc_muscle_length_speed(orc_ctx* c, int im, const double* q, const double* u
 }
 
 int orc_eval_dae(orc_ctx* c, int32_t np, const double* in, double* out) {
-    int NI = 1 + c->NS + c->NC, NO = c->NQ + c->NZ;
+    int NI = 1 + c->NP, NO = c->NQ + c->NZ;
 #pragma omp parallel num_threads(c->nthreads)
     {
         dae_ws w;
@@ -1219,27 +1304,38 @@ static void times_of(const orc_ctx* c, const double* x, double* t) {
     for (int k = 0; k < c->G; ++k) t[k] = (tf - t0) * c->grid[k] + t0;
 }
 
+/* st: states; ct: controls followed (implicit) by the accelerations */
 static void gather_point(const orc_ctx* c, const double* x, int k, double* st, double* ct) {
     memcpy(st, x + col_state(c, k, 0), sizeof(double) * (size_t)c->NS);
     if (c->NC) memcpy(ct, x + col_control(c, k, 0), sizeof(double) * (size_t)c->NC);
+    if (c->NDV) memcpy(ct + c->NC, x + col_deriv(c, k, 0), sizeof(double) * (size_t)c->NDV);
 }
 
-/* xdot at all grid points: qdot = u (CasOCTranscription.cpp:313-314) and
- * callback outputs for the rest. xd: NS x G (grid-major). */
-static void all_xdot(orc_ctx* c, const double* x, const double* times, double* xd) {
-    int NS = c->NS, NC = c->NC, NQ = c->NQ;
+/* xdot at all grid points: qdot = u (CasOCTranscription.cpp:313-314),
+ * udot = the derivative variables in implicit mode (:339-341), callback
+ * outputs for the rest. xd: NS x G (grid-major); res: NQ x G multibody
+ * residuals (implicit mode, else unused). */
+static void all_xdot(orc_ctx* c, const double* x, const double* times, double* xd, double* res) {
+    int NS = c->NS, NC = c->NC, NQ = c->NQ, NO = c->NQ + c->NZ;
 #pragma omp parallel num_threads(c->nthreads)
     {
         dae_ws w;
         ws_alloc(c, &w);
-        double* st = (double*)malloc(sizeof(double) * (size_t)(NS + NC + 1));
+        double* st = (double*)malloc(sizeof(double) * (size_t)(c->NP + NO + 1));
         double* ct = st + NS;
+        double* y = ct + NC + c->NDV;
 #pragma omp for schedule(static)
         for (int k = 0; k < c->G; ++k) {
             gather_point(c, x, k, st, ct);
             double* o = xd + (int64_t)k * NS;
             for (int j = 0; j < NQ; ++j) o[j] = st[NQ + j];
-            eval_dae_point(c, &w, times[k], st, ct, o + NQ);
+            eval_dae_point(c, &w, times[k], st, ct, y);
+            if (c->implicit) {
+                for (int j = 0; j < NQ; ++j) { o[NQ + j] = ct[NC + j]; res[(int64_t)k * NQ + j] = y[j]; }
+            } else {
+                for (int j = 0; j < NQ; ++j) o[NQ + j] = y[j];
+            }
+            for (int z = 0; z < c->NZ; ++z) o[2 * NQ + z] = y[NQ + z];
         }
         free(st);
         ws_free(&w);
@@ -1247,14 +1343,21 @@ static void all_xdot(orc_ctx* c, const double* x, const double* times, double* x
 }
 
 int orc_eval_g(orc_ctx* c, const double* x, double* g) {
-    int NS = c->NS, NC = c->NC;
+    int NS = c->NS, NC = c->NC, NR = nres(c);
     double* times = (double*)malloc(sizeof(double) * (size_t)c->G);
     double* xd = (double*)malloc(sizeof(double) * (size_t)c->G * (size_t)NS);
+    double* res = (double*)malloc(sizeof(double) * ((size_t)c->G * (size_t)NR + 1));
     times_of(c, x, times);
-    all_xdot(c, x, times, xd);
+    all_xdot(c, x, times, xd, res);
     int rpi = rows_per_interval(c);
     for (int i = 0; i < c->N; ++i) {
         double* gi = g + (int64_t)i * rpi;
+        /* residual rows of the interval's grid points first */
+        int npts = c->scheme == MH_HERMITE_SIMPSON ? 2 : 1;
+        int k0 = c->scheme == MH_HERMITE_SIMPSON ? 2 * i : i;
+        for (int p = 0; p < npts; ++p)
+            for (int o = 0; o < NR; ++o) gi[p * NR + o] = res[(int64_t)(k0 + p) * NR + o];
+        gi += npts * NR;
         if (c->scheme == MH_HERMITE_SIMPSON) {
             int ki = 2 * i, km = 2 * i + 1, kp = 2 * i + 2;
             double h = times[kp] - times[ki];
@@ -1282,8 +1385,10 @@ int orc_eval_g(orc_ctx* c, const double* x, double* g) {
             for (int s = 0; s < NS; ++s) gi[s] = xp[s] - (xi[s] + 0.5 * h * (fp[s] + fi[s]));
         }
     }
+    for (int o = 0; o < NR; ++o) g[(int64_t)c->N * rpi + o] = res[(int64_t)(c->G - 1) * NR + o];
     free(times);
     free(xd);
+    free(res);
     return MH_OK;
 }
 
@@ -1352,6 +1457,7 @@ static void fd_blocks(orc_ctx* c, const double* x, const double* times, double* 
 static double xdot_deriv(const orc_ctx* c, const double* D, int k, int s, int d) {
     int NQ = c->NQ, NO = c->NQ + c->NZ, ND = c->NP + 2;
     if (s < NQ) return (d == 2 + NQ + s) ? 1.0 : 0.0;
+    if (c->implicit && s < 2 * NQ) return (d == 2 + c->NS + c->NC + (s - NQ)) ? 1.0 : 0.0;
     return D[((int64_t)k * ND + d) * NO + (s - NQ)];
 }
 
@@ -1365,8 +1471,14 @@ static int col_to_dir(const orc_ctx* c, int64_t col, int* k) {
         return 2 + (int)(r % c->NS);
     }
     int64_t r = col - 2 - sblock;
-    *k = (int)(r / c->NC);
-    return 2 + c->NS + (int)(r % c->NC);
+    int64_t cblock = (int64_t)c->NC * c->G;
+    if (r < cblock) {
+        *k = (int)(r / c->NC);
+        return 2 + c->NS + (int)(r % c->NC);
+    }
+    r -= cblock;
+    *k = (int)(r / c->NDV);
+    return 2 + c->NS + c->NC + (int)(r % c->NDV);
 }
 
 int orc_eval_jac_g(orc_ctx* c, const double* x, double* values) {
@@ -1375,12 +1487,13 @@ int orc_eval_jac_g(orc_ctx* c, const double* x, double* values) {
     double* times = (double*)malloc(sizeof(double) * (size_t)c->G);
     double* xd = (double*)malloc(sizeof(double) * (size_t)c->G * (size_t)NS);
     double* D = (double*)malloc(sizeof(double) * (size_t)c->G * (size_t)ND * (size_t)NO);
+    int NR = nres(c);
+    double* res = (double*)malloc(sizeof(double) * ((size_t)c->G * (size_t)NR + 1));
     times_of(c, x, times);
-    all_xdot(c, x, times, xd);
+    all_xdot(c, x, times, xd, res);
     fd_blocks(c, x, times, D);
     int rpi = rows_per_interval(c);
-    double t0 = x[0], tf = x[1];
-    (void)t0; (void)tf;
+    int npts_res = c->scheme == MH_HERMITE_SIMPSON ? 2 : 1;
     for (int64_t e = 0; e < c->nnz; ++e) {
         int64_t row = c->iRow[e], col = c->jCol[e];
         int i = (int)(row / rpi);
@@ -1388,6 +1501,16 @@ int orc_eval_jac_g(orc_ctx* c, const double* x, double* values) {
         double v = 0.0;
         int kc;
         int dir = col_to_dir(c, col, &kc);
+        if (row >= (int64_t)c->N * rpi) {   /* residual of the final grid point */
+            values[e] = D[((int64_t)(c->G - 1) * ND + dir) * NO + (int)(row - (int64_t)c->N * rpi)];
+            continue;
+        }
+        if (rl < npts_res * NR) {           /* residual rows of the interval's points */
+            int kr = (c->scheme == MH_HERMITE_SIMPSON ? 2 * i : i) + rl / NR;
+            values[e] = D[((int64_t)kr * ND + dir) * NO + rl % NR];
+            continue;
+        }
+        rl -= npts_res * NR;
         if (c->scheme == MH_HERMITE_SIMPSON) {
             int ki = 2 * i, km = 2 * i + 1, kp = 2 * i + 2;
             double gi = c->grid[ki], gp = c->grid[kp];
@@ -1466,6 +1589,7 @@ int orc_eval_jac_g(orc_ctx* c, const double* x, double* values) {
     free(times);
     free(xd);
     free(D);
+    free(res);
     return MH_OK;
 }
 
@@ -1499,7 +1623,7 @@ static int goal_has_integral(const mh_goal* G) { return G->kind != MH_GOAL_FINAL
 
 int orc_eval_f(orc_ctx* c, const double* x, double* f) {
     double* times = (double*)malloc(sizeof(double) * (size_t)c->G);
-    double* st = (double*)malloc(sizeof(double) * (size_t)(c->NS + c->NC + 1));
+    double* st = (double*)malloc(sizeof(double) * (size_t)(c->NP + 1));
     double* ct = st + c->NS;
     times_of(c, x, times);
     double total = 0.0;
@@ -1562,7 +1686,8 @@ int orc_eval_grad_f(orc_ctx* c, const double* x, double* grad) {
                 if (d == 0) col = 0;
                 else if (d == 1) col = 1;
                 else if (idx < NS) col = col_state(c, k, idx);
-                else col = col_control(c, k, idx - NS);
+                else if (idx < NS + c->NC) col = col_control(c, k, idx - NS);
+                else col = col_deriv(c, k, idx - NS - c->NC);
                 grad[col] += wq * dL;
             }
         }

@@ -326,3 +326,88 @@ def _gso_errors(m):
         w = mu.optimal_fiber_length * math.sin(mu.pennation_angle_at_optimal)
         nfl[:, c] = np.sqrt((Lg[:, c] - mu.tendon_slack_length) ** 2 + w * w) / mu.optimal_fiber_length
     return np.abs(nfl - gso[:, 1:])
+
+
+# ---- implicit multibody dynamics ----------------------------
+
+@pytest.mark.parametrize("case", ["double_pendulum", "gait_rigid", "gait_compliant"])
+def test_implicit_residual_vanishes_at_explicit_accelerations(case):
+    """calcMultibodySystemImplicit (MocoCasOCProblem.h:245-297): the residual
+    findMotionForces returns is M w + C - f_applied, zero exactly when w is
+    the forward-dynamics udot; zdot is the same as in explicit mode."""
+    mk = {"double_pendulum": lambda d: configs.double_pendulum(3, dynamics=d),
+          "gait_rigid": lambda d: configs.gait10dof18musc(3, dynamics=d),
+          "gait_compliant": lambda d: configs.gait10dof18musc(3, tendon_compliance=True, dynamics=d)}[case]
+    ex = OracleNLP(mk("explicit").problem.create_rep(), mk("explicit").solver.options())
+    st = mk("implicit")
+    im = OracleNLP(st.problem.create_rep(), st.solver.options())
+    assert im.NDV == im.NQ and ex.NDV == 0
+    xm = ex.initial_guess_from_bounds()
+    rng = np.random.default_rng(11)
+    NQ, NS, NC = ex.NQ, ex.NS, ex.NC
+    for k in range(4):
+        s_ = xm[2 + k * NS:2 + (k + 1) * NS].copy()
+        s_[:2 * NQ] += rng.uniform(-0.2, 0.2, 2 * NQ)
+        c_ = rng.uniform(0.05, 0.5, NC)
+        P = np.concatenate([[0.3], s_, c_])[None, :]
+        y = ex.eval_dae(P)[0]
+        r = im.eval_dae(np.concatenate([P[0], y[:NQ]])[None, :])[0]
+        scale = 1.0 + np.abs(y[:NQ]).max()
+        assert np.abs(r[:NQ]).max() < 1e-9 * scale, r[:NQ]
+        assert np.array_equal(r[NQ:], y[NQ:])
+        w2 = y[:NQ] + 0.1
+        r2 = im.eval_dae(np.concatenate([P[0], w2])[None, :])[0]
+        assert np.abs(r2[:NQ]).max() > 1e-3
+
+
+@pytest.mark.parametrize("scheme", ["hermite-simpson", "trapezoidal"])
+def test_implicit_layout_bounds_and_structure(scheme):
+    """Derivative variables after the controls with [-1000, 1000] bounds
+    (CasOCTranscription.cpp:134-135,222-226); residual rows of each interval's
+    grid points before its defects and the final point's residual last
+    (CasOCTranscription.h:219-313); speed defects depend on the derivative
+    variables only (udot = w, :339-341)."""
+    N = 4
+    st = configs.double_pendulum(N, scheme, dynamics="implicit")
+    nlp = OracleNLP(st.problem.create_rep(), st.solver.options())
+    NQ, NS, NC, G = nlp.NQ, nlp.NS, nlp.NC, nlp.G
+    hs = scheme == "hermite-simpson"
+    assert nlp.n == 2 + (NS + NC + NQ) * G
+    rpi = (2 * NQ + 2 * NS + NC) if hs else (NQ + NS)
+    assert nlp.m == N * rpi + NQ
+    xl, xu, gl, gu = nlp.bounds()
+    d0 = 2 + (NS + NC) * G
+    assert np.all(xl[d0:] == -1000) and np.all(xu[d0:] == 1000)
+    ir, jc = nlp.jac_structure()
+    S = set(zip(ir.tolist(), jc.tolist()))
+    x = nlp.random_iterate(np.random.default_rng(1).uniform(-1, 1, nlp.n))
+    x[1] = 2.0
+    g0 = nlp.eval_g(x)
+    for j in range(nlp.n):
+        xp = x.copy()
+        xp[j] += 1e-3
+        for r in np.nonzero(nlp.eval_g(xp) != g0)[0]:
+            assert (int(r), j) in S
+    # residual rows at the final grid point depend on its inputs and the time
+    tail = set(jc[ir == nlp.m - 1].tolist())
+    assert {0, 1} <= tail and 2 + (G - 1) * NS in tail and d0 + (G - 1) * NQ in tail
+
+
+@pytest.mark.parametrize("scheme", ["hermite-simpson", "trapezoidal"])
+def test_implicit_jacobian_matches_numerical_derivative(scheme):
+    st = configs.double_pendulum(3, scheme, dynamics="implicit")
+    nlp = OracleNLP(st.problem.create_rep(), st.solver.options())
+    x = nlp.random_iterate(np.random.default_rng(2).uniform(-1, 1, nlp.n))
+    x[1] = 1.5
+    d0 = 2 + (nlp.NS + nlp.NC) * nlp.G
+    x[d0:] *= 1e-2      # accelerations of O(10): FD noise eps*|residual|/h stays < 1e-6
+    ir, jc = nlp.jac_structure()
+    J = np.zeros((nlp.m, nlp.n))
+    J[ir, jc] = nlp.eval_jac_g(x)
+    Jn = _numjac(nlp.eval_g, x, range(nlp.n))
+    # h = 1e-8 differences carry ~eps*|g|/h of rounding noise (|g| ~ 1e3 here)
+    noise = 100 * np.finfo(float).eps * np.abs(nlp.eval_g(x)).max() / st.solver.fd_step
+    assert np.allclose(J, Jn, rtol=1e-5, atol=max(1e-6, noise))
+    gf = nlp.eval_grad_f(x)
+    gn = _numjac(lambda z: np.array([nlp.eval_f(z)]), x, range(nlp.n))[0]
+    assert np.allclose(gf, gn, rtol=1e-6, atol=1e-7)
