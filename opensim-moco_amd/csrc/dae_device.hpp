@@ -21,6 +21,7 @@ namespace mh {
 
 struct DevModel {
     int nq, nb, nmus, nact, next, ns, nz, nc, no, np;
+    int implicit;   // MH_DYNAMICS_IMPLICIT: inputs carry udot after the controls
     double gravity[3];
     double tau_act, tau_deact;
     const mh_body* bodies;
@@ -291,14 +292,19 @@ struct Work {
 
 __device__ __forceinline__ int tri(int i, int j) { return i * (i + 1) / 2 + j; }  // i >= j
 
-// Full explicit DAE.  q,u,z packed in x (NS); controls in c (NC); outputs
-// [udot(NQ), zdot(NZ)] into out.
+// Full DAE.  q,u,z packed in x (NS); controls in c (NC), followed in
+// implicit mode by the generalized accelerations (NQ).  Outputs
+// [udot(NQ), zdot(NZ)] (explicit) or [residual(NQ), zdot(NZ)] (implicit:
+// residual = M udot + C - f_applied by RNEA with the accelerations, the
+// mobility forces Simbody's findMotionForces returns,
+// MocoCasOCProblem.h:245-297).
 template <int MB, int MQ, int MP>
 __device__ void dae_eval(const DevModel& M, Work<MB, MQ, MP>& w, double time, const double* x,
         const double* c, double* out) {
     const int NQ = M.nq;
     const double* q = x;
     const double* u = x + NQ;
+    const double* wacc = M.implicit ? c + M.nc : nullptr;
     // ---- kinematics + RNEA forward pass --------------------------------
     w.X[0] = Pose{{1, 0, 0, 0, 1, 0, 0, 0, 1}, {0, 0, 0}};
     w.V[0] = sv_zero();
@@ -342,7 +348,9 @@ __device__ void dae_eval(const DevModel& M, Work<MB, MQ, MP>& w, double time, co
             SV s = sv_zero();
             mv3(RGF, X.dir[0], X.dir[1], X.dir[2], s.v0, s.v1, s.v2);
             SV sd = crm(Vpar, s);
-            const double thd = d1 * uj, thdd = d2 * uj * uj;
+            const double thd = d1 * uj;
+            double thdd = d2 * uj * uj;
+            if (wacc) thdd += d1 * wacc[F.coord];
             V.v0 += s.v0 * thd; V.v1 += s.v1 * thd; V.v2 += s.v2 * thd;
             A.w0 += sd.w0 * thd; A.w1 += sd.w1 * thd; A.w2 += sd.w2 * thd;
             A.v0 += sd.v0 * thd + s.v0 * thdd; A.v1 += sd.v1 * thd + s.v1 * thdd;
@@ -365,7 +373,9 @@ __device__ void dae_eval(const DevModel& M, Work<MB, MQ, MP>& w, double time, co
                 cross3(oM0, oM1, oM2, s.w0, s.w1, s.w2, s.v0, s.v1, s.v2);
                 SV sd = crm(V, s);
                 const double uj = u[F.coord];
-                const double thd = d1 * uj, thdd = d2 * uj * uj;
+                const double thd = d1 * uj;
+                double thdd = d2 * uj * uj;
+                if (wacc) thdd += d1 * wacc[F.coord];
                 V.w0 += s.w0 * thd; V.w1 += s.w1 * thd; V.w2 += s.w2 * thd;
                 V.v0 += s.v0 * thd; V.v1 += s.v1 * thd; V.v2 += s.v2 * thd;
                 A.w0 += sd.w0 * thd + s.w0 * thdd; A.w1 += sd.w1 * thd + s.w1 * thdd;
@@ -557,6 +567,10 @@ __device__ void dae_eval(const DevModel& M, Work<MB, MQ, MP>& w, double time, co
         }
     }
     for (int j = 0; j < NQ; ++j) w.tau[j] -= svdot(w.S[j], w.F[M.coord_body[j] + 1]);
+    if (wacc) {
+        for (int j = 0; j < NQ; ++j) out[j] = -w.tau[j];
+        return;
+    }
     // ---- CRBA: composite inertias re-derived per body (reuse F slots is not
     //      possible; recompute the ground-frame inertia from the stored pose).
     RBI Ic[MB + 1];

@@ -78,7 +78,8 @@ extern "C" const char* mh_last_error(void) { return g_err.c_str(); }
 // ------------------------------------------------------------------------
 enum TplKind : uint8_t {
     T_HERM_T = 0, T_SIMP_T = 1, T_HERM_X = 2, T_SIMP_X = 3, T_INTERP = 4,
-    T_TRAP_T = 5, T_TRAP_X = 6
+    T_TRAP_T = 5, T_TRAP_X = 6,
+    T_RES = 7      // implicit multibody residual output s at point pt
 };
 struct TplEntry {
     int16_t row;   // row within the interval
@@ -88,18 +89,17 @@ struct TplEntry {
     int16_t s;     // state index of the row (defects) / control index (interp)
 };
 // 4-byte form of a template entry (staged in LDS by k_interval):
-// kind | pt << 3 | dir << 5 | row << 16; s is implied by the row.
+// kind | pt << 3 | dir << 5 | s << 16 (the row is not needed to evaluate it).
 __host__ __device__ __forceinline__ uint32_t tpl_pack(const TplEntry& e) {
-    return (uint32_t)e.kind | ((uint32_t)e.pt << 3) | ((uint32_t)e.dir << 5) | ((uint32_t)e.row << 16);
+    return (uint32_t)e.kind | ((uint32_t)e.pt << 3) | ((uint32_t)e.dir << 5) | ((uint32_t)e.s << 16);
 }
-__host__ __device__ __forceinline__ TplEntry tpl_unpack(uint32_t u, int NS, bool hs) {
+__host__ __device__ __forceinline__ TplEntry tpl_unpack(uint32_t u) {
     TplEntry e;
     e.kind = (uint8_t)(u & 7u);
     e.pt = (uint8_t)((u >> 3) & 3u);
     e.dir = (int16_t)((u >> 5) & 2047u);
-    const int r = (int)(u >> 16);
-    e.row = (int16_t)r;
-    e.s = (int16_t)(hs ? (r < NS ? r : (r < 2 * NS ? r - NS : r - 2 * NS)) : r);
+    e.row = 0;
+    e.s = (int16_t)(u >> 16);
     return e;
 }
 
@@ -125,10 +125,11 @@ struct GenericDae {
 };
 
 struct Layout {
-    int NS, NC, NQ, NO, NI;  // NI = NS + NC
+    int NS, NC, NQ, NO, NI;  // NI = NS + NC + NDV
     int G;                   // grid points (full problem)
     int k0;                  // first grid point of this shard
     int nk;                  // grid points in this shard
+    int NDV;                 // derivative variables per grid point (implicit: NQ)
 };
 
 // Per grid point the evaluation lanes are laid out as
@@ -150,11 +151,13 @@ __device__ __forceinline__ void load_point(const double* __restrict__ x, const L
         double (&in)[D::MI]) {
     const double* xs = x + 2 + (long)k * L.NS;
     const double* xc = x + 2 + (long)L.NS * L.G + (long)k * L.NC;
+    const double* xd = x + 2 + (long)(L.NS + L.NC) * L.G + (long)k * L.NDV;
 #pragma unroll
     for (int i = 0; i < D::MI; ++i) {
         double v = 0.0;
         if (i < L.NS) v = xs[i];
-        else if (i < L.NI) v = xc[i - L.NS];
+        else if (i < L.NS + L.NC) v = xc[i - L.NS];
+        else if (i < L.NI) v = xd[i - L.NS - L.NC];
         in[i] = v;
     }
 }
@@ -228,10 +231,11 @@ template <class D>
 struct LaneIn {
     const double* __restrict__ xs;
     const double* __restrict__ xc;
+    const double* __restrict__ xd;   // implicit: accelerations (inputs NS + NC ..)
     int pi;
     double step;
     __device__ __forceinline__ double operator[](int i) const {
-        const double v = i < D::NS ? xs[i] : xc[i - D::NS];
+        const double v = i < D::NS ? xs[i] : (i < D::NS + D::NC ? xc[i - D::NS] : xd[i - D::NS - D::NC]);
         return i == pi ? v + step : v;
     }
 };
@@ -250,10 +254,11 @@ template <class D>
 struct LaneInL {
     const lds_double* xs;
     const lds_double* xc;
+    const lds_double* xd;
     int pi;
     double step;
     __device__ __forceinline__ double operator[](int i) const {
-        const double v = i < D::NS ? xs[i] : xc[i - D::NS];
+        const double v = i < D::NS ? xs[i] : (i < D::NS + D::NC ? xc[i - D::NS] : xd[i - D::NS - D::NC]);
         return i == pi ? v + step : v;
     }
 };
@@ -283,10 +288,12 @@ __device__ __forceinline__ LaneIn<D> lane_input(const Src& S, const Lanes& Ln, i
     if (S.pts) {
         const double* p = S.pts + (long)kl * (1 + D::NI);
         t = p[0];
-        return LaneIn<D>{p + 1, p + 1 + D::NS, -1, 0.0};
+        return LaneIn<D>{p + 1, p + 1 + D::NS, p + 1 + D::NS + D::NC, -1, 0.0};
     }
     const int k = S.k0 + kl;
-    LaneIn<D> in{S.x + 2 + (long)k * D::NS, S.x + 2 + (long)D::NS * S.G + (long)k * D::NC, -1, 0.0};
+    constexpr int NDV = D::NI - D::NS - D::NC;
+    LaneIn<D> in{S.x + 2 + (long)k * D::NS, S.x + 2 + (long)D::NS * S.G + (long)k * D::NC,
+                 S.x + 2 + (long)(D::NS + D::NC) * S.G + (long)k * NDV, -1, 0.0};
     t = lane_time(Ln, S.grid[k], S.x[0], S.x[1], r, in.pi, in.step);
     return in;
 }
@@ -508,6 +515,14 @@ struct Interval {
     int ib;          // first interval of shard
     int rpi;         // rows per interval
     int nnz_int;     // nonzeros per interval
+    int nres;        // multibody residual rows per grid point (implicit: NQ)
+    int N;           // mesh intervals of the whole problem
+    int nnz_tail;    // nonzeros of the final grid point's residual rows
+    // The interval N-1 also owns the final grid point's residual rows
+    // (flattenConstraints, CasOCTranscription.h:306-308): rows rpi..rpi+nres
+    // after its own, template entries nnz_int.. nnz_int+nnz_tail.
+    __device__ __forceinline__ int rows(int i) const { return rpi + (i == N - 1 ? nres : 0); }
+    __device__ __forceinline__ int entries(int i) const { return nnz_int + (i == N - 1 ? nnz_tail : 0); }
 };
 
 __device__ __forceinline__ int grid_of(const Interval& I, int i, int pt) {
@@ -531,6 +546,10 @@ struct YG {
     __device__ __forceinline__ double xc(int k, int j) const {
         return x[2 + (long)NS * G + (long)k * NC + j];
     }
+    int NDV;
+    __device__ __forceinline__ double xd(int k, int j) const {
+        return x[2 + (long)(NS + NC) * G + (long)k * NDV + j];
+    }
     __device__ __forceinline__ const double* row(int k, int o) const {
         return Y + ((long)(k - k0) * NO + o) * stride;
     }
@@ -547,6 +566,9 @@ struct YS {
     int NS, NC;
     __device__ __forceinline__ double xs(int k, int s) const { return sxs[(k - kf) * NS + s]; }
     __device__ __forceinline__ double xc(int k, int j) const { return sxc[(k - kf) * NC + j]; }
+    const lds_double* sxd;
+    int NDV;
+    __device__ __forceinline__ double xd(int k, int j) const { return sxd[(k - kf) * NDV + j]; }
     __device__ __forceinline__ const lds_double* row(int k, int o) const {
         return Y + ((k - kf) * NO + o) * stride;
     }
@@ -558,6 +580,7 @@ template <class YV>
 __device__ __forceinline__ double xdot_at(const Layout& L, const Lanes& Ln,
         const double* __restrict__ x, const YV& Y, int k, int s) {
     if (s < L.NQ) return Y.xs(k, L.NQ + s);
+    if (L.NDV && s < 2 * L.NQ) return Y.xd(k, s - L.NQ);   // implicit: udot = w
     return Y.row(k, s - L.NQ)[Ln.base];
 }
 
@@ -565,6 +588,13 @@ template <class YV>
 __device__ __forceinline__ double defect_row(const Layout& L, const Interval& I, const Lanes& Ln,
         const double* __restrict__ x, const YV& Y, int i, int r) {
     const int NS = L.NS;
+    // residual rows: the interval's grid points (HS: 2, trapezoidal: 1), and
+    // for the last interval the final grid point after all its other rows
+    const int npres = I.scheme == MH_HERMITE_SIMPSON ? 2 : 1;
+    const int k_first = I.scheme == MH_HERMITE_SIMPSON ? 2 * i : i;
+    if (r < npres * I.nres) return Y.row(k_first + r / I.nres, r % I.nres)[Ln.base];
+    if (r >= I.rpi) return Y.row(k_first + npres, r - I.rpi)[Ln.base];
+    r -= npres * I.nres;
     if (I.scheme == MH_HERMITE_SIMPSON) {
         const int ki = 2 * i, km = ki + 1, kp = ki + 2;
         const double h = Y.t(kp) - Y.t(ki);
@@ -592,18 +622,26 @@ __device__ __forceinline__ double defect_row(const Layout& L, const Interval& I,
     return xp - (xi + 0.5 * h * (fp + fi));
 }
 
+// d (DAE output o) / d dir at grid point k (the finite-difference quotient).
+template <class YV>
+__device__ __forceinline__ double dout(const Lanes& Ln, const YV& Y, int k, int o, int dir) {
+    const auto y = Y.row(k, o);
+    if (Y.q) return y[dir];
+    if (Ln.fd == MH_FD_CENTRAL) return (y[dir] - y[Ln.ND + dir]) / (2.0 * Ln.h);
+    if (Ln.fd == MH_FD_FORWARD) return (y[dir] - y[Ln.base]) / Ln.h;
+    return (y[Ln.base] - y[dir]) / Ln.h;
+}
+
 // d xdot[s] / d dir at grid point k from the raw lane outputs
 // (CasADi FiniteDiff formulas: (f+ - f-)/2h, (f+ - f0)/h, (f0 - f-)/h).
 template <class YV>
 __device__ __forceinline__ double dxdot(const Layout& L, const Lanes& Ln, const YV& Y, int k, int s,
         int dir) {
     if (s < L.NQ) return dir == 2 + L.NQ + s ? 1.0 : 0.0;
-    const auto y = Y.row(k, s - L.NQ);
-    if (Y.q) return y[dir];
-    if (Ln.fd == MH_FD_CENTRAL) return (y[dir] - y[Ln.ND + dir]) / (2.0 * Ln.h);
-    if (Ln.fd == MH_FD_FORWARD) return (y[dir] - y[Ln.base]) / Ln.h;
-    return (y[Ln.base] - y[dir]) / Ln.h;
+    if (L.NDV && s < 2 * L.NQ) return dir == 2 + L.NS + L.NC + (s - L.NQ) ? 1.0 : 0.0;
+    return dout(Ln, Y, k, s - L.NQ, dir);
 }
+
 
 constexpr int ASM_CHUNK = 1024;   // nonzeros per assembly workgroup
 
@@ -660,6 +698,9 @@ __device__ __forceinline__ double jac_entry(const Layout& L, const Lanes& Ln,
     case T_INTERP:
         v = T.pt == 1 ? 1.0 : -0.5;
         break;
+    case T_RES:
+        v = dout(Ln, Y, k_first + T.pt, s, dir);
+        break;
     case T_TRAP_T: {
         const int ki = k_first, kp = k_first + 1;
         const double fi = xdot_at(L, Ln, x, Y, ki, s), fp = xdot_at(L, Ln, x, Y, kp, s);
@@ -695,18 +736,18 @@ __global__ void __launch_bounds__(256) k_transcribe(Layout L, Interval I, Lanes 
         int nchunks, int yq) {
     const int il = blockIdx.y;
     const int i = I.ib + il;
-    const YG YV{Y, times, L.NO, Ln.stride, L.k0, yq, x, L.NS, L.NC, L.G};
+    const YG YV{Y, times, L.NO, Ln.stride, L.k0, yq, x, L.NS, L.NC, L.G, L.NDV};
     if ((int)blockIdx.x < nchunks) {
         int k_first, k_last;
         interval_span(I, i, k_first, k_last);
         const IvC C = iv_const(YV.t(k_last) - YV.t(k_first), grid[k_last] - grid[k_first]);
         double* vi = values + (long)il * I.nnz_int;
-        const int e_end = min(I.nnz_int, ((int)blockIdx.x + 1) * ASM_CHUNK);
+        const int e_end = min(I.entries(i), ((int)blockIdx.x + 1) * ASM_CHUNK);
         for (int e = (int)blockIdx.x * ASM_CHUNK + threadIdx.x; e < e_end; e += blockDim.x)
             vi[e] = jac_entry(L, Ln, x, YV, tpl[e], k_first, C);
     } else {
         double* gi = g + (long)il * I.rpi;
-        for (int r = threadIdx.x; r < I.rpi; r += blockDim.x) gi[r] = defect_row(L, I, Ln, x, YV, i, r);
+        for (int r = threadIdx.x; r < I.rows(i); r += blockDim.x) gi[r] = defect_row(L, I, Ln, x, YV, i, r);
     }
 }
 
@@ -725,7 +766,7 @@ __global__ void __launch_bounds__(256) k_transcribe_gs(Layout L, Interval I, Lan
         const double* __restrict__ grid, const double* __restrict__ times,
         const double* __restrict__ Y, double* __restrict__ g, double* __restrict__ values,
         int nint, int yq) {
-    const YG YV{Y, times, L.NO, Ln.stride, L.k0, yq, x, L.NS, L.NC, L.G};
+    const YG YV{Y, times, L.NO, Ln.stride, L.k0, yq, x, L.NS, L.NC, L.G, L.NDV};
     const int nthreads = gridDim.x * blockDim.x;
     const int tid = blockIdx.x * blockDim.x + threadIdx.x;
     if (values) {
@@ -748,6 +789,21 @@ __global__ void __launch_bounds__(256) k_transcribe_gs(Layout L, Interval I, Lan
             const int il = div_exact(w, I.rpi, inv);
             g[w] = defect_row(L, I, Ln, x, YV, I.ib + il, w - il * I.rpi);
         }
+    }
+    // the final grid point's residual rows (implicit mode), owned by the
+    // shard holding the last interval
+    if (I.ib + nint == I.N && (I.nres > 0)) {
+        const int i = I.N - 1, il = nint - 1;
+        int k_first, k_last;
+        interval_span(I, i, k_first, k_last);
+        if (values) {
+            const IvC C = iv_const(YV.t(k_last) - YV.t(k_first), grid[k_last] - grid[k_first]);
+            for (int e = I.nnz_int + tid; e < I.entries(i); e += nthreads)
+                values[(long)il * I.nnz_int + e] = jac_entry(L, Ln, x, YV, tpl[e], k_first, C);
+        }
+        if (g)
+            for (int r = I.rpi + tid; r < I.rows(i); r += nthreads)
+                g[(long)il * I.rpi + r] = defect_row(L, I, Ln, x, YV, i, r);
     }
 }
 
@@ -780,10 +836,11 @@ __global__ void __launch_bounds__(1024) k_interval(DevModel M, Src S, Lanes Ln, 
     // tables_lds: the packed Jacobian template and the role -> slot table
     // are staged too, so that the combine and the assembly issue no global
     // loads after this one round trip
-    const int ntp = (I.nnz_int + 1) / 2;     // in doubles
-    double* sXs = sH + npts * nh;            // [npts][NS] states, [npts][NC] controls
-    double* sXc = sXs + npts * L.NS;
-    double* sTpl = sXc + npts * L.NC;
+    const int ntp = (I.nnz_int + I.nnz_tail + 1) / 2;     // in doubles (tail entries included)
+    double* sXs = sH + npts * nh;            // [npts][NS] states, [npts][NC] controls,
+    double* sXc = sXs + npts * L.NS;         // [npts][NDV] accelerations (implicit)
+    double* sXd = sXc + npts * L.NC;
+    double* sTpl = sXd + npts * L.NDV;
     // the interval's points are consecutive local grid points: their T (and
     // H) slabs are one contiguous run each
     const int kl0 = k_first - S.k0;
@@ -793,13 +850,15 @@ __global__ void __launch_bounds__(1024) k_interval(DevModel M, Src S, Lanes Ln, 
     if (tables_lds && values) stage_lds<8>(sTpl, (const double*)tplp, ntp);
     stage_lds<1>(sXs, S.x + 2 + (long)k_first * L.NS, npts * L.NS);
     if (L.NC > 0) stage_lds<1>(sXc, S.x + 2 + (long)L.NS * L.G + (long)k_first * L.NC, npts * L.NC);
+    if (L.NDV > 0)
+        stage_lds<1>(sXd, S.x + 2 + (long)(L.NS + L.NC) * L.G + (long)k_first * L.NDV, npts * L.NDV);
     const __attribute__((address_space(3))) uint32_t* tp = (const __attribute__((address_space(3))) uint32_t*)sTpl;
     const double t0 = S.x[0], tf = S.x[1];
     __syncthreads();
     MH_IV_STAMP(1)
     for (int w = threadIdx.x; w < npts * Ln.stride; w += blockDim.x) {
         const int p = w / Ln.stride, r = w - p * Ln.stride;
-        LaneInL<D> in{lds(sXs + p * L.NS), lds(sXc + p * L.NC), -1, 0.0};
+        LaneInL<D> in{lds(sXs + p * L.NS), lds(sXc + p * L.NC), lds(sXd + p * L.NDV), -1, 0.0};
         const double t = lane_time(Ln, S.grid[k_first + p], t0, tf, r, in.pi, in.step);
         if (r == Ln.base) sTimes[p] = t;
         const TaskLoadLds<D> TL{lds(sT + p * nt), lds(sH + p * nh), TK.jd, r};
@@ -828,32 +887,33 @@ __global__ void __launch_bounds__(1024) k_interval(DevModel M, Src S, Lanes Ln, 
         __syncthreads();
     }
     MH_IV_STAMP(2)
-    const YS YV{lds(sY), lds(sTimes), D::NO, Ln.stride, k_first, quot, lds(sXs), lds(sXc), L.NS, L.NC};
+    const YS YV{lds(sY), lds(sTimes), D::NO, Ln.stride, k_first, quot, lds(sXs), lds(sXc), L.NS, L.NC,
+                lds(sXd), L.NDV};
     if (g) {
         double* gi = g + (long)il * I.rpi;
-        for (int r = threadIdx.x; r < I.rpi; r += blockDim.x) gi[r] = defect_row(L, I, Ln, S.x, YV, i, r);
+        for (int r = threadIdx.x; r < I.rows(i); r += blockDim.x) gi[r] = defect_row(L, I, Ln, S.x, YV, i, r);
     }
     if (values) {
         const IvC C = iv_const(YV.t(k_last) - YV.t(k_first), S.grid[k_last] - S.grid[k_first]);
         double* vi = values + (long)il * I.nnz_int;
+        const int ne = I.entries(i);
         const int B = blockDim.x;
         int e = threadIdx.x;
-        const bool hs = I.scheme == MH_HERMITE_SIMPSON;
         if (tables_lds) {
-            for (; e < I.nnz_int; e += B)
-                vi[e] = jac_entry(L, Ln, S.x, YV, tpl_unpack(tp[e], L.NS, hs), k_first, C);
-            e = I.nnz_int;
+            for (; e < ne; e += B)
+                vi[e] = jac_entry(L, Ln, S.x, YV, tpl_unpack(tp[e]), k_first, C);
+            e = ne;
         }
         // template entries for IV_UNROLL iterations are loaded before any is
         // evaluated (independent loads in flight, then LDS reads + stores)
-        for (; e + (IV_UNROLL - 1) * B < I.nnz_int; e += IV_UNROLL * B) {
+        for (; e + (IV_UNROLL - 1) * B < ne; e += IV_UNROLL * B) {
             TplEntry te[IV_UNROLL];
 #pragma unroll
             for (int u = 0; u < IV_UNROLL; ++u) te[u] = tpl[e + u * B];
 #pragma unroll
             for (int u = 0; u < IV_UNROLL; ++u) vi[e + u * B] = jac_entry(L, Ln, S.x, YV, te[u], k_first, C);
         }
-        for (; e < I.nnz_int; e += B) vi[e] = jac_entry(L, Ln, S.x, YV, tpl[e], k_first, C);
+        for (; e < ne; e += B) vi[e] = jac_entry(L, Ln, S.x, YV, tpl[e], k_first, C);
     }
     MH_IV_STAMP(3)
 }
@@ -863,8 +923,10 @@ __device__ __forceinline__ void gather_inputs(const double* __restrict__ x, cons
         int k, double* in, int NI) {
     const double* xs = x + 2 + (long)k * L.NS;
     const double* xc = x + 2 + (long)L.NS * L.G + (long)k * L.NC;
+    const double* xd = x + 2 + (long)(L.NS + L.NC) * L.G + (long)k * L.NDV;
     for (int s = 0; s < L.NS; ++s) in[s] = xs[s];
     for (int j = 0; j < L.NC; ++j) in[L.NS + j] = xc[j];
+    for (int j = 0; j < L.NDV; ++j) in[L.NS + L.NC + j] = xd[j];
     (void)NI;
 }
 
@@ -959,7 +1021,8 @@ __global__ void __launch_bounds__(64) k_grad(DevModel M, Layout L, GoalSet GS, i
     }
     if (d < 2) tpart[(long)k * 2 + d] = acc;
     else if (d - 2 < L.NS) grad[2 + (long)k * L.NS + (d - 2)] = acc;
-    else grad[2 + (long)L.NS * L.G + (long)k * L.NC + (d - 2 - L.NS)] = acc;
+    else if (d - 2 < L.NS + L.NC) grad[2 + (long)L.NS * L.G + (long)k * L.NC + (d - 2 - L.NS)] = acc;
+    else grad[2 + (long)(L.NS + L.NC) * L.G + (long)k * L.NDV + (d - 2 - L.NS - L.NC)] = acc;
 }
 
 // Single-workgroup deterministic reduction of the objective (mode 0) or of
@@ -1226,6 +1289,8 @@ struct mh_ctx {
     // problem
     int NQ = 0, NZ = 0, NS = 0, NC = 0, NO = 0, NI = 0;
     int scheme = 0, N = 0, G = 0, interp = 0, rpi = 0, nnz_int = 0;
+    int NDV = 0, nnz_tail = 0;     // implicit: accelerations per point, tail nonzeros
+    double acc_lo = -1000.0, acc_hi = 1000.0;
     int ib = 0, ie = 0, k0 = 0, nk = 0;
     int fd = 0;
     double h = 1e-8;
@@ -1304,26 +1369,36 @@ static int64_t col_state(const mh_ctx* c, int64_t k, int s) { return 2 + k * c->
 static int64_t col_control(const mh_ctx* c, int64_t k, int j) {
     return 2 + (int64_t)c->NS * c->G + k * c->NC + j;
 }
+// implicit mode: accelerations (CasOC "derivatives", sorted after controls)
+static int64_t col_deriv(const mh_ctx* c, int64_t k, int j) {
+    return 2 + (int64_t)(c->NS + c->NC) * c->G + k * c->NDV + j;
+}
 
 // Build the per-interval template in CasOC row order with columns sorted
-// ascending (the block-dense structural rule).
+// ascending (the block-dense structural rule), then
+// (implicit mode) the tail template: the final grid point's residual rows,
+// evaluated by the last interval.
 static void build_template(mh_ctx* c) {
-    const int NS = c->NS, NQ = c->NQ, NC = c->NC;
+    const int NS = c->NS, NQ = c->NQ, NC = c->NC, NDV = c->NDV;
+    const bool implicit = NDV > 0;
     struct Col { int pt; int dir; };  // dir: 0/1 time, 2+input
     auto key = [&](const Col& col) -> int64_t {
         // column index for interval 0
         if (col.dir < 2) return col.dir;
         const int j = col.dir - 2;
         if (j < NS) return col_state(c, col.pt, j);
-        return col_control(c, col.pt, j - NS);
+        if (j < NS + NC) return col_control(c, col.pt, j - NS);
+        return col_deriv(c, col.pt, j - NS - NC);
     };
-    auto emit_row = [&](int row, uint8_t kind_t, uint8_t kind_x, int s, std::vector<Col> cols) {
+    // time columns carry pt_time (the residual rows' grid point; 0 otherwise)
+    auto emit_row = [&](int row, uint8_t kind_t, uint8_t kind_x, int s, std::vector<Col> cols,
+            int pt_time = 0) {
         std::sort(cols.begin(), cols.end(), [&](const Col& a, const Col& b) { return key(a) < key(b); });
         for (const auto& col : cols) {
             TplEntry e{};
             e.row = (int16_t)row;
             e.kind = col.dir < 2 ? kind_t : kind_x;
-            e.pt = (uint8_t)(col.dir < 2 ? 0 : col.pt);
+            e.pt = (uint8_t)(col.dir < 2 ? pt_time : col.pt);
             e.dir = (int16_t)col.dir;
             e.s = (int16_t)s;
             c->tpl.push_back(e);
@@ -1331,15 +1406,32 @@ static void build_template(mh_ctx* c) {
         }
     };
     auto point_all = [&](int pt, std::vector<Col>& v) {
-        for (int j = 0; j < NS + NC; ++j) v.push_back({pt, 2 + j});
+        for (int j = 0; j < NS + NC + NDV; ++j) v.push_back({pt, 2 + j});
     };
+    // multibody residual rows of point pt: every input of the point + time
+    auto residual_rows = [&](int& row, int pt) {
+        for (int o = 0; o < (implicit ? NQ : 0); ++o) {
+            std::vector<Col> v{{pt, 0}, {pt, 1}};
+            point_all(pt, v);
+            emit_row(row++, T_RES, T_RES, o, v, pt);
+        }
+    };
+    // implicit speed rows: udot = the acceleration variable (direct MX
+    // expression, CasOCTranscription.cpp:339-341): own state + acceleration
+    auto speed_sparse = [&](int s) { return implicit && s >= NQ && s < 2 * NQ; };
+    const int adir = 2 + NS + NC;   // direction of acceleration 0
     int row = 0;
     if (c->scheme == MH_HERMITE_SIMPSON) {
+        residual_rows(row, 0);
+        residual_rows(row, 1);
         for (int s = 0; s < NS; ++s) {
             std::vector<Col> v{{0, 0}, {0, 1}};
             if (s < NQ) {
                 v.push_back({1, 2 + s}); v.push_back({0, 2 + s}); v.push_back({2, 2 + s});
                 v.push_back({0, 2 + NQ + s}); v.push_back({2, 2 + NQ + s});
+            } else if (speed_sparse(s)) {
+                v.push_back({1, 2 + s}); v.push_back({0, 2 + s}); v.push_back({2, 2 + s});
+                v.push_back({0, adir + s - NQ}); v.push_back({2, adir + s - NQ});
             } else {
                 v.push_back({1, 2 + s});
                 point_all(0, v); point_all(2, v);
@@ -1351,6 +1443,9 @@ static void build_template(mh_ctx* c) {
             if (s < NQ) {
                 v.push_back({0, 2 + s}); v.push_back({2, 2 + s});
                 v.push_back({0, 2 + NQ + s}); v.push_back({1, 2 + NQ + s}); v.push_back({2, 2 + NQ + s});
+            } else if (speed_sparse(s)) {
+                v.push_back({0, 2 + s}); v.push_back({2, 2 + s});
+                v.push_back({0, adir + s - NQ}); v.push_back({1, adir + s - NQ}); v.push_back({2, adir + s - NQ});
             } else {
                 point_all(0, v); point_all(1, v); point_all(2, v);
             }
@@ -1363,11 +1458,15 @@ static void build_template(mh_ctx* c) {
             }
         }
     } else {
+        residual_rows(row, 0);
         for (int s = 0; s < NS; ++s) {
             std::vector<Col> v{{0, 0}, {0, 1}};
             if (s < NQ) {
                 v.push_back({0, 2 + s}); v.push_back({1, 2 + s});
                 v.push_back({0, 2 + NQ + s}); v.push_back({1, 2 + NQ + s});
+            } else if (speed_sparse(s)) {
+                v.push_back({0, 2 + s}); v.push_back({1, 2 + s});
+                v.push_back({0, adir + s - NQ}); v.push_back({1, adir + s - NQ});
             } else {
                 point_all(0, v); point_all(1, v);
             }
@@ -1376,6 +1475,10 @@ static void build_template(mh_ctx* c) {
     }
     c->rpi = row;
     c->nnz_int = (int)c->tpl.size();
+    // tail: residual rows of the last grid point (point 2 of the HS interval,
+    // 1 of the trapezoidal one), rows rpi.. relative to the last interval
+    residual_rows(row, c->scheme == MH_HERMITE_SIMPSON ? 2 : 1);
+    c->nnz_tail = (int)c->tpl.size() - c->nnz_int;
 }
 
 static int validate_and_layout(mh_ctx* c, const mh_problem* p, const mh_options* o,
@@ -1413,7 +1516,14 @@ static int validate_and_layout(mh_ctx* c, const mh_problem* p, const mh_options*
     c->NZ = z - 2 * M.nq;
     c->NC = M.nactuators;
     c->NO = c->NQ + c->NZ;
-    c->NI = c->NS + c->NC;
+    if (o->multibody_dynamics_mode != MH_DYNAMICS_EXPLICIT && o->multibody_dynamics_mode != MH_DYNAMICS_IMPLICIT)
+        return set_err(MH_ERR_INVALID, "unknown multibody dynamics mode %d", o->multibody_dynamics_mode);
+    c->NDV = o->multibody_dynamics_mode == MH_DYNAMICS_IMPLICIT ? c->NQ : 0;
+    if (o->implicit_accel_bounds[0] != 0.0 || o->implicit_accel_bounds[1] != 0.0) {
+        c->acc_lo = o->implicit_accel_bounds[0];
+        c->acc_hi = o->implicit_accel_bounds[1];
+    }
+    c->NI = c->NS + c->NC + c->NDV;
     for (int ia = 0; ia < M.nactuators; ++ia) {
         const mh_actuator& a = M.actuators[ia];
         if (a.kind == MH_ACT_MUSCLE) {
@@ -1497,10 +1607,10 @@ static int validate_and_layout(mh_ctx* c, const mh_problem* p, const mh_options*
             c->quad[i + 1] += 0.5 * dm;
         }
     }
-    c->n = 2 + (int64_t)(c->NS + c->NC) * c->G;
+    c->n = 2 + (int64_t)(c->NS + c->NC + c->NDV) * c->G;
     build_template(c);
-    c->m = (int64_t)c->rpi * c->N;
-    c->nnz = (int64_t)c->nnz_int * c->N;
+    c->m = (int64_t)c->rpi * c->N + c->NDV;      // + the final point's residuals
+    c->nnz = (int64_t)c->nnz_int * c->N + c->nnz_tail;
     c->ib = std::max(0, o->interval_begin);
     c->ie = o->interval_end > 0 ? std::min(o->interval_end, c->N) : c->N;
     if (c->ib >= c->ie) return set_err(MH_ERR_INVALID, "empty interval shard [%d, %d)", c->ib, c->ie);
@@ -1634,8 +1744,8 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     c->tplp.clear();
     for (const TplEntry& e : c->tpl) {
         c->tplp.push_back(tpl_pack(e));
-        const TplEntry u = tpl_unpack(c->tplp.back(), c->NS, c->scheme == MH_HERMITE_SIMPSON);
-        if (u.row != e.row || u.kind != e.kind || u.pt != e.pt || u.dir != e.dir || u.s != e.s)
+        const TplEntry u = tpl_unpack(c->tplp.back());
+        if (u.kind != e.kind || u.pt != e.pt || u.dir != e.dir || u.s != e.s || e.dir > 2047 || e.s < 0)
             return set_err(MH_ERR_UNSUPPORTED, "Jacobian template entry does not pack into 32 bits");
     }
     if (c->tplp.size() % 2) c->tplp.push_back(0u);
@@ -1650,8 +1760,8 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     c->lanes_g = Lanes{c->fd, ND, 1, 0, c->h};
     const size_t o_Y = A.reserve(sizeof(double) * (size_t)c->nk * std::max(1, c->NO) * stride);
     const size_t o_Yg = A.reserve(sizeof(double) * (size_t)c->nk * std::max(1, c->NO));
-    const size_t o_g = A.reserve(sizeof(double) * (size_t)nint * c->rpi);
-    const size_t o_vals = A.reserve(sizeof(double) * (size_t)nint * c->nnz_int);
+    const size_t o_g = A.reserve(sizeof(double) * ((size_t)nint * c->rpi + c->NDV));
+    const size_t o_vals = A.reserve(sizeof(double) * ((size_t)nint * c->nnz_int + c->nnz_tail));
     const size_t o_C = A.reserve(sizeof(double) * (size_t)c->G * std::max(1, p->ngoals));
     const size_t o_grad = A.reserve(sizeof(double) * c->n);
     const size_t o_tpart = A.reserve(sizeof(double) * 2 * (size_t)c->G);
@@ -1675,6 +1785,7 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     DevModel& D = c->M;
     D.nq = M.nq; D.nb = M.nbodies; D.nmus = M.nmuscles; D.nact = M.nactuators; D.next = M.nexternal;
     D.ns = c->NS; D.nz = c->NZ; D.nc = c->NC; D.no = c->NO; D.np = c->NI;
+    D.implicit = c->NDV > 0 ? 1 : 0;
     for (int i = 0; i < 3; ++i) D.gravity[i] = M.gravity[i];
     D.tau_act = tau_act; D.tau_deact = tau_deact;
     D.bodies = (const mh_body*)(b + o_bodies); D.axes = (const mh_axis*)(b + o_axes);
@@ -1761,9 +1872,9 @@ extern "C" int mh_get_nlp_info(const mh_ctx* c, mh_nlp_info* info) {
     info->num_states = c->NS;
     info->num_controls = c->NC;
     info->row_begin = (int64_t)c->ib * c->rpi;
-    info->row_end = (int64_t)c->ie * c->rpi;
+    info->row_end = (int64_t)c->ie * c->rpi + (c->ie == c->N ? c->NDV : 0);
     info->nnz_begin = (int64_t)c->ib * c->nnz_int;
-    info->nnz_end = (int64_t)c->ie * c->nnz_int;
+    info->nnz_end = (int64_t)c->ie * c->nnz_int + (c->ie == c->N ? c->nnz_tail : 0);
     return MH_OK;
 }
 
@@ -1791,6 +1902,9 @@ extern "C" int mh_get_bounds(const mh_ctx* c, double* xl, double* xu, double* gl
     };
     for (int s = 0; s < c->NS; ++s) fill(c->sinfo[s], [&](int k) { return col_state(c, k, s); });
     for (int j = 0; j < c->NC; ++j) fill(c->cinfo[j], [&](int k) { return col_control(c, k, j); });
+    // implicit: acceleration bounds at every grid point (CasOCTranscription.cpp:222-226)
+    for (int j = 0; j < c->NDV; ++j)
+        for (int k = 0; k < c->G; ++k) { xl[col_deriv(c, k, j)] = c->acc_lo; xu[col_deriv(c, k, j)] = c->acc_hi; }
     if (gl && gu)
         for (int64_t r = 0; r < c->m; ++r) { gl[r] = 0.0; gu[r] = 0.0; }
     return MH_OK;
@@ -1828,7 +1942,9 @@ extern "C" int mh_get_jac_structure(const mh_ctx* c, int32_t* iRow, int32_t* jCo
     const int step = c->scheme == MH_HERMITE_SIMPSON ? 2 : 1;
     int64_t e = 0;
     for (int i = 0; i < c->N; ++i) {
-        for (size_t t = 0; t < c->tpl.size(); ++t) {
+        // the last interval also carries the tail (final-point residual rows)
+        const size_t ne = (size_t)c->nnz_int + (i == c->N - 1 ? (size_t)c->nnz_tail : 0);
+        for (size_t t = 0; t < ne; ++t) {
             const TplEntry& T = c->tpl[t];
             iRow[e] = (int32_t)((int64_t)i * c->rpi + T.row);
             int64_t col;
@@ -1836,7 +1952,8 @@ extern "C" int mh_get_jac_structure(const mh_ctx* c, int32_t* iRow, int32_t* jCo
             else {
                 const int j = T.dir - 2;
                 const int64_t k = (int64_t)i * step + T.pt;
-                col = j < c->NS ? col_state(c, k, j) : col_control(c, k, j - c->NS);
+                col = j < c->NS ? col_state(c, k, j)
+                                : (j < c->NS + c->NC ? col_control(c, k, j - c->NS) : col_deriv(c, k, j - c->NS - c->NC));
             }
             jCol[e] = (int32_t)col;
             ++e;
@@ -1867,7 +1984,7 @@ struct Backend {
 
 template <class D>
 static void be_eval_lane(mh_ctx* c, const double* x, int mode, double* Y) {
-    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, c->k0, c->nk};
+    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, c->k0, c->nk, c->NDV};
     const Lanes& ln = mode ? c->lanes_jac : c->lanes_g;
     const long lanes = (long)c->nk * ln.stride;
     hipLaunchKernelGGL(k_eval<D>, dim3((unsigned)((lanes + 63) / 64)), dim3(64), 0, c->stream, c->M, L,
@@ -1915,8 +2032,8 @@ static void be_eval_tasks(mh_ctx* c, const double* x, int mode, double* Y) {
 template <class D>
 static size_t interval_lds(const mh_ctx* c, const Lanes& ln, const TaskSet& ts, bool tables) {
     const size_t npts = c->scheme == MH_HERMITE_SIMPSON ? 3 : 2;
-    const size_t tab = tables ? (size_t)(c->nnz_int + 1) / 2 : 0;
-    return sizeof(double) * (npts * D::NO * ln.stride + 4 + npts * (size_t)(c->NS + c->NC) +
+    const size_t tab = tables ? (size_t)(c->nnz_int + c->nnz_tail + 1) / 2 : 0;
+    return sizeof(double) * (npts * D::NO * ln.stride + 4 + npts * (size_t)(c->NS + c->NC + c->NDV) +
                              npts * ((size_t)ts.dev.tdoubles + (size_t)ts.dev.nmass * D::NST) + tab);
 }
 template <class D>
@@ -1935,28 +2052,28 @@ static void be_interval(mh_ctx* c, const double* x, int mode, double* g, double*
     if (lds > 65536)
         (void)hipFuncSetAttribute((const void*)k_interval<D>, hipFuncAttributeMaxDynamicSharedMemorySize,
                 (int)lds);
-    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, c->k0, c->nk};
-    Interval I{c->scheme, c->interp, c->ib, c->rpi, c->nnz_int};
+    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, c->k0, c->nk, c->NDV};
+    Interval I{c->scheme, c->interp, c->ib, c->rpi, c->nnz_int, c->NDV, c->N, c->nnz_tail};
     const unsigned threads = v ? 1024u : 256u;
     hipLaunchKernelGGL(k_interval<D>, dim3((unsigned)(c->ie - c->ib)), dim3(threads), lds, c->stream, c->M,
             S, ln, ts.dev, L, I, c->d_tpl, c->d_tplp, tables, c->d_T, c->d_H, g, v);
 }
 template <class D>
 static void be_integrand(mh_ctx* c, const double* x) {
-    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, 0, c->G};
+    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, 0, c->G, c->NDV};
     hipLaunchKernelGGL(k_integrand<D>, dim3((c->G + 63) / 64), dim3(64), 0, c->stream, c->M, L,
             c->GS, x, c->d_grid, c->d_quad, c->d_C);
 }
 template <class D>
 static void be_grad(mh_ctx* c, const double* x) {
-    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, 0, c->G};
+    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, 0, c->G, c->NDV};
     const long tot = (long)c->G * (c->NI + 2);
     hipLaunchKernelGGL(k_grad<D>, dim3((unsigned)((tot + 63) / 64)), dim3(64), 0, c->stream, c->M, L,
             c->GS, c->fd, c->h, x, c->d_grid, c->d_quad, c->d_grad, c->d_tpart);
 }
 template <class D>
 static void be_probe_lane(mh_ctx* c, int np, const double* in, double* out) {
-    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, 0, 0};
+    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, 0, 0, c->NDV};
     hipLaunchKernelGGL(k_dae_probe<D>, dim3((np + 63) / 64), dim3(64), 0, c->stream, c->M, L, np, in,
             out);
 }
@@ -2018,11 +2135,11 @@ static int launch_stage(mh_ctx* c, int stage, int kind, const double* x, double*
         HIPCHK(hipGetLastError());
         return MH_OK;
     }
-    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, c->k0, c->nk};
-    Interval I{c->scheme, c->interp, c->ib, c->rpi, c->nnz_int};
+    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, c->k0, c->nk, c->NDV};
+    Interval I{c->scheme, c->interp, c->ib, c->rpi, c->nnz_int, c->NDV, c->N, c->nnz_tail};
     const Lanes& ln = kind == 0 ? c->lanes_g : c->lanes_jac;
     const double* Y = kind == 0 ? c->d_Yg : c->d_Y;
-    const int nchunks = kind == 0 ? 0 : (c->nnz_int + ASM_CHUNK - 1) / ASM_CHUNK;
+    const int nchunks = kind == 0 ? 0 : (c->nnz_int + (c->ie == c->N ? c->nnz_tail : 0) + ASM_CHUNK - 1) / ASM_CHUNK;
     double* g = kind == 1 ? nullptr : a;
     double* v = kind == 0 ? nullptr : (kind == 1 ? a : b);
     if (c->use_interval[kind == 0 ? 0 : 1]) {
@@ -2119,13 +2236,22 @@ static int finish(mh_ctx* c) {
     return MH_OK;
 }
 
+// rows / nonzeros of this context's shard (the last shard includes the
+// final grid point's residual rows in implicit mode)
+static size_t shard_rows(const mh_ctx* c) {
+    return (size_t)(c->ie - c->ib) * c->rpi + (c->ie == c->N ? c->NDV : 0);
+}
+static size_t shard_nnz(const mh_ctx* c) {
+    return (size_t)(c->ie - c->ib) * c->nnz_int + (c->ie == c->N ? c->nnz_tail : 0);
+}
+
 extern "C" int mh_eval_g(mh_ctx* c, const double* x, int, double* g) {
     if (!c || !x || !g) return set_err(MH_ERR_INVALID, "null argument");
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipMemcpyAsync(c->d_x, x, sizeof(double) * c->n, hipMemcpyHostToDevice, c->stream));
     int rc = run_cached(c, 0, c->d_x, c->d_g, nullptr);
     if (rc) return rc;
-    HIPCHK(hipMemcpyAsync(g, c->d_g, sizeof(double) * (size_t)(c->ie - c->ib) * c->rpi,
+    HIPCHK(hipMemcpyAsync(g, c->d_g, sizeof(double) * shard_rows(c),
             hipMemcpyDeviceToHost, c->stream));
     return finish(c);
 }
@@ -2136,7 +2262,7 @@ extern "C" int mh_eval_jac_g(mh_ctx* c, const double* x, int, double* values) {
     HIPCHK(hipMemcpyAsync(c->d_x, x, sizeof(double) * c->n, hipMemcpyHostToDevice, c->stream));
     int rc = run_cached(c, 1, c->d_x, c->d_vals, nullptr);
     if (rc) return rc;
-    HIPCHK(hipMemcpyAsync(values, c->d_vals, sizeof(double) * (size_t)(c->ie - c->ib) * c->nnz_int,
+    HIPCHK(hipMemcpyAsync(values, c->d_vals, sizeof(double) * shard_nnz(c),
             hipMemcpyDeviceToHost, c->stream));
     return finish(c);
 }
@@ -2171,9 +2297,9 @@ extern "C" int mh_eval_g_jac_g(mh_ctx* c, const double* x, double* g, double* va
     HIPCHK(hipMemcpyAsync(c->d_x, x, sizeof(double) * c->n, hipMemcpyHostToDevice, c->stream));
     int rc = run_cached(c, 2, c->d_x, c->d_g, c->d_vals);
     if (rc) return rc;
-    HIPCHK(hipMemcpyAsync(g, c->d_g, sizeof(double) * (size_t)(c->ie - c->ib) * c->rpi,
+    HIPCHK(hipMemcpyAsync(g, c->d_g, sizeof(double) * shard_rows(c),
             hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipMemcpyAsync(values, c->d_vals, sizeof(double) * (size_t)(c->ie - c->ib) * c->nnz_int,
+    HIPCHK(hipMemcpyAsync(values, c->d_vals, sizeof(double) * shard_nnz(c),
             hipMemcpyDeviceToHost, c->stream));
     return finish(c);
 }
@@ -2184,7 +2310,7 @@ extern "C" int mh_eval_f(mh_ctx* c, const double* x, int, double* f) {
     (void)hipGetLastError();   // report only this call's launch errors
     HIPCHK(hipMemcpyAsync(c->d_x, x, sizeof(double) * c->n, hipMemcpyHostToDevice, c->stream));
     if (c->timing) HIPCHK(hipEventRecord(c->ev[0], c->stream));
-    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, 0, c->G};
+    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, 0, c->G, c->NDV};
     if (c->ngoals > 0) {
         c->be->integrand(c, c->d_x);
         HIPCHK(hipGetLastError());
@@ -2204,7 +2330,7 @@ extern "C" int mh_eval_grad_f(mh_ctx* c, const double* x, int, double* grad) {
     (void)hipGetLastError();   // report only this call's launch errors
     HIPCHK(hipMemcpyAsync(c->d_x, x, sizeof(double) * c->n, hipMemcpyHostToDevice, c->stream));
     if (c->timing) HIPCHK(hipEventRecord(c->ev[0], c->stream));
-    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, 0, c->G};
+    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, 0, c->G, c->NDV};
     HIPCHK(hipMemsetAsync(c->d_grad, 0, sizeof(double) * c->n, c->stream));
     HIPCHK(hipMemsetAsync(c->d_tpart, 0, sizeof(double) * 2 * c->G, c->stream));
     HIPCHK(hipMemsetAsync(c->d_C, 0, sizeof(double) * c->G * std::max(1, c->ngoals), c->stream));
@@ -2309,14 +2435,23 @@ extern "C" int mh_get_work(const mh_ctx* c, double* work4) {
     return MH_OK;
 }
 
+// Generated back ends are keyed by the model hash, salted for implicit
+// multibody dynamics (a different DAE: residual outputs, acceleration
+// inputs, no mass-matrix factor).
+constexpr uint64_t kImplicitSalt = 0x9e3779b97f4a7c15ULL;
+static uint64_t backend_key(uint64_t model_hash, bool implicit) {
+    return implicit ? model_hash ^ kImplicitSalt : model_hash;
+}
+
 static const Backend* select_backend(mh_ctx* c, const mh_problem* p) {
     c->model_hash = model_hash(&p->model);
     const char* force = std::getenv("MOCOHIP_BACKEND");
     const bool generic = force && std::strcmp(force, "generic") == 0;
     const bool lane = force && std::strcmp(force, "lane") == 0;
     if (!generic) {
+        const uint64_t key = backend_key(c->model_hash, c->NDV > 0);
         for (const GenEntry& e : kGeneratedModels)
-            if (e.hash == c->model_hash) return lane ? &e.lane : &e.tasks;
+            if (e.hash == key) return lane ? &e.lane : &e.tasks;
     }
     return &kGeneric[c->size_class];
 }

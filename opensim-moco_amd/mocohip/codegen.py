@@ -254,7 +254,7 @@ def _uniform_guess(br):
 
 
 class _Layout:
-    def __init__(self, M: ModelView):
+    def __init__(self, M: ModelView, implicit: bool = False):
         NQ = M.nq
         z = 2 * NQ
         self.act_state, self.ftn_state = [], []
@@ -273,7 +273,11 @@ class _Layout:
         self.NQ, self.NS, self.NC = NQ, z, len(M.acts)
         self.NZ = z - 2 * NQ
         self.NO = NQ + self.NZ
-        self.NI = self.NS + self.NC
+        # implicit multibody dynamics: the generalized accelerations are
+        # point inputs after the controls; outputs [residual, zdot]
+        self.implicit = implicit
+        self.NDV = NQ if implicit else 0
+        self.NI = self.NS + self.NC + self.NDV
         for ia, a in enumerate(M.acts):
             if a.kind == abi.MH_ACT_MUSCLE:
                 self.mus_control[a.target] = ia
@@ -289,6 +293,7 @@ class _Emitter:
         self.q = self.inp[:Lo.NQ]
         self.u = self.inp[Lo.NQ:2 * Lo.NQ]
         self.ctrl = self.inp[Lo.NS:Lo.NS + Lo.NC]
+        self.wacc = self.inp[Lo.NS + Lo.NC:Lo.NI] if Lo.implicit else None
         self.fcache: Dict[int, Tuple[S, S, S]] = {}
         self.touched = set()
 
@@ -377,6 +382,8 @@ class _Emitter:
                 if accel:
                     sd = g.crm(Vframe, s)
                     thdd = g.mul(fv[2], g.mul(u[j], u[j]))
+                    if self.wacc is not None:   # implicit: RNEA with udot = w
+                        thdd = g.add(thdd, g.mul(fv[1], self.wacc[j]))
                     Ab = g.svadd(Ab, g.svadd(g.svscale(sd, thd), g.svscale(s, thdd)))
                 Sj[j] = g.svadd(Sj.get(j, (Z3, Z3)), g.svscale(s, fv[1]))
             for ax, fv in zip(axes, fvals):
@@ -683,11 +690,13 @@ def _multibody_front(E: _Emitter, with_muscles: bool):
             E.muscle(im, R, P, V, Facc, tau, lambda s, v: zd.__setitem__(s, v))
     E.external_forces(P, Facc)
     E.backward(allb, Facc, Sj, coord_body, tau)
+    if Lo.implicit:
+        return tau, None, None, zd
     lam, H = E.mass_matrix_factor(Ibody, Sj, [coord_body[j] for j in range(Lo.NQ)])
     return tau, lam, H, zd
 
 
-def generate(cm, struct_name: str) -> Tuple[str, Dict]:
+def generate(cm, struct_name: str, implicit: bool = False) -> Tuple[str, Dict]:
     """Return (C++ source of `struct <struct_name>`, info dict).
 
     The struct has
@@ -700,15 +709,19 @@ def generate(cm, struct_name: str) -> Tuple[str, Dict]:
     plus the group metadata (fields, inputs read, time dependence, FP64 op
     counts) the host uses to build the task tables."""
     M = ModelView(cm)
-    Lo = _Layout(M)
+    Lo = _Layout(M, implicit)
     NQ, NZ = Lo.NQ, Lo.NZ
     parts = []
-    info = {"NQ": NQ, "NS": Lo.NS, "NC": Lo.NC}
+    info = {"NQ": NQ, "NS": Lo.NS, "NC": Lo.NC, "implicit": implicit}
 
     # ---- single-lane eval ---------------------------------------------------
     E = _Emitter(M, Lo)
     tau, lam, H, zd = _multibody_front(E, with_muscles=True)
-    xs = E.solve(lam, H, [S(n=t) for t in tau])
+    if implicit:
+        # residual = M w + C - f_applied = -(tau of the RNEA with udot = w)
+        xs = [E.g.neg(S(n=t)) for t in tau]
+    else:
+        xs = E.solve(lam, H, [S(n=t) for t in tau])
     for i in range(NQ):
         E.g.raw(f"out[{i}] = {xs[i]};")
     for zi in range(NZ):
@@ -758,6 +771,7 @@ def generate(cm, struct_name: str) -> Tuple[str, Dict]:
     lst = lambda v: "{" + ", ".join(str(x) for x in v) + "}"
     src = f"""struct {struct_name} {{
     static constexpr int NQ = {NQ}, NZ = {NZ}, NS = {Lo.NS}, NC = {Lo.NC}, NO = {Lo.NO}, NI = {Lo.NI};
+    static constexpr bool IMPLICIT = {"true" if implicit else "false"};
     static constexpr int MI = NI, MO = NO;
     static constexpr double FLOPS_PER_EVAL = {float(fl['total'])};
     // task decomposition: group 0 = mass matrix factor (NST values), groups
@@ -809,18 +823,25 @@ def _emit_groups(M: ModelView, Lo: _Layout) -> List[_Group]:
     allb = list(range(M.nb))
     out = []
 
-    # mass
+    # mass (implicit mode: the residual needs no mass matrix -- the group is
+    # an empty placeholder so group 0 keeps its role in the task tables)
     E = _Emitter(M, Lo)
-    R, P, _, _, Sj, cb = E.kinematics(allb, accel=False, vel=False)
-    Ib = {b: E.inertia(b, R, P) for b in allb}
-    lam, H = E.mass_matrix_factor(Ib, Sj, [cb[j] for j in range(NQ)])
-    keys = sorted(H.keys())
-    for f, k in enumerate(keys):
-        E.g.raw(f"out[{f}] = {H[k]};")
-    r, t = _reads_of(E.g.lines)
-    g0 = _Group("mass", E.g.lines, [("H", k) for k in keys], r, t, sum(E.g.flops.values()))
-    g0.lam = lam
-    out.append(g0)
+    if Lo.implicit:
+        E.g.raw("out[0] = 0.0;")
+        g0 = _Group("mass", E.g.lines, [("H", (0, 0))], set(), False, 0)
+        g0.lam = None
+        out.append(g0)
+    else:
+        R, P, _, _, Sj, cb = E.kinematics(allb, accel=False, vel=False)
+        Ib = {b: E.inertia(b, R, P) for b in allb}
+        lam, H = E.mass_matrix_factor(Ib, Sj, [cb[j] for j in range(NQ)])
+        keys = sorted(H.keys())
+        for f, k in enumerate(keys):
+            E.g.raw(f"out[{f}] = {H[k]};")
+        r, t = _reads_of(E.g.lines)
+        g0 = _Group("mass", E.g.lines, [("H", k) for k in keys], r, t, sum(E.g.flops.values()))
+        g0.lam = lam
+        out.append(g0)
 
     def finish(Eg, name, tv, zf=None):
         fields = []
@@ -915,9 +936,12 @@ def _emit_combine(M: ModelView, Lo: _Layout, groups: List[_Group]):
             ts = [g.add(ts[i], ts[i + 1]) if i + 1 < len(ts) else ts[i] for i in range(0, len(ts), 2)]
         return ts[0]
     bvec = [tree(t) for t in terms]
-    keys = [k for _, k in groups[0].fields]
-    Hs = {k: S(n=f"T.h({f})") for f, k in enumerate(keys)}
-    xs = E.solve(groups[0].lam, Hs, bvec)
+    if Lo.implicit:
+        xs = [g.neg(b) for b in bvec]     # residual = -(applied - bias with udot = w)
+    else:
+        keys = [k for _, k in groups[0].fields]
+        Hs = {k: S(n=f"T.h({f})") for f, k in enumerate(keys)}
+        xs = E.solve(groups[0].lam, Hs, bvec)
     for i in range(NQ):
         g.raw(f"out[{i}] = {xs[i]};")
     for gi, gr in enumerate(groups[1:], start=1):

@@ -34,6 +34,14 @@ CASES = {
     "gait_compliant_central": lambda: configs.gait10dof18musc(8, tendon_compliance=True,
                                                                fd_scheme="central"),
     "gait_torque_driven": lambda: configs.gait10dof18musc(10, muscles=False),
+    # implicit multibody dynamics (testImplicit.cpp solves the
+    # double pendulum in both modes)
+    "sliding_mass_implicit": lambda: configs.sliding_mass(20, dynamics="implicit"),
+    "double_pendulum_implicit_hs": lambda: configs.double_pendulum(30, dynamics="implicit"),
+    "double_pendulum_implicit_trap": lambda: configs.double_pendulum(20, "trapezoidal", dynamics="implicit"),
+    "gait_rigid_implicit": lambda: configs.gait10dof18musc(8, dynamics="implicit"),
+    "gait_compliant_implicit_central": lambda: configs.gait10dof18musc(
+        6, tendon_compliance=True, fd_scheme="central", dynamics="implicit"),
 }
 
 
@@ -70,27 +78,52 @@ def _scale(v):
     return np.where(_regular(v), np.abs(v), 0.0)
 
 
+def _rows(nlp):
+    """(rows per interval, tail rows): implicit mode appends the final grid
+    point's residual rows after the last interval."""
+    N = nlp.opts.num_mesh_intervals
+    tail = nlp.NDV
+    return (nlp.m - tail) // N, tail
+
+
+def _per_row(nlp, per_interval):
+    """Expand a per-interval array to g rows (tail rows take the last
+    interval's value)."""
+    rpi, tail = _rows(nlp)
+    return np.concatenate([np.repeat(per_interval, rpi), np.full(tail, per_interval[-1])])
+
+
+def _row_interval(nlp, rows):
+    rpi, _ = _rows(nlp)
+    return np.minimum(rows // rpi, nlp.opts.num_mesh_intervals - 1)
+
+
 def _row_mask(ref, x):
     """Per g row: True when every DAE output the row depends on is regular at
-    the interval's grid points (defect rows of state s >= NQ depend on
-    xdot_s; the others on x only)."""
+    the interval's grid points (residual rows on their output; defect rows of
+    states s >= NQ (s >= 2NQ in implicit mode) on xdot_s; the others on x
+    only)."""
     P = _points(ref, x)
     Y0 = ref.eval_dae(P)
     R = _regular(Y0)
-    NQ, NS, NC = ref.NQ, ref.NS, ref.NC
+    NQ, NS = ref.NQ, ref.NS
     N = ref.opts.num_mesh_intervals
     hs = ref.opts.transcription == 0
     step = 2 if hs else 1
-    rpi = ref.m // N
+    rpi, tail = _rows(ref)
+    nres = ref.NDV
+    npres = step if nres else 0
     mask = np.ones((N, rpi), bool)
     ndef = 2 * NS if hs else NS
     for i in range(N):
         ok = R[i * step:i * step + step + 1].all(0)
+        for row in range(npres * nres):
+            mask[i, row] = R[i * step + row // nres, row % nres]
         for row in range(ndef):
             s = row % NS
-            if s >= NQ:
-                mask[i, row] = ok[s - NQ]
-    return mask.reshape(-1)
+            if s >= (2 * NQ if nres else NQ):
+                mask[i, npres * nres + row] = ok[s - NQ]
+    return np.concatenate([mask.reshape(-1), R[-1, :tail]])
 
 
 BACKENDS = ["auto", "lane", "generic"]
@@ -128,16 +161,20 @@ def _pair(name, backend="auto", tasks=None, env=None):
     if backend == "generic":
         assert name_.startswith("generic"), name_
     elif backend == "lane":
+        if name_.startswith("generic"):
+            pytest.skip(f"{name}: no generated back end for this model / dynamics mode")
         assert name_.startswith("generated-lane:"), name_
     return gpu, OracleNLP(rep, opts, threads=8), st
 
 
 def _points(nlp, x):
-    G, NS, NC = nlp.G, nlp.NS, nlp.NC
+    """Per grid point DAE inputs [t, states, controls(, accelerations)]."""
+    G, NS, NC, NDV = nlp.G, nlp.NS, nlp.NC, nlp.NDV
     t = np.array([(x[1] - x[0]) * g + x[0] for g in _grid(nlp)])
     S = x[2:2 + NS * G].reshape(G, NS)
-    U = x[2 + NS * G:].reshape(G, NC)
-    return np.concatenate([t[:, None], S, U], 1)
+    U = x[2 + NS * G:2 + (NS + NC) * G].reshape(G, NC)
+    W = x[2 + (NS + NC) * G:].reshape(G, NDV)
+    return np.concatenate([t[:, None], S, U, W], 1)
 
 
 def _grid(nlp):
@@ -208,14 +245,15 @@ def test_dae_probe(name, backend):
 @pytest.mark.parametrize("name", list(CASES))
 def test_eval_g(name, backend):
     gpu, ref, _ = _pair(name, backend)
-    rpi = gpu.m // gpu.opts.num_mesh_intervals
     for _, x in _iterates(gpu):
         g, g0 = gpu.eval_g(x), ref.eval_g(x)
         Fi, hi = _interval_scale(ref, x)
         # rounding of the DAE itself (measured through mh_eval_dae, the same
-        # kernel path) enters the defects scaled by the interval length
+        # kernel path) enters the defects scaled by the interval length, and
+        # the implicit residual rows unscaled
         dYi = _interval_dae_diff(gpu, ref, x)
-        _assert_close(g, g0, np.repeat(1e-10 * (Fi * hi + np.abs(x).max() + 1.0) + 2 * dYi * hi, rpi),
+        _assert_close(g, g0, _per_row(ref, 1e-10 * (Fi * (hi + 1.0) + np.abs(x).max() + 1.0)
+                                     + 2 * dYi * (hi + 1.0)),
                       _row_mask(ref, x))
 
 
@@ -223,18 +261,18 @@ def test_eval_g(name, backend):
 @pytest.mark.parametrize("name", list(CASES))
 def test_eval_jac_g(name, backend):
     gpu, ref, st = _pair(name, backend)
-    rpi = gpu.m // gpu.opts.num_mesh_intervals
     ir, _ = gpu.jac_structure()
     for _, x in _iterates(gpu):
         J, J0 = gpu.eval_jac_g(x), ref.eval_jac_g(x)
         Fi, hi = _interval_scale(ref, x)
         dYi = _interval_dae_diff(gpu, ref, x)
         tau_int = 4 * (dYi + 64 * EPS * (Fi + 1.0)) * (hi + 1.0) / st.solver.fd_step
-        _assert_close(J, J0, 1e-8 * _scale(J0) + tau_int[ir // rpi], _row_mask(ref, x)[ir])
+        _assert_close(J, J0, 1e-8 * _scale(J0) + tau_int[_row_interval(gpu, ir)], _row_mask(ref, x)[ir])
 
 
 @pytest.mark.parametrize("name", ["sliding_mass", "double_pendulum_hs", "gait_rigid_forward",
-                                  "gait_compliant_central"])
+                                  "gait_compliant_central", "double_pendulum_implicit_hs",
+                                  "gait_rigid_implicit"])
 def test_objective_and_gradient(name):
     gpu, ref, st = _pair(name)
     for _, x in _iterates(gpu):
@@ -245,7 +283,8 @@ def test_objective_and_gradient(name):
         assert np.all(np.abs(gf - gf0) <= tol)
 
 
-@pytest.mark.parametrize("name", ["double_pendulum_hs", "gait_rigid_forward"])
+@pytest.mark.parametrize("name", ["double_pendulum_hs", "gait_rigid_forward", "double_pendulum_implicit_hs",
+                                  "gait_rigid_implicit"])
 def test_shards_reassemble_bit_exact(name):
     """Mesh-interval shards (the multi-GPU partition) concatenate to exactly
     the unsharded g and Jacobian values."""
@@ -257,9 +296,10 @@ def test_shards_reassemble_bit_exact(name):
     g, J = full.eval_g(x), full.eval_jac_g(x)
     cuts = [0, N // 3, (2 * N) // 3, N]
     gs, Js = [], []
+    rpi, tail = _rows(full)
     for a, b in zip(cuts[:-1], cuts[1:]):
         sh = HipNLP(rep, st.solver.options(a, b))
-        assert (sh.row_begin, sh.row_end) == (a * full.m // N, b * full.m // N)
+        assert (sh.row_begin, sh.row_end) == (a * rpi, b * rpi + (tail if b == N else 0))
         gs.append(sh.eval_g(x))
         Js.append(sh.eval_jac_g(x))
     assert np.array_equal(np.concatenate(gs), g)
@@ -290,7 +330,8 @@ def test_repeatable_bitwise():
 
 def test_generated_backends_are_selected_for_bundled_models():
     for name in ["sliding_mass", "double_pendulum_hs", "gait_rigid_forward",
-                 "gait_compliant_central", "gait_torque_driven"]:
+                 "gait_compliant_central", "gait_torque_driven", "sliding_mass_implicit",
+                 "double_pendulum_implicit_hs", "gait_rigid_implicit"]:
         gpu, _, _ = _pair(name)
         be, flops, _ = gpu.backend()
         assert be.startswith("generated:"), (name, be)
@@ -307,7 +348,7 @@ def test_fused_g_jac_identical_to_separate_calls(name):
 
 
 @pytest.mark.parametrize("name", ["double_pendulum_hs", "gait_rigid_forward", "gait_rigid_central",
-                                  "gait_compliant_central", "gait_torque_driven"])
+                                  "gait_compliant_central", "gait_torque_driven", "gait_rigid_implicit"])
 def test_pruned_tasks_bit_identical(name):
     """Re-evaluating only the groups a direction perturbs gives exactly the
     Jacobian of re-evaluating every group for every direction: the reused
@@ -324,7 +365,9 @@ def test_pruned_tasks_bit_identical(name):
 
 @pytest.mark.parametrize("name", ["sliding_mass", "double_pendulum_hs", "double_pendulum_trap",
                                   "gait_rigid_forward", "gait_rigid_central", "gait_rigid_backward",
-                                  "gait_compliant_central", "gait_torque_driven"])
+                                  "gait_compliant_central", "gait_torque_driven",
+                                  "double_pendulum_implicit_hs", "double_pendulum_implicit_trap",
+                                  "gait_rigid_implicit"])
 @pytest.mark.parametrize("variant", [{"MOCOHIP_INTERVAL": "0"},
                                      {"MOCOHIP_INTERVAL": "0", "MOCOHIP_ASM": "gs"},
                                      {"MOCOHIP_INTERVAL": "0", "MOCOHIP_QUOT": "1"},
