@@ -1,0 +1,61 @@
+"""Problem tape files: a compiled MocoProblemRep (the mh_problem the C ABI
+receives) plus the solver options, written to one binary file so that
+native host code (opensim-moco_amd/csrc/host/mh_driver.cpp, or a C++
+MocoSolver plugin) can drive libmocohip without Python.
+
+Layout (little endian, x86-64 struct layout of include/mocohip.h):
+  magic "MHTAPE01", int32 version, int32 NS, int32 NC, mh_options,
+  the 12 mh_model counts, gravity[3], time bounds (2 x mh_bounds),
+  ngoals, nterms, then the arrays in mh_model / mh_problem field order,
+  each as (int64 byte count, bytes)."""
+from __future__ import annotations
+
+import ctypes as C
+import struct
+
+from . import abi
+
+MAGIC = b"MHTAPE01"
+VERSION = 1
+
+# (field, element type, count attribute of mh_model / None for problem arrays)
+_MODEL_ARRAYS = [
+    ("bodies", abi.mh_body, "nbodies"), ("axes", abi.mh_axis, "naxes"),
+    ("functions", abi.mh_function, "nfunctions"), ("knot_x", C.c_double, "nknots"),
+    ("knot_y", C.c_double, "nknots"), ("muscles", abi.mh_muscle, "nmuscles"),
+    ("points", abi.mh_path_point, "npoints"), ("actuators", abi.mh_actuator, "nactuators"),
+    ("tables", abi.mh_table, "ntables"), ("table_breaks", C.c_double, "nbreaks"),
+    ("table_coefs", C.c_double, "ncoefs"), ("external", abi.mh_external_force, "nexternal"),
+]
+_COUNTS = ["nq", "nbodies", "naxes", "nfunctions", "nknots", "nmuscles", "npoints",
+           "nactuators", "ntables", "nbreaks", "ncoefs", "nexternal"]
+
+
+def _blob(ptr, ctype, count: int) -> bytes:
+    if count <= 0 or not ptr:
+        return b""
+    return C.string_at(ptr, C.sizeof(ctype) * count)
+
+
+def write_tape(rep, opts: abi.mh_options, path: str) -> None:
+    """Serialize ``rep`` (a ProblemRep) and ``opts`` to ``path``."""
+    p = rep.struct
+    m = p.model
+    ns, nc = len(rep.state_names), len(rep.control_names)
+    out = [MAGIC, struct.pack("<iii", VERSION, ns, nc), bytes(opts)]
+    out.append(struct.pack("<12i", *[getattr(m, k) for k in _COUNTS]))
+    out.append(struct.pack("<3d", *m.gravity))
+    out.append(bytes(p.time_initial) + bytes(p.time_final))
+    out.append(struct.pack("<ii", p.ngoals, p.nterms))
+    blobs = [_blob(getattr(m, f), t, getattr(m, cnt)) for f, t, cnt in _MODEL_ARRAYS]
+    blobs += [_blob(p.state_infos, abi.mh_variable_info, ns),
+              _blob(p.control_infos, abi.mh_variable_info, nc),
+              _blob(p.goals, abi.mh_goal, p.ngoals),
+              _blob(p.goal_index, C.c_int32, p.nterms),
+              _blob(p.goal_column, C.c_int32, p.nterms),
+              _blob(p.goal_weight, C.c_double, p.nterms)]
+    for b in blobs:
+        out.append(struct.pack("<q", len(b)))
+        out.append(b)
+    with open(path, "wb") as fh:
+        fh.write(b"".join(out))

@@ -23,5 +23,6 @@ d["source"] = sys.argv[1]
 json.dump(d, open("profiles/pmc_current.json", "w"), indent=1)
 PY
 fi
+[ -f "gpurun_out/$TAG/driver.json" ] && cp "gpurun_out/$TAG/driver.json" "$DEST/driver.json"
 [ -f "gpurun_out/$TAG/host.txt" ] && head -20 "gpurun_out/$TAG/host.txt" > "$DEST/host.txt"
 ls "$DEST"

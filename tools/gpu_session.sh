@@ -18,6 +18,7 @@ if [[ $WHAT == tests || $WHAT == all ]]; then
 fi
 if [[ $WHAT == bench || $WHAT == all ]]; then
     timeout -k 10 300 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
+    timeout -k 10 120 python tools/driver_bench.py 200 > "$OUT/driver.json" 2> "$OUT/driver.err"
 fi
 if [[ $WHAT == profile || $WHAT == all ]]; then
     timeout -k 10 900 bash tools/profile_gpu.sh "$TAG"

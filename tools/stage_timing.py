@@ -19,9 +19,9 @@ def main():
     from mocohip import configs
     from mocohip.solver import HipNLP
     Ns = [int(a) for a in sys.argv[1:]] or [200, 400]
-    variants = [{}, {"MOCOHIP_INTERVAL": "0"}]
+    variants = [{}, {"MOCOHIP_GRAPHS": "1"}, {"MOCOHIP_SPIN": "1"}, {"MOCOHIP_GRAPHS": "1", "MOCOHIP_SPIN": "1"}]
     for N, var in [(N, v) for N in Ns for v in variants]:
-        for k in ("MOCOHIP_ORDER", "MOCOHIP_INTERVAL", "MOCOHIP_ASM", "MOCOHIP_QUOT", "MOCOHIP_EVENTS", "MOCOHIP_TABLES", "MOCOHIP_ROWSEG"):
+        for k in ("MOCOHIP_ORDER", "MOCOHIP_INTERVAL", "MOCOHIP_ASM", "MOCOHIP_QUOT", "MOCOHIP_EVENTS", "MOCOHIP_TABLES", "MOCOHIP_GRAPHS", "MOCOHIP_SPIN"):
             os.environ.pop(k, None)
         os.environ.update(var)
         st = configs.gait10dof18musc(N, fd_scheme="forward")
