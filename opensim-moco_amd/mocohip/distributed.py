@@ -32,33 +32,38 @@ def shard_counts(num_intervals: int, world: int) -> List[int]:
 class ShardGather:
     """Fixed-size segment buffers and their all-gather.
 
-    Each rank writes its shard's g rows into ``gseg[:count*rows_per_interval]``
-    and its Jacobian values into ``vseg[:count*nnz_per_interval]``.
+    Each rank writes its shard's g rows into ``gseg[:g_sizes[rank]]`` and its
+    Jacobian values into ``vseg[:v_sizes[rank]]``.
     ``gather()`` all-gathers both. The results are padded per rank to the
     largest shard; ``full_g()`` / ``full_values()`` return the unpadded full
     vectors in the global row / nonzero order.
     """
 
     def __init__(self, num_intervals: int, rows_per_interval: int, nnz_per_interval: int,
-                 world: int, device, group=None):
+                 world: int, device, group=None, tail_rows: int = 0, tail_nnz: int = 0):
+        """``tail_rows`` / ``tail_nnz``: rows and nonzeros after the last
+        interval (implicit dynamics: the final grid point's residuals), owned
+        by the last rank (mh_nlp_info row_end / nnz_end)."""
         import torch
         self.N, self.rpi, self.nzi, self.world = num_intervals, rows_per_interval, nnz_per_interval, world
         self.group = group
         self.counts = shard_counts(num_intervals, world)
-        self.seg_int = max(self.counts)
+        self.tail = (tail_rows, tail_nnz)
+        self.g_sizes = [c * rows_per_interval + (tail_rows if r == world - 1 else 0)
+                        for r, c in enumerate(self.counts)]
+        self.v_sizes = [c * nnz_per_interval + (tail_nnz if r == world - 1 else 0)
+                        for r, c in enumerate(self.counts)]
         f64 = torch.float64
-        self.gseg = torch.zeros(self.seg_int * rows_per_interval, dtype=f64, device=device)
-        self.vseg = torch.zeros(self.seg_int * nnz_per_interval, dtype=f64, device=device)
+        self.gseg = torch.zeros(max(self.g_sizes), dtype=f64, device=device)
+        self.vseg = torch.zeros(max(self.v_sizes), dtype=f64, device=device)
         self.gall = torch.zeros(world * self.gseg.numel(), dtype=f64, device=device)
         self.vall = torch.zeros(world * self.vseg.numel(), dtype=f64, device=device)
-        self._g_index = self._unpad_index(rows_per_interval, device)
-        self._v_index = self._unpad_index(nnz_per_interval, device)
+        self._g_index = self._unpad_index(self.g_sizes, self.gseg.numel(), device)
+        self._v_index = self._unpad_index(self.v_sizes, self.vseg.numel(), device)
 
-    def _unpad_index(self, per_interval: int, device):
+    def _unpad_index(self, sizes, seg: int, device):
         import torch
-        parts = [torch.arange(r * self.seg_int * per_interval,
-                              r * self.seg_int * per_interval + c * per_interval, device=device)
-                 for r, c in enumerate(self.counts)]
+        parts = [torch.arange(r * seg, r * seg + n, device=device) for r, n in enumerate(sizes)]
         return torch.cat(parts)
 
     def gather(self):

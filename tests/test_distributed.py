@@ -46,18 +46,27 @@ def _worker(rank, world, port, case, N, out):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         st = {"pendulum": lambda: configs.double_pendulum(N),
-              "gait": lambda: configs.gait10dof18musc(N)}[case]()
+              "gait": lambda: configs.gait10dof18musc(N),
+              "pendulum_implicit": lambda: configs.double_pendulum(N, dynamics="implicit")}[case]()
         rep = st.problem.create_rep()
         ref = OracleNLP(rep, st.solver.options(), threads=1)
         x = ref.random_iterate(np.random.default_rng(3).uniform(-1, 1, ref.n))
         g, J = ref.eval_g(x), ref.eval_jac_g(x)
-        rpi, nzi = ref.m // N, ref.nnz // N
-        sg = ShardGather(N, rpi, nzi, world, "cpu")
+        # implicit dynamics: the final point's residual rows follow the last
+        # interval (tail), owned by the last rank
+        tail_rows = ref.NDV
+        ir, _ = ref.jac_structure()
+        tail_nnz = int((ir >= ref.m - tail_rows).sum())
+        rpi, nzi = (ref.m - tail_rows) // N, (ref.nnz - tail_nnz) // N
+        sg = ShardGather(N, rpi, nzi, world, "cpu", tail_rows=tail_rows, tail_nnz=tail_nnz)
         ib, ie = interval_shard(N, rank, world)
+        rows = (ie - ib) * rpi + (tail_rows if ie == N else 0)
+        nz = (ie - ib) * nzi + (tail_nnz if ie == N else 0)
+        assert rows == sg.g_sizes[rank] and nz == sg.v_sizes[rank]
         sg.gseg.zero_()
         sg.vseg.zero_()
-        sg.gseg[:(ie - ib) * rpi] = torch.from_numpy(g[ib * rpi:ie * rpi])
-        sg.vseg[:(ie - ib) * nzi] = torch.from_numpy(J[ib * nzi:ie * nzi])
+        sg.gseg[:rows] = torch.from_numpy(g[ib * rpi:ib * rpi + rows])
+        sg.vseg[:nz] = torch.from_numpy(J[ib * nzi:ib * nzi + nz])
         sg.gather()
         ok = (np.array_equal(sg.full_g().numpy(), g)
               and np.array_equal(sg.full_values().numpy(), J))
@@ -66,7 +75,8 @@ def _worker(rank, world, port, case, N, out):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("case,N,world", [("pendulum", 7, 2), ("pendulum", 10, 3), ("gait", 5, 2)])
+@pytest.mark.parametrize("case,N,world", [("pendulum", 7, 2), ("pendulum", 10, 3), ("gait", 5, 2),
+                                          ("pendulum_implicit", 7, 3)])
 def test_shard_gather_reassembles_full_vectors(case, N, world):
     ctx = mp.get_context("spawn")
     out = ctx.Array("i", [0] * world)
