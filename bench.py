@@ -52,6 +52,9 @@ def parse():
                     help="separate: eval_g then eval_jac_g C-ABI calls; fused: one "
                          "mh_eval_g_jac_g call (IPOPT new_x=false pattern)")
     ap.add_argument("--multi", choices=["replicas", "mesh"], default="replicas")
+    ap.add_argument("--single-mode", action="store_true",
+                    help="measure only --mode (no secondary mode, no batch): for profiler runs, so "
+                         "that every launch of a kernel has the same shape")
     ap.add_argument("--batch", type=int, default=8,
                     help="also measure B independent NLPs per GPU evaluated concurrently, one "
                          "context (HIP stream) and host thread each (the configs[4] batch layout); "
@@ -148,11 +151,13 @@ def main():
     # secondary: the same K steps as one fused call each (IPOPT's
     # eval_g(new_x) -> eval_jac_g(!new_x) pair from one DAE pass)
     other = "fused" if args.mode == "separate" else "separate"
-    mode0, args.mode = args.mode, other
-    for _ in range(args.warmup):
-        step()
-    other_elapsed = timed(args.steps, False)
-    args.mode = mode0
+    other_elapsed = None
+    if not args.single_mode:
+        mode0, args.mode = args.mode, other
+        for _ in range(args.warmup):
+            step()
+        other_elapsed = timed(args.steps, False)
+        args.mode = mode0
     # instrumented pass (roofline): same K steps with stage events
     nlp.set_timing(True)
     inst_elapsed = timed(args.steps, True)
@@ -161,7 +166,7 @@ def main():
     ms_per_step = 1e3 * elapsed / args.steps
     value = (args.steps if mesh else args.steps * world) / elapsed
     batch = None
-    if args.batch > 1 and not mesh:
+    if args.batch > 1 and not mesh and not args.single_mode:
         batch = batch_throughput(args, rep, st, local, rank, world, dev, torch, dist)
 
     if rank == 0:
@@ -227,7 +232,8 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
         }
-        line[f"value_{other}"] = round((args.steps if mesh else args.steps * world) / other_elapsed, 3)
+        if other_elapsed:
+            line[f"value_{other}"] = round((args.steps if mesh else args.steps * world) / other_elapsed, 3)
         if batch:
             line["batch"] = batch
         if cpu and cpu.get("value"):

@@ -11,7 +11,7 @@ ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-B="$ROOT/bench.py --steps 50 --warmup 5 --no-cpu-baseline"
+B="$ROOT/bench.py --steps 50 --warmup 5 --no-cpu-baseline --single-mode"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_fused" -o run \
     -- python3 $B --mode fused > "$OUT/trace_fused.log" 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_separate" -o run \
