@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define MH_ABI_VERSION 1
+#define MH_ABI_VERSION 2
 
 enum mh_status {
     MH_OK = 0,
@@ -232,6 +232,29 @@ typedef struct mh_goal {
     double weight;       /* MocoGoal weight                                */
 } mh_goal;
 
+/* Path constraints: MocoPathConstraint errors evaluated
+ * at every mesh point (CasOCTranscription.cpp:419-433), rows placed before
+ * the mesh point's residuals (flattenConstraints, CasOCTranscription.h:
+ * 286-311).  A MocoControlBoundConstraint
+ * (MocoControlBoundConstraint.cpp:38-146) expands, per control path in
+ * order, to one equation per bound function (lower, then upper):
+ *     error = control[index] - bound(t)
+ * with g bounds [0, inf] (lower), [-inf, 0] (upper) or [0, 0]
+ * (equality_with_lower).  bound(t) is the piecewise polynomial column
+ * `column` of model table `table` (Constant: table = -1, `value`).  Each
+ * equation's Jacobian row is block-dense over t0, tf and the mesh point's
+ * inputs, and its values are the finite-difference quotients of the
+ * path-constraint function, as for the DAE outputs. */
+enum mh_path_kind { MH_PATH_CONTROL_BOUND = 0 };
+typedef struct mh_path_equation {
+    int32_t kind;        /* mh_path_kind                                   */
+    int32_t index;       /* control index                                  */
+    int32_t table;       /* bound function: model table, -1 = constant     */
+    int32_t column;      /* table column                                   */
+    double value;        /* constant bound (table = -1)                    */
+    mh_bounds g;         /* bounds on the constraint row                   */
+} mh_path_equation;
+
 typedef struct mh_problem {
     mh_model model;
     mh_bounds time_initial;      /* bounds on initial_time                  */
@@ -244,6 +267,9 @@ typedef struct mh_problem {
     const int32_t* goal_index;   /* control index / state index per term    */
     const int32_t* goal_column;  /* tracking: table column per term         */
     const double* goal_weight;   /* per-term weight                         */
+    int32_t npath;               /* path-constraint equations per mesh point */
+    int32_t reserved;
+    const mh_path_equation* path;
 } mh_problem;
 
 enum mh_scheme { MH_HERMITE_SIMPSON = 0, MH_TRAPEZOIDAL = 1 };

@@ -73,6 +73,7 @@ struct Tape {
     std::vector<mh_goal> goals;
     std::vector<int32_t> gidx, gcol;
     std::vector<double> gw;
+    std::vector<mh_path_equation> path;
     mh_problem prob{};
 };
 
@@ -94,7 +95,7 @@ bool read_tape(const char* path, Tape& t, std::string& err) {
     const int version = r.pod<int32_t>();
     t.ns = r.pod<int32_t>();
     t.nc = r.pod<int32_t>();
-    if (version != 1) { err = "unsupported tape version"; return false; }
+    if (version != 1 && version != 2) { err = "unsupported tape version"; return false; }
     t.opts = r.pod<mh_options>();
     mh_model& m = t.prob.model;
     int32_t* counts[] = {&m.nq, &m.nbodies, &m.naxes, &m.nfunctions, &m.nknots, &m.nmuscles,
@@ -123,6 +124,10 @@ bool read_tape(const char* path, Tape& t, std::string& err) {
     t.gidx = r.array<int32_t>(t.prob.nterms);
     t.gcol = r.array<int32_t>(t.prob.nterms);
     t.gw = r.array<double>(t.prob.nterms);
+    if (version >= 2) {   // path-constraint equations
+        t.prob.npath = r.pod<int32_t>();
+        t.path = r.array<mh_path_equation>(t.prob.npath);
+    }
     if (!r.ok || r.pos != r.buf.size()) { err = "truncated or malformed tape"; return false; }
     m.bodies = t.bodies.data(); m.axes = t.axes.data(); m.functions = t.functions.data();
     m.knot_x = t.knot_x.data(); m.knot_y = t.knot_y.data(); m.muscles = t.muscles.data();
@@ -134,6 +139,7 @@ bool read_tape(const char* path, Tape& t, std::string& err) {
     t.prob.goal_index = t.gidx.data();
     t.prob.goal_column = t.gcol.data();
     t.prob.goal_weight = t.gw.data();
+    t.prob.path = t.path.data();
     return true;
 }
 

@@ -79,7 +79,8 @@ extern "C" const char* mh_last_error(void) { return g_err.c_str(); }
 enum TplKind : uint8_t {
     T_HERM_T = 0, T_SIMP_T = 1, T_HERM_X = 2, T_SIMP_X = 3, T_INTERP = 4,
     T_TRAP_T = 5, T_TRAP_X = 6,
-    T_RES = 7      // implicit multibody residual output s at point pt
+    T_RES = 7,     // implicit multibody residual output s at point pt
+    T_PATH = 8     // path-constraint equation s at mesh point pt
 };
 struct TplEntry {
     int16_t row;   // row within the interval
@@ -89,15 +90,15 @@ struct TplEntry {
     int16_t s;     // state index of the row (defects) / control index (interp)
 };
 // 4-byte form of a template entry (staged in LDS by k_interval):
-// kind | pt << 3 | dir << 5 | s << 16 (the row is not needed to evaluate it).
+// kind | pt << 4 | dir << 6 | s << 16 (the row is not needed to evaluate it).
 __host__ __device__ __forceinline__ uint32_t tpl_pack(const TplEntry& e) {
-    return (uint32_t)e.kind | ((uint32_t)e.pt << 3) | ((uint32_t)e.dir << 5) | ((uint32_t)e.s << 16);
+    return (uint32_t)e.kind | ((uint32_t)e.pt << 4) | ((uint32_t)e.dir << 6) | ((uint32_t)e.s << 16);
 }
 __host__ __device__ __forceinline__ TplEntry tpl_unpack(uint32_t u) {
     TplEntry e;
-    e.kind = (uint8_t)(u & 7u);
-    e.pt = (uint8_t)((u >> 3) & 3u);
-    e.dir = (int16_t)((u >> 5) & 2047u);
+    e.kind = (uint8_t)(u & 15u);
+    e.pt = (uint8_t)((u >> 4) & 3u);
+    e.dir = (int16_t)((u >> 6) & 1023u);
     e.row = 0;
     e.s = (int16_t)(u >> 16);
     return e;
@@ -509,6 +510,17 @@ __global__ void __launch_bounds__(1024) k_combine(DevModel M, Src S, Lanes Ln, T
     }
 }
 
+// Path-constraint equations (include/mocohip.h mh_path_equation) and the
+// tables / grid their bound functions and time seeds read.
+struct PathEqs {
+    int npc;         // equations per mesh point
+    const mh_path_equation* __restrict__ eq;
+    const mh_table* __restrict__ tabs;
+    const double* __restrict__ brk;
+    const double* __restrict__ coef;
+    const double* __restrict__ grid;
+};
+
 struct Interval {
     int scheme;      // MH_HERMITE_SIMPSON / MH_TRAPEZOIDAL
     int interp;
@@ -517,13 +529,75 @@ struct Interval {
     int nnz_int;     // nonzeros per interval
     int nres;        // multibody residual rows per grid point (implicit: NQ)
     int N;           // mesh intervals of the whole problem
-    int nnz_tail;    // nonzeros of the final grid point's residual rows
-    // The interval N-1 also owns the final grid point's residual rows
-    // (flattenConstraints, CasOCTranscription.h:306-308): rows rpi..rpi+nres
-    // after its own, template entries nnz_int.. nnz_int+nnz_tail.
-    __device__ __forceinline__ int rows(int i) const { return rpi + (i == N - 1 ? nres : 0); }
+    int nnz_tail;    // nonzeros of the tail rows
+    int ntail;       // tail rows: final mesh point's path rows + final residuals
+    PathEqs P;
+    // Every interval opens with its mesh point's path rows.  The interval
+    // N-1 also owns the tail (flattenConstraints, CasOCTranscription.h:
+    // 286-308): the final mesh point's path rows, then the final grid
+    // point's residual rows, as rows rpi..rpi+ntail after its own and
+    // template entries nnz_int..nnz_int+nnz_tail.
+    __device__ __forceinline__ int rows(int i) const { return rpi + (i == N - 1 ? ntail : 0); }
     __device__ __forceinline__ int entries(int i) const { return nnz_int + (i == N - 1 ? nnz_tail : 0); }
 };
+
+// Path-constraint arithmetic, evaluated in order without contraction so
+// that the finite-difference quotients see the same roundings as the CPU
+// restatement (the perturbed time t + h*seed, the Horner steps).
+__device__ __forceinline__ double path_bound(const PathEqs& P, const mh_path_equation& E, double t) {
+#pragma clang fp contract(off)
+    if (E.table < 0) return E.value;
+    const mh_table T = P.tabs[E.table];
+    const double* br = P.brk + T.break_begin;
+    int s;
+    if (t <= br[0]) s = 0;
+    else if (t >= br[T.nseg]) s = T.nseg - 1;
+    else {
+        int lo = 0, hi = T.nseg;
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (t < br[mid]) hi = mid; else lo = mid;
+        }
+        s = lo;
+    }
+    const double* cf = P.coef + T.coef_begin + ((long)s * T.ncol + E.column) * (T.degree + 1);
+    const double dt = t - br[s];
+    double v = cf[T.degree];
+    for (int k = T.degree - 1; k >= 0; --k) v = v * dt + cf[k];
+    return v;
+}
+// MocoControlBoundConstraint::calcPathConstraintErrorsImpl
+// (MocoControlBoundConstraint.cpp:130-146): control - bound(t).
+__device__ __forceinline__ double path_value(const PathEqs& P, int e, double t, double control) {
+    const mh_path_equation E = P.eq[e];
+    return control - path_bound(P, E, t);
+}
+// FD quotient of equation e at grid point k along direction dir (0 = t0,
+// 1 = tf, 2 + j = point input j), CasADi FiniteDiff as for the DAE lanes.
+// The equation reads only its control and the time: along any other input
+// the perturbed and base values are equal and the quotient is exactly 0.
+__device__ __forceinline__ double path_quot(const PathEqs& P, const Lanes& Ln, int NS, int e, int k,
+        double t, double control, int dir) {
+#pragma clang fp contract(off)
+    const mh_path_equation E = P.eq[e];
+    if (dir >= 2 && dir != 2 + NS + E.index) return 0.0;
+    const double h = Ln.h;
+    double tp = t, tm = t, cp = control, cm = control;
+    if (dir < 2) {
+        const double g = P.grid[k];
+        const double seed = dir == 0 ? 1.0 - g : g;
+        tp = t + h * seed;
+        tm = t - h * seed;
+    } else {
+        cp = control + h;
+        cm = control - h;
+    }
+    if (Ln.fd == MH_FD_CENTRAL)
+        return ((cp - path_bound(P, E, tp)) - (cm - path_bound(P, E, tm))) / (2.0 * h);
+    const double v0 = control - path_bound(P, E, t);
+    if (Ln.fd == MH_FD_FORWARD) return ((cp - path_bound(P, E, tp)) - v0) / h;
+    return (v0 - (cm - path_bound(P, E, tm))) / h;
+}
 
 __device__ __forceinline__ int grid_of(const Interval& I, int i, int pt) {
     return I.scheme == MH_HERMITE_SIMPSON ? 2 * i + pt : i + pt;
@@ -592,8 +666,15 @@ __device__ __forceinline__ double defect_row(const Layout& L, const Interval& I,
     // for the last interval the final grid point after all its other rows
     const int npres = I.scheme == MH_HERMITE_SIMPSON ? 2 : 1;
     const int k_first = I.scheme == MH_HERMITE_SIMPSON ? 2 * i : i;
+    const int npc = I.P.npc;
+    if (r >= I.rpi) {   // tail: final mesh point's path rows, then its residuals
+        const int rt = r - I.rpi, kl = k_first + npres;
+        if (rt < npc) return path_value(I.P, rt, Y.t(kl), Y.xc(kl, I.P.eq[rt].index));
+        return Y.row(kl, rt - npc)[Ln.base];
+    }
+    if (r < npc) return path_value(I.P, r, Y.t(k_first), Y.xc(k_first, I.P.eq[r].index));
+    r -= npc;
     if (r < npres * I.nres) return Y.row(k_first + r / I.nres, r % I.nres)[Ln.base];
-    if (r >= I.rpi) return Y.row(k_first + npres, r - I.rpi)[Ln.base];
     r -= npres * I.nres;
     if (I.scheme == MH_HERMITE_SIMPSON) {
         const int ki = 2 * i, km = ki + 1, kp = ki + 2;
@@ -655,8 +736,10 @@ __device__ __forceinline__ IvC iv_const(double h, double dgap) {
 // Jacobian value of template entry T of the interval whose first grid point
 // is k_first (HS: d/d[t0,tf] of -(h/8)(f_i - f_p) with dh/dt0 = -dgap,
 // dh/dtf = dgap, etc.).
-template <class YV>
-__device__ __forceinline__ double jac_entry(const Layout& L, const Lanes& Ln,
+// WITH_PATH = false compiles the path-constraint case out (k_interval
+// evaluates those entries in a loop of their own, off the hot loop).
+template <bool WITH_PATH = true, class YV>
+__device__ __forceinline__ double jac_entry(const Layout& L, const Lanes& Ln, const PathEqs& P,
         const double* __restrict__ x, const YV& Y, const TplEntry T, int k_first, const IvC& C) {
     const int s = T.s, dir = T.dir;
     double v = 0.0;
@@ -701,6 +784,12 @@ __device__ __forceinline__ double jac_entry(const Layout& L, const Lanes& Ln,
     case T_RES:
         v = dout(Ln, Y, k_first + T.pt, s, dir);
         break;
+    case T_PATH:
+        if constexpr (WITH_PATH) {
+            const int k = k_first + T.pt;
+            v = path_quot(P, Ln, L.NS, s, k, Y.t(k), Y.xc(k, P.eq[s].index), dir);
+        }
+        break;
     case T_TRAP_T: {
         const int ki = k_first, kp = k_first + 1;
         const double fi = xdot_at(L, Ln, x, Y, ki, s), fp = xdot_at(L, Ln, x, Y, kp, s);
@@ -744,7 +833,7 @@ __global__ void __launch_bounds__(256) k_transcribe(Layout L, Interval I, Lanes 
         double* vi = values + (long)il * I.nnz_int;
         const int e_end = min(I.entries(i), ((int)blockIdx.x + 1) * ASM_CHUNK);
         for (int e = (int)blockIdx.x * ASM_CHUNK + threadIdx.x; e < e_end; e += blockDim.x)
-            vi[e] = jac_entry(L, Ln, x, YV, tpl[e], k_first, C);
+            vi[e] = jac_entry(L, Ln, I.P, x, YV, tpl[e], k_first, C);
     } else {
         double* gi = g + (long)il * I.rpi;
         for (int r = threadIdx.x; r < I.rows(i); r += blockDim.x) gi[r] = defect_row(L, I, Ln, x, YV, i, r);
@@ -779,7 +868,7 @@ __global__ void __launch_bounds__(256) k_transcribe_gs(Layout L, Interval I, Lan
             int k_first, k_last;
             interval_span(I, i, k_first, k_last);
             const IvC C = iv_const(YV.t(k_last) - YV.t(k_first), grid[k_last] - grid[k_first]);
-            values[w] = jac_entry(L, Ln, x, YV, tpl[e], k_first, C);
+            values[w] = jac_entry(L, Ln, I.P, x, YV, tpl[e], k_first, C);
         }
     }
     if (g) {
@@ -792,14 +881,14 @@ __global__ void __launch_bounds__(256) k_transcribe_gs(Layout L, Interval I, Lan
     }
     // the final grid point's residual rows (implicit mode), owned by the
     // shard holding the last interval
-    if (I.ib + nint == I.N && (I.nres > 0)) {
+    if (I.ib + nint == I.N && (I.ntail > 0)) {
         const int i = I.N - 1, il = nint - 1;
         int k_first, k_last;
         interval_span(I, i, k_first, k_last);
         if (values) {
             const IvC C = iv_const(YV.t(k_last) - YV.t(k_first), grid[k_last] - grid[k_first]);
             for (int e = I.nnz_int + tid; e < I.entries(i); e += nthreads)
-                values[(long)il * I.nnz_int + e] = jac_entry(L, Ln, x, YV, tpl[e], k_first, C);
+                values[(long)il * I.nnz_int + e] = jac_entry(L, Ln, I.P, x, YV, tpl[e], k_first, C);
         }
         if (g)
             for (int r = I.rpi + tid; r < I.rows(i); r += nthreads)
@@ -899,9 +988,13 @@ __global__ void __launch_bounds__(1024) k_interval(DevModel M, Src S, Lanes Ln, 
         const int ne = I.entries(i);
         const int B = blockDim.x;
         int e = threadIdx.x;
+        // path-constraint entries (the first npe of the interval and of
+        // the tail) are written by their own loop below
         if (tables_lds) {
-            for (; e < ne; e += B)
-                vi[e] = jac_entry(L, Ln, S.x, YV, tpl_unpack(tp[e]), k_first, C);
+            for (; e < ne; e += B) {
+                const TplEntry te = tpl_unpack(tp[e]);
+                if (te.kind != T_PATH) vi[e] = jac_entry<false>(L, Ln, I.P, S.x, YV, te, k_first, C);
+            }
             e = ne;
         }
         // template entries for IV_UNROLL iterations are loaded before any is
@@ -911,9 +1004,21 @@ __global__ void __launch_bounds__(1024) k_interval(DevModel M, Src S, Lanes Ln, 
 #pragma unroll
             for (int u = 0; u < IV_UNROLL; ++u) te[u] = tpl[e + u * B];
 #pragma unroll
-            for (int u = 0; u < IV_UNROLL; ++u) vi[e + u * B] = jac_entry(L, Ln, S.x, YV, te[u], k_first, C);
+            for (int u = 0; u < IV_UNROLL; ++u)
+                if (te[u].kind != T_PATH) vi[e + u * B] = jac_entry<false>(L, Ln, I.P, S.x, YV, te[u], k_first, C);
         }
-        for (; e < ne; e += B) vi[e] = jac_entry(L, Ln, S.x, YV, tpl[e], k_first, C);
+        for (; e < ne; e += B) {
+            const TplEntry te = tpl[e];
+            if (te.kind != T_PATH) vi[e] = jac_entry<false>(L, Ln, I.P, S.x, YV, te, k_first, C);
+        }
+        if (I.P.npc > 0) {
+            const int npe = I.P.npc * (2 + L.NI);
+            const int nw = i == I.N - 1 ? 2 * npe : npe;
+            for (int w = threadIdx.x; w < nw; w += B) {
+                const int ep = w < npe ? w : I.nnz_int + (w - npe);
+                vi[ep] = jac_entry<true>(L, Ln, I.P, S.x, YV, tpl[ep], k_first, C);
+            }
+        }
     }
     MH_IV_STAMP(3)
 }
@@ -1290,6 +1395,9 @@ struct mh_ctx {
     int NQ = 0, NZ = 0, NS = 0, NC = 0, NO = 0, NI = 0;
     int scheme = 0, N = 0, G = 0, interp = 0, rpi = 0, nnz_int = 0;
     int NDV = 0, nnz_tail = 0;     // implicit: accelerations per point, tail nonzeros
+    int npc = 0, ntail = 0;        // path equations per mesh point; tail rows (npc + NDV)
+    std::vector<mh_path_equation> pc;
+    PathEqs P{};
     double acc_lo = -1000.0, acc_hi = 1000.0;
     int ib = 0, ie = 0, k0 = 0, nk = 0;
     int fd = 0;
@@ -1416,12 +1524,22 @@ static void build_template(mh_ctx* c) {
             emit_row(row++, T_RES, T_RES, o, v, pt);
         }
     };
+    // path-constraint rows of mesh point pt: block-dense like the residuals
+    // (CasOCTranscription.cpp:419-433, sparsity detection "none")
+    auto path_rows = [&](int& row, int pt) {
+        for (int e = 0; e < c->npc; ++e) {
+            std::vector<Col> v{{pt, 0}, {pt, 1}};
+            point_all(pt, v);
+            emit_row(row++, T_PATH, T_PATH, e, v, pt);
+        }
+    };
     // implicit speed rows: udot = the acceleration variable (direct MX
     // expression, CasOCTranscription.cpp:339-341): own state + acceleration
     auto speed_sparse = [&](int s) { return implicit && s >= NQ && s < 2 * NQ; };
     const int adir = 2 + NS + NC;   // direction of acceleration 0
     int row = 0;
     if (c->scheme == MH_HERMITE_SIMPSON) {
+        path_rows(row, 0);
         residual_rows(row, 0);
         residual_rows(row, 1);
         for (int s = 0; s < NS; ++s) {
@@ -1458,6 +1576,7 @@ static void build_template(mh_ctx* c) {
             }
         }
     } else {
+        path_rows(row, 0);
         residual_rows(row, 0);
         for (int s = 0; s < NS; ++s) {
             std::vector<Col> v{{0, 0}, {0, 1}};
@@ -1475,10 +1594,25 @@ static void build_template(mh_ctx* c) {
     }
     c->rpi = row;
     c->nnz_int = (int)c->tpl.size();
-    // tail: residual rows of the last grid point (point 2 of the HS interval,
-    // 1 of the trapezoidal one), rows rpi.. relative to the last interval
+    // tail: path rows of the final mesh point, then residual rows of the
+    // last grid point (point 2 of the HS interval, 1 of the trapezoidal one),
+    // rows rpi.. relative to the last interval
+    path_rows(row, c->scheme == MH_HERMITE_SIMPSON ? 2 : 1);
     residual_rows(row, c->scheme == MH_HERMITE_SIMPSON ? 2 : 1);
     c->nnz_tail = (int)c->tpl.size() - c->nnz_int;
+    c->ntail = row - c->rpi;
+}
+
+// k_interval writes the path-constraint entries in a loop of their own over
+// the first npc * (2 + NI) entries of the interval and of the tail.
+static bool path_entries_lead(const mh_ctx* c) {
+    const int npe = c->npc * (2 + c->NI);
+    if (npe > c->nnz_int || npe > c->nnz_tail) return c->npc == 0;
+    for (int e = 0; e < (int)c->tpl.size(); ++e) {
+        const bool lead = e < npe || (e >= c->nnz_int && e < c->nnz_int + npe);
+        if ((c->tpl[e].kind == T_PATH) != lead) return false;
+    }
+    return true;
 }
 
 static int validate_and_layout(mh_ctx* c, const mh_problem* p, const mh_options* o,
@@ -1524,6 +1658,17 @@ static int validate_and_layout(mh_ctx* c, const mh_problem* p, const mh_options*
         c->acc_hi = o->implicit_accel_bounds[1];
     }
     c->NI = c->NS + c->NC + c->NDV;
+    if (p->npath < 0 || (p->npath > 0 && !p->path)) return set_err(MH_ERR_INVALID, "bad path constraints");
+    c->npc = p->npath;
+    c->pc.assign(p->path, p->path + p->npath);
+    for (int e = 0; e < c->npc; ++e) {
+        const mh_path_equation& E = c->pc[e];
+        if (E.kind != MH_PATH_CONTROL_BOUND)
+            return set_err(MH_ERR_UNSUPPORTED, "path equation %d: kind %d", e, E.kind);
+        if (E.index < 0 || E.index >= c->NC || E.table < -1 || E.table >= M.ntables ||
+                (E.table >= 0 && (E.column < 0 || E.column >= M.tables[E.table].ncol)))
+            return set_err(MH_ERR_INVALID, "path equation %d: bad control/table", e);
+    }
     for (int ia = 0; ia < M.nactuators; ++ia) {
         const mh_actuator& a = M.actuators[ia];
         if (a.kind == MH_ACT_MUSCLE) {
@@ -1609,7 +1754,8 @@ static int validate_and_layout(mh_ctx* c, const mh_problem* p, const mh_options*
     }
     c->n = 2 + (int64_t)(c->NS + c->NC + c->NDV) * c->G;
     build_template(c);
-    c->m = (int64_t)c->rpi * c->N + c->NDV;      // + the final point's residuals
+    if (!path_entries_lead(c)) return set_err(MH_ERR_INVALID, "internal: path-constraint template layout");
+    c->m = (int64_t)c->rpi * c->N + c->ntail;    // + the final mesh point's path rows and residuals
     c->nnz = (int64_t)c->nnz_int * c->N + c->nnz_tail;
     c->ib = std::max(0, o->interval_begin);
     c->ie = o->interval_end > 0 ? std::min(o->interval_end, c->N) : c->N;
@@ -1638,7 +1784,9 @@ static int validate_and_layout(mh_ctx* c, const mh_problem* p, const mh_options*
 }
 
 // FNV-1a 64 over everything the per-point DAE depends on (table *values* are
-// excluded: they are read from HBM at run time).  Selects generated back ends.
+// excluded: they are read from HBM at run time; so are tables the DAE never
+// reads, e.g. tracking references and path-constraint bounds).  Selects
+// generated back ends.
 static uint64_t fnv1a(uint64_t h, const void* p, size_t n) {
     const unsigned char* b = (const unsigned char*)p;
     for (size_t i = 0; i < n; ++i) { h ^= b[i]; h *= 1099511628211ULL; }
@@ -1647,7 +1795,7 @@ static uint64_t fnv1a(uint64_t h, const void* p, size_t n) {
 static uint64_t model_hash(const mh_model* M) {
     uint64_t h = 1469598103934665603ULL;
     const int32_t counts[] = {M->nq, M->nbodies, M->naxes, M->nfunctions, M->nknots, M->nmuscles,
-            M->npoints, M->nactuators, M->ntables, M->nexternal};
+            M->npoints, M->nactuators, M->nexternal};
     h = fnv1a(h, counts, sizeof counts);
     h = fnv1a(h, M->gravity, sizeof M->gravity);
     h = fnv1a(h, M->bodies, sizeof(mh_body) * (size_t)M->nbodies);
@@ -1659,7 +1807,9 @@ static uint64_t model_hash(const mh_model* M) {
     h = fnv1a(h, M->points, sizeof(mh_path_point) * (size_t)M->npoints);
     h = fnv1a(h, M->actuators, sizeof(mh_actuator) * (size_t)M->nactuators);
     h = fnv1a(h, M->external, sizeof(mh_external_force) * (size_t)M->nexternal);
-    for (int t = 0; t < M->ntables; ++t) {
+    for (int e = 0; e < M->nexternal; ++e) {
+        const int t = M->external[e].table;
+        if (t < 0 || t >= M->ntables) continue;
         const int32_t shape[2] = {M->tables[t].degree, M->tables[t].ncol};
         h = fnv1a(h, shape, sizeof shape);
     }
@@ -1739,13 +1889,14 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
                  o_gcol = A.put(p->goal_column, p->nterms), o_gw = A.put(p->goal_weight, p->nterms),
                  o_grid = A.put(c->grid.data(), c->grid.size()),
                  o_quad = A.put(c->quad.data(), c->quad.size()),
-                 o_tpl = A.put(c->tpl.data(), c->tpl.size());
+                 o_tpl = A.put(c->tpl.data(), c->tpl.size()),
+                 o_pc = A.put(c->pc.data(), c->pc.size());
     // packed template, padded to whole doubles (staged in LDS as doubles)
     c->tplp.clear();
     for (const TplEntry& e : c->tpl) {
         c->tplp.push_back(tpl_pack(e));
         const TplEntry u = tpl_unpack(c->tplp.back());
-        if (u.kind != e.kind || u.pt != e.pt || u.dir != e.dir || u.s != e.s || e.dir > 2047 || e.s < 0)
+        if (u.kind != e.kind || u.pt != e.pt || u.dir != e.dir || u.s != e.s || e.dir > 1023 || e.s < 0)
             return set_err(MH_ERR_UNSUPPORTED, "Jacobian template entry does not pack into 32 bits");
     }
     if (c->tplp.size() % 2) c->tplp.push_back(0u);
@@ -1760,7 +1911,7 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     c->lanes_g = Lanes{c->fd, ND, 1, 0, c->h};
     const size_t o_Y = A.reserve(sizeof(double) * (size_t)c->nk * std::max(1, c->NO) * stride);
     const size_t o_Yg = A.reserve(sizeof(double) * (size_t)c->nk * std::max(1, c->NO));
-    const size_t o_g = A.reserve(sizeof(double) * ((size_t)nint * c->rpi + c->NDV));
+    const size_t o_g = A.reserve(sizeof(double) * ((size_t)nint * c->rpi + c->ntail));
     const size_t o_vals = A.reserve(sizeof(double) * ((size_t)nint * c->nnz_int + c->nnz_tail));
     const size_t o_C = A.reserve(sizeof(double) * (size_t)c->G * std::max(1, p->ngoals));
     const size_t o_grad = A.reserve(sizeof(double) * c->n);
@@ -1807,6 +1958,7 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     c->d_grid = (double*)(b + o_grid); c->d_quad = (double*)(b + o_quad);
     c->d_tpl = (TplEntry*)(b + o_tpl);
     c->d_tplp = (uint32_t*)(b + o_tplp);
+    c->P = PathEqs{c->npc, (const mh_path_equation*)(b + o_pc), D.tabs, D.brk, D.coef, c->d_grid};
 
     c->d_x = (double*)(b + o_x); c->d_times = (double*)(b + o_times); c->d_Y = (double*)(b + o_Y);
     c->d_Yg = (double*)(b + o_Yg); c->d_g = (double*)(b + o_g); c->d_vals = (double*)(b + o_vals);
@@ -1872,7 +2024,7 @@ extern "C" int mh_get_nlp_info(const mh_ctx* c, mh_nlp_info* info) {
     info->num_states = c->NS;
     info->num_controls = c->NC;
     info->row_begin = (int64_t)c->ib * c->rpi;
-    info->row_end = (int64_t)c->ie * c->rpi + (c->ie == c->N ? c->NDV : 0);
+    info->row_end = (int64_t)c->ie * c->rpi + (c->ie == c->N ? c->ntail : 0);
     info->nnz_begin = (int64_t)c->ib * c->nnz_int;
     info->nnz_end = (int64_t)c->ie * c->nnz_int + (c->ie == c->N ? c->nnz_tail : 0);
     return MH_OK;
@@ -1905,8 +2057,16 @@ extern "C" int mh_get_bounds(const mh_ctx* c, double* xl, double* xu, double* gl
     // implicit: acceleration bounds at every grid point (CasOCTranscription.cpp:222-226)
     for (int j = 0; j < c->NDV; ++j)
         for (int k = 0; k < c->G; ++k) { xl[col_deriv(c, k, j)] = c->acc_lo; xu[col_deriv(c, k, j)] = c->acc_hi; }
-    if (gl && gu)
+    if (gl && gu) {
         for (int64_t r = 0; r < c->m; ++r) { gl[r] = 0.0; gu[r] = 0.0; }
+        // path rows: the equation's bounds at every mesh point
+        // (CasOCTranscription.cpp:429-432); mesh point N opens the tail
+        for (int i = 0; i <= c->N; ++i)
+            for (int e = 0; e < c->npc; ++e) {
+                gl[(int64_t)i * c->rpi + e] = c->pc[e].g.lower;
+                gu[(int64_t)i * c->rpi + e] = c->pc[e].g.upper;
+            }
+    }
     return MH_OK;
 }
 
@@ -2053,7 +2213,7 @@ static void be_interval(mh_ctx* c, const double* x, int mode, double* g, double*
         (void)hipFuncSetAttribute((const void*)k_interval<D>, hipFuncAttributeMaxDynamicSharedMemorySize,
                 (int)lds);
     Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, c->k0, c->nk, c->NDV};
-    Interval I{c->scheme, c->interp, c->ib, c->rpi, c->nnz_int, c->NDV, c->N, c->nnz_tail};
+    Interval I{c->scheme, c->interp, c->ib, c->rpi, c->nnz_int, c->NDV, c->N, c->nnz_tail, c->ntail, c->P};
     const unsigned threads = v ? 1024u : 256u;
     hipLaunchKernelGGL(k_interval<D>, dim3((unsigned)(c->ie - c->ib)), dim3(threads), lds, c->stream, c->M,
             S, ln, ts.dev, L, I, c->d_tpl, c->d_tplp, tables, c->d_T, c->d_H, g, v);
@@ -2136,7 +2296,7 @@ static int launch_stage(mh_ctx* c, int stage, int kind, const double* x, double*
         return MH_OK;
     }
     Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, c->k0, c->nk, c->NDV};
-    Interval I{c->scheme, c->interp, c->ib, c->rpi, c->nnz_int, c->NDV, c->N, c->nnz_tail};
+    Interval I{c->scheme, c->interp, c->ib, c->rpi, c->nnz_int, c->NDV, c->N, c->nnz_tail, c->ntail, c->P};
     const Lanes& ln = kind == 0 ? c->lanes_g : c->lanes_jac;
     const double* Y = kind == 0 ? c->d_Yg : c->d_Y;
     const int nchunks = kind == 0 ? 0 : (c->nnz_int + (c->ie == c->N ? c->nnz_tail : 0) + ASM_CHUNK - 1) / ASM_CHUNK;
@@ -2239,7 +2399,7 @@ static int finish(mh_ctx* c) {
 // rows / nonzeros of this context's shard (the last shard includes the
 // final grid point's residual rows in implicit mode)
 static size_t shard_rows(const mh_ctx* c) {
-    return (size_t)(c->ie - c->ib) * c->rpi + (c->ie == c->N ? c->NDV : 0);
+    return (size_t)(c->ie - c->ib) * c->rpi + (c->ie == c->N ? c->ntail : 0);
 }
 static size_t shard_nnz(const mh_ctx* c) {
     return (size_t)(c->ie - c->ib) * c->nnz_int + (c->ie == c->N ? c->nnz_tail : 0);

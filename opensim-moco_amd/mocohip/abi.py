@@ -113,6 +113,15 @@ class mh_goal(C.Structure):
                 ("weight", f64)]
 
 
+MH_ABI_VERSION = 2     # include/mocohip.h
+MH_PATH_CONTROL_BOUND = 0
+
+
+class mh_path_equation(C.Structure):
+    _fields_ = [("kind", i32), ("index", i32), ("table", i32), ("column", i32),
+                ("value", f64), ("g", mh_bounds)]
+
+
 class mh_problem(C.Structure):
     _fields_ = [("model", mh_model), ("time_initial", mh_bounds),
                 ("time_final", mh_bounds),
@@ -120,7 +129,8 @@ class mh_problem(C.Structure):
                 ("control_infos", P(mh_variable_info)),
                 ("ngoals", i32), ("nterms", i32), ("goals", P(mh_goal)),
                 ("goal_index", P(i32)), ("goal_column", P(i32)),
-                ("goal_weight", P(f64))]
+                ("goal_weight", P(f64)),
+                ("npath", i32), ("reserved", i32), ("path", P(mh_path_equation))]
 
 
 class mh_options(C.Structure):
@@ -221,7 +231,11 @@ def load_mocohip(path: str | None = None):
             raise RuntimeError(
                 f"libmocohip.so not built at {path}; run "
                 "`python -c 'import __graft_entry__ as g; g.build()'`")
-        _libs[path] = _bind(C.CDLL(path), MOCOHIP_SYMBOLS)
+        lib = _bind(C.CDLL(path), MOCOHIP_SYMBOLS)
+        if lib.mh_abi_version() != MH_ABI_VERSION:
+            raise RuntimeError(f"{path}: ABI version {lib.mh_abi_version()}, "
+                               f"this binding expects {MH_ABI_VERSION}; rebuild")
+        _libs[path] = lib
     return _libs[path]
 
 

@@ -24,8 +24,9 @@ import numpy as np
 from .model import (Body, Coordinate, CoordinateActuator, DataTable,
                     ExternalForce, Joint, Model, model_from_dict)
 from .osim import add_reserves
-from .problem import (MocoControlGoal, MocoFinalTimeGoal, MocoProblem,
-                      MocoStateTrackingGoal)
+from .problem import (Constant, GCVSpline, MocoControlBoundConstraint, MocoControlGoal,
+                      MocoFinalTimeGoal, MocoProblem, MocoStateTrackingGoal,
+                      PiecewiseLinearFunction)
 from .solver import MocoHipSolver, MocoStudy
 
 DATA = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data")
@@ -80,6 +81,47 @@ def double_pendulum(num_mesh_intervals: int = 100, scheme: str = "hermite-simpso
     return MocoStudy(p, s)
 
 
+def pendulum_control_bound(num_mesh_intervals: int = 20, section: str = "lower",
+                           scheme: str = "hermite-simpson",
+                           dynamics: str = "explicit") -> MocoStudy:
+    """The MocoControlBoundConstraint problems of testConstraints.cpp:1460-1540
+    (ModelFactory::createPendulum): "lower" (Constant 0.1318 lower bound),
+    "upper" (Constant 11.236 upper bound, free final time), "equality"
+    (PiecewiseLinearFunction lower bound with equality_with_lower), and
+    "both" (GCVSpline lower and Constant upper bound, two equations)."""
+    m = n_link_pendulum(1)
+    p = MocoProblem(m)
+    c = p.add_path_constraint(MocoControlBoundConstraint())
+    c.add_control_path("/tau0")
+    if section == "upper":
+        p.set_time_bounds(0.0, (0.1, 10.0))
+        p.set_state_info("/jointset/j0/q0/value", (0, 1), 0, 0.53)
+        p.set_state_info("/jointset/j0/q0/speed", (-10, 10), 0, 0)
+        p.set_control_info("/tau0", (-20, 20))
+        p.add_goal(MocoFinalTimeGoal())
+        c.set_upper_bound(Constant(11.236))
+    else:
+        p.set_time_bounds(0.0, 1.0)
+        p.set_state_info("/jointset/j0/q0/value", (-10, 10), 0)
+        p.set_state_info("/jointset/j0/q0/speed", (-10, 10), 0)
+        p.set_control_info("/tau0", (-5, 5))
+        p.add_goal(MocoControlGoal())
+        if section == "lower":
+            c.set_lower_bound(Constant(0.1318))
+        elif section == "equality":
+            c.set_lower_bound(PiecewiseLinearFunction([0, 0.2, 0.7, 1], [0, 0.5316, -0.3137, 0.0319]))
+            c.set_equality_with_lower(True)
+        elif section == "both":
+            c.set_lower_bound(GCVSpline(5, [0, 0.2, 0.45, 0.7, 0.85, 1.0],
+                                        [-0.4, 0.1, -0.2, 0.3, 0.0, -0.1]))
+            c.set_upper_bound(Constant(2.5))
+        else:
+            raise ValueError(section)
+    s = MocoHipSolver(num_mesh_intervals=num_mesh_intervals, transcription_scheme=scheme,
+                      multibody_dynamics_mode=dynamics)
+    return MocoStudy(p, s)
+
+
 def _load(name):
     with open(os.path.join(DATA, name)) as fh:
         return json.load(fh)
@@ -110,10 +152,15 @@ def gait10dof18musc_model(muscles: bool = True, tendon_compliance: bool = False,
 
 def gait10dof18musc(num_mesh_intervals: int = 200, muscles: bool = True,
                     tendon_compliance: bool = False,
-                    fd_scheme: str = "forward", dynamics: str = "explicit") -> MocoStudy:
+                    fd_scheme: str = "forward", dynamics: str = "explicit",
+                    control_bounds: bool = False) -> MocoStudy:
     """MocoTrack gait10dof18musc (config 3).  MocoTrack: states tracking goal
     (weight 1, GCVSpline reference), control effort goal (0.001), time
-    [0.01, 1.3], explicit dynamics, forward FD (MocoTrack.cpp:54-132)."""
+    [0.01, 1.3], explicit dynamics, forward FD (MocoTrack.cpp:54-132).
+    control_bounds: adds a MocoControlBoundConstraint on the soleus and
+    tibialis anterior excitations (GCVSpline lower, Constant upper bound) and
+    one on the hip flexor reserve (Constant upper bound) as path constraints
+    (not part of the reference MocoTrack setup)."""
     m = gait10dof18musc_model(muscles=muscles, tendon_compliance=tendon_compliance)
     ref = _load("walk_gait1018_state_reference.json")
     cols = {k: np.asarray(v) for k, v in ref["columns"].items()}
@@ -123,6 +170,18 @@ def gait10dof18musc(num_mesh_intervals: int = 200, muscles: bool = True,
         "state_reference", np.asarray(ref["time"]), cols, degree=5)))
     p.add_goal(MocoControlGoal("control_effort", 0.001))
     p.set_time_bounds(0.01, 1.3)
+    if control_bounds:
+        names = m.control_names()
+        picks = [n for n in names if n.endswith(("soleus_r", "tib_ant_r"))] if muscles else []
+        c = p.add_path_constraint(MocoControlBoundConstraint("excitation_band"))
+        for n in picks:
+            c.add_control_path(n)
+        c.set_lower_bound(GCVSpline(5, np.linspace(0.0, 1.4, 8),
+                                    0.02 + 0.01 * np.sin(np.linspace(0.0, 3.0, 8))))
+        c.set_upper_bound(Constant(0.9))
+        r = p.add_path_constraint(MocoControlBoundConstraint("reserve_cap"))
+        r.add_control_path(names[-1])
+        r.set_upper_bound(Constant(0.5))
     s = MocoHipSolver(num_mesh_intervals=num_mesh_intervals,
                       optim_finite_difference_scheme=fd_scheme, multibody_dynamics_mode=dynamics)
     return MocoStudy(p, s)

@@ -210,6 +210,9 @@ class DataTable:
     times: np.ndarray
     columns: Dict[str, np.ndarray]
     degree: int = 3
+    # explicit piecewise polynomial (breaks[nseg+1], coefs[nseg, ncol,
+    # degree+1]) instead of splining the samples (path-constraint bounds)
+    ppoly: Optional[tuple] = None
 
 
 @dataclass
@@ -304,8 +307,11 @@ class Model:
         return [a.path for a in self.actuators]
 
     # lowering ---------------------------------------------------------------
-    def compile(self) -> "CompiledModel":
-        return CompiledModel(self)
+    def compile(self, extra_tables: Sequence[DataTable] = ()) -> "CompiledModel":
+        """Lower to mh_model.  ``extra_tables`` (problem-level functions of
+        time, e.g. path-constraint bounds) are appended after the model's
+        own tables, which keep their indices."""
+        return CompiledModel(self, extra_tables)
 
 
 def _arr(struct_type, items):
@@ -319,7 +325,7 @@ def _arr(struct_type, items):
 class CompiledModel:
     """Owns the C arrays that back an mh_model."""
 
-    def __init__(self, model: Model):
+    def __init__(self, model: Model, extra_tables: Sequence[DataTable] = ()):
         self.model = model
         qidx = model.coordinate_index()
         self.qidx = qidx
@@ -422,12 +428,16 @@ class CompiledModel:
         tables, breaks, coefs = [], [], []
         self.table_index: Dict[str, int] = {}
         self.table_columns: Dict[str, List[str]] = {}
-        for name, t in model.tables.items():
+        all_tables = list(model.tables.items()) + [(t.name, t) for t in extra_tables]
+        for name, t in all_tables:
             cols = list(t.columns.keys())
-            br, cf = gcv_interpolating_ppoly(
-                np.asarray(t.times, float),
-                np.stack([np.asarray(t.columns[c], float) for c in cols], 1),
-                t.degree)
+            if t.ppoly is not None:
+                br, cf = t.ppoly
+            else:
+                br, cf = gcv_interpolating_ppoly(
+                    np.asarray(t.times, float),
+                    np.stack([np.asarray(t.columns[c], float) for c in cols], 1),
+                    t.degree)
             ts = abi.mh_table()
             ts.nseg = len(br) - 1
             ts.degree = cf.shape[-1] - 1

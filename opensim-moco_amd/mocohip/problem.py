@@ -17,6 +17,7 @@ import numpy as np
 from . import abi
 from .model import CompiledModel, CoordinateActuator, DataTable, \
     DeGrooteFregly2016Muscle, Model
+from .splines import gcv_interpolating_ppoly
 
 NAN = float("nan")
 
@@ -81,6 +82,70 @@ class MocoSumSquaredStateGoal:
     state_weights: Dict[str, float] = field(default_factory=dict)
 
 
+# ------------------------------------------------- functions of time ----
+@dataclass
+class Constant:
+    """OpenSim::Constant."""
+    value: float
+
+    def ppoly(self):
+        return None
+
+
+@dataclass
+class PiecewiseLinearFunction:
+    """OpenSim::PiecewiseLinearFunction: linear between points, extended
+    linearly with the end segments' slopes."""
+    x: Sequence[float]
+    y: Sequence[float]
+
+    def ppoly(self):
+        x, y = np.asarray(self.x, float), np.asarray(self.y, float)
+        if len(x) < 2 or np.any(np.diff(x) <= 0):
+            raise ValueError("PiecewiseLinearFunction needs >= 2 increasing points")
+        coefs = np.zeros((len(x) - 1, 1, 2))
+        coefs[:, 0, 0] = y[:-1]
+        coefs[:, 0, 1] = np.diff(y) / np.diff(x)
+        return x, coefs
+
+
+@dataclass
+class GCVSpline:
+    """OpenSim::GCVSpline through (x, y) (interpolating; splines.py)."""
+    degree: int
+    x: Sequence[float]
+    y: Sequence[float]
+
+    def ppoly(self):
+        return gcv_interpolating_ppoly(np.asarray(self.x, float), np.asarray(self.y, float),
+                                       int(self.degree))
+
+
+# ----------------------------------------------------- path constraints ----
+@dataclass
+class MocoControlBoundConstraint:
+    """MocoControlBoundConstraint (Moco/Moco/MocoControlBoundConstraint.cpp):
+    lower_bound(t) <= control <= upper_bound(t) for each control path, as
+    path-constraint equations control - bound(t) at every mesh point."""
+    name: str = "control_bound"
+    control_paths: List[str] = field(default_factory=list)
+    lower_bound: Optional[object] = None
+    upper_bound: Optional[object] = None
+    equality_with_lower: bool = False
+
+    def add_control_path(self, path: str):
+        self.control_paths.append(path)
+
+    def set_lower_bound(self, f):
+        self.lower_bound = f
+
+    def set_upper_bound(self, f):
+        self.upper_bound = f
+
+    def set_equality_with_lower(self, v: bool):
+        self.equality_with_lower = bool(v)
+
+
 class MocoProblem:
     """Single-phase MocoProblem (MocoProblem.h)."""
 
@@ -91,6 +156,7 @@ class MocoProblem:
         self.state_infos: Dict[str, MocoVariableInfo] = {}
         self.control_infos: Dict[str, MocoVariableInfo] = {}
         self.goals: List[object] = []
+        self.path_constraints: List[object] = []
         self.default_speed_bounds = MocoBounds(-50.0, 50.0)
         self.bound_activation_from_excitation = True
 
@@ -113,6 +179,10 @@ class MocoProblem:
         self.goals.append(goal)
         return goal
 
+    def add_path_constraint(self, constraint):
+        self.path_constraints.append(constraint)
+        return constraint
+
     def create_rep(self) -> "ProblemRep":
         return ProblemRep(self)
 
@@ -131,7 +201,8 @@ class ProblemRep:
     def __init__(self, problem: MocoProblem):
         self.problem = problem
         model = problem.model
-        self.compiled: CompiledModel = model.compile()
+        path_eqs, bound_tables = self._path_equations(problem)
+        self.compiled: CompiledModel = model.compile(extra_tables=bound_tables)
         self.state_names = self.compiled.state_names
         self.control_names = self.compiled.control_names
         sinfo: Dict[str, MocoVariableInfo] = {}
@@ -237,7 +308,81 @@ class ProblemRep:
         p.goal_index = abi.iptr(self._gidx)
         p.goal_column = abi.iptr(self._gcol)
         p.goal_weight = abi.dptr(self._gw)
+        for e in path_eqs:
+            if e.table >= 0:   # bound table index: after the model's own
+                e.table = self.compiled.table_index[bound_tables[e.table].name]
+        self._path = (abi.mh_path_equation * max(1, len(path_eqs)))(*path_eqs)
+        p.npath = len(path_eqs)
+        p.path = self._path
+        self.num_path_equations = len(path_eqs)
         self.struct = p
         self.num_states = len(self.state_names)
         self.num_controls = len(self.control_names)
         self.nq = self.compiled.nq
+
+    @staticmethod
+    def _path_equations(problem: MocoProblem):
+        """Expand path constraints to mh_path_equation rows, with the
+        initializeOnModel checks of MocoControlBoundConstraint.cpp:38-118.
+        Bound functions other than Constant become piecewise polynomial
+        tables appended to the model's (indices into the returned list)."""
+        names = problem.model.control_names()
+        cidx = {n: i for i, n in enumerate(names)}
+        eqs: List[abi.mh_path_equation] = []
+        tables: List[DataTable] = []
+        for ci, pc in enumerate(problem.path_constraints):
+            if not isinstance(pc, MocoControlBoundConstraint):
+                raise TypeError(f"unsupported path constraint {type(pc).__name__}")
+            has_lo, has_up = pc.lower_bound is not None, pc.upper_bound is not None
+            if pc.control_paths and not (has_lo or has_up):
+                continue   # the reference warns and adds no equations
+            for path in pc.control_paths:
+                if path not in cidx:
+                    raise ValueError(f"Control path '{path}' was provided but no such "
+                                     "control exists in the model.")
+            if pc.equality_with_lower and has_up:
+                raise ValueError("If equality_with_lower==true, upper bound function "
+                                 "must not be set.")
+            if pc.equality_with_lower and not has_lo:
+                raise ValueError("If equality_with_lower==true, lower bound function "
+                                 "must be set.")
+            for f in (pc.lower_bound, pc.upper_bound):
+                if isinstance(f, GCVSpline):
+                    lo, hi = min(f.x), max(f.x)
+                    if lo > problem.time_initial.lower:
+                        raise ValueError(f"The function's minimum domain value ({lo}) must be "
+                                         "less than or equal to the minimum possible initial "
+                                         f"time ({problem.time_initial.lower}).")
+                    if hi < problem.time_final.upper:
+                        raise ValueError(f"The function's maximum domain value ({hi}) must be "
+                                         "greater than or equal to the maximum possible final "
+                                         f"time ({problem.time_final.upper}).")
+
+            def bound_ref(f, which):
+                pp = f.ppoly()
+                if pp is None:
+                    return -1, 0, float(f.value)
+                name = f"__path{ci}_{which}"
+                if not any(t.name == name for t in tables):
+                    br, cf = pp
+                    tables.append(DataTable(name=name, times=np.asarray(br, float),
+                                            columns={"bound": np.zeros(len(br))},
+                                            ppoly=(np.asarray(br, float), np.asarray(cf, float))))
+                return [t.name for t in tables].index(name), 0, 0.0
+
+            for path in pc.control_paths:
+                for which, f in (("lower", pc.lower_bound), ("upper", pc.upper_bound)):
+                    if f is None:
+                        continue
+                    e = abi.mh_path_equation()
+                    e.kind = abi.MH_PATH_CONTROL_BOUND
+                    e.index = cidx[path]
+                    e.table, e.column, e.value = bound_ref(f, which)
+                    if pc.equality_with_lower:
+                        e.g.lower, e.g.upper = 0.0, 0.0
+                    elif which == "lower":
+                        e.g.lower, e.g.upper = 0.0, math.inf
+                    else:
+                        e.g.lower, e.g.upper = -math.inf, 0.0
+                    eqs.append(e)
+        return eqs, tables

@@ -143,6 +143,17 @@ class _NLPBase:
         """Derivative variables per grid point (implicit mode: NQ)."""
         return self.NQ if self.opts.multibody_dynamics_mode == abi.MH_DYNAMICS_IMPLICIT else 0
 
+    @property
+    def NPC(self) -> int:
+        """Path-constraint equations per mesh point."""
+        return self.rep.num_path_equations
+
+    @property
+    def tail_rows(self) -> int:
+        """Rows after the last interval's own: the final mesh point's path
+        rows and the final grid point's residuals."""
+        return self.NPC + self.NDV
+
     def eval_dae(self, inputs: np.ndarray) -> np.ndarray:
         """Per-point DAE: rows [t, states, controls(, accelerations)] ->
         [udot or multibody residual, zdot]."""

@@ -7,7 +7,8 @@ Layout (little endian, x86-64 struct layout of include/mocohip.h):
   magic "MHTAPE01", int32 version, int32 NS, int32 NC, mh_options,
   the 12 mh_model counts, gravity[3], time bounds (2 x mh_bounds),
   ngoals, nterms, then the arrays in mh_model / mh_problem field order,
-  each as (int64 byte count, bytes)."""
+  each as (int64 byte count, bytes); version 2 appends npath and the
+  mh_path_equation array."""
 from __future__ import annotations
 
 import ctypes as C
@@ -16,7 +17,7 @@ import struct
 from . import abi
 
 MAGIC = b"MHTAPE01"
-VERSION = 1
+VERSION = 2   # 2: + path-constraint equations (mh_problem.npath/path)
 
 # (field, element type, count attribute of mh_model / None for problem arrays)
 _MODEL_ARRAYS = [
@@ -57,5 +58,7 @@ def write_tape(rep, opts: abi.mh_options, path: str) -> None:
     for b in blobs:
         out.append(struct.pack("<q", len(b)))
         out.append(b)
+    pb = _blob(p.path, abi.mh_path_equation, p.npath)
+    out += [struct.pack("<i", p.npath), struct.pack("<q", len(pb)), pb]
     with open(path, "wb") as fh:
         fh.write(b"".join(out))

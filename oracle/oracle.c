@@ -234,6 +234,8 @@ struct orc_ctx {
     double *brk, *coef; mh_external_force* ext;
     mh_variable_info *sinfo, *cinfo; mh_goal* goals; int32_t *gidx, *gcol;
     double* gw;
+    int NPC;                /* path-constraint equations per mesh point  */
+    mh_path_equation* pc;
     /* derived sizes */
     int NQ, NZ, NS, NC, NP; /* NP = per-point inputs excluding time */
     int implicit;           /* MH_DYNAMICS_IMPLICIT                     */
@@ -278,6 +280,8 @@ static int64_t col_deriv(const orc_ctx* c, int k, int j) {
 }
 /* multibody residual rows per grid point (implicit mode) */
 static int nres(const orc_ctx* c) { return c->implicit ? c->NQ : 0; }
+/* the mesh point that opens interval i (and closes interval i-1) */
+static int mesh_point(const orc_ctx* c, int i) { return c->scheme == MH_HERMITE_SIMPSON ? 2 * i : i; }
 
 /* Sorted columns of all point inputs at grid point k (excluding t0/tf). */
 static int point_cols(const orc_ctx* c, int k, int64_t* out) {
@@ -308,6 +312,20 @@ static int64_t residual_rows(const orc_ctx* c, int k, int64_t row, row_fn emit, 
     }
     return row;
 }
+/* Path-constraint rows of mesh grid point k: like the residuals, one
+ * block-dense row per equation over time and the point's inputs (the path
+ * function's Jacobian with sparsity detection "none", CasOCFunction.cpp:
+ * 25-105), evaluated at mesh points only (CasOCTranscription.cpp:419-433). */
+static int64_t path_rows(const orc_ctx* c, int k, int64_t row, row_fn emit, void* ud,
+        int64_t* cols) {
+    for (int e = 0; e < c->NPC; ++e) {
+        int n = 0;
+        cols[n++] = 0; cols[n++] = 1;
+        n += point_cols(c, k, cols + n);
+        emit(ud, row++, cols, n);
+    }
+    return row;
+}
 /* Implicit mode: the speed rows (NQ <= s < 2NQ) have udot = the derivative
  * variable, a direct MX expression (CasOCTranscription.cpp:339-341), so they
  * depend on the point's own state s and derivative s - NQ only. */
@@ -319,8 +337,10 @@ static void interval_rows(const orc_ctx* c, int i, int64_t row0, row_fn emit, vo
     int64_t row = row0;
     if (c->scheme == MH_HERMITE_SIMPSON) {
         int ki = 2 * i, km = 2 * i + 1, kp = 2 * i + 2;
-        /* flattenConstraints: residuals of the interval's grid points before
-         * its defects (CasOCTranscription.h:290-300) */
+        /* flattenConstraints: the mesh point's path rows, then the residuals
+         * of the interval's grid points, then its defects
+         * (CasOCTranscription.h:286-300) */
+        row = path_rows(c, ki, row, emit, ud, cols);
         row = residual_rows(c, ki, row, emit, ud, cols);
         row = residual_rows(c, km, row, emit, ud, cols);
         /* Hermite rows, then Simpson rows (CasOCHermiteSimpson.cpp:79-84). */
@@ -374,6 +394,7 @@ static void interval_rows(const orc_ctx* c, int i, int64_t row0, row_fn emit, vo
         }
     } else { /* trapezoidal (CasOCTrapezoidal.cpp:43-59) */
         int ki = i, kp = i + 1;
+        row = path_rows(c, ki, row, emit, ud, cols);
         row = residual_rows(c, ki, row, emit, ud, cols);
         for (int s = 0; s < NS; ++s) {
             int n = 0;
@@ -409,14 +430,17 @@ static void emit_fill(void* ud, int64_t row, const int64_t* cols, int n) {
     }
 }
 static int rows_per_interval(const orc_ctx* c) {
-    return 2 * c->NS * (c->scheme == MH_HERMITE_SIMPSON) + c->NS * (c->scheme == MH_TRAPEZOIDAL) +
+    return c->NPC + 2 * c->NS * (c->scheme == MH_HERMITE_SIMPSON) + c->NS * (c->scheme == MH_TRAPEZOIDAL) +
            (c->scheme == MH_HERMITE_SIMPSON && c->interp ? c->NC : 0) +
            nres(c) * (c->scheme == MH_HERMITE_SIMPSON ? 2 : 1);
 }
-/* residual rows of the final grid point, after all intervals
- * (CasOCTranscription.h:306-308) */
+/* after all intervals: the final mesh point's path rows (the last pass of
+ * the mesh loop), then the final grid point's residual rows
+ * (CasOCTranscription.h:286-308) */
+static int ntail(const orc_ctx* c) { return c->NPC + nres(c); }
 static void tail_rows(const orc_ctx* c, int64_t row0, row_fn emit, void* ud) {
     int64_t* cols = (int64_t*)malloc(sizeof(int64_t) * (size_t)(c->NS + c->NC + c->NDV + 4));
+    row0 = path_rows(c, c->G - 1, row0, emit, ud, cols);
     residual_rows(c, c->G - 1, row0, emit, ud, cols);
     free(cols);
 }
@@ -446,6 +470,12 @@ int orc_create(const mh_problem* p, const mh_options* o, orc_ctx** out) {
     c->gidx = DUP(int32_t, p->goal_index, p->nterms);
     c->gcol = DUP(int32_t, p->goal_column, p->nterms);
     c->gw = dup_d(p->goal_weight, (size_t)p->nterms);
+    c->NPC = p->npath;
+    c->pc = DUP(mh_path_equation, p->path, p->npath);
+    if (p->npath < 0 || (p->npath > 0 && !p->path)) {
+        orc_destroy(c);
+        return fail(MH_ERR_INVALID, "bad path constraints");
+    }
 
     /* spline coefficients */
     c->kb = (double*)calloc((size_t)M->nknots + 1, sizeof(double));
@@ -501,6 +531,15 @@ int orc_create(const mh_problem* p, const mh_options* o, orc_ctx** out) {
         c->acc_hi = o->implicit_accel_bounds[1];
     }
     c->NP = c->NS + c->NC + c->NDV;
+    for (int e = 0; e < c->NPC; ++e) {
+        const mh_path_equation* E = &c->pc[e];
+        if (E->kind != MH_PATH_CONTROL_BOUND || E->index < 0 || E->index >= c->NC ||
+                E->table < -1 || E->table >= M->ntables ||
+                (E->table >= 0 && (E->column < 0 || E->column >= c->tabs[E->table].ncol))) {
+            orc_destroy(c);
+            return fail(MH_ERR_INVALID, "path equation %d: bad control/table", e);
+        }
+    }
     for (int ia = 0; ia < M->nactuators; ++ia) {
         if (c->acts[ia].kind == MH_ACT_MUSCLE) {
             int t = c->acts[ia].target;
@@ -566,7 +605,7 @@ int orc_create(const mh_problem* p, const mh_options* o, orc_ctx** out) {
     }
     free(mesh);
     c->n = 2 + (int64_t)(c->NS + c->NC + c->NDV) * c->G;
-    c->m = (int64_t)rows_per_interval(c) * c->N + nres(c);
+    c->m = (int64_t)rows_per_interval(c) * c->N + ntail(c);
     /* structure */
     emit_state e = {0, NULL, NULL};
     for (int i = 0; i < c->N; ++i) interval_rows(c, i, 0, emit_count, &e);
@@ -588,7 +627,7 @@ void orc_destroy(orc_ctx* c) {
     if (!c) return;
     void* ptrs[] = {c->bodies, c->axes, c->funcs, c->kx, c->ky, c->kb, c->kc, c->kd,
             c->mus, c->pts, c->acts, c->tabs, c->brk, c->coef, c->ext, c->sinfo, c->cinfo,
-            c->goals, c->gidx, c->gcol, c->gw, c->mus_act_state, c->mus_ftn_state,
+            c->goals, c->gidx, c->gcol, c->gw, c->pc, c->mus_act_state, c->mus_ftn_state,
             c->mus_control, c->coord_body, c->grid, c->quad, c->iRow, c->jCol};
     for (size_t i = 0; i < sizeof ptrs / sizeof ptrs[0]; ++i) free(ptrs[i]);
     free(c);
@@ -648,6 +687,15 @@ int orc_get_bounds(const orc_ctx* c, double* xl, double* xu, double* gl, double*
     /* defects, residuals and interpolating-control rows: equality to 0
      * (CasOCTranscription.cpp:275-278, 440-443) */
     if (gl) for (int64_t r = 0; r < c->m; ++r) { gl[r] = 0.0; gu[r] = 0.0; }
+    /* path rows: the equation's bounds repeated at every mesh point
+     * (CasOCTranscription.cpp:429-432) */
+    if (gl && c->NPC) {
+        int rpi = rows_per_interval(c);
+        for (int i = 0; i <= c->N; ++i) {
+            int64_t r0 = (int64_t)i * rpi;
+            for (int e = 0; e < c->NPC; ++e) { gl[r0 + e] = c->pc[e].g.lower; gu[r0 + e] = c->pc[e].g.upper; }
+        }
+    }
     return MH_OK;
 }
 
@@ -1342,6 +1390,14 @@ static void all_xdot(orc_ctx* c, const double* x, const double* times, double* x
     }
 }
 
+/* MocoControlBoundConstraint::calcPathConstraintErrorsImpl
+ * (MocoControlBoundConstraint.cpp:130-146): error = control - bound(t). */
+static double path_value(const orc_ctx* c, int e, double t, const double* ct) {
+    const mh_path_equation* E = &c->pc[e];
+    double b = E->table < 0 ? E->value : table_eval(c, E->table, E->column, t);
+    return ct[E->index] - b;
+}
+
 int orc_eval_g(orc_ctx* c, const double* x, double* g) {
     int NS = c->NS, NC = c->NC, NR = nres(c);
     double* times = (double*)malloc(sizeof(double) * (size_t)c->G);
@@ -1350,8 +1406,17 @@ int orc_eval_g(orc_ctx* c, const double* x, double* g) {
     times_of(c, x, times);
     all_xdot(c, x, times, xd, res);
     int rpi = rows_per_interval(c);
+    double* pin = (double*)malloc(sizeof(double) * (size_t)(c->NP + 1));
+    /* path rows of every mesh point: interval i opens with mesh point i's,
+     * the tail with the final mesh point's */
+    for (int i = 0; i <= c->N && c->NPC; ++i) {
+        int k = mesh_point(c, i);
+        gather_point(c, x, k, pin, pin + NS);
+        for (int e = 0; e < c->NPC; ++e) g[(int64_t)i * rpi + e] = path_value(c, e, times[k], pin + NS);
+    }
+    free(pin);
     for (int i = 0; i < c->N; ++i) {
-        double* gi = g + (int64_t)i * rpi;
+        double* gi = g + (int64_t)i * rpi + c->NPC;
         /* residual rows of the interval's grid points first */
         int npts = c->scheme == MH_HERMITE_SIMPSON ? 2 : 1;
         int k0 = c->scheme == MH_HERMITE_SIMPSON ? 2 * i : i;
@@ -1385,7 +1450,7 @@ int orc_eval_g(orc_ctx* c, const double* x, double* g) {
             for (int s = 0; s < NS; ++s) gi[s] = xp[s] - (xi[s] + 0.5 * h * (fp[s] + fi[s]));
         }
     }
-    for (int o = 0; o < NR; ++o) g[(int64_t)c->N * rpi + o] = res[(int64_t)(c->G - 1) * NR + o];
+    for (int o = 0; o < NR; ++o) g[(int64_t)c->N * rpi + c->NPC + o] = res[(int64_t)(c->G - 1) * NR + o];
     free(times);
     free(xd);
     free(res);
@@ -1452,6 +1517,55 @@ static void fd_blocks(orc_ctx* c, const double* x, const double* times, double* 
     }
 }
 
+/* FD blocks of the path-constraint equations at every mesh point:
+ * Dp[(i * ND + d) * NPC + e], directions and seeds as in fd_blocks (the
+ * path function has its own FiniteDiff, CasOCTranscription.cpp:424-428). */
+static void path_blocks(const orc_ctx* c, const double* x, const double* times, double* Dp) {
+    int NS = c->NS, NP = c->NP, NPC = c->NPC, ND = NP + 2;
+    double h = c->h;
+    double* in = (double*)malloc(sizeof(double) * (size_t)(NP + 1));
+    for (int i = 0; i <= c->N; ++i) {
+        int k = mesh_point(c, i);
+        gather_point(c, x, k, in, in + NS);
+        double t = times[k];
+        for (int d = 0; d < ND; ++d) {
+            double seed;
+            int idx = -1;
+            if (d == 0) seed = 1.0 - c->grid[k];
+            else if (d == 1) seed = c->grid[k];
+            else { seed = 1.0; idx = d - 2; }
+            for (int e = 0; e < NPC; ++e) {
+                double vp = 0.0, vm = 0.0, v0 = 0.0;
+                if (c->fd != MH_FD_CENTRAL) v0 = path_value(c, e, t, in + NS);
+                if (c->fd != MH_FD_BACKWARD) {
+                    if (idx < 0) vp = path_value(c, e, t + h * seed, in + NS);
+                    else {
+                        double sv = in[idx];
+                        in[idx] = sv + h * seed;
+                        vp = path_value(c, e, t, in + NS);
+                        in[idx] = sv;
+                    }
+                }
+                if (c->fd != MH_FD_FORWARD) {
+                    if (idx < 0) vm = path_value(c, e, t - h * seed, in + NS);
+                    else {
+                        double sv = in[idx];
+                        in[idx] = sv - h * seed;
+                        vm = path_value(c, e, t, in + NS);
+                        in[idx] = sv;
+                    }
+                }
+                double q;
+                if (c->fd == MH_FD_CENTRAL) q = (vp - vm) / (2.0 * h);
+                else if (c->fd == MH_FD_FORWARD) q = (vp - v0) / h;
+                else q = (v0 - vm) / h;
+                Dp[((int64_t)i * ND + d) * NPC + e] = q;
+            }
+        }
+    }
+    free(in);
+}
+
 /* Derivative of xdot[s] at grid point k along direction d (0=t0, 1=tf,
  * 2+j = input j).  For s < NQ, qdot = u exactly. */
 static double xdot_deriv(const orc_ctx* c, const double* D, int k, int s, int d) {
@@ -1492,6 +1606,9 @@ int orc_eval_jac_g(orc_ctx* c, const double* x, double* values) {
     times_of(c, x, times);
     all_xdot(c, x, times, xd, res);
     fd_blocks(c, x, times, D);
+    int NPC = c->NPC;
+    double* Dp = (double*)malloc(sizeof(double) * ((size_t)(c->N + 1) * (size_t)ND * (size_t)NPC + 1));
+    if (NPC) path_blocks(c, x, times, Dp);
     int rpi = rows_per_interval(c);
     int npts_res = c->scheme == MH_HERMITE_SIMPSON ? 2 : 1;
     for (int64_t e = 0; e < c->nnz; ++e) {
@@ -1501,10 +1618,17 @@ int orc_eval_jac_g(orc_ctx* c, const double* x, double* values) {
         double v = 0.0;
         int kc;
         int dir = col_to_dir(c, col, &kc);
-        if (row >= (int64_t)c->N * rpi) {   /* residual of the final grid point */
-            values[e] = D[((int64_t)(c->G - 1) * ND + dir) * NO + (int)(row - (int64_t)c->N * rpi)];
+        if (row >= (int64_t)c->N * rpi) {   /* final mesh point: path rows, then residuals */
+            int rt = (int)(row - (int64_t)c->N * rpi);
+            if (rt < NPC) values[e] = Dp[((int64_t)c->N * ND + dir) * NPC + rt];
+            else values[e] = D[((int64_t)(c->G - 1) * ND + dir) * NO + (rt - NPC)];
             continue;
         }
+        if (rl < NPC) {                     /* path rows of the interval's mesh point */
+            values[e] = Dp[((int64_t)i * ND + dir) * NPC + rl];
+            continue;
+        }
+        rl -= NPC;
         if (rl < npts_res * NR) {           /* residual rows of the interval's points */
             int kr = (c->scheme == MH_HERMITE_SIMPSON ? 2 * i : i) + rl / NR;
             values[e] = D[((int64_t)kr * ND + dir) * NO + rl % NR];
@@ -1586,6 +1710,7 @@ int orc_eval_jac_g(orc_ctx* c, const double* x, double* values) {
         values[e] = v;
     }
     (void)NQ;
+    free(Dp);
     free(times);
     free(xd);
     free(D);

@@ -47,14 +47,18 @@ def _worker(rank, world, port, case, N, out):
     try:
         st = {"pendulum": lambda: configs.double_pendulum(N),
               "gait": lambda: configs.gait10dof18musc(N),
-              "pendulum_implicit": lambda: configs.double_pendulum(N, dynamics="implicit")}[case]()
+              "pendulum_implicit": lambda: configs.double_pendulum(N, dynamics="implicit"),
+              "gait_pathcon": lambda: configs.gait10dof18musc(N, control_bounds=True),
+              "bound_implicit": lambda: configs.pendulum_control_bound(N, "both",
+                                                                       dynamics="implicit")}[case]()
         rep = st.problem.create_rep()
         ref = OracleNLP(rep, st.solver.options(), threads=1)
         x = ref.random_iterate(np.random.default_rng(3).uniform(-1, 1, ref.n))
         g, J = ref.eval_g(x), ref.eval_jac_g(x)
-        # implicit dynamics: the final point's residual rows follow the last
-        # interval (tail), owned by the last rank
-        tail_rows = ref.NDV
+        # the final mesh point's path rows and (implicit dynamics) the final
+        # point's residual rows follow the last interval (tail), owned by the
+        # last rank
+        tail_rows = ref.tail_rows
         ir, _ = ref.jac_structure()
         tail_nnz = int((ir >= ref.m - tail_rows).sum())
         rpi, nzi = (ref.m - tail_rows) // N, (ref.nnz - tail_nnz) // N
@@ -76,7 +80,8 @@ def _worker(rank, world, port, case, N, out):
 
 
 @pytest.mark.parametrize("case,N,world", [("pendulum", 7, 2), ("pendulum", 10, 3), ("gait", 5, 2),
-                                          ("pendulum_implicit", 7, 3)])
+                                          ("pendulum_implicit", 7, 3), ("gait_pathcon", 4, 2),
+                                          ("bound_implicit", 9, 3)])
 def test_shard_gather_reassembles_full_vectors(case, N, world):
     ctx = mp.get_context("spawn")
     out = ctx.Array("i", [0] * world)

@@ -42,6 +42,17 @@ CASES = {
     "gait_rigid_implicit": lambda: configs.gait10dof18musc(8, dynamics="implicit"),
     "gait_compliant_implicit_central": lambda: configs.gait10dof18musc(
         6, tendon_compliance=True, fd_scheme="central", dynamics="implicit"),
+    # path constraints: the MocoControlBoundConstraint
+    # problems of testConstraints.cpp:1460-1540 and a gait variant
+    "pendulum_bound_lower": lambda: configs.pendulum_control_bound(20, "lower"),
+    "pendulum_bound_upper": lambda: configs.pendulum_control_bound(10, "upper"),
+    "pendulum_bound_equality_trap": lambda: configs.pendulum_control_bound(16, "equality",
+                                                                           "trapezoidal"),
+    "pendulum_bound_both_implicit": lambda: configs.pendulum_control_bound(12, "both",
+                                                                           dynamics="implicit"),
+    "gait_rigid_pathcon": lambda: configs.gait10dof18musc(8, control_bounds=True),
+    "gait_rigid_pathcon_implicit_central": lambda: configs.gait10dof18musc(
+        6, fd_scheme="central", dynamics="implicit", control_bounds=True),
 }
 
 
@@ -79,10 +90,11 @@ def _scale(v):
 
 
 def _rows(nlp):
-    """(rows per interval, tail rows): implicit mode appends the final grid
-    point's residual rows after the last interval."""
+    """(rows per interval, tail rows): the final mesh point's path rows and
+    (implicit mode) the final grid point's residual rows follow the last
+    interval."""
     N = nlp.opts.num_mesh_intervals
-    tail = nlp.NDV
+    tail = nlp.tail_rows
     return (nlp.m - tail) // N, tail
 
 
@@ -101,8 +113,8 @@ def _row_interval(nlp, rows):
 def _row_mask(ref, x):
     """Per g row: True when every DAE output the row depends on is regular at
     the interval's grid points (residual rows on their output; defect rows of
-    states s >= NQ (s >= 2NQ in implicit mode) on xdot_s; the others on x
-    only)."""
+    states s >= NQ (s >= 2NQ in implicit mode) on xdot_s; path rows and the
+    others on x only)."""
     P = _points(ref, x)
     Y0 = ref.eval_dae(P)
     R = _regular(Y0)
@@ -111,19 +123,19 @@ def _row_mask(ref, x):
     hs = ref.opts.transcription == 0
     step = 2 if hs else 1
     rpi, tail = _rows(ref)
-    nres = ref.NDV
+    nres, npc = ref.NDV, ref.NPC
     npres = step if nres else 0
     mask = np.ones((N, rpi), bool)
     ndef = 2 * NS if hs else NS
     for i in range(N):
         ok = R[i * step:i * step + step + 1].all(0)
         for row in range(npres * nres):
-            mask[i, row] = R[i * step + row // nres, row % nres]
+            mask[i, npc + row] = R[i * step + row // nres, row % nres]
         for row in range(ndef):
             s = row % NS
             if s >= (2 * NQ if nres else NQ):
-                mask[i, npres * nres + row] = ok[s - NQ]
-    return np.concatenate([mask.reshape(-1), R[-1, :tail]])
+                mask[i, npc + npres * nres + row] = ok[s - NQ]
+    return np.concatenate([mask.reshape(-1), np.ones(npc, bool), R[-1, :nres]])
 
 
 BACKENDS = ["auto", "lane", "generic"]
@@ -284,7 +296,8 @@ def test_objective_and_gradient(name):
 
 
 @pytest.mark.parametrize("name", ["double_pendulum_hs", "gait_rigid_forward", "double_pendulum_implicit_hs",
-                                  "gait_rigid_implicit"])
+                                  "gait_rigid_implicit", "gait_rigid_pathcon",
+                                  "pendulum_bound_both_implicit"])
 def test_shards_reassemble_bit_exact(name):
     """Mesh-interval shards (the multi-GPU partition) concatenate to exactly
     the unsharded g and Jacobian values."""
@@ -331,7 +344,7 @@ def test_repeatable_bitwise():
 def test_generated_backends_are_selected_for_bundled_models():
     for name in ["sliding_mass", "double_pendulum_hs", "gait_rigid_forward",
                  "gait_compliant_central", "gait_torque_driven", "sliding_mass_implicit",
-                 "double_pendulum_implicit_hs", "gait_rigid_implicit"]:
+                 "double_pendulum_implicit_hs", "gait_rigid_implicit", "gait_rigid_pathcon"]:
         gpu, _, _ = _pair(name)
         be, flops, _ = gpu.backend()
         assert be.startswith("generated:"), (name, be)
@@ -367,7 +380,8 @@ def test_pruned_tasks_bit_identical(name):
                                   "gait_rigid_forward", "gait_rigid_central", "gait_rigid_backward",
                                   "gait_compliant_central", "gait_torque_driven",
                                   "double_pendulum_implicit_hs", "double_pendulum_implicit_trap",
-                                  "gait_rigid_implicit"])
+                                  "gait_rigid_implicit", "gait_rigid_pathcon",
+                                  "pendulum_bound_equality_trap", "pendulum_bound_both_implicit"])
 @pytest.mark.parametrize("variant", [{"MOCOHIP_INTERVAL": "0"},
                                      {"MOCOHIP_INTERVAL": "0", "MOCOHIP_ASM": "gs"},
                                      {"MOCOHIP_INTERVAL": "0", "MOCOHIP_QUOT": "1"},

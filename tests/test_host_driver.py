@@ -31,7 +31,7 @@ def test_driver_loads_tape_and_fails_loudly_without_gpu(tmp_path):
     import torch
     if torch.cuda.is_available():
         pytest.skip("GPU present")
-    st = configs.gait10dof18musc(4)
+    st = configs.gait10dof18musc(4, control_bounds=True)
     path = tmp_path / "gait.tape"
     write_tape(st.problem.create_rep(), st.solver.options(), str(path))
     r = _run(path)
@@ -46,6 +46,7 @@ def test_driver_loads_tape_and_fails_loudly_without_gpu(tmp_path):
 @pytest.mark.parametrize("name,mk", [
     ("gait_rigid", lambda: configs.gait10dof18musc(20)),
     ("double_pendulum_implicit", lambda: configs.double_pendulum(20, dynamics="implicit")),
+    ("gait_pathcon", lambda: configs.gait10dof18musc(10, control_bounds=True)),
 ])
 def test_driver_matches_python_binding_bit_exact(tmp_path, name, mk):
     """The C++ host and the ctypes binding drive the same library: same g and

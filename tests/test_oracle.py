@@ -411,3 +411,124 @@ def test_implicit_jacobian_matches_numerical_derivative(scheme):
     gf = nlp.eval_grad_f(x)
     gn = _numjac(lambda z: np.array([nlp.eval_f(z)]), x, range(nlp.n))[0]
     assert np.allclose(gf, gn, rtol=1e-6, atol=1e-7)
+
+
+# --------------------------------------------------------------------------
+# Path constraints: MocoControlBoundConstraint.
+# --------------------------------------------------------------------------
+def _bound_value(f, t):
+    from mocohip.problem import Constant
+    if isinstance(f, Constant):
+        return np.full_like(np.asarray(t, float), f.value)
+    br, cf = f.ppoly()
+    return ppoly_eval(br, cf, np.asarray(t, float), 0)
+
+
+@pytest.mark.parametrize("section,scheme", [("lower", "hermite-simpson"), ("upper", "trapezoidal"),
+                                            ("equality", "trapezoidal"), ("both", "hermite-simpson"),
+                                            ("both", "trapezoidal")])
+def test_path_constraint_layout_bounds_values(section, scheme):
+    """Path rows open every mesh interval and the tail (flattenConstraints,
+    CasOCTranscription.h:286-311); bounds [0, inf] / [-inf, 0] / [0, 0]
+    repeated per mesh point (MocoControlBoundConstraint.cpp:99-118,
+    CasOCTranscription.cpp:429-432); values control - bound(t) (:130-146);
+    rows block-dense over t0, tf and the mesh point's inputs."""
+    N = 6
+    st = configs.pendulum_control_bound(N, section, scheme)
+    rep = st.problem.create_rep()
+    nlp = OracleNLP(rep, st.solver.options())
+    pc = st.problem.path_constraints[0]
+    npc = {"lower": 1, "upper": 1, "equality": 1, "both": 2}[section]
+    assert rep.num_path_equations == nlp.NPC == npc
+    hs = scheme == "hermite-simpson"
+    NS, NC, G = nlp.NS, nlp.NC, nlp.G
+    rpi = npc + (2 * NS + NC if hs else NS)
+    assert nlp.m == N * rpi + npc and nlp.tail_rows == npc
+    x = nlp.random_iterate(np.random.default_rng(3).uniform(-1, 1, nlp.n))
+    g = nlp.eval_g(x)
+    xl, xu, gl, gu = nlp.bounds()
+    fns = [f for f in (pc.lower_bound, pc.upper_bound) if f is not None]
+    step = 2 if hs else 1
+    grid = np.arange(G) / (G - 1)
+    t = (x[1] - x[0]) * grid + x[0]
+    ir, jc = nlp.jac_structure()
+    for i in range(N + 1):
+        k = i * step
+        u = x[2 + NS * G + k * NC]
+        for e, f in enumerate(fns):
+            r = i * rpi + e
+            assert g[r] == pytest.approx(u - _bound_value(f, t[k]), abs=1e-13)
+            lo, hi = ((0.0, 0.0) if pc.equality_with_lower else
+                      (0.0, np.inf) if f is pc.lower_bound else (-np.inf, 0.0))
+            assert (gl[r], gu[r]) == (lo, hi)
+            cols = jc[ir == r].tolist()
+            pts = [2 + k * NS + s for s in range(NS)] + [2 + NS * G + k * NC + j for j in range(NC)]
+            assert cols == [0, 1] + pts
+    # every other row is an equality
+    path_rows = {i * rpi + e for i in range(N + 1) for e in range(npc)}
+    others = np.array([r for r in range(nlp.m) if r not in path_rows])
+    assert np.all(gl[others] == 0) and np.all(gu[others] == 0)
+
+
+@pytest.mark.parametrize("section,scheme,dynamics", [("equality", "hermite-simpson", "explicit"),
+                                                     ("both", "trapezoidal", "explicit"),
+                                                     ("both", "hermite-simpson", "implicit")])
+def test_path_constraint_jacobian_matches_numerical_derivative(section, scheme, dynamics):
+    st = configs.pendulum_control_bound(4, section, scheme, dynamics)
+    nlp = OracleNLP(st.problem.create_rep(), st.solver.options())
+    x = nlp.random_iterate(np.random.default_rng(2).uniform(-1, 1, nlp.n))
+    if nlp.NDV:
+        x[2 + (nlp.NS + nlp.NC) * nlp.G:] *= 1e-2
+    ir, jc = nlp.jac_structure()
+    J = np.zeros((nlp.m, nlp.n))
+    J[ir, jc] = nlp.eval_jac_g(x)
+    Jn = _numjac(nlp.eval_g, x, range(nlp.n))
+    noise = 100 * np.finfo(float).eps * max(np.abs(nlp.eval_g(x)).max(), 1.0) / st.solver.fd_step
+    assert np.allclose(J, Jn, rtol=1e-5, atol=max(1e-6, noise))
+
+
+def test_path_constraint_rejections():
+    """initializeOnModel checks (MocoControlBoundConstraint.cpp:53-93) and
+    "Time range of bounds function is too small" (testConstraints.cpp)."""
+    from mocohip.problem import GCVSpline, MocoControlBoundConstraint, Constant
+    st = configs.pendulum_control_bound(4, "lower")
+    p = st.problem
+    p.path_constraints[0].control_paths.append("/nonexistent")
+    with pytest.raises(ValueError, match="no such control"):
+        p.create_rep()
+    p.path_constraints[0].control_paths.pop()
+    p.path_constraints[0].set_upper_bound(Constant(1.0))
+    p.path_constraints[0].set_equality_with_lower(True)
+    with pytest.raises(ValueError, match="upper bound function must not be set"):
+        p.create_rep()
+    p.path_constraints = []
+    p.set_time_bounds((-31, 0), (1, 50))
+    c = p.add_path_constraint(MocoControlBoundConstraint())
+    c.add_control_path("/tau0")
+    c.set_lower_bound(GCVSpline(5, [-30.9999, 0, 0.5, 0.7, 0.8, 0.9, 50], [0, 0, 0, 0, 0, 0, 0.319]))
+    with pytest.raises(ValueError, match="must be less than or equal to the minimum"):
+        p.create_rep()
+    c.lower_bound = None
+    c.set_upper_bound(GCVSpline(5, [-31, 0, 0.5, 0.7, 0.8, 0.9, 49.99999], [0, 0, 0, 0, 0, 0, .0319]))
+    with pytest.raises(ValueError, match="must be greater than or equal to the maximum"):
+        p.create_rep()
+    # "Can omit both bounds": a constraint without bounds adds no rows
+    c.upper_bound = None
+    assert p.create_rep().num_path_equations == 0
+
+
+def test_gait_path_constraints_layout():
+    st = configs.gait10dof18musc(4, control_bounds=True)
+    rep = st.problem.create_rep()
+    nlp = OracleNLP(rep, st.solver.options())
+    base = OracleNLP(configs.gait10dof18musc(4).problem.create_rep(), st.solver.options())
+    npc = rep.num_path_equations
+    assert npc == 2 * 2 + 1
+    assert nlp.m == base.m + 5 * npc and nlp.n == base.n
+    assert nlp.nnz == base.nnz + 5 * npc * (2 + nlp.NS + nlp.NC)
+    # the DAE is untouched: same model hash inputs, same defects
+    x = base.random_iterate(np.random.default_rng(0).uniform(-1, 1, base.n))
+    g, g0 = nlp.eval_g(x), base.eval_g(x)
+    rpi, rpi0 = (nlp.m - npc) // 4, base.m // 4
+    for i in range(4):
+        assert np.array_equal(g[i * rpi + npc:(i + 1) * rpi], g0[i * rpi0:(i + 1) * rpi0])
