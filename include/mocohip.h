@@ -315,8 +315,9 @@ typedef struct mh_nlp_info {
     int64_t num_grid_points;
     int64_t num_states, num_controls;
     /* shard: rows [row_begin,row_end) and nonzeros [nnz_begin,nnz_end).
-     * Implicit mode adds the residual rows of the final grid point after the
-     * last interval; the shard owning the last interval owns them too.     */
+     * The tail -- the final mesh point's path rows, then (implicit mode) the
+     * final grid point's residual rows -- follows the last interval; the
+     * shard owning the last interval owns it too.                          */
     int64_t row_begin, row_end;
     int64_t nnz_begin, nnz_end;
 } mh_nlp_info;
