@@ -300,7 +300,30 @@ typedef struct mh_options {
     /* implicit_multibody_acceleration_bounds; {0, 0} = the reference default
      * [-1000, 1000] (MocoDirectCollocationSolver.cpp:39-40). */
     double implicit_accel_bounds[2];
+    /* optim_sparsity_detection (MocoCasADiSolver.h:120-123; CasOCSolver.cpp:
+     * 70-92; CasOCFunction.cpp:25-105).  NONE: every callback output
+     * depends on every input of its grid point (block-dense rows).  RANDOM /
+     * INITIAL_GUESS: at mh_create the DAE and path-constraint callbacks are
+     * evaluated on the device at the first grid point (time = initial_time)
+     * of each detection iterate, each input perturbed by +1e-5; an output
+     * depends on an input iff its value changes (or is NaN), OR-ed over the
+     * iterates, and Jacobian rows keep only those columns.  RANDOM uses
+     * sparsity_random_count iterates (<= 0: 3) from mh_get_random_iterate on
+     * uniform(-1, 1) numbers drawn from splitmix64 with seed 0, n per
+     * iterate (the reference's SimTK::Random::Uniform stream is not
+     * reproducible here); INITIAL_GUESS uses sparsity_guess (n doubles;
+     * NULL: the bounds-midpoint guess of mh_get_initial_guess_from_bounds). */
+    int32_t sparsity_detection;          /* mh_sparsity                      */
+    int32_t sparsity_random_count;
+    const double* sparsity_guess;
+    /* GIVEN: the callback sparsity itself, as mh_get_callback_sparsity
+     * returns it (e.g. detected once and reused by every shard / replica). */
+    const uint8_t* sparsity_pattern;
 } mh_options;
+
+enum mh_sparsity {
+    MH_SPARSITY_NONE = 0, MH_SPARSITY_RANDOM = 1, MH_SPARSITY_INITIAL_GUESS = 2, MH_SPARSITY_GIVEN = 3
+};
 
 enum mh_dynamics_mode { MH_DYNAMICS_EXPLICIT = 0, MH_DYNAMICS_IMPLICIT = 1 };
 
@@ -379,6 +402,11 @@ int mh_get_backend(const mh_ctx* ctx, char* name, int32_t name_len,
  * ("tasks interval" = task kernels with the fused per-interval transcription
  * for the Jacobian lanes; "lane", "generic", "split", ...). */
 int mh_get_backend_flags(const mh_ctx* ctx, char* flags, int32_t len);
+/* The callback sparsity the Jacobian structure was built from: (NQ + NZ)
+ * DAE outputs then npath path equations, each a row of 1 + NS + NC + NDV
+ * flags [time, states, controls, accelerations] (all 1 without detection).
+ * len = the capacity of `pattern` in bytes. */
+int mh_get_callback_sparsity(const mh_ctx* ctx, uint8_t* pattern, int64_t len);
 /* FNV-1a hash of everything the per-point DAE depends on (host only). */
 int mh_model_hash(const mh_model* model, uint64_t* hash);
 

@@ -74,6 +74,8 @@ struct Tape {
     std::vector<int32_t> gidx, gcol;
     std::vector<double> gw;
     std::vector<mh_path_equation> path;
+    std::vector<double> guess;
+    std::vector<uint8_t> pattern;
     mh_problem prob{};
 };
 
@@ -127,6 +129,21 @@ bool read_tape(const char* path, Tape& t, std::string& err) {
     if (version >= 2) {   // path-constraint equations
         t.prob.npath = r.pod<int32_t>();
         t.path = r.array<mh_path_equation>(t.prob.npath);
+        const int64_t gbytes = r.pod<int64_t>();   // sparsity-detection guess
+        if (r.ok && gbytes >= 0 && gbytes % 8 == 0 && r.pos + (size_t)gbytes <= r.buf.size()) {
+            t.guess.resize((size_t)gbytes / 8);
+            if (gbytes) std::memcpy(t.guess.data(), r.buf.data() + r.pos, (size_t)gbytes);
+            r.pos += (size_t)gbytes;
+        } else {
+            r.ok = false;
+        }
+        const int64_t pbytes = r.pod<int64_t>();   // given callback sparsity
+        if (r.ok && pbytes >= 0 && r.pos + (size_t)pbytes <= r.buf.size()) {
+            t.pattern.assign(r.buf.data() + r.pos, r.buf.data() + r.pos + pbytes);
+            r.pos += (size_t)pbytes;
+        } else {
+            r.ok = false;
+        }
     }
     if (!r.ok || r.pos != r.buf.size()) { err = "truncated or malformed tape"; return false; }
     m.bodies = t.bodies.data(); m.axes = t.axes.data(); m.functions = t.functions.data();
@@ -140,6 +157,8 @@ bool read_tape(const char* path, Tape& t, std::string& err) {
     t.prob.goal_column = t.gcol.data();
     t.prob.goal_weight = t.gw.data();
     t.prob.path = t.path.data();
+    t.opts.sparsity_guess = t.guess.empty() ? nullptr : t.guess.data();
+    t.opts.sparsity_pattern = t.pattern.empty() ? nullptr : t.pattern.data();
     return true;
 }
 

@@ -531,6 +531,7 @@ struct Interval {
     int N;           // mesh intervals of the whole problem
     int nnz_tail;    // nonzeros of the tail rows
     int ntail;       // tail rows: final mesh point's path rows + final residuals
+    int npe;         // path-constraint entries per mesh point (lead the interval / tail)
     PathEqs P;
     // Every interval opens with its mesh point's path rows.  The interval
     // N-1 also owns the tail (flattenConstraints, CasOCTranscription.h:
@@ -1011,8 +1012,8 @@ __global__ void __launch_bounds__(1024) k_interval(DevModel M, Src S, Lanes Ln, 
             const TplEntry te = tpl[e];
             if (te.kind != T_PATH) vi[e] = jac_entry<false>(L, Ln, I.P, S.x, YV, te, k_first, C);
         }
-        if (I.P.npc > 0) {
-            const int npe = I.P.npc * (2 + L.NI);
+        if (I.npe > 0) {
+            const int npe = I.npe;
             const int nw = i == I.N - 1 ? 2 * npe : npe;
             for (int w = threadIdx.x; w < nw; w += B) {
                 const int ep = w < npe ? w : I.nnz_int + (w - npe);
@@ -1396,6 +1397,8 @@ struct mh_ctx {
     int scheme = 0, N = 0, G = 0, interp = 0, rpi = 0, nnz_int = 0;
     int NDV = 0, nnz_tail = 0;     // implicit: accelerations per point, tail nonzeros
     int npc = 0, ntail = 0;        // path equations per mesh point; tail rows (npc + NDV)
+    int npe = 0;                   // path-constraint template entries per mesh point
+    std::vector<uint8_t> sp, sp_pc;  // detected sparsity [output][time, inputs] (empty: dense)
     std::vector<mh_path_equation> pc;
     PathEqs P{};
     double acc_lo = -1000.0, acc_hi = 1000.0;
@@ -1513,23 +1516,32 @@ static void build_template(mh_ctx* c) {
             c->tpl_col_pt.push_back(col.dir < 2 ? -1 : col.pt);
         }
     };
-    auto point_all = [&](int pt, std::vector<Col>& v) {
-        for (int j = 0; j < NS + NC + NDV; ++j) v.push_back({pt, 2 + j});
+    // Inputs of point pt that callback output o reads: all of them without
+    // sparsity detection (block-dense, CasOCFunction.cpp:25-105 "none"),
+    // else the detected ones (sp: [output][time, inputs]); plus the point's
+    // own state s_ident (the defects' identity terms).
+    const int W = 1 + NS + NC + NDV;
+    auto point_dep = [&](const std::vector<uint8_t>& sp, int o, int pt, int s_ident, std::vector<Col>& v) {
+        for (int j = 0; j < NS + NC + NDV; ++j)
+            if (sp.empty() || sp[(size_t)o * W + 1 + j] || j == s_ident) v.push_back({pt, 2 + j});
     };
-    // multibody residual rows of point pt: every input of the point + time
+    auto time_dep = [&](const std::vector<uint8_t>& sp, int o) { return sp.empty() || sp[(size_t)o * W] != 0; };
+    // multibody residual rows of point pt: the point's inputs + time
     auto residual_rows = [&](int& row, int pt) {
         for (int o = 0; o < (implicit ? NQ : 0); ++o) {
-            std::vector<Col> v{{pt, 0}, {pt, 1}};
-            point_all(pt, v);
+            std::vector<Col> v;
+            if (time_dep(c->sp, o)) { v.push_back({pt, 0}); v.push_back({pt, 1}); }
+            point_dep(c->sp, o, pt, -1, v);
             emit_row(row++, T_RES, T_RES, o, v, pt);
         }
     };
-    // path-constraint rows of mesh point pt: block-dense like the residuals
-    // (CasOCTranscription.cpp:419-433, sparsity detection "none")
+    // path-constraint rows of mesh point pt, like the residuals
+    // (CasOCTranscription.cpp:419-433)
     auto path_rows = [&](int& row, int pt) {
         for (int e = 0; e < c->npc; ++e) {
-            std::vector<Col> v{{pt, 0}, {pt, 1}};
-            point_all(pt, v);
+            std::vector<Col> v;
+            if (time_dep(c->sp_pc, e)) { v.push_back({pt, 0}); v.push_back({pt, 1}); }
+            point_dep(c->sp_pc, e, pt, -1, v);
             emit_row(row++, T_PATH, T_PATH, e, v, pt);
         }
     };
@@ -1551,8 +1563,10 @@ static void build_template(mh_ctx* c) {
                 v.push_back({1, 2 + s}); v.push_back({0, 2 + s}); v.push_back({2, 2 + s});
                 v.push_back({0, adir + s - NQ}); v.push_back({2, adir + s - NQ});
             } else {
+                // callback output s - NQ (explicit: udot / zdot; implicit:
+                // zdot after the NQ residuals)
                 v.push_back({1, 2 + s});
-                point_all(0, v); point_all(2, v);
+                point_dep(c->sp, s - NQ, 0, s, v); point_dep(c->sp, s - NQ, 2, s, v);
             }
             emit_row(row++, T_HERM_T, T_HERM_X, s, v);
         }
@@ -1565,7 +1579,8 @@ static void build_template(mh_ctx* c) {
                 v.push_back({0, 2 + s}); v.push_back({2, 2 + s});
                 v.push_back({0, adir + s - NQ}); v.push_back({1, adir + s - NQ}); v.push_back({2, adir + s - NQ});
             } else {
-                point_all(0, v); point_all(1, v); point_all(2, v);
+                point_dep(c->sp, s - NQ, 0, s, v); point_dep(c->sp, s - NQ, 1, -1, v);
+                point_dep(c->sp, s - NQ, 2, s, v);
             }
             emit_row(row++, T_SIMP_T, T_SIMP_X, s, v);
         }
@@ -1587,7 +1602,7 @@ static void build_template(mh_ctx* c) {
                 v.push_back({0, 2 + s}); v.push_back({1, 2 + s});
                 v.push_back({0, adir + s - NQ}); v.push_back({1, adir + s - NQ});
             } else {
-                point_all(0, v); point_all(1, v);
+                point_dep(c->sp, s - NQ, 0, s, v); point_dep(c->sp, s - NQ, 1, s, v);
             }
             emit_row(row++, T_TRAP_T, T_TRAP_X, s, v);
         }
@@ -1601,12 +1616,14 @@ static void build_template(mh_ctx* c) {
     residual_rows(row, c->scheme == MH_HERMITE_SIMPSON ? 2 : 1);
     c->nnz_tail = (int)c->tpl.size() - c->nnz_int;
     c->ntail = row - c->rpi;
+    c->npe = 0;
+    for (int e = 0; e < c->nnz_int; ++e) c->npe += c->tpl[e].kind == T_PATH;
 }
 
 // k_interval writes the path-constraint entries in a loop of their own over
 // the first npc * (2 + NI) entries of the interval and of the tail.
 static bool path_entries_lead(const mh_ctx* c) {
-    const int npe = c->npc * (2 + c->NI);
+    const int npe = c->npe;
     if (npe > c->nnz_int || npe > c->nnz_tail) return c->npc == 0;
     for (int e = 0; e < (int)c->tpl.size(); ++e) {
         const bool lead = e < npe || (e >= c->nnz_int && e < c->nnz_int + npe);
@@ -1823,6 +1840,7 @@ extern "C" int mh_model_hash(const mh_model* M, uint64_t* hash) {
 }
 
 static const Backend* select_backend(mh_ctx* c, const mh_problem* p);
+static int detect_sparsity(mh_ctx* c, const mh_options* o);
 static const TaskInfo* backend_tasks(const Backend* b);
 static bool interval_fits(const mh_ctx* c, int mode);
 
@@ -1992,6 +2010,26 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
         c->timing = ee && std::strcmp(ee, "1") == 0;
         const char* eq = std::getenv("MOCOHIP_QUOT");
         c->quot = eq && std::strcmp(eq, "1") == 0;   // opt-in: measured slower
+        if (o->sparsity_detection != MH_SPARSITY_NONE) {
+            // detect on the device, then rebuild the (smaller) template in
+            // place of the block-dense one
+            const size_t cap = c->tpl.size();
+            int rc2 = detect_sparsity(c.get(), o);
+            if (rc2) return rc2;
+            c->tpl.clear();
+            c->tpl_col_pt.clear();
+            build_template(c.get());
+            if (!path_entries_lead(c.get()) || c->tpl.size() > cap)
+                return set_err(MH_ERR_INVALID, "internal: detected template layout");
+            c->nnz = (int64_t)c->nnz_int * c->N + c->nnz_tail;
+            c->tplp.clear();
+            for (const TplEntry& e : c->tpl) c->tplp.push_back(tpl_pack(e));
+            if (c->tplp.size() % 2) c->tplp.push_back(0u);
+            HIPCHK(hipMemcpy(c->d_tpl, c->tpl.data(), sizeof(TplEntry) * c->tpl.size(), hipMemcpyHostToDevice));
+            HIPCHK(hipMemcpy(c->d_tplp, c->tplp.data(), sizeof(uint32_t) * c->tplp.size(),
+                    hipMemcpyHostToDevice));
+            c->P.npc = c->npc;
+        }
         for (int mode = 0; mode < 2; ++mode)
             c->use_interval[mode] = allow && interval_fits(c.get(), mode);
     }
@@ -2213,7 +2251,7 @@ static void be_interval(mh_ctx* c, const double* x, int mode, double* g, double*
         (void)hipFuncSetAttribute((const void*)k_interval<D>, hipFuncAttributeMaxDynamicSharedMemorySize,
                 (int)lds);
     Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, c->k0, c->nk, c->NDV};
-    Interval I{c->scheme, c->interp, c->ib, c->rpi, c->nnz_int, c->NDV, c->N, c->nnz_tail, c->ntail, c->P};
+    Interval I{c->scheme, c->interp, c->ib, c->rpi, c->nnz_int, c->NDV, c->N, c->nnz_tail, c->ntail, c->npe, c->P};
     const unsigned threads = v ? 1024u : 256u;
     hipLaunchKernelGGL(k_interval<D>, dim3((unsigned)(c->ie - c->ib)), dim3(threads), lds, c->stream, c->M,
             S, ln, ts.dev, L, I, c->d_tpl, c->d_tplp, tables, c->d_T, c->d_H, g, v);
@@ -2296,7 +2334,7 @@ static int launch_stage(mh_ctx* c, int stage, int kind, const double* x, double*
         return MH_OK;
     }
     Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, c->k0, c->nk, c->NDV};
-    Interval I{c->scheme, c->interp, c->ib, c->rpi, c->nnz_int, c->NDV, c->N, c->nnz_tail, c->ntail, c->P};
+    Interval I{c->scheme, c->interp, c->ib, c->rpi, c->nnz_int, c->NDV, c->N, c->nnz_tail, c->ntail, c->npe, c->P};
     const Lanes& ln = kind == 0 ? c->lanes_g : c->lanes_jac;
     const double* Y = kind == 0 ? c->d_Yg : c->d_Y;
     const int nchunks = kind == 0 ? 0 : (c->nnz_int + (c->ie == c->N ? c->nnz_tail : 0) + ASM_CHUNK - 1) / ASM_CHUNK;
@@ -2529,6 +2567,113 @@ extern "C" int mh_eval_dae(mh_ctx* c, int32_t np, const double* inputs, double* 
 }
 
 
+// Path-constraint values of np probe rows [t, states, controls, ...]
+// (sparsity detection of the path-constraint callbacks).
+__global__ void __launch_bounds__(256) k_path_probe(PathEqs P, int np, int NS, int W,
+        const double* __restrict__ in, double* __restrict__ out) {
+    const int w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= np * P.npc) return;
+    const int q = w / P.npc, e = w - q * P.npc;
+    const double* r = in + (long)q * W;
+    out[w] = path_value(P, e, r[0], r[1 + NS + P.eq[e].index]);
+}
+
+// splitmix64 uniform(-1, 1) stream (include/mocohip.h
+// mh_options.sparsity_detection; stands in for SimTK::Random::Uniform).
+static double splitmix_uniform(uint64_t& st) {
+    uint64_t z = (st += 0x9e3779b97f4a7c15ULL);
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+    z ^= z >> 31;
+    return (double)(z >> 11) * (2.0 / 9007199254740992.0) - 1.0;
+}
+
+// calcJacobianSparsityWithPerturbation (CasOCFunction.cpp:25-71) of the DAE
+// callback and of each path equation, evaluated on the device at
+// getSubsetPoint of each detection iterate (CasOCFunction.h:72-86: time =
+// initial_time, the first grid point's variables; iterates per
+// CasOCSolver.cpp:70-92): input j perturbed by +1e-5, a change (or NaN)
+// marks the dependency; OR over the iterates.
+static int detect_sparsity(mh_ctx* c, const mh_options* o) {
+    const int W = 1 + c->NI, NO = c->NO, NPC = c->npc;
+    std::vector<double> pts;
+    int npts = 1;
+    if (o->sparsity_detection == MH_SPARSITY_RANDOM) {
+        npts = o->sparsity_random_count > 0 ? o->sparsity_random_count : 3;
+        pts.resize((size_t)c->n * npts);
+        std::vector<double> r(c->n);
+        uint64_t st = 0;
+        for (int q = 0; q < npts; ++q) {
+            for (auto& v : r) v = splitmix_uniform(st);
+            mh_get_random_iterate(c, r.data(), pts.data() + (size_t)q * c->n);
+        }
+    } else if (o->sparsity_detection == MH_SPARSITY_INITIAL_GUESS) {
+        // no guess given: the default "bounds" guess (midpoints,
+        // CasOCTranscription.cpp:1123-1149)
+        if (o->sparsity_guess) pts.assign(o->sparsity_guess, o->sparsity_guess + c->n);
+        else {
+            pts.resize(c->n);
+            mh_get_initial_guess_from_bounds(c, pts.data());
+        }
+    } else if (o->sparsity_detection == MH_SPARSITY_GIVEN) {
+        if (!o->sparsity_pattern) return set_err(MH_ERR_INVALID, "GIVEN sparsity needs sparsity_pattern");
+        c->sp.assign(o->sparsity_pattern, o->sparsity_pattern + (size_t)NO * W);
+        c->sp_pc.assign(o->sparsity_pattern + (size_t)NO * W, o->sparsity_pattern + (size_t)(NO + NPC) * W);
+        return MH_OK;
+    } else {
+        return set_err(MH_ERR_INVALID, "unknown sparsity detection %d", o->sparsity_detection);
+    }
+    const int rows = npts * (1 + W);
+    std::vector<double> in((size_t)rows * W);
+    for (int q = 0; q < npts; ++q) {
+        const double* x = pts.data() + (size_t)q * c->n;
+        double* base = in.data() + (size_t)q * (1 + W) * W;
+        base[0] = x[0];
+        for (int s = 0; s < c->NS; ++s) base[1 + s] = x[col_state(c, 0, s)];
+        for (int j = 0; j < c->NC; ++j) base[1 + c->NS + j] = x[col_control(c, 0, j)];
+        for (int j = 0; j < c->NDV; ++j) base[1 + c->NS + c->NC + j] = x[col_deriv(c, 0, j)];
+        for (int j = 0; j < W; ++j) {
+            double* r = base + (size_t)(1 + j) * W;
+            std::memcpy(r, base, sizeof(double) * W);
+            r[j] = base[j] + 1e-5;
+        }
+    }
+    std::vector<double> out((size_t)rows * std::max(NO, 1)), pout((size_t)rows * std::max(NPC, 1));
+    if (NO > 0) {
+        const int rc = mh_eval_dae(c, rows, in.data(), out.data());
+        if (rc) return rc;
+    }
+    if (NPC > 0) {
+        double *din = nullptr, *dout = nullptr;
+        HIPCHK(hipMalloc(&din, sizeof(double) * in.size()));
+        HIPCHK(hipMalloc(&dout, sizeof(double) * pout.size()));
+        HIPCHK(hipMemcpyAsync(din, in.data(), sizeof(double) * in.size(), hipMemcpyHostToDevice, c->stream));
+        const int nthr = rows * NPC;
+        k_path_probe<<<(nthr + 255) / 256, 256, 0, c->stream>>>(c->P, rows, c->NS, W, din, dout);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(pout.data(), dout, sizeof(double) * pout.size(), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        (void)hipFree(din);
+        (void)hipFree(dout);
+    }
+    c->sp.assign((size_t)NO * W, 0);
+    c->sp_pc.assign((size_t)NPC * W, 0);
+    for (int q = 0; q < npts; ++q) {
+        const size_t r0 = (size_t)q * (1 + W);
+        for (int j = 0; j < W; ++j) {
+            for (int k = 0; k < NO; ++k) {
+                const double d = out[(r0 + 1 + j) * NO + k] - out[r0 * NO + k];
+                if (std::isnan(d) || d != 0) c->sp[(size_t)k * W + j] = 1;
+            }
+            for (int e = 0; e < NPC; ++e) {
+                const double d = pout[(r0 + 1 + j) * NPC + e] - pout[r0 * NPC + e];
+                if (std::isnan(d) || d != 0) c->sp_pc[(size_t)e * W + j] = 1;
+            }
+        }
+    }
+    return MH_OK;
+}
+
 #ifdef MH_TASK_TIMING
 extern "C" int mh_debug_task_timing(long long* out, int nslots) {
     const int n = std::min(nslots, TIMING_SLOTS);
@@ -2563,6 +2708,17 @@ extern "C" int mh_get_backend(const mh_ctx* c, char* name, int32_t name_len, dou
     }
     if (flops_per_eval) *flops_per_eval = c->be->flops_per_eval;
     if (model_hash) *model_hash = c->model_hash;
+    return MH_OK;
+}
+
+extern "C" int mh_get_callback_sparsity(const mh_ctx* c, uint8_t* pattern, int64_t len) {
+    if (!c || !pattern) return set_err(MH_ERR_INVALID, "null argument");
+    const size_t W = 1 + (size_t)c->NI, need = ((size_t)c->NO + c->npc) * W;
+    if (len < (int64_t)need) return set_err(MH_ERR_INVALID, "pattern needs %zu bytes", need);
+    for (size_t i = 0; i < need; ++i) {
+        const size_t nd = (size_t)c->NO * W;
+        pattern[i] = i < nd ? (c->sp.empty() ? 1 : c->sp[i]) : (c->sp_pc.empty() ? 1 : c->sp_pc[i - nd]);
+    }
     return MH_OK;
 }
 

@@ -139,7 +139,12 @@ class mh_options(C.Structure):
                 ("finite_difference_scheme", i32), ("fd_step", f64),
                 ("interval_begin", i32), ("interval_end", i32),
                 ("device", i32), ("multibody_dynamics_mode", i32),
-                ("implicit_accel_bounds", f64 * 2)]
+                ("implicit_accel_bounds", f64 * 2),
+                ("sparsity_detection", i32), ("sparsity_random_count", i32),
+                ("sparsity_guess", P(f64)), ("sparsity_pattern", P(C.c_uint8))]
+
+
+MH_SPARSITY_NONE, MH_SPARSITY_RANDOM, MH_SPARSITY_INITIAL_GUESS, MH_SPARSITY_GIVEN = 0, 1, 2, 3
 
 
 class mh_nlp_info(C.Structure):
@@ -176,6 +181,7 @@ MOCOHIP_SYMBOLS = {
     "mh_last_timings": (i32, [C.c_void_p, P(f64)]),
     "mh_get_backend": (i32, [C.c_void_p, C.c_char_p, i32, P(f64), P(C.c_uint64)]),
     "mh_model_hash": (i32, [P(mh_model), P(C.c_uint64)]),
+    "mh_get_callback_sparsity": (i32, [C.c_void_p, P(C.c_uint8), C.c_int64]),
     "mh_get_work": (i32, [C.c_void_p, P(f64)]),
 }
 
@@ -198,6 +204,7 @@ ORACLE_SYMBOLS = {
     "orc_muscle_length_speed": (i32, [C.c_void_p, C.c_int, P(f64), P(f64),
                                       P(f64)]),
     "orc_eval_function": (i32, [C.c_void_p, C.c_int, f64, P(f64)]),
+    "orc_get_callback_sparsity": (i32, [C.c_void_p, P(C.c_uint8), C.c_int64]),
 }
 
 LIBMOCOHIP_PATH = os.path.join(PKG_ROOT, "csrc", "build", "libmocohip.so")

@@ -26,6 +26,9 @@ _SCHEMES = {"hermite-simpson": abi.MH_HERMITE_SIMPSON,
             "trapezoidal": abi.MH_TRAPEZOIDAL}
 _FD = {"central": abi.MH_FD_CENTRAL, "forward": abi.MH_FD_FORWARD,
        "backward": abi.MH_FD_BACKWARD}
+_SPARSITY = {"none": abi.MH_SPARSITY_NONE, "random": abi.MH_SPARSITY_RANDOM,
+             "initial-guess": abi.MH_SPARSITY_INITIAL_GUESS,
+             "given": abi.MH_SPARSITY_GIVEN}
 
 
 @dataclass
@@ -35,7 +38,14 @@ class MocoHipSolver:
     interpolate_control_midpoints: bool = True
     multibody_dynamics_mode: str = "explicit"
     optim_finite_difference_scheme: str = "central"
+    # "none" (block-dense), "random" (3 iterates, CasOCSolver.cpp:70-92) or
+    # "initial-guess" (sparsity_guess, default the bounds-midpoint guess)
     optim_sparsity_detection: str = "none"
+    optim_sparsity_detection_random_count: int = 3
+    sparsity_guess: Optional[np.ndarray] = None
+    # "given": the callback sparsity itself (HipNLP.callback_sparsity()),
+    # e.g. detected once and shared by every shard / replica
+    sparsity_pattern: Optional[np.ndarray] = None
     fd_step: float = 1e-8
     device: int = 0
     # MocoDirectCollocationSolver implicit_multibody_acceleration_bounds
@@ -51,8 +61,9 @@ class MocoHipSolver:
                              "central, forward, backward")
         if self.multibody_dynamics_mode not in ("explicit", "implicit"):
             raise ValueError("multibody_dynamics_mode must be 'explicit' or 'implicit'")
-        if self.optim_sparsity_detection != "none":
-            raise NotImplementedError("sparsity detection: not yet on the HIP path")
+        if self.optim_sparsity_detection not in _SPARSITY:
+            raise ValueError("optim_sparsity_detection must be one of none, random, "
+                             "initial-guess")   # MocoCasADiSolver.cpp:248-249
         o = abi.mh_options()
         o.num_mesh_intervals = int(self.num_mesh_intervals)
         o.transcription = _SCHEMES[self.transcription_scheme]
@@ -67,6 +78,18 @@ class MocoHipSolver:
         lo, hi = self.implicit_multibody_acceleration_bounds
         o.implicit_accel_bounds[0] = float(lo)
         o.implicit_accel_bounds[1] = float(hi)
+        o.sparsity_detection = _SPARSITY[self.optim_sparsity_detection]
+        o.sparsity_random_count = int(self.optim_sparsity_detection_random_count)
+        if self.sparsity_guess is not None:
+            if self.optim_sparsity_detection != "initial-guess":
+                raise ValueError("sparsity_guess needs optim_sparsity_detection='initial-guess'")
+            self._guess = np.ascontiguousarray(self.sparsity_guess, float)
+            o.sparsity_guess = abi.dptr(self._guess)
+        if (self.sparsity_pattern is not None) != (self.optim_sparsity_detection == "given"):
+            raise ValueError("optim_sparsity_detection='given' goes with sparsity_pattern")
+        if self.sparsity_pattern is not None:
+            self._pattern = np.ascontiguousarray(self.sparsity_pattern, np.uint8)
+            o.sparsity_pattern = self._pattern.ctypes.data_as(C.POINTER(C.c_uint8))
         return o
 
 
@@ -142,6 +165,16 @@ class _NLPBase:
     def NDV(self) -> int:
         """Derivative variables per grid point (implicit mode: NQ)."""
         return self.NQ if self.opts.multibody_dynamics_mode == abi.MH_DYNAMICS_IMPLICIT else 0
+
+    def callback_sparsity(self) -> np.ndarray:
+        """The callback sparsity behind the Jacobian structure: (NQ + NZ)
+        DAE outputs then the path equations, rows of [time, inputs] flags."""
+        W = 1 + self.NS + self.NC + self.NDV
+        NO = self.NS - self.NQ            # NQ + NZ
+        buf = np.zeros((NO + self.NPC) * W, np.uint8)
+        self._check(self._fn("get_callback_sparsity")(
+            self.ctx, buf.ctypes.data_as(C.POINTER(C.c_uint8)), buf.size))
+        return buf
 
     @property
     def NPC(self) -> int:

@@ -8,7 +8,8 @@ Layout (little endian, x86-64 struct layout of include/mocohip.h):
   the 12 mh_model counts, gravity[3], time bounds (2 x mh_bounds),
   ngoals, nterms, then the arrays in mh_model / mh_problem field order,
   each as (int64 byte count, bytes); version 2 appends npath and the
-  mh_path_equation array."""
+  mh_path_equation array, then the sparsity-detection guess (n doubles or
+  empty) and the given callback sparsity (bytes or empty)."""
 from __future__ import annotations
 
 import ctypes as C
@@ -43,7 +44,21 @@ def write_tape(rep, opts: abi.mh_options, path: str) -> None:
     p = rep.struct
     m = p.model
     ns, nc = len(rep.state_names), len(rep.control_names)
-    out = [MAGIC, struct.pack("<iii", VERSION, ns, nc), bytes(opts)]
+    # pointers inside mh_options do not travel: the sparsity guess is a blob
+    guess = b""
+    if opts.sparsity_guess:
+        G = (2 * opts.num_mesh_intervals + 1 if opts.transcription == abi.MH_HERMITE_SIMPSON
+             else opts.num_mesh_intervals + 1)
+        ndv = m.nq if opts.multibody_dynamics_mode == abi.MH_DYNAMICS_IMPLICIT else 0
+        guess = C.string_at(opts.sparsity_guess, 8 * (2 + (ns + nc + ndv) * G))
+    pattern = b""
+    if opts.sparsity_pattern:
+        W = 1 + ns + nc + (m.nq if opts.multibody_dynamics_mode == abi.MH_DYNAMICS_IMPLICIT else 0)
+        pattern = C.string_at(opts.sparsity_pattern, (ns - m.nq + p.npath) * W)
+    o2 = abi.mh_options.from_buffer_copy(bytes(opts))
+    o2.sparsity_guess = None
+    o2.sparsity_pattern = None
+    out = [MAGIC, struct.pack("<iii", VERSION, ns, nc), bytes(o2)]
     out.append(struct.pack("<12i", *[getattr(m, k) for k in _COUNTS]))
     out.append(struct.pack("<3d", *m.gravity))
     out.append(bytes(p.time_initial) + bytes(p.time_final))
@@ -60,5 +75,6 @@ def write_tape(rep, opts: abi.mh_options, path: str) -> None:
         out.append(b)
     pb = _blob(p.path, abi.mh_path_equation, p.npath)
     out += [struct.pack("<i", p.npath), struct.pack("<q", len(pb)), pb]
+    out += [struct.pack("<q", len(guess)), guess, struct.pack("<q", len(pattern)), pattern]
     with open(path, "wb") as fh:
         fh.write(b"".join(out))

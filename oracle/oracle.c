@@ -236,6 +236,9 @@ struct orc_ctx {
     double* gw;
     int NPC;                /* path-constraint equations per mesh point  */
     mh_path_equation* pc;
+    /* detected callback sparsity (NULL: block-dense): [output][1 + input],
+     * column 0 = time; DAE outputs (NQ + NZ) and path equations */
+    uint8_t *sp, *sp_pc;
     /* derived sizes */
     int NQ, NZ, NS, NC, NP; /* NP = per-point inputs excluding time */
     int implicit;           /* MH_DYNAMICS_IMPLICIT                     */
@@ -283,18 +286,25 @@ static int nres(const orc_ctx* c) { return c->implicit ? c->NQ : 0; }
 /* the mesh point that opens interval i (and closes interval i-1) */
 static int mesh_point(const orc_ctx* c, int i) { return c->scheme == MH_HERMITE_SIMPSON ? 2 * i : i; }
 
-/* Sorted columns of all point inputs at grid point k (excluding t0/tf). */
-static int point_cols(const orc_ctx* c, int k, int64_t* out) {
-    int n = 0;
-    for (int s = 0; s < c->NS; ++s) out[n++] = col_state(c, k, s);
-    for (int j = 0; j < c->NC; ++j) out[n++] = col_control(c, k, j);
-    for (int j = 0; j < c->NDV; ++j) out[n++] = col_deriv(c, k, j);
-    return n;
-}
-
 static int cmp64(const void* a, const void* b) {
     int64_t x = *(const int64_t*)a, y = *(const int64_t*)b;
     return x < y ? -1 : x > y;
+}
+
+/* Does callback output o (DAE: sp, path equation: sp_pc) read input j
+ * (-1 = time)?  Block-dense (no detection): always. */
+static int dep(const uint8_t* sp, int NP, int o, int j) { return !sp || sp[(int64_t)o * (1 + NP) + 1 + j]; }
+/* Columns of grid point k that callback output o reads, plus (if s >= 0)
+ * the point's own state s (the defects' identity terms), ascending. */
+static int point_cols_dep(const orc_ctx* c, const uint8_t* sp, int o, int k, int s, int64_t* out) {
+    int n = 0;
+    for (int j = 0; j < c->NP; ++j) {
+        if (!(dep(sp, c->NP, o, j) || j == s)) continue;
+        if (j < c->NS) out[n++] = col_state(c, k, j);
+        else if (j < c->NS + c->NC) out[n++] = col_control(c, k, j - c->NS);
+        else out[n++] = col_deriv(c, k, j - c->NS - c->NC);
+    }
+    return n;
 }
 
 /* Emits the sorted column set of every row of interval i, in row order.
@@ -306,8 +316,8 @@ static int64_t residual_rows(const orc_ctx* c, int k, int64_t row, row_fn emit, 
         int64_t* cols) {
     for (int o = 0; o < nres(c); ++o) {
         int n = 0;
-        cols[n++] = 0; cols[n++] = 1;
-        n += point_cols(c, k, cols + n);
+        if (dep(c->sp, c->NP, o, -1)) { cols[n++] = 0; cols[n++] = 1; }
+        n += point_cols_dep(c, c->sp, o, k, -1, cols + n);
         emit(ud, row++, cols, n);
     }
     return row;
@@ -320,8 +330,8 @@ static int64_t path_rows(const orc_ctx* c, int k, int64_t row, row_fn emit, void
         int64_t* cols) {
     for (int e = 0; e < c->NPC; ++e) {
         int n = 0;
-        cols[n++] = 0; cols[n++] = 1;
-        n += point_cols(c, k, cols + n);
+        if (dep(c->sp_pc, c->NP, e, -1)) { cols[n++] = 0; cols[n++] = 1; }
+        n += point_cols_dep(c, c->sp_pc, e, k, -1, cols + n);
         emit(ud, row++, cols, n);
     }
     return row;
@@ -371,14 +381,17 @@ static void interval_rows(const orc_ctx* c, int i, int64_t row0, row_fn emit, vo
                         cols[n++] = col_deriv(c, kp, j);
                     }
                 } else {
+                    /* callback output s - NQ (explicit: udot / zdot;
+                     * implicit: zdot after the NQ residuals) */
+                    int o = s - NQ;
                     if (pass == 0) {
                         cols[n++] = col_state(c, km, s);
-                        n += point_cols(c, ki, cols + n);
-                        n += point_cols(c, kp, cols + n);
+                        n += point_cols_dep(c, c->sp, o, ki, s, cols + n);
+                        n += point_cols_dep(c, c->sp, o, kp, s, cols + n);
                     } else {
-                        n += point_cols(c, ki, cols + n);
-                        n += point_cols(c, km, cols + n);
-                        n += point_cols(c, kp, cols + n);
+                        n += point_cols_dep(c, c->sp, o, ki, s, cols + n);
+                        n += point_cols_dep(c, c->sp, o, km, -1, cols + n);
+                        n += point_cols_dep(c, c->sp, o, kp, s, cols + n);
                     }
                 }
                 qsort(cols, (size_t)n, sizeof(int64_t), cmp64);
@@ -406,8 +419,8 @@ static void interval_rows(const orc_ctx* c, int i, int64_t row0, row_fn emit, vo
                 cols[n++] = col_state(c, ki, s); cols[n++] = col_state(c, kp, s);
                 cols[n++] = col_deriv(c, ki, s - NQ); cols[n++] = col_deriv(c, kp, s - NQ);
             } else {
-                n += point_cols(c, ki, cols + n);
-                n += point_cols(c, kp, cols + n);
+                n += point_cols_dep(c, c->sp, s - NQ, ki, s, cols + n);
+                n += point_cols_dep(c, c->sp, s - NQ, kp, s, cols + n);
             }
             qsort(cols, (size_t)n, sizeof(int64_t), cmp64);
             emit(ud, row++, cols, n);
@@ -444,6 +457,10 @@ static void tail_rows(const orc_ctx* c, int64_t row0, row_fn emit, void* ud) {
     residual_rows(c, c->G - 1, row0, emit, ud, cols);
     free(cols);
 }
+
+#ifndef ORACLE_COUNTING
+static int detect_sparsity(orc_ctx* c, const mh_options* o);
+#endif
 
 int orc_create(const mh_problem* p, const mh_options* o, orc_ctx** out) {
     if (!p || !o || !out) return fail(MH_ERR_INVALID, "null argument");
@@ -606,6 +623,17 @@ int orc_create(const mh_problem* p, const mh_options* o, orc_ctx** out) {
     free(mesh);
     c->n = 2 + (int64_t)(c->NS + c->NC + c->NDV) * c->G;
     c->m = (int64_t)rows_per_interval(c) * c->N + ntail(c);
+    c->fd = o->finite_difference_scheme;
+    c->h = o->fd_step > 0 ? o->fd_step : 1e-8;
+    if (o->sparsity_detection != MH_SPARSITY_NONE) {
+#ifndef ORACLE_COUNTING
+        int rc = detect_sparsity(c, o);
+        if (rc) { orc_destroy(c); return rc; }
+#else
+        orc_destroy(c);
+        return fail(MH_ERR_UNSUPPORTED, "sparsity detection");
+#endif
+    }
     /* structure */
     emit_state e = {0, NULL, NULL};
     for (int i = 0; i < c->N; ++i) interval_rows(c, i, 0, emit_count, &e);
@@ -617,8 +645,6 @@ int orc_create(const mh_problem* p, const mh_options* o, orc_ctx** out) {
     int rpi = rows_per_interval(c);
     for (int i = 0; i < c->N; ++i) interval_rows(c, i, (int64_t)i * rpi, emit_fill, &e);
     tail_rows(c, (int64_t)c->N * rpi, emit_fill, &e);
-    c->fd = o->finite_difference_scheme;
-    c->h = o->fd_step > 0 ? o->fd_step : 1e-8;
     *out = c;
     return MH_OK;
 }
@@ -627,7 +653,7 @@ void orc_destroy(orc_ctx* c) {
     if (!c) return;
     void* ptrs[] = {c->bodies, c->axes, c->funcs, c->kx, c->ky, c->kb, c->kc, c->kd,
             c->mus, c->pts, c->acts, c->tabs, c->brk, c->coef, c->ext, c->sinfo, c->cinfo,
-            c->goals, c->gidx, c->gcol, c->gw, c->pc, c->mus_act_state, c->mus_ftn_state,
+            c->goals, c->gidx, c->gcol, c->gw, c->pc, c->sp, c->sp_pc, c->mus_act_state, c->mus_ftn_state,
             c->mus_control, c->coord_body, c->grid, c->quad, c->iRow, c->jCol};
     for (size_t i = 0; i < sizeof ptrs / sizeof ptrs[0]; ++i) free(ptrs[i]);
     free(c);
@@ -1396,6 +1422,91 @@ static double path_value(const orc_ctx* c, int e, double t, const double* ct) {
     const mh_path_equation* E = &c->pc[e];
     double b = E->table < 0 ? E->value : table_eval(c, E->table, E->column, t);
     return ct[E->index] - b;
+}
+
+/* splitmix64 uniform(-1, 1) stream, seed 0 (include/mocohip.h
+ * mh_options.sparsity_detection; stands in for SimTK::Random::Uniform). */
+static double splitmix_uniform(uint64_t* st) {
+    uint64_t z = (*st += 0x9e3779b97f4a7c15ULL);
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+    z ^= z >> 31;
+    return (double)(z >> 11) * (2.0 / 9007199254740992.0) - 1.0;
+}
+
+/* calcJacobianSparsityWithPerturbation (CasOCFunction.cpp:25-71) for the
+ * DAE callback and each path equation, at getSubsetPoint of every
+ * detection iterate (CasOCFunction.h:72-86: time = initial_time, the first
+ * grid point's variables); iterates per CasOCSolver.cpp:70-92. */
+static int detect_sparsity(orc_ctx* c, const mh_options* o) {
+    int NS = c->NS, NP = c->NP, NO = c->NQ + c->NZ, W = 1 + NP, NPC = c->NPC;
+    int npts = 1;
+    double* pts;
+    if (o->sparsity_detection == MH_SPARSITY_RANDOM) {
+        npts = o->sparsity_random_count > 0 ? o->sparsity_random_count : 3;
+        pts = (double*)malloc(sizeof(double) * (size_t)c->n * (size_t)npts);
+        double* r = (double*)malloc(sizeof(double) * (size_t)c->n);
+        uint64_t st = 0;
+        for (int q = 0; q < npts; ++q) {
+            for (int64_t i = 0; i < c->n; ++i) r[i] = splitmix_uniform(&st);
+            orc_get_random_iterate(c, r, pts + (int64_t)q * c->n);
+        }
+        free(r);
+    } else if (o->sparsity_detection == MH_SPARSITY_INITIAL_GUESS) {
+        pts = (double*)malloc(sizeof(double) * (size_t)c->n);
+        if (o->sparsity_guess) memcpy(pts, o->sparsity_guess, sizeof(double) * (size_t)c->n);
+        else orc_get_initial_guess_from_bounds(c, pts);   /* the default "bounds" guess */
+    } else if (o->sparsity_detection == MH_SPARSITY_GIVEN) {
+        if (!o->sparsity_pattern) return fail(MH_ERR_INVALID, "GIVEN sparsity needs sparsity_pattern");
+        c->sp = (uint8_t*)malloc((size_t)NO * W + 1);
+        c->sp_pc = (uint8_t*)malloc((size_t)NPC * W + 1);
+        memcpy(c->sp, o->sparsity_pattern, (size_t)NO * W);
+        memcpy(c->sp_pc, o->sparsity_pattern + (size_t)NO * W, (size_t)NPC * W);
+        return MH_OK;
+    } else {
+        return fail(MH_ERR_INVALID, "unknown sparsity detection %d", o->sparsity_detection);
+    }
+    c->sp = (uint8_t*)calloc((size_t)NO * W + 1, 1);
+    c->sp_pc = (uint8_t*)calloc((size_t)NPC * W + 1, 1);
+    dae_ws w;
+    ws_alloc(c, &w);
+    double* in = (double*)malloc(sizeof(double) * (size_t)(W + 2 * NO + 2 * NPC + 2));
+    double *y0 = in + W, *y = y0 + NO, *p0 = y + NO, *pv = p0 + NPC;
+    const double eps = 1e-5;
+    for (int q = 0; q < npts; ++q) {
+        const double* x = pts + (int64_t)q * c->n;
+        in[0] = x[0];
+        gather_point(c, x, 0, in + 1, in + 1 + NS);
+        eval_dae_point(c, &w, in[0], in + 1, in + 1 + NS, y0);
+        for (int e = 0; e < NPC; ++e) p0[e] = path_value(c, e, in[0], in + 1 + NS);
+        for (int j = 0; j < W; ++j) {
+            double sv = in[j];
+            in[j] = sv + eps;
+            eval_dae_point(c, &w, in[0], in + 1, in + 1 + NS, y);
+            for (int e = 0; e < NPC; ++e) pv[e] = path_value(c, e, in[0], in + 1 + NS);
+            in[j] = sv;
+            for (int k = 0; k < NO; ++k) {
+                double d = y[k] - y0[k];
+                if (isnan(d) || d != 0) c->sp[(int64_t)k * W + j] = 1;
+            }
+            for (int e = 0; e < NPC; ++e) {
+                double d = pv[e] - p0[e];
+                if (isnan(d) || d != 0) c->sp_pc[(int64_t)e * W + j] = 1;
+            }
+        }
+    }
+    free(in);
+    free(pts);
+    ws_free(&w);
+    return MH_OK;
+}
+
+int orc_get_callback_sparsity(const orc_ctx* c, uint8_t* pattern, int64_t len) {
+    int64_t W = 1 + c->NP, nd = (int64_t)(c->NQ + c->NZ) * W, need = nd + (int64_t)c->NPC * W;
+    if (!pattern || len < need) return fail(MH_ERR_INVALID, "pattern needs %lld bytes", (long long)need);
+    for (int64_t i = 0; i < need; ++i)
+        pattern[i] = i < nd ? (c->sp ? c->sp[i] : 1) : (c->sp_pc ? c->sp_pc[i - nd] : 1);
+    return MH_OK;
 }
 
 int orc_eval_g(orc_ctx* c, const double* x, double* g) {

@@ -68,6 +68,8 @@ int orc_muscle_length_speed(orc_ctx* ctx, int im, const double* q,
         const double* u, double* out);
 /* Evaluate a model function (joint axis / moving point) and derivatives. */
 int orc_eval_function(orc_ctx* ctx, int ifn, double q, double* out3);
+/* The callback sparsity behind the structure (mh_get_callback_sparsity). */
+int orc_get_callback_sparsity(const orc_ctx* ctx, uint8_t* pattern, int64_t len);
 
 #ifdef __cplusplus
 }

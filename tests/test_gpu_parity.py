@@ -23,6 +23,28 @@ from mocohip.solver import HipNLP, OracleNLP
 pytestmark = pytest.mark.gpu
 EPS = np.finfo(float).eps
 
+def _sparse(st, mode="random"):
+    """optim_sparsity_detection."""
+    st.solver.optim_sparsity_detection = mode
+    return st
+
+
+def _physiological_guess(st):
+    """initial-guess detection at the bounds midpoint with activations 0.5
+    and normalized tendon forces 0.1 (a regular point of the DGF model)."""
+    rep = st.problem.create_rep()
+    ref = OracleNLP(rep, st.solver.options())
+    x = ref.initial_guess_from_bounds()
+    S = x[2:2 + ref.NS * ref.G].reshape(ref.G, ref.NS)
+    for i, n in enumerate(rep.state_names):
+        if n.endswith("/activation"):
+            S[:, i] = 0.5
+        elif n.endswith("/normalized_tendon_force"):
+            S[:, i] = 0.1
+    st.solver.sparsity_guess = x
+    return _sparse(st, "initial-guess")
+
+
 CASES = {
     "sliding_mass": lambda: configs.sliding_mass(50),
     "double_pendulum_hs": lambda: configs.double_pendulum(100),
@@ -53,6 +75,19 @@ CASES = {
     "gait_rigid_pathcon": lambda: configs.gait10dof18musc(8, control_bounds=True),
     "gait_rigid_pathcon_implicit_central": lambda: configs.gait10dof18musc(
         6, fd_scheme="central", dynamics="implicit", control_bounds=True),
+    # detected sparsity: rows keep only the callback dependencies found by
+    # perturbation on the device (structure must equal the oracle's)
+    "double_pendulum_sparse_random": lambda: _sparse(configs.double_pendulum(30)),
+    "gait_rigid_sparse_random": lambda: _sparse(configs.gait10dof18musc(8)),
+    # (random iterates and the bounds midpoint put the compliant tendon where
+    # the DAE is inf/NaN or ~1e250, where detection is rounding-dependent:
+    # a physiological guess here)
+    "gait_compliant_sparse_central": lambda: _physiological_guess(configs.gait10dof18musc(
+        6, tendon_compliance=True, fd_scheme="central")),
+    "gait_implicit_pathcon_sparse": lambda: _sparse(configs.gait10dof18musc(
+        6, dynamics="implicit", control_bounds=True)),
+    "pendulum_bound_sparse_guess_trap": lambda: _sparse(configs.pendulum_control_bound(
+        12, "both", "trapezoidal"), "initial-guess"),
 }
 
 
@@ -170,6 +205,13 @@ def _pair(name, backend="auto", tasks=None, env=None):
             if v is not None:
                 os.environ[k] = v
     name_ = gpu.backend()[0]
+    if st.solver.optim_sparsity_detection != "none":
+        # detection decides weak (rounding-level) couplings by whether a
+        # 1e-5 perturbation changes an output's last bits, which differs
+        # between two libm/FMA implementations: the oracle is built from the
+        # pattern the device detected (test_sparsity_detection_agrees checks
+        # the two detections differ only on such couplings)
+        opts = _given(st, gpu.callback_sparsity())
     if backend == "generic":
         assert name_.startswith("generic"), name_
     elif backend == "lane":
@@ -177,6 +219,45 @@ def _pair(name, backend="auto", tasks=None, env=None):
             pytest.skip(f"{name}: no generated back end for this model / dynamics mode")
         assert name_.startswith("generated-lane:"), name_
     return gpu, OracleNLP(rep, opts, threads=8), st
+
+
+_KEEP = []   # solvers owning the pattern buffers mh_options points at
+
+
+def _given(st, pattern):
+    import copy
+    s2 = copy.copy(st.solver)
+    s2.optim_sparsity_detection, s2.sparsity_guess, s2.sparsity_pattern = "given", None, pattern
+    _KEEP.append(s2)
+    return s2.options()
+
+
+_M64 = (1 << 64) - 1
+
+
+def _splitmix_uniform(n, state):
+    """include/mocohip.h sparsity_detection RANDOM stream (splitmix64)."""
+    out = np.empty(n)
+    for i in range(n):
+        state = (state + 0x9e3779b97f4a7c15) & _M64
+        z = state
+        z = ((z ^ (z >> 30)) * 0xbf58476d1ce4e5b9) & _M64
+        z = ((z ^ (z >> 27)) * 0x94d049bb133111eb) & _M64
+        z ^= z >> 31
+        out[i] = (z >> 11) * (2.0 / 9007199254740992.0) - 1.0
+    return out, state
+
+
+def _detection_points(nlp, solver):
+    if solver.optim_sparsity_detection == "random":
+        pts, state = [], 0
+        for _ in range(solver.optim_sparsity_detection_random_count):
+            r, state = _splitmix_uniform(nlp.n, state)
+            pts.append(nlp.random_iterate(r))
+        return pts
+    if solver.sparsity_guess is not None:
+        return [np.asarray(solver.sparsity_guess, float)]
+    return [nlp.initial_guess_from_bounds()]
 
 
 def _points(nlp, x):
@@ -297,7 +378,8 @@ def test_objective_and_gradient(name):
 
 @pytest.mark.parametrize("name", ["double_pendulum_hs", "gait_rigid_forward", "double_pendulum_implicit_hs",
                                   "gait_rigid_implicit", "gait_rigid_pathcon",
-                                  "pendulum_bound_both_implicit"])
+                                  "pendulum_bound_both_implicit", "gait_rigid_sparse_random",
+                                  "gait_implicit_pathcon_sparse"])
 def test_shards_reassemble_bit_exact(name):
     """Mesh-interval shards (the multi-GPU partition) concatenate to exactly
     the unsharded g and Jacobian values."""
@@ -381,7 +463,8 @@ def test_pruned_tasks_bit_identical(name):
                                   "gait_compliant_central", "gait_torque_driven",
                                   "double_pendulum_implicit_hs", "double_pendulum_implicit_trap",
                                   "gait_rigid_implicit", "gait_rigid_pathcon",
-                                  "pendulum_bound_equality_trap", "pendulum_bound_both_implicit"])
+                                  "pendulum_bound_equality_trap", "pendulum_bound_both_implicit",
+                                  "gait_rigid_sparse_random", "gait_implicit_pathcon_sparse"])
 @pytest.mark.parametrize("variant", [{"MOCOHIP_INTERVAL": "0"},
                                      {"MOCOHIP_INTERVAL": "0", "MOCOHIP_ASM": "gs"},
                                      {"MOCOHIP_INTERVAL": "0", "MOCOHIP_QUOT": "1"},
@@ -407,3 +490,42 @@ def test_work_accounting():
     w, wl = gpu.work(), lane.work()
     assert w[3] == wl[3] == gpu.G * (gpu.NS + gpu.NC + 3)
     assert 0 < w[0] < wl[0] and w[2] > 0 and wl[2] == 0
+
+
+SPARSE = [n for n in CASES if "sparse" in n]
+
+
+@pytest.mark.parametrize("name", SPARSE)
+def test_sparsity_detection_agrees(name):
+    """The device detection (mh_create) and the oracle's agree on every
+    coupling except rounding-level ones: where they differ, the oracle's
+    output change under the 1e-5 perturbation is within 64 eps of the DAE's
+    magnitude (or non-finite) at every detection iterate, i.e. the coupling
+    is numerical noise in both.  The structures built from one pattern are
+    bit-identical (test_structure_bounds_guess_bit_exact)."""
+    st = CASES[name]()
+    rep = st.problem.create_rep()
+    gpu = HipNLP(rep, st.solver.options())
+    ref = OracleNLP(rep, st.solver.options())
+    a, b = gpu.callback_sparsity(), ref.callback_sparsity()
+    assert a.shape == b.shape
+    W = 1 + gpu.NS + gpu.NC + gpu.NDV
+    NO = gpu.NS - gpu.NQ
+    diff = np.argwhere((a != b).reshape(-1, W))
+    assert len(diff) <= 0.2 * max(b.sum(), 1), (len(diff), b.sum())
+    for x in _detection_points(ref, st.solver):
+        P = _points(ref, x)[0]
+        rows = [P] + [P + np.eye(len(P))[j] * 1e-5 for j in range(len(P))]
+        # the detection perturbs exactly x + 1e-5
+        for j in range(len(P)):
+            rows[1 + j][j] = P[j] + 1e-5
+        Y = ref.eval_dae(np.array(rows))
+        # rounding level of the DAE at this point: its terms are as large as
+        # its largest output (e.g. M w with |w| up to 1000; a muscle's force
+        # couple cancels to this level on coordinates it does not cross)
+        scale = max(np.abs(Y[0][np.isfinite(Y[0])]).max(initial=0.0), 1.0)
+        for o, j in diff:
+            assert o < NO, "path-equation sparsity must agree exactly"
+            d = Y[1 + j, o] - Y[0, o]
+            ok = (not np.isfinite(d)) or abs(d) <= 64 * np.finfo(float).eps * scale
+            assert ok, (o, j, d, Y[0, o], scale)

@@ -532,3 +532,91 @@ def test_gait_path_constraints_layout():
     rpi, rpi0 = (nlp.m - npc) // 4, base.m // 4
     for i in range(4):
         assert np.array_equal(g[i * rpi + npc:(i + 1) * rpi], g0[i * rpi0:(i + 1) * rpi0])
+
+
+# --------------------------------------------------------------------------
+# Sparsity detection: optim_sparsity_detection.
+# --------------------------------------------------------------------------
+SPARSE_CASES = {
+    "double_pendulum": lambda: configs.double_pendulum(3),
+    "double_pendulum_trap_implicit": lambda: configs.double_pendulum(3, "trapezoidal", dynamics="implicit"),
+    "gait_rigid": lambda: configs.gait10dof18musc(2),
+    "gait_compliant": lambda: configs.gait10dof18musc(2, tendon_compliance=True),
+    "gait_implicit_pathcon": lambda: configs.gait10dof18musc(2, dynamics="implicit", control_bounds=True),
+    "pendulum_bound": lambda: configs.pendulum_control_bound(3, "both"),
+}
+
+
+def _grid0_inputs(nlp, x):
+    G = nlp.G
+    st = x[2:2 + nlp.NS]
+    ct = x[2 + nlp.NS * G:2 + nlp.NS * G + nlp.NC]
+    dv = x[2 + (nlp.NS + nlp.NC) * G:2 + (nlp.NS + nlp.NC) * G + nlp.NDV]
+    return np.concatenate([[x[0]], st, ct, dv])
+
+
+def _replicated_iterate(nlp, seed=6):
+    """A random iterate whose grid points all hold grid point 0's values, so
+    that detection at grid point 0 sees every grid point's dependencies."""
+    x = nlp.random_iterate(np.random.default_rng(seed).uniform(-1, 1, nlp.n))
+    G = nlp.G
+    off = 2
+    for width in (nlp.NS, nlp.NC, nlp.NDV):
+        if width:
+            blk = x[off:off + width * G].reshape(G, width)
+            blk[:] = blk[0]
+        off += width * G
+    return x
+
+
+@pytest.mark.parametrize("name", list(SPARSE_CASES))
+def test_sparsity_detection_initial_guess(name):
+    """Detected rows are a subset of the block-dense rows with the same
+    finite-difference values, and every dropped entry is exactly zero at the
+    detection iterate (CasOCFunction.cpp:25-71)."""
+    st = SPARSE_CASES[name]()
+    st.solver.optim_finite_difference_scheme = "forward"
+    rep = st.problem.create_rep()
+    dense = OracleNLP(rep, st.solver.options())
+    x = _replicated_iterate(dense)
+    st.solver.optim_sparsity_detection = "initial-guess"
+    st.solver.sparsity_guess = x
+    sp = OracleNLP(rep, st.solver.options())
+    assert (sp.n, sp.m) == (dense.n, dense.m) and sp.nnz <= dense.nnz
+    ir, jc = dense.jac_structure()
+    irs, jcs = sp.jac_structure()
+    where = {(int(r), int(c)): i for i, (r, c) in enumerate(zip(ir, jc))}
+    idx = np.array([where[(int(r), int(c))] for r, c in zip(irs, jcs)])
+    assert np.all(np.diff(idx) > 0)          # same row-major order
+    J, Js = dense.eval_jac_g(x), sp.eval_jac_g(x)
+    assert np.array_equal(J[idx], Js, equal_nan=True)
+    dropped = np.setdiff1d(np.arange(dense.nnz), idx)
+    # a dropped entry is zero up to the rounding noise a 1e-8 difference
+    # quotient picks up (eps |y| / h_fd, y the DAE outputs) where the 1e-5
+    # detection perturbation left the output bit-identical
+    P = _grid0_inputs(dense, x)
+    F = max(np.abs(dense.eval_dae(P[None, :])).max(), 1.0)
+    noise = 64 * np.finfo(float).eps * F / st.solver.fd_step * max(x[1] - x[0], 1.0)
+    assert np.all(np.abs(np.nan_to_num(J[dropped])) <= noise)
+    assert np.mean(J[dropped] == 0) > 0.99
+    assert np.array_equal(sp.eval_g(x), dense.eval_g(x), equal_nan=True)
+    xl, xu, gl, gu = sp.bounds()
+    assert all(np.array_equal(a, b) for a, b in zip((xl, xu, gl, gu), dense.bounds()))
+
+
+def test_sparsity_detection_random_is_deterministic_and_smaller():
+    """"random": 3 iterates from a fixed seed (CasOCSolver.cpp:76-86), so the
+    pattern is the same every time; the gait model's tree and muscle paths
+    leave most of each block empty."""
+    st = configs.gait10dof18musc(3)
+    st.solver.optim_sparsity_detection = "random"
+    rep = st.problem.create_rep()
+    a, b = OracleNLP(rep, st.solver.options()), OracleNLP(rep, st.solver.options())
+    assert np.array_equal(a.jac_structure()[0], b.jac_structure()[0])
+    assert np.array_equal(a.jac_structure()[1], b.jac_structure()[1])
+    st.solver.optim_sparsity_detection = "none"
+    dense = OracleNLP(rep, st.solver.options())
+    assert a.nnz < dense.nnz / 2
+    with pytest.raises(ValueError):
+        st.solver.optim_sparsity_detection = "bogus"
+        st.solver.options()
