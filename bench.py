@@ -163,6 +163,39 @@ def main():
     inst_elapsed = timed(args.steps, True)
     nlp.set_timing(False)
 
+    # secondary: the same workload with optim_sparsity_detection "random"
+    # (MocoInverse's setting, MocoInverse.cpp:111): detected callback
+    # couplings only, same iterate, separate calls
+    sparse = None
+    if not args.single_mode and not mesh:
+        import copy
+        s2 = copy.copy(st.solver)
+        s2.optim_sparsity_detection = "random"
+        nls = HipNLP(rep, s2.options())
+        vs = torch.empty(nls.nnz, dtype=torch.float64, device=dev)
+        gs = torch.empty(nls.m, dtype=torch.float64, device=dev)
+
+        def sstep():
+            nls.eval_g_device(xd.data_ptr(), gs.data_ptr())
+            nls.eval_jac_g_device(xd.data_ptr(), vs.data_ptr())
+        for _ in range(args.warmup):
+            sstep()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            sstep()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        sparse = {"value": round(args.steps * world / el, 3), "unit": "calls/s", "nnz_jac": nls.nnz,
+                  "mode": "separate", "note": "optim_sparsity_detection=random (3 iterates)"}
+        nls.close()
+
     ms_per_step = 1e3 * elapsed / args.steps
     value = (args.steps if mesh else args.steps * world) / elapsed
     batch = None
@@ -236,6 +269,8 @@ def main():
             line[f"value_{other}"] = round((args.steps if mesh else args.steps * world) / other_elapsed, 3)
         if batch:
             line["batch"] = batch
+        if sparse:
+            line["sparsity_random"] = sparse
         if cpu and cpu.get("value"):
             line["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 2)
         print(json.dumps(line), flush=True)
