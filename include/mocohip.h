@@ -130,7 +130,13 @@ typedef struct mh_muscle {
     int32_t ignore_activation_dynamics;
     int32_t ignore_tendon_compliance;
     int32_t ignore_passive_fiber_force;
-    int32_t tendon_dynamics_implicit;   /* must be 0 (explicit) for now   */
+    int32_t tendon_dynamics_implicit;   /* tendon_compliance_dynamics_mode
+                                         * "implicit" (compliant only):
+                                         * the normalized tendon force
+                                         * derivative is a derivative
+                                         * variable and the equilibrium
+                                         * FT - FM cos(alpha) an auxiliary
+                                         * residual row per grid point   */
     double max_isometric_force;
     double optimal_fiber_length;
     double tendon_slack_length;
@@ -319,6 +325,11 @@ typedef struct mh_options {
     /* GIVEN: the callback sparsity itself, as mh_get_callback_sparsity
      * returns it (e.g. detected once and reused by every shard / replica). */
     const uint8_t* sparsity_pattern;
+    /* implicit_auxiliary_derivative_bounds (MocoDirectCollocationSolver.cpp:
+     * 41): bounds on the derivative variables of implicit auxiliary dynamics
+     * (DGF normalized tendon force with tendon_dynamics_implicit); {0, 0} =
+     * the reference default [-1000, 1000]. */
+    double implicit_aux_bounds[2];
 } mh_options;
 
 enum mh_sparsity {

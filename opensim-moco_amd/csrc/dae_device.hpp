@@ -22,6 +22,9 @@ namespace mh {
 struct DevModel {
     int nq, nb, nmus, nact, next, ns, nz, nc, no, np;
     int implicit;   // MH_DYNAMICS_IMPLICIT: inputs carry udot after the controls
+    int nacc;       // acceleration inputs after the controls (implicit: nq)
+    const int* mus_ider;  // muscle -> implicit tendon-force derivative input
+                          // (index after the controls), -1 = explicit
     double gravity[3];
     double tau_act, tau_deact;
     const mh_body* bodies;
@@ -222,9 +225,13 @@ __device__ __forceinline__ double dgf_fv_inv(double fv) {
 }
 
 // Muscle tendon force and auxiliary derivatives.
+// implicit_tendon: tendon_compliance_dynamics_mode "implicit" with the
+// normalized tendon force derivative dft as input; resid = the equilibrium
+// residual FT - FM cos(alpha) (DeGrooteFregly2016Muscle.cpp:826-848).
 __device__ __forceinline__ void dgf_eval(const DevModel& M, int im, double LMT, double VMT,
         double act, double exc, bool has_act, double ftn, bool compliant, double& T,
-        double& adot, double& ftdot) {
+        double& adot, double& ftdot, bool implicit_tendon = false, double dft = 0.0,
+        double* resid = nullptr) {
     const mh_muscle& mu = M.mus[im];
     const double* dv = M.mus_derived + (long)im * MUS_DERIVED;
     const double fiberWidth = dv[0], sqW = dv[1], vmax = dv[2], kT = dv[3];
@@ -244,7 +251,7 @@ __device__ __forceinline__ void dgf_eval(const DevModel& M, int im, double LMT, 
     }
     double fAL = dgf_fal(mu.active_force_width_scale, nfl);
     double nfv, fV, ntv;
-    if (compliant) {
+    if (compliant && !implicit_tendon) {
         double nff = ftn / cosPenn;
         fV = (nff - fPE) / (act * fAL);
         nfv = dgf_fv_inv(fV);
@@ -253,7 +260,9 @@ __device__ __forceinline__ void dgf_eval(const DevModel& M, int im, double LMT, 
         double tendonVelocity = VMT - fvat;
         ntv = tendonVelocity / lts;
     } else {
-        ntv = 0.0;
+        // rigid, or implicit: tendon velocity from the force derivative
+        // (calcTendonForceLengthInverseCurveDerivative, .h:471-476)
+        ntv = compliant ? dft / (DGF_c1 * kT * exp(kT * (normTendonLength - DGF_c2))) : 0.0;
         double tendonVelocity = lts * ntv;
         double fvat = VMT - tendonVelocity;
         double fiberVelocity = fvat * cosPenn;
@@ -266,6 +275,7 @@ __device__ __forceinline__ void dgf_eval(const DevModel& M, int im, double LMT, 
     double nonCon = Fmax * mu.fiber_damping * nfv;
     double total = activeF + conPass + nonCon;
     T = compliant ? Fmax * ftn : total * cosPenn;
+    if (implicit_tendon) *resid = T - total * cosPenn;
     if (has_act) {
         double tcf = 0.5 + 1.5 * act;
         double tempAct = 1.0 / (M.tau_act * tcf);
@@ -274,7 +284,8 @@ __device__ __forceinline__ void dgf_eval(const DevModel& M, int im, double LMT, 
         double timeConst = tempAct * (f + 0.5) + tempDeact * (-f + 0.5);
         adot = timeConst * (exc - act);
     }
-    if (compliant) ftdot = ntv * (DGF_c1 * kT * exp(kT * (normTendonLength - DGF_c2)));
+    if (compliant)
+        ftdot = implicit_tendon ? dft : ntv * (DGF_c1 * kT * exp(kT * (normTendonLength - DGF_c2)));
     (void)fiberWidth;
 }
 
@@ -490,10 +501,14 @@ __device__ void dae_eval(const DevModel& M, Work<MB, MQ, MP>& w, double time, co
         const int sa = M.mus_act_state[im], sf = M.mus_ftn_state[im];
         const double act = sa >= 0 ? x[sa] : exc;
         const double ftn = sf >= 0 ? x[sf] : 0.0;
-        double T, adot = 0, ftdot = 0;
-        dgf_eval(M, im, L, S, act, exc, sa >= 0, ftn, sf >= 0, T, adot, ftdot);
+        double T, adot = 0, ftdot = 0, resid = 0;
+        const int id = M.mus_ider[im];
+        dgf_eval(M, im, L, S, act, exc, sa >= 0, ftn, sf >= 0, T, adot, ftdot, id >= 0,
+                id >= 0 ? c[M.nc + id] : 0.0, &resid);
         if (sa >= 0) zdot[sa - 2 * NQ] = adot;
         if (sf >= 0) zdot[sf - 2 * NQ] = ftdot;
+        // auxiliary residual outputs after zdot (CasOCFunction.cpp:208-230)
+        if (id >= 0) out[NQ + M.nz + (id - M.nacc)] = resid;
         for (int k = 1; k < np; ++k) {
             double d0 = P[k][0] - P[k - 1][0], d1 = P[k][1] - P[k - 1][1], d2 = P[k][2] - P[k - 1][2];
             double l = sqrt(d0 * d0 + d1 * d1 + d2 * d2);

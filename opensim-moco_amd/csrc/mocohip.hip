@@ -130,7 +130,8 @@ struct Layout {
     int G;                   // grid points (full problem)
     int k0;                  // first grid point of this shard
     int nk;                  // grid points in this shard
-    int NDV;                 // derivative variables per grid point (implicit: NQ)
+    int NDV;                 // derivative variables per grid point: accelerations, aux derivatives
+    int NACC;                // acceleration variables per grid point (implicit multibody: NQ)
 };
 
 // Per grid point the evaluation lanes are laid out as
@@ -527,7 +528,11 @@ struct Interval {
     int ib;          // first interval of shard
     int rpi;         // rows per interval
     int nnz_int;     // nonzeros per interval
-    int nres;        // multibody residual rows per grid point (implicit: NQ)
+    int nres;        // residual rows per grid point: multibody (implicit: NQ), then auxiliary
+    int nacc;        // multibody residual rows per grid point
+    int oaux;        // callback output of the first auxiliary residual (NQ + NZ)
+    // callback output behind residual row r of a grid point
+    __device__ __forceinline__ int rout(int r) const { return r < nacc ? r : oaux + (r - nacc); }
     int N;           // mesh intervals of the whole problem
     int nnz_tail;    // nonzeros of the tail rows
     int ntail;       // tail rows: final mesh point's path rows + final residuals
@@ -655,7 +660,7 @@ template <class YV>
 __device__ __forceinline__ double xdot_at(const Layout& L, const Lanes& Ln,
         const double* __restrict__ x, const YV& Y, int k, int s) {
     if (s < L.NQ) return Y.xs(k, L.NQ + s);
-    if (L.NDV && s < 2 * L.NQ) return Y.xd(k, s - L.NQ);   // implicit: udot = w
+    if (L.NACC && s < 2 * L.NQ) return Y.xd(k, s - L.NQ);   // implicit: udot = w
     return Y.row(k, s - L.NQ)[Ln.base];
 }
 
@@ -671,11 +676,11 @@ __device__ __forceinline__ double defect_row(const Layout& L, const Interval& I,
     if (r >= I.rpi) {   // tail: final mesh point's path rows, then its residuals
         const int rt = r - I.rpi, kl = k_first + npres;
         if (rt < npc) return path_value(I.P, rt, Y.t(kl), Y.xc(kl, I.P.eq[rt].index));
-        return Y.row(kl, rt - npc)[Ln.base];
+        return Y.row(kl, I.rout(rt - npc))[Ln.base];
     }
     if (r < npc) return path_value(I.P, r, Y.t(k_first), Y.xc(k_first, I.P.eq[r].index));
     r -= npc;
-    if (r < npres * I.nres) return Y.row(k_first + r / I.nres, r % I.nres)[Ln.base];
+    if (r < npres * I.nres) return Y.row(k_first + r / I.nres, I.rout(r % I.nres))[Ln.base];
     r -= npres * I.nres;
     if (I.scheme == MH_HERMITE_SIMPSON) {
         const int ki = 2 * i, km = ki + 1, kp = ki + 2;
@@ -720,7 +725,7 @@ template <class YV>
 __device__ __forceinline__ double dxdot(const Layout& L, const Lanes& Ln, const YV& Y, int k, int s,
         int dir) {
     if (s < L.NQ) return dir == 2 + L.NQ + s ? 1.0 : 0.0;
-    if (L.NDV && s < 2 * L.NQ) return dir == 2 + L.NS + L.NC + (s - L.NQ) ? 1.0 : 0.0;
+    if (L.NACC && s < 2 * L.NQ) return dir == 2 + L.NS + L.NC + (s - L.NQ) ? 1.0 : 0.0;
     return dout(Ln, Y, k, s - L.NQ, dir);
 }
 
@@ -1396,7 +1401,10 @@ struct mh_ctx {
     int NQ = 0, NZ = 0, NS = 0, NC = 0, NO = 0, NI = 0;
     int scheme = 0, N = 0, G = 0, interp = 0, rpi = 0, nnz_int = 0;
     int NDV = 0, nnz_tail = 0;     // implicit: accelerations per point, tail nonzeros
-    int npc = 0, ntail = 0;        // path equations per mesh point; tail rows (npc + NDV)
+    int npc = 0, ntail = 0;        // path equations per mesh point; tail rows (npc + residuals)
+    int NACC = 0, NAR = 0;         // accelerations (implicit multibody), implicit aux residuals per point
+    std::vector<int> mus_ider;     // muscle -> aux derivative index after the controls (-1)
+    double aux_lo = -1000.0, aux_hi = 1000.0;
     int npe = 0;                   // path-constraint template entries per mesh point
     std::vector<uint8_t> sp, sp_pc;  // detected sparsity [output][time, inputs] (empty: dense)
     std::vector<mh_path_equation> pc;
@@ -1491,7 +1499,7 @@ static int64_t col_deriv(const mh_ctx* c, int64_t k, int j) {
 // evaluated by the last interval.
 static void build_template(mh_ctx* c) {
     const int NS = c->NS, NQ = c->NQ, NC = c->NC, NDV = c->NDV;
-    const bool implicit = NDV > 0;
+    const bool implicit = c->NACC > 0;
     struct Col { int pt; int dir; };  // dir: 0/1 time, 2+input
     auto key = [&](const Col& col) -> int64_t {
         // column index for interval 0
@@ -1526,9 +1534,12 @@ static void build_template(mh_ctx* c) {
             if (sp.empty() || sp[(size_t)o * W + 1 + j] || j == s_ident) v.push_back({pt, 2 + j});
     };
     auto time_dep = [&](const std::vector<uint8_t>& sp, int o) { return sp.empty() || sp[(size_t)o * W] != 0; };
-    // multibody residual rows of point pt: the point's inputs + time
+    // residual rows of point pt (multibody residuals in implicit mode, then
+    // the implicit auxiliary residuals): the point's inputs + time; the
+    // entry's s is the callback output
     auto residual_rows = [&](int& row, int pt) {
-        for (int o = 0; o < (implicit ? NQ : 0); ++o) {
+        for (int r = 0; r < c->NACC + c->NAR; ++r) {
+            const int o = r < c->NACC ? r : NQ + c->NZ + (r - c->NACC);
             std::vector<Col> v;
             if (time_dep(c->sp, o)) { v.push_back({pt, 0}); v.push_back({pt, 1}); }
             point_dep(c->sp, o, pt, -1, v);
@@ -1651,8 +1662,6 @@ static int validate_and_layout(mh_ctx* c, const mh_problem* p, const mh_options*
     mus_control.assign(M.nmuscles, -1);
     for (int im = 0; im < M.nmuscles; ++im) {
         const mh_muscle& mu = M.muscles[im];
-        if (mu.tendon_dynamics_implicit && !mu.ignore_tendon_compliance)
-            return set_err(MH_ERR_UNSUPPORTED, "implicit tendon compliance dynamics not supported");
         if (mu.point_begin < 0 || mu.point_begin + mu.point_count > M.npoints)
             return set_err(MH_ERR_INVALID, "muscle %d: bad path point range", im);
         act_state[im] = mu.ignore_activation_dynamics ? -1 : z++;
@@ -1669,7 +1678,20 @@ static int validate_and_layout(mh_ctx* c, const mh_problem* p, const mh_options*
     c->NO = c->NQ + c->NZ;
     if (o->multibody_dynamics_mode != MH_DYNAMICS_EXPLICIT && o->multibody_dynamics_mode != MH_DYNAMICS_IMPLICIT)
         return set_err(MH_ERR_INVALID, "unknown multibody dynamics mode %d", o->multibody_dynamics_mode);
-    c->NDV = o->multibody_dynamics_mode == MH_DYNAMICS_IMPLICIT ? c->NQ : 0;
+    // derivative variables: accelerations, then the implicit auxiliary
+    // derivatives in component order (MocoCasOCProblem.cpp:85-94)
+    c->NACC = o->multibody_dynamics_mode == MH_DYNAMICS_IMPLICIT ? c->NQ : 0;
+    c->NAR = 0;
+    c->mus_ider.assign(M.nmuscles, -1);
+    for (int im = 0; im < M.nmuscles; ++im)
+        if (M.muscles[im].tendon_dynamics_implicit && !M.muscles[im].ignore_tendon_compliance)
+            c->mus_ider[im] = c->NACC + c->NAR++;
+    c->NDV = c->NACC + c->NAR;
+    c->NO = c->NQ + c->NZ + c->NAR;
+    if (o->implicit_aux_bounds[0] != 0.0 || o->implicit_aux_bounds[1] != 0.0) {
+        c->aux_lo = o->implicit_aux_bounds[0];
+        c->aux_hi = o->implicit_aux_bounds[1];
+    }
     if (o->implicit_accel_bounds[0] != 0.0 || o->implicit_accel_bounds[1] != 0.0) {
         c->acc_lo = o->implicit_accel_bounds[0];
         c->acc_hi = o->implicit_accel_bounds[1];
@@ -1902,6 +1924,7 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
                  o_as = A.put(act_state.data(), act_state.size()),
                  o_fs = A.put(ftn_state.data(), ftn_state.size()),
                  o_mc = A.put(mus_control.data(), mus_control.size()),
+                 o_mi = A.put(c->mus_ider.data(), c->mus_ider.size()),
                  o_md = A.put(mder.data(), mder.size()),
                  o_goals = A.put(p->goals, p->ngoals), o_gidx = A.put(p->goal_index, p->nterms),
                  o_gcol = A.put(p->goal_column, p->nterms), o_gw = A.put(p->goal_weight, p->nterms),
@@ -1954,7 +1977,9 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     DevModel& D = c->M;
     D.nq = M.nq; D.nb = M.nbodies; D.nmus = M.nmuscles; D.nact = M.nactuators; D.next = M.nexternal;
     D.ns = c->NS; D.nz = c->NZ; D.nc = c->NC; D.no = c->NO; D.np = c->NI;
-    D.implicit = c->NDV > 0 ? 1 : 0;
+    D.implicit = c->NACC > 0 ? 1 : 0;
+    D.nacc = c->NACC;
+    D.mus_ider = (const int*)(b + o_mi);
     for (int i = 0; i < 3; ++i) D.gravity[i] = M.gravity[i];
     D.tau_act = tau_act; D.tau_deact = tau_deact;
     D.bodies = (const mh_body*)(b + o_bodies); D.axes = (const mh_axis*)(b + o_axes);
@@ -2093,8 +2118,14 @@ extern "C" int mh_get_bounds(const mh_ctx* c, double* xl, double* xu, double* gl
     for (int s = 0; s < c->NS; ++s) fill(c->sinfo[s], [&](int k) { return col_state(c, k, s); });
     for (int j = 0; j < c->NC; ++j) fill(c->cinfo[j], [&](int k) { return col_control(c, k, j); });
     // implicit: acceleration bounds at every grid point (CasOCTranscription.cpp:222-226)
-    for (int j = 0; j < c->NDV; ++j)
-        for (int k = 0; k < c->G; ++k) { xl[col_deriv(c, k, j)] = c->acc_lo; xu[col_deriv(c, k, j)] = c->acc_hi; }
+    // implicit auxiliary derivatives after them (CasOCTranscription.cpp:228-232)
+    for (int j = 0; j < c->NDV; ++j) {
+        const bool aux = j >= c->NACC;
+        for (int k = 0; k < c->G; ++k) {
+            xl[col_deriv(c, k, j)] = aux ? c->aux_lo : c->acc_lo;
+            xu[col_deriv(c, k, j)] = aux ? c->aux_hi : c->acc_hi;
+        }
+    }
     if (gl && gu) {
         for (int64_t r = 0; r < c->m; ++r) { gl[r] = 0.0; gu[r] = 0.0; }
         // path rows: the equation's bounds at every mesh point
@@ -2182,7 +2213,7 @@ struct Backend {
 
 template <class D>
 static void be_eval_lane(mh_ctx* c, const double* x, int mode, double* Y) {
-    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, c->k0, c->nk, c->NDV};
+    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, c->k0, c->nk, c->NDV, c->NACC};
     const Lanes& ln = mode ? c->lanes_jac : c->lanes_g;
     const long lanes = (long)c->nk * ln.stride;
     hipLaunchKernelGGL(k_eval<D>, dim3((unsigned)((lanes + 63) / 64)), dim3(64), 0, c->stream, c->M, L,
@@ -2250,28 +2281,29 @@ static void be_interval(mh_ctx* c, const double* x, int mode, double* g, double*
     if (lds > 65536)
         (void)hipFuncSetAttribute((const void*)k_interval<D>, hipFuncAttributeMaxDynamicSharedMemorySize,
                 (int)lds);
-    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, c->k0, c->nk, c->NDV};
-    Interval I{c->scheme, c->interp, c->ib, c->rpi, c->nnz_int, c->NDV, c->N, c->nnz_tail, c->ntail, c->npe, c->P};
+    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, c->k0, c->nk, c->NDV, c->NACC};
+    Interval I{c->scheme, c->interp, c->ib, c->rpi, c->nnz_int, c->NACC + c->NAR, c->NACC, c->NQ + c->NZ,
+               c->N, c->nnz_tail, c->ntail, c->npe, c->P};
     const unsigned threads = v ? 1024u : 256u;
     hipLaunchKernelGGL(k_interval<D>, dim3((unsigned)(c->ie - c->ib)), dim3(threads), lds, c->stream, c->M,
             S, ln, ts.dev, L, I, c->d_tpl, c->d_tplp, tables, c->d_T, c->d_H, g, v);
 }
 template <class D>
 static void be_integrand(mh_ctx* c, const double* x) {
-    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, 0, c->G, c->NDV};
+    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, 0, c->G, c->NDV, c->NACC};
     hipLaunchKernelGGL(k_integrand<D>, dim3((c->G + 63) / 64), dim3(64), 0, c->stream, c->M, L,
             c->GS, x, c->d_grid, c->d_quad, c->d_C);
 }
 template <class D>
 static void be_grad(mh_ctx* c, const double* x) {
-    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, 0, c->G, c->NDV};
+    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, 0, c->G, c->NDV, c->NACC};
     const long tot = (long)c->G * (c->NI + 2);
     hipLaunchKernelGGL(k_grad<D>, dim3((unsigned)((tot + 63) / 64)), dim3(64), 0, c->stream, c->M, L,
             c->GS, c->fd, c->h, x, c->d_grid, c->d_quad, c->d_grad, c->d_tpart);
 }
 template <class D>
 static void be_probe_lane(mh_ctx* c, int np, const double* in, double* out) {
-    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, 0, 0, c->NDV};
+    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, 0, 0, c->NDV, c->NACC};
     hipLaunchKernelGGL(k_dae_probe<D>, dim3((np + 63) / 64), dim3(64), 0, c->stream, c->M, L, np, in,
             out);
 }
@@ -2333,8 +2365,9 @@ static int launch_stage(mh_ctx* c, int stage, int kind, const double* x, double*
         HIPCHK(hipGetLastError());
         return MH_OK;
     }
-    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, c->k0, c->nk, c->NDV};
-    Interval I{c->scheme, c->interp, c->ib, c->rpi, c->nnz_int, c->NDV, c->N, c->nnz_tail, c->ntail, c->npe, c->P};
+    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, c->k0, c->nk, c->NDV, c->NACC};
+    Interval I{c->scheme, c->interp, c->ib, c->rpi, c->nnz_int, c->NACC + c->NAR, c->NACC, c->NQ + c->NZ,
+               c->N, c->nnz_tail, c->ntail, c->npe, c->P};
     const Lanes& ln = kind == 0 ? c->lanes_g : c->lanes_jac;
     const double* Y = kind == 0 ? c->d_Yg : c->d_Y;
     const int nchunks = kind == 0 ? 0 : (c->nnz_int + (c->ie == c->N ? c->nnz_tail : 0) + ASM_CHUNK - 1) / ASM_CHUNK;
@@ -2508,7 +2541,7 @@ extern "C" int mh_eval_f(mh_ctx* c, const double* x, int, double* f) {
     (void)hipGetLastError();   // report only this call's launch errors
     HIPCHK(hipMemcpyAsync(c->d_x, x, sizeof(double) * c->n, hipMemcpyHostToDevice, c->stream));
     if (c->timing) HIPCHK(hipEventRecord(c->ev[0], c->stream));
-    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, 0, c->G, c->NDV};
+    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, 0, c->G, c->NDV, c->NACC};
     if (c->ngoals > 0) {
         c->be->integrand(c, c->d_x);
         HIPCHK(hipGetLastError());
@@ -2528,7 +2561,7 @@ extern "C" int mh_eval_grad_f(mh_ctx* c, const double* x, int, double* grad) {
     (void)hipGetLastError();   // report only this call's launch errors
     HIPCHK(hipMemcpyAsync(c->d_x, x, sizeof(double) * c->n, hipMemcpyHostToDevice, c->stream));
     if (c->timing) HIPCHK(hipEventRecord(c->ev[0], c->stream));
-    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, 0, c->G, c->NDV};
+    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, 0, c->G, c->NDV, c->NACC};
     HIPCHK(hipMemsetAsync(c->d_grad, 0, sizeof(double) * c->n, c->stream));
     HIPCHK(hipMemsetAsync(c->d_tpart, 0, sizeof(double) * 2 * c->G, c->stream));
     HIPCHK(hipMemsetAsync(c->d_C, 0, sizeof(double) * c->G * std::max(1, c->ngoals), c->stream));
@@ -2765,7 +2798,7 @@ static const Backend* select_backend(mh_ctx* c, const mh_problem* p) {
     const bool generic = force && std::strcmp(force, "generic") == 0;
     const bool lane = force && std::strcmp(force, "lane") == 0;
     if (!generic) {
-        const uint64_t key = backend_key(c->model_hash, c->NDV > 0);
+        const uint64_t key = backend_key(c->model_hash, c->NACC > 0);
         for (const GenEntry& e : kGeneratedModels)
             if (e.hash == key) return lane ? &e.lane : &e.tasks;
     }

@@ -141,7 +141,8 @@ class mh_options(C.Structure):
                 ("device", i32), ("multibody_dynamics_mode", i32),
                 ("implicit_accel_bounds", f64 * 2),
                 ("sparsity_detection", i32), ("sparsity_random_count", i32),
-                ("sparsity_guess", P(f64)), ("sparsity_pattern", P(C.c_uint8))]
+                ("sparsity_guess", P(f64)), ("sparsity_pattern", P(C.c_uint8)),
+                ("implicit_aux_bounds", f64 * 2)]
 
 
 MH_SPARSITY_NONE, MH_SPARSITY_RANDOM, MH_SPARSITY_INITIAL_GUESS, MH_SPARSITY_GIVEN = 0, 1, 2, 3

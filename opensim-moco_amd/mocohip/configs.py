@@ -128,13 +128,18 @@ def _load(name):
 
 
 def gait10dof18musc_model(muscles: bool = True, tendon_compliance: bool = False,
-                          reserves: float = 100.0, external_loads: bool = True) -> Model:
+                          reserves: float = 100.0, external_loads: bool = True,
+                          tendon_dynamics: str = "explicit") -> Model:
+    """tendon_dynamics: DeGrooteFregly2016Muscle tendon_compliance_dynamics_mode
+    of the compliant tendons ("implicit": the MocoInverse test setting,
+    ModOpTendonComplianceDynamicsModeDGF("implicit"), testMocoInverse.cpp:127)."""
     m = model_from_dict(_load("gait10dof18musc.json"))
     if not muscles:
         m.actuators = [a for a in m.actuators if not hasattr(a, "points")]
         m.muscles = []
     for mu in m.muscles:
         mu.ignore_tendon_compliance = not tendon_compliance
+        mu.tendon_compliance_dynamics_mode = tendon_dynamics
     if reserves:
         add_reserves(m, reserves)
     if external_loads:
@@ -153,7 +158,7 @@ def gait10dof18musc_model(muscles: bool = True, tendon_compliance: bool = False,
 def gait10dof18musc(num_mesh_intervals: int = 200, muscles: bool = True,
                     tendon_compliance: bool = False,
                     fd_scheme: str = "forward", dynamics: str = "explicit",
-                    control_bounds: bool = False) -> MocoStudy:
+                    control_bounds: bool = False, tendon_dynamics: str = "explicit") -> MocoStudy:
     """MocoTrack gait10dof18musc (config 3).  MocoTrack: states tracking goal
     (weight 1, GCVSpline reference), control effort goal (0.001), time
     [0.01, 1.3], explicit dynamics, forward FD (MocoTrack.cpp:54-132).
@@ -161,7 +166,8 @@ def gait10dof18musc(num_mesh_intervals: int = 200, muscles: bool = True,
     tibialis anterior excitations (GCVSpline lower, Constant upper bound) and
     one on the hip flexor reserve (Constant upper bound) as path constraints
     (not part of the reference MocoTrack setup)."""
-    m = gait10dof18musc_model(muscles=muscles, tendon_compliance=tendon_compliance)
+    m = gait10dof18musc_model(muscles=muscles, tendon_compliance=tendon_compliance,
+                              tendon_dynamics=tendon_dynamics)
     ref = _load("walk_gait1018_state_reference.json")
     cols = {k: np.asarray(v) for k, v in ref["columns"].items()}
     m.add_table(DataTable("state_reference", np.asarray(ref["time"]), cols, degree=5))

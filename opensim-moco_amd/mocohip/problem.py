@@ -319,6 +319,12 @@ class ProblemRep:
         self.num_states = len(self.state_names)
         self.num_controls = len(self.control_names)
         self.nq = self.compiled.nq
+        # implicit auxiliary dynamics: DGF muscles with compliant tendons in
+        # tendon_compliance_dynamics_mode "implicit" (one derivative variable
+        # and one residual row per grid point each)
+        self.num_aux_residuals = sum(
+            1 for m in model.muscles
+            if not m.ignore_tendon_compliance and m.tendon_compliance_dynamics_mode == "implicit")
 
     @staticmethod
     def _path_equations(problem: MocoProblem):

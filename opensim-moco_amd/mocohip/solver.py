@@ -51,6 +51,8 @@ class MocoHipSolver:
     # MocoDirectCollocationSolver implicit_multibody_acceleration_bounds
     # (default [-1000, 1000], MocoDirectCollocationSolver.cpp:39-40)
     implicit_multibody_acceleration_bounds: tuple = (-1000.0, 1000.0)
+    # implicit_auxiliary_derivative_bounds (MocoDirectCollocationSolver.cpp:41)
+    implicit_auxiliary_derivative_bounds: tuple = (-1000.0, 1000.0)
 
     def options(self, interval_begin: int = 0, interval_end: int = 0) -> abi.mh_options:
         if self.transcription_scheme not in _SCHEMES:
@@ -78,6 +80,9 @@ class MocoHipSolver:
         lo, hi = self.implicit_multibody_acceleration_bounds
         o.implicit_accel_bounds[0] = float(lo)
         o.implicit_accel_bounds[1] = float(hi)
+        lo, hi = self.implicit_auxiliary_derivative_bounds
+        o.implicit_aux_bounds[0] = float(lo)
+        o.implicit_aux_bounds[1] = float(hi)
         o.sparsity_detection = _SPARSITY[self.optim_sparsity_detection]
         o.sparsity_random_count = int(self.optim_sparsity_detection_random_count)
         if self.sparsity_guess is not None:
@@ -162,16 +167,37 @@ class _NLPBase:
         return ir[:self.nnz], jc[:self.nnz]
 
     @property
-    def NDV(self) -> int:
-        """Derivative variables per grid point (implicit mode: NQ)."""
+    def NACC(self) -> int:
+        """Acceleration variables per grid point (implicit mode: NQ)."""
         return self.NQ if self.opts.multibody_dynamics_mode == abi.MH_DYNAMICS_IMPLICIT else 0
+
+    @property
+    def NAR(self) -> int:
+        """Implicit auxiliary derivatives / residuals per grid point."""
+        return self.rep.num_aux_residuals
+
+    @property
+    def NDV(self) -> int:
+        """Derivative variables per grid point: accelerations, then the
+        implicit auxiliary derivatives."""
+        return self.NACC + self.NAR
+
+    @property
+    def NO(self) -> int:
+        """DAE callback outputs: udot or multibody residual, zdot, auxiliary
+        residuals."""
+        return self.NS - self.NQ + self.NAR
+
+    @property
+    def NRES(self) -> int:
+        """Residual rows per grid point (multibody, then auxiliary)."""
+        return self.NACC + self.NAR
 
     def callback_sparsity(self) -> np.ndarray:
         """The callback sparsity behind the Jacobian structure: (NQ + NZ)
         DAE outputs then the path equations, rows of [time, inputs] flags."""
         W = 1 + self.NS + self.NC + self.NDV
-        NO = self.NS - self.NQ            # NQ + NZ
-        buf = np.zeros((NO + self.NPC) * W, np.uint8)
+        buf = np.zeros((self.NO + self.NPC) * W, np.uint8)
         self._check(self._fn("get_callback_sparsity")(
             self.ctx, buf.ctypes.data_as(C.POINTER(C.c_uint8)), buf.size))
         return buf
@@ -185,15 +211,15 @@ class _NLPBase:
     def tail_rows(self) -> int:
         """Rows after the last interval's own: the final mesh point's path
         rows and the final grid point's residuals."""
-        return self.NPC + self.NDV
+        return self.NPC + self.NRES
 
     def eval_dae(self, inputs: np.ndarray) -> np.ndarray:
-        """Per-point DAE: rows [t, states, controls(, accelerations)] ->
-        [udot or multibody residual, zdot]."""
+        """Per-point DAE: rows [t, states, controls, derivatives] ->
+        [udot or multibody residual, zdot, auxiliary residuals]."""
         inputs = np.ascontiguousarray(inputs, float)
         npts = inputs.shape[0]
         assert inputs.shape[1] == 1 + self.NS + self.NC + self.NDV
-        out = np.empty((npts, self.NS - self.NQ))
+        out = np.empty((npts, self.NO))
         self._check(self._fn("eval_dae")(self.ctx, npts, abi.dptr(inputs), abi.dptr(out)))
         return out
 

@@ -244,6 +244,11 @@ struct orc_ctx {
     int implicit;           /* MH_DYNAMICS_IMPLICIT                     */
     int NDV;                /* derivative variables per grid point      */
     double acc_lo, acc_hi;  /* implicit multibody acceleration bounds   */
+    int NACC;               /* acceleration variables per point (implicit) */
+    int NAR;                /* implicit auxiliary residuals per point      */
+    int* mus_ider;          /* muscle -> its tendon-force derivative's index
+                             * in the derivative block (-1: explicit)     */
+    double aux_lo, aux_hi;  /* implicit auxiliary derivative bounds      */
     int* mus_act_state;     /* state index of activation (-1)          */
     int* mus_ftn_state;     /* state index of normalized tendon force   */
     int* mus_control;       /* control index of excitation (-1)        */
@@ -281,8 +286,14 @@ static int64_t col_control(const orc_ctx* c, int k, int j) {
 static int64_t col_deriv(const orc_ctx* c, int k, int j) {
     return 2 + (int64_t)(c->NS + c->NC) * c->G + (int64_t)k * c->NDV + j;
 }
-/* multibody residual rows per grid point (implicit mode) */
-static int nres(const orc_ctx* c) { return c->implicit ? c->NQ : 0; }
+/* DAE callback outputs: [udot or multibody residual (NQ), zdot (NZ),
+ * auxiliary residuals (NAR)] (CasOCFunction.cpp:208-230) */
+static int nout(const orc_ctx* c) { return c->NQ + c->NZ + c->NAR; }
+/* residual rows per grid point: multibody residuals (implicit mode), then
+ * auxiliary residuals (flattenConstraints, CasOCTranscription.h:290-296) */
+static int nres(const orc_ctx* c) { return c->NACC + c->NAR; }
+/* callback output behind residual row r of a grid point */
+static int res_out(const orc_ctx* c, int r) { return r < c->NACC ? r : c->NQ + c->NZ + (r - c->NACC); }
 /* the mesh point that opens interval i (and closes interval i-1) */
 static int mesh_point(const orc_ctx* c, int i) { return c->scheme == MH_HERMITE_SIMPSON ? 2 * i : i; }
 
@@ -314,8 +325,8 @@ typedef void (*row_fn)(void* ud, int64_t row, const int64_t* cols, int ncols);
  * output depends on every input of the point and on the time. */
 static int64_t residual_rows(const orc_ctx* c, int k, int64_t row, row_fn emit, void* ud,
         int64_t* cols) {
-    for (int o = 0; o < nres(c); ++o) {
-        int n = 0;
+    for (int r = 0; r < nres(c); ++r) {
+        int n = 0, o = res_out(c, r);
         if (dep(c->sp, c->NP, o, -1)) { cols[n++] = 0; cols[n++] = 1; }
         n += point_cols_dep(c, c->sp, o, k, -1, cols + n);
         emit(ud, row++, cols, n);
@@ -519,10 +530,6 @@ int orc_create(const mh_problem* p, const mh_options* o, orc_ctx** out) {
     c->tau_act = c->tau_deact = NAN;
     for (int im = 0; im < M->nmuscles; ++im) {
         const mh_muscle* mu = &c->mus[im];
-        if (mu->tendon_dynamics_implicit && !mu->ignore_tendon_compliance) {
-            orc_destroy(c);
-            return fail(MH_ERR_UNSUPPORTED, "implicit tendon dynamics not supported");
-        }
         c->mus_act_state[im] = mu->ignore_activation_dynamics ? -1 : z++;
         c->mus_ftn_state[im] = mu->ignore_tendon_compliance ? -1 : z++;
         c->mus_control[im] = -1;
@@ -541,7 +548,23 @@ int orc_create(const mh_problem* p, const mh_options* o, orc_ctx** out) {
         orc_destroy(c);
         return fail(MH_ERR_INVALID, "unknown multibody dynamics mode %d", o->multibody_dynamics_mode);
     }
-    c->NDV = c->implicit ? c->NQ : 0;
+    /* derivative variables: accelerations, then the implicit auxiliary
+     * derivatives in component order (MocoCasOCProblem.cpp:85-94,
+     * MocoCasOCProblem.h:605-620) */
+    c->NACC = c->implicit ? c->NQ : 0;
+    c->mus_ider = (int*)malloc(sizeof(int) * (size_t)(M->nmuscles + 1));
+    c->NAR = 0;
+    for (int im = 0; im < M->nmuscles; ++im) {
+        const mh_muscle* mu = &c->mus[im];
+        c->mus_ider[im] = (mu->tendon_dynamics_implicit && !mu->ignore_tendon_compliance)
+                ? c->NACC + c->NAR++ : -1;
+    }
+    c->NDV = c->NACC + c->NAR;
+    c->aux_lo = -1000.0; c->aux_hi = 1000.0;
+    if (o->implicit_aux_bounds[0] != 0.0 || o->implicit_aux_bounds[1] != 0.0) {
+        c->aux_lo = o->implicit_aux_bounds[0];
+        c->aux_hi = o->implicit_aux_bounds[1];
+    }
     c->acc_lo = -1000.0; c->acc_hi = 1000.0;
     if (o->implicit_accel_bounds[0] != 0.0 || o->implicit_accel_bounds[1] != 0.0) {
         c->acc_lo = o->implicit_accel_bounds[0];
@@ -653,7 +676,7 @@ void orc_destroy(orc_ctx* c) {
     if (!c) return;
     void* ptrs[] = {c->bodies, c->axes, c->funcs, c->kx, c->ky, c->kb, c->kc, c->kd,
             c->mus, c->pts, c->acts, c->tabs, c->brk, c->coef, c->ext, c->sinfo, c->cinfo,
-            c->goals, c->gidx, c->gcol, c->gw, c->pc, c->sp, c->sp_pc, c->mus_act_state, c->mus_ftn_state,
+            c->goals, c->gidx, c->gcol, c->gw, c->pc, c->sp, c->sp_pc, c->mus_ider, c->mus_act_state, c->mus_ftn_state,
             c->mus_control, c->coord_body, c->grid, c->quad, c->iRow, c->jCol};
     for (size_t i = 0; i < sizeof ptrs / sizeof ptrs[0]; ++i) free(ptrs[i]);
     free(c);
@@ -709,7 +732,11 @@ int orc_get_bounds(const orc_ctx* c, double* xl, double* xu, double* gl, double*
     }
     /* implicit: accelerations at every grid point (CasOCTranscription.cpp:222-226) */
     for (int j = 0; j < c->NDV; ++j)
-        for (int k = 0; k < c->G; ++k) { xl[col_deriv(c, k, j)] = c->acc_lo; xu[col_deriv(c, k, j)] = c->acc_hi; }
+        for (int k = 0; k < c->G; ++k) {
+            int aux = j >= c->NACC;   /* CasOCTranscription.cpp:228-232 */
+            xl[col_deriv(c, k, j)] = aux ? c->aux_lo : c->acc_lo;
+            xu[col_deriv(c, k, j)] = aux ? c->aux_hi : c->acc_hi;
+        }
     /* defects, residuals and interpolating-control rows: equality to 0
      * (CasOCTranscription.cpp:275-278, 440-443) */
     if (gl) for (int64_t r = 0; r < c->m; ++r) { gl[r] = 0.0; gu[r] = 0.0; }
@@ -885,7 +912,8 @@ double orc_dgf_curve(const mh_muscle* mu, int which, double x) {
  * (DeGrooteFregly2016Muscle.cpp:186-233, 240-425). */
 static void dgf_muscle(const orc_ctx* c, const mh_muscle* mu, real LMT, real VMT,
         real activation, real excitation, int has_act, real normTendonForce,
-        int compliant, real* tendonForce, real* adot, real* ftdot) {
+        int compliant, int implicit_tendon, real normTendonForceDerivative,
+        real* tendonForce, real* adot, real* ftdot, real* residual) {
     /* calcMuscleLengthInfoHelper (:240-275) */
     real normTendonLength = compliant ? dgf_ft_inv(mu, normTendonForce) : 1.0;
     real tendonLength = mu->tendon_slack_length * normTendonLength;
@@ -900,7 +928,7 @@ static void dgf_muscle(const orc_ctx* c, const mh_muscle* mu, real LMT, real VMT
     real vmax = mu->max_contraction_velocity * mu->optimal_fiber_length;
     /* calcFiberVelocityInfoHelper (:277-323) */
     real normFiberVelocity, fV, normTendonVelocity;
-    if (compliant) {
+    if (compliant && !implicit_tendon) {
         real normFiberForce = normTendonForce / cosPenn;
         fV = (normFiberForce - fPE) / (activation * fAL);
         normFiberVelocity = dgf_fv_inv(fV);
@@ -909,7 +937,13 @@ static void dgf_muscle(const orc_ctx* c, const mh_muscle* mu, real LMT, real VMT
         real tendonVelocity = VMT - fiberVelocityAlongTendon;
         normTendonVelocity = tendonVelocity / mu->tendon_slack_length;
     } else {
-        normTendonVelocity = 0.0;
+        /* rigid, or implicit tendon dynamics: the tendon velocity from the
+         * normalized tendon force derivative (calcTendonForceLengthInverse-
+         * CurveDerivative, DeGrooteFregly2016Muscle.h:471-476) */
+        normTendonVelocity = compliant
+                ? normTendonForceDerivative /
+                  (DGF_c1 * dgf_kT(mu) * exp(dgf_kT(mu) * (normTendonLength - DGF_c2)))
+                : 0.0;
         real tendonVelocity = mu->tendon_slack_length * normTendonVelocity;
         real fiberVelocityAlongTendon = VMT - tendonVelocity;
         real fiberVelocity = fiberVelocityAlongTendon * cosPenn;
@@ -924,6 +958,9 @@ static void dgf_muscle(const orc_ctx* c, const mh_muscle* mu, real LMT, real VMT
     real totalFiberForce = activeFiberForce + conPassive + nonConPassive;
     if (compliant) *tendonForce = Fmax * normTendonForce;
     else *tendonForce = totalFiberForce * cosPenn;
+    /* getEquilibriumResidual = tendon force - fiber force along the tendon
+     * (.cpp:826-848, .h:638-642) */
+    if (implicit_tendon) *residual = *tendonForce - totalFiberForce * cosPenn;
     /* computeStateVariableDerivatives (:186-233) */
     if (has_act) {
         real timeConstFactor = 0.5 + 1.5 * activation;
@@ -933,7 +970,11 @@ static void dgf_muscle(const orc_ctx* c, const mh_muscle* mu, real LMT, real VMT
         real timeConst = tempAct * (f + 0.5) + tempDeact * (-f + 0.5);
         *adot = timeConst * (excitation - activation);
     }
-    if (compliant) *ftdot = normTendonVelocity * dgf_ft_deriv(mu, normTendonLength);
+    if (compliant) {
+        /* implicit: the derivative variable itself (.cpp:215-229) */
+        if (implicit_tendon) *ftdot = normTendonForceDerivative;
+        else *ftdot = normTendonVelocity * dgf_ft_deriv(mu, normTendonLength);
+    }
 }
 
 /* Workspace for one DAE evaluation. */
@@ -1237,10 +1278,13 @@ static void eval_dae_point(const orc_ctx* c, dae_ws* w, real time, const real* x
         int sa = c->mus_act_state[im], sf = c->mus_ftn_state[im];
         real a = sa >= 0 ? x[sa] : e;
         real ftn = sf >= 0 ? x[sf] : NAN;
-        real T, adot = 0, ftdot = 0;
-        dgf_muscle(c, mu, L, V, a, e, sa >= 0, ftn, sf >= 0, &T, &adot, &ftdot);
+        real T, adot = 0, ftdot = 0, resid = 0;
+        int id = c->mus_ider[im];
+        real dft = id >= 0 ? ctrl[c->NC + id] : 0.0;
+        dgf_muscle(c, mu, L, V, a, e, sa >= 0, ftn, sf >= 0, id >= 0, dft, &T, &adot, &ftdot, &resid);
         if (sa >= 0) zdot[sa - 2 * NQ] = adot;
         if (sf >= 0) zdot[sf - 2 * NQ] = ftdot;
+        if (id >= 0) out[NQ + c->NZ + (id - c->NACC)] = resid;
         /* Tension along each segment of the current path. */
         int prev = -1;
         for (int i = mu->point_begin; i < mu->point_begin + mu->point_count; ++i) {
@@ -1354,7 +1398,7 @@ int orc_muscle_length_speed(orc_ctx* c, int im, const double* q, const double* u
 }
 
 int orc_eval_dae(orc_ctx* c, int32_t np, const double* in, double* out) {
-    int NI = 1 + c->NP, NO = c->NQ + c->NZ;
+    int NI = 1 + c->NP, NO = nout(c);
 #pragma omp parallel num_threads(c->nthreads)
     {
         dae_ws w;
@@ -1390,7 +1434,7 @@ static void gather_point(const orc_ctx* c, const double* x, int k, double* st, d
  * outputs for the rest. xd: NS x G (grid-major); res: NQ x G multibody
  * residuals (implicit mode, else unused). */
 static void all_xdot(orc_ctx* c, const double* x, const double* times, double* xd, double* res) {
-    int NS = c->NS, NC = c->NC, NQ = c->NQ, NO = c->NQ + c->NZ;
+    int NS = c->NS, NC = c->NC, NQ = c->NQ, NO = nout(c), NR = nres(c);
 #pragma omp parallel num_threads(c->nthreads)
     {
         dae_ws w;
@@ -1404,11 +1448,9 @@ static void all_xdot(orc_ctx* c, const double* x, const double* times, double* x
             double* o = xd + (int64_t)k * NS;
             for (int j = 0; j < NQ; ++j) o[j] = st[NQ + j];
             eval_dae_point(c, &w, times[k], st, ct, y);
-            if (c->implicit) {
-                for (int j = 0; j < NQ; ++j) { o[NQ + j] = ct[NC + j]; res[(int64_t)k * NQ + j] = y[j]; }
-            } else {
-                for (int j = 0; j < NQ; ++j) o[NQ + j] = y[j];
-            }
+            if (c->implicit) for (int j = 0; j < NQ; ++j) o[NQ + j] = ct[NC + j];
+            else for (int j = 0; j < NQ; ++j) o[NQ + j] = y[j];
+            for (int r = 0; r < NR; ++r) res[(int64_t)k * NR + r] = y[res_out(c, r)];
             for (int z = 0; z < c->NZ; ++z) o[2 * NQ + z] = y[NQ + z];
         }
         free(st);
@@ -1439,7 +1481,7 @@ static double splitmix_uniform(uint64_t* st) {
  * detection iterate (CasOCFunction.h:72-86: time = initial_time, the first
  * grid point's variables); iterates per CasOCSolver.cpp:70-92. */
 static int detect_sparsity(orc_ctx* c, const mh_options* o) {
-    int NS = c->NS, NP = c->NP, NO = c->NQ + c->NZ, W = 1 + NP, NPC = c->NPC;
+    int NS = c->NS, NP = c->NP, NO = nout(c), W = 1 + NP, NPC = c->NPC;
     int npts = 1;
     double* pts;
     if (o->sparsity_detection == MH_SPARSITY_RANDOM) {
@@ -1502,7 +1544,7 @@ static int detect_sparsity(orc_ctx* c, const mh_options* o) {
 }
 
 int orc_get_callback_sparsity(const orc_ctx* c, uint8_t* pattern, int64_t len) {
-    int64_t W = 1 + c->NP, nd = (int64_t)(c->NQ + c->NZ) * W, need = nd + (int64_t)c->NPC * W;
+    int64_t W = 1 + c->NP, nd = (int64_t)nout(c) * W, need = nd + (int64_t)c->NPC * W;
     if (!pattern || len < need) return fail(MH_ERR_INVALID, "pattern needs %lld bytes", (long long)need);
     for (int64_t i = 0; i < need; ++i)
         pattern[i] = i < nd ? (c->sp ? c->sp[i] : 1) : (c->sp_pc ? c->sp_pc[i - nd] : 1);
@@ -1574,7 +1616,7 @@ int orc_eval_g(orc_ctx* c, const double* x, double* g) {
  * (CasOCFunction.h:38-44); time seeds are d(time_k)/d(t0) = 1-grid_k and
  * d(time_k)/d(tf) = grid_k (CasOCTranscription.cpp:126-127,1189). */
 static void fd_blocks(orc_ctx* c, const double* x, const double* times, double* D) {
-    int NS = c->NS, NP = c->NP, NO = c->NQ + c->NZ;
+    int NS = c->NS, NP = c->NP, NO = nout(c);
     int ND = NP + 2;
     double h = c->h;
 #pragma omp parallel num_threads(c->nthreads)
@@ -1680,7 +1722,7 @@ static void path_blocks(const orc_ctx* c, const double* x, const double* times, 
 /* Derivative of xdot[s] at grid point k along direction d (0=t0, 1=tf,
  * 2+j = input j).  For s < NQ, qdot = u exactly. */
 static double xdot_deriv(const orc_ctx* c, const double* D, int k, int s, int d) {
-    int NQ = c->NQ, NO = c->NQ + c->NZ, ND = c->NP + 2;
+    int NQ = c->NQ, NO = nout(c), ND = c->NP + 2;
     if (s < NQ) return (d == 2 + NQ + s) ? 1.0 : 0.0;
     if (c->implicit && s < 2 * NQ) return (d == 2 + c->NS + c->NC + (s - NQ)) ? 1.0 : 0.0;
     return D[((int64_t)k * ND + d) * NO + (s - NQ)];
@@ -1708,7 +1750,7 @@ static int col_to_dir(const orc_ctx* c, int64_t col, int* k) {
 
 int orc_eval_jac_g(orc_ctx* c, const double* x, double* values) {
     int NS = c->NS, NQ = c->NQ;
-    int NO = c->NQ + c->NZ, ND = c->NP + 2;
+    int NO = nout(c), ND = c->NP + 2;
     double* times = (double*)malloc(sizeof(double) * (size_t)c->G);
     double* xd = (double*)malloc(sizeof(double) * (size_t)c->G * (size_t)NS);
     double* D = (double*)malloc(sizeof(double) * (size_t)c->G * (size_t)ND * (size_t)NO);
@@ -1732,7 +1774,7 @@ int orc_eval_jac_g(orc_ctx* c, const double* x, double* values) {
         if (row >= (int64_t)c->N * rpi) {   /* final mesh point: path rows, then residuals */
             int rt = (int)(row - (int64_t)c->N * rpi);
             if (rt < NPC) values[e] = Dp[((int64_t)c->N * ND + dir) * NPC + rt];
-            else values[e] = D[((int64_t)(c->G - 1) * ND + dir) * NO + (rt - NPC)];
+            else values[e] = D[((int64_t)(c->G - 1) * ND + dir) * NO + res_out(c, rt - NPC)];
             continue;
         }
         if (rl < NPC) {                     /* path rows of the interval's mesh point */
@@ -1742,7 +1784,7 @@ int orc_eval_jac_g(orc_ctx* c, const double* x, double* values) {
         rl -= NPC;
         if (rl < npts_res * NR) {           /* residual rows of the interval's points */
             int kr = (c->scheme == MH_HERMITE_SIMPSON ? 2 * i : i) + rl / NR;
-            values[e] = D[((int64_t)kr * ND + dir) * NO + rl % NR];
+            values[e] = D[((int64_t)kr * ND + dir) * NO + res_out(c, rl % NR)];
             continue;
         }
         rl -= npts_res * NR;

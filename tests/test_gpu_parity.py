@@ -88,6 +88,18 @@ CASES = {
         6, dynamics="implicit", control_bounds=True)),
     "pendulum_bound_sparse_guess_trap": lambda: _sparse(configs.pendulum_control_bound(
         12, "both", "trapezoidal"), "initial-guess"),
+    # implicit tendon dynamics: tendon-force derivative
+    # variables and equilibrium residual rows; with implicit multibody
+    # dynamics, path constraints and detected sparsity this is the
+    # MocoInverse-style transcription of configs[4]
+    "gait_implicit_tendon": lambda: configs.gait10dof18musc(
+        6, tendon_compliance=True, tendon_dynamics="implicit"),
+    "gait_implicit_both_central": lambda: configs.gait10dof18musc(
+        5, tendon_compliance=True, tendon_dynamics="implicit", fd_scheme="central",
+        dynamics="implicit"),
+    "gait_inverse_style_sparse": lambda: _physiological_guess(configs.gait10dof18musc(
+        4, tendon_compliance=True, tendon_dynamics="implicit", dynamics="implicit",
+        control_bounds=True)),
 }
 
 
@@ -158,19 +170,21 @@ def _row_mask(ref, x):
     hs = ref.opts.transcription == 0
     step = 2 if hs else 1
     rpi, tail = _rows(ref)
-    nres, npc = ref.NDV, ref.NPC
+    nres, npc, nacc = ref.NRES, ref.NPC, ref.NACC
+    # residual row r of a grid point -> its callback output
+    rout = [r if r < nacc else ref.NO - ref.NAR + (r - nacc) for r in range(nres)]
     npres = step if nres else 0
     mask = np.ones((N, rpi), bool)
     ndef = 2 * NS if hs else NS
     for i in range(N):
         ok = R[i * step:i * step + step + 1].all(0)
         for row in range(npres * nres):
-            mask[i, npc + row] = R[i * step + row // nres, row % nres]
+            mask[i, npc + row] = R[i * step + row // nres, rout[row % nres]]
         for row in range(ndef):
             s = row % NS
-            if s >= (2 * NQ if nres else NQ):
+            if s >= (2 * NQ if nacc else NQ):
                 mask[i, npc + npres * nres + row] = ok[s - NQ]
-    return np.concatenate([mask.reshape(-1), np.ones(npc, bool), R[-1, :nres]])
+    return np.concatenate([mask.reshape(-1), np.ones(npc, bool), R[-1, rout]])
 
 
 BACKENDS = ["auto", "lane", "generic"]
@@ -379,7 +393,7 @@ def test_objective_and_gradient(name):
 @pytest.mark.parametrize("name", ["double_pendulum_hs", "gait_rigid_forward", "double_pendulum_implicit_hs",
                                   "gait_rigid_implicit", "gait_rigid_pathcon",
                                   "pendulum_bound_both_implicit", "gait_rigid_sparse_random",
-                                  "gait_implicit_pathcon_sparse"])
+                                  "gait_implicit_pathcon_sparse", "gait_inverse_style_sparse"])
 def test_shards_reassemble_bit_exact(name):
     """Mesh-interval shards (the multi-GPU partition) concatenate to exactly
     the unsharded g and Jacobian values."""
@@ -510,7 +524,7 @@ def test_sparsity_detection_agrees(name):
     a, b = gpu.callback_sparsity(), ref.callback_sparsity()
     assert a.shape == b.shape
     W = 1 + gpu.NS + gpu.NC + gpu.NDV
-    NO = gpu.NS - gpu.NQ
+    NO = gpu.NO
     diff = np.argwhere((a != b).reshape(-1, W))
     assert len(diff) <= 0.2 * max(b.sum(), 1), (len(diff), b.sum())
     for x in _detection_points(ref, st.solver):

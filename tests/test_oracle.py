@@ -620,3 +620,93 @@ def test_sparsity_detection_random_is_deterministic_and_smaller():
     with pytest.raises(ValueError):
         st.solver.optim_sparsity_detection = "bogus"
         st.solver.options()
+
+
+# --------------------------------------------------------------------------
+# Implicit tendon dynamics (SURVEY §8(f) F4): DGF tendon_compliance_dynamics_mode
+# "implicit".
+# --------------------------------------------------------------------------
+def _physio_point(nlp, rep):
+    """[t, states, controls] at the bounds midpoint with activations 0.5 and
+    normalized tendon forces 0.1 (a regular point of the DGF model)."""
+    x = nlp.initial_guess_from_bounds()
+    st = x[2:2 + nlp.NS].copy()
+    for i, n in enumerate(rep.state_names):
+        if n.endswith("/activation"):
+            st[i] = 0.5
+        elif n.endswith("/normalized_tendon_force"):
+            st[i] = 0.1
+    ct = np.random.default_rng(3).uniform(0.05, 0.3, nlp.NC)
+    return np.concatenate([[0.3], st, ct])
+
+
+@pytest.mark.parametrize("dynamics", ["explicit", "implicit"])
+def test_implicit_tendon_residual_vanishes_at_explicit_derivative(dynamics):
+    """The equilibrium residual FT - FM cos(alpha) (DeGrooteFregly2016Muscle
+    .cpp:826-848) is zero when the derivative variable equals the explicit
+    model's normalized tendon force derivative (.cpp:211-232), and the other
+    outputs agree; a perturbed derivative gives a nonzero residual."""
+    ex_st = configs.gait10dof18musc(2, tendon_compliance=True, dynamics=dynamics)
+    im_st = configs.gait10dof18musc(2, tendon_compliance=True, dynamics=dynamics,
+                                    tendon_dynamics="implicit")
+    # the explicit form inverts the force-velocity curve without the fiber
+    # damping term (.cpp:285-292), so the two agree exactly only undamped
+    for s_ in (ex_st, im_st):
+        for mu in s_.problem.model.muscles:
+            mu.fiber_damping = 0.0
+    ex_rep, im_rep = ex_st.problem.create_rep(), im_st.problem.create_rep()
+    ex = OracleNLP(ex_rep, ex_st.solver.options())
+    im = OracleNLP(im_rep, im_st.solver.options())
+    assert im.NAR == 18 and ex.NAR == 0 and im.NDV == ex.NDV + 18
+    P = _physio_point(ex, ex_rep)
+    acc = np.random.default_rng(5).uniform(-1, 1, ex.NACC)
+    Yx = ex.eval_dae(np.concatenate([P, acc])[None, :])[0]
+    NQ, NZ = ex.NQ, ex.NS - 2 * ex.NQ
+    ftn_idx = [i for i, n in enumerate(ex_rep.state_names) if n.endswith("/normalized_tendon_force")]
+    dft = Yx[[i - NQ for i in ftn_idx]]          # explicit zdot of the tendon states
+    Yi = im.eval_dae(np.concatenate([P, acc, dft])[None, :])[0]
+    assert Yi.shape == (NQ + NZ + 18,)
+    fmax = max(m.max_isometric_force for m in im_st.problem.model.muscles)
+    assert np.all(np.abs(Yi[NQ + NZ:]) <= 1e-9 * fmax), np.abs(Yi[NQ + NZ:]).max()
+    assert np.allclose(Yi[:NQ + NZ], Yx, rtol=1e-9, atol=1e-9)
+    Yp = im.eval_dae(np.concatenate([P, acc, dft + 0.05])[None, :])[0]
+    assert np.all(np.abs(Yp[NQ + NZ:]) > 1e-6)
+
+
+@pytest.mark.parametrize("scheme", ["hermite-simpson", "trapezoidal"])
+def test_implicit_tendon_layout_bounds_and_jacobian(scheme):
+    """Derivative variables [accelerations, tendon-force derivatives] with
+    implicit_auxiliary_derivative_bounds (CasOCTranscription.cpp:222-232);
+    auxiliary residual rows after the multibody residuals at every grid
+    point and in the tail (CasOCTranscription.h:286-311); Jacobian vs a
+    numerical derivative of eval_g at a regular iterate."""
+    N = 2
+    st = configs.gait10dof18musc(N, tendon_compliance=True, dynamics="implicit",
+                                 tendon_dynamics="implicit")
+    st.solver.transcription_scheme = scheme
+    st.solver.implicit_auxiliary_derivative_bounds = (-50.0, 60.0)
+    rep = st.problem.create_rep()
+    nlp = OracleNLP(rep, st.solver.options())
+    NQ, NS, NC, G = nlp.NQ, nlp.NS, nlp.NC, nlp.G
+    assert nlp.NDV == NQ + 18 and nlp.NRES == NQ + 18
+    assert nlp.n == 2 + (NS + NC + NQ + 18) * G
+    xl, xu, _, _ = nlp.bounds()
+    d0 = 2 + (NS + NC) * G
+    D = (xl[d0:].reshape(G, NQ + 18), xu[d0:].reshape(G, NQ + 18))
+    assert np.all(D[0][:, :NQ] == -1000) and np.all(D[1][:, NQ:] == 60) and np.all(D[0][:, NQ:] == -50)
+    hs = scheme == "hermite-simpson"
+    rpi = (2 if hs else 1) * nlp.NRES + (2 * NS + NC if hs else NS)
+    assert nlp.m == N * rpi + nlp.NRES
+    # regular iterate: the physiological point at every grid point
+    P = _physio_point(nlp, rep)
+    x = nlp.initial_guess_from_bounds()
+    x[2:2 + NS * G] = np.tile(P[1:1 + NS], G)
+    x[2 + NS * G:2 + (NS + NC) * G] = np.tile(P[1 + NS:], G)
+    x[d0:] = np.random.default_rng(8).uniform(-0.5, 0.5, (NQ + 18) * G)
+    ir, jc = nlp.jac_structure()
+    J = np.zeros((nlp.m, nlp.n))
+    J[ir, jc] = nlp.eval_jac_g(x)
+    cols = sorted(set(range(0, nlp.n, 7)) | {0, 1, d0, d0 + NQ, nlp.n - 1})
+    Jn = _numjac(nlp.eval_g, x, cols, h=1e-5)
+    noise = 100 * np.finfo(float).eps * np.abs(nlp.eval_g(x)).max() / st.solver.fd_step
+    assert np.allclose(J[:, cols], Jn, rtol=1e-4, atol=max(1e-5, noise))
