@@ -276,6 +276,19 @@ typedef struct mh_problem {
     int32_t npath;               /* path-constraint equations per mesh point */
     int32_t reserved;
     const mh_path_equation* path;
+    /* Prescribed kinematics (PositionMotion, Components/PositionMotion.cpp;
+     * MocoProblemRep.cpp:74-101): prescribed_kinematics = 1 prescribes every
+     * coordinate j as column kinematics_column[j] of that model table (q, and
+     * its first / second time derivatives for u and udot).  The coordinate
+     * values and speeds are then not NLP states (MocoProblemRep.cpp:541-555:
+     * state_infos lists the auxiliary states only), there are no
+     * acceleration variables, and every grid point carries nq multibody
+     * residual rows (findMotionForces with the prescribed motion,
+     * CasOCProblem.h:496-503).  Requires MH_DYNAMICS_IMPLICIT
+     * (MocoCasADiSolver.cpp:147-151). */
+    int32_t prescribed_kinematics; /* 0: none (zero-initialised default)   */
+    int32_t kinematics_table;
+    const int32_t* kinematics_column;
 } mh_problem;
 
 enum mh_scheme { MH_HERMITE_SIMPSON = 0, MH_TRAPEZOIDAL = 1 };

@@ -25,6 +25,9 @@ struct DevModel {
     int nacc;       // acceleration inputs after the controls (implicit: nq)
     const int* mus_ider;  // muscle -> implicit tendon-force derivative input
                           // (index after the controls), -1 = explicit
+    int presc;            // prescribed kinematics: q, u, udot from kin_table
+    int kin_table;
+    const int* kin_col;   // [nq] table column of each coordinate
     double gravity[3];
     double tau_act, tau_deact;
     const mh_body* bodies;
@@ -178,6 +181,34 @@ __device__ __forceinline__ void fn_eval(const DevModel& M, int f, const double* 
     v *= F.scale; d1 *= F.scale; d2 *= F.scale;
 }
 
+// Value, first and second derivative of a table column (PositionMotion:
+// q, u = dq/dt, udot = d2q/dt2 of one spline, PositionMotion.cpp:36-70).
+__device__ __forceinline__ void table_eval_d(const DevModel& M, int ti, int col, double t, double& v,
+        double& d1, double& d2) {
+    const mh_table T = M.tabs[ti];
+    const double* br = M.brk + T.break_begin;
+    int s;
+    if (t <= br[0]) s = 0;
+    else if (t >= br[T.nseg]) s = T.nseg - 1;
+    else {
+        int lo = 0, hi = T.nseg;
+        while (hi - lo > 1) {
+            int mid = (lo + hi) >> 1;
+            if (t < br[mid]) hi = mid; else lo = mid;
+        }
+        s = lo;
+    }
+    const double* cf = M.coef + T.coef_begin + ((long)s * T.ncol + col) * (T.degree + 1);
+    const double dt = t - br[s];
+    double p = cf[T.degree], dp = 0.0, ddp = 0.0;
+    for (int k = T.degree - 1; k >= 0; --k) {
+        ddp = ddp * dt + 2.0 * dp;
+        dp = dp * dt + p;
+        p = p * dt + cf[k];
+    }
+    v = p; d1 = dp; d2 = ddp;
+}
+
 __device__ __forceinline__ double table_eval(const DevModel& M, int ti, int col, double t) {
     const mh_table T = M.tabs[ti];
     const double* br = M.brk + T.break_begin;
@@ -311,11 +342,13 @@ __device__ __forceinline__ int tri(int i, int j) { return i * (i + 1) / 2 + j; }
 // MocoCasOCProblem.h:245-297).
 template <int MB, int MQ, int MP>
 __device__ void dae_eval(const DevModel& M, Work<MB, MQ, MP>& w, double time, const double* x,
-        const double* c, double* out) {
+        const double* c, double* out, const double* wacc_presc = nullptr) {
     const int NQ = M.nq;
     const double* q = x;
     const double* u = x + NQ;
-    const double* wacc = M.implicit ? c + M.nc : nullptr;
+    // implicit: the acceleration inputs; prescribed kinematics: the motion's
+    // udot (both give the multibody residual outputs)
+    const double* wacc = wacc_presc ? wacc_presc : (M.implicit ? c + M.nc : nullptr);
     // ---- kinematics + RNEA forward pass --------------------------------
     w.X[0] = Pose{{1, 0, 0, 0, 1, 0, 0, 0, 1}, {0, 0, 0}};
     w.V[0] = sv_zero();

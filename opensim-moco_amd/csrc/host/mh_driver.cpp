@@ -76,6 +76,7 @@ struct Tape {
     std::vector<mh_path_equation> path;
     std::vector<double> guess;
     std::vector<uint8_t> pattern;
+    std::vector<int32_t> kin_col;
     mh_problem prob{};
 };
 
@@ -144,6 +145,9 @@ bool read_tape(const char* path, Tape& t, std::string& err) {
         } else {
             r.ok = false;
         }
+        t.prob.prescribed_kinematics = r.pod<int32_t>();   // prescribed kinematics
+        t.prob.kinematics_table = r.pod<int32_t>();
+        t.kin_col = r.array<int32_t>(t.prob.prescribed_kinematics ? m.nq : 0);
     }
     if (!r.ok || r.pos != r.buf.size()) { err = "truncated or malformed tape"; return false; }
     m.bodies = t.bodies.data(); m.axes = t.axes.data(); m.functions = t.functions.data();
@@ -159,6 +163,7 @@ bool read_tape(const char* path, Tape& t, std::string& err) {
     t.prob.path = t.path.data();
     t.opts.sparsity_guess = t.guess.empty() ? nullptr : t.guess.data();
     t.opts.sparsity_pattern = t.pattern.empty() ? nullptr : t.pattern.data();
+    t.prob.kinematics_column = t.kin_col.empty() ? nullptr : t.kin_col.data();
     return true;
 }
 

@@ -121,6 +121,16 @@ struct GenericDae {
     __device__ __forceinline__ static void eval(const DevModel& M, double t, const double* in,
             double* out) {
         Work<Z::MB, Z::MQ, Z::MP> w;
+        if (M.presc) {
+            // prescribed kinematics: [q, u] and udot from the motion, the
+            // NLP states are the auxiliary states
+            double xf[2 * Z::MQ + Z::MI], ud[Z::MQ];
+            for (int j = 0; j < M.nq; ++j)
+                table_eval_d(M, M.kin_table, M.kin_col[j], t, xf[j], xf[M.nq + j], ud[j]);
+            for (int k = 0; k < M.nz; ++k) xf[2 * M.nq + k] = in[k];
+            dae_eval<Z::MB, Z::MQ, Z::MP>(M, w, t, xf, in + M.ns, out, ud);
+            return;
+        }
         dae_eval<Z::MB, Z::MQ, Z::MP>(M, w, t, in, in + M.ns, out);
     }
 };
@@ -132,6 +142,7 @@ struct Layout {
     int nk;                  // grid points in this shard
     int NDV;                 // derivative variables per grid point: accelerations, aux derivatives
     int NACC;                // acceleration variables per grid point (implicit multibody: NQ)
+    int SO;                  // callback output of state s's derivative: s + SO (s >= NQ)
 };
 
 // Per grid point the evaluation lanes are laid out as
@@ -661,7 +672,7 @@ __device__ __forceinline__ double xdot_at(const Layout& L, const Lanes& Ln,
         const double* __restrict__ x, const YV& Y, int k, int s) {
     if (s < L.NQ) return Y.xs(k, L.NQ + s);
     if (L.NACC && s < 2 * L.NQ) return Y.xd(k, s - L.NQ);   // implicit: udot = w
-    return Y.row(k, s - L.NQ)[Ln.base];
+    return Y.row(k, s + L.SO)[Ln.base];
 }
 
 template <class YV>
@@ -726,7 +737,7 @@ __device__ __forceinline__ double dxdot(const Layout& L, const Lanes& Ln, const 
         int dir) {
     if (s < L.NQ) return dir == 2 + L.NQ + s ? 1.0 : 0.0;
     if (L.NACC && s < 2 * L.NQ) return dir == 2 + L.NS + L.NC + (s - L.NQ) ? 1.0 : 0.0;
-    return dout(Ln, Y, k, s - L.NQ, dir);
+    return dout(Ln, Y, k, s + L.SO, dir);
 }
 
 
@@ -1403,6 +1414,11 @@ struct mh_ctx {
     int NDV = 0, nnz_tail = 0;     // implicit: accelerations per point, tail nonzeros
     int npc = 0, ntail = 0;        // path equations per mesh point; tail rows (npc + residuals)
     int NACC = 0, NAR = 0;         // accelerations (implicit multibody), implicit aux residuals per point
+    int NMB = 0;                   // multibody residual rows per point (implicit / prescribed: NQ)
+    int TQ = 0;                    // coordinates among the NLP states (0: prescribed kinematics)
+    int SO = 0;                    // callback output of state s's derivative: s + SO
+    int presc = 0, kin_table = -1;
+    std::vector<int> kin_col;
     std::vector<int> mus_ider;     // muscle -> aux derivative index after the controls (-1)
     double aux_lo = -1000.0, aux_hi = 1000.0;
     int npe = 0;                   // path-constraint template entries per mesh point
@@ -1498,7 +1514,7 @@ static int64_t col_deriv(const mh_ctx* c, int64_t k, int j) {
 // (implicit mode) the tail template: the final grid point's residual rows,
 // evaluated by the last interval.
 static void build_template(mh_ctx* c) {
-    const int NS = c->NS, NQ = c->NQ, NC = c->NC, NDV = c->NDV;
+    const int NS = c->NS, NQ = c->TQ, NC = c->NC, NDV = c->NDV;   // NQ: coordinates among the states
     const bool implicit = c->NACC > 0;
     struct Col { int pt; int dir; };  // dir: 0/1 time, 2+input
     auto key = [&](const Col& col) -> int64_t {
@@ -1538,8 +1554,8 @@ static void build_template(mh_ctx* c) {
     // the implicit auxiliary residuals): the point's inputs + time; the
     // entry's s is the callback output
     auto residual_rows = [&](int& row, int pt) {
-        for (int r = 0; r < c->NACC + c->NAR; ++r) {
-            const int o = r < c->NACC ? r : NQ + c->NZ + (r - c->NACC);
+        for (int r = 0; r < c->NMB + c->NAR; ++r) {
+            const int o = r < c->NMB ? r : c->NQ + c->NZ + (r - c->NMB);
             std::vector<Col> v;
             if (time_dep(c->sp, o)) { v.push_back({pt, 0}); v.push_back({pt, 1}); }
             point_dep(c->sp, o, pt, -1, v);
@@ -1574,10 +1590,10 @@ static void build_template(mh_ctx* c) {
                 v.push_back({1, 2 + s}); v.push_back({0, 2 + s}); v.push_back({2, 2 + s});
                 v.push_back({0, adir + s - NQ}); v.push_back({2, adir + s - NQ});
             } else {
-                // callback output s - NQ (explicit: udot / zdot; implicit:
-                // zdot after the NQ residuals)
+                // callback output s + SO (explicit: udot / zdot; implicit /
+                // prescribed: zdot after the NQ residuals)
                 v.push_back({1, 2 + s});
-                point_dep(c->sp, s - NQ, 0, s, v); point_dep(c->sp, s - NQ, 2, s, v);
+                point_dep(c->sp, s + c->SO, 0, s, v); point_dep(c->sp, s + c->SO, 2, s, v);
             }
             emit_row(row++, T_HERM_T, T_HERM_X, s, v);
         }
@@ -1590,8 +1606,8 @@ static void build_template(mh_ctx* c) {
                 v.push_back({0, 2 + s}); v.push_back({2, 2 + s});
                 v.push_back({0, adir + s - NQ}); v.push_back({1, adir + s - NQ}); v.push_back({2, adir + s - NQ});
             } else {
-                point_dep(c->sp, s - NQ, 0, s, v); point_dep(c->sp, s - NQ, 1, -1, v);
-                point_dep(c->sp, s - NQ, 2, s, v);
+                point_dep(c->sp, s + c->SO, 0, s, v); point_dep(c->sp, s + c->SO, 1, -1, v);
+                point_dep(c->sp, s + c->SO, 2, s, v);
             }
             emit_row(row++, T_SIMP_T, T_SIMP_X, s, v);
         }
@@ -1613,7 +1629,7 @@ static void build_template(mh_ctx* c) {
                 v.push_back({0, 2 + s}); v.push_back({1, 2 + s});
                 v.push_back({0, adir + s - NQ}); v.push_back({1, adir + s - NQ});
             } else {
-                point_dep(c->sp, s - NQ, 0, s, v); point_dep(c->sp, s - NQ, 1, s, v);
+                point_dep(c->sp, s + c->SO, 0, s, v); point_dep(c->sp, s + c->SO, 1, s, v);
             }
             emit_row(row++, T_TRAP_T, T_TRAP_X, s, v);
         }
@@ -1680,7 +1696,25 @@ static int validate_and_layout(mh_ctx* c, const mh_problem* p, const mh_options*
         return set_err(MH_ERR_INVALID, "unknown multibody dynamics mode %d", o->multibody_dynamics_mode);
     // derivative variables: accelerations, then the implicit auxiliary
     // derivatives in component order (MocoCasOCProblem.cpp:85-94)
-    c->NACC = o->multibody_dynamics_mode == MH_DYNAMICS_IMPLICIT ? c->NQ : 0;
+    // prescribed kinematics (PositionMotion): q, u not NLP states, no
+    // acceleration variables, nq multibody residual rows per point
+    c->presc = p->prescribed_kinematics ? 1 : 0;
+    if (c->presc) {
+        if (o->multibody_dynamics_mode != MH_DYNAMICS_IMPLICIT)
+            return set_err(MH_ERR_INVALID, "Prescribed kinematics (PositionMotion) requires implicit dynamics mode.");
+        if (p->kinematics_table < 0 || p->kinematics_table >= M.ntables || !p->kinematics_column)
+            return set_err(MH_ERR_INVALID, "bad kinematics table");
+        c->kin_table = p->kinematics_table;
+        c->kin_col.assign(p->kinematics_column, p->kinematics_column + M.nq);
+        for (int j = 0; j < M.nq; ++j)
+            if (c->kin_col[j] < 0 || c->kin_col[j] >= M.tables[c->kin_table].ncol)
+                return set_err(MH_ERR_INVALID, "kinematics column %d out of range", j);
+        c->NS = c->NZ;
+    }
+    c->TQ = c->presc ? 0 : c->NQ;
+    c->SO = c->presc ? c->NQ : -c->NQ;
+    c->NACC = o->multibody_dynamics_mode == MH_DYNAMICS_IMPLICIT && !c->presc ? c->NQ : 0;
+    c->NMB = o->multibody_dynamics_mode == MH_DYNAMICS_IMPLICIT ? c->NQ : 0;
     c->NAR = 0;
     c->mus_ider.assign(M.nmuscles, -1);
     for (int im = 0; im < M.nmuscles; ++im)
@@ -1925,6 +1959,7 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
                  o_fs = A.put(ftn_state.data(), ftn_state.size()),
                  o_mc = A.put(mus_control.data(), mus_control.size()),
                  o_mi = A.put(c->mus_ider.data(), c->mus_ider.size()),
+                 o_kcol = A.put(c->kin_col.data(), c->kin_col.size()),
                  o_md = A.put(mder.data(), mder.size()),
                  o_goals = A.put(p->goals, p->ngoals), o_gidx = A.put(p->goal_index, p->nterms),
                  o_gcol = A.put(p->goal_column, p->nterms), o_gw = A.put(p->goal_weight, p->nterms),
@@ -1980,6 +2015,9 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     D.implicit = c->NACC > 0 ? 1 : 0;
     D.nacc = c->NACC;
     D.mus_ider = (const int*)(b + o_mi);
+    D.presc = c->presc;
+    D.kin_table = c->kin_table;
+    D.kin_col = (const int*)(b + o_kcol);
     for (int i = 0; i < 3; ++i) D.gravity[i] = M.gravity[i];
     D.tau_act = tau_act; D.tau_deact = tau_deact;
     D.bodies = (const mh_body*)(b + o_bodies); D.axes = (const mh_axis*)(b + o_axes);
@@ -2213,7 +2251,7 @@ struct Backend {
 
 template <class D>
 static void be_eval_lane(mh_ctx* c, const double* x, int mode, double* Y) {
-    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, c->k0, c->nk, c->NDV, c->NACC};
+    Layout L{c->NS, c->NC, c->TQ, c->NO, c->NI, c->G, c->k0, c->nk, c->NDV, c->NACC, c->SO};
     const Lanes& ln = mode ? c->lanes_jac : c->lanes_g;
     const long lanes = (long)c->nk * ln.stride;
     hipLaunchKernelGGL(k_eval<D>, dim3((unsigned)((lanes + 63) / 64)), dim3(64), 0, c->stream, c->M, L,
@@ -2281,8 +2319,8 @@ static void be_interval(mh_ctx* c, const double* x, int mode, double* g, double*
     if (lds > 65536)
         (void)hipFuncSetAttribute((const void*)k_interval<D>, hipFuncAttributeMaxDynamicSharedMemorySize,
                 (int)lds);
-    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, c->k0, c->nk, c->NDV, c->NACC};
-    Interval I{c->scheme, c->interp, c->ib, c->rpi, c->nnz_int, c->NACC + c->NAR, c->NACC, c->NQ + c->NZ,
+    Layout L{c->NS, c->NC, c->TQ, c->NO, c->NI, c->G, c->k0, c->nk, c->NDV, c->NACC, c->SO};
+    Interval I{c->scheme, c->interp, c->ib, c->rpi, c->nnz_int, c->NMB + c->NAR, c->NMB, c->NQ + c->NZ,
                c->N, c->nnz_tail, c->ntail, c->npe, c->P};
     const unsigned threads = v ? 1024u : 256u;
     hipLaunchKernelGGL(k_interval<D>, dim3((unsigned)(c->ie - c->ib)), dim3(threads), lds, c->stream, c->M,
@@ -2290,20 +2328,20 @@ static void be_interval(mh_ctx* c, const double* x, int mode, double* g, double*
 }
 template <class D>
 static void be_integrand(mh_ctx* c, const double* x) {
-    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, 0, c->G, c->NDV, c->NACC};
+    Layout L{c->NS, c->NC, c->TQ, c->NO, c->NI, c->G, 0, c->G, c->NDV, c->NACC, c->SO};
     hipLaunchKernelGGL(k_integrand<D>, dim3((c->G + 63) / 64), dim3(64), 0, c->stream, c->M, L,
             c->GS, x, c->d_grid, c->d_quad, c->d_C);
 }
 template <class D>
 static void be_grad(mh_ctx* c, const double* x) {
-    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, 0, c->G, c->NDV, c->NACC};
+    Layout L{c->NS, c->NC, c->TQ, c->NO, c->NI, c->G, 0, c->G, c->NDV, c->NACC, c->SO};
     const long tot = (long)c->G * (c->NI + 2);
     hipLaunchKernelGGL(k_grad<D>, dim3((unsigned)((tot + 63) / 64)), dim3(64), 0, c->stream, c->M, L,
             c->GS, c->fd, c->h, x, c->d_grid, c->d_quad, c->d_grad, c->d_tpart);
 }
 template <class D>
 static void be_probe_lane(mh_ctx* c, int np, const double* in, double* out) {
-    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, 0, 0, c->NDV, c->NACC};
+    Layout L{c->NS, c->NC, c->TQ, c->NO, c->NI, c->G, 0, 0, c->NDV, c->NACC, c->SO};
     hipLaunchKernelGGL(k_dae_probe<D>, dim3((np + 63) / 64), dim3(64), 0, c->stream, c->M, L, np, in,
             out);
 }
@@ -2365,8 +2403,8 @@ static int launch_stage(mh_ctx* c, int stage, int kind, const double* x, double*
         HIPCHK(hipGetLastError());
         return MH_OK;
     }
-    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, c->k0, c->nk, c->NDV, c->NACC};
-    Interval I{c->scheme, c->interp, c->ib, c->rpi, c->nnz_int, c->NACC + c->NAR, c->NACC, c->NQ + c->NZ,
+    Layout L{c->NS, c->NC, c->TQ, c->NO, c->NI, c->G, c->k0, c->nk, c->NDV, c->NACC, c->SO};
+    Interval I{c->scheme, c->interp, c->ib, c->rpi, c->nnz_int, c->NMB + c->NAR, c->NMB, c->NQ + c->NZ,
                c->N, c->nnz_tail, c->ntail, c->npe, c->P};
     const Lanes& ln = kind == 0 ? c->lanes_g : c->lanes_jac;
     const double* Y = kind == 0 ? c->d_Yg : c->d_Y;
@@ -2541,7 +2579,7 @@ extern "C" int mh_eval_f(mh_ctx* c, const double* x, int, double* f) {
     (void)hipGetLastError();   // report only this call's launch errors
     HIPCHK(hipMemcpyAsync(c->d_x, x, sizeof(double) * c->n, hipMemcpyHostToDevice, c->stream));
     if (c->timing) HIPCHK(hipEventRecord(c->ev[0], c->stream));
-    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, 0, c->G, c->NDV, c->NACC};
+    Layout L{c->NS, c->NC, c->TQ, c->NO, c->NI, c->G, 0, c->G, c->NDV, c->NACC, c->SO};
     if (c->ngoals > 0) {
         c->be->integrand(c, c->d_x);
         HIPCHK(hipGetLastError());
@@ -2561,7 +2599,7 @@ extern "C" int mh_eval_grad_f(mh_ctx* c, const double* x, int, double* grad) {
     (void)hipGetLastError();   // report only this call's launch errors
     HIPCHK(hipMemcpyAsync(c->d_x, x, sizeof(double) * c->n, hipMemcpyHostToDevice, c->stream));
     if (c->timing) HIPCHK(hipEventRecord(c->ev[0], c->stream));
-    Layout L{c->NS, c->NC, c->NQ, c->NO, c->NI, c->G, 0, c->G, c->NDV, c->NACC};
+    Layout L{c->NS, c->NC, c->TQ, c->NO, c->NI, c->G, 0, c->G, c->NDV, c->NACC, c->SO};
     HIPCHK(hipMemsetAsync(c->d_grad, 0, sizeof(double) * c->n, c->stream));
     HIPCHK(hipMemsetAsync(c->d_tpart, 0, sizeof(double) * 2 * c->G, c->stream));
     HIPCHK(hipMemsetAsync(c->d_C, 0, sizeof(double) * c->G * std::max(1, c->ngoals), c->stream));
@@ -2797,7 +2835,7 @@ static const Backend* select_backend(mh_ctx* c, const mh_problem* p) {
     const char* force = std::getenv("MOCOHIP_BACKEND");
     const bool generic = force && std::strcmp(force, "generic") == 0;
     const bool lane = force && std::strcmp(force, "lane") == 0;
-    if (!generic) {
+    if (!generic && !c->presc) {   // no generated back end for prescribed kinematics
         const uint64_t key = backend_key(c->model_hash, c->NACC > 0);
         for (const GenEntry& e : kGeneratedModels)
             if (e.hash == key) return lane ? &e.lane : &e.tasks;

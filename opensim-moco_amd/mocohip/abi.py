@@ -130,7 +130,9 @@ class mh_problem(C.Structure):
                 ("ngoals", i32), ("nterms", i32), ("goals", P(mh_goal)),
                 ("goal_index", P(i32)), ("goal_column", P(i32)),
                 ("goal_weight", P(f64)),
-                ("npath", i32), ("reserved", i32), ("path", P(mh_path_equation))]
+                ("npath", i32), ("reserved", i32), ("path", P(mh_path_equation)),
+                ("prescribed_kinematics", i32), ("kinematics_table", i32),
+                ("kinematics_column", P(i32))]
 
 
 class mh_options(C.Structure):

@@ -193,8 +193,35 @@ def gait10dof18musc(num_mesh_intervals: int = 200, muscles: bool = True,
     return MocoStudy(p, s)
 
 
+def gait10dof18musc_inverse(num_mesh_intervals: int = 25, fd_scheme: str = "forward",
+                            sparsity: str = "random") -> MocoStudy:
+    """MocoInverse on gait10dof18musc (configs[4], one solve of the batch):
+    kinematics prescribed by a PositionMotion of the coordinate trajectories
+    (MocoInverse.cpp:46-66; GCVSpline degree 5, PositionMotion.cpp:121-155),
+    DeGrooteFregly2016 muscles with compliant tendons in implicit mode
+    (testMocoInverse.cpp:120-130), reserves, ExternalLoads, control effort
+    goal (MocoInverse.cpp:76-80), implicit dynamics, forward differences and
+    "random" sparsity detection (MocoInverse.cpp:104-114).  The kinematics
+    are the bundled walking coordinate trajectories, clipped by 1e-3 at both
+    ends (clip_time_range, MocoInverse.cpp:70-74)."""
+    m = gait10dof18musc_model(tendon_compliance=True, tendon_dynamics="implicit")
+    ref = _load("walk_gait1018_state_reference.json")
+    t = np.asarray(ref["time"])
+    kin = DataTable("kinematics", t, {k: np.asarray(v) for k, v in ref["columns"].items()
+                                      if k.endswith("/value")}, degree=5)
+    p = MocoProblem(m)
+    p.set_position_motion(kin)
+    p.set_time_bounds(float(t[0]) + 1e-3, float(t[-1]) - 1e-3)
+    p.add_goal(MocoControlGoal("excitation_effort", 1.0))
+    s = MocoHipSolver(num_mesh_intervals=num_mesh_intervals,
+                      optim_finite_difference_scheme=fd_scheme, multibody_dynamics_mode="implicit",
+                      optim_sparsity_detection=sparsity)
+    return MocoStudy(p, s)
+
+
 CONFIGS = {
     "sliding_mass": sliding_mass,
     "double_pendulum": double_pendulum,
     "gait10dof18musc": gait10dof18musc,
+    "gait10dof18musc_inverse": gait10dof18musc_inverse,
 }

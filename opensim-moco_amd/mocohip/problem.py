@@ -157,6 +157,7 @@ class MocoProblem:
         self.control_infos: Dict[str, MocoVariableInfo] = {}
         self.goals: List[object] = []
         self.path_constraints: List[object] = []
+        self.position_motion: Optional[DataTable] = None
         self.default_speed_bounds = MocoBounds(-50.0, 50.0)
         self.bound_activation_from_excitation = True
 
@@ -178,6 +179,13 @@ class MocoProblem:
     def add_goal(self, goal):
         self.goals.append(goal)
         return goal
+
+    def set_position_motion(self, kinematics: DataTable):
+        """PositionMotion::createFromTable (Components/PositionMotion.cpp:
+        121-155): every coordinate prescribed by a GCVSpline (degree 5 unless
+        the table says otherwise) of the column named by its value path
+        ("/jointset/<joint>/<coordinate>/value")."""
+        self.position_motion = kinematics
 
     def add_path_constraint(self, constraint):
         self.path_constraints.append(constraint)
@@ -202,8 +210,23 @@ class ProblemRep:
         self.problem = problem
         model = problem.model
         path_eqs, bound_tables = self._path_equations(problem)
-        self.compiled: CompiledModel = model.compile(extra_tables=bound_tables)
-        self.state_names = self.compiled.state_names
+        kin = problem.position_motion
+        extra = list(bound_tables)
+        if kin is not None:
+            qpaths = [c.path + "/value" for c in model.coordinates()]
+            missing = [q for q in qpaths if q not in kin.columns]
+            if missing:
+                raise ValueError(f"PositionMotion: no kinematics for {missing}")
+            extra.append(DataTable("__position_motion", np.asarray(kin.times, float),
+                                   {q: np.asarray(kin.columns[q], float) for q in qpaths},
+                                   degree=kin.degree))
+        self.compiled: CompiledModel = model.compile(extra_tables=extra)
+        # prescribed kinematics: coordinate values and speeds are not states
+        # (MocoProblemRep.cpp:541-555)
+        self.prescribed_kinematics = kin is not None
+        self.state_names = [n for n in self.compiled.state_names
+                            if not (self.prescribed_kinematics and
+                                    (n.endswith("/value") or n.endswith("/speed")))]
         self.control_names = self.compiled.control_names
         sinfo: Dict[str, MocoVariableInfo] = {}
         cinfo: Dict[str, MocoVariableInfo] = {}
@@ -312,6 +335,12 @@ class ProblemRep:
             if e.table >= 0:   # bound table index: after the model's own
                 e.table = self.compiled.table_index[bound_tables[e.table].name]
         self._path = (abi.mh_path_equation * max(1, len(path_eqs)))(*path_eqs)
+        p.prescribed_kinematics = 0
+        if kin is not None:
+            p.prescribed_kinematics = 1
+            p.kinematics_table = self.compiled.table_index["__position_motion"]
+            self._kin_cols = np.arange(self.compiled.nq, dtype=np.int32)
+            p.kinematics_column = abi.iptr(self._kin_cols)
         p.npath = len(path_eqs)
         p.path = self._path
         self.num_path_equations = len(path_eqs)

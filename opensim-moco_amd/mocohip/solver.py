@@ -167,9 +167,38 @@ class _NLPBase:
         return ir[:self.nnz], jc[:self.nnz]
 
     @property
+    def prescribed(self) -> bool:
+        """Prescribed kinematics (PositionMotion): q, u not NLP states."""
+        return bool(getattr(self.rep, "prescribed_kinematics", False))
+
+    @property
+    def TQ(self) -> int:
+        """Coordinates among the NLP states (0 with prescribed kinematics)."""
+        return 0 if self.prescribed else self.NQ
+
+    @property
+    def NZ(self) -> int:
+        return self.NS - 2 * self.TQ
+
+    @property
+    def SO(self) -> int:
+        """Callback output of state s's derivative: s + SO (s >= TQ)."""
+        return self.NQ if self.prescribed else -self.NQ
+
+    @property
+    def implicit(self) -> bool:
+        return self.opts.multibody_dynamics_mode == abi.MH_DYNAMICS_IMPLICIT
+
+    @property
     def NACC(self) -> int:
-        """Acceleration variables per grid point (implicit mode: NQ)."""
-        return self.NQ if self.opts.multibody_dynamics_mode == abi.MH_DYNAMICS_IMPLICIT else 0
+        """Acceleration variables per grid point (implicit mode: NQ; none
+        with prescribed kinematics)."""
+        return self.NQ if self.implicit and not self.prescribed else 0
+
+    @property
+    def NMB(self) -> int:
+        """Multibody residual rows per grid point."""
+        return self.NQ if self.implicit else 0
 
     @property
     def NAR(self) -> int:
@@ -186,12 +215,12 @@ class _NLPBase:
     def NO(self) -> int:
         """DAE callback outputs: udot or multibody residual, zdot, auxiliary
         residuals."""
-        return self.NS - self.NQ + self.NAR
+        return self.NQ + self.NZ + self.NAR
 
     @property
     def NRES(self) -> int:
         """Residual rows per grid point (multibody, then auxiliary)."""
-        return self.NACC + self.NAR
+        return self.NMB + self.NAR
 
     def callback_sparsity(self) -> np.ndarray:
         """The callback sparsity behind the Jacobian structure: (NQ + NZ)

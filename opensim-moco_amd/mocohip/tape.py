@@ -9,7 +9,8 @@ Layout (little endian, x86-64 struct layout of include/mocohip.h):
   ngoals, nterms, then the arrays in mh_model / mh_problem field order,
   each as (int64 byte count, bytes); version 2 appends npath and the
   mh_path_equation array, then the sparsity-detection guess (n doubles or
-  empty) and the given callback sparsity (bytes or empty)."""
+  empty), the given callback sparsity (bytes or empty) and the prescribed
+  kinematics (table index, per-coordinate columns)."""
 from __future__ import annotations
 
 import ctypes as C
@@ -76,5 +77,7 @@ def write_tape(rep, opts: abi.mh_options, path: str) -> None:
     pb = _blob(p.path, abi.mh_path_equation, p.npath)
     out += [struct.pack("<i", p.npath), struct.pack("<q", len(pb)), pb]
     out += [struct.pack("<q", len(guess)), guess, struct.pack("<q", len(pattern)), pattern]
+    kc = _blob(p.kinematics_column, C.c_int32, m.nq) if p.prescribed_kinematics else b""
+    out += [struct.pack("<ii", p.prescribed_kinematics, p.kinematics_table), struct.pack("<q", len(kc)), kc]
     with open(path, "wb") as fh:
         fh.write(b"".join(out))

@@ -249,6 +249,13 @@ struct orc_ctx {
     int* mus_ider;          /* muscle -> its tendon-force derivative's index
                              * in the derivative block (-1: explicit)     */
     double aux_lo, aux_hi;  /* implicit auxiliary derivative bounds      */
+    /* prescribed kinematics (PositionMotion): q, u, udot from a table; the
+     * NLP states are the auxiliary states only */
+    int presc, kin_table;
+    int32_t* kin_col;
+    int TQ;                 /* coordinates among the NLP states (0 if prescribed) */
+    int NMB;                /* multibody residual rows per point          */
+    int SO;                 /* callback output of state s's derivative: s + SO */
     int* mus_act_state;     /* state index of activation (-1)          */
     int* mus_ftn_state;     /* state index of normalized tendon force   */
     int* mus_control;       /* control index of excitation (-1)        */
@@ -291,9 +298,9 @@ static int64_t col_deriv(const orc_ctx* c, int k, int j) {
 static int nout(const orc_ctx* c) { return c->NQ + c->NZ + c->NAR; }
 /* residual rows per grid point: multibody residuals (implicit mode), then
  * auxiliary residuals (flattenConstraints, CasOCTranscription.h:290-296) */
-static int nres(const orc_ctx* c) { return c->NACC + c->NAR; }
+static int nres(const orc_ctx* c) { return c->NMB + c->NAR; }
 /* callback output behind residual row r of a grid point */
-static int res_out(const orc_ctx* c, int r) { return r < c->NACC ? r : c->NQ + c->NZ + (r - c->NACC); }
+static int res_out(const orc_ctx* c, int r) { return r < c->NMB ? r : c->NQ + c->NZ + (r - c->NMB); }
 /* the mesh point that opens interval i (and closes interval i-1) */
 static int mesh_point(const orc_ctx* c, int i) { return c->scheme == MH_HERMITE_SIMPSON ? 2 * i : i; }
 
@@ -350,10 +357,10 @@ static int64_t path_rows(const orc_ctx* c, int k, int64_t row, row_fn emit, void
 /* Implicit mode: the speed rows (NQ <= s < 2NQ) have udot = the derivative
  * variable, a direct MX expression (CasOCTranscription.cpp:339-341), so they
  * depend on the point's own state s and derivative s - NQ only. */
-static int speed_row_sparse(const orc_ctx* c, int s) { return c->implicit && s >= c->NQ && s < 2 * c->NQ; }
+static int speed_row_sparse(const orc_ctx* c, int s) { return c->NACC && s >= c->TQ && s < 2 * c->TQ; }
 
 static void interval_rows(const orc_ctx* c, int i, int64_t row0, row_fn emit, void* ud) {
-    int NQ = c->NQ, NS = c->NS, NC = c->NC;
+    int NQ = c->TQ, NS = c->NS, NC = c->NC;   /* NQ: coordinates among the states */
     int64_t* cols = (int64_t*)malloc(sizeof(int64_t) * (size_t)(3 * (NS + NC + c->NDV) + 8));
     int64_t row = row0;
     if (c->scheme == MH_HERMITE_SIMPSON) {
@@ -392,9 +399,9 @@ static void interval_rows(const orc_ctx* c, int i, int64_t row0, row_fn emit, vo
                         cols[n++] = col_deriv(c, kp, j);
                     }
                 } else {
-                    /* callback output s - NQ (explicit: udot / zdot;
-                     * implicit: zdot after the NQ residuals) */
-                    int o = s - NQ;
+                    /* callback output s + SO (explicit: udot / zdot;
+                     * implicit / prescribed: zdot after the NQ residuals) */
+                    int o = s + c->SO;
                     if (pass == 0) {
                         cols[n++] = col_state(c, km, s);
                         n += point_cols_dep(c, c->sp, o, ki, s, cols + n);
@@ -430,8 +437,8 @@ static void interval_rows(const orc_ctx* c, int i, int64_t row0, row_fn emit, vo
                 cols[n++] = col_state(c, ki, s); cols[n++] = col_state(c, kp, s);
                 cols[n++] = col_deriv(c, ki, s - NQ); cols[n++] = col_deriv(c, kp, s - NQ);
             } else {
-                n += point_cols_dep(c, c->sp, s - NQ, ki, s, cols + n);
-                n += point_cols_dep(c, c->sp, s - NQ, kp, s, cols + n);
+                n += point_cols_dep(c, c->sp, s + c->SO, ki, s, cols + n);
+                n += point_cols_dep(c, c->sp, s + c->SO, kp, s, cols + n);
             }
             qsort(cols, (size_t)n, sizeof(int64_t), cmp64);
             emit(ud, row++, cols, n);
@@ -540,8 +547,12 @@ int orc_create(const mh_problem* p, const mh_options* o, orc_ctx** out) {
             c->tau_deact = mu->deactivation_time_constant;
         }
     }
-    c->NS = z;
     c->NZ = z - 2 * c->NQ;
+    c->presc = p->prescribed_kinematics != 0;
+    c->kin_table = p->kinematics_table;
+    c->NS = c->presc ? c->NZ : z;       /* NLP states */
+    c->TQ = c->presc ? 0 : c->NQ;
+    c->SO = c->presc ? c->NQ : -c->NQ;
     c->NC = M->nactuators;
     c->implicit = o->multibody_dynamics_mode == MH_DYNAMICS_IMPLICIT;
     if (o->multibody_dynamics_mode != MH_DYNAMICS_EXPLICIT && !c->implicit) {
@@ -551,7 +562,24 @@ int orc_create(const mh_problem* p, const mh_options* o, orc_ctx** out) {
     /* derivative variables: accelerations, then the implicit auxiliary
      * derivatives in component order (MocoCasOCProblem.cpp:85-94,
      * MocoCasOCProblem.h:605-620) */
-    c->NACC = c->implicit ? c->NQ : 0;
+    if (c->presc && !c->implicit) {
+        orc_destroy(c);
+        return fail(MH_ERR_INVALID, "Prescribed kinematics (PositionMotion) requires implicit dynamics mode.");
+    }
+    c->NACC = c->implicit && !c->presc ? c->NQ : 0;
+    c->NMB = c->implicit ? c->NQ : 0;
+    if (c->presc) {
+        if (p->kinematics_table < 0 || p->kinematics_table >= M->ntables || !p->kinematics_column) {
+            orc_destroy(c);
+            return fail(MH_ERR_INVALID, "bad kinematics table");
+        }
+        c->kin_col = DUP(int32_t, p->kinematics_column, c->NQ);
+        for (int j = 0; j < c->NQ; ++j)
+            if (c->kin_col[j] < 0 || c->kin_col[j] >= c->tabs[c->kin_table].ncol) {
+                orc_destroy(c);
+                return fail(MH_ERR_INVALID, "kinematics column %d out of range", j);
+            }
+    }
     c->mus_ider = (int*)malloc(sizeof(int) * (size_t)(M->nmuscles + 1));
     c->NAR = 0;
     for (int im = 0; im < M->nmuscles; ++im) {
@@ -676,7 +704,8 @@ void orc_destroy(orc_ctx* c) {
     if (!c) return;
     void* ptrs[] = {c->bodies, c->axes, c->funcs, c->kx, c->ky, c->kb, c->kc, c->kd,
             c->mus, c->pts, c->acts, c->tabs, c->brk, c->coef, c->ext, c->sinfo, c->cinfo,
-            c->goals, c->gidx, c->gcol, c->gw, c->pc, c->sp, c->sp_pc, c->mus_ider, c->mus_act_state, c->mus_ftn_state,
+            c->goals, c->gidx, c->gcol, c->gw, c->pc, c->sp, c->sp_pc, c->mus_ider, c->kin_col,
+            c->mus_act_state, c->mus_ftn_state,
             c->mus_control, c->coord_body, c->grid, c->quad, c->iRow, c->jCol};
     for (size_t i = 0; i < sizeof ptrs / sizeof ptrs[0]; ++i) free(ptrs[i]);
     free(c);
@@ -989,6 +1018,8 @@ typedef struct {
     real* pvel;
     int* pact;
     real* fvals;    /* function value/d1/d2 per axis (3 per axis)        */
+    real* xfull;    /* prescribed kinematics: [q, u, z]                  */
+    real* udot;     /* prescribed kinematics: udot                       */
 } dae_ws;
 
 static void ws_alloc(const orc_ctx* c, dae_ws* w) {
@@ -1007,10 +1038,13 @@ static void ws_alloc(const orc_ctx* c, dae_ws* w) {
     w->pvel = (real*)malloc(sizeof(real) * 3 * (size_t)(M->npoints + 1));
     w->pact = (int*)malloc(sizeof(int) * (size_t)(M->npoints + 1));
     w->fvals = (real*)malloc(sizeof(real) * 3 * (size_t)(M->naxes + 1));
+    w->xfull = (real*)malloc(sizeof(real) * (size_t)(2 * c->NQ + c->NZ + 1));
+    w->udot = (real*)malloc(sizeof(real) * (size_t)(c->NQ + 1));
 }
 static void ws_free(dae_ws* w) {
     free(w->R); free(w->p); free(w->V); free(w->A); free(w->F); free(w->S); free(w->I);
     free(w->M); free(w->tau); free(w->ppos); free(w->pvel); free(w->pact); free(w->fvals);
+    free(w->xfull); free(w->udot);
 }
 
 /* Forward kinematics, velocities and velocity-product accelerations in the
@@ -1216,13 +1250,58 @@ static void apply_point_force(const orc_ctx* c, dae_ws* w, const real* q, int i,
  * MocoCasOCProblem.h:245-297: residual = the mobility forces
  * findMotionForces needs for udot = w, i.e. M w + C - f_applied, computed by
  * RNEA with the accelerations included). */
+/* Value and first / second derivative of a table column (the prescribed
+ * q(t), u = dq/dt, udot = d2q/dt2 of PositionMotion, PositionMotion.cpp:
+ * 36-70: calcValue and calcDerivative of the same spline). */
+static void table_eval_d(const orc_ctx* c, int ti, int col, real t, real* v, real* d1, real* d2) {
+    const mh_table* T = &c->tabs[ti];
+    const double* br = c->brk + T->break_begin;
+    int s;
+    if (t <= br[0]) s = 0;
+    else if (t >= br[T->nseg]) s = T->nseg - 1;
+    else {
+        int lo = 0, hi = T->nseg;
+        while (hi - lo > 1) {
+            int mid = (lo + hi) / 2;
+            if (t < br[mid]) hi = mid; else lo = mid;
+        }
+        s = lo;
+    }
+    const double* cf = c->coef + T->coef_begin + ((int64_t)s * T->ncol + col) * (T->degree + 1);
+    real dt = t - br[s];
+    real p = cf[T->degree], dp = 0.0, ddp = 0.0;
+    for (int k = T->degree - 1; k >= 0; --k) {
+        ddp = ddp * dt + 2.0 * dp;
+        dp = dp * dt + p;
+        p = p * dt + cf[k];
+    }
+    *v = p; *d1 = dp; *d2 = ddp;
+}
+
+static void eval_dae_full(const orc_ctx* c, dae_ws* w, real time, const real* x,
+        const real* ctrl, const real* wacc, real* out);
+
+/* The DAE callback on NLP inputs: explicit / implicit mode pass through;
+ * prescribed kinematics assemble [q, u, z] and udot from the motion. */
 static void eval_dae_point(const orc_ctx* c, dae_ws* w, real time, const real* x,
         const real* ctrl, real* out) {
+    if (!c->presc) {
+        eval_dae_full(c, w, time, x, ctrl, c->implicit ? ctrl + c->NC : NULL, out);
+        return;
+    }
+    int NQ = c->NQ;
+    for (int j = 0; j < NQ; ++j)
+        table_eval_d(c, c->kin_table, c->kin_col[j], time, &w->xfull[j], &w->xfull[NQ + j], &w->udot[j]);
+    for (int k = 0; k < c->NZ; ++k) w->xfull[2 * NQ + k] = x[k];
+    eval_dae_full(c, w, time, w->xfull, ctrl, w->udot, out);
+}
+
+static void eval_dae_full(const orc_ctx* c, dae_ws* w, real time, const real* x,
+        const real* ctrl, const real* wacc, real* out) {
     const mh_model* Mo = &c->P.model;
     int NQ = c->NQ;
     const real* q = x;
     const real* u = x + NQ;
-    const real* wacc = c->implicit ? ctrl + c->NC : NULL;
     kinematics(c, q, u, wacc, w);
     path_points(c, q, u, w);
     /* Body inertias in ground about the origin; RNEA body forces. */
@@ -1434,7 +1513,7 @@ static void gather_point(const orc_ctx* c, const double* x, int k, double* st, d
  * outputs for the rest. xd: NS x G (grid-major); res: NQ x G multibody
  * residuals (implicit mode, else unused). */
 static void all_xdot(orc_ctx* c, const double* x, const double* times, double* xd, double* res) {
-    int NS = c->NS, NC = c->NC, NQ = c->NQ, NO = nout(c), NR = nres(c);
+    int NS = c->NS, NC = c->NC, NO = nout(c), NR = nres(c);
 #pragma omp parallel num_threads(c->nthreads)
     {
         dae_ws w;
@@ -1446,12 +1525,14 @@ static void all_xdot(orc_ctx* c, const double* x, const double* times, double* x
         for (int k = 0; k < c->G; ++k) {
             gather_point(c, x, k, st, ct);
             double* o = xd + (int64_t)k * NS;
-            for (int j = 0; j < NQ; ++j) o[j] = st[NQ + j];
+            int TQ = c->TQ;
             eval_dae_point(c, &w, times[k], st, ct, y);
-            if (c->implicit) for (int j = 0; j < NQ; ++j) o[NQ + j] = ct[NC + j];
-            else for (int j = 0; j < NQ; ++j) o[NQ + j] = y[j];
+            for (int s = 0; s < NS; ++s) {
+                if (s < TQ) o[s] = st[TQ + s];                          /* qdot = u */
+                else if (c->NACC && s < 2 * TQ) o[s] = ct[NC + s - TQ];  /* udot = w */
+                else o[s] = y[s + c->SO];                               /* callback */
+            }
             for (int r = 0; r < NR; ++r) res[(int64_t)k * NR + r] = y[res_out(c, r)];
-            for (int z = 0; z < c->NZ; ++z) o[2 * NQ + z] = y[NQ + z];
         }
         free(st);
         ws_free(&w);
@@ -1722,10 +1803,10 @@ static void path_blocks(const orc_ctx* c, const double* x, const double* times, 
 /* Derivative of xdot[s] at grid point k along direction d (0=t0, 1=tf,
  * 2+j = input j).  For s < NQ, qdot = u exactly. */
 static double xdot_deriv(const orc_ctx* c, const double* D, int k, int s, int d) {
-    int NQ = c->NQ, NO = nout(c), ND = c->NP + 2;
+    int NQ = c->TQ, NO = nout(c), ND = c->NP + 2;
     if (s < NQ) return (d == 2 + NQ + s) ? 1.0 : 0.0;
-    if (c->implicit && s < 2 * NQ) return (d == 2 + c->NS + c->NC + (s - NQ)) ? 1.0 : 0.0;
-    return D[((int64_t)k * ND + d) * NO + (s - NQ)];
+    if (c->NACC && s < 2 * NQ) return (d == 2 + c->NS + c->NC + (s - NQ)) ? 1.0 : 0.0;
+    return D[((int64_t)k * ND + d) * NO + (s + c->SO)];
 }
 
 /* Map a Jacobian column to (grid point, direction) for an interval row. */

@@ -29,6 +29,11 @@ def _sparse(st, mode="random"):
     return st
 
 
+def _trap(st):
+    st.solver.transcription_scheme = "trapezoidal"
+    return st
+
+
 def _physiological_guess(st):
     """initial-guess detection at the bounds midpoint with activations 0.5
     and normalized tendon forces 0.1 (a regular point of the DGF model)."""
@@ -100,6 +105,12 @@ CASES = {
     "gait_inverse_style_sparse": lambda: _physiological_guess(configs.gait10dof18musc(
         4, tendon_compliance=True, tendon_dynamics="implicit", dynamics="implicit",
         control_bounds=True)),
+    # MocoInverse (configs[4]): prescribed kinematics (PositionMotion), implicit
+    # tendons, residual rows only for the multibody dynamics
+    "gait_inverse": lambda: configs.gait10dof18musc_inverse(4, sparsity="none"),
+    "gait_inverse_central_trap": lambda: _trap(configs.gait10dof18musc_inverse(
+        5, fd_scheme="central", sparsity="none")),
+    "gait_inverse_sparse": lambda: _physiological_guess(configs.gait10dof18musc_inverse(4)),
 }
 
 
@@ -170,9 +181,9 @@ def _row_mask(ref, x):
     hs = ref.opts.transcription == 0
     step = 2 if hs else 1
     rpi, tail = _rows(ref)
-    nres, npc, nacc = ref.NRES, ref.NPC, ref.NACC
+    nres, npc, nacc, nmb = ref.NRES, ref.NPC, ref.NACC, ref.NMB
     # residual row r of a grid point -> its callback output
-    rout = [r if r < nacc else ref.NO - ref.NAR + (r - nacc) for r in range(nres)]
+    rout = [r if r < nmb else ref.NO - ref.NAR + (r - nmb) for r in range(nres)]
     npres = step if nres else 0
     mask = np.ones((N, rpi), bool)
     ndef = 2 * NS if hs else NS
@@ -180,10 +191,11 @@ def _row_mask(ref, x):
         ok = R[i * step:i * step + step + 1].all(0)
         for row in range(npres * nres):
             mask[i, npc + row] = R[i * step + row // nres, rout[row % nres]]
+        TQ = ref.TQ
         for row in range(ndef):
             s = row % NS
-            if s >= (2 * NQ if nacc else NQ):
-                mask[i, npc + npres * nres + row] = ok[s - NQ]
+            if s >= (2 * TQ if nacc else TQ):
+                mask[i, npc + npres * nres + row] = ok[s + ref.SO]
     return np.concatenate([mask.reshape(-1), np.ones(npc, bool), R[-1, rout]])
 
 
@@ -303,7 +315,7 @@ def _interval_scale(ref, x):
     """(F_i, h_i) per mesh interval from the oracle's DAE at the grid."""
     P = _points(ref, x)
     Y = ref.eval_dae(P)
-    u = np.abs(P[:, 1 + ref.NQ:1 + 2 * ref.NQ]).max(1) if ref.NQ else 0
+    u = np.abs(P[:, 1 + ref.TQ:1 + 2 * ref.TQ]).max(1) if ref.TQ else 0
     F = np.maximum(_scale(Y).max(1), u)
     hs = ref.opts.transcription == 0
     N = ref.opts.num_mesh_intervals
@@ -393,7 +405,8 @@ def test_objective_and_gradient(name):
 @pytest.mark.parametrize("name", ["double_pendulum_hs", "gait_rigid_forward", "double_pendulum_implicit_hs",
                                   "gait_rigid_implicit", "gait_rigid_pathcon",
                                   "pendulum_bound_both_implicit", "gait_rigid_sparse_random",
-                                  "gait_implicit_pathcon_sparse", "gait_inverse_style_sparse"])
+                                  "gait_implicit_pathcon_sparse", "gait_inverse_style_sparse",
+                                  "gait_inverse_sparse"])
 def test_shards_reassemble_bit_exact(name):
     """Mesh-interval shards (the multi-GPU partition) concatenate to exactly
     the unsharded g and Jacobian values."""

@@ -710,3 +710,71 @@ def test_implicit_tendon_layout_bounds_and_jacobian(scheme):
     Jn = _numjac(nlp.eval_g, x, cols, h=1e-5)
     noise = 100 * np.finfo(float).eps * np.abs(nlp.eval_g(x)).max() / st.solver.fd_step
     assert np.allclose(J[:, cols], Jn, rtol=1e-4, atol=max(1e-5, noise))
+
+
+# --------------------------------------------------------------------------
+# Prescribed kinematics: PositionMotion / MocoInverse.
+# --------------------------------------------------------------------------
+def test_prescribed_kinematics_layout_and_equivalence():
+    """With a PositionMotion the coordinates are not NLP states
+    (MocoProblemRep.cpp:541-555), there are no acceleration variables and
+    every grid point has nq multibody residual rows (CasOCProblem.h:486-503)
+    plus the implicit tendon residuals.  The callback equals the implicit
+    one evaluated at q(t), dq/dt, d2q/dt2 of the same spline (PositionMotion
+    .cpp:36-70), bit for bit."""
+    from mocohip.splines import gcv_interpolating_ppoly
+    N = 3
+    inv = configs.gait10dof18musc_inverse(N, sparsity="none")
+    rep = inv.problem.create_rep()
+    nlp = OracleNLP(rep, inv.solver.options())
+    assert all(not (n.endswith("/value") or n.endswith("/speed")) for n in rep.state_names)
+    NZ, NC, G, NQ = nlp.NS, nlp.NC, nlp.G, nlp.NQ
+    assert (nlp.TQ, nlp.NACC, nlp.NMB, nlp.NAR) == (0, 0, NQ, 18)
+    assert nlp.n == 2 + (NZ + NC + 18) * G
+    rpi = 2 * (NQ + 18) + 2 * NZ + NC
+    assert nlp.m == N * rpi + NQ + 18
+    # the equivalent implicit problem (q, u states, accelerations)
+    imp = configs.gait10dof18musc(N, tendon_compliance=True, tendon_dynamics="implicit",
+                                  dynamics="implicit")
+    irep = imp.problem.create_rep()
+    inlp = OracleNLP(irep, imp.solver.options())
+    kin = inv.problem.position_motion
+    qpaths = [c.path + "/value" for c in inv.problem.model.coordinates()]
+    br, cf = gcv_interpolating_ppoly(kin.times, np.stack([kin.columns[q] for q in qpaths], 1), 5)
+    t = 0.731
+    s = np.clip(np.searchsorted(br, t, side="right") - 1, 0, len(br) - 2)
+    dt = t - br[s]
+    pw = np.array([dt ** k for k in range(6)])
+    q = cf[s] @ pw
+    u = cf[s] @ np.array([k * dt ** (k - 1) if k else 0.0 for k in range(6)])
+    w = cf[s] @ np.array([k * (k - 1) * dt ** (k - 2) if k > 1 else 0.0 for k in range(6)])
+    z = np.where([n.endswith("activation") for n in rep.state_names], 0.4, 0.12)
+    ctl = np.random.default_rng(1).uniform(0.0, 0.3, NC)
+    dft = np.random.default_rng(2).uniform(-0.5, 0.5, 18)
+    Yp = nlp.eval_dae(np.concatenate([[t], z, ctl, dft])[None, :])[0]
+    Yi = inlp.eval_dae(np.concatenate([[t], q, u, z, ctl, w, dft])[None, :])[0]
+    assert np.allclose(Yp, Yi, rtol=1e-10, atol=1e-8 * max(1.0, np.abs(Yi).max()))
+    with pytest.raises(RuntimeError, match="requires implicit"):
+        inv.solver.multibody_dynamics_mode = "explicit"
+        OracleNLP(rep, inv.solver.options())
+
+
+def test_prescribed_kinematics_jacobian_matches_numerical_derivative():
+    inv = configs.gait10dof18musc_inverse(2, sparsity="none")
+    rep = inv.problem.create_rep()
+    nlp = OracleNLP(rep, inv.solver.options())
+    x = nlp.initial_guess_from_bounds()
+    G, NZ, NC = nlp.G, nlp.NS, nlp.NC
+    S = x[2:2 + NZ * G].reshape(G, NZ)
+    for i, n in enumerate(rep.state_names):
+        S[:, i] = 0.5 if n.endswith("/activation") else 0.1
+    x[2 + NZ * G:2 + (NZ + NC) * G] = np.random.default_rng(4).uniform(0.05, 0.3, NC * G)
+    d0 = 2 + (NZ + NC) * G
+    x[d0:] = np.random.default_rng(5).uniform(-0.3, 0.3, nlp.n - d0)
+    ir, jc = nlp.jac_structure()
+    J = np.zeros((nlp.m, nlp.n))
+    J[ir, jc] = nlp.eval_jac_g(x)
+    cols = sorted(set(range(0, nlp.n, 5)) | {0, 1, d0, nlp.n - 1})
+    Jn = _numjac(nlp.eval_g, x, cols, h=1e-5)
+    noise = 100 * np.finfo(float).eps * np.abs(nlp.eval_g(x)).max() / inv.solver.fd_step
+    assert np.allclose(J[:, cols], Jn, rtol=1e-4, atol=max(1e-5, noise))
