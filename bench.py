@@ -55,6 +55,10 @@ def parse():
     ap.add_argument("--single-mode", action="store_true",
                     help="measure only --mode (no secondary mode, no batch): for profiler runs, so "
                          "that every launch of a kernel has the same shape")
+    ap.add_argument("--inverse-batch", type=int, default=8,
+                    help="also measure B MocoInverse NLPs per GPU (configs[4]: prescribed "
+                         "kinematics, implicit tendons, random sparsity, mesh_interval 0.02 s), "
+                         "0 = skip")
     ap.add_argument("--batch", type=int, default=8,
                     help="also measure B independent NLPs per GPU evaluated concurrently, one "
                          "context (HIP stream) and host thread each (the configs[4] batch layout); "
@@ -201,6 +205,17 @@ def main():
     batch = None
     if args.batch > 1 and not mesh and not args.single_mode:
         batch = batch_throughput(args, rep, st, local, rank, world, dev, torch, dist)
+    inverse = None
+    if args.inverse_batch > 0 and not mesh and not args.single_mode:
+        # MocoTool mesh_interval 0.02 s: ceil((2.499 - 0.001) / 0.02) = 125
+        # intervals (MocoTool.cpp:27,68-69)
+        ist = configs.gait10dof18musc_inverse(125, fd_scheme="forward", sparsity="random")
+        ist.solver.device = local
+        irep = ist.problem.create_rep()
+        inverse = batch_throughput(args, irep, ist, local, rank, world, dev, torch, dist,
+                                   B=args.inverse_batch, make_x=inverse_iterate)
+        inverse["workload"] = ("MocoInverse gait10dof18musc (configs[4]): PositionMotion, implicit DGF "
+                               "tendons, reserves, N=125, forward FD, random sparsity detection")
 
     if rank == 0:
         J = np.array(rec["jac"])          # [whole, DAE stage, transcription stage, k_groups] ms
@@ -271,6 +286,8 @@ def main():
             line["batch"] = batch
         if sparse:
             line["sparsity_random"] = sparse
+        if inverse:
+            line["inverse_batch"] = inverse
         if cpu and cpu.get("value"):
             line["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 2)
         print(json.dumps(line), flush=True)
@@ -278,20 +295,44 @@ def main():
         dist.destroy_process_group()
 
 
-def batch_throughput(args, rep, st, local, rank, world, dev, torch, dist):
+def track_iterate(nlp, seed):
+    """Bounds-midpoint states (where the muscle model is regular), uniform
+    random controls within bounds."""
+    x = nlp.random_iterate(np.random.default_rng(seed).uniform(-1, 1, nlp.n))
+    xm = nlp.initial_guess_from_bounds()
+    x[2:2 + nlp.NS * nlp.G] = xm[2:2 + nlp.NS * nlp.G]
+    return x
+
+
+def inverse_iterate(nlp, seed):
+    """MocoInverse iterate: activations and normalized tendon forces in their
+    physiological range, random excitations / reserves and tendon-force
+    derivatives (a regular point of the DGF model)."""
+    r = np.random.default_rng(seed)
+    x = nlp.initial_guess_from_bounds()
+    G, NS, NC = nlp.G, nlp.NS, nlp.NC
+    S = x[2:2 + NS * G].reshape(G, NS)
+    for i, n in enumerate(nlp.rep.state_names):
+        S[:, i] = r.uniform(0.2, 0.6, G) if n.endswith("/activation") else r.uniform(0.05, 0.3, G)
+    x[2 + NS * G:2 + (NS + NC) * G] = r.uniform(0.05, 0.4, NC * G)
+    d0 = 2 + (NS + NC) * G
+    x[d0:] = r.uniform(-0.5, 0.5, nlp.n - d0)
+    return x
+
+
+def batch_throughput(args, rep, st, local, rank, world, dev, torch, dist, B=None,
+                     make_x=track_iterate):
     """B independent NLPs of the same workload per GPU (different iterates),
     each on its own context / HIP stream and driven by its own host thread
     (ctypes releases the GIL inside the C ABI calls): aggregate eval_g +
     eval_jac_g calls/s over all NLPs and ranks."""
     from concurrent.futures import ThreadPoolExecutor
     from mocohip.solver import HipNLP
-    B = args.batch
+    B = B or args.batch
     items = []
     for b in range(B):
         nlp = HipNLP(rep, st.solver.options())
-        x = nlp.random_iterate(np.random.default_rng(1000 + rank * B + b).uniform(-1, 1, nlp.n))
-        xm = nlp.initial_guess_from_bounds()
-        x[2:2 + nlp.NS * nlp.G] = xm[2:2 + nlp.NS * nlp.G]
+        x = make_x(nlp, 1000 + rank * B + b)
         xd = torch.tensor(x, dtype=torch.float64, device=dev)
         gd = torch.zeros(nlp.m, dtype=torch.float64, device=dev)
         vd = torch.zeros(nlp.nnz, dtype=torch.float64, device=dev)
@@ -321,10 +362,12 @@ def batch_throughput(args, rep, st, local, rank, world, dev, torch, dist):
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
+    be = items[0][0].backend()[0] if items else None
     for nlp, *_ in items:
         nlp.close()
     return {"nlps_per_gpu": B, "value": round(B * world * args.steps / el, 3), "unit": "calls/s",
-            "mode": args.mode, "layout": "one context (HIP stream) + host thread per NLP"}
+            "mode": args.mode, "layout": "one context (HIP stream) + host thread per NLP",
+            "backend": be}
 
 
 def cpu_baseline(rep, opts, x, budget_s):

@@ -2826,8 +2826,12 @@ extern "C" int mh_get_work(const mh_ctx* c, double* work4) {
 // multibody dynamics (a different DAE: residual outputs, acceleration
 // inputs, no mass-matrix factor).
 constexpr uint64_t kImplicitSalt = 0x9e3779b97f4a7c15ULL;
-static uint64_t backend_key(uint64_t model_hash, bool implicit) {
-    return implicit ? model_hash ^ kImplicitSalt : model_hash;
+constexpr uint64_t kPrescribedSalt = 0xc2b2ae3d27d4eb4fULL;
+// implicit: residual outputs with acceleration inputs; prescribed: residual
+// outputs with the PositionMotion's q, u, udot (implicit tendons are part of
+// the model hash through mh_muscle)
+static uint64_t backend_key(uint64_t model_hash, bool implicit, bool prescribed) {
+    return model_hash ^ (implicit ? kImplicitSalt : 0) ^ (prescribed ? kPrescribedSalt : 0);
 }
 
 static const Backend* select_backend(mh_ctx* c, const mh_problem* p) {
@@ -2835,8 +2839,8 @@ static const Backend* select_backend(mh_ctx* c, const mh_problem* p) {
     const char* force = std::getenv("MOCOHIP_BACKEND");
     const bool generic = force && std::strcmp(force, "generic") == 0;
     const bool lane = force && std::strcmp(force, "lane") == 0;
-    if (!generic && !c->presc) {   // no generated back end for prescribed kinematics
-        const uint64_t key = backend_key(c->model_hash, c->NACC > 0);
+    if (!generic) {
+        const uint64_t key = backend_key(c->model_hash, c->NMB > 0, c->presc != 0);
         for (const GenEntry& e : kGeneratedModels)
             if (e.hash == key) return lane ? &e.lane : &e.tasks;
     }

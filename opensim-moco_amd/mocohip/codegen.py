@@ -254,15 +254,23 @@ def _uniform_guess(br):
 
 
 class _Layout:
-    def __init__(self, M: ModelView, implicit: bool = False):
+    def __init__(self, M: ModelView, implicit: bool = False, prescribed: bool = False):
         NQ = M.nq
         z = 2 * NQ
         self.act_state, self.ftn_state = [], []
         self.mus_control = [-1] * len(M.muscles)
         self.tau_act = self.tau_deact = None
-        for mu in M.muscles:
+        # prescribed kinematics: q, u, udot from the PositionMotion table
+        # (implicit mode only); the NLP states are the auxiliary states
+        self.prescribed = prescribed
+        implicit = implicit or prescribed
+        self.NACC = NQ if implicit and not prescribed else 0
+        self.ider = [-1] * len(M.muscles)   # implicit tendon: derivative input after the controls
+        nar = 0
+        for im, mu in enumerate(M.muscles):
             if mu.tendon_dynamics_implicit and not mu.ignore_tendon_compliance:
-                raise NotImplementedError("implicit tendon dynamics")
+                self.ider[im] = self.NACC + nar
+                nar += 1
             self.act_state.append(-1 if mu.ignore_activation_dynamics else z)
             z += 0 if mu.ignore_activation_dynamics else 1
             self.ftn_state.append(-1 if mu.ignore_tendon_compliance else z)
@@ -270,17 +278,24 @@ class _Layout:
             if not mu.ignore_activation_dynamics and self.tau_act is None:
                 self.tau_act = mu.activation_time_constant
                 self.tau_deact = mu.deactivation_time_constant
-        self.NQ, self.NS, self.NC = NQ, z, len(M.acts)
+        self.NQ, self.NC = NQ, len(M.acts)
         self.NZ = z - 2 * NQ
-        self.NO = NQ + self.NZ
+        self.NS = self.NZ if prescribed else z          # NLP states
+        self.NAR = nar
+        self.NO = NQ + self.NZ + nar
         # implicit multibody dynamics: the generalized accelerations are
-        # point inputs after the controls; outputs [residual, zdot]
+        # point inputs after the controls, then the implicit auxiliary
+        # derivatives; outputs [residual, zdot, auxiliary residuals]
         self.implicit = implicit
-        self.NDV = NQ if implicit else 0
+        self.NDV = self.NACC + nar
         self.NI = self.NS + self.NC + self.NDV
         for ia, a in enumerate(M.acts):
             if a.kind == abi.MH_ACT_MUSCLE:
                 self.mus_control[a.target] = ia
+
+    def sin(self, s_full: int) -> int:
+        """Point-input index of full-state index s_full ([q, u, z])."""
+        return s_full - 2 * self.NQ if self.prescribed else s_full
 
 
 class _Emitter:
@@ -290,10 +305,16 @@ class _Emitter:
         self.M, self.Lo = M, Lo
         self.g = Gen()
         self.inp = [S(n=f"in[{i}]") for i in range(Lo.NI)]
-        self.q = self.inp[:Lo.NQ]
-        self.u = self.inp[Lo.NQ:2 * Lo.NQ]
+        if Lo.prescribed:
+            # the motion's q, dq/dt, d2q/dt2 (declared by _presc_prelude)
+            self.q = [S(n=f"pq{j}") for j in range(Lo.NQ)]
+            self.u = [S(n=f"pu{j}") for j in range(Lo.NQ)]
+            self.wacc = [S(n=f"pw{j}") for j in range(Lo.NQ)]
+        else:
+            self.q = self.inp[:Lo.NQ]
+            self.u = self.inp[Lo.NQ:2 * Lo.NQ]
+            self.wacc = self.inp[Lo.NS + Lo.NC:Lo.NS + Lo.NC + Lo.NACC] if Lo.implicit else None
         self.ctrl = self.inp[Lo.NS:Lo.NS + Lo.NC]
-        self.wacc = self.inp[Lo.NS + Lo.NC:Lo.NI] if Lo.implicit else None
         self.fcache: Dict[int, Tuple[S, S, S]] = {}
         self.touched = set()
 
@@ -446,7 +467,7 @@ class _Emitter:
         self.g.raw(f"{name} {'+=' if sign > 0 else '-='} {val};")
         self.g.flops["add"] += 1
 
-    def muscle(self, im, R, P, V, Facc, tau, zdot_sink, with_adot: bool = True):
+    def muscle(self, im, R, P, V, Facc, tau, zdot_sink, with_adot: bool = True, resid_sink=None):
         """Path geometry, DGF and tension point forces of muscle im.  Point
         forces are subtracted into the body accumulators Facc (RNEA sign
         convention), MovingPathPoint terms added into tau; zdot values are
@@ -503,14 +524,18 @@ class _Emitter:
             seginfo.append((j, i, d, l, ind))
         exc = self.ctrl[Lo.mus_control[im]]
         sa, sf = Lo.act_state[im], Lo.ftn_state[im]
-        a_ = self.inp[sa] if sa >= 0 else exc
-        ftn = self.inp[sf] if sf >= 0 else None
-        T, adot, ftdot = _dgf(g, mu, L, Sp, a_, exc, sa >= 0 and with_adot, ftn, sf >= 0,
-                              Lo.tau_act, Lo.tau_deact)
+        a_ = self.inp[Lo.sin(sa)] if sa >= 0 else exc
+        ftn = self.inp[Lo.sin(sf)] if sf >= 0 else None
+        idv = Lo.ider[im]
+        dft = self.inp[Lo.NS + Lo.NC + idv] if idv >= 0 else None
+        T, adot, ftdot, resid = _dgf(g, mu, L, Sp, a_, exc, sa >= 0 and with_adot, ftn, sf >= 0,
+                                     Lo.tau_act, Lo.tau_deact, dft)
         if sa >= 0 and with_adot:
             zdot_sink(sa, adot)
         if sf >= 0:
             zdot_sink(sf, ftdot)
+        if resid is not None and resid_sink is not None:
+            resid_sink(idv - Lo.NACC, resid)
         for (j, i, d, l, ind) in seginfo:
             Tl = g.div(T, l) if ind is None else g.mul(ind, g.div(T, l))
             Fv = g.vscale(d, Tl)
@@ -685,9 +710,11 @@ def _multibody_front(E: _Emitter, with_muscles: bool):
     tau = [g.var(_c(0.0)) for _ in range(Lo.NQ)]
     E.actuators(tau)
     zd = {}
+    E.resid = {}
     if with_muscles:
         for im in range(len(M.muscles)):
-            E.muscle(im, R, P, V, Facc, tau, lambda s, v: zd.__setitem__(s, v))
+            E.muscle(im, R, P, V, Facc, tau, lambda s, v: zd.__setitem__(s, v),
+                     resid_sink=lambda k, v: E.resid.__setitem__(k, v))
     E.external_forces(P, Facc)
     E.backward(allb, Facc, Sj, coord_body, tau)
     if Lo.implicit:
@@ -696,7 +723,18 @@ def _multibody_front(E: _Emitter, with_muscles: bool):
     return tau, lam, H, zd
 
 
-def generate(cm, struct_name: str, implicit: bool = False) -> Tuple[str, Dict]:
+_PRESC_RE = re.compile(r"\bp[quw](\d+)\b")
+
+
+def _presc_prelude(lines):
+    """Declarations of the prescribed q_j, u_j, udot_j the lines use: one
+    spline evaluation (value, first and second derivative) per coordinate."""
+    used = sorted({int(m) for l in lines for m in _PRESC_RE.findall(l)})
+    return [f"double pq{j}, pu{j}, pw{j}; mh::table_eval_d(M, M.kin_table, M.kin_col[{j}], t, "
+            f"pq{j}, pu{j}, pw{j});" for j in used]
+
+
+def generate(cm, struct_name: str, implicit: bool = False, prescribed: bool = False) -> Tuple[str, Dict]:
     """Return (C++ source of `struct <struct_name>`, info dict).
 
     The struct has
@@ -709,10 +747,11 @@ def generate(cm, struct_name: str, implicit: bool = False) -> Tuple[str, Dict]:
     plus the group metadata (fields, inputs read, time dependence, FP64 op
     counts) the host uses to build the task tables."""
     M = ModelView(cm)
-    Lo = _Layout(M, implicit)
+    Lo = _Layout(M, implicit, prescribed)
+    implicit = Lo.implicit
     NQ, NZ = Lo.NQ, Lo.NZ
     parts = []
-    info = {"NQ": NQ, "NS": Lo.NS, "NC": Lo.NC, "implicit": implicit}
+    info = {"NQ": NQ, "NS": Lo.NS, "NC": Lo.NC, "implicit": implicit, "prescribed": prescribed}
 
     # ---- single-lane eval ---------------------------------------------------
     E = _Emitter(M, Lo)
@@ -726,12 +765,14 @@ def generate(cm, struct_name: str, implicit: bool = False) -> Tuple[str, Dict]:
         E.g.raw(f"out[{i}] = {xs[i]};")
     for zi in range(NZ):
         E.g.raw(f"out[{NQ + zi}] = {zd.get(2 * NQ + zi, _c(0.0))};")
+    for k in range(Lo.NAR):
+        E.g.raw(f"out[{NQ + NZ + k}] = {E.resid[k]};")
     fl = dict(E.g.flops)
     fl["total"] = sum(fl.values())
     info["flops"] = fl
     info["lines"] = len(E.g.lines)
     parts.append(("eval", "const mh::DevModel& M, const double t, const double* __restrict__ in, "
-                          "double* __restrict__ out", E.g.lines))
+                          "double* __restrict__ out", _presc_prelude(E.g.lines) + E.g.lines))
 
     # ---- task decomposition ------------------------------------------------
     groups = _emit_groups(M, Lo)
@@ -772,6 +813,7 @@ def generate(cm, struct_name: str, implicit: bool = False) -> Tuple[str, Dict]:
     src = f"""struct {struct_name} {{
     static constexpr int NQ = {NQ}, NZ = {NZ}, NS = {Lo.NS}, NC = {Lo.NC}, NO = {Lo.NO}, NI = {Lo.NI};
     static constexpr bool IMPLICIT = {"true" if implicit else "false"};
+    static constexpr bool PRESCRIBED = {"true" if prescribed else "false"};
     static constexpr int MI = NI, MO = NO;
     static constexpr double FLOPS_PER_EVAL = {float(fl['total'])};
     // task decomposition: group 0 = mass matrix factor (NST values), groups
@@ -843,7 +885,7 @@ def _emit_groups(M: ModelView, Lo: _Layout) -> List[_Group]:
         g0.lam = lam
         out.append(g0)
 
-    def finish(Eg, name, tv, zf=None):
+    def finish(Eg, name, tv, zf=None, rf=None):
         fields = []
         for j in range(NQ):
             if tv[j] in Eg.touched:
@@ -852,8 +894,12 @@ def _emit_groups(M: ModelView, Lo: _Layout) -> List[_Group]:
         if zf is not None:
             Eg.g.raw(f"out[{len(fields)}] = {zf[1]};")
             fields.append(("z", zf[0]))
-        r, t = _reads_of(Eg.g.lines)
-        out.append(_Group(name, Eg.g.lines, fields, r, t, sum(Eg.g.flops.values())))
+        if rf is not None:     # implicit tendon: the equilibrium residual
+            Eg.g.raw(f"out[{len(fields)}] = {rf[1]};")
+            fields.append(("r", rf[0]))
+        lines = _presc_prelude(Eg.g.lines) + Eg.g.lines
+        r, t = _reads_of(lines)
+        out.append(_Group(name, lines, fields, r, t, sum(Eg.g.flops.values())))
 
     # bias
     E = _Emitter(M, Lo)
@@ -887,7 +933,8 @@ def _emit_groups(M: ModelView, Lo: _Layout) -> List[_Group]:
         if sa < 0:
             continue
         E = _Emitter(M, Lo)
-        adot = _activation_dot(E.g, E.inp[sa], E.ctrl[Lo.mus_control[im]], Lo.tau_act, Lo.tau_deact)
+        adot = _activation_dot(E.g, E.inp[Lo.sin(sa)], E.ctrl[Lo.mus_control[im]], Lo.tau_act,
+                               Lo.tau_deact)
         E.g.raw(f"out[0] = {adot};")
         r, t = _reads_of(E.g.lines)
         out.append(_Group(f"activation_{im}", E.g.lines, [("z", sa - 2 * NQ)], r, t,
@@ -902,13 +949,15 @@ def _emit_groups(M: ModelView, Lo: _Layout) -> List[_Group]:
         R, P, V, _, Sj, cb = E.kinematics(cl, accel=False)
         Facc = E.body_force_vars(cl, None)
         tv = [E.g.var(_c(0.0)) for _ in range(NQ)]
-        zs = {}
-        E.muscle(im, R, P, V, Facc, tv, lambda si, v: zs.__setitem__(si, v), with_adot=False)
+        zs, rs = {}, {}
+        E.muscle(im, R, P, V, Facc, tv, lambda si, v: zs.__setitem__(si, v), with_adot=False,
+                 resid_sink=lambda k, v: rs.__setitem__(k, v))
         E.backward(cl, Facc, Sj, cb, tv)
         zf = None
         if Lo.ftn_state[im] >= 0:
             zf = (Lo.ftn_state[im] - 2 * NQ, zs[Lo.ftn_state[im]])
-        finish(E, f"muscle_{im}", tv, zf)
+        rf = next(iter(rs.items()), None)
+        finish(E, f"muscle_{im}", tv, zf, rf)
     return out
 
 
@@ -948,6 +997,8 @@ def _emit_combine(M: ModelView, Lo: _Layout, groups: List[_Group]):
         for f, (kind, zi) in enumerate(gr.fields):
             if kind == "z":
                 g.raw(f"out[{NQ + zi}] = T({gi}, {f});")
+            elif kind == "r":
+                g.raw(f"out[{NQ + Lo.NZ + zi}] = T({gi}, {f});")
     return g.lines, sum(g.flops.values())
 
 
@@ -965,8 +1016,10 @@ def _activation_dot(g: Gen, act: S, exc: S, tau_act, tau_deact) -> S:
 
 
 def _dgf(g: Gen, mu, LMT: S, VMT: S, act: S, exc: S, has_act: bool, ftn: Optional[S],
-         compliant: bool, tau_act, tau_deact):
-    """DeGrooteFregly2016Muscle (DeGrooteFregly2016Muscle.cpp:186-425)."""
+         compliant: bool, tau_act, tau_deact, dft: Optional[S] = None):
+    """DeGrooteFregly2016Muscle (DeGrooteFregly2016Muscle.cpp:186-425).  dft:
+    the normalized tendon force derivative input of implicit tendon dynamics
+    (returns the equilibrium residual FT - FM cos(alpha), .cpp:826-848)."""
     c1, c2, c3 = 0.2, 1.0, 0.2
     d1, d2, d3, d4 = -0.3211346127989808, -8.149, -0.374, 0.8825327733249912
     lopt, lts, Fmax = mu.optimal_fiber_length, mu.tendon_slack_length, mu.max_isometric_force
@@ -1002,7 +1055,7 @@ def _dgf(g: Gen, mu, LMT: S, VMT: S, act: S, exc: S, has_act: bool, ftn: Optiona
     fAL = g.add(g.add(gl(0.8150671134243542, 1.055033428970575, 0.162384573599574, 0.063303448465465),
                       gl(0.433004984392647, 0.716775413397760, -0.029947116970696, 0.200356847296188)),
                 gl(0.1, 1.0, 0.353553390593274, 0.0))
-    if compliant:
+    if compliant and dft is None:
         nff = g.div(ftn, cosP)
         fV = g.div(g.sub(nff, fPE), g.mul(act, fAL))
         nfv = g.div(g.sub(g.fn("sinh", g.mul(C(1.0 / d1), g.sub(fV, C(d4)))), C(d3)), C(d2))
@@ -1011,8 +1064,13 @@ def _dgf(g: Gen, mu, LMT: S, VMT: S, act: S, exc: S, has_act: bool, ftn: Optiona
         tendonVelocity = g.sub(VMT, fvat)
         ntv = g.div(tendonVelocity, C(lts))
     else:
-        ntv = C(0.0)
-        fvat = VMT
+        if dft is not None:
+            # calcTendonForceLengthInverseCurveDerivative (.h:471-476)
+            ntv = g.div(dft, g.mul(C(c1 * kT), g.fn("exp", g.mul(C(kT), g.sub(ntl, C(c2))))))
+            fvat = g.sub(VMT, g.mul(C(lts), ntv))
+        else:
+            ntv = C(0.0)
+            fvat = VMT
         fiberVelocity = g.mul(fvat, cosP)
         nfv = g.div(fiberVelocity, C(vmax))
         tv = g.add(g.mul(C(d2), nfv), C(d3))
@@ -1026,6 +1084,10 @@ def _dgf(g: Gen, mu, LMT: S, VMT: S, act: S, exc: S, has_act: bool, ftn: Optiona
     adot = ftdot = C(0.0)
     if has_act:
         adot = _activation_dot(g, act, exc, tau_act, tau_deact)
-    if compliant:
+    resid = None
+    if compliant and dft is not None:
+        ftdot = dft
+        resid = g.sub(T, g.mul(total, cosP))
+    elif compliant:
         ftdot = g.mul(ntv, g.mul(C(c1 * kT), g.fn("exp", g.mul(C(kT), g.sub(ntl, C(c2))))))
-    return T, adot, ftdot
+    return T, adot, ftdot, resid

@@ -453,7 +453,8 @@ def test_repeatable_bitwise():
 def test_generated_backends_are_selected_for_bundled_models():
     for name in ["sliding_mass", "double_pendulum_hs", "gait_rigid_forward",
                  "gait_compliant_central", "gait_torque_driven", "sliding_mass_implicit",
-                 "double_pendulum_implicit_hs", "gait_rigid_implicit", "gait_rigid_pathcon"]:
+                 "double_pendulum_implicit_hs", "gait_rigid_implicit", "gait_rigid_pathcon",
+                 "gait_implicit_tendon", "gait_implicit_both_central", "gait_inverse"]:
         gpu, _, _ = _pair(name)
         be, flops, _ = gpu.backend()
         assert be.startswith("generated:"), (name, be)
@@ -470,7 +471,8 @@ def test_fused_g_jac_identical_to_separate_calls(name):
 
 
 @pytest.mark.parametrize("name", ["double_pendulum_hs", "gait_rigid_forward", "gait_rigid_central",
-                                  "gait_compliant_central", "gait_torque_driven", "gait_rigid_implicit"])
+                                  "gait_compliant_central", "gait_torque_driven", "gait_rigid_implicit",
+                                  "gait_implicit_tendon", "gait_inverse"])
 def test_pruned_tasks_bit_identical(name):
     """Re-evaluating only the groups a direction perturbs gives exactly the
     Jacobian of re-evaluating every group for every direction: the reused
