@@ -226,7 +226,13 @@ enum mh_goal_kind {
     MH_GOAL_CONTROL = 0,        /* MocoControlGoal                         */
     MH_GOAL_STATE_TRACKING = 1, /* MocoStateTrackingGoal                   */
     MH_GOAL_FINAL_TIME = 2,     /* MocoFinalTimeGoal                       */
-    MH_GOAL_SUM_SQUARED_STATE = 3 /* MocoSumSquaredStateGoal (no reference) */
+    MH_GOAL_SUM_SQUARED_STATE = 3, /* MocoSumSquaredStateGoal (no reference) */
+    /* minimize_implicit_auxiliary_derivatives (CasOCTranscription.cpp:534-545:
+     * weight * duration * quadrature of the sum of squared implicit auxiliary
+     * derivatives; MocoInverse sets it with weight 0.01, MocoInverse.cpp:
+     * 106-107).  Terms index the auxiliary derivatives (0 = the first one
+     * after the accelerations). */
+    MH_GOAL_AUX_DERIVATIVES = 4
 };
 typedef struct mh_goal {
     int32_t kind;

@@ -1054,6 +1054,7 @@ __device__ __forceinline__ void gather_inputs(const double* __restrict__ x, cons
 
 struct GoalSet {
     int ngoals;
+    int nc, nacc;   // controls; accelerations before the auxiliary derivatives
     const mh_goal* goals;
     const int* gidx;
     const int* gcol;
@@ -1075,6 +1076,9 @@ __device__ double goal_integrand(const DevModel& M, const GoalSet& GS, int g, do
             L += w * (d * d);
         } else if (G.kind == MH_GOAL_SUM_SQUARED_STATE) {
             const double v = st[idx];
+            L += w * (v * v);
+        } else if (G.kind == MH_GOAL_AUX_DERIVATIVES) {
+            const double v = ct[GS.nc + GS.nacc + idx];   // derivatives follow the controls
             L += w * (v * v);
         }
     }
@@ -1793,6 +1797,8 @@ static int validate_and_layout(mh_ctx* c, const mh_problem* p, const mh_options*
             return set_err(MH_ERR_INVALID, "goal %d: bad terms", g);
         if (G.kind == MH_GOAL_STATE_TRACKING && (G.table < 0 || G.table >= M.ntables))
             return set_err(MH_ERR_INVALID, "goal %d: bad table", g);
+        if (G.kind < MH_GOAL_CONTROL || G.kind > MH_GOAL_AUX_DERIVATIVES)
+            return set_err(MH_ERR_INVALID, "goal %d: unknown kind %d", g, G.kind);
     }
     for (int e = 0; e < M.nexternal; ++e) {
         const mh_external_force& E = M.external[e];
@@ -2032,6 +2038,8 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     D.mus_ftn_state = (const int*)(b + o_fs); D.mus_control = (const int*)(b + o_mc);
     D.mus_derived = (const double*)(b + o_md);
     c->GS.ngoals = p->ngoals;
+    c->GS.nc = c->NC;
+    c->GS.nacc = c->NACC;
     c->GS.goals = (const mh_goal*)(b + o_goals);
     c->GS.gidx = (const int*)(b + o_gidx);
     c->GS.gcol = (const int*)(b + o_gcol);

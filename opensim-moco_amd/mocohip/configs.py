@@ -24,7 +24,8 @@ import numpy as np
 from .model import (Body, Coordinate, CoordinateActuator, DataTable,
                     ExternalForce, Joint, Model, model_from_dict)
 from .osim import add_reserves
-from .problem import (Constant, GCVSpline, MocoControlBoundConstraint, MocoControlGoal,
+from .problem import (Constant, GCVSpline, ImplicitAuxiliaryDerivativesTerm,
+                      MocoControlBoundConstraint, MocoControlGoal,
                       MocoFinalTimeGoal, MocoProblem, MocoStateTrackingGoal,
                       PiecewiseLinearFunction)
 from .solver import MocoHipSolver, MocoStudy
@@ -213,6 +214,8 @@ def gait10dof18musc_inverse(num_mesh_intervals: int = 25, fd_scheme: str = "forw
     p.set_position_motion(kin)
     p.set_time_bounds(float(t[0]) + 1e-3, float(t[-1]) - 1e-3)
     p.add_goal(MocoControlGoal("excitation_effort", 1.0))
+    # minimize_implicit_auxiliary_derivatives, weight 0.01 (MocoInverse.cpp:106-107)
+    p.add_goal(ImplicitAuxiliaryDerivativesTerm(weight=0.01))
     s = MocoHipSolver(num_mesh_intervals=num_mesh_intervals,
                       optim_finite_difference_scheme=fd_scheme, multibody_dynamics_mode="implicit",
                       optim_sparsity_detection=sparsity)

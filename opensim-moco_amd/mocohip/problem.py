@@ -146,6 +146,16 @@ class MocoControlBoundConstraint:
         self.equality_with_lower = bool(v)
 
 
+@dataclass
+class ImplicitAuxiliaryDerivativesTerm:
+    """MocoDirectCollocationSolver minimize_implicit_auxiliary_derivatives /
+    implicit_auxiliary_derivatives_weight as an objective term
+    (CasOCTranscription.cpp:534-545): weight * integral of the sum of squared
+    implicit auxiliary derivatives."""
+    name: str = "auxiliary_derivatives"
+    weight: float = 1.0
+
+
 class MocoProblem:
     """Single-phase MocoProblem (MocoProblem.h)."""
 
@@ -300,6 +310,12 @@ class ProblemRep:
                     gw.append(float(g.state_weights.get(n, 1.0)))
             elif isinstance(g, MocoFinalTimeGoal):
                 gs.kind = abi.MH_GOAL_FINAL_TIME
+            elif isinstance(g, ImplicitAuxiliaryDerivativesTerm):
+                gs.kind = abi.MH_GOAL_AUX_DERIVATIVES
+                naux = sum(1 for m in model.muscles if not m.ignore_tendon_compliance
+                           and m.tendon_compliance_dynamics_mode == "implicit")
+                for k in range(naux):
+                    gidx.append(k); gcol.append(-1); gw.append(1.0)
             elif isinstance(g, MocoSumSquaredStateGoal):
                 gs.kind = abi.MH_GOAL_SUM_SQUARED_STATE
                 for n in self.state_names:

@@ -1974,6 +1974,9 @@ static double goal_integrand(const orc_ctx* c, const mh_goal* G, double t, const
         } else if (G->kind == MH_GOAL_SUM_SQUARED_STATE) {
             double v = st[idx];
             L += w * (v * v);
+        } else if (G->kind == MH_GOAL_AUX_DERIVATIVES) {
+            double v = ct[c->NC + c->NACC + idx];   /* derivatives follow the controls */
+            L += w * (v * v);
         }
     }
     return L;

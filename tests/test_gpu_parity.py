@@ -391,7 +391,7 @@ def test_eval_jac_g(name, backend):
 
 @pytest.mark.parametrize("name", ["sliding_mass", "double_pendulum_hs", "gait_rigid_forward",
                                   "gait_compliant_central", "double_pendulum_implicit_hs",
-                                  "gait_rigid_implicit"])
+                                  "gait_rigid_implicit", "gait_inverse", "pendulum_bound_both_implicit"])
 def test_objective_and_gradient(name):
     gpu, ref, st = _pair(name)
     for _, x in _iterates(gpu):

@@ -778,3 +778,31 @@ def test_prescribed_kinematics_jacobian_matches_numerical_derivative():
     Jn = _numjac(nlp.eval_g, x, cols, h=1e-5)
     noise = 100 * np.finfo(float).eps * np.abs(nlp.eval_g(x)).max() / inv.solver.fd_step
     assert np.allclose(J[:, cols], Jn, rtol=1e-4, atol=max(1e-5, noise))
+
+
+def test_implicit_auxiliary_derivatives_term():
+    """minimize_implicit_auxiliary_derivatives (CasOCTranscription.cpp:534-545):
+    weight * duration * sum_k quad_k * sum_j w_jk^2, here on top of the
+    MocoInverse control effort; gradient vs numerical derivative."""
+    inv = configs.gait10dof18musc_inverse(3, sparsity="none")
+    rep = inv.problem.create_rep()
+    nlp = OracleNLP(rep, inv.solver.options())
+    x = nlp.initial_guess_from_bounds()
+    G, NZ, NC = nlp.G, nlp.NS, nlp.NC
+    x[2 + NZ * G:2 + (NZ + NC) * G] = np.random.default_rng(1).uniform(0, 0.3, NC * G)
+    d0 = 2 + (NZ + NC) * G
+    W = np.random.default_rng(2).uniform(-2, 2, (G, 18))
+    x[d0:] = W.reshape(-1)
+    f = nlp.eval_f(x)
+    dur = x[1] - x[0]
+    quad = np.zeros(G)
+    for i in range(3):
+        dm = 1.0 / 3
+        quad[2 * i] += dm / 6; quad[2 * i + 1] += 2 * dm / 3; quad[2 * i + 2] += dm / 6
+    U = x[2 + NZ * G:2 + (NZ + NC) * G].reshape(G, NC)
+    expect = dur * quad @ (U ** 2).sum(1) + 0.01 * dur * quad @ (W ** 2).sum(1)
+    assert f == pytest.approx(expect, rel=1e-12)
+    gf = nlp.eval_grad_f(x)
+    cols = list(range(d0, nlp.n, 7))
+    gn = _numjac(lambda z: np.array([nlp.eval_f(z)]), x, cols, h=1e-5)[0]
+    assert np.allclose(gf[cols], gn, rtol=1e-6, atol=1e-8)
