@@ -1,0 +1,1264 @@
+// core.hpp — device kernels (templates over the DAE back end), the
+// context struct and the back-end launchers shared by every translation
+// unit of libmocohip.so: mocohip.hip (C ABI, host side, non-template
+// kernels), generic.hip (device interpreter back ends) and one
+// generated/gen_<model>.hip per model-specialized back end, so that the
+// model back ends compile in parallel.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/mocohip.h"
+#include "dae_device.hpp"
+
+using namespace mh;
+
+constexpr size_t kMaxLds = 160 * 1024;   // gfx950 LDS per workgroup
+
+// LDS-qualified views of dynamic shared memory.  Kept in address space 3 so
+// that a load that may come from LDS or from global memory (e.g. xdot_at) is
+// never merged into one flat load: flat loads wait on vmcnt, i.e. on every
+// outstanding global store of the thread.
+typedef __attribute__((address_space(3))) double lds_double;
+typedef __attribute__((address_space(3))) int lds_int;
+__device__ __forceinline__ lds_double* lds(double* p) { return (lds_double*)p; }
+
+// ------------------------------------------------------------------------
+// Jacobian template (per mesh interval; identical for every interval).
+// ------------------------------------------------------------------------
+enum TplKind : uint8_t {
+    T_HERM_T = 0, T_SIMP_T = 1, T_HERM_X = 2, T_SIMP_X = 3, T_INTERP = 4,
+    T_TRAP_T = 5, T_TRAP_X = 6,
+    T_RES = 7,     // implicit multibody residual output s at point pt
+    T_PATH = 8     // path-constraint equation s at mesh point pt
+};
+struct TplEntry {
+    int16_t row;   // row within the interval
+    uint8_t kind;
+    uint8_t pt;    // 0 = first point of interval, 1 = mid (HS), 2 = last (HS) / 1 last (trap)
+    int16_t dir;   // 0 = t0, 1 = tf, 2 + j = point input j
+    int16_t s;     // state index of the row (defects) / control index (interp)
+};
+// 4-byte form of a template entry (staged in LDS by k_interval):
+// kind | pt << 4 | dir << 6 | s << 16 (the row is not needed to evaluate it).
+__host__ __device__ __forceinline__ uint32_t tpl_pack(const TplEntry& e) {
+    return (uint32_t)e.kind | ((uint32_t)e.pt << 4) | ((uint32_t)e.dir << 6) | ((uint32_t)e.s << 16);
+}
+__host__ __device__ __forceinline__ TplEntry tpl_unpack(uint32_t u) {
+    TplEntry e;
+    e.kind = (uint8_t)(u & 15u);
+    e.pt = (uint8_t)((u >> 4) & 3u);
+    e.dir = (int16_t)((u >> 6) & 1023u);
+    e.row = 0;
+    e.s = (int16_t)(u >> 16);
+    return e;
+}
+
+// ------------------------------------------------------------------------
+// DAE back ends.  Generic: the interpreter of dae_device.hpp with size-class
+// bounded per-lane arrays.  Generated: a model-specialized straight-line
+// struct from mocohip/codegen.py (see generated/models.inc), selected by
+// model hash at mh_create.
+// ------------------------------------------------------------------------
+struct SzSmall { static constexpr int MB = 4, MQ = 4, MP = 4, MI = 24, MO = 12; };
+struct SzMedium { static constexpr int MB = 16, MQ = 16, MP = 8, MI = 128, MO = 64; };
+struct SzLarge { static constexpr int MB = 32, MQ = 40, MP = 12, MI = 384, MO = 192; };
+
+template <class Z>
+struct GenericDae {
+    static constexpr int MI = Z::MI, MO = Z::MO;
+    static constexpr bool SPLIT = false;
+    __device__ __forceinline__ static void eval(const DevModel& M, double t, const double* in,
+            double* out) {
+        Work<Z::MB, Z::MQ, Z::MP> w;
+        if (M.presc) {
+            // prescribed kinematics: [q, u] and udot from the motion, the
+            // NLP states are the auxiliary states
+            double xf[2 * Z::MQ + Z::MI], ud[Z::MQ];
+            for (int j = 0; j < M.nq; ++j)
+                table_eval_d(M, M.kin_table, M.kin_col[j], t, xf[j], xf[M.nq + j], ud[j]);
+            for (int k = 0; k < M.nz; ++k) xf[2 * M.nq + k] = in[k];
+            dae_eval<Z::MB, Z::MQ, Z::MP>(M, w, t, xf, in + M.ns, out, ud);
+            return;
+        }
+        dae_eval<Z::MB, Z::MQ, Z::MP>(M, w, t, in, in + M.ns, out);
+    }
+};
+
+struct Layout {
+    int NS, NC, NQ, NO, NI;  // NI = NS + NC + NDV
+    int G;                   // grid points (full problem)
+    int k0;                  // first grid point of this shard
+    int nk;                  // grid points in this shard
+    int NDV;                 // derivative variables per grid point: accelerations, aux derivatives
+    int NACC;                // acceleration variables per grid point (implicit multibody: NQ)
+    int SO;                  // callback output of state s's derivative: s + SO (s >= NQ)
+};
+
+// Per grid point the evaluation lanes are laid out as
+//   forward/backward: [dir 0 .. ND-1 perturbed, ND = unperturbed base]
+//   central:          [dir 0 .. ND-1 at +h, ND .. 2ND-1 at -h, 2ND = base]
+// (dir 0 = t0 seed, dir 1 = tf seed, dir 2+j = point input j) and raw DAE
+// outputs are stored Y[(kl*NO + o)*stride + lane]; eval_g uses stride 1
+// with the base lane only.
+struct Lanes {
+    int fd;       // MH_FD_*
+    int ND;       // directions
+    int stride;   // lanes per grid point
+    int base;     // index of the base lane
+    double h;     // FD step
+};
+
+template <class D>
+__device__ __forceinline__ void load_point(const double* __restrict__ x, const Layout& L, int k,
+        double (&in)[D::MI]) {
+    const double* xs = x + 2 + (long)k * L.NS;
+    const double* xc = x + 2 + (long)L.NS * L.G + (long)k * L.NC;
+    const double* xd = x + 2 + (long)(L.NS + L.NC) * L.G + (long)k * L.NDV;
+#pragma unroll
+    for (int i = 0; i < D::MI; ++i) {
+        double v = 0.0;
+        if (i < L.NS) v = xs[i];
+        else if (i < L.NS + L.NC) v = xc[i - L.NS];
+        else if (i < L.NI) v = xd[i - L.NS - L.NC];
+        in[i] = v;
+    }
+}
+
+// Time and inputs of evaluation lane r of grid point k (Lanes layout above).
+template <class D>
+__device__ __forceinline__ double lane_inputs(const Layout& L, const Lanes& Ln,
+        const double* __restrict__ x, double g, int k, int r, double (&in)[D::MI]) {
+    const double t0 = x[0], tf = x[1];
+    double t = (tf - t0) * g + t0;
+    load_point<D>(x, L, k, in);
+    if (r != Ln.base) {
+        int dir = r;
+        double step = Ln.fd == MH_FD_BACKWARD ? -Ln.h : Ln.h;
+        if (Ln.fd == MH_FD_CENTRAL && r >= Ln.ND) { dir = r - Ln.ND; step = -Ln.h; }
+        if (dir == 0) t = t + step * (1.0 - g);
+        else if (dir == 1) t = t + step * g;
+        const int pi = dir - 2;
+#pragma unroll
+        for (int i = 0; i < D::MI; ++i) in[i] = (i == pi) ? in[i] + step : in[i];
+    }
+    return t;
+}
+
+// One lane = one DAE evaluation (grid point kl, lane role r).
+template <class D>
+__global__ void __launch_bounds__(64) k_eval(DevModel M, Layout L, Lanes Ln,
+        const double* __restrict__ x, const double* __restrict__ grid,
+        double* __restrict__ times, double* __restrict__ Y) {
+    const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= (long)L.nk * Ln.stride) return;
+    const int kl = (int)(gid / Ln.stride);
+    const int r = (int)(gid - (long)kl * Ln.stride);
+    const int k = L.k0 + kl;
+    double in[D::MI];
+    double out[D::MO];
+    const double t = lane_inputs<D>(L, Ln, x, grid[k], k, r, in);
+    if (r == Ln.base) times[kl] = t;
+    D::eval(M, t, in, out);
+    double* Yk = Y + (long)kl * L.NO * Ln.stride + r;
+#pragma unroll
+    for (int o = 0; o < D::MO; ++o)
+        if (o < L.NO) Yk[(long)o * Ln.stride] = out[o];
+}
+
+// ------------------------------------------------------------------------
+// Task-decomposed evaluation for generated models.
+//
+// A DAE evaluation is split into independent groups (mocohip/codegen.py
+// _emit_groups): the mass-matrix factor, the RNEA bias forces, one group per
+// external load and one per muscle.  Each group reads a known subset of the
+// point inputs, so a finite-difference lane only re-evaluates the groups
+// that read its perturbed input and takes every other group's result from
+// the unperturbed (base) lane of the same grid point:
+//
+//   k_groups   one wave = one group for 64 (grid point, lane role) tasks;
+//              results to T (force groups) / H (mass factor) in HBM.
+//   k_combine  one lane = one (grid point, lane role): sums the generalized
+//              forces of all groups in a fixed order, adds the coordinate
+//              actuators, solves with the mass factor, evaluates activation
+//              dynamics, writes the raw outputs Y.
+//
+// The fixed summation order makes a reused group result bit-identical to
+// re-evaluating it, so the Jacobian equals that of full re-evaluation per
+// direction (tests/test_gpu_parity.py::test_pruned_tasks_bit_identical).
+// ------------------------------------------------------------------------
+
+// Inputs of one evaluation lane read where used (L1/L2-resident x) instead
+// of held in VGPRs.
+template <class D>
+struct LaneIn {
+    const double* __restrict__ xs;
+    const double* __restrict__ xc;
+    const double* __restrict__ xd;   // implicit: accelerations (inputs NS + NC ..)
+    int pi;
+    double step;
+    __device__ __forceinline__ double operator[](int i) const {
+        const double v = i < D::NS ? xs[i] : (i < D::NS + D::NC ? xc[i - D::NS] : xd[i - D::NS - D::NC]);
+        return i == pi ? v + step : v;
+    }
+};
+
+// Where lane inputs come from: the NLP iterate x (grid times) or explicit
+// points [t, states, controls] (mh_eval_dae).
+struct Src {
+    const double* x;
+    const double* grid;
+    const double* pts;   // non-null: explicit points
+    int G, k0;
+};
+
+// Same, reading a grid point's inputs staged in LDS (k_interval).
+template <class D>
+struct LaneInL {
+    const lds_double* xs;
+    const lds_double* xc;
+    const lds_double* xd;
+    int pi;
+    double step;
+    __device__ __forceinline__ double operator[](int i) const {
+        const double v = i < D::NS ? xs[i] : (i < D::NS + D::NC ? xc[i - D::NS] : xd[i - D::NS - D::NC]);
+        return i == pi ? v + step : v;
+    }
+};
+
+// Time, perturbed input and step of evaluation lane r at normalized grid
+// time g (Lanes layout above).  The single definition of the lane
+// arithmetic: every kernel that evaluates lanes goes through it.
+__device__ __forceinline__ double lane_time(const Lanes& Ln, double g, double t0, double tf, int r,
+        int& pi, double& step) {
+    double t = (tf - t0) * g + t0;
+    pi = -1;
+    step = 0.0;
+    if (r != Ln.base) {
+        int dir = r;
+        step = Ln.fd == MH_FD_BACKWARD ? -Ln.h : Ln.h;
+        if (Ln.fd == MH_FD_CENTRAL && r >= Ln.ND) { dir = r - Ln.ND; step = -Ln.h; }
+        if (dir == 0) t = t + step * (1.0 - g);
+        else if (dir == 1) t = t + step * g;
+        pi = dir - 2;
+    }
+    return t;
+}
+
+template <class D>
+__device__ __forceinline__ LaneIn<D> lane_input(const Src& S, const Lanes& Ln, int kl, int r,
+        double& t) {
+    if (S.pts) {
+        const double* p = S.pts + (long)kl * (1 + D::NI);
+        t = p[0];
+        return LaneIn<D>{p + 1, p + 1 + D::NS, p + 1 + D::NS + D::NC, -1, 0.0};
+    }
+    const int k = S.k0 + kl;
+    constexpr int NDV = D::NI - D::NS - D::NC;
+    LaneIn<D> in{S.x + 2 + (long)k * D::NS, S.x + 2 + (long)D::NS * S.G + (long)k * D::NC,
+                 S.x + 2 + (long)(D::NS + D::NC) * S.G + (long)k * NDV, -1, 0.0};
+    t = lane_time(Ln, S.grid[k], S.x[0], S.x[1], r, in.pi, in.step);
+    return in;
+}
+
+// Device task tables (built on the host per lane configuration).
+struct Tasks {
+    int ng, stride, tdoubles, nmass, nk;   // tdoubles: T doubles per grid point
+    const int* dlen;     // [ng] tasks per grid point of group g
+    const int* off;      // [ng] slot offset of force group g within a grid point
+    const int* roles;    // [ng][stride] j -> lane role
+    const int* jd;       // [stride][ng] lane role -> slot of group g within the grid
+                         // point (g = 0: index of the mass factor; base = first)
+    const int4* blk;     // [nblocks] (group, first task, tasks per grid point, 1/n as float bits)
+};
+
+#define MH_IV_STAMP(i)
+
+template <class D>
+__global__ void __launch_bounds__(64) k_groups(DevModel M, Src S, Lanes Ln, Tasks TK,
+        double* __restrict__ T, double* __restrict__ H) {
+    const int lane = threadIdx.x;
+    const int4 rec = TK.blk[blockIdx.x];   // one scalar load: no dependent table chain
+    const int g = __builtin_amdgcn_readfirstlane(rec.x);
+    const int first = __builtin_amdgcn_readfirstlane(rec.y);
+    const int n = __builtin_amdgcn_readfirstlane(rec.z);
+    const float inv = __int_as_float(__builtin_amdgcn_readfirstlane(rec.w));
+    const int task = first + lane;
+    const bool live = task < TK.nk * n;
+    const int tc = live ? task : 0;
+    // tc / n through the float reciprocal, corrected to the exact quotient
+    int kl = (int)((float)tc * inv);
+    kl += (kl + 1) * n <= tc ? 1 : 0;
+    kl -= kl * n > tc ? 1 : 0;
+    const int j = tc - kl * n;
+    const int r = TK.roles[g * TK.stride + j];
+    double t;
+    const LaneIn<D> in = lane_input<D>(S, Ln, kl, r, t);
+    constexpr int NOUT = D::NST > D::NF ? D::NST : D::NF;
+    double out[NOUT];
+    // the mass-matrix and bias groups are the longest tasks: give them issue
+    // priority over the short muscle tasks sharing their SIMD
+    if (g < 2) __builtin_amdgcn_s_setprio(2);
+    D::group(g, M, t, in, out);
+    if (!live) return;
+    if (g == 0) {
+        double* dst = H + ((long)kl * TK.nmass + j) * D::NST;
+#pragma unroll
+        for (int f = 0; f < D::NST; ++f) dst[f] = out[f];
+    } else {
+        // compact slab: group g's slots hold exactly its GROUP_NF[g] fields
+        const int nf = D::GROUP_NF[g];
+        double* dst = T + (long)kl * TK.tdoubles + TK.off[g] + j * nf;
+#pragma unroll
+        for (int f = 0; f < D::NF; ++f)
+            if (f < nf) dst[f] = out[f];
+    }
+}
+
+// Combine: one workgroup per grid point.  The grid point's group results
+// (contiguous in T and H) are staged in LDS with coalesced loads; each lane
+// (one lane role) then reads the slots it needs from LDS.
+template <class D>
+struct TaskLoadLds {
+    const lds_double* sT;
+    const lds_double* sH;
+    const int* __restrict__ slot;   // [stride][ng]: slot of group g for this role
+    int r;
+    __device__ __forceinline__ double operator()(int g, int f) const {
+        return sT[slot[r * D::NG + g] + f];
+    }
+    __device__ __forceinline__ double h(int f) const {
+        return sH[slot[r * D::NG] * D::NST + f];
+    }
+};
+
+// Same arithmetic reading T/H straight from global memory: used when the
+// grid point's slots do not fit in LDS (e.g. MOCOHIP_TASKS=all with central
+// differences).
+template <class D>
+struct TaskLoadGlobal {
+    const double* __restrict__ sT;
+    const double* __restrict__ sH;
+    const int* __restrict__ slot;
+    int r;
+    __device__ __forceinline__ double operator()(int g, int f) const {
+        return sT[slot[r * D::NG + g] + f];
+    }
+    __device__ __forceinline__ double h(int f) const {
+        return sH[slot[r * D::NG] * D::NST + f];
+    }
+};
+
+template <class D>
+__global__ void __launch_bounds__(64) k_combine_global(DevModel M, Src S, Lanes Ln, Tasks TK,
+        const double* __restrict__ T, const double* __restrict__ H, double* __restrict__ times,
+        double* __restrict__ Y, long ystride_pt) {
+    const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= (long)TK.nk * Ln.stride) return;
+    const int kl = (int)(gid / Ln.stride);
+    const int r = (int)(gid - (long)kl * Ln.stride);
+    double t;
+    const LaneIn<D> in = lane_input<D>(S, Ln, kl, r, t);
+    if (r == Ln.base && times) times[kl] = t;
+    const TaskLoadGlobal<D> TL{T + (long)kl * TK.tdoubles, H + (long)kl * TK.nmass * D::NST,
+                               TK.jd, r};
+    double out[D::NO];
+    D::combine(M, t, in, TL, out);
+    double* Yk = Y + (long)kl * ystride_pt + r;
+#pragma unroll
+    for (int o = 0; o < D::NO; ++o) Yk[(long)o * Ln.stride] = out[o];
+}
+
+// Copy n doubles to LDS with U loads in flight per thread before the first
+// store (a plain strided loop serializes one memory round trip per pass).
+template <int U>
+__device__ __forceinline__ void stage_lds(double* __restrict__ dst, const double* __restrict__ src,
+        int n) {
+    for (int b = 0; b < n; b += U * (int)blockDim.x) {
+        double v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = b + u * (int)blockDim.x + (int)threadIdx.x;
+            v[u] = src[i < n ? i : n - 1];   // unconditional: no branch per load
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = b + u * (int)blockDim.x + (int)threadIdx.x;
+            if (i < n) dst[i] = v[u];
+        }
+    }
+}
+
+// With quot != 0 (Jacobian lanes) the kernel writes, per output o, the
+// finite-difference quotient of direction r into Y slot r instead of the raw
+// lane value (CasADi FiniteDiff formulas (f+ - f-)/2h, (f+ - f0)/h,
+// (f0 - f-)/h; the base slot keeps the raw base value): one division per
+// (grid point, output, direction) instead of one per Jacobian nonzero that
+// reads it.  The lanes exchange their raw values through LDS.
+template <class D>
+__global__ void __launch_bounds__(1024) k_combine(DevModel M, Src S, Lanes Ln, Tasks TK,
+        const double* __restrict__ T, const double* __restrict__ H, double* __restrict__ times,
+        double* __restrict__ Y, long ystride_pt, int quot) {
+    extern __shared__ double smem[];
+    const int kl = blockIdx.x;
+    const int nt = TK.tdoubles, nh = TK.nmass * D::NST;
+    double* sT = smem;
+    double* sH = smem + nt;
+    const double* Tk = T + (long)kl * nt;
+    const double* Hk = H + (long)kl * nh;
+    if (nt > 0) stage_lds<16>(sT, Tk, nt);
+    if (nh > 0) stage_lds<8>(sH, Hk, nh);
+    __syncthreads();
+    const int r = threadIdx.x;
+    const bool act = r < Ln.stride;
+    double out[D::NO];
+    if (act) {
+        double t;
+        const LaneIn<D> in = lane_input<D>(S, Ln, kl, r, t);
+        if (r == Ln.base && times) times[kl] = t;
+        const TaskLoadLds<D> TL{lds(sT), lds(sH), TK.jd, r};
+        D::combine(M, t, in, TL, out);
+    }
+    // Y[(kl*NO + o)*stride + r]  (ystride_pt = NO*stride; explicit points:
+    // stride 1 -> out[p*NO + o])
+    double* Yk = Y + (long)kl * ystride_pt + r;
+    if (!quot) {
+        if (act) {
+#pragma unroll
+            for (int o = 0; o < D::NO; ++o) Yk[(long)o * Ln.stride] = out[o];
+        }
+        return;
+    }
+    __syncthreads();                 // every lane is done reading sT / sH
+    double* sY = smem;               // [NO][stride] raw lane values
+    if (act) {
+#pragma unroll
+        for (int o = 0; o < D::NO; ++o) sY[o * Ln.stride + r] = out[o];
+    }
+    __syncthreads();
+    if (!act) return;
+#pragma unroll
+    for (int o = 0; o < D::NO; ++o) {
+        const double* y = sY + o * Ln.stride;
+        double v;
+        if (r == Ln.base) v = out[o];
+        else if (Ln.fd == MH_FD_CENTRAL) v = r < Ln.ND ? (out[o] - y[Ln.ND + r]) / (2.0 * Ln.h) : 0.0;
+        else if (Ln.fd == MH_FD_FORWARD) v = (out[o] - y[Ln.base]) / Ln.h;
+        else v = (y[Ln.base] - out[o]) / Ln.h;
+        Yk[(long)o * Ln.stride] = v;
+    }
+}
+
+// Path-constraint equations (include/mocohip.h mh_path_equation) and the
+// tables / grid their bound functions and time seeds read.
+struct PathEqs {
+    int npc;         // equations per mesh point
+    const mh_path_equation* __restrict__ eq;
+    const mh_table* __restrict__ tabs;
+    const double* __restrict__ brk;
+    const double* __restrict__ coef;
+    const double* __restrict__ grid;
+};
+
+struct Interval {
+    int scheme;      // MH_HERMITE_SIMPSON / MH_TRAPEZOIDAL
+    int interp;
+    int ib;          // first interval of shard
+    int rpi;         // rows per interval
+    int nnz_int;     // nonzeros per interval
+    int nres;        // residual rows per grid point: multibody (implicit: NQ), then auxiliary
+    int nacc;        // multibody residual rows per grid point
+    int oaux;        // callback output of the first auxiliary residual (NQ + NZ)
+    // callback output behind residual row r of a grid point
+    __device__ __forceinline__ int rout(int r) const { return r < nacc ? r : oaux + (r - nacc); }
+    int N;           // mesh intervals of the whole problem
+    int nnz_tail;    // nonzeros of the tail rows
+    int ntail;       // tail rows: final mesh point's path rows + final residuals
+    int npe;         // path-constraint entries per mesh point (lead the interval / tail)
+    PathEqs P;
+    // Every interval opens with its mesh point's path rows.  The interval
+    // N-1 also owns the tail (flattenConstraints, CasOCTranscription.h:
+    // 286-308): the final mesh point's path rows, then the final grid
+    // point's residual rows, as rows rpi..rpi+ntail after its own and
+    // template entries nnz_int..nnz_int+nnz_tail.
+    __device__ __forceinline__ int rows(int i) const { return rpi + (i == N - 1 ? ntail : 0); }
+    __device__ __forceinline__ int entries(int i) const { return nnz_int + (i == N - 1 ? nnz_tail : 0); }
+};
+
+// Path-constraint arithmetic, evaluated in order without contraction so
+// that the finite-difference quotients see the same roundings as the CPU
+// restatement (the perturbed time t + h*seed, the Horner steps).
+__device__ __forceinline__ double path_bound(const PathEqs& P, const mh_path_equation& E, double t) {
+#pragma clang fp contract(off)
+    if (E.table < 0) return E.value;
+    const mh_table T = P.tabs[E.table];
+    const double* br = P.brk + T.break_begin;
+    int s;
+    if (t <= br[0]) s = 0;
+    else if (t >= br[T.nseg]) s = T.nseg - 1;
+    else {
+        int lo = 0, hi = T.nseg;
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (t < br[mid]) hi = mid; else lo = mid;
+        }
+        s = lo;
+    }
+    const double* cf = P.coef + T.coef_begin + ((long)s * T.ncol + E.column) * (T.degree + 1);
+    const double dt = t - br[s];
+    double v = cf[T.degree];
+    for (int k = T.degree - 1; k >= 0; --k) v = v * dt + cf[k];
+    return v;
+}
+// MocoControlBoundConstraint::calcPathConstraintErrorsImpl
+// (MocoControlBoundConstraint.cpp:130-146): control - bound(t).
+__device__ __forceinline__ double path_value(const PathEqs& P, int e, double t, double control) {
+    const mh_path_equation E = P.eq[e];
+    return control - path_bound(P, E, t);
+}
+// FD quotient of equation e at grid point k along direction dir (0 = t0,
+// 1 = tf, 2 + j = point input j), CasADi FiniteDiff as for the DAE lanes.
+// The equation reads only its control and the time: along any other input
+// the perturbed and base values are equal and the quotient is exactly 0.
+__device__ __forceinline__ double path_quot(const PathEqs& P, const Lanes& Ln, int NS, int e, int k,
+        double t, double control, int dir) {
+#pragma clang fp contract(off)
+    const mh_path_equation E = P.eq[e];
+    if (dir >= 2 && dir != 2 + NS + E.index) return 0.0;
+    const double h = Ln.h;
+    double tp = t, tm = t, cp = control, cm = control;
+    if (dir < 2) {
+        const double g = P.grid[k];
+        const double seed = dir == 0 ? 1.0 - g : g;
+        tp = t + h * seed;
+        tm = t - h * seed;
+    } else {
+        cp = control + h;
+        cm = control - h;
+    }
+    if (Ln.fd == MH_FD_CENTRAL)
+        return ((cp - path_bound(P, E, tp)) - (cm - path_bound(P, E, tm))) / (2.0 * h);
+    const double v0 = control - path_bound(P, E, t);
+    if (Ln.fd == MH_FD_FORWARD) return ((cp - path_bound(P, E, tp)) - v0) / h;
+    return (v0 - (cm - path_bound(P, E, tm))) / h;
+}
+
+__device__ __forceinline__ int grid_of(const Interval& I, int i, int pt) {
+    return I.scheme == MH_HERMITE_SIMPSON ? 2 * i + pt : i + pt;
+}
+
+// Raw DAE outputs of a grid point's lanes and the grid point's time, as
+// read by the transcription arithmetic.  YG: Y and the base-lane times in
+// HBM (written by k_combine, indexed by local grid point k - k0).  YS: the
+// same values staged in LDS by k_interval for the interval's own points
+// (indexed by k - kf, kf = the interval's first grid point).
+struct YG {
+    const double* __restrict__ Y;
+    const double* __restrict__ times;
+    int NO, stride, k0;
+    int q;   // Y holds finite-difference quotients (k_combine quot mode)
+    const double* __restrict__ x;
+    int NS, NC, G;
+    // state s / control j of grid point k from the iterate
+    __device__ __forceinline__ double xs(int k, int s) const { return x[2 + (long)k * NS + s]; }
+    __device__ __forceinline__ double xc(int k, int j) const {
+        return x[2 + (long)NS * G + (long)k * NC + j];
+    }
+    int NDV;
+    __device__ __forceinline__ double xd(int k, int j) const {
+        return x[2 + (long)(NS + NC) * G + (long)k * NDV + j];
+    }
+    __device__ __forceinline__ const double* row(int k, int o) const {
+        return Y + ((long)(k - k0) * NO + o) * stride;
+    }
+    __device__ __forceinline__ double t(int k) const { return times[k - k0]; }
+};
+struct YS {
+    const lds_double* Y;
+    const lds_double* times;
+    int NO, stride, kf;
+    int q;
+    // the interval's states / controls staged in LDS ([point][NS], [point][NC])
+    const lds_double* sxs;
+    const lds_double* sxc;
+    int NS, NC;
+    __device__ __forceinline__ double xs(int k, int s) const { return sxs[(k - kf) * NS + s]; }
+    __device__ __forceinline__ double xc(int k, int j) const { return sxc[(k - kf) * NC + j]; }
+    const lds_double* sxd;
+    int NDV;
+    __device__ __forceinline__ double xd(int k, int j) const { return sxd[(k - kf) * NDV + j]; }
+    __device__ __forceinline__ const lds_double* row(int k, int o) const {
+        return Y + ((k - kf) * NO + o) * stride;
+    }
+    __device__ __forceinline__ double t(int k) const { return times[k - kf]; }
+};
+
+// xdot[s] at grid point k.
+template <class YV>
+__device__ __forceinline__ double xdot_at(const Layout& L, const Lanes& Ln,
+        const double* __restrict__ x, const YV& Y, int k, int s) {
+    if (s < L.NQ) return Y.xs(k, L.NQ + s);
+    if (L.NACC && s < 2 * L.NQ) return Y.xd(k, s - L.NQ);   // implicit: udot = w
+    return Y.row(k, s + L.SO)[Ln.base];
+}
+
+template <class YV>
+__device__ __forceinline__ double defect_row(const Layout& L, const Interval& I, const Lanes& Ln,
+        const double* __restrict__ x, const YV& Y, int i, int r) {
+    const int NS = L.NS;
+    // residual rows: the interval's grid points (HS: 2, trapezoidal: 1), and
+    // for the last interval the final grid point after all its other rows
+    const int npres = I.scheme == MH_HERMITE_SIMPSON ? 2 : 1;
+    const int k_first = I.scheme == MH_HERMITE_SIMPSON ? 2 * i : i;
+    const int npc = I.P.npc;
+    if (r >= I.rpi) {   // tail: final mesh point's path rows, then its residuals
+        const int rt = r - I.rpi, kl = k_first + npres;
+        if (rt < npc) return path_value(I.P, rt, Y.t(kl), Y.xc(kl, I.P.eq[rt].index));
+        return Y.row(kl, I.rout(rt - npc))[Ln.base];
+    }
+    if (r < npc) return path_value(I.P, r, Y.t(k_first), Y.xc(k_first, I.P.eq[r].index));
+    r -= npc;
+    if (r < npres * I.nres) return Y.row(k_first + r / I.nres, I.rout(r % I.nres))[Ln.base];
+    r -= npres * I.nres;
+    if (I.scheme == MH_HERMITE_SIMPSON) {
+        const int ki = 2 * i, km = ki + 1, kp = ki + 2;
+        const double h = Y.t(kp) - Y.t(ki);
+        if (r < NS) {
+            const int s = r;
+            const double xi = Y.xs(ki, s), xm = Y.xs(km, s), xp = Y.xs(kp, s);
+            const double fi = xdot_at(L, Ln, x, Y, ki, s), fp = xdot_at(L, Ln, x, Y, kp, s);
+            return xm - 0.5 * (xp + xi) - (h / 8.0) * (fi - fp);
+        }
+        if (r < 2 * NS) {
+            const int s = r - NS;
+            const double xi = Y.xs(ki, s), xp = Y.xs(kp, s);
+            const double fi = xdot_at(L, Ln, x, Y, ki, s), fm = xdot_at(L, Ln, x, Y, km, s),
+                         fp = xdot_at(L, Ln, x, Y, kp, s);
+            return xp - xi - (h / 6.0) * (fp + 4.0 * fm + fi);
+        }
+        const int j = r - 2 * NS;
+        return Y.xc(km, j) - 0.5 * (Y.xc(kp, j) + Y.xc(ki, j));
+    }
+    const int ki = i, kp = i + 1;
+    const double h = Y.t(kp) - Y.t(ki);
+    const int s = r;
+    const double xi = Y.xs(ki, s), xp = Y.xs(kp, s);
+    const double fi = xdot_at(L, Ln, x, Y, ki, s), fp = xdot_at(L, Ln, x, Y, kp, s);
+    return xp - (xi + 0.5 * h * (fp + fi));
+}
+
+// d (DAE output o) / d dir at grid point k (the finite-difference quotient).
+template <class YV>
+__device__ __forceinline__ double dout(const Lanes& Ln, const YV& Y, int k, int o, int dir) {
+    const auto y = Y.row(k, o);
+    if (Y.q) return y[dir];
+    if (Ln.fd == MH_FD_CENTRAL) return (y[dir] - y[Ln.ND + dir]) / (2.0 * Ln.h);
+    if (Ln.fd == MH_FD_FORWARD) return (y[dir] - y[Ln.base]) / Ln.h;
+    return (y[Ln.base] - y[dir]) / Ln.h;
+}
+
+// d xdot[s] / d dir at grid point k from the raw lane outputs
+// (CasADi FiniteDiff formulas: (f+ - f-)/2h, (f+ - f0)/h, (f0 - f-)/h).
+template <class YV>
+__device__ __forceinline__ double dxdot(const Layout& L, const Lanes& Ln, const YV& Y, int k, int s,
+        int dir) {
+    if (s < L.NQ) return dir == 2 + L.NQ + s ? 1.0 : 0.0;
+    if (L.NACC && s < 2 * L.NQ) return dir == 2 + L.NS + L.NC + (s - L.NQ) ? 1.0 : 0.0;
+    return dout(Ln, Y, k, s + L.SO, dir);
+}
+
+
+constexpr int ASM_CHUNK = 1024;   // nonzeros per assembly workgroup
+
+// Per-interval constants of the Jacobian formulas (computed once per
+// interval; exactly the subexpressions the formulas would form per entry).
+struct IvC { double h8, h6, hh, g8, g6, gh; };
+__device__ __forceinline__ IvC iv_const(double h, double dgap) {
+    return IvC{h / 8.0, h / 6.0, 0.5 * h, dgap / 8.0, dgap / 6.0, 0.5 * dgap};
+}
+
+// Jacobian value of template entry T of the interval whose first grid point
+// is k_first (HS: d/d[t0,tf] of -(h/8)(f_i - f_p) with dh/dt0 = -dgap,
+// dh/dtf = dgap, etc.).
+// WITH_PATH = false compiles the path-constraint case out (k_interval
+// evaluates those entries in a loop of their own, off the hot loop).
+template <bool WITH_PATH = true, class YV>
+__device__ __forceinline__ double jac_entry(const Layout& L, const Lanes& Ln, const PathEqs& P,
+        const double* __restrict__ x, const YV& Y, const TplEntry T, int k_first, const IvC& C) {
+    const int s = T.s, dir = T.dir;
+    double v = 0.0;
+    switch (T.kind) {
+    case T_HERM_T: {
+        const int ki = k_first, kp = k_first + 2;
+        const double fi = xdot_at(L, Ln, x, Y, ki, s), fp = xdot_at(L, Ln, x, Y, kp, s);
+        v = (dir == 0 ? C.g8 : -C.g8) * (fi - fp) -
+            C.h8 * (dxdot(L, Ln, Y, ki, s, dir) - dxdot(L, Ln, Y, kp, s, dir));
+        break;
+    }
+    case T_SIMP_T: {
+        const int ki = k_first, km = k_first + 1, kp = k_first + 2;
+        const double fi = xdot_at(L, Ln, x, Y, ki, s), fm = xdot_at(L, Ln, x, Y, km, s),
+                     fp = xdot_at(L, Ln, x, Y, kp, s);
+        v = (dir == 0 ? C.g6 : -C.g6) * (fp + 4.0 * fm + fi) -
+            C.h6 * (dxdot(L, Ln, Y, kp, s, dir) + 4.0 * dxdot(L, Ln, Y, km, s, dir) +
+                    dxdot(L, Ln, Y, ki, s, dir));
+        break;
+    }
+    case T_HERM_X: {
+        const int k = k_first + T.pt;
+        const bool ident = dir == 2 + s;
+        if (T.pt == 1) { v = ident ? 1.0 : 0.0; break; }
+        if (ident) v += -0.5;
+        const double dv = dxdot(L, Ln, Y, k, s, dir);
+        v += (T.pt == 0 ? -C.h8 : C.h8) * dv;
+        break;
+    }
+    case T_SIMP_X: {
+        const int k = k_first + T.pt;
+        const bool ident = dir == 2 + s;
+        const double dv = dxdot(L, Ln, Y, k, s, dir);
+        if (T.pt == 2) { if (ident) v += 1.0; v += -C.h6 * dv; }
+        else if (T.pt == 0) { if (ident) v += -1.0; v += -C.h6 * dv; }
+        else v += -C.h6 * 4.0 * dv;
+        break;
+    }
+    case T_INTERP:
+        v = T.pt == 1 ? 1.0 : -0.5;
+        break;
+    case T_RES:
+        v = dout(Ln, Y, k_first + T.pt, s, dir);
+        break;
+    case T_PATH:
+        if constexpr (WITH_PATH) {
+            const int k = k_first + T.pt;
+            v = path_quot(P, Ln, L.NS, s, k, Y.t(k), Y.xc(k, P.eq[s].index), dir);
+        }
+        break;
+    case T_TRAP_T: {
+        const int ki = k_first, kp = k_first + 1;
+        const double fi = xdot_at(L, Ln, x, Y, ki, s), fp = xdot_at(L, Ln, x, Y, kp, s);
+        v = (dir == 0 ? C.gh : -C.gh) * (fp + fi) -
+            C.hh * (dxdot(L, Ln, Y, kp, s, dir) + dxdot(L, Ln, Y, ki, s, dir));
+        break;
+    }
+    case T_TRAP_X: {
+        const int k = k_first + T.pt;
+        const bool ident = dir == 2 + s;
+        const double dv = dxdot(L, Ln, Y, k, s, dir);
+        if (T.pt == 1) { if (ident) v += 1.0; v += -C.hh * dv; }
+        else { if (ident) v += -1.0; v += -C.hh * dv; }
+        break;
+    }
+    }
+    return v;
+}
+
+__device__ __forceinline__ void interval_span(const Interval& I, int i, int& k_first, int& k_last) {
+    k_first = grid_of(I, i, 0);
+    k_last = k_first + (I.scheme == MH_HERMITE_SIMPSON ? 2 : 1);
+}
+
+// Fused combine + transcription: one workgroup per mesh interval.  The
+// group results (T, H) of the interval's 2-3 grid points are staged in LDS
+// together, every (grid point, lane role) is combined in parallel into
+// LDS-resident raw outputs, and the whole workgroup then writes the
+// interval's g rows and Jacobian values from LDS.  Same arithmetic as
+// k_combine + k_transcribe (bit-identical results) with Y never touching
+// HBM and one kernel less per evaluation.  Launched when the LDS budget
+// allows (interval_lds), otherwise the split path runs.
+constexpr int IV_UNROLL = 4;
+template <class D>
+__global__ void __launch_bounds__(1024) k_interval(DevModel M, Src S, Lanes Ln, Tasks TK, Layout L,
+        Interval I, const TplEntry* __restrict__ tpl, const uint32_t* __restrict__ tplp, int tables_lds,
+        const double* __restrict__ T, const double* __restrict__ H, double* __restrict__ g,
+        double* __restrict__ values) {
+    extern __shared__ double smem[];
+    const int il = blockIdx.x;
+    const int i = I.ib + il;
+    int k_first, k_last;
+    interval_span(I, i, k_first, k_last);
+    const int npts = k_last - k_first + 1;
+    const int nt = TK.tdoubles, nh = TK.nmass * D::NST;
+    const int ny = D::NO * Ln.stride;
+    double* sY = smem;                       // [npts][NO][stride]
+    double* sTimes = sY + npts * ny;         // [npts]
+    double* sT = sTimes + 4;                 // [npts][nt]
+    double* sH = sT + npts * nt;             // [npts][nh]
+    // tables_lds: the packed Jacobian template and the role -> slot table
+    // are staged too, so that the combine and the assembly issue no global
+    // loads after this one round trip
+    const int ntp = (I.nnz_int + I.nnz_tail + 1) / 2;     // in doubles (tail entries included)
+    double* sXs = sH + npts * nh;            // [npts][NS] states, [npts][NC] controls,
+    double* sXc = sXs + npts * L.NS;         // [npts][NDV] accelerations (implicit)
+    double* sXd = sXc + npts * L.NC;
+    double* sTpl = sXd + npts * L.NDV;
+    // the interval's points are consecutive local grid points: their T (and
+    // H) slabs are one contiguous run each
+    const int kl0 = k_first - S.k0;
+    if (nt > 0) stage_lds<16>(sT, T + (long)kl0 * nt, npts * nt);
+    if (nh > 0) stage_lds<8>(sH, H + (long)kl0 * nh, npts * nh);
+    if (tables_lds && values) stage_lds<8>(sTpl, (const double*)tplp, ntp);
+    stage_lds<1>(sXs, S.x + 2 + (long)k_first * L.NS, npts * L.NS);
+    if (L.NC > 0) stage_lds<1>(sXc, S.x + 2 + (long)L.NS * L.G + (long)k_first * L.NC, npts * L.NC);
+    if (L.NDV > 0)
+        stage_lds<1>(sXd, S.x + 2 + (long)(L.NS + L.NC) * L.G + (long)k_first * L.NDV, npts * L.NDV);
+    const __attribute__((address_space(3))) uint32_t* tp = (const __attribute__((address_space(3))) uint32_t*)sTpl;
+    const double t0 = S.x[0], tf = S.x[1];
+    __syncthreads();
+    for (int w = threadIdx.x; w < npts * Ln.stride; w += blockDim.x) {
+        const int p = w / Ln.stride, r = w - p * Ln.stride;
+        LaneInL<D> in{lds(sXs + p * L.NS), lds(sXc + p * L.NC), lds(sXd + p * L.NDV), -1, 0.0};
+        const double t = lane_time(Ln, S.grid[k_first + p], t0, tf, r, in.pi, in.step);
+        if (r == Ln.base) sTimes[p] = t;
+        const TaskLoadLds<D> TL{lds(sT + p * nt), lds(sH + p * nh), TK.jd, r};
+        double out[D::NO];
+        D::combine(M, t, in, TL, out);
+        lds_double* Yp = lds(sY + p * ny + r);
+#pragma unroll
+        for (int o = 0; o < D::NO; ++o) Yp[o * Ln.stride] = out[o];
+    }
+    __syncthreads();
+    // finite-difference quotients in place (CasADi FiniteDiff formulas), once
+    // per (point, output, direction) instead of once per Jacobian entry that
+    // reads them; the base slot keeps the raw value for the defect rows
+    const int quot = values && Ln.stride > 1;
+    if (quot) {
+        const int ndir = Ln.ND;
+        for (int w = threadIdx.x; w < npts * D::NO * ndir; w += blockDim.x) {
+            const int po = w / ndir, d = w - po * ndir;
+            lds_double* y = lds(sY + po * Ln.stride);
+            double q;
+            if (Ln.fd == MH_FD_CENTRAL) q = (y[d] - y[Ln.ND + d]) / (2.0 * Ln.h);
+            else if (Ln.fd == MH_FD_FORWARD) q = (y[d] - y[Ln.base]) / Ln.h;
+            else q = (y[Ln.base] - y[d]) / Ln.h;
+            y[d] = q;
+        }
+        __syncthreads();
+    }
+    const YS YV{lds(sY), lds(sTimes), D::NO, Ln.stride, k_first, quot, lds(sXs), lds(sXc), L.NS, L.NC,
+                lds(sXd), L.NDV};
+    if (g) {
+        double* gi = g + (long)il * I.rpi;
+        for (int r = threadIdx.x; r < I.rows(i); r += blockDim.x) gi[r] = defect_row(L, I, Ln, S.x, YV, i, r);
+    }
+    if (values) {
+        const IvC C = iv_const(YV.t(k_last) - YV.t(k_first), S.grid[k_last] - S.grid[k_first]);
+        double* vi = values + (long)il * I.nnz_int;
+        const int ne = I.entries(i);
+        const int B = blockDim.x;
+        int e = threadIdx.x;
+        // path-constraint entries (the first npe of the interval and of
+        // the tail) are written by their own loop below
+        if (tables_lds) {
+            for (; e < ne; e += B) {
+                const TplEntry te = tpl_unpack(tp[e]);
+                if (te.kind != T_PATH) vi[e] = jac_entry<false>(L, Ln, I.P, S.x, YV, te, k_first, C);
+            }
+            e = ne;
+        }
+        // template entries for IV_UNROLL iterations are loaded before any is
+        // evaluated (independent loads in flight, then LDS reads + stores)
+        for (; e + (IV_UNROLL - 1) * B < ne; e += IV_UNROLL * B) {
+            TplEntry te[IV_UNROLL];
+#pragma unroll
+            for (int u = 0; u < IV_UNROLL; ++u) te[u] = tpl[e + u * B];
+#pragma unroll
+            for (int u = 0; u < IV_UNROLL; ++u)
+                if (te[u].kind != T_PATH) vi[e + u * B] = jac_entry<false>(L, Ln, I.P, S.x, YV, te[u], k_first, C);
+        }
+        for (; e < ne; e += B) {
+            const TplEntry te = tpl[e];
+            if (te.kind != T_PATH) vi[e] = jac_entry<false>(L, Ln, I.P, S.x, YV, te, k_first, C);
+        }
+        if (I.npe > 0) {
+            const int npe = I.npe;
+            const int nw = i == I.N - 1 ? 2 * npe : npe;
+            for (int w = threadIdx.x; w < nw; w += B) {
+                const int ep = w < npe ? w : I.nnz_int + (w - npe);
+                vi[ep] = jac_entry<true>(L, Ln, I.P, S.x, YV, tpl[ep], k_first, C);
+            }
+        }
+    }
+}
+
+// ---- objective -------------------------------------------------------------
+__device__ __forceinline__ void gather_inputs(const double* __restrict__ x, const Layout& L,
+        int k, double* in, int NI) {
+    const double* xs = x + 2 + (long)k * L.NS;
+    const double* xc = x + 2 + (long)L.NS * L.G + (long)k * L.NC;
+    const double* xd = x + 2 + (long)(L.NS + L.NC) * L.G + (long)k * L.NDV;
+    for (int s = 0; s < L.NS; ++s) in[s] = xs[s];
+    for (int j = 0; j < L.NC; ++j) in[L.NS + j] = xc[j];
+    for (int j = 0; j < L.NDV; ++j) in[L.NS + L.NC + j] = xd[j];
+    (void)NI;
+}
+
+struct GoalSet {
+    int ngoals;
+    int nc, nacc;   // controls; accelerations before the auxiliary derivatives
+    const mh_goal* goals;
+    const int* gidx;
+    const int* gcol;
+    const double* gw;
+};
+
+__device__ double goal_integrand(const DevModel& M, const GoalSet& GS, int g, double t,
+        const double* st, const double* ct) {
+    const mh_goal G = GS.goals[g];
+    double L = 0.0;
+    for (int k = G.term_begin; k < G.term_begin + G.term_count; ++k) {
+        const int idx = GS.gidx[k];
+        const double w = GS.gw[k];
+        if (G.kind == MH_GOAL_CONTROL) {
+            const double v = ct[idx];
+            L += w * (G.exponent == 2 ? v * v : pow(fabs(v), (double)G.exponent));
+        } else if (G.kind == MH_GOAL_STATE_TRACKING) {
+            const double d = st[idx] - table_eval(M, G.table, GS.gcol[k], t);
+            L += w * (d * d);
+        } else if (G.kind == MH_GOAL_SUM_SQUARED_STATE) {
+            const double v = st[idx];
+            L += w * (v * v);
+        } else if (G.kind == MH_GOAL_AUX_DERIVATIVES) {
+            const double v = ct[GS.nc + GS.nacc + idx];   // derivatives follow the controls
+            L += w * (v * v);
+        }
+    }
+    return L;
+}
+
+// Per-point quad-weighted integrands: C[k*ngoals + g] = quad_k * L_g(k).
+template <class Z>
+__global__ void __launch_bounds__(64) k_integrand(DevModel M, Layout L, GoalSet GS,
+        const double* __restrict__ x, const double* __restrict__ grid,
+        const double* __restrict__ quad, double* __restrict__ C) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= L.G) return;
+    const double t = (x[1] - x[0]) * grid[k] + x[0];
+    double in[Z::MI];
+    gather_inputs(x, L, k, in, L.NI);
+    for (int g = 0; g < GS.ngoals; ++g) {
+        const bool integral = GS.goals[g].kind != MH_GOAL_FINAL_TIME;
+        C[(long)k * GS.ngoals + g] =
+                integral ? quad[k] * goal_integrand(M, GS, g, t, in, in + L.NS) : 0.0;
+    }
+}
+
+// Gradient of the integral terms: one lane per (grid point, direction).
+template <class Z>
+__global__ void __launch_bounds__(64) k_grad(DevModel M, Layout L, GoalSet GS, int fd, double h,
+        const double* __restrict__ x, const double* __restrict__ grid,
+        const double* __restrict__ quad, double* __restrict__ grad, double* __restrict__ tpart) {
+    const int ND = L.NI + 2;
+    const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (tid >= (long)L.G * ND) return;
+    const int k = (int)(tid / ND), d = (int)(tid % ND);
+    const double g = grid[k];
+    const double dur = x[1] - x[0];
+    const double t = dur * g + x[0];
+    double in[Z::MI];
+    gather_inputs(x, L, k, in, L.NI);
+    double acc = 0.0;
+    for (int gi = 0; gi < GS.ngoals; ++gi) {
+        const mh_goal G = GS.goals[gi];
+        if (G.kind == MH_GOAL_FINAL_TIME) continue;
+        const double seed = d == 0 ? 1.0 - g : (d == 1 ? g : 1.0);
+        double lp = 0.0, lm = 0.0, l0 = 0.0;
+        if (fd != MH_FD_CENTRAL) l0 = goal_integrand(M, GS, gi, t, in, in + L.NS);
+        if (fd != MH_FD_BACKWARD) {
+            if (d < 2) lp = goal_integrand(M, GS, gi, t + h * seed, in, in + L.NS);
+            else {
+                const double s = in[d - 2];
+                in[d - 2] = s + h;
+                lp = goal_integrand(M, GS, gi, t, in, in + L.NS);
+                in[d - 2] = s;
+            }
+        }
+        if (fd != MH_FD_FORWARD) {
+            if (d < 2) lm = goal_integrand(M, GS, gi, t - h * seed, in, in + L.NS);
+            else {
+                const double s = in[d - 2];
+                in[d - 2] = s - h;
+                lm = goal_integrand(M, GS, gi, t, in, in + L.NS);
+                in[d - 2] = s;
+            }
+        }
+        const double dL = fd == MH_FD_CENTRAL ? (lp - lm) / (2.0 * h)
+                        : (fd == MH_FD_FORWARD ? (lp - l0) / h : (l0 - lm) / h);
+        acc += G.weight * dur * quad[k] * dL;
+    }
+    if (d < 2) tpart[(long)k * 2 + d] = acc;
+    else if (d - 2 < L.NS) grad[2 + (long)k * L.NS + (d - 2)] = acc;
+    else if (d - 2 < L.NS + L.NC) grad[2 + (long)L.NS * L.G + (long)k * L.NC + (d - 2 - L.NS)] = acc;
+    else grad[2 + (long)(L.NS + L.NC) * L.G + (long)k * L.NDV + (d - 2 - L.NS - L.NC)] = acc;
+}
+
+
+// DAE probe: one lane per input row [time, states, controls].
+template <class D>
+__global__ void __launch_bounds__(64) k_dae_probe(DevModel M, Layout L, int npts,
+        const double* __restrict__ in, double* __restrict__ outp) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= npts) return;
+    const double* r = in + (long)p * (1 + L.NI);
+    double v[D::MI];
+    double out[D::MO];
+#pragma unroll
+    for (int i = 0; i < D::MI; ++i) v[i] = i < L.NI ? r[1 + i] : 0.0;
+    D::eval(M, r[0], v, out);
+#pragma unroll
+    for (int o = 0; o < D::MO; ++o)
+        if (o < L.NO) outp[(long)p * L.NO + o] = out[o];
+}
+
+// ------------------------------------------------------------------------
+// Host-side structures shared by the translation units.
+// ------------------------------------------------------------------------
+// Static description of a task-decomposed generated model (codegen.py).
+struct TaskInfo {
+    int ng, nst, nf, rw;
+    const int* group_nf;
+    const unsigned long long* reads;   // [ng][rw] bit i = group reads point input i
+    const unsigned char* time;         // [ng] group reads the time
+    const double* gflops;              // [ng] FP64 ops per group evaluation
+    double combine_flops;
+};
+
+// Task tables for one lane configuration (host copy + device view).
+struct TaskSet {
+    Tasks dev{};
+    int nblocks = 0;
+    double flops = 0.0;     // FP64 ops per launch (groups + combine)
+    double ntasks = 0.0;    // group evaluations per launch
+    std::vector<int> dlen, off, roles, jd, blk;
+    size_t t_doubles = 0, h_doubles = 0;
+};
+struct Backend;
+
+struct mh_ctx {
+    // problem
+    int NQ = 0, NZ = 0, NS = 0, NC = 0, NO = 0, NI = 0;
+    int scheme = 0, N = 0, G = 0, interp = 0, rpi = 0, nnz_int = 0;
+    int NDV = 0, nnz_tail = 0;     // implicit: accelerations per point, tail nonzeros
+    int npc = 0, ntail = 0;        // path equations per mesh point; tail rows (npc + residuals)
+    int NACC = 0, NAR = 0;         // accelerations (implicit multibody), implicit aux residuals per point
+    int NMB = 0;                   // multibody residual rows per point (implicit / prescribed: NQ)
+    int TQ = 0;                    // coordinates among the NLP states (0: prescribed kinematics)
+    int SO = 0;                    // callback output of state s's derivative: s + SO
+    int presc = 0, kin_table = -1;
+    std::vector<int> kin_col;
+    std::vector<int> mus_ider;     // muscle -> aux derivative index after the controls (-1)
+    double aux_lo = -1000.0, aux_hi = 1000.0;
+    int npe = 0;                   // path-constraint template entries per mesh point
+    std::vector<uint8_t> sp, sp_pc;  // detected sparsity [output][time, inputs] (empty: dense)
+    std::vector<mh_path_equation> pc;
+    PathEqs P{};
+    double acc_lo = -1000.0, acc_hi = 1000.0;
+    int ib = 0, ie = 0, k0 = 0, nk = 0;
+    int fd = 0;
+    double h = 1e-8;
+    int size_class = 0;
+    const struct Backend* be = nullptr;
+    Lanes lanes_jac{}, lanes_g{};
+    uint64_t model_hash = 0;
+    int64_t n = 0, m = 0, nnz = 0;
+    std::vector<double> grid, quad;
+    std::vector<TplEntry> tpl;
+    std::vector<int> tpl_col_pt;   // template column: point (0..2) or -1 for t0/tf
+    std::vector<int64_t> tpl_col_off;  // template column offset within point block
+    std::vector<mh_variable_info> sinfo, cinfo;
+    mh_bounds t_init{}, t_final{};
+    int ngoals = 0;
+    // device
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[5] = {};         // stage boundaries (+ ev[4] after k_groups)
+    char* dmem = nullptr;
+    DevModel M{};
+    GoalSet GS{};
+    double *d_x = nullptr, *d_grid = nullptr, *d_quad = nullptr, *d_times = nullptr, *d_Y = nullptr,
+           *d_Yg = nullptr, *d_g = nullptr, *d_vals = nullptr, *d_C = nullptr, *d_grad = nullptr,
+           *d_tpart = nullptr, *d_f = nullptr;
+    TplEntry* d_tpl = nullptr;
+    uint32_t* d_tplp = nullptr;    // packed template (k_interval)
+    std::vector<uint32_t> tplp;
+    float timings[4] = {0, 0, 0, 0};
+    // task-decomposed back ends
+    TaskSet ts_jac, ts_g, ts_probe;
+    double *d_T = nullptr, *d_H = nullptr;
+    char* probe_mem = nullptr;     // tables + T/H of the last mh_eval_dae size
+    double *d_pT = nullptr, *d_pH = nullptr;
+    int probe_np = -1;
+    // captured launch sequences, keyed by (kind, x, out pointers)
+    struct GraphEntry { int kind; const void *x, *a, *b; hipGraphExec_t exec; };
+    std::vector<GraphEntry> graphs;
+    bool use_graphs = false;
+    bool spin_wait = false;
+    // per lane configuration (0: eval_g lanes, 1: Jacobian lanes): combine
+    // and transcription fused in k_interval (LDS-resident raw outputs)
+    bool use_interval[2] = {false, false};
+    int nsimd = 1024;              // SIMDs of the device (4 per CU)
+    bool tables_lds = false;       // k_interval stages the packed template (MOCOHIP_TABLES=1)
+    bool asm_grid_stride = false;  // k_transcribe_gs (MOCOHIP_ASM=gs) instead of k_transcribe
+    bool quot = false;             // k_combine writes FD quotients (MOCOHIP_QUOT=1)
+    int yq[2] = {0, 0};            // per lane configuration: Y of the last evaluation holds quotients
+    bool timing = false;           // stage events for mh_last_timings (mh_set_timing)
+    bool groups_timed = false;     // the last evaluation recorded ev[4]
+};
+
+// Task tables and T/H buffers for an mh_eval_dae call (mocohip.hip).
+int probe_tasks(mh_ctx* c, const TaskInfo& ti, const Lanes& ln, int np);
+
+struct Backend {
+    const char* name;
+    // one evaluation stage: raw DAE outputs of every lane of c->lanes_g
+    // (mode 0) or c->lanes_jac (mode 1) into Y, base-lane times into d_times
+    void (*eval)(mh_ctx*, const double* x, int mode, double* Y);
+    void (*integrand)(mh_ctx*, const double* x);
+    void (*grad)(mh_ctx*, const double* x);
+    void (*probe)(mh_ctx*, int np, const double* in, double* out);
+    double flops_per_eval;   // generated back ends: emitted FP64 ops per DAE
+    const TaskInfo* tasks;   // task-decomposed back ends (else one lane per DAE)
+    // task back ends: fused combine + transcription (k_interval) for lanes
+    // of mode 0/1 writing g and/or values; null for one-lane back ends
+    void (*interval)(mh_ctx*, const double* x, int mode, double* g, double* v);
+    size_t (*interval_bytes)(const mh_ctx*, int mode);   // its LDS need
+};
+
+template <class D>
+static void be_eval_lane(mh_ctx* c, const double* x, int mode, double* Y) {
+    Layout L{c->NS, c->NC, c->TQ, c->NO, c->NI, c->G, c->k0, c->nk, c->NDV, c->NACC, c->SO};
+    const Lanes& ln = mode ? c->lanes_jac : c->lanes_g;
+    const long lanes = (long)c->nk * ln.stride;
+    hipLaunchKernelGGL(k_eval<D>, dim3((unsigned)((lanes + 63) / 64)), dim3(64), 0, c->stream, c->M, L,
+            ln, x, c->d_grid, c->d_times, Y);
+}
+template <class D>
+// Returns 1 when Y holds finite-difference quotients (k_combine quot mode,
+// Jacobian lanes staged in LDS), 0 when it holds raw lane values.
+static int launch_tasks(mh_ctx* c, const Src& S, const Lanes& ln, const TaskSet& ts, double* T,
+        double* H, double* times, double* Y, bool quot) {
+    hipLaunchKernelGGL(k_groups<D>, dim3((unsigned)ts.nblocks), dim3(64), 0, c->stream, c->M, S, ln,
+            ts.dev, T, H);
+    if (c->timing && times) (void)hipEventRecord(c->ev[4], c->stream);
+    const unsigned threads = (unsigned)((ln.stride + 63) / 64 * 64);
+    quot = quot && ln.stride > 1;
+    size_t lds = sizeof(double) * ((size_t)ts.dev.tdoubles + (size_t)ts.dev.nmass * D::NST);
+    if (quot) lds = std::max(lds, sizeof(double) * (size_t)D::NO * ln.stride);
+    if (threads <= 1024 && lds <= kMaxLds) {
+        if (lds > 65536)
+            (void)hipFuncSetAttribute((const void*)k_combine<D>,
+                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL(k_combine<D>, dim3((unsigned)ts.dev.nk), dim3(threads), lds, c->stream, c->M,
+                S, ln, ts.dev, T, H, times, Y, (long)D::NO * ln.stride, quot ? 1 : 0);
+        return quot ? 1 : 0;
+    } else {
+        const long lanes = (long)ts.dev.nk * ln.stride;
+        hipLaunchKernelGGL(k_combine_global<D>, dim3((unsigned)((lanes + 63) / 64)), dim3(64), 0,
+                c->stream, c->M, S, ln, ts.dev, T, H, times, Y, (long)D::NO * ln.stride);
+    }
+    return 0;
+}
+template <class D>
+static void be_eval_tasks(mh_ctx* c, const double* x, int mode, double* Y) {
+    const Src S{x, c->d_grid, nullptr, c->G, c->k0};
+    const Lanes& ln = mode ? c->lanes_jac : c->lanes_g;
+    const TaskSet& ts = mode ? c->ts_jac : c->ts_g;
+    if (c->use_interval[mode]) {   // combine happens inside k_interval
+        hipLaunchKernelGGL(k_groups<D>, dim3((unsigned)ts.nblocks), dim3(64), 0, c->stream, c->M, S, ln,
+                ts.dev, c->d_T, c->d_H);
+        return;
+    }
+    c->yq[mode] = launch_tasks<D>(c, S, ln, ts, c->d_T, c->d_H, c->d_times, Y, mode == 1 && c->quot);
+}
+// LDS bytes of k_interval for one lane configuration (0: does not apply).
+template <class D>
+static size_t interval_lds(const mh_ctx* c, const Lanes& ln, const TaskSet& ts, bool tables) {
+    const size_t npts = c->scheme == MH_HERMITE_SIMPSON ? 3 : 2;
+    const size_t tab = tables ? (size_t)(c->nnz_int + c->nnz_tail + 1) / 2 : 0;
+    return sizeof(double) * (npts * D::NO * ln.stride + 4 + npts * (size_t)(c->NS + c->NC + c->NDV) +
+                             npts * ((size_t)ts.dev.tdoubles + (size_t)ts.dev.nmass * D::NST) + tab);
+}
+template <class D>
+static size_t be_interval_bytes(const mh_ctx* c, int mode) {
+    return interval_lds<D>(c, mode ? c->lanes_jac : c->lanes_g, mode ? c->ts_jac : c->ts_g, false);
+}
+template <class D>
+static void be_interval(mh_ctx* c, const double* x, int mode, double* g, double* v) {
+    const Src S{x, c->d_grid, nullptr, c->G, c->k0};
+    const Lanes& ln = mode ? c->lanes_jac : c->lanes_g;
+    const TaskSet& ts = mode ? c->ts_jac : c->ts_g;
+    // stage the packed template too when it fits and MOCOHIP_TABLES=1
+    const size_t lds_tab = interval_lds<D>(c, ln, ts, true);
+    const int tables = c->tables_lds && lds_tab <= kMaxLds ? 1 : 0;
+    const size_t lds = tables ? lds_tab : interval_lds<D>(c, ln, ts, false);
+    if (lds > 65536)
+        (void)hipFuncSetAttribute((const void*)k_interval<D>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                (int)lds);
+    Layout L{c->NS, c->NC, c->TQ, c->NO, c->NI, c->G, c->k0, c->nk, c->NDV, c->NACC, c->SO};
+    Interval I{c->scheme, c->interp, c->ib, c->rpi, c->nnz_int, c->NMB + c->NAR, c->NMB, c->NQ + c->NZ,
+               c->N, c->nnz_tail, c->ntail, c->npe, c->P};
+    const unsigned threads = v ? 1024u : 256u;
+    hipLaunchKernelGGL(k_interval<D>, dim3((unsigned)(c->ie - c->ib)), dim3(threads), lds, c->stream, c->M,
+            S, ln, ts.dev, L, I, c->d_tpl, c->d_tplp, tables, c->d_T, c->d_H, g, v);
+}
+template <class D>
+static void be_integrand(mh_ctx* c, const double* x) {
+    Layout L{c->NS, c->NC, c->TQ, c->NO, c->NI, c->G, 0, c->G, c->NDV, c->NACC, c->SO};
+    hipLaunchKernelGGL(k_integrand<D>, dim3((c->G + 63) / 64), dim3(64), 0, c->stream, c->M, L,
+            c->GS, x, c->d_grid, c->d_quad, c->d_C);
+}
+template <class D>
+static void be_grad(mh_ctx* c, const double* x) {
+    Layout L{c->NS, c->NC, c->TQ, c->NO, c->NI, c->G, 0, c->G, c->NDV, c->NACC, c->SO};
+    const long tot = (long)c->G * (c->NI + 2);
+    hipLaunchKernelGGL(k_grad<D>, dim3((unsigned)((tot + 63) / 64)), dim3(64), 0, c->stream, c->M, L,
+            c->GS, c->fd, c->h, x, c->d_grid, c->d_quad, c->d_grad, c->d_tpart);
+}
+template <class D>
+static void be_probe_lane(mh_ctx* c, int np, const double* in, double* out) {
+    Layout L{c->NS, c->NC, c->TQ, c->NO, c->NI, c->G, 0, 0, c->NDV, c->NACC, c->SO};
+    hipLaunchKernelGGL(k_dae_probe<D>, dim3((np + 63) / 64), dim3(64), 0, c->stream, c->M, L, np, in,
+            out);
+}
+// mh_eval_dae through the task kernels: explicit points, base lanes only.
+template <class D>
+static void be_probe_tasks(mh_ctx* c, int np, const double* in, double* out) {
+    const Lanes ln{c->fd, c->NI + 2, 1, 0, c->h};
+    if (probe_tasks(c, *c->be->tasks, ln, np) != MH_OK) return;
+    const Src S{nullptr, nullptr, in, 0, 0};
+    (void)launch_tasks<D>(c, S, ln, c->ts_probe, c->d_pT, c->d_pH, nullptr, out, false);
+}
+template <class D>
+static constexpr Backend make_backend_lane(const char* name, double flops) {
+    return Backend{name, &be_eval_lane<D>, &be_integrand<D>, &be_grad<D>, &be_probe_lane<D>, flops,
+                   nullptr, nullptr, nullptr};
+}
+template <class D>
+struct TaskInfoOf {
+    static constexpr TaskInfo value{D::NG, D::NST, D::NF, D::RW, D::GROUP_NF, &D::GROUP_READS[0][0],
+                                    D::GROUP_TIME, D::GROUP_FLOPS, D::COMBINE_FLOPS};
+};
+template <class D>
+static constexpr Backend make_backend_tasks(const char* name, double flops) {
+    return Backend{name, &be_eval_tasks<D>, &be_integrand<D>, &be_grad<D>, &be_probe_tasks<D>, flops,
+                   &TaskInfoOf<D>::value, &be_interval<D>, &be_interval_bytes<D>};
+}
+
+// Generic device-interpreter back ends (generic.hip), one per size class.
+const Backend* generic_backends();
+// A model-specialized back end (generated/gen_<model>.hip): the task kernels
+// (default) and the one-lane-per-DAE kernel (MOCOHIP_BACKEND=lane).
+struct GenEntry { uint64_t hash; Backend tasks, lane; };
+#define MH_GEN_ENTRY(T, H, NAME)                                                   \
+    GenEntry{H, make_backend_tasks<T>("generated:" NAME, T::FLOPS_PER_EVAL),        \
+             make_backend_lane<T>("generated-lane:" NAME, T::FLOPS_PER_EVAL)}
+

@@ -259,6 +259,39 @@ def load_oracle(path: str | None = None):
     return _libs[path]
 
 
+def _fnv1a(h: int, data: bytes) -> int:
+    for b in data:
+        h = ((h ^ b) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
+    return h
+
+
+def model_hash(m: "mh_model") -> int:
+    """mh_model_hash (mocohip.hip model_hash) restated on the host: FNV-1a
+    64 over the model tape's counts, gravity, bodies, axes, functions, knots,
+    muscles, path points, actuators, external loads and their tables' shapes
+    (the keys of the generated back ends; tests/test_abi.py checks it against
+    the library)."""
+    h = 1469598103934665603
+    h = _fnv1a(h, bytes((i32 * 9)(m.nq, m.nbodies, m.naxes, m.nfunctions, m.nknots,
+                                    m.nmuscles, m.npoints, m.nactuators, m.nexternal)))
+    h = _fnv1a(h, bytes(m.gravity))
+
+    def arr(ptr, T, n):
+        return C.string_at(ptr, C.sizeof(T) * n) if n > 0 else b""
+    for ptr, T, n in ((m.bodies, mh_body, m.nbodies), (m.axes, mh_axis, m.naxes),
+                      (m.functions, mh_function, m.nfunctions), (m.knot_x, f64, m.nknots),
+                      (m.knot_y, f64, m.nknots), (m.muscles, mh_muscle, m.nmuscles),
+                      (m.points, mh_path_point, m.npoints),
+                      (m.actuators, mh_actuator, m.nactuators),
+                      (m.external, mh_external_force, m.nexternal)):
+        h = _fnv1a(h, arr(ptr, T, n))
+    for e in range(m.nexternal):
+        t = m.external[e].table
+        if 0 <= t < m.ntables:
+            h = _fnv1a(h, bytes((i32 * 2)(m.tables[t].degree, m.tables[t].ncol)))
+    return h
+
+
 def dptr(a):
     """ctypes double* of a contiguous float64 numpy array."""
     return a.ctypes.data_as(P(f64))

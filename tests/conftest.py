@@ -22,5 +22,6 @@ def _built():
     subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
     lib = os.path.join(PKG, "csrc", "build", "libmocohip.so")
     if not os.path.exists(lib):
-        subprocess.run(["make", "-s", "-C", os.path.join(PKG, "csrc")], check=True)
+        import __graft_entry__
+        __graft_entry__.build()
     yield

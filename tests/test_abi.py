@@ -40,6 +40,18 @@ def test_library_loads_and_exports_every_symbol():
     assert set(abi.MOCOHIP_SYMBOLS) <= exported
 
 
+@pytest.mark.parametrize("name", ["sliding_mass", "double_pendulum", "gait10dof18musc"])
+def test_host_model_hash_matches_library(name):
+    """tools/gen_models.py keys the generated back ends with abi.model_hash
+    (host restatement); mh_create selects them with mh_model_hash."""
+    from mocohip import configs
+    lib = abi.load_mocohip()
+    rep = configs.CONFIGS[name](4).problem.create_rep()
+    h = C.c_uint64()
+    assert lib.mh_model_hash(C.byref(rep.struct.model), C.byref(h)) == 0
+    assert h.value == abi.model_hash(rep.struct.model)
+
+
 def test_library_is_gfx950_code_object():
     out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "-n", abi.LIBMOCOHIP_PATH],
                          capture_output=True, text=True)
