@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define MH_ABI_VERSION 2
+#define MH_ABI_VERSION 3
 
 enum mh_status {
     MH_OK = 0,
@@ -267,6 +267,30 @@ typedef struct mh_path_equation {
     mh_bounds g;         /* bounds on the constraint row                   */
 } mh_path_equation;
 
+/* Endpoint constraints (CasOC endpoint constraint functions; MocoGoal in
+ * Mode::EndpointConstraint, MocoGoal.h:96-137): one row of g per equation,
+ * ALL of them before the first mesh point's rows (flattenConstraints,
+ * CasOCTranscription.h:283-285; values CasOCTranscription.cpp:548-584).
+ * An equation is a function of the Endpoint callback's inputs
+ * (CasOCFunction.h:167-240): initial_time, the initial grid point's
+ * states / controls / derivatives, final_time, the final grid point's.
+ * Without sparsity detection its Jacobian row is dense over all of those
+ * columns (ascending x order); its values are finite-difference quotients
+ * of the function along each column, as for the per-point callbacks. */
+enum mh_endpoint_kind {
+    /* MocoInitialActivationGoal (MocoInitialActivationGoal.cpp:41-58):
+     * initial control[index_a] (excitation) - initial state[index_b]
+     * (activation); bounds default [0, 0] (MocoConstraintInfo.h:44-54) */
+    MH_ENDPOINT_INITIAL_ACTIVATION = 0
+};
+typedef struct mh_endpoint_equation {
+    int32_t kind;        /* mh_endpoint_kind                               */
+    int32_t index_a;
+    int32_t index_b;
+    int32_t reserved;
+    mh_bounds g;         /* bounds on the row                              */
+} mh_endpoint_equation;
+
 typedef struct mh_problem {
     mh_model model;
     mh_bounds time_initial;      /* bounds on initial_time                  */
@@ -295,6 +319,9 @@ typedef struct mh_problem {
     int32_t prescribed_kinematics; /* 0: none (zero-initialised default)   */
     int32_t kinematics_table;
     const int32_t* kinematics_column;
+    int32_t nendpoint;           /* endpoint-constraint equations (rows 0..) */
+    int32_t reserved2;
+    const mh_endpoint_equation* endpoint;
 } mh_problem;
 
 enum mh_scheme { MH_HERMITE_SIMPSON = 0, MH_TRAPEZOIDAL = 1 };
@@ -368,9 +395,11 @@ typedef struct mh_nlp_info {
     int64_t num_grid_points;
     int64_t num_states, num_controls;
     /* shard: rows [row_begin,row_end) and nonzeros [nnz_begin,nnz_end).
-     * The tail -- the final mesh point's path rows, then (implicit mode) the
-     * final grid point's residual rows -- follows the last interval; the
-     * shard owning the last interval owns it too.                          */
+     * The head -- the endpoint-constraint rows -- precedes the first
+     * interval and belongs to the shard owning it.  The tail -- the final
+     * mesh point's path rows, then (implicit mode) the final grid point's
+     * residual rows -- follows the last interval; the shard owning the last
+     * interval owns it too.                                                */
     int64_t row_begin, row_end;
     int64_t nnz_begin, nnz_end;
 } mh_nlp_info;
@@ -432,9 +461,11 @@ int mh_get_backend(const mh_ctx* ctx, char* name, int32_t name_len,
  * ("tasks interval" = task kernels with the fused per-interval transcription
  * for the Jacobian lanes; "lane", "generic", "split", ...). */
 int mh_get_backend_flags(const mh_ctx* ctx, char* flags, int32_t len);
-/* The callback sparsity the Jacobian structure was built from: (NQ + NZ)
- * DAE outputs then npath path equations, each a row of 1 + NS + NC + NDV
- * flags [time, states, controls, accelerations] (all 1 without detection).
+/* The callback sparsity the Jacobian structure was built from: the NO DAE
+ * outputs then the npath path equations, each a row of W = 1 + NS + NC +
+ * NDV flags [time, states, controls, derivatives], then the nendpoint
+ * endpoint equations, each a row of 2 W flags [initial_time, initial point
+ * inputs, final_time, final point inputs] (all 1 without detection).
  * len = the capacity of `pattern` in bytes. */
 int mh_get_callback_sparsity(const mh_ctx* ctx, uint8_t* pattern, int64_t len);
 /* FNV-1a hash of everything the per-point DAE depends on (host only). */
@@ -446,6 +477,19 @@ int mh_model_hash(const mh_model* model, uint64_t* hash);
  * finite-difference lane would need per eval_jac_g.  0 where unknown (the
  * generic interpreter's op count is not tracked). */
 int mh_get_work(const mh_ctx* ctx, double* work4);
+
+/* Test / debug entry (parity tests): the raw finite-difference lane outputs
+ * behind mh_eval_jac_g at x (host pointers; unsharded contexts only), so a
+ * checker can re-derive the Jacobian values from the same DAE outputs.
+ * times[G]: each grid point's time (t0 + (tf - t0) grid_k, as the lanes
+ * use it); Y[(k NO + o) S + r]: callback output o of lane r at grid point k.
+ * With ND = 2 + NS + NC + NDV directions (t0, tf, then the point inputs):
+ * forward / backward, S = ND + 1: lane d < ND perturbs direction d by +h /
+ * -h, lane ND is unperturbed; central, S = 2 ND + 1: lanes 0..ND-1 at +h,
+ * ND..2ND-1 at -h, lane 2 ND unperturbed.  A t0 / tf lane moves the time by
+ * step (1 - grid_k) / step grid_k (CasOCTranscription.cpp:126-127). */
+int mh_debug_jacobian_lanes(mh_ctx* ctx, const double* x, double* times,
+        double* Y);
 
 /* Stage timing: when on, every evaluation records HIP events between its
  * stages on the context stream and mh_last_timings reports them.  Off by

@@ -39,7 +39,8 @@ enum TplKind : uint8_t {
     T_HERM_T = 0, T_SIMP_T = 1, T_HERM_X = 2, T_SIMP_X = 3, T_INTERP = 4,
     T_TRAP_T = 5, T_TRAP_X = 6,
     T_RES = 7,     // implicit multibody residual output s at point pt
-    T_PATH = 8     // path-constraint equation s at mesh point pt
+    T_PATH = 8,    // path-constraint equation s at mesh point pt
+    T_EP = 9       // endpoint equation row along endpoint input dir (EndpointEqs)
 };
 struct TplEntry {
     int16_t row;   // row within the interval
@@ -138,6 +139,7 @@ __device__ __forceinline__ void load_point(const double* __restrict__ x, const L
 template <class D>
 __device__ __forceinline__ double lane_inputs(const Layout& L, const Lanes& Ln,
         const double* __restrict__ x, double g, int k, int r, double (&in)[D::MI]) {
+#pragma clang fp contract(off)
     const double t0 = x[0], tf = x[1];
     double t = (tf - t0) * g + t0;
     load_point<D>(x, L, k, in);
@@ -240,6 +242,7 @@ struct LaneInL {
 // arithmetic: every kernel that evaluates lanes goes through it.
 __device__ __forceinline__ double lane_time(const Lanes& Ln, double g, double t0, double tf, int r,
         int& pi, double& step) {
+#pragma clang fp contract(off)
     double t = (tf - t0) * g + t0;
     pi = -1;
     step = 0.0;
@@ -469,6 +472,18 @@ struct PathEqs {
     const double* __restrict__ grid;
 };
 
+// Endpoint-constraint equations (include/mocohip.h mh_endpoint_equation):
+// rows 0..nep of g and Jacobian entries 0..nnz of the shard that owns the
+// first mesh interval.  The Endpoint callback's input vector (CasOCFunction.h:
+// 167-240) is [initial_time, initial point inputs (NI), final_time, final
+// point inputs]; W = 1 + NI per point.  Template entry: row = equation,
+// dir = index into that vector.
+struct EndpointEqs {
+    int nep, nnz, W;
+    const mh_endpoint_equation* __restrict__ eq;
+    const TplEntry* __restrict__ tpl;
+};
+
 struct Interval {
     int scheme;      // MH_HERMITE_SIMPSON / MH_TRAPEZOIDAL
     int interp;
@@ -485,6 +500,11 @@ struct Interval {
     int ntail;       // tail rows: final mesh point's path rows + final residuals
     int npe;         // path-constraint entries per mesh point (lead the interval / tail)
     PathEqs P;
+    // the head (endpoint rows), written by the first interval's block when
+    // this shard owns it: gh / vh = the shard's g / values (null otherwise)
+    EndpointEqs E;
+    double* gh;
+    double* vh;
     // Every interval opens with its mesh point's path rows.  The interval
     // N-1 also owns the tail (flattenConstraints, CasOCTranscription.h:
     // 286-308): the final mesh point's path rows, then the final grid
@@ -552,6 +572,53 @@ __device__ __forceinline__ double path_quot(const PathEqs& P, const Lanes& Ln, i
     return (v0 - (cm - path_bound(P, E, tm))) / h;
 }
 
+// x index of endpoint input si (initial / final grid point, see EndpointEqs).
+__device__ __forceinline__ long ep_xindex(const Layout& L, int W, int si) {
+    const int pt = si >= W ? 1 : 0, j = si - pt * W - 1;
+    if (j < 0) return pt;   // initial_time = x[0], final_time = x[1]
+    const long k = pt ? L.G - 1 : 0;
+    if (j < L.NS) return 2 + k * L.NS + j;
+    if (j < L.NS + L.NC) return 2 + (long)L.NS * L.G + k * L.NC + (j - L.NS);
+    return 2 + (long)(L.NS + L.NC) * L.G + k * L.NDV + (j - L.NS - L.NC);
+}
+// An endpoint equation on its input vector (accessor in(si)).
+// MH_ENDPOINT_INITIAL_ACTIVATION: MocoInitialActivationGoal::calcGoalImpl in
+// endpoint-constraint mode (MocoInitialActivationGoal.cpp:41-58).
+template <class A>
+__device__ __forceinline__ double ep_eval(const mh_endpoint_equation& Q, int NS, const A& in) {
+    return in(1 + NS + Q.index_a) - in(1 + Q.index_b);
+}
+// Value of equation e at iterate x with input pi perturbed by step (-1: none).
+__device__ __forceinline__ double ep_value(const Layout& L, const EndpointEqs& E, const double* __restrict__ x,
+        int e, int pi, double step) {
+    const mh_endpoint_equation Q = E.eq[e];
+    return ep_eval(Q, L.NS, [&](int si) {
+        const double v = x[ep_xindex(L, E.W, si)];
+        return si == pi ? v + step : v;
+    });
+}
+// The head: endpoint rows of g and their Jacobian entries (CasADi
+// FiniteDiff quotients along each structural column, as for the DAE lanes).
+__device__ __forceinline__ void endpoint_head(const Layout& L, const Lanes& Ln, const EndpointEqs& E,
+        const double* __restrict__ x, double* __restrict__ g, double* __restrict__ v, int tid, int nthr) {
+#pragma clang fp contract(off)
+    if (g)
+        for (int r = tid; r < E.nep; r += nthr) g[r] = ep_value(L, E, x, r, -1, 0.0);
+    if (v)
+        for (int q = tid; q < E.nnz; q += nthr) {
+            const TplEntry T = E.tpl[q];
+            const double h = Ln.h;
+            double d;
+            if (Ln.fd == MH_FD_CENTRAL)
+                d = (ep_value(L, E, x, T.row, T.dir, h) - ep_value(L, E, x, T.row, T.dir, -h)) / (2.0 * h);
+            else if (Ln.fd == MH_FD_FORWARD)
+                d = (ep_value(L, E, x, T.row, T.dir, h) - ep_value(L, E, x, T.row, -1, 0.0)) / h;
+            else
+                d = (ep_value(L, E, x, T.row, -1, 0.0) - ep_value(L, E, x, T.row, T.dir, -h)) / h;
+            v[q] = d;
+        }
+}
+
 __device__ __forceinline__ int grid_of(const Interval& I, int i, int pt) {
     return I.scheme == MH_HERMITE_SIMPSON ? 2 * i + pt : i + pt;
 }
@@ -606,6 +673,7 @@ struct YS {
 template <class YV>
 __device__ __forceinline__ double xdot_at(const Layout& L, const Lanes& Ln,
         const double* __restrict__ x, const YV& Y, int k, int s) {
+#pragma clang fp contract(off)
     if (s < L.NQ) return Y.xs(k, L.NQ + s);
     if (L.NACC && s < 2 * L.NQ) return Y.xd(k, s - L.NQ);   // implicit: udot = w
     return Y.row(k, s + L.SO)[Ln.base];
@@ -614,6 +682,7 @@ __device__ __forceinline__ double xdot_at(const Layout& L, const Lanes& Ln,
 template <class YV>
 __device__ __forceinline__ double defect_row(const Layout& L, const Interval& I, const Lanes& Ln,
         const double* __restrict__ x, const YV& Y, int i, int r) {
+#pragma clang fp contract(off)
     const int NS = L.NS;
     // residual rows: the interval's grid points (HS: 2, trapezoidal: 1), and
     // for the last interval the final grid point after all its other rows
@@ -659,6 +728,7 @@ __device__ __forceinline__ double defect_row(const Layout& L, const Interval& I,
 // d (DAE output o) / d dir at grid point k (the finite-difference quotient).
 template <class YV>
 __device__ __forceinline__ double dout(const Lanes& Ln, const YV& Y, int k, int o, int dir) {
+#pragma clang fp contract(off)
     const auto y = Y.row(k, o);
     if (Y.q) return y[dir];
     if (Ln.fd == MH_FD_CENTRAL) return (y[dir] - y[Ln.ND + dir]) / (2.0 * Ln.h);
@@ -683,6 +753,7 @@ constexpr int ASM_CHUNK = 1024;   // nonzeros per assembly workgroup
 // interval; exactly the subexpressions the formulas would form per entry).
 struct IvC { double h8, h6, hh, g8, g6, gh; };
 __device__ __forceinline__ IvC iv_const(double h, double dgap) {
+#pragma clang fp contract(off)
     return IvC{h / 8.0, h / 6.0, 0.5 * h, dgap / 8.0, dgap / 6.0, 0.5 * dgap};
 }
 
@@ -694,6 +765,11 @@ __device__ __forceinline__ IvC iv_const(double h, double dgap) {
 template <bool WITH_PATH = true, class YV>
 __device__ __forceinline__ double jac_entry(const Layout& L, const Lanes& Ln, const PathEqs& P,
         const double* __restrict__ x, const YV& Y, const TplEntry T, int k_first, const IvC& C) {
+    // no contraction anywhere in the Jacobian / defect arithmetic: every
+    // product and sum rounds on its own, exactly as the checker's (oracle)
+    // restatement of the same formulas does (tests/test_gpu_parity.py
+    // test_jacobian_assembly_bit_exact_from_device_lanes)
+#pragma clang fp contract(off)
     const int s = T.s, dir = T.dir;
     double v = 0.0;
     switch (T.kind) {
@@ -832,6 +908,7 @@ __global__ void __launch_bounds__(1024) k_interval(DevModel M, Src S, Lanes Ln, 
     // reads them; the base slot keeps the raw value for the defect rows
     const int quot = values && Ln.stride > 1;
     if (quot) {
+#pragma clang fp contract(off)
         const int ndir = Ln.ND;
         for (int w = threadIdx.x; w < npts * D::NO * ndir; w += blockDim.x) {
             const int po = w / ndir, d = w - po * ndir;
@@ -888,6 +965,8 @@ __global__ void __launch_bounds__(1024) k_interval(DevModel M, Src S, Lanes Ln, 
             }
         }
     }
+    if (i == 0 && (I.gh || I.vh))
+        endpoint_head(L, Ln, I.E, S.x, g ? I.gh : nullptr, values ? I.vh : nullptr, threadIdx.x, blockDim.x);
 }
 
 // ---- objective -------------------------------------------------------------
@@ -1061,6 +1140,13 @@ struct mh_ctx {
     std::vector<uint8_t> sp, sp_pc;  // detected sparsity [output][time, inputs] (empty: dense)
     std::vector<mh_path_equation> pc;
     PathEqs P{};
+    // endpoint constraints: the head of g (rows 0..nep) and of the Jacobian
+    // (entries 0..nnz_ep), owned by the shard with interval 0
+    int nep = 0, nnz_ep = 0;
+    std::vector<mh_endpoint_equation> ep;
+    std::vector<TplEntry> eptpl;       // row = equation, dir = endpoint input index
+    std::vector<uint8_t> sp_ep;        // detected [equation][2 (1 + NI)] (empty: dense)
+    EndpointEqs E{};
     double acc_lo = -1000.0, acc_hi = 1000.0;
     int ib = 0, ie = 0, k0 = 0, nk = 0;
     int fd = 0;
@@ -1114,6 +1200,21 @@ struct mh_ctx {
     bool groups_timed = false;     // the last evaluation recorded ev[4]
 };
 
+// The transcription's per-call view of the context.  g / v (this shard's
+// rows / nonzeros) are advanced past the head, which the first interval's
+// block writes through I.gh / I.vh when this shard owns it.
+inline Interval make_interval(const mh_ctx* c, double*& g, double*& v) {
+    Interval I{c->scheme, c->interp, c->ib, c->rpi, c->nnz_int, c->NMB + c->NAR, c->NMB, c->NQ + c->NZ,
+               c->N, c->nnz_tail, c->ntail, c->npe, c->P, c->E, nullptr, nullptr};
+    if (c->ib == 0 && c->nep > 0) {
+        I.gh = g;
+        I.vh = v;
+        if (g) g += c->nep;
+        if (v) v += c->nnz_ep;
+    }
+    return I;
+}
+
 // Task tables and T/H buffers for an mh_eval_dae call (mocohip.hip).
 int probe_tasks(mh_ctx* c, const TaskInfo& ti, const Lanes& ln, int np);
 
@@ -1131,6 +1232,10 @@ struct Backend {
     // of mode 0/1 writing g and/or values; null for one-lane back ends
     void (*interval)(mh_ctx*, const double* x, int mode, double* g, double* v);
     size_t (*interval_bytes)(const mh_ctx*, int mode);   // its LDS need
+    // raw outputs of every Jacobian lane into Y ([point][output][lane]) and
+    // the base-lane times into d_times, whatever path eval_jac_g takes
+    // (mh_debug_jacobian_lanes)
+    void (*lanes)(mh_ctx*, const double* x, double* Y);
 };
 
 template <class D>
@@ -1204,8 +1309,7 @@ static void be_interval(mh_ctx* c, const double* x, int mode, double* g, double*
         (void)hipFuncSetAttribute((const void*)k_interval<D>, hipFuncAttributeMaxDynamicSharedMemorySize,
                 (int)lds);
     Layout L{c->NS, c->NC, c->TQ, c->NO, c->NI, c->G, c->k0, c->nk, c->NDV, c->NACC, c->SO};
-    Interval I{c->scheme, c->interp, c->ib, c->rpi, c->nnz_int, c->NMB + c->NAR, c->NMB, c->NQ + c->NZ,
-               c->N, c->nnz_tail, c->ntail, c->npe, c->P};
+    const Interval I = make_interval(c, g, v);
     const unsigned threads = v ? 1024u : 256u;
     hipLaunchKernelGGL(k_interval<D>, dim3((unsigned)(c->ie - c->ib)), dim3(threads), lds, c->stream, c->M,
             S, ln, ts.dev, L, I, c->d_tpl, c->d_tplp, tables, c->d_T, c->d_H, g, v);
@@ -1238,9 +1342,16 @@ static void be_probe_tasks(mh_ctx* c, int np, const double* in, double* out) {
     (void)launch_tasks<D>(c, S, ln, c->ts_probe, c->d_pT, c->d_pH, nullptr, out, false);
 }
 template <class D>
+static void be_lanes_lane(mh_ctx* c, const double* x, double* Y) { be_eval_lane<D>(c, x, 1, Y); }
+template <class D>
+static void be_lanes_tasks(mh_ctx* c, const double* x, double* Y) {
+    const Src S{x, c->d_grid, nullptr, c->G, c->k0};
+    (void)launch_tasks<D>(c, S, c->lanes_jac, c->ts_jac, c->d_T, c->d_H, c->d_times, Y, false);
+}
+template <class D>
 static constexpr Backend make_backend_lane(const char* name, double flops) {
     return Backend{name, &be_eval_lane<D>, &be_integrand<D>, &be_grad<D>, &be_probe_lane<D>, flops,
-                   nullptr, nullptr, nullptr};
+                   nullptr, nullptr, nullptr, &be_lanes_lane<D>};
 }
 template <class D>
 struct TaskInfoOf {
@@ -1250,7 +1361,7 @@ struct TaskInfoOf {
 template <class D>
 static constexpr Backend make_backend_tasks(const char* name, double flops) {
     return Backend{name, &be_eval_tasks<D>, &be_integrand<D>, &be_grad<D>, &be_probe_tasks<D>, flops,
-                   &TaskInfoOf<D>::value, &be_interval<D>, &be_interval_bytes<D>};
+                   &TaskInfoOf<D>::value, &be_interval<D>, &be_interval_bytes<D>, &be_lanes_tasks<D>};
 }
 
 // Generic device-interpreter back ends (generic.hip), one per size class.

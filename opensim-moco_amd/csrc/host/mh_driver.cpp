@@ -74,6 +74,7 @@ struct Tape {
     std::vector<int32_t> gidx, gcol;
     std::vector<double> gw;
     std::vector<mh_path_equation> path;
+    std::vector<mh_endpoint_equation> endpoint;
     std::vector<double> guess;
     std::vector<uint8_t> pattern;
     std::vector<int32_t> kin_col;
@@ -98,7 +99,7 @@ bool read_tape(const char* path, Tape& t, std::string& err) {
     const int version = r.pod<int32_t>();
     t.ns = r.pod<int32_t>();
     t.nc = r.pod<int32_t>();
-    if (version != 1 && version != 2) { err = "unsupported tape version"; return false; }
+    if (version < 1 || version > 3) { err = "unsupported tape version"; return false; }
     t.opts = r.pod<mh_options>();
     mh_model& m = t.prob.model;
     int32_t* counts[] = {&m.nq, &m.nbodies, &m.naxes, &m.nfunctions, &m.nknots, &m.nmuscles,
@@ -149,6 +150,10 @@ bool read_tape(const char* path, Tape& t, std::string& err) {
         t.prob.kinematics_table = r.pod<int32_t>();
         t.kin_col = r.array<int32_t>(t.prob.prescribed_kinematics ? m.nq : 0);
     }
+    if (version >= 3) {   // endpoint-constraint equations
+        t.prob.nendpoint = r.pod<int32_t>();
+        t.endpoint = r.array<mh_endpoint_equation>(t.prob.nendpoint);
+    }
     if (!r.ok || r.pos != r.buf.size()) { err = "truncated or malformed tape"; return false; }
     m.bodies = t.bodies.data(); m.axes = t.axes.data(); m.functions = t.functions.data();
     m.knot_x = t.knot_x.data(); m.knot_y = t.knot_y.data(); m.muscles = t.muscles.data();
@@ -164,6 +169,7 @@ bool read_tape(const char* path, Tape& t, std::string& err) {
     t.opts.sparsity_guess = t.guess.empty() ? nullptr : t.guess.data();
     t.opts.sparsity_pattern = t.pattern.empty() ? nullptr : t.pattern.data();
     t.prob.kinematics_column = t.kin_col.empty() ? nullptr : t.kin_col.data();
+    t.prob.endpoint = t.endpoint.empty() ? nullptr : t.endpoint.data();
     return true;
 }
 

@@ -74,6 +74,8 @@ __global__ void __launch_bounds__(256) k_transcribe(Layout L, Interval I, Lanes 
         double* gi = g + (long)il * I.rpi;
         for (int r = threadIdx.x; r < I.rows(i); r += blockDim.x) gi[r] = defect_row(L, I, Ln, x, YV, i, r);
     }
+    if (i == 0 && blockIdx.x == 0 && (I.gh || I.vh))
+        endpoint_head(L, Ln, I.E, x, g ? I.gh : nullptr, values ? I.vh : nullptr, threadIdx.x, blockDim.x);
 }
 
 // Transcription stage of the split path as a grid-stride loop over the
@@ -130,6 +132,8 @@ __global__ void __launch_bounds__(256) k_transcribe_gs(Layout L, Interval I, Lan
             for (int r = I.rpi + tid; r < I.rows(i); r += nthreads)
                 g[(long)il * I.rpi + r] = defect_row(L, I, Ln, x, YV, i, r);
     }
+    if (I.ib == 0 && (I.gh || I.vh))
+        endpoint_head(L, Ln, I.E, x, g ? I.gh : nullptr, values ? I.vh : nullptr, tid, nthreads);
 }
 
 // Single-workgroup deterministic reduction of the objective (mode 0) or of
@@ -386,6 +390,17 @@ static int64_t col_deriv(const mh_ctx* c, int64_t k, int j) {
     return 2 + (int64_t)(c->NS + c->NC) * c->G + k * c->NDV + j;
 }
 
+// x column of endpoint input si: [initial_time, initial point inputs,
+// final_time, final point inputs] (EndpointEqs, CasOCFunction.h:167-240).
+static int64_t ep_col(const mh_ctx* c, int si) {
+    const int W = 1 + c->NI, pt = si / W, j = si % W - 1;
+    if (j < 0) return pt;
+    const int64_t k = pt ? c->G - 1 : 0;
+    if (j < c->NS) return col_state(c, k, j);
+    if (j < c->NS + c->NC) return col_control(c, k, j - c->NS);
+    return col_deriv(c, k, j - c->NS - c->NC);
+}
+
 // Build the per-interval template in CasOC row order with columns sorted
 // ascending (the block-dense structural rule), then
 // (implicit mode) the tail template: the final grid point's residual rows,
@@ -522,6 +537,27 @@ static void build_template(mh_ctx* c) {
     c->ntail = row - c->rpi;
     c->npe = 0;
     for (int e = 0; e < c->nnz_int; ++e) c->npe += c->tpl[e].kind == T_PATH;
+    // the head: each endpoint equation's row over its inputs (all of them
+    // without detection, Endpoint callback dense Jacobian; else the detected
+    // ones), columns ascending (the initial and the final point's blocks
+    // interleave per variable kind)
+    c->eptpl.clear();
+    const int WE = 2 * W;
+    for (int e = 0; e < c->nep; ++e) {
+        std::vector<std::pair<int64_t, int>> cols;
+        for (int si = 0; si < WE; ++si)
+            if (c->sp_ep.empty() || c->sp_ep[(size_t)e * WE + si]) cols.push_back({ep_col(c, si), si});
+        std::sort(cols.begin(), cols.end());
+        for (const auto& cs : cols) {
+            TplEntry t{};
+            t.row = (int16_t)e;
+            t.kind = T_EP;
+            t.dir = (int16_t)cs.second;
+            t.s = (int16_t)e;
+            c->eptpl.push_back(t);
+        }
+    }
+    c->nnz_ep = (int)c->eptpl.size();
 }
 
 // k_interval writes the path-constraint entries in a loop of their own over
@@ -619,6 +655,17 @@ static int validate_and_layout(mh_ctx* c, const mh_problem* p, const mh_options*
                 (E.table >= 0 && (E.column < 0 || E.column >= M.tables[E.table].ncol)))
             return set_err(MH_ERR_INVALID, "path equation %d: bad control/table", e);
     }
+    if (p->nendpoint < 0 || (p->nendpoint > 0 && !p->endpoint))
+        return set_err(MH_ERR_INVALID, "bad endpoint constraints");
+    c->nep = p->nendpoint;
+    c->ep.assign(p->endpoint, p->endpoint + p->nendpoint);
+    for (int e = 0; e < c->nep; ++e) {
+        const mh_endpoint_equation& E = c->ep[e];
+        if (E.kind != MH_ENDPOINT_INITIAL_ACTIVATION)
+            return set_err(MH_ERR_UNSUPPORTED, "endpoint equation %d: kind %d", e, E.kind);
+        if (E.index_a < 0 || E.index_a >= c->NC || E.index_b < 0 || E.index_b >= c->NS)
+            return set_err(MH_ERR_INVALID, "endpoint equation %d: bad control/state", e);
+    }
     for (int ia = 0; ia < M.nactuators; ++ia) {
         const mh_actuator& a = M.actuators[ia];
         if (a.kind == MH_ACT_MUSCLE) {
@@ -707,8 +754,10 @@ static int validate_and_layout(mh_ctx* c, const mh_problem* p, const mh_options*
     c->n = 2 + (int64_t)(c->NS + c->NC + c->NDV) * c->G;
     build_template(c);
     if (!path_entries_lead(c)) return set_err(MH_ERR_INVALID, "internal: path-constraint template layout");
-    c->m = (int64_t)c->rpi * c->N + c->ntail;    // + the final mesh point's path rows and residuals
-    c->nnz = (int64_t)c->nnz_int * c->N + c->nnz_tail;
+    // endpoint rows first, then the intervals, then the tail (the final mesh
+    // point's path rows and residuals)
+    c->m = c->nep + (int64_t)c->rpi * c->N + c->ntail;
+    c->nnz = c->nnz_ep + (int64_t)c->nnz_int * c->N + c->nnz_tail;
     c->ib = std::max(0, o->interval_begin);
     c->ie = o->interval_end > 0 ? std::min(o->interval_end, c->N) : c->N;
     if (c->ib >= c->ie) return set_err(MH_ERR_INVALID, "empty interval shard [%d, %d)", c->ib, c->ie);
@@ -845,7 +894,9 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
                  o_grid = A.put(c->grid.data(), c->grid.size()),
                  o_quad = A.put(c->quad.data(), c->quad.size()),
                  o_tpl = A.put(c->tpl.data(), c->tpl.size()),
-                 o_pc = A.put(c->pc.data(), c->pc.size());
+                 o_pc = A.put(c->pc.data(), c->pc.size()),
+                 o_ep = A.put(c->ep.data(), c->ep.size()),
+                 o_eptpl = A.put(c->eptpl.data(), c->eptpl.size());
     // packed template, padded to whole doubles (staged in LDS as doubles)
     c->tplp.clear();
     for (const TplEntry& e : c->tpl) {
@@ -866,8 +917,8 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     c->lanes_g = Lanes{c->fd, ND, 1, 0, c->h};
     const size_t o_Y = A.reserve(sizeof(double) * (size_t)c->nk * std::max(1, c->NO) * stride);
     const size_t o_Yg = A.reserve(sizeof(double) * (size_t)c->nk * std::max(1, c->NO));
-    const size_t o_g = A.reserve(sizeof(double) * ((size_t)nint * c->rpi + c->ntail));
-    const size_t o_vals = A.reserve(sizeof(double) * ((size_t)nint * c->nnz_int + c->nnz_tail));
+    const size_t o_g = A.reserve(sizeof(double) * ((size_t)c->nep + (size_t)nint * c->rpi + c->ntail));
+    const size_t o_vals = A.reserve(sizeof(double) * ((size_t)c->nnz_ep + (size_t)nint * c->nnz_int + c->nnz_tail));
     const size_t o_C = A.reserve(sizeof(double) * (size_t)c->G * std::max(1, p->ngoals));
     const size_t o_grad = A.reserve(sizeof(double) * c->n);
     const size_t o_tpart = A.reserve(sizeof(double) * 2 * (size_t)c->G);
@@ -921,6 +972,8 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     c->d_tpl = (TplEntry*)(b + o_tpl);
     c->d_tplp = (uint32_t*)(b + o_tplp);
     c->P = PathEqs{c->npc, (const mh_path_equation*)(b + o_pc), D.tabs, D.brk, D.coef, c->d_grid};
+    c->E = EndpointEqs{c->nep, c->nnz_ep, 1 + c->NI, (const mh_endpoint_equation*)(b + o_ep),
+                       (const TplEntry*)(b + o_eptpl)};
 
     c->d_x = (double*)(b + o_x); c->d_times = (double*)(b + o_times); c->d_Y = (double*)(b + o_Y);
     c->d_Yg = (double*)(b + o_Yg); c->d_g = (double*)(b + o_g); c->d_vals = (double*)(b + o_vals);
@@ -957,15 +1010,19 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
         if (o->sparsity_detection != MH_SPARSITY_NONE) {
             // detect on the device, then rebuild the (smaller) template in
             // place of the block-dense one
-            const size_t cap = c->tpl.size();
+            const size_t cap = c->tpl.size(), cap_ep = c->eptpl.size();
             int rc2 = detect_sparsity(c.get(), o);
             if (rc2) return rc2;
             c->tpl.clear();
             c->tpl_col_pt.clear();
             build_template(c.get());
-            if (!path_entries_lead(c.get()) || c->tpl.size() > cap)
+            if (!path_entries_lead(c.get()) || c->tpl.size() > cap || c->eptpl.size() > cap_ep)
                 return set_err(MH_ERR_INVALID, "internal: detected template layout");
-            c->nnz = (int64_t)c->nnz_int * c->N + c->nnz_tail;
+            if (!c->eptpl.empty())
+                HIPCHK(hipMemcpy((void*)c->E.tpl, c->eptpl.data(), sizeof(TplEntry) * c->eptpl.size(),
+                        hipMemcpyHostToDevice));
+            c->E.nnz = c->nnz_ep;
+            c->nnz = c->nnz_ep + (int64_t)c->nnz_int * c->N + c->nnz_tail;
             c->tplp.clear();
             for (const TplEntry& e : c->tpl) c->tplp.push_back(tpl_pack(e));
             if (c->tplp.size() % 2) c->tplp.push_back(0u);
@@ -1005,10 +1062,11 @@ extern "C" int mh_get_nlp_info(const mh_ctx* c, mh_nlp_info* info) {
     info->num_grid_points = c->G;
     info->num_states = c->NS;
     info->num_controls = c->NC;
-    info->row_begin = (int64_t)c->ib * c->rpi;
-    info->row_end = (int64_t)c->ie * c->rpi + (c->ie == c->N ? c->ntail : 0);
-    info->nnz_begin = (int64_t)c->ib * c->nnz_int;
-    info->nnz_end = (int64_t)c->ie * c->nnz_int + (c->ie == c->N ? c->nnz_tail : 0);
+    // the head (endpoint rows) belongs to the shard owning interval 0
+    info->row_begin = c->ib == 0 ? 0 : c->nep + (int64_t)c->ib * c->rpi;
+    info->row_end = c->nep + (int64_t)c->ie * c->rpi + (c->ie == c->N ? c->ntail : 0);
+    info->nnz_begin = c->ib == 0 ? 0 : c->nnz_ep + (int64_t)c->ib * c->nnz_int;
+    info->nnz_end = c->nnz_ep + (int64_t)c->ie * c->nnz_int + (c->ie == c->N ? c->nnz_tail : 0);
     return MH_OK;
 }
 
@@ -1047,12 +1105,14 @@ extern "C" int mh_get_bounds(const mh_ctx* c, double* xl, double* xu, double* gl
     }
     if (gl && gu) {
         for (int64_t r = 0; r < c->m; ++r) { gl[r] = 0.0; gu[r] = 0.0; }
+        // endpoint rows: the constraint info's bounds (CasOCTranscription.cpp:582-583)
+        for (int e = 0; e < c->nep; ++e) { gl[e] = c->ep[e].g.lower; gu[e] = c->ep[e].g.upper; }
         // path rows: the equation's bounds at every mesh point
         // (CasOCTranscription.cpp:429-432); mesh point N opens the tail
         for (int i = 0; i <= c->N; ++i)
             for (int e = 0; e < c->npc; ++e) {
-                gl[(int64_t)i * c->rpi + e] = c->pc[e].g.lower;
-                gu[(int64_t)i * c->rpi + e] = c->pc[e].g.upper;
+                gl[c->nep + (int64_t)i * c->rpi + e] = c->pc[e].g.lower;
+                gu[c->nep + (int64_t)i * c->rpi + e] = c->pc[e].g.upper;
             }
     }
     return MH_OK;
@@ -1089,12 +1149,17 @@ extern "C" int mh_get_jac_structure(const mh_ctx* c, int32_t* iRow, int32_t* jCo
     if (!c || !iRow || !jCol) return set_err(MH_ERR_INVALID, "null argument");
     const int step = c->scheme == MH_HERMITE_SIMPSON ? 2 : 1;
     int64_t e = 0;
+    for (const TplEntry& T : c->eptpl) {   // the head: endpoint rows
+        iRow[e] = T.row;
+        jCol[e] = (int32_t)ep_col(c, T.dir);
+        ++e;
+    }
     for (int i = 0; i < c->N; ++i) {
         // the last interval also carries the tail (final-point residual rows)
         const size_t ne = (size_t)c->nnz_int + (i == c->N - 1 ? (size_t)c->nnz_tail : 0);
         for (size_t t = 0; t < ne; ++t) {
             const TplEntry& T = c->tpl[t];
-            iRow[e] = (int32_t)((int64_t)i * c->rpi + T.row);
+            iRow[e] = (int32_t)(c->nep + (int64_t)i * c->rpi + T.row);
             int64_t col;
             if (T.dir < 2) col = T.dir;
             else {
@@ -1143,8 +1208,6 @@ static int launch_stage(mh_ctx* c, int stage, int kind, const double* x, double*
         return MH_OK;
     }
     Layout L{c->NS, c->NC, c->TQ, c->NO, c->NI, c->G, c->k0, c->nk, c->NDV, c->NACC, c->SO};
-    Interval I{c->scheme, c->interp, c->ib, c->rpi, c->nnz_int, c->NMB + c->NAR, c->NMB, c->NQ + c->NZ,
-               c->N, c->nnz_tail, c->ntail, c->npe, c->P};
     const Lanes& ln = kind == 0 ? c->lanes_g : c->lanes_jac;
     const double* Y = kind == 0 ? c->d_Yg : c->d_Y;
     const int nchunks = kind == 0 ? 0 : (c->nnz_int + (c->ie == c->N ? c->nnz_tail : 0) + ASM_CHUNK - 1) / ASM_CHUNK;
@@ -1155,6 +1218,7 @@ static int launch_stage(mh_ctx* c, int stage, int kind, const double* x, double*
         HIPCHK(hipGetLastError());
         return MH_OK;
     }
+    const Interval I = make_interval(c, g, v);
     const int nint = c->ie - c->ib;
     if (c->asm_grid_stride) {
         const long work = (long)nint * ((v ? c->nnz_int : 0) + (g ? c->rpi : 0));
@@ -1247,10 +1311,11 @@ static int finish(mh_ctx* c) {
 // rows / nonzeros of this context's shard (the last shard includes the
 // final grid point's residual rows in implicit mode)
 static size_t shard_rows(const mh_ctx* c) {
-    return (size_t)(c->ie - c->ib) * c->rpi + (c->ie == c->N ? c->ntail : 0);
+    return (c->ib == 0 ? (size_t)c->nep : 0) + (size_t)(c->ie - c->ib) * c->rpi + (c->ie == c->N ? c->ntail : 0);
 }
 static size_t shard_nnz(const mh_ctx* c) {
-    return (size_t)(c->ie - c->ib) * c->nnz_int + (c->ie == c->N ? c->nnz_tail : 0);
+    return (c->ib == 0 ? (size_t)c->nnz_ep : 0) + (size_t)(c->ie - c->ib) * c->nnz_int +
+           (c->ie == c->N ? c->nnz_tail : 0);
 }
 
 extern "C" int mh_eval_g(mh_ctx* c, const double* x, int, double* g) {
@@ -1388,6 +1453,17 @@ __global__ void __launch_bounds__(256) k_path_probe(PathEqs P, int np, int NS, i
     out[w] = path_value(P, e, r[0], r[1 + NS + P.eq[e].index]);
 }
 
+// Endpoint-equation values of np probe rows [initial_time, initial inputs,
+// final_time, final inputs] (sparsity detection of the Endpoint callbacks).
+__global__ void __launch_bounds__(256) k_endpoint_probe(EndpointEqs E, int np, int NS,
+        const double* __restrict__ in, double* __restrict__ out) {
+    const int w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= np * E.nep) return;
+    const int q = w / E.nep, e = w - q * E.nep;
+    const double* r = in + (long)q * 2 * E.W;
+    out[w] = ep_eval(E.eq[e], NS, [&](int si) { return r[si]; });
+}
+
 // splitmix64 uniform(-1, 1) stream (include/mocohip.h
 // mh_options.sparsity_detection; stands in for SimTK::Random::Uniform).
 static double splitmix_uniform(uint64_t& st) {
@@ -1429,6 +1505,8 @@ static int detect_sparsity(mh_ctx* c, const mh_options* o) {
         if (!o->sparsity_pattern) return set_err(MH_ERR_INVALID, "GIVEN sparsity needs sparsity_pattern");
         c->sp.assign(o->sparsity_pattern, o->sparsity_pattern + (size_t)NO * W);
         c->sp_pc.assign(o->sparsity_pattern + (size_t)NO * W, o->sparsity_pattern + (size_t)(NO + NPC) * W);
+        c->sp_ep.assign(o->sparsity_pattern + (size_t)(NO + NPC) * W,
+                        o->sparsity_pattern + (size_t)(NO + NPC + 2 * c->nep) * W);
         return MH_OK;
     } else {
         return set_err(MH_ERR_INVALID, "unknown sparsity detection %d", o->sparsity_detection);
@@ -1466,6 +1544,44 @@ static int detect_sparsity(mh_ctx* c, const mh_options* o) {
         (void)hipFree(din);
         (void)hipFree(dout);
     }
+    // the endpoint functions at their subset point (Endpoint::getSubsetPoint,
+    // CasOCFunction.h:214-237: the integral input is 0 there and, being no NLP
+    // variable, adds no column): every input perturbed by +1e-5
+    const int WE = 2 * W, NEP = c->nep;
+    const int erows = npts * (1 + WE);
+    std::vector<double> ein((size_t)erows * WE), eout((size_t)erows * std::max(NEP, 1));
+    if (NEP > 0) {
+        for (int q = 0; q < npts; ++q) {
+            const double* x = pts.data() + (size_t)q * c->n;
+            double* base = ein.data() + (size_t)q * (1 + WE) * WE;
+            for (int si = 0; si < WE; ++si) base[si] = x[ep_col(c, si)];
+            for (int j = 0; j < WE; ++j) {
+                double* r = base + (size_t)(1 + j) * WE;
+                std::memcpy(r, base, sizeof(double) * WE);
+                r[j] = base[j] + 1e-5;
+            }
+        }
+        double *din = nullptr, *dout = nullptr;
+        HIPCHK(hipMalloc(&din, sizeof(double) * ein.size()));
+        HIPCHK(hipMalloc(&dout, sizeof(double) * eout.size()));
+        HIPCHK(hipMemcpyAsync(din, ein.data(), sizeof(double) * ein.size(), hipMemcpyHostToDevice, c->stream));
+        const int nthr = erows * NEP;
+        k_endpoint_probe<<<(nthr + 255) / 256, 256, 0, c->stream>>>(c->E, erows, c->NS, din, dout);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(eout.data(), dout, sizeof(double) * eout.size(), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        (void)hipFree(din);
+        (void)hipFree(dout);
+    }
+    c->sp_ep.assign((size_t)NEP * WE, 0);
+    for (int q = 0; q < npts; ++q) {
+        const size_t r0 = (size_t)q * (1 + WE);
+        for (int j = 0; j < WE; ++j)
+            for (int e = 0; e < NEP; ++e) {
+                const double d = eout[(r0 + 1 + j) * NEP + e] - eout[r0 * NEP + e];
+                if (std::isnan(d) || d != 0) c->sp_ep[(size_t)e * WE + j] = 1;
+            }
+    }
     c->sp.assign((size_t)NO * W, 0);
     c->sp_pc.assign((size_t)NPC * W, 0);
     for (int q = 0; q < npts; ++q) {
@@ -1484,6 +1600,21 @@ static int detect_sparsity(mh_ctx* c, const mh_options* o) {
     return MH_OK;
 }
 
+
+extern "C" int mh_debug_jacobian_lanes(mh_ctx* c, const double* x, double* times, double* Y) {
+    if (!c || !x || !times || !Y) return set_err(MH_ERR_INVALID, "null argument");
+    if (c->ib != 0 || c->ie != c->N) return set_err(MH_ERR_INVALID, "mh_debug_jacobian_lanes: unsharded contexts only");
+    HIPCHK(hipSetDevice(c->device));
+    (void)hipGetLastError();
+    HIPCHK(hipMemcpyAsync(c->d_x, x, sizeof(double) * c->n, hipMemcpyHostToDevice, c->stream));
+    c->be->lanes(c, c->d_x, c->d_Y);
+    HIPCHK(hipGetLastError());
+    const size_t ny = (size_t)c->nk * c->NO * c->lanes_jac.stride;
+    HIPCHK(hipMemcpyAsync(times, c->d_times, sizeof(double) * c->nk, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(Y, c->d_Y, sizeof(double) * ny, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return MH_OK;
+}
 
 extern "C" int mh_set_timing(mh_ctx* c, int on) {
     if (!c) return set_err(MH_ERR_INVALID, "null argument");
@@ -1511,12 +1642,13 @@ extern "C" int mh_get_backend(const mh_ctx* c, char* name, int32_t name_len, dou
 
 extern "C" int mh_get_callback_sparsity(const mh_ctx* c, uint8_t* pattern, int64_t len) {
     if (!c || !pattern) return set_err(MH_ERR_INVALID, "null argument");
-    const size_t W = 1 + (size_t)c->NI, need = ((size_t)c->NO + c->npc) * W;
+    const size_t W = 1 + (size_t)c->NI, nd = (size_t)c->NO * W, np = nd + (size_t)c->npc * W;
+    const size_t need = np + (size_t)c->nep * 2 * W;
     if (len < (int64_t)need) return set_err(MH_ERR_INVALID, "pattern needs %zu bytes", need);
-    for (size_t i = 0; i < need; ++i) {
-        const size_t nd = (size_t)c->NO * W;
-        pattern[i] = i < nd ? (c->sp.empty() ? 1 : c->sp[i]) : (c->sp_pc.empty() ? 1 : c->sp_pc[i - nd]);
-    }
+    for (size_t i = 0; i < need; ++i)
+        pattern[i] = i < nd ? (c->sp.empty() ? 1 : c->sp[i])
+                   : i < np ? (c->sp_pc.empty() ? 1 : c->sp_pc[i - nd])
+                            : (c->sp_ep.empty() ? 1 : c->sp_ep[i - np]);
     return MH_OK;
 }
 

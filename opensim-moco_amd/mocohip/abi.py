@@ -113,8 +113,14 @@ class mh_goal(C.Structure):
                 ("weight", f64)]
 
 
-MH_ABI_VERSION = 2     # include/mocohip.h
+MH_ABI_VERSION = 3     # include/mocohip.h
 MH_PATH_CONTROL_BOUND = 0
+MH_ENDPOINT_INITIAL_ACTIVATION = 0
+
+
+class mh_endpoint_equation(C.Structure):
+    _fields_ = [("kind", i32), ("index_a", i32), ("index_b", i32), ("reserved", i32),
+                ("g", mh_bounds)]
 
 
 class mh_path_equation(C.Structure):
@@ -132,7 +138,8 @@ class mh_problem(C.Structure):
                 ("goal_weight", P(f64)),
                 ("npath", i32), ("reserved", i32), ("path", P(mh_path_equation)),
                 ("prescribed_kinematics", i32), ("kinematics_table", i32),
-                ("kinematics_column", P(i32))]
+                ("kinematics_column", P(i32)),
+                ("nendpoint", i32), ("reserved2", i32), ("endpoint", P(mh_endpoint_equation))]
 
 
 class mh_options(C.Structure):
@@ -186,6 +193,7 @@ MOCOHIP_SYMBOLS = {
     "mh_model_hash": (i32, [P(mh_model), P(C.c_uint64)]),
     "mh_get_callback_sparsity": (i32, [C.c_void_p, P(C.c_uint8), C.c_int64]),
     "mh_get_work": (i32, [C.c_void_p, P(f64)]),
+    "mh_debug_jacobian_lanes": (i32, [C.c_void_p, P(f64), P(f64), P(f64)]),
 }
 
 ORACLE_SYMBOLS = {
@@ -208,6 +216,7 @@ ORACLE_SYMBOLS = {
                                       P(f64)]),
     "orc_eval_function": (i32, [C.c_void_p, C.c_int, f64, P(f64)]),
     "orc_get_callback_sparsity": (i32, [C.c_void_p, P(C.c_uint8), C.c_int64]),
+    "orc_assemble_from_lanes": (i32, [C.c_void_p, P(f64), P(f64), P(f64), P(f64), P(f64)]),
 }
 
 LIBMOCOHIP_PATH = os.path.join(PKG_ROOT, "csrc", "build", "libmocohip.so")

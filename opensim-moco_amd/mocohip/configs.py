@@ -25,7 +25,7 @@ from .model import (Body, Coordinate, CoordinateActuator, DataTable,
                     ExternalForce, Joint, Model, model_from_dict)
 from .osim import add_reserves
 from .problem import (Constant, GCVSpline, ImplicitAuxiliaryDerivativesTerm,
-                      MocoControlBoundConstraint, MocoControlGoal,
+                      MocoControlBoundConstraint, MocoControlGoal, MocoInitialActivationGoal,
                       MocoFinalTimeGoal, MocoProblem, MocoStateTrackingGoal,
                       PiecewiseLinearFunction)
 from .solver import MocoHipSolver, MocoStudy
@@ -201,10 +201,12 @@ def gait10dof18musc_inverse(num_mesh_intervals: int = 25, fd_scheme: str = "forw
     (MocoInverse.cpp:46-66; GCVSpline degree 5, PositionMotion.cpp:121-155),
     DeGrooteFregly2016 muscles with compliant tendons in implicit mode
     (testMocoInverse.cpp:120-130), reserves, ExternalLoads, control effort
-    goal (MocoInverse.cpp:76-80), implicit dynamics, forward differences and
-    "random" sparsity detection (MocoInverse.cpp:104-114).  The kinematics
-    are the bundled walking coordinate trajectories, clipped by 1e-3 at both
-    ends (clip_time_range, MocoInverse.cpp:70-74)."""
+    goal with reserves weight 1 (MocoInverse.cpp:89-90), the initial-
+    activation endpoint constraint (MocoInverse.cpp:93), implicit dynamics,
+    no control-midpoint interpolation, forward differences and "random"
+    sparsity detection (MocoInverse.cpp:104-114).  The kinematics are the
+    bundled walking coordinate trajectories, clipped by 1e-3 at both ends
+    (clip_time_range, MocoInverse.cpp:82-86)."""
     m = gait10dof18musc_model(tendon_compliance=True, tendon_dynamics="implicit")
     ref = _load("walk_gait1018_state_reference.json")
     t = np.asarray(ref["time"])
@@ -214,10 +216,13 @@ def gait10dof18musc_inverse(num_mesh_intervals: int = 25, fd_scheme: str = "forw
     p.set_position_motion(kin)
     p.set_time_bounds(float(t[0]) + 1e-3, float(t[-1]) - 1e-3)
     p.add_goal(MocoControlGoal("excitation_effort", 1.0))
+    # prevent "free" activation at the beginning of the motion (MocoInverse.cpp:93)
+    p.add_goal(MocoInitialActivationGoal("initial_activation"))
     # minimize_implicit_auxiliary_derivatives, weight 0.01 (MocoInverse.cpp:106-107)
     p.add_goal(ImplicitAuxiliaryDerivativesTerm(weight=0.01))
     s = MocoHipSolver(num_mesh_intervals=num_mesh_intervals,
                       optim_finite_difference_scheme=fd_scheme, multibody_dynamics_mode="implicit",
+                      interpolate_control_midpoints=False,   # MocoInverse.cpp:105
                       optim_sparsity_detection=sparsity)
     return MocoStudy(p, s)
 

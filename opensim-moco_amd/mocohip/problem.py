@@ -82,6 +82,20 @@ class MocoSumSquaredStateGoal:
     state_weights: Dict[str, float] = field(default_factory=dict)
 
 
+@dataclass
+class MocoInitialActivationGoal:
+    """MocoInitialActivationGoal (Moco/Moco/MocoGoal/MocoInitialActivationGoal.
+    {h,cpp}): for every muscle with activation dynamics, the initial
+    excitation equals the initial activation.  An endpoint constraint by
+    default (getDefaultModeImpl, .h:40-42; MocoGoal.h:254-271 sets the weight
+    to 1 in that mode); one equation per muscle in model order
+    (initializeOnModelImpl, .cpp:23-39), bounds [0, 0]
+    (MocoConstraintInfo.h:44-54)."""
+    name: str = "initial_activation"
+    mode: str = "endpoint_constraint"
+    weight: float = 1.0
+
+
 # ------------------------------------------------- functions of time ----
 @dataclass
 class Constant:
@@ -276,12 +290,29 @@ class ProblemRep:
         self.state_infos = [sinfo.get(n, MocoVariableInfo()) for n in self.state_names]
         self.control_infos = [cinfo.get(n, MocoVariableInfo()) for n in self.control_names]
 
-        # goals
+        # goals (endpoint-constraint mode goals become endpoint equations,
+        # in goal order: MocoProblemRep::createEndpointConstraintNames)
         goals, gidx, gcol, gw = [], [], [], []
+        endpoint: List[abi.mh_endpoint_equation] = []
         sidx = {n: i for i, n in enumerate(self.state_names)}
         cidx = {n: i for i, n in enumerate(self.control_names)}
         self.extra_tables: List[DataTable] = []
         for g in problem.goals:
+            if isinstance(g, MocoInitialActivationGoal):
+                if g.mode != "endpoint_constraint":
+                    raise NotImplementedError("MocoInitialActivationGoal in cost mode "
+                                              "(only the endpoint-constraint default is on the "
+                                              "hot path)")
+                for mu in model.muscles:
+                    if mu.ignore_activation_dynamics:
+                        continue
+                    e = abi.mh_endpoint_equation()
+                    e.kind = abi.MH_ENDPOINT_INITIAL_ACTIVATION
+                    e.index_a = cidx[mu.path]
+                    e.index_b = sidx[mu.path + "/activation"]
+                    e.g.lower, e.g.upper = 0.0, 0.0
+                    endpoint.append(e)
+                continue
             gs = abi.mh_goal()
             gs.weight = float(g.weight)
             gs.term_begin = len(gidx)
@@ -359,6 +390,10 @@ class ProblemRep:
             p.kinematics_column = abi.iptr(self._kin_cols)
         p.npath = len(path_eqs)
         p.path = self._path
+        self._endpoint = (abi.mh_endpoint_equation * max(1, len(endpoint)))(*endpoint)
+        p.nendpoint = len(endpoint)
+        p.endpoint = self._endpoint
+        self.num_endpoint_equations = len(endpoint)
         self.num_path_equations = len(path_eqs)
         self.struct = p
         self.num_states = len(self.state_names)

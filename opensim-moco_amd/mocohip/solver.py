@@ -222,11 +222,17 @@ class _NLPBase:
         """Residual rows per grid point (multibody, then auxiliary)."""
         return self.NMB + self.NAR
 
+    @property
+    def NEP(self) -> int:
+        """Endpoint-constraint equations (rows 0 .. NEP of g)."""
+        return getattr(self.rep, "num_endpoint_equations", 0)
+
     def callback_sparsity(self) -> np.ndarray:
-        """The callback sparsity behind the Jacobian structure: (NQ + NZ)
-        DAE outputs then the path equations, rows of [time, inputs] flags."""
+        """The callback sparsity behind the Jacobian structure: the NO DAE
+        outputs then the path equations, rows of W = [time, inputs] flags,
+        then the endpoint equations, rows of 2 W flags."""
         W = 1 + self.NS + self.NC + self.NDV
-        buf = np.zeros((self.NO + self.NPC) * W, np.uint8)
+        buf = np.zeros((self.NO + self.NPC + 2 * self.NEP) * W, np.uint8)
         self._check(self._fn("get_callback_sparsity")(
             self.ctx, buf.ctypes.data_as(C.POINTER(C.c_uint8)), buf.size))
         return buf
@@ -302,6 +308,21 @@ class HipNLP(_NLPBase):
     def eval_jac_g_device(self, x_ptr: int, v_ptr: int):
         self._check(self.lib.mh_eval_jac_g_device(self.ctx, C.c_void_p(x_ptr), C.c_void_p(v_ptr)))
 
+    def lane_stride(self) -> int:
+        """Finite-difference lanes per grid point (mh_debug_jacobian_lanes)."""
+        ND = 2 + self.NS + self.NC + self.NDV
+        return 2 * ND + 1 if self.opts.finite_difference_scheme == abi.MH_FD_CENTRAL else ND + 1
+
+    def jacobian_lanes(self, x):
+        """(times[G], Y[G, NO, S]): the raw lane outputs behind eval_jac_g(x)
+        (mh_debug_jacobian_lanes; parity tests)."""
+        x = np.ascontiguousarray(x, float)
+        S = self.lane_stride()
+        t = np.empty(self.G)
+        Y = np.empty(self.G * self.NO * S)
+        self._check(self.lib.mh_debug_jacobian_lanes(self.ctx, abi.dptr(x), abi.dptr(t), abi.dptr(Y)))
+        return t, Y.reshape(self.G, self.NO, S)
+
     def backend(self):
         """(back-end name, FP64 ops per generated DAE eval, model hash)."""
         buf = C.create_string_buffer(128)
@@ -371,6 +392,21 @@ class OracleNLP(_NLPBase):
         v = np.empty(max(self.nnz, 1))
         self._check(self.lib.orc_eval_jac_g(self.ctx, abi.dptr(x), abi.dptr(v)))
         return v[:self.nnz]
+
+
+def _oracle_assemble(self, x, times, Y):
+    """(g, J) re-derived by the oracle from raw lanes (orc_assemble_from_lanes)."""
+    x = np.ascontiguousarray(x, float)
+    times = np.ascontiguousarray(times, float)
+    Y = np.ascontiguousarray(Y, float)
+    g = np.empty(max(self.m, 1))
+    v = np.empty(max(self.nnz, 1))
+    self._check(self.lib.orc_assemble_from_lanes(self.ctx, abi.dptr(x), abi.dptr(times), abi.dptr(Y),
+                                                 abi.dptr(g), abi.dptr(v)))
+    return g[:self.m], v[:self.nnz]
+
+
+OracleNLP.assemble_from_lanes = _oracle_assemble
 
 
 class MocoStudy:

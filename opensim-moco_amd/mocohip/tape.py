@@ -10,7 +10,8 @@ Layout (little endian, x86-64 struct layout of include/mocohip.h):
   each as (int64 byte count, bytes); version 2 appends npath and the
   mh_path_equation array, then the sparsity-detection guess (n doubles or
   empty), the given callback sparsity (bytes or empty) and the prescribed
-  kinematics (table index, per-coordinate columns)."""
+  kinematics (table index, per-coordinate columns); version 3 appends the
+  endpoint-constraint equations (mh_problem.nendpoint/endpoint)."""
 from __future__ import annotations
 
 import ctypes as C
@@ -19,7 +20,7 @@ import struct
 from . import abi
 
 MAGIC = b"MHTAPE01"
-VERSION = 2   # 2: + path-constraint equations (mh_problem.npath/path)
+VERSION = 3   # 2: + path-constraint equations; 3: + endpoint constraints
 
 # (field, element type, count attribute of mh_model / None for problem arrays)
 _MODEL_ARRAYS = [
@@ -47,15 +48,22 @@ def write_tape(rep, opts: abi.mh_options, path: str) -> None:
     ns, nc = len(rep.state_names), len(rep.control_names)
     # pointers inside mh_options do not travel: the sparsity guess is a blob
     guess = b""
+    implicit = opts.multibody_dynamics_mode == abi.MH_DYNAMICS_IMPLICIT
+    presc = bool(p.prescribed_kinematics)
+    nar = getattr(rep, "num_aux_residuals", 0)
+    ndv = (m.nq if implicit and not presc else 0) + nar
     if opts.sparsity_guess:
         G = (2 * opts.num_mesh_intervals + 1 if opts.transcription == abi.MH_HERMITE_SIMPSON
              else opts.num_mesh_intervals + 1)
-        ndv = m.nq if opts.multibody_dynamics_mode == abi.MH_DYNAMICS_IMPLICIT else 0
         guess = C.string_at(opts.sparsity_guess, 8 * (2 + (ns + nc + ndv) * G))
     pattern = b""
     if opts.sparsity_pattern:
-        W = 1 + ns + nc + (m.nq if opts.multibody_dynamics_mode == abi.MH_DYNAMICS_IMPLICIT else 0)
-        pattern = C.string_at(opts.sparsity_pattern, (ns - m.nq + p.npath) * W)
+        # mh_get_callback_sparsity layout: NO DAE outputs and the path
+        # equations (W flags each), the endpoint equations (2 W flags each)
+        W = 1 + ns + nc + ndv
+        nz = ns if presc else ns - 2 * m.nq
+        no = m.nq + nz + nar
+        pattern = C.string_at(opts.sparsity_pattern, (no + p.npath + 2 * p.nendpoint) * W)
     o2 = abi.mh_options.from_buffer_copy(bytes(opts))
     o2.sparsity_guess = None
     o2.sparsity_pattern = None
@@ -79,5 +87,7 @@ def write_tape(rep, opts: abi.mh_options, path: str) -> None:
     out += [struct.pack("<q", len(guess)), guess, struct.pack("<q", len(pattern)), pattern]
     kc = _blob(p.kinematics_column, C.c_int32, m.nq) if p.prescribed_kinematics else b""
     out += [struct.pack("<ii", p.prescribed_kinematics, p.kinematics_table), struct.pack("<q", len(kc)), kc]
+    eb = _blob(p.endpoint, abi.mh_endpoint_equation, p.nendpoint)
+    out += [struct.pack("<i", p.nendpoint), struct.pack("<q", len(eb)), eb]
     with open(path, "wb") as fh:
         fh.write(b"".join(out))

@@ -236,6 +236,9 @@ struct orc_ctx {
     double* gw;
     int NPC;                /* path-constraint equations per mesh point  */
     mh_path_equation* pc;
+    int NEP;                /* endpoint-constraint equations (rows 0..NEP) */
+    mh_endpoint_equation* ep;
+    uint8_t* sp_ep;         /* detected endpoint sparsity [eq][2 (1 + NP)] */
     /* detected callback sparsity (NULL: block-dense): [output][1 + input],
      * column 0 = time; DAE outputs (NQ + NZ) and path equations */
     uint8_t *sp, *sp_pc;
@@ -476,6 +479,57 @@ static void tail_rows(const orc_ctx* c, int64_t row0, row_fn emit, void* ud) {
     free(cols);
 }
 
+/* Endpoint-constraint rows (CasOCTranscription.h:283-285: first in g).  The
+ * Endpoint callback's inputs (CasOCFunction.h:167-240) are [initial_time,
+ * initial point inputs, final_time, final point inputs] (no multipliers or
+ * parameters here; the integral input is a constant NaN when the goal has
+ * no integrand, CasOCTranscription.cpp:562-564).  Subset index si of that
+ * vector -> NLP column. */
+static int ep_width(const orc_ctx* c) { return 2 * (1 + c->NP); }
+static int64_t ep_col(const orc_ctx* c, int si) {
+    int W = 1 + c->NP;
+    int pt = si / W, j = si % W - 1;
+    if (j < 0) return pt;                 /* initial_time: 0, final_time: 1 */
+    int k = pt ? c->G - 1 : 0;
+    if (j < c->NS) return col_state(c, k, j);
+    if (j < c->NS + c->NC) return col_control(c, k, j - c->NS);
+    return col_deriv(c, k, j - c->NS - c->NC);
+}
+/* Columns of endpoint row e, ascending: every input (block-dense) or the
+ * detected ones; si[] receives the matching subset indices. */
+static int ep_row_cols(const orc_ctx* c, int e, int64_t* cols, int* si) {
+    int WE = ep_width(c), n = 0;
+    for (int i = 0; i < WE; ++i)
+        if (!c->sp_ep || c->sp_ep[(int64_t)e * WE + i]) { cols[n] = ep_col(c, i); si[n] = i; ++n; }
+    /* insertion sort by column (the initial point's block and the final
+     * point's interleave per variable kind) */
+    for (int a = 1; a < n; ++a) {
+        int64_t cv = cols[a]; int sv = si[a]; int b = a - 1;
+        while (b >= 0 && cols[b] > cv) { cols[b + 1] = cols[b]; si[b + 1] = si[b]; --b; }
+        cols[b + 1] = cv; si[b + 1] = sv;
+    }
+    return n;
+}
+static void endpoint_rows(const orc_ctx* c, row_fn emit, void* ud) {
+    int64_t* cols = (int64_t*)malloc(sizeof(int64_t) * (size_t)(ep_width(c) + 1));
+    int* si = (int*)malloc(sizeof(int) * (size_t)(ep_width(c) + 1));
+    for (int e = 0; e < c->NEP; ++e) emit(ud, e, cols, ep_row_cols(c, e, cols, si));
+    free(cols); free(si);
+}
+/* The endpoint subset vector of iterate x. */
+static void ep_gather(const orc_ctx* c, const double* x, double* in) {
+    int W = 1 + c->NP;
+    for (int pt = 0; pt < 2; ++pt)
+        for (int i = 0; i < W; ++i) in[pt * W + i] = x[ep_col(c, pt * W + i)];
+}
+/* MocoInitialActivationGoal::calcGoalImpl in endpoint-constraint mode
+ * (MocoInitialActivationGoal.cpp:41-58): initial excitation - initial
+ * activation. */
+static double endpoint_value(const orc_ctx* c, int e, const double* in) {
+    const mh_endpoint_equation* E = &c->ep[e];
+    return in[1 + c->NS + E->index_a] - in[1 + E->index_b];
+}
+
 #ifndef ORACLE_COUNTING
 static int detect_sparsity(orc_ctx* c, const mh_options* o);
 #endif
@@ -511,6 +565,12 @@ int orc_create(const mh_problem* p, const mh_options* o, orc_ctx** out) {
         orc_destroy(c);
         return fail(MH_ERR_INVALID, "bad path constraints");
     }
+    c->NEP = p->nendpoint;
+    if (p->nendpoint < 0 || (p->nendpoint > 0 && !p->endpoint)) {
+        orc_destroy(c);
+        return fail(MH_ERR_INVALID, "bad endpoint constraints");
+    }
+    c->ep = DUP(mh_endpoint_equation, p->endpoint, p->nendpoint);
 
     /* spline coefficients */
     c->kb = (double*)calloc((size_t)M->nknots + 1, sizeof(double));
@@ -608,6 +668,14 @@ int orc_create(const mh_problem* p, const mh_options* o, orc_ctx** out) {
             return fail(MH_ERR_INVALID, "path equation %d: bad control/table", e);
         }
     }
+    for (int e = 0; e < c->NEP; ++e) {
+        const mh_endpoint_equation* E = &c->ep[e];
+        if (E->kind != MH_ENDPOINT_INITIAL_ACTIVATION || E->index_a < 0 || E->index_a >= c->NC ||
+                E->index_b < 0 || E->index_b >= c->NS) {
+            orc_destroy(c);
+            return fail(MH_ERR_INVALID, "endpoint equation %d: bad kind/control/state", e);
+        }
+    }
     for (int ia = 0; ia < M->nactuators; ++ia) {
         if (c->acts[ia].kind == MH_ACT_MUSCLE) {
             int t = c->acts[ia].target;
@@ -673,7 +741,7 @@ int orc_create(const mh_problem* p, const mh_options* o, orc_ctx** out) {
     }
     free(mesh);
     c->n = 2 + (int64_t)(c->NS + c->NC + c->NDV) * c->G;
-    c->m = (int64_t)rows_per_interval(c) * c->N + ntail(c);
+    c->m = c->NEP + (int64_t)rows_per_interval(c) * c->N + ntail(c);
     c->fd = o->finite_difference_scheme;
     c->h = o->fd_step > 0 ? o->fd_step : 1e-8;
     if (o->sparsity_detection != MH_SPARSITY_NONE) {
@@ -687,6 +755,7 @@ int orc_create(const mh_problem* p, const mh_options* o, orc_ctx** out) {
     }
     /* structure */
     emit_state e = {0, NULL, NULL};
+    endpoint_rows(c, emit_count, &e);
     for (int i = 0; i < c->N; ++i) interval_rows(c, i, 0, emit_count, &e);
     tail_rows(c, 0, emit_count, &e);
     c->nnz = e.count;
@@ -694,8 +763,9 @@ int orc_create(const mh_problem* p, const mh_options* o, orc_ctx** out) {
     c->jCol = (int32_t*)malloc(sizeof(int32_t) * (size_t)(c->nnz + 1));
     e.count = 0; e.ir = c->iRow; e.jc = c->jCol;
     int rpi = rows_per_interval(c);
-    for (int i = 0; i < c->N; ++i) interval_rows(c, i, (int64_t)i * rpi, emit_fill, &e);
-    tail_rows(c, (int64_t)c->N * rpi, emit_fill, &e);
+    endpoint_rows(c, emit_fill, &e);
+    for (int i = 0; i < c->N; ++i) interval_rows(c, i, c->NEP + (int64_t)i * rpi, emit_fill, &e);
+    tail_rows(c, c->NEP + (int64_t)c->N * rpi, emit_fill, &e);
     *out = c;
     return MH_OK;
 }
@@ -705,6 +775,7 @@ void orc_destroy(orc_ctx* c) {
     void* ptrs[] = {c->bodies, c->axes, c->funcs, c->kx, c->ky, c->kb, c->kc, c->kd,
             c->mus, c->pts, c->acts, c->tabs, c->brk, c->coef, c->ext, c->sinfo, c->cinfo,
             c->goals, c->gidx, c->gcol, c->gw, c->pc, c->sp, c->sp_pc, c->mus_ider, c->kin_col,
+            c->ep, c->sp_ep,
             c->mus_act_state, c->mus_ftn_state,
             c->mus_control, c->coord_body, c->grid, c->quad, c->iRow, c->jCol};
     for (size_t i = 0; i < sizeof ptrs / sizeof ptrs[0]; ++i) free(ptrs[i]);
@@ -771,10 +842,13 @@ int orc_get_bounds(const orc_ctx* c, double* xl, double* xu, double* gl, double*
     if (gl) for (int64_t r = 0; r < c->m; ++r) { gl[r] = 0.0; gu[r] = 0.0; }
     /* path rows: the equation's bounds repeated at every mesh point
      * (CasOCTranscription.cpp:429-432) */
+    /* endpoint rows: the constraint info's bounds (CasOCTranscription.cpp:
+     * 582-583) */
+    if (gl) for (int e = 0; e < c->NEP; ++e) { gl[e] = c->ep[e].g.lower; gu[e] = c->ep[e].g.upper; }
     if (gl && c->NPC) {
         int rpi = rows_per_interval(c);
         for (int i = 0; i <= c->N; ++i) {
-            int64_t r0 = (int64_t)i * rpi;
+            int64_t r0 = c->NEP + (int64_t)i * rpi;
             for (int e = 0; e < c->NPC; ++e) { gl[r0 + e] = c->pc[e].g.lower; gu[r0 + e] = c->pc[e].g.upper; }
         }
     }
@@ -1583,14 +1657,17 @@ static int detect_sparsity(orc_ctx* c, const mh_options* o) {
         if (!o->sparsity_pattern) return fail(MH_ERR_INVALID, "GIVEN sparsity needs sparsity_pattern");
         c->sp = (uint8_t*)malloc((size_t)NO * W + 1);
         c->sp_pc = (uint8_t*)malloc((size_t)NPC * W + 1);
+        c->sp_ep = (uint8_t*)malloc((size_t)c->NEP * 2 * W + 1);
         memcpy(c->sp, o->sparsity_pattern, (size_t)NO * W);
         memcpy(c->sp_pc, o->sparsity_pattern + (size_t)NO * W, (size_t)NPC * W);
+        memcpy(c->sp_ep, o->sparsity_pattern + (size_t)(NO + NPC) * W, (size_t)c->NEP * 2 * W);
         return MH_OK;
     } else {
         return fail(MH_ERR_INVALID, "unknown sparsity detection %d", o->sparsity_detection);
     }
     c->sp = (uint8_t*)calloc((size_t)NO * W + 1, 1);
     c->sp_pc = (uint8_t*)calloc((size_t)NPC * W + 1, 1);
+    c->sp_ep = (uint8_t*)calloc((size_t)c->NEP * 2 * W + 1, 1);
     dae_ws w;
     ws_alloc(c, &w);
     double* in = (double*)malloc(sizeof(double) * (size_t)(W + 2 * NO + 2 * NPC + 2));
@@ -1617,6 +1694,24 @@ static int detect_sparsity(orc_ctx* c, const mh_options* o) {
                 if (isnan(d) || d != 0) c->sp_pc[(int64_t)e * W + j] = 1;
             }
         }
+        /* the endpoint functions at their subset point (Endpoint::
+         * getSubsetPoint, CasOCFunction.h:214-237; the integral input is 0
+         * there and, being no NLP variable, adds no column) */
+        if (c->NEP) {
+            double* ein = (double*)malloc(sizeof(double) * (size_t)(2 * W));
+            ep_gather(c, x, ein);
+            for (int j = 0; j < 2 * W; ++j) {
+                double sv = ein[j];
+                for (int e = 0; e < c->NEP; ++e) {
+                    double v0 = endpoint_value(c, e, ein);
+                    ein[j] = sv + eps;
+                    double d = endpoint_value(c, e, ein) - v0;
+                    ein[j] = sv;
+                    if (isnan(d) || d != 0) c->sp_ep[(int64_t)e * 2 * W + j] = 1;
+                }
+            }
+            free(ein);
+        }
     }
     free(in);
     free(pts);
@@ -1625,21 +1720,29 @@ static int detect_sparsity(orc_ctx* c, const mh_options* o) {
 }
 
 int orc_get_callback_sparsity(const orc_ctx* c, uint8_t* pattern, int64_t len) {
-    int64_t W = 1 + c->NP, nd = (int64_t)nout(c) * W, need = nd + (int64_t)c->NPC * W;
+    int64_t W = 1 + c->NP, nd = (int64_t)nout(c) * W, np = nd + (int64_t)c->NPC * W;
+    int64_t need = np + (int64_t)c->NEP * 2 * W;
     if (!pattern || len < need) return fail(MH_ERR_INVALID, "pattern needs %lld bytes", (long long)need);
     for (int64_t i = 0; i < need; ++i)
-        pattern[i] = i < nd ? (c->sp ? c->sp[i] : 1) : (c->sp_pc ? c->sp_pc[i - nd] : 1);
+        pattern[i] = i < nd ? (c->sp ? c->sp[i] : 1)
+                   : i < np ? (c->sp_pc ? c->sp_pc[i - nd] : 1) : (c->sp_ep ? c->sp_ep[i - np] : 1);
     return MH_OK;
 }
 
-int orc_eval_g(orc_ctx* c, const double* x, double* g) {
+/* g from the grid times, xdot (xd: NS per point) and residual outputs
+ * (res: nres per point) at every grid point (flattenConstraints order). */
+static void g_assemble(const orc_ctx* c, const double* x, const double* times, const double* xd,
+        const double* res, double* g) {
     int NS = c->NS, NC = c->NC, NR = nres(c);
-    double* times = (double*)malloc(sizeof(double) * (size_t)c->G);
-    double* xd = (double*)malloc(sizeof(double) * (size_t)c->G * (size_t)NS);
-    double* res = (double*)malloc(sizeof(double) * ((size_t)c->G * (size_t)NR + 1));
-    times_of(c, x, times);
-    all_xdot(c, x, times, xd, res);
     int rpi = rows_per_interval(c);
+    /* endpoint rows first */
+    if (c->NEP) {
+        double* ein = (double*)malloc(sizeof(double) * (size_t)ep_width(c));
+        ep_gather(c, x, ein);
+        for (int e = 0; e < c->NEP; ++e) g[e] = endpoint_value(c, e, ein);
+        free(ein);
+    }
+    g += c->NEP;
     double* pin = (double*)malloc(sizeof(double) * (size_t)(c->NP + 1));
     /* path rows of every mesh point: interval i opens with mesh point i's,
      * the tail with the final mesh point's */
@@ -1685,6 +1788,16 @@ int orc_eval_g(orc_ctx* c, const double* x, double* g) {
         }
     }
     for (int o = 0; o < NR; ++o) g[(int64_t)c->N * rpi + c->NPC + o] = res[(int64_t)(c->G - 1) * NR + o];
+}
+
+int orc_eval_g(orc_ctx* c, const double* x, double* g) {
+    int NS = c->NS, NR = nres(c);
+    double* times = (double*)malloc(sizeof(double) * (size_t)c->G);
+    double* xd = (double*)malloc(sizeof(double) * (size_t)c->G * (size_t)NS);
+    double* res = (double*)malloc(sizeof(double) * ((size_t)c->G * (size_t)NR + 1));
+    times_of(c, x, times);
+    all_xdot(c, x, times, xd, res);
+    g_assemble(c, x, times, xd, res, g);
     free(times);
     free(xd);
     free(res);
@@ -1829,24 +1942,45 @@ static int col_to_dir(const orc_ctx* c, int64_t col, int* k) {
     return 2 + c->NS + c->NC + (int)(r % c->NDV);
 }
 
-int orc_eval_jac_g(orc_ctx* c, const double* x, double* values) {
+/* Jacobian values from the grid times, xdot at every grid point (xd), the
+ * DAE FD blocks (D) and the path-constraint FD blocks (Dp): the chain rule
+ * through the defect formulas (CasOCHermiteSimpson.cpp:53-105,
+ * CasOCTrapezoidal.cpp:43-59), in structure order.  Written without fused
+ * operations (the build uses -ffp-contract=off) so that the same inputs give
+ * the same bits as the device's assembly. */
+static void jac_assemble(const orc_ctx* c, const double* x, const double* times, const double* xd,
+        const double* D, const double* Dp, double* values) {
     int NS = c->NS, NQ = c->NQ;
     int NO = nout(c), ND = c->NP + 2;
-    double* times = (double*)malloc(sizeof(double) * (size_t)c->G);
-    double* xd = (double*)malloc(sizeof(double) * (size_t)c->G * (size_t)NS);
-    double* D = (double*)malloc(sizeof(double) * (size_t)c->G * (size_t)ND * (size_t)NO);
     int NR = nres(c);
-    double* res = (double*)malloc(sizeof(double) * ((size_t)c->G * (size_t)NR + 1));
-    times_of(c, x, times);
-    all_xdot(c, x, times, xd, res);
-    fd_blocks(c, x, times, D);
     int NPC = c->NPC;
-    double* Dp = (double*)malloc(sizeof(double) * ((size_t)(c->N + 1) * (size_t)ND * (size_t)NPC + 1));
-    if (NPC) path_blocks(c, x, times, Dp);
     int rpi = rows_per_interval(c);
     int npts_res = c->scheme == MH_HERMITE_SIMPSON ? 2 : 1;
-    for (int64_t e = 0; e < c->nnz; ++e) {
-        int64_t row = c->iRow[e], col = c->jCol[e];
+    /* endpoint rows: FD quotients of the endpoint function along each of its
+     * structural columns (the Endpoint callback's FiniteDiff, step h) */
+    int64_t e0 = 0;
+    if (c->NEP) {
+        int WE = ep_width(c);
+        double* ein = (double*)malloc(sizeof(double) * (size_t)WE);
+        int64_t* cols = (int64_t*)malloc(sizeof(int64_t) * (size_t)(WE + 1));
+        int* si = (int*)malloc(sizeof(int) * (size_t)(WE + 1));
+        ep_gather(c, x, ein);
+        for (int r = 0; r < c->NEP; ++r) {
+            int nc = ep_row_cols(c, r, cols, si);
+            double v0 = endpoint_value(c, r, ein);
+            for (int q = 0; q < nc; ++q) {
+                double sv = ein[si[q]], vp = 0.0, vm = 0.0;
+                if (c->fd != MH_FD_BACKWARD) { ein[si[q]] = sv + c->h; vp = endpoint_value(c, r, ein); }
+                if (c->fd != MH_FD_FORWARD) { ein[si[q]] = sv - c->h; vm = endpoint_value(c, r, ein); }
+                ein[si[q]] = sv;
+                values[e0++] = c->fd == MH_FD_CENTRAL ? (vp - vm) / (2.0 * c->h)
+                             : (c->fd == MH_FD_FORWARD ? (vp - v0) / c->h : (v0 - vm) / c->h);
+            }
+        }
+        free(ein); free(cols); free(si);
+    }
+    for (int64_t e = e0; e < c->nnz; ++e) {
+        int64_t row = c->iRow[e] - c->NEP, col = c->jCol[e];
         int i = (int)(row / rpi);
         int rl = (int)(row % rpi);
         double v = 0.0;
@@ -1944,8 +2078,65 @@ int orc_eval_jac_g(orc_ctx* c, const double* x, double* values) {
         values[e] = v;
     }
     (void)NQ;
+}
+
+int orc_eval_jac_g(orc_ctx* c, const double* x, double* values) {
+    int NS = c->NS, NO = nout(c), ND = c->NP + 2, NR = nres(c), NPC = c->NPC;
+    double* times = (double*)malloc(sizeof(double) * (size_t)c->G);
+    double* xd = (double*)malloc(sizeof(double) * (size_t)c->G * (size_t)NS);
+    double* D = (double*)malloc(sizeof(double) * (size_t)c->G * (size_t)ND * (size_t)NO);
+    double* res = (double*)malloc(sizeof(double) * ((size_t)c->G * (size_t)NR + 1));
+    double* Dp = (double*)malloc(sizeof(double) * ((size_t)(c->N + 1) * (size_t)ND * (size_t)NPC + 1));
+    times_of(c, x, times);
+    all_xdot(c, x, times, xd, res);
+    fd_blocks(c, x, times, D);
+    if (NPC) path_blocks(c, x, times, Dp);
+    jac_assemble(c, x, times, xd, D, Dp, values);
     free(Dp);
     free(times);
+    free(xd);
+    free(D);
+    free(res);
+    return MH_OK;
+}
+
+/* g and the Jacobian values from given raw lane outputs (the layout of
+ * mh_debug_jacobian_lanes): CasADi's FiniteDiff quotients of the lanes
+ * (CasOCFunction.h:38-44) then g_assemble / jac_assemble.  The checker for
+ * the device's quotient + assembly arithmetic. */
+int orc_assemble_from_lanes(orc_ctx* c, const double* x, const double* times, const double* Y,
+        double* g, double* values) {
+    int NS = c->NS, NO = nout(c), ND = c->NP + 2, NR = nres(c), NPC = c->NPC, TQ = c->TQ;
+    int S = c->fd == MH_FD_CENTRAL ? 2 * ND + 1 : ND + 1, base = S - 1;
+    double h = c->h;
+    double* xd = (double*)malloc(sizeof(double) * (size_t)c->G * (size_t)NS);
+    double* D = (double*)malloc(sizeof(double) * (size_t)c->G * (size_t)ND * (size_t)NO);
+    double* res = (double*)malloc(sizeof(double) * ((size_t)c->G * (size_t)NR + 1));
+    double* Dp = (double*)malloc(sizeof(double) * ((size_t)(c->N + 1) * (size_t)ND * (size_t)NPC + 1));
+    for (int k = 0; k < c->G; ++k) {
+        const double* Yk = Y + (int64_t)k * NO * S;
+        for (int s = 0; s < NS; ++s) {
+            double v;
+            if (s < TQ) v = x[col_state(c, k, TQ + s)];                     /* qdot = u */
+            else if (c->NACC && s < 2 * TQ) v = x[col_deriv(c, k, s - TQ)];  /* udot = w */
+            else v = Yk[(int64_t)(s + c->SO) * S + base];
+            xd[(int64_t)k * NS + s] = v;
+        }
+        for (int r = 0; r < NR; ++r) res[(int64_t)k * NR + r] = Yk[(int64_t)res_out(c, r) * S + base];
+        for (int d = 0; d < ND; ++d)
+            for (int o = 0; o < NO; ++o) {
+                const double* y = Yk + (int64_t)o * S;
+                double q;
+                if (c->fd == MH_FD_CENTRAL) q = (y[d] - y[ND + d]) / (2.0 * h);
+                else if (c->fd == MH_FD_FORWARD) q = (y[d] - y[base]) / h;
+                else q = (y[base] - y[d]) / h;
+                D[((int64_t)k * ND + d) * NO + o] = q;
+            }
+    }
+    if (NPC) path_blocks(c, x, times, Dp);
+    if (g) g_assemble(c, x, times, xd, res, g);
+    if (values) jac_assemble(c, x, times, xd, D, Dp, values);
+    free(Dp);
     free(xd);
     free(D);
     free(res);

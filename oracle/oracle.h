@@ -49,6 +49,13 @@ int orc_eval_grad_f(orc_ctx* ctx, const double* x, double* grad_f);
 int orc_eval_g(orc_ctx* ctx, const double* x, double* g);
 int orc_eval_jac_g(orc_ctx* ctx, const double* x, double* values);
 
+/* g (m) and Jacobian values (nnz) re-derived from raw finite-difference
+ * lane outputs Y and grid times in the layout of mh_debug_jacobian_lanes
+ * (include/mocohip.h): the checker of the device's quotient and assembly
+ * arithmetic.  g or values may be NULL. */
+int orc_assemble_from_lanes(orc_ctx* ctx, const double* x, const double* times,
+        const double* Y, double* g, double* values);
+
 /* inputs per point: [time, states(NS), controls(NC)];
  * outputs per point: [udot(NQ), zdot(NZ)]. */
 int orc_eval_dae(orc_ctx* ctx, int32_t npoints, const double* inputs,

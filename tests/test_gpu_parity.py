@@ -1,22 +1,29 @@
 """GPU (libmocohip.so on gfx950) vs the CPU oracle, through the C ABI.
 
-Tolerances (the oracle and the kernels use different libm implementations
-and FMA contraction, so bit equality is not expected for floating point):
+What is compared, and how tightly:
   * structure (iRow/jCol), bounds, initial guesses: bit-exact;
-  * DAE outputs and g: |d| <= 1e-10 * (row scale);
-  * Jacobian: |dJ| <= 1e-8 |J| + tau_row, with the finite-difference
-    cancellation bound tau_row = 4 (dY_i + 64 eps F_i)(h_i + 1) / h_fd, where
-    dY_i is the measured GPU-vs-oracle DAE output difference on the
-    interval's grid points, F_i the largest |xdot| there, h_i the interval
-    duration and h_fd the FD step: a difference quotient amplifies the two
-    implementations' function-value rounding differences by 1/h_fd.
-Entries that depend on DAE outputs beyond REGULAR (numerical blow-ups of
-the muscle model at random iterates) are excluded; at least half of every
-compared array must remain.
+  * the Jacobian's finite-difference quotients and chain rule (exact
+    arithmetic on the DAE lane outputs): bit-exact -- the oracle re-derives
+    g and every Jacobian value from the device's own lane outputs
+    (mh_debug_jacobian_lanes -> orc_assemble_from_lanes) and must reproduce
+    the device's eval_g / eval_jac_g bit for bit
+    (test_jacobian_assembly_bit_exact_from_device_lanes);
+  * the lane outputs themselves (DAE values at the perturbed inputs): within
+    1e-10 of each output's scale of the oracle's DAE at exactly the same
+    inputs (the two use different libm implementations);
+  * end to end: |dJ| <= 1e-8 |J| + 4 dY_i (h_i + 1) / h_fd with dY_i the
+    MEASURED lane-output difference on the interval's grid points, run at
+    h_fd = 1e-4 so that the bound is tight (test_jacobian_tight_bound);
+  * DAE outputs and g: |d| <= 1e-10 * (row scale).
+Iterates are physiological (muscle states and excitations in their working
+range, everything else random within bounds): at least 99 % of every
+compared array must be regular (finite, below REGULAR), and the compared
+fraction and the largest relative error are reported on failure.
 """
 import numpy as np
 import pytest
 
+import _lanes
 from mocohip import configs
 from mocohip.solver import HipNLP, OracleNLP
 
@@ -31,6 +38,11 @@ def _sparse(st, mode="random"):
 
 def _trap(st):
     st.solver.transcription_scheme = "trapezoidal"
+    return st
+
+
+def _nointerp(st):
+    st.solver.interpolate_control_midpoints = False
     return st
 
 
@@ -107,10 +119,16 @@ CASES = {
         control_bounds=True)),
     # MocoInverse (configs[4]): prescribed kinematics (PositionMotion), implicit
     # tendons, residual rows only for the multibody dynamics
+    # (MocoInverse.cpp:93,105: the initial-activation endpoint rows lead g,
+    # no control-midpoint interpolation rows)
     "gait_inverse": lambda: configs.gait10dof18musc_inverse(4, sparsity="none"),
     "gait_inverse_central_trap": lambda: _trap(configs.gait10dof18musc_inverse(
         5, fd_scheme="central", sparsity="none")),
     "gait_inverse_sparse": lambda: _physiological_guess(configs.gait10dof18musc_inverse(4)),
+    "gait_inverse_random": lambda: configs.gait10dof18musc_inverse(3),
+    # interpolate_control_midpoints = false outside MocoInverse too
+    "double_pendulum_nointerp": lambda: _nointerp(configs.double_pendulum(12)),
+    "gait_rigid_nointerp_trap": lambda: _nointerp(_trap(configs.gait10dof18musc(6))),
 }
 
 
@@ -126,21 +144,25 @@ def _regular(v):
     return np.isfinite(v) & (np.abs(np.nan_to_num(v, nan=0.0)) < REGULAR)
 
 
-def _assert_close(a, b, tol, mask=None):
+def _assert_close(a, b, tol, mask=None, min_fraction=0.99):
     """a ~ b elementwise where the oracle value is regular (finite, below
-    REGULAR) and ``mask`` allows; irregular entries are garbage in both
+    REGULAR) and ``mask`` allows; at least ``min_fraction`` of the entries
+    must be compared.  Irregular entries are garbage in both
     implementations (generated kernels fold x*0 to 0, so their NaN
     propagation legitimately differs there)."""
     tol = np.broadcast_to(tol, b.shape)
     fin = _regular(b)
     if mask is not None:
         fin &= mask
-    assert fin.mean() > 0.5, fin.mean()
-    assert np.all(np.isfinite(a[fin]))
+    frac = float(fin.mean()) if fin.size else 1.0
     err = np.abs(a[fin] - b[fin])
+    rel = float((err / (np.abs(b[fin]) + 1e-300)).max()) if err.size else 0.0
+    info = f"compared {frac:.4f} of {fin.size}, max |d| {err.max() if err.size else 0:.3e}, max rel {rel:.3e}"
+    assert frac >= min_fraction, info
+    assert np.all(np.isfinite(a[fin])), info
     idx = np.where(fin)[0] if b.ndim == 1 else None
-    bad = np.argmax(err - tol[fin])
-    assert np.all(err <= tol[fin]), (err.max(), bad if idx is None else idx[bad])
+    bad = int(np.argmax(err - tol[fin])) if err.size else 0
+    assert np.all(err <= tol[fin]), (info, bad if idx is None else int(idx[bad]))
 
 
 def _scale(v):
@@ -148,24 +170,26 @@ def _scale(v):
 
 
 def _rows(nlp):
-    """(rows per interval, tail rows): the final mesh point's path rows and
-    (implicit mode) the final grid point's residual rows follow the last
-    interval."""
+    """(rows per interval, tail rows): the endpoint rows (NEP) lead g, the
+    final mesh point's path rows and (implicit mode) the final grid point's
+    residual rows follow the last interval."""
     N = nlp.opts.num_mesh_intervals
     tail = nlp.tail_rows
-    return (nlp.m - tail) // N, tail
+    return (nlp.m - tail - nlp.NEP) // N, tail
 
 
 def _per_row(nlp, per_interval):
-    """Expand a per-interval array to g rows (tail rows take the last
-    interval's value)."""
+    """Expand a per-interval array to g rows (head rows take the first
+    interval's value, tail rows the last interval's)."""
     rpi, tail = _rows(nlp)
-    return np.concatenate([np.repeat(per_interval, rpi), np.full(tail, per_interval[-1])])
+    return np.concatenate([np.full(nlp.NEP, per_interval[0]), np.repeat(per_interval, rpi),
+                           np.full(tail, per_interval[-1])])
 
 
 def _row_interval(nlp, rows):
+    """Mesh interval of g rows (head rows: 0, tail rows: N - 1)."""
     rpi, _ = _rows(nlp)
-    return np.minimum(rows // rpi, nlp.opts.num_mesh_intervals - 1)
+    return np.clip((rows - nlp.NEP) // rpi, 0, nlp.opts.num_mesh_intervals - 1)
 
 
 def _row_mask(ref, x):
@@ -196,7 +220,7 @@ def _row_mask(ref, x):
             s = row % NS
             if s >= (2 * TQ if nacc else TQ):
                 mask[i, npc + npres * nres + row] = ok[s + ref.SO]
-    return np.concatenate([mask.reshape(-1), np.ones(npc, bool), R[-1, rout]])
+    return np.concatenate([np.ones(ref.NEP, bool), mask.reshape(-1), np.ones(npc, bool), R[-1, rout]])
 
 
 BACKENDS = ["auto", "lane", "generic"]
@@ -305,10 +329,63 @@ def _grid(nlp):
     return mesh
 
 
+_WALK = {}
+
+
+def _walking_reference():
+    if not _WALK:
+        import json
+        import os
+        from mocohip import configs as _c
+        with open(os.path.join(_c.DATA, "walk_gait1018_state_reference.json")) as fh:
+            d = json.load(fh)
+        _WALK["time"] = np.asarray(d["time"])
+        _WALK.update({k: np.asarray(v) for k, v in d["columns"].items()})
+    return _WALK
+
+
+def physiological_iterate(nlp, seed=0):
+    """Random within bounds, with the muscle model in its working range:
+    activations in [0.2, 0.6], normalized tendon forces in [0.05, 0.3],
+    muscle excitations in [0.05, 0.4], implicit tendon-force derivatives in
+    [-0.5, 0.5] (elsewhere the DGF curves under- or overflow and the DAE is
+    inf / NaN / ~1e250 garbage in both implementations)."""
+    r = np.random.default_rng(seed)
+    x = nlp.random_iterate(r.uniform(-1, 1, nlp.n))
+    G, NS, NC = nlp.G, nlp.NS, nlp.NC
+    S = x[2:2 + NS * G].reshape(G, NS)
+    # gait models: coordinates and speeds near the reference walking motion
+    # (walk_gait1018_state_reference, +-2 %), where every muscle path is in
+    # its physiological range
+    ref = _walking_reference()
+    tk = _lanes.oracle_times(nlp, x)
+    for i, n in enumerate(nlp.rep.state_names):
+        base = n[:-len("/speed")] + "/value" if n.endswith("/speed") else n
+        if base in ref:
+            tt, qq = ref["time"], ref[base]
+            v = np.interp(tk, tt, np.gradient(qq, tt) if n.endswith("/speed") else qq)
+            S[:, i] = v * r.uniform(0.98, 1.02, G)
+    for i, n in enumerate(nlp.rep.state_names):
+        if n.endswith("/activation"):
+            S[:, i] = r.uniform(0.2, 0.6, G)
+        elif n.endswith("/normalized_tendon_force"):
+            S[:, i] = r.uniform(0.05, 0.3, G)
+    U = x[2 + NS * G:2 + (NS + NC) * G].reshape(G, NC)
+    muscles = {m.path for m in getattr(nlp.rep.problem.model, "muscles", [])}
+    for j, n in enumerate(nlp.rep.control_names):
+        if n in muscles:
+            U[:, j] = r.uniform(0.05, 0.4, G)
+    if nlp.NAR:
+        W = x[2 + (NS + NC) * G:].reshape(G, nlp.NDV)
+        W[:, nlp.NACC:] = r.uniform(-0.5, 0.5, (G, nlp.NAR))
+    return x
+
+
 def _iterates(nlp):
-    xr = nlp.random_iterate(np.random.default_rng(0).uniform(-1, 1, nlp.n))
-    xm = nlp.initial_guess_from_bounds()
-    return [("random", xr), ("midpoint", xm)]
+    xp = physiological_iterate(nlp, 0)
+    xq = physiological_iterate(nlp, 1)
+    xq[:2] = nlp.initial_guess_from_bounds()[:2]   # bounds-midpoint times
+    return [("physiological", xp), ("physiological-midtime", xq)]
 
 
 def _interval_scale(ref, x):
@@ -406,7 +483,7 @@ def test_objective_and_gradient(name):
                                   "gait_rigid_implicit", "gait_rigid_pathcon",
                                   "pendulum_bound_both_implicit", "gait_rigid_sparse_random",
                                   "gait_implicit_pathcon_sparse", "gait_inverse_style_sparse",
-                                  "gait_inverse_sparse"])
+                                  "gait_inverse_sparse", "gait_inverse", "gait_inverse_random"])
 def test_shards_reassemble_bit_exact(name):
     """Mesh-interval shards (the multi-GPU partition) concatenate to exactly
     the unsharded g and Jacobian values."""
@@ -419,9 +496,11 @@ def test_shards_reassemble_bit_exact(name):
     cuts = [0, N // 3, (2 * N) // 3, N]
     gs, Js = [], []
     rpi, tail = _rows(full)
+    H = full.NEP
     for a, b in zip(cuts[:-1], cuts[1:]):
         sh = HipNLP(rep, st.solver.options(a, b))
-        assert (sh.row_begin, sh.row_end) == (a * rpi, b * rpi + (tail if b == N else 0))
+        assert (sh.row_begin, sh.row_end) == (0 if a == 0 else H + a * rpi,
+                                              H + b * rpi + (tail if b == N else 0))
         gs.append(sh.eval_g(x))
         Js.append(sh.eval_jac_g(x))
     assert np.array_equal(np.concatenate(gs), g)
@@ -558,3 +637,168 @@ def test_sparsity_detection_agrees(name):
             d = Y[1 + j, o] - Y[0, o]
             ok = (not np.isfinite(d)) or abs(d) <= 64 * np.finfo(float).eps * scale
             assert ok, (o, j, d, Y[0, o], scale)
+
+
+# ---------------------------------------------------------------------------
+# The Jacobian, end to end, tight enough to fail
+# ---------------------------------------------------------------------------
+def _lanes_pair(name, backend="auto", **kw):
+    gpu, ref, st = _pair(name, backend, **kw)
+    return gpu, ref, st
+
+
+def _device_lanes_check(gpu, ref, x):
+    """(times, Y_device, Y_oracle at the same lane inputs)."""
+    t, Y = gpu.jacobian_lanes(x)
+    Y0 = _lanes.oracle_lanes(ref, x, t)
+    return t, Y, Y0
+
+
+LANE_CASES = [n for n in CASES if n not in ("gait_compliant_sparse_central",)]
+
+
+@pytest.mark.parametrize("backend", ["auto", "lane"])
+@pytest.mark.parametrize("name", LANE_CASES)
+def test_jacobian_assembly_bit_exact_from_device_lanes(name, backend):
+    """The finite-difference quotients and the transcription chain rule are
+    exact arithmetic on the DAE lane outputs (CasOCFunction.h:38-44,
+    CasOCHermiteSimpson.cpp:53-105, CasOCTrapezoidal.cpp:43-59): the oracle,
+    fed with the device's own lanes and grid times, reproduces the device's
+    Jacobian values and g (fused eval_g + eval_jac_g pass, which takes g
+    from the same lanes' base lane) bit for bit.  Times are the oracle's
+    own formula, bit for bit too."""
+    gpu, ref, _ = _pair(name, backend)
+    for _, x in _iterates(gpu):
+        t, Y = gpu.jacobian_lanes(x)
+        assert np.array_equal(t, _lanes.oracle_times(ref, x))
+        g0, J0 = ref.assemble_from_lanes(x, t, Y)
+        g, J = gpu.eval_g_jac_g(x)
+        assert np.array_equal(J, J0, equal_nan=True), np.nanmax(np.abs(J - J0))
+        assert np.array_equal(g, g0, equal_nan=True), np.nanmax(np.abs(g - g0))
+        assert np.array_equal(gpu.eval_jac_g(x), J, equal_nan=True)
+
+
+@pytest.mark.parametrize("name", LANE_CASES)
+def test_jacobian_lanes_match_oracle_dae(name):
+    """Every lane output (the DAE at a perturbed input) against the oracle's
+    DAE at exactly the same input: within 1e-10 of the output's scale."""
+    gpu, ref, _ = _pair(name)
+    for _, x in _iterates(gpu):
+        t, Y, Y0 = _device_lanes_check(gpu, ref, x)
+        scale = np.where(_regular(Y0), np.abs(Y0), 0.0).max(axis=(0, 2), keepdims=True) + 1.0
+        _assert_close(Y.reshape(-1), Y0.reshape(-1),
+                      np.broadcast_to(1e-10 * scale, Y.shape).reshape(-1))
+
+
+def _tight_bound(gpu, ref, x, J0, Y, Y0, h_fd):
+    """Per entry: 1e-8 |J0| + 4 dY_i (h_i + 1) / h_fd, dY_i = the measured
+    largest lane-output difference on interval i's grid points (the head
+    and tail rows take their interval's)."""
+    ok = _regular(Y0) & np.isfinite(Y)
+    d = np.where(ok, np.abs(Y - Y0), 0.0).max(axis=(1, 2))
+    hs = ref.opts.transcription == 0
+    N = ref.opts.num_mesh_intervals
+    step = 2 if hs else 1
+    dYi = np.array([d[i * step:i * step + step + 1].max() for i in range(N)])
+    _, hi = _interval_scale(ref, x)
+    ir, _ = gpu.jac_structure()
+    tau = 4 * dYi * (hi + 1.0) / h_fd
+    return 1e-8 * _scale(J0) + tau[_row_interval(gpu, ir)]
+
+
+@pytest.mark.parametrize("name", ["double_pendulum_hs", "double_pendulum_trap", "gait_rigid_forward",
+                                  "gait_rigid_central", "gait_compliant_central", "gait_rigid_implicit",
+                                  "gait_rigid_pathcon", "gait_implicit_tendon", "gait_inverse",
+                                  "gait_inverse_random", "gait_rigid_nointerp_trap"])
+def test_jacobian_tight_bound(name):
+    """End to end at h_fd = 1e-4 (CasADi-style quotients of the same
+    callbacks): |J_gpu - J_oracle| <= 1e-8 |J| + 4 dY_i (h_i + 1) / h_fd
+    with dY_i MEASURED per interval from the lanes.  A wrong t0/tf seed or a
+    mis-indexed entry moves a value by O(|J|), far outside this bound
+    (test_jacobian_check_catches_mutations)."""
+    gpu, ref, st = _pair(name, env={})
+    st.solver.fd_step = 1e-4
+    rep = st.problem.create_rep()
+    gpu = HipNLP(rep, st.solver.options())
+    ref = OracleNLP(rep, st.solver.options() if st.solver.optim_sparsity_detection == "none"
+                    else _given(st, gpu.callback_sparsity()), threads=8)
+    for _, x in _iterates(gpu):
+        J, J0 = gpu.eval_jac_g(x), ref.eval_jac_g(x)
+        _, Y, Y0 = _device_lanes_check(gpu, ref, x)
+        bound = _tight_bound(gpu, ref, x, J0, Y, Y0, 1e-4)
+        ir, _ = gpu.jac_structure()
+        _assert_close(J, J0, bound, _row_mask(ref, x)[ir])
+
+
+def test_jacobian_check_catches_mutations():
+    """The checks above can fail: a t0 / tf seed swap, a permuted pair of
+    entries within a row and a one-ulp change of one lane are each caught."""
+    gpu, ref, st = _pair("gait_rigid_forward")
+    x = physiological_iterate(gpu, 7)
+    t, Y = gpu.jacobian_lanes(x)
+    J = gpu.eval_jac_g(x)
+    _, J0 = ref.assemble_from_lanes(x, t, Y)
+    assert np.array_equal(J, J0)
+    # (1) the t0 and tf lanes exchanged (a wrong time seed)
+    Ym = Y.copy()
+    Ym[:, :, [0, 1]] = Ym[:, :, [1, 0]]
+    assert not np.array_equal(ref.assemble_from_lanes(x, t, Ym)[1], J)
+    # (2) one lane's output one ulp off
+    Ym = Y.copy()
+    Ym[5, 3, 7] = np.nextafter(Ym[5, 3, 7], np.inf)
+    assert not np.array_equal(ref.assemble_from_lanes(x, t, Ym)[1], J)
+    # (3) two entries of one row swapped (a mis-indexed template entry)
+    ir, jc = gpu.jac_structure()
+    row = ir[len(ir) // 2]
+    e = np.where((ir == row) & (np.abs(J) > 1e-3))[0][:2]
+    Jm = J.copy()
+    Jm[e] = Jm[e[::-1]]
+    st.solver.fd_step = 1e-4
+    rep = st.problem.create_rep()
+    g4, r4 = HipNLP(rep, st.solver.options()), OracleNLP(rep, st.solver.options(), threads=8)
+    J4, J40 = g4.eval_jac_g(x), r4.eval_jac_g(x)
+    _, Y4, Y40 = _device_lanes_check(g4, r4, x)
+    bound = _tight_bound(g4, r4, x, J40, Y4, Y40, 1e-4)
+    assert np.all(np.abs(J4 - J40) <= bound)
+    J4m = J4.copy()
+    J4m[e] = J4m[e[::-1]]
+    assert not np.all(np.abs(J4m - J40) <= bound)
+
+
+# ---------------------------------------------------------------------------
+# The BASELINE configurations at their own sizes
+# ---------------------------------------------------------------------------
+SIZES = {
+    "gait_N200": lambda: configs.gait10dof18musc(200),          # configs[2], the bench workload
+    "gait_N400": lambda: configs.gait10dof18musc(400),          # the north-star size
+    "inverse_N125": lambda: configs.gait10dof18musc_inverse(125),  # configs[4]: MocoInverse, mesh 0.02 s
+}
+
+
+@pytest.mark.parametrize("name", list(SIZES))
+def test_config_at_full_size(name):
+    """Structure bit-exact; assembly bit-exact from the device lanes; lanes
+    within 1e-10 of the oracle's DAE; eval_g within 1e-10 of row scale."""
+    st = SIZES[name]()
+    rep = st.problem.create_rep()
+    gpu = HipNLP(rep, st.solver.options())
+    opts = (st.solver.options() if st.solver.optim_sparsity_detection == "none"
+            else _given(st, gpu.callback_sparsity()))
+    ref = OracleNLP(rep, opts, threads=16)
+    assert (gpu.n, gpu.m, gpu.nnz) == (ref.n, ref.m, ref.nnz)
+    ir, jc = gpu.jac_structure()
+    ir0, jc0 = ref.jac_structure()
+    assert np.array_equal(ir, ir0) and np.array_equal(jc, jc0)
+    x = physiological_iterate(gpu, 11)
+    t, Y = gpu.jacobian_lanes(x)
+    g0, J0 = ref.assemble_from_lanes(x, t, Y)
+    g, J = gpu.eval_g_jac_g(x)
+    assert np.array_equal(J, J0) and np.array_equal(g, g0)
+    Yo = _lanes.oracle_lanes(ref, x, t)
+    scale = np.where(_regular(Yo), np.abs(Yo), 0.0).max(axis=(0, 2), keepdims=True) + 1.0
+    _assert_close(Y.reshape(-1), Yo.reshape(-1), np.broadcast_to(1e-10 * scale, Y.shape).reshape(-1))
+    gg, gr = gpu.eval_g(x), ref.eval_g(x)
+    assert np.array_equal(gg, g)
+    Fi, hi = _interval_scale(ref, x)
+    _assert_close(gg, gr, _per_row(ref, 1e-10 * (Fi * (hi + 1.0) + np.abs(x).max() + 1.0)),
+                  _row_mask(ref, x))

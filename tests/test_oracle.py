@@ -2,6 +2,7 @@
 files.  CPU only."""
 import ctypes as C
 import math
+import os
 
 import numpy as np
 import pytest
@@ -10,6 +11,8 @@ from mocohip import abi, configs
 from mocohip.problem import MocoControlGoal, MocoProblem
 from mocohip.solver import MocoHipSolver, OracleNLP
 from mocohip.splines import SimmSpline, gcv_interpolating_ppoly, ppoly_eval
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 lib = abi.load_oracle()
 
@@ -731,8 +734,10 @@ def test_prescribed_kinematics_layout_and_equivalence():
     NZ, NC, G, NQ = nlp.NS, nlp.NC, nlp.G, nlp.NQ
     assert (nlp.TQ, nlp.NACC, nlp.NMB, nlp.NAR) == (0, 0, NQ, 18)
     assert nlp.n == 2 + (NZ + NC + 18) * G
-    rpi = 2 * (NQ + 18) + 2 * NZ + NC
-    assert nlp.m == N * rpi + NQ + 18
+    # MocoInverse: no control-midpoint interpolation rows (MocoInverse.cpp:105);
+    # one initial-activation endpoint row per muscle first (MocoInverse.cpp:93)
+    rpi = 2 * (NQ + 18) + 2 * NZ
+    assert nlp.m == 18 + N * rpi + NQ + 18
     # the equivalent implicit problem (q, u states, accelerations)
     imp = configs.gait10dof18musc(N, tendon_compliance=True, tendon_dynamics="implicit",
                                   dynamics="implicit")
@@ -806,3 +811,145 @@ def test_implicit_auxiliary_derivatives_term():
     cols = list(range(d0, nlp.n, 7))
     gn = _numjac(lambda z: np.array([nlp.eval_f(z)]), x, cols, h=1e-5)[0]
     assert np.allclose(gf[cols], gn, rtol=1e-6, atol=1e-8)
+
+
+# ---------------------------------------------------------------------------
+# Endpoint constraints (MocoInitialActivationGoal, MocoInverse.cpp:93) and the
+# MocoInverse layout without control-midpoint interpolation (MocoInverse.cpp:105)
+# ---------------------------------------------------------------------------
+def _inverse(N, sparsity="none", scheme="hermite-simpson"):
+    st = configs.gait10dof18musc_inverse(N, sparsity=sparsity)
+    st.solver.transcription_scheme = scheme
+    rep = st.problem.create_rep()
+    return st, rep, OracleNLP(rep, st.solver.options())
+
+
+def _inverse_iterate(nlp, seed=0):
+    r = np.random.default_rng(seed)
+    x = nlp.initial_guess_from_bounds()
+    G, NS, NC = nlp.G, nlp.NS, nlp.NC
+    S = x[2:2 + NS * G].reshape(G, NS)
+    for i, n in enumerate(nlp.rep.state_names):
+        S[:, i] = r.uniform(0.2, 0.6, G) if n.endswith("/activation") else r.uniform(0.05, 0.3, G)
+    x[2 + NS * G:2 + (NS + NC) * G] = r.uniform(0.05, 0.4, NC * G)
+    d0 = 2 + (NS + NC) * G
+    x[d0:] = r.uniform(-0.5, 0.5, nlp.n - d0)
+    return x
+
+
+@pytest.mark.parametrize("sparsity", ["none", "random"])
+def test_initial_activation_endpoint_rows(sparsity):
+    """One endpoint row per muscle with activation dynamics, ahead of every
+    mesh point's rows (flattenConstraints, CasOCTranscription.h:283-285),
+    bounds [0, 0] (MocoConstraintInfo.h:44-54), value initial excitation -
+    initial activation (MocoInitialActivationGoal.cpp:41-58).  Without
+    detection the row is dense over the Endpoint callback's inputs (t0, the
+    initial point, tf, the final point; CasOCFunction.h:167-240); with it,
+    exactly the two columns the function reads."""
+    st, rep, nlp = _inverse(3, sparsity)
+    NEP, G, NS, NC, NDV = 18, nlp.G, nlp.NS, nlp.NC, nlp.NDV
+    assert nlp.NEP == NEP
+    ir, jc = nlp.jac_structure()
+    nhead = int((ir < NEP).sum())
+    assert np.all(ir[:nhead] < NEP) and np.all(ir[nhead:] >= NEP)
+    assert np.all(np.diff(ir[:nhead]) >= 0)
+    sidx = {n: i for i, n in enumerate(rep.state_names)}
+    cidx = {n: i for i, n in enumerate(rep.control_names)}
+    muscles = [m for m in st.problem.model.muscles if not m.ignore_activation_dynamics]
+    W = 1 + NS + NC + NDV
+
+    def pt_cols(k):
+        return ([2 + k * NS + s for s in range(NS)] + [2 + NS * G + k * NC + j for j in range(NC)]
+                + [2 + (NS + NC) * G + k * NDV + j for j in range(NDV)])
+    dense = sorted([0, 1] + pt_cols(0) + pt_cols(G - 1))
+    x = _inverse_iterate(nlp)
+    g, J = nlp.eval_g(x), nlp.eval_jac_g(x)
+    xl, xu, gl, gu = nlp.bounds()
+    for e, mu in enumerate(muscles):
+        cols = jc[:nhead][ir[:nhead] == e]
+        a_col = 2 + sidx[mu.path + "/activation"]
+        e_col = 2 + NS * G + cidx[mu.path]
+        if sparsity == "none":
+            assert list(cols) == dense and len(cols) == 2 * W
+        else:
+            assert list(cols) == sorted([a_col, e_col])
+        assert g[e] == x[e_col] - x[a_col]
+        assert gl[e] == 0.0 and gu[e] == 0.0
+        vals = dict(zip(cols, J[:nhead][ir[:nhead] == e]))
+        assert abs(vals[e_col] - 1.0) < 1e-7 and abs(vals[a_col] + 1.0) < 1e-7
+        assert all(v == 0.0 for c, v in vals.items() if c not in (a_col, e_col))
+
+
+def test_initial_activation_pinned_by_reference_golden_row():
+    """The reference's converged MocoInverse solution
+    (Moco/Tests/std_testMocoInverse_subject_18musc_solution.sto, fixture
+    tests/golden/inverse_initial_activation.npz) has initial excitation ==
+    initial activation for each of its 18 muscles: the endpoint rows vanish
+    there, and our MocoInverse transcription has one such row per muscle."""
+    d = np.load(os.path.join(GOLDEN, "inverse_initial_activation.npz"))
+    assert len(d["muscles"]) == 18
+    assert np.array_equal(d["excitation"], d["activation"])
+    st, rep, nlp = _inverse(2)
+    x = _inverse_iterate(nlp)
+    sidx = {n: i for i, n in enumerate(rep.state_names)}
+    cidx = {n: i for i, n in enumerate(rep.control_names)}
+    muscles = [m for m in st.problem.model.muscles if not m.ignore_activation_dynamics]
+    assert len(muscles) == len(d["muscles"])
+    for mu, ex, ac in zip(muscles, d["excitation"], d["activation"]):
+        x[2 + sidx[mu.path + "/activation"]] = ac
+        x[2 + nlp.NS * nlp.G + cidx[mu.path]] = ex
+    assert np.all(nlp.eval_g(x)[:18] == 0.0)
+
+
+@pytest.mark.parametrize("scheme", ["hermite-simpson", "trapezoidal"])
+def test_inverse_layout_without_interp_and_jacobian(scheme):
+    """interpolate_control_midpoints = false (MocoInverse.cpp:105): no
+    interp rows; the whole Jacobian (endpoint head included) matches a
+    numerical derivative of eval_g."""
+    st, rep, nlp = _inverse(2, scheme=scheme)
+    st.solver.optim_finite_difference_scheme = "central"   # O(h^2) truncation for the check
+    nlp = OracleNLP(rep, st.solver.options())
+    NQ, NS, NAR, N = nlp.NQ, nlp.NS, 18, 2
+    npts = 2 if scheme == "hermite-simpson" else 1
+    ndef = 2 * NS if scheme == "hermite-simpson" else NS
+    assert nlp.m == 18 + N * (npts * (NQ + NAR) + ndef) + NQ + NAR
+    st.solver.interpolate_control_midpoints = True
+    with_interp = OracleNLP(rep, st.solver.options())
+    assert with_interp.m == nlp.m + (N * nlp.NC if scheme == "hermite-simpson" else 0)
+    x = _inverse_iterate(nlp, 3)
+    ir, jc = nlp.jac_structure()
+    J = np.zeros((nlp.m, nlp.n))
+    J[ir, jc] = nlp.eval_jac_g(x)
+    cols = np.unique(jc)
+    Jn = _numjac(nlp.eval_g, x, cols)
+    # central FD at h=1e-8: eps|f|/h rounding relative to the row's scale
+    scale = np.abs(Jn).max(1, keepdims=True) + 1.0
+    err = np.abs(J[:, cols] - Jn) / scale
+    assert err.max() <= 1e-6, err.max()
+
+
+@pytest.mark.parametrize("case", ["pendulum_hs_forward", "pendulum_trap_central", "gait_backward",
+                                  "gait_implicit_pathcon", "inverse_random"])
+def test_assembly_from_lanes_equals_eval_jac_g(case):
+    """orc_assemble_from_lanes (the checker of the device's quotient +
+    assembly arithmetic) fed with the oracle's own DAE at the lane inputs of
+    mh_debug_jacobian_lanes' layout reproduces orc_eval_g / orc_eval_jac_g
+    bit for bit: the lane layout, the FD quotients (CasOCFunction.h:38-44)
+    and the transcription chain rule agree with the direct evaluation."""
+    import _lanes
+    st = {"pendulum_hs_forward": lambda: configs.double_pendulum(5),
+          "pendulum_trap_central": lambda: configs.double_pendulum(4, "trapezoidal"),
+          "gait_backward": lambda: configs.gait10dof18musc(2, fd_scheme="backward"),
+          "gait_implicit_pathcon": lambda: configs.gait10dof18musc(2, dynamics="implicit",
+                                                                  control_bounds=True),
+          "inverse_random": lambda: configs.gait10dof18musc_inverse(2)}[case]()
+    if case == "pendulum_hs_forward":
+        st.solver.optim_finite_difference_scheme = "forward"
+    nlp = OracleNLP(st.problem.create_rep(), st.solver.options(), threads=4)
+    x = (_inverse_iterate(nlp, 5) if case == "inverse_random"
+         else nlp.random_iterate(np.random.default_rng(4).uniform(-1, 1, nlp.n)))
+    t = _lanes.oracle_times(nlp, x)
+    Y = _lanes.oracle_lanes(nlp, x, t)
+    g, J = nlp.assemble_from_lanes(x, t, Y)
+    assert np.array_equal(g, nlp.eval_g(x), equal_nan=True)
+    assert np.array_equal(J, nlp.eval_jac_g(x), equal_nan=True)

@@ -9,6 +9,9 @@ Inputs (all under /root/reference, read as data):
   Moco/Tests/walk_gait1018_subject01_grf.xml               (ExternalLoads)
   Moco/Tests/walk_gait1018_state_reference.mot             (MocoTrack reference)
   Moco/Tests/std_testMocoTrackGait10dof18musc_solution.sto (golden solution)
+  Moco/Tests/std_testMocoInverse_subject_18musc_solution.sto (MocoInverse
+      golden solution: its initial row pins the initial-activation endpoint
+      constraint, MocoInverse.cpp:93)
 """
 import json
 import math
@@ -79,6 +82,18 @@ def main():
     labels, data, hdr = read_storage(os.path.join(REF, "Moco/Tests/std_testMocoTrackGait10dof18musc_solution.sto"))
     np.savez_compressed(os.path.join(GOLDEN, "std_testMocoTrackGait10dof18musc_solution.npz"),
                         labels=np.array(labels), data=data,
+                        header=np.array([f"{k}={v}" for k, v in hdr.items()]))
+    # MocoInverse golden solution (Rajagopal 18 muscles, N=11): the initial
+    # row's excitation / activation pairs of every muscle
+    labels, data, hdr = read_storage(os.path.join(REF, "Moco/Tests/std_testMocoInverse_subject_18musc_solution.sto"))
+    col = {l: i for i, l in enumerate(labels)}
+    mus = [l[:-len("/activation")] for l in labels if l.endswith("/activation")
+           and l[:-len("/activation")] in col]
+    np.savez_compressed(os.path.join(GOLDEN, "inverse_initial_activation.npz"),
+                        muscles=np.array(mus),
+                        excitation=np.array([data[0, col[m]] for m in mus]),
+                        activation=np.array([data[0, col[m + "/activation"]] for m in mus]),
+                        time=data[0, 0],
                         header=np.array([f"{k}={v}" for k, v in hdr.items()]))
     print("wrote", DATA, GOLDEN)
 
