@@ -5,22 +5,35 @@ GRF external loads, Hermite-Simpson, forward finite differences),
 BASELINE.json configs[2] (N=200 mesh intervals).
 
 One step = one eval_g and one eval_jac_g of the full NLP at an iterate
-resident in HBM (device-pointer C ABI), results left in HBM
-(--mode fused: the one-call form IPOPT's eval_g(new_x) -> eval_jac_g(!new_x)
-pair allows; identical results).
-
-Timed region: K steps without per-call instrumentation.  The roofline
-numbers come from a second, instrumented pass of the same K steps right
-after it (HIP events between the stages on the context stream; they cost
-microseconds per call, so they stay out of `value`).
+resident in HBM (device-pointer C ABI), results left in HBM.  The calls are
+asynchronous (mh_set_async) on torch's current stream: each returns once its
+kernels are enqueued and the timed region ends with torch.cuda.synchronize()
+(barrier + synchronize on both sides).  Beside the headline:
+  value_fused     the IPOPT eval_g(new_x) -> eval_jac_g(!new_x) pair as one
+                  mh_eval_g_jac_g_device call (identical results);
+  value_blocking  every call synchronizes before returning (what a blocking
+                  host caller sees per call, device-resident data);
+  n400            the same workload at N=400 (the north-star size);
+  host_inclusive  host-pointer calls on page-locked buffers: x host->device,
+                  g and the Jacobian device->host every call (what a host
+                  IPOPT sees), at N=200 and N=400;
+  batch / inverse_batch / sparsity_random  concurrent independent NLPs and
+                  the detected-sparsity variants (configs[4] layout);
+  roofline        the longest kernel of eval_jac_g, timed with HIP events
+                  on the context stream in a second, instrumented pass;
+  cpu_baseline    the CPU oracle (kind "port"), 1 thread and all the box's
+                  cores, on a bounded sample of the same workload.
 
 --gpus N > 1 (one process per GPU, torch.distributed.run):
-  --multi replicas (default): every rank evaluates its own copy of the NLP
-      (the configs[4] batch layout: independent NLPs, one per GPU, no
-      collective on the data path) -> "scaling": "weak".
-  --multi mesh: the mesh intervals of ONE NLP are sharded over the ranks and
-      the g / Jacobian segments all-gathered over RCCL every step (what a
-      single host IPOPT needs) -> "scaling": "strong".
+  --multi replicas (default): every rank evaluates its own NLP (independent
+      trials, the configs[4] batch layout), no collective on the data path
+      -> "scaling": "weak".
+  --multi mesh: ONE NLP for one host IPOPT, its mesh intervals sharded over
+      the ranks: x is broadcast over RCCL, each rank evaluates its shard and
+      copies its contiguous g / Jacobian slice into its offset of one
+      page-locked host buffer shared by the node's ranks over its own PCIe
+      link (mocohip.distributed.HostGather) -> host-inclusive calls/s,
+      "scaling": "strong".
 
 Prints one JSON line on rank 0.
 """
@@ -29,6 +42,7 @@ import json
 import os
 import sys
 import time
+import uuid
 
 import numpy as np
 
@@ -46,23 +60,20 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--intervals", type=int, default=200)
     ap.add_argument("--fd", default="forward")
-    ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", choices=["separate", "fused"], default="separate",
                     help="separate: eval_g then eval_jac_g C-ABI calls; fused: one "
                          "mh_eval_g_jac_g call (IPOPT new_x=false pattern)")
+    ap.add_argument("--blocking", action="store_true",
+                    help="every C-ABI call synchronizes before returning (default: asynchronous "
+                         "device calls, synchronized at the end of the timed region)")
     ap.add_argument("--multi", choices=["replicas", "mesh"], default="replicas")
     ap.add_argument("--single-mode", action="store_true",
-                    help="measure only --mode (no secondary mode, no batch): for profiler runs, so "
+                    help="measure only the headline (no secondary lines): for profiler runs, so "
                          "that every launch of a kernel has the same shape")
-    ap.add_argument("--inverse-batch", type=int, default=8,
-                    help="also measure B MocoInverse NLPs per GPU (configs[4]: prescribed "
-                         "kinematics, implicit tendons, random sparsity, mesh_interval 0.02 s), "
-                         "0 = skip")
-    ap.add_argument("--batch", type=int, default=8,
-                    help="also measure B independent NLPs per GPU evaluated concurrently, one "
-                         "context (HIP stream) and host thread each (the configs[4] batch layout); "
-                         "reported beside the headline, 0 = skip")
+    ap.add_argument("--inverse-batch", type=int, default=8)
+    ap.add_argument("--batch", type=int, default=8)
     return ap.parse_args()
 
 
@@ -76,223 +87,6 @@ def latest_pmc():
     with open(path) as fh:
         d = json.load(fh)
     return d, d.get("source", "profiles/pmc_current.json")
-
-
-def main():
-    args = parse()
-    import torch
-    import torch.distributed as dist
-    from mocohip import configs
-    from mocohip.distributed import ShardGather, interval_shard
-    from mocohip.solver import HipNLP
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    mesh = world > 1 and args.multi == "mesh"
-
-    N = args.intervals
-    st = configs.gait10dof18musc(N, fd_scheme=args.fd)
-    st.solver.device = local
-    rep = st.problem.create_rep()
-    ib, ie = interval_shard(N, rank, world) if mesh else (0, N)
-    nlp = HipNLP(rep, st.solver.options(ib, ie))
-    # iterate: bounds midpoint for the states (where the muscle model is
-    # regular), uniform random controls within bounds (seed 0; replicas use
-    # seed = rank: independent trials)
-    x = nlp.random_iterate(np.random.default_rng(rank if not mesh else 0).uniform(-1, 1, nlp.n))
-    xm = nlp.initial_guess_from_bounds()
-    x[2:2 + nlp.NS * nlp.G] = xm[2:2 + nlp.NS * nlp.G]
-    dev = torch.device("cuda", local)
-    xd = torch.tensor(x, dtype=torch.float64, device=dev)
-    rpi = nlp.m // N
-    nzi = nlp.nnz // N
-    sg = ShardGather(N, rpi, nzi, world if mesh else 1, dev)
-    gseg, vseg = sg.gseg, sg.vseg
-
-    rec = {"g": [], "jac": []}
-
-    def step(record=False):
-        if args.mode == "fused":
-            nlp.eval_g_jac_g_device(xd.data_ptr(), gseg.data_ptr(), vseg.data_ptr())
-            if record:
-                rec["jac"].append(nlp.last_timings())
-        else:
-            nlp.eval_g_device(xd.data_ptr(), gseg.data_ptr())
-            if record:
-                rec["g"].append(nlp.last_timings())
-            nlp.eval_jac_g_device(xd.data_ptr(), vseg.data_ptr())
-            if record:
-                rec["jac"].append(nlp.last_timings())
-        if mesh:
-            sg.gather()
-
-    def timed(k, record):
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(k):
-            step(record)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        el = time.perf_counter() - t0
-        if world > 1:
-            t = torch.tensor([el], dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            el = float(t.item())
-        return el
-
-    for _ in range(args.warmup):
-        step()
-    elapsed = timed(args.steps, False)
-    # secondary: the same K steps as one fused call each (IPOPT's
-    # eval_g(new_x) -> eval_jac_g(!new_x) pair from one DAE pass)
-    other = "fused" if args.mode == "separate" else "separate"
-    other_elapsed = None
-    if not args.single_mode:
-        mode0, args.mode = args.mode, other
-        for _ in range(args.warmup):
-            step()
-        other_elapsed = timed(args.steps, False)
-        args.mode = mode0
-    # instrumented pass (roofline): same K steps with stage events
-    nlp.set_timing(True)
-    inst_elapsed = timed(args.steps, True)
-    nlp.set_timing(False)
-
-    # secondary: the same workload with optim_sparsity_detection "random"
-    # (MocoInverse's setting, MocoInverse.cpp:111): detected callback
-    # couplings only, same iterate, separate calls
-    sparse = None
-    if not args.single_mode and not mesh:
-        import copy
-        s2 = copy.copy(st.solver)
-        s2.optim_sparsity_detection = "random"
-        nls = HipNLP(rep, s2.options())
-        vs = torch.empty(nls.nnz, dtype=torch.float64, device=dev)
-        gs = torch.empty(nls.m, dtype=torch.float64, device=dev)
-
-        def sstep():
-            nls.eval_g_device(xd.data_ptr(), gs.data_ptr())
-            nls.eval_jac_g_device(xd.data_ptr(), vs.data_ptr())
-        for _ in range(args.warmup):
-            sstep()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            sstep()
-        torch.cuda.synchronize()
-        el = time.perf_counter() - t0
-        if world > 1:
-            t = torch.tensor([el], dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            el = float(t.item())
-        sparse = {"value": round(args.steps * world / el, 3), "unit": "calls/s", "nnz_jac": nls.nnz,
-                  "mode": "separate", "note": "optim_sparsity_detection=random (3 iterates)"}
-        nls.close()
-
-    ms_per_step = 1e3 * elapsed / args.steps
-    value = (args.steps if mesh else args.steps * world) / elapsed
-    batch = None
-    if args.batch > 1 and not mesh and not args.single_mode:
-        batch = batch_throughput(args, rep, st, local, rank, world, dev, torch, dist)
-    inverse = None
-    if args.inverse_batch > 0 and not mesh and not args.single_mode:
-        # MocoTool mesh_interval 0.02 s: ceil((2.499 - 0.001) / 0.02) = 125
-        # intervals (MocoTool.cpp:27,68-69)
-        ist = configs.gait10dof18musc_inverse(125, fd_scheme="forward", sparsity="random")
-        ist.solver.device = local
-        irep = ist.problem.create_rep()
-        inverse = batch_throughput(args, irep, ist, local, rank, world, dev, torch, dist,
-                                   B=args.inverse_batch, make_x=inverse_iterate)
-        inverse["workload"] = ("MocoInverse gait10dof18musc (configs[4]): PositionMotion, implicit DGF "
-                               "tendons, reserves, N=125, forward FD, random sparsity detection")
-
-    if rank == 0:
-        J = np.array(rec["jac"])          # [whole, DAE stage, transcription stage, k_groups] ms
-        dae_ms = float(np.median(J[:, 1]))
-        tr_ms = float(np.median(J[:, 2]))
-        G_local = nlp.G if not mesh else (2 * (ie - ib) + 1)
-        ND = nlp.NS + nlp.NC + 2              # FD directions incl. t0, tf
-        n_dae = G_local * (ND + 1) if args.fd != "central" else G_local * (2 * ND + 1)
-        be_name, f_dae, mhash = nlp.backend()
-        work = nlp.work()                     # executed FP64 ops of the (pruned) task kernels
-        flops = n_dae * f_dae                 # algorithmic: one full DAE per FD lane
-        nnz_local = (ie - ib) * nzi
-        alg_bytes_jac = 8 * (nlp.n + nnz_local)   # x in, Jacobian values out
-        fused_iv = nlp.uses_interval_kernel()
-        tr_kernel = "k_interval" if fused_iv else "k_transcribe"
-        pmc, pmc_src = latest_pmc()
-        traffic = dae_traffic = None
-        if pmc and pmc.get("workload") == f"N={N},fd={args.fd}":
-            kb = pmc.get("kernels", {})
-            traffic = kb.get(tr_kernel, {}).get("hbm_bytes")
-            dae_traffic = kb.get("k_groups", {}).get("hbm_bytes")
-        achieved = alg_bytes_jac / (tr_ms * 1e-3) / 1e9
-        dae_tf = flops / (dae_ms * 1e-3) / 1e12
-        roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                "kernel": (f"{tr_kernel}: finite-difference quotients + Jacobian assembly per mesh interval"
-                           + (" (group results combined in LDS)" if fused_iv else "")
-                           + "; the longest kernel of eval_jac_g"),
-                "kernel_ms": round(tr_ms, 5), "algorithmic_bytes": alg_bytes_jac,
-                "traffic_source": pmc_src if traffic is not None else None,
-                "dae_stage": {"kernel": "k_groups" if fused_iv else "k_groups + k_combine",
-                              "bound": "mfma", "unit": "TFLOP/s",
-                              "note": "FP64 VALU; MI355X FP64 vector peak = FP64 matrix peak",
-                              "achieved": round(dae_tf, 4), "peak": FP64_PEAK_TFLOPS,
-                              "frac": round(dae_tf / FP64_PEAK_TFLOPS, 5), "ms": round(dae_ms, 5),
-                              "algorithmic_flops_per_launch": flops, "dae_evals_per_launch": n_dae,
-                              "flops_per_dae": f_dae, "executed_flops_per_launch": float(work[0]),
-                              "executed_TFLOPs": round(float(work[0]) / (dae_ms * 1e-3) / 1e12, 4),
-                              "traffic": dae_traffic},
-                "backend": be_name, "model_hash": f"0x{mhash:016x}",
-                "instrumented_ms_per_step": round(1e3 * inst_elapsed / args.steps, 4)}
-        if rec["g"]:
-            Gt = np.array(rec["g"])
-            roof["eval_g_stage_ms"] = [round(float(np.median(Gt[:, i])), 5) for i in range(4)]
-        cpu = None
-        if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(rep, st.solver.options(), x, args.cpu_baseline_seconds)
-        line = {
-            "metric": "NLP eval_g+eval_jac_g calls/sec (gait10dof18musc)",
-            "value": round(value, 3), "unit": "calls/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 5), "higher_is_better": True,
-            "scaling": "strong" if mesh else "weak", "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic",
-            "config": {"workload": "MocoTrack gait10dof18musc DGF rigid tendon (configs[2])",
-                       "mesh_intervals": N, "grid_points": nlp.G, "n": nlp.n, "m": nlp.m,
-                       "nnz_jac": nlp.nnz, "transcription": "hermite-simpson",
-                       "fd": args.fd, "mode": args.mode,
-                       "parallelism": (f"mesh-shard{world}+rccl-allgather" if mesh
-                                       else f"replicas{world}" if world > 1 else "single"),
-                       "iterate": "bounds-midpoint states, uniform random controls"},
-            "roofline": roof,
-            "cpu_baseline": cpu,
-        }
-        if other_elapsed:
-            line[f"value_{other}"] = round((args.steps if mesh else args.steps * world) / other_elapsed, 3)
-        if batch:
-            line["batch"] = batch
-        if sparse:
-            line["sparsity_random"] = sparse
-        if inverse:
-            line["inverse_batch"] = inverse
-        if cpu and cpu.get("value"):
-            line["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 2)
-        print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
 
 
 def track_iterate(nlp, seed):
@@ -320,61 +114,215 @@ def inverse_iterate(nlp, seed):
     return x
 
 
-def batch_throughput(args, rep, st, local, rank, world, dev, torch, dist, B=None,
-                     make_x=track_iterate):
+class Ctx:
+    """torch / torch.distributed plumbing of one rank."""
+
+    def __init__(self, args):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist = torch, dist
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(self.local)
+        self.dev = torch.device("cuda", self.local)
+        if self.world > 1:
+            dist.init_process_group("nccl", device_id=self.dev)
+
+    def stream(self):
+        return self.torch.cuda.current_stream().cuda_stream
+
+    def timed(self, step, k):
+        """K steps bracketed by barrier + synchronize; max over ranks."""
+        torch, dist = self.torch, self.dist
+        torch.cuda.synchronize()
+        if self.world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(k):
+            step()
+        torch.cuda.synchronize()
+        if self.world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        if self.world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=self.dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el
+
+
+def make_nlp(cx, st, ib=0, ie=0, blocking=False):
+    from mocohip.solver import HipNLP
+    st.solver.device = cx.local
+    rep = st.problem.create_rep()
+    nlp = HipNLP(rep, st.solver.options(ib, ie))
+    nlp.set_stream(cx.stream())
+    nlp.set_async(not blocking)
+    return nlp
+
+
+def device_steps(cx, nlp, x):
+    """(step_separate, step_fused) on device buffers."""
+    torch = cx.torch
+    xd = torch.tensor(x, dtype=torch.float64, device=cx.dev)
+    gd = torch.zeros(max(nlp.row_end - nlp.row_begin, 1), dtype=torch.float64, device=cx.dev)
+    vd = torch.zeros(max(nlp.nnz_end - nlp.nnz_begin, 1), dtype=torch.float64, device=cx.dev)
+    xp, gp, vp = xd.data_ptr(), gd.data_ptr(), vd.data_ptr()
+
+    def separate():
+        nlp.eval_g_device(xp, gp)
+        nlp.eval_jac_g_device(xp, vp)
+
+    def fused():
+        nlp.eval_g_jac_g_device(xp, gp, vp)
+    return separate, fused, (xd, gd, vd)
+
+
+def measure(cx, step, args, k=None, w=None):
+    for _ in range(args.warmup if w is None else w):
+        step()
+    k = args.steps if k is None else k
+    return k, cx.timed(step, k)
+
+
+def host_inclusive(cx, nlp, x, args):
+    """eval_g + eval_jac_g through the host-pointer entries on page-locked
+    buffers: x to the device, g and all Jacobian values back, every call."""
+    torch = cx.torch
+    xh = torch.from_numpy(np.ascontiguousarray(x)).pin_memory()
+    gh = torch.empty(nlp.m, dtype=torch.float64).pin_memory()
+    vh = torch.empty(nlp.nnz, dtype=torch.float64).pin_memory()
+    xn, gn, vn = xh.numpy(), gh.numpy(), vh.numpy()
+    from mocohip import abi
+    lib, ctx = nlp.lib, nlp.ctx
+    xp, gp, vp = abi.dptr(xn), abi.dptr(gn), abi.dptr(vn)
+
+    def step():
+        lib.mh_eval_g(ctx, xp, 1, gp)
+        lib.mh_eval_jac_g(ctx, xp, 0, vp)
+    k = max(20, args.steps // 4)
+    k, el = measure(cx, step, args, k=k, w=5)
+    return {"value": round(k / el, 3), "unit": "calls/s", "ms_per_step": round(1e3 * el / k, 4),
+            "bytes_to_host_per_step": 8 * (nlp.m + nlp.nnz),
+            "note": "mh_eval_g + mh_eval_jac_g on page-locked host buffers (x in, g and J out over "
+                    "PCIe every call); never the headline"}
+
+
+def roofline(cx, nlp, steps, args, mode):
+    """Instrumented pass: HIP events between the stages on the context
+    stream (mh_set_timing) -> per-launch kernel times of eval_jac_g."""
+    nlp.set_timing(True)
+    rec = {"g": [], "jac": []}
+
+    def step():
+        if mode == "fused":
+            steps[1]()
+            rec["jac"].append(nlp.last_timings())
+        else:
+            nlp.eval_g_device(*steps[2])
+            rec["g"].append(nlp.last_timings())
+            nlp.eval_jac_g_device(*steps[3])
+            rec["jac"].append(nlp.last_timings())
+    _, el = measure(cx, step, args, w=2)
+    nlp.set_timing(False)
+    J = np.array(rec["jac"])          # [whole, DAE stage, transcription stage, k_groups] ms
+    dae_ms, tr_ms = float(np.median(J[:, 1])), float(np.median(J[:, 2]))
+    G, ND = nlp.G, nlp.NS + nlp.NC + 2
+    n_dae = G * (ND + 1) if args.fd != "central" else G * (2 * ND + 1)
+    be_name, f_dae, mhash = nlp.backend()
+    work = nlp.work()                     # executed FP64 ops of the (pruned) task kernels
+    alg_flops = n_dae * f_dae             # a full DAE per FD lane (the algorithm's work)
+    alg_bytes = 8 * (nlp.n + nlp.nnz)     # SURVEY §8(d): x in, Jacobian values out
+    fused_iv = nlp.uses_interval_kernel()
+    tr_kernel = "k_interval" if fused_iv else "k_transcribe"
+    pmc, pmc_src = latest_pmc()
+    traffic = dae_traffic = None
+    if pmc and pmc.get("workload") == f"N={args.intervals},fd={args.fd}":
+        kb = pmc.get("kernels", {})
+        traffic = kb.get(tr_kernel, {}).get("hbm_bytes")
+        dae_traffic = kb.get("k_groups", {}).get("hbm_bytes")
+    gbs = alg_bytes / (tr_ms * 1e-3) / 1e9
+    tf_exec = float(work[0]) / (dae_ms * 1e-3) / 1e12
+    hbm = {"kernel": f"{tr_kernel}: finite-difference quotients + Jacobian assembly per mesh interval"
+                     + (" (group results combined in LDS)" if fused_iv else ""),
+           "bound": "hbm", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(gbs / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel_ms": round(tr_ms, 5),
+           "algorithmic_bytes": alg_bytes,
+           "traffic_source": pmc_src if traffic is not None else None}
+    fp64 = {"kernel": "k_groups" if fused_iv else "k_groups + k_combine",
+            "bound": "mfma", "unit": "TFLOP/s",
+            "note": "FP64 VALU (MI355X FP64 vector peak = FP64 matrix peak); achieved = FP64 ops the "
+                    "pruned task kernels EXECUTE per launch / kernel time",
+            "achieved": round(tf_exec, 4), "peak": FP64_PEAK_TFLOPS,
+            "frac": round(tf_exec / FP64_PEAK_TFLOPS, 5), "kernel_ms": round(dae_ms, 5),
+            "executed_flops_per_launch": float(work[0]),
+            "algorithmic_flops_per_launch": alg_flops,
+            "algorithmic_note": f"{n_dae} DAE evaluations x {f_dae:.0f} ops (one full DAE per FD lane)",
+            "traffic": dae_traffic}
+    # the dominant (longest) kernel of eval_jac_g is the headline roofline
+    main, other = (hbm, fp64) if tr_ms >= dae_ms else (fp64, hbm)
+    roof = dict(main)
+    roof["other_kernel"] = other
+    roof.update({"backend": be_name, "model_hash": f"0x{mhash:016x}",
+                 "instrumented_ms_per_step": round(1e3 * el / args.steps, 4)})
+    if rec["g"]:
+        Gt = np.array(rec["g"])
+        roof["eval_g_stage_ms"] = [round(float(np.median(Gt[:, i])), 5) for i in range(4)]
+    return roof
+
+
+def batch_throughput(cx, st_fn, make_x, args, B):
     """B independent NLPs of the same workload per GPU (different iterates),
-    each on its own context / HIP stream and driven by its own host thread
-    (ctypes releases the GIL inside the C ABI calls): aggregate eval_g +
-    eval_jac_g calls/s over all NLPs and ranks."""
+    each on its own HIP stream and driven by its own host thread (ctypes
+    releases the GIL inside the C ABI calls): aggregate eval_g + eval_jac_g
+    calls/s over all NLPs and ranks.  Asynchronous calls, each thread
+    synchronizing its stream after its K steps."""
     from concurrent.futures import ThreadPoolExecutor
     from mocohip.solver import HipNLP
-    B = B or args.batch
+    torch = cx.torch
     items = []
     for b in range(B):
-        nlp = HipNLP(rep, st.solver.options())
-        x = make_x(nlp, 1000 + rank * B + b)
-        xd = torch.tensor(x, dtype=torch.float64, device=dev)
-        gd = torch.zeros(nlp.m, dtype=torch.float64, device=dev)
-        vd = torch.zeros(nlp.nnz, dtype=torch.float64, device=dev)
-        items.append((nlp, xd, gd, vd))
+        st = st_fn()
+        st.solver.device = cx.local
+        nlp = HipNLP(st.problem.create_rep(), st.solver.options())
+        s = torch.cuda.Stream(device=cx.dev)
+        nlp.set_stream(s.cuda_stream)
+        nlp.set_async(not args.blocking)
+        x = make_x(nlp, 1000 + cx.rank * B + b)
+        xd = torch.tensor(x, dtype=torch.float64, device=cx.dev)
+        gd = torch.zeros(nlp.m, dtype=torch.float64, device=cx.dev)
+        vd = torch.zeros(nlp.nnz, dtype=torch.float64, device=cx.dev)
+        items.append((nlp, s, xd, gd, vd))
 
     def run(item, k):
-        nlp, xd, gd, vd = item
+        nlp, s, xd, gd, vd = item
         for _ in range(k):
             if args.mode == "fused":
                 nlp.eval_g_jac_g_device(xd.data_ptr(), gd.data_ptr(), vd.data_ptr())
             else:
                 nlp.eval_g_device(xd.data_ptr(), gd.data_ptr())
                 nlp.eval_jac_g_device(xd.data_ptr(), vd.data_ptr())
+        nlp.synchronize()
 
     with ThreadPoolExecutor(B) as pool:
         list(pool.map(lambda it: run(it, args.warmup), items))
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        t0 = time.perf_counter()
-        list(pool.map(lambda it: run(it, args.steps), items))
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        el = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+        el = cx.timed(lambda: list(pool.map(lambda it: run(it, args.steps), items)), 1)
     be = items[0][0].backend()[0] if items else None
+    out = {"nlps_per_gpu": B, "value": round(B * cx.world * args.steps / el, 3), "unit": "calls/s",
+           "mode": args.mode, "layout": "one context (HIP stream) + host thread per NLP",
+           "backend": be, "nnz_jac": items[0][0].nnz, "m": items[0][0].m}
     for nlp, *_ in items:
         nlp.close()
-    return {"nlps_per_gpu": B, "value": round(B * world * args.steps / el, 3), "unit": "calls/s",
-            "mode": args.mode, "layout": "one context (HIP stream) + host thread per NLP",
-            "backend": be}
+    return out
 
 
-def cpu_baseline(rep, opts, x, budget_s):
+def cpu_baseline(rep, opts, x, budget_s, threads):
     """The CPU oracle (C restatement, OpenMP over grid points like CasADi's
     thread map) timed on this host, on a bounded sample of the workload."""
     from mocohip.solver import OracleNLP
-    threads = min(16, os.cpu_count() or 1)
     ref = OracleNLP(rep, opts, threads=threads)
     ref.eval_g(x)
     calls = 0
@@ -389,7 +337,166 @@ def cpu_baseline(rep, opts, x, budget_s):
     ref.close()
     return {"value": round(calls / el, 4), "unit": "calls/s", "cores": threads, "kind": "port",
             "sample": f"{calls} eval_g+eval_jac_g calls of the same workload (N={opts.num_mesh_intervals}) "
-                      f"in {el:.1f}s (oracle/oracle.c, OpenMP over grid points, {threads} threads)"}
+                      f"in {el:.1f}s (oracle/oracle.c, OpenMP over grid points, {threads} thread"
+                      f"{'s' if threads > 1 else ''}; host nproc {os.cpu_count()}, box share "
+                      f"{os.environ.get('OMP_NUM_THREADS', '?')} threads)"}
+
+
+def mesh_main(cx, args):
+    """--multi mesh: one NLP, sharded; host-inclusive strong scaling."""
+    from mocohip import configs
+    from mocohip.distributed import HostGather, interval_shard
+    torch, dist = cx.torch, cx.dist
+    N = args.intervals
+    ib, ie = interval_shard(N, cx.rank, cx.world)
+    st = configs.gait10dof18musc(N, fd_scheme=args.fd)
+    nlp = make_nlp(cx, st, ib, ie, blocking=False)
+    x = track_iterate(nlp, 0)
+    sep, fused, (xd, gd, vd) = device_steps(cx, nlp, x)
+    tag = os.environ.get("MOCOHIP_BENCH_TAG") or f"mocohip_bench_{os.getppid()}"
+    barrier = dist.barrier if cx.world > 1 else (lambda: None)
+    hg = HostGather(tag, nlp.m, nlp.nnz, (nlp.row_begin, nlp.row_end), (nlp.nnz_begin, nlp.nnz_end),
+                    cx.rank, barrier, pin=True)
+    stream = cx.stream()
+
+    def step():
+        if cx.world > 1:
+            dist.broadcast(xd, src=0)          # IPOPT's iterate to every rank (RCCL)
+        (fused if args.mode == "fused" else sep)()
+        hg.copy_from_device_async(gd.data_ptr(), vd.data_ptr(), stream)
+        torch.cuda.current_stream().synchronize()
+        if cx.world > 1:
+            dist.barrier()                     # every slice has landed on the IPOPT host
+    k, el = measure(cx, step, args)
+    ok = None
+    if cx.rank == 0:
+        # the reassembled host vectors against one unsharded evaluation
+        full = make_nlp(cx, configs.gait10dof18musc(N, fd_scheme=args.fd), blocking=True)
+        ok = bool(np.array_equal(hg.full_g(), full.eval_g(x))
+                  and np.array_equal(hg.full_values(), full.eval_jac_g(x)))
+        full.close()
+    barrier()
+    hg.close(unlink=cx.rank == 0)
+    if cx.rank == 0:
+        line = {"metric": "NLP eval_g+eval_jac_g calls/sec (gait10dof18musc)",
+                "value": round(k / el, 3), "unit": "calls/s", "n_gpus": cx.world, "steps": k,
+                "warmup": args.warmup, "ms_per_step": round(1e3 * el / k, 5), "higher_is_better": True,
+                "scaling": "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+                "config": {"workload": "MocoTrack gait10dof18musc DGF rigid tendon (configs[2]), one NLP "
+                                       "sharded by mesh interval for one host IPOPT",
+                           "mesh_intervals": N, "n": nlp.n, "m": nlp.m, "nnz_jac": nlp.nnz,
+                           "fd": args.fd, "mode": args.mode,
+                           "parallelism": f"mesh-shard{cx.world}: RCCL broadcast of x + per-rank DMA "
+                                          "of its g/J slice into one page-locked host buffer",
+                           "host_inclusive": True, "reassembly_bit_exact": ok}}
+        print(json.dumps(line), flush=True)
+
+
+def main():
+    args = parse()
+    cx = Ctx(args)
+    if args.multi == "mesh":
+        mesh_main(cx, args)
+        if cx.world > 1:
+            cx.dist.destroy_process_group()
+        return
+    from mocohip import configs
+    N = args.intervals
+    st = configs.gait10dof18musc(N, fd_scheme=args.fd)
+    nlp = make_nlp(cx, st, blocking=args.blocking)
+    # iterate: bounds midpoint for the states (where the muscle model is
+    # regular), uniform random controls within bounds (replicas: seed =
+    # rank, independent trials)
+    x = track_iterate(nlp, cx.rank)
+    sep, fused, bufs = device_steps(cx, nlp, x)
+    xd, gd, vd = bufs
+    head = fused if args.mode == "fused" else sep
+    k, elapsed = measure(cx, head, args)
+    value = k * cx.world / elapsed
+    extra = {}
+    if not args.single_mode:
+        other = sep if args.mode == "fused" else fused
+        _, el = measure(cx, other, args)
+        extra["value_fused" if args.mode == "separate" else "value_separate"] = round(k * cx.world / el, 3)
+        nlp.set_async(False)
+        _, el = measure(cx, head, args)
+        extra["value_blocking"] = round(k * cx.world / el, 3)
+        nlp.set_async(not args.blocking)
+    roof = roofline(cx, nlp, (sep, fused, (xd.data_ptr(), gd.data_ptr()), (xd.data_ptr(), vd.data_ptr())),
+                    args, args.mode)
+    if not args.single_mode:
+        # the north-star size
+        st4 = configs.gait10dof18musc(400, fd_scheme=args.fd)
+        n4 = make_nlp(cx, st4, blocking=args.blocking)
+        x4 = track_iterate(n4, cx.rank)
+        s4, f4, b4 = device_steps(cx, n4, x4)
+        k4, e4 = measure(cx, s4, args)
+        _, ef4 = measure(cx, f4, args)
+        hi4 = host_inclusive(cx, n4, x4, args)
+        extra["n400"] = {"value": round(k4 * cx.world / e4, 3), "unit": "calls/s",
+                         "ms_per_step": round(1e3 * e4 / k4, 5),
+                         "value_fused": round(k4 * cx.world / ef4, 3),
+                         "n": n4.n, "m": n4.m, "nnz_jac": n4.nnz, "host_inclusive": hi4,
+                         "workload": "configs[2] workload at N=400 (north_star target size)"}
+        n4.close()
+        extra["host_inclusive"] = host_inclusive(cx, nlp, x, args)
+        # optim_sparsity_detection "random" (MocoInverse's setting,
+        # MocoInverse.cpp:111): detected callback couplings only
+        from mocohip.solver import HipNLP
+        s2 = configs.gait10dof18musc(N, fd_scheme=args.fd)
+        s2.solver.optim_sparsity_detection = "random"
+        ns = make_nlp(cx, s2, blocking=args.blocking)
+        ss, _, _ = device_steps(cx, ns, x)
+        ks, es = measure(cx, ss, args)
+        extra["sparsity_random"] = {"value": round(ks * cx.world / es, 3), "unit": "calls/s",
+                                    "nnz_jac": ns.nnz, "mode": "separate",
+                                    "note": "optim_sparsity_detection=random (3 iterates)"}
+        ns.close()
+        if args.batch > 1:
+            extra["batch"] = batch_throughput(
+                cx, lambda: configs.gait10dof18musc(N, fd_scheme=args.fd), track_iterate, args, args.batch)
+        if args.inverse_batch > 0:
+            # MocoTool mesh_interval 0.02 s: ceil((2.499 - 0.001) / 0.02) = 125
+            # intervals (MocoTool.cpp:27,68-69)
+            inv = batch_throughput(cx, lambda: configs.gait10dof18musc_inverse(125), inverse_iterate,
+                                   args, args.inverse_batch)
+            inv["workload"] = ("MocoInverse gait10dof18musc (configs[4]): PositionMotion, implicit DGF "
+                               "tendons, reserves, initial-activation endpoint constraints, no control "
+                               "interpolation, N=125, forward FD, random sparsity detection")
+            extra["inverse_batch"] = inv
+    if cx.rank == 0:
+        cpu = cpu1 = None
+        if cx.world == 1 and not args.no_cpu_baseline:
+            box = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+            threads = max(1, min(box, os.cpu_count() or 1))
+            cpu = cpu_baseline(nlp.rep, st.solver.options(), x, args.cpu_baseline_seconds, threads)
+            if not args.single_mode:
+                cpu1 = cpu_baseline(nlp.rep, st.solver.options(), x, args.cpu_baseline_seconds, 1)
+        line = {
+            "metric": "NLP eval_g+eval_jac_g calls/sec (gait10dof18musc)",
+            "value": round(value, 3), "unit": "calls/s", "n_gpus": cx.world,
+            "steps": k, "warmup": args.warmup,
+            "ms_per_step": round(1e3 * elapsed / k, 5), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic",
+            "config": {"workload": "MocoTrack gait10dof18musc DGF rigid tendon (configs[2])",
+                       "mesh_intervals": N, "grid_points": nlp.G, "n": nlp.n, "m": nlp.m,
+                       "nnz_jac": nlp.nnz, "transcription": "hermite-simpson",
+                       "fd": args.fd, "mode": args.mode,
+                       "calls": "blocking" if args.blocking else "asynchronous (device pointers, torch stream)",
+                       "parallelism": f"replicas{cx.world}" if cx.world > 1 else "single",
+                       "iterate": "bounds-midpoint states, uniform random controls"},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        line.update(extra)
+        if cpu1:
+            line["cpu_baseline_1thread"] = cpu1
+        if cpu and cpu.get("value"):
+            line["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 2)
+        print(json.dumps(line), flush=True)
+    if cx.world > 1:
+        cx.dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -30,8 +30,11 @@
  *  - Indices are 0-based (IPOPT C_STYLE).
  *  - Host-pointer entry points copy x to the device and results back; the
  *    *_device variants take device pointers (e.g. torch tensor data_ptr())
- *    and never touch host memory.  Both are asynchronous w.r.t. nothing:
- *    they return after the results are complete.
+ *    and never touch host memory.  All work is ordered on one HIP stream:
+ *    the context's own, or the caller's (mh_set_stream).  By default every
+ *    entry returns after its results are complete; with mh_set_async(ctx,
+ *    1) the *_device entries return once their kernels are enqueued, and
+ *    the caller orders consumers on that stream or calls mh_synchronize.
  *  - Every function returns MH_OK (0) or an error code; mh_last_error()
  *    gives a thread-local message.  A context is used by one host thread at
  *    a time; distinct contexts may run concurrently (one HIP stream each).
@@ -429,8 +432,10 @@ int mh_eval_g(mh_ctx* ctx, const double* x, int new_x, double* g);
 int mh_eval_jac_g(mh_ctx* ctx, const double* x, int new_x, double* values);
 
 /* Device-pointer evaluations (x, g, values in device memory of the
- * context's device; stream-ordered on the context stream and synchronized
- * before returning). */
+ * context's device), ordered on the context's stream after everything
+ * enqueued on it before -- so a producer of x on that stream (see
+ * mh_set_stream) needs no extra synchronization -- and synchronized before
+ * returning unless the context is asynchronous (mh_set_async). */
 int mh_eval_g_device(mh_ctx* ctx, const double* x_dev, double* g_dev);
 int mh_eval_jac_g_device(mh_ctx* ctx, const double* x_dev,
         double* values_dev);
@@ -441,6 +446,18 @@ int mh_eval_jac_g_device(mh_ctx* ctx, const double* x_dev,
 int mh_eval_g_jac_g(mh_ctx* ctx, const double* x, double* g, double* values);
 int mh_eval_g_jac_g_device(mh_ctx* ctx, const double* x_dev, double* g_dev,
         double* values_dev);
+
+/* Order all of this context's work on `stream` (a hipStream_t of the
+ * context's device, e.g. torch.cuda.current_stream().cuda_stream); NULL
+ * returns to the context's own stream.  Work already enqueued on the
+ * previous stream completes first. */
+int mh_set_stream(mh_ctx* ctx, void* stream);
+/* on != 0: mh_eval_g_device / mh_eval_jac_g_device / mh_eval_g_jac_g_device
+ * return once enqueued (no host synchronization); host-pointer entries
+ * always complete before returning. */
+int mh_set_async(mh_ctx* ctx, int on);
+/* Wait for all work enqueued on the context's stream. */
+int mh_synchronize(mh_ctx* ctx);
 
 /* Per-point DAE probe (CasOC::Problem::calcMultibodySystemExplicit /
  * calcMultibodySystemImplicit, CasOCProblem.h:313-332) evaluated on the

@@ -49,20 +49,6 @@ struct TplEntry {
     int16_t dir;   // 0 = t0, 1 = tf, 2 + j = point input j
     int16_t s;     // state index of the row (defects) / control index (interp)
 };
-// 4-byte form of a template entry (staged in LDS by k_interval):
-// kind | pt << 4 | dir << 6 | s << 16 (the row is not needed to evaluate it).
-__host__ __device__ __forceinline__ uint32_t tpl_pack(const TplEntry& e) {
-    return (uint32_t)e.kind | ((uint32_t)e.pt << 4) | ((uint32_t)e.dir << 6) | ((uint32_t)e.s << 16);
-}
-__host__ __device__ __forceinline__ TplEntry tpl_unpack(uint32_t u) {
-    TplEntry e;
-    e.kind = (uint8_t)(u & 15u);
-    e.pt = (uint8_t)((u >> 4) & 3u);
-    e.dir = (int16_t)((u >> 6) & 1023u);
-    e.row = 0;
-    e.s = (int16_t)(u >> 16);
-    return e;
-}
 
 // ------------------------------------------------------------------------
 // DAE back ends.  Generic: the interpreter of dae_device.hpp with size-class
@@ -505,6 +491,7 @@ struct Interval {
     EndpointEqs E;
     double* gh;
     double* vh;
+    int dbg_stop;    // diagnostic timing build only: return after phase n (0: full)
     // Every interval opens with its mesh point's path rows.  The interval
     // N-1 also owns the tail (flattenConstraints, CasOCTranscription.h:
     // 286-308): the final mesh point's path rows, then the final grid
@@ -852,9 +839,33 @@ __device__ __forceinline__ void interval_span(const Interval& I, int i, int& k_f
 // HBM and one kernel less per evaluation.  Launched when the LDS budget
 // allows (interval_lds), otherwise the split path runs.
 constexpr int IV_UNROLL = 4;
+// Compiled Jacobian template (k_interval's assembly): one word per template
+// entry of the Jacobian lane layout.  A value is base + coef * q, with q one
+// double in the interval's LDS (a finite-difference quotient of sY, or the
+// constant 0 / 1 of dxdot's exact qdot = u rows), or q itself (raw: residual
+// rows); entries along t0 / tf (several f and dxdot terms) take the general
+// jac_entry path, path-constraint entries their own loop.  Same operations in
+// the same order as jac_entry, so the two agree bit for bit
+// (test_kernel_variants_bit_identical, MOCOHIP_CTPL=0).
+enum : uint32_t {
+    CT_OFF = 0xFFFFFu,          // bits 0-19: LDS offset of q relative to sY
+    CT_RAW = 1u << 26,
+    CT_GEN = 1u << 27,
+    CT_PATH = 1u << 28
+};
+__device__ __host__ __forceinline__ uint32_t ct_word(uint32_t off, uint32_t coef, uint32_t base) {
+    return off | (coef << 20) | (base << 23);
+}
+// LDS constants after the times: [0] 0.0, [1] 1.0, [2..7] the interval's
+// coefficients {0, -h/8, h/8, -h/6, (-h/6) 4, -h/2}, [8..11] the bases {0,
+// -1/2, 1, -1}.
+constexpr int CT_CONST = 4;      // offset of the constants after sTimes
+constexpr int CT_NCONST = 12;
+
 template <class D>
 __global__ void __launch_bounds__(1024) k_interval(DevModel M, Src S, Lanes Ln, Tasks TK, Layout L,
-        Interval I, const TplEntry* __restrict__ tpl, const uint32_t* __restrict__ tplp, int tables_lds,
+        Interval I, const TplEntry* __restrict__ tpl, const uint32_t* __restrict__ ctpl,
+        const int* __restrict__ ctgen, int nctgen,
         const double* __restrict__ T, const double* __restrict__ H, double* __restrict__ g,
         double* __restrict__ values) {
     extern __shared__ double smem[];
@@ -866,30 +877,25 @@ __global__ void __launch_bounds__(1024) k_interval(DevModel M, Src S, Lanes Ln, 
     const int nt = TK.tdoubles, nh = TK.nmass * D::NST;
     const int ny = D::NO * Ln.stride;
     double* sY = smem;                       // [npts][NO][stride]
-    double* sTimes = sY + npts * ny;         // [npts]
-    double* sT = sTimes + 4;                 // [npts][nt]
+    double* sTimes = sY + npts * ny;         // [npts] (+ pad)
+    double* sK = sTimes + CT_CONST;          // compiled-template constants
+    double* sT = sK + CT_NCONST;             // [npts][nt]
     double* sH = sT + npts * nt;             // [npts][nh]
-    // tables_lds: the packed Jacobian template and the role -> slot table
-    // are staged too, so that the combine and the assembly issue no global
-    // loads after this one round trip
-    const int ntp = (I.nnz_int + I.nnz_tail + 1) / 2;     // in doubles (tail entries included)
     double* sXs = sH + npts * nh;            // [npts][NS] states, [npts][NC] controls,
     double* sXc = sXs + npts * L.NS;         // [npts][NDV] accelerations (implicit)
     double* sXd = sXc + npts * L.NC;
-    double* sTpl = sXd + npts * L.NDV;
     // the interval's points are consecutive local grid points: their T (and
     // H) slabs are one contiguous run each
     const int kl0 = k_first - S.k0;
     if (nt > 0) stage_lds<16>(sT, T + (long)kl0 * nt, npts * nt);
     if (nh > 0) stage_lds<8>(sH, H + (long)kl0 * nh, npts * nh);
-    if (tables_lds && values) stage_lds<8>(sTpl, (const double*)tplp, ntp);
     stage_lds<1>(sXs, S.x + 2 + (long)k_first * L.NS, npts * L.NS);
     if (L.NC > 0) stage_lds<1>(sXc, S.x + 2 + (long)L.NS * L.G + (long)k_first * L.NC, npts * L.NC);
     if (L.NDV > 0)
         stage_lds<1>(sXd, S.x + 2 + (long)(L.NS + L.NC) * L.G + (long)k_first * L.NDV, npts * L.NDV);
-    const __attribute__((address_space(3))) uint32_t* tp = (const __attribute__((address_space(3))) uint32_t*)sTpl;
     const double t0 = S.x[0], tf = S.x[1];
     __syncthreads();
+    if (I.dbg_stop == 1) return;
     for (int w = threadIdx.x; w < npts * Ln.stride; w += blockDim.x) {
         const int p = w / Ln.stride, r = w - p * Ln.stride;
         LaneInL<D> in{lds(sXs + p * L.NS), lds(sXc + p * L.NC), lds(sXd + p * L.NDV), -1, 0.0};
@@ -906,27 +912,50 @@ __global__ void __launch_bounds__(1024) k_interval(DevModel M, Src S, Lanes Ln, 
     // finite-difference quotients in place (CasADi FiniteDiff formulas), once
     // per (point, output, direction) instead of once per Jacobian entry that
     // reads them; the base slot keeps the raw value for the defect rows
+    if (I.dbg_stop == 2) return;
     const int quot = values && Ln.stride > 1;
     if (quot) {
 #pragma clang fp contract(off)
-        const int ndir = Ln.ND;
-        for (int w = threadIdx.x; w < npts * D::NO * ndir; w += blockDim.x) {
-            const int po = w / ndir, d = w - po * ndir;
+        // one (point, output) row of lanes per wave: lanes = directions
+        const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nwave = blockDim.x >> 6;
+        const double h = Ln.h, h2 = 2.0 * Ln.h;
+        for (int po = wave; po < npts * D::NO; po += nwave) {
             lds_double* y = lds(sY + po * Ln.stride);
-            double q;
-            if (Ln.fd == MH_FD_CENTRAL) q = (y[d] - y[Ln.ND + d]) / (2.0 * Ln.h);
-            else if (Ln.fd == MH_FD_FORWARD) q = (y[d] - y[Ln.base]) / Ln.h;
-            else q = (y[Ln.base] - y[d]) / Ln.h;
-            y[d] = q;
+            const double yb = y[Ln.base];
+            for (int d = lane; d < Ln.ND; d += 64) {
+                double q;
+                if (Ln.fd == MH_FD_CENTRAL) q = (y[d] - y[Ln.ND + d]) / h2;
+                else if (Ln.fd == MH_FD_FORWARD) q = (y[d] - yb) / h;
+                else q = (yb - y[d]) / h;
+                y[d] = q;
+            }
         }
         __syncthreads();
     }
     const YS YV{lds(sY), lds(sTimes), D::NO, Ln.stride, k_first, quot, lds(sXs), lds(sXc), L.NS, L.NC,
                 lds(sXd), L.NDV};
+    if (I.dbg_stop == 3) return;
+    if (I.dbg_stop >= 5 && values) {
+        // diagnostic: the assembly's stores alone (5) / its template loads,
+        // LDS reads and arithmetic alone (6)
+        double* vi = values + (long)il * I.nnz_int;
+        const int ne = I.entries(i);
+        double acc = 0.0;
+        for (int e = threadIdx.x; e < ne; e += blockDim.x) {
+            if (I.dbg_stop == 5) vi[e] = 0.0;
+            else {
+                const uint32_t wu = ctpl ? ctpl[e] : 0u;
+                acc += sY[wu & CT_OFF] * (double)(wu >> 20);
+            }
+        }
+        if (I.dbg_stop == 6 && acc == 12345.678) vi[threadIdx.x] = acc;
+        return;
+    }
     if (g) {
         double* gi = g + (long)il * I.rpi;
         for (int r = threadIdx.x; r < I.rows(i); r += blockDim.x) gi[r] = defect_row(L, I, Ln, S.x, YV, i, r);
     }
+    if (I.dbg_stop == 4) return;
     if (values) {
         const IvC C = iv_const(YV.t(k_last) - YV.t(k_first), S.grid[k_last] - S.grid[k_first]);
         double* vi = values + (long)il * I.nnz_int;
@@ -935,10 +964,40 @@ __global__ void __launch_bounds__(1024) k_interval(DevModel M, Src S, Lanes Ln, 
         int e = threadIdx.x;
         // path-constraint entries (the first npe of the interval and of
         // the tail) are written by their own loop below
-        if (tables_lds) {
+        if (ctpl) {
+#pragma clang fp contract(off)
+            if (threadIdx.x < 2) sK[threadIdx.x] = threadIdx.x ? 1.0 : 0.0;
+            __syncthreads();
+            const lds_double* q0 = lds(sY);
+            // coefficient / base of a word, selected in registers
+            const double c1 = -C.h8, c2 = C.h8, c3 = -C.h6, c4 = -C.h6 * 4.0, c5 = -C.hh;
+            auto value = [&](uint32_t wu, double q) {
+                const uint32_t ks = (wu >> 20) & 7, bs = (wu >> 23) & 7;
+                const double coef = ks == 1 ? c1 : ks == 2 ? c2 : ks == 3 ? c3 : ks == 4 ? c4 : ks == 5 ? c5 : 0.0;
+                const double base = bs == 1 ? -0.5 : bs == 2 ? 1.0 : bs == 3 ? -1.0 : 0.0;
+                return (wu & CT_RAW) ? q : base + coef * q;
+            };
+            // the bulk: one LDS value, a product and a sum per entry; the
+            // t0 / tf columns of the defect rows (CT_GEN) and the path
+            // entries are written by the loops below
+            for (; e + (IV_UNROLL - 1) * B < ne; e += IV_UNROLL * B) {
+                uint32_t w[IV_UNROLL];
+                double q[IV_UNROLL];
+#pragma unroll
+                for (int u = 0; u < IV_UNROLL; ++u) w[u] = ctpl[e + u * B];
+#pragma unroll
+                for (int u = 0; u < IV_UNROLL; ++u) q[u] = q0[w[u] & CT_OFF];
+#pragma unroll
+                for (int u = 0; u < IV_UNROLL; ++u)
+                    if (!(w[u] & (CT_GEN | CT_PATH))) vi[e + u * B] = value(w[u], q[u]);
+            }
             for (; e < ne; e += B) {
-                const TplEntry te = tpl_unpack(tp[e]);
-                if (te.kind != T_PATH) vi[e] = jac_entry<false>(L, Ln, I.P, S.x, YV, te, k_first, C);
+                const uint32_t wu = ctpl[e];
+                if (!(wu & (CT_GEN | CT_PATH))) vi[e] = value(wu, q0[wu & CT_OFF]);
+            }
+            for (int j = threadIdx.x; j < nctgen; j += B) {
+                const int eg = ctgen[j];
+                vi[eg] = jac_entry<false>(L, Ln, I.P, S.x, YV, tpl[eg], k_first, C);
             }
             e = ne;
         }
@@ -966,6 +1025,243 @@ __global__ void __launch_bounds__(1024) k_interval(DevModel M, Src S, Lanes Ln, 
         }
     }
     if (i == 0 && (I.gh || I.vh))
+        endpoint_head(L, Ln, I.E, S.x, g ? I.gh : nullptr, values ? I.vh : nullptr, threadIdx.x, blockDim.x);
+}
+
+// ------------------------------------------------------------------------
+// k_role: the Jacobian transcription with one workgroup per (mesh interval,
+// grid point of the interval) -- 3 per Hermite-Simpson interval, 2 per
+// trapezoidal one.  Each block stages and combines only ITS point's group
+// results (all of its lanes), forms that point's finite-difference
+// quotients, and writes the Jacobian entries of the interval that read that
+// point (the point's columns of every defect row, its residual and path
+// rows).  The entries that couple the points -- the t0 / tf columns of the
+// defect rows -- and the defect / interpolation rows of g belong to the
+// "time role" (the midpoint; trapezoidal: the first point), which also
+// combines the few lanes it needs of the other points (t0, tf and the
+// unperturbed lane) straight from their group results in global memory.
+// Against k_interval: a third of the staging, combine and stores per block
+// and three times the blocks (several per CU, overlapping their phases);
+// the same arithmetic, bit for bit (test_kernel_variants_bit_identical).
+// ------------------------------------------------------------------------
+struct RowR {   // a row of lanes of one point; r == full_base -> its base lane
+    const lds_double* p;
+    int full_base, base;
+    __device__ __forceinline__ double operator[](int r) const { return p[r == full_base ? base : r]; }
+};
+struct YR {
+    const lds_double* Y[3];
+    int stride[3], base[3];
+    int full_base, NO, kf, q;
+    const lds_double* times;
+    const lds_double* sxs;
+    const lds_double* sxc;
+    const lds_double* sxd;
+    int NS, NC, NDV;
+    __device__ __forceinline__ double xs(int k, int s) const { return sxs[(k - kf) * NS + s]; }
+    __device__ __forceinline__ double xc(int k, int j) const { return sxc[(k - kf) * NC + j]; }
+    __device__ __forceinline__ double xd(int k, int j) const { return sxd[(k - kf) * NDV + j]; }
+    __device__ __forceinline__ double t(int k) const { return times[k - kf]; }
+    __device__ __forceinline__ RowR row(int k, int o) const {
+        const int p = k - kf;
+        return RowR{Y[p] + o * stride[p], full_base, base[p]};
+    }
+};
+// Per role: the (entry, compiled word) lists (own-point LDS offsets), and the
+// tail's list for the last role of the last interval.
+struct RoleLists {
+    const int* __restrict__ e;
+    const uint32_t* __restrict__ w;
+    int off[4];        // role r: [off[r], off[r + 1])
+    int tail0, tail1;  // the tail's entries
+};
+// Lanes of a neighbor point the time role combines: t0, tf, (central: t0-,
+// tf-), unperturbed.
+__device__ __forceinline__ int nb_lanes(const Lanes& Ln) { return Ln.fd == MH_FD_CENTRAL ? 5 : 3; }
+__device__ __forceinline__ int nb_role(const Lanes& Ln, int j) {
+    const int NL = nb_lanes(Ln);
+    return j == NL - 1 ? Ln.base : (j < 2 ? j : Ln.ND + (j - 2));
+}
+
+template <class D>
+__global__ void __launch_bounds__(512) k_role(DevModel M, Src S, Lanes Ln, Tasks TK, Layout L,
+        Interval I, const TplEntry* __restrict__ tpl, RoleLists RL, const int* __restrict__ ctgen, int nctgen,
+        const double* __restrict__ T, const double* __restrict__ H, double* __restrict__ g,
+        double* __restrict__ values) {
+#pragma clang fp contract(off)
+    extern __shared__ double smem[];
+    const bool hs = I.scheme == MH_HERMITE_SIMPSON;
+    const int R = hs ? 3 : 2, TR = hs ? 1 : 0;
+    const int il = blockIdx.x / R, role = blockIdx.x - il * R;
+    const int i = I.ib + il;
+    int k_first, k_last;
+    interval_span(I, i, k_first, k_last);
+    const int S_ = Ln.stride, NO = D::NO, NL = nb_lanes(Ln);
+    const int nt = TK.tdoubles, nh = TK.nmass * D::NST;
+    double* sY = smem;                          // own point [NO][S]
+    double* sYn = sY + NO * S_;                 // neighbors [R - 1][NO][NL] (time role)
+    double* sTimes = sYn + (R - 1) * NO * NL;   // [R] (+ pad)
+    double* sK = sTimes + CT_CONST;             // 0.0, 1.0
+    double* sT = sK + 2;                        // own [nt]
+    double* sH = sT + nt;                       // own [nh]
+    double* sXs = sH + nh;                      // [R][NS], [R][NC], [R][NDV]
+    double* sXc = sXs + R * L.NS;
+    double* sXd = sXc + R * L.NC;
+    const int kown = k_first + role;
+    const int klo = kown - S.k0;
+    if (nt > 0) stage_lds<8>(sT, T + (long)klo * nt, nt);
+    if (nh > 0) stage_lds<4>(sH, H + (long)klo * nh, nh);
+    stage_lds<1>(sXs, S.x + 2 + (long)k_first * L.NS, R * L.NS);
+    if (L.NC > 0) stage_lds<1>(sXc, S.x + 2 + (long)L.NS * L.G + (long)k_first * L.NC, R * L.NC);
+    if (L.NDV > 0)
+        stage_lds<1>(sXd, S.x + 2 + (long)(L.NS + L.NC) * L.G + (long)k_first * L.NDV, R * L.NDV);
+    if (threadIdx.x < 2) sK[threadIdx.x] = threadIdx.x ? 1.0 : 0.0;
+    const double t0 = S.x[0], tf = S.x[1];
+    if (threadIdx.x < R) {   // every role's formulas use the interval's base times
+        int pi;
+        double st;
+        sTimes[threadIdx.x] = lane_time(Ln, S.grid[k_first + threadIdx.x], t0, tf, Ln.base, pi, st);
+    }
+    __syncthreads();
+    // own lanes from LDS; the time role's neighbor lanes from global memory
+    const int nnb = role == TR ? (R - 1) * NL : 0;
+    for (int w = threadIdx.x; w < S_ + nnb; w += blockDim.x) {
+        int p = role, r = w;
+        double* Yd;
+        int ys;
+        if (w < S_) {
+            Yd = sY + r;
+            ys = S_;
+        } else {
+            const int q = (w - S_) / NL, j = (w - S_) - q * NL;
+            p = q < TR ? q : q + 1;
+            r = nb_role(Ln, j);
+            Yd = sYn + q * NO * NL + j;
+            ys = NL;
+        }
+        LaneInL<D> in{lds(sXs + p * L.NS), lds(sXc + p * L.NC), lds(sXd + p * L.NDV), -1, 0.0};
+        const double t = lane_time(Ln, S.grid[k_first + p], t0, tf, r, in.pi, in.step);
+        double out[D::NO];
+        if (p == role) {
+            const TaskLoadLds<D> TL{lds(sT), lds(sH), TK.jd, r};
+            D::combine(M, t, in, TL, out);
+        } else {
+            const int kl = k_first + p - S.k0;
+            const TaskLoadGlobal<D> TG{T + (long)kl * nt, H + (long)kl * nh, TK.jd, r};
+            D::combine(M, t, in, TG, out);
+        }
+        lds_double* Yp = lds(Yd);
+#pragma unroll
+        for (int o = 0; o < D::NO; ++o) Yp[o * ys] = out[o];
+    }
+    __syncthreads();
+    // finite-difference quotients in place: own point, one output row of
+    // lanes per wave; the neighbors' t0 / tf lanes
+    {
+        const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nwave = blockDim.x >> 6;
+        const double h = Ln.h, h2 = 2.0 * Ln.h;
+        for (int o = wave; o < NO; o += nwave) {
+            lds_double* y = lds(sY + o * S_);
+            const double yb = y[Ln.base];
+            for (int d = lane; d < Ln.ND; d += 64) {
+                double q;
+                if (Ln.fd == MH_FD_CENTRAL) q = (y[d] - y[Ln.ND + d]) / h2;
+                else if (Ln.fd == MH_FD_FORWARD) q = (y[d] - yb) / h;
+                else q = (yb - y[d]) / h;
+                y[d] = q;
+            }
+        }
+        for (int w = threadIdx.x; w < (role == TR ? (R - 1) * NO * 2 : 0); w += blockDim.x) {
+            const int qo = w >> 1, d = w & 1;
+            lds_double* y = lds(sYn + qo * NL);
+            double q;
+            if (Ln.fd == MH_FD_CENTRAL) q = (y[d] - y[2 + d]) / h2;
+            else if (Ln.fd == MH_FD_FORWARD) q = (y[d] - y[NL - 1]) / h;
+            else q = (y[NL - 1] - y[d]) / h;
+            y[d] = q;
+        }
+        __syncthreads();
+    }
+    YR YV;
+    YV.full_base = Ln.base;
+    YV.NO = NO;
+    YV.kf = k_first;
+    YV.q = 1;
+    YV.times = lds(sTimes);
+    YV.sxs = lds(sXs);
+    YV.sxc = lds(sXc);
+    YV.sxd = lds(sXd);
+    YV.NS = L.NS;
+    YV.NC = L.NC;
+    YV.NDV = L.NDV;
+    for (int p = 0, q = 0; p < 3; ++p) {
+        if (p == role) { YV.Y[p] = lds(sY); YV.stride[p] = S_; YV.base[p] = Ln.base; }
+        else if (p < R) { YV.Y[p] = lds(sYn + (q++) * NO * NL); YV.stride[p] = NL; YV.base[p] = NL - 1; }
+        else { YV.Y[p] = lds(sY); YV.stride[p] = S_; YV.base[p] = Ln.base; }
+    }
+    const int B = blockDim.x;
+    const int npres = hs ? 2 : 1;
+    if (g) {
+        // this role's rows: path rows (role 0), its point's residual rows,
+        // defect / interpolation rows (time role), the tail (last role)
+        double* gi = g + (long)il * I.rpi;
+        const int npc = I.P.npc;
+        for (int r = threadIdx.x; r < I.rows(i); r += B) {
+            int owner;
+            if (r >= I.rpi) owner = R - 1;
+            else if (r < npc) owner = 0;
+            else if (r < npc + npres * I.nres) owner = (r - npc) / I.nres;
+            else owner = TR;
+            if (owner == role) gi[r] = defect_row(L, I, Ln, S.x, YV, i, r);
+        }
+    }
+    if (values) {
+        const IvC C = iv_const(YV.t(k_last) - YV.t(k_first), S.grid[k_last] - S.grid[k_first]);
+        double* vi = values + (long)il * I.nnz_int;
+        const lds_double* q0 = lds(sY);
+        const double c1 = -C.h8, c2 = C.h8, c3 = -C.h6, c4 = -C.h6 * 4.0, c5 = -C.hh;
+        auto value = [&](uint32_t wu, double q) {
+            const uint32_t ks = (wu >> 20) & 7, bs = (wu >> 23) & 7;
+            const double coef = ks == 1 ? c1 : ks == 2 ? c2 : ks == 3 ? c3 : ks == 4 ? c4 : ks == 5 ? c5 : 0.0;
+            const double base = bs == 1 ? -0.5 : bs == 2 ? 1.0 : bs == 3 ? -1.0 : 0.0;
+            return (wu & CT_RAW) ? q : base + coef * q;
+        };
+        auto run = [&](int a, int b) {
+            int e = a + threadIdx.x;
+            for (; e + (IV_UNROLL - 1) * B < b; e += IV_UNROLL * B) {
+                uint32_t w[IV_UNROLL];
+                int ee[IV_UNROLL];
+                double q[IV_UNROLL];
+#pragma unroll
+                for (int u = 0; u < IV_UNROLL; ++u) { w[u] = RL.w[e + u * B]; ee[u] = RL.e[e + u * B]; }
+#pragma unroll
+                for (int u = 0; u < IV_UNROLL; ++u) q[u] = q0[w[u] & CT_OFF];
+#pragma unroll
+                for (int u = 0; u < IV_UNROLL; ++u) vi[ee[u]] = value(w[u], q[u]);
+            }
+            for (; e < b; e += B) {
+                const uint32_t wu = RL.w[e];
+                vi[RL.e[e]] = value(wu, q0[wu & CT_OFF]);
+            }
+        };
+        run(RL.off[role], RL.off[role + 1]);
+        if (i == I.N - 1 && role == R - 1) run(RL.tail0, RL.tail1);
+        if (role == TR)
+            for (int j = threadIdx.x; j < nctgen; j += B) {
+                const int eg = ctgen[j];
+                vi[eg] = jac_entry<false>(L, Ln, I.P, S.x, YV, tpl[eg], k_first, C);
+            }
+        // path-constraint entries at the mesh point (role 0) and, in the
+        // tail, at the final mesh point (last role of the last interval)
+        if (I.npe > 0 && (role == 0 || (role == R - 1 && i == I.N - 1))) {
+            const int npe = I.npe;
+            for (int w = threadIdx.x; w < npe; w += B) {
+                const int ep = role == 0 ? w : I.nnz_int + w;
+                vi[ep] = jac_entry<true>(L, Ln, I.P, S.x, YV, tpl[ep], k_first, C);
+            }
+        }
+    }
+    if (i == 0 && role == 0 && (I.gh || I.vh))
         endpoint_head(L, Ln, I.E, S.x, g ? I.gh : nullptr, values ? I.vh : nullptr, threadIdx.x, blockDim.x);
 }
 
@@ -1165,7 +1461,10 @@ struct mh_ctx {
     int ngoals = 0;
     // device
     int device = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;      // the stream all work is ordered on
+    hipStream_t own_stream = nullptr;  // the context's own (mh_set_stream(NULL))
+    bool async = false;                // *_device entries return once enqueued
+    int iv_dbg_stop = 0;               // diagnostic: k_interval stops after phase n
     hipEvent_t ev[5] = {};         // stage boundaries (+ ev[4] after k_groups)
     char* dmem = nullptr;
     DevModel M{};
@@ -1174,8 +1473,19 @@ struct mh_ctx {
            *d_Yg = nullptr, *d_g = nullptr, *d_vals = nullptr, *d_C = nullptr, *d_grad = nullptr,
            *d_tpart = nullptr, *d_f = nullptr;
     TplEntry* d_tpl = nullptr;
-    uint32_t* d_tplp = nullptr;    // packed template (k_interval)
-    std::vector<uint32_t> tplp;
+    uint32_t* d_ctpl = nullptr;    // compiled template of the Jacobian lanes (k_interval)
+    std::vector<uint32_t> ctpl;
+    int* d_ctgen = nullptr;        // the entries it leaves to jac_entry (t0 / tf of defect rows)
+    std::vector<int> ctgen;
+    // k_role: per role (grid point of the interval) the entries it writes
+    // and their words compiled against the role's own-point LDS layout
+    std::vector<int> rl_e;
+    std::vector<uint32_t> rl_w;
+    int rl_off[4] = {0, 0, 0, 0}, rl_tail[2] = {0, 0};
+    int* d_rl_e = nullptr;
+    uint32_t* d_rl_w = nullptr;
+    bool use_roles = true;         // MOCOHIP_ROLES=0: k_interval for the Jacobian lanes
+    bool use_ctpl = true;          // MOCOHIP_CTPL=0: k_interval assembles through jac_entry
     float timings[4] = {0, 0, 0, 0};
     // task-decomposed back ends
     TaskSet ts_jac, ts_g, ts_probe;
@@ -1192,7 +1502,6 @@ struct mh_ctx {
     // and transcription fused in k_interval (LDS-resident raw outputs)
     bool use_interval[2] = {false, false};
     int nsimd = 1024;              // SIMDs of the device (4 per CU)
-    bool tables_lds = false;       // k_interval stages the packed template (MOCOHIP_TABLES=1)
     bool asm_grid_stride = false;  // k_transcribe_gs (MOCOHIP_ASM=gs) instead of k_transcribe
     bool quot = false;             // k_combine writes FD quotients (MOCOHIP_QUOT=1)
     int yq[2] = {0, 0};            // per lane configuration: Y of the last evaluation holds quotients
@@ -1205,7 +1514,7 @@ struct mh_ctx {
 // block writes through I.gh / I.vh when this shard owns it.
 inline Interval make_interval(const mh_ctx* c, double*& g, double*& v) {
     Interval I{c->scheme, c->interp, c->ib, c->rpi, c->nnz_int, c->NMB + c->NAR, c->NMB, c->NQ + c->NZ,
-               c->N, c->nnz_tail, c->ntail, c->npe, c->P, c->E, nullptr, nullptr};
+               c->N, c->nnz_tail, c->ntail, c->npe, c->P, c->E, nullptr, nullptr, c->iv_dbg_stop};
     if (c->ib == 0 && c->nep > 0) {
         I.gh = g;
         I.vh = v;
@@ -1286,33 +1595,52 @@ static void be_eval_tasks(mh_ctx* c, const double* x, int mode, double* Y) {
 }
 // LDS bytes of k_interval for one lane configuration (0: does not apply).
 template <class D>
-static size_t interval_lds(const mh_ctx* c, const Lanes& ln, const TaskSet& ts, bool tables) {
+static size_t interval_lds(const mh_ctx* c, const Lanes& ln, const TaskSet& ts) {
     const size_t npts = c->scheme == MH_HERMITE_SIMPSON ? 3 : 2;
-    const size_t tab = tables ? (size_t)(c->nnz_int + c->nnz_tail + 1) / 2 : 0;
-    return sizeof(double) * (npts * D::NO * ln.stride + 4 + npts * (size_t)(c->NS + c->NC + c->NDV) +
-                             npts * ((size_t)ts.dev.tdoubles + (size_t)ts.dev.nmass * D::NST) + tab);
+    return sizeof(double) * (npts * D::NO * ln.stride + CT_CONST + CT_NCONST +
+                             npts * (size_t)(c->NS + c->NC + c->NDV) +
+                             npts * ((size_t)ts.dev.tdoubles + (size_t)ts.dev.nmass * D::NST));
+}
+// LDS bytes of k_role (Jacobian lanes).
+template <class D>
+static size_t role_lds(const mh_ctx* c) {
+    const size_t R = c->scheme == MH_HERMITE_SIMPSON ? 3 : 2, NL = c->fd == MH_FD_CENTRAL ? 5 : 3;
+    const TaskSet& ts = c->ts_jac;
+    return sizeof(double) * ((size_t)D::NO * c->lanes_jac.stride + (R - 1) * D::NO * NL + CT_CONST + 2 +
+                             (size_t)ts.dev.tdoubles + (size_t)ts.dev.nmass * D::NST +
+                             R * (size_t)(c->NS + c->NC + c->NDV));
 }
 template <class D>
 static size_t be_interval_bytes(const mh_ctx* c, int mode) {
-    return interval_lds<D>(c, mode ? c->lanes_jac : c->lanes_g, mode ? c->ts_jac : c->ts_g, false);
+    if (mode == 1 && c->use_roles && role_lds<D>(c) <= kMaxLds) return role_lds<D>(c);
+    return interval_lds<D>(c, mode ? c->lanes_jac : c->lanes_g, mode ? c->ts_jac : c->ts_g);
 }
 template <class D>
 static void be_interval(mh_ctx* c, const double* x, int mode, double* g, double* v) {
     const Src S{x, c->d_grid, nullptr, c->G, c->k0};
     const Lanes& ln = mode ? c->lanes_jac : c->lanes_g;
     const TaskSet& ts = mode ? c->ts_jac : c->ts_g;
-    // stage the packed template too when it fits and MOCOHIP_TABLES=1
-    const size_t lds_tab = interval_lds<D>(c, ln, ts, true);
-    const int tables = c->tables_lds && lds_tab <= kMaxLds ? 1 : 0;
-    const size_t lds = tables ? lds_tab : interval_lds<D>(c, ln, ts, false);
+    const size_t lds = interval_lds<D>(c, ln, ts);
     if (lds > 65536)
         (void)hipFuncSetAttribute((const void*)k_interval<D>, hipFuncAttributeMaxDynamicSharedMemorySize,
                 (int)lds);
     Layout L{c->NS, c->NC, c->TQ, c->NO, c->NI, c->G, c->k0, c->nk, c->NDV, c->NACC, c->SO};
     const Interval I = make_interval(c, g, v);
+    if (mode == 1 && c->use_roles && role_lds<D>(c) <= kMaxLds) {
+        const size_t rl = role_lds<D>(c);
+        if (rl > 65536)
+            (void)hipFuncSetAttribute((const void*)k_role<D>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)rl);
+        const unsigned R = c->scheme == MH_HERMITE_SIMPSON ? 3 : 2;
+        RoleLists RL{c->d_rl_e, c->d_rl_w, {c->rl_off[0], c->rl_off[1], c->rl_off[2], c->rl_off[3]},
+                     c->rl_tail[0], c->rl_tail[1]};
+        hipLaunchKernelGGL(k_role<D>, dim3(R * (unsigned)(c->ie - c->ib)), dim3(512), rl, c->stream, c->M, S,
+                ln, ts.dev, L, I, c->d_tpl, RL, c->d_ctgen, (int)c->ctgen.size(), c->d_T, c->d_H, g, v);
+        return;
+    }
     const unsigned threads = v ? 1024u : 256u;
     hipLaunchKernelGGL(k_interval<D>, dim3((unsigned)(c->ie - c->ib)), dim3(threads), lds, c->stream, c->M,
-            S, ln, ts.dev, L, I, c->d_tpl, c->d_tplp, tables, c->d_T, c->d_H, g, v);
+            S, ln, ts.dev, L, I, c->d_tpl, (mode == 1 && c->use_ctpl) ? c->d_ctpl : nullptr, c->d_ctgen,
+            (int)c->ctgen.size(), c->d_T, c->d_H, g, v);
 }
 template <class D>
 static void be_integrand(mh_ctx* c, const double* x) {

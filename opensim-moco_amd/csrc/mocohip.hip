@@ -572,6 +572,111 @@ static bool path_entries_lead(const mh_ctx* c) {
     return true;
 }
 
+// The compiled template (core.hpp CT_*) of c->tpl for the Jacobian lane
+// layout: per entry the LDS offset of the quotient (or constant) it scales,
+// its coefficient and base -- the operations jac_entry performs for it.
+static bool compile_template(mh_ctx* c) {
+    const int NS = c->NS, NQ = c->TQ, NC = c->NC, NO = c->NO;
+    const int stride = c->fd == MH_FD_CENTRAL ? 2 * (c->NI + 2) + 1 : (c->NI + 2) + 1;
+    const int npts = c->scheme == MH_HERMITE_SIMPSON ? 3 : 2;
+    const uint32_t kconst = (uint32_t)(npts * NO * stride + CT_CONST);   // sK relative to sY
+    if ((size_t)kconst + CT_NCONST > CT_OFF) return false;
+    // LDS offset of dxdot[s] along direction dir at point pt (jac_entry's
+    // dxdot: exact 0 / 1 for qdot = u and implicit udot = w)
+    auto dx = [&](int pt, int s, int dir) -> uint32_t {
+        if (s < NQ) return kconst + (dir == 2 + NQ + s ? 1u : 0u);
+        if (c->NACC && s < 2 * NQ) return kconst + (dir == 2 + NS + NC + (s - NQ) ? 1u : 0u);
+        return (uint32_t)((pt * NO + s + c->SO) * stride + dir);
+    };
+    c->ctpl.clear();
+    for (const TplEntry& T : c->tpl) {
+        const int s = T.s, dir = T.dir, pt = T.pt;
+        const bool ident = dir == 2 + s;
+        uint32_t w;
+        switch (T.kind) {
+        case T_HERM_X:
+            if (pt == 1) w = ct_word(kconst, 0, ident ? 2 : 0);
+            else w = ct_word(dx(pt, s, dir), pt == 0 ? 1 : 2, ident ? 1 : 0);
+            break;
+        case T_SIMP_X:
+            if (pt == 2) w = ct_word(dx(pt, s, dir), 3, ident ? 2 : 0);
+            else if (pt == 0) w = ct_word(dx(pt, s, dir), 3, ident ? 3 : 0);
+            else w = ct_word(dx(pt, s, dir), 4, 0);
+            break;
+        case T_TRAP_X:
+            w = ct_word(dx(pt, s, dir), 5, ident ? (pt == 1 ? 2 : 3) : 0);
+            break;
+        case T_INTERP:
+            w = ct_word(kconst, 0, pt == 1 ? 2 : 1);
+            break;
+        case T_RES:
+            w = (uint32_t)((pt * NO + s) * stride + dir) | CT_RAW;
+            break;
+        case T_PATH:
+            w = CT_PATH;
+            break;
+        default:   // along t0 / tf (HERM_T, SIMP_T, TRAP_T)
+            w = CT_GEN;
+        }
+        c->ctpl.push_back(w);
+    }
+    c->ctgen.clear();
+    for (int e = 0; e < c->nnz_int + c->nnz_tail; ++e)
+        if (c->ctpl[e] & CT_GEN) c->ctgen.push_back(e);
+    // k_role lists: entry e goes to the role of its point, its word against
+    // that role's own-point layout (q at o * stride + dir)
+    const int R = npts, NL = c->fd == MH_FD_CENTRAL ? 5 : 3;
+    const uint32_t rconst = (uint32_t)(NO * stride + (R - 1) * NO * NL + CT_CONST);
+    auto rdx = [&](int s, int dir) -> uint32_t {
+        if (s < NQ) return rconst + (dir == 2 + NQ + s ? 1u : 0u);
+        if (c->NACC && s < 2 * NQ) return rconst + (dir == 2 + NS + NC + (s - NQ) ? 1u : 0u);
+        return (uint32_t)((s + c->SO) * stride + dir);
+    };
+    auto rword = [&](const TplEntry& T) -> uint32_t {
+        const int s = T.s, dir = T.dir, pt = T.pt;
+        const bool ident = dir == 2 + s;
+        switch (T.kind) {
+        case T_HERM_X:
+            if (pt == 1) return ct_word(rconst, 0, ident ? 2 : 0);
+            return ct_word(rdx(s, dir), pt == 0 ? 1 : 2, ident ? 1 : 0);
+        case T_SIMP_X:
+            if (pt == 2) return ct_word(rdx(s, dir), 3, ident ? 2 : 0);
+            if (pt == 0) return ct_word(rdx(s, dir), 3, ident ? 3 : 0);
+            return ct_word(rdx(s, dir), 4, 0);
+        case T_TRAP_X: return ct_word(rdx(s, dir), 5, ident ? (pt == 1 ? 2 : 3) : 0);
+        case T_INTERP: return ct_word(rconst, 0, pt == 1 ? 2 : 1);
+        case T_RES: return (uint32_t)(s * stride + dir) | CT_RAW;
+        default: return CT_GEN;
+        }
+    };
+    if ((size_t)rconst + 2 > CT_OFF) return false;
+    c->rl_e.clear();
+    c->rl_w.clear();
+    for (int r = 0; r < R; ++r) {
+        c->rl_off[r] = (int)c->rl_e.size();
+        for (int e = 0; e < c->nnz_int; ++e) {
+            const TplEntry& T = c->tpl[e];
+            if (T.kind == T_PATH || T.pt != r) continue;
+            const uint32_t w = rword(T);
+            if (w & CT_GEN) continue;   // t0 / tf columns: the time role's jac_entry loop
+            c->rl_e.push_back(e);
+            c->rl_w.push_back(w);
+        }
+    }
+    c->rl_off[R] = (int)c->rl_e.size();
+    for (int r = R + 1; r < 4; ++r) c->rl_off[r] = c->rl_off[R];
+    c->rl_tail[0] = (int)c->rl_e.size();
+    for (int e = c->nnz_int; e < c->nnz_int + c->nnz_tail; ++e) {
+        const TplEntry& T = c->tpl[e];
+        if (T.kind == T_PATH) continue;
+        if (T.pt != R - 1) return false;
+        c->rl_e.push_back(e);
+        c->rl_w.push_back(rword(T));
+    }
+    c->rl_tail[1] = (int)c->rl_e.size();
+    return true;
+}
+
 static int validate_and_layout(mh_ctx* c, const mh_problem* p, const mh_options* o,
         std::vector<int>& coord_body, std::vector<int>& act_state, std::vector<int>& ftn_state,
         std::vector<int>& mus_control, double& tau_act, double& tau_deact) {
@@ -897,16 +1002,13 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
                  o_pc = A.put(c->pc.data(), c->pc.size()),
                  o_ep = A.put(c->ep.data(), c->ep.size()),
                  o_eptpl = A.put(c->eptpl.data(), c->eptpl.size());
-    // packed template, padded to whole doubles (staged in LDS as doubles)
-    c->tplp.clear();
-    for (const TplEntry& e : c->tpl) {
-        c->tplp.push_back(tpl_pack(e));
-        const TplEntry u = tpl_unpack(c->tplp.back());
-        if (u.kind != e.kind || u.pt != e.pt || u.dir != e.dir || u.s != e.s || e.dir > 1023 || e.s < 0)
-            return set_err(MH_ERR_UNSUPPORTED, "Jacobian template entry does not pack into 32 bits");
-    }
-    if (c->tplp.size() % 2) c->tplp.push_back(0u);
-    const size_t o_tplp = A.put(c->tplp.data(), c->tplp.size());
+    // compiled template of the Jacobian lanes (k_interval), capacity of the
+    // block-dense template (sparsity detection only removes entries)
+    if (!compile_template(c.get())) return set_err(MH_ERR_UNSUPPORTED, "Jacobian template does not compile");
+    const size_t o_ctpl = A.put(c->ctpl.data(), c->ctpl.size());
+    const size_t o_ctgen = A.put(c->ctgen.data(), c->ctgen.size());
+    const size_t o_rl_e = A.put(c->rl_e.data(), c->rl_e.size());
+    const size_t o_rl_w = A.put(c->rl_w.data(), c->rl_w.size());
 
     const int nint = c->ie - c->ib;
     const int ND = c->NI + 2;
@@ -970,7 +1072,10 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     c->GS.gw = (const double*)(b + o_gw);
     c->d_grid = (double*)(b + o_grid); c->d_quad = (double*)(b + o_quad);
     c->d_tpl = (TplEntry*)(b + o_tpl);
-    c->d_tplp = (uint32_t*)(b + o_tplp);
+    c->d_ctpl = (uint32_t*)(b + o_ctpl);
+    c->d_ctgen = (int*)(b + o_ctgen);
+    c->d_rl_e = (int*)(b + o_rl_e);
+    c->d_rl_w = (uint32_t*)(b + o_rl_w);
     c->P = PathEqs{c->npc, (const mh_path_equation*)(b + o_pc), D.tabs, D.brk, D.coef, c->d_grid};
     c->E = EndpointEqs{c->nep, c->nnz_ep, 1 + c->NI, (const mh_endpoint_equation*)(b + o_ep),
                        (const TplEntry*)(b + o_eptpl)};
@@ -985,8 +1090,14 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
         c->d_T = (double*)(b + o_T);
         c->d_H = (double*)(b + o_H);
     }
-    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
+    c->stream = c->own_stream;
     {
+        // diagnostic (profiling the phases of k_interval; results are
+        // incomplete): MOCOHIP_IV_DEBUG_STOP=1 returns after staging, 2 after
+        // the combine
+        const char* ed = std::getenv("MOCOHIP_IV_DEBUG_STOP");
+        c->iv_dbg_stop = ed ? std::atoi(ed) : 0;
         // hipGraph replay of the stages: measured slower than direct launches
         // on ROCm 7.2 for this sequence (opt-in, MOCOHIP_GRAPHS=1)
         const char* eg = std::getenv("MOCOHIP_GRAPHS");
@@ -999,8 +1110,10 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
         // budget is exceeded (MOCOHIP_INTERVAL=0 forces the split path)
         const char* ei = std::getenv("MOCOHIP_INTERVAL");
         const bool allow = !(ei && std::strcmp(ei, "0") == 0);
-        const char* et = std::getenv("MOCOHIP_TABLES");
-        c->tables_lds = et && std::strcmp(et, "1") == 0;   // opt-in: measured slower
+        const char* ec = std::getenv("MOCOHIP_CTPL");
+        c->use_ctpl = !(ec && std::strcmp(ec, "0") == 0);
+        const char* er = std::getenv("MOCOHIP_ROLES");
+        c->use_roles = !(er && std::strcmp(er, "0") == 0);
         const char* ea = std::getenv("MOCOHIP_ASM");
         c->asm_grid_stride = ea && std::strcmp(ea, "gs") == 0;
         const char* ee = std::getenv("MOCOHIP_EVENTS");
@@ -1023,12 +1136,18 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
                         hipMemcpyHostToDevice));
             c->E.nnz = c->nnz_ep;
             c->nnz = c->nnz_ep + (int64_t)c->nnz_int * c->N + c->nnz_tail;
-            c->tplp.clear();
-            for (const TplEntry& e : c->tpl) c->tplp.push_back(tpl_pack(e));
-            if (c->tplp.size() % 2) c->tplp.push_back(0u);
+            if (!compile_template(c.get())) return set_err(MH_ERR_UNSUPPORTED, "Jacobian template does not compile");
             HIPCHK(hipMemcpy(c->d_tpl, c->tpl.data(), sizeof(TplEntry) * c->tpl.size(), hipMemcpyHostToDevice));
-            HIPCHK(hipMemcpy(c->d_tplp, c->tplp.data(), sizeof(uint32_t) * c->tplp.size(),
+            HIPCHK(hipMemcpy(c->d_ctpl, c->ctpl.data(), sizeof(uint32_t) * c->ctpl.size(),
                     hipMemcpyHostToDevice));
+            if (!c->ctgen.empty())
+                HIPCHK(hipMemcpy(c->d_ctgen, c->ctgen.data(), sizeof(int) * c->ctgen.size(),
+                        hipMemcpyHostToDevice));
+            if (!c->rl_e.empty()) {
+                HIPCHK(hipMemcpy(c->d_rl_e, c->rl_e.data(), sizeof(int) * c->rl_e.size(), hipMemcpyHostToDevice));
+                HIPCHK(hipMemcpy(c->d_rl_w, c->rl_w.data(), sizeof(uint32_t) * c->rl_w.size(),
+                        hipMemcpyHostToDevice));
+            }
             c->P.npc = c->npc;
         }
         for (int mode = 0; mode < 2; ++mode)
@@ -1045,7 +1164,10 @@ extern "C" void mh_destroy(mh_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);
-    if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->own_stream) {
+        (void)hipStreamSynchronize(c->own_stream);
+        (void)hipStreamDestroy(c->own_stream);
+    }
     if (c->dmem) (void)hipFree(c->dmem);
     if (c->probe_mem) (void)hipFree(c->probe_mem);
     for (auto& e : c->graphs) (void)hipGraphExecDestroy(e.exec);
@@ -1284,7 +1406,9 @@ static int run_cached(mh_ctx* c, int kind, const double* x, double* a, double* b
     return MH_OK;
 }
 
-static int finish(mh_ctx* c) {
+// async: the device entries return once their work is enqueued
+static int finish(mh_ctx* c, bool device_entry = false) {
+    if (device_entry && c->async && !c->timing) return MH_OK;
     if (!c->timing) {
         HIPCHK(hipStreamSynchronize(c->stream));
         return MH_OK;
@@ -1345,7 +1469,7 @@ extern "C" int mh_eval_g_device(mh_ctx* c, const double* x_dev, double* g_dev) {
     HIPCHK(hipSetDevice(c->device));
     int rc = run_cached(c, 0, x_dev, g_dev, nullptr);
     if (rc) return rc;
-    return finish(c);
+    return finish(c, true);
 }
 
 extern "C" int mh_eval_jac_g_device(mh_ctx* c, const double* x_dev, double* v_dev) {
@@ -1353,7 +1477,7 @@ extern "C" int mh_eval_jac_g_device(mh_ctx* c, const double* x_dev, double* v_de
     HIPCHK(hipSetDevice(c->device));
     int rc = run_cached(c, 1, x_dev, v_dev, nullptr);
     if (rc) return rc;
-    return finish(c);
+    return finish(c, true);
 }
 
 extern "C" int mh_eval_g_jac_g_device(mh_ctx* c, const double* x_dev, double* g_dev, double* v_dev) {
@@ -1361,7 +1485,7 @@ extern "C" int mh_eval_g_jac_g_device(mh_ctx* c, const double* x_dev, double* g_
     HIPCHK(hipSetDevice(c->device));
     int rc = run_cached(c, 2, x_dev, g_dev, v_dev);
     if (rc) return rc;
-    return finish(c);
+    return finish(c, true);
 }
 
 extern "C" int mh_eval_g_jac_g(mh_ctx* c, const double* x, double* g, double* values) {
@@ -1616,6 +1740,33 @@ extern "C" int mh_debug_jacobian_lanes(mh_ctx* c, const double* x, double* times
     return MH_OK;
 }
 
+extern "C" int mh_set_stream(mh_ctx* c, void* stream) {
+    if (!c) return set_err(MH_ERR_INVALID, "null argument");
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->own_stream;
+    if (s != c->stream) {
+        // work already enqueued on the previous stream completes first
+        HIPCHK(hipStreamSynchronize(c->stream));
+        for (auto& e : c->graphs) (void)hipGraphExecDestroy(e.exec);
+        c->graphs.clear();
+        c->stream = s;
+    }
+    return MH_OK;
+}
+
+extern "C" int mh_set_async(mh_ctx* c, int on) {
+    if (!c) return set_err(MH_ERR_INVALID, "null argument");
+    c->async = on != 0;
+    return MH_OK;
+}
+
+extern "C" int mh_synchronize(mh_ctx* c) {
+    if (!c) return set_err(MH_ERR_INVALID, "null argument");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return MH_OK;
+}
+
 extern "C" int mh_set_timing(mh_ctx* c, int on) {
     if (!c) return set_err(MH_ERR_INVALID, "null argument");
     c->timing = on != 0;
@@ -1657,7 +1808,8 @@ extern "C" int mh_get_backend_flags(const mh_ctx* c, char* flags, int32_t len) {
     std::string f = c->be->tasks ? "tasks" : (std::strncmp(c->be->name, "generic", 7) == 0 ? "generic" : "lane");
     f += c->use_interval[1] ? " interval" : " split";
     if (c->use_interval[0]) f += " interval-g";
-    if (c->tables_lds) f += " tables";
+    if (!c->use_ctpl) f += " no-ctpl";
+    if (c->use_roles && c->use_interval[1]) f += " roles";
     if (c->quot) f += " quot";
     if (c->asm_grid_stride) f += " asm-gs";
     std::strncpy(flags, f.c_str(), (size_t)len - 1);

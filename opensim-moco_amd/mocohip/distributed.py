@@ -1,21 +1,32 @@
-"""Mesh-interval sharding over ranks (one process per GPU).
+"""Mesh-interval sharding over ranks (one process per GPU) for ONE host IPOPT.
 
-The g rows and Jacobian nonzeros of mesh interval i are contiguous, and
-every interval has the same row count and the same nonzero count
-(CasOCTranscription.h:219-313). So rank r owns the
-intervals [N*r/W, N*(r+1)/W) and evaluates only those (mh_options
-interval_begin/interval_end). One all-gather of the fixed-size, padded
-segments rebuilds the full g and Jacobian values on every rank, which is
-what a single host IPOPT needs. The boundary grid point
-between two shards is evaluated by both ranks: recomputing it is cheaper
-than exchanging it.
+The g rows and Jacobian nonzeros of mesh interval i are contiguous, every
+interval has the same row and nonzero counts, the endpoint rows (the head)
+precede interval 0 and the final mesh point's rows (the tail) follow
+interval N-1 (CasOCTranscription.h:219-313).  So rank r owns
+the intervals [N*r/W, N*(r+1)/W) (mh_options interval_begin/interval_end),
+evaluates only those, and its results are ONE contiguous slice of g and one
+of the Jacobian values (mh_nlp_info row_begin/row_end, nnz_begin/nnz_end).
+The boundary grid point between two shards is evaluated by both ranks:
+recomputing it is cheaper than exchanging it.
 
-The same code runs over RCCL (backend "nccl", device tensors, bench.py) and
-over gloo on the CPU (tests/test_distributed.py).
+Reassembly for a single host IPOPT needs no device
+collective on g / J: every rank copies its slice straight into its offset of
+one host buffer shared by the node's ranks (``HostGather``: POSIX shared
+memory, page-locked with hipHostRegister so the copy is DMA over that GPU's
+own PCIe link).  The only collective on the data path is the broadcast of
+IPOPT's iterate x to every rank (RCCL over xGMI in bench.py, gloo on the CPU
+in tests/test_distributed.py); objective partials are one all-reduce of two
+doubles.
 """
 from __future__ import annotations
 
+import ctypes as C
+import mmap
+import os
 from typing import List, Tuple
+
+import numpy as np
 
 
 def interval_shard(num_intervals: int, rank: int, world: int) -> Tuple[int, int]:
@@ -29,54 +40,96 @@ def shard_counts(num_intervals: int, world: int) -> List[int]:
     return [e - b for b, e in (interval_shard(num_intervals, r, world) for r in range(world))]
 
 
-class ShardGather:
-    """Fixed-size segment buffers and their all-gather.
+_hip = None
 
-    Each rank writes its shard's g rows into ``gseg[:g_sizes[rank]]`` and its
-    Jacobian values into ``vseg[:v_sizes[rank]]``.
-    ``gather()`` all-gathers both. The results are padded per rank to the
-    largest shard; ``full_g()`` / ``full_values()`` return the unpadded full
-    vectors in the global row / nonzero order.
-    """
 
-    def __init__(self, num_intervals: int, rows_per_interval: int, nnz_per_interval: int,
-                 world: int, device, group=None, tail_rows: int = 0, tail_nnz: int = 0):
-        """``tail_rows`` / ``tail_nnz``: rows and nonzeros after the last
-        interval (implicit dynamics: the final grid point's residuals), owned
-        by the last rank (mh_nlp_info row_end / nnz_end)."""
-        import torch
-        self.N, self.rpi, self.nzi, self.world = num_intervals, rows_per_interval, nnz_per_interval, world
-        self.group = group
-        self.counts = shard_counts(num_intervals, world)
-        self.tail = (tail_rows, tail_nnz)
-        self.g_sizes = [c * rows_per_interval + (tail_rows if r == world - 1 else 0)
-                        for r, c in enumerate(self.counts)]
-        self.v_sizes = [c * nnz_per_interval + (tail_nnz if r == world - 1 else 0)
-                        for r, c in enumerate(self.counts)]
-        f64 = torch.float64
-        self.gseg = torch.zeros(max(self.g_sizes), dtype=f64, device=device)
-        self.vseg = torch.zeros(max(self.v_sizes), dtype=f64, device=device)
-        self.gall = torch.zeros(world * self.gseg.numel(), dtype=f64, device=device)
-        self.vall = torch.zeros(world * self.vseg.numel(), dtype=f64, device=device)
-        self._g_index = self._unpad_index(self.g_sizes, self.gseg.numel(), device)
-        self._v_index = self._unpad_index(self.v_sizes, self.vseg.numel(), device)
+def _hip_runtime():
+    """The HIP runtime libmocohip and torch share (for hipHostRegister /
+    hipMemcpyAsync on the shared buffer)."""
+    global _hip
+    if _hip is None:
+        _hip = C.CDLL("libamdhip64.so")
+        _hip.hipHostRegister.argtypes = [C.c_void_p, C.c_size_t, C.c_uint]
+        _hip.hipHostRegister.restype = C.c_int
+        _hip.hipHostUnregister.argtypes = [C.c_void_p]
+        _hip.hipHostUnregister.restype = C.c_int
+        _hip.hipMemcpyAsync.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p]
+        _hip.hipMemcpyAsync.restype = C.c_int
+    return _hip
 
-    def _unpad_index(self, sizes, seg: int, device):
-        import torch
-        parts = [torch.arange(r * seg, r * seg + n, device=device) for r, n in enumerate(sizes)]
-        return torch.cat(parts)
 
-    def gather(self):
-        import torch.distributed as dist
-        if self.world == 1:
-            self.gall.copy_(self.gseg)
-            self.vall.copy_(self.vseg)
-            return
-        dist.all_gather_into_tensor(self.gall, self.gseg, group=self.group)
-        dist.all_gather_into_tensor(self.vall, self.vseg, group=self.group)
+HIP_MEMCPY_DEVICE_TO_HOST = 2
 
+
+class HostGather:
+    """One node-wide host buffer [g (m doubles) | Jacobian values (nnz)] that
+    every rank fills with its shard's slice; the IPOPT rank reads the full
+    vectors from it.
+
+    ``name``: a tag unique to the job (rank 0 creates /dev/shm/<name>, the
+    others map it after ``barrier()``).  ``rows`` / ``nnz``: this rank's
+    [begin, end) ranges (mh_nlp_info).  ``pin``: page-lock the mapping for
+    device-to-host DMA (GPU runs)."""
+
+    def __init__(self, name: str, m: int, nnz: int, rows: Tuple[int, int], nz: Tuple[int, int],
+                 rank: int, barrier, pin: bool = False):
+        self.m, self.nnz = int(m), int(nnz)
+        self.rows, self.nz = (int(rows[0]), int(rows[1])), (int(nz[0]), int(nz[1]))
+        self.rank = rank
+        self.path = os.path.join("/dev/shm", name)
+        self.bytes = 8 * (self.m + self.nnz)
+        if rank == 0:
+            with open(self.path, "wb") as fh:
+                fh.truncate(self.bytes)
+        barrier()
+        fd = os.open(self.path, os.O_RDWR)
+        try:
+            self._mm = mmap.mmap(fd, self.bytes)
+        finally:
+            os.close(fd)
+        self.buf = np.frombuffer(self._mm, dtype=np.float64)
+        self.g = self.buf[:self.m]
+        self.values = self.buf[self.m:]
+        self._pinned = False
+        if pin:
+            rc = _hip_runtime().hipHostRegister(self.buf.ctypes.data, self.bytes, 0)
+            if rc != 0:
+                raise RuntimeError(f"hipHostRegister failed ({rc})")
+            self._pinned = True
+
+    # -- filling this rank's slice
+    def copy_from_host(self, g_slice, v_slice):
+        self.g[self.rows[0]:self.rows[1]] = g_slice
+        self.values[self.nz[0]:self.nz[1]] = v_slice
+
+    def copy_from_device_async(self, g_dev: int, v_dev: int, stream: int):
+        """hipMemcpyAsync of this rank's g / values slices (device pointers)
+        into the pinned shared buffer, ordered on ``stream``."""
+        hip = _hip_runtime()
+        dst_g = self.buf.ctypes.data + 8 * self.rows[0]
+        dst_v = self.buf.ctypes.data + 8 * (self.m + self.nz[0])
+        for dst, src, n in ((dst_g, g_dev, self.rows[1] - self.rows[0]),
+                            (dst_v, v_dev, self.nz[1] - self.nz[0])):
+            if n:
+                rc = hip.hipMemcpyAsync(dst, src, 8 * n, HIP_MEMCPY_DEVICE_TO_HOST, stream)
+                if rc != 0:
+                    raise RuntimeError(f"hipMemcpyAsync failed ({rc})")
+
+    # -- the IPOPT rank's view (after every rank's copy completed + barrier)
     def full_g(self):
-        return self.gall[self._g_index]
+        return self.g
 
     def full_values(self):
-        return self.vall[self._v_index]
+        return self.values
+
+    def close(self, unlink: bool = False):
+        if self._pinned:
+            _hip_runtime().hipHostUnregister(self.buf.ctypes.data)
+            self._pinned = False
+        self.g = self.values = self.buf = None
+        try:
+            self._mm.close()
+        except BufferError:
+            pass
+        if unlink and os.path.exists(self.path):
+            os.unlink(self.path)

@@ -348,6 +348,18 @@ class HipNLP(_NLPBase):
         self._check(self.lib.mh_get_backend_flags(self.ctx, buf, 256))
         return buf.value.decode()
 
+    def set_stream(self, stream: int | None):
+        """Order this context's work on a HIP stream (e.g.
+        torch.cuda.current_stream().cuda_stream); None = its own stream."""
+        self._check(self.lib.mh_set_stream(self.ctx, C.c_void_p(stream or 0)))
+
+    def set_async(self, on: bool):
+        """*_device entries return once enqueued (mh_set_async)."""
+        self._check(self.lib.mh_set_async(self.ctx, int(bool(on))))
+
+    def synchronize(self):
+        self._check(self.lib.mh_synchronize(self.ctx))
+
     def set_timing(self, on: bool):
         """Record stage events on every evaluation (mh_set_timing)."""
         self._check(self.lib.mh_set_timing(self.ctx, int(bool(on))))
@@ -382,16 +394,20 @@ class OracleNLP(_NLPBase):
         return g
 
     def eval_g(self, x, new_x=True):
+        """This context's rows (all of g unless it is a shard)."""
         x = np.ascontiguousarray(x, float)
-        g = np.empty(max(self.m, 1))
+        nr = self.row_end - self.row_begin
+        g = np.empty(max(nr, 1))
         self._check(self.lib.orc_eval_g(self.ctx, abi.dptr(x), abi.dptr(g)))
-        return g[:self.m]
+        return g[:nr]
 
     def eval_jac_g(self, x, new_x=True):
+        """This context's nonzeros (all of them unless it is a shard)."""
         x = np.ascontiguousarray(x, float)
-        v = np.empty(max(self.nnz, 1))
+        nz = self.nnz_end - self.nnz_begin
+        v = np.empty(max(nz, 1))
         self._check(self.lib.orc_eval_jac_g(self.ctx, abi.dptr(x), abi.dptr(v)))
-        return v[:self.nnz]
+        return v[:nz]
 
 
 def _oracle_assemble(self, x, times, Y):

@@ -270,6 +270,11 @@ struct orc_ctx {
     double* quad;   /* G quadrature coefficients */
     int64_t n, m, nnz;
     int32_t *iRow, *jCol;
+    /* mesh-interval shard [ib, ie) (mh_options interval_begin/end): its grid
+     * points gk0..gk1 are the only ones evaluated, and g / values receive its
+     * rows [row_begin, row_end) / nonzeros [nnz_begin, nnz_end) */
+    int ib, ie, gk0, gk1;
+    int64_t row_begin, row_end, nnz_begin, nnz_end;
     int fd; double h;
 };
 
@@ -766,6 +771,18 @@ int orc_create(const mh_problem* p, const mh_options* o, orc_ctx** out) {
     endpoint_rows(c, emit_fill, &e);
     for (int i = 0; i < c->N; ++i) interval_rows(c, i, c->NEP + (int64_t)i * rpi, emit_fill, &e);
     tail_rows(c, c->NEP + (int64_t)c->N * rpi, emit_fill, &e);
+    /* shard (the head belongs to the first shard, the tail to the last) */
+    c->ib = o->interval_begin > 0 ? o->interval_begin : 0;
+    c->ie = o->interval_end > 0 && o->interval_end < c->N ? o->interval_end : c->N;
+    if (c->ib >= c->ie) { orc_destroy(c); return fail(MH_ERR_INVALID, "empty interval shard"); }
+    c->gk0 = mesh_point(c, c->ib);
+    c->gk1 = mesh_point(c, c->ie);
+    c->row_begin = c->ib == 0 ? 0 : c->NEP + (int64_t)c->ib * rpi;
+    c->row_end = c->NEP + (int64_t)c->ie * rpi + (c->ie == c->N ? ntail(c) : 0);
+    c->nnz_begin = 0;
+    while (c->nnz_begin < c->nnz && c->iRow[c->nnz_begin] < c->row_begin) ++c->nnz_begin;
+    c->nnz_end = c->nnz_begin;
+    while (c->nnz_end < c->nnz && c->iRow[c->nnz_end] < c->row_end) ++c->nnz_end;
     *out = c;
     return MH_OK;
 }
@@ -786,7 +803,8 @@ int orc_get_nlp_info(const orc_ctx* c, mh_nlp_info* info) {
     memset(info, 0, sizeof *info);
     info->n = c->n; info->m = c->m; info->nnz_jac_g = c->nnz; info->nnz_h_lag = 0;
     info->num_grid_points = c->G; info->num_states = c->NS; info->num_controls = c->NC;
-    info->row_begin = 0; info->row_end = c->m; info->nnz_begin = 0; info->nnz_end = c->nnz;
+    info->row_begin = c->row_begin; info->row_end = c->row_end;
+    info->nnz_begin = c->nnz_begin; info->nnz_end = c->nnz_end;
     return MH_OK;
 }
 
@@ -1596,7 +1614,7 @@ static void all_xdot(orc_ctx* c, const double* x, const double* times, double* x
         double* ct = st + NS;
         double* y = ct + NC + c->NDV;
 #pragma omp for schedule(static)
-        for (int k = 0; k < c->G; ++k) {
+        for (int k = c->gk0; k <= c->gk1; ++k) {
             gather_point(c, x, k, st, ct);
             double* o = xd + (int64_t)k * NS;
             int TQ = c->TQ;
@@ -1790,14 +1808,25 @@ static void g_assemble(const orc_ctx* c, const double* x, const double* times, c
     for (int o = 0; o < NR; ++o) g[(int64_t)c->N * rpi + c->NPC + o] = res[(int64_t)(c->G - 1) * NR + o];
 }
 
+/* A shard context evaluates its grid points only and returns its rows /
+ * nonzeros: the full-layout assembly goes through a scratch vector. */
+static int sharded(const orc_ctx* c) { return c->ib != 0 || c->ie != c->N; }
+
 int orc_eval_g(orc_ctx* c, const double* x, double* g) {
     int NS = c->NS, NR = nres(c);
     double* times = (double*)malloc(sizeof(double) * (size_t)c->G);
-    double* xd = (double*)malloc(sizeof(double) * (size_t)c->G * (size_t)NS);
-    double* res = (double*)malloc(sizeof(double) * ((size_t)c->G * (size_t)NR + 1));
+    double* xd = (double*)calloc((size_t)c->G * (size_t)NS + 1, sizeof(double));
+    double* res = (double*)calloc((size_t)c->G * (size_t)NR + 1, sizeof(double));
     times_of(c, x, times);
     all_xdot(c, x, times, xd, res);
-    g_assemble(c, x, times, xd, res, g);
+    if (sharded(c)) {
+        double* full = (double*)calloc((size_t)c->m + 1, sizeof(double));
+        g_assemble(c, x, times, xd, res, full);
+        memcpy(g, full + c->row_begin, sizeof(double) * (size_t)(c->row_end - c->row_begin));
+        free(full);
+    } else {
+        g_assemble(c, x, times, xd, res, g);
+    }
     free(times);
     free(xd);
     free(res);
@@ -1822,7 +1851,7 @@ static void fd_blocks(orc_ctx* c, const double* x, const double* times, double* 
         double* ym = yp + NO;
         double* y0 = ym + NO;
 #pragma omp for schedule(static)
-        for (int k = 0; k < c->G; ++k) {
+        for (int k = c->gk0; k <= c->gk1; ++k) {
             gather_point(c, x, k, in, in + NS);
             double t = times[k];
             if (c->fd != MH_FD_CENTRAL) eval_dae_point(c, &w, t, in, in + NS, y0);
@@ -1871,7 +1900,7 @@ static void path_blocks(const orc_ctx* c, const double* x, const double* times, 
     int NS = c->NS, NP = c->NP, NPC = c->NPC, ND = NP + 2;
     double h = c->h;
     double* in = (double*)malloc(sizeof(double) * (size_t)(NP + 1));
-    for (int i = 0; i <= c->N; ++i) {
+    for (int i = c->ib; i <= c->ie; ++i) {
         int k = mesh_point(c, i);
         gather_point(c, x, k, in, in + NS);
         double t = times[k];
@@ -2083,15 +2112,22 @@ static void jac_assemble(const orc_ctx* c, const double* x, const double* times,
 int orc_eval_jac_g(orc_ctx* c, const double* x, double* values) {
     int NS = c->NS, NO = nout(c), ND = c->NP + 2, NR = nres(c), NPC = c->NPC;
     double* times = (double*)malloc(sizeof(double) * (size_t)c->G);
-    double* xd = (double*)malloc(sizeof(double) * (size_t)c->G * (size_t)NS);
-    double* D = (double*)malloc(sizeof(double) * (size_t)c->G * (size_t)ND * (size_t)NO);
-    double* res = (double*)malloc(sizeof(double) * ((size_t)c->G * (size_t)NR + 1));
-    double* Dp = (double*)malloc(sizeof(double) * ((size_t)(c->N + 1) * (size_t)ND * (size_t)NPC + 1));
+    double* xd = (double*)calloc((size_t)c->G * (size_t)NS + 1, sizeof(double));
+    double* D = (double*)calloc((size_t)c->G * (size_t)ND * (size_t)NO + 1, sizeof(double));
+    double* res = (double*)calloc((size_t)c->G * (size_t)NR + 1, sizeof(double));
+    double* Dp = (double*)calloc((size_t)(c->N + 1) * (size_t)ND * (size_t)NPC + 1, sizeof(double));
     times_of(c, x, times);
     all_xdot(c, x, times, xd, res);
     fd_blocks(c, x, times, D);
     if (NPC) path_blocks(c, x, times, Dp);
-    jac_assemble(c, x, times, xd, D, Dp, values);
+    if (sharded(c)) {
+        double* full = (double*)calloc((size_t)c->nnz + 1, sizeof(double));
+        jac_assemble(c, x, times, xd, D, Dp, full);
+        memcpy(values, full + c->nnz_begin, sizeof(double) * (size_t)(c->nnz_end - c->nnz_begin));
+        free(full);
+    } else {
+        jac_assemble(c, x, times, xd, D, Dp, values);
+    }
     free(Dp);
     free(times);
     free(xd);

@@ -1,16 +1,21 @@
-"""Mesh-interval sharding and the all-gather reassembly (mocohip.distributed)
-on the CPU: world_size 2 and 3 over gloo.
+"""Mesh-interval sharding for one host IPOPT (mocohip.distributed) on the
+CPU: world size 2 and 3 over gloo.
 
-Each rank takes its shard's g rows and Jacobian values from the CPU oracle's
-full evaluation. That is what its shard context writes on the GPU, because
-the rows and nonzeros of a shard are a contiguous slice
-(tests/test_gpu_parity.py::test_shards_reassemble_bit_exact checks that on
-the device). The rank then puts the slice in the padded segment and
-all-gathers it. The reassembled vectors must equal the full evaluation
-bit for bit. bench.py runs the same ShardGather over RCCL.
+Each rank creates a SHARD context of the CPU oracle (mh_options
+interval_begin/interval_end: it evaluates only its grid points and returns
+its own rows / nonzeros), receives IPOPT's iterate x by broadcast from rank 0
+(the one collective on the data path), and copies its slices into its offset
+of the node-wide HostGather buffer.  Rank 0 -- the IPOPT rank -- then holds g
+and the Jacobian values of the whole NLP; they must equal an unsharded
+evaluation bit for bit.  The device shard contexts' slices are checked
+against the unsharded device evaluation in
+tests/test_gpu_parity.py::test_shards_reassemble_bit_exact; bench.py
+--multi mesh runs the same HostGather with hipMemcpyAsync over each GPU's
+PCIe link and RCCL for the broadcast.
 """
 import os
 import socket
+import uuid
 
 import numpy as np
 import pytest
@@ -19,7 +24,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from mocohip import configs
-from mocohip.distributed import ShardGather, interval_shard, shard_counts
+from mocohip.distributed import HostGather, interval_shard, shard_counts
 from mocohip.solver import OracleNLP
 
 
@@ -41,52 +46,58 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, case, N, out):
+CASES = {"pendulum": lambda N: configs.double_pendulum(N),
+         "gait": lambda N: configs.gait10dof18musc(N),
+         "pendulum_implicit": lambda N: configs.double_pendulum(N, dynamics="implicit"),
+         "gait_pathcon": lambda N: configs.gait10dof18musc(N, control_bounds=True),
+         "bound_implicit": lambda N: configs.pendulum_control_bound(N, "both", dynamics="implicit"),
+         "inverse": lambda N: configs.gait10dof18musc_inverse(N, sparsity="none")}
+
+
+def _worker(rank, world, port, case, N, tag, out):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    hg = None
     try:
-        st = {"pendulum": lambda: configs.double_pendulum(N),
-              "gait": lambda: configs.gait10dof18musc(N),
-              "pendulum_implicit": lambda: configs.double_pendulum(N, dynamics="implicit"),
-              "gait_pathcon": lambda: configs.gait10dof18musc(N, control_bounds=True),
-              "bound_implicit": lambda: configs.pendulum_control_bound(N, "both",
-                                                                       dynamics="implicit")}[case]()
+        st = CASES[case](N)
         rep = st.problem.create_rep()
-        ref = OracleNLP(rep, st.solver.options(), threads=1)
-        x = ref.random_iterate(np.random.default_rng(3).uniform(-1, 1, ref.n))
-        g, J = ref.eval_g(x), ref.eval_jac_g(x)
-        # the final mesh point's path rows and (implicit dynamics) the final
-        # point's residual rows follow the last interval (tail), owned by the
-        # last rank
-        tail_rows = ref.tail_rows
-        ir, _ = ref.jac_structure()
-        tail_nnz = int((ir >= ref.m - tail_rows).sum())
-        rpi, nzi = (ref.m - tail_rows) // N, (ref.nnz - tail_nnz) // N
-        sg = ShardGather(N, rpi, nzi, world, "cpu", tail_rows=tail_rows, tail_nnz=tail_nnz)
         ib, ie = interval_shard(N, rank, world)
-        rows = (ie - ib) * rpi + (tail_rows if ie == N else 0)
-        nz = (ie - ib) * nzi + (tail_nnz if ie == N else 0)
-        assert rows == sg.g_sizes[rank] and nz == sg.v_sizes[rank]
-        sg.gseg.zero_()
-        sg.vseg.zero_()
-        sg.gseg[:rows] = torch.from_numpy(g[ib * rpi:ib * rpi + rows])
-        sg.vseg[:nz] = torch.from_numpy(J[ib * nzi:ib * nzi + nz])
-        sg.gather()
-        ok = (np.array_equal(sg.full_g().numpy(), g)
-              and np.array_equal(sg.full_values().numpy(), J))
+        shard = OracleNLP(rep, st.solver.options(ib, ie), threads=1)
+        # IPOPT's iterate, on rank 0, broadcast to every rank
+        x = torch.zeros(shard.n, dtype=torch.float64)
+        if rank == 0:
+            x[:] = torch.from_numpy(shard.random_iterate(np.random.default_rng(3).uniform(-1, 1, shard.n)))
+        dist.broadcast(x, src=0)
+        xn = x.numpy()
+        hg = HostGather(tag, shard.m, shard.nnz, (shard.row_begin, shard.row_end),
+                        (shard.nnz_begin, shard.nnz_end), rank, dist.barrier)
+        g, J = shard.eval_g(xn), shard.eval_jac_g(xn)
+        assert len(g) == shard.row_end - shard.row_begin and len(J) == shard.nnz_end - shard.nnz_begin
+        hg.copy_from_host(g, J)
+        dist.barrier()
+        ok = True
+        if rank == 0:
+            full = OracleNLP(rep, st.solver.options(), threads=1)
+            ok = (np.array_equal(hg.full_g(), full.eval_g(xn))
+                  and np.array_equal(hg.full_values(), full.eval_jac_g(xn)))
         out[rank] = int(ok)
+        dist.barrier()
     finally:
+        if hg is not None:
+            hg.close(unlink=rank == 0)
         dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("case,N,world", [("pendulum", 7, 2), ("pendulum", 10, 3), ("gait", 5, 2),
                                           ("pendulum_implicit", 7, 3), ("gait_pathcon", 4, 2),
-                                          ("bound_implicit", 9, 3)])
-def test_shard_gather_reassembles_full_vectors(case, N, world):
+                                          ("bound_implicit", 9, 3), ("inverse", 4, 2), ("inverse", 5, 3)])
+def test_shard_contexts_reassemble_on_the_ipopt_host(case, N, world):
     ctx = mp.get_context("spawn")
     out = ctx.Array("i", [0] * world)
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, case, N, out)) for r in range(world)]
+    tag = f"mocohip_test_{uuid.uuid4().hex[:12]}"
+    procs = [ctx.Process(target=_worker, args=(r, world, port, case, N, tag, out))
+             for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:

@@ -241,7 +241,8 @@ def _pair(name, backend="auto", tasks=None, env=None):
     rep = st.problem.create_rep()
     opts = st.solver.options()
     saved = {k: os.environ.pop(k, None) for k in ("MOCOHIP_BACKEND", "MOCOHIP_TASKS", "MOCOHIP_INTERVAL",
-                                                  "MOCOHIP_ASM", "MOCOHIP_QUOT", "MOCOHIP_TABLES")}
+                                                  "MOCOHIP_ASM", "MOCOHIP_QUOT", "MOCOHIP_CTPL",
+                                                  "MOCOHIP_ROLES")}
     if backend != "auto":
         os.environ["MOCOHIP_BACKEND"] = backend
     if tasks:
@@ -521,6 +522,35 @@ def test_device_pointer_entry_points():
     assert np.array_equal(vd.cpu().numpy(), gpu.eval_jac_g(x))
 
 
+def test_async_calls_on_a_caller_stream():
+    """mh_set_stream + mh_set_async: device calls enqueue on the caller's
+    (torch) stream after its producer of x, return before completion, and
+    give the blocking calls' results once the stream is synchronized."""
+    import torch
+    gpu, _, _ = _pair("gait_rigid_forward")
+    x = physiological_iterate(gpu, 4)
+    g_ref, J_ref = gpu.eval_g(x), gpu.eval_jac_g(x)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        xd = torch.zeros(gpu.n, dtype=torch.float64, device="cuda")
+        gd = torch.empty(gpu.m, dtype=torch.float64, device="cuda")
+        vd = torch.empty(gpu.nnz, dtype=torch.float64, device="cuda")
+        gpu.set_stream(s.cuda_stream)
+        gpu.set_async(True)
+        for _ in range(3):
+            xd.copy_(torch.from_numpy(x), non_blocking=False)   # producer on s
+            gpu.eval_g_device(xd.data_ptr(), gd.data_ptr())
+            gpu.eval_jac_g_device(xd.data_ptr(), vd.data_ptr())
+        s.synchronize()
+        assert np.array_equal(gd.cpu().numpy(), g_ref) and np.array_equal(vd.cpu().numpy(), J_ref)
+        gpu.eval_g_jac_g_device(xd.data_ptr(), gd.data_ptr(), vd.data_ptr())
+        gpu.synchronize()
+        assert np.array_equal(gd.cpu().numpy(), g_ref) and np.array_equal(vd.cpu().numpy(), J_ref)
+    gpu.set_async(False)
+    gpu.set_stream(None)
+    assert np.array_equal(gpu.eval_jac_g(x), J_ref)
+
+
 def test_repeatable_bitwise():
     gpu, _, _ = _pair("gait_rigid_forward")
     x = gpu.random_iterate(np.random.default_rng(3).uniform(-1, 1, gpu.n))
@@ -572,16 +602,21 @@ def test_pruned_tasks_bit_identical(name):
                                   "double_pendulum_implicit_hs", "double_pendulum_implicit_trap",
                                   "gait_rigid_implicit", "gait_rigid_pathcon",
                                   "pendulum_bound_equality_trap", "pendulum_bound_both_implicit",
-                                  "gait_rigid_sparse_random", "gait_implicit_pathcon_sparse"])
+                                  "gait_rigid_sparse_random", "gait_implicit_pathcon_sparse",
+                                  "gait_inverse_random", "double_pendulum_nointerp",
+                                  "gait_rigid_nointerp_trap"])
 @pytest.mark.parametrize("variant", [{"MOCOHIP_INTERVAL": "0"},
                                      {"MOCOHIP_INTERVAL": "0", "MOCOHIP_ASM": "gs"},
                                      {"MOCOHIP_INTERVAL": "0", "MOCOHIP_QUOT": "1"},
-                                     {"MOCOHIP_TABLES": "1"}])
+                                     {"MOCOHIP_CTPL": "0"},
+                                     {"MOCOHIP_ROLES": "0"}])
 def test_kernel_variants_bit_identical(name, variant):
-    """The default k_interval (combine + transcription per mesh interval,
-    raw outputs in LDS) writes exactly what the split path writes through
-    HBM: k_combine + k_transcribe (chunked or grid-stride), with raw lane
-    values or with finite-difference quotients in Y."""
+    """The default fused path (k_role for the Jacobian lanes: one workgroup
+    per mesh interval and grid point; k_interval for g) writes exactly what
+    k_interval writes for the Jacobian (MOCOHIP_ROLES=0), what k_interval
+    writes through jac_entry (MOCOHIP_CTPL=0) and what the split path writes
+    through HBM: k_combine + k_transcribe (chunked or grid-stride), with raw
+    lane values or with finite-difference quotients in Y."""
     gpu, _, _ = _pair(name)
     split, _, _ = _pair(name, env=variant)
     for _, x in _iterates(gpu):
