@@ -56,8 +56,8 @@ HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md (spec; 6.29 TB/s measured copy)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=1000)
     ap.add_argument("--intervals", type=int, default=200)
     ap.add_argument("--fd", default="forward")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=8.0)
@@ -229,7 +229,12 @@ def roofline(cx, nlp, steps, args, mode):
     _, el = measure(cx, step, args, w=2)
     nlp.set_timing(False)
     J = np.array(rec["jac"])          # [whole, DAE stage, transcription stage, k_groups] ms
-    dae_ms, tr_ms = float(np.median(J[:, 1])), float(np.median(J[:, 2]))
+    ev_dae_ms, ev_tr_ms = float(np.median(J[:, 1])), float(np.median(J[:, 2]))
+    # per-launch kernel durations: each stage of eval_jac_g alone, launched
+    # back to back (the queue ahead of the GPU), between HIP events on the
+    # context stream (mh_debug_time_stages) -- the figure a rocprofv3 kernel
+    # trace of the same launches gives, plus the inter-kernel gap
+    dae_ms, tr_ms = nlp.time_stages(steps[3][0], kind=1, reps=max(50, args.steps))
     G, ND = nlp.G, nlp.NS + nlp.NC + 2
     n_dae = G * (ND + 1) if args.fd != "central" else G * (2 * ND + 1)
     be_name, f_dae, mhash = nlp.backend()
@@ -267,7 +272,10 @@ def roofline(cx, nlp, steps, args, mode):
     roof = dict(main)
     roof["other_kernel"] = other
     roof.update({"backend": be_name, "model_hash": f"0x{mhash:016x}",
-                 "instrumented_ms_per_step": round(1e3 * el / args.steps, 4)})
+                 "backend_flags": nlp.backend_flags(),
+                 "timing": "mh_debug_time_stages: back-to-back launches of one stage between HIP events",
+                 "instrumented_ms_per_step": round(1e3 * el / args.steps, 4),
+                 "in_call_stage_ms": [round(ev_dae_ms, 5), round(ev_tr_ms, 5)]})
     if rec["g"]:
         Gt = np.array(rec["g"])
         roof["eval_g_stage_ms"] = [round(float(np.median(Gt[:, i])), 5) for i in range(4)]

@@ -492,6 +492,7 @@ struct Interval {
     double* gh;
     double* vh;
     int dbg_stop;    // diagnostic timing build only: return after phase n (0: full)
+    int pf;          // k_interval prefetches its first IV_PF assembly words per thread
     // Every interval opens with its mesh point's path rows.  The interval
     // N-1 also owns the tail (flattenConstraints, CasOCTranscription.h:
     // 286-308): the final mesh point's path rows, then the final grid
@@ -839,6 +840,7 @@ __device__ __forceinline__ void interval_span(const Interval& I, int i, int& k_f
 // HBM and one kernel less per evaluation.  Launched when the LDS budget
 // allows (interval_lds), otherwise the split path runs.
 constexpr int IV_UNROLL = 4;
+constexpr int IV_PF = 12;   // k_interval: assembly words per thread prefetched before the quotients
 // Compiled Jacobian template (k_interval's assembly): one word per template
 // entry of the Jacobian lane layout.  A value is base + coef * q, with q one
 // double in the interval's LDS (a finite-difference quotient of sY, or the
@@ -887,6 +889,7 @@ __global__ void __launch_bounds__(1024) k_interval(DevModel M, Src S, Lanes Ln, 
     // the interval's points are consecutive local grid points: their T (and
     // H) slabs are one contiguous run each
     const int kl0 = k_first - S.k0;
+    if (I.dbg_stop == 7) return;   // diagnostic: the launch floor
     if (nt > 0) stage_lds<16>(sT, T + (long)kl0 * nt, npts * nt);
     if (nh > 0) stage_lds<8>(sH, H + (long)kl0 * nh, npts * nh);
     stage_lds<1>(sXs, S.x + 2 + (long)k_first * L.NS, npts * L.NS);
@@ -894,6 +897,7 @@ __global__ void __launch_bounds__(1024) k_interval(DevModel M, Src S, Lanes Ln, 
     if (L.NDV > 0)
         stage_lds<1>(sXd, S.x + 2 + (long)(L.NS + L.NC) * L.G + (long)k_first * L.NDV, npts * L.NDV);
     const double t0 = S.x[0], tf = S.x[1];
+    if (threadIdx.x < 2) sK[threadIdx.x] = threadIdx.x ? 1.0 : 0.0;
     __syncthreads();
     if (I.dbg_stop == 1) return;
     for (int w = threadIdx.x; w < npts * Ln.stride; w += blockDim.x) {
@@ -907,6 +911,24 @@ __global__ void __launch_bounds__(1024) k_interval(DevModel M, Src S, Lanes Ln, 
         lds_double* Yp = lds(sY + p * ny + r);
 #pragma unroll
         for (int o = 0; o < D::NO; ++o) Yp[o * Ln.stride] = out[o];
+    }
+    // the compiled words of this thread's first IV_PF assembly entries,
+    // loaded now: their latency hides behind the quotients and the g rows
+    // (on CDNA a wave's loads and stores share one counter -- loaded after
+    // the g rows' stores, they would wait for those to complete)
+    const int ne_iv = values ? I.entries(i) : 0;
+    uint32_t pw[IV_PF];
+#pragma unroll
+    for (int u = 0; u < IV_PF; ++u) {
+        const int e = threadIdx.x + u * blockDim.x;
+        pw[u] = I.pf && ctpl && e < ne_iv ? ctpl[e] : CT_GEN;
+    }
+    // likewise the template entry of this thread's first t0 / tf entry
+    int eg0 = -1;
+    TplEntry tg0{};
+    if (I.pf && ctpl && values && (int)threadIdx.x < nctgen) {
+        eg0 = ctgen[threadIdx.x];
+        tg0 = tpl[eg0];
     }
     __syncthreads();
     // finite-difference quotients in place (CasADi FiniteDiff formulas), once
@@ -966,8 +988,6 @@ __global__ void __launch_bounds__(1024) k_interval(DevModel M, Src S, Lanes Ln, 
         // the tail) are written by their own loop below
         if (ctpl) {
 #pragma clang fp contract(off)
-            if (threadIdx.x < 2) sK[threadIdx.x] = threadIdx.x ? 1.0 : 0.0;
-            __syncthreads();
             const lds_double* q0 = lds(sY);
             // coefficient / base of a word, selected in registers
             const double c1 = -C.h8, c2 = C.h8, c3 = -C.h6, c4 = -C.h6 * 4.0, c5 = -C.hh;
@@ -980,6 +1000,10 @@ __global__ void __launch_bounds__(1024) k_interval(DevModel M, Src S, Lanes Ln, 
             // the bulk: one LDS value, a product and a sum per entry; the
             // t0 / tf columns of the defect rows (CT_GEN) and the path
             // entries are written by the loops below
+#pragma unroll
+            for (int u = 0; u < IV_PF; ++u)
+                if (!(pw[u] & (CT_GEN | CT_PATH))) vi[e + u * B] = value(pw[u], q0[pw[u] & CT_OFF]);
+            if (I.pf) e += IV_PF * B;
             for (; e + (IV_UNROLL - 1) * B < ne; e += IV_UNROLL * B) {
                 uint32_t w[IV_UNROLL];
                 double q[IV_UNROLL];
@@ -995,7 +1019,8 @@ __global__ void __launch_bounds__(1024) k_interval(DevModel M, Src S, Lanes Ln, 
                 const uint32_t wu = ctpl[e];
                 if (!(wu & (CT_GEN | CT_PATH))) vi[e] = value(wu, q0[wu & CT_OFF]);
             }
-            for (int j = threadIdx.x; j < nctgen; j += B) {
+            if (eg0 >= 0) vi[eg0] = jac_entry<false>(L, Ln, I.P, S.x, YV, tg0, k_first, C);
+            for (int j = threadIdx.x + (I.pf ? B : 0); j < nctgen; j += B) {
                 const int eg = ctgen[j];
                 vi[eg] = jac_entry<false>(L, Ln, I.P, S.x, YV, tpl[eg], k_first, C);
             }
@@ -1036,23 +1061,30 @@ __global__ void __launch_bounds__(1024) k_interval(DevModel M, Src S, Lanes Ln, 
 // quotients, and writes the Jacobian entries of the interval that read that
 // point (the point's columns of every defect row, its residual and path
 // rows).  The entries that couple the points -- the t0 / tf columns of the
-// defect rows -- and the defect / interpolation rows of g belong to the
-// "time role" (the midpoint; trapezoidal: the first point), which also
-// combines the few lanes it needs of the other points (t0, tf and the
-// unperturbed lane) straight from their group results in global memory.
-// Against k_interval: a third of the staging, combine and stores per block
-// and three times the blocks (several per CU, overlapping their phases);
-// the same arithmetic, bit for bit (test_kernel_variants_bit_identical).
+// defect rows -- and the defect / interpolation rows of g need, of every
+// point, only the t0 / tf quotients and the unperturbed outputs: each block
+// publishes those (3 x NO doubles) to the interval's exchange slot and
+// k_couple, launched next on the stream, writes them.  (Handing them to the
+// interval's last-arriving block in the same launch needs an agent-scope
+// release per block; on gfx950, whose XCDs' L2s are not coherent, that is an
+// L2 write-back per block -- measured 9x slower than the extra launch.)
+// Against k_interval: a third of the staging, combine and stores per block,
+// three times the blocks (several per CU, overlapping their phases) and no
+// idle waves at a 1024-thread barrier; the same arithmetic, bit for bit
+// (test_kernel_variants_bit_identical, MOCOHIP_ROLES=0).
 // ------------------------------------------------------------------------
-struct RowR {   // a row of lanes of one point; r == full_base -> its base lane
+struct RowX {   // a point's exchanged row: lanes 0 / 1 (t0 / tf quotients), full_base -> 2
     const lds_double* p;
-    int full_base, base;
-    __device__ __forceinline__ double operator[](int r) const { return p[r == full_base ? base : r]; }
+    int full_base;
+    __device__ __forceinline__ double operator[](int r) const { return p[r == full_base ? 2 : r]; }
 };
+// The interval's grid points as k_role sees them: OWN = true -- only the
+// block's own point, all lanes (row ignores k); OWN = false -- every point,
+// the exchanged columns [R][NO][XCH_W].
+template <bool OWN>
 struct YR {
-    const lds_double* Y[3];
-    int stride[3], base[3];
-    int full_base, NO, kf, q;
+    const lds_double* Y;
+    int stride, full_base, NO, kf, q;
     const lds_double* times;
     const lds_double* sxs;
     const lds_double* sxc;
@@ -1062,9 +1094,9 @@ struct YR {
     __device__ __forceinline__ double xc(int k, int j) const { return sxc[(k - kf) * NC + j]; }
     __device__ __forceinline__ double xd(int k, int j) const { return sxd[(k - kf) * NDV + j]; }
     __device__ __forceinline__ double t(int k) const { return times[k - kf]; }
-    __device__ __forceinline__ RowR row(int k, int o) const {
-        const int p = k - kf;
-        return RowR{Y[p] + o * stride[p], full_base, base[p]};
+    __device__ __forceinline__ auto row(int k, int o) const {
+        if constexpr (OWN) return Y + o * stride;
+        else return RowX{Y + ((k - kf) * NO + o) * stride, full_base};
     }
 };
 // Per role: the (entry, compiled word) lists (own-point LDS offsets), and the
@@ -1074,20 +1106,31 @@ struct RoleLists {
     const uint32_t* __restrict__ w;
     int off[4];        // role r: [off[r], off[r + 1])
     int tail0, tail1;  // the tail's entries
+    int couple;        // 1: the time role writes the coupling rows / entries; 0: k_couple does
 };
-// Lanes of a neighbor point the time role combines: t0, tf, (central: t0-,
-// tf-), unperturbed.
+// Exchanged columns of a point's rows: t0 quotient, tf quotient, unperturbed
+// output ([point][NO][XCH_W]; k_couple's input in global memory, the time
+// role's in LDS).
+constexpr int XCH_W = 3;
+constexpr int NB_MAX = 5;   // lanes of a neighbor point the time role combines (central)
+constexpr int ROLE_PF = 16; // assembly entries per thread whose words are prefetched
 __device__ __forceinline__ int nb_lanes(const Lanes& Ln) { return Ln.fd == MH_FD_CENTRAL ? 5 : 3; }
-__device__ __forceinline__ int nb_role(const Lanes& Ln, int j) {
+// lane of neighbor column j: t0, tf, (central: t0-, tf-), unperturbed
+__device__ __forceinline__ int nb_lane(const Lanes& Ln, int j) {
     const int NL = nb_lanes(Ln);
     return j == NL - 1 ? Ln.base : (j < 2 ? j : Ln.ND + (j - 2));
 }
+// LDS doubles before k_role's constants (sK): own rows, neighbor lanes,
+// exchanged columns, times.
+__host__ __device__ __forceinline__ int role_kconst(int NO, int S, int R) {
+    return NO * S + (R - 1) * NO * NB_MAX + R * NO * XCH_W + CT_CONST;
+}
 
 template <class D>
-__global__ void __launch_bounds__(512) k_role(DevModel M, Src S, Lanes Ln, Tasks TK, Layout L,
-        Interval I, const TplEntry* __restrict__ tpl, RoleLists RL, const int* __restrict__ ctgen, int nctgen,
-        const double* __restrict__ T, const double* __restrict__ H, double* __restrict__ g,
-        double* __restrict__ values) {
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k_role(DevModel M, Src S, Lanes Ln, Tasks TK, Layout L,
+        Interval I, const TplEntry* __restrict__ tpl, RoleLists RL, double* __restrict__ xch,
+        const int* __restrict__ ctgen, int nctgen, const double* __restrict__ T, const double* __restrict__ H,
+        double* __restrict__ g, double* __restrict__ values) {
 #pragma clang fp contract(off)
     extern __shared__ double smem[];
     const bool hs = I.scheme == MH_HERMITE_SIMPSON;
@@ -1096,11 +1139,13 @@ __global__ void __launch_bounds__(512) k_role(DevModel M, Src S, Lanes Ln, Tasks
     const int i = I.ib + il;
     int k_first, k_last;
     interval_span(I, i, k_first, k_last);
-    const int S_ = Ln.stride, NO = D::NO, NL = nb_lanes(Ln);
+    const int S_ = Ln.stride, NO = D::NO, NL = nb_lanes(Ln), B = blockDim.x;
+    const bool tr = RL.couple && role == TR;   // this block writes the coupling rows / entries
     const int nt = TK.tdoubles, nh = TK.nmass * D::NST;
     double* sY = smem;                          // own point [NO][S]
-    double* sYn = sY + NO * S_;                 // neighbors [R - 1][NO][NL] (time role)
-    double* sTimes = sYn + (R - 1) * NO * NL;   // [R] (+ pad)
+    double* sYn = sY + NO * S_;                 // neighbor lanes [R - 1][NO][NB_MAX] (time role)
+    double* sYx = sYn + (R - 1) * NO * NB_MAX;  // exchanged columns [R][NO][XCH_W]
+    double* sTimes = sYx + R * NO * XCH_W;      // [R] (+ pad)
     double* sK = sTimes + CT_CONST;             // 0.0, 1.0
     double* sT = sK + 2;                        // own [nt]
     double* sH = sT + nt;                       // own [nh]
@@ -1117,32 +1162,35 @@ __global__ void __launch_bounds__(512) k_role(DevModel M, Src S, Lanes Ln, Tasks
         stage_lds<1>(sXd, S.x + 2 + (long)(L.NS + L.NC) * L.G + (long)k_first * L.NDV, R * L.NDV);
     if (threadIdx.x < 2) sK[threadIdx.x] = threadIdx.x ? 1.0 : 0.0;
     const double t0 = S.x[0], tf = S.x[1];
-    if (threadIdx.x < R) {   // every role's formulas use the interval's base times
+    if (threadIdx.x < R) {   // every block's formulas use the interval's base times
         int pi;
         double st;
         sTimes[threadIdx.x] = lane_time(Ln, S.grid[k_first + threadIdx.x], t0, tf, Ln.base, pi, st);
     }
     __syncthreads();
-    // own lanes from LDS; the time role's neighbor lanes from global memory
-    const int nnb = role == TR ? (R - 1) * NL : 0;
-    for (int w = threadIdx.x; w < S_ + nnb; w += blockDim.x) {
+    if (I.dbg_stop == 1) return;
+    // own lanes: combine the point's group results from LDS; the time role
+    // also the neighbor points' t0 / tf / unperturbed lanes, from theirs in
+    // global memory (few lanes, on threads of their own)
+    const int nnb = tr ? (R - 1) * NL : 0;
+    for (int w = threadIdx.x; w < S_ + nnb; w += B) {
         int p = role, r = w;
-        double* Yd;
+        lds_double* Yp;
         int ys;
         if (w < S_) {
-            Yd = sY + r;
+            Yp = lds(sY + r);
             ys = S_;
         } else {
             const int q = (w - S_) / NL, j = (w - S_) - q * NL;
             p = q < TR ? q : q + 1;
-            r = nb_role(Ln, j);
-            Yd = sYn + q * NO * NL + j;
-            ys = NL;
+            r = nb_lane(Ln, j);
+            Yp = lds(sYn + q * NO * NB_MAX + j);
+            ys = NB_MAX;
         }
         LaneInL<D> in{lds(sXs + p * L.NS), lds(sXc + p * L.NC), lds(sXd + p * L.NDV), -1, 0.0};
         const double t = lane_time(Ln, S.grid[k_first + p], t0, tf, r, in.pi, in.step);
         double out[D::NO];
-        if (p == role) {
+        if (w < S_) {
             const TaskLoadLds<D> TL{lds(sT), lds(sH), TK.jd, r};
             D::combine(M, t, in, TL, out);
         } else {
@@ -1150,30 +1198,41 @@ __global__ void __launch_bounds__(512) k_role(DevModel M, Src S, Lanes Ln, Tasks
             const TaskLoadGlobal<D> TG{T + (long)kl * nt, H + (long)kl * nh, TK.jd, r};
             D::combine(M, t, in, TG, out);
         }
-        lds_double* Yp = lds(Yd);
 #pragma unroll
         for (int o = 0; o < D::NO; ++o) Yp[o * ys] = out[o];
     }
-    __syncthreads();
-    // finite-difference quotients in place: own point, one output row of
-    // lanes per wave; the neighbors' t0 / tf lanes
-    {
-        const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nwave = blockDim.x >> 6;
-        const double h = Ln.h, h2 = 2.0 * Ln.h;
-        for (int o = wave; o < NO; o += nwave) {
-            lds_double* y = lds(sY + o * S_);
-            const double yb = y[Ln.base];
-            for (int d = lane; d < Ln.ND; d += 64) {
-                double q;
-                if (Ln.fd == MH_FD_CENTRAL) q = (y[d] - y[Ln.ND + d]) / h2;
-                else if (Ln.fd == MH_FD_FORWARD) q = (y[d] - yb) / h;
-                else q = (yb - y[d]) / h;
-                y[d] = q;
-            }
+    // the assembly's compiled words: prefetched now, consumed after the quotients
+    const int ra = role == 0 ? RL.off[0] : role == 1 ? RL.off[1] : RL.off[2];
+    const int rb = role == 0 ? RL.off[1] : role == 1 ? RL.off[2] : RL.off[3];
+    uint32_t pw[ROLE_PF];
+    int pe[ROLE_PF];
+    if (values) {
+#pragma unroll
+        for (int u = 0; u < ROLE_PF; ++u) {
+            const int e = ra + threadIdx.x + u * B;
+            pw[u] = e < rb ? RL.w[e] : 0u;
+            pe[u] = e < rb ? RL.e[e] : -1;
         }
-        for (int w = threadIdx.x; w < (role == TR ? (R - 1) * NO * 2 : 0); w += blockDim.x) {
+    }
+    __syncthreads();
+    if (I.dbg_stop == 2) return;
+    // finite-difference quotients in place (own: every direction; neighbors:
+    // t0 / tf), then the exchanged columns
+    {
+        const double h = Ln.h, h2 = 2.0 * Ln.h;
+        const int nq = NO * Ln.ND;
+        for (int w = threadIdx.x; w < nq; w += B) {
+            const int o = w / Ln.ND, d = w - o * Ln.ND;
+            lds_double* y = lds(sY + o * S_);
+            double q;
+            if (Ln.fd == MH_FD_CENTRAL) q = (y[d] - y[Ln.ND + d]) / h2;
+            else if (Ln.fd == MH_FD_FORWARD) q = (y[d] - y[Ln.base]) / h;
+            else q = (y[Ln.base] - y[d]) / h;
+            y[d] = q;
+        }
+        for (int w = threadIdx.x; w < (tr ? (R - 1) * NO * 2 : 0); w += B) {
             const int qo = w >> 1, d = w & 1;
-            lds_double* y = lds(sYn + qo * NL);
+            lds_double* y = lds(sYn + qo * NB_MAX);
             double q;
             if (Ln.fd == MH_FD_CENTRAL) q = (y[d] - y[2 + d]) / h2;
             else if (Ln.fd == MH_FD_FORWARD) q = (y[d] - y[NL - 1]) / h;
@@ -1182,42 +1241,47 @@ __global__ void __launch_bounds__(512) k_role(DevModel M, Src S, Lanes Ln, Tasks
         }
         __syncthreads();
     }
-    YR YV;
-    YV.full_base = Ln.base;
-    YV.NO = NO;
-    YV.kf = k_first;
-    YV.q = 1;
-    YV.times = lds(sTimes);
-    YV.sxs = lds(sXs);
-    YV.sxc = lds(sXc);
-    YV.sxd = lds(sXd);
-    YV.NS = L.NS;
-    YV.NC = L.NC;
-    YV.NDV = L.NDV;
-    for (int p = 0, q = 0; p < 3; ++p) {
-        if (p == role) { YV.Y[p] = lds(sY); YV.stride[p] = S_; YV.base[p] = Ln.base; }
-        else if (p < R) { YV.Y[p] = lds(sYn + (q++) * NO * NL); YV.stride[p] = NL; YV.base[p] = NL - 1; }
-        else { YV.Y[p] = lds(sY); YV.stride[p] = S_; YV.base[p] = Ln.base; }
+    if (RL.couple) {
+        if (tr)
+            for (int w = threadIdx.x; w < R * NO * XCH_W; w += B) {
+                const int p = w / (NO * XCH_W), rem = w - p * NO * XCH_W;
+                const int o = rem / XCH_W, j = rem - o * XCH_W;
+                if (p == role) {
+                    sYx[w] = sY[o * S_ + (j < 2 ? j : Ln.base)];
+                } else {
+                    const int q = p < role ? p : p - 1;
+                    sYx[w] = sYn[(q * NO + o) * NB_MAX + (j < 2 ? j : NL - 1)];
+                }
+            }
+    } else {
+        // publish this point's columns for k_couple
+        double* xo = xch + ((long)il * R + role) * NO * XCH_W;
+        for (int w = threadIdx.x; w < NO * XCH_W; w += B) {
+            const int o = w / XCH_W, j = w - o * XCH_W;
+            xo[w] = sY[o * S_ + (j < 2 ? j : Ln.base)];
+        }
     }
-    const int B = blockDim.x;
+    if (I.dbg_stop == 3) return;
+    const YR<true> YV{lds(sY), S_, Ln.base, NO, k_first, 1, lds(sTimes), lds(sXs), lds(sXc), lds(sXd),
+                      L.NS, L.NC, L.NDV};
     const int npres = hs ? 2 : 1;
-    if (g) {
-        // this role's rows: path rows (role 0), its point's residual rows,
-        // defect / interpolation rows (time role), the tail (last role)
-        double* gi = g + (long)il * I.rpi;
-        const int npc = I.P.npc;
+    const int npc = I.P.npc;
+    double* gi = g ? g + (long)il * I.rpi : nullptr;
+    // this point's rows of g: path rows (first point), its residual rows, the
+    // tail (last point of the last interval)
+    if (g)
         for (int r = threadIdx.x; r < I.rows(i); r += B) {
             int owner;
             if (r >= I.rpi) owner = R - 1;
             else if (r < npc) owner = 0;
             else if (r < npc + npres * I.nres) owner = (r - npc) / I.nres;
-            else owner = TR;
+            else owner = -1;
             if (owner == role) gi[r] = defect_row(L, I, Ln, S.x, YV, i, r);
         }
-    }
+    if (I.dbg_stop == 4) return;
+    const IvC C = iv_const(YV.t(k_last) - YV.t(k_first), S.grid[k_last] - S.grid[k_first]);
+    double* vi = values ? values + (long)il * I.nnz_int : nullptr;
     if (values) {
-        const IvC C = iv_const(YV.t(k_last) - YV.t(k_first), S.grid[k_last] - S.grid[k_first]);
-        double* vi = values + (long)il * I.nnz_int;
         const lds_double* q0 = lds(sY);
         const double c1 = -C.h8, c2 = C.h8, c3 = -C.h6, c4 = -C.h6 * 4.0, c5 = -C.hh;
         auto value = [&](uint32_t wu, double q) {
@@ -1226,33 +1290,20 @@ __global__ void __launch_bounds__(512) k_role(DevModel M, Src S, Lanes Ln, Tasks
             const double base = bs == 1 ? -0.5 : bs == 2 ? 1.0 : bs == 3 ? -1.0 : 0.0;
             return (wu & CT_RAW) ? q : base + coef * q;
         };
-        auto run = [&](int a, int b) {
-            int e = a + threadIdx.x;
-            for (; e + (IV_UNROLL - 1) * B < b; e += IV_UNROLL * B) {
-                uint32_t w[IV_UNROLL];
-                int ee[IV_UNROLL];
-                double q[IV_UNROLL];
 #pragma unroll
-                for (int u = 0; u < IV_UNROLL; ++u) { w[u] = RL.w[e + u * B]; ee[u] = RL.e[e + u * B]; }
-#pragma unroll
-                for (int u = 0; u < IV_UNROLL; ++u) q[u] = q0[w[u] & CT_OFF];
-#pragma unroll
-                for (int u = 0; u < IV_UNROLL; ++u) vi[ee[u]] = value(w[u], q[u]);
-            }
-            for (; e < b; e += B) {
+        for (int u = 0; u < ROLE_PF; ++u)
+            if (pe[u] >= 0) vi[pe[u]] = value(pw[u], q0[pw[u] & CT_OFF]);
+        for (int e = ra + ROLE_PF * B + threadIdx.x; e < rb; e += B) {
+            const uint32_t wu = RL.w[e];
+            vi[RL.e[e]] = value(wu, q0[wu & CT_OFF]);
+        }
+        if (i == I.N - 1 && role == R - 1)
+            for (int e = RL.tail0 + threadIdx.x; e < RL.tail1; e += B) {
                 const uint32_t wu = RL.w[e];
                 vi[RL.e[e]] = value(wu, q0[wu & CT_OFF]);
             }
-        };
-        run(RL.off[role], RL.off[role + 1]);
-        if (i == I.N - 1 && role == R - 1) run(RL.tail0, RL.tail1);
-        if (role == TR)
-            for (int j = threadIdx.x; j < nctgen; j += B) {
-                const int eg = ctgen[j];
-                vi[eg] = jac_entry<false>(L, Ln, I.P, S.x, YV, tpl[eg], k_first, C);
-            }
-        // path-constraint entries at the mesh point (role 0) and, in the
-        // tail, at the final mesh point (last role of the last interval)
+        // path-constraint entries at the mesh point (first point) and, in the
+        // tail, at the final mesh point (last point of the last interval)
         if (I.npe > 0 && (role == 0 || (role == R - 1 && i == I.N - 1))) {
             const int npe = I.npe;
             for (int w = threadIdx.x; w < npe; w += B) {
@@ -1263,6 +1314,67 @@ __global__ void __launch_bounds__(512) k_role(DevModel M, Src S, Lanes Ln, Tasks
     }
     if (i == 0 && role == 0 && (I.gh || I.vh))
         endpoint_head(L, Ln, I.E, S.x, g ? I.gh : nullptr, values ? I.vh : nullptr, threadIdx.x, blockDim.x);
+    if (tr) {
+        // the coupling rows of g and t0 / tf entries of the defect rows
+        __syncthreads();
+        const YR<false> YA{lds(sYx), XCH_W, Ln.base, NO, k_first, 1, lds(sTimes), lds(sXs), lds(sXc), lds(sXd),
+                           L.NS, L.NC, L.NDV};
+        if (g)
+            for (int r = npc + npres * I.nres + threadIdx.x; r < I.rpi; r += B)
+                gi[r] = defect_row(L, I, Ln, S.x, YA, i, r);
+        if (values)
+            for (int j = threadIdx.x; j < nctgen; j += B) {
+                const int eg = ctgen[j];
+                vi[eg] = jac_entry<false>(L, Ln, I.P, S.x, YA, tpl[eg], k_first, C);
+            }
+    }
+}
+
+// The coupling rows of g (defects, interpolation) and the t0 / tf entries of
+// the defect rows, per mesh interval from k_role's exchange.
+template <class D>
+__global__ void __launch_bounds__(256) k_couple(Src S, Lanes Ln, Layout L, Interval I,
+        const TplEntry* __restrict__ tpl, const int* __restrict__ ctgen, int nctgen,
+        const double* __restrict__ xch, double* __restrict__ g, double* __restrict__ values) {
+#pragma clang fp contract(off)
+    extern __shared__ double smem[];
+    const bool hs = I.scheme == MH_HERMITE_SIMPSON;
+    const int R = hs ? 3 : 2, NO = D::NO, B = blockDim.x;
+    const int il = blockIdx.x, i = I.ib + il;
+    int k_first, k_last;
+    interval_span(I, i, k_first, k_last);
+    double* sYx = smem;                         // [R][NO][XCH_W]
+    double* sTimes = sYx + R * NO * XCH_W;      // [R]
+    double* sXs = sTimes + 4;                   // [R][NS], [R][NC], [R][NDV]
+    double* sXc = sXs + R * L.NS;
+    double* sXd = sXc + R * L.NC;
+    stage_lds<1>(sYx, xch + (long)il * R * NO * XCH_W, R * NO * XCH_W);
+    stage_lds<1>(sXs, S.x + 2 + (long)k_first * L.NS, R * L.NS);
+    if (L.NC > 0) stage_lds<1>(sXc, S.x + 2 + (long)L.NS * L.G + (long)k_first * L.NC, R * L.NC);
+    if (L.NDV > 0)
+        stage_lds<1>(sXd, S.x + 2 + (long)(L.NS + L.NC) * L.G + (long)k_first * L.NDV, R * L.NDV);
+    if (threadIdx.x < R) {
+        int pi;
+        double st;
+        sTimes[threadIdx.x] = lane_time(Ln, S.grid[k_first + threadIdx.x], S.x[0], S.x[1], Ln.base, pi, st);
+    }
+    __syncthreads();
+    const YR<false> YA{lds(sYx), XCH_W, Ln.base, NO, k_first, 1, lds(sTimes), lds(sXs), lds(sXc), lds(sXd),
+                       L.NS, L.NC, L.NDV};
+    const int npres = hs ? 2 : 1;
+    if (g) {
+        double* gi = g + (long)il * I.rpi;
+        for (int r = I.P.npc + npres * I.nres + threadIdx.x; r < I.rpi; r += B)
+            gi[r] = defect_row(L, I, Ln, S.x, YA, i, r);
+    }
+    if (values) {
+        const IvC C = iv_const(YA.t(k_last) - YA.t(k_first), S.grid[k_last] - S.grid[k_first]);
+        double* vi = values + (long)il * I.nnz_int;
+        for (int j = threadIdx.x; j < nctgen; j += B) {
+            const int eg = ctgen[j];
+            vi[eg] = jac_entry<false>(L, Ln, I.P, S.x, YA, tpl[eg], k_first, C);
+        }
+    }
 }
 
 // ---- objective -------------------------------------------------------------
@@ -1465,6 +1577,7 @@ struct mh_ctx {
     hipStream_t own_stream = nullptr;  // the context's own (mh_set_stream(NULL))
     bool async = false;                // *_device entries return once enqueued
     int iv_dbg_stop = 0;               // diagnostic: k_interval stops after phase n
+    int iv_pf = 1;                     // MOCOHIP_IV_PF=0: no assembly-word prefetch (A/B)
     hipEvent_t ev[5] = {};         // stage boundaries (+ ev[4] after k_groups)
     char* dmem = nullptr;
     DevModel M{};
@@ -1484,7 +1597,10 @@ struct mh_ctx {
     int rl_off[4] = {0, 0, 0, 0}, rl_tail[2] = {0, 0};
     int* d_rl_e = nullptr;
     uint32_t* d_rl_w = nullptr;
-    bool use_roles = true;         // MOCOHIP_ROLES=0: k_interval for the Jacobian lanes
+    double* d_xch = nullptr;       // k_role -> k_couple exchange [interval][point][NO][3]
+    bool use_roles = false;        // MOCOHIP_ROLES=1: k_role (+ k_couple) for the Jacobian lanes
+    int role_threads = 256;        // k_role workgroup size (MOCOHIP_ROLE_THREADS: 64..512)
+    bool role_couple = true;       // coupling in k_role's time role (MOCOHIP_ROLE_COUPLE=0: k_couple)
     bool use_ctpl = true;          // MOCOHIP_CTPL=0: k_interval assembles through jac_entry
     float timings[4] = {0, 0, 0, 0};
     // task-decomposed back ends
@@ -1514,7 +1630,7 @@ struct mh_ctx {
 // block writes through I.gh / I.vh when this shard owns it.
 inline Interval make_interval(const mh_ctx* c, double*& g, double*& v) {
     Interval I{c->scheme, c->interp, c->ib, c->rpi, c->nnz_int, c->NMB + c->NAR, c->NMB, c->NQ + c->NZ,
-               c->N, c->nnz_tail, c->ntail, c->npe, c->P, c->E, nullptr, nullptr, c->iv_dbg_stop};
+               c->N, c->nnz_tail, c->ntail, c->npe, c->P, c->E, nullptr, nullptr, c->iv_dbg_stop, c->iv_pf};
     if (c->ib == 0 && c->nep > 0) {
         I.gh = g;
         I.vh = v;
@@ -1604,9 +1720,9 @@ static size_t interval_lds(const mh_ctx* c, const Lanes& ln, const TaskSet& ts) 
 // LDS bytes of k_role (Jacobian lanes).
 template <class D>
 static size_t role_lds(const mh_ctx* c) {
-    const size_t R = c->scheme == MH_HERMITE_SIMPSON ? 3 : 2, NL = c->fd == MH_FD_CENTRAL ? 5 : 3;
+    const size_t R = c->scheme == MH_HERMITE_SIMPSON ? 3 : 2;
     const TaskSet& ts = c->ts_jac;
-    return sizeof(double) * ((size_t)D::NO * c->lanes_jac.stride + (R - 1) * D::NO * NL + CT_CONST + 2 +
+    return sizeof(double) * ((size_t)role_kconst(D::NO, c->lanes_jac.stride, (int)R) + 2 +
                              (size_t)ts.dev.tdoubles + (size_t)ts.dev.nmass * D::NST +
                              R * (size_t)(c->NS + c->NC + c->NDV));
 }
@@ -1620,23 +1736,30 @@ static void be_interval(mh_ctx* c, const double* x, int mode, double* g, double*
     const Src S{x, c->d_grid, nullptr, c->G, c->k0};
     const Lanes& ln = mode ? c->lanes_jac : c->lanes_g;
     const TaskSet& ts = mode ? c->ts_jac : c->ts_g;
-    const size_t lds = interval_lds<D>(c, ln, ts);
-    if (lds > 65536)
-        (void)hipFuncSetAttribute((const void*)k_interval<D>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                (int)lds);
     Layout L{c->NS, c->NC, c->TQ, c->NO, c->NI, c->G, c->k0, c->nk, c->NDV, c->NACC, c->SO};
     const Interval I = make_interval(c, g, v);
+    // (a failed hipFuncSetAttribute would surface as the launch's error:
+    // only the launched kernel's attribute is set, and only when it fits)
     if (mode == 1 && c->use_roles && role_lds<D>(c) <= kMaxLds) {
         const size_t rl = role_lds<D>(c);
         if (rl > 65536)
             (void)hipFuncSetAttribute((const void*)k_role<D>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)rl);
         const unsigned R = c->scheme == MH_HERMITE_SIMPSON ? 3 : 2;
         RoleLists RL{c->d_rl_e, c->d_rl_w, {c->rl_off[0], c->rl_off[1], c->rl_off[2], c->rl_off[3]},
-                     c->rl_tail[0], c->rl_tail[1]};
-        hipLaunchKernelGGL(k_role<D>, dim3(R * (unsigned)(c->ie - c->ib)), dim3(512), rl, c->stream, c->M, S,
-                ln, ts.dev, L, I, c->d_tpl, RL, c->d_ctgen, (int)c->ctgen.size(), c->d_T, c->d_H, g, v);
+                     c->rl_tail[0], c->rl_tail[1], c->role_couple ? 1 : 0};
+        const unsigned nint = (unsigned)(c->ie - c->ib);
+        hipLaunchKernelGGL(k_role<D>, dim3(R * nint), dim3((unsigned)c->role_threads), rl, c->stream, c->M, S,
+                ln, ts.dev, L, I, c->d_tpl, RL, c->d_xch, c->d_ctgen, (int)c->ctgen.size(), c->d_T, c->d_H, g, v);
+        if (c->role_couple) return;
+        const size_t cl = sizeof(double) * (R * (size_t)D::NO * XCH_W + 4 + R * (size_t)(c->NS + c->NC + c->NDV));
+        hipLaunchKernelGGL(k_couple<D>, dim3(nint), dim3(256), cl, c->stream, S, ln, L, I, c->d_tpl,
+                c->d_ctgen, (int)c->ctgen.size(), c->d_xch, g, v);
         return;
     }
+    const size_t lds = interval_lds<D>(c, ln, ts);
+    if (lds > 65536)
+        (void)hipFuncSetAttribute((const void*)k_interval<D>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                (int)lds);
     const unsigned threads = v ? 1024u : 256u;
     hipLaunchKernelGGL(k_interval<D>, dim3((unsigned)(c->ie - c->ib)), dim3(threads), lds, c->stream, c->M,
             S, ln, ts.dev, L, I, c->d_tpl, (mode == 1 && c->use_ctpl) ? c->d_ctpl : nullptr, c->d_ctgen,

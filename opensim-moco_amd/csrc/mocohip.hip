@@ -625,8 +625,8 @@ static bool compile_template(mh_ctx* c) {
         if (c->ctpl[e] & CT_GEN) c->ctgen.push_back(e);
     // k_role lists: entry e goes to the role of its point, its word against
     // that role's own-point layout (q at o * stride + dir)
-    const int R = npts, NL = c->fd == MH_FD_CENTRAL ? 5 : 3;
-    const uint32_t rconst = (uint32_t)(NO * stride + (R - 1) * NO * NL + CT_CONST);
+    const int R = npts;
+    const uint32_t rconst = (uint32_t)role_kconst(NO, stride, R);
     auto rdx = [&](int s, int dir) -> uint32_t {
         if (s < NQ) return rconst + (dir == 2 + NQ + s ? 1u : 0u);
         if (c->NACC && s < 2 * NQ) return rconst + (dir == 2 + NS + NC + (s - NQ) ? 1u : 0u);
@@ -1025,6 +1025,9 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     const size_t o_grad = A.reserve(sizeof(double) * c->n);
     const size_t o_tpart = A.reserve(sizeof(double) * 2 * (size_t)c->G);
     const size_t o_f = A.reserve(sizeof(double) * 4);
+    const int npts_iv = c->scheme == MH_HERMITE_SIMPSON ? 3 : 2;
+    const size_t o_xch = A.reserve(sizeof(double) * (size_t)std::max(nint, 1) * npts_iv * std::max(1, c->NO) * XCH_W);
+
     TaskOffsets to_jac{}, to_g{};
     size_t o_T = 0, o_H = 0;
     const TaskInfo* ti = backend_tasks(c->be);
@@ -1084,6 +1087,7 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     c->d_Yg = (double*)(b + o_Yg); c->d_g = (double*)(b + o_g); c->d_vals = (double*)(b + o_vals);
     c->d_C = (double*)(b + o_C); c->d_grad = (double*)(b + o_grad); c->d_tpart = (double*)(b + o_tpart);
     c->d_f = (double*)(b + o_f);
+    c->d_xch = (double*)(b + o_xch);
     if (ti) {
         bind_taskset(b, to_jac, c->ts_jac);
         bind_taskset(b, to_g, c->ts_g);
@@ -1098,6 +1102,8 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
         // the combine
         const char* ed = std::getenv("MOCOHIP_IV_DEBUG_STOP");
         c->iv_dbg_stop = ed ? std::atoi(ed) : 0;
+        const char* ef = std::getenv("MOCOHIP_IV_PF");
+        c->iv_pf = ef && std::strcmp(ef, "0") == 0 ? 0 : 1;
         // hipGraph replay of the stages: measured slower than direct launches
         // on ROCm 7.2 for this sequence (opt-in, MOCOHIP_GRAPHS=1)
         const char* eg = std::getenv("MOCOHIP_GRAPHS");
@@ -1113,7 +1119,11 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
         const char* ec = std::getenv("MOCOHIP_CTPL");
         c->use_ctpl = !(ec && std::strcmp(ec, "0") == 0);
         const char* er = std::getenv("MOCOHIP_ROLES");
-        c->use_roles = !(er && std::strcmp(er, "0") == 0);
+        c->use_roles = er && std::strcmp(er, "1") == 0;   // measured slower
+        const char* et = std::getenv("MOCOHIP_ROLE_THREADS");
+        if (et) c->role_threads = std::min(512, std::max(64, std::atoi(et) / 64 * 64));
+        const char* eo = std::getenv("MOCOHIP_ROLE_COUPLE");
+        c->role_couple = !(eo && std::strcmp(eo, "0") == 0);
         const char* ea = std::getenv("MOCOHIP_ASM");
         c->asm_grid_stride = ea && std::strcmp(ea, "gs") == 0;
         const char* ee = std::getenv("MOCOHIP_EVENTS");
@@ -1764,6 +1774,29 @@ extern "C" int mh_synchronize(mh_ctx* c) {
     if (!c) return set_err(MH_ERR_INVALID, "null argument");
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipStreamSynchronize(c->stream));
+    return MH_OK;
+}
+
+extern "C" int mh_debug_time_stages(mh_ctx* c, const double* x, int kind, int reps, double* ms2) {
+    if (!c || !x || !ms2 || reps < 1 || kind < 0 || kind > 1) return set_err(MH_ERR_INVALID, "bad argument");
+    HIPCHK(hipSetDevice(c->device));
+    (void)hipGetLastError();
+    double* a = kind == 0 ? c->d_g : c->d_vals;
+    int rc = launch_stage(c, 0, kind, x, a, nullptr);   // warm: the transcription reads its results
+    if (!rc) rc = launch_stage(c, 1, kind, x, a, nullptr);
+    if (rc) return rc;
+    HIPCHK(hipEventRecord(c->ev[0], c->stream));
+    for (int r = 0; r < reps && !rc; ++r) rc = launch_stage(c, 0, kind, x, a, nullptr);
+    HIPCHK(hipEventRecord(c->ev[1], c->stream));
+    for (int r = 0; r < reps && !rc; ++r) rc = launch_stage(c, 1, kind, x, a, nullptr);
+    HIPCHK(hipEventRecord(c->ev[2], c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (rc) return rc;
+    float t0 = 0, t1 = 0;
+    HIPCHK(hipEventElapsedTime(&t0, c->ev[0], c->ev[1]));
+    HIPCHK(hipEventElapsedTime(&t1, c->ev[1], c->ev[2]));
+    ms2[0] = t0 / reps;
+    ms2[1] = t1 / reps;
     return MH_OK;
 }
 

@@ -194,6 +194,7 @@ MOCOHIP_SYMBOLS = {
     "mh_get_callback_sparsity": (i32, [C.c_void_p, P(C.c_uint8), C.c_int64]),
     "mh_get_work": (i32, [C.c_void_p, P(f64)]),
     "mh_debug_jacobian_lanes": (i32, [C.c_void_p, P(f64), P(f64), P(f64)]),
+    "mh_debug_time_stages": (i32, [C.c_void_p, C.c_void_p, i32, i32, P(f64)]),
     "mh_set_stream": (i32, [C.c_void_p, C.c_void_p]),
     "mh_set_async": (i32, [C.c_void_p, i32]),
     "mh_synchronize": (i32, [C.c_void_p]),

@@ -323,6 +323,15 @@ class HipNLP(_NLPBase):
         self._check(self.lib.mh_debug_jacobian_lanes(self.ctx, abi.dptr(x), abi.dptr(t), abi.dptr(Y)))
         return t, Y.reshape(self.G, self.NO, S)
 
+    def time_stages(self, x_ptr: int, kind: int = 1, reps: int = 50):
+        """(DAE stage ms, transcription stage ms): average device duration
+        over ``reps`` back-to-back launches of each stage alone at the device
+        iterate ``x_ptr`` (mh_debug_time_stages; bench roofline)."""
+        ms = np.zeros(2)
+        self._check(self.lib.mh_debug_time_stages(self.ctx, C.c_void_p(x_ptr), int(kind), int(reps),
+                                                  abi.dptr(ms)))
+        return float(ms[0]), float(ms[1])
+
     def backend(self):
         """(back-end name, FP64 ops per generated DAE eval, model hash)."""
         buf = C.create_string_buffer(128)

@@ -242,7 +242,7 @@ def _pair(name, backend="auto", tasks=None, env=None):
     opts = st.solver.options()
     saved = {k: os.environ.pop(k, None) for k in ("MOCOHIP_BACKEND", "MOCOHIP_TASKS", "MOCOHIP_INTERVAL",
                                                   "MOCOHIP_ASM", "MOCOHIP_QUOT", "MOCOHIP_CTPL",
-                                                  "MOCOHIP_ROLES")}
+                                                  "MOCOHIP_ROLES", "MOCOHIP_ROLE_COUPLE")}
     if backend != "auto":
         os.environ["MOCOHIP_BACKEND"] = backend
     if tasks:
@@ -609,14 +609,16 @@ def test_pruned_tasks_bit_identical(name):
                                      {"MOCOHIP_INTERVAL": "0", "MOCOHIP_ASM": "gs"},
                                      {"MOCOHIP_INTERVAL": "0", "MOCOHIP_QUOT": "1"},
                                      {"MOCOHIP_CTPL": "0"},
-                                     {"MOCOHIP_ROLES": "0"}])
+                                     {"MOCOHIP_ROLES": "1"},
+                                     {"MOCOHIP_ROLES": "1", "MOCOHIP_ROLE_COUPLE": "0"}])
 def test_kernel_variants_bit_identical(name, variant):
-    """The default fused path (k_role for the Jacobian lanes: one workgroup
-    per mesh interval and grid point; k_interval for g) writes exactly what
-    k_interval writes for the Jacobian (MOCOHIP_ROLES=0), what k_interval
-    writes through jac_entry (MOCOHIP_CTPL=0) and what the split path writes
-    through HBM: k_combine + k_transcribe (chunked or grid-stride), with raw
-    lane values or with finite-difference quotients in Y."""
+    """The default k_interval (combine + transcription per mesh interval,
+    raw outputs in LDS) writes exactly what k_interval writes through
+    jac_entry (MOCOHIP_CTPL=0), what k_role writes (one workgroup per mesh
+    interval and grid point, the coupling entries in the time role or in
+    k_couple) and what the split path writes through HBM: k_combine +
+    k_transcribe (chunked or grid-stride), with raw lane values or with
+    finite-difference quotients in Y."""
     gpu, _, _ = _pair(name)
     split, _, _ = _pair(name, env=variant)
     for _, x in _iterates(gpu):

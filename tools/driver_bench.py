@@ -3,7 +3,9 @@ workload (gait10dof18musc, N=200, forward FD) at the bench iterate: the
 IPOPT-iteration rate on host buffers (PCIe-inclusive: eval_f, eval_grad_f,
 eval_g, eval_jac_g with g / J copied to the host) and the device-pointer
 eval_g + eval_jac_g rate without Python in the loop.
-usage: python tools/driver_bench.py [N] [steps]"""
+usage: python tools/driver_bench.py [N] [steps] [keep_dir]
+(keep_dir: write the tape and iterate there, kept, e.g. to profile the
+driver binary itself under rocprofv3)"""
 import os
 import subprocess
 import sys
@@ -29,7 +31,11 @@ def main():
     x = ref.random_iterate(np.random.default_rng(0).uniform(-1, 1, ref.n))
     xm = ref.initial_guess_from_bounds()
     x[2:2 + ref.NS * ref.G] = xm[2:2 + ref.NS * ref.G]
+    keep = sys.argv[3] if len(sys.argv) > 3 else None
     with tempfile.TemporaryDirectory() as d:
+        if keep:
+            os.makedirs(keep, exist_ok=True)
+            d = keep
         tape, xf = os.path.join(d, "p.tape"), os.path.join(d, "x.bin")
         write_tape(rep, st.solver.options(), tape)
         x.tofile(xf)

@@ -1,6 +1,6 @@
 #!/bin/bash
-# Diagnostic: where k_interval's time goes (cuts 1-6 run with MOCOHIP_ROLES=0;
-# stop0 is the default k_role path, noroles k_interval whole).  The bench's fused step under a
+# Diagnostic: where k_interval's time goes; k_role (MOCOHIP_ROLES=1) whole
+# for the A/B.  The bench's fused step under a
 # rocprofv3 kernel trace with k_interval cut after staging (1), after the
 # combine (2), after the quotients (3), after the g rows (4), with the
 # assembly's stores alone (5) or its loads and arithmetic alone (6), and
@@ -14,13 +14,21 @@ ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/phases_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-# the Jacobian through k_interval (k_role off) whole, for the A/B against stop0
-MOCOHIP_ROLES=0 timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv \
+# the Jacobian through k_interval whole, without the assembly-word prefetch
+MOCOHIP_IV_PF=0 timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv \
     -d "$OUT/noroles" -o run -- python3 "$ROOT/bench.py" --steps 50 --warmup 5 --no-cpu-baseline \
     --single-mode --mode fused --intervals "$N" > "$OUT/noroles.log" 2>&1
-for s in 0 1 2 3 4 5 6; do
-    R=1; [ "$s" != 0 ] && R=0   # the cuts are k_interval's
-    MOCOHIP_ROLES=$R MOCOHIP_IV_DEBUG_STOP=$s timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv \
+for t in 256 c0; do
+    (
+    export MOCOHIP_ROLES=1
+    if [ "$t" = c0 ]; then export MOCOHIP_ROLE_COUPLE=0; else export MOCOHIP_ROLE_THREADS=$t; fi
+    timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv \
+        -d "$OUT/roles$t" -o run -- python3 "$ROOT/bench.py" --steps 50 --warmup 5 --no-cpu-baseline \
+        --single-mode --mode fused --intervals "$N" > "$OUT/roles$t.log" 2>&1
+    )
+done
+for s in 0 7 1 2 3 4 5 6; do
+    MOCOHIP_IV_DEBUG_STOP=$s timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv \
         -d "$OUT/stop$s" -o run -- python3 "$ROOT/bench.py" --steps 50 --warmup 5 --no-cpu-baseline \
         --single-mode --mode fused --intervals "$N" > "$OUT/stop$s.log" 2>&1
 done
