@@ -2,7 +2,7 @@
 # One GPU-box session: GPU parity tests, smoke, the default bench line, the
 # k_interval phase cut and the round profile (kernel trace + PMC passes).
 # Every GPU step has its own time limit; the script stops at the first failure.
-#   usage: tools/gpu_round.sh <tag> [tests] [bench] [phases] [profile]
+#   usage: tools/gpu_round.sh <tag> [tests] [bench] [mesh] [phases] [profile]
 set -e
 TAG=$1; shift
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -21,6 +21,9 @@ for what in "$@"; do
     bench)
         timeout -k 10 400 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
         timeout -k 10 120 python tools/driver_bench.py 200 > "$OUT/driver.json" 2> "$OUT/driver.err" || true;;
+    mesh)
+        timeout -k 10 300 python bench.py --multi mesh --steps 500 --warmup 200 > "$OUT/mesh.json" 2> "$OUT/mesh.err"
+        tail -1 "$OUT/mesh.json";;
     phases)
         timeout -k 10 600 bash tools/iv_phases.sh "$TAG" 200;;
     profile)
