@@ -235,7 +235,17 @@ enum mh_goal_kind {
      * derivatives; MocoInverse sets it with weight 0.01, MocoInverse.cpp:
      * 106-107).  Terms index the auxiliary derivatives (0 = the first one
      * after the accelerations). */
-    MH_GOAL_AUX_DERIVATIVES = 4
+    MH_GOAL_AUX_DERIVATIVES = 4,
+    /* MocoMarkerFinalGoal (MocoMarkerFinalGoal.cpp:29-34): weight *
+     * |p_G(q(tf)) - r|^2 for a point fixed on a body, at the final grid
+     * point's coordinates (states required; not with prescribed
+     * kinematics).  Six terms: goal_index = the body (mh_model body index,
+     * -1 = ground) in each, goal_column = 0..5, goal_weight = the point's
+     * location in the body frame (x, y, z) then the reference location in
+     * ground (x, y, z).  An endpoint cost: no integral; its gradient is the
+     * finite difference of the cost over the final coordinates (the CasADi
+     * FD of the cost callback, CasOCFunction.h:38-44). */
+    MH_GOAL_MARKER_FINAL = 5
 };
 typedef struct mh_goal {
     int32_t kind;

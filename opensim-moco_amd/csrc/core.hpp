@@ -1389,6 +1389,13 @@ __device__ __forceinline__ void gather_inputs(const double* __restrict__ x, cons
     (void)NI;
 }
 
+// Goals with an integral (quadrature of an integrand): all but the endpoint
+// costs (final time, final marker).
+__host__ __device__ __forceinline__ bool goal_integral(int kind) {
+    return kind != MH_GOAL_FINAL_TIME && kind != MH_GOAL_MARKER_FINAL;
+}
+constexpr int MH_MARKER_MAX_Q = 64;   // coordinates a marker goal's kernel holds per lane
+
 struct GoalSet {
     int ngoals;
     int nc, nacc;   // controls; accelerations before the auxiliary derivatives
@@ -1433,7 +1440,7 @@ __global__ void __launch_bounds__(64) k_integrand(DevModel M, Layout L, GoalSet 
     double in[Z::MI];
     gather_inputs(x, L, k, in, L.NI);
     for (int g = 0; g < GS.ngoals; ++g) {
-        const bool integral = GS.goals[g].kind != MH_GOAL_FINAL_TIME;
+        const bool integral = goal_integral(GS.goals[g].kind);
         C[(long)k * GS.ngoals + g] =
                 integral ? quad[k] * goal_integrand(M, GS, g, t, in, in + L.NS) : 0.0;
     }
@@ -1456,7 +1463,7 @@ __global__ void __launch_bounds__(64) k_grad(DevModel M, Layout L, GoalSet GS, i
     double acc = 0.0;
     for (int gi = 0; gi < GS.ngoals; ++gi) {
         const mh_goal G = GS.goals[gi];
-        if (G.kind == MH_GOAL_FINAL_TIME) continue;
+        if (!goal_integral(G.kind)) continue;
         const double seed = d == 0 ? 1.0 - g : (d == 1 ? g : 1.0);
         double lp = 0.0, lm = 0.0, l0 = 0.0;
         if (fd != MH_FD_CENTRAL) l0 = goal_integrand(M, GS, gi, t, in, in + L.NS);
@@ -1598,6 +1605,8 @@ struct mh_ctx {
     int* d_rl_e = nullptr;
     uint32_t* d_rl_w = nullptr;
     double* d_xch = nullptr;       // k_role -> k_couple exchange [interval][point][NO][3]
+    double* d_ep = nullptr;        // endpoint-cost values per goal (k_marker_final)
+    bool has_marker = false;
     bool use_roles = false;        // MOCOHIP_ROLES=1: k_role (+ k_couple) for the Jacobian lanes
     int role_threads = 256;        // k_role workgroup size (MOCOHIP_ROLE_THREADS: 64..512)
     bool role_couple = true;       // coupling in k_role's time role (MOCOHIP_ROLE_COUPLE=0: k_couple)

@@ -140,7 +140,7 @@ __global__ void __launch_bounds__(256) k_transcribe_gs(Layout L, Interval I, Lan
 // the t0/tf gradient entries (mode 1).
 __global__ void __launch_bounds__(256) k_reduce_obj(Layout L, GoalSet GS, int mode,
         const double* __restrict__ x, const double* __restrict__ C,
-        const double* __restrict__ tpart, double* __restrict__ out) {
+        const double* __restrict__ tpart, const double* __restrict__ ep, double* __restrict__ out) {
     __shared__ double red[256];
     const int ng = GS.ngoals;
     double total = 0.0, g0 = 0.0, g1 = 0.0;
@@ -159,6 +159,8 @@ __global__ void __launch_bounds__(256) k_reduce_obj(Layout L, GoalSet GS, int mo
         if (G.kind == MH_GOAL_FINAL_TIME) {
             total += G.weight * x[1];
             g1 += G.weight;
+        } else if (G.kind == MH_GOAL_MARKER_FINAL) {
+            total += G.weight * ep[gi];   // its gradient: k_marker_final
         } else {
             total += G.weight * ((x[1] - x[0]) * acc);
             g0 += -G.weight * acc;
@@ -180,6 +182,100 @@ __global__ void __launch_bounds__(256) k_reduce_obj(Layout L, GoalSet GS, int mo
         }
         if (threadIdx.x == 0) out[c] = red[0] + (c == 0 ? g0 : g1);
         __syncthreads();
+    }
+}
+
+// Pose of body b in ground at coordinates q (the position part of dae_eval's
+// forward pass, dae_device.hpp: parent pose x joint frames x coordinate
+// functions), walking b's ancestors from the ground.
+__device__ void body_pose(const DevModel& M, const double* q, int b, double* R, double* p) {
+    int chain[MH_MARKER_MAX_Q + 1];
+    int n = 0;
+    for (int x = b; x >= 0 && n <= MH_MARKER_MAX_Q; x = M.bodies[x].parent) chain[n++] = x;
+    double Rp[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, pp[3] = {0, 0, 0};
+    for (int ci = n - 1; ci >= 0; --ci) {
+        const mh_body& B = M.bodies[chain[ci]];
+        double RGF[9], t0, t1, t2;
+        mm3(Rp, B.R_PF, RGF);
+        mv3(Rp, B.p_PF[0], B.p_PF[1], B.p_PF[2], t0, t1, t2);
+        const double pGF0 = pp[0] + t0, pGF1 = pp[1] + t1, pGF2 = pp[2] + t2;
+        double pFM0 = 0, pFM1 = 0, pFM2 = 0;
+        for (int a = B.axis_begin; a < B.axis_begin + B.axis_count; ++a) {
+            const mh_axis X = M.axes[a];
+            if (X.type != MH_AXIS_TRANSLATION) continue;
+            double v, d1, d2;
+            fn_eval(M, X.func, q, v, d1, d2);
+            pFM0 += v * X.dir[0]; pFM1 += v * X.dir[1]; pFM2 += v * X.dir[2];
+        }
+        mv3(RGF, pFM0, pFM1, pFM2, t0, t1, t2);
+        const double oM0 = pGF0 + t0, oM1 = pGF1 + t1, oM2 = pGF2 + t2;
+        double Rcur[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+        for (int a = B.axis_begin; a < B.axis_begin + B.axis_count; ++a) {
+            const mh_axis X = M.axes[a];
+            if (X.type != MH_AXIS_ROTATION) continue;
+            double v, d1, d2;
+            fn_eval(M, X.func, q, v, d1, d2);
+            double Rk[9];
+            axis_rot(X.dir[0], X.dir[1], X.dir[2], v, Rk);
+            mm3(Rcur, Rk, Rcur);
+        }
+        double RGM[9];
+        mm3(RGF, Rcur, RGM);
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j)
+                Rp[3 * i + j] = RGM[3 * i] * B.R_BM[3 * j] + RGM[3 * i + 1] * B.R_BM[3 * j + 1] +
+                                RGM[3 * i + 2] * B.R_BM[3 * j + 2];
+        mv3(Rp, B.p_BM[0], B.p_BM[1], B.p_BM[2], t0, t1, t2);
+        pp[0] = oM0 - t0; pp[1] = oM1 - t1; pp[2] = oM2 - t2;
+    }
+    for (int i = 0; i < 9; ++i) R[i] = Rp[i];
+    for (int i = 0; i < 3; ++i) p[i] = pp[i];
+}
+
+// MocoMarkerFinalGoal (MocoMarkerFinalGoal.cpp:29-34): |p_G(q(tf)) - r|^2
+// of a body-fixed point; block gi = goal gi.  Lane 0: the final grid
+// point's coordinates; mode 1 (gradient): lane 1 + s perturbs coordinate s by
+// +h (backward: -h), central also lane 1 + NQ + s by -h, and lane 0 adds
+// weight * the FD quotient to grad's final-state entries (after k_grad).
+__global__ void __launch_bounds__(128) k_marker_final(DevModel M, Layout L, GoalSet GS, int fd, double h,
+        int mode, const double* __restrict__ x, double* __restrict__ ep, double* __restrict__ grad) {
+    const int gi = blockIdx.x;
+    const mh_goal G = GS.goals[gi];
+    if (G.kind != MH_GOAL_MARKER_FINAL) return;
+    __shared__ double cost[2 * MH_MARKER_MAX_Q + 1];
+    const int NQ = L.NQ;
+    const int nl = 1 + (mode ? (fd == MH_FD_CENTRAL ? 2 * NQ : NQ) : 0);
+    const double* xs = x + 2 + (long)(L.G - 1) * L.NS;
+    const int k0 = G.term_begin;
+    const int b = GS.gidx[k0];
+    for (int j = threadIdx.x; j < nl; j += blockDim.x) {
+        double q[MH_MARKER_MAX_Q];
+        for (int s = 0; s < NQ; ++s) q[s] = xs[s];
+        if (j > 0) {
+            const int s = (j - 1) % NQ;
+            const bool minus = fd == MH_FD_BACKWARD || j > NQ;
+            q[s] = minus ? xs[s] - h : xs[s] + h;
+        }
+        double R[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, p[3] = {0, 0, 0};
+        if (b >= 0) body_pose(M, q, b, R, p);
+        double y0, y1, y2;
+        mv3(R, GS.gw[k0], GS.gw[k0 + 1], GS.gw[k0 + 2], y0, y1, y2);
+        const double d0 = (p[0] + y0) - GS.gw[k0 + 3], d1 = (p[1] + y1) - GS.gw[k0 + 4],
+                     d2 = (p[2] + y2) - GS.gw[k0 + 5];
+        double s2 = 0.0;
+        s2 += d0 * d0;
+        s2 += d1 * d1;
+        s2 += d2 * d2;
+        cost[j] = s2;
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    ep[gi] = cost[0];
+    if (!mode) return;
+    for (int s = 0; s < NQ; ++s) {
+        const double d = fd == MH_FD_CENTRAL ? (cost[1 + s] - cost[1 + NQ + s]) / (2.0 * h)
+                       : (fd == MH_FD_FORWARD ? (cost[1 + s] - cost[0]) / h : (cost[0] - cost[1 + s]) / h);
+        grad[2 + (long)(L.G - 1) * L.NS + s] += G.weight * d;
     }
 }
 
@@ -816,14 +912,36 @@ static int validate_and_layout(mh_ctx* c, const mh_problem* p, const mh_options*
         if (pt.kind == MH_PP_CONDITIONAL && (pt.coord < 0 || pt.coord >= M.nq))
             return set_err(MH_ERR_INVALID, "path point %d: bad coordinate", i);
     }
+    // goals: kind, term range, and every term index within its kind's range
+    // (a bad index would be an out-of-bounds device read)
     for (int g = 0; g < p->ngoals; ++g) {
         const mh_goal& G = p->goals[g];
-        if (G.term_begin < 0 || G.term_begin + G.term_count > p->nterms)
+        if (G.kind < MH_GOAL_CONTROL || G.kind > MH_GOAL_MARKER_FINAL)
+            return set_err(MH_ERR_INVALID, "goal %d: unknown kind %d", g, G.kind);
+        if (G.term_begin < 0 || G.term_count < 0 || G.term_begin + G.term_count > p->nterms ||
+                (G.kind == MH_GOAL_MARKER_FINAL && G.term_count != 6))
             return set_err(MH_ERR_INVALID, "goal %d: bad terms", g);
         if (G.kind == MH_GOAL_STATE_TRACKING && (G.table < 0 || G.table >= M.ntables))
             return set_err(MH_ERR_INVALID, "goal %d: bad table", g);
-        if (G.kind < MH_GOAL_CONTROL || G.kind > MH_GOAL_AUX_DERIVATIVES)
-            return set_err(MH_ERR_INVALID, "goal %d: unknown kind %d", g, G.kind);
+        if (G.kind == MH_GOAL_MARKER_FINAL && (c->presc || M.nq > MH_MARKER_MAX_Q))
+            return set_err(MH_ERR_UNSUPPORTED, "goal %d: marker goal needs coordinate states (<= %d)", g,
+                    MH_MARKER_MAX_Q);
+        for (int k = G.term_begin; k < G.term_begin + G.term_count; ++k) {
+            const int idx = p->goal_index[k];
+            int hi;
+            switch (G.kind) {
+            case MH_GOAL_CONTROL: hi = c->NC; break;
+            case MH_GOAL_STATE_TRACKING: case MH_GOAL_SUM_SQUARED_STATE: hi = c->NS; break;
+            case MH_GOAL_AUX_DERIVATIVES: hi = c->NAR; break;
+            case MH_GOAL_MARKER_FINAL: hi = M.nbodies; break;
+            default: hi = INT32_MAX; break;   // final time: no terms read
+            }
+            if (idx < (G.kind == MH_GOAL_MARKER_FINAL ? -1 : 0) || idx >= hi)
+                return set_err(MH_ERR_INVALID, "goal %d: term %d index %d out of range", g, k, idx);
+            if (G.kind == MH_GOAL_STATE_TRACKING &&
+                    (p->goal_column[k] < 0 || p->goal_column[k] >= M.tables[G.table].ncol))
+                return set_err(MH_ERR_INVALID, "goal %d: term %d column out of range", g, k);
+        }
     }
     for (int e = 0; e < M.nexternal; ++e) {
         const mh_external_force& E = M.external[e];
@@ -1025,6 +1143,7 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     const size_t o_grad = A.reserve(sizeof(double) * c->n);
     const size_t o_tpart = A.reserve(sizeof(double) * 2 * (size_t)c->G);
     const size_t o_f = A.reserve(sizeof(double) * 4);
+    const size_t o_epc = A.reserve(sizeof(double) * (size_t)std::max(1, p->ngoals));   // endpoint costs
     const int npts_iv = c->scheme == MH_HERMITE_SIMPSON ? 3 : 2;
     const size_t o_xch = A.reserve(sizeof(double) * (size_t)std::max(nint, 1) * npts_iv * std::max(1, c->NO) * XCH_W);
 
@@ -1087,6 +1206,9 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     c->d_Yg = (double*)(b + o_Yg); c->d_g = (double*)(b + o_g); c->d_vals = (double*)(b + o_vals);
     c->d_C = (double*)(b + o_C); c->d_grad = (double*)(b + o_grad); c->d_tpart = (double*)(b + o_tpart);
     c->d_f = (double*)(b + o_f);
+    c->d_ep = (double*)(b + o_epc);
+    c->has_marker = false;
+    for (int g = 0; g < p->ngoals; ++g) c->has_marker |= p->goals[g].kind == MH_GOAL_MARKER_FINAL;
     c->d_xch = (double*)(b + o_xch);
     if (ti) {
         bind_taskset(b, to_jac, c->ts_jac);
@@ -1522,9 +1644,12 @@ extern "C" int mh_eval_f(mh_ctx* c, const double* x, int, double* f) {
         c->be->integrand(c, c->d_x);
         HIPCHK(hipGetLastError());
     }
+    if (c->has_marker)
+        hipLaunchKernelGGL(k_marker_final, dim3((unsigned)c->ngoals), dim3(128), 0, c->stream, c->M, L, c->GS,
+                c->fd, c->h, 0, c->d_x, c->d_ep, c->d_grad);
     if (c->timing) HIPCHK(hipEventRecord(c->ev[1], c->stream));
     hipLaunchKernelGGL(k_reduce_obj, dim3(1), dim3(256), 0, c->stream, L, c->GS, 0, c->d_x, c->d_C,
-            c->d_tpart, c->d_f);
+            c->d_tpart, c->d_ep, c->d_f);
     HIPCHK(hipGetLastError());
     if (c->timing) HIPCHK(hipEventRecord(c->ev[2], c->stream));
     HIPCHK(hipMemcpyAsync(f, c->d_f, sizeof(double), hipMemcpyDeviceToHost, c->stream));
@@ -1546,9 +1671,12 @@ extern "C" int mh_eval_grad_f(mh_ctx* c, const double* x, int, double* grad) {
         c->be->grad(c, c->d_x);
         HIPCHK(hipGetLastError());
     }
+    if (c->has_marker)   // after k_grad: adds to the final coordinates' entries
+        hipLaunchKernelGGL(k_marker_final, dim3((unsigned)c->ngoals), dim3(128), 0, c->stream, c->M, L, c->GS,
+                c->fd, c->h, 1, c->d_x, c->d_ep, c->d_grad);
     if (c->timing) HIPCHK(hipEventRecord(c->ev[1], c->stream));
     hipLaunchKernelGGL(k_reduce_obj, dim3(1), dim3(256), 0, c->stream, L, c->GS, 1, c->d_x, c->d_C,
-            c->d_tpart, c->d_f);
+            c->d_tpart, c->d_ep, c->d_f);
     HIPCHK(hipGetLastError());
     if (c->timing) HIPCHK(hipEventRecord(c->ev[2], c->stream));
     HIPCHK(hipMemcpyAsync(c->d_grad, c->d_f, sizeof(double) * 2, hipMemcpyDeviceToDevice, c->stream));

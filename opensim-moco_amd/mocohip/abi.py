@@ -19,7 +19,7 @@ MH_AXIS_ROTATION, MH_AXIS_TRANSLATION = 0, 1
 MH_PP_FIXED, MH_PP_CONDITIONAL, MH_PP_MOVING = 0, 1, 2
 MH_ACT_MUSCLE, MH_ACT_COORDINATE = 0, 1
 MH_GOAL_CONTROL, MH_GOAL_STATE_TRACKING, MH_GOAL_FINAL_TIME, \
-    MH_GOAL_SUM_SQUARED_STATE, MH_GOAL_AUX_DERIVATIVES = 0, 1, 2, 3, 4
+    MH_GOAL_SUM_SQUARED_STATE, MH_GOAL_AUX_DERIVATIVES, MH_GOAL_MARKER_FINAL = 0, 1, 2, 3, 4, 5
 MH_HERMITE_SIMPSON, MH_TRAPEZOIDAL = 0, 1
 MH_DYNAMICS_EXPLICIT, MH_DYNAMICS_IMPLICIT = 0, 1
 MH_FD_CENTRAL, MH_FD_FORWARD, MH_FD_BACKWARD = 0, 1, 2

@@ -22,11 +22,11 @@ from typing import Optional
 import numpy as np
 
 from .model import (Body, Coordinate, CoordinateActuator, DataTable,
-                    ExternalForce, Joint, Model, model_from_dict)
+                    ExternalForce, Joint, Marker, Model, model_from_dict)
 from .osim import add_reserves
 from .problem import (Constant, GCVSpline, ImplicitAuxiliaryDerivativesTerm,
                       MocoControlBoundConstraint, MocoControlGoal, MocoInitialActivationGoal,
-                      MocoFinalTimeGoal, MocoProblem, MocoStateTrackingGoal,
+                      MocoFinalTimeGoal, MocoMarkerFinalGoal, MocoProblem, MocoStateTrackingGoal,
                       PiecewiseLinearFunction)
 from .solver import MocoHipSolver, MocoStudy
 
@@ -60,6 +60,8 @@ def n_link_pendulum(num_links: int) -> Model:
         prev = f"b{i}"
     for i in range(num_links):
         m.add_coordinate_actuator(CoordinateActuator(f"tau{i}", f"q{i}", 1.0, path=f"/tau{i}"))
+    for i in range(num_links):   # ModelFactory.cpp:74-75: at each body's origin
+        m.add_marker(Marker(f"marker{i}", f"b{i}", (0.0, 0.0, 0.0)))
     return m
 
 
@@ -77,6 +79,28 @@ def double_pendulum(num_mesh_intervals: int = 100, scheme: str = "hermite-simpso
     p.set_control_info("/tau1", (-100, 100))
     p.add_goal(MocoFinalTimeGoal(weight=0.001))
     p.add_goal(MocoControlGoal(weight=1e-3))
+    s = MocoHipSolver(num_mesh_intervals=num_mesh_intervals, transcription_scheme=scheme,
+                      multibody_dynamics_mode=dynamics)
+    return MocoStudy(p, s)
+
+
+def double_pendulum_swingup(num_mesh_intervals: int = 29, scheme: str = "trapezoidal",
+                            dynamics: str = "explicit") -> MocoStudy:
+    """testImplicit.cpp:30-100 (solveDoublePendulumSwingup): final-time goal
+    (weight 0.001) + MocoMarkerFinalGoal on /markerset/marker1 to (0, 2, 0)
+    (weight 1000), trapezoidal, N=29, both dynamics modes."""
+    m = n_link_pendulum(2)
+    p = MocoProblem(m)
+    p.set_time_bounds(0.0, (0.0, 5.0))
+    p.set_state_info("/jointset/j0/q0/value", (-10, 10), 0)
+    p.set_state_info("/jointset/j0/q0/speed", (-50, 50), 0, 0)
+    p.set_state_info("/jointset/j1/q1/value", (-10, 10), 0)
+    p.set_state_info("/jointset/j1/q1/speed", (-50, 50), 0, 0)
+    p.set_control_info("/tau0", (-100, 100))
+    p.set_control_info("/tau1", (-100, 100))
+    p.add_goal(MocoFinalTimeGoal(weight=0.001))
+    p.add_goal(MocoMarkerFinalGoal("final", weight=1000.0, point_name="/markerset/marker1",
+                                   reference_location=(0.0, 2.0, 0.0)))
     s = MocoHipSolver(num_mesh_intervals=num_mesh_intervals, transcription_scheme=scheme,
                       multibody_dynamics_mode=dynamics)
     return MocoStudy(p, s)
@@ -230,6 +254,7 @@ def gait10dof18musc_inverse(num_mesh_intervals: int = 25, fd_scheme: str = "forw
 CONFIGS = {
     "sliding_mass": sliding_mass,
     "double_pendulum": double_pendulum,
+    "double_pendulum_swingup": double_pendulum_swingup,
     "gait10dof18musc": gait10dof18musc,
     "gait10dof18musc_inverse": gait10dof18musc_inverse,
 }

@@ -204,6 +204,16 @@ class CoordinateActuator:
 
 
 @dataclass
+class Marker:
+    """OpenSim::Marker: a point fixed on a body (``location`` in the body
+    frame); path /markerset/<name>."""
+    name: str
+    body: str                # body name or "ground"
+    location: Sequence[float] = (0.0, 0.0, 0.0)
+    path: str = ""
+
+
+@dataclass
 class DataTable:
     """Time series; splined with the GCVSpline restatement (splines.py)."""
     name: str
@@ -235,6 +245,7 @@ class Model:
         self.actuators: List[object] = []       # force-set order
         self.tables: Dict[str, DataTable] = {}
         self.external_forces: List[ExternalForce] = []
+        self.markers: Dict[str, Marker] = {}    # by path
 
     # building ---------------------------------------------------------------
     def add_body(self, body: Body):
@@ -268,6 +279,12 @@ class Model:
     def add_external_force(self, e: ExternalForce):
         self.external_forces.append(e)
         return e
+
+    def add_marker(self, mk: Marker):
+        if not mk.path:
+            mk.path = f"/markerset/{mk.name}"
+        self.markers[mk.path] = mk
+        return mk
 
     # ordering ---------------------------------------------------------------
     def tree_order(self) -> List[Joint]:
@@ -560,6 +577,8 @@ def model_to_dict(m: Model) -> dict:
               "min_control": a.min_control, "max_control": a.max_control,
               "path": a.path})
             for a in m.actuators],
+        "markers": [{"name": k.name, "body": k.body, "location": list(k.location), "path": k.path}
+                    for k in m.markers.values()],
     }
 
 
@@ -585,4 +604,6 @@ def model_from_dict(d: dict) -> Model:
             m.add_coordinate_actuator(CoordinateActuator(
                 a["name"], a["coordinate"], a["optimal_force"], a["min_control"],
                 a["max_control"], a["path"]))
+    for k in d.get("markers", []):
+        m.add_marker(Marker(k["name"], k["body"], tuple(k["location"]), k.get("path", "")))
     return m

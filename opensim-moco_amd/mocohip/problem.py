@@ -96,6 +96,18 @@ class MocoInitialActivationGoal:
     weight: float = 1.0
 
 
+@dataclass
+class MocoMarkerFinalGoal:
+    """MocoMarkerFinalGoal (Moco/Moco/MocoGoal/MocoMarkerFinalGoal.{h,cpp}):
+    cost = |location in ground of ``point_name`` at the final state -
+    ``reference_location``|^2 (calcGoalImpl, .cpp:29-34; realizes Position
+    only, so it depends on the final coordinates), times the weight."""
+    name: str = "marker_final"
+    weight: float = 1.0
+    point_name: str = ""
+    reference_location: Sequence[float] = (0.0, 0.0, 0.0)
+
+
 # ------------------------------------------------- functions of time ----
 @dataclass
 class Constant:
@@ -341,6 +353,18 @@ class ProblemRep:
                     gw.append(float(g.state_weights.get(n, 1.0)))
             elif isinstance(g, MocoFinalTimeGoal):
                 gs.kind = abi.MH_GOAL_FINAL_TIME
+            elif isinstance(g, MocoMarkerFinalGoal):
+                if kin is not None:
+                    raise NotImplementedError("MocoMarkerFinalGoal with prescribed kinematics "
+                                              "(the final coordinates are not NLP states)")
+                mk = model.markers.get(g.point_name)
+                if mk is None:
+                    raise ValueError(f"MocoMarkerFinalGoal: no point '{g.point_name}' in the model")
+                body = self.compiled.body_index[mk.body]
+                gs.kind = abi.MH_GOAL_MARKER_FINAL
+                ref = [float(v) for v in g.reference_location]
+                for ci, v in enumerate([float(v) for v in mk.location] + ref):
+                    gidx.append(body); gcol.append(ci); gw.append(v)
             elif isinstance(g, ImplicitAuxiliaryDerivativesTerm):
                 gs.kind = abi.MH_GOAL_AUX_DERIVATIVES
                 naux = sum(1 for m in model.muscles if not m.ignore_tendon_compliance

@@ -673,6 +673,47 @@ int orc_create(const mh_problem* p, const mh_options* o, orc_ctx** out) {
             return fail(MH_ERR_INVALID, "path equation %d: bad control/table", e);
         }
     }
+    /* goals: kind, term range, and every term index within its kind's range
+     * (controls, states, implicit auxiliary derivatives, bodies) */
+    for (int g = 0; g < p->ngoals; ++g) {
+        const mh_goal* G = &c->goals[g];
+        if (G->kind < MH_GOAL_CONTROL || G->kind > MH_GOAL_MARKER_FINAL) {
+            orc_destroy(c);
+            return fail(MH_ERR_INVALID, "goal %d: unknown kind %d", g, G->kind);
+        }
+        if (G->term_begin < 0 || G->term_count < 0 || G->term_begin + G->term_count > p->nterms ||
+                (G->kind == MH_GOAL_MARKER_FINAL && G->term_count != 6)) {
+            orc_destroy(c);
+            return fail(MH_ERR_INVALID, "goal %d: bad terms", g);
+        }
+        if (G->kind == MH_GOAL_STATE_TRACKING && (G->table < 0 || G->table >= M->ntables)) {
+            orc_destroy(c);
+            return fail(MH_ERR_INVALID, "goal %d: bad table", g);
+        }
+        if (G->kind == MH_GOAL_MARKER_FINAL && c->presc) {
+            orc_destroy(c);
+            return fail(MH_ERR_INVALID, "goal %d: marker goal with prescribed kinematics", g);
+        }
+        for (int k = G->term_begin; k < G->term_begin + G->term_count; ++k) {
+            int idx = c->gidx[k], hi;
+            switch (G->kind) {
+            case MH_GOAL_CONTROL: hi = c->NC; break;
+            case MH_GOAL_STATE_TRACKING: case MH_GOAL_SUM_SQUARED_STATE: hi = c->NS; break;
+            case MH_GOAL_AUX_DERIVATIVES: hi = c->NAR; break;
+            case MH_GOAL_MARKER_FINAL: hi = M->nbodies; if (idx == -1) continue; break;
+            default: hi = 0x7fffffff; break;   /* final time: no terms read */
+            }
+            if (idx < 0 || idx >= hi) {
+                orc_destroy(c);
+                return fail(MH_ERR_INVALID, "goal %d: term %d index %d out of range", g, k, idx);
+            }
+            if (G->kind == MH_GOAL_STATE_TRACKING &&
+                    (c->gcol[k] < 0 || c->gcol[k] >= c->tabs[G->table].ncol)) {
+                orc_destroy(c);
+                return fail(MH_ERR_INVALID, "goal %d: term %d column out of range", g, k);
+            }
+        }
+    }
     for (int e = 0; e < c->NEP; ++e) {
         const mh_endpoint_equation* E = &c->ep[e];
         if (E->kind != MH_ENDPOINT_INITIAL_ACTIVATION || E->index_a < 0 || E->index_a >= c->NC ||
@@ -2208,7 +2249,27 @@ static double goal_integrand(const orc_ctx* c, const mh_goal* G, double t, const
     }
     return L;
 }
-static int goal_has_integral(const mh_goal* G) { return G->kind != MH_GOAL_FINAL_TIME; }
+static int goal_has_integral(const mh_goal* G) {
+    return G->kind != MH_GOAL_FINAL_TIME && G->kind != MH_GOAL_MARKER_FINAL;
+}
+
+/* MocoMarkerFinalGoal::calcGoalImpl (MocoMarkerFinalGoal.cpp:29-34):
+ * realizePosition at the final state, |location in ground - reference|^2
+ * (SimTK normSqr: x*x + y*y + z*z).  st: the final grid point's states. */
+static double marker_cost(const orc_ctx* c, const mh_goal* G, const double* st, dae_ws* w) {
+    int k0 = G->term_begin, b = c->gidx[k0];
+    kinematics(c, st, st + c->NQ, NULL, w);
+    const real* R = w->R + 9 * (b + 1);
+    const real* p = w->p + 3 * (b + 1);
+    real loc[3] = {c->gw[k0], c->gw[k0 + 1], c->gw[k0 + 2]}, y[3];
+    mat_vec(R, loc, y);
+    double s = 0.0;
+    for (int i = 0; i < 3; ++i) {
+        double d = (p[i] + y[i]) - c->gw[k0 + 3 + i];
+        s += d * d;
+    }
+    return s;
+}
 
 int orc_eval_f(orc_ctx* c, const double* x, double* f) {
     double* times = (double*)malloc(sizeof(double) * (size_t)c->G);
@@ -2220,7 +2281,13 @@ int orc_eval_f(orc_ctx* c, const double* x, double* f) {
     for (int g = 0; g < c->P.ngoals; ++g) {
         const mh_goal* G = &c->goals[g];
         double cost;
-        if (goal_has_integral(G)) {
+        if (G->kind == MH_GOAL_MARKER_FINAL) {
+            dae_ws w;
+            ws_alloc(c, &w);
+            gather_point(c, x, c->G - 1, st, ct);
+            cost = G->weight * marker_cost(c, G, st, &w);
+            ws_free(&w);
+        } else if (goal_has_integral(G)) {
             double acc = 0.0;
             for (int k = 0; k < c->G; ++k) {
                 gather_point(c, x, k, st, ct);
@@ -2249,6 +2316,25 @@ int orc_eval_grad_f(orc_ctx* c, const double* x, double* grad) {
     double dur = x[1] - x[0];
     for (int g = 0; g < c->P.ngoals; ++g) {
         const mh_goal* G = &c->goals[g];
+        if (G->kind == MH_GOAL_MARKER_FINAL) {
+            /* FD of the cost over the final coordinates (the other final
+             * states do not change a Position-stage cost: exactly 0) */
+            dae_ws w;
+            ws_alloc(c, &w);
+            gather_point(c, x, c->G - 1, in, in + NS);
+            double c0 = marker_cost(c, G, in, &w);
+            for (int s = 0; s < c->NQ; ++s) {
+                double v = in[s], cp = 0.0, cm = 0.0;
+                if (c->fd != MH_FD_BACKWARD) { in[s] = v + h; cp = marker_cost(c, G, in, &w); }
+                if (c->fd != MH_FD_FORWARD) { in[s] = v - h; cm = marker_cost(c, G, in, &w); }
+                in[s] = v;
+                double d = c->fd == MH_FD_CENTRAL ? (cp - cm) / (2.0 * h)
+                         : (c->fd == MH_FD_FORWARD ? (cp - c0) / h : (c0 - cm) / h);
+                grad[col_state(c, c->G - 1, s)] += G->weight * d;
+            }
+            ws_free(&w);
+            continue;
+        }
         if (!goal_has_integral(G)) { grad[1] += G->weight; continue; }
         double acc = 0.0;
         for (int k = 0; k < c->G; ++k) {

@@ -46,6 +46,11 @@ def _nointerp(st):
     return st
 
 
+def _central(st):
+    st.solver.finite_difference_scheme = "central"
+    return st
+
+
 def _physiological_guess(st):
     """initial-guess detection at the bounds midpoint with activations 0.5
     and normalized tendon forces 0.1 (a regular point of the DGF model)."""
@@ -128,6 +133,10 @@ CASES = {
     "gait_inverse_random": lambda: configs.gait10dof18musc_inverse(3),
     # interpolate_control_midpoints = false outside MocoInverse too
     "double_pendulum_nointerp": lambda: _nointerp(configs.double_pendulum(12)),
+    # testImplicit.cpp swing-up: MocoMarkerFinalGoal + final time, both modes
+    "double_pendulum_swingup": lambda: configs.double_pendulum_swingup(29),
+    "double_pendulum_swingup_implicit_central": lambda: _central(
+        configs.double_pendulum_swingup(29, dynamics="implicit")),
     "gait_rigid_nointerp_trap": lambda: _nointerp(_trap(configs.gait10dof18musc(6))),
 }
 
@@ -469,7 +478,8 @@ def test_eval_jac_g(name, backend):
 
 @pytest.mark.parametrize("name", ["sliding_mass", "double_pendulum_hs", "gait_rigid_forward",
                                   "gait_compliant_central", "double_pendulum_implicit_hs",
-                                  "gait_rigid_implicit", "gait_inverse", "pendulum_bound_both_implicit"])
+                                  "gait_rigid_implicit", "gait_inverse", "pendulum_bound_both_implicit",
+                                  "double_pendulum_swingup", "double_pendulum_swingup_implicit_central"])
 def test_objective_and_gradient(name):
     gpu, ref, st = _pair(name)
     for _, x in _iterates(gpu):

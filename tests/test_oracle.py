@@ -953,3 +953,60 @@ def test_assembly_from_lanes_equals_eval_jac_g(case):
     g, J = nlp.assemble_from_lanes(x, t, Y)
     assert np.array_equal(g, nlp.eval_g(x), equal_nan=True)
     assert np.array_equal(J, nlp.eval_jac_g(x), equal_nan=True)
+
+
+# ------------------------------------------------ MocoMarkerFinalGoal ----
+def _pendulum_tip(q0, q1):
+    """/markerset/marker1 of ModelFactory::createNLinkPendulum(2) in ground:
+    body i's origin sits 1 m along its x axis from its pin (ModelFactory.cpp:
+    60-75), so the tip is (cos q0 + cos(q0+q1), sin q0 + sin(q0+q1), 0)."""
+    return np.array([math.cos(q0) + math.cos(q0 + q1), math.sin(q0) + math.sin(q0 + q1), 0.0])
+
+
+@pytest.mark.parametrize("fd", ["forward", "central", "backward"])
+def test_marker_final_goal_closed_form_and_gradient(fd):
+    """testImplicit.cpp:76-79: weight 1000 on |marker1(tf) - (0, 2, 0)|^2
+    (MocoMarkerFinalGoal.cpp:29-34) plus the final-time goal (0.001 tf)."""
+    st = configs.double_pendulum_swingup(5)
+    st.solver.finite_difference_scheme = fd
+    nlp = OracleNLP(st.problem.create_rep(), st.solver.options())
+    for seed in range(3):
+        x = nlp.random_iterate(np.random.default_rng(seed).uniform(-1, 1, nlp.n))
+        x[1] = 2.0
+        kf = 2 + (nlp.G - 1) * nlp.NS
+        tip = _pendulum_tip(x[kf], x[kf + 1])
+        f = 1000.0 * float(np.sum((tip - np.array([0.0, 2.0, 0.0])) ** 2)) + 0.001 * x[1]
+        assert nlp.eval_f(x) == pytest.approx(f, rel=1e-13, abs=1e-12)
+        g = nlp.eval_grad_f(x)
+        gn = _numjac(lambda z: np.array([nlp.eval_f(z)]), x, range(nlp.n))[0]
+        # analytic gradient of the marker term at the final coordinates
+        q0, q1 = x[kf], x[kf + 1]
+        d = tip - np.array([0.0, 2.0, 0.0])
+        J = np.array([[-math.sin(q0) - math.sin(q0 + q1), -math.sin(q0 + q1)],
+                      [math.cos(q0) + math.cos(q0 + q1), math.cos(q0 + q1)]])
+        ga = 2000.0 * d[:2] @ J
+        tol = 1e-5 * np.abs(ga) + 1e-4 * max(1.0, abs(f)) * math.sqrt(st.solver.fd_step)
+        assert np.all(np.abs(g[kf:kf + 2] - ga) <= tol + 2e-3)
+        assert np.allclose(g, gn, rtol=1e-4, atol=2e-3)
+        # only tf and the final coordinates carry gradient
+        nz = set(np.flatnonzero(g))
+        assert nz <= {1, kf, kf + 1}
+
+
+def test_goal_term_indices_validated():
+    """A term index outside its kind's range (controls, states, bodies) is
+    MH_ERR_INVALID at create, in the oracle and in the library's validation
+    (out-of-bounds device reads otherwise)."""
+    st = configs.double_pendulum(3)
+    rep = st.problem.create_rep()
+    for bad in (rep.num_controls, -1, 1000):
+        rep._gidx[0] = bad
+        with pytest.raises(RuntimeError, match="out of range"):
+            OracleNLP(rep, st.solver.options())
+    rep._gidx[0] = 0
+    OracleNLP(rep, st.solver.options())
+    st = configs.double_pendulum_swingup(3)
+    rep = st.problem.create_rep()
+    rep._gidx[0] = 7      # a body that does not exist
+    with pytest.raises(RuntimeError, match="out of range"):
+        OracleNLP(rep, st.solver.options())
