@@ -53,6 +53,65 @@ class MocoHipSolver:
     implicit_multibody_acceleration_bounds: tuple = (-1000.0, 1000.0)
     # implicit_auxiliary_derivative_bounds (MocoDirectCollocationSolver.cpp:41)
     implicit_auxiliary_derivative_bounds: tuple = (-1000.0, 1000.0)
+    # the optimizer settings (MocoDirectCollocationSolver.cpp:23-42), mapped
+    # to Ipopt options by ipopt_options()
+    verbosity: int = 2
+    optim_solver: str = "ipopt"
+    optim_max_iterations: int = -1
+    optim_convergence_tolerance: float = -1.0
+    optim_constraint_tolerance: float = -1.0
+    optim_hessian_approximation: str = "limited-memory"
+    optim_ipopt_print_level: int = -1
+    # guess: a MocoTrajectory (or a .sto path, guess_file), resampled onto
+    # the transcription grid (CasOCTranscription.cpp:593-597); default the
+    # bounds-midpoint guess
+    guess_file: str = ""
+
+    def ipopt_options(self) -> dict:
+        """The Ipopt options MocoCasADiSolver sets from these properties
+        (MocoCasADiSolver.cpp:210-246, incl. its range checks), for a host
+        Ipopt driving the C ABI (csrc/host/mh_ipopt_tnlp.hpp
+        applies the same mapping)."""
+        if self.optim_max_iterations < 0 and self.optim_max_iterations != -1:
+            raise ValueError("optim_max_iterations must be >= 0 or -1")
+        for name in ("optim_convergence_tolerance", "optim_constraint_tolerance"):
+            v = getattr(self, name)
+            if v < 0 and v != -1:
+                raise ValueError(f"{name} must be >= 0 or -1")
+        if self.verbosity not in (0, 1, 2):
+            raise ValueError("verbosity must be 0, 1 or 2")
+        opts: dict = {}
+        if self.optim_solver != "ipopt":
+            return opts
+        opts["print_user_options"] = "yes"
+        if self.verbosity < 2:
+            opts["print_level"] = 0
+        elif self.optim_ipopt_print_level != -1:
+            opts["print_level"] = int(self.optim_ipopt_print_level)
+        opts["hessian_approximation"] = self.optim_hessian_approximation
+        if self.optim_max_iterations != -1:
+            opts["max_iter"] = int(self.optim_max_iterations)
+        if self.optim_convergence_tolerance != -1:
+            tol = float(self.optim_convergence_tolerance)
+            for k in ("tol", "dual_inf_tol", "compl_inf_tol", "acceptable_tol",
+                      "acceptable_dual_inf_tol", "acceptable_compl_inf_tol"):
+                opts[k] = tol
+        if self.optim_constraint_tolerance != -1:
+            tol = float(self.optim_constraint_tolerance)
+            opts["constr_viol_tol"] = tol
+            opts["acceptable_constr_viol_tol"] = tol
+        return opts
+
+    def starting_point(self, nlp, guess=None) -> np.ndarray:
+        """IPOPT's starting point for ``nlp``: ``guess`` (a MocoTrajectory),
+        else ``guess_file`` (.sto), resampled onto the grid; else the
+        bounds-midpoint guess (CasOCTranscription.cpp:1123-1149)."""
+        from .trajectory import MocoTrajectory
+        if guess is None and self.guess_file:
+            guess = MocoTrajectory.read(self.guess_file)
+        if guess is None:
+            return nlp.initial_guess_from_bounds()
+        return guess.to_iterate(nlp)
 
     def options(self, interval_begin: int = 0, interval_end: int = 0) -> abi.mh_options:
         if self.transcription_scheme not in _SCHEMES:

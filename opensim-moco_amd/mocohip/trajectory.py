@@ -1,0 +1,295 @@
+"""MocoTrajectory: the solver's guess / solution container, its ``.sto``
+file format and its resampling, plus the conversion to and from the NLP
+iterate x the C ABI consumes.
+
+Reference behaviour restated here:
+  * columns = states, controls, multipliers, derivatives, slacks, parameters,
+    in that order (MocoTrajectory::convertToTable, MocoTrajectory.cpp:
+    786-800); parameters fill the first row, NaN below (:830-838);
+  * header keys num_states / num_controls / num_multipliers /
+    num_derivatives / num_slacks / num_parameters (read back by the file
+    constructor, MocoTrajectory.cpp:662-700, and required to add up to the
+    column count, :719-731);
+  * resample(time) (:581-660): slack NaNs are first filled by linear
+    interpolation, then every column is re-evaluated from a GCVSplineSet of
+    degree min(#times - 1, 5) (zero error variance: the interpolating natural
+    spline of ``splines.gcv_interpolating_ppoly``); new times must lie within
+    the old ones and be non-decreasing; a zero-duration trajectory is
+    broadcast from its first row;
+  * the guess handed to the transcription is the trajectory resampled at the
+    grid times t0 + (tf - t0) grid (CasOCTranscription.cpp:593-597).
+
+The ``.sto`` writer prints 17 significant digits (a lossless round trip);
+the reference's TimeSeriesTable writer prints fewer, which any reader
+(this one included) parses the same way.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+from .splines import gcv_interpolating_ppoly, ppoly_eval
+
+_BLOCKS = ("states", "controls", "multipliers", "derivatives", "slacks", "parameters")
+
+
+@dataclass
+class MocoTrajectory:
+    time: np.ndarray
+    state_names: List[str] = field(default_factory=list)
+    control_names: List[str] = field(default_factory=list)
+    multiplier_names: List[str] = field(default_factory=list)
+    derivative_names: List[str] = field(default_factory=list)
+    slack_names: List[str] = field(default_factory=list)
+    parameter_names: List[str] = field(default_factory=list)
+    states: Optional[np.ndarray] = None        # [ntime, nstates]
+    controls: Optional[np.ndarray] = None
+    multipliers: Optional[np.ndarray] = None
+    derivatives: Optional[np.ndarray] = None
+    slacks: Optional[np.ndarray] = None
+    parameters: Optional[np.ndarray] = None    # [nparameters]
+    metadata: Dict[str, str] = field(default_factory=dict)
+
+    def __post_init__(self):
+        self.time = np.asarray(self.time, float)
+        nt = len(self.time)
+        for b in _BLOCKS[:-1]:
+            names = getattr(self, b[:-1] + "_names")
+            arr = getattr(self, b)
+            arr = np.zeros((nt, len(names))) if arr is None else np.asarray(arr, float).reshape(nt, len(names))
+            setattr(self, b, arr)
+        p = np.zeros(len(self.parameter_names)) if self.parameters is None else self.parameters
+        self.parameters = np.asarray(p, float).reshape(len(self.parameter_names))
+
+    # -------------------------------------------------------------- access
+    @property
+    def num_times(self) -> int:
+        return len(self.time)
+
+    def labels(self) -> List[str]:
+        return (self.state_names + self.control_names + self.multiplier_names +
+                self.derivative_names + self.slack_names + self.parameter_names)
+
+    def get_state(self, name: str) -> np.ndarray:
+        return self.states[:, self.state_names.index(name)]
+
+    def get_control(self, name: str) -> np.ndarray:
+        return self.controls[:, self.control_names.index(name)]
+
+    def set_state(self, name: str, values: Sequence[float]):
+        self.states[:, self.state_names.index(name)] = np.asarray(values, float)
+
+    def set_control(self, name: str, values: Sequence[float]):
+        self.controls[:, self.control_names.index(name)] = np.asarray(values, float)
+
+    def table(self) -> np.ndarray:
+        """convertToTable's data block [ntime, ncolumns] (parameters in the
+        first row, NaN below)."""
+        nt = self.num_times
+        par = np.full((nt, len(self.parameter_names)), np.nan)
+        if nt and len(self.parameter_names):
+            par[0] = self.parameters
+        return np.hstack([self.states, self.controls, self.multipliers, self.derivatives,
+                          self.slacks, par]) if nt else np.zeros((0, len(self.labels())))
+
+    # -------------------------------------------------------------- .sto I/O
+    def write(self, path: str, name: str = "MocoTrajectory"):
+        counts = {"num_states": len(self.state_names), "num_controls": len(self.control_names),
+                  "num_multipliers": len(self.multiplier_names),
+                  "num_derivatives": len(self.derivative_names),
+                  "num_slacks": len(self.slack_names), "num_parameters": len(self.parameter_names)}
+        meta = dict(self.metadata)
+        for k, v in counts.items():
+            meta[k] = str(v)
+        lines = [name]
+        for k in sorted(meta):
+            lines.append(f"{k}={meta[k]}")
+        lines += ["DataType=double", "version=3", "endheader", "\t".join(["time"] + self.labels())]
+        data = self.table()
+        for i in range(self.num_times):
+            lines.append("\t".join(_num(v) for v in [self.time[i]] + list(data[i])))
+        with open(path, "w") as fh:
+            fh.write("\n".join(lines) + "\n")
+
+    @staticmethod
+    def read(path: str) -> "MocoTrajectory":
+        header: Dict[str, str] = {}
+        with open(path) as fh:
+            lines = fh.read().splitlines()
+        i = 0
+        while i < len(lines) and lines[i].strip().lower() != "endheader":
+            if "=" in lines[i]:
+                k, v = lines[i].split("=", 1)
+                header[k.strip()] = v.strip()
+            i += 1
+        if i >= len(lines):
+            raise ValueError(f"{path}: no endheader")
+        labels = [s.strip() for s in lines[i + 1].split("\t") if s.strip() != ""]
+        if not labels or labels[0] != "time":
+            raise ValueError(f"{path}: first column must be time")
+        labels = labels[1:]
+        rows = [[float(v) for v in ln.split()] for ln in lines[i + 2:] if ln.strip()]
+        data = np.array(rows, float).reshape(len(rows), len(labels) + 1)
+        counts = []
+        for key in ("num_states", "num_controls", "num_multipliers", "num_derivatives",
+                    "num_slacks", "num_parameters"):
+            if key not in header:
+                raise ValueError(f"{path}: header has no {key}")
+            v = int(header[key])
+            if v < 0:
+                raise ValueError(f"Invalid {key}.")
+            counts.append(v)
+        if sum(counts) != len(labels):
+            raise ValueError("Expected num_states + num_controls + num_multipliers + num_derivatives "
+                             "+ num_slacks + num_parameters = number of columns, but "
+                             f"{counts} sum to {sum(counts)} != {len(labels)}.")
+        names, blocks, off = [], [], 0
+        for n in counts:
+            names.append(labels[off:off + n])
+            blocks.append(data[:, 1 + off:1 + off + n])
+            off += n
+        meta = {k: v for k, v in header.items()
+                if not k.startswith("num_") and k not in ("DataType", "version")}
+        return MocoTrajectory(data[:, 0], *names, *blocks[:5],
+                              parameters=blocks[5][0] if len(data) else np.zeros(counts[5]),
+                              metadata=meta)
+
+    # -------------------------------------------------------------- resample
+    def resample(self, time: Sequence[float]) -> "MocoTrajectory":
+        """MocoTrajectory::resample (MocoTrajectory.cpp:581-660); in place,
+        returns self."""
+        time = np.asarray(time, float)
+        if self.num_times < 2:
+            raise ValueError("Cannot resample if number of times is 0 or 1.")
+        if time[0] < self.time[0]:
+            raise ValueError(f"New initial time ({time[0]}) cannot be less than existing initial "
+                             f"time ({self.time[0]})")
+        if time[-1] > self.time[-1]:
+            raise ValueError(f"New final time ({time[-1]}) cannot be less than existing final time "
+                             f"({self.time[-1]})")
+        if np.any(np.diff(time) < 0):
+            raise ValueError("New times must be non-decreasing.")
+        # slack NaNs: linear interpolation over the valid samples (:606-610)
+        for c in range(self.slacks.shape[1]):
+            col = self.slacks[:, c]
+            ok = ~np.isnan(col)
+            if ok.any() and not ok.all():
+                self.slacks[:, c] = np.interp(self.time, self.time[ok], col[ok])
+        data = np.hstack([self.states, self.controls, self.multipliers, self.derivatives,
+                          self.slacks])
+        nt = len(time)
+        if time[-1] == time[0]:
+            new = np.repeat(data[:1], nt, axis=0)
+        else:
+            degree = min(self.num_times - 1, 5)
+            if degree % 2 == 0:
+                # GCVSplineSet(table, {}, min(n - 1, 5)) hands GCVSpline an
+                # even degree here, which it rejects (odd degrees only)
+                raise ValueError(f"GCVSpline degree must be odd (got {degree} for "
+                                 f"{self.num_times} times)")
+            new = np.zeros((nt, data.shape[1]))
+            if data.shape[1]:
+                br, co = gcv_interpolating_ppoly(self.time, data, degree)
+                for c in range(data.shape[1]):
+                    new[:, c] = ppoly_eval(br, co, time, c)
+        self.time = time
+        off = 0
+        for b in _BLOCKS[:-1]:
+            n = getattr(self, b).shape[1]
+            setattr(self, b, new[:, off:off + n].copy())
+            off += n
+        return self
+
+    def resample_with_num_times(self, num_times: int) -> "MocoTrajectory":
+        """resampleWithNumTimes: uniformly spaced over the current span."""
+        return self.resample(np.linspace(self.time[0], self.time[-1], int(num_times)))
+
+    # -------------------------------------------------------------- NLP iterate
+    def to_iterate(self, nlp) -> np.ndarray:
+        """The iterate x of ``nlp`` (HipNLP / OracleNLP: its problem's state
+        and control names, derivative count and transcription grid): t0 / tf
+        from the trajectory's first and last times, every block resampled at
+        the grid times (CasOCTranscription.cpp:593-597; columns matched by
+        name as convertToCasOCIterate does).  Derivative variables are taken
+        in order; missing ones are zero."""
+        rep = nlp.rep
+        grid = nlp_grid(nlp)
+        t0, tf = float(self.time[0]), float(self.time[-1])
+        times = (tf - t0) * grid + t0
+        r = MocoTrajectory(self.time.copy(), list(self.state_names), list(self.control_names),
+                           list(self.multiplier_names), list(self.derivative_names),
+                           list(self.slack_names), list(self.parameter_names),
+                           self.states.copy(), self.controls.copy(), self.multipliers.copy(),
+                           self.derivatives.copy(), self.slacks.copy(), self.parameters.copy())
+        r.resample(times)
+        G, ndv = len(grid), nlp.NDV
+        S = np.zeros((G, nlp.NS))
+        for i, n in enumerate(rep.state_names):
+            if n not in self.state_names:
+                raise ValueError(f"guess has no state '{n}'")
+            S[:, i] = r.states[:, self.state_names.index(n)]
+        Cm = np.zeros((G, nlp.NC))
+        for j, n in enumerate(rep.control_names):
+            if n not in self.control_names:
+                raise ValueError(f"guess has no control '{n}'")
+            Cm[:, j] = r.controls[:, self.control_names.index(n)]
+        D = np.zeros((G, ndv))
+        for j in range(min(ndv, r.derivatives.shape[1])):
+            D[:, j] = r.derivatives[:, j]
+        return np.concatenate([[t0, tf], S.ravel(), Cm.ravel(), D.ravel()])
+
+    @staticmethod
+    def from_iterate(nlp, x: np.ndarray) -> "MocoTrajectory":
+        """The trajectory an iterate x of ``nlp`` describes (times
+        t0 + (tf - t0) grid)."""
+        rep = nlp.rep
+        grid = nlp_grid(nlp)
+        G, ns, nc, ndv = len(grid), nlp.NS, nlp.NC, nlp.NDV
+        x = np.asarray(x, float)
+        if len(x) != 2 + (ns + nc + ndv) * G:
+            raise ValueError("iterate size does not match the problem and grid")
+        t0, tf = x[0], x[1]
+        S = x[2:2 + ns * G].reshape(G, ns)
+        Cm = x[2 + ns * G:2 + (ns + nc) * G].reshape(G, nc)
+        D = x[2 + (ns + nc) * G:].reshape(G, ndv)
+        dn = [f"derivative_{j}" for j in range(ndv)]
+        return MocoTrajectory((tf - t0) * grid + t0, list(rep.state_names), list(rep.control_names),
+                              [], dn, [], [], S, Cm, None, D)
+
+    def is_numerically_equal(self, other: "MocoTrajectory", tol: float = 1e-12) -> bool:
+        if self.labels() != other.labels() or self.num_times != other.num_times:
+            return False
+        a, b = self.table(), other.table()
+        return bool(np.allclose(self.time, other.time, rtol=0, atol=tol) and
+                    np.allclose(a, b, rtol=0, atol=tol, equal_nan=True))
+
+
+def nlp_grid(nlp) -> np.ndarray:
+    from . import abi
+    scheme = "hermite-simpson" if nlp.opts.transcription == abi.MH_HERMITE_SIMPSON else "trapezoidal"
+    return transcription_grid(scheme, nlp.opts.num_mesh_intervals)
+
+
+def transcription_grid(scheme: str, num_mesh_intervals: int) -> np.ndarray:
+    """Normalized grid of the transcription (uniform mesh, CasOCSolver.h:
+    38-42; Hermite-Simpson adds the interval midpoints, CasOCHermiteSimpson.h:
+    45-68)."""
+    N = int(num_mesh_intervals)
+    mesh = np.array([i / N for i in range(N + 1)])
+    if scheme == "trapezoidal":
+        return mesh
+    g = np.zeros(2 * N + 1)
+    g[0::2] = mesh
+    g[1::2] = 0.5 * (mesh[:-1] + mesh[1:])
+    return g
+
+
+def _num(v: float) -> str:
+    if math.isnan(v):
+        return "NaN"
+    if math.isinf(v):
+        return "Inf" if v > 0 else "-Inf"
+    return repr(float(v))

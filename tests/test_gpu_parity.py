@@ -47,7 +47,7 @@ def _nointerp(st):
 
 
 def _central(st):
-    st.solver.finite_difference_scheme = "central"
+    st.solver.optim_finite_difference_scheme = "central"
     return st
 
 

@@ -968,7 +968,7 @@ def test_marker_final_goal_closed_form_and_gradient(fd):
     """testImplicit.cpp:76-79: weight 1000 on |marker1(tf) - (0, 2, 0)|^2
     (MocoMarkerFinalGoal.cpp:29-34) plus the final-time goal (0.001 tf)."""
     st = configs.double_pendulum_swingup(5)
-    st.solver.finite_difference_scheme = fd
+    st.solver.optim_finite_difference_scheme = fd
     nlp = OracleNLP(st.problem.create_rep(), st.solver.options())
     for seed in range(3):
         x = nlp.random_iterate(np.random.default_rng(seed).uniform(-1, 1, nlp.n))
