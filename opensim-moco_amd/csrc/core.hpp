@@ -493,6 +493,8 @@ struct Interval {
     double* vh;
     int dbg_stop;    // diagnostic timing build only: return after phase n (0: full)
     int pf;          // k_interval prefetches its first IV_PF assembly words per thread
+    int qfuse;       // k_interval forms each finite-difference quotient in the assembly
+                     // (no in-place quotient pass)
     // Every interval opens with its mesh point's path rows.  The interval
     // N-1 also owns the tail (flattenConstraints, CasOCTranscription.h:
     // 286-308): the final mesh point's path rows, then the final grid
@@ -905,8 +907,8 @@ __global__ void __launch_bounds__(1024) k_interval(DevModel M, Src S, Lanes Ln, 
         LaneInL<D> in{lds(sXs + p * L.NS), lds(sXc + p * L.NC), lds(sXd + p * L.NDV), -1, 0.0};
         const double t = lane_time(Ln, S.grid[k_first + p], t0, tf, r, in.pi, in.step);
         if (r == Ln.base) sTimes[p] = t;
-        const TaskLoadLds<D> TL{lds(sT + p * nt), lds(sH + p * nh), TK.jd, r};
         double out[D::NO];
+        const TaskLoadLds<D> TL{lds(sT + p * nt), lds(sH + p * nh), TK.jd, r};
         D::combine(M, t, in, TL, out);
         lds_double* Yp = lds(sY + p * ny + r);
 #pragma unroll
@@ -935,7 +937,7 @@ __global__ void __launch_bounds__(1024) k_interval(DevModel M, Src S, Lanes Ln, 
     // per (point, output, direction) instead of once per Jacobian entry that
     // reads them; the base slot keeps the raw value for the defect rows
     if (I.dbg_stop == 2) return;
-    const int quot = values && Ln.stride > 1;
+    const int quot = values && Ln.stride > 1 && !I.qfuse;
     if (quot) {
 #pragma clang fp contract(off)
         // one (point, output) row of lanes per wave: lanes = directions
@@ -991,6 +993,24 @@ __global__ void __launch_bounds__(1024) k_interval(DevModel M, Src S, Lanes Ln, 
             const lds_double* q0 = lds(sY);
             // coefficient / base of a word, selected in registers
             const double c1 = -C.h8, c2 = C.h8, c3 = -C.h6, c4 = -C.h6 * 4.0, c5 = -C.hh;
+            // I.qfuse: the word's LDS offset names the raw value of the
+            // perturbed lane; the quotient (CasADi FiniteDiff) is formed here
+            // from it and its row's base (forward / backward) or mirror
+            // (central) lane -- the quotient pass's arithmetic, bit for bit
+            const int nyall = npts * ny;
+            const int fuse = values && Ln.stride > 1 && I.qfuse;
+            const float inv_stride = 1.0f / (float)Ln.stride;
+            const double h1 = Ln.h, h2 = 2.0 * Ln.h;
+            auto qat = [&](uint32_t off) -> double {
+                const double y = q0[off];
+                if (!fuse || (int)off >= nyall) return y;
+                if (Ln.fd == MH_FD_CENTRAL) return (y - q0[off + Ln.ND]) / h2;
+                int row = (int)((float)off * inv_stride);
+                row += (row + 1) * Ln.stride <= (int)off ? 1 : 0;
+                row -= row * Ln.stride > (int)off ? 1 : 0;
+                const double yb = q0[row * Ln.stride + Ln.base];
+                return Ln.fd == MH_FD_FORWARD ? (y - yb) / h1 : (yb - y) / h1;
+            };
             auto value = [&](uint32_t wu, double q) {
                 const uint32_t ks = (wu >> 20) & 7, bs = (wu >> 23) & 7;
                 const double coef = ks == 1 ? c1 : ks == 2 ? c2 : ks == 3 ? c3 : ks == 4 ? c4 : ks == 5 ? c5 : 0.0;
@@ -1002,7 +1022,7 @@ __global__ void __launch_bounds__(1024) k_interval(DevModel M, Src S, Lanes Ln, 
             // entries are written by the loops below
 #pragma unroll
             for (int u = 0; u < IV_PF; ++u)
-                if (!(pw[u] & (CT_GEN | CT_PATH))) vi[e + u * B] = value(pw[u], q0[pw[u] & CT_OFF]);
+                if (!(pw[u] & (CT_GEN | CT_PATH))) vi[e + u * B] = value(pw[u], qat(pw[u] & CT_OFF));
             if (I.pf) e += IV_PF * B;
             for (; e + (IV_UNROLL - 1) * B < ne; e += IV_UNROLL * B) {
                 uint32_t w[IV_UNROLL];
@@ -1010,14 +1030,14 @@ __global__ void __launch_bounds__(1024) k_interval(DevModel M, Src S, Lanes Ln, 
 #pragma unroll
                 for (int u = 0; u < IV_UNROLL; ++u) w[u] = ctpl[e + u * B];
 #pragma unroll
-                for (int u = 0; u < IV_UNROLL; ++u) q[u] = q0[w[u] & CT_OFF];
+                for (int u = 0; u < IV_UNROLL; ++u) q[u] = qat(w[u] & CT_OFF);
 #pragma unroll
                 for (int u = 0; u < IV_UNROLL; ++u)
                     if (!(w[u] & (CT_GEN | CT_PATH))) vi[e + u * B] = value(w[u], q[u]);
             }
             for (; e < ne; e += B) {
                 const uint32_t wu = ctpl[e];
-                if (!(wu & (CT_GEN | CT_PATH))) vi[e] = value(wu, q0[wu & CT_OFF]);
+                if (!(wu & (CT_GEN | CT_PATH))) vi[e] = value(wu, qat(wu & CT_OFF));
             }
             if (eg0 >= 0) vi[eg0] = jac_entry<false>(L, Ln, I.P, S.x, YV, tg0, k_first, C);
             for (int j = threadIdx.x + (I.pf ? B : 0); j < nctgen; j += B) {
@@ -1585,6 +1605,7 @@ struct mh_ctx {
     bool async = false;                // *_device entries return once enqueued
     int iv_dbg_stop = 0;               // diagnostic: k_interval stops after phase n
     int iv_pf = 1;                     // MOCOHIP_IV_PF=0: no assembly-word prefetch (A/B)
+    int iv_qfuse = 1;                  // MOCOHIP_IV_QFUSE=0: in-place quotient pass (A/B)
     hipEvent_t ev[5] = {};         // stage boundaries (+ ev[4] after k_groups)
     char* dmem = nullptr;
     DevModel M{};
@@ -1609,6 +1630,7 @@ struct mh_ctx {
     bool has_marker = false;
     bool use_roles = false;        // MOCOHIP_ROLES=1: k_role (+ k_couple) for the Jacobian lanes
     int role_threads = 256;        // k_role workgroup size (MOCOHIP_ROLE_THREADS: 64..512)
+    int iv_threads = 1024;         // k_interval workgroup size, Jacobian lanes (MOCOHIP_IV_THREADS: 256..1024)
     bool role_couple = true;       // coupling in k_role's time role (MOCOHIP_ROLE_COUPLE=0: k_couple)
     bool use_ctpl = true;          // MOCOHIP_CTPL=0: k_interval assembles through jac_entry
     float timings[4] = {0, 0, 0, 0};
@@ -1639,7 +1661,7 @@ struct mh_ctx {
 // block writes through I.gh / I.vh when this shard owns it.
 inline Interval make_interval(const mh_ctx* c, double*& g, double*& v) {
     Interval I{c->scheme, c->interp, c->ib, c->rpi, c->nnz_int, c->NMB + c->NAR, c->NMB, c->NQ + c->NZ,
-               c->N, c->nnz_tail, c->ntail, c->npe, c->P, c->E, nullptr, nullptr, c->iv_dbg_stop, c->iv_pf};
+               c->N, c->nnz_tail, c->ntail, c->npe, c->P, c->E, nullptr, nullptr, c->iv_dbg_stop, c->iv_pf, c->iv_qfuse};
     if (c->ib == 0 && c->nep > 0) {
         I.gh = g;
         I.vh = v;
@@ -1766,11 +1788,11 @@ static void be_interval(mh_ctx* c, const double* x, int mode, double* g, double*
         return;
     }
     const size_t lds = interval_lds<D>(c, ln, ts);
+    auto kern = k_interval<D>;
     if (lds > 65536)
-        (void)hipFuncSetAttribute((const void*)k_interval<D>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                (int)lds);
-    const unsigned threads = v ? 1024u : 256u;
-    hipLaunchKernelGGL(k_interval<D>, dim3((unsigned)(c->ie - c->ib)), dim3(threads), lds, c->stream, c->M,
+        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    const unsigned threads = v ? (unsigned)c->iv_threads : 256u;
+    hipLaunchKernelGGL(kern, dim3((unsigned)(c->ie - c->ib)), dim3(threads), lds, c->stream, c->M,
             S, ln, ts.dev, L, I, c->d_tpl, (mode == 1 && c->use_ctpl) ? c->d_ctpl : nullptr, c->d_ctgen,
             (int)c->ctgen.size(), c->d_T, c->d_H, g, v);
 }

@@ -309,8 +309,9 @@ void simm_coefficients(int n, const double* x, const double* y, double* b, doubl
     if (n > 3) {
         const double d1 = c[2] / (x[3] - x[1]) - c[1] / (x[2] - x[0]);
         const double d2 = c[nm1 - 1] / (x[nm1] - x[n - 3]) - c[n - 3] / (x[nm1 - 1] - x[n - 4]);
-        c[0] = d[0] * d1 / (x[3] - x[0]);
-        c[nm1] = -d[n - 2] * d2 / (x[nm1] - x[n - 4]);
+        // third-derivative end conditions, d(1)**2 and d(n-1)**2 (FMM spline)
+        c[0] = d1 * d[0] * d[0] / (x[3] - x[0]);
+        c[nm1] = -(d2 * d[n - 2] * d[n - 2]) / (x[nm1] - x[n - 4]);
     }
     for (int i = 1; i < n; ++i) {
         const double t = d[i - 1] / b[i - 1];
@@ -1244,6 +1245,10 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
         c->use_roles = er && std::strcmp(er, "1") == 0;   // measured slower
         const char* et = std::getenv("MOCOHIP_ROLE_THREADS");
         if (et) c->role_threads = std::min(512, std::max(64, std::atoi(et) / 64 * 64));
+        const char* eqf = std::getenv("MOCOHIP_IV_QFUSE");
+        c->iv_qfuse = !(eqf && std::strcmp(eqf, "0") == 0);   // default: measured faster
+        const char* eth = std::getenv("MOCOHIP_IV_THREADS");
+        if (eth) c->iv_threads = std::min(1024, std::max(256, std::atoi(eth) / 64 * 64));
         const char* eo = std::getenv("MOCOHIP_ROLE_COUPLE");
         c->role_couple = !(eo && std::strcmp(eo, "0") == 0);
         const char* ea = std::getenv("MOCOHIP_ASM");

@@ -103,8 +103,8 @@ class SimmSpline:
             if n > 3:
                 d1 = c[2] / (x[3] - x[1]) - c[1] / (x[2] - x[0])
                 d2 = c[nm1 - 1] / (x[nm1] - x[n - 3]) - c[n - 3] / (x[nm1 - 1] - x[n - 4])
-                c[0] = d[0] * d1 / (x[3] - x[0])
-                c[nm1] = -d[n - 2] * d2 / (x[nm1] - x[n - 4])
+                c[0] = d1 * d[0] * d[0] / (x[3] - x[0])
+                c[nm1] = -(d2 * d[n - 2] * d[n - 2]) / (x[nm1] - x[n - 4])
             for i in range(1, n):
                 t = d[i - 1] / b[i - 1]
                 b[i] -= t * d[i - 1]

@@ -166,8 +166,10 @@ static void simm_coefficients(int n, const double* x, const double* y,
                     c[n - 3] / (x[nm1 - 1] - x[n - 4]);
         double d31 = x[3] - x[0];
         double d32 = x[nm1] - x[n - 4];
-        c[0] = d[0] * d1 / d31;
-        c[nm1] = -d[n - 2] * d2 / d32;
+        /* d(1)**2 and d(n-1)**2 of the FMM routine (SimmSpline.cpp
+         * calcCoefficients: _c[0] * _d[0] * _d[0] / d30) */
+        c[0] = d1 * d[0] * d[0] / d31;
+        c[nm1] = -(d2 * d[n - 2] * d[n - 2]) / d32;
     }
     for (int i = 1; i < n; ++i) {
         double t = d[i - 1] / b[i - 1];

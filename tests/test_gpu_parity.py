@@ -251,7 +251,8 @@ def _pair(name, backend="auto", tasks=None, env=None):
     opts = st.solver.options()
     saved = {k: os.environ.pop(k, None) for k in ("MOCOHIP_BACKEND", "MOCOHIP_TASKS", "MOCOHIP_INTERVAL",
                                                   "MOCOHIP_ASM", "MOCOHIP_QUOT", "MOCOHIP_CTPL",
-                                                  "MOCOHIP_ROLES", "MOCOHIP_ROLE_COUPLE")}
+                                                  "MOCOHIP_ROLES", "MOCOHIP_ROLE_COUPLE",
+                                                  "MOCOHIP_IV_QFUSE", "MOCOHIP_IV_THREADS")}
     if backend != "auto":
         os.environ["MOCOHIP_BACKEND"] = backend
     if tasks:
@@ -620,7 +621,10 @@ def test_pruned_tasks_bit_identical(name):
                                      {"MOCOHIP_INTERVAL": "0", "MOCOHIP_QUOT": "1"},
                                      {"MOCOHIP_CTPL": "0"},
                                      {"MOCOHIP_ROLES": "1"},
-                                     {"MOCOHIP_ROLES": "1", "MOCOHIP_ROLE_COUPLE": "0"}])
+                                     {"MOCOHIP_ROLES": "1", "MOCOHIP_ROLE_COUPLE": "0"},
+                                     {"MOCOHIP_IV_THREADS": "512"},
+                                     {"MOCOHIP_IV_QFUSE": "0"},
+                                     {"MOCOHIP_IV_QFUSE": "0", "MOCOHIP_CTPL": "0"}])
 def test_kernel_variants_bit_identical(name, variant):
     """The default k_interval (combine + transcription per mesh interval,
     raw outputs in LDS) writes exactly what k_interval writes through
