@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define MH_ABI_VERSION 3
+#define MH_ABI_VERSION 4
 
 enum mh_status {
     MH_OK = 0,
@@ -184,6 +184,27 @@ typedef struct mh_external_force {
     int32_t reserved;
 } mh_external_force;
 
+/* Kinematic constraints (CasOCTranscription.cpp:298-333,
+ * MocoCasOCProblem.h:298-332,570-732).  OpenSim CoordinateCouplerConstraint
+ * with one independent coordinate: the Simbody CoordinateCoupler of the
+ * function  phi(q) = scale * f(q[f.coord]) - q[dependent]  (OpenSim's
+ * CompoundFunction; f = functions[func], itself possibly a
+ * MultiplierFunction).  One holonomic equation: position error phi,
+ * velocity error  scale f'(q_i) u_i - u_d,  acceleration error
+ * scale f'(q_i) udot_i - udot_d + scale f''(q_i) u_i u_i;  constraint
+ * Jacobian row G = d phi / d q (mobility space: qdot = u); the multiplier
+ * lambda adds  -G^T lambda  to the applied generalized forces (Moco negates
+ * the multipliers so that Simbody's constraint forces act as applied
+ * forces, MocoCasOCProblem.h:643-662). */
+enum mh_constraint_kind { MH_KC_COORDINATE_COUPLER = 0 };
+typedef struct mh_constraint {
+    int32_t kind;        /* mh_constraint_kind                              */
+    int32_t dependent;   /* coordinate index of the dependent coordinate    */
+    int32_t func;        /* index into mh_model.functions (non-constant)    */
+    int32_t reserved;
+    double scale;        /* CoordinateCouplerConstraint scale_factor        */
+} mh_constraint;
+
 typedef struct mh_model {
     int32_t nq;          /* coordinates (= speeds)                          */
     int32_t nbodies;
@@ -210,6 +231,9 @@ typedef struct mh_model {
     const double* table_breaks;
     const double* table_coefs;
     const mh_external_force* external;
+    int32_t nconstraints;   /* enabled kinematic constraints (ABI v4)        */
+    int32_t reserved_kc;
+    const mh_constraint* constraints;
 } mh_model;
 
 /* ------------------------------------------------------------------------ */
@@ -335,6 +359,14 @@ typedef struct mh_problem {
     int32_t nendpoint;           /* endpoint-constraint equations (rows 0..) */
     int32_t reserved2;
     const mh_endpoint_equation* endpoint;
+    /* Kinematic constraints (model.nconstraints > 0): MocoPhase
+     * multiplier_bounds (bounds of the Lagrange multipliers at every grid
+     * point, initial and final alike; NaN/NaN = the reference default
+     * [-1000, 1000], MocoProblem.cpp:43, MocoProblemRep.cpp:162-165) and
+     * kinematic_constraint_bounds (bounds of every kinematic-constraint row;
+     * NaN/NaN = the default [0, 0], MocoProblem.cpp:42). */
+    mh_bounds multiplier_bounds;
+    mh_bounds kinematic_constraint_bounds;
 } mh_problem;
 
 enum mh_scheme { MH_HERMITE_SIMPSON = 0, MH_TRAPEZOIDAL = 1 };
@@ -389,6 +421,18 @@ typedef struct mh_options {
      * (DGF normalized tendon force with tendon_dynamics_implicit); {0, 0} =
      * the reference default [-1000, 1000]. */
     double implicit_aux_bounds[2];
+    /* Kinematic constraints (ABI v4; MocoDirectCollocationSolver.cpp:29-42).
+     * enforce_constraint_derivatives (reference default true): 0 = enforce
+     * (position, velocity and acceleration errors as rows at every mesh
+     * point; one slack "gamma" per multiplier at every mesh-interval
+     * midpoint of Hermite-Simpson, whose velocity correction G^T gamma is
+     * added to qdot there, CasOCTranscription.cpp:316-333), 1 = do not
+     * (position errors only, no slacks).  velocity_correction_bounds: slack
+     * bounds, {0, 0} = the default [-0.1, 0.1].  minimize_lagrange_multipliers
+     * is not implemented (MH_ERR_UNSUPPORTED if nonzero). */
+    int32_t ignore_constraint_derivatives;
+    int32_t minimize_lagrange_multipliers;
+    double velocity_correction_bounds[2];
 } mh_options;
 
 enum mh_sparsity {

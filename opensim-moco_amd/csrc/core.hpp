@@ -82,13 +82,21 @@ struct GenericDae {
 };
 
 struct Layout {
-    int NS, NC, NQ, NO, NI;  // NI = NS + NC + NDV
+    int NS, NC, NQ, NO, NI;  // NI = NS + NC + NDV + NM + NSL (per-point inputs)
     int G;                   // grid points (full problem)
     int k0;                  // first grid point of this shard
     int nk;                  // grid points in this shard
     int NDV;                 // derivative variables per grid point: accelerations, aux derivatives
     int NACC;                // acceleration variables per grid point (implicit multibody: NQ)
     int SO;                  // callback output of state s's derivative: s + SO (s >= NQ)
+    // kinematic constraints: NM multipliers per grid point, NSL slacks per
+    // mesh interval (inputs of its midpoint only; NSL > 0 only with
+    // Hermite-Simpson); OQC = callback output of the velocity correction
+    int NM, NSL, OQC;
+    long XM, XL, DB;         // x index of the multipliers, slacks, derivatives
+    // the slack inputs of grid point k (global index): the interval's at a
+    // mesh-interval midpoint (odd k), none elsewhere
+    __host__ __device__ __forceinline__ bool vc(int k) const { return NSL > 0 && (k & 1); }
 };
 
 // Per grid point the evaluation lanes are laid out as
@@ -110,13 +118,18 @@ __device__ __forceinline__ void load_point(const double* __restrict__ x, const L
         double (&in)[D::MI]) {
     const double* xs = x + 2 + (long)k * L.NS;
     const double* xc = x + 2 + (long)L.NS * L.G + (long)k * L.NC;
-    const double* xd = x + 2 + (long)(L.NS + L.NC) * L.G + (long)k * L.NDV;
+    const double* xd = x + L.DB + (long)k * L.NDV;
+    const double* xm = x + L.XM + (long)k * L.NM;
+    const double* xl = x + L.XL + (long)((k - 1) >> 1) * L.NSL;
+    const int id = L.NS + L.NC + L.NDV, im = id + L.NM;
 #pragma unroll
     for (int i = 0; i < D::MI; ++i) {
         double v = 0.0;
         if (i < L.NS) v = xs[i];
         else if (i < L.NS + L.NC) v = xc[i - L.NS];
-        else if (i < L.NI) v = xd[i - L.NS - L.NC];
+        else if (i < id) v = xd[i - L.NS - L.NC];
+        else if (i < im) v = xm[i - id];
+        else if (i < L.NI && L.vc(k)) v = xl[i - im];
         in[i] = v;
     }
 }
@@ -485,6 +498,8 @@ struct Interval {
     int nnz_tail;    // nonzeros of the tail rows
     int ntail;       // tail rows: final mesh point's path rows + final residuals
     int npe;         // path-constraint entries per mesh point (lead the interval / tail)
+    int nkr;         // kinematic-constraint rows per mesh point (first in the interval / tail)
+    int okc;         // callback output of the first kinematic error
     PathEqs P;
     // the head (endpoint rows), written by the first interval's block when
     // this shard owns it: gh / vh = the shard's g / values (null otherwise)
@@ -569,7 +584,7 @@ __device__ __forceinline__ long ep_xindex(const Layout& L, int W, int si) {
     const long k = pt ? L.G - 1 : 0;
     if (j < L.NS) return 2 + k * L.NS + j;
     if (j < L.NS + L.NC) return 2 + (long)L.NS * L.G + k * L.NC + (j - L.NS);
-    return 2 + (long)(L.NS + L.NC) * L.G + k * L.NDV + (j - L.NS - L.NC);
+    return L.DB + k * L.NDV + (j - L.NS - L.NC);
 }
 // An endpoint equation on its input vector (accessor in(si)).
 // MH_ENDPOINT_INITIAL_ACTIVATION: MocoInitialActivationGoal::calcGoalImpl in
@@ -631,9 +646,8 @@ struct YG {
         return x[2 + (long)NS * G + (long)k * NC + j];
     }
     int NDV;
-    __device__ __forceinline__ double xd(int k, int j) const {
-        return x[2 + (long)(NS + NC) * G + (long)k * NDV + j];
-    }
+    long DB;
+    __device__ __forceinline__ double xd(int k, int j) const { return x[DB + (long)k * NDV + j]; }
     __device__ __forceinline__ const double* row(int k, int o) const {
         return Y + ((long)(k - k0) * NO + o) * stride;
     }
@@ -664,7 +678,12 @@ template <class YV>
 __device__ __forceinline__ double xdot_at(const Layout& L, const Lanes& Ln,
         const double* __restrict__ x, const YV& Y, int k, int s) {
 #pragma clang fp contract(off)
-    if (s < L.NQ) return Y.xs(k, L.NQ + s);
+    if (s < L.NQ) {
+        // qdot = u, plus the velocity correction G^T gamma at a mesh-interval
+        // midpoint (CasOCTranscription.cpp:316-333)
+        if (L.vc(k)) return Y.xs(k, L.NQ + s) + Y.row(k, L.OQC + s)[Ln.base];
+        return Y.xs(k, L.NQ + s);
+    }
     if (L.NACC && s < 2 * L.NQ) return Y.xd(k, s - L.NQ);   // implicit: udot = w
     return Y.row(k, s + L.SO)[Ln.base];
 }
@@ -679,11 +698,17 @@ __device__ __forceinline__ double defect_row(const Layout& L, const Interval& I,
     const int npres = I.scheme == MH_HERMITE_SIMPSON ? 2 : 1;
     const int k_first = I.scheme == MH_HERMITE_SIMPSON ? 2 * i : i;
     const int npc = I.P.npc;
-    if (r >= I.rpi) {   // tail: final mesh point's path rows, then its residuals
-        const int rt = r - I.rpi, kl = k_first + npres;
+    if (r >= I.rpi) {   // tail: final mesh point's kinematic and path rows, then its residuals
+        int rt = r - I.rpi;
+        const int kl = k_first + npres;
+        if (rt < I.nkr) return Y.row(kl, I.okc + rt)[Ln.base];
+        rt -= I.nkr;
         if (rt < npc) return path_value(I.P, rt, Y.t(kl), Y.xc(kl, I.P.eq[rt].index));
         return Y.row(kl, I.rout(rt - npc))[Ln.base];
     }
+    // the mesh point's kinematic-constraint rows (callback outputs okc..)
+    if (r < I.nkr) return Y.row(k_first, I.okc + r)[Ln.base];
+    r -= I.nkr;
     if (r < npc) return path_value(I.P, r, Y.t(k_first), Y.xc(k_first, I.P.eq[r].index));
     r -= npc;
     if (r < npres * I.nres) return Y.row(k_first + r / I.nres, I.rout(r % I.nres))[Ln.base];
@@ -731,7 +756,12 @@ __device__ __forceinline__ double dout(const Lanes& Ln, const YV& Y, int k, int 
 template <class YV>
 __device__ __forceinline__ double dxdot(const Layout& L, const Lanes& Ln, const YV& Y, int k, int s,
         int dir) {
-    if (s < L.NQ) return dir == 2 + L.NQ + s ? 1.0 : 0.0;
+#pragma clang fp contract(off)
+    if (s < L.NQ) {
+        const double v = dir == 2 + L.NQ + s ? 1.0 : 0.0;
+        if (L.vc(k)) return v + dout(Ln, Y, k, L.OQC + s, dir);   // + the correction's quotient
+        return v;
+    }
     if (L.NACC && s < 2 * L.NQ) return dir == 2 + L.NS + L.NC + (s - L.NQ) ? 1.0 : 0.0;
     return dout(Ln, Y, k, s + L.SO, dir);
 }
@@ -897,7 +927,7 @@ __global__ void __launch_bounds__(1024) k_interval(DevModel M, Src S, Lanes Ln, 
     stage_lds<1>(sXs, S.x + 2 + (long)k_first * L.NS, npts * L.NS);
     if (L.NC > 0) stage_lds<1>(sXc, S.x + 2 + (long)L.NS * L.G + (long)k_first * L.NC, npts * L.NC);
     if (L.NDV > 0)
-        stage_lds<1>(sXd, S.x + 2 + (long)(L.NS + L.NC) * L.G + (long)k_first * L.NDV, npts * L.NDV);
+        stage_lds<1>(sXd, S.x + L.DB + (long)k_first * L.NDV, npts * L.NDV);
     const double t0 = S.x[0], tf = S.x[1];
     if (threadIdx.x < 2) sK[threadIdx.x] = threadIdx.x ? 1.0 : 0.0;
     __syncthreads();
@@ -1179,7 +1209,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
     stage_lds<1>(sXs, S.x + 2 + (long)k_first * L.NS, R * L.NS);
     if (L.NC > 0) stage_lds<1>(sXc, S.x + 2 + (long)L.NS * L.G + (long)k_first * L.NC, R * L.NC);
     if (L.NDV > 0)
-        stage_lds<1>(sXd, S.x + 2 + (long)(L.NS + L.NC) * L.G + (long)k_first * L.NDV, R * L.NDV);
+        stage_lds<1>(sXd, S.x + L.DB + (long)k_first * L.NDV, R * L.NDV);
     if (threadIdx.x < 2) sK[threadIdx.x] = threadIdx.x ? 1.0 : 0.0;
     const double t0 = S.x[0], tf = S.x[1];
     if (threadIdx.x < R) {   // every block's formulas use the interval's base times
@@ -1372,7 +1402,7 @@ __global__ void __launch_bounds__(256) k_couple(Src S, Lanes Ln, Layout L, Inter
     stage_lds<1>(sXs, S.x + 2 + (long)k_first * L.NS, R * L.NS);
     if (L.NC > 0) stage_lds<1>(sXc, S.x + 2 + (long)L.NS * L.G + (long)k_first * L.NC, R * L.NC);
     if (L.NDV > 0)
-        stage_lds<1>(sXd, S.x + 2 + (long)(L.NS + L.NC) * L.G + (long)k_first * L.NDV, R * L.NDV);
+        stage_lds<1>(sXd, S.x + L.DB + (long)k_first * L.NDV, R * L.NDV);
     if (threadIdx.x < R) {
         int pi;
         double st;
@@ -1402,11 +1432,13 @@ __device__ __forceinline__ void gather_inputs(const double* __restrict__ x, cons
         int k, double* in, int NI) {
     const double* xs = x + 2 + (long)k * L.NS;
     const double* xc = x + 2 + (long)L.NS * L.G + (long)k * L.NC;
-    const double* xd = x + 2 + (long)(L.NS + L.NC) * L.G + (long)k * L.NDV;
+    const double* xd = x + L.DB + (long)k * L.NDV;
+    const double* xm = x + L.XM + (long)k * L.NM;
     for (int s = 0; s < L.NS; ++s) in[s] = xs[s];
     for (int j = 0; j < L.NC; ++j) in[L.NS + j] = xc[j];
     for (int j = 0; j < L.NDV; ++j) in[L.NS + L.NC + j] = xd[j];
-    (void)NI;
+    for (int j = 0; j < L.NM; ++j) in[L.NS + L.NC + L.NDV + j] = xm[j];
+    for (int j = L.NS + L.NC + L.NDV + L.NM; j < NI; ++j) in[j] = 0.0;   // slacks: no goal reads them
 }
 
 // Goals with an integral (quadrature of an integrand): all but the endpoint
@@ -1471,7 +1503,7 @@ template <class Z>
 __global__ void __launch_bounds__(64) k_grad(DevModel M, Layout L, GoalSet GS, int fd, double h,
         const double* __restrict__ x, const double* __restrict__ grid,
         const double* __restrict__ quad, double* __restrict__ grad, double* __restrict__ tpart) {
-    const int ND = L.NI + 2;
+    const int ND = L.NI - L.NSL + 2;   // the goal callback's inputs: no slacks
     const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (tid >= (long)L.G * ND) return;
     const int k = (int)(tid / ND), d = (int)(tid % ND);
@@ -1512,7 +1544,8 @@ __global__ void __launch_bounds__(64) k_grad(DevModel M, Layout L, GoalSet GS, i
     if (d < 2) tpart[(long)k * 2 + d] = acc;
     else if (d - 2 < L.NS) grad[2 + (long)k * L.NS + (d - 2)] = acc;
     else if (d - 2 < L.NS + L.NC) grad[2 + (long)L.NS * L.G + (long)k * L.NC + (d - 2 - L.NS)] = acc;
-    else grad[2 + (long)(L.NS + L.NC) * L.G + (long)k * L.NDV + (d - 2 - L.NS - L.NC)] = acc;
+    else if (d - 2 < L.NS + L.NC + L.NDV) grad[L.DB + (long)k * L.NDV + (d - 2 - L.NS - L.NC)] = acc;
+    else grad[L.XM + (long)k * L.NM + (d - 2 - L.NS - L.NC - L.NDV)] = acc;
 }
 
 
@@ -1569,6 +1602,12 @@ struct mh_ctx {
     int SO = 0;                    // callback output of state s's derivative: s + SO
     int presc = 0, kin_table = -1;
     std::vector<int> kin_col;
+    // kinematic constraints (mh_constraint): couplers, multipliers per grid
+    // point, kinematic rows per mesh point, slacks per mesh interval, the
+    // callback outputs of the errors / velocity correction, bounds
+    int NKC = 0, NM = 0, NK = 0, NSL = 0, OKC = 0, OQC = 0, enforce = 1;
+    std::vector<mh_constraint> kcs;
+    double mult_lo = -1000.0, mult_hi = 1000.0, kc_lo = 0.0, kc_hi = 0.0, vc_lo = -0.1, vc_hi = 0.1;
     std::vector<int> mus_ider;     // muscle -> aux derivative index after the controls (-1)
     double aux_lo = -1000.0, aux_hi = 1000.0;
     int npe = 0;                   // path-constraint template entries per mesh point
@@ -1656,12 +1695,22 @@ struct mh_ctx {
     bool groups_timed = false;     // the last evaluation recorded ev[4]
 };
 
+// The per-call layout view of the context (grid points [k0, k0 + nk)).
+inline Layout make_layout(const mh_ctx* c, int k0, int nk) {
+    Layout L{c->NS, c->NC, c->TQ, c->NO, c->NI, c->G, k0, nk, c->NDV, c->NACC, c->SO,
+             c->NM, c->NSL, c->OQC, 0, 0, 0};
+    L.XM = 2 + (long)(c->NS + c->NC) * c->G;
+    L.XL = L.XM + (long)c->NM * c->G;
+    L.DB = L.XL + (long)c->NSL * c->N;
+    return L;
+}
+
 // The transcription's per-call view of the context.  g / v (this shard's
 // rows / nonzeros) are advanced past the head, which the first interval's
 // block writes through I.gh / I.vh when this shard owns it.
 inline Interval make_interval(const mh_ctx* c, double*& g, double*& v) {
     Interval I{c->scheme, c->interp, c->ib, c->rpi, c->nnz_int, c->NMB + c->NAR, c->NMB, c->NQ + c->NZ,
-               c->N, c->nnz_tail, c->ntail, c->npe, c->P, c->E, nullptr, nullptr, c->iv_dbg_stop, c->iv_pf, c->iv_qfuse};
+               c->N, c->nnz_tail, c->ntail, c->npe, c->NK, c->OKC, c->P, c->E, nullptr, nullptr, c->iv_dbg_stop, c->iv_pf, c->iv_qfuse};
     if (c->ib == 0 && c->nep > 0) {
         I.gh = g;
         I.vh = v;
@@ -1696,7 +1745,7 @@ struct Backend {
 
 template <class D>
 static void be_eval_lane(mh_ctx* c, const double* x, int mode, double* Y) {
-    Layout L{c->NS, c->NC, c->TQ, c->NO, c->NI, c->G, c->k0, c->nk, c->NDV, c->NACC, c->SO};
+    Layout L = make_layout(c, c->k0, c->nk);
     const Lanes& ln = mode ? c->lanes_jac : c->lanes_g;
     const long lanes = (long)c->nk * ln.stride;
     hipLaunchKernelGGL(k_eval<D>, dim3((unsigned)((lanes + 63) / 64)), dim3(64), 0, c->stream, c->M, L,
@@ -1767,7 +1816,7 @@ static void be_interval(mh_ctx* c, const double* x, int mode, double* g, double*
     const Src S{x, c->d_grid, nullptr, c->G, c->k0};
     const Lanes& ln = mode ? c->lanes_jac : c->lanes_g;
     const TaskSet& ts = mode ? c->ts_jac : c->ts_g;
-    Layout L{c->NS, c->NC, c->TQ, c->NO, c->NI, c->G, c->k0, c->nk, c->NDV, c->NACC, c->SO};
+    Layout L = make_layout(c, c->k0, c->nk);
     const Interval I = make_interval(c, g, v);
     // (a failed hipFuncSetAttribute would surface as the launch's error:
     // only the launched kernel's attribute is set, and only when it fits)
@@ -1798,20 +1847,20 @@ static void be_interval(mh_ctx* c, const double* x, int mode, double* g, double*
 }
 template <class D>
 static void be_integrand(mh_ctx* c, const double* x) {
-    Layout L{c->NS, c->NC, c->TQ, c->NO, c->NI, c->G, 0, c->G, c->NDV, c->NACC, c->SO};
+    Layout L = make_layout(c, 0, c->G);
     hipLaunchKernelGGL(k_integrand<D>, dim3((c->G + 63) / 64), dim3(64), 0, c->stream, c->M, L,
             c->GS, x, c->d_grid, c->d_quad, c->d_C);
 }
 template <class D>
 static void be_grad(mh_ctx* c, const double* x) {
-    Layout L{c->NS, c->NC, c->TQ, c->NO, c->NI, c->G, 0, c->G, c->NDV, c->NACC, c->SO};
+    Layout L = make_layout(c, 0, c->G);
     const long tot = (long)c->G * (c->NI + 2);
     hipLaunchKernelGGL(k_grad<D>, dim3((unsigned)((tot + 63) / 64)), dim3(64), 0, c->stream, c->M, L,
             c->GS, c->fd, c->h, x, c->d_grid, c->d_quad, c->d_grad, c->d_tpart);
 }
 template <class D>
 static void be_probe_lane(mh_ctx* c, int np, const double* in, double* out) {
-    Layout L{c->NS, c->NC, c->TQ, c->NO, c->NI, c->G, 0, 0, c->NDV, c->NACC, c->SO};
+    Layout L = make_layout(c, 0, 0);
     hipLaunchKernelGGL(k_dae_probe<D>, dim3((np + 63) / 64), dim3(64), 0, c->stream, c->M, L, np, in,
             out);
 }

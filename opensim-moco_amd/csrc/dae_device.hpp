@@ -50,6 +50,14 @@ struct DevModel {
     const int* mus_ftn_state;
     const int* mus_control;
     const double* mus_derived;   // per muscle: fiberWidth, squareFiberWidth, vmax, kT, e0 offset, passive denom
+    // kinematic constraints (CoordinateCoupler, include/mocohip.h
+    // mh_constraint): count, table, callback output of the first error and
+    // of the velocity correction (-1: none), derivative levels enforced,
+    // offset of the multipliers after the controls pointer (the slacks
+    // follow them)
+    int nkc;
+    const mh_constraint* kcs;
+    int okc, oqc, enforce, mult;
 };
 constexpr int MUS_DERIVED = 6;
 
@@ -340,6 +348,38 @@ __device__ __forceinline__ int tri(int i, int j) { return i * (i + 1) / 2 + j; }
 // residual = M udot + C - f_applied by RNEA with the accelerations, the
 // mobility forces Simbody's findMotionForces returns,
 // MocoCasOCProblem.h:245-297).
+// Kinematic-constraint outputs (MocoCasOCProblem.h:664-732): per
+// CoordinateCoupler phi = scale f(q_i) - q_d the position errors, then (when
+// enforced) the velocity and acceleration errors; the velocity correction
+// G^T gamma from the slack inputs (MocoCasOCProblem.h:298-332).  The
+// oracle's kc_outputs (oracle/oracle.c), operation for operation.
+__device__ inline void kc_outputs(const DevModel& M, const double* q, const double* u,
+        const double* udot, const double* c, double* out) {
+#pragma clang fp contract(off)
+    const int n = M.nkc;
+    double* e = out + M.okc;
+    const double* lam = c + M.mult;
+    const double* gam = lam + n;
+    if (M.oqc >= 0)
+        for (int j = 0; j < M.nq; ++j) out[M.oqc + j] = 0.0;
+    for (int i = 0; i < n; ++i) {
+        const mh_constraint K = M.kcs[i];
+        const int ci = M.funcs[K.func].coord, d = K.dependent;
+        double v, d1, d2;
+        fn_eval(M, K.func, q, v, d1, d2);
+        const double gi = K.scale * d1;
+        e[i] = K.scale * v - q[d];
+        if (M.enforce) {
+            e[n + i] = gi * u[ci] - u[d];
+            e[2 * n + i] = (gi * udot[ci] - udot[d]) + K.scale * d2 * u[ci] * u[ci];
+        }
+        if (M.oqc >= 0) {
+            out[M.oqc + ci] += gi * gam[i];
+            out[M.oqc + d] -= gam[i];
+        }
+    }
+}
+
 template <int MB, int MQ, int MP>
 __device__ void dae_eval(const DevModel& M, Work<MB, MQ, MP>& w, double time, const double* x,
         const double* c, double* out, const double* wacc_presc = nullptr) {
@@ -479,6 +519,15 @@ __device__ void dae_eval(const DevModel& M, Work<MB, MQ, MP>& w, double time, co
         const mh_actuator A = M.acts[ia];
         if (A.kind == MH_ACT_COORDINATE) w.tau[A.target] += c[ia] * A.optimal_force;
     }
+    // ---- kinematic constraint forces -G^T lambda (MocoCasOCProblem.h:643-662)
+    for (int i = 0; i < M.nkc; ++i) {
+        const mh_constraint K = M.kcs[i];
+        double v, d1, d2;
+        fn_eval(M, K.func, q, v, d1, d2);
+        const double lam = c[M.mult + i];
+        w.tau[M.funcs[K.func].coord] -= (K.scale * d1) * lam;
+        w.tau[K.dependent] -= -lam;
+    }
     // ---- muscles: path geometry, DGF, tension as point forces -------------
     for (int im = 0; im < M.nmus; ++im) {
         const mh_muscle& mu = M.mus[im];
@@ -617,6 +666,7 @@ __device__ void dae_eval(const DevModel& M, Work<MB, MQ, MP>& w, double time, co
     for (int j = 0; j < NQ; ++j) w.tau[j] -= svdot(w.S[j], w.F[M.coord_body[j] + 1]);
     if (wacc) {
         for (int j = 0; j < NQ; ++j) out[j] = -w.tau[j];
+        if (M.nkc) kc_outputs(M, q, u, wacc, c, out);
         return;
     }
     // ---- CRBA: composite inertias re-derived per body (reuse F slots is not
@@ -690,6 +740,7 @@ __device__ void dae_eval(const DevModel& M, Work<MB, MQ, MP>& w, double time, co
         for (int k = i + 1; k < NQ; ++k) t -= w.Mm[tri(k, i)] * y[k];
         y[i] = t / w.Mm[tri(i, i)];
     }
+    if (M.nkc) kc_outputs(M, q, u, y, c, out);
 }
 
 }  // namespace mh

@@ -61,7 +61,7 @@ __global__ void __launch_bounds__(256) k_transcribe(Layout L, Interval I, Lanes 
         int nchunks, int yq) {
     const int il = blockIdx.y;
     const int i = I.ib + il;
-    const YG YV{Y, times, L.NO, Ln.stride, L.k0, yq, x, L.NS, L.NC, L.G, L.NDV};
+    const YG YV{Y, times, L.NO, Ln.stride, L.k0, yq, x, L.NS, L.NC, L.G, L.NDV, L.DB};
     if ((int)blockIdx.x < nchunks) {
         int k_first, k_last;
         interval_span(I, i, k_first, k_last);
@@ -93,7 +93,7 @@ __global__ void __launch_bounds__(256) k_transcribe_gs(Layout L, Interval I, Lan
         const double* __restrict__ grid, const double* __restrict__ times,
         const double* __restrict__ Y, double* __restrict__ g, double* __restrict__ values,
         int nint, int yq) {
-    const YG YV{Y, times, L.NO, Ln.stride, L.k0, yq, x, L.NS, L.NC, L.G, L.NDV};
+    const YG YV{Y, times, L.NO, Ln.stride, L.k0, yq, x, L.NS, L.NC, L.G, L.NDV, L.DB};
     const int nthreads = gridDim.x * blockDim.x;
     const int tid = blockIdx.x * blockDim.x + threadIdx.x;
     if (values) {
@@ -482,9 +482,29 @@ static int64_t col_state(const mh_ctx* c, int64_t k, int s) { return 2 + k * c->
 static int64_t col_control(const mh_ctx* c, int64_t k, int j) {
     return 2 + (int64_t)c->NS * c->G + k * c->NC + j;
 }
-// implicit mode: accelerations (CasOC "derivatives", sorted after controls)
+// Lagrange multipliers (NM x G) and slacks (NSL x mesh-interval midpoints)
+// after the controls, then the "derivatives" (implicit mode: accelerations,
+// implicit auxiliary derivatives) -- CasOCIterate.h:27-44 key order
+static int64_t col_mult(const mh_ctx* c, int64_t k, int j) {
+    return 2 + (int64_t)(c->NS + c->NC) * c->G + k * c->NM + j;
+}
+static int64_t col_slack(const mh_ctx* c, int64_t i, int l) {
+    return 2 + (int64_t)(c->NS + c->NC + c->NM) * c->G + i * c->NSL + l;
+}
 static int64_t col_deriv(const mh_ctx* c, int64_t k, int j) {
-    return 2 + (int64_t)(c->NS + c->NC) * c->G + k * c->NDV + j;
+    return 2 + (int64_t)(c->NS + c->NC + c->NM) * c->G + (int64_t)c->NSL * c->N + k * c->NDV + j;
+}
+// x column of per-point input j of grid point k: [states, controls,
+// derivatives, multipliers, slacks (mesh-interval midpoints: the interval's)]
+static int64_t col_input(const mh_ctx* c, int64_t k, int j) {
+    if (j < c->NS) return col_state(c, k, j);
+    j -= c->NS;
+    if (j < c->NC) return col_control(c, k, j);
+    j -= c->NC;
+    if (j < c->NDV) return col_deriv(c, k, j);
+    j -= c->NDV;
+    if (j < c->NM) return col_mult(c, k, j);
+    return col_slack(c, (k - 1) / 2, j - c->NM);
 }
 
 // x column of endpoint input si: [initial_time, initial point inputs,
@@ -509,10 +529,7 @@ static void build_template(mh_ctx* c) {
     auto key = [&](const Col& col) -> int64_t {
         // column index for interval 0
         if (col.dir < 2) return col.dir;
-        const int j = col.dir - 2;
-        if (j < NS) return col_state(c, col.pt, j);
-        if (j < NS + NC) return col_control(c, col.pt, j - NS);
-        return col_deriv(c, col.pt, j - NS - NC);
+        return col_input(c, col.pt, col.dir - 2);
     };
     // time columns carry pt_time (the residual rows' grid point; 0 otherwise)
     auto emit_row = [&](int row, uint8_t kind_t, uint8_t kind_x, int s, std::vector<Col> cols,
@@ -534,8 +551,9 @@ static void build_template(mh_ctx* c) {
     // else the detected ones (sp: [output][time, inputs]); plus the point's
     // own state s_ident (the defects' identity terms).
     const int W = 1 + NS + NC + NDV;
+    const int NPD = NS + NC + NDV + c->NM;   // callback inputs (no slacks)
     auto point_dep = [&](const std::vector<uint8_t>& sp, int o, int pt, int s_ident, std::vector<Col>& v) {
-        for (int j = 0; j < NS + NC + NDV; ++j)
+        for (int j = 0; j < NPD; ++j)
             if (sp.empty() || sp[(size_t)o * W + 1 + j] || j == s_ident) v.push_back({pt, 2 + j});
     };
     auto time_dep = [&](const std::vector<uint8_t>& sp, int o) { return sp.empty() || sp[(size_t)o * W] != 0; };
@@ -561,12 +579,23 @@ static void build_template(mh_ctx* c) {
             emit_row(row++, T_PATH, T_PATH, e, v, pt);
         }
     };
+    // kinematic-constraint rows of mesh point pt (outputs OKC.. of the
+    // multibody callback; block-dense over time and the point's inputs),
+    // first among the mesh point's rows (CasOCTranscription.h:283-289)
+    auto kc_rows = [&](int& row, int pt) {
+        for (int r = 0; r < c->NK; ++r) {
+            std::vector<Col> v{{pt, 0}, {pt, 1}};
+            point_dep({}, 0, pt, -1, v);
+            emit_row(row++, T_RES, T_RES, c->OKC + r, v, pt);
+        }
+    };
     // implicit speed rows: udot = the acceleration variable (direct MX
     // expression, CasOCTranscription.cpp:339-341): own state + acceleration
     auto speed_sparse = [&](int s) { return implicit && s >= NQ && s < 2 * NQ; };
     const int adir = 2 + NS + NC;   // direction of acceleration 0
     int row = 0;
     if (c->scheme == MH_HERMITE_SIMPSON) {
+        kc_rows(row, 0);
         path_rows(row, 0);
         residual_rows(row, 0);
         residual_rows(row, 1);
@@ -588,7 +617,15 @@ static void build_template(mh_ctx* c) {
         }
         for (int s = 0; s < NS; ++s) {
             std::vector<Col> v{{0, 0}, {0, 1}};
-            if (s < NQ) {
+            if (s < NQ && c->NSL) {
+                // qdot at the midpoint = u + G^T gamma: the velocity
+                // correction reads the midpoint's q, u and the interval's
+                // slacks (block-dense, CasOCTranscription.cpp:316-333)
+                v.push_back({0, 2 + s}); v.push_back({2, 2 + s});
+                v.push_back({0, 2 + NQ + s}); v.push_back({2, 2 + NQ + s});
+                for (int j = 0; j < 2 * NQ; ++j) v.push_back({1, 2 + j});
+                for (int l = 0; l < c->NSL; ++l) v.push_back({1, 2 + NPD + l});
+            } else if (s < NQ) {
                 v.push_back({0, 2 + s}); v.push_back({2, 2 + s});
                 v.push_back({0, 2 + NQ + s}); v.push_back({1, 2 + NQ + s}); v.push_back({2, 2 + NQ + s});
             } else if (speed_sparse(s)) {
@@ -607,6 +644,7 @@ static void build_template(mh_ctx* c) {
             }
         }
     } else {
+        kc_rows(row, 0);
         path_rows(row, 0);
         residual_rows(row, 0);
         for (int s = 0; s < NS; ++s) {
@@ -628,6 +666,7 @@ static void build_template(mh_ctx* c) {
     // tail: path rows of the final mesh point, then residual rows of the
     // last grid point (point 2 of the HS interval, 1 of the trapezoidal one),
     // rows rpi.. relative to the last interval
+    kc_rows(row, c->scheme == MH_HERMITE_SIMPSON ? 2 : 1);
     path_rows(row, c->scheme == MH_HERMITE_SIMPSON ? 2 : 1);
     residual_rows(row, c->scheme == MH_HERMITE_SIMPSON ? 2 : 1);
     c->nnz_tail = (int)c->tpl.size() - c->nnz_int;
@@ -845,7 +884,41 @@ static int validate_and_layout(mh_ctx* c, const mh_problem* p, const mh_options*
         c->acc_lo = o->implicit_accel_bounds[0];
         c->acc_hi = o->implicit_accel_bounds[1];
     }
-    c->NI = c->NS + c->NC + c->NDV;
+    // kinematic constraints (MocoCasOCProblem.cpp:96-215)
+    const int NKC = M.nconstraints;
+    if (NKC < 0 || (NKC > 0 && !M.constraints)) return set_err(MH_ERR_INVALID, "bad kinematic constraints");
+    c->kcs.assign(M.constraints, M.constraints + NKC);
+    for (int i = 0; i < NKC; ++i) {
+        const mh_constraint& K = c->kcs[i];
+        const int f = K.func;
+        if (K.kind != MH_KC_COORDINATE_COUPLER || f < 0 || f >= M.nfunctions ||
+                M.functions[f].kind == MH_FN_CONSTANT || M.functions[f].coord < 0 ||
+                M.functions[f].coord >= M.nq || K.dependent < 0 || K.dependent >= M.nq ||
+                K.dependent == M.functions[f].coord)
+            return set_err(MH_ERR_INVALID, "kinematic constraint %d: bad kind/function/coordinate", i);
+    }
+    if (NKC && (c->presc || p->nendpoint > 0 || o->sparsity_detection != MH_SPARSITY_NONE ||
+                o->minimize_lagrange_multipliers))
+        return set_err(MH_ERR_UNSUPPORTED, "kinematic constraints with prescribed kinematics, endpoint "
+                       "constraints, sparsity detection or minimize_lagrange_multipliers");
+    c->NKC = NKC;
+    c->enforce = !o->ignore_constraint_derivatives;
+    c->NM = NKC;
+    c->NK = c->enforce ? 3 * NKC : NKC;
+    c->NSL = c->enforce && o->transcription == MH_HERMITE_SIMPSON ? NKC : 0;
+    c->OKC = c->NQ + c->NZ + c->NAR;
+    c->OQC = c->OKC + c->NK;
+    c->NO = c->OQC + (c->NSL ? c->NQ : 0);
+    if (!std::isnan(p->multiplier_bounds.lower) || !std::isnan(p->multiplier_bounds.upper)) {
+        c->mult_lo = p->multiplier_bounds.lower; c->mult_hi = p->multiplier_bounds.upper;
+    }
+    if (!std::isnan(p->kinematic_constraint_bounds.lower) || !std::isnan(p->kinematic_constraint_bounds.upper)) {
+        c->kc_lo = p->kinematic_constraint_bounds.lower; c->kc_hi = p->kinematic_constraint_bounds.upper;
+    }
+    if (o->velocity_correction_bounds[0] != 0.0 || o->velocity_correction_bounds[1] != 0.0) {
+        c->vc_lo = o->velocity_correction_bounds[0]; c->vc_hi = o->velocity_correction_bounds[1];
+    }
+    c->NI = c->NS + c->NC + c->NDV + c->NM + c->NSL;
     if (p->npath < 0 || (p->npath > 0 && !p->path)) return set_err(MH_ERR_INVALID, "bad path constraints");
     c->npc = p->npath;
     c->pc.assign(p->path, p->path + p->npath);
@@ -975,9 +1048,11 @@ static int validate_and_layout(mh_ctx* c, const mh_problem* p, const mh_options*
             c->quad[i + 1] += 0.5 * dm;
         }
     }
-    c->n = 2 + (int64_t)(c->NS + c->NC + c->NDV) * c->G;
+    c->n = 2 + (int64_t)(c->NS + c->NC + c->NDV + c->NM) * c->G + (int64_t)c->NSL * c->N;
     build_template(c);
-    if (!path_entries_lead(c)) return set_err(MH_ERR_INVALID, "internal: path-constraint template layout");
+    // (kinematic rows precede the path rows: such contexts never run
+    // k_interval, whose path loop needs the path entries first)
+    if (!c->NK && !path_entries_lead(c)) return set_err(MH_ERR_INVALID, "internal: path-constraint template layout");
     // endpoint rows first, then the intervals, then the tail (the final mesh
     // point's path rows and residuals)
     c->m = c->nep + (int64_t)c->rpi * c->N + c->ntail;
@@ -1120,7 +1195,8 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
                  o_tpl = A.put(c->tpl.data(), c->tpl.size()),
                  o_pc = A.put(c->pc.data(), c->pc.size()),
                  o_ep = A.put(c->ep.data(), c->ep.size()),
-                 o_eptpl = A.put(c->eptpl.data(), c->eptpl.size());
+                 o_eptpl = A.put(c->eptpl.data(), c->eptpl.size()),
+                 o_kcs = A.put(c->kcs.data(), c->kcs.size());
     // compiled template of the Jacobian lanes (k_interval), capacity of the
     // block-dense template (sparsity detection only removes entries)
     if (!compile_template(c.get())) return set_err(MH_ERR_UNSUPPORTED, "Jacobian template does not compile");
@@ -1170,6 +1246,12 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     D.implicit = c->NACC > 0 ? 1 : 0;
     D.nacc = c->NACC;
     D.mus_ider = (const int*)(b + o_mi);
+    D.nkc = c->NKC;
+    D.kcs = (const mh_constraint*)(b + o_kcs);
+    D.okc = c->OKC;
+    D.oqc = c->NSL ? c->OQC : -1;
+    D.enforce = c->enforce;
+    D.mult = c->NC + c->NDV;   // multipliers after the controls and derivatives
     D.presc = c->presc;
     D.kin_table = c->kin_table;
     D.kin_col = (const int*)(b + o_kcol);
@@ -1362,16 +1444,28 @@ extern "C" int mh_get_bounds(const mh_ctx* c, double* xl, double* xu, double* gl
             xu[col_deriv(c, k, j)] = aux ? c->aux_hi : c->acc_hi;
         }
     }
+    // multipliers: multiplier_bounds everywhere (CasOCTranscription.cpp:
+    // 209-219); slacks: velocity_correction_bounds (:235-241)
+    for (int j = 0; j < c->NM; ++j)
+        for (int k = 0; k < c->G; ++k) { xl[col_mult(c, k, j)] = c->mult_lo; xu[col_mult(c, k, j)] = c->mult_hi; }
+    for (int l = 0; l < c->NSL; ++l)
+        for (int i = 0; i < c->N; ++i) { xl[col_slack(c, i, l)] = c->vc_lo; xu[col_slack(c, i, l)] = c->vc_hi; }
     if (gl && gu) {
         for (int64_t r = 0; r < c->m; ++r) { gl[r] = 0.0; gu[r] = 0.0; }
+        // kinematic rows: kinematic_constraint_bounds (CasOCTranscription.cpp:303-309)
+        for (int i = 0; i <= c->N; ++i)
+            for (int r = 0; r < c->NK; ++r) {
+                gl[c->nep + (int64_t)i * c->rpi + r] = c->kc_lo;
+                gu[c->nep + (int64_t)i * c->rpi + r] = c->kc_hi;
+            }
         // endpoint rows: the constraint info's bounds (CasOCTranscription.cpp:582-583)
         for (int e = 0; e < c->nep; ++e) { gl[e] = c->ep[e].g.lower; gu[e] = c->ep[e].g.upper; }
         // path rows: the equation's bounds at every mesh point
         // (CasOCTranscription.cpp:429-432); mesh point N opens the tail
         for (int i = 0; i <= c->N; ++i)
             for (int e = 0; e < c->npc; ++e) {
-                gl[c->nep + (int64_t)i * c->rpi + e] = c->pc[e].g.lower;
-                gu[c->nep + (int64_t)i * c->rpi + e] = c->pc[e].g.upper;
+                gl[c->nep + (int64_t)i * c->rpi + c->NK + e] = c->pc[e].g.lower;
+                gu[c->nep + (int64_t)i * c->rpi + c->NK + e] = c->pc[e].g.upper;
             }
     }
     return MH_OK;
@@ -1421,12 +1515,7 @@ extern "C" int mh_get_jac_structure(const mh_ctx* c, int32_t* iRow, int32_t* jCo
             iRow[e] = (int32_t)(c->nep + (int64_t)i * c->rpi + T.row);
             int64_t col;
             if (T.dir < 2) col = T.dir;
-            else {
-                const int j = T.dir - 2;
-                const int64_t k = (int64_t)i * step + T.pt;
-                col = j < c->NS ? col_state(c, k, j)
-                                : (j < c->NS + c->NC ? col_control(c, k, j - c->NS) : col_deriv(c, k, j - c->NS - c->NC));
-            }
+            else col = col_input(c, (int64_t)i * step + T.pt, T.dir - 2);
             jCol[e] = (int32_t)col;
             ++e;
         }
@@ -1466,7 +1555,7 @@ static int launch_stage(mh_ctx* c, int stage, int kind, const double* x, double*
         HIPCHK(hipGetLastError());
         return MH_OK;
     }
-    Layout L{c->NS, c->NC, c->TQ, c->NO, c->NI, c->G, c->k0, c->nk, c->NDV, c->NACC, c->SO};
+    Layout L = make_layout(c, c->k0, c->nk);
     const Lanes& ln = kind == 0 ? c->lanes_g : c->lanes_jac;
     const double* Y = kind == 0 ? c->d_Yg : c->d_Y;
     const int nchunks = kind == 0 ? 0 : (c->nnz_int + (c->ie == c->N ? c->nnz_tail : 0) + ASM_CHUNK - 1) / ASM_CHUNK;
@@ -1644,7 +1733,7 @@ extern "C" int mh_eval_f(mh_ctx* c, const double* x, int, double* f) {
     (void)hipGetLastError();   // report only this call's launch errors
     HIPCHK(hipMemcpyAsync(c->d_x, x, sizeof(double) * c->n, hipMemcpyHostToDevice, c->stream));
     if (c->timing) HIPCHK(hipEventRecord(c->ev[0], c->stream));
-    Layout L{c->NS, c->NC, c->TQ, c->NO, c->NI, c->G, 0, c->G, c->NDV, c->NACC, c->SO};
+    Layout L = make_layout(c, 0, c->G);
     if (c->ngoals > 0) {
         c->be->integrand(c, c->d_x);
         HIPCHK(hipGetLastError());
@@ -1667,7 +1756,7 @@ extern "C" int mh_eval_grad_f(mh_ctx* c, const double* x, int, double* grad) {
     (void)hipGetLastError();   // report only this call's launch errors
     HIPCHK(hipMemcpyAsync(c->d_x, x, sizeof(double) * c->n, hipMemcpyHostToDevice, c->stream));
     if (c->timing) HIPCHK(hipEventRecord(c->ev[0], c->stream));
-    Layout L{c->NS, c->NC, c->TQ, c->NO, c->NI, c->G, 0, c->G, c->NDV, c->NACC, c->SO};
+    Layout L = make_layout(c, 0, c->G);
     HIPCHK(hipMemsetAsync(c->d_grad, 0, sizeof(double) * c->n, c->stream));
     HIPCHK(hipMemsetAsync(c->d_tpart, 0, sizeof(double) * 2 * c->G, c->stream));
     HIPCHK(hipMemsetAsync(c->d_C, 0, sizeof(double) * c->G * std::max(1, c->ngoals), c->stream));
@@ -2016,7 +2105,9 @@ static const Backend* select_backend(mh_ctx* c, const mh_problem* p) {
     const char* force = std::getenv("MOCOHIP_BACKEND");
     const bool generic = force && std::strcmp(force, "generic") == 0;
     const bool lane = force && std::strcmp(force, "lane") == 0;
-    if (!generic) {
+    // the generated back ends carry no kinematic constraints (the model hash
+    // does not cover them): such problems run the generic interpreter
+    if (!generic && c->NKC == 0) {
         const uint64_t key = backend_key(c->model_hash, c->NMB > 0, c->presc != 0);
         for (auto entry : kGeneratedModels) {
             const GenEntry& e = entry();

@@ -83,6 +83,14 @@ class mh_external_force(C.Structure):
                 ("point_col", i32), ("torque_col", i32), ("reserved", i32)]
 
 
+MH_KC_COORDINATE_COUPLER = 0
+
+
+class mh_constraint(C.Structure):
+    _fields_ = [("kind", i32), ("dependent", i32), ("func", i32), ("reserved", i32),
+                ("scale", f64)]
+
+
 class mh_model(C.Structure):
     _fields_ = [("nq", i32), ("nbodies", i32), ("naxes", i32),
                 ("nfunctions", i32), ("nknots", i32), ("nmuscles", i32),
@@ -95,7 +103,8 @@ class mh_model(C.Structure):
                 ("points", P(mh_path_point)), ("actuators", P(mh_actuator)),
                 ("tables", P(mh_table)), ("table_breaks", P(f64)),
                 ("table_coefs", P(f64)),
-                ("external", P(mh_external_force))]
+                ("external", P(mh_external_force)),
+                ("nconstraints", i32), ("reserved_kc", i32), ("constraints", P(mh_constraint))]
 
 
 class mh_bounds(C.Structure):
@@ -113,7 +122,7 @@ class mh_goal(C.Structure):
                 ("weight", f64)]
 
 
-MH_ABI_VERSION = 3     # include/mocohip.h
+MH_ABI_VERSION = 4     # include/mocohip.h
 MH_PATH_CONTROL_BOUND = 0
 MH_ENDPOINT_INITIAL_ACTIVATION = 0
 
@@ -139,7 +148,8 @@ class mh_problem(C.Structure):
                 ("npath", i32), ("reserved", i32), ("path", P(mh_path_equation)),
                 ("prescribed_kinematics", i32), ("kinematics_table", i32),
                 ("kinematics_column", P(i32)),
-                ("nendpoint", i32), ("reserved2", i32), ("endpoint", P(mh_endpoint_equation))]
+                ("nendpoint", i32), ("reserved2", i32), ("endpoint", P(mh_endpoint_equation)),
+                ("multiplier_bounds", mh_bounds), ("kinematic_constraint_bounds", mh_bounds)]
 
 
 class mh_options(C.Structure):
@@ -151,7 +161,9 @@ class mh_options(C.Structure):
                 ("implicit_accel_bounds", f64 * 2),
                 ("sparsity_detection", i32), ("sparsity_random_count", i32),
                 ("sparsity_guess", P(f64)), ("sparsity_pattern", P(C.c_uint8)),
-                ("implicit_aux_bounds", f64 * 2)]
+                ("implicit_aux_bounds", f64 * 2),
+                ("ignore_constraint_derivatives", i32), ("minimize_lagrange_multipliers", i32),
+                ("velocity_correction_bounds", f64 * 2)]
 
 
 MH_SPARSITY_NONE, MH_SPARSITY_RANDOM, MH_SPARSITY_INITIAL_GUESS, MH_SPARSITY_GIVEN = 0, 1, 2, 3

@@ -84,6 +84,40 @@ def double_pendulum(num_mesh_intervals: int = 100, scheme: str = "hermite-simpso
     return MocoStudy(p, s)
 
 
+def double_pendulum_coupled(num_mesh_intervals: int = 20, scheme: str = "hermite-simpson",
+                           dynamics: str = "explicit", enforce_constraint_derivatives: bool = True,
+                           coupler: str = "linear") -> MocoStudy:
+    """testConstraints.cpp:620-690 (testDoublePendulumCoordinateCoupler): a
+    CoordinateCouplerConstraint q1 = -2 q0 + pi (LinearFunction(-2, pi)),
+    control goal, HS N=20, both dynamics modes, with and without enforcing
+    the constraint derivatives.  (The reference also minimizes the Lagrange
+    multipliers with weight 10 -- not implemented here.)  coupler="spline":
+    the same constraint through a SimmSpline of the linear relation plus a
+    quadratic term, so that f'' != 0 (acceleration errors and the
+    velocity-correction Jacobian see the curvature)."""
+    from .model import CoordinateCouplerConstraint, Function
+    m = n_link_pendulum(2)
+    if coupler == "linear":
+        f = Function.linear("q0", -2.0, math.pi)
+    else:
+        xs = np.linspace(-6.0, 6.0, 13)
+        f = Function.simm_spline("q0", xs, -2.0 * xs + math.pi + 0.1 * xs * xs)
+    m.add_constraint(CoordinateCouplerConstraint("q0_q1_coupler", "q1", f))
+    p = MocoProblem(m)
+    p.set_time_bounds(0.0, 1.0)
+    p.set_state_info("/jointset/j0/q0/value", (-5, 5), 0, math.pi / 2)
+    p.set_state_info("/jointset/j0/q0/speed", (-10, 10), 0, 0)
+    p.set_state_info("/jointset/j1/q1/value", (-10, 10))
+    p.set_state_info("/jointset/j1/q1/speed", (-5, 5), 0, 0)
+    p.set_control_info("/tau0", (-50, 50))
+    p.set_control_info("/tau1", (-50, 50))
+    p.add_goal(MocoControlGoal())
+    s = MocoHipSolver(num_mesh_intervals=num_mesh_intervals, transcription_scheme=scheme,
+                      multibody_dynamics_mode=dynamics,
+                      enforce_constraint_derivatives=enforce_constraint_derivatives)
+    return MocoStudy(p, s)
+
+
 def double_pendulum_swingup(num_mesh_intervals: int = 29, scheme: str = "trapezoidal",
                             dynamics: str = "explicit") -> MocoStudy:
     """testImplicit.cpp:30-100 (solveDoublePendulumSwingup): final-time goal
@@ -255,6 +289,7 @@ CONFIGS = {
     "sliding_mass": sliding_mass,
     "double_pendulum": double_pendulum,
     "double_pendulum_swingup": double_pendulum_swingup,
+    "double_pendulum_coupled": double_pendulum_coupled,
     "gait10dof18musc": gait10dof18musc,
     "gait10dof18musc_inverse": gait10dof18musc_inverse,
 }

@@ -235,6 +235,18 @@ class ExternalForce:
     torque_identifier: Optional[str] = None
 
 
+@dataclass
+class CoordinateCouplerConstraint:
+    """OpenSim CoordinateCouplerConstraint with one independent coordinate:
+    q[dependent] = scale_factor * function(q[independent]) (the Simbody
+    CoordinateCoupler of OpenSim's CompoundFunction; include/mocohip.h
+    mh_constraint).  ``function.coord`` names the independent coordinate."""
+    name: str
+    dependent: str
+    function: Function
+    scale_factor: float = 1.0
+
+
 class Model:
     def __init__(self, name: str = "model", gravity=(0, -9.80665, 0)):
         self.name = name
@@ -246,6 +258,7 @@ class Model:
         self.tables: Dict[str, DataTable] = {}
         self.external_forces: List[ExternalForce] = []
         self.markers: Dict[str, Marker] = {}    # by path
+        self.constraints: List[CoordinateCouplerConstraint] = []   # enabled ones
 
     # building ---------------------------------------------------------------
     def add_body(self, body: Body):
@@ -279,6 +292,10 @@ class Model:
     def add_external_force(self, e: ExternalForce):
         self.external_forces.append(e)
         return e
+
+    def add_constraint(self, k: CoordinateCouplerConstraint):
+        self.constraints.append(k)
+        return k
 
     def add_marker(self, mk: Marker):
         if not mk.path:
@@ -497,6 +514,22 @@ class CompiledModel:
         self._breaks = np.ascontiguousarray(breaks + [0.0], float)
         self._coefs = np.ascontiguousarray(coefs + [0.0], float)
         self._ext = _arr(abi.mh_external_force, ext)
+        # kinematic constraints: their functions after every other function
+        # (models without constraints keep their function list and hash)
+        kcs = []
+        for k in model.constraints:
+            if k.function.kind == abi.MH_FN_CONSTANT or k.function.coord is None:
+                raise ValueError(f"constraint {k.name}: needs a function of the independent coordinate")
+            ks = abi.mh_constraint()
+            ks.kind = abi.MH_KC_COORDINATE_COUPLER
+            ks.dependent = qidx[k.dependent]
+            ks.func = add_function(k.function)
+            ks.scale = float(k.scale_factor)
+            kcs.append(ks)
+        self._funcs = _arr(abi.mh_function, funcs)
+        self._kx = np.ascontiguousarray(knot_x + [0.0], float)
+        self._ky = np.ascontiguousarray(knot_y + [0.0], float)
+        self._kcs = _arr(abi.mh_constraint, kcs)
 
         mm = abi.mh_model()
         mm.nq = len(qidx)
@@ -504,6 +537,8 @@ class CompiledModel:
         mm.naxes = len(axes)
         mm.nfunctions = len(funcs)
         mm.nknots = len(knot_x)
+        mm.nconstraints = len(kcs)
+        mm.constraints = self._kcs
         mm.nmuscles = len(muscles)
         mm.npoints = len(points)
         mm.nactuators = len(acts)

@@ -196,9 +196,19 @@ class MocoProblem:
         self.position_motion: Optional[DataTable] = None
         self.default_speed_bounds = MocoBounds(-50.0, 50.0)
         self.bound_activation_from_excitation = True
+        # MocoPhase kinematic_constraint_bounds / multiplier_bounds
+        # (MocoProblem.cpp:42-43)
+        self.kinematic_constraint_bounds = MocoBounds(0.0, 0.0)
+        self.multiplier_bounds = MocoBounds(-1000.0, 1000.0)
 
     def set_model(self, model: Model):
         self.model = model
+
+    def set_kinematic_constraint_bounds(self, bounds):
+        self.kinematic_constraint_bounds = MocoBounds.of(bounds)
+
+    def set_multiplier_bounds(self, bounds):
+        self.multiplier_bounds = MocoBounds.of(bounds)
 
     def set_time_bounds(self, initial, final):
         self.time_initial = MocoBounds.of(initial)
@@ -417,6 +427,11 @@ class ProblemRep:
         self._endpoint = (abi.mh_endpoint_equation * max(1, len(endpoint)))(*endpoint)
         p.nendpoint = len(endpoint)
         p.endpoint = self._endpoint
+        p.multiplier_bounds.lower = problem.multiplier_bounds.lower
+        p.multiplier_bounds.upper = problem.multiplier_bounds.upper
+        p.kinematic_constraint_bounds.lower = problem.kinematic_constraint_bounds.lower
+        p.kinematic_constraint_bounds.upper = problem.kinematic_constraint_bounds.upper
+        self.num_kinematic_constraints = len(model.constraints)
         self.num_endpoint_equations = len(endpoint)
         self.num_path_equations = len(path_eqs)
         self.struct = p

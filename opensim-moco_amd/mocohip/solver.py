@@ -53,6 +53,10 @@ class MocoHipSolver:
     implicit_multibody_acceleration_bounds: tuple = (-1000.0, 1000.0)
     # implicit_auxiliary_derivative_bounds (MocoDirectCollocationSolver.cpp:41)
     implicit_auxiliary_derivative_bounds: tuple = (-1000.0, 1000.0)
+    # kinematic constraints (MocoDirectCollocationSolver.cpp:29-42)
+    enforce_constraint_derivatives: bool = True
+    velocity_correction_bounds: tuple = (-0.1, 0.1)
+    minimize_lagrange_multipliers: bool = False
     # the optimizer settings (MocoDirectCollocationSolver.cpp:23-42), mapped
     # to Ipopt options by ipopt_options()
     verbosity: int = 2
@@ -142,6 +146,11 @@ class MocoHipSolver:
         lo, hi = self.implicit_auxiliary_derivative_bounds
         o.implicit_aux_bounds[0] = float(lo)
         o.implicit_aux_bounds[1] = float(hi)
+        o.ignore_constraint_derivatives = 0 if self.enforce_constraint_derivatives else 1
+        o.minimize_lagrange_multipliers = int(bool(self.minimize_lagrange_multipliers))
+        lo, hi = self.velocity_correction_bounds
+        o.velocity_correction_bounds[0] = float(lo)
+        o.velocity_correction_bounds[1] = float(hi)
         o.sparsity_detection = _SPARSITY[self.optim_sparsity_detection]
         o.sparsity_random_count = int(self.optim_sparsity_detection_random_count)
         if self.sparsity_guess is not None:
@@ -271,10 +280,57 @@ class _NLPBase:
         return self.NACC + self.NAR
 
     @property
+    def NKC(self) -> int:
+        """Kinematic constraints (CoordinateCouplers) of the model."""
+        return getattr(self.rep, "num_kinematic_constraints", 0)
+
+    @property
+    def NM(self) -> int:
+        """Lagrange multipliers per grid point."""
+        return self.NKC
+
+    @property
+    def NK(self) -> int:
+        """Kinematic-constraint rows per mesh point (position, velocity and
+        acceleration errors when enforcing constraint derivatives)."""
+        return self.NKC * (1 if self.opts.ignore_constraint_derivatives else 3)
+
+    @property
+    def NSL(self) -> int:
+        """Velocity-correction slacks per mesh interval (Hermite-Simpson,
+        enforcing derivatives)."""
+        return (self.NKC if not self.opts.ignore_constraint_derivatives
+                and self.opts.transcription == abi.MH_HERMITE_SIMPSON else 0)
+
+    @property
+    def NI(self) -> int:
+        """Per-point inputs: states, controls, derivatives, multipliers,
+        slacks."""
+        return self.NS + self.NC + self.NDV + self.NM + self.NSL
+
+    @property
     def NO(self) -> int:
         """DAE callback outputs: udot or multibody residual, zdot, auxiliary
-        residuals."""
-        return self.NQ + self.NZ + self.NAR
+        residuals, kinematic errors, velocity correction (with slacks)."""
+        return self.NQ + self.NZ + self.NAR + self.NK + (self.NQ if self.NSL else 0)
+
+    def point_inputs(self, x: np.ndarray) -> np.ndarray:
+        """[G, NI] per grid point inputs from iterate x (the column layout of
+        include/mocohip.h: t0, tf, states, controls, multipliers, slacks,
+        derivatives; a grid point's slacks are its interval's at a
+        mesh-interval midpoint, 0 elsewhere)."""
+        G, NS, NC, NDV, NM, NSL = self.G, self.NS, self.NC, self.NDV, self.NM, self.NSL
+        N = self.opts.num_mesh_intervals
+        o = 2
+        S = x[o:o + NS * G].reshape(G, NS); o += NS * G
+        U = x[o:o + NC * G].reshape(G, NC); o += NC * G
+        M = x[o:o + NM * G].reshape(G, NM); o += NM * G
+        L = x[o:o + NSL * N].reshape(N, NSL); o += NSL * N
+        W = x[o:o + NDV * G].reshape(G, NDV)
+        Lg = np.zeros((G, NSL))
+        if NSL:
+            Lg[1::2] = L
+        return np.concatenate([S, U, W, M, Lg], 1)
 
     @property
     def NRES(self) -> int:
@@ -305,14 +361,14 @@ class _NLPBase:
     def tail_rows(self) -> int:
         """Rows after the last interval's own: the final mesh point's path
         rows and the final grid point's residuals."""
-        return self.NPC + self.NRES
+        return self.NK + self.NPC + self.NRES
 
     def eval_dae(self, inputs: np.ndarray) -> np.ndarray:
         """Per-point DAE: rows [t, states, controls, derivatives] ->
         [udot or multibody residual, zdot, auxiliary residuals]."""
         inputs = np.ascontiguousarray(inputs, float)
         npts = inputs.shape[0]
-        assert inputs.shape[1] == 1 + self.NS + self.NC + self.NDV
+        assert inputs.shape[1] == 1 + self.NI
         out = np.empty((npts, self.NO))
         self._check(self._fn("eval_dae")(self.ctx, npts, abi.dptr(inputs), abi.dptr(out)))
         return out

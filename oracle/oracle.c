@@ -278,6 +278,16 @@ struct orc_ctx {
     int ib, ie, gk0, gk1;
     int64_t row_begin, row_end, nnz_begin, nnz_end;
     int fd; double h;
+    /* kinematic constraints (CoordinateCouplerConstraint):
+     * NKC couplers, NM = NKC multipliers per grid point, NK kinematic rows
+     * per mesh point (3 NKC enforcing constraint derivatives, else NKC),
+     * NSL = NKC slacks per mesh interval (Hermite-Simpson, enforcing
+     * derivatives), OKC / OQC: callback outputs of the kinematic errors /
+     * the velocity correction G^T gamma (NQ, when NSL) */
+    int NKC, NM, NK, NSL, OKC, OQC, enforce;
+    mh_constraint* kcs;
+    double mult_lo, mult_hi, kc_lo, kc_hi, vc_lo, vc_hi;
+    int NPD;               /* callback inputs per point: NS + NC + NDV + NM */
 };
 
 static double* dup_d(const double* p, size_t n) {
@@ -298,14 +308,41 @@ static int64_t col_state(const orc_ctx* c, int k, int s) { return 2 + (int64_t)k
 static int64_t col_control(const orc_ctx* c, int k, int j) {
     return 2 + (int64_t)c->NS * c->G + (int64_t)k * c->NC + j;
 }
-/* implicit mode: generalized accelerations ("derivatives" variables, sorted
- * after controls and (empty) multipliers / slacks, CasOCIterate.h:27-44) */
-static int64_t col_deriv(const orc_ctx* c, int k, int j) {
-    return 2 + (int64_t)(c->NS + c->NC) * c->G + (int64_t)k * c->NDV + j;
+/* Lagrange multipliers (NM x G) and slacks (NSL x mesh-interval midpoints)
+ * after the controls, then the "derivatives" variables (implicit mode:
+ * generalized accelerations, implicit auxiliary derivatives) -- the sorted
+ * key order of CasOCIterate.h:27-44 */
+static int64_t col_mult(const orc_ctx* c, int k, int j) {
+    return 2 + (int64_t)(c->NS + c->NC) * c->G + (int64_t)k * c->NM + j;
 }
+static int64_t col_slack(const orc_ctx* c, int i, int l) {
+    return 2 + (int64_t)(c->NS + c->NC + c->NM) * c->G + (int64_t)i * c->NSL + l;
+}
+static int64_t col_deriv(const orc_ctx* c, int k, int j) {
+    return 2 + (int64_t)(c->NS + c->NC + c->NM) * c->G + (int64_t)c->NSL * c->N + (int64_t)k * c->NDV + j;
+}
+/* Column of per-point input j of grid point k: [states, controls,
+ * derivatives, multipliers, slacks]; a slack is an input of the mesh
+ * interval midpoints only (-1 elsewhere). */
+static int64_t col_input(const orc_ctx* c, int k, int j) {
+    if (j < c->NS) return col_state(c, k, j);
+    j -= c->NS;
+    if (j < c->NC) return col_control(c, k, j);
+    j -= c->NC;
+    if (j < c->NDV) return col_deriv(c, k, j);
+    j -= c->NDV;
+    if (j < c->NM) return col_mult(c, k, j);
+    j -= c->NM;
+    if (c->scheme != MH_HERMITE_SIMPSON || k % 2 == 0) return -1;
+    return col_slack(c, (k - 1) / 2, j);
+}
+/* is grid point k a mesh-interval midpoint carrying slacks? */
+static int vc_point(const orc_ctx* c, int k) { return c->NSL && c->scheme == MH_HERMITE_SIMPSON && k % 2; }
 /* DAE callback outputs: [udot or multibody residual (NQ), zdot (NZ),
- * auxiliary residuals (NAR)] (CasOCFunction.cpp:208-230) */
-static int nout(const orc_ctx* c) { return c->NQ + c->NZ + c->NAR; }
+ * auxiliary residuals (NAR), kinematic errors (NK)] (CasOCFunction.cpp:
+ * 208-230), then the velocity correction (NQ, the VelocityCorrection
+ * function of CasOCFunction.cpp:250-291, when there are slacks) */
+static int nout(const orc_ctx* c) { return c->NQ + c->NZ + c->NAR + c->NK + (c->NSL ? c->NQ : 0); }
 /* residual rows per grid point: multibody residuals (implicit mode), then
  * auxiliary residuals (flattenConstraints, CasOCTranscription.h:290-296) */
 static int nres(const orc_ctx* c) { return c->NMB + c->NAR; }
@@ -326,11 +363,9 @@ static int dep(const uint8_t* sp, int NP, int o, int j) { return !sp || sp[(int6
  * the point's own state s (the defects' identity terms), ascending. */
 static int point_cols_dep(const orc_ctx* c, const uint8_t* sp, int o, int k, int s, int64_t* out) {
     int n = 0;
-    for (int j = 0; j < c->NP; ++j) {
+    for (int j = 0; j < c->NPD; ++j) {   /* callback inputs (no slacks) */
         if (!(dep(sp, c->NP, o, j) || j == s)) continue;
-        if (j < c->NS) out[n++] = col_state(c, k, j);
-        else if (j < c->NS + c->NC) out[n++] = col_control(c, k, j - c->NS);
-        else out[n++] = col_deriv(c, k, j - c->NS - c->NC);
+        out[n++] = col_input(c, k, j);
     }
     return n;
 }
@@ -364,6 +399,20 @@ static int64_t path_rows(const orc_ctx* c, int k, int64_t row, row_fn emit, void
     }
     return row;
 }
+/* Kinematic-constraint rows of mesh grid point k (CasOCTranscription.cpp:
+ * 298-309, 355-363/388-394: the errors are outputs of the mesh points'
+ * multibody callback): block-dense over time and the point's callback
+ * inputs; placed before the path rows (flattenConstraints,
+ * CasOCTranscription.h:283-289). */
+static int64_t kc_rows(const orc_ctx* c, int k, int64_t row, row_fn emit, void* ud, int64_t* cols) {
+    for (int r = 0; r < c->NK; ++r) {
+        int n = 0;
+        cols[n++] = 0; cols[n++] = 1;
+        n += point_cols_dep(c, NULL, 0, k, -1, cols + n);
+        emit(ud, row++, cols, n);
+    }
+    return row;
+}
 /* Implicit mode: the speed rows (NQ <= s < 2NQ) have udot = the derivative
  * variable, a direct MX expression (CasOCTranscription.cpp:339-341), so they
  * depend on the point's own state s and derivative s - NQ only. */
@@ -371,13 +420,14 @@ static int speed_row_sparse(const orc_ctx* c, int s) { return c->NACC && s >= c-
 
 static void interval_rows(const orc_ctx* c, int i, int64_t row0, row_fn emit, void* ud) {
     int NQ = c->TQ, NS = c->NS, NC = c->NC;   /* NQ: coordinates among the states */
-    int64_t* cols = (int64_t*)malloc(sizeof(int64_t) * (size_t)(3 * (NS + NC + c->NDV) + 8));
+    int64_t* cols = (int64_t*)malloc(sizeof(int64_t) * (size_t)(3 * c->NP + 8));
     int64_t row = row0;
     if (c->scheme == MH_HERMITE_SIMPSON) {
         int ki = 2 * i, km = 2 * i + 1, kp = 2 * i + 2;
-        /* flattenConstraints: the mesh point's path rows, then the residuals
-         * of the interval's grid points, then its defects
-         * (CasOCTranscription.h:286-300) */
+        /* flattenConstraints: the mesh point's kinematic and path rows, then
+         * the residuals of the interval's grid points, then its defects
+         * (CasOCTranscription.h:283-300) */
+        row = kc_rows(c, ki, row, emit, ud, cols);
         row = path_rows(c, ki, row, emit, ud, cols);
         row = residual_rows(c, ki, row, emit, ud, cols);
         row = residual_rows(c, km, row, emit, ud, cols);
@@ -392,6 +442,15 @@ static void interval_rows(const orc_ctx* c, int i, int64_t row0, row_fn emit, vo
                         cols[n++] = col_state(c, km, s);
                         cols[n++] = col_state(c, ki, s); cols[n++] = col_state(c, kp, s);
                         cols[n++] = col_state(c, ki, NQ + s); cols[n++] = col_state(c, kp, NQ + s);
+                    } else if (c->NSL) {
+                        /* qdot at the midpoint = u + G^T gamma: the velocity
+                         * correction function reads the midpoint's q, u and
+                         * the interval's slacks (block-dense,
+                         * CasOCTranscription.cpp:316-333) */
+                        cols[n++] = col_state(c, ki, s); cols[n++] = col_state(c, kp, s);
+                        cols[n++] = col_state(c, ki, NQ + s); cols[n++] = col_state(c, kp, NQ + s);
+                        for (int j = 0; j < 2 * NQ; ++j) cols[n++] = col_state(c, km, j);
+                        for (int l = 0; l < c->NSL; ++l) cols[n++] = col_slack(c, i, l);
                     } else {
                         cols[n++] = col_state(c, ki, s); cols[n++] = col_state(c, kp, s);
                         cols[n++] = col_state(c, ki, NQ + s); cols[n++] = col_state(c, km, NQ + s);
@@ -435,6 +494,7 @@ static void interval_rows(const orc_ctx* c, int i, int64_t row0, row_fn emit, vo
         }
     } else { /* trapezoidal (CasOCTrapezoidal.cpp:43-59) */
         int ki = i, kp = i + 1;
+        row = kc_rows(c, ki, row, emit, ud, cols);
         row = path_rows(c, ki, row, emit, ud, cols);
         row = residual_rows(c, ki, row, emit, ud, cols);
         for (int s = 0; s < NS; ++s) {
@@ -471,16 +531,17 @@ static void emit_fill(void* ud, int64_t row, const int64_t* cols, int n) {
     }
 }
 static int rows_per_interval(const orc_ctx* c) {
-    return c->NPC + 2 * c->NS * (c->scheme == MH_HERMITE_SIMPSON) + c->NS * (c->scheme == MH_TRAPEZOIDAL) +
+    return c->NK + c->NPC + 2 * c->NS * (c->scheme == MH_HERMITE_SIMPSON) + c->NS * (c->scheme == MH_TRAPEZOIDAL) +
            (c->scheme == MH_HERMITE_SIMPSON && c->interp ? c->NC : 0) +
            nres(c) * (c->scheme == MH_HERMITE_SIMPSON ? 2 : 1);
 }
 /* after all intervals: the final mesh point's path rows (the last pass of
  * the mesh loop), then the final grid point's residual rows
  * (CasOCTranscription.h:286-308) */
-static int ntail(const orc_ctx* c) { return c->NPC + nres(c); }
+static int ntail(const orc_ctx* c) { return c->NK + c->NPC + nres(c); }
 static void tail_rows(const orc_ctx* c, int64_t row0, row_fn emit, void* ud) {
-    int64_t* cols = (int64_t*)malloc(sizeof(int64_t) * (size_t)(c->NS + c->NC + c->NDV + 4));
+    int64_t* cols = (int64_t*)malloc(sizeof(int64_t) * (size_t)(c->NP + 4));
+    row0 = kc_rows(c, c->G - 1, row0, emit, ud, cols);
     row0 = path_rows(c, c->G - 1, row0, emit, ud, cols);
     residual_rows(c, c->G - 1, row0, emit, ud, cols);
     free(cols);
@@ -665,7 +726,51 @@ int orc_create(const mh_problem* p, const mh_options* o, orc_ctx** out) {
         c->acc_lo = o->implicit_accel_bounds[0];
         c->acc_hi = o->implicit_accel_bounds[1];
     }
-    c->NP = c->NS + c->NC + c->NDV;
+    /* kinematic constraints (MocoCasOCProblem.cpp:96-215: one multiplier per
+     * holonomic equation and, enforcing derivatives, one slack "gamma" per
+     * multiplier; MocoProblemRep.cpp:150-215 for the bounds) */
+    c->NKC = M->nconstraints;
+    if (c->NKC < 0 || (c->NKC > 0 && !M->constraints)) {
+        orc_destroy(c);
+        return fail(MH_ERR_INVALID, "bad kinematic constraints");
+    }
+    c->kcs = DUP(mh_constraint, M->constraints, c->NKC);
+    for (int i = 0; i < c->NKC; ++i) {
+        const mh_constraint* K = &c->kcs[i];
+        int f = K->func;
+        if (K->kind != MH_KC_COORDINATE_COUPLER || f < 0 || f >= M->nfunctions ||
+                c->funcs[f].kind == MH_FN_CONSTANT || c->funcs[f].coord < 0 || c->funcs[f].coord >= c->NQ ||
+                K->dependent < 0 || K->dependent >= c->NQ || K->dependent == c->funcs[f].coord) {
+            orc_destroy(c);
+            return fail(MH_ERR_INVALID, "kinematic constraint %d: bad kind/function/coordinate", i);
+        }
+    }
+    if (c->NKC && (c->presc || p->nendpoint > 0 || o->sparsity_detection != MH_SPARSITY_NONE ||
+                   o->minimize_lagrange_multipliers)) {
+        orc_destroy(c);
+        return fail(MH_ERR_UNSUPPORTED, "kinematic constraints with prescribed kinematics, endpoint "
+                    "constraints, sparsity detection or minimize_lagrange_multipliers");
+    }
+    c->enforce = !o->ignore_constraint_derivatives;
+    c->NM = c->NKC;
+    c->NK = c->enforce ? 3 * c->NKC : c->NKC;
+    c->NSL = c->enforce && o->transcription == MH_HERMITE_SIMPSON ? c->NKC : 0;
+    c->OKC = c->NQ + c->NZ + c->NAR;
+    c->OQC = c->OKC + c->NK;
+    c->mult_lo = -1000.0; c->mult_hi = 1000.0;
+    if (!isnan(p->multiplier_bounds.lower) || !isnan(p->multiplier_bounds.upper)) {
+        c->mult_lo = p->multiplier_bounds.lower; c->mult_hi = p->multiplier_bounds.upper;
+    }
+    c->kc_lo = 0.0; c->kc_hi = 0.0;
+    if (!isnan(p->kinematic_constraint_bounds.lower) || !isnan(p->kinematic_constraint_bounds.upper)) {
+        c->kc_lo = p->kinematic_constraint_bounds.lower; c->kc_hi = p->kinematic_constraint_bounds.upper;
+    }
+    c->vc_lo = -0.1; c->vc_hi = 0.1;
+    if (o->velocity_correction_bounds[0] != 0.0 || o->velocity_correction_bounds[1] != 0.0) {
+        c->vc_lo = o->velocity_correction_bounds[0]; c->vc_hi = o->velocity_correction_bounds[1];
+    }
+    c->NPD = c->NS + c->NC + c->NDV + c->NM;
+    c->NP = c->NPD + c->NSL;
     for (int e = 0; e < c->NPC; ++e) {
         const mh_path_equation* E = &c->pc[e];
         if (E->kind != MH_PATH_CONTROL_BOUND || E->index < 0 || E->index >= c->NC ||
@@ -788,7 +893,7 @@ int orc_create(const mh_problem* p, const mh_options* o, orc_ctx** out) {
         }
     }
     free(mesh);
-    c->n = 2 + (int64_t)(c->NS + c->NC + c->NDV) * c->G;
+    c->n = 2 + (int64_t)(c->NS + c->NC + c->NDV + c->NM) * c->G + (int64_t)c->NSL * c->N;
     c->m = c->NEP + (int64_t)rows_per_interval(c) * c->N + ntail(c);
     c->fd = o->finite_difference_scheme;
     c->h = o->fd_step > 0 ? o->fd_step : 1e-8;
@@ -835,7 +940,7 @@ void orc_destroy(orc_ctx* c) {
     void* ptrs[] = {c->bodies, c->axes, c->funcs, c->kx, c->ky, c->kb, c->kc, c->kd,
             c->mus, c->pts, c->acts, c->tabs, c->brk, c->coef, c->ext, c->sinfo, c->cinfo,
             c->goals, c->gidx, c->gcol, c->gw, c->pc, c->sp, c->sp_pc, c->mus_ider, c->kin_col,
-            c->ep, c->sp_ep,
+            c->ep, c->sp_ep, c->kcs,
             c->mus_act_state, c->mus_ftn_state,
             c->mus_control, c->coord_body, c->grid, c->quad, c->iRow, c->jCol};
     for (size_t i = 0; i < sizeof ptrs / sizeof ptrs[0]; ++i) free(ptrs[i]);
@@ -898,9 +1003,25 @@ int orc_get_bounds(const orc_ctx* c, double* xl, double* xu, double* gl, double*
             xl[col_deriv(c, k, j)] = aux ? c->aux_lo : c->acc_lo;
             xu[col_deriv(c, k, j)] = aux ? c->aux_hi : c->acc_hi;
         }
+    /* multipliers: multiplier_bounds at every grid point, initial and final
+     * alike (CasOCTranscription.cpp:209-219); slacks: velocity_correction_
+     * bounds (:235-241) */
+    for (int j = 0; j < c->NM; ++j)
+        for (int k = 0; k < c->G; ++k) { xl[col_mult(c, k, j)] = c->mult_lo; xu[col_mult(c, k, j)] = c->mult_hi; }
+    for (int l = 0; l < c->NSL; ++l)
+        for (int i = 0; i < c->N; ++i) { xl[col_slack(c, i, l)] = c->vc_lo; xu[col_slack(c, i, l)] = c->vc_hi; }
     /* defects, residuals and interpolating-control rows: equality to 0
      * (CasOCTranscription.cpp:275-278, 440-443) */
     if (gl) for (int64_t r = 0; r < c->m; ++r) { gl[r] = 0.0; gu[r] = 0.0; }
+    /* kinematic rows: kinematic_constraint_bounds at every mesh point
+     * (CasOCTranscription.cpp:303-309) */
+    if (gl && c->NK) {
+        int rpi = rows_per_interval(c);
+        for (int i = 0; i <= c->N; ++i) {
+            int64_t r0 = c->NEP + (int64_t)i * rpi;
+            for (int r = 0; r < c->NK; ++r) { gl[r0 + r] = c->kc_lo; gu[r0 + r] = c->kc_hi; }
+        }
+    }
     /* path rows: the equation's bounds repeated at every mesh point
      * (CasOCTranscription.cpp:429-432) */
     /* endpoint rows: the constraint info's bounds (CasOCTranscription.cpp:
@@ -909,7 +1030,7 @@ int orc_get_bounds(const orc_ctx* c, double* xl, double* xu, double* gl, double*
     if (gl && c->NPC) {
         int rpi = rows_per_interval(c);
         for (int i = 0; i <= c->N; ++i) {
-            int64_t r0 = c->NEP + (int64_t)i * rpi;
+            int64_t r0 = c->NEP + (int64_t)i * rpi + c->NK;
             for (int e = 0; e < c->NPC; ++e) { gl[r0 + e] = c->pc[e].g.lower; gu[r0 + e] = c->pc[e].g.upper; }
         }
     }
@@ -1416,6 +1537,40 @@ static void table_eval_d(const orc_ctx* c, int ti, int col, real t, real* v, rea
 static void eval_dae_full(const orc_ctx* c, dae_ws* w, real time, const real* x,
         const real* ctrl, const real* wacc, real* out);
 
+/* Kinematic-constraint outputs of the DAE callback: the errors of each
+ * CoordinateCoupler phi = scale f(q_i) - q_d (Simbody position, velocity and
+ * acceleration errors; MocoCasOCProblem.h:664-732 copies qerr, uerr, udoterr
+ * in that order: all position errors, then all velocity errors, then all
+ * acceleration errors, the last two only when enforcing derivatives), and
+ * the velocity correction G^T gamma (MocoCasOCProblem.h:298-332) from the
+ * slack inputs.  udot: the callback's accelerations (explicit: the forward
+ * dynamics result; implicit: the acceleration variables). */
+static void kc_outputs(const orc_ctx* c, const real* q, const real* u, const real* udot,
+        const real* ctrl, real* out) {
+    int NKC = c->NKC;
+    if (!NKC) return;
+    real* e = out + c->OKC;
+    const real* gam = ctrl + c->NC + c->NDV + c->NM;
+    real* qc = c->NSL ? out + c->OQC : NULL;
+    if (qc) for (int j = 0; j < c->NQ; ++j) qc[j] = 0.0;
+    for (int i = 0; i < NKC; ++i) {
+        const mh_constraint* K = &c->kcs[i];
+        int ci = c->funcs[K->func].coord, d = K->dependent;
+        real fv[3];
+        eval_function(c, K->func, q, fv);
+        real gi = K->scale * fv[1];
+        e[i] = K->scale * fv[0] - q[d];
+        if (c->enforce) {
+            e[NKC + i] = gi * u[ci] - u[d];
+            e[2 * NKC + i] = (gi * udot[ci] - udot[d]) + K->scale * fv[2] * u[ci] * u[ci];
+        }
+        if (qc) {
+            qc[ci] += gi * gam[i];
+            qc[d] -= gam[i];
+        }
+    }
+}
+
 /* The DAE callback on NLP inputs: explicit / implicit mode pass through;
  * prescribed kinematics assemble [q, u, z] and udot from the motion. */
 static void eval_dae_point(const orc_ctx* c, dae_ws* w, real time, const real* x,
@@ -1484,6 +1639,17 @@ static void eval_dae_full(const orc_ctx* c, dae_ws* w, real time, const real* x,
             w->tau[A->target] += ctrl[ia] * A->optimal_force;
         }
     }
+    /* Kinematic constraint forces from the multipliers, applied like applied
+     * forces: -G^T lambda (MocoCasOCProblem.h:643-662) */
+    const real* lam = ctrl + c->NC + c->NDV;
+    for (int i = 0; i < c->NKC; ++i) {
+        const mh_constraint* K = &c->kcs[i];
+        real fv[3];
+        eval_function(c, K->func, q, fv);
+        real gi = K->scale * fv[1];
+        w->tau[c->funcs[K->func].coord] -= gi * lam[i];
+        w->tau[K->dependent] -= -lam[i];
+    }
     for (int im = 0; im < Mo->nmuscles; ++im) {
         const mh_muscle* mu = &c->mus[im];
         real L, V;
@@ -1541,6 +1707,7 @@ static void eval_dae_full(const orc_ctx* c, dae_ws* w, real time, const real* x,
     for (int j = 0; j < NQ; ++j) w->tau[j] -= sv_dot(w->S[j], w->F[c->coord_body[j] + 1]);
     if (wacc) {
         for (int j = 0; j < NQ; ++j) out[j] = -w->tau[j];
+        kc_outputs(c, q, u, wacc, ctrl, out);
         return;
     }
     /* CRBA mass matrix. */
@@ -1597,6 +1764,7 @@ static void eval_dae_full(const orc_ctx* c, dae_ws* w, real time, const real* x,
         for (int k = i + 1; k < NQ; ++k) t -= L[k * NQ + i] * y[k];
         y[i] = t / L[i * NQ + i];
     }
+    kc_outputs(c, q, u, y, ctrl, out);
 }
 
 #ifndef ORACLE_COUNTING
@@ -1636,18 +1804,24 @@ static void times_of(const orc_ctx* c, const double* x, double* t) {
     for (int k = 0; k < c->G; ++k) t[k] = (tf - t0) * c->grid[k] + t0;
 }
 
-/* st: states; ct: controls followed (implicit) by the accelerations */
+/* st: states; ct: controls, the derivative variables (implicit), the
+ * multipliers, then the slacks (the interval's at a mesh-interval midpoint,
+ * 0 elsewhere) */
 static void gather_point(const orc_ctx* c, const double* x, int k, double* st, double* ct) {
     memcpy(st, x + col_state(c, k, 0), sizeof(double) * (size_t)c->NS);
     if (c->NC) memcpy(ct, x + col_control(c, k, 0), sizeof(double) * (size_t)c->NC);
     if (c->NDV) memcpy(ct + c->NC, x + col_deriv(c, k, 0), sizeof(double) * (size_t)c->NDV);
+    if (c->NM) memcpy(ct + c->NC + c->NDV, x + col_mult(c, k, 0), sizeof(double) * (size_t)c->NM);
+    for (int l = 0; l < c->NSL; ++l)
+        ct[c->NC + c->NDV + c->NM + l] = vc_point(c, k) ? x[col_slack(c, (k - 1) / 2, l)] : 0.0;
 }
 
 /* xdot at all grid points: qdot = u (CasOCTranscription.cpp:313-314),
  * udot = the derivative variables in implicit mode (:339-341), callback
  * outputs for the rest. xd: NS x G (grid-major); res: NQ x G multibody
  * residuals (implicit mode, else unused). */
-static void all_xdot(orc_ctx* c, const double* x, const double* times, double* xd, double* res) {
+static void all_xdot(orc_ctx* c, const double* x, const double* times, double* xd, double* res,
+        double* kce) {
     int NS = c->NS, NC = c->NC, NO = nout(c), NR = nres(c);
 #pragma omp parallel num_threads(c->nthreads)
     {
@@ -1655,7 +1829,7 @@ static void all_xdot(orc_ctx* c, const double* x, const double* times, double* x
         ws_alloc(c, &w);
         double* st = (double*)malloc(sizeof(double) * (size_t)(c->NP + NO + 1));
         double* ct = st + NS;
-        double* y = ct + NC + c->NDV;
+        double* y = ct + (c->NP - NS);
 #pragma omp for schedule(static)
         for (int k = c->gk0; k <= c->gk1; ++k) {
             gather_point(c, x, k, st, ct);
@@ -1663,11 +1837,17 @@ static void all_xdot(orc_ctx* c, const double* x, const double* times, double* x
             int TQ = c->TQ;
             eval_dae_point(c, &w, times[k], st, ct, y);
             for (int s = 0; s < NS; ++s) {
-                if (s < TQ) o[s] = st[TQ + s];                          /* qdot = u */
+                if (s < TQ) {                                           /* qdot = u */
+                    o[s] = st[TQ + s];
+                    /* + the velocity correction at a mesh-interval midpoint
+                     * (CasOCTranscription.cpp:316-333) */
+                    if (vc_point(c, k)) o[s] = st[TQ + s] + y[c->OQC + s];
+                }
                 else if (c->NACC && s < 2 * TQ) o[s] = ct[NC + s - TQ];  /* udot = w */
                 else o[s] = y[s + c->SO];                               /* callback */
             }
             for (int r = 0; r < NR; ++r) res[(int64_t)k * NR + r] = y[res_out(c, r)];
+            for (int r = 0; r < c->NK; ++r) kce[(int64_t)k * c->NK + r] = y[c->OKC + r];
         }
         free(st);
         ws_free(&w);
@@ -1793,7 +1973,7 @@ int orc_get_callback_sparsity(const orc_ctx* c, uint8_t* pattern, int64_t len) {
 /* g from the grid times, xdot (xd: NS per point) and residual outputs
  * (res: nres per point) at every grid point (flattenConstraints order). */
 static void g_assemble(const orc_ctx* c, const double* x, const double* times, const double* xd,
-        const double* res, double* g) {
+        const double* res, const double* kce, double* g) {
     int NS = c->NS, NC = c->NC, NR = nres(c);
     int rpi = rows_per_interval(c);
     /* endpoint rows first */
@@ -1805,16 +1985,18 @@ static void g_assemble(const orc_ctx* c, const double* x, const double* times, c
     }
     g += c->NEP;
     double* pin = (double*)malloc(sizeof(double) * (size_t)(c->NP + 1));
-    /* path rows of every mesh point: interval i opens with mesh point i's,
-     * the tail with the final mesh point's */
-    for (int i = 0; i <= c->N && c->NPC; ++i) {
+    /* kinematic and path rows of every mesh point: interval i opens with
+     * mesh point i's, the tail with the final mesh point's */
+    for (int i = 0; i <= c->N; ++i) {
         int k = mesh_point(c, i);
+        for (int r = 0; r < c->NK; ++r) g[(int64_t)i * rpi + r] = kce[(int64_t)k * c->NK + r];
+        if (!c->NPC) continue;
         gather_point(c, x, k, pin, pin + NS);
-        for (int e = 0; e < c->NPC; ++e) g[(int64_t)i * rpi + e] = path_value(c, e, times[k], pin + NS);
+        for (int e = 0; e < c->NPC; ++e) g[(int64_t)i * rpi + c->NK + e] = path_value(c, e, times[k], pin + NS);
     }
     free(pin);
     for (int i = 0; i < c->N; ++i) {
-        double* gi = g + (int64_t)i * rpi + c->NPC;
+        double* gi = g + (int64_t)i * rpi + c->NK + c->NPC;
         /* residual rows of the interval's grid points first */
         int npts = c->scheme == MH_HERMITE_SIMPSON ? 2 : 1;
         int k0 = c->scheme == MH_HERMITE_SIMPSON ? 2 * i : i;
@@ -1848,7 +2030,7 @@ static void g_assemble(const orc_ctx* c, const double* x, const double* times, c
             for (int s = 0; s < NS; ++s) gi[s] = xp[s] - (xi[s] + 0.5 * h * (fp[s] + fi[s]));
         }
     }
-    for (int o = 0; o < NR; ++o) g[(int64_t)c->N * rpi + c->NPC + o] = res[(int64_t)(c->G - 1) * NR + o];
+    for (int o = 0; o < NR; ++o) g[(int64_t)c->N * rpi + c->NK + c->NPC + o] = res[(int64_t)(c->G - 1) * NR + o];
 }
 
 /* A shard context evaluates its grid points only and returns its rows /
@@ -1860,19 +2042,21 @@ int orc_eval_g(orc_ctx* c, const double* x, double* g) {
     double* times = (double*)malloc(sizeof(double) * (size_t)c->G);
     double* xd = (double*)calloc((size_t)c->G * (size_t)NS + 1, sizeof(double));
     double* res = (double*)calloc((size_t)c->G * (size_t)NR + 1, sizeof(double));
+    double* kce = (double*)calloc((size_t)c->G * (size_t)c->NK + 1, sizeof(double));
     times_of(c, x, times);
-    all_xdot(c, x, times, xd, res);
+    all_xdot(c, x, times, xd, res, kce);
     if (sharded(c)) {
         double* full = (double*)calloc((size_t)c->m + 1, sizeof(double));
-        g_assemble(c, x, times, xd, res, full);
+        g_assemble(c, x, times, xd, res, kce, full);
         memcpy(g, full + c->row_begin, sizeof(double) * (size_t)(c->row_end - c->row_begin));
         free(full);
     } else {
-        g_assemble(c, x, times, xd, res, g);
+        g_assemble(c, x, times, xd, res, kce, g);
     }
     free(times);
     free(xd);
     free(res);
+    free(kce);
     return MH_OK;
 }
 
@@ -1989,7 +2173,12 @@ static void path_blocks(const orc_ctx* c, const double* x, const double* times, 
  * 2+j = input j).  For s < NQ, qdot = u exactly. */
 static double xdot_deriv(const orc_ctx* c, const double* D, int k, int s, int d) {
     int NQ = c->TQ, NO = nout(c), ND = c->NP + 2;
-    if (s < NQ) return (d == 2 + NQ + s) ? 1.0 : 0.0;
+    if (s < NQ) {
+        double v = (d == 2 + NQ + s) ? 1.0 : 0.0;
+        /* midpoint: + the velocity correction's FD quotient */
+        if (vc_point(c, k)) v = v + D[((int64_t)k * ND + d) * NO + (c->OQC + s)];
+        return v;
+    }
     if (c->NACC && s < 2 * NQ) return (d == 2 + c->NS + c->NC + (s - NQ)) ? 1.0 : 0.0;
     return D[((int64_t)k * ND + d) * NO + (s + c->SO)];
 }
@@ -2010,6 +2199,18 @@ static int col_to_dir(const orc_ctx* c, int64_t col, int* k) {
         return 2 + c->NS + (int)(r % c->NC);
     }
     r -= cblock;
+    int64_t mblock = (int64_t)c->NM * c->G;
+    if (r < mblock) {
+        *k = (int)(r / c->NM);
+        return 2 + c->NS + c->NC + c->NDV + (int)(r % c->NM);
+    }
+    r -= mblock;
+    int64_t lblock = (int64_t)c->NSL * c->N;
+    if (r < lblock) {   /* slack l of interval i: an input of the midpoint */
+        *k = 2 * (int)(r / c->NSL) + 1;
+        return 2 + c->NPD + (int)(r % c->NSL);
+    }
+    r -= lblock;
     *k = (int)(r / c->NDV);
     return 2 + c->NS + c->NC + (int)(r % c->NDV);
 }
@@ -2058,12 +2259,19 @@ static void jac_assemble(const orc_ctx* c, const double* x, const double* times,
         double v = 0.0;
         int kc;
         int dir = col_to_dir(c, col, &kc);
-        if (row >= (int64_t)c->N * rpi) {   /* final mesh point: path rows, then residuals */
+        if (row >= (int64_t)c->N * rpi) {   /* final mesh point: kinematic and path rows, then residuals */
             int rt = (int)(row - (int64_t)c->N * rpi);
+            if (rt < c->NK) { values[e] = D[((int64_t)(c->G - 1) * ND + dir) * NO + c->OKC + rt]; continue; }
+            rt -= c->NK;
             if (rt < NPC) values[e] = Dp[((int64_t)c->N * ND + dir) * NPC + rt];
             else values[e] = D[((int64_t)(c->G - 1) * ND + dir) * NO + res_out(c, rt - NPC)];
             continue;
         }
+        if (rl < c->NK) {                   /* kinematic rows of the interval's mesh point */
+            values[e] = D[((int64_t)mesh_point(c, i) * ND + dir) * NO + c->OKC + rl];
+            continue;
+        }
+        rl -= c->NK;
         if (rl < NPC) {                     /* path rows of the interval's mesh point */
             values[e] = Dp[((int64_t)i * ND + dir) * NPC + rl];
             continue;
@@ -2159,8 +2367,10 @@ int orc_eval_jac_g(orc_ctx* c, const double* x, double* values) {
     double* D = (double*)calloc((size_t)c->G * (size_t)ND * (size_t)NO + 1, sizeof(double));
     double* res = (double*)calloc((size_t)c->G * (size_t)NR + 1, sizeof(double));
     double* Dp = (double*)calloc((size_t)(c->N + 1) * (size_t)ND * (size_t)NPC + 1, sizeof(double));
+    double* kce = (double*)calloc((size_t)c->G * (size_t)c->NK + 1, sizeof(double));
     times_of(c, x, times);
-    all_xdot(c, x, times, xd, res);
+    all_xdot(c, x, times, xd, res, kce);
+    free(kce);
     fd_blocks(c, x, times, D);
     if (NPC) path_blocks(c, x, times, Dp);
     if (sharded(c)) {
@@ -2191,12 +2401,17 @@ int orc_assemble_from_lanes(orc_ctx* c, const double* x, const double* times, co
     double* xd = (double*)malloc(sizeof(double) * (size_t)c->G * (size_t)NS);
     double* D = (double*)malloc(sizeof(double) * (size_t)c->G * (size_t)ND * (size_t)NO);
     double* res = (double*)malloc(sizeof(double) * ((size_t)c->G * (size_t)NR + 1));
+    double* kce = (double*)malloc(sizeof(double) * ((size_t)c->G * (size_t)c->NK + 1));
     double* Dp = (double*)malloc(sizeof(double) * ((size_t)(c->N + 1) * (size_t)ND * (size_t)NPC + 1));
     for (int k = 0; k < c->G; ++k) {
         const double* Yk = Y + (int64_t)k * NO * S;
+        for (int r = 0; r < c->NK; ++r) kce[(int64_t)k * c->NK + r] = Yk[(int64_t)(c->OKC + r) * S + base];
         for (int s = 0; s < NS; ++s) {
             double v;
-            if (s < TQ) v = x[col_state(c, k, TQ + s)];                     /* qdot = u */
+            if (s < TQ) {                                                   /* qdot = u */
+                v = x[col_state(c, k, TQ + s)];
+                if (vc_point(c, k)) v = v + Yk[(int64_t)(c->OQC + s) * S + base];
+            }
             else if (c->NACC && s < 2 * TQ) v = x[col_deriv(c, k, s - TQ)];  /* udot = w */
             else v = Yk[(int64_t)(s + c->SO) * S + base];
             xd[(int64_t)k * NS + s] = v;
@@ -2213,8 +2428,9 @@ int orc_assemble_from_lanes(orc_ctx* c, const double* x, const double* times, co
             }
     }
     if (NPC) path_blocks(c, x, times, Dp);
-    if (g) g_assemble(c, x, times, xd, res, g);
+    if (g) g_assemble(c, x, times, xd, res, kce, g);
     if (values) jac_assemble(c, x, times, xd, D, Dp, values);
+    free(kce);
     free(Dp);
     free(xd);
     free(D);
@@ -2345,7 +2561,7 @@ int orc_eval_grad_f(orc_ctx* c, const double* x, double* grad) {
             double L0 = goal_integrand(c, G, t, in, in + NS);
             acc += c->quad[k] * L0;
             double wq = G->weight * dur * c->quad[k];
-            for (int d = 0; d < NP + 2; ++d) {
+            for (int d = 0; d < c->NPD + 2; ++d) {   /* the goal callback's inputs */
                 double seed = d == 0 ? 1.0 - c->grid[k] : (d == 1 ? c->grid[k] : 1.0);
                 double lp = 0, lm = 0;
                 int idx = d - 2;
@@ -2362,9 +2578,7 @@ int orc_eval_grad_f(orc_ctx* c, const double* x, double* grad) {
                 int64_t col;
                 if (d == 0) col = 0;
                 else if (d == 1) col = 1;
-                else if (idx < NS) col = col_state(c, k, idx);
-                else if (idx < NS + c->NC) col = col_control(c, k, idx - NS);
-                else col = col_deriv(c, k, idx - NS - c->NC);
+                else col = col_input(c, k, idx);
                 grad[col] += wq * dL;
             }
         }

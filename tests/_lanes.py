@@ -16,11 +16,9 @@ def grid(nlp):
 
 
 def point_inputs(nlp, x):
-    """[G, NS + NC + NDV]: each grid point's callback inputs."""
-    G, NS, NC, NDV = nlp.G, nlp.NS, nlp.NC, nlp.NDV
-    return np.concatenate([x[2:2 + NS * G].reshape(G, NS),
-                           x[2 + NS * G:2 + (NS + NC) * G].reshape(G, NC),
-                           x[2 + (NS + NC) * G:].reshape(G, NDV)], 1)
+    """[G, NI]: each grid point's inputs (states, controls, derivatives,
+    multipliers, slacks)."""
+    return nlp.point_inputs(x)
 
 
 def lane_rows(nlp, x, times):

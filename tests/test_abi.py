@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "mocohip.h")
 
 STRUCTS = ["mh_function", "mh_axis", "mh_body", "mh_path_point", "mh_muscle",
-           "mh_actuator", "mh_table", "mh_external_force", "mh_model",
+           "mh_actuator", "mh_table", "mh_external_force", "mh_constraint", "mh_model",
            "mh_bounds", "mh_variable_info", "mh_goal", "mh_path_equation", "mh_endpoint_equation",
            "mh_problem",
            "mh_options", "mh_nlp_info"]
@@ -34,7 +34,7 @@ def test_library_loads_and_exports_every_symbol():
     lib = abi.load_mocohip()
     for name in abi.MOCOHIP_SYMBOLS:
         assert hasattr(lib, name), name
-    assert lib.mh_abi_version() == abi.MH_ABI_VERSION == 3
+    assert lib.mh_abi_version() == abi.MH_ABI_VERSION == 4
     out = subprocess.run(["nm", "-D", "--defined-only", abi.LIBMOCOHIP_PATH],
                          capture_output=True, text=True, check=True).stdout
     exported = set(re.findall(r" T (mh_\w+)", out))

@@ -138,6 +138,18 @@ CASES = {
     "double_pendulum_swingup_implicit_central": lambda: _central(
         configs.double_pendulum_swingup(29, dynamics="implicit")),
     "gait_rigid_nointerp_trap": lambda: _nointerp(_trap(configs.gait10dof18musc(6))),
+    # kinematic constraints: testConstraints.cpp's
+    # CoordinateCoupler double pendulum, multipliers, kinematic rows at the
+    # mesh points, velocity-correction slacks at the HS midpoints
+    "coupled_pendulum": lambda: configs.double_pendulum_coupled(20),
+    "coupled_pendulum_spline_central": lambda: _central(configs.double_pendulum_coupled(12, coupler="spline")),
+    "coupled_pendulum_implicit": lambda: configs.double_pendulum_coupled(16, dynamics="implicit",
+                                                                         coupler="spline"),
+    "coupled_pendulum_noderiv_trap": lambda: configs.double_pendulum_coupled(
+        14, "trapezoidal", enforce_constraint_derivatives=False, coupler="spline"),
+    "coupled_pendulum_trap_implicit": lambda: configs.double_pendulum_coupled(10, "trapezoidal", "implicit"),
+    "coupled_pendulum_noderiv_hs": lambda: configs.double_pendulum_coupled(
+        10, enforce_constraint_derivatives=False),
 }
 
 
@@ -216,20 +228,24 @@ def _row_mask(ref, x):
     rpi, tail = _rows(ref)
     nres, npc, nacc, nmb = ref.NRES, ref.NPC, ref.NACC, ref.NMB
     # residual row r of a grid point -> its callback output
-    rout = [r if r < nmb else ref.NO - ref.NAR + (r - nmb) for r in range(nres)]
+    rout = [r if r < nmb else ref.NQ + ref.NZ + (r - nmb) for r in range(nres)]
     npres = step if nres else 0
     mask = np.ones((N, rpi), bool)
     ndef = 2 * NS if hs else NS
+    lead = ref.NK + npc   # the mesh point's kinematic and path rows
+    okc = ref.NQ + ref.NZ + ref.NAR
     for i in range(N):
         ok = R[i * step:i * step + step + 1].all(0)
+        mask[i, :ref.NK] = R[i * step, okc:okc + ref.NK]
         for row in range(npres * nres):
-            mask[i, npc + row] = R[i * step + row // nres, rout[row % nres]]
+            mask[i, lead + row] = R[i * step + row // nres, rout[row % nres]]
         TQ = ref.TQ
         for row in range(ndef):
             s = row % NS
             if s >= (2 * TQ if nacc else TQ):
-                mask[i, npc + npres * nres + row] = ok[s + ref.SO]
-    return np.concatenate([np.ones(ref.NEP, bool), mask.reshape(-1), np.ones(npc, bool), R[-1, rout]])
+                mask[i, lead + npres * nres + row] = ok[s + ref.SO]
+    return np.concatenate([np.ones(ref.NEP, bool), mask.reshape(-1), R[-1, okc:okc + ref.NK],
+                           np.ones(npc, bool), R[-1, rout]])
 
 
 BACKENDS = ["auto", "lane", "generic"]
@@ -323,12 +339,8 @@ def _detection_points(nlp, solver):
 
 def _points(nlp, x):
     """Per grid point DAE inputs [t, states, controls(, accelerations)]."""
-    G, NS, NC, NDV = nlp.G, nlp.NS, nlp.NC, nlp.NDV
     t = np.array([(x[1] - x[0]) * g + x[0] for g in _grid(nlp)])
-    S = x[2:2 + NS * G].reshape(G, NS)
-    U = x[2 + NS * G:2 + (NS + NC) * G].reshape(G, NC)
-    W = x[2 + (NS + NC) * G:].reshape(G, NDV)
-    return np.concatenate([t[:, None], S, U, W], 1)
+    return np.concatenate([t[:, None], nlp.point_inputs(x)], 1)
 
 
 def _grid(nlp):
@@ -480,7 +492,8 @@ def test_eval_jac_g(name, backend):
 @pytest.mark.parametrize("name", ["sliding_mass", "double_pendulum_hs", "gait_rigid_forward",
                                   "gait_compliant_central", "double_pendulum_implicit_hs",
                                   "gait_rigid_implicit", "gait_inverse", "pendulum_bound_both_implicit",
-                                  "double_pendulum_swingup", "double_pendulum_swingup_implicit_central"])
+                                  "double_pendulum_swingup", "double_pendulum_swingup_implicit_central",
+                                  "coupled_pendulum", "coupled_pendulum_implicit"])
 def test_objective_and_gradient(name):
     gpu, ref, st = _pair(name)
     for _, x in _iterates(gpu):
@@ -495,7 +508,8 @@ def test_objective_and_gradient(name):
                                   "gait_rigid_implicit", "gait_rigid_pathcon",
                                   "pendulum_bound_both_implicit", "gait_rigid_sparse_random",
                                   "gait_implicit_pathcon_sparse", "gait_inverse_style_sparse",
-                                  "gait_inverse_sparse", "gait_inverse", "gait_inverse_random"])
+                                  "gait_inverse_sparse", "gait_inverse", "gait_inverse_random",
+                                  "coupled_pendulum", "coupled_pendulum_noderiv_trap"])
 def test_shards_reassemble_bit_exact(name):
     """Mesh-interval shards (the multi-GPU partition) concatenate to exactly
     the unsharded g and Jacobian values."""
@@ -760,7 +774,8 @@ def _tight_bound(gpu, ref, x, J0, Y, Y0, h_fd):
 @pytest.mark.parametrize("name", ["double_pendulum_hs", "double_pendulum_trap", "gait_rigid_forward",
                                   "gait_rigid_central", "gait_compliant_central", "gait_rigid_implicit",
                                   "gait_rigid_pathcon", "gait_implicit_tendon", "gait_inverse",
-                                  "gait_inverse_random", "gait_rigid_nointerp_trap"])
+                                  "gait_inverse_random", "gait_rigid_nointerp_trap", "coupled_pendulum",
+                                  "coupled_pendulum_implicit"])
 def test_jacobian_tight_bound(name):
     """End to end at h_fd = 1e-4 (CasADi-style quotients of the same
     callbacks): |J_gpu - J_oracle| <= 1e-8 |J| + 4 dY_i (h_i + 1) / h_fd

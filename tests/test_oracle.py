@@ -1057,3 +1057,110 @@ def test_goal_term_indices_validated():
     rep._gidx[0] = 7      # a body that does not exist
     with pytest.raises(RuntimeError, match="out of range"):
         OracleNLP(rep, st.solver.options())
+
+
+# ---- kinematic constraints --------------------------------
+
+def _kc(N=6, scheme="hermite-simpson", dynamics="explicit", enforce=True, coupler="linear"):
+    st = configs.double_pendulum_coupled(N, scheme, dynamics, enforce, coupler)
+    return OracleNLP(st.problem.create_rep(), st.solver.options()), st
+
+
+@pytest.mark.parametrize("scheme", ["hermite-simpson", "trapezoidal"])
+@pytest.mark.parametrize("enforce", [True, False])
+@pytest.mark.parametrize("dynamics", ["explicit", "implicit"])
+def test_kinematic_constraint_layout(scheme, enforce, dynamics):
+    """CasOCTranscription.cpp:103-140,209-241,298-309 and flattenConstraints
+    (CasOCTranscription.h:219-313): one multiplier per holonomic equation at
+    every grid point (bounds multiplier_bounds, default [-1000, 1000]), with
+    enforced derivatives one slack per multiplier at each mesh-interval
+    midpoint (HS only; velocity_correction_bounds [-0.1, 0.1]) and
+    position + velocity + acceleration error rows (else position only) at
+    every mesh point, first among the mesh point's rows, bounds [0, 0]."""
+    N = 5
+    nlp, st = _kc(N, scheme, dynamics, enforce)
+    hs = scheme == "hermite-simpson"
+    G = 2 * N + 1 if hs else N + 1
+    NS, NC, NM = 4, 2, 1
+    NDV = 2 if dynamics == "implicit" else 0
+    NSL = 1 if (enforce and hs) else 0
+    NK = 3 if enforce else 1
+    assert nlp.n == 2 + (NS + NC + NM + NDV) * G + NSL * N
+    nres = 2 if dynamics == "implicit" else 0
+    rpi = NK + (2 * NS + NC if hs else NS) + nres * (2 if hs else 1)
+    assert nlp.m == N * rpi + NK + nres
+    xl, xu, gl, gu = nlp.bounds()
+    mult = 2 + (NS + NC) * G
+    assert np.all(xl[mult:mult + G] == -1000) and np.all(xu[mult:mult + G] == 1000)
+    assert np.all(xl[mult + G:mult + G + NSL * N] == -0.1) and np.all(xu[mult + G:mult + G + NSL * N] == 0.1)
+    assert np.all(gl == 0) and np.all(gu == 0)
+    # the kinematic rows of mesh point i read its multiplier (block-dense
+    # over the point's callback inputs), never a slack
+    ir, jc = nlp.jac_structure()
+    for i in range(N + 1):
+        k = 2 * i if hs else i
+        rows = i * rpi + np.arange(NK)
+        cols = jc[np.isin(ir, rows)]
+        assert mult + k in cols
+        assert not np.any((cols >= mult + G) & (cols < mult + G + NSL * N))
+    # Simpson q-rows read the interval's slack (velocity correction)
+    if NSL:
+        for i in range(N):
+            srow = i * rpi + NK + nres * 2 + NS          # first Simpson row
+            assert mult + G + i in jc[ir == srow]
+
+
+@pytest.mark.parametrize("scheme", ["hermite-simpson", "trapezoidal"])
+@pytest.mark.parametrize("enforce", [True, False])
+@pytest.mark.parametrize("dynamics", ["explicit", "implicit"])
+def test_kinematic_constraint_jacobian_numerical(scheme, enforce, dynamics):
+    """eval_jac_g (FD quotients through the transcription chain rule) against
+    a central numerical derivative of eval_g, and every dependence of g
+    inside the structure (SimmSpline coupler: curvature in the acceleration
+    errors and the velocity correction)."""
+    nlp, _ = _kc(5, scheme, dynamics, enforce, "spline")
+    x = nlp.random_iterate(np.random.default_rng(3).uniform(-1, 1, nlp.n))
+    J = nlp.eval_jac_g(x)
+    ir, jc = nlp.jac_structure()
+    inside = np.zeros((nlp.m, nlp.n), bool)
+    inside[ir, jc] = True
+    Jn = np.zeros((nlp.m, nlp.n))
+    for c in range(nlp.n):
+        e = np.zeros(nlp.n)
+        e[c] = 1e-6
+        Jn[:, c] = (nlp.eval_g(x + e) - nlp.eval_g(x - e)) / 2e-6
+    assert np.abs(Jn[~inside]).max(initial=0.0) == 0.0
+    scale = np.abs(Jn).max() + 1.0
+    assert np.abs(J - Jn[ir, jc]).max() <= 1e-6 * scale
+
+
+def test_kinematic_constraint_physics():
+    """CoordinateCoupler q1 = -2 q0 + pi (testConstraints.cpp:629-645) on the
+    DAE callback: the position and velocity errors vanish on a consistent
+    state; the acceleration error is affine in the multiplier and the
+    multiplier that zeroes it exists; the constraint force follows Simbody's
+    M udot + G^T lambda = f (d paerr / d lambda = -G M^-1 G^T < 0); the
+    implicit residual vanishes at the explicit accelerations under the same
+    multiplier; the velocity correction is G^T gamma = (-2 gamma, -gamma)."""
+    nlp, st = _kc(2)
+    q0, u0 = 0.3, -0.7
+    q = np.array([q0, -2 * q0 + math.pi])
+    u = np.array([u0, -2 * u0])
+    tau = np.array([1.5, -0.4])
+
+    def row(lam, gam=0.0):   # [t, q, u, tau, lambda, gamma]
+        return np.concatenate([[0.2], q, u, tau, [lam, gam]])
+    y = nlp.eval_dae(np.array([row(0.0), row(1.0), row(0.0, 0.05)]))
+    okc, oqc = 2, 5   # outputs: udot (2), kinematic errors (3), correction (2)
+    assert abs(y[0, okc]) < 1e-15 and abs(y[0, okc + 1]) < 1e-15
+    a0, a1 = y[0, okc + 2], y[1, okc + 2]
+    assert a1 - a0 < 0                                  # -G M^-1 G^T
+    lam = -a0 / (a1 - a0)
+    ys = nlp.eval_dae(np.array([row(lam)]))[0]
+    assert abs(ys[okc + 2]) < 1e-9 * (abs(a0) + 1)
+    assert abs(ys[1] + 2 * ys[0]) < 1e-9 * (abs(ys[0]) + 1)   # q1dd = -2 q0dd
+    np.testing.assert_allclose(y[2, oqc:oqc + 2], [-2 * 0.05, -0.05], rtol=0, atol=1e-15)
+    # implicit: M w + C - f + G^T lambda = 0 at w = the explicit udot
+    imp, _ = _kc(2, dynamics="implicit")
+    r = imp.eval_dae(np.array([np.concatenate([[0.2], q, u, tau, ys[:2], [lam, 0.0]])]))[0]
+    assert np.abs(r[:2]).max() < 1e-9 * (np.abs(tau).max() + 1)
