@@ -75,6 +75,7 @@ struct Tape {
     std::vector<double> gw;
     std::vector<mh_path_equation> path;
     std::vector<mh_endpoint_equation> endpoint;
+    std::vector<mh_constraint> constraints;
     std::vector<double> guess;
     std::vector<uint8_t> pattern;
     std::vector<int32_t> kin_col;
@@ -99,7 +100,8 @@ bool read_tape(const char* path, Tape& t, std::string& err) {
     const int version = r.pod<int32_t>();
     t.ns = r.pod<int32_t>();
     t.nc = r.pod<int32_t>();
-    if (version < 1 || version > 3) { err = "unsupported tape version"; return false; }
+    // version 4 = ABI v4's mh_options; earlier tapes carry a shorter one
+    if (version != 4) { err = "unsupported tape version (this build reads version 4)"; return false; }
     t.opts = r.pod<mh_options>();
     mh_model& m = t.prob.model;
     int32_t* counts[] = {&m.nq, &m.nbodies, &m.naxes, &m.nfunctions, &m.nknots, &m.nmuscles,
@@ -154,6 +156,12 @@ bool read_tape(const char* path, Tape& t, std::string& err) {
         t.prob.nendpoint = r.pod<int32_t>();
         t.endpoint = r.array<mh_endpoint_equation>(t.prob.nendpoint);
     }
+    if (version >= 4) {   // kinematic constraints, multiplier / kinematic-row bounds
+        m.nconstraints = r.pod<int32_t>();
+        t.constraints = r.array<mh_constraint>(m.nconstraints);
+        t.prob.multiplier_bounds = r.pod<mh_bounds>();
+        t.prob.kinematic_constraint_bounds = r.pod<mh_bounds>();
+    }
     if (!r.ok || r.pos != r.buf.size()) { err = "truncated or malformed tape"; return false; }
     m.bodies = t.bodies.data(); m.axes = t.axes.data(); m.functions = t.functions.data();
     m.knot_x = t.knot_x.data(); m.knot_y = t.knot_y.data(); m.muscles = t.muscles.data();
@@ -170,6 +178,7 @@ bool read_tape(const char* path, Tape& t, std::string& err) {
     t.opts.sparsity_pattern = t.pattern.empty() ? nullptr : t.pattern.data();
     t.prob.kinematics_column = t.kin_col.empty() ? nullptr : t.kin_col.data();
     t.prob.endpoint = t.endpoint.empty() ? nullptr : t.endpoint.data();
+    m.constraints = t.constraints.empty() ? nullptr : t.constraints.data();
     return true;
 }
 

@@ -425,7 +425,7 @@ class HipNLP(_NLPBase):
 
     def lane_stride(self) -> int:
         """Finite-difference lanes per grid point (mh_debug_jacobian_lanes)."""
-        ND = 2 + self.NS + self.NC + self.NDV
+        ND = 2 + self.NI
         return 2 * ND + 1 if self.opts.finite_difference_scheme == abi.MH_FD_CENTRAL else ND + 1
 
     def jacobian_lanes(self, x):

@@ -11,7 +11,10 @@ Layout (little endian, x86-64 struct layout of include/mocohip.h):
   mh_path_equation array, then the sparsity-detection guess (n doubles or
   empty), the given callback sparsity (bytes or empty) and the prescribed
   kinematics (table index, per-coordinate columns); version 3 appends the
-  endpoint-constraint equations (mh_problem.nendpoint/endpoint)."""
+  endpoint-constraint equations (mh_problem.nendpoint/endpoint); version 4
+  (ABI v4: mh_options grew) appends the kinematic constraints
+  (mh_model.nconstraints/constraints) and the multiplier and
+  kinematic-constraint bounds.  Readers accept version 4 only."""
 from __future__ import annotations
 
 import ctypes as C
@@ -20,7 +23,7 @@ import struct
 from . import abi
 
 MAGIC = b"MHTAPE01"
-VERSION = 3   # 2: + path-constraint equations; 3: + endpoint constraints
+VERSION = 4   # 2: + path constraints; 3: + endpoint constraints; 4: + kinematic constraints
 
 # (field, element type, count attribute of mh_model / None for problem arrays)
 _MODEL_ARRAYS = [
@@ -89,5 +92,8 @@ def write_tape(rep, opts: abi.mh_options, path: str) -> None:
     out += [struct.pack("<ii", p.prescribed_kinematics, p.kinematics_table), struct.pack("<q", len(kc)), kc]
     eb = _blob(p.endpoint, abi.mh_endpoint_equation, p.nendpoint)
     out += [struct.pack("<i", p.nendpoint), struct.pack("<q", len(eb)), eb]
+    kb = _blob(m.constraints, abi.mh_constraint, m.nconstraints)
+    out += [struct.pack("<i", m.nconstraints), struct.pack("<q", len(kb)), kb,
+            bytes(p.multiplier_bounds), bytes(p.kinematic_constraint_bounds)]
     with open(path, "wb") as fh:
         fh.write(b"".join(out))

@@ -381,6 +381,7 @@ static int64_t residual_rows(const orc_ctx* c, int k, int64_t row, row_fn emit, 
         int n = 0, o = res_out(c, r);
         if (dep(c->sp, c->NP, o, -1)) { cols[n++] = 0; cols[n++] = 1; }
         n += point_cols_dep(c, c->sp, o, k, -1, cols + n);
+        qsort(cols, (size_t)n, sizeof(int64_t), cmp64);   /* multipliers precede derivatives in x */
         emit(ud, row++, cols, n);
     }
     return row;
@@ -395,6 +396,7 @@ static int64_t path_rows(const orc_ctx* c, int k, int64_t row, row_fn emit, void
         int n = 0;
         if (dep(c->sp_pc, c->NP, e, -1)) { cols[n++] = 0; cols[n++] = 1; }
         n += point_cols_dep(c, c->sp_pc, e, k, -1, cols + n);
+        qsort(cols, (size_t)n, sizeof(int64_t), cmp64);
         emit(ud, row++, cols, n);
     }
     return row;
@@ -409,6 +411,7 @@ static int64_t kc_rows(const orc_ctx* c, int k, int64_t row, row_fn emit, void* 
         int n = 0;
         cols[n++] = 0; cols[n++] = 1;
         n += point_cols_dep(c, NULL, 0, k, -1, cols + n);
+        qsort(cols, (size_t)n, sizeof(int64_t), cmp64);
         emit(ud, row++, cols, n);
     }
     return row;

@@ -399,7 +399,7 @@ def physiological_iterate(nlp, seed=0):
         if n in muscles:
             U[:, j] = r.uniform(0.05, 0.4, G)
     if nlp.NAR:
-        W = x[2 + (NS + NC) * G:].reshape(G, nlp.NDV)
+        W = x[x.size - nlp.NDV * G:].reshape(G, nlp.NDV)   # the derivatives close x
         W[:, nlp.NACC:] = r.uniform(-0.5, 0.5, (G, nlp.NAR))
     return x
 

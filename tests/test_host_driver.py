@@ -8,6 +8,7 @@ import numpy as np
 import pytest
 
 from mocohip import configs
+from mocohip.model import CoordinateCouplerConstraint, Function
 from mocohip.tape import write_tape
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -32,6 +33,9 @@ def test_driver_loads_tape_and_fails_loudly_without_gpu(tmp_path):
     if torch.cuda.is_available():
         pytest.skip("GPU present")
     st = configs.gait10dof18musc(4, control_bounds=True)
+    # with a kinematic constraint: the tape carries it (version 4)
+    st.problem.model.add_constraint(CoordinateCouplerConstraint(
+        "knee_coupler", "knee_angle_l", Function.linear("knee_angle_r", 1.0, 0.0)))
     path = tmp_path / "gait.tape"
     write_tape(st.problem.create_rep(), st.solver.options(), str(path))
     r = _run(path)
@@ -47,6 +51,7 @@ def test_driver_loads_tape_and_fails_loudly_without_gpu(tmp_path):
     ("gait_rigid", lambda: configs.gait10dof18musc(20)),
     ("double_pendulum_implicit", lambda: configs.double_pendulum(20, dynamics="implicit")),
     ("gait_pathcon", lambda: configs.gait10dof18musc(10, control_bounds=True)),
+    ("coupled_pendulum", lambda: configs.double_pendulum_coupled(12, coupler="spline")),
 ])
 def test_driver_matches_python_binding_bit_exact(tmp_path, name, mk):
     """The C++ host and the ctypes binding drive the same library: same g and
