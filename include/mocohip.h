@@ -269,7 +269,14 @@ enum mh_goal_kind {
      * ground (x, y, z).  An endpoint cost: no integral; its gradient is the
      * finite difference of the cost over the final coordinates (the CasADi
      * FD of the cost callback, CasOCFunction.h:38-44). */
-    MH_GOAL_MARKER_FINAL = 5
+    MH_GOAL_MARKER_FINAL = 5,
+    /* minimize_lagrange_multipliers (CasOCTranscription.cpp:513-521):
+     * weight * duration * quadrature of the sum of squared Lagrange
+     * multipliers; terms index the multipliers.  Appended by the library
+     * when mh_options.minimize_lagrange_multipliers is set (weight
+     * lagrange_multiplier_weight); its gradient is exact (the reference
+     * differentiates this MX expression with AD, not by finite differences). */
+    MH_GOAL_LAGRANGE_MULTIPLIERS = 6
 };
 typedef struct mh_goal {
     int32_t kind;
@@ -429,10 +436,13 @@ typedef struct mh_options {
      * added to qdot there, CasOCTranscription.cpp:316-333), 1 = do not
      * (position errors only, no slacks).  velocity_correction_bounds: slack
      * bounds, {0, 0} = the default [-0.1, 0.1].  minimize_lagrange_multipliers
-     * is not implemented (MH_ERR_UNSUPPORTED if nonzero). */
+     * adds the MH_GOAL_LAGRANGE_MULTIPLIERS term with weight
+     * lagrange_multiplier_weight (0 = the default 1.0); it needs kinematic
+     * constraints (MocoCasOCProblem.cpp:101-107). */
     int32_t ignore_constraint_derivatives;
     int32_t minimize_lagrange_multipliers;
     double velocity_correction_bounds[2];
+    double lagrange_multiplier_weight;
 } mh_options;
 
 enum mh_sparsity {

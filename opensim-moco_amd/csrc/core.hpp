@@ -1451,6 +1451,7 @@ constexpr int MH_MARKER_MAX_Q = 64;   // coordinates a marker goal's kernel hold
 struct GoalSet {
     int ngoals;
     int nc, nacc;   // controls; accelerations before the auxiliary derivatives
+    int ndv;        // derivative variables (the multipliers follow them)
     const mh_goal* goals;
     const int* gidx;
     const int* gcol;
@@ -1475,6 +1476,9 @@ __device__ double goal_integrand(const DevModel& M, const GoalSet& GS, int g, do
             L += w * (v * v);
         } else if (G.kind == MH_GOAL_AUX_DERIVATIVES) {
             const double v = ct[GS.nc + GS.nacc + idx];   // derivatives follow the controls
+            L += w * (v * v);
+        } else if (G.kind == MH_GOAL_LAGRANGE_MULTIPLIERS) {
+            const double v = ct[GS.nc + GS.ndv + idx];    // multipliers follow the derivatives
             L += w * (v * v);
         }
     }
@@ -1537,8 +1541,13 @@ __global__ void __launch_bounds__(64) k_grad(DevModel M, Layout L, GoalSet GS, i
                 in[d - 2] = s;
             }
         }
-        const double dL = fd == MH_FD_CENTRAL ? (lp - lm) / (2.0 * h)
-                        : (fd == MH_FD_FORWARD ? (lp - l0) / h : (l0 - lm) / h);
+        double dL = fd == MH_FD_CENTRAL ? (lp - lm) / (2.0 * h)
+                  : (fd == MH_FD_FORWARD ? (lp - l0) / h : (l0 - lm) / h);
+        if (G.kind == MH_GOAL_LAGRANGE_MULTIPLIERS) {
+            // exact, like the reference's AD of this MX term: w 2 lambda
+            const int j = d - 2 - (L.NS + L.NC + L.NDV);
+            dL = (d >= 2 && j >= 0 && j < L.NM) ? GS.gw[G.term_begin + j] * (2.0 * in[d - 2]) : 0.0;
+        }
         acc += G.weight * dur * quad[k] * dL;
     }
     if (d < 2) tpart[(long)k * 2 + d] = acc;
@@ -1614,6 +1623,10 @@ struct mh_ctx {
     std::vector<uint8_t> sp, sp_pc;  // detected sparsity [output][time, inputs] (empty: dense)
     std::vector<mh_path_equation> pc;
     PathEqs P{};
+    // goals as uploaded: the problem's, then the internal multiplier term
+    std::vector<mh_goal> goals;
+    std::vector<int32_t> gidx, gcol;
+    std::vector<double> gw;
     // endpoint constraints: the head of g (rows 0..nep) and of the Jacobian
     // (entries 0..nnz_ep), owned by the shard with interval 0
     int nep = 0, nnz_ep = 0;

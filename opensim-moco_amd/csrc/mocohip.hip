@@ -897,10 +897,27 @@ static int validate_and_layout(mh_ctx* c, const mh_problem* p, const mh_options*
                 K.dependent == M.functions[f].coord)
             return set_err(MH_ERR_INVALID, "kinematic constraint %d: bad kind/function/coordinate", i);
     }
-    if (NKC && (c->presc || p->nendpoint > 0 || o->sparsity_detection != MH_SPARSITY_NONE ||
-                o->minimize_lagrange_multipliers))
+    if (NKC && (c->presc || p->nendpoint > 0 || o->sparsity_detection != MH_SPARSITY_NONE))
         return set_err(MH_ERR_UNSUPPORTED, "kinematic constraints with prescribed kinematics, endpoint "
-                       "constraints, sparsity detection or minimize_lagrange_multipliers");
+                       "constraints or sparsity detection");
+    if (o->minimize_lagrange_multipliers && !NKC)   // MocoCasOCProblem.cpp:101-107
+        return set_err(MH_ERR_INVALID, "Solver property 'minimize_lagrange_multipliers' was enabled but no "
+                       "enabled kinematic constraints exist in the model.");
+    // the goals as the device sees them: the problem's, then (minimize_
+    // lagrange_multipliers, CasOCTranscription.cpp:513-521) the multiplier term
+    c->goals.assign(p->goals, p->goals + p->ngoals);
+    c->gidx.assign(p->goal_index, p->goal_index + p->nterms);
+    c->gcol.assign(p->goal_column, p->goal_column + p->nterms);
+    c->gw.assign(p->goal_weight, p->goal_weight + p->nterms);
+    if (o->minimize_lagrange_multipliers) {
+        mh_goal G{};
+        G.kind = MH_GOAL_LAGRANGE_MULTIPLIERS;
+        G.term_begin = p->nterms;
+        G.term_count = NKC;
+        G.weight = o->lagrange_multiplier_weight != 0.0 ? o->lagrange_multiplier_weight : 1.0;
+        c->goals.push_back(G);
+        for (int j = 0; j < NKC; ++j) { c->gidx.push_back(j); c->gcol.push_back(0); c->gw.push_back(1.0); }
+    }
     c->NKC = NKC;
     c->enforce = !o->ignore_constraint_derivatives;
     c->NM = NKC;
@@ -1069,7 +1086,7 @@ static int validate_and_layout(mh_ctx* c, const mh_problem* p, const mh_options*
     c->cinfo.assign(p->control_infos, p->control_infos + c->NC);
     c->t_init = p->time_initial;
     c->t_final = p->time_final;
-    c->ngoals = p->ngoals;
+    c->ngoals = (int)c->goals.size();
     // size class
     int maxpts = 0;
     for (int im = 0; im < M.nmuscles; ++im) maxpts = std::max(maxpts, M.muscles[im].point_count);
@@ -1188,8 +1205,8 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
                  o_mi = A.put(c->mus_ider.data(), c->mus_ider.size()),
                  o_kcol = A.put(c->kin_col.data(), c->kin_col.size()),
                  o_md = A.put(mder.data(), mder.size()),
-                 o_goals = A.put(p->goals, p->ngoals), o_gidx = A.put(p->goal_index, p->nterms),
-                 o_gcol = A.put(p->goal_column, p->nterms), o_gw = A.put(p->goal_weight, p->nterms),
+                 o_goals = A.put(c->goals.data(), c->goals.size()), o_gidx = A.put(c->gidx.data(), c->gidx.size()),
+                 o_gcol = A.put(c->gcol.data(), c->gcol.size()), o_gw = A.put(c->gw.data(), c->gw.size()),
                  o_grid = A.put(c->grid.data(), c->grid.size()),
                  o_quad = A.put(c->quad.data(), c->quad.size()),
                  o_tpl = A.put(c->tpl.data(), c->tpl.size()),
@@ -1216,11 +1233,11 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     const size_t o_Yg = A.reserve(sizeof(double) * (size_t)c->nk * std::max(1, c->NO));
     const size_t o_g = A.reserve(sizeof(double) * ((size_t)c->nep + (size_t)nint * c->rpi + c->ntail));
     const size_t o_vals = A.reserve(sizeof(double) * ((size_t)c->nnz_ep + (size_t)nint * c->nnz_int + c->nnz_tail));
-    const size_t o_C = A.reserve(sizeof(double) * (size_t)c->G * std::max(1, p->ngoals));
+    const size_t o_C = A.reserve(sizeof(double) * (size_t)c->G * std::max(1, c->ngoals));
     const size_t o_grad = A.reserve(sizeof(double) * c->n);
     const size_t o_tpart = A.reserve(sizeof(double) * 2 * (size_t)c->G);
     const size_t o_f = A.reserve(sizeof(double) * 4);
-    const size_t o_epc = A.reserve(sizeof(double) * (size_t)std::max(1, p->ngoals));   // endpoint costs
+    const size_t o_epc = A.reserve(sizeof(double) * (size_t)std::max(1, c->ngoals));   // endpoint costs
     const int npts_iv = c->scheme == MH_HERMITE_SIMPSON ? 3 : 2;
     const size_t o_xch = A.reserve(sizeof(double) * (size_t)std::max(nint, 1) * npts_iv * std::max(1, c->NO) * XCH_W);
 
@@ -1268,7 +1285,8 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     D.coord_body = (const int*)(b + o_cb); D.mus_act_state = (const int*)(b + o_as);
     D.mus_ftn_state = (const int*)(b + o_fs); D.mus_control = (const int*)(b + o_mc);
     D.mus_derived = (const double*)(b + o_md);
-    c->GS.ngoals = p->ngoals;
+    c->GS.ngoals = c->ngoals;
+    c->GS.ndv = c->NDV;
     c->GS.nc = c->NC;
     c->GS.nacc = c->NACC;
     c->GS.goals = (const mh_goal*)(b + o_goals);

@@ -163,7 +163,7 @@ class mh_options(C.Structure):
                 ("sparsity_guess", P(f64)), ("sparsity_pattern", P(C.c_uint8)),
                 ("implicit_aux_bounds", f64 * 2),
                 ("ignore_constraint_derivatives", i32), ("minimize_lagrange_multipliers", i32),
-                ("velocity_correction_bounds", f64 * 2)]
+                ("velocity_correction_bounds", f64 * 2), ("lagrange_multiplier_weight", f64)]
 
 
 MH_SPARSITY_NONE, MH_SPARSITY_RANDOM, MH_SPARSITY_INITIAL_GUESS, MH_SPARSITY_GIVEN = 0, 1, 2, 3

@@ -86,12 +86,12 @@ def double_pendulum(num_mesh_intervals: int = 100, scheme: str = "hermite-simpso
 
 def double_pendulum_coupled(num_mesh_intervals: int = 20, scheme: str = "hermite-simpson",
                            dynamics: str = "explicit", enforce_constraint_derivatives: bool = True,
-                           coupler: str = "linear") -> MocoStudy:
+                           coupler: str = "linear", minimize_multipliers: bool = True) -> MocoStudy:
     """testConstraints.cpp:620-690 (testDoublePendulumCoordinateCoupler): a
     CoordinateCouplerConstraint q1 = -2 q0 + pi (LinearFunction(-2, pi)),
     control goal, HS N=20, both dynamics modes, with and without enforcing
-    the constraint derivatives.  (The reference also minimizes the Lagrange
-    multipliers with weight 10 -- not implemented here.)  coupler="spline":
+    the constraint derivatives, minimizing the Lagrange multipliers with
+    weight 10.  coupler="spline":
     the same constraint through a SimmSpline of the linear relation plus a
     quadratic term, so that f'' != 0 (acceleration errors and the
     velocity-correction Jacobian see the curvature)."""
@@ -114,7 +114,8 @@ def double_pendulum_coupled(num_mesh_intervals: int = 20, scheme: str = "hermite
     p.add_goal(MocoControlGoal())
     s = MocoHipSolver(num_mesh_intervals=num_mesh_intervals, transcription_scheme=scheme,
                       multibody_dynamics_mode=dynamics,
-                      enforce_constraint_derivatives=enforce_constraint_derivatives)
+                      enforce_constraint_derivatives=enforce_constraint_derivatives,
+                      minimize_lagrange_multipliers=minimize_multipliers, lagrange_multiplier_weight=10.0)
     return MocoStudy(p, s)
 
 

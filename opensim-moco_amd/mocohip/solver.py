@@ -57,6 +57,7 @@ class MocoHipSolver:
     enforce_constraint_derivatives: bool = True
     velocity_correction_bounds: tuple = (-0.1, 0.1)
     minimize_lagrange_multipliers: bool = False
+    lagrange_multiplier_weight: float = 1.0
     # the optimizer settings (MocoDirectCollocationSolver.cpp:23-42), mapped
     # to Ipopt options by ipopt_options()
     verbosity: int = 2
@@ -148,6 +149,7 @@ class MocoHipSolver:
         o.implicit_aux_bounds[1] = float(hi)
         o.ignore_constraint_derivatives = 0 if self.enforce_constraint_derivatives else 1
         o.minimize_lagrange_multipliers = int(bool(self.minimize_lagrange_multipliers))
+        o.lagrange_multiplier_weight = float(self.lagrange_multiplier_weight)
         lo, hi = self.velocity_correction_bounds
         o.velocity_correction_bounds[0] = float(lo)
         o.velocity_correction_bounds[1] = float(hi)

@@ -748,11 +748,34 @@ int orc_create(const mh_problem* p, const mh_options* o, orc_ctx** out) {
             return fail(MH_ERR_INVALID, "kinematic constraint %d: bad kind/function/coordinate", i);
         }
     }
-    if (c->NKC && (c->presc || p->nendpoint > 0 || o->sparsity_detection != MH_SPARSITY_NONE ||
-                   o->minimize_lagrange_multipliers)) {
+    if (c->NKC && (c->presc || p->nendpoint > 0 || o->sparsity_detection != MH_SPARSITY_NONE)) {
         orc_destroy(c);
         return fail(MH_ERR_UNSUPPORTED, "kinematic constraints with prescribed kinematics, endpoint "
-                    "constraints, sparsity detection or minimize_lagrange_multipliers");
+                    "constraints or sparsity detection");
+    }
+    if (o->minimize_lagrange_multipliers && !c->NKC) {   /* MocoCasOCProblem.cpp:101-107 */
+        orc_destroy(c);
+        return fail(MH_ERR_INVALID, "Solver property 'minimize_lagrange_multipliers' was enabled but no "
+                    "enabled kinematic constraints exist in the model.");
+    }
+    if (o->minimize_lagrange_multipliers) {
+        /* the multiplier term (CasOCTranscription.cpp:513-521) as one more
+         * goal, one term per multiplier */
+        int ng = c->P.ngoals, nt = c->P.nterms;
+        c->goals = (mh_goal*)realloc(c->goals, sizeof(mh_goal) * (size_t)(ng + 1));
+        c->gidx = (int32_t*)realloc(c->gidx, sizeof(int32_t) * (size_t)(nt + c->NKC));
+        c->gcol = (int32_t*)realloc(c->gcol, sizeof(int32_t) * (size_t)(nt + c->NKC));
+        c->gw = (double*)realloc(c->gw, sizeof(double) * (size_t)(nt + c->NKC));
+        mh_goal G;
+        memset(&G, 0, sizeof G);
+        G.kind = MH_GOAL_LAGRANGE_MULTIPLIERS;
+        G.term_begin = nt;
+        G.term_count = c->NKC;
+        G.weight = o->lagrange_multiplier_weight != 0.0 ? o->lagrange_multiplier_weight : 1.0;
+        c->goals[ng] = G;
+        for (int j = 0; j < c->NKC; ++j) { c->gidx[nt + j] = j; c->gcol[nt + j] = 0; c->gw[nt + j] = 1.0; }
+        c->P.ngoals = ng + 1;
+        c->P.nterms = nt + c->NKC;
     }
     c->enforce = !o->ignore_constraint_derivatives;
     c->NM = c->NKC;
@@ -2466,6 +2489,9 @@ static double goal_integrand(const orc_ctx* c, const mh_goal* G, double t, const
         } else if (G->kind == MH_GOAL_AUX_DERIVATIVES) {
             double v = ct[c->NC + c->NACC + idx];   /* derivatives follow the controls */
             L += w * (v * v);
+        } else if (G->kind == MH_GOAL_LAGRANGE_MULTIPLIERS) {
+            double v = ct[c->NC + c->NDV + idx];    /* multipliers follow the derivatives */
+            L += w * (v * v);
         }
     }
     return L;
@@ -2578,6 +2604,12 @@ int orc_eval_grad_f(orc_ctx* c, const double* x, double* grad) {
                 }
                 double dL = c->fd == MH_FD_CENTRAL ? (lp - lm) / (2.0 * h)
                           : (c->fd == MH_FD_FORWARD ? (lp - L0) / h : (L0 - lm) / h);
+                if (G->kind == MH_GOAL_LAGRANGE_MULTIPLIERS) {
+                    /* exact (the reference differentiates this MX term with
+                     * AD): d(w lambda^2)/d lambda = w 2 lambda */
+                    int j = idx - (NS + c->NC + c->NDV);
+                    dL = (idx >= 0 && j >= 0 && j < c->NM) ? c->gw[G->term_begin + j] * (2.0 * in[idx]) : 0.0;
+                }
                 int64_t col;
                 if (d == 0) col = 0;
                 else if (d == 1) col = 1;

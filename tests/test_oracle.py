@@ -1164,3 +1164,35 @@ def test_kinematic_constraint_physics():
     imp, _ = _kc(2, dynamics="implicit")
     r = imp.eval_dae(np.array([np.concatenate([[0.2], q, u, tau, ys[:2], [lam, 0.0]])]))[0]
     assert np.abs(r[:2]).max() < 1e-9 * (np.abs(tau).max() + 1)
+
+
+def test_lagrange_multiplier_term():
+    """minimize_lagrange_multipliers (CasOCTranscription.cpp:513-521):
+    f gains weight * duration * sum_k quad_k sum_j lambda_kj^2; its gradient
+    is exact (the reference differentiates the MX term with AD); without
+    kinematic constraints the option is rejected (MocoCasOCProblem.cpp:
+    101-107)."""
+    nlp, st = _kc(6)
+    off, _ = _kc(6)
+    st.solver.minimize_lagrange_multipliers = False
+    off = OracleNLP(st.problem.create_rep(), st.solver.options())
+    x = nlp.random_iterate(np.random.default_rng(2).uniform(-1, 1, nlp.n))
+    G = nlp.G
+    lam = x[2 + 6 * G:2 + 7 * G]
+    N = 6
+    mesh = np.arange(N + 1) / N
+    quad = np.zeros(G)
+    for i in range(N):
+        dm = mesh[i + 1] - mesh[i]
+        quad[2 * i] += dm / 6
+        quad[2 * i + 1] += 2 * dm / 3
+        quad[2 * i + 2] += dm / 6
+    extra = 10.0 * (x[1] - x[0]) * np.dot(quad, lam ** 2)
+    assert nlp.eval_f(x) - off.eval_f(x) == pytest.approx(extra, rel=1e-12)
+    g = nlp.eval_grad_f(x) - off.eval_grad_f(x)
+    np.testing.assert_allclose(g[2 + 6 * G:2 + 7 * G], 10.0 * (x[1] - x[0]) * quad * 2 * lam, rtol=1e-12)
+    assert g[1] == pytest.approx(10.0 * np.dot(quad, lam ** 2), rel=1e-9)
+    st2 = configs.double_pendulum(4)
+    st2.solver.minimize_lagrange_multipliers = True
+    with pytest.raises(RuntimeError, match="minimize_lagrange_multipliers"):
+        OracleNLP(st2.problem.create_rep(), st2.solver.options())
