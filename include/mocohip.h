@@ -443,7 +443,20 @@ typedef struct mh_options {
     int32_t minimize_lagrange_multipliers;
     double velocity_correction_bounds[2];
     double lagrange_multiplier_weight;
+    /* How eval_jac_g differentiates (mh_jacobian_mode).  CALLBACK_FD (0,
+     * MocoCasADiSolver): finite differences of each per-point callback
+     * (fd_step, finite_difference_scheme), chained through the
+     * transcription.  GLOBAL_SEEDS (1, tropter's IPOPT decorator,
+     * ProblemDecorator_double.cpp:261-291): central differences of the whole
+     * constraint function g along the seed directions of a column partial
+     * distance-2 coloring of the Jacobian structure (GraphColoring.cpp:
+     * 91-94), step sqrt(DBL_EPSILON), recovered per nonzero.  Unsharded
+     * contexts only. */
+    int32_t jacobian_mode;
+    int32_t reserved_jm;
 } mh_options;
+
+enum mh_jacobian_mode { MH_JACOBIAN_CALLBACK_FD = 0, MH_JACOBIAN_GLOBAL_SEEDS = 1 };
 
 enum mh_sparsity {
     MH_SPARSITY_NONE = 0, MH_SPARSITY_RANDOM = 1, MH_SPARSITY_INITIAL_GUESS = 2, MH_SPARSITY_GIVEN = 3
@@ -551,6 +564,19 @@ int mh_get_backend_flags(const mh_ctx* ctx, char* flags, int32_t len);
 int mh_get_callback_sparsity(const mh_ctx* ctx, uint8_t* pattern, int64_t len);
 /* FNV-1a hash of everything the per-point DAE depends on (host only). */
 int mh_model_hash(const mh_model* model, uint64_t* hash);
+
+/* Column partial distance-2 coloring of a sparsity pattern (the seeds of
+ * tropter's JacobianColoring, GraphColoring.cpp:71-120; ColPack
+ * COLUMN_PARTIAL_DISTANCE_TWO): two columns share a color only if no row has
+ * both.  Greedy over columns in natural order (ColPack orders them
+ * SMALLEST_LAST: the seed count may differ, the recovered values do not).
+ * color[ncols] receives each column's seed, *ncolors the seed count.  Host
+ * only (no device, no context). */
+int mh_color_jacobian(int64_t nrows, int64_t ncols, int64_t nnz, const int32_t* iRow,
+                      const int32_t* jCol, int32_t* color, int32_t* ncolors);
+/* The seed of every x column (n entries) that eval_jac_g uses in
+ * MH_JACOBIAN_GLOBAL_SEEDS mode (the coloring of mh_get_jac_structure). */
+int mh_get_jacobian_seeds(const mh_ctx* ctx, int32_t* color, int32_t* nseeds);
 
 /* Work of one DAE stage on this context: [0] FP64 operations executed per
  * eval_jac_g, [1] per eval_g, [2] group evaluations per eval_jac_g (task

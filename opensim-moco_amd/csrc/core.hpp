@@ -1706,6 +1706,13 @@ struct mh_ctx {
     int yq[2] = {0, 0};            // per lane configuration: Y of the last evaluation holds quotients
     bool timing = false;           // stage events for mh_last_timings (mh_set_timing)
     bool groups_timed = false;     // the last evaluation recorded ev[4]
+    // MH_JACOBIAN_GLOBAL_SEEDS (tropter): column coloring, per seed its
+    // columns and its (nonzero, row) pairs, perturbed iterates and g's
+    int jac_seeds = 0, nseeds = 0;
+    std::vector<int32_t> seed_color;           // [n]
+    std::vector<int32_t> seed_col_off, seed_cols, seed_ent_off, seed_ents, seed_rows;
+    int32_t *d_seed_cols = nullptr, *d_seed_ents = nullptr, *d_seed_rows = nullptr;
+    double *d_xp = nullptr, *d_xm = nullptr, *d_gp = nullptr, *d_gm = nullptr;
 };
 
 // The per-call layout view of the context (grid points [k0, k0 + nk)).

@@ -26,6 +26,7 @@
 #include "core.hpp"
 
 #include <cstdarg>
+#include <limits>
 
 // ------------------------------------------------------------------------
 // error handling
@@ -1141,6 +1142,7 @@ extern "C" int mh_model_hash(const mh_model* M, uint64_t* hash) {
 
 static const Backend* select_backend(mh_ctx* c, const mh_problem* p);
 static int detect_sparsity(mh_ctx* c, const mh_options* o);
+static int build_seeds(mh_ctx* c);
 static const TaskInfo* backend_tasks(const Backend* b);
 static bool interval_fits(const mh_ctx* c, int mode);
 
@@ -1240,6 +1242,26 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     const size_t o_epc = A.reserve(sizeof(double) * (size_t)std::max(1, c->ngoals));   // endpoint costs
     const int npts_iv = c->scheme == MH_HERMITE_SIMPSON ? 3 : 2;
     const size_t o_xch = A.reserve(sizeof(double) * (size_t)std::max(nint, 1) * npts_iv * std::max(1, c->NO) * XCH_W);
+    // tropter global seeds: the coloring and per-seed lists, perturbed
+    // iterates and constraint vectors
+    c->jac_seeds = o->jacobian_mode == MH_JACOBIAN_GLOBAL_SEEDS;
+    if (o->jacobian_mode != MH_JACOBIAN_CALLBACK_FD && !c->jac_seeds)
+        return set_err(MH_ERR_INVALID, "unknown jacobian_mode %d", o->jacobian_mode);
+    if (c->jac_seeds && (c->ib != 0 || c->ie != c->N || o->sparsity_detection != MH_SPARSITY_NONE))
+        return set_err(MH_ERR_UNSUPPORTED, "MH_JACOBIAN_GLOBAL_SEEDS needs an unsharded context and "
+                       "the block-dense structure");
+    size_t o_scol = 0, o_sent = 0, o_srow = 0, o_xp = 0, o_xm = 0, o_gp = 0, o_gm = 0;
+    if (c->jac_seeds) {
+        int rc2 = build_seeds(c.get());
+        if (rc2) return rc2;
+        o_scol = A.put(c->seed_cols.data(), c->seed_cols.size());
+        o_sent = A.put(c->seed_ents.data(), c->seed_ents.size());
+        o_srow = A.put(c->seed_rows.data(), c->seed_rows.size());
+        o_xp = A.reserve(sizeof(double) * c->n);
+        o_xm = A.reserve(sizeof(double) * c->n);
+        o_gp = A.reserve(sizeof(double) * std::max<int64_t>(1, c->m));
+        o_gm = A.reserve(sizeof(double) * std::max<int64_t>(1, c->m));
+    }
 
     TaskOffsets to_jac{}, to_g{};
     size_t o_T = 0, o_H = 0;
@@ -1311,6 +1333,13 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     c->has_marker = false;
     for (int g = 0; g < p->ngoals; ++g) c->has_marker |= p->goals[g].kind == MH_GOAL_MARKER_FINAL;
     c->d_xch = (double*)(b + o_xch);
+    if (c->jac_seeds) {
+        c->d_seed_cols = (int32_t*)(b + o_scol);
+        c->d_seed_ents = (int32_t*)(b + o_sent);
+        c->d_seed_rows = (int32_t*)(b + o_srow);
+        c->d_xp = (double*)(b + o_xp); c->d_xm = (double*)(b + o_xm);
+        c->d_gp = (double*)(b + o_gp); c->d_gm = (double*)(b + o_gm);
+    }
     if (ti) {
         bind_taskset(b, to_jac, c->ts_jac);
         bind_taskset(b, to_g, c->ts_g);
@@ -1637,7 +1666,166 @@ static int run_stage(mh_ctx* c, int stage, int kind, const double* x, double* a,
 // between the stages on the context stream.  Off by default: each event
 // packet costs several microseconds on a call that is itself tens of
 // microseconds.
+// ------------------------------------------------------------------------
+// MH_JACOBIAN_GLOBAL_SEEDS: tropter's Jacobian (ProblemDecorator_double.cpp:
+// 261-291).  For every seed of the column coloring, g at x + eps d and
+// x - eps d (d = the seed's columns), central quotient, recovered into the
+// nonzeros of the seed's columns (each row meets at most one of them, so
+// the quotient is that column's derivative).
+// ------------------------------------------------------------------------
+// Greedy column partial distance-2 coloring over CSR rows / CSC columns.
+static int color_columns(int64_t nrows, int64_t ncols, int64_t nnz, const int32_t* iRow,
+        const int32_t* jCol, int32_t* color) {
+    std::vector<int64_t> roff(nrows + 1, 0), coff(ncols + 1, 0);
+    for (int64_t e = 0; e < nnz; ++e) {
+        if (iRow[e] < 0 || iRow[e] >= nrows || jCol[e] < 0 || jCol[e] >= ncols) return -1;
+        ++roff[iRow[e] + 1];
+        ++coff[jCol[e] + 1];
+    }
+    for (int64_t r = 0; r < nrows; ++r) roff[r + 1] += roff[r];
+    for (int64_t j = 0; j < ncols; ++j) coff[j + 1] += coff[j];
+    std::vector<int32_t> rcol(nnz), crow(nnz);
+    {
+        std::vector<int64_t> rp(roff.begin(), roff.end() - 1), cp(coff.begin(), coff.end() - 1);
+        for (int64_t e = 0; e < nnz; ++e) {
+            rcol[rp[iRow[e]]++] = jCol[e];
+            crow[cp[jCol[e]]++] = iRow[e];
+        }
+    }
+    std::vector<int64_t> stamp;   // stamp[color] == column: color forbidden for it
+    int32_t ncolors = 0;
+    for (int64_t j = 0; j < ncols; ++j) color[j] = -1;
+    for (int64_t j = 0; j < ncols; ++j) {
+        for (int64_t q = coff[j]; q < coff[j + 1]; ++q) {
+            const int32_t r = crow[q];
+            for (int64_t t = roff[r]; t < roff[r + 1]; ++t) {
+                const int32_t k = color[rcol[t]];
+                if (k >= 0) stamp[k] = j;
+            }
+        }
+        int32_t k = 0;
+        while (k < ncolors && stamp[k] == j) ++k;
+        if (k == ncolors) { ++ncolors; stamp.push_back(-1); }
+        color[j] = k;
+    }
+    return ncolors;
+}
+
+extern "C" int mh_color_jacobian(int64_t nrows, int64_t ncols, int64_t nnz, const int32_t* iRow,
+        const int32_t* jCol, int32_t* color, int32_t* ncolors) {
+    if (nrows < 0 || ncols < 0 || nnz < 0 || (nnz && (!iRow || !jCol)) || (ncols && !color) || !ncolors)
+        return set_err(MH_ERR_INVALID, "bad argument");
+    const int k = color_columns(nrows, ncols, nnz, iRow, jCol, color);
+    if (k < 0) return set_err(MH_ERR_INVALID, "index out of range");
+    *ncolors = k;
+    return MH_OK;
+}
+
+extern "C" int mh_get_jacobian_seeds(const mh_ctx* c, int32_t* color, int32_t* nseeds) {
+    if (!c || !color || !nseeds) return set_err(MH_ERR_INVALID, "null argument");
+    if (!c->jac_seeds) return set_err(MH_ERR_INVALID, "context not in MH_JACOBIAN_GLOBAL_SEEDS mode");
+    std::memcpy(color, c->seed_color.data(), sizeof(int32_t) * c->n);
+    *nseeds = c->nseeds;
+    return MH_OK;
+}
+
+// The coloring of the Jacobian structure and its per-seed lists (mh_create).
+static int build_seeds(mh_ctx* c) {
+    std::vector<int32_t> ir(c->nnz), jc(c->nnz);
+    int rc = mh_get_jac_structure(c, ir.data(), jc.data());
+    if (rc) return rc;
+    c->seed_color.assign(c->n, -1);
+    c->nseeds = color_columns(c->m, c->n, c->nnz, ir.data(), jc.data(), c->seed_color.data());
+    if (c->nseeds < 0) return set_err(MH_ERR_INVALID, "internal: Jacobian structure out of range");
+    const int S = c->nseeds;
+    c->seed_col_off.assign(S + 1, 0);
+    c->seed_ent_off.assign(S + 1, 0);
+    for (int64_t j = 0; j < c->n; ++j) ++c->seed_col_off[c->seed_color[j] + 1];
+    for (int64_t e = 0; e < c->nnz; ++e) ++c->seed_ent_off[c->seed_color[jc[e]] + 1];
+    for (int k = 0; k < S; ++k) {
+        c->seed_col_off[k + 1] += c->seed_col_off[k];
+        c->seed_ent_off[k + 1] += c->seed_ent_off[k];
+    }
+    c->seed_cols.resize(c->n);
+    c->seed_ents.resize(c->nnz);
+    c->seed_rows.resize(c->nnz);
+    std::vector<int32_t> cp(c->seed_col_off.begin(), c->seed_col_off.end() - 1),
+            ep(c->seed_ent_off.begin(), c->seed_ent_off.end() - 1);
+    for (int64_t j = 0; j < c->n; ++j) c->seed_cols[cp[c->seed_color[j]]++] = (int32_t)j;
+    for (int64_t e = 0; e < c->nnz; ++e) {
+        const int k = c->seed_color[jc[e]];
+        c->seed_ents[ep[k]] = (int32_t)e;
+        c->seed_rows[ep[k]] = ir[e];
+        ++ep[k];
+    }
+    return MH_OK;
+}
+
+// xp / xm: columns [b, e) of the seed list at x +- eps (set = 1) or back at
+// x (set = 0); tropter: x0 + eps * direction with direction entries 1.
+__global__ void __launch_bounds__(256) k_seed_set(const double* __restrict__ x, double* __restrict__ xp,
+        double* __restrict__ xm, const int32_t* __restrict__ cols, int b, int e, double eps, int set) {
+    const int i = b + (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (i >= e) return;
+    const int j = cols[i];
+    xp[j] = set ? x[j] + eps : x[j];
+    xm[j] = set ? x[j] - eps : x[j];
+}
+// values of the seed's nonzeros: (g+ - g-) / (2 eps) of their rows.
+__global__ void __launch_bounds__(256) k_seed_recover(const double* __restrict__ gp,
+        const double* __restrict__ gm, const int32_t* __restrict__ ents, const int32_t* __restrict__ rows,
+        int b, int e, double two_eps, double* __restrict__ values) {
+    const int i = b + (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (i >= e) return;
+    const int r = rows[i];
+    values[ents[i]] = (gp[r] - gm[r]) / two_eps;
+}
+
+static int run_seeds(mh_ctx* c, const double* x, double* values) {
+    const double eps = std::sqrt(std::numeric_limits<double>::epsilon());
+    const double two_eps = 2 * eps;
+    HIPCHK(hipMemcpyAsync(c->d_xp, x, sizeof(double) * c->n, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->d_xm, x, sizeof(double) * c->n, hipMemcpyDeviceToDevice, c->stream));
+    for (int k = 0; k < c->nseeds; ++k) {
+        const int cb = c->seed_col_off[k], ce = c->seed_col_off[k + 1];
+        const int eb = c->seed_ent_off[k], ee = c->seed_ent_off[k + 1];
+        const unsigned gc = (unsigned)std::max(1, (ce - cb + 255) / 256), ge = (unsigned)std::max(1, (ee - eb + 255) / 256);
+        hipLaunchKernelGGL(k_seed_set, dim3(gc), dim3(256), 0, c->stream, x, c->d_xp, c->d_xm, c->d_seed_cols,
+                cb, ce, eps, 1);
+        for (int side = 0; side < 2; ++side) {
+            const double* xs = side ? c->d_xm : c->d_xp;
+            double* gs = side ? c->d_gm : c->d_gp;
+            int rc = launch_stage(c, 0, 0, xs, gs, nullptr);
+            if (rc) return rc;
+            rc = launch_stage(c, 1, 0, xs, gs, nullptr);
+            if (rc) return rc;
+        }
+        hipLaunchKernelGGL(k_seed_recover, dim3(ge), dim3(256), 0, c->stream, c->d_gp, c->d_gm, c->d_seed_ents,
+                c->d_seed_rows, eb, ee, two_eps, values);
+        hipLaunchKernelGGL(k_seed_set, dim3(gc), dim3(256), 0, c->stream, x, c->d_xp, c->d_xm, c->d_seed_cols,
+                cb, ce, eps, 0);
+    }
+    HIPCHK(hipGetLastError());
+    return MH_OK;
+}
+
 static int run_cached(mh_ctx* c, int kind, const double* x, double* a, double* b) {
+    if (c->jac_seeds && kind != 0) {   // tropter's global-seed Jacobian
+        if (kind == 2) {
+            int rc = run_stage(c, 0, 0, x, a, nullptr);
+            if (rc) return rc;
+            rc = run_stage(c, 1, 0, x, a, nullptr);
+            if (rc) return rc;
+        }
+        c->groups_timed = false;
+        if (c->timing) HIPCHK(hipEventRecord(c->ev[0], c->stream));
+        int rc = run_seeds(c, x, kind == 1 ? a : b);
+        if (c->timing) {
+            HIPCHK(hipEventRecord(c->ev[1], c->stream));
+            HIPCHK(hipEventRecord(c->ev[2], c->stream));
+        }
+        return rc;
+    }
     // ev[4] (after k_groups) is recorded only by the split task path
     c->groups_timed = c->timing && c->be->tasks && !c->use_interval[kind == 0 ? 0 : 1];
     if (c->timing) HIPCHK(hipEventRecord(c->ev[0], c->stream));

@@ -84,6 +84,7 @@ class mh_external_force(C.Structure):
 
 
 MH_KC_COORDINATE_COUPLER = 0
+MH_JACOBIAN_CALLBACK_FD, MH_JACOBIAN_GLOBAL_SEEDS = 0, 1
 
 
 class mh_constraint(C.Structure):
@@ -163,7 +164,8 @@ class mh_options(C.Structure):
                 ("sparsity_guess", P(f64)), ("sparsity_pattern", P(C.c_uint8)),
                 ("implicit_aux_bounds", f64 * 2),
                 ("ignore_constraint_derivatives", i32), ("minimize_lagrange_multipliers", i32),
-                ("velocity_correction_bounds", f64 * 2), ("lagrange_multiplier_weight", f64)]
+                ("velocity_correction_bounds", f64 * 2), ("lagrange_multiplier_weight", f64),
+                ("jacobian_mode", i32), ("reserved_jm", i32)]
 
 
 MH_SPARSITY_NONE, MH_SPARSITY_RANDOM, MH_SPARSITY_INITIAL_GUESS, MH_SPARSITY_GIVEN = 0, 1, 2, 3
@@ -205,6 +207,8 @@ MOCOHIP_SYMBOLS = {
     "mh_model_hash": (i32, [P(mh_model), P(C.c_uint64)]),
     "mh_get_callback_sparsity": (i32, [C.c_void_p, P(C.c_uint8), C.c_int64]),
     "mh_get_work": (i32, [C.c_void_p, P(f64)]),
+    "mh_color_jacobian": (i32, [C.c_int64, C.c_int64, C.c_int64, P(i32), P(i32), P(i32), P(i32)]),
+    "mh_get_jacobian_seeds": (i32, [C.c_void_p, P(i32), P(i32)]),
     "mh_debug_jacobian_lanes": (i32, [C.c_void_p, P(f64), P(f64), P(f64)]),
     "mh_debug_time_stages": (i32, [C.c_void_p, C.c_void_p, i32, i32, P(f64)]),
     "mh_set_stream": (i32, [C.c_void_p, C.c_void_p]),
@@ -232,6 +236,7 @@ ORACLE_SYMBOLS = {
                                       P(f64)]),
     "orc_eval_function": (i32, [C.c_void_p, C.c_int, f64, P(f64)]),
     "orc_get_callback_sparsity": (i32, [C.c_void_p, P(C.c_uint8), C.c_int64]),
+    "orc_get_jacobian_seeds": (i32, [C.c_void_p, P(i32), P(i32)]),
     "orc_assemble_from_lanes": (i32, [C.c_void_p, P(f64), P(f64), P(f64), P(f64), P(f64)]),
 }
 

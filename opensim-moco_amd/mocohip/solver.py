@@ -58,6 +58,10 @@ class MocoHipSolver:
     velocity_correction_bounds: tuple = (-0.1, 0.1)
     minimize_lagrange_multipliers: bool = False
     lagrange_multiplier_weight: float = 1.0
+    # "callback-fd" (MocoCasADiSolver: FD of each per-point callback) or
+    # "global-seeds" (tropter: central FD of g along colored seed columns,
+    # ProblemDecorator_double.cpp:261-291)
+    jacobian_mode: str = "callback-fd"
     # the optimizer settings (MocoDirectCollocationSolver.cpp:23-42), mapped
     # to Ipopt options by ipopt_options()
     verbosity: int = 2
@@ -150,6 +154,10 @@ class MocoHipSolver:
         o.ignore_constraint_derivatives = 0 if self.enforce_constraint_derivatives else 1
         o.minimize_lagrange_multipliers = int(bool(self.minimize_lagrange_multipliers))
         o.lagrange_multiplier_weight = float(self.lagrange_multiplier_weight)
+        modes = {"callback-fd": abi.MH_JACOBIAN_CALLBACK_FD, "global-seeds": abi.MH_JACOBIAN_GLOBAL_SEEDS}
+        if self.jacobian_mode not in modes:
+            raise ValueError("jacobian_mode must be 'callback-fd' or 'global-seeds'")
+        o.jacobian_mode = modes[self.jacobian_mode]
         lo, hi = self.velocity_correction_bounds
         o.velocity_correction_bounds[0] = float(lo)
         o.velocity_correction_bounds[1] = float(hi)
@@ -364,6 +372,14 @@ class _NLPBase:
         """Rows after the last interval's own: the final mesh point's path
         rows and the final grid point's residuals."""
         return self.NK + self.NPC + self.NRES
+
+    def jacobian_seeds(self):
+        """(color per x column, seed count) of the global-seed Jacobian
+        (jacobian_mode "global-seeds")."""
+        color = np.empty(self.n, np.int32)
+        k = C.c_int32()
+        self._check(self._fn("get_jacobian_seeds")(self.ctx, abi.iptr(color), C.byref(k)))
+        return color, int(k.value)
 
     def eval_dae(self, inputs: np.ndarray) -> np.ndarray:
         """Per-point DAE: rows [t, states, controls, derivatives] ->

@@ -288,6 +288,9 @@ struct orc_ctx {
     mh_constraint* kcs;
     double mult_lo, mult_hi, kc_lo, kc_hi, vc_lo, vc_hi;
     int NPD;               /* callback inputs per point: NS + NC + NDV + NM */
+    /* MH_JACOBIAN_GLOBAL_SEEDS: the seed (color) of every x column */
+    int jac_seeds, nseeds;
+    int32_t* seed_color;
 };
 
 static double* dup_d(const double* p, size_t n) {
@@ -604,6 +607,42 @@ static double endpoint_value(const orc_ctx* c, int e, const double* in) {
 #ifndef ORACLE_COUNTING
 static int detect_sparsity(orc_ctx* c, const mh_options* o);
 #endif
+static int sharded(const orc_ctx* c);
+
+/* Column partial distance-2 coloring, greedy in natural column order: the
+ * smallest color no column sharing a row already has (ColPack's
+ * COLUMN_PARTIAL_DISTANCE_TWO, GraphColoring.cpp:91-94; ColPack orders the
+ * columns SMALLEST_LAST -- only the seed count depends on the order).
+ * Returns the color count. */
+static int color_columns(int64_t nrows, int64_t ncols, int64_t nnz, const int32_t* iRow,
+        const int32_t* jCol, int32_t* color) {
+    int64_t* roff = (int64_t*)calloc((size_t)nrows + 1, sizeof(int64_t));
+    int64_t* coff = (int64_t*)calloc((size_t)ncols + 1, sizeof(int64_t));
+    int32_t* rcol = (int32_t*)malloc(sizeof(int32_t) * (size_t)(nnz + 1));
+    int32_t* crow = (int32_t*)malloc(sizeof(int32_t) * (size_t)(nnz + 1));
+    int64_t* rp = (int64_t*)malloc(sizeof(int64_t) * (size_t)(nrows + 1));
+    int64_t* cp = (int64_t*)malloc(sizeof(int64_t) * (size_t)(ncols + 1));
+    int64_t* stamp = (int64_t*)malloc(sizeof(int64_t) * (size_t)(ncols + 1));
+    for (int64_t e = 0; e < nnz; ++e) { ++roff[iRow[e] + 1]; ++coff[jCol[e] + 1]; }
+    for (int64_t r = 0; r < nrows; ++r) roff[r + 1] += roff[r];
+    for (int64_t j = 0; j < ncols; ++j) coff[j + 1] += coff[j];
+    memcpy(rp, roff, sizeof(int64_t) * (size_t)nrows);
+    memcpy(cp, coff, sizeof(int64_t) * (size_t)ncols);
+    for (int64_t e = 0; e < nnz; ++e) { rcol[rp[iRow[e]]++] = jCol[e]; crow[cp[jCol[e]]++] = iRow[e]; }
+    int ncolors = 0;
+    for (int64_t j = 0; j < ncols; ++j) color[j] = -1;
+    for (int64_t j = 0; j < ncols; ++j) {
+        for (int64_t q = coff[j]; q < coff[j + 1]; ++q)
+            for (int64_t t = roff[crow[q]]; t < roff[crow[q] + 1]; ++t)
+                if (color[rcol[t]] >= 0) stamp[color[rcol[t]]] = j;
+        int k = 0;
+        while (k < ncolors && stamp[k] == j) ++k;
+        if (k == ncolors) stamp[ncolors++] = -1;
+        color[j] = k;
+    }
+    free(roff); free(coff); free(rcol); free(crow); free(rp); free(cp); free(stamp);
+    return ncolors;
+}
 
 int orc_create(const mh_problem* p, const mh_options* o, orc_ctx** out) {
     if (!p || !o || !out) return fail(MH_ERR_INVALID, "null argument");
@@ -957,7 +996,30 @@ int orc_create(const mh_problem* p, const mh_options* o, orc_ctx** out) {
     while (c->nnz_begin < c->nnz && c->iRow[c->nnz_begin] < c->row_begin) ++c->nnz_begin;
     c->nnz_end = c->nnz_begin;
     while (c->nnz_end < c->nnz && c->iRow[c->nnz_end] < c->row_end) ++c->nnz_end;
+    /* tropter's global-seed Jacobian (ProblemDecorator_double.cpp:261-291):
+     * greedy column partial distance-2 coloring of the structure */
+    c->jac_seeds = o->jacobian_mode == MH_JACOBIAN_GLOBAL_SEEDS;
+    if (o->jacobian_mode != MH_JACOBIAN_CALLBACK_FD && !c->jac_seeds) {
+        orc_destroy(c);
+        return fail(MH_ERR_INVALID, "unknown jacobian_mode %d", o->jacobian_mode);
+    }
+    if (c->jac_seeds) {
+        if (sharded(c) || o->sparsity_detection != MH_SPARSITY_NONE) {
+            orc_destroy(c);
+            return fail(MH_ERR_UNSUPPORTED, "MH_JACOBIAN_GLOBAL_SEEDS needs an unsharded context and the "
+                        "block-dense structure");
+        }
+        c->seed_color = (int32_t*)malloc(sizeof(int32_t) * (size_t)(c->n + 1));
+        c->nseeds = color_columns(c->m, c->n, c->nnz, c->iRow, c->jCol, c->seed_color);
+    }
     *out = c;
+    return MH_OK;
+}
+
+int orc_get_jacobian_seeds(const orc_ctx* c, int32_t* color, int32_t* nseeds) {
+    if (!c->jac_seeds) return fail(MH_ERR_INVALID, "context not in MH_JACOBIAN_GLOBAL_SEEDS mode");
+    memcpy(color, c->seed_color, sizeof(int32_t) * (size_t)c->n);
+    *nseeds = c->nseeds;
     return MH_OK;
 }
 
@@ -966,7 +1028,7 @@ void orc_destroy(orc_ctx* c) {
     void* ptrs[] = {c->bodies, c->axes, c->funcs, c->kx, c->ky, c->kb, c->kc, c->kd,
             c->mus, c->pts, c->acts, c->tabs, c->brk, c->coef, c->ext, c->sinfo, c->cinfo,
             c->goals, c->gidx, c->gcol, c->gw, c->pc, c->sp, c->sp_pc, c->mus_ider, c->kin_col,
-            c->ep, c->sp_ep, c->kcs,
+            c->ep, c->sp_ep, c->kcs, c->seed_color,
             c->mus_act_state, c->mus_ftn_state,
             c->mus_control, c->coord_body, c->grid, c->quad, c->iRow, c->jCol};
     for (size_t i = 0; i < sizeof ptrs / sizeof ptrs[0]; ++i) free(ptrs[i]);
@@ -2386,7 +2448,31 @@ static void jac_assemble(const orc_ctx* c, const double* x, const double* times,
     (void)NQ;
 }
 
+/* tropter's calc_jacobian (ProblemDecorator_double.cpp:261-291): per seed,
+ * g at x +- eps * seed (eps = sqrt(DBL_EPSILON)), central quotient,
+ * recovered into the seed's nonzeros. */
+static int jac_global_seeds(orc_ctx* c, const double* x, double* values) {
+    double eps = sqrt(DBL_EPSILON), two_eps = 2 * eps;
+    double* xp = (double*)malloc(sizeof(double) * (size_t)c->n);
+    double* xm = (double*)malloc(sizeof(double) * (size_t)c->n);
+    double* gp = (double*)malloc(sizeof(double) * (size_t)(c->m + 1));
+    double* gm = (double*)malloc(sizeof(double) * (size_t)(c->m + 1));
+    for (int k = 0; k < c->nseeds; ++k) {
+        for (int64_t j = 0; j < c->n; ++j) {
+            xp[j] = c->seed_color[j] == k ? x[j] + eps : x[j];
+            xm[j] = c->seed_color[j] == k ? x[j] - eps : x[j];
+        }
+        orc_eval_g(c, xp, gp);
+        orc_eval_g(c, xm, gm);
+        for (int64_t e = 0; e < c->nnz; ++e)
+            if (c->seed_color[c->jCol[e]] == k) values[e] = (gp[c->iRow[e]] - gm[c->iRow[e]]) / two_eps;
+    }
+    free(xp); free(xm); free(gp); free(gm);
+    return MH_OK;
+}
+
 int orc_eval_jac_g(orc_ctx* c, const double* x, double* values) {
+    if (c->jac_seeds) return jac_global_seeds(c, x, values);
     int NS = c->NS, NO = nout(c), ND = c->NP + 2, NR = nres(c), NPC = c->NPC;
     double* times = (double*)malloc(sizeof(double) * (size_t)c->G);
     double* xd = (double*)calloc((size_t)c->G * (size_t)NS + 1, sizeof(double));

@@ -77,6 +77,7 @@ int orc_muscle_length_speed(orc_ctx* ctx, int im, const double* q,
 int orc_eval_function(orc_ctx* ctx, int ifn, double q, double* out3);
 /* The callback sparsity behind the structure (mh_get_callback_sparsity). */
 int orc_get_callback_sparsity(const orc_ctx* ctx, uint8_t* pattern, int64_t len);
+int orc_get_jacobian_seeds(const orc_ctx* c, int32_t* color, int32_t* nseeds);
 
 #ifdef __cplusplus
 }
