@@ -460,6 +460,19 @@ def main():
                                     "nnz_jac": ns.nnz, "mode": "separate",
                                     "note": "optim_sparsity_detection=random (3 iterates)"}
         ns.close()
+        # tropter's Jacobian on the same NLP and GPU (jacobian_mode
+        # "global-seeds": central FD of g along the column-coloring seeds,
+        # ProblemDecorator_double.cpp:261-291) -- the reference's other
+        # algorithm, for comparison with the per-callback lanes
+        s3 = configs.gait10dof18musc(N, fd_scheme=args.fd)
+        s3.solver.jacobian_mode = "global-seeds"
+        n3 = make_nlp(cx, s3, blocking=args.blocking)
+        sg, _, _ = device_steps(cx, n3, x)
+        kg, eg = measure(cx, sg, args, k=max(3, args.steps // 200), w=2)
+        extra["global_seeds"] = {"value": round(kg * cx.world / eg, 3), "unit": "calls/s",
+                                 "seeds": n3.jacobian_seeds()[1], "steps": kg, "mode": "separate",
+                                 "note": "jacobian_mode=global-seeds (tropter: 2 g evaluations per seed)"}
+        n3.close()
         if args.batch > 1:
             extra["batch"] = batch_throughput(
                 cx, lambda: configs.gait10dof18musc(N, fd_scheme=args.fd), track_iterate, args, args.batch)

@@ -685,7 +685,9 @@ def test_sparsity_detection_agrees(name):
     W = 1 + gpu.NS + gpu.NC + gpu.NDV
     NO = gpu.NO
     diff = np.argwhere((a != b).reshape(-1, W))
-    assert len(diff) <= 0.2 * max(b.sum(), 1), (len(diff), b.sum())
+    # disagreements are rare (rounding-level couplings only, checked one by
+    # one below): at most 2 % of the detected couplings
+    assert len(diff) <= 0.02 * max(b.sum(), 1), (len(diff), int(b.sum()), len(diff) / max(b.sum(), 1))
     for x in _detection_points(ref, st.solver):
         P = _points(ref, x)[0]
         rows = [P] + [P + np.eye(len(P))[j] * 1e-5 for j in range(len(P))]
