@@ -74,6 +74,8 @@ def parse():
                          "that every launch of a kernel has the same shape")
     ap.add_argument("--inverse-batch", type=int, default=8)
     ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--batch-only", action="store_true",
+                    help="print only the batch line (A/B of queue / launch settings)")
     return ap.parse_args()
 
 
@@ -410,6 +412,13 @@ def main():
         return
     from mocohip import configs
     N = args.intervals
+    if args.batch_only:
+        out = batch_throughput(cx, lambda: configs.gait10dof18musc(N, fd_scheme=args.fd), track_iterate,
+                               args, args.batch)
+        out["env"] = {k: os.environ[k] for k in ("GPU_MAX_HW_QUEUES", "MOCOHIP_GRAPHS") if k in os.environ}
+        if cx.rank == 0:
+            print(json.dumps(out), flush=True)
+        return
     st = configs.gait10dof18musc(N, fd_scheme=args.fd)
     nlp = make_nlp(cx, st, blocking=args.blocking)
     # iterate: bounds midpoint for the states (where the muscle model is
