@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define MH_ABI_VERSION 4
+#define MH_ABI_VERSION 5
 
 enum mh_status {
     MH_OK = 0,
@@ -205,6 +205,36 @@ typedef struct mh_constraint {
     double scale;        /* CoordinateCouplerConstraint scale_factor        */
 } mh_constraint;
 
+/* Wrap surfaces (ABI v5; OpenSim WrapCylinder in a body's WrapObjectSet)
+ * and the PathWrap list of each muscle's GeometryPath.  The cylinder frame
+ * W is fixed in the body: its z axis is the cylinder axis; a station s_W maps
+ * to the body as  R_BW s_W + p_BW  (WrapObject's xyz_body_rotation, a
+ * body-fixed X-Y-Z sequence, and translation).  quadrant "+x" / "-x" / "+y"
+ * / "-y" constrains the wrap to that half-space of W (wrap_axis 0 / 1,
+ * wrap_sign +1 / -1); "all" leaves it unconstrained (wrap_sign 0).  The
+ * path algorithm is restated in oracle/oracle.c (wrap_cylinder,
+ * apply_wraps) and dae_device.hpp. */
+enum mh_wrap_kind { MH_WRAP_CYLINDER = 0 };
+typedef struct mh_wrap_object {
+    int32_t kind;        /* mh_wrap_kind                                     */
+    int32_t body;        /* -1 = ground                                      */
+    int32_t wrap_axis;   /* 0: x, 1: y (quadrant constraint axis)            */
+    int32_t wrap_sign;   /* +1 / -1 constrained, 0 unconstrained ("all")     */
+    double R_BW[9];      /* cylinder frame in the body (row-major)           */
+    double p_BW[3];
+    double radius;
+    double length;       /* recorded; the cylinder is treated as infinite    */
+} mh_wrap_object;
+/* One PathWrap of a muscle, in the path's PathWrapSet order: muscles list
+ * theirs contiguously (mh_muscle.wrap_begin / wrap_count below are carried
+ * here as muscle + order). */
+typedef struct mh_path_wrap {
+    int32_t muscle;      /* muscle index (entries grouped by muscle, in order)*/
+    int32_t wrap;        /* index into mh_model.wraps                         */
+    int32_t range_begin; /* PathWrap range, 1-based path points; < 1 = first  */
+    int32_t range_end;   /*                                       < 1 = last  */
+} mh_path_wrap;
+
 typedef struct mh_model {
     int32_t nq;          /* coordinates (= speeds)                          */
     int32_t nbodies;
@@ -234,6 +264,10 @@ typedef struct mh_model {
     int32_t nconstraints;   /* enabled kinematic constraints (ABI v4)        */
     int32_t reserved_kc;
     const mh_constraint* constraints;
+    int32_t nwraps;         /* wrap surfaces (ABI v5)                          */
+    int32_t npathwraps;     /* PathWrap entries over all muscles               */
+    const mh_wrap_object* wraps;
+    const mh_path_wrap* pathwraps;
 } mh_model;
 
 /* ------------------------------------------------------------------------ */

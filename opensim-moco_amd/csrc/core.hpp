@@ -1616,6 +1616,8 @@ struct mh_ctx {
     // callback outputs of the errors / velocity correction, bounds
     int NKC = 0, NM = 0, NK = 0, NSL = 0, OKC = 0, OQC = 0, enforce = 1;
     std::vector<mh_constraint> kcs;
+    // muscle wrapping: per muscle the first PathWrap entry and their count
+    std::vector<int> mus_pw_begin, mus_pw_count;
     double mult_lo = -1000.0, mult_hi = 1000.0, kc_lo = 0.0, kc_hi = 0.0, vc_lo = -0.1, vc_hi = 0.1;
     std::vector<int> mus_ider;     // muscle -> aux derivative index after the controls (-1)
     double aux_lo = -1000.0, aux_hi = 1000.0;

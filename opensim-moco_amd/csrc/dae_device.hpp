@@ -58,6 +58,12 @@ struct DevModel {
     int nkc;
     const mh_constraint* kcs;
     int okc, oqc, enforce, mult;
+    // muscle wrapping (ABI v5): wrap surfaces, PathWrap entries grouped by
+    // muscle, each muscle's first entry and count
+    const mh_wrap_object* wr;
+    const mh_path_wrap* pw;
+    const int* mus_pw_begin;
+    const int* mus_pw_count;
 };
 constexpr int MUS_DERIVED = 6;
 
@@ -328,6 +334,201 @@ __device__ __forceinline__ void dgf_eval(const DevModel& M, int im, double LMT, 
     (void)fiberWidth;
 }
 
+// ---- muscle wrapping over cylinders -------------------------------------
+// The oracle's wrap_cylinder / wrap_segment / apply_wraps (oracle/oracle.c:
+// GeometryPath::applyWrapObjects, WrapObject::wrapPathSegment,
+// WrapCylinder::wrapLine restated), operation for operation.
+enum { DW_NONE = 0, DW_INSIDE = 1, DW_WRAPPED = 2 };
+__device__ inline int dev_wrap_cylinder(const mh_wrap_object& W, const double* a, const double* b,
+        double* r1, double* r2, double& wlen) {
+#pragma clang fp contract(off)
+    const double R = W.radius, R2 = R * R;
+    const double a2 = a[0] * a[0] + a[1] * a[1], b2 = b[0] * b[0] + b[1] * b[1];
+    if (a2 < R2 || b2 < R2) return DW_INSIDE;
+    const double d0 = b[0] - a[0], d1 = b[1] - a[1];
+    const double dd = d0 * d0 + d1 * d1;
+    const double t = dd > 0.0 ? -(a[0] * d0 + a[1] * d1) / dd : 0.0;
+    const double n0 = a[0] + t * d0, n1 = a[1] + t * d1;
+    const bool hits = (n0 * n0 + n1 * n1 < R2) && t > 0.0 && t < 1.0;
+    const double cr = a[0] * b[1] - a[1] * b[0];
+    const double sshort = cr < 0.0 ? -1.0 : 1.0;
+    double sigma = sshort;
+    if (W.wrap_sign != 0) {
+        const double nk = W.wrap_axis == 0 ? n0 : n1;
+        if (nk * (double)W.wrap_sign >= 0.0) {
+            if (!hits) return DW_NONE;
+        } else {
+            sigma = -sshort;
+        }
+    } else if (!hits) {
+        return DW_NONE;
+    }
+    const double ra = sqrt(a2), rb = sqrt(b2);
+    const double th1 = atan2(a[1], a[0]) + sigma * acos(R / ra);
+    const double th2 = atan2(b[1], b[0]) - sigma * acos(R / rb);
+    double dth = sigma * (th2 - th1);
+    const double twopi = 6.283185307179586;
+    while (dth < 0.0) dth = dth + twopi;
+    while (dth >= twopi) dth = dth - twopi;
+    const double l1 = sqrt(a2 - R2), l2 = sqrt(b2 - R2), arc = R * dth;
+    const double Lxy = l1 + arc + l2;
+    const double dz = b[2] - a[2];
+    const double z1 = a[2] + dz * (l1 / Lxy), z2 = a[2] + dz * ((l1 + arc) / Lxy);
+    r1[0] = R * cos(th1); r1[1] = R * sin(th1); r1[2] = z1;
+    r2[0] = R * cos(th2); r2[1] = R * sin(th2); r2[2] = z2;
+    const double zz = z2 - z1;
+    wlen = sqrt(arc * arc + zz * zz);
+    return DW_WRAPPED;
+}
+
+// A muscle's current path on the device: ground positions / velocities,
+// the path point (>= 0) or -1 for a tangent point, its PathWrap entry, the
+// body it is on, the surface length stored on a wrap's second point.
+template <int MP>
+struct CPath {
+    double P[MP][3], V[MP][3];
+    int pt[MP], pwi[MP], body[MP];
+    double wlen[MP];
+    int n;
+    __device__ __forceinline__ bool arc(int k) const {   // segment k-1 -> k over a surface
+        return pt[k] < 0 && pt[k - 1] < 0 && pwi[k] == pwi[k - 1];
+    }
+    __device__ __forceinline__ void move(int dst, int src) {
+        for (int d = 0; d < 3; ++d) { P[dst][d] = P[src][d]; V[dst][d] = V[src][d]; }
+        pt[dst] = pt[src]; pwi[dst] = pwi[src]; body[dst] = body[src]; wlen[dst] = wlen[src];
+    }
+};
+
+__device__ __forceinline__ double dev_dist3(const double* a, const double* b) {
+#pragma clang fp contract(off)
+    const double d0 = b[0] - a[0], d1 = b[1] - a[1], d2 = b[2] - a[2];
+    return sqrt(d0 * d0 + d1 * d1 + d2 * d2);
+}
+
+template <int MP>
+__device__ inline double dev_cpath_length(const CPath<MP>& C) {
+#pragma clang fp contract(off)
+    double L = 0.0;
+    for (int k = 1; k < C.n; ++k) L += C.arc(k) ? C.wlen[k] : dev_dist3(C.P[k - 1], C.P[k]);
+    return L;
+}
+
+template <class POSE, class VEL>
+__device__ inline void dev_body_station(const POSE& Pb, const VEL& Vb, const double* loc, double* P, double* V) {
+#pragma clang fp contract(off)
+    double t0, t1, t2;
+    t0 = Pb.R[0] * loc[0] + Pb.R[1] * loc[1] + Pb.R[2] * loc[2];
+    t1 = Pb.R[3] * loc[0] + Pb.R[4] * loc[1] + Pb.R[5] * loc[2];
+    t2 = Pb.R[6] * loc[0] + Pb.R[7] * loc[1] + Pb.R[8] * loc[2];
+    P[0] = Pb.p[0] + t0; P[1] = Pb.p[1] + t1; P[2] = Pb.p[2] + t2;
+    if (V) {
+        cross3(Vb.w0, Vb.w1, Vb.w2, P[0], P[1], P[2], t0, t1, t2);
+        V[0] = Vb.v0 + t0; V[1] = Vb.v1 + t1; V[2] = Vb.v2 + t2;
+    }
+}
+
+// WrapObject::wrapPathSegment: ends to the cylinder frame, wrapLine, tangent
+// points back to the body frame.
+template <class POSE>
+__device__ inline int dev_wrap_segment(const mh_wrap_object& W, const POSE& Pb, const double* A,
+        const double* B, double* r1B, double* r2B, double& wlen) {
+#pragma clang fp contract(off)
+    double pw[2][3];
+    const double* E[2] = {A, B};
+    for (int e = 0; e < 2; ++e) {
+        const double g0 = E[e][0] - Pb.p[0], g1 = E[e][1] - Pb.p[1], g2 = E[e][2] - Pb.p[2];
+        double sb[3];
+        for (int i = 0; i < 3; ++i) sb[i] = Pb.R[i] * g0 + Pb.R[3 + i] * g1 + Pb.R[6 + i] * g2;
+        for (int i = 0; i < 3; ++i) sb[i] = sb[i] - W.p_BW[i];
+        for (int i = 0; i < 3; ++i) pw[e][i] = W.R_BW[i] * sb[0] + W.R_BW[3 + i] * sb[1] + W.R_BW[6 + i] * sb[2];
+    }
+    double r1[3], r2[3];
+    const int res = dev_wrap_cylinder(W, pw[0], pw[1], r1, r2, wlen);
+    if (res != DW_WRAPPED) return res;
+    for (int i = 0; i < 3; ++i) {
+        r1B[i] = W.R_BW[3 * i] * r1[0] + W.R_BW[3 * i + 1] * r1[1] + W.R_BW[3 * i + 2] * r1[2] + W.p_BW[i];
+        r2B[i] = W.R_BW[3 * i] * r2[0] + W.R_BW[3 * i + 1] * r2[1] + W.R_BW[3 * i + 2] * r2[2] + W.p_BW[i];
+    }
+    return res;
+}
+
+// GeometryPath::applyWrapObjects on the current path C of muscle im
+// (pact(i): whether original path point i is active).
+template <int MP, class POSES, class VELS, class ACTIVE>
+__device__ inline void dev_apply_wraps(const DevModel& M, int im, const POSES& X, const VELS& Vs,
+        const ACTIVE& pact, CPath<MP>& C) {
+#pragma clang fp contract(off)
+    const mh_muscle& mu = M.mus[im];
+    int nw = M.mus_pw_count[im];
+    const int pb = M.mus_pw_begin[im];
+    int order[8], result[8];
+    if (nw > 8) nw = 8;
+    for (int i = 0; i < nw; ++i) { order[i] = i; result[i] = DW_NONE; }
+    const int maxit = nw < 2 ? 1 : 8;
+    double last = __builtin_inf();
+    for (int kk = 0; kk < maxit; ++kk) {
+        for (int i = 0; i < nw; ++i) {
+            result[i] = DW_NONE;
+            const int pwi = pb + order[i];
+            const mh_path_wrap PW = M.pw[pwi];
+            const mh_wrap_object& W = M.wr[PW.wrap];
+            for (int j = 0; j < C.n; ++j)
+                if (C.pt[j] < 0 && C.pwi[j] == pwi) {
+                    for (int k = j; k + 2 < C.n; ++k) C.move(k, k + 2);
+                    C.n -= 2;
+                    break;
+                }
+            const int ws = PW.range_begin < 1 ? 0 : PW.range_begin - 1;
+            const int we = PW.range_end < 1 ? mu.point_count - 1 : PW.range_end - 1;
+            int jf = ws, jr = we;
+            while (jf <= we && !pact(mu.point_begin + jf)) ++jf;
+            if (jf > we) return;
+            while (jr >= ws && !pact(mu.point_begin + jr)) --jr;
+            if (jr < ws) return;
+            int start = -1, end = -1;
+            for (int j = 0; j < C.n; ++j) {
+                if (C.pt[j] == mu.point_begin + jf) start = j;
+                if (C.pt[j] == mu.point_begin + jr) end = j;
+            }
+            if (start < 0 || end < 0) return;
+            const int bs = W.body + 1;
+            int best = -1;
+            double bestc = __builtin_inf(), br1[3] = {0, 0, 0}, br2[3] = {0, 0, 0}, bl = 0.0;
+            for (int k = start; k < end; ++k) {
+                if (C.arc(k + 1)) continue;
+                double r1[3], r2[3], wl;
+                result[i] = dev_wrap_segment(W, X[bs], C.P[k], C.P[k + 1], r1, r2, wl);
+                if (result[i] != DW_WRAPPED) continue;
+                double g1[3], g2[3];
+                dev_body_station(X[bs], Vs[bs], r1, g1, (double*)nullptr);
+                dev_body_station(X[bs], Vs[bs], r2, g2, (double*)nullptr);
+                const double chg = dev_dist3(C.P[k], g1) + wl + dev_dist3(g2, C.P[k + 1]) -
+                                   dev_dist3(C.P[k], C.P[k + 1]);
+                if (chg < bestc) {
+                    bestc = chg; best = k; bl = wl;
+                    for (int d = 0; d < 3; ++d) { br1[d] = r1[d]; br2[d] = r2[d]; }
+                }
+            }
+            if (best >= 0 && C.n + 2 <= MP) {
+                for (int k = C.n - 1; k > best; --k) C.move(k + 2, k);
+                C.n += 2;
+                for (int e = 0; e < 2; ++e) {
+                    const int q = best + 1 + e;
+                    C.pt[q] = -1; C.pwi[q] = pwi; C.body[q] = W.body;
+                    C.wlen[q] = e ? bl : 0.0;
+                    dev_body_station(X[bs], Vs[bs], e ? br2 : br1, C.P[q], C.V[q]);
+                }
+            }
+        }
+        const double L = dev_cpath_length(C);
+        if (fabs(L - last) < 0.0005) break;
+        last = L;
+        if (kk == 0 && nw > 1 && result[0] == DW_NONE && result[1] == DW_INSIDE) {
+            const int t = order[0]; order[0] = order[1]; order[1] = t;
+        }
+    }
+}
+
 // Per-lane workspace.  MB = max bodies (excluding ground), MQ = max
 // coordinates, MP = max path points per muscle.
 template <int MB, int MQ, int MP>
@@ -357,6 +558,7 @@ __device__ inline void kc_outputs(const DevModel& M, const double* q, const doub
         const double* udot, const double* c, double* out) {
 #pragma clang fp contract(off)
     const int n = M.nkc;
+    if (M.okc < 0 && M.oqc < 0) return;   // prescribed kinematics: multipliers only
     double* e = out + M.okc;
     const double* lam = c + M.mult;
     const double* gam = lam + n;
@@ -531,8 +733,10 @@ __device__ void dae_eval(const DevModel& M, Work<MB, MQ, MP>& w, double time, co
     // ---- muscles: path geometry, DGF, tension as point forces -------------
     for (int im = 0; im < M.nmus; ++im) {
         const mh_muscle& mu = M.mus[im];
-        double P[MP][3], Vp[MP][3];
-        int pidx[MP];
+        CPath<MP> C;
+        double (&P)[MP][3] = C.P;
+        double (&Vp)[MP][3] = C.V;
+        int (&pidx)[MP] = C.pt;
         int np = 0;
         for (int i = mu.point_begin; i < mu.point_begin + mu.point_count && np < MP; ++i) {
             const mh_path_point pt = M.pts[i];
@@ -569,13 +773,29 @@ __device__ void dae_eval(const DevModel& M, Work<MB, MQ, MP>& w, double time, co
             mv3(Pb.R, dl0, dl1, dl2, r0, r1, r2);
             Vp[np][0] = Vb.v0 + t0 + r0; Vp[np][1] = Vb.v1 + t1 + r1; Vp[np][2] = Vb.v2 + t2 + r2;
             pidx[np] = i;
+            C.pwi[np] = -1;
+            C.body[np] = pt.body;
+            C.wlen[np] = 0.0;
             ++np;
+        }
+        C.n = np;
+        if (M.mus_pw_count && M.mus_pw_count[im] > 0) {
+            const int pb0 = mu.point_begin, pc0 = mu.point_count;
+            auto active = [&](int i) {
+                for (int k = 0; k < C.n; ++k)
+                    if (C.pt[k] == i) return true;
+                (void)pb0; (void)pc0;
+                return false;
+            };
+            dev_apply_wraps<MP>(M, im, w.X, w.V, active, C);
+            np = C.n;
         }
         double L = 0.0, S = 0.0;
         for (int k = 1; k < np; ++k) {
             double d0 = P[k][0] - P[k - 1][0], d1 = P[k][1] - P[k - 1][1], d2 = P[k][2] - P[k - 1][2];
             double l = sqrt(d0 * d0 + d1 * d1 + d2 * d2);
-            L += l;
+            if (C.arc(k)) L += C.wlen[k];
+            else L += l;
             double e0 = Vp[k][0] - Vp[k - 1][0], e1 = Vp[k][1] - Vp[k - 1][1], e2 = Vp[k][2] - Vp[k - 1][2];
             S += (d0 * e0 + d1 * e1 + d2 * e2) / l;
         }
@@ -592,6 +812,7 @@ __device__ void dae_eval(const DevModel& M, Work<MB, MQ, MP>& w, double time, co
         // auxiliary residual outputs after zdot (CasOCFunction.cpp:208-230)
         if (id >= 0) out[NQ + M.nz + (id - M.nacc)] = resid;
         for (int k = 1; k < np; ++k) {
+            if (C.arc(k)) continue;   // a wrap's surface part: both ends on one body
             double d0 = P[k][0] - P[k - 1][0], d1 = P[k][1] - P[k - 1][1], d2 = P[k][2] - P[k - 1][2];
             double l = sqrt(d0 * d0 + d1 * d1 + d2 * d2);
             double F0 = T * d0 / l, F1 = T * d1 / l, F2 = T * d2 / l;
@@ -601,6 +822,15 @@ __device__ void dae_eval(const DevModel& M, Work<MB, MQ, MP>& w, double time, co
                 const int kk = side == 0 ? k - 1 : k;
                 const double sg = side == 0 ? 1.0 : -1.0;
                 const double f0 = sg * F0, f1 = sg * F1, f2 = sg * F2;
+                if (pidx[kk] < 0) {   // tangent point: a force at that station of the wrap body
+                    if (C.body[kk] < 0) continue;
+                    double n0, n1, n2;
+                    cross3(P[kk][0], P[kk][1], P[kk][2], f0, f1, f2, n0, n1, n2);
+                    SV& Fw = w.F[C.body[kk] + 1];
+                    Fw.w0 -= n0; Fw.w1 -= n1; Fw.w2 -= n2;
+                    Fw.v0 -= f0; Fw.v1 -= f1; Fw.v2 -= f2;
+                    continue;
+                }
                 const mh_path_point pt = M.pts[pidx[kk]];
                 if (pt.body < 0) continue;
                 const int bs = pt.body + 1;

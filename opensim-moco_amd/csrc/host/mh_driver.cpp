@@ -76,6 +76,8 @@ struct Tape {
     std::vector<mh_path_equation> path;
     std::vector<mh_endpoint_equation> endpoint;
     std::vector<mh_constraint> constraints;
+    std::vector<mh_wrap_object> wraps;
+    std::vector<mh_path_wrap> pathwraps;
     std::vector<double> guess;
     std::vector<uint8_t> pattern;
     std::vector<int32_t> kin_col;
@@ -100,8 +102,12 @@ bool read_tape(const char* path, Tape& t, std::string& err) {
     const int version = r.pod<int32_t>();
     t.ns = r.pod<int32_t>();
     t.nc = r.pod<int32_t>();
-    // version 4 = ABI v4's mh_options; earlier tapes carry a shorter one
-    if (version != 4) { err = "unsupported tape version (this build reads version 4)"; return false; }
+    // version 4 = ABI v4's mh_options (unchanged in v5); earlier tapes carry a
+    // shorter one; version 5 appends the wrap surfaces
+    if (version != 4 && version != 5) {
+        err = "unsupported tape version (this build reads versions 4 and 5)";
+        return false;
+    }
     t.opts = r.pod<mh_options>();
     mh_model& m = t.prob.model;
     int32_t* counts[] = {&m.nq, &m.nbodies, &m.naxes, &m.nfunctions, &m.nknots, &m.nmuscles,
@@ -162,6 +168,12 @@ bool read_tape(const char* path, Tape& t, std::string& err) {
         t.prob.multiplier_bounds = r.pod<mh_bounds>();
         t.prob.kinematic_constraint_bounds = r.pod<mh_bounds>();
     }
+    if (version >= 5) {   // wrap surfaces and PathWraps
+        m.nwraps = r.pod<int32_t>();
+        t.wraps = r.array<mh_wrap_object>(m.nwraps);
+        m.npathwraps = r.pod<int32_t>();
+        t.pathwraps = r.array<mh_path_wrap>(m.npathwraps);
+    }
     if (!r.ok || r.pos != r.buf.size()) { err = "truncated or malformed tape"; return false; }
     m.bodies = t.bodies.data(); m.axes = t.axes.data(); m.functions = t.functions.data();
     m.knot_x = t.knot_x.data(); m.knot_y = t.knot_y.data(); m.muscles = t.muscles.data();
@@ -179,6 +191,8 @@ bool read_tape(const char* path, Tape& t, std::string& err) {
     t.prob.kinematics_column = t.kin_col.empty() ? nullptr : t.kin_col.data();
     t.prob.endpoint = t.endpoint.empty() ? nullptr : t.endpoint.data();
     m.constraints = t.constraints.empty() ? nullptr : t.constraints.data();
+    m.wraps = t.wraps.empty() ? nullptr : t.wraps.data();
+    m.pathwraps = t.pathwraps.empty() ? nullptr : t.pathwraps.data();
     return true;
 }
 

@@ -516,7 +516,8 @@ static int64_t ep_col(const mh_ctx* c, int si) {
     const int64_t k = pt ? c->G - 1 : 0;
     if (j < c->NS) return col_state(c, k, j);
     if (j < c->NS + c->NC) return col_control(c, k, j - c->NS);
-    return col_deriv(c, k, j - c->NS - c->NC);
+    if (j < c->NS + c->NC + c->NDV) return col_deriv(c, k, j - c->NS - c->NC);
+    return col_mult(c, k, j - c->NS - c->NC - c->NDV);
 }
 
 // Build the per-interval template in CasOC row order with columns sorted
@@ -551,7 +552,7 @@ static void build_template(mh_ctx* c) {
     // sparsity detection (block-dense, CasOCFunction.cpp:25-105 "none"),
     // else the detected ones (sp: [output][time, inputs]); plus the point's
     // own state s_ident (the defects' identity terms).
-    const int W = 1 + NS + NC + NDV;
+    const int W = 1 + c->NI;                 // detected pattern: [time, every input]
     const int NPD = NS + NC + NDV + c->NM;   // callback inputs (no slacks)
     auto point_dep = [&](const std::vector<uint8_t>& sp, int o, int pt, int s_ident, std::vector<Col>& v) {
         for (int j = 0; j < NPD; ++j)
@@ -898,9 +899,11 @@ static int validate_and_layout(mh_ctx* c, const mh_problem* p, const mh_options*
                 K.dependent == M.functions[f].coord)
             return set_err(MH_ERR_INVALID, "kinematic constraint %d: bad kind/function/coordinate", i);
     }
-    if (NKC && (c->presc || p->nendpoint > 0 || o->sparsity_detection != MH_SPARSITY_NONE))
-        return set_err(MH_ERR_UNSUPPORTED, "kinematic constraints with prescribed kinematics, endpoint "
-                       "constraints or sparsity detection");
+    // prescribed kinematics: multipliers (constraint forces in the residual),
+    // no kinematic rows, no slacks (CasOCProblem.h:508-521)
+    if (NKC && !c->presc && (p->nendpoint > 0 || o->sparsity_detection != MH_SPARSITY_NONE))
+        return set_err(MH_ERR_UNSUPPORTED, "kinematic constraints (without prescribed kinematics) with "
+                       "endpoint constraints or sparsity detection");
     if (o->minimize_lagrange_multipliers && !NKC)   // MocoCasOCProblem.cpp:101-107
         return set_err(MH_ERR_INVALID, "Solver property 'minimize_lagrange_multipliers' was enabled but no "
                        "enabled kinematic constraints exist in the model.");
@@ -922,8 +925,8 @@ static int validate_and_layout(mh_ctx* c, const mh_problem* p, const mh_options*
     c->NKC = NKC;
     c->enforce = !o->ignore_constraint_derivatives;
     c->NM = NKC;
-    c->NK = c->enforce ? 3 * NKC : NKC;
-    c->NSL = c->enforce && o->transcription == MH_HERMITE_SIMPSON ? NKC : 0;
+    c->NK = c->presc ? 0 : (c->enforce ? 3 * NKC : NKC);
+    c->NSL = !c->presc && c->enforce && o->transcription == MH_HERMITE_SIMPSON ? NKC : 0;
     c->OKC = c->NQ + c->NZ + c->NAR;
     c->OQC = c->OKC + c->NK;
     c->NO = c->OQC + (c->NSL ? c->NQ : 0);
@@ -1003,6 +1006,26 @@ static int validate_and_layout(mh_ctx* c, const mh_problem* p, const mh_options*
         if (pt.body < -1 || pt.body >= M.nbodies) return set_err(MH_ERR_INVALID, "path point %d: bad body", i);
         if (pt.kind == MH_PP_CONDITIONAL && (pt.coord < 0 || pt.coord >= M.nq))
             return set_err(MH_ERR_INVALID, "path point %d: bad coordinate", i);
+    }
+    // wrap surfaces and PathWraps (grouped by muscle, at most 8 per muscle)
+    if (M.nwraps < 0 || M.npathwraps < 0 || (M.nwraps > 0 && !M.wraps) || (M.npathwraps > 0 && !M.pathwraps))
+        return set_err(MH_ERR_INVALID, "bad wrap objects");
+    for (int i = 0; i < M.nwraps; ++i) {
+        const mh_wrap_object& W = M.wraps[i];
+        if (W.kind != MH_WRAP_CYLINDER || W.body < -1 || W.body >= M.nbodies || !(W.radius > 0.0) ||
+                W.wrap_axis < 0 || W.wrap_axis > 1 || W.wrap_sign < -1 || W.wrap_sign > 1)
+            return set_err(MH_ERR_INVALID, "wrap object %d: bad kind/body/radius/quadrant", i);
+    }
+    c->mus_pw_begin.assign(M.nmuscles, 0);
+    c->mus_pw_count.assign(M.nmuscles, 0);
+    for (int k = 0; k < M.npathwraps; ++k) {
+        const mh_path_wrap& W = M.pathwraps[k];
+        if (W.muscle < 0 || W.muscle >= M.nmuscles || W.wrap < 0 || W.wrap >= M.nwraps ||
+                (k > 0 && W.muscle < M.pathwraps[k - 1].muscle))
+            return set_err(MH_ERR_INVALID, "path wrap %d: bad muscle/wrap or not grouped by muscle", k);
+        if (c->mus_pw_count[W.muscle]++ == 0) c->mus_pw_begin[W.muscle] = k;
+        if (c->mus_pw_count[W.muscle] > 8)
+            return set_err(MH_ERR_UNSUPPORTED, "muscle %d: more than 8 PathWraps", W.muscle);
     }
     // goals: kind, term range, and every term index within its kind's range
     // (a bad index would be an out-of-bounds device read)
@@ -1089,8 +1112,9 @@ static int validate_and_layout(mh_ctx* c, const mh_problem* p, const mh_options*
     c->t_final = p->time_final;
     c->ngoals = (int)c->goals.size();
     // size class
-    int maxpts = 0;
-    for (int im = 0; im < M.nmuscles; ++im) maxpts = std::max(maxpts, M.muscles[im].point_count);
+    int maxpts = 0;   // current-path capacity: points + 2 tangent points per PathWrap
+    for (int im = 0; im < M.nmuscles; ++im)
+        maxpts = std::max(maxpts, M.muscles[im].point_count + 2 * c->mus_pw_count[im]);
     auto fits = [&](int MB, int MQ, int MP, int MI, int MO) {
         return M.nbodies <= MB && M.nq <= MQ && maxpts <= MP && c->NI <= MI && c->NO <= MO;
     };
@@ -1130,6 +1154,14 @@ static uint64_t model_hash(const mh_model* M) {
         if (t < 0 || t >= M->ntables) continue;
         const int32_t shape[2] = {M->tables[t].degree, M->tables[t].ncol};
         h = fnv1a(h, shape, sizeof shape);
+    }
+    // wrapping (ABI v5) salts the hash only when present, so that models
+    // without wraps keep their generated back ends
+    if (M->nwraps > 0 || M->npathwraps > 0) {
+        const int32_t wc[2] = {M->nwraps, M->npathwraps};
+        h = fnv1a(h, wc, sizeof wc);
+        if (M->wraps) h = fnv1a(h, M->wraps, sizeof(mh_wrap_object) * (size_t)M->nwraps);
+        if (M->pathwraps) h = fnv1a(h, M->pathwraps, sizeof(mh_path_wrap) * (size_t)M->npathwraps);
     }
     return h;
 }
@@ -1207,6 +1239,9 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
                  o_mi = A.put(c->mus_ider.data(), c->mus_ider.size()),
                  o_kcol = A.put(c->kin_col.data(), c->kin_col.size()),
                  o_md = A.put(mder.data(), mder.size()),
+                 o_wr = A.put(M.wraps, M.nwraps), o_pw = A.put(M.pathwraps, M.npathwraps),
+                 o_pwb = A.put(c->mus_pw_begin.data(), c->mus_pw_begin.size()),
+                 o_pwc = A.put(c->mus_pw_count.data(), c->mus_pw_count.size()),
                  o_goals = A.put(c->goals.data(), c->goals.size()), o_gidx = A.put(c->gidx.data(), c->gidx.size()),
                  o_gcol = A.put(c->gcol.data(), c->gcol.size()), o_gw = A.put(c->gw.data(), c->gw.size()),
                  o_grid = A.put(c->grid.data(), c->grid.size()),
@@ -1287,7 +1322,7 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     D.mus_ider = (const int*)(b + o_mi);
     D.nkc = c->NKC;
     D.kcs = (const mh_constraint*)(b + o_kcs);
-    D.okc = c->OKC;
+    D.okc = c->NK ? c->OKC : -1;
     D.oqc = c->NSL ? c->OQC : -1;
     D.enforce = c->enforce;
     D.mult = c->NC + c->NDV;   // multipliers after the controls and derivatives
@@ -1307,6 +1342,10 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     D.coord_body = (const int*)(b + o_cb); D.mus_act_state = (const int*)(b + o_as);
     D.mus_ftn_state = (const int*)(b + o_fs); D.mus_control = (const int*)(b + o_mc);
     D.mus_derived = (const double*)(b + o_md);
+    D.wr = (const mh_wrap_object*)(b + o_wr);
+    D.pw = (const mh_path_wrap*)(b + o_pw);
+    D.mus_pw_begin = (const int*)(b + o_pwb);
+    D.mus_pw_count = (const int*)(b + o_pwc);
     c->GS.ngoals = c->ngoals;
     c->GS.ndv = c->NDV;
     c->GS.nc = c->NC;

@@ -92,6 +92,18 @@ class mh_constraint(C.Structure):
                 ("scale", f64)]
 
 
+MH_WRAP_CYLINDER = 0
+
+
+class mh_wrap_object(C.Structure):
+    _fields_ = [("kind", i32), ("body", i32), ("wrap_axis", i32), ("wrap_sign", i32),
+                ("R_BW", f64 * 9), ("p_BW", f64 * 3), ("radius", f64), ("length", f64)]
+
+
+class mh_path_wrap(C.Structure):
+    _fields_ = [("muscle", i32), ("wrap", i32), ("range_begin", i32), ("range_end", i32)]
+
+
 class mh_model(C.Structure):
     _fields_ = [("nq", i32), ("nbodies", i32), ("naxes", i32),
                 ("nfunctions", i32), ("nknots", i32), ("nmuscles", i32),
@@ -105,7 +117,9 @@ class mh_model(C.Structure):
                 ("tables", P(mh_table)), ("table_breaks", P(f64)),
                 ("table_coefs", P(f64)),
                 ("external", P(mh_external_force)),
-                ("nconstraints", i32), ("reserved_kc", i32), ("constraints", P(mh_constraint))]
+                ("nconstraints", i32), ("reserved_kc", i32), ("constraints", P(mh_constraint)),
+                ("nwraps", i32), ("npathwraps", i32), ("wraps", P(mh_wrap_object)),
+                ("pathwraps", P(mh_path_wrap))]
 
 
 class mh_bounds(C.Structure):
@@ -123,7 +137,7 @@ class mh_goal(C.Structure):
                 ("weight", f64)]
 
 
-MH_ABI_VERSION = 4     # include/mocohip.h
+MH_ABI_VERSION = 5     # include/mocohip.h
 MH_PATH_CONTROL_BOUND = 0
 MH_ENDPOINT_INITIAL_ACTIVATION = 0
 
@@ -234,6 +248,7 @@ ORACLE_SYMBOLS = {
     "orc_dgf_curve": (f64, [P(mh_muscle), C.c_int, f64]),
     "orc_muscle_length_speed": (i32, [C.c_void_p, C.c_int, P(f64), P(f64),
                                       P(f64)]),
+    "orc_muscle_path": (i32, [C.c_void_p, C.c_int, P(f64), P(f64), C.c_int, P(C.c_int), P(f64)]),
     "orc_eval_function": (i32, [C.c_void_p, C.c_int, f64, P(f64)]),
     "orc_get_callback_sparsity": (i32, [C.c_void_p, P(C.c_uint8), C.c_int64]),
     "orc_get_jacobian_seeds": (i32, [C.c_void_p, P(i32), P(i32)]),
@@ -319,6 +334,10 @@ def model_hash(m: "mh_model") -> int:
         t = m.external[e].table
         if 0 <= t < m.ntables:
             h = _fnv1a(h, bytes((i32 * 2)(m.tables[t].degree, m.tables[t].ncol)))
+    if m.nwraps > 0 or m.npathwraps > 0:
+        h = _fnv1a(h, bytes((i32 * 2)(m.nwraps, m.npathwraps)))
+        h = _fnv1a(h, arr(m.wraps, mh_wrap_object, m.nwraps))
+        h = _fnv1a(h, arr(m.pathwraps, mh_path_wrap, m.npathwraps))
     return h
 
 

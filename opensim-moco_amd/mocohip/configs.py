@@ -286,6 +286,153 @@ def gait10dof18musc_inverse(num_mesh_intervals: int = 25, fd_scheme: str = "forw
     return MocoStudy(p, s)
 
 
+def wrapped_pendulum(num_mesh_intervals: int = 20, scheme: str = "hermite-simpson",
+                     dynamics: str = "explicit", tendon_compliance: bool = False,
+                     quadrant: str = "all") -> MocoStudy:
+    """A one-link pendulum (ModelFactory::createNLinkPendulum(1)) driven by a
+    DeGrooteFregly2016 muscle whose path wraps over a WrapCylinder about the
+    pin axis (the GeometryPath / WrapCylinder geometry of SURVEY §8 A9 on a
+    model small enough for every kernel variant).  Not a BASELINE config."""
+    from .model import DeGrooteFregly2016Muscle, PathPoint, WrapCylinder
+    m = n_link_pendulum(1)
+    m.add_wrap(WrapCylinder("pin_cyl", "ground", 0.1, 0.2, (0.0, 0.0, 0.0), (0.0, 0.0, 0.0), quadrant))
+    mu = DeGrooteFregly2016Muscle("flexor", [PathPoint("ground", (-0.3, 0.15, 0.05), name="origin"),
+                                             PathPoint("b0", (-0.7, 0.12, -0.04), name="insertion")],
+                                  max_isometric_force=200.0, optimal_fiber_length=0.2,
+                                  tendon_slack_length=0.25, pennation_angle_at_optimal=0.1,
+                                  path_wraps=[("pin_cyl", -1, -1)])
+    mu.ignore_tendon_compliance = not tendon_compliance
+    m.actuators = [a for a in m.actuators]
+    m.add_muscle(mu)
+    p = MocoProblem(m)
+    p.set_time_bounds(0.0, 1.0)
+    p.set_state_info("/jointset/j0/q0/value", (-1.5, 1.5), 0.5)
+    p.set_state_info("/jointset/j0/q0/speed", (-20, 20), 0)
+    p.set_control_info("/tau0", (-50, 50))
+    p.add_goal(MocoControlGoal())
+    s = MocoHipSolver(num_mesh_intervals=num_mesh_intervals, transcription_scheme=scheme,
+                      multibody_dynamics_mode=dynamics)
+    return MocoStudy(p, s)
+
+
+def _walk_armless_grf(m: Model):
+    """ModOpAddExternalLoads(subject_walk_armless_external_loads.xml / grf_walk.xml):
+    ground-expressed force, point and torque on calcn_r / calcn_l."""
+    grf = _load("subject_walk_armless_grf.json")
+    cols = {k: np.asarray(v) for k, v in grf["columns"].items()}
+    m.add_table(DataTable("grf", np.asarray(grf["time"]), cols, degree=3))
+    for ef in grf["external_forces"]:
+        if ef["force_expressed_in_body"] != "ground" or ef["point_expressed_in_body"] != "ground":
+            raise NotImplementedError("ExternalForce must be expressed in ground")
+        m.add_external_force(ExternalForce(ef["name"], ef["body"], "grf", ef["force_identifier"],
+                                           ef["point_identifier"], ef["torque_identifier"]))
+
+
+def _walk_armless_kinematics(m: Model, lowpass: float = 6.0) -> DataTable:
+    """TableProcessor("subject_walk_armless_coordinates.mot") |
+    TabOpLowPassFilter(6), in radians, columns renamed to the model's
+    coordinate value paths (extra columns dropped: kinematics_allow_extra_columns)."""
+    from .splines import filter_lowpass_table
+    kin = _load("subject_walk_armless_coordinates.json")
+    byname = {c.name: c for c in m.coordinates()}
+    cols = {byname[k].path + "/value": np.asarray(v) for k, v in kin["columns"].items() if k in byname}
+    tp, fcols = filter_lowpass_table(kin["time"], cols, lowpass)
+    return DataTable("kinematics", tp, fcols, degree=5)
+
+
+def _replaced(m: Model, keep_path_wraps: bool = False) -> Model:
+    """ModOpReplaceMusclesWithDeGrooteFregly2016 on a model stored with its
+    Millard muscles' PathWrapSets: replaceMuscles copies the path points only
+    (DeGrooteFregly2016Muscle.cpp:1007-1020), so the wraps go."""
+    if not keep_path_wraps:
+        for mu in m.muscles:
+            mu.path_wraps = []
+    return m
+
+
+def rajagopal18_model(keep_path_wraps: bool = False) -> Model:
+    """testMocoInverse.cpp:121-128: subject_walk_armless_18musc.osim |
+    ModOpReplaceJointsWithWelds(subtalar, mtp) | ModOpReplaceMusclesWith
+    DeGrooteFregly2016 | ModOpIgnorePassiveFiberForcesDGF |
+    ModOpTendonComplianceDynamicsModeDGF("implicit") | ModOpAddExternalLoads.
+    18 muscles over 16 PathWraps on WrapCylinders, 2 patellofemoral
+    CoordinateCouplerConstraints, the model's own reserve actuators."""
+    m = _replaced(model_from_dict(_load("rajagopal18.json")), keep_path_wraps)
+    m.replace_joints_with_welds(["subtalar_r", "subtalar_l", "mtp_r", "mtp_l"])
+    for mu in m.muscles:
+        mu.ignore_passive_fiber_force = True
+        mu.tendon_compliance_dynamics_mode = "implicit"
+    _walk_armless_grf(m)
+    return m
+
+
+def rajagopal18_inverse(num_mesh_intervals: int = 11, fd_scheme: str = "forward",
+                        sparsity: str = "random", keep_path_wraps: bool = False) -> MocoStudy:
+    """MocoInverse Rajagopal2016, 18 muscles (testMocoInverse.cpp:118-147):
+    time [0.45, 1.0], mesh_interval 0.05 (N = 11), kinematics low-pass
+    filtered at 6 Hz and prescribed by a PositionMotion, the MocoInverse
+    goals and solver settings (MocoInverse.cpp:46-120; see
+    gait10dof18musc_inverse).  The coupler multipliers stay NLP variables
+    (constraint forces in the residual), without kinematic rows.  Its
+    converged solution is std_testMocoInverse_subject_18musc_solution.sto.
+    keep_path_wraps=True keeps the Millard muscles' PathWraps (16 on
+    WrapCylinders), which the reference's replaceMuscles drops."""
+    m = rajagopal18_model(keep_path_wraps)
+    kin = _walk_armless_kinematics(m)
+    p = MocoProblem(m)
+    p.set_position_motion(kin)
+    p.set_time_bounds(0.45, 1.0)
+    p.add_goal(MocoControlGoal("excitation_effort", 1.0))
+    p.add_goal(MocoInitialActivationGoal("initial_activation"))
+    p.add_goal(ImplicitAuxiliaryDerivativesTerm(weight=0.01))
+    s = MocoHipSolver(num_mesh_intervals=num_mesh_intervals,
+                      optim_finite_difference_scheme=fd_scheme, multibody_dynamics_mode="implicit",
+                      interpolate_control_midpoints=False, optim_sparsity_detection=sparsity)
+    return MocoStudy(p, s)
+
+
+def rajagopal80_model(keep_path_wraps: bool = False) -> Model:
+    """example3DWalking muscleDrivenStateTracking (exampleMocoTrack.cpp):
+    subject_walk_armless.osim | ModOpAddExternalLoads(grf_walk.xml) |
+    ModOpIgnoreTendonCompliance | ModOpReplaceMusclesWithDeGrooteFregly2016 |
+    ModOpIgnorePassiveFiberForcesDGF | ModOpScaleActiveFiberForceCurveWidthDGF(1.5):
+    80 DGF muscles (rigid tendons; their 46 PathWraps dropped by
+    replaceMuscles unless keep_path_wraps), 18 coordinates, 2 patellofemoral
+    couplers, the model's 6 pelvis actuators."""
+    m = _replaced(model_from_dict(_load("rajagopal80.json")), keep_path_wraps)
+    for mu in m.muscles:
+        mu.ignore_tendon_compliance = True
+        mu.ignore_passive_fiber_force = True
+        mu.active_force_width_scale = 1.5
+    _walk_armless_grf(m)
+    return m
+
+
+def rajagopal80(num_mesh_intervals: int = 400, fd_scheme: str = "forward",
+                scheme: str = "hermite-simpson", keep_path_wraps: bool = False) -> MocoStudy:
+    """BASELINE configs[3]: the Rajagopal 80-muscle gait NLP at N = 400.  The
+    reference's 80-muscle problem (example3DWalking exampleMocoTrack.cpp
+    muscleDrivenStateTracking: states tracking weight 10, control effort,
+    time [0.81, 1.65], explicit dynamics with the patellofemoral couplers
+    and their derivatives enforced, forward FD) on the filtered coordinate
+    trajectories; BASELINE names a predictive problem, whose contact models
+    are outside this path, so the goals here are the tracking example's
+    (the NLP's layout, DAE and Jacobian are the same).  Block-dense callback
+    sparsity (detection with kinematic constraints is rejected: SURVEY §8
+    F2 note in DESIGN.md).  keep_path_wraps=True: with the 46 PathWraps."""
+    m = rajagopal80_model(keep_path_wraps)
+    kin = _walk_armless_kinematics(m)
+    m.add_table(DataTable("state_reference", kin.times, kin.columns, degree=5))
+    p = MocoProblem(m)
+    p.add_goal(MocoStateTrackingGoal("state_tracking", 10.0, DataTable(
+        "state_reference", kin.times, kin.columns, degree=5)))
+    p.add_goal(MocoControlGoal("control_effort", 1.0))
+    p.set_time_bounds(0.81, 1.65)
+    s = MocoHipSolver(num_mesh_intervals=num_mesh_intervals, transcription_scheme=scheme,
+                      optim_finite_difference_scheme=fd_scheme)
+    return MocoStudy(p, s)
+
+
 CONFIGS = {
     "sliding_mass": sliding_mass,
     "double_pendulum": double_pendulum,
@@ -293,4 +440,7 @@ CONFIGS = {
     "double_pendulum_coupled": double_pendulum_coupled,
     "gait10dof18musc": gait10dof18musc,
     "gait10dof18musc_inverse": gait10dof18musc_inverse,
+    "wrapped_pendulum": wrapped_pendulum,
+    "rajagopal18_inverse": rajagopal18_inverse,
+    "rajagopal80": rajagopal80,
 }

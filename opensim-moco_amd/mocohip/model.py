@@ -191,6 +191,40 @@ class DeGrooteFregly2016Muscle:
     min_control: float = 0.0
     max_control: float = 1.0
     path: str = ""
+    # GeometryPath PathWrapSet, in order: (wrap object name, range begin,
+    # range end) with OpenSim's 1-based point range (< 1: first / last)
+    path_wraps: List[tuple] = field(default_factory=list)
+
+
+@dataclass
+class WrapCylinder:
+    """OpenSim WrapCylinder in a body's WrapObjectSet: axis = the z axis of
+    its frame, which is rotated by the body-fixed X-Y-Z sequence
+    ``xyz_body_rotation`` and translated by ``translation`` in the body;
+    ``quadrant`` "all" / "+x" / "-x" / "+y" / "-y" (include/mocohip.h
+    mh_wrap_object)."""
+    name: str
+    body: str
+    radius: float
+    length: float = 1.0
+    xyz_body_rotation: Sequence[float] = (0.0, 0.0, 0.0)
+    translation: Sequence[float] = (0.0, 0.0, 0.0)
+    quadrant: str = "all"
+    active: bool = True
+
+
+def quadrant_axis_sign(quadrant: str):
+    """WrapObject quadrant -> (wrap axis, wrap sign); "all" -> (0, 0)."""
+    q = quadrant.strip().lower()
+    if q in ("all", ""):
+        return 0, 0
+    sign = -1 if q.startswith("-") else 1
+    ax = q.lstrip("+-")
+    if ax not in ("x", "y", "z"):
+        raise ValueError(f"bad wrap quadrant {quadrant!r}")
+    if ax == "z":
+        raise NotImplementedError("WrapCylinder quadrant along its axis")
+    return "xy".index(ax), sign
 
 
 @dataclass
@@ -259,6 +293,7 @@ class Model:
         self.external_forces: List[ExternalForce] = []
         self.markers: Dict[str, Marker] = {}    # by path
         self.constraints: List[CoordinateCouplerConstraint] = []   # enabled ones
+        self.wraps: Dict[str, WrapCylinder] = {}
 
     # building ---------------------------------------------------------------
     def add_body(self, body: Body):
@@ -296,6 +331,34 @@ class Model:
     def add_constraint(self, k: CoordinateCouplerConstraint):
         self.constraints.append(k)
         return k
+
+    def add_wrap(self, w: WrapCylinder):
+        self.wraps[w.name] = w
+        return w
+
+    def replace_joints_with_welds(self, names: Sequence[str]):
+        """ModOpReplaceJointsWithWelds (ModelFactory::replaceJointWithWeldJoint,
+        Moco/Moco/ModelOperators.h, ModelFactory.cpp): each named joint becomes
+        a WeldJoint with the same parent / child frames; its coordinates, and
+        the actuators on them, are removed."""
+        gone = set()
+        for j in self.joints:
+            if j.name in names:
+                gone.update(c.name for c in j.coordinates)
+                j.coordinates = []
+                j.axes = []
+        missing = set(names) - {j.name for j in self.joints}
+        if missing:
+            raise ValueError(f"no joints {sorted(missing)}")
+        for m in self.muscles:
+            for p in m.points:
+                for f in (p.fx, p.fy, p.fz):
+                    if f is not None and f.coord in gone:
+                        raise NotImplementedError(f"{m.name}: moving point on welded {f.coord}")
+                if p.coord in gone:
+                    raise NotImplementedError(f"{m.name}: conditional point on welded {p.coord}")
+        self.actuators = [a for a in self.actuators
+                          if not (isinstance(a, CoordinateActuator) and a.coordinate in gone)]
 
     def add_marker(self, mk: Marker):
         if not mk.path:
@@ -444,6 +507,35 @@ class CompiledModel:
                 setattr(ms, k, float(getattr(m, k)))
             muscles.append(ms)
 
+        # wrap surfaces (in model order) and the PathWrap list per muscle
+        wraps, pathwraps = [], []
+        wrap_index = {}
+        for w in model.wraps.values():
+            if not w.active:
+                continue
+            ws = abi.mh_wrap_object()
+            ws.kind = abi.MH_WRAP_CYLINDER
+            ws.body = body_index[w.body]
+            ws.wrap_axis, ws.wrap_sign = quadrant_axis_sign(w.quadrant)
+            ws.R_BW[:] = body_fixed_xyz(w.xyz_body_rotation).reshape(-1).tolist()
+            ws.p_BW[:] = list(map(float, w.translation))
+            ws.radius = float(w.radius)
+            ws.length = float(w.length)
+            wrap_index[w.name] = len(wraps)
+            wraps.append(ws)
+        for im, m in enumerate(model.muscles):
+            for (wname, r0, r1) in m.path_wraps:
+                if wname not in wrap_index:
+                    if wname in model.wraps:
+                        continue        # inactive wrap object
+                    raise ValueError(f"{m.name}: unknown wrap object {wname}")
+                pw = abi.mh_path_wrap()
+                pw.muscle, pw.wrap = im, wrap_index[wname]
+                pw.range_begin, pw.range_end = int(r0), int(r1)
+                pathwraps.append(pw)
+        self._wraps = _arr(abi.mh_wrap_object, wraps)
+        self._pathwraps = _arr(abi.mh_path_wrap, pathwraps)
+
         muscle_index = {id(m): i for i, m in enumerate(model.muscles)}
         acts = []
         for a in model.actuators:
@@ -559,6 +651,10 @@ class CompiledModel:
         mm.table_breaks = abi.dptr(self._breaks)
         mm.table_coefs = abi.dptr(self._coefs)
         mm.external = self._ext
+        mm.nwraps = len(wraps)
+        mm.npathwraps = len(pathwraps)
+        mm.wraps = self._wraps
+        mm.pathwraps = self._pathwraps
         self.struct = mm
         self.nq = mm.nq
         self.state_names = model.state_names()
@@ -614,6 +710,12 @@ def model_to_dict(m: Model) -> dict:
             for a in m.actuators],
         "markers": [{"name": k.name, "body": k.body, "location": list(k.location), "path": k.path}
                     for k in m.markers.values()],
+        "wraps": [{"name": w.name, "body": w.body, "radius": w.radius, "length": w.length,
+                   "xyz_body_rotation": list(w.xyz_body_rotation),
+                   "translation": list(w.translation), "quadrant": w.quadrant,
+                   "active": w.active} for w in m.wraps.values()],
+        "constraints": [{"name": k.name, "dependent": k.dependent, "function": _fn_to(k.function),
+                         "scale_factor": k.scale_factor} for k in m.constraints],
     }
 
 
@@ -634,6 +736,7 @@ def model_from_dict(d: dict) -> Model:
                              tuple(p["range"]), _fn_from(p["fx"]), _fn_from(p["fy"]),
                              _fn_from(p["fz"]), p["name"]) for p in a["points"]]
             kw = {k: v for k, v in a.items() if k not in ("type", "points")}
+            kw["path_wraps"] = [tuple(w) for w in kw.get("path_wraps", [])]
             m.add_muscle(DeGrooteFregly2016Muscle(points=pts, **kw))
         else:
             m.add_coordinate_actuator(CoordinateActuator(
@@ -641,4 +744,11 @@ def model_from_dict(d: dict) -> Model:
                 a["max_control"], a["path"]))
     for k in d.get("markers", []):
         m.add_marker(Marker(k["name"], k["body"], tuple(k["location"]), k.get("path", "")))
+    for w in d.get("wraps", []):
+        m.add_wrap(WrapCylinder(w["name"], w["body"], w["radius"], w["length"],
+                                tuple(w["xyz_body_rotation"]), tuple(w["translation"]),
+                                w["quadrant"], w["active"]))
+    for k in d.get("constraints", []):
+        m.add_constraint(CoordinateCouplerConstraint(k["name"], k["dependent"],
+                                                     _fn_from(k["function"]), k["scale_factor"]))
     return m

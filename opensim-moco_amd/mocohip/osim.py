@@ -20,8 +20,8 @@ from typing import Dict, List, Optional
 
 from . import abi
 from .model import (Axis, Body, Coordinate, CoordinateActuator,
-                    DeGrooteFregly2016Muscle, Function, Joint, Model,
-                    PathPoint)
+                    CoordinateCouplerConstraint, DeGrooteFregly2016Muscle,
+                    Function, Joint, Model, PathPoint, WrapCylinder)
 
 # opensim-core Millard2012EquilibriumMuscle defaults (restated).
 MILLARD_DEFAULTS = dict(fiber_damping=0.1, default_activation=0.05,
@@ -53,13 +53,17 @@ def _bool(el, tag, default=False):
     return default if t is None else t.strip().lower() == "true"
 
 
+FUNCTION_TAGS = ("Constant", "LinearFunction", "SimmSpline", "MultiplierFunction",
+                 "PiecewiseLinearFunction", "NaturalCubicSpline", "GCVSpline", "PolynomialFunction")
+
+
 def parse_function(fel, coord: Optional[str]) -> Function:
     """Parse the single function element below ``fel``."""
     if fel is None:
         return Function.constant(0.0)
     kids = list(fel)
     f = kids[0] if fel.tag in ("function", "x_location", "y_location",
-                               "z_location") else fel
+                               "z_location", "coupled_coordinates_function") else fel
     tag = f.tag
     if tag == "Constant":
         return Function.constant(_float(f, "value", 0.0))
@@ -110,7 +114,11 @@ def _axes_for(jel, jtype: str, coords: List[Coordinate]) -> List[Axis]:
             if len(cn) > 1:
                 raise NotImplementedError("TransformAxis with >1 coordinate")
             coord = cn[0] if cn else None
-            fn = parse_function(ta.find("function"), coord)
+            # OpenSim 3: <function><Kind/></function>; OpenSim 4: <Kind name="function"/>
+            fel = ta.find("function")
+            if fel is None:
+                fel = next((ch for ch in ta if ch.tag in FUNCTION_TAGS), None)
+            fn = parse_function(fel, coord)
             if coord is None and fn.kind != abi.MH_FN_CONSTANT:
                 raise ValueError("non-constant TransformAxis without a coordinate")
             ax = Axis(abi.MH_AXIS_ROTATION if name.startswith("rotation")
@@ -146,10 +154,67 @@ def _path_points(gp) -> List[PathPoint]:
     return pts
 
 
-def _muscle_to_dgf(m, tendon_compliance: Optional[bool]) -> DeGrooteFregly2016Muscle:
-    """DeGrooteFregly2016Muscle::replaceMuscles mapping (.cpp:948-1010)."""
+def _path_wraps(gp) -> List[tuple]:
+    """GeometryPath PathWrapSet: (wrap object, range begin, range end)."""
+    out = []
+    ws = gp.find("PathWrapSet/objects") if gp is not None else None
+    if ws is None:
+        return out
+    for w in ws.findall("PathWrap"):
+        rng = [int(round(v)) for v in _floats(_text(w, "range", "-1 -1"))] or [-1, -1]
+        out.append((_text(w, "wrap_object"), rng[0], rng[1]))
+    return out
+
+
+def _wrap_objects(bel, body: str) -> List[WrapCylinder]:
+    """A body's WrapObjectSet (WrapCylinder only)."""
+    out = []
+    ws = bel.find("WrapObjectSet/objects")
+    if ws is None:
+        return out
+    for w in list(ws):
+        if w.tag != "WrapCylinder":
+            raise NotImplementedError(f"wrap object {w.tag} ({w.get('name')})")
+        out.append(WrapCylinder(
+            w.get("name"), body, _float(w, "radius", 0.0), _float(w, "length", 1.0),
+            tuple(_floats(_text(w, "xyz_body_rotation", "0 0 0"))),
+            tuple(_floats(_text(w, "translation", "0 0 0"))),
+            _text(w, "quadrant", "all"), _bool(w, "active", True)))
+    return out
+
+
+def _constraints(mel) -> List[CoordinateCouplerConstraint]:
+    """Enabled CoordinateCouplerConstraints with one independent coordinate
+    (OpenSim 4: isEnforced; OpenSim 3: isDisabled)."""
+    out = []
+    cs = mel.find("ConstraintSet/objects")
+    if cs is None:
+        return out
+    for k in list(cs):
+        if k.tag != "CoordinateCouplerConstraint":
+            raise NotImplementedError(f"constraint {k.tag}")
+        if not _bool(k, "isEnforced", True) or _bool(k, "isDisabled", False):
+            continue
+        ind = (_text(k, "independent_coordinate_names", "") or "").split()
+        if len(ind) != 1:
+            raise NotImplementedError(f"{k.get('name')}: {len(ind)} independent coordinates")
+        fn = parse_function(k.find("coupled_coordinates_function"), ind[0])
+        out.append(CoordinateCouplerConstraint(k.get("name"), _text(k, "dependent_coordinate_name"),
+                                               fn, _float(k, "scale_factor", 1.0)))
+    return out
+
+
+def _muscle_to_dgf(m, tendon_compliance: Optional[bool],
+                   keep_path_wraps: bool = False) -> DeGrooteFregly2016Muscle:
+    """DeGrooteFregly2016Muscle::replaceMuscles mapping (.cpp:948-1010).
+    replaceMuscles copies the PathPointSet only (.cpp:1007-1020): a replaced
+    Millard / Thelen muscle loses its PathWrapSet, as in the reference
+    (keep_path_wraps=True keeps it: not the reference's behaviour).  Native
+    DeGrooteFregly2016Muscle elements keep theirs."""
     tag = m.tag
     d = DeGrooteFregly2016Muscle(m.get("name"), _path_points(m.find("GeometryPath")))
+    if tag == "DeGrooteFregly2016Muscle" or keep_path_wraps:
+        d.path_wraps = _path_wraps(m.find("GeometryPath"))
     if tag == "Millard2012EquilibriumMuscle":
         d.default_activation = _float(m, "default_activation", MILLARD_DEFAULTS["default_activation"])
         d.activation_time_constant = _float(m, "activation_time_constant",
@@ -203,7 +268,8 @@ MUSCLE_TAGS = ("Millard2012EquilibriumMuscle", "Thelen2003Muscle",
 
 
 def read_osim(path: str, remove_muscles: bool = False,
-              tendon_compliance: Optional[bool] = None) -> Model:
+              tendon_compliance: Optional[bool] = None,
+              keep_path_wraps: bool = False) -> Model:
     root = ET.parse(path).getroot()
     mel = root.find("Model")
     model = Model(mel.get("name"), tuple(_floats(_text(mel, "gravity", "0 -9.80665 0"))))
@@ -217,6 +283,8 @@ def read_osim(path: str, remove_muscles: bool = False,
                                                    "inertia_xy", "inertia_xz", "inertia_yz")]
             model.add_body(Body(name, _float(b, "mass", 0.0),
                                 tuple(_floats(_text(b, "mass_center", "0 0 0"))), inertia))
+            for w in _wrap_objects(b, name):
+                model.add_wrap(w)
             jwrap = b.find("Joint")
             jel = list(jwrap)[0] if jwrap is not None and len(list(jwrap)) else None
             if jel is None:
@@ -234,6 +302,8 @@ def read_osim(path: str, remove_muscles: bool = False,
             inertia6 = _floats(_text(b, "inertia", "0 0 0 0 0 0"))
             model.add_body(Body(b.get("name"), _float(b, "mass", 0.0),
                                 tuple(_floats(_text(b, "mass_center", "0 0 0"))), inertia6))
+            for w in _wrap_objects(b, b.get("name")):
+                model.add_wrap(w)
         for jel in list(mel.find("JointSet/objects")):
             frames = {f.get("name"): f for f in jel.findall("frames/PhysicalOffsetFrame")}
 
@@ -250,6 +320,8 @@ def read_osim(path: str, remove_muscles: bool = False,
             coords = _coordinates(jel)
             model.add_joint(Joint(jel.get("name"), pname, cname, coords,
                                   _axes_for(jel, jel.tag, coords), pl, po, cl, co))
+    for k in _constraints(mel):
+        model.add_constraint(k)
     # forces, in force-set order
     fs = mel.find("ForceSet/objects")
     if fs is not None:
@@ -259,7 +331,7 @@ def read_osim(path: str, remove_muscles: bool = False,
                     continue
                 if _bool(f, "isDisabled", False) or not _bool(f, "appliesForce", True):
                     continue
-                model.add_muscle(_muscle_to_dgf(f, tendon_compliance))
+                model.add_muscle(_muscle_to_dgf(f, tendon_compliance, keep_path_wraps))
             elif f.tag == "CoordinateActuator":
                 model.add_coordinate_actuator(CoordinateActuator(
                     f.get("name"), _text(f, "coordinate"),

@@ -136,3 +136,43 @@ class SimmSpline:
         if deriv == 1:
             return b[k] + dx * (2.0 * c[k] + 3.0 * dx * d[k])
         return 2.0 * c[k] + 6.0 * dx * d[k]
+
+
+def pad_odd(x: np.ndarray, p: int) -> np.ndarray:
+    """Signal::Pad (TableUtilities::pad / Storage::pad): p samples at each
+    end, reflected about the end sample and negated (odd reflection)."""
+    x = np.asarray(x, float)
+    n = len(x)
+    return np.concatenate([2 * x[0] - x[p:0:-1], x, 2 * x[-1] - x[n - 2:n - 2 - p:-1]])
+
+
+def lowpass_iir(dt: float, fc: float, sig: np.ndarray) -> np.ndarray:
+    """Signal::LowpassIIR: third-order Butterworth (prewarped bilinear
+    transform) run forward then backward, the first three outputs of each
+    pass set to its inputs."""
+    wa = math.tan(2 * math.pi * fc * dt / 2)
+    wa2, wa3 = wa * wa, wa * wa * wa
+    den = 1 + 2 * wa + 2 * wa2 + wa3
+    b = np.array([wa3, 3 * wa3, 3 * wa3, wa3]) / den
+    a = np.array([(-3 - 2 * wa + 2 * wa2 + 3 * wa3), (3 - 2 * wa - 2 * wa2 + 3 * wa3),
+                  (-1 + 2 * wa - 2 * wa2 + wa3)]) / den
+
+    def run(s):
+        f = s.copy()
+        for i in range(3, len(s)):
+            f[i] = (b[0] * s[i] + b[1] * s[i - 1] + b[2] * s[i - 2] + b[3] * s[i - 3]
+                    - a[0] * f[i - 1] - a[1] * f[i - 2] - a[2] * f[i - 3])
+        return f
+    return run(run(np.asarray(sig, float))[::-1])[::-1]
+
+
+def filter_lowpass_table(times, columns: dict, fc: float):
+    """TableUtilities::filterLowpass(table, fc, padData=true) (TabOpLowPassFilter):
+    pad nrows/2 samples at both ends (times extended by the same odd
+    reflection, i.e. uniformly), then LowpassIIR with the sampling interval;
+    the padded rows stay in the table."""
+    t = np.asarray(times, float)
+    p = len(t) // 2
+    tp = pad_odd(t, p)
+    dt = t[1] - t[0]
+    return tp, {k: lowpass_iir(dt, fc, pad_odd(np.asarray(v, float), p)) for k, v in columns.items()}

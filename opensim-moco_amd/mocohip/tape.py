@@ -14,7 +14,9 @@ Layout (little endian, x86-64 struct layout of include/mocohip.h):
   endpoint-constraint equations (mh_problem.nendpoint/endpoint); version 4
   (ABI v4: mh_options grew) appends the kinematic constraints
   (mh_model.nconstraints/constraints) and the multiplier and
-  kinematic-constraint bounds.  Readers accept version 4 only."""
+  kinematic-constraint bounds; version 5 (ABI v5) appends the wrap surfaces
+  and PathWraps (mh_model.nwraps/wraps, npathwraps/pathwraps).  Readers
+  accept versions 4 and 5."""
 from __future__ import annotations
 
 import ctypes as C
@@ -23,7 +25,7 @@ import struct
 from . import abi
 
 MAGIC = b"MHTAPE01"
-VERSION = 4   # 2: + path constraints; 3: + endpoint constraints; 4: + kinematic constraints
+VERSION = 5   # 2: + path constraints; 3: + endpoint constraints; 4: + kinematic constraints; 5: + wraps
 
 # (field, element type, count attribute of mh_model / None for problem arrays)
 _MODEL_ARRAYS = [
@@ -95,5 +97,9 @@ def write_tape(rep, opts: abi.mh_options, path: str) -> None:
     kb = _blob(m.constraints, abi.mh_constraint, m.nconstraints)
     out += [struct.pack("<i", m.nconstraints), struct.pack("<q", len(kb)), kb,
             bytes(p.multiplier_bounds), bytes(p.kinematic_constraint_bounds)]
+    wb = _blob(m.wraps, abi.mh_wrap_object, m.nwraps)
+    pw = _blob(m.pathwraps, abi.mh_path_wrap, m.npathwraps)
+    out += [struct.pack("<i", m.nwraps), struct.pack("<q", len(wb)), wb,
+            struct.pack("<i", m.npathwraps), struct.pack("<q", len(pw)), pw]
     with open(path, "wb") as fh:
         fh.write(b"".join(out))

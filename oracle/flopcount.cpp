@@ -43,7 +43,8 @@ static inline bool operator>=(Counted a, Counted b) { return a.v >= b.v; }
 static inline bool operator==(Counted a, Counted b) { return a.v == b.v; }
 #define CFN(name) \
     static inline Counted name(Counted a) { g_tally.fn++; return Counted(std::name(a.v)); }
-CFN(sqrt) CFN(exp) CFN(log) CFN(sin) CFN(cos) CFN(tanh) CFN(sinh) CFN(asin)
+CFN(sqrt) CFN(exp) CFN(log) CFN(sin) CFN(cos) CFN(tanh) CFN(sinh) CFN(asin) CFN(acos)
+static inline Counted atan2(Counted a, Counted b) { g_tally.fn++; return Counted(std::atan2(a.v, b.v)); }
 static inline Counted fabs(Counted a) { return Counted(std::fabs(a.v)); }
 static inline Counted pow(Counted a, double b) { g_tally.fn++; return Counted(std::pow(a.v, b)); }
 static inline bool isnan(Counted a) { return std::isnan(a.v); }

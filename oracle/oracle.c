@@ -291,6 +291,14 @@ struct orc_ctx {
     /* MH_JACOBIAN_GLOBAL_SEEDS: the seed (color) of every x column */
     int jac_seeds, nseeds;
     int32_t* seed_color;
+    /* muscle wrapping (ABI v5): wrap surfaces, PathWrap entries grouped by
+     * muscle, each muscle's first entry and count, and the current-path
+     * capacity (points + 2 per PathWrap) */
+    int NWR, NPW;
+    mh_wrap_object* wr;
+    mh_path_wrap* pw;
+    int *mus_pw_begin, *mus_pw_count;
+    int maxcp;
 };
 
 static double* dup_d(const double* p, size_t n) {
@@ -555,8 +563,9 @@ static void tail_rows(const orc_ctx* c, int64_t row0, row_fn emit, void* ud) {
 
 /* Endpoint-constraint rows (CasOCTranscription.h:283-285: first in g).  The
  * Endpoint callback's inputs (CasOCFunction.h:167-240) are [initial_time,
- * initial point inputs, final_time, final point inputs] (no multipliers or
- * parameters here; the integral input is a constant NaN when the goal has
+ * initial point inputs, final_time, final point inputs] (the point inputs
+ * in this build's lane order: states, controls, derivatives, multipliers;
+ * no parameters here; the integral input is a constant NaN when the goal has
  * no integrand, CasOCTranscription.cpp:562-564).  Subset index si of that
  * vector -> NLP column. */
 static int ep_width(const orc_ctx* c) { return 2 * (1 + c->NP); }
@@ -567,7 +576,8 @@ static int64_t ep_col(const orc_ctx* c, int si) {
     int k = pt ? c->G - 1 : 0;
     if (j < c->NS) return col_state(c, k, j);
     if (j < c->NS + c->NC) return col_control(c, k, j - c->NS);
-    return col_deriv(c, k, j - c->NS - c->NC);
+    if (j < c->NS + c->NC + c->NDV) return col_deriv(c, k, j - c->NS - c->NC);
+    return col_mult(c, k, j - c->NS - c->NC - c->NDV);
 }
 /* Columns of endpoint row e, ascending: every input (block-dense) or the
  * detected ones; si[] receives the matching subset indices. */
@@ -777,6 +787,39 @@ int orc_create(const mh_problem* p, const mh_options* o, orc_ctx** out) {
         return fail(MH_ERR_INVALID, "bad kinematic constraints");
     }
     c->kcs = DUP(mh_constraint, M->constraints, c->NKC);
+    /* wrap surfaces and PathWraps (grouped by muscle, in path order) */
+    c->NWR = M->nwraps;
+    c->NPW = M->npathwraps;
+    if (c->NWR < 0 || c->NPW < 0 || (c->NWR > 0 && !M->wraps) || (c->NPW > 0 && !M->pathwraps)) {
+        orc_destroy(c);
+        return fail(MH_ERR_INVALID, "bad wrap objects");
+    }
+    c->wr = DUP(mh_wrap_object, M->wraps, c->NWR);
+    c->pw = DUP(mh_path_wrap, M->pathwraps, c->NPW);
+    c->mus_pw_begin = (int*)calloc((size_t)M->nmuscles + 1, sizeof(int));
+    c->mus_pw_count = (int*)calloc((size_t)M->nmuscles + 1, sizeof(int));
+    for (int i = 0; i < c->NWR; ++i) {
+        const mh_wrap_object* W = &c->wr[i];
+        if (W->kind != MH_WRAP_CYLINDER || W->body < -1 || W->body >= M->nbodies || !(W->radius > 0.0) ||
+                W->wrap_axis < 0 || W->wrap_axis > 1 || W->wrap_sign < -1 || W->wrap_sign > 1) {
+            orc_destroy(c);
+            return fail(MH_ERR_INVALID, "wrap object %d: bad kind/body/radius/quadrant", i);
+        }
+    }
+    for (int k = 0; k < c->NPW; ++k) {
+        const mh_path_wrap* W = &c->pw[k];
+        if (W->muscle < 0 || W->muscle >= M->nmuscles || W->wrap < 0 || W->wrap >= c->NWR ||
+                (k > 0 && W->muscle < c->pw[k - 1].muscle)) {
+            orc_destroy(c);
+            return fail(MH_ERR_INVALID, "path wrap %d: bad muscle/wrap or not grouped by muscle", k);
+        }
+        if (c->mus_pw_count[W->muscle]++ == 0) c->mus_pw_begin[W->muscle] = k;
+    }
+    c->maxcp = 1;
+    for (int im = 0; im < M->nmuscles; ++im) {
+        int cap = M->muscles[im].point_count + 2 * c->mus_pw_count[im];
+        if (cap > c->maxcp) c->maxcp = cap;
+    }
     for (int i = 0; i < c->NKC; ++i) {
         const mh_constraint* K = &c->kcs[i];
         int f = K->func;
@@ -787,10 +830,14 @@ int orc_create(const mh_problem* p, const mh_options* o, orc_ctx** out) {
             return fail(MH_ERR_INVALID, "kinematic constraint %d: bad kind/function/coordinate", i);
         }
     }
-    if (c->NKC && (c->presc || p->nendpoint > 0 || o->sparsity_detection != MH_SPARSITY_NONE)) {
+    /* with prescribed kinematics the constraints keep their multipliers
+     * (constraint forces in the residual) but no kinematic rows and no
+     * slacks: the motion is assumed to obey them (CasOCProblem.h:508-521,
+     * MocoCasOCProblem.h:664-676, CasOCTranscription.cpp:316-318) */
+    if (c->NKC && !c->presc && (p->nendpoint > 0 || o->sparsity_detection != MH_SPARSITY_NONE)) {
         orc_destroy(c);
-        return fail(MH_ERR_UNSUPPORTED, "kinematic constraints with prescribed kinematics, endpoint "
-                    "constraints or sparsity detection");
+        return fail(MH_ERR_UNSUPPORTED, "kinematic constraints (without prescribed kinematics) with "
+                    "endpoint constraints or sparsity detection");
     }
     if (o->minimize_lagrange_multipliers && !c->NKC) {   /* MocoCasOCProblem.cpp:101-107 */
         orc_destroy(c);
@@ -818,8 +865,8 @@ int orc_create(const mh_problem* p, const mh_options* o, orc_ctx** out) {
     }
     c->enforce = !o->ignore_constraint_derivatives;
     c->NM = c->NKC;
-    c->NK = c->enforce ? 3 * c->NKC : c->NKC;
-    c->NSL = c->enforce && o->transcription == MH_HERMITE_SIMPSON ? c->NKC : 0;
+    c->NK = c->presc ? 0 : (c->enforce ? 3 * c->NKC : c->NKC);
+    c->NSL = !c->presc && c->enforce && o->transcription == MH_HERMITE_SIMPSON ? c->NKC : 0;
     c->OKC = c->NQ + c->NZ + c->NAR;
     c->OQC = c->OKC + c->NK;
     c->mult_lo = -1000.0; c->mult_hi = 1000.0;
@@ -1028,7 +1075,7 @@ void orc_destroy(orc_ctx* c) {
     void* ptrs[] = {c->bodies, c->axes, c->funcs, c->kx, c->ky, c->kb, c->kc, c->kd,
             c->mus, c->pts, c->acts, c->tabs, c->brk, c->coef, c->ext, c->sinfo, c->cinfo,
             c->goals, c->gidx, c->gcol, c->gw, c->pc, c->sp, c->sp_pc, c->mus_ider, c->kin_col,
-            c->ep, c->sp_ep, c->kcs, c->seed_color,
+            c->ep, c->sp_ep, c->kcs, c->seed_color, c->wr, c->pw, c->mus_pw_begin, c->mus_pw_count,
             c->mus_act_state, c->mus_ftn_state,
             c->mus_control, c->coord_body, c->grid, c->quad, c->iRow, c->jCol};
     for (size_t i = 0; i < sizeof ptrs / sizeof ptrs[0]; ++i) free(ptrs[i]);
@@ -1350,6 +1397,18 @@ static void dgf_muscle(const orc_ctx* c, const mh_muscle* mu, real LMT, real VMT
     }
 }
 
+/* An entry of a muscle's current path (OpenSim GeometryPath::getCurrentPath):
+ * an active path point (pt >= 0) or a PathWrapPoint of PathWrap entry pwi
+ * (pt < 0; wp = 1 / 2 for the wrap's first / second tangent point, on the
+ * wrap object's body at body-frame location loc; wlen = the length over the
+ * surface from the first tangent point, stored on the second). */
+typedef struct {
+    int pt, pwi, wp, body;
+    real loc[3];
+    real wlen;
+    real P[3], V[3];
+} cpoint;
+
 /* Workspace for one DAE evaluation. */
 typedef struct {
     real *R, *p;    /* body pose (world): 9, 3 per body                  */
@@ -1364,6 +1423,7 @@ typedef struct {
     real* fvals;    /* function value/d1/d2 per axis (3 per axis)        */
     real* xfull;    /* prescribed kinematics: [q, u, z]                  */
     real* udot;     /* prescribed kinematics: udot                       */
+    cpoint* cp;     /* one muscle's current path (points + wrap points)  */
 } dae_ws;
 
 static void ws_alloc(const orc_ctx* c, dae_ws* w) {
@@ -1384,11 +1444,12 @@ static void ws_alloc(const orc_ctx* c, dae_ws* w) {
     w->fvals = (real*)malloc(sizeof(real) * 3 * (size_t)(M->naxes + 1));
     w->xfull = (real*)malloc(sizeof(real) * (size_t)(2 * c->NQ + c->NZ + 1));
     w->udot = (real*)malloc(sizeof(real) * (size_t)(c->NQ + 1));
+    w->cp = (cpoint*)malloc(sizeof(cpoint) * (size_t)(c->maxcp + 1));
 }
 static void ws_free(dae_ws* w) {
     free(w->R); free(w->p); free(w->V); free(w->A); free(w->F); free(w->S); free(w->I);
     free(w->M); free(w->tau); free(w->ppos); free(w->pvel); free(w->pact); free(w->fvals);
-    free(w->xfull); free(w->udot);
+    free(w->xfull); free(w->udot); free(w->cp);
 }
 
 /* Forward kinematics, velocities and velocity-product accelerations in the
@@ -1536,24 +1597,243 @@ static void path_points(const orc_ctx* c, const real* q, const real* u, dae_ws* 
     }
 }
 
-static void muscle_length_speed(const orc_ctx* c, const dae_ws* w, int im, real* len, real* spd) {
+/* ------------------------------------------------------------------------
+ * Muscle wrapping over cylinders (opensim-core @b0222c2, third-party and
+ * absent here: GeometryPath::applyWrapObjects / calcPathLengthChange,
+ * WrapObject::wrapPathSegment, WrapCylinder::wrapLine; restated from their
+ * documented algorithm: the shortest path around the cylinder).  Parity
+ * with opensim-core's WrapCylinder is unpinned: no reference fixture holds
+ * a wrapped path, because DeGrooteFregly2016Muscle::replaceMuscles
+ * (DeGrooteFregly2016Muscle.cpp:1007-1020) copies only the PathPointSet, so
+ * every reference problem that converts muscles to DGF (MocoInverse,
+ * example3DWalking) runs without its PathWraps -- which the reference's
+ * converged Rajagopal 18-muscle MocoInverse confirms (tests/test_oracle.py
+ * test_rajagopal18_inverse_golden_solution).  Native DGF muscles with a
+ * PathWrapSet wrap here.
+ * ------------------------------------------------------------------------ */
+enum { WRAP_NONE = 0, WRAP_INSIDE = 1, WRAP_WRAPPED = 2 };
+
+/* Ground position of body-frame station loc of body b (-1 = ground) and the
+ * velocity of that body-fixed point. */
+static void body_station(const dae_ws* w, int body, const real* loc, real* P, real* V) {
+    int bs = body + 1;
+    const real* R = w->R + 9 * bs;
+    const real* p = w->p + 3 * bs;
+    real t[3];
+    mat_vec(R, loc, t);
+    for (int d = 0; d < 3; ++d) P[d] = p[d] + t[d];
+    if (V) {
+        cross(w->V[bs].w, P, t);
+        for (int d = 0; d < 3; ++d) V[d] = w->V[bs].v[d] + t[d];
+    }
+}
+
+/* WrapCylinder::wrapLine in the cylinder frame (axis z, radius R): the
+ * shortest path from a to b that stays outside the cylinder.  Its
+ * projection on the xy plane is tangent - arc - tangent; along the axis it
+ * rises linearly with the projected length (the unrolled cylinder makes the
+ * path straight), so the surface part is a helix of length
+ * sqrt((R dtheta)^2 + dz^2).  No wrap when a point lies inside the radius
+ * (insideRadius) or when the segment's projection misses the circle; a
+ * quadrant constraint (wrap_sign != 0) forces the wrap onto its half-space:
+ * a segment passing on the other side wraps around the constrained side. */
+static int wrap_cylinder(const mh_wrap_object* W, const real* a, const real* b, real* r1, real* r2,
+        real* wlen) {
+    real R = W->radius, R2 = R * R;
+    real a2 = a[0] * a[0] + a[1] * a[1], b2 = b[0] * b[0] + b[1] * b[1];
+    if (a2 < R2 || b2 < R2) return WRAP_INSIDE;
+    real d0 = b[0] - a[0], d1 = b[1] - a[1];
+    real dd = d0 * d0 + d1 * d1;
+    real t = dd > 0.0 ? -(a[0] * d0 + a[1] * d1) / dd : 0.0;
+    real n0 = a[0] + t * d0, n1 = a[1] + t * d1;
+    int hits = (n0 * n0 + n1 * n1 < R2) && t > 0.0 && t < 1.0;
+    real cr = a[0] * b[1] - a[1] * b[0];
+    real sshort = cr < 0.0 ? -1.0 : 1.0;
+    real sigma = sshort;
+    if (W->wrap_sign != 0) {
+        real nk = W->wrap_axis == 0 ? n0 : n1;
+        if (nk * (real)W->wrap_sign >= 0.0) {
+            if (!hits) return WRAP_NONE;
+        } else {
+            sigma = -sshort;   /* around the constrained side */
+        }
+    } else if (!hits) {
+        return WRAP_NONE;
+    }
+    real ra = sqrt(a2), rb = sqrt(b2);
+    real th1 = atan2(a[1], a[0]) + sigma * acos(R / ra);
+    real th2 = atan2(b[1], b[0]) - sigma * acos(R / rb);
+    real dth = sigma * (th2 - th1);
+    const real twopi = 6.283185307179586;
+    while (dth < 0.0) dth = dth + twopi;
+    while (dth >= twopi) dth = dth - twopi;
+    real l1 = sqrt(a2 - R2), l2 = sqrt(b2 - R2), arc = R * dth;
+    real Lxy = l1 + arc + l2;
+    real dz = b[2] - a[2];
+    real z1 = a[2] + dz * (l1 / Lxy), z2 = a[2] + dz * ((l1 + arc) / Lxy);
+    r1[0] = R * cos(th1); r1[1] = R * sin(th1); r1[2] = z1;
+    r2[0] = R * cos(th2); r2[1] = R * sin(th2); r2[2] = z2;
+    real zz = z2 - z1;
+    *wlen = sqrt(arc * arc + zz * zz);
+    return WRAP_WRAPPED;
+}
+
+/* WrapObject::wrapPathSegment: the segment's ends in the wrap object's
+ * frame (ground -> body -> cylinder), wrapLine, tangent points back to the
+ * body frame. */
+static int wrap_segment(const orc_ctx* c, const dae_ws* w, const mh_wrap_object* W, const cpoint* A,
+        const cpoint* B, real* r1B, real* r2B, real* wlen) {
+    int bs = W->body + 1;
+    const real* R = w->R + 9 * bs;
+    const real* p = w->p + 3 * bs;
+    real pw[2][3];
+    const cpoint* E[2] = {A, B};
+    for (int e = 0; e < 2; ++e) {
+        real g[3] = {E[e]->P[0] - p[0], E[e]->P[1] - p[1], E[e]->P[2] - p[2]};
+        real sb[3];
+        for (int i = 0; i < 3; ++i) sb[i] = R[i] * g[0] + R[3 + i] * g[1] + R[6 + i] * g[2];   /* R^T g */
+        for (int i = 0; i < 3; ++i) sb[i] = sb[i] - W->p_BW[i];
+        for (int i = 0; i < 3; ++i)
+            pw[e][i] = W->R_BW[i] * sb[0] + W->R_BW[3 + i] * sb[1] + W->R_BW[6 + i] * sb[2];
+    }
+    real r1[3], r2[3];
+    int res = wrap_cylinder(W, pw[0], pw[1], r1, r2, wlen);
+    (void)c;
+    if (res != WRAP_WRAPPED) return res;
+    for (int i = 0; i < 3; ++i) {
+        r1B[i] = W->R_BW[3 * i] * r1[0] + W->R_BW[3 * i + 1] * r1[1] + W->R_BW[3 * i + 2] * r1[2] + W->p_BW[i];
+        r2B[i] = W->R_BW[3 * i] * r2[0] + W->R_BW[3 * i + 1] * r2[1] + W->R_BW[3 * i + 2] * r2[2] + W->p_BW[i];
+    }
+    return res;
+}
+
+static real dist3(const real* a, const real* b) {
+    real d[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]};
+    return sqrt(dot3(d, d));
+}
+
+/* Length of a current path: straight segments, except between the two
+ * tangent points of one wrap (the stored surface length). */
+static real cpath_length(const cpoint* cp, int n) {
+    real L = 0.0;
+    for (int k = 1; k < n; ++k) {
+        if (cp[k].pt < 0 && cp[k - 1].pt < 0 && cp[k].pwi == cp[k - 1].pwi) L += cp[k].wlen;
+        else L += dist3(cp[k - 1].P, cp[k].P);
+    }
+    return L;
+}
+
+/* GeometryPath::applyWrapObjects: each PathWrap (in order) removes its
+ * tangent points, tries every segment of its point range (the first and
+ * last ACTIVE original points of [range_begin, range_end]) that is not the
+ * surface part of one wrap, keeps the wrapped segment with the smallest
+ * length change (|p1 r1| + surface + |r2 p2| - |p1 p2|) and inserts its two
+ * tangent points there.  Two or more PathWraps iterate (at most 8 passes)
+ * until the path length changes by less than 0.0005; after the first pass,
+ * a no-wrap first object and an inside-radius second one swap order. */
+static int apply_wraps(const orc_ctx* c, const dae_ws* w, int im, cpoint* cp, int n) {
     const mh_muscle* mu = &c->mus[im];
-    real L = 0.0, S = 0.0;
-    int prev = -1;
+    int nw = c->mus_pw_count[im], pb = c->mus_pw_begin[im];
+    int order[64], result[64];
+    if (nw > 64) nw = 64;
+    for (int i = 0; i < nw; ++i) { order[i] = i; result[i] = WRAP_NONE; }
+    int maxit = nw < 2 ? 1 : 8;
+    real last = INFINITY;
+    for (int kk = 0; kk < maxit; ++kk) {
+        for (int i = 0; i < nw; ++i) {
+            result[i] = WRAP_NONE;
+            int pwi = pb + order[i];
+            const mh_path_wrap* PW = &c->pw[pwi];
+            const mh_wrap_object* W = &c->wr[PW->wrap];
+            for (int j = 0; j < n; ++j)
+                if (cp[j].pt < 0 && cp[j].pwi == pwi) {
+                    for (int k = j; k + 2 < n; ++k) cp[k] = cp[k + 2];
+                    n -= 2;
+                    break;
+                }
+            int ws = PW->range_begin < 1 ? 0 : PW->range_begin - 1;
+            int we = PW->range_end < 1 ? mu->point_count - 1 : PW->range_end - 1;
+            int jf = ws, jr = we;
+            while (jf <= we && !w->pact[mu->point_begin + jf]) ++jf;
+            if (jf > we) return n;
+            while (jr >= ws && !w->pact[mu->point_begin + jr]) --jr;
+            if (jr < ws) return n;
+            int start = -1, end = -1;
+            for (int j = 0; j < n; ++j) {
+                if (cp[j].pt == mu->point_begin + jf) start = j;
+                if (cp[j].pt == mu->point_begin + jr) end = j;
+            }
+            if (start < 0 || end < 0) return n;
+            int best = -1;
+            real bestc = INFINITY, br1[3] = {0, 0, 0}, br2[3] = {0, 0, 0}, bl = 0.0;
+            for (int k = start; k < end; ++k) {
+                if (cp[k].pt < 0 && cp[k + 1].pt < 0 && cp[k].pwi == cp[k + 1].pwi) continue;
+                real r1[3], r2[3], wl;
+                result[i] = wrap_segment(c, w, W, &cp[k], &cp[k + 1], r1, r2, &wl);
+                if (result[i] != WRAP_WRAPPED) continue;
+                real g1[3], g2[3];
+                body_station(w, W->body, r1, g1, NULL);
+                body_station(w, W->body, r2, g2, NULL);
+                real chg = dist3(cp[k].P, g1) + wl + dist3(g2, cp[k + 1].P) - dist3(cp[k].P, cp[k + 1].P);
+                if (chg < bestc) {
+                    bestc = chg; best = k; bl = wl;
+                    for (int d = 0; d < 3; ++d) { br1[d] = r1[d]; br2[d] = r2[d]; }
+                }
+            }
+            if (best >= 0) {
+                for (int k = n - 1; k > best; --k) cp[k + 2] = cp[k];
+                n += 2;
+                for (int e = 0; e < 2; ++e) {
+                    cpoint* q = &cp[best + 1 + e];
+                    q->pt = -1; q->pwi = pwi; q->wp = e + 1; q->body = W->body;
+                    for (int d = 0; d < 3; ++d) q->loc[d] = e ? br2[d] : br1[d];
+                    q->wlen = e ? bl : 0.0;
+                    body_station(w, W->body, q->loc, q->P, q->V);
+                }
+            }
+        }
+        real L = cpath_length(cp, n);
+        if (fabs(L - last) < 0.0005) break;
+        last = L;
+        if (kk == 0 && nw > 1 && result[0] == WRAP_NONE && result[1] == WRAP_INSIDE) {
+            int t = order[0]; order[0] = order[1]; order[1] = t;
+        }
+    }
+    return n;
+}
+
+/* The muscle's current path: its active points, then the wraps. */
+static int current_path(const orc_ctx* c, const dae_ws* w, int im, cpoint* cp) {
+    const mh_muscle* mu = &c->mus[im];
+    int n = 0;
     for (int i = mu->point_begin; i < mu->point_begin + mu->point_count; ++i) {
         if (!w->pact[i]) continue;
-        if (prev >= 0) {
-            const real* a = w->ppos + 3 * prev;
-            const real* b = w->ppos + 3 * i;
-            real d[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]};
-            real l = sqrt(dot3(d, d));
-            L += l;
-            const real* va = w->pvel + 3 * prev;
-            const real* vb = w->pvel + 3 * i;
-            real dv[3] = {vb[0] - va[0], vb[1] - va[1], vb[2] - va[2]};
-            S += dot3(d, dv) / l;
-        }
-        prev = i;
+        cp[n].pt = i; cp[n].pwi = -1; cp[n].wp = 0; cp[n].body = c->pts[i].body; cp[n].wlen = 0.0;
+        for (int d = 0; d < 3; ++d) { cp[n].P[d] = w->ppos[3 * i + d]; cp[n].V[d] = w->pvel[3 * i + d]; }
+        ++n;
+    }
+    if (c->mus_pw_count[im] > 0) n = apply_wraps(c, w, im, cp, n);
+    return n;
+}
+
+/* GeometryPath length and lengthening speed over the current path: the
+ * speed sums the relative velocity of consecutive points along their chord,
+ * tangent points included (PathPoint::calcSpeedBetween on every segment). */
+static void muscle_length_speed(const orc_ctx* c, const dae_ws* w, const cpoint* cp, int n, real* len,
+        real* spd) {
+    (void)c; (void)w;
+    real L = 0.0, S = 0.0;
+    for (int k = 1; k < n; ++k) {
+        const real* a = cp[k - 1].P;
+        const real* b = cp[k].P;
+        real d[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]};
+        real l = sqrt(dot3(d, d));
+        if (cp[k].pt < 0 && cp[k - 1].pt < 0 && cp[k].pwi == cp[k - 1].pwi) L += cp[k].wlen;
+        else L += l;
+        const real* va = cp[k - 1].V;
+        const real* vb = cp[k].V;
+        real dv[3] = {vb[0] - va[0], vb[1] - va[1], vb[2] - va[2]};
+        S += dot3(d, dv) / l;
     }
     *len = L;
     *spd = S;
@@ -1584,6 +1864,20 @@ static void apply_point_force(const orc_ctx* c, dae_ws* w, const real* q, int i,
             w->tau[F->coord] += g;
         }
     }
+}
+
+/* Point force at a current-path entry: a path point as above, a tangent
+ * point as a force at that station of the wrap object's body. */
+static void apply_cpoint_force(const orc_ctx* c, dae_ws* w, const real* q, const cpoint* A, const real* Fp) {
+    if (A->pt >= 0) {
+        apply_point_force(c, w, q, A->pt, Fp);
+        return;
+    }
+    if (A->body < 0) return;
+    int bs = A->body + 1;
+    real t[3];
+    cross(A->P, Fp, t);
+    for (int d = 0; d < 3; ++d) { w->F[bs].w[d] -= t[d]; w->F[bs].v[d] -= Fp[d]; }
 }
 
 /* The explicit per-point DAE (MocoCasOCProblem::calcMultibodySystemExplicit,
@@ -1636,7 +1930,7 @@ static void eval_dae_full(const orc_ctx* c, dae_ws* w, real time, const real* x,
 static void kc_outputs(const orc_ctx* c, const real* q, const real* u, const real* udot,
         const real* ctrl, real* out) {
     int NKC = c->NKC;
-    if (!NKC) return;
+    if (!c->NK && !c->NSL) return;   /* prescribed kinematics: multipliers only */
     real* e = out + c->OKC;
     const real* gam = ctrl + c->NC + c->NDV + c->NM;
     real* qc = c->NSL ? out + c->OQC : NULL;
@@ -1741,7 +2035,9 @@ static void eval_dae_full(const orc_ctx* c, dae_ws* w, real time, const real* x,
     for (int im = 0; im < Mo->nmuscles; ++im) {
         const mh_muscle* mu = &c->mus[im];
         real L, V;
-        muscle_length_speed(c, w, im, &L, &V);
+        int ncp = current_path(c, w, im, w->cp);
+        muscle_length_speed(c, w, w->cp, ncp, &L, &V);
+        (void)mu;
         real e = ctrl[c->mus_control[im]];
         int sa = c->mus_act_state[im], sf = c->mus_ftn_state[im];
         real a = sa >= 0 ? x[sa] : e;
@@ -1753,21 +2049,19 @@ static void eval_dae_full(const orc_ctx* c, dae_ws* w, real time, const real* x,
         if (sa >= 0) zdot[sa - 2 * NQ] = adot;
         if (sf >= 0) zdot[sf - 2 * NQ] = ftdot;
         if (id >= 0) out[NQ + c->NZ + (id - c->NACC)] = resid;
-        /* Tension along each segment of the current path. */
-        int prev = -1;
-        for (int i = mu->point_begin; i < mu->point_begin + mu->point_count; ++i) {
-            if (!w->pact[i]) continue;
-            if (prev >= 0) {
-                const real* pa = w->ppos + 3 * prev;
-                const real* pb = w->ppos + 3 * i;
-                real d[3] = {pb[0] - pa[0], pb[1] - pa[1], pb[2] - pa[2]};
-                real l = sqrt(dot3(d, d));
-                real Fa[3], Fb[3];
-                for (int k = 0; k < 3; ++k) { Fa[k] = T * d[k] / l; Fb[k] = -Fa[k]; }
-                apply_point_force(c, w, q, prev, Fa);
-                apply_point_force(c, w, q, i, Fb);
-            }
-            prev = i;
+        /* Tension along each segment of the current path
+         * (GeometryPath::addInEquivalentForces); the surface part of a wrap
+         * joins two points of one body and applies nothing. */
+        for (int k = 1; k < ncp; ++k) {
+            const cpoint* A = &w->cp[k - 1];
+            const cpoint* B = &w->cp[k];
+            if (A->pt < 0 && B->pt < 0 && A->pwi == B->pwi) continue;
+            real d[3] = {B->P[0] - A->P[0], B->P[1] - A->P[1], B->P[2] - A->P[2]};
+            real l = sqrt(dot3(d, d));
+            real Fa[3], Fb[3];
+            for (int j = 0; j < 3; ++j) { Fa[j] = T * d[j] / l; Fb[j] = -Fa[j]; }
+            apply_cpoint_force(c, w, q, A, Fa);
+            apply_cpoint_force(c, w, q, B, Fb);
         }
     }
     /* External forces (ExternalForce, ground-expressed force and point). */
@@ -1862,7 +2156,27 @@ int orc_muscle_length_speed(orc_ctx* c, int im, const double* q, const double* u
     ws_alloc(c, &w);
     kinematics(c, q, u, NULL, &w);
     path_points(c, q, u, &w);
-    muscle_length_speed(c, &w, im, &out[0], &out[1]);
+    int n = current_path(c, &w, im, w.cp);
+    muscle_length_speed(c, &w, w.cp, n, &out[0], &out[1]);
+    ws_free(&w);
+    return MH_OK;
+}
+
+/* The current path of muscle im at (q, u): *n entries of [x, y, z, kind]
+ * in ground (kind: path point index >= 0, or -1 / -2 for a wrap's first /
+ * second tangent point); at most cap entries are written. */
+int orc_muscle_path(orc_ctx* c, int im, const double* q, const double* u, int cap, int* n, double* pts) {
+    if (im < 0 || im >= c->P.model.nmuscles) return fail(MH_ERR_INVALID, "bad muscle");
+    dae_ws w;
+    ws_alloc(c, &w);
+    kinematics(c, q, u, NULL, &w);
+    path_points(c, q, u, &w);
+    int m = current_path(c, &w, im, w.cp);
+    *n = m;
+    for (int k = 0; k < m && k < cap; ++k) {
+        for (int d = 0; d < 3; ++d) pts[4 * k + d] = w.cp[k].P[d];
+        pts[4 * k + 3] = w.cp[k].pt >= 0 ? (double)w.cp[k].pt : -(double)w.cp[k].wp;
+    }
     ws_free(&w);
     return MH_OK;
 }

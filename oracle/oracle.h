@@ -73,6 +73,10 @@ double orc_dgf_curve(const mh_muscle* muscle, int which, double x);
  * probes at a state (q,u): out = [length, speed] for muscle im. */
 int orc_muscle_length_speed(orc_ctx* ctx, int im, const double* q,
         const double* u, double* out);
+/* The muscle's current path (points and wrap tangent points) in ground:
+ * *n entries of [x, y, z, kind], kind = path point index or -1 / -2. */
+int orc_muscle_path(orc_ctx* ctx, int im, const double* q, const double* u, int cap, int* n,
+        double* pts);
 /* Evaluate a model function (joint axis / moving point) and derivatives. */
 int orc_eval_function(orc_ctx* ctx, int ifn, double q, double* out3);
 /* The callback sparsity behind the structure (mh_get_callback_sparsity). */

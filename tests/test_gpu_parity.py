@@ -150,6 +150,25 @@ CASES = {
     "coupled_pendulum_trap_implicit": lambda: configs.double_pendulum_coupled(10, "trapezoidal", "implicit"),
     "coupled_pendulum_noderiv_hs": lambda: configs.double_pendulum_coupled(
         10, enforce_constraint_derivatives=False),
+    # muscle wrapping over a WrapCylinder, unconstrained and
+    # quadrant-constrained, both dynamics modes, compliant tendon
+    "wrapped_pendulum": lambda: configs.wrapped_pendulum(20),
+    "wrapped_pendulum_trap_implicit_neg_y": lambda: configs.wrapped_pendulum(
+        12, "trapezoidal", "implicit", quadrant="-y"),
+    "wrapped_pendulum_compliant_central_pos_y": lambda: _central(configs.wrapped_pendulum(
+        10, tendon_compliance=True, quadrant="+y")),
+    # Rajagopal 2016: the reference's MocoInverse test model
+    # (18 muscles, 21 coordinates, patellofemoral coupler multipliers with
+    # prescribed kinematics, implicit tendons, endpoint rows), with its
+    # PathWraps kept (16 WrapCylinders, two per gastrocnemius), and the
+    # 80-muscle configs[3] model (explicit, couplers with derivatives,
+    # velocity-correction slacks), with and without its 46 PathWraps
+    "rajagopal18_inverse": lambda: configs.rajagopal18_inverse(11, sparsity="none"),
+    "rajagopal18_inverse_sparse": lambda: _physiological_guess(configs.rajagopal18_inverse(4)),
+    "rajagopal18_inverse_wrapped": lambda: configs.rajagopal18_inverse(3, sparsity="none",
+                                                                      keep_path_wraps=True),
+    "rajagopal80": lambda: configs.rajagopal80(3),
+    "rajagopal80_wrapped_trap": lambda: _trap(configs.rajagopal80(2, keep_path_wraps=True)),
 }
 
 
@@ -355,16 +374,25 @@ def _grid(nlp):
 _WALK = {}
 
 
-def _walking_reference():
-    if not _WALK:
+def _walking_reference(model=None):
+    """Coordinate trajectories keyed by value path: the gait10dof18musc state
+    reference, or for the Rajagopal models (OpenSim model name
+    subject_scale_walk) their filtered walking coordinates."""
+    raja = getattr(model, "name", "") == "subject_scale_walk"
+    key = "raja" if raja else "gait"
+    if key not in _WALK:
         import json
         import os
         from mocohip import configs as _c
-        with open(os.path.join(_c.DATA, "walk_gait1018_state_reference.json")) as fh:
-            d = json.load(fh)
-        _WALK["time"] = np.asarray(d["time"])
-        _WALK.update({k: np.asarray(v) for k, v in d["columns"].items()})
-    return _WALK
+        if raja:
+            kin = _c._walk_armless_kinematics(model)
+            d = {"time": np.asarray(kin.times), **{k: np.asarray(v) for k, v in kin.columns.items()}}
+        else:
+            with open(os.path.join(_c.DATA, "walk_gait1018_state_reference.json")) as fh:
+                j = json.load(fh)
+            d = {"time": np.asarray(j["time"]), **{k: np.asarray(v) for k, v in j["columns"].items()}}
+        _WALK[key] = d
+    return _WALK[key]
 
 
 def physiological_iterate(nlp, seed=0):
@@ -380,7 +408,7 @@ def physiological_iterate(nlp, seed=0):
     # gait models: coordinates and speeds near the reference walking motion
     # (walk_gait1018_state_reference, +-2 %), where every muscle path is in
     # its physiological range
-    ref = _walking_reference()
+    ref = _walking_reference(getattr(nlp.rep.problem, "model", None))
     tk = _lanes.oracle_times(nlp, x)
     for i, n in enumerate(nlp.rep.state_names):
         base = n[:-len("/speed")] + "/value" if n.endswith("/speed") else n
@@ -781,7 +809,9 @@ def _tight_bound(gpu, ref, x, J0, Y, Y0, h_fd):
                                   "gait_rigid_central", "gait_compliant_central", "gait_rigid_implicit",
                                   "gait_rigid_pathcon", "gait_implicit_tendon", "gait_inverse",
                                   "gait_inverse_random", "gait_rigid_nointerp_trap", "coupled_pendulum",
-                                  "coupled_pendulum_implicit"])
+                                  "coupled_pendulum_implicit", "wrapped_pendulum",
+                                  "wrapped_pendulum_trap_implicit_neg_y", "rajagopal18_inverse",
+                                  "rajagopal18_inverse_wrapped", "rajagopal80"])
 def test_jacobian_tight_bound(name):
     """End to end at h_fd = 1e-4 (CasADi-style quotients of the same
     callbacks): |J_gpu - J_oracle| <= 1e-8 |J| + 4 dY_i (h_i + 1) / h_fd
@@ -844,6 +874,7 @@ SIZES = {
     "gait_N200": lambda: configs.gait10dof18musc(200),          # configs[2], the bench workload
     "gait_N400": lambda: configs.gait10dof18musc(400),          # the north-star size
     "inverse_N125": lambda: configs.gait10dof18musc_inverse(125),  # configs[4]: MocoInverse, mesh 0.02 s
+    "rajagopal80_N400": lambda: configs.rajagopal80(400),       # configs[3]: 80 muscles, 41 M nonzeros
 }
 
 

@@ -1281,3 +1281,161 @@ def test_global_seed_jacobian_is_columnwise_fd_of_g(case):
     # drives the DAE to ~1e5)
     Jc = cb.eval_jac_g(x)
     assert np.abs(J - Jc).max() <= 1e-3 * (np.abs(Jc).max() + 1.0)
+
+
+# ---------------------------------------------------------------------------
+# Rajagopal 2016: the reference's converged MocoInverse of the
+# 18-muscle model pins multibody dynamics of the 21-coordinate CustomJoint
+# model, the patellofemoral couplers' multipliers with prescribed
+# kinematics, DGF implicit tendons and the muscle paths
+# ---------------------------------------------------------------------------
+def _rajagopal18_golden_iterate(nlp, rep):
+    d = np.load(os.path.join(os.path.dirname(__file__), "golden",
+                             "std_testMocoInverse_subject_18musc_solution.npz"))
+    labels, data = list(d["labels"]), d["data"]
+    col = {l: i for i, l in enumerate(labels)}
+    G, NS, NC, NDV, NM = nlp.G, nlp.NS, nlp.NC, nlp.NDV, 2
+    assert data.shape[0] == G
+    mult = [l for l in labels if l.startswith("lambda")]
+    der = [l for l in labels if "implicitderiv" in l]
+    assert len(mult) == NM and len(der) == NDV
+    blocks = [(rep.state_names, NS), (rep.control_names, NC), (mult, NM), (der, NDV)]
+    x = [data[0, 0], data[-1, 0]]
+    for names, w in blocks:
+        x += [data[k, col[n]] for k in range(G) for n in names]
+    return np.array(x), labels
+
+
+def _rajagopal18_residuals(keep_path_wraps=False, shift=None):
+    st = configs.rajagopal18_inverse(keep_path_wraps=keep_path_wraps)
+    if shift is not None:
+        mu = [m for m in st.problem.model.muscles if m.name == shift][0]
+        mu.points[0].loc = tuple(np.asarray(mu.points[0].loc, float) + [0.001, 0.0, 0.0])
+    rep = st.problem.create_rep()
+    nlp = OracleNLP(rep, st.solver.options())
+    x, labels = _rajagopal18_golden_iterate(nlp, rep)
+    g = nlp.eval_g(x)
+    NEP, N, NQ, NAR = 18, 11, rep.nq, rep.num_aux_residuals
+    rpi = 2 * (NQ + NAR) + 2 * nlp.NS
+    assert len(g) == NEP + N * rpi + NQ + NAR
+    gi = g[NEP:NEP + N * rpi].reshape(N, rpi)
+    res = np.concatenate([gi[:, :2 * (NQ + NAR)].reshape(N, 2, NQ + NAR).reshape(-1, NQ + NAR),
+                          g[NEP + N * rpi:][None, :]])
+    return g[:NEP], res[:, :NQ], res[:, NQ:], gi[:, 2 * (NQ + NAR):], nlp, rep
+
+
+def test_rajagopal18_inverse_layout():
+    """testMocoInverse.cpp:118-147 on the Rajagopal 18-muscle model: 21
+    coordinates after welding subtalar / mtp, 28 states (18 activations, 10
+    implicit tendon forces), 33 controls, 10 tendon-force derivatives, 2
+    coupler multipliers per grid point and no kinematic rows or slacks with
+    prescribed kinematics (CasOCProblem.h:508-521), HS N = 11, 18 endpoint
+    rows first (MocoInitialActivationGoal), no control interpolation."""
+    st = configs.rajagopal18_inverse()
+    rep = st.problem.create_rep()
+    nlp = OracleNLP(rep, st.solver.options())
+    assert (rep.nq, nlp.NS, nlp.NC, nlp.NDV, rep.num_kinematic_constraints) == (21, 28, 33, 10, 2)
+    G = 23
+    assert nlp.n == 2 + (28 + 33 + 2 + 10) * G
+    assert nlp.m == 18 + 11 * (2 * (21 + 10) + 2 * 28) + (21 + 10)
+    d = np.load(os.path.join(os.path.dirname(__file__), "golden",
+                             "std_testMocoInverse_subject_18musc_solution.npz"))
+    hdr = dict(h.split("=", 1) for h in d["header"])
+    assert (int(hdr["num_states"]) - 2 * rep.nq, int(hdr["num_controls"]), int(hdr["num_multipliers"]),
+            int(hdr["num_derivatives"]), int(hdr["num_slacks"])) == (28, 33, 2, 10, 0)
+
+
+def test_rajagopal18_inverse_golden_solution():
+    """The reference's converged iterate
+    (Moco/Tests/std_testMocoInverse_subject_18musc_solution.sto, MocoInverse
+    constraint tolerance 1e-3) satisfies our g: every defect and endpoint
+    row, the 10 implicit tendon equilibrium residuals within 0.03 N
+    (Fmax 2-10 kN), the 21 multibody residuals within 1.5 N / N m (GRFs up
+    to ~1 kN; the largest are the pelvis rows, from the kinematics and GRF
+    splines); the patella rows vanish with the golden multipliers.
+    Sensitivity: the Millard muscles' 16 PathWraps kept (which
+    DeGrooteFregly2016Muscle::replaceMuscles drops,
+    DeGrooteFregly2016Muscle.cpp:1007-1020) or one path point moved by
+    1 mm is far outside these bounds."""
+    ep, mb, aux, defects, nlp, rep = _rajagopal18_residuals()
+    assert np.abs(ep).max() == 0.0
+    assert np.abs(defects).max() < 1e-3   # the solve's constraint tolerance
+    assert np.abs(aux).max() < 0.03, np.abs(aux).max(0)
+    assert np.abs(mb).max() < 1.5, np.abs(mb).max(0)
+    qn = [c.name for c in rep.problem.model.coordinates()]
+    betas = [qn.index(b) for b in ("knee_angle_r_beta", "knee_angle_l_beta")]
+    assert np.abs(mb[:, betas]).max() < 1e-4
+    # the multipliers' sign convention (-G^T lambda applied) is what zeroes them
+    x, _ = _rajagopal18_golden_iterate(nlp, rep)
+    G, NS, NC = nlp.G, nlp.NS, nlp.NC
+    o = 2 + (NS + NC) * G
+    x[o:o + 2 * G] *= -1.0
+    g = nlp.eval_g(x)
+    NQ, NAR = rep.nq, rep.num_aux_residuals
+    rpi = 2 * (NQ + NAR) + 2 * NS
+    gb = g[18:18 + 11 * rpi].reshape(11, rpi)[:, :NQ]
+    assert np.abs(gb[:, betas]).max() > 1.0
+    _, mbw, auxw, _, _, _ = _rajagopal18_residuals(keep_path_wraps=True)
+    assert max(np.abs(mbw).max(), np.abs(auxw).max()) > 20.0
+    _, _, auxs, _, _, _ = _rajagopal18_residuals(shift="vas_int_r")
+    assert np.abs(auxs).max() > 0.3
+
+
+def test_wrap_cylinder_geometry():
+    """WrapCylinder on wrapped_pendulum: where the straight
+    path crosses the cylinder, the current path is p1 -> r1 -> r2 -> p2 with
+    r1, r2 on the surface, p1 r1 and r2 p2 tangent to it, and a length equal
+    to the shortest path around the cylinder computed independently
+    (tangent lengths sqrt(d^2 - R^2), the arc between the tangent points,
+    the axial rise over the unrolled length); the short way unconstrained,
+    the constrained side with a quadrant; no wrap where the straight path
+    misses (unconstrained) or passes on the constrained side; the speed is
+    the path length's time derivative (cylinder fixed with the origin)."""
+    import ctypes as C
+    from mocohip import abi
+    lib = abi.load_oracle()
+    R = 0.1
+
+    def shortest(a, b, sigma):
+        da, db = np.hypot(*a[:2]), np.hypot(*b[:2])
+        ang = ((math.atan2(b[1], b[0]) - math.atan2(a[1], a[0])) * sigma) % (2 * math.pi)
+        arc = ang - math.acos(R / da) - math.acos(R / db)
+        Lxy = math.sqrt(da * da - R * R) + R * arc + math.sqrt(db * db - R * R)
+        return math.hypot(Lxy, b[2] - a[2])
+
+    for quad in ("all", "+y", "-y"):
+        st = configs.wrapped_pendulum(quadrant=quad)
+        nlp = OracleNLP(st.problem.create_rep(), st.solver.options())
+        nwrap = 0
+        for q0 in np.linspace(-1.4, 1.4, 15):
+            q, u = np.array([q0]), np.array([0.3])
+            pts, n, out = np.zeros(40), C.c_int(), np.zeros(2)
+            assert lib.orc_muscle_path(nlp.ctx, 0, abi.dptr(q), abi.dptr(u), 10, C.byref(n), abi.dptr(pts)) == 0
+            assert lib.orc_muscle_length_speed(nlp.ctx, 0, abi.dptr(q), abi.dptr(u), abi.dptr(out)) == 0
+            P = pts[:4 * n.value].reshape(-1, 4)
+            a, b = P[0, :3], P[-1, :3]
+            cr = a[0] * b[1] - a[1] * b[0]
+            short = 1.0 if cr >= 0 else -1.0
+            if n.value == 2:
+                assert out[0] == pytest.approx(np.linalg.norm(b - a), rel=1e-14)
+                continue
+            nwrap += 1
+            assert n.value == 4 and list(P[1:3, 3]) == [-1.0, -2.0]
+            for r, p in ((P[1, :3], a), (P[2, :3], b)):
+                assert np.hypot(*r[:2]) == pytest.approx(R, rel=1e-13)
+                assert abs(np.dot(p[:2] - r[:2], r[:2])) < 1e-15
+            sides = [short] if quad == "all" else [short, -short]
+            Ls = [shortest(a, b, s) for s in sides]
+            assert min(abs(out[0] - L) for L in Ls) < 1e-13
+            if quad == "all":
+                assert out[0] == pytest.approx(Ls[0], abs=1e-13)
+            # constrained: the wrap midpoint direction lies on the quadrant's side
+            mid = P[1, :2] + P[2, :2]
+            if quad != "all" and np.linalg.norm(mid) > 1e-9:
+                assert np.sign(mid[1]) == (1 if quad == "+y" else -1)
+            h = 1e-6
+            Lp, Lm = np.zeros(2), np.zeros(2)
+            lib.orc_muscle_length_speed(nlp.ctx, 0, abi.dptr(q + h), abi.dptr(u), abi.dptr(Lp))
+            lib.orc_muscle_length_speed(nlp.ctx, 0, abi.dptr(q - h), abi.dptr(u), abi.dptr(Lm))
+            assert out[1] == pytest.approx((Lp[0] - Lm[0]) / (2 * h) * u[0], rel=1e-6, abs=1e-9)
+        assert nwrap >= 6

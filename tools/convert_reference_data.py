@@ -11,7 +11,13 @@ Inputs (all under /root/reference, read as data):
   Moco/Tests/std_testMocoTrackGait10dof18musc_solution.sto (golden solution)
   Moco/Tests/std_testMocoInverse_subject_18musc_solution.sto (MocoInverse
       golden solution: its initial row pins the initial-activation endpoint
-      constraint, MocoInverse.cpp:93)
+      constraint, MocoInverse.cpp:93; the whole solution pins the Rajagopal
+      18-muscle model's wrapping, couplers and dynamics at solution level)
+  Moco/Tests/subject_walk_armless_18musc.osim, subject_walk_armless_coordinates.mot,
+      subject_walk_armless_grfs.mot, subject_walk_armless_external_loads.xml
+      (testMocoInverse.cpp:118-147)
+  Moco/Examples/C++/example3DWalking/subject_walk_armless.osim (80 muscles,
+      BASELINE configs[3])
 """
 import json
 import math
@@ -94,6 +100,46 @@ def main():
                         excitation=np.array([data[0, col[m]] for m in mus]),
                         activation=np.array([data[0, col[m + "/activation"]] for m in mus]),
                         time=data[0, 0],
+                        header=np.array([f"{k}={v}" for k, v in hdr.items()]))
+    # Rajagopal 2016 models (SURVEY §8 X1 / configs[3], and the MocoInverse
+    # 18-muscle test model with its golden solution), kinematics, GRFs
+    raja = [("rajagopal18.json", "Moco/Tests/subject_walk_armless_18musc.osim"),
+            ("rajagopal80.json", "Moco/Examples/C++/example3DWalking/subject_walk_armless.osim")]
+    for out, src in raja:
+        # the models as written (PathWrapSets kept on the muscles); the
+        # configs drop them where replaceMuscles does (configs._replaced)
+        with open(os.path.join(DATA, out), "w") as fh:
+            json.dump(model_to_dict(read_osim(os.path.join(REF, src), keep_path_wraps=True)), fh)
+    labels, data, hdr = read_storage(os.path.join(REF, "Moco/Tests/subject_walk_armless_coordinates.mot"))
+    r18 = read_osim(os.path.join(REF, "Moco/Tests/subject_walk_armless_18musc.osim"))
+    rot = {c.name for j in r18.joints for c in j.coordinates if c.motion_type == "rotational"}
+    in_deg = hdr.get("inDegrees", "no").lower() == "yes"
+    cols = {}
+    for i, l in enumerate(labels):
+        if i == 0:
+            continue
+        v = data[:, i]
+        if in_deg and l in rot:     # TableProcessor::processAndConvertToRadians
+            v = v * math.pi / 180.0
+        cols[l] = v.tolist()
+    with open(os.path.join(DATA, "subject_walk_armless_coordinates.json"), "w") as fh:
+        json.dump({"time": data[:, 0].tolist(), "columns": cols}, fh)
+    labels, data, hdr = read_storage(os.path.join(REF, "Moco/Tests/subject_walk_armless_grfs.mot"))
+    xml = ET.parse(os.path.join(REF, "Moco/Tests/subject_walk_armless_external_loads.xml")).getroot()
+    forces = []
+    for ef in xml.iter("ExternalForce"):
+        forces.append({k: ef.findtext(k).strip() for k in (
+            "applied_to_body", "force_expressed_in_body", "point_expressed_in_body",
+            "force_identifier", "point_identifier", "torque_identifier")})
+        forces[-1]["name"] = ef.get("name")
+        forces[-1]["body"] = forces[-1].pop("applied_to_body")
+    with open(os.path.join(DATA, "subject_walk_armless_grf.json"), "w") as fh:
+        json.dump({"labels": labels, "time": data[:, 0].tolist(),
+                   "columns": {l: data[:, i].tolist() for i, l in enumerate(labels) if i > 0},
+                   "external_forces": forces}, fh)
+    labels, data, hdr = read_storage(os.path.join(REF, "Moco/Tests/std_testMocoInverse_subject_18musc_solution.sto"))
+    np.savez_compressed(os.path.join(GOLDEN, "std_testMocoInverse_subject_18musc_solution.npz"),
+                        labels=np.array(labels), data=data,
                         header=np.array([f"{k}={v}" for k, v in hdr.items()]))
     print("wrote", DATA, GOLDEN)
 
