@@ -72,6 +72,10 @@ def parse():
     ap.add_argument("--single-mode", action="store_true",
                     help="measure only the headline (no secondary lines): for profiler runs, so "
                          "that every launch of a kernel has the same shape")
+    ap.add_argument("--config3", type=int, default=400,
+                    help="mesh intervals of the configs[3] Rajagopal 80-muscle line (0: skip)")
+    ap.add_argument("--config", choices=["gait", "rajagopal80"], default="gait",
+                    help="--multi mesh workload: configs[2] gait10dof18musc or configs[3] Rajagopal")
     ap.add_argument("--inverse-batch", type=int, default=8)
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--batch-only", action="store_true",
@@ -352,6 +356,41 @@ def cpu_baseline(rep, opts, x, budget_s, threads):
                       f"{os.environ.get('OMP_NUM_THREADS', '?')} threads)"}
 
 
+def config3_line(cx, args):
+    """configs[3]: the Rajagopal 80-muscle NLP (configs.rajagopal80: 18
+    coordinates, 80 DGF muscles, patellofemoral couplers with derivatives and
+    velocity-correction slacks, explicit) at N = --config3 on this GPU:
+    eval_g + eval_jac_g calls/s on device pointers, the per-launch times of
+    its two eval_jac_g kernels (the generic device interpreter, one lane per
+    DAE; then the transcription), and a bounded CPU-oracle sample."""
+    from mocohip import configs
+    st = configs.rajagopal80(args.config3, fd_scheme=args.fd)
+    nlp = make_nlp(cx, st, blocking=args.blocking)
+    x = track_iterate(nlp, cx.rank)
+    sep, fused, (xd, gd, vd) = device_steps(cx, nlp, x)
+    k, el = measure(cx, sep, args, k=max(5, args.steps // 100), w=3)
+    dae_ms, tr_ms = nlp.time_stages(xd.data_ptr(), kind=1, reps=5)
+    alg_bytes = 8 * (nlp.n + nlp.nnz)
+    gbs = alg_bytes / (tr_ms * 1e-3) / 1e9
+    out = {"value": round(k * cx.world / el, 3), "unit": "calls/s", "ms_per_step": round(1e3 * el / k, 4),
+           "steps": k, "mesh_intervals": args.config3, "n": nlp.n, "m": nlp.m, "nnz_jac": nlp.nnz,
+           "backend": nlp.backend()[0],
+           "kernels_ms": {"dae (k_eval, generic interpreter)": round(dae_ms, 4),
+                          "transcription": round(tr_ms, 4)},
+           "transcription_roofline": {"bound": "hbm", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS,
+                                      "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 5),
+                                      "algorithmic_bytes": alg_bytes},
+           "workload": "configs[3] Rajagopal 80-muscle gait NLP (example3DWalking muscle-driven "
+                       "problem, DGF rigid tendons, patellofemoral couplers), HS, forward FD, "
+                       "block-dense callback sparsity, 1 GPU"}
+    if cx.world == 1 and cx.rank == 0 and not args.no_cpu_baseline:
+        box = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+        out["cpu_baseline"] = cpu_baseline(nlp.rep, st.solver.options(), x, args.cpu_baseline_seconds,
+                                           max(1, min(box, os.cpu_count() or 1)))
+    nlp.close()
+    return out
+
+
 def mesh_main(cx, args):
     """--multi mesh: one NLP, sharded; host-inclusive strong scaling."""
     from mocohip import configs
@@ -359,7 +398,9 @@ def mesh_main(cx, args):
     torch, dist = cx.torch, cx.dist
     N = args.intervals
     ib, ie = interval_shard(N, cx.rank, cx.world)
-    st = configs.gait10dof18musc(N, fd_scheme=args.fd)
+    build = ((lambda: configs.rajagopal80(N, fd_scheme=args.fd)) if args.config == "rajagopal80"
+             else (lambda: configs.gait10dof18musc(N, fd_scheme=args.fd)))
+    st = build()
     nlp = make_nlp(cx, st, ib, ie, blocking=False)
     x = track_iterate(nlp, 0)
     sep, fused, (xd, gd, vd) = device_steps(cx, nlp, x)
@@ -381,19 +422,21 @@ def mesh_main(cx, args):
     ok = None
     if cx.rank == 0:
         # the reassembled host vectors against one unsharded evaluation
-        full = make_nlp(cx, configs.gait10dof18musc(N, fd_scheme=args.fd), blocking=True)
+        full = make_nlp(cx, build(), blocking=True)
         ok = bool(np.array_equal(hg.full_g(), full.eval_g(x))
                   and np.array_equal(hg.full_values(), full.eval_jac_g(x)))
         full.close()
     barrier()
     hg.close(unlink=cx.rank == 0)
     if cx.rank == 0:
-        line = {"metric": "NLP eval_g+eval_jac_g calls/sec (gait10dof18musc)",
+        wl = ("Rajagopal 80-muscle gait NLP (configs[3])" if args.config == "rajagopal80"
+              else "MocoTrack gait10dof18musc DGF rigid tendon (configs[2])")
+        line = {"metric": "NLP eval_g+eval_jac_g calls/sec (gait10dof18musc)" if args.config == "gait"
+                          else "NLP eval_g+eval_jac_g calls/sec (Rajagopal 80-muscle)",
                 "value": round(k / el, 3), "unit": "calls/s", "n_gpus": cx.world, "steps": k,
                 "warmup": args.warmup, "ms_per_step": round(1e3 * el / k, 5), "higher_is_better": True,
                 "scaling": "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-                "config": {"workload": "MocoTrack gait10dof18musc DGF rigid tendon (configs[2]), one NLP "
-                                       "sharded by mesh interval for one host IPOPT",
+                "config": {"workload": wl + ", one NLP sharded by mesh interval for one host IPOPT",
                            "mesh_intervals": N, "n": nlp.n, "m": nlp.m, "nnz_jac": nlp.nnz,
                            "fd": args.fd, "mode": args.mode,
                            "parallelism": f"mesh-shard{cx.world}: RCCL broadcast of x + per-rank DMA "
@@ -485,6 +528,8 @@ def main():
         if args.batch > 1:
             extra["batch"] = batch_throughput(
                 cx, lambda: configs.gait10dof18musc(N, fd_scheme=args.fd), track_iterate, args, args.batch)
+        if args.config3 > 0:
+            extra["config3"] = config3_line(cx, args)
         if args.inverse_batch > 0:
             # MocoTool mesh_interval 0.02 s: ceil((2.499 - 0.001) / 0.02) = 125
             # intervals (MocoTool.cpp:27,68-69)

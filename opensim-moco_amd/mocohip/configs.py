@@ -289,6 +289,9 @@ def gait10dof18musc_inverse(num_mesh_intervals: int = 25, fd_scheme: str = "forw
 def wrapped_pendulum(num_mesh_intervals: int = 20, scheme: str = "hermite-simpson",
                      dynamics: str = "explicit", tendon_compliance: bool = False,
                      quadrant: str = "all") -> MocoStudy:
+    # (compliant tendon: the angle range over which the path wraps, with
+    # tendon slack and fiber lengths that keep the muscle near its optimal
+    # fiber length there, so the explicit tendon dynamics stay regular)
     """A one-link pendulum (ModelFactory::createNLinkPendulum(1)) driven by a
     DeGrooteFregly2016 muscle whose path wraps over a WrapCylinder about the
     pin axis (the GeometryPath / WrapCylinder geometry of SURVEY §8 A9 on a
@@ -298,16 +301,19 @@ def wrapped_pendulum(num_mesh_intervals: int = 20, scheme: str = "hermite-simpso
     m.add_wrap(WrapCylinder("pin_cyl", "ground", 0.1, 0.2, (0.0, 0.0, 0.0), (0.0, 0.0, 0.0), quadrant))
     mu = DeGrooteFregly2016Muscle("flexor", [PathPoint("ground", (-0.3, 0.15, 0.05), name="origin"),
                                              PathPoint("b0", (-0.7, 0.12, -0.04), name="insertion")],
-                                  max_isometric_force=200.0, optimal_fiber_length=0.2,
-                                  tendon_slack_length=0.25, pennation_angle_at_optimal=0.1,
+                                  max_isometric_force=200.0,
+                                  optimal_fiber_length=0.22 if tendon_compliance else 0.2,
+                                  tendon_slack_length=0.45 if tendon_compliance else 0.25,
+                                  pennation_angle_at_optimal=0.1,
                                   path_wraps=[("pin_cyl", -1, -1)])
     mu.ignore_tendon_compliance = not tendon_compliance
     m.actuators = [a for a in m.actuators]
     m.add_muscle(mu)
     p = MocoProblem(m)
     p.set_time_bounds(0.0, 1.0)
-    p.set_state_info("/jointset/j0/q0/value", (-1.5, 1.5), 0.5)
-    p.set_state_info("/jointset/j0/q0/speed", (-20, 20), 0)
+    p.set_state_info("/jointset/j0/q0/value", (-1.0, -0.4) if tendon_compliance else (-1.5, 1.5),
+                     -0.7 if tendon_compliance else 0.5)
+    p.set_state_info("/jointset/j0/q0/speed", (-3, 3), 0)
     p.set_control_info("/tau0", (-50, 50))
     p.add_goal(MocoControlGoal())
     s = MocoHipSolver(num_mesh_intervals=num_mesh_intervals, transcription_scheme=scheme,

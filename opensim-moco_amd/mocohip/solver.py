@@ -302,7 +302,10 @@ class _NLPBase:
     @property
     def NK(self) -> int:
         """Kinematic-constraint rows per mesh point (position, velocity and
-        acceleration errors when enforcing constraint derivatives)."""
+        acceleration errors when enforcing constraint derivatives); none with
+        prescribed kinematics (CasOCProblem.h:508-521)."""
+        if getattr(self.rep, "prescribed_kinematics", False):
+            return 0
         return self.NKC * (1 if self.opts.ignore_constraint_derivatives else 3)
 
     @property
@@ -310,7 +313,8 @@ class _NLPBase:
         """Velocity-correction slacks per mesh interval (Hermite-Simpson,
         enforcing derivatives)."""
         return (self.NKC if not self.opts.ignore_constraint_derivatives
-                and self.opts.transcription == abi.MH_HERMITE_SIMPSON else 0)
+                and self.opts.transcription == abi.MH_HERMITE_SIMPSON
+                and not getattr(self.rep, "prescribed_kinematics", False) else 0)
 
     @property
     def NI(self) -> int:
@@ -356,7 +360,7 @@ class _NLPBase:
         """The callback sparsity behind the Jacobian structure: the NO DAE
         outputs then the path equations, rows of W = [time, inputs] flags,
         then the endpoint equations, rows of 2 W flags."""
-        W = 1 + self.NS + self.NC + self.NDV
+        W = 1 + self.NI
         buf = np.zeros((self.NO + self.NPC + 2 * self.NEP) * W, np.uint8)
         self._check(self._fn("get_callback_sparsity")(
             self.ctx, buf.ctypes.data_as(C.POINTER(C.c_uint8)), buf.size))

@@ -65,7 +65,7 @@ def write_tape(rep, opts: abi.mh_options, path: str) -> None:
     if opts.sparsity_pattern:
         # mh_get_callback_sparsity layout: NO DAE outputs and the path
         # equations (W flags each), the endpoint equations (2 W flags each)
-        W = 1 + ns + nc + ndv
+        W = 1 + ns + nc + ndv + (m.nconstraints if presc else 0)   # + multipliers
         nz = ns if presc else ns - 2 * m.nq
         no = m.nq + nz + nar
         pattern = C.string_at(opts.sparsity_pattern, (no + p.npath + 2 * p.nendpoint) * W)
