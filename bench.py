@@ -288,6 +288,47 @@ def roofline(cx, nlp, steps, args, mode):
     return roof
 
 
+def batched_throughput(cx, st_fn, make_x, args, B):
+    """B independent NLPs of the same workload per GPU (different iterates)
+    evaluated through one mh_batch: one k_groups and one k_interval launch
+    per stage for all B, on one stream, driven by one host thread."""
+    from mocohip.solver import HipBatch, HipNLP
+    torch = cx.torch
+    nlps, xs, gs, vs = [], [], [], []
+    for b in range(B):
+        st = st_fn()
+        st.solver.device = cx.local
+        nlp = HipNLP(st.problem.create_rep(), st.solver.options())
+        nlp.set_stream(cx.stream())
+        nlp.set_async(not args.blocking)
+        nlps.append(nlp)
+        xs.append(torch.tensor(make_x(nlp, 1000 + cx.rank * B + b), dtype=torch.float64, device=cx.dev))
+        gs.append(torch.zeros(nlp.m, dtype=torch.float64, device=cx.dev))
+        vs.append(torch.zeros(nlp.nnz, dtype=torch.float64, device=cx.dev))
+    bt = HipBatch(nlps)
+    xp, gp, vp = [t.data_ptr() for t in xs], [t.data_ptr() for t in gs], [t.data_ptr() for t in vs]
+
+    def step():
+        if args.mode == "fused":
+            bt.eval_g_jac_g_device(xp, gp, vp)
+        else:
+            bt.eval_g_device(xp, gp)
+            bt.eval_jac_g_device(xp, vp)
+    k, el = measure(cx, step, args)
+    out = {"nlps_per_gpu": B, "value": round(B * cx.world * k / el, 3), "unit": "calls/s",
+           "mode": args.mode, "layout": "mh_batch: one launch per kernel for all B NLPs, one stream",
+           "backend": nlps[0].backend()[0], "nnz_jac": nlps[0].nnz, "m": nlps[0].m}
+    if args.mode == "separate":
+        def fstep():
+            bt.eval_g_jac_g_device(xp, gp, vp)
+        kf, ef = measure(cx, fstep, args)
+        out["value_fused"] = round(B * cx.world * kf / ef, 3)
+    bt.close()
+    for nlp in nlps:
+        nlp.close()
+    return out
+
+
 def batch_throughput(cx, st_fn, make_x, args, B):
     """B independent NLPs of the same workload per GPU (different iterates),
     each on its own HIP stream and driven by its own host thread (ctypes
@@ -458,6 +499,8 @@ def main():
     if args.batch_only:
         out = batch_throughput(cx, lambda: configs.gait10dof18musc(N, fd_scheme=args.fd), track_iterate,
                                args, args.batch)
+        out["batched"] = batched_throughput(cx, lambda: configs.gait10dof18musc(N, fd_scheme=args.fd),
+                                            track_iterate, args, args.batch)
         out["env"] = {k: os.environ[k] for k in ("GPU_MAX_HW_QUEUES", "MOCOHIP_GRAPHS") if k in os.environ}
         if cx.rank == 0:
             print(json.dumps(out), flush=True)
@@ -528,6 +571,8 @@ def main():
         if args.batch > 1:
             extra["batch"] = batch_throughput(
                 cx, lambda: configs.gait10dof18musc(N, fd_scheme=args.fd), track_iterate, args, args.batch)
+            extra["batched"] = batched_throughput(
+                cx, lambda: configs.gait10dof18musc(N, fd_scheme=args.fd), track_iterate, args, args.batch)
         if args.config3 > 0:
             extra["config3"] = config3_line(cx, args)
         if args.inverse_batch > 0:
@@ -539,6 +584,10 @@ def main():
                                "tendons, reserves, initial-activation endpoint constraints, no control "
                                "interpolation, N=125, forward FD, random sparsity detection")
             extra["inverse_batch"] = inv
+            invb = batched_throughput(cx, lambda: configs.gait10dof18musc_inverse(125), inverse_iterate,
+                                      args, args.inverse_batch)
+            invb["workload"] = inv["workload"]
+            extra["inverse_batched"] = invb
     if cx.rank == 0:
         cpu = cpu1 = None
         if cx.world == 1 and not args.no_cpu_baseline:

@@ -570,6 +570,33 @@ int mh_set_async(mh_ctx* ctx, int on);
 /* Wait for all work enqueued on the context's stream. */
 int mh_synchronize(mh_ctx* ctx);
 
+/* Batches (BASELINE configs[4]: many IPOPT solves of one problem shape per
+ * GPU, e.g. a subject / trial sweep of MocoInverse).  A batch groups 1..16
+ * contexts created from structurally identical problems -- same model
+ * structure (mh_model_hash up to table values), layout, options and
+ * Jacobian template; each keeps its own model data (kinematics tables,
+ * GRFs), iterate and outputs -- and evaluates them with one launch per
+ * kernel instead of one per context (the tropter / CasADi callbacks of
+ * each NLP, IPOPTSolver.cpp:417-447, for B NLPs at once).  Every batch
+ * call takes B device pointers (x[b], g[b], values[b] of context b), runs
+ * on the first context's stream and follows its mh_set_async setting.
+ * Results are identical, bit for bit, to the contexts' own
+ * mh_eval_*_device calls.  Contexts must use the task back end with the
+ * fused interval kernel (generated models; no global-seed Jacobian, no
+ * k_role); MH_ERR_UNSUPPORTED otherwise.  The contexts must outlive the
+ * batch and must not be used concurrently with it. */
+typedef struct mh_batch mh_batch;
+int mh_batch_create(mh_ctx* const* ctxs, int32_t count, mh_batch** out);
+void mh_batch_destroy(mh_batch* batch);
+int mh_batch_eval_g_device(mh_batch* batch, const double* const* x_dev, double* const* g_dev);
+int mh_batch_eval_jac_g_device(mh_batch* batch, const double* const* x_dev, double* const* v_dev);
+int mh_batch_eval_g_jac_g_device(mh_batch* batch, const double* const* x_dev, double* const* g_dev,
+        double* const* v_dev);
+/* global_memory != 0 (default): the batched k_interval reads the group
+ * results from global memory (a third of the LDS, several interval blocks
+ * per CU); 0: stages them in LDS like the per-context kernel. */
+int mh_batch_set_group_results_global(mh_batch* batch, int global_memory);
+
 /* Per-point DAE probe (CasOC::Problem::calcMultibodySystemExplicit /
  * calcMultibodySystemImplicit, CasOCProblem.h:313-332) evaluated on the
  * device for npoints inputs laid out as [time, states(NS), controls(NC)]

@@ -286,10 +286,10 @@ struct Tasks {
 #define MH_IV_STAMP(i)
 
 template <class D>
-__global__ void __launch_bounds__(64) k_groups(DevModel M, Src S, Lanes Ln, Tasks TK,
-        double* __restrict__ T, double* __restrict__ H) {
+__device__ __forceinline__ void groups_body(const DevModel& M, const Src& S, const Lanes& Ln, const Tasks& TK,
+        double* __restrict__ T, double* __restrict__ H, int blk) {
     const int lane = threadIdx.x;
-    const int4 rec = TK.blk[blockIdx.x];   // one scalar load: no dependent table chain
+    const int4 rec = TK.blk[blk];   // one scalar load: no dependent table chain
     const int g = __builtin_amdgcn_readfirstlane(rec.x);
     const int first = __builtin_amdgcn_readfirstlane(rec.y);
     const int n = __builtin_amdgcn_readfirstlane(rec.z);
@@ -324,6 +324,12 @@ __global__ void __launch_bounds__(64) k_groups(DevModel M, Src S, Lanes Ln, Task
         for (int f = 0; f < D::NF; ++f)
             if (f < nf) dst[f] = out[f];
     }
+}
+
+template <class D>
+__global__ void __launch_bounds__(64) k_groups(DevModel M, Src S, Lanes Ln, Tasks TK,
+        double* __restrict__ T, double* __restrict__ H) {
+    groups_body<D>(M, S, Ln, TK, T, H, blockIdx.x);
 }
 
 // Combine: one workgroup per grid point.  The grid point's group results
@@ -896,14 +902,17 @@ __device__ __host__ __forceinline__ uint32_t ct_word(uint32_t off, uint32_t coef
 constexpr int CT_CONST = 4;      // offset of the constants after sTimes
 constexpr int CT_NCONST = 12;
 
-template <class D>
-__global__ void __launch_bounds__(1024) k_interval(DevModel M, Src S, Lanes Ln, Tasks TK, Layout L,
-        Interval I, const TplEntry* __restrict__ tpl, const uint32_t* __restrict__ ctpl,
+// GM: the combine reads the group results straight from global memory (T,
+// H) instead of staging them in LDS -- a third of the LDS, so that several
+// interval blocks share a CU (the batched launches, where many blocks queue);
+// the same arithmetic in the same order, bit for bit.
+template <class D, bool GM>
+__device__ __forceinline__ void interval_body(const DevModel& M, const Src& S, const Lanes& Ln, const Tasks& TK,
+        const Layout& L, const Interval& I, const TplEntry* __restrict__ tpl, const uint32_t* __restrict__ ctpl,
         const int* __restrict__ ctgen, int nctgen,
         const double* __restrict__ T, const double* __restrict__ H, double* __restrict__ g,
-        double* __restrict__ values) {
+        double* __restrict__ values, int il) {
     extern __shared__ double smem[];
-    const int il = blockIdx.x;
     const int i = I.ib + il;
     int k_first, k_last;
     interval_span(I, i, k_first, k_last);
@@ -913,17 +922,17 @@ __global__ void __launch_bounds__(1024) k_interval(DevModel M, Src S, Lanes Ln, 
     double* sY = smem;                       // [npts][NO][stride]
     double* sTimes = sY + npts * ny;         // [npts] (+ pad)
     double* sK = sTimes + CT_CONST;          // compiled-template constants
-    double* sT = sK + CT_NCONST;             // [npts][nt]
-    double* sH = sT + npts * nt;             // [npts][nh]
-    double* sXs = sH + npts * nh;            // [npts][NS] states, [npts][NC] controls,
+    double* sT = sK + CT_NCONST;             // [npts][nt] (GM: none)
+    double* sH = sT + (GM ? 0 : npts * nt);  // [npts][nh] (GM: none)
+    double* sXs = sH + (GM ? 0 : npts * nh); // [npts][NS] states, [npts][NC] controls,
     double* sXc = sXs + npts * L.NS;         // [npts][NDV] accelerations (implicit)
     double* sXd = sXc + npts * L.NC;
     // the interval's points are consecutive local grid points: their T (and
     // H) slabs are one contiguous run each
     const int kl0 = k_first - S.k0;
     if (I.dbg_stop == 7) return;   // diagnostic: the launch floor
-    if (nt > 0) stage_lds<16>(sT, T + (long)kl0 * nt, npts * nt);
-    if (nh > 0) stage_lds<8>(sH, H + (long)kl0 * nh, npts * nh);
+    if (!GM && nt > 0) stage_lds<16>(sT, T + (long)kl0 * nt, npts * nt);
+    if (!GM && nh > 0) stage_lds<8>(sH, H + (long)kl0 * nh, npts * nh);
     stage_lds<1>(sXs, S.x + 2 + (long)k_first * L.NS, npts * L.NS);
     if (L.NC > 0) stage_lds<1>(sXc, S.x + 2 + (long)L.NS * L.G + (long)k_first * L.NC, npts * L.NC);
     if (L.NDV > 0)
@@ -938,8 +947,13 @@ __global__ void __launch_bounds__(1024) k_interval(DevModel M, Src S, Lanes Ln, 
         const double t = lane_time(Ln, S.grid[k_first + p], t0, tf, r, in.pi, in.step);
         if (r == Ln.base) sTimes[p] = t;
         double out[D::NO];
-        const TaskLoadLds<D> TL{lds(sT + p * nt), lds(sH + p * nh), TK.jd, r};
-        D::combine(M, t, in, TL, out);
+        if constexpr (GM) {
+            const TaskLoadGlobal<D> TL{T + (long)(kl0 + p) * nt, H + (long)(kl0 + p) * nh, TK.jd, r};
+            D::combine(M, t, in, TL, out);
+        } else {
+            const TaskLoadLds<D> TL{lds(sT + p * nt), lds(sH + p * nh), TK.jd, r};
+            D::combine(M, t, in, TL, out);
+        }
         lds_double* Yp = lds(sY + p * ny + r);
 #pragma unroll
         for (int o = 0; o < D::NO; ++o) Yp[o * Ln.stride] = out[o];
@@ -1101,6 +1115,70 @@ __global__ void __launch_bounds__(1024) k_interval(DevModel M, Src S, Lanes Ln, 
     }
     if (i == 0 && (I.gh || I.vh))
         endpoint_head(L, Ln, I.E, S.x, g ? I.gh : nullptr, values ? I.vh : nullptr, threadIdx.x, blockDim.x);
+}
+
+template <class D>
+__global__ void __launch_bounds__(1024) k_interval(DevModel M, Src S, Lanes Ln, Tasks TK, Layout L,
+        Interval I, const TplEntry* __restrict__ tpl, const uint32_t* __restrict__ ctpl,
+        const int* __restrict__ ctgen, int nctgen,
+        const double* __restrict__ T, const double* __restrict__ H, double* __restrict__ g,
+        double* __restrict__ values) {
+    interval_body<D, false>(M, S, Ln, TK, L, I, tpl, ctpl, ctgen, nctgen, T, H, g, values, blockIdx.x);
+}
+
+// ------------------------------------------------------------------------
+// Batched launches (mh_batch): B structurally identical NLPs (same model
+// structure, problem layout and template; their own model data, iterate,
+// group-result buffers and outputs) evaluated by ONE k_groups and ONE
+// k_interval launch, blockIdx.y = the NLP.  The per-NLP constants (device
+// model, group-result slabs, path / endpoint tables, grid) live in device
+// memory; the per-call pointers travel as kernel arguments.
+// ------------------------------------------------------------------------
+constexpr int MH_BATCH_MAX = 16;
+struct BatchItem {
+    DevModel M;
+    double* T;
+    double* H;
+    PathEqs P;
+    EndpointEqs E;
+    const double* grid;
+};
+struct BatchPtrs {
+    const double* x[MH_BATCH_MAX];
+    double* g[MH_BATCH_MAX];
+    double* v[MH_BATCH_MAX];
+};
+
+template <class D>
+__global__ void __launch_bounds__(64) kb_groups(const BatchItem* __restrict__ items, BatchPtrs BP, Lanes Ln,
+        Tasks TK, int G, int k0) {
+    const int b = blockIdx.y;
+    const BatchItem& it = items[b];
+    const Src S{BP.x[b], it.grid, nullptr, G, k0};
+    groups_body<D>(it.M, S, Ln, TK, it.T, it.H, blockIdx.x);
+}
+
+template <class D, bool GM>
+__global__ void __launch_bounds__(1024) kb_interval(const BatchItem* __restrict__ items, BatchPtrs BP, Lanes Ln,
+        Tasks TK, Layout L, Interval I0, const TplEntry* __restrict__ tpl, const uint32_t* __restrict__ ctpl,
+        const int* __restrict__ ctgen, int nctgen, int with_g, int with_v, int nep, int nnz_ep) {
+    const int b = blockIdx.y;
+    const BatchItem& it = items[b];
+    const Src S{BP.x[b], it.grid, nullptr, L.G, L.k0};
+    Interval I = I0;
+    I.P = it.P;
+    I.E = it.E;
+    double* g = with_g ? BP.g[b] : nullptr;
+    double* v = with_v ? BP.v[b] : nullptr;
+    // the head (endpoint rows) precedes the intervals' rows (make_interval)
+    I.gh = I.vh = nullptr;
+    if (I.ib == 0 && nep > 0) {
+        I.gh = g;
+        I.vh = v;
+        if (g) g += nep;
+        if (v) v += nnz_ep;
+    }
+    interval_body<D, GM>(it.M, S, Ln, TK, L, I, tpl, ctpl, ctgen, nctgen, it.T, it.H, g, v, blockIdx.x);
 }
 
 // ------------------------------------------------------------------------
@@ -1745,6 +1823,15 @@ inline Interval make_interval(const mh_ctx* c, double*& g, double*& v) {
 // Task tables and T/H buffers for an mh_eval_dae call (mocohip.hip).
 int probe_tasks(mh_ctx* c, const TaskInfo& ti, const Lanes& ln, int np);
 
+// A batch of structurally identical contexts evaluated together (mh_batch_*,
+// include/mocohip.h); built by mh_batch_create (mocohip.hip).
+struct mh_batch {
+    std::vector<mh_ctx*> ctx;
+    int B = 0;
+    BatchItem* d_items = nullptr;   // [B] per-NLP constants
+    bool gm = true;                 // k_interval reads group results from global memory
+};
+
 struct Backend {
     const char* name;
     // one evaluation stage: raw DAE outputs of every lane of c->lanes_g
@@ -1763,6 +1850,9 @@ struct Backend {
     // the base-lane times into d_times, whatever path eval_jac_g takes
     // (mh_debug_jacobian_lanes)
     void (*lanes)(mh_ctx*, const double* x, double* Y);
+    // task back ends: one k_groups + one k_interval launch for every NLP of
+    // a batch (lanes of mode 0/1; g and / or values written per NLP)
+    void (*batch)(mh_batch*, int mode, const BatchPtrs& P, int with_g, int with_v);
 };
 
 template <class D>
@@ -1832,6 +1922,33 @@ template <class D>
 static size_t be_interval_bytes(const mh_ctx* c, int mode) {
     if (mode == 1 && c->use_roles && role_lds<D>(c) <= kMaxLds) return role_lds<D>(c);
     return interval_lds<D>(c, mode ? c->lanes_jac : c->lanes_g, mode ? c->ts_jac : c->ts_g);
+}
+// LDS bytes of k_interval reading the group results from global memory.
+template <class D>
+static size_t interval_lds_gm(const mh_ctx* c, const Lanes& ln) {
+    const size_t npts = c->scheme == MH_HERMITE_SIMPSON ? 3 : 2;
+    return sizeof(double) * (npts * D::NO * ln.stride + CT_CONST + CT_NCONST +
+                             npts * (size_t)(c->NS + c->NC + c->NDV));
+}
+template <class D>
+static void be_batch(mh_batch* bt, int mode, const BatchPtrs& BP, int with_g, int with_v) {
+    mh_ctx* c = bt->ctx[0];
+    const Lanes& ln = mode ? c->lanes_jac : c->lanes_g;
+    const TaskSet& ts = mode ? c->ts_jac : c->ts_g;
+    const unsigned B = (unsigned)bt->B;
+    hipLaunchKernelGGL(kb_groups<D>, dim3((unsigned)ts.nblocks, B), dim3(64), 0, c->stream, bt->d_items, BP, ln,
+            ts.dev, c->G, c->k0);
+    Layout L = make_layout(c, c->k0, c->nk);
+    double *g0 = nullptr, *v0 = nullptr;
+    const Interval I = make_interval(c, g0, v0);
+    const size_t lds = bt->gm ? interval_lds_gm<D>(c, ln) : interval_lds<D>(c, ln, ts);
+    auto kern = bt->gm ? kb_interval<D, true> : kb_interval<D, false>;
+    if (lds > 65536)
+        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    const unsigned threads = with_v ? (unsigned)c->iv_threads : 256u;
+    hipLaunchKernelGGL(kern, dim3((unsigned)(c->ie - c->ib), B), dim3(threads), lds, c->stream, bt->d_items, BP,
+            ln, ts.dev, L, I, c->d_tpl, (mode == 1 && c->use_ctpl) ? c->d_ctpl : nullptr, c->d_ctgen,
+            (int)c->ctgen.size(), with_g, with_v, c->nep, c->nnz_ep);
 }
 template <class D>
 static void be_interval(mh_ctx* c, const double* x, int mode, double* g, double* v) {
@@ -1904,7 +2021,7 @@ static void be_lanes_tasks(mh_ctx* c, const double* x, double* Y) {
 template <class D>
 static constexpr Backend make_backend_lane(const char* name, double flops) {
     return Backend{name, &be_eval_lane<D>, &be_integrand<D>, &be_grad<D>, &be_probe_lane<D>, flops,
-                   nullptr, nullptr, nullptr, &be_lanes_lane<D>};
+                   nullptr, nullptr, nullptr, &be_lanes_lane<D>, nullptr};
 }
 template <class D>
 struct TaskInfoOf {
@@ -1914,7 +2031,8 @@ struct TaskInfoOf {
 template <class D>
 static constexpr Backend make_backend_tasks(const char* name, double flops) {
     return Backend{name, &be_eval_tasks<D>, &be_integrand<D>, &be_grad<D>, &be_probe_tasks<D>, flops,
-                   &TaskInfoOf<D>::value, &be_interval<D>, &be_interval_bytes<D>, &be_lanes_tasks<D>};
+                   &TaskInfoOf<D>::value, &be_interval<D>, &be_interval_bytes<D>, &be_lanes_tasks<D>,
+                   &be_batch<D>};
 }
 
 // Generic device-interpreter back ends (generic.hip), one per size class.

@@ -1959,6 +1959,95 @@ extern "C" int mh_eval_g_jac_g_device(mh_ctx* c, const double* x_dev, double* g_
     return finish(c, true);
 }
 
+// ---- batches (include/mocohip.h mh_batch_*) -------------------------------
+extern "C" int mh_batch_create(mh_ctx* const* ctxs, int32_t count, mh_batch** out) {
+    if (!ctxs || !out || count < 1) return set_err(MH_ERR_INVALID, "null argument or empty batch");
+    if (count > MH_BATCH_MAX) return set_err(MH_ERR_INVALID, "at most %d contexts per batch", MH_BATCH_MAX);
+    *out = nullptr;
+    const mh_ctx* a = ctxs[0];
+    for (int b = 0; b < count; ++b) {
+        const mh_ctx* c = ctxs[b];
+        if (!c) return set_err(MH_ERR_INVALID, "null context %d", b);
+        if (!c->be->batch || !c->use_interval[0] || !c->use_interval[1] || c->jac_seeds || c->use_roles)
+            return set_err(MH_ERR_UNSUPPORTED, "context %d: batches need the task back end with the fused "
+                           "interval kernel (no global seeds, no k_role)", b);
+        // the same problem shape: back end, layout, lanes, tasks, template
+        const bool same = c->be == a->be && c->device == a->device && c->N == a->N && c->G == a->G &&
+                c->ib == a->ib && c->ie == a->ie && c->k0 == a->k0 && c->nk == a->nk &&
+                c->scheme == a->scheme && c->n == a->n && c->m == a->m && c->nnz == a->nnz &&
+                c->nnz_int == a->nnz_int && c->rpi == a->rpi && c->nep == a->nep && c->nnz_ep == a->nnz_ep &&
+                c->fd == a->fd && c->h == a->h && c->NS == a->NS && c->NC == a->NC && c->NDV == a->NDV &&
+                c->NM == a->NM && c->NSL == a->NSL && c->lanes_jac.stride == a->lanes_jac.stride &&
+                c->lanes_g.stride == a->lanes_g.stride && c->ts_jac.nblocks == a->ts_jac.nblocks &&
+                c->ts_g.nblocks == a->ts_g.nblocks && c->ts_jac.t_doubles == a->ts_jac.t_doubles &&
+                c->ts_jac.h_doubles == a->ts_jac.h_doubles && c->iv_threads == a->iv_threads &&
+                c->use_ctpl == a->use_ctpl && c->tpl.size() == a->tpl.size() &&
+                std::memcmp(c->tpl.data(), a->tpl.data(), sizeof(TplEntry) * a->tpl.size()) == 0 &&
+                c->ctgen == a->ctgen;
+        if (!same) return set_err(MH_ERR_INVALID, "context %d: problem shape differs from context 0", b);
+    }
+    auto* bt = new mh_batch();
+    bt->ctx.assign(ctxs, ctxs + count);
+    bt->B = count;
+    const char* eg = std::getenv("MOCOHIP_BATCH_GM");
+    if (eg) bt->gm = std::atoi(eg) != 0;
+    std::vector<BatchItem> items(count);
+    for (int b = 0; b < count; ++b) {
+        const mh_ctx* c = ctxs[b];
+        items[b] = BatchItem{c->M, c->d_T, c->d_H, c->P, c->E, c->d_grid};
+    }
+    if (hipSetDevice(a->device) != hipSuccess ||
+            hipMalloc(&bt->d_items, sizeof(BatchItem) * count) != hipSuccess ||
+            hipMemcpy(bt->d_items, items.data(), sizeof(BatchItem) * count, hipMemcpyHostToDevice) != hipSuccess) {
+        if (bt->d_items) (void)hipFree(bt->d_items);
+        delete bt;
+        return set_err(MH_ERR_HIP, "batch allocation failed");
+    }
+    *out = bt;
+    return MH_OK;
+}
+extern "C" void mh_batch_destroy(mh_batch* bt) {
+    if (!bt) return;
+    if (bt->d_items) {
+        (void)hipSetDevice(bt->ctx[0]->device);
+        (void)hipFree(bt->d_items);
+    }
+    delete bt;
+}
+extern "C" int mh_batch_set_group_results_global(mh_batch* bt, int on) {
+    if (!bt) return set_err(MH_ERR_INVALID, "null batch");
+    bt->gm = on != 0;
+    return MH_OK;
+}
+static int batch_run(mh_batch* bt, int kind, const double* const* x, double* const* g, double* const* v) {
+    if (!bt || !x || (kind != 1 && !g) || (kind != 0 && !v)) return set_err(MH_ERR_INVALID, "null argument");
+    BatchPtrs P{};
+    for (int b = 0; b < bt->B; ++b) {
+        if (!x[b] || (kind != 1 && !g[b]) || (kind != 0 && !v[b]))
+            return set_err(MH_ERR_INVALID, "null pointer for batch item %d", b);
+        P.x[b] = x[b];
+        P.g[b] = kind != 1 ? g[b] : nullptr;
+        P.v[b] = kind != 0 ? v[b] : nullptr;
+    }
+    mh_ctx* c = bt->ctx[0];
+    HIPCHK(hipSetDevice(c->device));
+    c->be->batch(bt, kind == 0 ? 0 : 1, P, kind != 1, kind != 0);
+    HIPCHK(hipGetLastError());
+    if (c->async) return MH_OK;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return MH_OK;
+}
+extern "C" int mh_batch_eval_g_device(mh_batch* bt, const double* const* x, double* const* g) {
+    return batch_run(bt, 0, x, g, nullptr);
+}
+extern "C" int mh_batch_eval_jac_g_device(mh_batch* bt, const double* const* x, double* const* v) {
+    return batch_run(bt, 1, x, nullptr, v);
+}
+extern "C" int mh_batch_eval_g_jac_g_device(mh_batch* bt, const double* const* x, double* const* g,
+        double* const* v) {
+    return batch_run(bt, 2, x, g, v);
+}
+
 extern "C" int mh_eval_g_jac_g(mh_ctx* c, const double* x, double* g, double* values) {
     if (!c || !x || !g || !values) return set_err(MH_ERR_INVALID, "null argument");
     HIPCHK(hipSetDevice(c->device));

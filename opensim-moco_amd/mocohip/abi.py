@@ -227,6 +227,13 @@ MOCOHIP_SYMBOLS = {
     "mh_debug_time_stages": (i32, [C.c_void_p, C.c_void_p, i32, i32, P(f64)]),
     "mh_set_stream": (i32, [C.c_void_p, C.c_void_p]),
     "mh_set_async": (i32, [C.c_void_p, i32]),
+    "mh_batch_create": (i32, [C.POINTER(C.c_void_p), i32, C.POINTER(C.c_void_p)]),
+    "mh_batch_destroy": (None, [C.c_void_p]),
+    "mh_batch_eval_g_device": (i32, [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]),
+    "mh_batch_eval_jac_g_device": (i32, [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]),
+    "mh_batch_eval_g_jac_g_device": (i32, [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
+                                           C.POINTER(C.c_void_p)]),
+    "mh_batch_set_group_results_global": (i32, [C.c_void_p, i32]),
     "mh_synchronize": (i32, [C.c_void_p]),
 }
 

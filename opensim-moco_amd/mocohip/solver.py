@@ -396,6 +396,52 @@ class _NLPBase:
         return out
 
 
+class HipBatch:
+    """mh_batch: structurally identical HipNLPs evaluated by one launch per
+    kernel (include/mocohip.h mh_batch_*).  Calls take one device pointer
+    per NLP and run on the first NLP's stream."""
+
+    def __init__(self, nlps, group_results_global: bool | None = None):
+        self.nlps = list(nlps)
+        self.lib = self.nlps[0].lib
+        arr = (C.c_void_p * len(self.nlps))(*[n.ctx.value for n in self.nlps])
+        self.batch = C.c_void_p()
+        rc = self.lib.mh_batch_create(arr, len(self.nlps), C.byref(self.batch))
+        if rc:
+            raise RuntimeError(f"mh_batch_create: error {rc}: {self.lib.mh_last_error().decode()}")
+        if group_results_global is not None:
+            self._check(self.lib.mh_batch_set_group_results_global(self.batch, int(bool(group_results_global))))
+
+    def _check(self, rc):
+        if rc:
+            raise RuntimeError(f"mh_batch: error {rc}: {self.lib.mh_last_error().decode()}")
+
+    @staticmethod
+    def _ptrs(ptrs):
+        return (C.c_void_p * len(ptrs))(*[C.c_void_p(p) for p in ptrs])
+
+    def eval_g_device(self, xs, gs):
+        self._check(self.lib.mh_batch_eval_g_device(self.batch, self._ptrs(xs), self._ptrs(gs)))
+
+    def eval_jac_g_device(self, xs, vs):
+        self._check(self.lib.mh_batch_eval_jac_g_device(self.batch, self._ptrs(xs), self._ptrs(vs)))
+
+    def eval_g_jac_g_device(self, xs, gs, vs):
+        self._check(self.lib.mh_batch_eval_g_jac_g_device(self.batch, self._ptrs(xs), self._ptrs(gs),
+                                                          self._ptrs(vs)))
+
+    def close(self):
+        if self.batch:
+            self.lib.mh_batch_destroy(self.batch)
+            self.batch = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class HipNLP(_NLPBase):
     """NLP backed by libmocohip.so (the product path)."""
     prefix = "mh_"

@@ -954,3 +954,72 @@ def test_global_seed_jacobian(name):
     J0 = ref.eval_jac_g(x)
     dg = np.abs(gpu.eval_g(x) - ref.eval_g(x)).max()
     _assert_close(J, J0, 1e-8 * _scale(J0) + 4 * (dg + 64 * EPS * (np.abs(g).max() + 1.0)) / (2 * eps))
+
+
+# ---- batches: B structurally identical NLPs, one launch per kernel ---------
+
+BATCH_CASES = {
+    "gait_rigid_forward": lambda: configs.gait10dof18musc(12),
+    "gait_rigid_central": lambda: configs.gait10dof18musc(6, fd_scheme="central"),
+    "double_pendulum_implicit_trap": lambda: configs.double_pendulum(20, "trapezoidal", dynamics="implicit"),
+    "gait_inverse_random": lambda: configs.gait10dof18musc_inverse(4),
+    "gait_pathcon_implicit": lambda: configs.gait10dof18musc(6, dynamics="implicit", control_bounds=True),
+}
+
+
+@pytest.mark.parametrize("gm", [True, False])
+@pytest.mark.parametrize("name", list(BATCH_CASES))
+def test_batch_bit_identical(name, gm):
+    """mh_batch_*: three NLPs of one problem shape (different iterates; the
+    third with its own model data -- a 1 % heavier body, the trial-sweep
+    case) evaluated by one k_groups and one k_interval launch give, bit for
+    bit, each context's own eval_g / eval_jac_g / fused results; group
+    results staged in LDS or read from global memory alike."""
+    import torch
+    from mocohip.solver import HipBatch
+    nlps = []
+    for b in range(3):
+        st = BATCH_CASES[name]()
+        if b == 2 and "grf" in st.problem.model.tables:
+            # its own data: ground reactions 1 % larger (table values live
+            # in HBM; the generated code folds only the model's constants)
+            t = st.problem.model.tables["grf"]
+            t.columns = {k: np.asarray(v) * 1.01 for k, v in t.columns.items()}
+        nlps.append(HipNLP(st.problem.create_rep(), st.solver.options()))
+    bt = HipBatch(nlps, group_results_global=gm)
+    dev = torch.device("cuda", 0)
+    xs = [torch.tensor(physiological_iterate(n, 20 + b), dtype=torch.float64, device=dev)
+          for b, n in enumerate(nlps)]
+    gs = [torch.full((n.m,), np.nan, dtype=torch.float64, device=dev) for n in nlps]
+    vs = [torch.full((n.nnz,), np.nan, dtype=torch.float64, device=dev) for n in nlps]
+    ptr = lambda ts: [t.data_ptr() for t in ts]
+    ref = [(n.eval_g(x.cpu().numpy()), n.eval_jac_g(x.cpu().numpy())) for n, x in zip(nlps, xs)]
+    bt.eval_g_device(ptr(xs), ptr(gs))
+    bt.eval_jac_g_device(ptr(xs), ptr(vs))
+    torch.cuda.synchronize()
+    for b in range(3):
+        assert np.array_equal(gs[b].cpu().numpy(), ref[b][0], equal_nan=True)
+        assert np.array_equal(vs[b].cpu().numpy(), ref[b][1], equal_nan=True)
+    for t in gs + vs:
+        t.fill_(np.nan)
+    bt.eval_g_jac_g_device(ptr(xs), ptr(gs), ptr(vs))
+    torch.cuda.synchronize()
+    for b, n in enumerate(nlps):
+        g2, J2 = n.eval_g_jac_g(xs[b].cpu().numpy())
+        assert np.array_equal(gs[b].cpu().numpy(), g2, equal_nan=True)
+        assert np.array_equal(vs[b].cpu().numpy(), J2, equal_nan=True)
+    if "grf" in nlps[0].rep.problem.model.tables:   # the third NLP's own data mattered
+        assert not np.array_equal(ref[2][0], nlps[0].eval_g(xs[2].cpu().numpy()), equal_nan=True)
+    bt.close()
+
+
+def test_batch_rejects_other_shapes():
+    from mocohip.solver import HipBatch
+    a = HipNLP(configs.gait10dof18musc(6).problem.create_rep(), configs.gait10dof18musc(6).solver.options())
+    b = HipNLP(configs.gait10dof18musc(8).problem.create_rep(), configs.gait10dof18musc(8).solver.options())
+    with pytest.raises(RuntimeError, match="shape differs"):
+        HipBatch([a, b])
+    st = configs.double_pendulum_coupled(6)    # generic interpreter: no task back end
+    c = HipNLP(st.problem.create_rep(), st.solver.options())
+    with pytest.raises(RuntimeError, match="error 3"):
+        HipBatch([c])
