@@ -58,6 +58,9 @@ struct TplEntry {
 // ------------------------------------------------------------------------
 struct SzSmall { static constexpr int MB = 4, MQ = 4, MP = 4, MI = 24, MO = 12; };
 struct SzMedium { static constexpr int MB = 16, MQ = 16, MP = 8, MI = 128, MO = 64; };
+// full-body gait models (Rajagopal 2016: 14 bodies, 18-21 coordinates, up
+// to 8 points + 2 wraps per path): a third of SzLarge's per-lane workspace
+struct SzBody { static constexpr int MB = 16, MQ = 24, MP = 12, MI = 256, MO = 128; };
 struct SzLarge { static constexpr int MB = 32, MQ = 40, MP = 12, MI = 384, MO = 192; };
 
 template <class Z>

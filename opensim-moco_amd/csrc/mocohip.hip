@@ -1120,6 +1120,7 @@ static int validate_and_layout(mh_ctx* c, const mh_problem* p, const mh_options*
     };
     if (fits(SzSmall::MB, SzSmall::MQ, SzSmall::MP, SzSmall::MI, SzSmall::MO)) c->size_class = 0;
     else if (fits(SzMedium::MB, SzMedium::MQ, SzMedium::MP, SzMedium::MI, SzMedium::MO)) c->size_class = 1;
+    else if (fits(SzBody::MB, SzBody::MQ, SzBody::MP, SzBody::MI, SzBody::MO)) c->size_class = 3;
     else if (fits(SzLarge::MB, SzLarge::MQ, SzLarge::MP, SzLarge::MI, SzLarge::MO)) c->size_class = 2;
     else return set_err(MH_ERR_UNSUPPORTED, "model exceeds the largest size class");
     return MH_OK;
