@@ -960,7 +960,7 @@ def test_global_seed_jacobian(name):
 
 BATCH_CASES = {
     "gait_rigid_forward": lambda: configs.gait10dof18musc(12),
-    "gait_rigid_central": lambda: configs.gait10dof18musc(6, fd_scheme="central"),
+    "gait_rigid_backward": lambda: configs.gait10dof18musc(6, fd_scheme="backward"),
     "double_pendulum_implicit_trap": lambda: configs.double_pendulum(20, "trapezoidal", dynamics="implicit"),
     "gait_inverse_random": lambda: configs.gait10dof18musc_inverse(4),
     "gait_pathcon_implicit": lambda: configs.gait10dof18musc(6, dynamics="implicit", control_bounds=True),
@@ -1023,3 +1023,9 @@ def test_batch_rejects_other_shapes():
     c = HipNLP(st.problem.create_rep(), st.solver.options())
     with pytest.raises(RuntimeError, match="error 3"):
         HipBatch([c])
+    # central differences at N=200: the per-context interval kernel does not
+    # fit the LDS (split path), so no batch
+    st = configs.gait10dof18musc(200, fd_scheme="central")
+    d = HipNLP(st.problem.create_rep(), st.solver.options())
+    with pytest.raises(RuntimeError, match="error 3"):
+        HipBatch([d])
