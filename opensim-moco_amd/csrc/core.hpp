@@ -1152,9 +1152,11 @@ struct BatchPtrs {
     double* v[MH_BATCH_MAX];
 };
 
-template <class D>
-__global__ void __launch_bounds__(64) kb_groups(const BatchItem* __restrict__ items, BatchPtrs BP, Lanes Ln,
-        Tasks TK, int G, int k0) {
+// W > 0: at least W waves per SIMD (the register budget shrinks to 512 / W
+// VGPRs; more waves hide the transcendental latency of a batch's many tasks)
+template <class D, int W>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(W > 0 ? W : 1)))
+kb_groups(const BatchItem* __restrict__ items, BatchPtrs BP, Lanes Ln, Tasks TK, int G, int k0) {
     const int b = blockIdx.y;
     const BatchItem& it = items[b];
     const Src S{BP.x[b], it.grid, nullptr, G, k0};
@@ -1833,6 +1835,7 @@ struct mh_batch {
     int B = 0;
     BatchItem* d_items = nullptr;   // [B] per-NLP constants
     bool gm = true;                 // k_interval reads group results from global memory
+    int waves = 0;                  // kb_groups: 0 = the compiler's register budget, 3 = >= 3 waves/SIMD
 };
 
 struct Backend {
@@ -1939,7 +1942,8 @@ static void be_batch(mh_batch* bt, int mode, const BatchPtrs& BP, int with_g, in
     const Lanes& ln = mode ? c->lanes_jac : c->lanes_g;
     const TaskSet& ts = mode ? c->ts_jac : c->ts_g;
     const unsigned B = (unsigned)bt->B;
-    hipLaunchKernelGGL(kb_groups<D>, dim3((unsigned)ts.nblocks, B), dim3(64), 0, c->stream, bt->d_items, BP, ln,
+    auto kg = bt->waves == 3 ? kb_groups<D, 3> : kb_groups<D, 0>;
+    hipLaunchKernelGGL(kg, dim3((unsigned)ts.nblocks, B), dim3(64), 0, c->stream, bt->d_items, BP, ln,
             ts.dev, c->G, c->k0);
     Layout L = make_layout(c, c->k0, c->nk);
     double *g0 = nullptr, *v0 = nullptr;

@@ -1992,6 +1992,8 @@ extern "C" int mh_batch_create(mh_ctx* const* ctxs, int32_t count, mh_batch** ou
     bt->B = count;
     const char* eg = std::getenv("MOCOHIP_BATCH_GM");
     if (eg) bt->gm = std::atoi(eg) != 0;
+    const char* ew = std::getenv("MOCOHIP_BATCH_WAVES");
+    if (ew) bt->waves = std::atoi(ew) == 3 ? 3 : 0;
     std::vector<BatchItem> items(count);
     for (int b = 0; b < count; ++b) {
         const mh_ctx* c = ctxs[b];
