@@ -1788,6 +1788,8 @@ struct mh_ctx {
     int nsimd = 1024;              // SIMDs of the device (4 per CU)
     bool asm_grid_stride = false;  // k_transcribe_gs (MOCOHIP_ASM=gs) instead of k_transcribe
     bool quot = false;             // k_combine writes FD quotients (MOCOHIP_QUOT=1)
+    const Backend* be_lane = nullptr;   // the generated model's one-lane back end (if any)
+    bool g_lane = false;           // eval_g alone through be_lane + the split transcription
     int yq[2] = {0, 0};            // per lane configuration: Y of the last evaluation holds quotients
     bool timing = false;           // stage events for mh_last_timings (mh_set_timing)
     bool groups_timed = false;     // the last evaluation recorded ev[4]

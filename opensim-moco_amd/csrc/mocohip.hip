@@ -1424,6 +1424,8 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
         c->asm_grid_stride = ea && std::strcmp(ea, "gs") == 0;
         const char* ee = std::getenv("MOCOHIP_EVENTS");
         c->timing = ee && std::strcmp(ee, "1") == 0;
+        const char* egl = std::getenv("MOCOHIP_G_LANE");
+        c->g_lane = egl && std::strcmp(egl, "1") == 0;
         const char* eq = std::getenv("MOCOHIP_QUOT");
         c->quot = eq && std::strcmp(eq, "1") == 0;   // opt-in: measured slower
         if (o->sparsity_detection != MH_SPARSITY_NONE) {
@@ -1637,8 +1639,11 @@ static const GenEntry& (*const kGeneratedModels[])() = {
 // from one DAE pass (the base lane of every grid point feeds the defects;
 // IPOPT's eval_g(new_x=true) -> eval_jac_g(new_x=false) sequence).
 static int launch_stage(mh_ctx* c, int stage, int kind, const double* x, double* a, double* b) {
+    // eval_g alone through the model's one-lane-per-DAE kernel (one lane per
+    // grid point) and the split transcription (MOCOHIP_G_LANE=1)
+    const bool glane = kind == 0 && c->g_lane && c->be_lane;
     if (stage == 0) {
-        c->be->eval(c, x, kind == 0 ? 0 : 1, kind == 0 ? c->d_Yg : c->d_Y);
+        (glane ? c->be_lane : c->be)->eval(c, x, kind == 0 ? 0 : 1, kind == 0 ? c->d_Yg : c->d_Y);
         HIPCHK(hipGetLastError());
         return MH_OK;
     }
@@ -1648,7 +1653,7 @@ static int launch_stage(mh_ctx* c, int stage, int kind, const double* x, double*
     const int nchunks = kind == 0 ? 0 : (c->nnz_int + (c->ie == c->N ? c->nnz_tail : 0) + ASM_CHUNK - 1) / ASM_CHUNK;
     double* g = kind == 1 ? nullptr : a;
     double* v = kind == 0 ? nullptr : (kind == 1 ? a : b);
-    if (c->use_interval[kind == 0 ? 0 : 1]) {
+    if (c->use_interval[kind == 0 ? 0 : 1] && !glane) {
         c->be->interval(c, x, kind == 0 ? 0 : 1, g, v);
         HIPCHK(hipGetLastError());
         return MH_OK;
@@ -2448,7 +2453,10 @@ static const Backend* select_backend(mh_ctx* c, const mh_problem* p) {
         const uint64_t key = backend_key(c->model_hash, c->NMB > 0, c->presc != 0);
         for (auto entry : kGeneratedModels) {
             const GenEntry& e = entry();
-            if (e.hash == key) return lane ? &e.lane : &e.tasks;
+            if (e.hash == key) {
+                c->be_lane = &e.lane;
+                return lane ? &e.lane : &e.tasks;
+            }
         }
     }
     return &generic_backends()[c->size_class];
