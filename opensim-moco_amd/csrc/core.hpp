@@ -1836,8 +1836,9 @@ struct mh_batch {
     std::vector<mh_ctx*> ctx;
     int B = 0;
     BatchItem* d_items = nullptr;   // [B] per-NLP constants
-    bool gm = true;                 // k_interval reads group results from global memory
-    int waves = 0;                  // kb_groups: 0 = the compiler's register budget, 3 = >= 3 waves/SIMD
+    bool gm = true;                 // kb_interval reads group results from global memory
+    int waves = 3;                  // kb_groups: 0 = the compiler's register budget, 3 = >= 3 waves/SIMD
+    int threads = 512;              // kb_interval workgroup (Jacobian lanes)
 };
 
 struct Backend {
@@ -1954,7 +1955,7 @@ static void be_batch(mh_batch* bt, int mode, const BatchPtrs& BP, int with_g, in
     auto kern = bt->gm ? kb_interval<D, true> : kb_interval<D, false>;
     if (lds > 65536)
         (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    const unsigned threads = with_v ? (unsigned)c->iv_threads : 256u;
+    const unsigned threads = with_v ? (unsigned)bt->threads : 256u;
     hipLaunchKernelGGL(kern, dim3((unsigned)(c->ie - c->ib), B), dim3(threads), lds, c->stream, bt->d_items, BP,
             ln, ts.dev, L, I, c->d_tpl, (mode == 1 && c->use_ctpl) ? c->d_ctpl : nullptr, c->d_ctgen,
             (int)c->ctgen.size(), with_g, with_v, c->nep, c->nnz_ep);

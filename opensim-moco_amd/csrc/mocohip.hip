@@ -1997,8 +1997,14 @@ extern "C" int mh_batch_create(mh_ctx* const* ctxs, int32_t count, mh_batch** ou
     bt->B = count;
     const char* eg = std::getenv("MOCOHIP_BATCH_GM");
     if (eg) bt->gm = std::atoi(eg) != 0;
+    // defaults measured on MI355X (8 gait NLPs, fused steps, tools/batch_threads_ab.sh):
+    // 512-thread interval blocks reading group results from global memory
+    // 54.4 k calls/s vs 47.3 k at 1024 threads with LDS staging; kb_groups
+    // at >= 3 waves / SIMD +1-2 %
     const char* ew = std::getenv("MOCOHIP_BATCH_WAVES");
     if (ew) bt->waves = std::atoi(ew) == 3 ? 3 : 0;
+    const char* et = std::getenv("MOCOHIP_BATCH_THREADS");
+    if (et) bt->threads = std::min(1024, std::max(256, std::atoi(et) / 64 * 64));
     std::vector<BatchItem> items(count);
     for (int b = 0; b < count; ++b) {
         const mh_ctx* c = ctxs[b];
