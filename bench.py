@@ -134,6 +134,12 @@ class Ctx:
         self.dev = torch.device("cuda", self.local)
         if self.world > 1:
             dist.init_process_group("nccl", device_id=self.dev)
+        # a dedicated (non-null) stream made current: the contexts, torch's
+        # tensors and the host copies all order on it (torch's default stream
+        # has handle 0, which mh_set_stream reads as "the context's own
+        # stream" -- a non-blocking stream that would not order with it)
+        self.s = torch.cuda.Stream(device=self.dev)
+        torch.cuda.set_stream(self.s)
 
     def stream(self):
         return self.torch.cuda.current_stream().cuda_stream
