@@ -525,7 +525,8 @@ def test_eval_jac_g(name, backend):
                                   "gait_compliant_central", "double_pendulum_implicit_hs",
                                   "gait_rigid_implicit", "gait_inverse", "pendulum_bound_both_implicit",
                                   "double_pendulum_swingup", "double_pendulum_swingup_implicit_central",
-                                  "coupled_pendulum", "coupled_pendulum_implicit"])
+                                  "coupled_pendulum", "coupled_pendulum_implicit", "wrapped_pendulum",
+                                  "rajagopal18_inverse", "rajagopal80"])
 def test_objective_and_gradient(name):
     gpu, ref, st = _pair(name)
     for _, x in _iterates(gpu):
@@ -541,7 +542,8 @@ def test_objective_and_gradient(name):
                                   "pendulum_bound_both_implicit", "gait_rigid_sparse_random",
                                   "gait_implicit_pathcon_sparse", "gait_inverse_style_sparse",
                                   "gait_inverse_sparse", "gait_inverse", "gait_inverse_random",
-                                  "coupled_pendulum", "coupled_pendulum_noderiv_trap"])
+                                  "coupled_pendulum", "coupled_pendulum_noderiv_trap",
+                                  "wrapped_pendulum", "rajagopal18_inverse", "rajagopal80"])
 def test_shards_reassemble_bit_exact(name):
     """Mesh-interval shards (the multi-GPU partition) concatenate to exactly
     the unsharded g and Jacobian values."""

@@ -40,6 +40,12 @@ def test_driver_loads_tape_and_fails_loudly_without_gpu(tmp_path):
     write_tape(st.problem.create_rep(), st.solver.options(), str(path))
     r = _run(path)
     assert r.returncode == 2 and "no CPU fallback" in r.stderr, r.stderr
+    # version 5: wraps (the Rajagopal model with its PathWraps kept)
+    st5 = configs.rajagopal18_inverse(2, keep_path_wraps=True)
+    p5 = tmp_path / "raja.tape"
+    write_tape(st5.problem.create_rep(), st5.solver.options(), str(p5))
+    r = _run(p5)
+    assert r.returncode == 2 and "no CPU fallback" in r.stderr, r.stderr
     data = path.read_bytes()
     (tmp_path / "cut.tape").write_bytes(data[:-8])
     r = _run(tmp_path / "cut.tape")
@@ -52,6 +58,10 @@ def test_driver_loads_tape_and_fails_loudly_without_gpu(tmp_path):
     ("double_pendulum_implicit", lambda: configs.double_pendulum(20, dynamics="implicit")),
     ("gait_pathcon", lambda: configs.gait10dof18musc(10, control_bounds=True)),
     ("coupled_pendulum", lambda: configs.double_pendulum_coupled(12, coupler="spline")),
+    # tape v5: wrap surfaces / PathWraps; prescribed kinematics with coupler
+    # multipliers, endpoint rows and detected sparsity
+    ("wrapped_pendulum", lambda: configs.wrapped_pendulum(12, quadrant="-y")),
+    ("rajagopal18_inverse_wrapped", lambda: configs.rajagopal18_inverse(3, keep_path_wraps=True)),
 ])
 def test_driver_matches_python_binding_bit_exact(tmp_path, name, mk):
     """The C++ host and the ctypes binding drive the same library: same g and
