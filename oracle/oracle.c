@@ -814,6 +814,10 @@ int orc_create(const mh_problem* p, const mh_options* o, orc_ctx** out) {
             return fail(MH_ERR_INVALID, "path wrap %d: bad muscle/wrap or not grouped by muscle", k);
         }
         if (c->mus_pw_count[W->muscle]++ == 0) c->mus_pw_begin[W->muscle] = k;
+        if (c->mus_pw_count[W->muscle] > 8) {   /* as the device (mh_create) */
+            orc_destroy(c);
+            return fail(MH_ERR_UNSUPPORTED, "muscle %d: more than 8 PathWraps", W->muscle);
+        }
     }
     c->maxcp = 1;
     for (int im = 0; im < M->nmuscles; ++im) {

@@ -15,7 +15,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "mocohip.h")
 
 STRUCTS = ["mh_function", "mh_axis", "mh_body", "mh_path_point", "mh_muscle",
-           "mh_actuator", "mh_table", "mh_external_force", "mh_constraint", "mh_model",
+           "mh_actuator", "mh_table", "mh_external_force", "mh_constraint", "mh_wrap_object",
+           "mh_path_wrap", "mh_model",
            "mh_bounds", "mh_variable_info", "mh_goal", "mh_path_equation", "mh_endpoint_equation",
            "mh_problem",
            "mh_options", "mh_nlp_info"]
