@@ -438,6 +438,22 @@ def config3_line(cx, args):
     return out
 
 
+def solve_lines():
+    """Wall-clock to a converged solve (the BASELINE metric's second half) on
+    the GPU path for the reference's small known-answer problems, with the
+    host driver mocohip.nlpsolve (scipy SLSQP; Ipopt is absent here)."""
+    from mocohip import configs
+    out = {}
+    for name, mk in (("sliding_mass_interface", configs.sliding_mass_interface),
+                     ("double_pendulum_swingup", lambda: configs.double_pendulum_swingup(29))):
+        sol = mk().solve()
+        r = sol.stats
+        out[name] = {"success": r.success, "wall_clock_s": round(r.duration, 4), "iterations": r.iterations,
+                     "objective": r.objective, "final_time": float(sol.time[-1]),
+                     "evaluations": r.evaluations, "optimizer": r.status.split(":")[0]}
+    return out
+
+
 def mesh_main(cx, args):
     """--multi mesh: one NLP, sharded; host-inclusive strong scaling."""
     from mocohip import configs
@@ -581,6 +597,8 @@ def main():
                 cx, lambda: configs.gait10dof18musc(N, fd_scheme=args.fd), track_iterate, args, args.batch)
         if args.config3 > 0:
             extra["config3"] = config3_line(cx, args)
+        if cx.world == 1:
+            extra["solve"] = solve_lines()
         if args.inverse_batch > 0:
             # MocoTool mesh_interval 0.02 s: ceil((2.499 - 0.001) / 0.02) = 125
             # intervals (MocoTool.cpp:27,68-69)

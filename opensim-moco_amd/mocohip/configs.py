@@ -49,6 +49,27 @@ def sliding_mass(num_mesh_intervals: int = 50, dynamics: str = "explicit") -> Mo
     return MocoStudy(p, s)
 
 
+def sliding_mass_interface(num_mesh_intervals: int = 19) -> MocoStudy:
+    """testMocoInterface.cpp:41-83 ("Sliding mass", :1701-1742): a 10 kg
+    mass on a slider, control in [-10, 10] N, from x = 0 to x = 1 at rest,
+    minimum final time in [0, 10], trapezoidal, 19 mesh intervals; the
+    reference's solution is bang-bang with final time 2.0."""
+    m = Model("sliding_mass", gravity=(0, 0, 0))
+    m.add_body(Body("body", 10.0, (0, 0, 0), (0, 0, 0, 0, 0, 0)))
+    pos = Coordinate("position", (-math.inf, math.inf), "translational", path="/slider/position")
+    m.add_joint(Joint.slider("slider", "ground", "body", pos))
+    m.add_coordinate_actuator(CoordinateActuator("actuator", "position", 1.0, -10.0, 10.0,
+                                                 path="/actuator"))
+    p = MocoProblem(m)
+    p.set_time_bounds(0.0, (0.0, 10.0))
+    p.set_state_info("/slider/position/value", (0, 1), 0, 1)
+    p.set_state_info("/slider/position/speed", (-100, 100), 0, 0)
+    p.add_goal(MocoFinalTimeGoal())
+    s = MocoHipSolver(num_mesh_intervals=num_mesh_intervals, transcription_scheme="trapezoidal",
+                      enforce_constraint_derivatives=False)
+    return MocoStudy(p, s)
+
+
 def n_link_pendulum(num_links: int) -> Model:
     """ModelFactory::createNLinkPendulum."""
     m = Model({1: "pendulum", 2: "double_pendulum"}.get(num_links, f"{num_links}_link_pendulum"))

@@ -633,3 +633,31 @@ class MocoStudy:
     def create_nlp(self, interval_begin: int = 0, interval_end: int = 0) -> HipNLP:
         rep = self.problem.create_rep()
         return HipNLP(rep, self.solver.options(interval_begin, interval_end))
+
+    def solve(self, guess=None, nlp=None):
+        """MocoStudy::solve (MocoStudy.cpp:79-101): transcribe on the HIP
+        path, optimize from the solver's starting point, return the
+        solution as a MocoTrajectory with the solve statistics in its
+        metadata (success, objective, num_iterations, solver_duration,
+        status; MocoSolver::setSolutionStats, MocoSolver.h:97-102).  The
+        optimizer is mocohip.nlpsolve (Ipopt is absent here); tolerances
+        from optim_convergence_tolerance / optim_constraint_tolerance
+        (default 1e-8), optim_max_iterations."""
+        from .nlpsolve import solve_nlp
+        from .trajectory import MocoTrajectory
+        own = nlp is None
+        nlp = nlp or self.create_nlp()
+        x0 = self.solver.starting_point(nlp, guess)
+        s = self.solver
+        tol = s.optim_convergence_tolerance if s.optim_convergence_tolerance > 0 else 1e-8
+        ctol = s.optim_constraint_tolerance if s.optim_constraint_tolerance > 0 else 1e-8
+        it = s.optim_max_iterations if s.optim_max_iterations > 0 else 5000
+        r = solve_nlp(nlp, x0, tol, ctol, it)
+        sol = MocoTrajectory.from_iterate(nlp, r.x)
+        sol.metadata.update({"success": "true" if r.success else "false", "objective": repr(r.objective),
+                             "num_iterations": str(r.iterations), "solver_duration": repr(r.duration),
+                             "status": r.status, "optimizer": "scipy trust-constr over the C ABI"})
+        sol.stats = r
+        if own:
+            nlp.close()
+        return sol
