@@ -248,16 +248,28 @@ class MocoTrajectory:
         rep = nlp.rep
         grid = nlp_grid(nlp)
         G, ns, nc, ndv = len(grid), nlp.NS, nlp.NC, nlp.NDV
+        nm, nsl = getattr(nlp, "NM", 0), getattr(nlp, "NSL", 0)
+        N = nlp.opts.num_mesh_intervals
         x = np.asarray(x, float)
-        if len(x) != 2 + (ns + nc + ndv) * G:
+        if len(x) != 2 + (ns + nc + nm + ndv) * G + nsl * N:
             raise ValueError("iterate size does not match the problem and grid")
         t0, tf = x[0], x[1]
-        S = x[2:2 + ns * G].reshape(G, ns)
-        Cm = x[2 + ns * G:2 + (ns + nc) * G].reshape(G, nc)
-        D = x[2 + (ns + nc) * G:].reshape(G, ndv)
+        o = 2
+        S = x[o:o + ns * G].reshape(G, ns); o += ns * G
+        Cm = x[o:o + nc * G].reshape(G, nc); o += nc * G
+        Mu = x[o:o + nm * G].reshape(G, nm); o += nm * G
+        L = x[o:o + nsl * N].reshape(N, nsl); o += nsl * N
+        D = x[o:o + ndv * G].reshape(G, ndv)
+        # slacks live at the mesh-interval midpoints (HS): NaN elsewhere,
+        # as MocoTrajectory holds them
+        Lg = np.full((G, nsl), np.nan)
+        if nsl:
+            Lg[1::2] = L
         dn = [f"derivative_{j}" for j in range(ndv)]
+        mn = [f"lambda_{j}" for j in range(nm)]
+        sn = [f"gamma_{j}" for j in range(nsl)]
         return MocoTrajectory((tf - t0) * grid + t0, list(rep.state_names), list(rep.control_names),
-                              [], dn, [], [], S, Cm, None, D)
+                              mn, dn, sn, [], S, Cm, Mu, D, Lg)
 
     def is_numerically_equal(self, other: "MocoTrajectory", tol: float = 1e-12) -> bool:
         if self.labels() != other.labels() or self.num_times != other.num_times:
