@@ -49,7 +49,8 @@ def sliding_mass(num_mesh_intervals: int = 50, dynamics: str = "explicit") -> Mo
     return MocoStudy(p, s)
 
 
-def sliding_mass_interface(num_mesh_intervals: int = 19) -> MocoStudy:
+def sliding_mass_interface(num_mesh_intervals: int = 19, scheme: str = "trapezoidal",
+                           dynamics: str = "explicit") -> MocoStudy:
     """testMocoInterface.cpp:41-83 ("Sliding mass", :1701-1742): a 10 kg
     mass on a slider, control in [-10, 10] N, from x = 0 to x = 1 at rest,
     minimum final time in [0, 10], trapezoidal, 19 mesh intervals; the
@@ -65,8 +66,8 @@ def sliding_mass_interface(num_mesh_intervals: int = 19) -> MocoStudy:
     p.set_state_info("/slider/position/value", (0, 1), 0, 1)
     p.set_state_info("/slider/position/speed", (-100, 100), 0, 0)
     p.add_goal(MocoFinalTimeGoal())
-    s = MocoHipSolver(num_mesh_intervals=num_mesh_intervals, transcription_scheme="trapezoidal",
-                      enforce_constraint_derivatives=False)
+    s = MocoHipSolver(num_mesh_intervals=num_mesh_intervals, transcription_scheme=scheme,
+                      multibody_dynamics_mode=dynamics, enforce_constraint_derivatives=False)
     return MocoStudy(p, s)
 
 
