@@ -29,8 +29,11 @@ def test_sliding_mass_known_solution(scheme, dynamics):
     spd = np.where(t < half, t, t[-1] - t)
     frc = np.where(t < half, 10.0, -10.0)
     mesh = np.arange(len(t)) % (1 if scheme == "trapezoidal" else 2) == 0
+    # (Hermite-Simpson: the midpoint of the interval holding the switch
+    # sits on the speed peak, which the cubic interpolant cuts by ~0.026)
+    near = (~mesh) & (np.abs(t - half) < 0.06)
     assert np.abs(sol.states[:, 0] - pos).max() < 1e-2
-    assert np.abs(sol.states[:, 1] - spd).max() < 1e-2
+    assert np.abs(sol.states[~near, 1] - spd[~near]).max() < 1e-2
     # the switch is inside one mesh interval: compare the force away from it
     away = mesh & (np.abs(t - half) > 0.15)
     assert np.abs(sol.controls[away, 0] - frc[away]).max() < 1e-2
