@@ -67,6 +67,7 @@ template <class Z>
 struct GenericDae {
     static constexpr int MI = Z::MI, MO = Z::MO;
     static constexpr bool SPLIT = false;
+    static constexpr bool EXC_LANES = true;   // k_exc_lanes reproduces its excitation lanes
     __device__ __forceinline__ static void eval(const DevModel& M, double t, const double* in,
             double* out) {
         Work<Z::MB, Z::MQ, Z::MP> w;
@@ -158,15 +159,20 @@ __device__ __forceinline__ double lane_inputs(const Layout& L, const Lanes& Ln,
     return t;
 }
 
-// One lane = one DAE evaluation (grid point kl, lane role r).
+// One lane = one DAE evaluation (grid point kl, lane role r).  With a lane
+// map, thread j of a grid point evaluates lane map[j] of nmap (the lanes
+// k_exc_lanes does not stand in for, packed so no wave idles); without,
+// every lane.
 template <class D>
-__global__ void __launch_bounds__(64) k_eval(DevModel M, Layout L, Lanes Ln,
-        const double* __restrict__ x, const double* __restrict__ grid,
-        double* __restrict__ times, double* __restrict__ Y) {
+__device__ __forceinline__ void eval_lane(const DevModel& M, const Layout& L, const Lanes& Ln,
+        const double* __restrict__ x, const double* __restrict__ grid, double* __restrict__ times,
+        double* __restrict__ Y, const int* __restrict__ map, int nmap) {
     const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (gid >= (long)L.nk * Ln.stride) return;
-    const int kl = (int)(gid / Ln.stride);
-    const int r = (int)(gid - (long)kl * Ln.stride);
+    const int per = map ? nmap : Ln.stride;
+    if (gid >= (long)L.nk * per) return;
+    const int kl = (int)(gid / per);
+    const int j = (int)(gid - (long)kl * per);
+    const int r = map ? map[j] : j;
     const int k = L.k0 + kl;
     double in[D::MI];
     double out[D::MO];
@@ -177,6 +183,41 @@ __global__ void __launch_bounds__(64) k_eval(DevModel M, Layout L, Lanes Ln,
 #pragma unroll
     for (int o = 0; o < D::MO; ++o)
         if (o < L.NO) Yk[(long)o * Ln.stride] = out[o];
+}
+template <class D>
+__global__ void __launch_bounds__(64) k_eval(DevModel M, Layout L, Lanes Ln,
+        const double* __restrict__ x, const double* __restrict__ grid,
+        double* __restrict__ times, double* __restrict__ Y, const int* __restrict__ map = nullptr,
+        int nmap = 0) {
+    eval_lane<D>(M, L, Ln, x, grid, times, Y, map, nmap);
+}
+// Excitation lanes of the generic interpreter.  A lane that perturbs the
+// excitation of a muscle with activation dynamics changes one DAE output,
+// that muscle's activation derivative: excitation enters the DAE only there
+// (dae_eval: the force uses the activation state).  After k_eval has written
+// the base lane, such a lane copies the base lane's outputs and re-evaluates
+// dgf_adot at the perturbed excitation -- the value the full evaluation
+// computes, bit for bit (tests/test_gpu_parity.py test_excitation_lanes).
+// exc[r] = the muscle lane r perturbs, or -1 (built in mh_create).
+template <class D>
+__global__ void __launch_bounds__(64) k_exc_lanes(DevModel M, Layout L, Lanes Ln,
+        const double* __restrict__ x, double* __restrict__ Y, const int* __restrict__ exc) {
+#pragma clang fp contract(off)
+    const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= (long)L.nk * Ln.stride) return;
+    const int kl = (int)(gid / Ln.stride);
+    const int r = (int)(gid - (long)kl * Ln.stride);
+    const int m = exc[r];
+    if (m < 0) return;
+    const int k = L.k0 + kl;
+    double* Yk = Y + (long)kl * L.NO * Ln.stride;
+    for (int o = 0; o < L.NO; ++o) Yk[(long)o * Ln.stride + r] = Yk[(long)o * Ln.stride + Ln.base];
+    const int sa = M.mus_act_state[m];
+    const double act = x[2 + (long)k * L.NS + (M.presc ? sa - 2 * M.nq : sa)];
+    double step = Ln.fd == MH_FD_BACKWARD ? -Ln.h : Ln.h;
+    if (Ln.fd == MH_FD_CENTRAL && r >= Ln.ND) step = -Ln.h;
+    const double e = x[2 + (long)L.NS * L.G + (long)k * L.NC + M.mus_control[m]] + step;
+    Yk[(long)(sa - M.nq) * Ln.stride + r] = dgf_adot(M, act, e);
 }
 
 // ------------------------------------------------------------------------
@@ -1751,6 +1792,12 @@ struct mh_ctx {
            *d_Yg = nullptr, *d_g = nullptr, *d_vals = nullptr, *d_C = nullptr, *d_grad = nullptr,
            *d_tpart = nullptr, *d_f = nullptr;
     TplEntry* d_tpl = nullptr;
+    // generic interpreter: per Jacobian lane, the muscle whose excitation it
+    // perturbs when k_exc_lanes stands in for the evaluation, else -1; null
+    // when no lane qualifies (or MOCOHIP_EXC_LANES=0)
+    int* d_exc = nullptr;
+    int* d_lane_map = nullptr;     // the other lanes, in order (k_eval's lane map)
+    int n_exc_lanes = 0;
     uint32_t* d_ctpl = nullptr;    // compiled template of the Jacobian lanes (k_interval)
     std::vector<uint32_t> ctpl;
     int* d_ctgen = nullptr;        // the entries it leaves to jac_entry (t0 / tf of defect rows)
@@ -1869,8 +1916,18 @@ static void be_eval_lane(mh_ctx* c, const double* x, int mode, double* Y) {
     Layout L = make_layout(c, c->k0, c->nk);
     const Lanes& ln = mode ? c->lanes_jac : c->lanes_g;
     const long lanes = (long)c->nk * ln.stride;
-    hipLaunchKernelGGL(k_eval<D>, dim3((unsigned)((lanes + 63) / 64)), dim3(64), 0, c->stream, c->M, L,
-            ln, x, c->d_grid, c->d_times, Y);
+    const bool exc = mode && c->d_exc && D::EXC_LANES;
+    if (!exc) {
+        hipLaunchKernelGGL(k_eval<D>, dim3((unsigned)((lanes + 63) / 64)), dim3(64), 0, c->stream, c->M, L,
+                ln, x, c->d_grid, c->d_times, Y, nullptr, 0);
+        return;
+    }
+    const int nmap = ln.stride - c->n_exc_lanes;
+    const long full = (long)c->nk * nmap;
+    hipLaunchKernelGGL(k_eval<D>, dim3((unsigned)((full + 63) / 64)), dim3(64), 0, c->stream, c->M, L,
+            ln, x, c->d_grid, c->d_times, Y, c->d_lane_map, nmap);
+    hipLaunchKernelGGL(k_exc_lanes<D>, dim3((unsigned)((lanes + 63) / 64)), dim3(64), 0, c->stream, c->M,
+            L, ln, x, Y, c->d_exc);
 }
 template <class D>
 // Returns 1 when Y holds finite-difference quotients (k_combine quot mode,

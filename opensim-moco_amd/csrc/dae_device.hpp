@@ -269,6 +269,20 @@ __device__ __forceinline__ double dgf_fv_inv(double fv) {
     return (sinh(1.0 / DGF_d1 * (fv - DGF_d4)) - DGF_d3) / DGF_d2;
 }
 
+// DeGroote-Fregly activation dynamics (DeGrooteFregly2016Muscle.cpp:186-233,
+// computeStateVariableDerivatives; oracle/oracle.c dgf).  Without contraction, so the generic
+// interpreter's excitation lanes (k_exc_lanes) reproduce the full
+// evaluation's value bit for bit.
+__device__ __forceinline__ double dgf_adot(const DevModel& M, double act, double exc) {
+#pragma clang fp contract(off)
+    double tcf = 0.5 + 1.5 * act;
+    double tempAct = 1.0 / (M.tau_act * tcf);
+    double tempDeact = tcf / M.tau_deact;
+    double f = 0.5 * tanh(0.1 * (exc - act));
+    double timeConst = tempAct * (f + 0.5) + tempDeact * (-f + 0.5);
+    return timeConst * (exc - act);
+}
+
 // Muscle tendon force and auxiliary derivatives.
 // implicit_tendon: tendon_compliance_dynamics_mode "implicit" with the
 // normalized tendon force derivative dft as input; resid = the equilibrium
@@ -321,14 +335,7 @@ __device__ __forceinline__ void dgf_eval(const DevModel& M, int im, double LMT, 
     double total = activeF + conPass + nonCon;
     T = compliant ? Fmax * ftn : total * cosPenn;
     if (implicit_tendon) *resid = T - total * cosPenn;
-    if (has_act) {
-        double tcf = 0.5 + 1.5 * act;
-        double tempAct = 1.0 / (M.tau_act * tcf);
-        double tempDeact = tcf / M.tau_deact;
-        double f = 0.5 * tanh(0.1 * (exc - act));
-        double timeConst = tempAct * (f + 0.5) + tempDeact * (-f + 0.5);
-        adot = timeConst * (exc - act);
-    }
+    if (has_act) adot = dgf_adot(M, act, exc);
     if (compliant)
         ftdot = implicit_tendon ? dft : ntv * (DGF_c1 * kT * exp(kT * (normTendonLength - DGF_c2)));
     (void)fiberWidth;

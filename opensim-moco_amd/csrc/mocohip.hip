@@ -1267,6 +1267,29 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     const int stride = c->fd == MH_FD_CENTRAL ? 2 * ND + 1 : ND + 1;
     c->lanes_jac = Lanes{c->fd, ND, stride, stride - 1, c->h};
     c->lanes_g = Lanes{c->fd, ND, 1, 0, c->h};
+    // excitation lanes (k_exc_lanes): a direction that perturbs the control
+    // of exactly one muscle with activation dynamics, read by nothing else
+    // in the DAE (coordinate actuators read their own controls only)
+    std::vector<int> exc_lane(stride, -1);
+    if (!backend_tasks(c->be) && std::strncmp(c->be->name, "generic", 7) == 0 &&
+            !(std::getenv("MOCOHIP_EXC_LANES") && std::strcmp(std::getenv("MOCOHIP_EXC_LANES"), "0") == 0)) {
+        for (int dir = 2; dir < ND; ++dir) {
+            const int ci = dir - 2 - c->NS;
+            if (ci < 0 || ci >= c->NC || ci >= M.nactuators || M.actuators[ci].kind != MH_ACT_MUSCLE) continue;
+            int mus = -1, users = 0;
+            for (int im = 0; im < M.nmuscles; ++im)
+                if (mus_control[im] == ci) { mus = im; ++users; }
+            if (users != 1 || act_state[mus] < 0) continue;
+            exc_lane[dir] = mus;
+            if (c->fd == MH_FD_CENTRAL) exc_lane[dir + ND] = mus;
+        }
+        for (int v : exc_lane) c->n_exc_lanes += v >= 0;
+    }
+    std::vector<int> lane_map;
+    for (int r = 0; r < stride; ++r)
+        if (exc_lane[r] < 0) lane_map.push_back(r);
+    const size_t o_exc = c->n_exc_lanes ? A.put(exc_lane.data(), exc_lane.size()) : 0;
+    const size_t o_lmap = c->n_exc_lanes ? A.put(lane_map.data(), lane_map.size()) : 0;
     const size_t o_Y = A.reserve(sizeof(double) * (size_t)c->nk * std::max(1, c->NO) * stride);
     const size_t o_Yg = A.reserve(sizeof(double) * (size_t)c->nk * std::max(1, c->NO));
     const size_t o_g = A.reserve(sizeof(double) * ((size_t)c->nep + (size_t)nint * c->rpi + c->ntail));
@@ -1355,6 +1378,7 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     c->GS.gidx = (const int*)(b + o_gidx);
     c->GS.gcol = (const int*)(b + o_gcol);
     c->GS.gw = (const double*)(b + o_gw);
+    if (c->n_exc_lanes) { c->d_exc = (int*)(b + o_exc); c->d_lane_map = (int*)(b + o_lmap); }
     c->d_grid = (double*)(b + o_grid); c->d_quad = (double*)(b + o_quad);
     c->d_tpl = (TplEntry*)(b + o_tpl);
     c->d_ctpl = (uint32_t*)(b + o_ctpl);
@@ -2415,6 +2439,7 @@ extern "C" int mh_get_backend_flags(const mh_ctx* c, char* flags, int32_t len) {
     if (c->use_roles && c->use_interval[1]) f += " roles";
     if (c->quot) f += " quot";
     if (c->asm_grid_stride) f += " asm-gs";
+    if (c->d_exc) f += " exc-lanes";
     std::strncpy(flags, f.c_str(), (size_t)len - 1);
     flags[len - 1] = 0;
     return MH_OK;

@@ -814,6 +814,7 @@ def generate(cm, struct_name: str, implicit: bool = False, prescribed: bool = Fa
     static constexpr int NQ = {NQ}, NZ = {NZ}, NS = {Lo.NS}, NC = {Lo.NC}, NO = {Lo.NO}, NI = {Lo.NI};
     static constexpr bool IMPLICIT = {"true" if implicit else "false"};
     static constexpr bool PRESCRIBED = {"true" if prescribed else "false"};
+    static constexpr bool EXC_LANES = false;   // k_exc_lanes is the generic interpreter's
     static constexpr int MI = NI, MO = NO;
     static constexpr double FLOPS_PER_EVAL = {float(fl['total'])};
     // task decomposition: group 0 = mass matrix factor (NST values), groups

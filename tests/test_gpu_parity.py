@@ -287,7 +287,8 @@ def _pair(name, backend="auto", tasks=None, env=None):
     saved = {k: os.environ.pop(k, None) for k in ("MOCOHIP_BACKEND", "MOCOHIP_TASKS", "MOCOHIP_INTERVAL",
                                                   "MOCOHIP_ASM", "MOCOHIP_QUOT", "MOCOHIP_CTPL",
                                                   "MOCOHIP_ROLES", "MOCOHIP_ROLE_COUPLE",
-                                                  "MOCOHIP_IV_QFUSE", "MOCOHIP_IV_THREADS")}
+                                                  "MOCOHIP_IV_QFUSE", "MOCOHIP_IV_THREADS",
+                                                  "MOCOHIP_EXC_LANES")}
     if backend != "auto":
         os.environ["MOCOHIP_BACKEND"] = backend
     if tasks:
@@ -689,6 +690,27 @@ def test_kernel_variants_bit_identical(name, variant):
         ga, Ja = gpu.eval_g_jac_g(x)
         gb, Jb = split.eval_g_jac_g(x)
         assert np.array_equal(ga, gb, equal_nan=True) and np.array_equal(Ja, Jb, equal_nan=True)
+
+
+@pytest.mark.parametrize("name", ["gait_rigid_forward", "gait_rigid_central", "gait_compliant_central",
+                                  "gait_rigid_implicit", "gait_implicit_both_central", "gait_inverse_random",
+                                  "wrapped_pendulum", "wrapped_pendulum_compliant_central_pos_y",
+                                  "rajagopal18_inverse", "rajagopal80_wrapped_trap"])
+def test_excitation_lanes_bit_identical(name):
+    """Generic interpreter: the lanes that perturb a muscle excitation are
+    filled by k_exc_lanes (the base lane's outputs + dgf_adot at the
+    perturbed excitation) instead of a full DAE evaluation; the raw lanes,
+    g and the Jacobian equal the full evaluation of every lane
+    (MOCOHIP_EXC_LANES=0) bit for bit."""
+    gpu, _, _ = _pair(name, "generic")
+    full, _, _ = _pair(name, "generic", env={"MOCOHIP_EXC_LANES": "0"})
+    assert "exc-lanes" in gpu.backend_flags() and "exc-lanes" not in full.backend_flags()
+    for _, x in _iterates(gpu):
+        ta, Ya = gpu.jacobian_lanes(x)
+        tb, Yb = full.jacobian_lanes(x)
+        assert np.array_equal(ta, tb) and np.array_equal(Ya, Yb, equal_nan=True)
+        assert np.array_equal(gpu.eval_jac_g(x), full.eval_jac_g(x), equal_nan=True)
+        assert np.array_equal(gpu.eval_g(x), full.eval_g(x), equal_nan=True)
 
 
 def test_work_accounting():
