@@ -1798,6 +1798,7 @@ struct mh_ctx {
     int* d_exc = nullptr;
     int* d_lane_map = nullptr;     // the other lanes, in order (k_eval's lane map)
     int n_exc_lanes = 0;
+    int g_block = 4;               // generic interpreter, eval_g: k_eval workgroup size (A/B: profiles/r02_l)
     uint32_t* d_ctpl = nullptr;    // compiled template of the Jacobian lanes (k_interval)
     std::vector<uint32_t> ctpl;
     int* d_ctgen = nullptr;        // the entries it leaves to jac_entry (t0 / tf of defect rows)
@@ -1918,7 +1919,11 @@ static void be_eval_lane(mh_ctx* c, const double* x, int mode, double* Y) {
     const long lanes = (long)c->nk * ln.stride;
     const bool exc = mode && c->d_exc && D::EXC_LANES;
     if (!exc) {
-        hipLaunchKernelGGL(k_eval<D>, dim3((unsigned)((lanes + 63) / 64)), dim3(64), 0, c->stream, c->M, L,
+        // eval_g of the generic interpreter: fewer lanes per workgroup (one
+        // wave each) keep a wave's scratch within its CU's L1
+        // (MOCOHIP_G_BLOCK; k_eval indexes by blockDim, any size <= 64 works)
+        const int tb = (mode == 0 && D::EXC_LANES) ? c->g_block : 64;
+        hipLaunchKernelGGL(k_eval<D>, dim3((unsigned)((lanes + tb - 1) / tb)), dim3(tb), 0, c->stream, c->M, L,
                 ln, x, c->d_grid, c->d_times, Y, nullptr, 0);
         return;
     }

@@ -288,7 +288,7 @@ def _pair(name, backend="auto", tasks=None, env=None):
                                                   "MOCOHIP_ASM", "MOCOHIP_QUOT", "MOCOHIP_CTPL",
                                                   "MOCOHIP_ROLES", "MOCOHIP_ROLE_COUPLE",
                                                   "MOCOHIP_IV_QFUSE", "MOCOHIP_IV_THREADS",
-                                                  "MOCOHIP_EXC_LANES")}
+                                                  "MOCOHIP_EXC_LANES", "MOCOHIP_G_BLOCK")}
     if backend != "auto":
         os.environ["MOCOHIP_BACKEND"] = backend
     if tasks:
@@ -711,6 +711,19 @@ def test_excitation_lanes_bit_identical(name):
         assert np.array_equal(ta, tb) and np.array_equal(Ya, Yb, equal_nan=True)
         assert np.array_equal(gpu.eval_jac_g(x), full.eval_jac_g(x), equal_nan=True)
         assert np.array_equal(gpu.eval_g(x), full.eval_g(x), equal_nan=True)
+
+
+@pytest.mark.parametrize("tb", ["1", "8", "64"])
+@pytest.mark.parametrize("name", ["gait_rigid_forward", "gait_inverse_random", "wrapped_pendulum",
+                                  "rajagopal18_inverse", "coupled_pendulum_implicit"])
+def test_eval_g_block_bit_identical(name, tb):
+    """Generic interpreter: eval_g's k_eval in workgroups of 1 / 8 / 64 lanes
+    (MOCOHIP_G_BLOCK) writes what the default 4-lane launch writes."""
+    gpu, _, _ = _pair(name, "generic")
+    small, _, _ = _pair(name, "generic", env={"MOCOHIP_G_BLOCK": tb})
+    for _, x in _iterates(gpu):
+        assert np.array_equal(gpu.eval_g(x), small.eval_g(x), equal_nan=True)
+        assert np.array_equal(gpu.eval_jac_g(x), small.eval_jac_g(x), equal_nan=True)
 
 
 def test_work_accounting():
