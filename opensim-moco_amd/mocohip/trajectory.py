@@ -271,6 +271,73 @@ class MocoTrajectory:
         return MocoTrajectory((tf - t0) * grid + t0, list(rep.state_names), list(rep.control_names),
                               mn, dn, sn, [], S, Cm, Mu, D, Lg)
 
+    # -------------------------------------------------------------- comparison
+    def compare_continuous_variables_rms(self, other: "MocoTrajectory", states=None, controls=None,
+                                         multipliers=None, derivatives=None) -> float:
+        """compareContinuousVariablesRMS (MocoTrajectory.cpp:1131-1263): per
+        block, the given names (None: all, which both trajectories must share;
+        ["none"]: skip the block); each column through an interpolating
+        GCV spline of degree min(n - 1, 5) per trajectory (0 outside its time
+        range), the summed squared error integrated by the trapezoidal rule on
+        max(n_self, n_other) uniform times over the union of both ranges;
+        sqrt(integral / duration / number of columns)."""
+        blocks = (("state", states), ("control", controls), ("multiplier", multipliers),
+                  ("derivative", derivatives))
+        chosen = []
+        for kind, names in blocks:
+            mine, theirs = getattr(self, kind + "_names"), getattr(other, kind + "_names")
+            if names is None:
+                if sorted(mine) != sorted(theirs):
+                    raise ValueError(f"Expected both trajectories to have the same {kind} names; "
+                                     f"consider specifying the {kind}s to compare.")
+                names = list(mine)
+            elif list(names) == ["none"]:
+                names = []
+            else:
+                for n in names:
+                    if n not in mine or n not in theirs:
+                        raise ValueError(f"Expected '{n}' to be a {kind} in both trajectories.")
+            chosen.append((kind + "s", list(names)))
+        ncols = sum(len(n) for _, n in chosen)
+        if ncols == 0:
+            return 0.0
+        t0 = min(self.time[0], other.time[0])
+        tf = max(self.time[-1], other.time[-1])
+        nt = max(self.num_times, other.num_times)
+        tt = np.linspace(t0, tf, nt)
+        dt = tt[1] - tt[0]
+
+        def sampled(traj, block, names):
+            labels = getattr(traj, block[:-1] + "_names")
+            data = getattr(traj, block)[:, [labels.index(n) for n in names]]
+            degree = min(traj.num_times - 1, 5)
+            if degree % 2 == 0:
+                raise ValueError(f"GCVSpline degree must be odd (got {degree} for {traj.num_times} times)")
+            br, co = gcv_interpolating_ppoly(traj.time, data, degree)
+            inside = (traj.time[0] <= tt) & (tt <= traj.time[-1])
+            out = np.zeros((nt, len(names)))
+            for c in range(len(names)):
+                out[inside, c] = ppoly_eval(br, co, tt[inside], c)
+            return out
+
+        sse = np.zeros(nt)
+        for block, names in chosen:
+            if names:
+                sse += ((sampled(self, block, names) - sampled(other, block, names)) ** 2).sum(axis=1)
+        integral = dt / 2.0 * (sse.sum() + sse[1:nt - 1].sum())
+        return float(np.sqrt(integral / (tf - t0) / ncols))
+
+    def compare_parameters_rms(self, other: "MocoTrajectory", names=None) -> float:
+        """compareParametersRMS (MocoTrajectory.cpp:1311-1340)."""
+        if names is None:
+            if sorted(self.parameter_names) != sorted(other.parameter_names):
+                raise ValueError("Expected both trajectories to have the same parameter names; "
+                                 "consider specifying the parameters to compare.")
+            names = list(self.parameter_names)
+        err = [(self.parameters[self.parameter_names.index(n)]
+                - other.parameters[other.parameter_names.index(n)]) ** 2 for n in names]
+        return float(np.sqrt(sum(err) / len(names)))
+
     def is_numerically_equal(self, other: "MocoTrajectory", tol: float = 1e-12) -> bool:
         if self.labels() != other.labels() or self.num_times != other.num_times:
             return False

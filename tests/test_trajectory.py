@@ -168,3 +168,41 @@ def test_ipopt_option_mapping():
     s.optim_convergence_tolerance, s.verbosity = -1, 3
     with pytest.raises(ValueError):
         s.ipopt_options()
+
+
+def _rms_pair(offset, n=21, shift=0.0):
+    t = np.linspace(0.0, 1.0, n)
+    s = np.column_stack([np.sin(3 * t), t ** 2])
+    c = np.column_stack([np.cos(t)])
+    a = MocoTrajectory(t, ["q", "u"], ["e"], [], [], [], ["p"], s, c, parameters=np.array([1.0]))
+    s2 = s.copy()
+    s2[:, 1] += offset
+    b = MocoTrajectory(t + shift, ["q", "u"], ["e"], [], [], [], ["p"], s2, c.copy(),
+                       parameters=np.array([1.5]))
+    return a, b
+
+
+def test_compare_continuous_variables_rms():
+    """compareContinuousVariablesRMS (MocoTrajectory.cpp:1131-1263): zero for
+    identical trajectories, c / sqrt(columns) for a constant offset c in one
+    of the compared columns (the trapezoidal rule integrates a constant
+    exactly), block selection by names and "none", and the name checks."""
+    a, b = _rms_pair(0.0)
+    assert a.compare_continuous_variables_rms(b) == pytest.approx(0.0, abs=1e-12)
+    a, b = _rms_pair(0.3)
+    assert a.compare_continuous_variables_rms(b) == pytest.approx(0.3 / np.sqrt(3), rel=1e-9)
+    assert a.compare_continuous_variables_rms(b, states=["u"], controls=["none"]) == \
+        pytest.approx(0.3, rel=1e-9)
+    assert a.compare_continuous_variables_rms(b, states=["q"]) == pytest.approx(0.0, abs=1e-12)
+    assert a.compare_continuous_variables_rms(b, states=["none"], controls=["none"]) == 0.0
+    with pytest.raises(ValueError):
+        a.compare_continuous_variables_rms(b, states=["w"])
+    c = MocoTrajectory(a.time, ["q"], ["e"], [], [], [], [], a.states[:, :1], a.controls)
+    with pytest.raises(ValueError):
+        a.compare_continuous_variables_rms(c)
+    # disjoint halves: each is compared against 0 where the other has no data
+    a, b = _rms_pair(0.0, shift=0.5)
+    assert a.compare_continuous_variables_rms(b) > 0.1
+    # parameters (compareParametersRMS, :1311-1340)
+    assert a.compare_parameters_rms(b) == pytest.approx(0.5)
+    assert a.compare_parameters_rms(a) == 0.0
