@@ -520,6 +520,9 @@ typedef struct mh_nlp_info {
 
 int mh_abi_version(void);
 const char* mh_last_error(void);
+/* Source hash the library was built from (tools/build_id.py: SHA-256 of
+ * csrc/ and this header); lets a host detect a stale prebuilt library. */
+const char* mh_build_id(void);
 
 int mh_create(const mh_problem* problem, const mh_options* options,
         mh_ctx** ctx);

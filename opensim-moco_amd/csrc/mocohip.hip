@@ -49,6 +49,10 @@ static int set_err(int code, const char* fmt, ...) {
     } while (0)
 
 extern "C" int mh_abi_version(void) { return MH_ABI_VERSION; }
+#ifndef MH_BUILD_ID
+#define MH_BUILD_ID "unknown"
+#endif
+extern "C" const char* mh_build_id(void) { return MH_BUILD_ID; }
 extern "C" const char* mh_last_error(void) { return g_err.c_str(); }
 
 // Transcription stage of the split path, one launch: blockIdx.y = mesh

@@ -197,6 +197,7 @@ class mh_nlp_info(C.Structure):
 # C-ABI test checks every one is exported (and matches include/mocohip.h).
 MOCOHIP_SYMBOLS = {
     "mh_abi_version": (i32, []),
+    "mh_build_id": (C.c_char_p, []),
     "mh_last_error": (C.c_char_p, []),
     "mh_create": (i32, [P(mh_problem), P(mh_options), P(C.c_void_p)]),
     "mh_destroy": (None, [C.c_void_p]),
@@ -297,8 +298,27 @@ def load_mocohip(path: str | None = None):
         if lib.mh_abi_version() != MH_ABI_VERSION:
             raise RuntimeError(f"{path}: ABI version {lib.mh_abi_version()}, "
                                f"this binding expects {MH_ABI_VERSION}; rebuild")
+        want = tree_build_id()
+        have = lib.mh_build_id().decode()
+        if want is not None and have != want:
+            raise RuntimeError(f"{path} was built from other sources (build id {have}, the tree's "
+                               f"is {want}); rebuild with __graft_entry__.build()")
         _libs[path] = lib
     return _libs[path]
+
+
+def tree_build_id():
+    """The source hash of the tree (tools/build_id.py), or None when the
+    sources are not present."""
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    tool = os.path.join(root, "tools", "build_id.py")
+    if not os.path.exists(tool):
+        return None
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("_mh_build_id", tool)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod.build_id()
 
 
 def load_oracle(path: str | None = None):

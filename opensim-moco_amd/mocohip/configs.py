@@ -275,6 +275,29 @@ def gait10dof18musc(num_mesh_intervals: int = 200, muscles: bool = True,
     return MocoStudy(p, s)
 
 
+def gait10dof18musc_track(num_mesh_intervals: int = 65) -> MocoStudy:
+    """The reference's MocoTrack golden-solution problem (testMocoTrack.cpp:
+    46-68): gait10dof18musc | ModOpRemoveMuscles | ModOpAddReserves(100) |
+    ModOpAddExternalLoads; states reference walk_gait1018_state_reference.mot
+    | TabOpLowPassFilter(6) tracked with weight 1 (GCVSpline of degree 5),
+    control effort 0.001, time [0.01, 1.3], mesh_interval 0.02 (N = 65),
+    explicit dynamics, forward differences, convergence and constraint
+    tolerances 1e-2, bounds guess (MocoTrack.cpp:54-132).  Its converged
+    solution is std_testMocoTrackGait10dof18musc_solution.sto."""
+    from .splines import filter_lowpass_table
+    m = gait10dof18musc_model(muscles=False)
+    ref = _load("walk_gait1018_state_reference.json")
+    tp, cols = filter_lowpass_table(ref["time"], {k: np.asarray(v) for k, v in ref["columns"].items()}, 6.0)
+    m.add_table(DataTable("state_reference", tp, cols, degree=5))
+    p = MocoProblem(m)
+    p.add_goal(MocoStateTrackingGoal("state_tracking", 1.0, DataTable("state_reference", tp, cols, degree=5)))
+    p.add_goal(MocoControlGoal("control_effort", 0.001))
+    p.set_time_bounds(0.01, 1.3)
+    s = MocoHipSolver(num_mesh_intervals=num_mesh_intervals, optim_finite_difference_scheme="forward",
+                      optim_convergence_tolerance=1e-2, optim_constraint_tolerance=1e-2)
+    return MocoStudy(p, s)
+
+
 def gait10dof18musc_inverse(num_mesh_intervals: int = 25, fd_scheme: str = "forward",
                             sparsity: str = "random") -> MocoStudy:
     """MocoInverse on gait10dof18musc (configs[4], one solve of the batch):
@@ -304,7 +327,10 @@ def gait10dof18musc_inverse(num_mesh_intervals: int = 25, fd_scheme: str = "forw
     s = MocoHipSolver(num_mesh_intervals=num_mesh_intervals,
                       optim_finite_difference_scheme=fd_scheme, multibody_dynamics_mode="implicit",
                       interpolate_control_midpoints=False,   # MocoInverse.cpp:105
-                      optim_sparsity_detection=sparsity)
+                      optim_sparsity_detection=sparsity,
+                      # MocoInverse convergence / constraint tolerance
+                      # defaults (MocoInverse.cpp:38-39, 108-109)
+                      optim_convergence_tolerance=1e-3, optim_constraint_tolerance=1e-3)
     return MocoStudy(p, s)
 
 
@@ -415,7 +441,8 @@ def rajagopal18_inverse(num_mesh_intervals: int = 11, fd_scheme: str = "forward"
     p.add_goal(ImplicitAuxiliaryDerivativesTerm(weight=0.01))
     s = MocoHipSolver(num_mesh_intervals=num_mesh_intervals,
                       optim_finite_difference_scheme=fd_scheme, multibody_dynamics_mode="implicit",
-                      interpolate_control_midpoints=False, optim_sparsity_detection=sparsity)
+                      interpolate_control_midpoints=False, optim_sparsity_detection=sparsity,
+                      optim_convergence_tolerance=1e-3, optim_constraint_tolerance=1e-3)
     return MocoStudy(p, s)
 
 
@@ -468,6 +495,7 @@ CONFIGS = {
     "double_pendulum_coupled": double_pendulum_coupled,
     "gait10dof18musc": gait10dof18musc,
     "gait10dof18musc_inverse": gait10dof18musc_inverse,
+    "gait10dof18musc_track": gait10dof18musc_track,
     "wrapped_pendulum": wrapped_pendulum,
     "rajagopal18_inverse": rajagopal18_inverse,
     "rajagopal80": rajagopal80,

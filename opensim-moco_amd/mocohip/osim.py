@@ -249,7 +249,13 @@ def _muscle_to_dgf(m, tendon_compliance: Optional[bool],
         d.tendon_compliance_dynamics_mode = _text(m, "tendon_compliance_dynamics_mode", "explicit")
     else:
         raise NotImplementedError(f"muscle {tag}")
-    d.min_control = _float(m, "min_control", 0.0 if tag != "DeGrooteFregly2016Muscle" else 0.0)
+    # Millard2012EquilibriumMuscle keeps its excitation above its
+    # minimum_activation (default 0.01): that is the min_control a
+    # DeGrooteFregly2016Muscle inherits in replaceMuscles
+    # (DeGrooteFregly2016Muscle.cpp:994-995); the MocoInverse golden solution
+    # std_testMocoInverse_subject_18musc_solution.sto sits on 0.01.
+    lo_default = _float(m, "minimum_activation", 0.01) if tag == "Millard2012EquilibriumMuscle" else 0.0
+    d.min_control = _float(m, "min_control", lo_default)
     d.max_control = _float(m, "max_control", 1.0)
     d.max_isometric_force = _float(m, "max_isometric_force", 1000.0)
     d.optimal_fiber_length = _float(m, "optimal_fiber_length", 0.1)

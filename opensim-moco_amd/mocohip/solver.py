@@ -634,30 +634,35 @@ class MocoStudy:
         rep = self.problem.create_rep()
         return HipNLP(rep, self.solver.options(interval_begin, interval_end))
 
-    def solve(self, guess=None, nlp=None):
+    def solve(self, guess=None, nlp=None, method: str = "ipm"):
         """MocoStudy::solve (MocoStudy.cpp:79-101): transcribe on the HIP
         path, optimize from the solver's starting point, return the
         solution as a MocoTrajectory with the solve statistics in its
         metadata (success, objective, num_iterations, solver_duration,
         status; MocoSolver::setSolutionStats, MocoSolver.h:97-102).  The
-        optimizer is mocohip.nlpsolve (Ipopt is absent here); tolerances
-        from optim_convergence_tolerance / optim_constraint_tolerance
-        (default 1e-8), optim_max_iterations."""
+        optimizer is mocohip.nlpsolve (Ipopt is absent here; default the
+        interior-point restatement mocohip.ipm) with the Ipopt options
+        MocoCasADiSolver sets from optim_convergence_tolerance /
+        optim_constraint_tolerance / optim_max_iterations
+        (MocoHipSolver.ipopt_options; Ipopt's defaults where unset)."""
         from .nlpsolve import solve_nlp
         from .trajectory import MocoTrajectory
         own = nlp is None
         nlp = nlp or self.create_nlp()
-        x0 = self.solver.starting_point(nlp, guess)
-        s = self.solver
-        tol = s.optim_convergence_tolerance if s.optim_convergence_tolerance > 0 else 1e-8
-        ctol = s.optim_constraint_tolerance if s.optim_constraint_tolerance > 0 else 1e-8
-        it = s.optim_max_iterations if s.optim_max_iterations > 0 else 5000
-        r = solve_nlp(nlp, x0, tol, ctol, it)
-        sol = MocoTrajectory.from_iterate(nlp, r.x)
+        try:
+            x0 = self.solver.starting_point(nlp, guess)
+            s = self.solver
+            tol = s.optim_convergence_tolerance if s.optim_convergence_tolerance > 0 else 1e-8
+            ctol = s.optim_constraint_tolerance if s.optim_constraint_tolerance > 0 else 1e-8
+            it = s.optim_max_iterations if s.optim_max_iterations > 0 else 5000
+            r = solve_nlp(nlp, x0, tol, ctol, it, method=method,
+                          ipopt_options=s.ipopt_options() if method == "ipm" else None)
+            sol = MocoTrajectory.from_iterate(nlp, r.x)
+        finally:
+            if own:
+                nlp.close()
         sol.metadata.update({"success": "true" if r.success else "false", "objective": repr(r.objective),
                              "num_iterations": str(r.iterations), "solver_duration": repr(r.duration),
-                             "status": r.status, "optimizer": "scipy trust-constr over the C ABI"})
+                             "status": r.status, "optimizer": r.optimizer + " over the C ABI"})
         sol.stats = r
-        if own:
-            nlp.close()
         return sol
