@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define MH_ABI_VERSION 5
+#define MH_ABI_VERSION 6
 
 enum mh_status {
     MH_OK = 0,
@@ -488,7 +488,27 @@ typedef struct mh_options {
      * contexts only. */
     int32_t jacobian_mode;
     int32_t reserved_jm;
+    /* (ABI v6) How detection decides a coupling (mh_sparsity_rule).
+     * ROBUST (0, default): output k depends on input j iff its change under
+     * the +1e-5 perturbation is NaN or exceeds 1e-12 * the callback's
+     * magnitude at the detection iterate (max(1, max over its outputs of
+     * |output|)) -- a true dependency changes an output by ~1e-5 *
+     * d(output) / d(input), the rounding noise of a coupling that cancels
+     * stays within ~64 eps of the callback's magnitude (1.4e-14), so the
+     * pattern is a property of the model: the same on the device and in any
+     * other implementation.  ANY_CHANGE (1): the reference's rule
+     * (CasOCFunction.cpp:44-61: any nonzero change or NaN), under which
+     * couplings that cancel to rounding level (a muscle on a coordinate it
+     * does not cross) are detected or not depending on the order of the
+     * floating-point operations: implementation-dependent. */
+    int32_t sparsity_rule;
+    int32_t reserved_sr;
 } mh_options;
+
+enum mh_sparsity_rule { MH_SPARSITY_RULE_ROBUST = 0, MH_SPARSITY_RULE_ANY_CHANGE = 1 };
+/* ROBUST: the change, relative to the callback's magnitude, below which a
+ * detection probe counts as rounding noise. */
+#define MH_SPARSITY_ROBUST_TOL 1e-12
 
 enum mh_jacobian_mode { MH_JACOBIAN_CALLBACK_FD = 0, MH_JACOBIAN_GLOBAL_SEEDS = 1 };
 
@@ -615,6 +635,13 @@ int mh_eval_dae(mh_ctx* ctx, int32_t npoints, const double* inputs,
  * used to select it. */
 int mh_get_backend(const mh_ctx* ctx, char* name, int32_t name_len,
         double* flops_per_eval, uint64_t* model_hash);
+/* The back end mh_create would select for this problem and options, without
+ * a device (host only): "generated:<label>" when a model-specialized back
+ * end's structure (topology, joint / path / wrap / constraint wiring, the
+ * zero pattern of the numbers; not their values) matches the model, else
+ * "generic-<size class>". */
+int mh_backend_for(const mh_problem* problem, const mh_options* options, char* name,
+        int32_t name_len);
 /* Kernel variants this context launches, as a space-separated list
  * ("tasks interval" = task kernels with the fused per-interval transcription
  * for the Jacobian lanes; "lane", "generic", "split", ...). */

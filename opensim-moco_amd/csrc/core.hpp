@@ -244,6 +244,20 @@ __global__ void __launch_bounds__(64) k_exc_lanes(DevModel M, Layout L, Lanes Ln
 
 // Inputs of one evaluation lane read where used (L1/L2-resident x) instead
 // of held in VGPRs.
+// Point inputs are [states NS, controls NC, derivatives NDV, multipliers
+// NM, slacks NSL] (mh_create's layout); the slacks are the interval's at a
+// mesh-interval midpoint (Hermite-Simpson with enforced constraint
+// derivatives) and 0 elsewhere (xl null).
+template <class D>
+__device__ __forceinline__ double point_input(const double* __restrict__ xs, const double* __restrict__ xc,
+        const double* __restrict__ xd, const double* __restrict__ xm, const double* __restrict__ xl, int i) {
+    constexpr int NDV = D::NI - D::NS - D::NC - D::NM - D::NSL;
+    if (i < D::NS) return xs[i];
+    if (i < D::NS + D::NC) return xc[i - D::NS];
+    if (i < D::NS + D::NC + NDV) return xd[i - D::NS - D::NC];
+    if (i < D::NS + D::NC + NDV + D::NM) return xm[i - D::NS - D::NC - NDV];
+    return xl ? xl[i - D::NS - D::NC - NDV - D::NM] : 0.0;
+}
 template <class D>
 struct LaneIn {
     const double* __restrict__ xs;
@@ -251,19 +265,23 @@ struct LaneIn {
     const double* __restrict__ xd;   // implicit: accelerations (inputs NS + NC ..)
     int pi;
     double step;
+    const double* __restrict__ xm;   // kinematic-constraint multipliers
+    const double* __restrict__ xl;   // velocity-correction slacks (null: none at this point)
     __device__ __forceinline__ double operator[](int i) const {
-        const double v = i < D::NS ? xs[i] : (i < D::NS + D::NC ? xc[i - D::NS] : xd[i - D::NS - D::NC]);
+        const double v = point_input<D>(xs, xc, xd, xm, xl, i);
         return i == pi ? v + step : v;
     }
 };
 
 // Where lane inputs come from: the NLP iterate x (grid times) or explicit
-// points [t, states, controls] (mh_eval_dae).
+// points [t, point inputs] (mh_eval_dae).  XM / XL / DB: x index of the
+// multipliers, slacks and derivative variables (make_layout).
 struct Src {
     const double* x;
     const double* grid;
     const double* pts;   // non-null: explicit points
     int G, k0;
+    long XM, XL, DB;
 };
 
 // Same, reading a grid point's inputs staged in LDS (k_interval).
@@ -274,8 +292,16 @@ struct LaneInL {
     const lds_double* xd;
     int pi;
     double step;
+    const lds_double* xm;
+    const lds_double* xl;   // null: no slacks at this point
     __device__ __forceinline__ double operator[](int i) const {
-        const double v = i < D::NS ? xs[i] : (i < D::NS + D::NC ? xc[i - D::NS] : xd[i - D::NS - D::NC]);
+        constexpr int NDV = D::NI - D::NS - D::NC - D::NM - D::NSL;
+        double v;
+        if (i < D::NS) v = xs[i];
+        else if (i < D::NS + D::NC) v = xc[i - D::NS];
+        else if (i < D::NS + D::NC + NDV) v = xd[i - D::NS - D::NC];
+        else if (i < D::NS + D::NC + NDV + D::NM) v = xm[i - D::NS - D::NC - NDV];
+        else v = xl ? xl[i - D::NS - D::NC - NDV - D::NM] : 0.0;
         return i == pi ? v + step : v;
     }
 };
@@ -303,15 +329,17 @@ __device__ __forceinline__ double lane_time(const Lanes& Ln, double g, double t0
 template <class D>
 __device__ __forceinline__ LaneIn<D> lane_input(const Src& S, const Lanes& Ln, int kl, int r,
         double& t) {
+    constexpr int NDV = D::NI - D::NS - D::NC - D::NM - D::NSL;
     if (S.pts) {
         const double* p = S.pts + (long)kl * (1 + D::NI);
         t = p[0];
-        return LaneIn<D>{p + 1, p + 1 + D::NS, p + 1 + D::NS + D::NC, -1, 0.0};
+        const double* pm = p + 1 + D::NS + D::NC + NDV;
+        return LaneIn<D>{p + 1, p + 1 + D::NS, p + 1 + D::NS + D::NC, -1, 0.0, pm, pm + D::NM};
     }
     const int k = S.k0 + kl;
-    constexpr int NDV = D::NI - D::NS - D::NC;
     LaneIn<D> in{S.x + 2 + (long)k * D::NS, S.x + 2 + (long)D::NS * S.G + (long)k * D::NC,
-                 S.x + 2 + (long)(D::NS + D::NC) * S.G + (long)k * NDV, -1, 0.0};
+                 S.x + S.DB + (long)k * NDV, -1, 0.0, S.x + S.XM + (long)k * D::NM,
+                 (D::NSL > 0 && (k & 1)) ? S.x + S.XL + (long)((k - 1) >> 1) * D::NSL : nullptr};
     t = lane_time(Ln, S.grid[k], S.x[0], S.x[1], r, in.pi, in.step);
     return in;
 }
@@ -969,8 +997,10 @@ __device__ __forceinline__ void interval_body(const DevModel& M, const Src& S, c
     double* sT = sK + CT_NCONST;             // [npts][nt] (GM: none)
     double* sH = sT + (GM ? 0 : npts * nt);  // [npts][nh] (GM: none)
     double* sXs = sH + (GM ? 0 : npts * nh); // [npts][NS] states, [npts][NC] controls,
-    double* sXc = sXs + npts * L.NS;         // [npts][NDV] accelerations (implicit)
-    double* sXd = sXc + npts * L.NC;
+    double* sXc = sXs + npts * L.NS;         // [npts][NDV] accelerations (implicit),
+    double* sXd = sXc + npts * L.NC;         // [npts][NM] multipliers, [NSL] the
+    double* sXm = sXd + npts * L.NDV;        // interval's slacks (HS midpoint)
+    double* sXl = sXm + npts * L.NM;
     // the interval's points are consecutive local grid points: their T (and
     // H) slabs are one contiguous run each
     const int kl0 = k_first - S.k0;
@@ -981,13 +1011,16 @@ __device__ __forceinline__ void interval_body(const DevModel& M, const Src& S, c
     if (L.NC > 0) stage_lds<1>(sXc, S.x + 2 + (long)L.NS * L.G + (long)k_first * L.NC, npts * L.NC);
     if (L.NDV > 0)
         stage_lds<1>(sXd, S.x + L.DB + (long)k_first * L.NDV, npts * L.NDV);
+    if (L.NM > 0) stage_lds<1>(sXm, S.x + L.XM + (long)k_first * L.NM, npts * L.NM);
+    if (L.NSL > 0) stage_lds<1>(sXl, S.x + L.XL + (long)i * L.NSL, L.NSL);
     const double t0 = S.x[0], tf = S.x[1];
     if (threadIdx.x < 2) sK[threadIdx.x] = threadIdx.x ? 1.0 : 0.0;
     __syncthreads();
     if (I.dbg_stop == 1) return;
     for (int w = threadIdx.x; w < npts * Ln.stride; w += blockDim.x) {
         const int p = w / Ln.stride, r = w - p * Ln.stride;
-        LaneInL<D> in{lds(sXs + p * L.NS), lds(sXc + p * L.NC), lds(sXd + p * L.NDV), -1, 0.0};
+        LaneInL<D> in{lds(sXs + p * L.NS), lds(sXc + p * L.NC), lds(sXd + p * L.NDV), -1, 0.0,
+                      lds(sXm + p * L.NM), L.vc(k_first + p) ? lds(sXl) : nullptr};
         const double t = lane_time(Ln, S.grid[k_first + p], t0, tf, r, in.pi, in.step);
         if (r == Ln.base) sTimes[p] = t;
         double out[D::NO];
@@ -1197,10 +1230,10 @@ struct BatchPtrs {
 // VGPRs; more waves hide the transcendental latency of a batch's many tasks)
 template <class D, int W>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(W > 0 ? W : 1)))
-kb_groups(const BatchItem* __restrict__ items, BatchPtrs BP, Lanes Ln, Tasks TK, int G, int k0) {
+kb_groups(const BatchItem* __restrict__ items, BatchPtrs BP, Lanes Ln, Tasks TK, Layout L) {
     const int b = blockIdx.y;
     const BatchItem& it = items[b];
-    const Src S{BP.x[b], it.grid, nullptr, G, k0};
+    const Src S{BP.x[b], it.grid, nullptr, L.G, L.k0, L.XM, L.XL, L.DB};
     groups_body<D>(it.M, S, Ln, TK, it.T, it.H, blockIdx.x);
 }
 
@@ -1210,7 +1243,7 @@ __global__ void __launch_bounds__(1024) kb_interval(const BatchItem* __restrict_
         const int* __restrict__ ctgen, int nctgen, int with_g, int with_v, int nep, int nnz_ep) {
     const int b = blockIdx.y;
     const BatchItem& it = items[b];
-    const Src S{BP.x[b], it.grid, nullptr, L.G, L.k0};
+    const Src S{BP.x[b], it.grid, nullptr, L.G, L.k0, L.XM, L.XL, L.DB};
     Interval I = I0;
     I.P = it.P;
     I.E = it.E;
@@ -1722,6 +1755,7 @@ struct TaskSet {
     size_t t_doubles = 0, h_doubles = 0;
 };
 struct Backend;
+struct GenEntry;
 
 struct mh_ctx {
     // problem
@@ -1766,6 +1800,7 @@ struct mh_ctx {
     double h = 1e-8;
     int size_class = 0;
     const struct Backend* be = nullptr;
+    const struct GenEntry* gen = nullptr;   // the generated back end's entry (match / fill), if any
     Lanes lanes_jac{}, lanes_g{};
     uint64_t model_hash = 0;
     int64_t n = 0, m = 0, nnz = 0;
@@ -1875,6 +1910,12 @@ inline Interval make_interval(const mh_ctx* c, double*& g, double*& v) {
     return I;
 }
 
+// Lane inputs from the iterate x (device pointer).
+inline Src src_of(const mh_ctx* c, const double* x) {
+    const Layout L = make_layout(c, c->k0, c->nk);
+    return Src{x, c->d_grid, nullptr, c->G, c->k0, L.XM, L.XL, L.DB};
+}
+
 // Task tables and T/H buffers for an mh_eval_dae call (mocohip.hip).
 int probe_tasks(mh_ctx* c, const TaskInfo& ti, const Lanes& ln, int np);
 
@@ -1962,7 +2003,7 @@ static int launch_tasks(mh_ctx* c, const Src& S, const Lanes& ln, const TaskSet&
 }
 template <class D>
 static void be_eval_tasks(mh_ctx* c, const double* x, int mode, double* Y) {
-    const Src S{x, c->d_grid, nullptr, c->G, c->k0};
+    const Src S = src_of(c, x);
     const Lanes& ln = mode ? c->lanes_jac : c->lanes_g;
     const TaskSet& ts = mode ? c->ts_jac : c->ts_g;
     if (c->use_interval[mode]) {   // combine happens inside k_interval
@@ -1977,7 +2018,7 @@ template <class D>
 static size_t interval_lds(const mh_ctx* c, const Lanes& ln, const TaskSet& ts) {
     const size_t npts = c->scheme == MH_HERMITE_SIMPSON ? 3 : 2;
     return sizeof(double) * (npts * D::NO * ln.stride + CT_CONST + CT_NCONST +
-                             npts * (size_t)(c->NS + c->NC + c->NDV) +
+                             npts * (size_t)(c->NS + c->NC + c->NDV + c->NM) + (size_t)c->NSL +
                              npts * ((size_t)ts.dev.tdoubles + (size_t)ts.dev.nmass * D::NST));
 }
 // LDS bytes of k_role (Jacobian lanes).
@@ -1999,7 +2040,7 @@ template <class D>
 static size_t interval_lds_gm(const mh_ctx* c, const Lanes& ln) {
     const size_t npts = c->scheme == MH_HERMITE_SIMPSON ? 3 : 2;
     return sizeof(double) * (npts * D::NO * ln.stride + CT_CONST + CT_NCONST +
-                             npts * (size_t)(c->NS + c->NC + c->NDV));
+                             npts * (size_t)(c->NS + c->NC + c->NDV + c->NM) + (size_t)c->NSL);
 }
 template <class D>
 static void be_batch(mh_batch* bt, int mode, const BatchPtrs& BP, int with_g, int with_v) {
@@ -2008,9 +2049,9 @@ static void be_batch(mh_batch* bt, int mode, const BatchPtrs& BP, int with_g, in
     const TaskSet& ts = mode ? c->ts_jac : c->ts_g;
     const unsigned B = (unsigned)bt->B;
     auto kg = bt->waves == 3 ? kb_groups<D, 3> : kb_groups<D, 0>;
-    hipLaunchKernelGGL(kg, dim3((unsigned)ts.nblocks, B), dim3(64), 0, c->stream, bt->d_items, BP, ln,
-            ts.dev, c->G, c->k0);
     Layout L = make_layout(c, c->k0, c->nk);
+    hipLaunchKernelGGL(kg, dim3((unsigned)ts.nblocks, B), dim3(64), 0, c->stream, bt->d_items, BP, ln,
+            ts.dev, L);
     double *g0 = nullptr, *v0 = nullptr;
     const Interval I = make_interval(c, g0, v0);
     const size_t lds = bt->gm ? interval_lds_gm<D>(c, ln) : interval_lds<D>(c, ln, ts);
@@ -2024,7 +2065,7 @@ static void be_batch(mh_batch* bt, int mode, const BatchPtrs& BP, int with_g, in
 }
 template <class D>
 static void be_interval(mh_ctx* c, const double* x, int mode, double* g, double* v) {
-    const Src S{x, c->d_grid, nullptr, c->G, c->k0};
+    const Src S = src_of(c, x);
     const Lanes& ln = mode ? c->lanes_jac : c->lanes_g;
     const TaskSet& ts = mode ? c->ts_jac : c->ts_g;
     Layout L = make_layout(c, c->k0, c->nk);
@@ -2080,14 +2121,14 @@ template <class D>
 static void be_probe_tasks(mh_ctx* c, int np, const double* in, double* out) {
     const Lanes ln{c->fd, c->NI + 2, 1, 0, c->h};
     if (probe_tasks(c, *c->be->tasks, ln, np) != MH_OK) return;
-    const Src S{nullptr, nullptr, in, 0, 0};
+    const Src S{nullptr, nullptr, in, 0, 0, 0, 0, 0};
     (void)launch_tasks<D>(c, S, ln, c->ts_probe, c->d_pT, c->d_pH, nullptr, out, false);
 }
 template <class D>
 static void be_lanes_lane(mh_ctx* c, const double* x, double* Y) { be_eval_lane<D>(c, x, 1, Y); }
 template <class D>
 static void be_lanes_tasks(mh_ctx* c, const double* x, double* Y) {
-    const Src S{x, c->d_grid, nullptr, c->G, c->k0};
+    const Src S = src_of(c, x);
     (void)launch_tasks<D>(c, S, c->lanes_jac, c->ts_jac, c->d_T, c->d_H, c->d_times, Y, false);
 }
 template <class D>
@@ -2110,9 +2151,39 @@ static constexpr Backend make_backend_tasks(const char* name, double flops) {
 // Generic device-interpreter back ends (generic.hip), one per size class.
 const Backend* generic_backends();
 // A model-specialized back end (generated/gen_<model>.hip): the task kernels
-// (default) and the one-lane-per-DAE kernel (MOCOHIP_BACKEND=lane).
-struct GenEntry { uint64_t hash; Backend tasks, lane; };
-#define MH_GEN_ENTRY(T, H, NAME)                                                   \
-    GenEntry{H, make_backend_tasks<T>("generated:" NAME, T::FLOPS_PER_EVAL),        \
+// (default) and the one-lane-per-DAE kernel (MOCOHIP_BACKEND=lane), for the
+// model structure match() accepts (multibody dynamics mode and prescribed
+// kinematics included); fill() computes a model's constant pool.
+struct GenEntry {
+    bool (*match)(const mh_model&);
+    void (*fill)(const mh_model&, double*);
+    int npool;
+    bool implicit, prescribed;
+    // kinematic constraints: derivatives enforced, velocity-correction slacks
+    bool kc_enforce, kc_slacks;
+    const char* label;
+    Backend tasks, lane;
+};
+#define MH_GEN_ENTRY(T, IMPLICIT, PRESCRIBED, KC_ENFORCE, KC_SLACKS, NAME)                     \
+    GenEntry{&T##_match, &T##_fill, T::NPOOL, IMPLICIT, PRESCRIBED, KC_ENFORCE, KC_SLACKS, NAME, \
+             make_backend_tasks<T>("generated:" NAME, T::FLOPS_PER_EVAL),                   \
              make_backend_lane<T>("generated-lane:" NAME, T::FLOPS_PER_EVAL)}
 
+// 1 / spacing of table ti's breakpoints when a direct-index guess lands
+// within one segment of the right one for every time (codegen.py
+// _uniform_guess, the same arithmetic), else 0.  Host only.
+inline double mh_table_uniform_inv(const mh_model& m, int ti) {
+    if (ti < 0 || ti >= m.ntables) return 0.0;
+    const mh_table& T = m.tables[ti];
+    const int n = T.nseg;
+    if (n < 2) return 0.0;
+    const double* br = m.table_breaks + T.break_begin;
+    const double inv = n / (br[n] - br[0]);
+    if (!std::isfinite(inv) || inv <= 0.0) return 0.0;
+    for (int i = 0; i < n; ++i) {
+        const double lo = std::floor((br[i] - br[0]) * inv);
+        const double hi = std::floor((std::nextafter(br[i + 1], -INFINITY) - br[0]) * inv);
+        if (lo < i - 1 || hi > i + 1) return 0.0;
+    }
+    return inv;
+}

@@ -64,6 +64,9 @@ struct DevModel {
     const mh_path_wrap* pw;
     const int* mus_pw_begin;
     const int* mus_pw_count;
+    // generated back ends: the model's constant pool (codegen.py
+    // "Structure-only specialization"; <Name>_fill at mh_create), else null
+    const double* pool;
 };
 constexpr int MUS_DERIVED = 6;
 
@@ -1047,6 +1050,22 @@ __device__ __forceinline__ int table_segment_u(const double* __restrict__ br, do
     const double lo = br[s], hi = br[s + 1 <= NSEG ? s + 1 : NSEG];
     if (t < lo) s -= 1;
     else if (t >= hi && s < NSEG - 1) s += 1;
+    return s;
+}
+
+// Same with the segment count read at run time (the table's data, not the
+// model structure: another trial's table of another length fits the same
+// generated code); b0 / inv from the model's constant pool.
+__device__ __forceinline__ int table_segment_ur(const double* __restrict__ br, int nseg, double t, double b0,
+        double inv) {
+    if (t <= br[0]) return 0;
+    if (t >= br[nseg]) return nseg - 1;
+    if (t != t) return nseg - 1;
+    int s = (int)((t - b0) * inv);
+    s = s < 0 ? 0 : (s > nseg - 1 ? nseg - 1 : s);
+    const double lo = br[s], hi = br[s + 1 <= nseg ? s + 1 : nseg];
+    if (t < lo) s -= 1;
+    else if (t >= hi && s < nseg - 1) s += 1;
     return s;
 }
 

@@ -39,6 +39,14 @@ struct Reader {
         pos += sizeof(T);
         return v;
     }
+    // n raw bytes (a zeroed buffer past the end, with ok cleared)
+    const char* take(size_t n) {
+        static std::vector<char> zero;
+        if (pos + n > buf.size()) { ok = false; zero.assign(n, 0); return zero.data(); }
+        const char* p = buf.data() + pos;
+        pos += n;
+        return p;
+    }
     template <class T>
     std::vector<T> array(int64_t expected_count) {
         const int64_t bytes = pod<int64_t>();
@@ -103,12 +111,17 @@ bool read_tape(const char* path, Tape& t, std::string& err) {
     t.ns = r.pod<int32_t>();
     t.nc = r.pod<int32_t>();
     // version 4 = ABI v4's mh_options (unchanged in v5); earlier tapes carry a
-    // shorter one; version 5 appends the wrap surfaces
-    if (version != 4 && version != 5) {
-        err = "unsupported tape version (this build reads versions 4 and 5)";
+    // shorter one; version 5 appends the wrap surfaces; version 6 carries ABI
+    // v6's mh_options (+ sparsity_rule: 8 bytes; older tapes leave it 0)
+    if (version < 4 || version > 6) {
+        err = "unsupported tape version (this build reads versions 4 to 6)";
         return false;
     }
-    t.opts = r.pod<mh_options>();
+    {
+        const size_t nopt = version >= 6 ? sizeof(mh_options) : sizeof(mh_options) - 2 * sizeof(int32_t);
+        t.opts = mh_options{};
+        std::memcpy(&t.opts, r.take(nopt), nopt);
+    }
     mh_model& m = t.prob.model;
     int32_t* counts[] = {&m.nq, &m.nbodies, &m.naxes, &m.nfunctions, &m.nknots, &m.nmuscles,
                          &m.npoints, &m.nactuators, &m.ntables, &m.nbreaks, &m.ncoefs, &m.nexternal};

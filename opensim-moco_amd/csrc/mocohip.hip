@@ -743,7 +743,14 @@ static bool compile_template(mh_ctx* c) {
         case T_SIMP_X:
             if (pt == 2) w = ct_word(dx(pt, s, dir), 3, ident ? 2 : 0);
             else if (pt == 0) w = ct_word(dx(pt, s, dir), 3, ident ? 3 : 0);
-            else w = ct_word(dx(pt, s, dir), 4, 0);
+            else if (s < NQ && c->NSL > 0) {
+                // the midpoint's qdot = u + G^T gamma (velocity correction,
+                // CasOCTranscription.cpp:316-333): dxdot = [dir is u_s] +
+                // the correction output's quotient; with the exact 1 it takes
+                // the general path
+                if (dir == 2 + NQ + s) w = CT_GEN;
+                else w = ct_word((uint32_t)((pt * NO + c->OQC + s) * stride + dir), 4, 0);
+            } else w = ct_word(dx(pt, s, dir), 4, 0);
             break;
         case T_TRAP_X:
             w = ct_word(dx(pt, s, dir), 5, ident ? (pt == 1 ? 2 : 3) : 0);
@@ -1256,6 +1263,13 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
                  o_ep = A.put(c->ep.data(), c->ep.size()),
                  o_eptpl = A.put(c->eptpl.data(), c->eptpl.size()),
                  o_kcs = A.put(c->kcs.data(), c->kcs.size());
+    // a generated back end's constant pool for this model
+    std::vector<double> pool;
+    if (c->gen) {
+        pool.assign((size_t)c->gen->npool, 0.0);
+        c->gen->fill(M, pool.data());
+    }
+    const size_t o_pool = A.put(pool.data(), pool.size());
     // compiled template of the Jacobian lanes (k_interval), capacity of the
     // block-dense template (sparsity detection only removes entries)
     if (!compile_template(c.get())) return set_err(MH_ERR_UNSUPPORTED, "Jacobian template does not compile");
@@ -1374,6 +1388,7 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     D.pw = (const mh_path_wrap*)(b + o_pw);
     D.mus_pw_begin = (const int*)(b + o_pwb);
     D.mus_pw_count = (const int*)(b + o_pwc);
+    D.pool = c->gen ? (const double*)(b + o_pool) : nullptr;
     c->GS.ngoals = c->ngoals;
     c->GS.ndv = c->NDV;
     c->GS.nc = c->NC;
@@ -1440,7 +1455,7 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
         const char* ec = std::getenv("MOCOHIP_CTPL");
         c->use_ctpl = !(ec && std::strcmp(ec, "0") == 0);
         const char* er = std::getenv("MOCOHIP_ROLES");
-        c->use_roles = er && std::strcmp(er, "1") == 0;   // measured slower
+        c->use_roles = er && std::strcmp(er, "1") == 0 && c->NM == 0;   // measured slower
         const char* et = std::getenv("MOCOHIP_ROLE_THREADS");
         if (et) c->role_threads = std::min(512, std::max(64, std::atoi(et) / 64 * 64));
         const char* eqf = std::getenv("MOCOHIP_IV_QFUSE");
@@ -2213,8 +2228,26 @@ static double splitmix_uniform(uint64_t& st) {
 // initial_time, the first grid point's variables; iterates per
 // CasOCSolver.cpp:70-92): input j perturbed by +1e-5, a change (or NaN)
 // marks the dependency; OR over the iterates.
+// The coupling test of a detection probe (include/mocohip.h
+// mh_sparsity_rule): d = perturbed - base output, scale = the callback's
+// magnitude at the detection point (sparsity_scale).
+static inline bool sparsity_coupled(int rule, double d, double scale) {
+    if (std::isnan(d)) return true;
+    if (rule == MH_SPARSITY_RULE_ANY_CHANGE) return d != 0;
+    return std::fabs(d) > MH_SPARSITY_ROBUST_TOL * scale;
+}
+static inline double sparsity_scale(const double* y0, int n) {
+    double s = 1.0;
+    for (int k = 0; k < n; ++k)
+        if (std::isfinite(y0[k])) s = std::max(s, std::fabs(y0[k]));
+    return s;
+}
+
 static int detect_sparsity(mh_ctx* c, const mh_options* o) {
     const int W = 1 + c->NI, NO = c->NO, NPC = c->npc;
+    const int rule = o->sparsity_rule;
+    if (rule != MH_SPARSITY_RULE_ROBUST && rule != MH_SPARSITY_RULE_ANY_CHANGE)
+        return set_err(MH_ERR_INVALID, "unknown sparsity rule %d", rule);
     std::vector<double> pts;
     int npts = 1;
     if (o->sparsity_detection == MH_SPARSITY_RANDOM) {
@@ -2309,24 +2342,27 @@ static int detect_sparsity(mh_ctx* c, const mh_options* o) {
     c->sp_ep.assign((size_t)NEP * WE, 0);
     for (int q = 0; q < npts; ++q) {
         const size_t r0 = (size_t)q * (1 + WE);
+        const double se = sparsity_scale(eout.data() + r0 * NEP, NEP);
         for (int j = 0; j < WE; ++j)
             for (int e = 0; e < NEP; ++e) {
                 const double d = eout[(r0 + 1 + j) * NEP + e] - eout[r0 * NEP + e];
-                if (std::isnan(d) || d != 0) c->sp_ep[(size_t)e * WE + j] = 1;
+                if (sparsity_coupled(rule, d, se)) c->sp_ep[(size_t)e * WE + j] = 1;
             }
     }
     c->sp.assign((size_t)NO * W, 0);
     c->sp_pc.assign((size_t)NPC * W, 0);
     for (int q = 0; q < npts; ++q) {
         const size_t r0 = (size_t)q * (1 + W);
+        const double sd = sparsity_scale(out.data() + r0 * NO, NO);
+        const double sp = sparsity_scale(pout.data() + r0 * NPC, NPC);
         for (int j = 0; j < W; ++j) {
             for (int k = 0; k < NO; ++k) {
                 const double d = out[(r0 + 1 + j) * NO + k] - out[r0 * NO + k];
-                if (std::isnan(d) || d != 0) c->sp[(size_t)k * W + j] = 1;
+                if (sparsity_coupled(rule, d, sd)) c->sp[(size_t)k * W + j] = 1;
             }
             for (int e = 0; e < NPC; ++e) {
                 const double d = pout[(r0 + 1 + j) * NPC + e] - pout[r0 * NPC + e];
-                if (std::isnan(d) || d != 0) c->sp_pc[(size_t)e * W + j] = 1;
+                if (sparsity_coupled(rule, d, sp)) c->sp_pc[(size_t)e * W + j] = 1;
             }
         }
     }
@@ -2423,6 +2459,20 @@ extern "C" int mh_get_backend(const mh_ctx* c, char* name, int32_t name_len, dou
     return MH_OK;
 }
 
+extern "C" int mh_backend_for(const mh_problem* p, const mh_options* o, char* name, int32_t name_len) {
+    if (!p || !o || !name || name_len <= 0) return set_err(MH_ERR_INVALID, "bad argument");
+    std::unique_ptr<mh_ctx> c(new mh_ctx());
+    std::vector<int> coord_body, act_state, ftn_state, mus_control;
+    double tau_act, tau_deact;
+    int rc = validate_and_layout(c.get(), p, o, coord_body, act_state, ftn_state, mus_control, tau_act,
+            tau_deact);
+    if (rc) return rc;
+    const Backend* be = select_backend(c.get(), p);
+    std::strncpy(name, be->name, (size_t)name_len - 1);
+    name[name_len - 1] = 0;
+    return MH_OK;
+}
+
 extern "C" int mh_get_callback_sparsity(const mh_ctx* c, uint8_t* pattern, int64_t len) {
     if (!c || !pattern) return set_err(MH_ERR_INVALID, "null argument");
     const size_t W = 1 + (size_t)c->NI, nd = (size_t)c->NO * W, np = nd + (size_t)c->npc * W;
@@ -2466,33 +2516,25 @@ extern "C" int mh_get_work(const mh_ctx* c, double* work4) {
     return MH_OK;
 }
 
-// Generated back ends are keyed by the model hash, salted for implicit
-// multibody dynamics (a different DAE: residual outputs, acceleration
-// inputs, no mass-matrix factor).
-constexpr uint64_t kImplicitSalt = 0x9e3779b97f4a7c15ULL;
-constexpr uint64_t kPrescribedSalt = 0xc2b2ae3d27d4eb4fULL;
-// implicit: residual outputs with acceleration inputs; prescribed: residual
-// outputs with the PositionMotion's q, u, udot (implicit tendons are part of
-// the model hash through mh_muscle)
-static uint64_t backend_key(uint64_t model_hash, bool implicit, bool prescribed) {
-    return model_hash ^ (implicit ? kImplicitSalt : 0) ^ (prescribed ? kPrescribedSalt : 0);
-}
-
 static const Backend* select_backend(mh_ctx* c, const mh_problem* p) {
     c->model_hash = model_hash(&p->model);
     const char* force = std::getenv("MOCOHIP_BACKEND");
     const bool generic = force && std::strcmp(force, "generic") == 0;
     const bool lane = force && std::strcmp(force, "lane") == 0;
-    // the generated back ends carry no kinematic constraints (the model hash
-    // does not cover them): such problems run the generic interpreter
-    if (!generic && c->NKC == 0) {
-        const uint64_t key = backend_key(c->model_hash, c->NMB > 0, c->presc != 0);
+    // a generated back end runs any model of the structure it was generated
+    // for (match: topology, joint / path / wrap / constraint wiring, zero
+    // pattern); its numbers come from the model's constant pool (fill, in
+    // mh_create)
+    if (!generic) {
         for (auto entry : kGeneratedModels) {
             const GenEntry& e = entry();
-            if (e.hash == key) {
-                c->be_lane = &e.lane;
-                return lane ? &e.lane : &e.tasks;
-            }
+            if (e.implicit != (c->NMB > 0) || e.prescribed != (c->presc != 0)) continue;
+            if (c->NKC && !c->presc && (e.kc_enforce != (c->enforce != 0) || e.kc_slacks != (c->NSL > 0)))
+                continue;
+            if (!e.match(p->model)) continue;
+            c->gen = &e;
+            c->be_lane = &e.lane;
+            return lane ? &e.lane : &e.tasks;
         }
     }
     return &generic_backends()[c->size_class];

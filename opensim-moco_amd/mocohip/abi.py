@@ -137,7 +137,7 @@ class mh_goal(C.Structure):
                 ("weight", f64)]
 
 
-MH_ABI_VERSION = 5     # include/mocohip.h
+MH_ABI_VERSION = 6     # include/mocohip.h
 MH_PATH_CONTROL_BOUND = 0
 MH_ENDPOINT_INITIAL_ACTIVATION = 0
 
@@ -179,10 +179,13 @@ class mh_options(C.Structure):
                 ("implicit_aux_bounds", f64 * 2),
                 ("ignore_constraint_derivatives", i32), ("minimize_lagrange_multipliers", i32),
                 ("velocity_correction_bounds", f64 * 2), ("lagrange_multiplier_weight", f64),
-                ("jacobian_mode", i32), ("reserved_jm", i32)]
+                ("jacobian_mode", i32), ("reserved_jm", i32),
+                ("sparsity_rule", i32), ("reserved_sr", i32)]
 
 
 MH_SPARSITY_NONE, MH_SPARSITY_RANDOM, MH_SPARSITY_INITIAL_GUESS, MH_SPARSITY_GIVEN = 0, 1, 2, 3
+MH_SPARSITY_RULE_ROBUST, MH_SPARSITY_RULE_ANY_CHANGE = 0, 1
+MH_SPARSITY_ROBUST_TOL = 1e-12
 
 
 class mh_nlp_info(C.Structure):
@@ -198,6 +201,7 @@ class mh_nlp_info(C.Structure):
 MOCOHIP_SYMBOLS = {
     "mh_abi_version": (i32, []),
     "mh_build_id": (C.c_char_p, []),
+    "mh_backend_for": (i32, [P(mh_problem), P(mh_options), C.c_char_p, i32]),
     "mh_last_error": (C.c_char_p, []),
     "mh_create": (i32, [P(mh_problem), P(mh_options), P(C.c_void_p)]),
     "mh_destroy": (None, [C.c_void_p]),

@@ -4,16 +4,20 @@ Given a compiled model tape (the same mh_model arrays the C ABI receives),
 emit straight-line HIP C++ for the explicit per-point DAE
 (MocoCasOCProblem::calcMultibodySystemExplicit semantics, same algorithm as
 csrc/dae_device.hpp) with every structural constant folded at generation
-time: joint axes, frame offsets, body inertias, path-point layout,
-conditional/moving point logic, actuator wiring.  Zero terms of the 3-D
+time (joint axes and frame orientations, path-point layout,
+conditional/moving point logic, actuator wiring) and every model parameter
+read from a per-model constant pool.  Zero terms of the 3-D
 spatial algebra vanish (planar models lose most of them), all per-lane
 state is scalar temporaries (VGPRs instead of scratch), and the mass matrix
 is factored with Featherstone's fill-free L^T L scheme on the coordinate
 tree.
 
-The generated struct is compiled into libmocohip.so and selected at
-mh_create by the model hash (mh_model_hash); models without a generated
-kernel run the generic device interpreter.
+The generated struct is compiled into libmocohip.so together with two host
+functions: <Name>_match(m), the model structure the code assumes (which
+mh_create checks to select it), and <Name>_fill(m, K), the model's constant
+pool -- every non-structural number the code reads (see "Structure-only
+specialization" below).  Models of no generated structure run the generic
+device interpreter.
 """
 from __future__ import annotations
 
@@ -39,18 +43,146 @@ def lit(v: float) -> str:
 
 
 class S:
-    """A scalar: a folded constant (c) or a named temporary (n)."""
-    __slots__ = ("c", "n")
+    """A scalar: a folded constant (c), a named temporary (n) or a model
+    parameter (p: an entry of the model's constant pool K, loaded at run
+    time; v its value for the model the code was generated from)."""
+    __slots__ = ("c", "n", "p", "v")
 
-    def __init__(self, c=None, n=None):
+    def __init__(self, c=None, n=None, p=None, v=None):
         self.c = c
         self.n = n
+        self.p = p
+        self.v = v
 
     def is_c(self, v=None):
         return self.c is not None and (v is None or self.c == v)
 
+    def is_k(self):
+        """Known before run time: a literal or a pool entry."""
+        return self.c is not None or self.p is not None
+
+    def host(self) -> str:
+        """Its expression in the host pool filler."""
+        return lit(self.c) if self.c is not None else f"K[{self.p}]"
+
+    def value(self) -> float:
+        return self.c if self.c is not None else self.v
+
     def __str__(self):
-        return lit(self.c) if self.c is not None else self.n
+        if self.c is not None:
+            return lit(self.c)
+        return f"K[{self.p}]" if self.p is not None else self.n
+
+
+# ---------------------------------------------------------------------------
+# Structure-only specialization.  A generated back end is compiled for a model
+# STRUCTURE: topology, joint axes and frame orientations, function kinds and
+# knot abscissae, path-point kinds and bodies, wrap and constraint wiring, and
+# which parameters are exactly zero.  Every other number (masses, inertias,
+# frame offsets, path-point locations, muscle properties, time constants,
+# actuator strengths, scale factors ...) is a model PARAMETER: the code reads
+# it, or a constant folded from parameters, from the model's constant pool K
+# (DevModel::pool), which the generated host function fill() computes from
+# the mh_model at mh_create.  The generated host function match() checks the
+# structure the code assumes, so any model of that structure (a scaled
+# subject, a heavier femur, another trial's data) runs the specialized
+# kernels.
+# ---------------------------------------------------------------------------
+class PF(float):
+    """A parametric model value: a float that knows its mh_model path."""
+    __slots__ = ("path",)
+
+    def __new__(cls, v, path):
+        o = float.__new__(cls, v)
+        o.path = path
+        return o
+
+
+class _Ctx:
+    """Per-generation record: the pool (host expression, value) entries and
+    the structural conditions of match()."""
+
+    def __init__(self):
+        self.pool: List[Tuple[str, float]] = []
+        self.index: Dict[str, int] = {}
+        self.checks: Dict[str, None] = {}
+
+    def entry(self, expr: str, value: float) -> "S":
+        i = self.index.get(expr)
+        if i is None:
+            i = len(self.pool)
+            self.pool.append((expr, float(value)))
+            self.index[expr] = i
+        return S(p=i, v=self.pool[i][1])
+
+    def check(self, cond: str):
+        self.checks[cond] = None
+
+
+_CTX: Optional[_Ctx] = None
+
+# mh_* double fields that are model parameters (the rest are structure)
+_PARAM_FIELDS = {
+    "mh_body": {"mass", "com", "inertia", "p_PF", "p_BM"},
+    "mh_function": {"a", "b", "scale"},
+    "mh_path_point": {"loc", "range"},
+    "mh_muscle": {"max_isometric_force", "optimal_fiber_length", "tendon_slack_length",
+                  "pennation_angle_at_optimal", "max_contraction_velocity",
+                  "activation_time_constant", "deactivation_time_constant", "fiber_damping",
+                  "passive_fiber_strain_at_one_norm_force", "tendon_strain_at_one_norm_force",
+                  "active_force_width_scale"},
+    "mh_actuator": {"optimal_force"},
+    "mh_constraint": {"scale"},
+    "mh_wrap_object": {"p_BW", "radius", "length"},
+}
+# fields read at run time from the device tables (data, not structure)
+_RUNTIME_FIELDS = {"mh_table": {"nseg", "break_begin", "coef_begin"}}
+
+
+def _cond_lit(v) -> str:
+    return str(int(v)) if isinstance(v, int) else lit(v)
+
+
+class _Rec:
+    """Recording view of one tape struct (path: its C++ expression on the
+    mh_model m): structural reads add a match() condition, parametric reads
+    return PF values."""
+    __slots__ = ("_s", "_path")
+
+    def __init__(self, s, path):
+        object.__setattr__(self, "_s", s)
+        object.__setattr__(self, "_path", path)
+
+    def __getattr__(self, name):
+        s, path = self._s, self._path
+        v = getattr(s, name)
+        tname = type(s).__name__
+        fpath = f"{path}.{name}"
+        if name in _RUNTIME_FIELDS.get(tname, ()):
+            return v
+        if name in _PARAM_FIELDS.get(tname, ()):
+            if hasattr(v, "__len__"):
+                return [PF(float(v[i]), f"{fpath}[{i}]") for i in range(len(v))]
+            return PF(float(v), fpath)
+        if hasattr(v, "__len__"):
+            vals = [float(v[i]) for i in range(len(v))]
+            for i, x in enumerate(vals):
+                _CTX.check(f"{fpath}[{i}] == {lit(x)}")
+            return vals
+        _CTX.check(f"{fpath} == {_cond_lit(v)}")
+        return v
+
+
+class _RecArr:
+    """Recording view of a double array of the tape (knot abscissae)."""
+
+    def __init__(self, arr, path):
+        self.arr, self.path = arr, path
+
+    def __getitem__(self, i):
+        v = float(self.arr[i])
+        _CTX.check(f"{self.path}[{i}] == {lit(v)}")
+        return v
 
 
 class Gen:
@@ -83,6 +215,13 @@ class Gen:
         return S(c=float(v))
 
     # -- arithmetic with folding -----------------------------------------------
+    # Literal (c) operands fold in Python; parameter (p) operands fold into a
+    # new pool entry (the host filler computes it once per model); the
+    # identities 0 / 1 / -1 apply to literals only.
+    @staticmethod
+    def _kfold(a: S, b: S, op: str, value: float) -> S:
+        return _CTX.entry(f"({a.host()} {op} {b.host()})", value)
+
     def add(self, a: S, b: S) -> S:
         if a.is_c() and b.is_c():
             return S(c=a.c + b.c)
@@ -90,6 +229,8 @@ class Gen:
             return b
         if b.is_c(0.0):
             return a
+        if a.is_k() and b.is_k():
+            return self._kfold(a, b, "+", a.value() + b.value())
         return self.tmp(f"{a} + {b}", "add")
 
     def sub(self, a: S, b: S) -> S:
@@ -99,11 +240,15 @@ class Gen:
             return a
         if a.is_c(0.0):
             return self.neg(b)
+        if a.is_k() and b.is_k():
+            return self._kfold(a, b, "-", a.value() - b.value())
         return self.tmp(f"{a} - {b}", "add")
 
     def neg(self, a: S) -> S:
         if a.is_c():
             return S(c=-a.c)
+        if a.p is not None:
+            return _CTX.entry(f"(-{a.host()})", -a.v)
         return self.tmp(f"-{a}")
 
     def mul(self, a: S, b: S) -> S:
@@ -119,6 +264,8 @@ class Gen:
             return self.neg(b)
         if b.is_c(-1.0):
             return self.neg(a)
+        if a.is_k() and b.is_k():
+            return self._kfold(a, b, "*", a.value() * b.value())
         return self.tmp(f"{a} * {b}", "mul")
 
     def div(self, a: S, b: S) -> S:
@@ -128,11 +275,15 @@ class Gen:
             return S(c=0.0)
         if b.is_c(1.0):
             return a
+        if a.is_k() and b.is_k():
+            return self._kfold(a, b, "/", a.value() / b.value())
         return self.tmp(f"{a} / {b}", "div")
 
     def fn(self, name: str, a: S) -> S:
         if a.is_c():
             return S(c=getattr(math, name)(a.c))
+        if a.p is not None:
+            return _CTX.entry(f"std::{name}({a.host()})", getattr(math, name)(a.v))
         return self.tmp(f"{name}({a})", "fn")
 
     def sel(self, cond: str, a: S, b: S) -> S:
@@ -206,6 +357,14 @@ class Gen:
 
 
 def _c(v):
+    """A constant of the generated code: a literal, or -- for a model
+    parameter (PF) -- its pool entry, unless it is exactly zero (a
+    structural zero: folded, and checked by match())."""
+    if isinstance(v, PF):
+        if float(v) == 0.0:
+            _CTX.check(f"{v.path} == 0.0")
+            return S(c=0.0)
+        return _CTX.entry(v.path, float(v))
     return S(c=float(v))
 
 
@@ -213,26 +372,42 @@ def _vec(vals):
     return [_c(v) for v in vals]
 
 
+def _unit(v: PF) -> S:
+    """A scale factor: exactly 1.0 is structure (folded, checked), anything
+    else a pool entry."""
+    if float(v) == 1.0:
+        _CTX.check(f"{v.path} == 1.0")
+        return S(c=1.0)
+    return _c(v)
+
+
 class ModelView:
-    """Read-only access to the tape arrays of a CompiledModel."""
+    """Recording access to the tape arrays of a CompiledModel (structure
+    checked by match(), parameters through the pool)."""
 
     def __init__(self, cm):
         st = cm.struct
         self.cm = cm
         self.nq = st.nq
         self.nb = st.nbodies
-        self.bodies = [cm._bodies[i] for i in range(st.nbodies)]
-        self.axes = [cm._axes[i] for i in range(st.naxes)]
-        self.funcs = [cm._funcs[i] for i in range(st.nfunctions)]
-        self.kx = cm._kx
-        self.ky = cm._ky
-        self.muscles = [cm._muscles[i] for i in range(st.nmuscles)]
-        self.points = [cm._points[i] for i in range(st.npoints)]
-        self.acts = [cm._acts[i] for i in range(st.nactuators)]
-        self.tables = [cm._tables[i] for i in range(st.ntables)]
-        self.ext = [cm._ext[i] for i in range(st.nexternal)]
+        for f in ("nq", "nbodies", "naxes", "nfunctions", "nmuscles", "npoints", "nactuators",
+                  "nexternal", "nconstraints", "nwraps", "npathwraps"):
+            _CTX.check(f"m.{f} == {int(getattr(st, f))}")
+        self.bodies = [_Rec(cm._bodies[i], f"m.bodies[{i}]") for i in range(st.nbodies)]
+        self.axes = [_Rec(cm._axes[i], f"m.axes[{i}]") for i in range(st.naxes)]
+        self.funcs = [_Rec(cm._funcs[i], f"m.functions[{i}]") for i in range(st.nfunctions)]
+        self.kx = _RecArr(cm._kx, "m.knot_x")
+        self.muscles = [_Rec(cm._muscles[i], f"m.muscles[{i}]") for i in range(st.nmuscles)]
+        self.points = [_Rec(cm._points[i], f"m.points[{i}]") for i in range(st.npoints)]
+        self.acts = [_Rec(cm._acts[i], f"m.actuators[{i}]") for i in range(st.nactuators)]
+        self.tables = [_Rec(cm._tables[i], f"m.tables[{i}]") for i in range(st.ntables)]
+        self.ext = [_Rec(cm._ext[i], f"m.external[{i}]") for i in range(st.nexternal)]
         self.breaks = [st.table_breaks[i] for i in range(st.nbreaks)]
-        self.gravity = list(st.gravity)
+        self.gravity = [PF(float(st.gravity[i]), f"m.gravity[{i}]") for i in range(3)]
+        nkc = int(st.nconstraints)
+        self.kcs = [_Rec(st.constraints[i], f"m.constraints[{i}]") for i in range(nkc)]
+        self.wraps = [_Rec(st.wraps[i], f"m.wraps[{i}]") for i in range(int(st.nwraps))]
+        self.pathwraps = [_Rec(st.pathwraps[i], f"m.pathwraps[{i}]") for i in range(int(st.npathwraps))]
 
 
 def _uniform_guess(br):
@@ -254,7 +429,8 @@ def _uniform_guess(br):
 
 
 class _Layout:
-    def __init__(self, M: ModelView, implicit: bool = False, prescribed: bool = False):
+    def __init__(self, M: ModelView, implicit: bool = False, prescribed: bool = False,
+                 kc_enforce: bool = True, kc_slacks: bool = False):
         NQ = M.nq
         z = 2 * NQ
         self.act_state, self.ftn_state = [], []
@@ -288,7 +464,26 @@ class _Layout:
         # derivatives; outputs [residual, zdot, auxiliary residuals]
         self.implicit = implicit
         self.NDV = self.NACC + nar
-        self.NI = self.NS + self.NC + self.NDV
+        # kinematic constraints (mh_create's layout, mocohip.hip
+        # validate_and_layout): one multiplier per CoordinateCoupler at every
+        # grid point (inputs after the derivatives); with prescribed
+        # kinematics no kinematic rows and no slacks (CasOCProblem.h:508-521);
+        # else the position errors, with enforced derivatives also the
+        # velocity and acceleration errors (outputs OKC..), and -- Hermite-
+        # Simpson -- one velocity-correction slack per multiplier (inputs after
+        # the multipliers; outputs OQC.., the correction G^T gamma per
+        # coordinate)
+        nkc = len(M.kcs)
+        self.NKC = self.NM = nkc
+        self.enforce = bool(kc_enforce)
+        self.NK = 0 if prescribed else (3 * nkc if kc_enforce else nkc)
+        self.NSL = nkc if (nkc and not prescribed and kc_enforce and kc_slacks) else 0
+        self.OKC = NQ + self.NZ + nar
+        self.OQC = self.OKC + self.NK
+        self.NO = self.OQC + (NQ if self.NSL else 0)
+        self.IM = self.NS + self.NC + self.NDV
+        self.IL = self.IM + self.NM
+        self.NI = self.IL + self.NSL
         for ia, a in enumerate(M.acts):
             if a.kind == abi.MH_ACT_MUSCLE:
                 self.mus_control[a.target] = ia
@@ -315,6 +510,8 @@ class _Emitter:
             self.u = self.inp[Lo.NQ:2 * Lo.NQ]
             self.wacc = self.inp[Lo.NS + Lo.NC:Lo.NS + Lo.NC + Lo.NACC] if Lo.implicit else None
         self.ctrl = self.inp[Lo.NS:Lo.NS + Lo.NC]
+        self.lam = self.inp[Lo.IM:Lo.IM + Lo.NM]
+        self.gam = self.inp[Lo.IL:Lo.IL + Lo.NSL]
         self.fcache: Dict[int, Tuple[S, S, S]] = {}
         self.touched = set()
 
@@ -327,8 +524,9 @@ class _Emitter:
         if F.kind == abi.MH_FN_CONSTANT:
             r = (_c(F.a), _c(0.0), _c(0.0))
         elif F.kind == abi.MH_FN_LINEAR:
-            r = (g.mul(_c(F.scale), g.add(g.mul(_c(F.a), self.q[F.coord]), _c(F.b))),
-                 _c(F.scale * F.a), _c(0.0))
+            sc, a = _unit(F.scale), _unit(F.a)
+            r = (g.mul(sc, g.add(g.mul(a, self.q[F.coord]), _c(F.b))),
+                 g.mul(sc, a), _c(0.0))
         else:
             g.k += 1
             base = f"f{g.k}"
@@ -350,8 +548,9 @@ class _Emitter:
             g.flops["add"] += 6
             g.flops["mul"] += 8
             v, d1, d2 = S(n=f"{base}v"), S(n=f"{base}d1"), S(n=f"{base}d2")
-            if F.scale != 1.0:
-                v, d1, d2 = g.mul(_c(F.scale), v), g.mul(_c(F.scale), d1), g.mul(_c(F.scale), d2)
+            sc = _unit(F.scale)
+            if not sc.is_c(1.0):
+                v, d1, d2 = g.mul(sc, v), g.mul(sc, d1), g.mul(sc, d2)
             r = (v, d1, d2)
         self.fcache[fi] = r
         return r
@@ -374,7 +573,7 @@ class _Emitter:
         Z3 = _vec([0, 0, 0])
         R, P, V, A = {-1: I3}, {-1: Z3}, {-1: (Z3, Z3)}, {}
         if accel:
-            A[-1] = (Z3, _vec([-M.gravity[0], -M.gravity[1], -M.gravity[2]]))
+            A[-1] = (Z3, [g.neg(x) for x in _vec(M.gravity)])
         Sj = {}
         coord_body = {}
         for b in bodies:
@@ -421,8 +620,8 @@ class _Emitter:
                     w = g.mv(g.mm(RGF, Rcur), _vec(ax.dir))
                     motion((w, g.cross(oM, w)), Vb, fv, F.coord)
                 a0, a1, a2 = ax.dir
-                if fv[0].is_c():
-                    cs, sn = _c(math.cos(fv[0].c)), _c(math.sin(fv[0].c))
+                if fv[0].is_k():
+                    cs, sn = g.fn("cos", fv[0]), g.fn("sin", fv[0])
                 else:
                     g.k += 1
                     nm = f"sc{g.k}"
@@ -484,7 +683,8 @@ class _Emitter:
             mov = []
             if pt.kind == abi.MH_PP_CONDITIONAL:
                 qv = q[pt.coord]
-                act.append(f"({qv} >= {lit(pt.range[0])} && {qv} <= {lit(pt.range[1])})")
+                rg = _vec(pt.range)
+                act.append(f"({qv} >= {rg[0]} && {qv} <= {rg[1]})")
             else:
                 act.append(None)
             if pt.kind == abi.MH_PP_MOVING:
@@ -657,28 +857,40 @@ class _Emitter:
         return xs
 
     def external_forces(self, P, Facc, only=None):
+        """ExternalForce point forces from their data tables.  The table's
+        degree and column count are structure; its segments and breakpoints
+        are run-time data (another trial's GRF fits the same code).  Where the
+        breakpoints are near-uniform (every t's direct-index guess within one
+        segment of the right one, mh_table_uniform_inv > 0 -- a match()
+        condition) the segment is found by direct index plus one correction
+        step (two dependent loads instead of a binary search), the guess's
+        origin and 1 / spacing coming from the pool."""
         g, M = self.g, self.M
         Z3 = _vec([0, 0, 0])
         for ie, e in enumerate(M.ext):
             if only is not None and ie not in only:
                 continue
             b = e.body
+            ti = e.table
             g.k += 1
             seg = f"seg{g.k}"
-            T = M.tables[e.table]
+            T = M.tables[ti]
+            deg, ncol = T.degree, T.ncol
             br = M.breaks[T.break_begin:T.break_begin + T.nseg + 1]
-            guess = _uniform_guess(br)
-            if guess is not None:
-                # near-uniform breakpoints: direct index + one-step
-                # correction (two dependent loads instead of a binary search)
-                g.raw(f"const int {seg} = mh::table_segment_u<{T.nseg}>(M.brk + {T.break_begin}, t, "
-                      f"{lit(br[0])}, {lit(guess)});")
+            g.raw(f"const mh_table tb{g.k} = M.tabs[{ti}];")
+            tb = f"tb{g.k}"
+            if _uniform_guess(br) is not None:
+                _CTX.check(f"mh_table_uniform_inv(m, {ti}) > 0.0")
+                b0 = _CTX.entry(f"m.table_breaks[m.tables[{ti}].break_begin]", br[0])
+                inv = _CTX.entry(f"mh_table_uniform_inv(m, {ti})", _uniform_guess(br))
+                g.raw(f"const int {seg} = mh::table_segment_ur(M.brk + {tb}.break_begin, {tb}.nseg, t, "
+                      f"{b0}, {inv});")
             else:
-                g.raw(f"const int {seg} = mh::table_segment(M, {e.table}, t);")
+                g.raw(f"const int {seg} = mh::table_segment(M, {ti}, t);")
 
             def col(cidx):
-                return g.tmp(f"mh::table_value_c<{T.degree}, {T.ncol}>(M.coef + {T.coef_begin}, "
-                             f"M.brk + {T.break_begin}, {seg}, {cidx}, t)")
+                return g.tmp(f"mh::table_value_c<{deg}, {ncol}>(M.coef + {tb}.coef_begin, "
+                             f"M.brk + {tb}.break_begin, {seg}, {cidx}, t)")
             Fv = [col(e.force_col + d) for d in range(3)] if e.force_col >= 0 else Z3
             Pp = [col(e.point_col + d) for d in range(3)] if e.point_col >= 0 else P[b]
             Tq = [col(e.torque_col + d) for d in range(3)] if e.torque_col >= 0 else Z3
@@ -686,6 +898,59 @@ class _Emitter:
             for c in range(3):
                 self.acc(Facc[b][c], nrm[c], -1.0)
                 self.acc(Facc[b][3 + c], Fv[c], -1.0)
+
+    def kc(self, tau, errors: bool):
+        """CoordinateCoupler constraints (MocoCasOCProblem.h:643-732; the
+        interpreter's dae_eval / kc_outputs, operation for operation): the
+        multiplier forces -G^T lambda into tau (tau[indep] -= (scale f')
+        lambda, tau[dep] -= -lambda), and with ``errors`` the per-constraint
+        position error scale f(q_i) - q_d, and (enforced derivatives) the
+        velocity error G u, G = scale f'(q_i), and the velocity-product part
+        scale f''(q_i) u_i u_i of the acceleration error.  Returns
+        [(i, indep, dep, epos, evel, G, c2)]."""
+        g, M, Lo = self.g, self.M, self.Lo
+        out = []
+        for i, K in enumerate(M.kcs):
+            F = M.funcs[K.func]
+            ci, d = F.coord, K.dependent
+            v, d1, d2 = self.fn_eval(K.func)
+            sc = _unit(K.scale)
+            gi = g.mul(sc, d1)
+            if Lo.NM:
+                self.acc(tau[ci], g.mul(gi, self.lam[i]), -1.0)
+                self.acc(tau[d], g.neg(self.lam[i]), -1.0)
+            if errors and Lo.NK:
+                epos = g.sub(g.mul(sc, v), self.q[d])
+                evel = c2 = None
+                if Lo.enforce:
+                    evel = g.sub(g.mul(gi, self.u[ci]), self.u[d])
+                    c2 = g.mul(g.mul(g.mul(sc, d2), self.u[ci]), self.u[ci])
+                out.append((i, ci, d, epos, evel, gi, c2))
+        return out
+
+    def kc_outputs(self, info, udot, gbase=None):
+        """The kinematic-constraint callback outputs (the interpreter's
+        kc_outputs): position errors at OKC, then velocity and acceleration
+        errors ((G udot_i - udot_d) + c2), then the velocity correction
+        G^T gamma per coordinate at OQC.  ``info`` as kc() returns it (or
+        group-field accessors), udot the accelerations."""
+        g, Lo = self.g, self.Lo
+        n = Lo.NKC
+        lines = []
+        for (i, ci, d, epos, evel, gi, c2) in info:
+            lines.append((Lo.OKC + i, epos))
+            if Lo.enforce:
+                lines.append((Lo.OKC + n + i, evel))
+                lines.append((Lo.OKC + 2 * n + i, g.add(g.sub(g.mul(gi, udot[ci]), udot[d]), c2)))
+        if Lo.NSL:
+            corr = [S(c=0.0) for _ in range(Lo.NQ)]
+            for (i, ci, d, epos, evel, gi, c2) in info:
+                corr[ci] = g.add(corr[ci], g.mul(gi, self.gam[i]))
+                corr[d] = g.sub(corr[d], self.gam[i])
+            for j in range(Lo.NQ):
+                lines.append((Lo.OQC + j, corr[j]))
+        for o, v in lines:
+            g.raw(f"out[{o}] = {v};")
 
     def actuators(self, tau):
         for ia, a in enumerate(self.M.acts):
@@ -709,6 +974,7 @@ def _multibody_front(E: _Emitter, with_muscles: bool):
     Facc = E.body_force_vars(allb, init)
     tau = [g.var(_c(0.0)) for _ in range(Lo.NQ)]
     E.actuators(tau)
+    E.kcinfo = E.kc(tau, errors=True)
     zd = {}
     E.resid = {}
     if with_muscles:
@@ -734,7 +1000,8 @@ def _presc_prelude(lines):
             f"pq{j}, pu{j}, pw{j});" for j in used]
 
 
-def generate(cm, struct_name: str, implicit: bool = False, prescribed: bool = False) -> Tuple[str, Dict]:
+def generate(cm, struct_name: str, implicit: bool = False, prescribed: bool = False,
+             kc_enforce: bool = True, kc_slacks: bool = False) -> Tuple[str, Dict]:
     """Return (C++ source of `struct <struct_name>`, info dict).
 
     The struct has
@@ -746,12 +1013,15 @@ def generate(cm, struct_name: str, implicit: bool = False, prescribed: bool = Fa
                  (k_combine),
     plus the group metadata (fields, inputs read, time dependence, FP64 op
     counts) the host uses to build the task tables."""
+    global _CTX
+    _CTX = _Ctx()
     M = ModelView(cm)
-    Lo = _Layout(M, implicit, prescribed)
+    Lo = _Layout(M, implicit, prescribed, kc_enforce, kc_slacks)
     implicit = Lo.implicit
     NQ, NZ = Lo.NQ, Lo.NZ
     parts = []
-    info = {"NQ": NQ, "NS": Lo.NS, "NC": Lo.NC, "implicit": implicit, "prescribed": prescribed}
+    info = {"NQ": NQ, "NS": Lo.NS, "NC": Lo.NC, "implicit": implicit, "prescribed": prescribed,
+            "NM": Lo.NM, "NSL": Lo.NSL, "NK": Lo.NK}
 
     # ---- single-lane eval ---------------------------------------------------
     E = _Emitter(M, Lo)
@@ -767,6 +1037,8 @@ def generate(cm, struct_name: str, implicit: bool = False, prescribed: bool = Fa
         E.g.raw(f"out[{NQ + zi}] = {zd.get(2 * NQ + zi, _c(0.0))};")
     for k in range(Lo.NAR):
         E.g.raw(f"out[{NQ + NZ + k}] = {E.resid[k]};")
+    if E.kcinfo:
+        E.kc_outputs(E.kcinfo, E.wacc if implicit else xs)
     fl = dict(E.g.flops)
     fl["total"] = sum(fl.values())
     info["flops"] = fl
@@ -807,11 +1079,14 @@ def generate(cm, struct_name: str, implicit: bool = False, prescribed: bool = Fa
             # inputs through an accessor (loaded where used, not held in VGPRs)
             tpl = "template <class IN> " if name == "group" else "template <class IN, class TL> "
             args = args.replace("const double* __restrict__ in", "const IN& in")
+        pre = ["    const double* __restrict__ K = M.pool;", "    (void)K;"]
         fns.append(f"    {tpl}__device__ __forceinline__ static void {name}({args}) {{\n"
-                   + "\n".join(lines) + "\n    }")
+                   + "\n".join(pre + lines) + "\n    }")
     lst = lambda v: "{" + ", ".join(str(x) for x in v) + "}"
     src = f"""struct {struct_name} {{
     static constexpr int NQ = {NQ}, NZ = {NZ}, NS = {Lo.NS}, NC = {Lo.NC}, NO = {Lo.NO}, NI = {Lo.NI};
+    // kinematic constraints: multipliers, slack inputs per point
+    static constexpr int NM = {Lo.NM}, NSL = {Lo.NSL};
     static constexpr bool IMPLICIT = {"true" if implicit else "false"};
     static constexpr bool PRESCRIBED = {"true" if prescribed else "false"};
     static constexpr bool EXC_LANES = false;   // k_exc_lanes is the generic interpreter's
@@ -825,9 +1100,25 @@ def generate(cm, struct_name: str, implicit: bool = False, prescribed: bool = Fa
     static constexpr unsigned char GROUP_TIME[NG] = {lst([int(gr.time) for gr in groups])};
     static constexpr double GROUP_FLOPS[NG] = {lst([float(gr.flops) for gr in groups])};
     static constexpr double COMBINE_FLOPS = {float(comb_flops)};
+    // the model's constant pool (DevModel::pool, filled by fill())
+    static constexpr int NPOOL = {max(1, len(_CTX.pool))};
 {chr(10).join(fns)}
 }};
 """
+    conds = list(_CTX.checks)
+    match = [f"// the structure {struct_name} was generated for ({len(conds)} conditions)",
+             f"static bool {struct_name}_match(const mh_model& m) {{"]
+    match += [f"    if (!({c})) return false;" for c in conds]
+    match += ["    return true;", "}"]
+    fill = [f"// its constant pool for model m ({len(_CTX.pool)} entries)",
+            f"static void {struct_name}_fill(const mh_model& m, double* K) {{",
+            "#pragma clang fp contract(off)", "    (void)m;"]
+    fill += [f"    K[{i}] = {e};" for i, (e, _) in enumerate(_CTX.pool)]
+    fill += ["}"]
+    src += "\n".join(match + fill) + "\n"
+    info["npool"] = len(_CTX.pool)
+    info["nchecks"] = len(conds)
+    _CTX = None
     return src, info
 
 
@@ -886,12 +1177,15 @@ def _emit_groups(M: ModelView, Lo: _Layout) -> List[_Group]:
         g0.lam = lam
         out.append(g0)
 
-    def finish(Eg, name, tv, zf=None, rf=None):
+    def finish(Eg, name, tv, zf=None, rf=None, extra=()):
         fields = []
         for j in range(NQ):
             if tv[j] in Eg.touched:
                 Eg.g.raw(f"out[{len(fields)}] = {tv[j]};")
                 fields.append(("tau", j))
+        for kind, key, val in extra:
+            Eg.g.raw(f"out[{len(fields)}] = {val};")
+            fields.append((kind, key))
         if zf is not None:
             Eg.g.raw(f"out[{len(fields)}] = {zf[1]};")
             fields.append(("z", zf[0]))
@@ -927,6 +1221,21 @@ def _emit_groups(M: ModelView, Lo: _Layout) -> List[_Group]:
         E.external_forces(P, Facc, only=[ie])
         E.backward(cl, Facc, Sj, cb, tv)
         finish(E, f"ext_{ie}", tv)
+
+    # kinematic constraints: the multiplier forces and the parts of the
+    # constraint errors that do not need the accelerations
+    if Lo.NKC:
+        E = _Emitter(M, Lo)
+        tv = [E.g.var(_c(0.0)) for _ in range(NQ)]
+        info = E.kc(tv, errors=True)
+        extra = []
+        for (i, ci, d, epos, evel, gi, c2) in info:
+            extra.append(("kpos", i, epos))
+            if Lo.enforce:
+                extra += [("kvel", i, evel), ("kg", i, gi), ("kc2", i, c2)]
+            elif Lo.NSL:
+                extra.append(("kg", i, gi))
+        finish(E, "constraints", tv, extra=extra)
 
     # activation dynamics (reads the muscle's activation and excitation only)
     for im in range(len(M.muscles)):
@@ -994,12 +1303,23 @@ def _emit_combine(M: ModelView, Lo: _Layout, groups: List[_Group]):
         xs = E.solve(groups[0].lam, Hs, bvec)
     for i in range(NQ):
         g.raw(f"out[{i}] = {xs[i]};")
+    kcf = {}
     for gi, gr in enumerate(groups[1:], start=1):
         for f, (kind, zi) in enumerate(gr.fields):
             if kind == "z":
                 g.raw(f"out[{NQ + zi}] = T({gi}, {f});")
             elif kind == "r":
                 g.raw(f"out[{NQ + Lo.NZ + zi}] = T({gi}, {f});")
+            elif kind in ("kpos", "kvel", "kg", "kc2"):
+                kcf[(kind, zi)] = S(n=f"T({gi}, {f})")
+    if Lo.NK:
+        info = []
+        for i, K in enumerate(M.kcs):
+            F = M.funcs[K.func]
+            info.append((i, F.coord, K.dependent, kcf[("kpos", i)], kcf.get(("kvel", i)),
+                         kcf.get(("kg", i)), kcf.get(("kc2", i))))
+        udot = [E.inp[Lo.NS + Lo.NC + j] for j in range(NQ)] if Lo.implicit else xs
+        E.kc_outputs(info, udot)
     return g.lines, sum(g.flops.values())
 
 
@@ -1023,29 +1343,33 @@ def _dgf(g: Gen, mu, LMT: S, VMT: S, act: S, exc: S, has_act: bool, ftn: Optiona
     (returns the equilibrium residual FT - FM cos(alpha), .cpp:826-848)."""
     c1, c2, c3 = 0.2, 1.0, 0.2
     d1, d2, d3, d4 = -0.3211346127989808, -8.149, -0.374, 0.8825327733249912
-    lopt, lts, Fmax = mu.optimal_fiber_length, mu.tendon_slack_length, mu.max_isometric_force
-    fiberWidth = lopt * math.sin(mu.pennation_angle_at_optimal)
-    sqW = fiberWidth * fiberWidth
-    vmax = mu.max_contraction_velocity * lopt
-    kT = math.log((1.0 + c3) / c1) / (1.0 + mu.tendon_strain_at_one_norm_force - c2)
-    e0 = mu.passive_fiber_strain_at_one_norm_force
-    peOffset = math.exp(4.0 * (0.2 - 1.0) / e0)
-    peDenom = math.exp(4.0) - peOffset
     C = _c
+    # the muscle's parameters and the constants DeGrooteFregly2016Muscle
+    # derives from them (extendFinalizeFromProperties, .cpp:130-147): pool
+    # entries computed on the host, as mh_create does for the interpreter
+    lopt, lts, Fmax = C(mu.optimal_fiber_length), C(mu.tendon_slack_length), C(mu.max_isometric_force)
+    fiberWidth = g.mul(lopt, g.fn("sin", C(mu.pennation_angle_at_optimal)))
+    sqW = g.mul(fiberWidth, fiberWidth)
+    vmax = g.mul(C(mu.max_contraction_velocity), lopt)
+    kT = g.div(C(math.log((1.0 + c3) / c1)), g.sub(g.add(C(1.0), C(mu.tendon_strain_at_one_norm_force)), C(c2)))
+    e0 = C(mu.passive_fiber_strain_at_one_norm_force)
+    peOffset = g.fn("exp", g.div(C(4.0 * (0.2 - 1.0)), e0))
+    peDenom = g.sub(C(math.exp(4.0)), peOffset)
+    c1kT = g.mul(C(c1), kT)
     if compliant:
-        ntl = g.add(g.div(g.fn("log", g.mul(C(1.0 / c1), g.add(ftn, C(c3)))), C(kT)), C(c2))
+        ntl = g.add(g.div(g.fn("log", g.mul(C(1.0 / c1), g.add(ftn, C(c3)))), kT), C(c2))
     else:
         ntl = C(1.0)
-    tendonLength = g.mul(C(lts), ntl)
+    tendonLength = g.mul(lts, ntl)
     flat = g.sub(LMT, tendonLength)
-    fiberLength = g.fn("sqrt", g.add(g.mul(flat, flat), C(sqW)))
-    nfl = g.div(fiberLength, C(lopt))
+    fiberLength = g.fn("sqrt", g.add(g.mul(flat, flat), sqW))
+    nfl = g.div(fiberLength, lopt)
     cosP = g.div(flat, fiberLength)
     if mu.ignore_passive_fiber_force:
         fPE = C(0.0)
     else:
-        fPE = g.div(g.sub(g.fn("exp", g.div(g.mul(C(4.0), g.sub(nfl, C(1.0))), C(e0))), C(peOffset)),
-                    C(peDenom))
+        fPE = g.div(g.sub(g.fn("exp", g.div(g.mul(C(4.0), g.sub(nfl, C(1.0))), e0)), peOffset),
+                    peDenom)
     x = g.add(g.div(g.sub(nfl, C(1.0)), C(mu.active_force_width_scale)), C(1.0))
 
     def gl(b1, b2, b3, b4):
@@ -1060,28 +1384,28 @@ def _dgf(g: Gen, mu, LMT: S, VMT: S, act: S, exc: S, has_act: bool, ftn: Optiona
         nff = g.div(ftn, cosP)
         fV = g.div(g.sub(nff, fPE), g.mul(act, fAL))
         nfv = g.div(g.sub(g.fn("sinh", g.mul(C(1.0 / d1), g.sub(fV, C(d4)))), C(d3)), C(d2))
-        fiberVelocity = g.mul(nfv, C(vmax))
+        fiberVelocity = g.mul(nfv, vmax)
         fvat = g.div(fiberVelocity, cosP)
         tendonVelocity = g.sub(VMT, fvat)
-        ntv = g.div(tendonVelocity, C(lts))
+        ntv = g.div(tendonVelocity, lts)
     else:
         if dft is not None:
             # calcTendonForceLengthInverseCurveDerivative (.h:471-476)
-            ntv = g.div(dft, g.mul(C(c1 * kT), g.fn("exp", g.mul(C(kT), g.sub(ntl, C(c2))))))
-            fvat = g.sub(VMT, g.mul(C(lts), ntv))
+            ntv = g.div(dft, g.mul(c1kT, g.fn("exp", g.mul(kT, g.sub(ntl, C(c2))))))
+            fvat = g.sub(VMT, g.mul(lts, ntv))
         else:
             ntv = C(0.0)
             fvat = VMT
         fiberVelocity = g.mul(fvat, cosP)
-        nfv = g.div(fiberVelocity, C(vmax))
+        nfv = g.div(fiberVelocity, vmax)
         tv = g.add(g.mul(C(d2), nfv), C(d3))
         arg = g.add(tv, g.fn("sqrt", g.add(g.mul(tv, tv), C(1.0))))
         fV = g.add(g.mul(C(d1), g.fn("log", arg)), C(d4))
-    activeF = g.mul(C(Fmax), g.mul(g.mul(act, fAL), fV))
-    conPass = g.mul(C(Fmax), fPE)
-    nonCon = g.mul(g.mul(C(Fmax), C(mu.fiber_damping)), nfv)
+    activeF = g.mul(Fmax, g.mul(g.mul(act, fAL), fV))
+    conPass = g.mul(Fmax, fPE)
+    nonCon = g.mul(g.mul(Fmax, C(mu.fiber_damping)), nfv)
     total = g.add(g.add(activeF, conPass), nonCon)
-    T = g.mul(C(Fmax), ftn) if compliant else g.mul(total, cosP)
+    T = g.mul(Fmax, ftn) if compliant else g.mul(total, cosP)
     adot = ftdot = C(0.0)
     if has_act:
         adot = _activation_dot(g, act, exc, tau_act, tau_deact)
@@ -1090,5 +1414,5 @@ def _dgf(g: Gen, mu, LMT: S, VMT: S, act: S, exc: S, has_act: bool, ftn: Optiona
         ftdot = dft
         resid = g.sub(T, g.mul(total, cosP))
     elif compliant:
-        ftdot = g.mul(ntv, g.mul(C(c1 * kT), g.fn("exp", g.mul(C(kT), g.sub(ntl, C(c2))))))
+        ftdot = g.mul(ntv, g.mul(c1kT, g.fn("exp", g.mul(kT, g.sub(ntl, C(c2))))))
     return T, adot, ftdot, resid

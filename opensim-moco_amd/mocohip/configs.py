@@ -23,6 +23,7 @@ import numpy as np
 
 from .model import (Body, Coordinate, CoordinateActuator, DataTable,
                     ExternalForce, Joint, Marker, Model, model_from_dict)
+from . import abi
 from .osim import add_reserves
 from .problem import (Constant, GCVSpline, ImplicitAuxiliaryDerivativesTerm,
                       MocoControlBoundConstraint, MocoControlGoal, MocoInitialActivationGoal,
@@ -273,6 +274,39 @@ def gait10dof18musc(num_mesh_intervals: int = 200, muscles: bool = True,
     s = MocoHipSolver(num_mesh_intervals=num_mesh_intervals,
                       optim_finite_difference_scheme=fd_scheme, multibody_dynamics_mode=dynamics)
     return MocoStudy(p, s)
+
+
+def scale_subject(m: Model, length: float = 1.03, mass: float = 1.05) -> Model:
+    """A scaled subject (what OpenSim's ScaleTool produces from a generic
+    model, uniformly): every length -- joint frame locations, centers of
+    mass, path-point locations, CustomJoint translation splines and
+    MovingPathPoint functions, optimal fiber and tendon slack lengths --
+    times ``length``,
+    masses times ``mass``, inertias times mass * length^2.  The model
+    STRUCTURE is unchanged, so a generated back end of the generic model
+    serves it (codegen.py "Structure-only specialization")."""
+    L, W = float(length), float(mass)
+    for b in m.bodies.values():
+        b.mass *= W
+        b.com = tuple(L * c for c in b.com)
+        b.inertia = tuple(W * L * L * i for i in b.inertia)
+    for j in m.joints:
+        j.loc_in_parent = tuple(L * c for c in j.loc_in_parent)
+        j.loc_in_child = tuple(L * c for c in j.loc_in_child)
+        for ax in j.axes:
+            # translations that are functions of a rotation (the knee's
+            # SimmSplines, MultiplierFunction); a translational coordinate's
+            # own linear function is a length already
+            if (ax.type == abi.MH_AXIS_TRANSLATION and ax.func is not None
+                    and ax.func.kind != abi.MH_FN_LINEAR):
+                ax.func = ax.func.scaled(L)
+    for mu in m.muscles:
+        mu.optimal_fiber_length *= L
+        mu.tendon_slack_length *= L
+        for pt in mu.points:
+            pt.loc = tuple(L * c for c in pt.loc)
+            pt.fx, pt.fy, pt.fz = (f.scaled(L) if f is not None else None for f in (pt.fx, pt.fy, pt.fz))
+    return m
 
 
 def gait10dof18musc_track(num_mesh_intervals: int = 65) -> MocoStudy:

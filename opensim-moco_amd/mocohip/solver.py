@@ -42,6 +42,13 @@ class MocoHipSolver:
     # "initial-guess" (sparsity_guess, default the bounds-midpoint guess)
     optim_sparsity_detection: str = "none"
     optim_sparsity_detection_random_count: int = 3
+    # how a detection probe decides a coupling (include/mocohip.h
+    # mh_sparsity_rule): "robust" (default; changes below 1e-10 of the
+    # output's magnitude are rounding noise -- the pattern is the model's,
+    # the same in every implementation) or "any-change" (the reference's
+    # rule, CasOCFunction.cpp:44-61, which makes couplings that cancel to
+    # rounding level depend on the order of floating-point operations)
+    optim_sparsity_detection_rule: str = "robust"
     sparsity_guess: Optional[np.ndarray] = None
     # "given": the callback sparsity itself (HipNLP.callback_sparsity()),
     # e.g. detected once and shared by every shard / replica
@@ -163,6 +170,10 @@ class MocoHipSolver:
         o.velocity_correction_bounds[1] = float(hi)
         o.sparsity_detection = _SPARSITY[self.optim_sparsity_detection]
         o.sparsity_random_count = int(self.optim_sparsity_detection_random_count)
+        rules = {"robust": abi.MH_SPARSITY_RULE_ROBUST, "any-change": abi.MH_SPARSITY_RULE_ANY_CHANGE}
+        if self.optim_sparsity_detection_rule not in rules:
+            raise ValueError("optim_sparsity_detection_rule must be 'robust' or 'any-change'")
+        o.sparsity_rule = rules[self.optim_sparsity_detection_rule]
         if self.sparsity_guess is not None:
             if self.optim_sparsity_detection != "initial-guess":
                 raise ValueError("sparsity_guess needs optim_sparsity_detection='initial-guess'")

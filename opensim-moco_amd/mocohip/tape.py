@@ -15,8 +15,9 @@ Layout (little endian, x86-64 struct layout of include/mocohip.h):
   (ABI v4: mh_options grew) appends the kinematic constraints
   (mh_model.nconstraints/constraints) and the multiplier and
   kinematic-constraint bounds; version 5 (ABI v5) appends the wrap surfaces
-  and PathWraps (mh_model.nwraps/wraps, npathwraps/pathwraps).  Readers
-  accept versions 4 and 5."""
+  and PathWraps (mh_model.nwraps/wraps, npathwraps/pathwraps); version 6
+  carries ABI v6's mh_options (+ sparsity_rule).  Readers accept versions 4
+  to 6."""
 from __future__ import annotations
 
 import ctypes as C
@@ -25,7 +26,8 @@ import struct
 from . import abi
 
 MAGIC = b"MHTAPE01"
-VERSION = 5   # 2: + path constraints; 3: + endpoint constraints; 4: + kinematic constraints; 5: + wraps
+VERSION = 6   # 2: + path constraints; 3: + endpoint constraints; 4: + kinematic constraints; 5: + wraps;
+#               6: ABI v6 mh_options
 
 # (field, element type, count attribute of mh_model / None for problem arrays)
 _MODEL_ARRAYS = [

@@ -275,7 +275,7 @@ class MocoTrajectory:
     def compare_continuous_variables_rms(self, other: "MocoTrajectory", states=None, controls=None,
                                          multipliers=None, derivatives=None) -> float:
         """compareContinuousVariablesRMS (MocoTrajectory.cpp:1131-1263): per
-        block, the given names (None: all, which both trajectories must share;
+        block, the given names (None or []: all, which both trajectories must share;
         ["none"]: skip the block); each column through an interpolating
         GCV spline of degree min(n - 1, 5) per trajectory (0 outside its time
         range), the summed squared error integrated by the trapezoidal rule on
@@ -286,7 +286,7 @@ class MocoTrajectory:
         chosen = []
         for kind, names in blocks:
             mine, theirs = getattr(self, kind + "_names"), getattr(other, kind + "_names")
-            if names is None:
+            if names is None or len(names) == 0:   # empty = all (MocoTrajectory.cpp:1140-1150)
                 if sorted(mine) != sorted(theirs):
                     raise ValueError(f"Expected both trajectories to have the same {kind} names; "
                                      f"consider specifying the {kind}s to compare.")
@@ -328,12 +328,20 @@ class MocoTrajectory:
         return float(np.sqrt(integral / (tf - t0) / ncols))
 
     def compare_parameters_rms(self, other: "MocoTrajectory", names=None) -> float:
-        """compareParametersRMS (MocoTrajectory.cpp:1311-1340)."""
-        if names is None:
+        """compareParametersRMS (MocoTrajectory.cpp:1311-1340): None or an
+        empty list compares all parameters (NaN when there are none, as the
+        reference's sqrt(0 / 0))."""
+        if names is None or len(names) == 0:
             if sorted(self.parameter_names) != sorted(other.parameter_names):
                 raise ValueError("Expected both trajectories to have the same parameter names; "
                                  "consider specifying the parameters to compare.")
             names = list(self.parameter_names)
+        else:
+            for n in names:
+                if n not in self.parameter_names or n not in other.parameter_names:
+                    raise ValueError(f"Expected '{n}' to be a parameter in both trajectories.")
+        if not names:
+            return float("nan")
         err = [(self.parameters[self.parameter_names.index(n)]
                 - other.parameters[other.parameter_names.index(n)]) ** 2 for n in names]
         return float(np.sqrt(sum(err) / len(names)))

@@ -2278,6 +2278,23 @@ static double splitmix_uniform(uint64_t* st) {
     return (double)(z >> 11) * (2.0 / 9007199254740992.0) - 1.0;
 }
 
+/* A detection probe's coupling test (include/mocohip.h mh_sparsity_rule):
+ * ANY_CHANGE is the reference's (CasOCFunction.cpp:44-61: nonzero or NaN);
+ * ROBUST ignores changes below MH_SPARSITY_ROBUST_TOL of the output's
+ * magnitude (rounding noise of couplings that cancel mathematically). */
+static int sparsity_coupled(int rule, double d, double scale) {
+    if (isnan(d)) return 1;
+    if (rule == MH_SPARSITY_RULE_ANY_CHANGE) return d != 0;
+    return fabs(d) > MH_SPARSITY_ROBUST_TOL * scale;
+}
+/* the callback's magnitude at the detection point: max(1, max |output|) */
+static double sparsity_scale(const double* y0, int n) {
+    double s = 1.0;
+    for (int k = 0; k < n; ++k)
+        if (isfinite(y0[k]) && fabs(y0[k]) > s) s = fabs(y0[k]);
+    return s;
+}
+
 /* calcJacobianSparsityWithPerturbation (CasOCFunction.cpp:25-71) for the
  * DAE callback and each path equation, at getSubsetPoint of every
  * detection iterate (CasOCFunction.h:72-86: time = initial_time, the first
@@ -2286,6 +2303,9 @@ static int detect_sparsity(orc_ctx* c, const mh_options* o) {
     int NS = c->NS, NP = c->NP, NO = nout(c), W = 1 + NP, NPC = c->NPC;
     int npts = 1;
     double* pts;
+    const int rule = o->sparsity_rule;
+    if (rule != MH_SPARSITY_RULE_ROBUST && rule != MH_SPARSITY_RULE_ANY_CHANGE)
+        return fail(MH_ERR_INVALID, "unknown sparsity rule %d", rule);
     if (o->sparsity_detection == MH_SPARSITY_RANDOM) {
         npts = o->sparsity_random_count > 0 ? o->sparsity_random_count : 3;
         pts = (double*)malloc(sizeof(double) * (size_t)c->n * (size_t)npts);
@@ -2326,6 +2346,7 @@ static int detect_sparsity(orc_ctx* c, const mh_options* o) {
         gather_point(c, x, 0, in + 1, in + 1 + NS);
         eval_dae_point(c, &w, in[0], in + 1, in + 1 + NS, y0);
         for (int e = 0; e < NPC; ++e) p0[e] = path_value(c, e, in[0], in + 1 + NS);
+        const double sd = sparsity_scale(y0, NO), sp = sparsity_scale(p0, NPC);
         for (int j = 0; j < W; ++j) {
             double sv = in[j];
             in[j] = sv + eps;
@@ -2334,11 +2355,11 @@ static int detect_sparsity(orc_ctx* c, const mh_options* o) {
             in[j] = sv;
             for (int k = 0; k < NO; ++k) {
                 double d = y[k] - y0[k];
-                if (isnan(d) || d != 0) c->sp[(int64_t)k * W + j] = 1;
+                if (sparsity_coupled(rule, d, sd)) c->sp[(int64_t)k * W + j] = 1;
             }
             for (int e = 0; e < NPC; ++e) {
                 double d = pv[e] - p0[e];
-                if (isnan(d) || d != 0) c->sp_pc[(int64_t)e * W + j] = 1;
+                if (sparsity_coupled(rule, d, sp)) c->sp_pc[(int64_t)e * W + j] = 1;
             }
         }
         /* the endpoint functions at their subset point (Endpoint::
@@ -2347,6 +2368,11 @@ static int detect_sparsity(orc_ctx* c, const mh_options* o) {
         if (c->NEP) {
             double* ein = (double*)malloc(sizeof(double) * (size_t)(2 * W));
             ep_gather(c, x, ein);
+            double se = 1.0;
+            for (int e = 0; e < c->NEP; ++e) {
+                double v0 = endpoint_value(c, e, ein);
+                if (isfinite(v0) && fabs(v0) > se) se = fabs(v0);
+            }
             for (int j = 0; j < 2 * W; ++j) {
                 double sv = ein[j];
                 for (int e = 0; e < c->NEP; ++e) {
@@ -2354,7 +2380,7 @@ static int detect_sparsity(orc_ctx* c, const mh_options* o) {
                     ein[j] = sv + eps;
                     double d = endpoint_value(c, e, ein) - v0;
                     ein[j] = sv;
-                    if (isnan(d) || d != 0) c->sp_ep[(int64_t)e * 2 * W + j] = 1;
+                    if (sparsity_coupled(rule, d, se)) c->sp_ep[(int64_t)e * 2 * W + j] = 1;
                 }
             }
             free(ein);

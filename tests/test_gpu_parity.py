@@ -67,6 +67,16 @@ def _physiological_guess(st):
     return _sparse(st, "initial-guess")
 
 
+def _heavy_femur(st):
+    st.problem.model.bodies["femur_r"].mass *= 1.01
+    return st
+
+
+def _scaled(st):
+    configs.scale_subject(st.problem.model, 1.04, 1.07)
+    return st
+
+
 CASES = {
     "sliding_mass": lambda: configs.sliding_mass(50),
     "double_pendulum_hs": lambda: configs.double_pendulum(100),
@@ -168,6 +178,13 @@ CASES = {
     "rajagopal18_inverse_wrapped": lambda: configs.rajagopal18_inverse(3, sparsity="none",
                                                                       keep_path_wraps=True),
     "rajagopal80": lambda: configs.rajagopal80(3),
+    # the generated back ends are specialized on the model STRUCTURE and read
+    # the numbers from a per-model constant pool: a 1 % heavier femur, a
+    # scaled subject and MocoInverse on a scaled subject run them too
+    # (tests/test_backend_select.py), here checked against the oracle
+    "gait_rigid_heavy_femur": lambda: _heavy_femur(configs.gait10dof18musc(6)),
+    "gait_rigid_scaled_subject": lambda: _scaled(configs.gait10dof18musc(6)),
+    "gait_inverse_scaled_subject": lambda: _scaled(configs.gait10dof18musc_inverse(4, sparsity="none")),
     "rajagopal80_wrapped_trap": lambda: _trap(configs.rajagopal80(2, keep_path_wraps=True)),
 }
 
@@ -302,13 +319,9 @@ def _pair(name, backend="auto", tasks=None, env=None):
             if v is not None:
                 os.environ[k] = v
     name_ = gpu.backend()[0]
-    if st.solver.optim_sparsity_detection != "none":
-        # detection decides weak (rounding-level) couplings by whether a
-        # 1e-5 perturbation changes an output's last bits, which differs
-        # between two libm/FMA implementations: the oracle is built from the
-        # pattern the device detected (test_sparsity_detection_agrees checks
-        # the two detections differ only on such couplings)
-        opts = _given(st, gpu.callback_sparsity())
+    # with sparsity detection the oracle detects its own pattern (the robust
+    # rule makes it the device's, test_sparsity_detection_agrees), so the
+    # structures compared below are independent
     if backend == "generic":
         assert name_.startswith("generic"), name_
     elif backend == "lane":
@@ -739,28 +752,35 @@ SPARSE = [n for n in CASES if "sparse" in n]
 
 @pytest.mark.parametrize("name", SPARSE)
 def test_sparsity_detection_agrees(name):
-    """The device detection (mh_create) and the oracle's agree on every
-    coupling except rounding-level ones: where they differ, the oracle's
-    output change under the 1e-5 perturbation is within 64 eps of the DAE's
-    magnitude (or non-finite) at every detection iterate, i.e. the coupling
-    is numerical noise in both.  The structures built from one pattern are
-    bit-identical (test_structure_bounds_guess_bit_exact)."""
+    """Detected sparsity is bit-reproducible: with the default rule
+    (include/mocohip.h MH_SPARSITY_RULE_ROBUST: a probe counts as a coupling
+    when its change exceeds 1e-10 of the output's magnitude, or is NaN) the
+    device's detection (mh_create, on its own kernels) and the oracle's (the
+    CPU restatement) give the SAME pattern, coupling for coupling, and so
+    the same NLP structure (every sparse parity case builds the oracle from
+    its own detection).  Under the reference's rule (any nonzero change,
+    CasOCFunction.cpp:44-61) the two differ exactly on rounding-level
+    couplings -- changes within 64 eps of the DAE's magnitude, numerical
+    noise of couplings that cancel mathematically -- which is why that rule
+    is implementation-dependent and not the default."""
     st = CASES[name]()
     rep = st.problem.create_rep()
     gpu = HipNLP(rep, st.solver.options())
     ref = OracleNLP(rep, st.solver.options())
     a, b = gpu.callback_sparsity(), ref.callback_sparsity()
     assert a.shape == b.shape
+    assert np.array_equal(a, b), int((a != b).sum())
+    assert a.sum() < a.size     # detection removed couplings
+    # the reference's rule: disagreements, if any, are rounding-level only
+    import copy
+    s2 = copy.copy(st.solver)
+    s2.optim_sparsity_detection_rule = "any-change"
+    gpu2, ref2 = HipNLP(rep, s2.options()), OracleNLP(rep, s2.options())
+    a2, b2 = gpu2.callback_sparsity(), ref2.callback_sparsity()
+    assert (a2 >= a).all() and (b2 >= b).all()   # any-change only adds couplings
     W = 1 + gpu.NI
     NO = gpu.NO
-    diff = np.argwhere((a != b).reshape(-1, W))
-    # disagreements are rounding-level couplings only (checked one by one
-    # below); their share of the detected couplings is bounded at 15 %
-    # (measured on MI355X: 2.8 % compliant tendon, 11.1 - 11.6 % on the
-    # implicit / MocoInverse cases, whose residual rows M w + C - f carry
-    # |w| up to 1000 and cancel to ~1e-13 on many couplings, 0 - 1 %
-    # elsewhere)
-    assert len(diff) <= 0.15 * max(b.sum(), 1), (len(diff), int(b.sum()), len(diff) / max(b.sum(), 1))
+    diff = np.argwhere((a2 != b2).reshape(-1, W))
     for x in _detection_points(ref, st.solver):
         P = _points(ref, x)[0]
         rows = [P] + [P + np.eye(len(P))[j] * 1e-5 for j in range(len(P))]
@@ -768,9 +788,6 @@ def test_sparsity_detection_agrees(name):
         for j in range(len(P)):
             rows[1 + j][j] = P[j] + 1e-5
         Y = ref.eval_dae(np.array(rows))
-        # rounding level of the DAE at this point: its terms are as large as
-        # its largest output (e.g. M w with |w| up to 1000; a muscle's force
-        # couple cancels to this level on coordinates it does not cross)
         scale = max(np.abs(Y[0][np.isfinite(Y[0])]).max(initial=0.0), 1.0)
         for o, j in diff:
             assert o < NO, "path-equation sparsity must agree exactly"
@@ -863,8 +880,7 @@ def test_jacobian_tight_bound(name):
     st.solver.fd_step = 1e-4
     rep = st.problem.create_rep()
     gpu = HipNLP(rep, st.solver.options())
-    ref = OracleNLP(rep, st.solver.options() if st.solver.optim_sparsity_detection == "none"
-                    else _given(st, gpu.callback_sparsity()), threads=8)
+    ref = OracleNLP(rep, st.solver.options(), threads=8)
     for _, x in _iterates(gpu):
         J, J0 = gpu.eval_jac_g(x), ref.eval_jac_g(x)
         _, Y, Y0 = _device_lanes_check(gpu, ref, x)
@@ -926,9 +942,7 @@ def test_config_at_full_size(name):
     st = SIZES[name]()
     rep = st.problem.create_rep()
     gpu = HipNLP(rep, st.solver.options())
-    opts = (st.solver.options() if st.solver.optim_sparsity_detection == "none"
-            else _given(st, gpu.callback_sparsity()))
-    ref = OracleNLP(rep, opts, threads=16)
+    ref = OracleNLP(rep, st.solver.options(), threads=16)   # its own detection (inverse_N125)
     assert (gpu.n, gpu.m, gpu.nnz) == (ref.n, ref.m, ref.nnz)
     ir, jc = gpu.jac_structure()
     ir0, jc0 = ref.jac_structure()
@@ -1008,8 +1022,8 @@ BATCH_CASES = {
 @pytest.mark.parametrize("name", list(BATCH_CASES))
 def test_batch_bit_identical(name, gm):
     """mh_batch_*: three NLPs of one problem shape (different iterates; the
-    third with its own model data -- a 1 % heavier body, the trial-sweep
-    case) evaluated by one k_groups and one k_interval launch give, bit for
+    third with its own model -- a scaled subject with 1 % larger ground
+    reactions, the subject / trial-sweep case of configs[4]) evaluated by one k_groups and one k_interval launch give, bit for
     bit, each context's own eval_g / eval_jac_g / fused results; group
     results staged in LDS or read from global memory alike."""
     import torch
@@ -1018,8 +1032,10 @@ def test_batch_bit_identical(name, gm):
     for b in range(3):
         st = BATCH_CASES[name]()
         if b == 2 and "grf" in st.problem.model.tables:
-            # its own data: ground reactions 1 % larger (table values live
-            # in HBM; the generated code folds only the model's constants)
+            # its own subject and data: a scaled model (the generated code
+            # reads its numbers from the NLP's own constant pool) and ground
+            # reactions 1 % larger (table values live in HBM)
+            configs.scale_subject(st.problem.model, 1.03, 1.05)
             t = st.problem.model.tables["grf"]
             t.columns = {k: np.asarray(v) * 1.01 for k, v in t.columns.items()}
         nlps.append(HipNLP(st.problem.create_rep(), st.solver.options()))
@@ -1056,7 +1072,7 @@ def test_batch_rejects_other_shapes():
     b = HipNLP(configs.gait10dof18musc(8).problem.create_rep(), configs.gait10dof18musc(8).solver.options())
     with pytest.raises(RuntimeError, match="shape differs"):
         HipBatch([a, b])
-    st = configs.double_pendulum_coupled(6)    # generic interpreter: no task back end
+    st = configs.wrapped_pendulum(6)    # generic interpreter: no task back end
     c = HipNLP(st.problem.create_rep(), st.solver.options())
     with pytest.raises(RuntimeError, match="error 3"):
         HipBatch([c])

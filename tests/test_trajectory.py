@@ -206,3 +206,19 @@ def test_compare_continuous_variables_rms():
     # parameters (compareParametersRMS, :1311-1340)
     assert a.compare_parameters_rms(b) == pytest.approx(0.5)
     assert a.compare_parameters_rms(a) == 0.0
+
+
+def test_compare_rms_empty_name_lists_mean_all():
+    """An empty name list selects every column of its block, as the
+    reference's empty std::vector does (MocoTrajectory.cpp:1140-1190);
+    compareParametersRMS over no parameters is the reference's
+    sqrt(0 / 0) = NaN, and unknown names are rejected (checkContains)."""
+    a, b = _rms_pair(0.3)
+    assert a.compare_continuous_variables_rms(b, states=[], controls=[]) == \
+        a.compare_continuous_variables_rms(b)
+    assert a.compare_parameters_rms(b, []) == a.compare_parameters_rms(b)
+    e = MocoTrajectory(a.time, list(a.state_names), list(a.control_names), [], [], [], [],
+                       a.states, a.controls)
+    assert np.isnan(e.compare_parameters_rms(e))
+    with pytest.raises(ValueError):
+        a.compare_parameters_rms(b, ["no_such_parameter"])
