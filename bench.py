@@ -25,15 +25,18 @@ kernels are enqueued and the timed region ends with torch.cuda.synchronize()
                   cores, on a bounded sample of the same workload.
 
 --gpus N > 1 (one process per GPU, torch.distributed.run):
-  --multi replicas (default): every rank evaluates its own NLP (independent
-      trials, the configs[4] batch layout), no collective on the data path
+  --multi mesh (default for N > 1): the north star's layout -- ONE NLP (the
+      headline's, so the driver's per-N values form a strong-scaling curve)
+      for one host IPOPT, its mesh intervals sharded over the ranks.  value =
+      device-resident calls/s: x broadcast over RCCL, every rank evaluates its
+      shard into HBM; "host_inclusive": the same plus each rank's DMA of its
+      contiguous g / Jacobian slice into its offset of one page-locked host
+      buffer shared by the node's ranks over its own PCIe link
+      (mocohip.distributed.HostGather); "scaling": "strong".  The replicas
+      layout is reported beside it ("replicas").
+  --multi replicas: every rank evaluates its own NLP (independent trials,
+      the configs[4] batch layout), no collective on the data path
       -> "scaling": "weak".
-  --multi mesh: ONE NLP for one host IPOPT, its mesh intervals sharded over
-      the ranks: x is broadcast over RCCL, each rank evaluates its shard and
-      copies its contiguous g / Jacobian slice into its offset of one
-      page-locked host buffer shared by the node's ranks over its own PCIe
-      link (mocohip.distributed.HostGather) -> host-inclusive calls/s,
-      "scaling": "strong".
 
 Prints one JSON line on rank 0.
 """
@@ -68,7 +71,8 @@ def parse():
     ap.add_argument("--blocking", action="store_true",
                     help="every C-ABI call synchronizes before returning (default: asynchronous "
                          "device calls, synchronized at the end of the timed region)")
-    ap.add_argument("--multi", choices=["replicas", "mesh"], default="replicas")
+    ap.add_argument("--multi", choices=["replicas", "mesh"], default=None,
+                    help="default: mesh when WORLD_SIZE > 1")
     ap.add_argument("--single-mode", action="store_true",
                     help="measure only the headline (no secondary lines): for profiler runs, so "
                          "that every launch of a kernel has the same shape")
@@ -439,23 +443,59 @@ def config3_line(cx, args):
 
 
 def solve_lines():
-    """Wall-clock to a converged solve (the BASELINE metric's second half) on
-    the GPU path for the reference's small known-answer problems, with the
-    host driver mocohip.nlpsolve (scipy SLSQP; Ipopt is absent here)."""
+    """Wall-clock to a converged solve (the BASELINE metric's second half):
+    MocoStudy.solve on the GPU path with the host interior-point solver
+    (mocohip.ipm: Ipopt's algorithm with its limited-memory Hessian; Ipopt is
+    absent here), at the reference's tolerances, for the reference's golden-
+    solution problems and configs[4]'s NLP."""
     from mocohip import configs
+    from mocohip.trajectory import MocoTrajectory
+    golden = os.path.join(ROOT, "tests", "golden")
+
+    def rms_vs(sol, rep, fname):
+        d = np.load(os.path.join(golden, fname))
+        labels = [str(l) for l in d["labels"]]
+        data = d["data"]
+        col = {l: i for i, l in enumerate(labels)}
+        sn, cn = list(rep.state_names), list(rep.control_names)
+        g = MocoTrajectory(data[:, 0], sn, cn, states=data[:, [col[n] for n in sn]],
+                           controls=data[:, [col[n] for n in cn]])
+        m = MocoTrajectory(sol.time, sn, cn, states=sol.states, controls=sol.controls)
+        return (round(g.compare_continuous_variables_rms(m, states=["none"]), 5),
+                round(g.compare_continuous_variables_rms(m, controls=["none"]), 5))
     out = {}
-    for name, mk in (("sliding_mass_interface", configs.sliding_mass_interface),
-                     ("double_pendulum_swingup", lambda: configs.double_pendulum_swingup(29))):
-        sol = mk().solve()
+    problems = (
+        ("moco_inverse_rajagopal18_N11", lambda: configs.rajagopal18_inverse(),
+         "std_testMocoInverse_subject_18musc_solution.npz",
+         "testMocoInverse.cpp:118-147; reference file: objective 1.087741, 52 Ipopt iterations, 54.5 s"),
+        ("moco_track_gait10dof18musc_N65", lambda: configs.gait10dof18musc_track(),
+         "std_testMocoTrackGait10dof18musc_solution.npz", "testMocoTrack.cpp:46-68 (tolerance 1e-2)"),
+        ("moco_inverse_gait10dof18musc_N125", lambda: configs.gait10dof18musc_inverse(125), None,
+         "configs[4]'s NLP (one solve of the batch)"),
+        ("sliding_mass_interface", configs.sliding_mass_interface, None,
+         "testMocoInterface.cpp:1701-1742"),
+    )
+    for name, mk, gold, ref in problems:
+        st = mk()
+        rep = st.problem.create_rep()
+        sol = st.solve()
         r = sol.stats
-        out[name] = {"success": r.success, "wall_clock_s": round(r.duration, 4), "iterations": r.iterations,
-                     "objective": r.objective, "final_time": float(sol.time[-1]),
-                     "evaluations": r.evaluations, "optimizer": r.status.split(":")[0]}
+        line = {"success": r.success, "wall_clock_s": round(r.duration, 3), "iterations": r.iterations,
+                "objective": r.objective, "status": r.status, "evaluations": r.evaluations,
+                "seconds_in_evaluations": round(r.timings.get("evaluations_s", 0.0), 3),
+                "seconds_in_kkt": round(r.timings.get("linear_algebra_s", 0.0), 3),
+                "optimizer": r.optimizer, "reference": ref}
+        if gold:
+            line["rms_controls_states_vs_golden"] = rms_vs(sol, rep, gold)
+        out[name] = line
     return out
 
 
 def mesh_main(cx, args):
-    """--multi mesh: one NLP, sharded; host-inclusive strong scaling."""
+    """--multi mesh: one NLP sharded by mesh interval (strong scaling).
+    value = device-resident (x broadcast + shard evaluation into HBM);
+    host_inclusive adds each rank's slice DMA into the shared page-locked
+    host buffer; replicas = every rank its own whole NLP."""
     from mocohip import configs
     from mocohip.distributed import HostGather, interval_shard
     torch, dist = cx.torch, cx.dist
@@ -472,16 +512,21 @@ def mesh_main(cx, args):
     hg = HostGather(tag, nlp.m, nlp.nnz, (nlp.row_begin, nlp.row_end), (nlp.nnz_begin, nlp.nnz_end),
                     cx.rank, barrier, pin=True)
     stream = cx.stream()
+    evaluate = fused if args.mode == "fused" else sep
 
-    def step():
+    def step_device():
         if cx.world > 1:
             dist.broadcast(xd, src=0)          # IPOPT's iterate to every rank (RCCL)
-        (fused if args.mode == "fused" else sep)()
+        evaluate()
+
+    def step_host():
+        step_device()
         hg.copy_from_device_async(gd.data_ptr(), vd.data_ptr(), stream)
         torch.cuda.current_stream().synchronize()
         if cx.world > 1:
             dist.barrier()                     # every slice has landed on the IPOPT host
-    k, el = measure(cx, step, args)
+    k, el = measure(cx, step_device, args)
+    kh, elh = measure(cx, step_host, args, k=max(50, args.steps // 4), w=max(10, args.warmup // 10))
     ok = None
     if cx.rank == 0:
         # the reassembled host vectors against one unsharded evaluation
@@ -491,6 +536,12 @@ def mesh_main(cx, args):
         full.close()
     barrier()
     hg.close(unlink=cx.rank == 0)
+    # replicas: every rank evaluates the whole NLP (independent trials)
+    nlp.close()
+    rnlp = make_nlp(cx, build(), blocking=False)
+    rsep, rfused, _ = device_steps(cx, rnlp, track_iterate(rnlp, cx.rank))
+    kr, elr = measure(cx, rfused if args.mode == "fused" else rsep, args)
+    rnlp.close()
     if cx.rank == 0:
         wl = ("Rajagopal 80-muscle gait NLP (configs[3])" if args.config == "rajagopal80"
               else "MocoTrack gait10dof18musc DGF rigid tendon (configs[2])")
@@ -502,15 +553,24 @@ def mesh_main(cx, args):
                 "config": {"workload": wl + ", one NLP sharded by mesh interval for one host IPOPT",
                            "mesh_intervals": N, "n": nlp.n, "m": nlp.m, "nnz_jac": nlp.nnz,
                            "fd": args.fd, "mode": args.mode,
-                           "parallelism": f"mesh-shard{cx.world}: RCCL broadcast of x + per-rank DMA "
-                                          "of its g/J slice into one page-locked host buffer",
-                           "host_inclusive": True, "reassembly_bit_exact": ok}}
+                           "parallelism": f"mesh-shard{cx.world}: RCCL broadcast of x, each rank its "
+                                          "contiguous intervals, g / J slices in its HBM",
+                           "calls": "asynchronous (device pointers, torch stream)"},
+                "host_inclusive": {"value": round(kh / elh, 3), "unit": "calls/s", "steps": kh,
+                                   "ms_per_step": round(1e3 * elh / kh, 5),
+                                   "note": "+ each rank's slice DMA into one page-locked host buffer "
+                                           "shared by the node's ranks (HostGather), barrier",
+                                   "reassembly_bit_exact": ok},
+                "replicas": {"value": round(kr * cx.world / elr, 3), "unit": "calls/s", "steps": kr,
+                             "scaling": "weak", "note": "every rank its own whole NLP, no collective"}}
         print(json.dumps(line), flush=True)
 
 
 def main():
     args = parse()
     cx = Ctx(args)
+    if args.multi is None:
+        args.multi = "mesh" if cx.world > 1 else "replicas"
     if args.multi == "mesh":
         mesh_main(cx, args)
         if cx.world > 1:
