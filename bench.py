@@ -412,8 +412,8 @@ def config3_line(cx, args):
     coordinates, 80 DGF muscles, patellofemoral couplers with derivatives and
     velocity-correction slacks, explicit) at N = --config3 on this GPU:
     eval_g + eval_jac_g calls/s on device pointers, the per-launch times of
-    its two eval_jac_g kernels (the generic device interpreter, one lane per
-    DAE; then the transcription), and a bounded CPU-oracle sample."""
+    its two eval_jac_g stages (the DAE stage of the selected back end, then
+    the transcription), and a bounded CPU-oracle sample."""
     from mocohip import configs
     st = configs.rajagopal80(args.config3, fd_scheme=args.fd)
     nlp = make_nlp(cx, st, blocking=args.blocking)
@@ -426,7 +426,7 @@ def config3_line(cx, args):
     out = {"value": round(k * cx.world / el, 3), "unit": "calls/s", "ms_per_step": round(1e3 * el / k, 4),
            "steps": k, "mesh_intervals": args.config3, "n": nlp.n, "m": nlp.m, "nnz_jac": nlp.nnz,
            "backend": nlp.backend()[0],
-           "kernels_ms": {"dae (k_eval, generic interpreter)": round(dae_ms, 4),
+           "kernels_ms": {f"dae ({nlp.backend()[0]})": round(dae_ms, 4),
                           "transcription": round(tr_ms, 4)},
            "transcription_roofline": {"bound": "hbm", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS,
                                       "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 5),

@@ -539,6 +539,104 @@ __device__ inline void dev_apply_wraps(const DevModel& M, int im, const POSES& X
     }
 }
 
+// ---- wrapped muscles in generated back ends (codegen.py wrapped_muscle) ----
+// The generated code builds the active path points (positions, velocities)
+// of a wrapped muscle in straight-line code, then hands the data-dependent
+// part -- GeometryPath::applyWrapObjects (dev_apply_wraps above, the
+// interpreter's own), the path length and lengthening speed, and the point
+// forces of the tension -- to these two helpers.  Poses / velocities of the
+// wrap bodies come from the generated kinematics (xb: pose index = body + 1).
+template <int NWB>
+struct GenWrapPoses {
+    const Pose* p;
+    const int* b;
+    __device__ __forceinline__ const Pose& operator[](int bs) const {
+        for (int i = 0; i + 1 < NWB; ++i)
+            if (b[i] == bs) return p[i];
+        return p[NWB - 1];
+    }
+};
+template <int NWB>
+struct GenWrapVels {
+    const SV* v;
+    const int* b;
+    __device__ __forceinline__ const SV& operator[](int bs) const {
+        for (int i = 0; i + 1 < NWB; ++i)
+            if (b[i] == bs) return v[i];
+        return v[NWB - 1];
+    }
+};
+
+template <int MP, int NWB>
+__device__ __noinline__ void gen_wrap_path(const DevModel& M, int im, const Pose* xp, const SV* xv,
+        const int* xb, CPath<MP>& C, double& L, double& S) {
+#pragma clang fp contract(off)
+    const GenWrapPoses<NWB> X{xp, xb};
+    const GenWrapVels<NWB> V{xv, xb};
+    auto active = [&](int i) {
+        for (int k = 0; k < C.n; ++k)
+            if (C.pt[k] == i) return true;
+        return false;
+    };
+    dev_apply_wraps<MP>(M, im, X, V, active, C);
+    // the interpreter's length / speed loop (dae_eval), operation for operation
+    L = 0.0;
+    S = 0.0;
+    for (int k = 1; k < C.n; ++k) {
+        const double d0 = C.P[k][0] - C.P[k - 1][0], d1 = C.P[k][1] - C.P[k - 1][1],
+                     d2 = C.P[k][2] - C.P[k - 1][2];
+        const double l = sqrt(d0 * d0 + d1 * d1 + d2 * d2);
+        if (C.arc(k)) L += C.wlen[k];
+        else L += l;
+        const double e0 = C.V[k][0] - C.V[k - 1][0], e1 = C.V[k][1] - C.V[k - 1][1],
+                     e2 = C.V[k][2] - C.V[k - 1][2];
+        S += (d0 * e0 + d1 * e1 + d2 * e2) / l;
+    }
+}
+
+// Point forces of tension T along the wrapped path: per original path point
+// (index within the muscle) and per PathWrap entry of the muscle (its
+// tangent points, on the wrap body), force f and moment P x f summed; zero
+// for inactive points and untouched surfaces.
+template <int MP, int NPT, int NW>
+__device__ __noinline__ void gen_wrap_forces(const DevModel& M, int im, const CPath<MP>& C, double T,
+        double (*fp)[3], double (*np)[3], double (*fw)[3], double (*nw)[3]) {
+#pragma clang fp contract(off)
+    for (int i = 0; i < NPT; ++i)
+        for (int d = 0; d < 3; ++d) { fp[i][d] = 0.0; np[i][d] = 0.0; }
+    for (int i = 0; i < NW; ++i)
+        for (int d = 0; d < 3; ++d) { fw[i][d] = 0.0; nw[i][d] = 0.0; }
+    const int pb = M.mus[im].point_begin, wb = M.mus_pw_begin[im];
+    for (int k = 1; k < C.n; ++k) {
+        if (C.arc(k)) continue;   // a wrap's surface part: both ends on one body
+        const double d0 = C.P[k][0] - C.P[k - 1][0], d1 = C.P[k][1] - C.P[k - 1][1],
+                     d2 = C.P[k][2] - C.P[k - 1][2];
+        const double l = sqrt(d0 * d0 + d1 * d1 + d2 * d2);
+        const double F0 = T * d0 / l, F1 = T * d1 / l, F2 = T * d2 / l;
+        for (int side = 0; side < 2; ++side) {
+            const int kk = side == 0 ? k - 1 : k;
+            const double sg = side == 0 ? 1.0 : -1.0;
+            const double f0 = sg * F0, f1 = sg * F1, f2 = sg * F2;
+            double n0, n1, n2;
+            cross3(C.P[kk][0], C.P[kk][1], C.P[kk][2], f0, f1, f2, n0, n1, n2);
+            double* fa;
+            double* na;
+            if (C.pt[kk] < 0) {
+                if (C.body[kk] < 0) continue;
+                const int s = C.pwi[kk] - wb;
+                if (s < 0 || s >= NW) continue;
+                fa = fw[s]; na = nw[s];
+            } else {
+                const int i = C.pt[kk] - pb;
+                if (i < 0 || i >= NPT) continue;
+                fa = fp[i]; na = np[i];
+            }
+            fa[0] += f0; fa[1] += f1; fa[2] += f2;
+            na[0] += n0; na[1] += n1; na[2] += n2;
+        }
+    }
+}
+
 // Per-lane workspace.  MB = max bodies (excluding ground), MQ = max
 // coordinates, MP = max path points per muscle.
 template <int MB, int MQ, int MP>

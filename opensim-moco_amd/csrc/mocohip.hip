@@ -407,7 +407,11 @@ static void build_taskset(const TaskInfo& ti, const Lanes& ln, int nk, int nsimd
     ts.blk.clear();
     ts.flops = 0.0;
     ts.ntasks = 0.0;
+    // timing diagnostic only (results invalid): launch group G's blocks alone
+    const char* dg = std::getenv("MOCOHIP_DEBUG_GROUP");
+    const int only = dg ? std::atoi(dg) : -1;
     for (int g : order) {
+        if (only >= 0 && g != only) continue;
         const long n = (long)nk * ts.dlen[g];
         const float inv = 1.0f / (float)ts.dlen[g];
         int inv_bits;

@@ -704,6 +704,11 @@ class _Emitter:
             pos.append(Pw)
             vel.append(Vw)
             dl_funcs.append(mov)
+        pws = self.path_wraps(im)
+        if pws:
+            self.wrapped_muscle(im, mu, pts, pos, vel, act, dl_funcs, pws, R, P, V, Facc, tau, zdot_sink,
+                                with_adot, resid_sink)
+            return
         segs = []
         for i in range(len(pts)):
             for j in range(i - 1, -1, -1):
@@ -722,20 +727,7 @@ class _Emitter:
             L = g.add(L, l if ind is None else g.mul(ind, l))
             Sp = g.add(Sp, sp if ind is None else g.mul(ind, sp))
             seginfo.append((j, i, d, l, ind))
-        exc = self.ctrl[Lo.mus_control[im]]
-        sa, sf = Lo.act_state[im], Lo.ftn_state[im]
-        a_ = self.inp[Lo.sin(sa)] if sa >= 0 else exc
-        ftn = self.inp[Lo.sin(sf)] if sf >= 0 else None
-        idv = Lo.ider[im]
-        dft = self.inp[Lo.NS + Lo.NC + idv] if idv >= 0 else None
-        T, adot, ftdot, resid = _dgf(g, mu, L, Sp, a_, exc, sa >= 0 and with_adot, ftn, sf >= 0,
-                                     Lo.tau_act, Lo.tau_deact, dft)
-        if sa >= 0 and with_adot:
-            zdot_sink(sa, adot)
-        if sf >= 0:
-            zdot_sink(sf, ftdot)
-        if resid is not None and resid_sink is not None:
-            resid_sink(idv - Lo.NACC, resid)
+        T = self.muscle_force(im, mu, L, Sp, zdot_sink, with_adot, resid_sink)
         for (j, i, d, l, ind) in seginfo:
             Tl = g.div(T, l) if ind is None else g.mul(ind, g.div(T, l))
             Fv = g.vscale(d, Tl)
@@ -752,6 +744,104 @@ class _Emitter:
                 for (dd, coord, d1) in dl_funcs[kk]:
                     Rb = R[pt.body]
                     self.acc(tau[coord], g.mul(g.dot([Rb[dd], Rb[3 + dd], Rb[6 + dd]], f), d1))
+
+    def muscle_force(self, im, mu, L: S, Sp: S, zdot_sink, with_adot, resid_sink) -> S:
+        """DeGroote-Fregly tension of muscle im at path length L and
+        lengthening speed Sp; the activation / tendon-force derivatives and
+        the implicit-tendon residual go to their sinks."""
+        g, Lo = self.g, self.Lo
+        exc = self.ctrl[Lo.mus_control[im]]
+        sa, sf = Lo.act_state[im], Lo.ftn_state[im]
+        a_ = self.inp[Lo.sin(sa)] if sa >= 0 else exc
+        ftn = self.inp[Lo.sin(sf)] if sf >= 0 else None
+        idv = Lo.ider[im]
+        dft = self.inp[Lo.NS + Lo.NC + idv] if idv >= 0 else None
+        T, adot, ftdot, resid = _dgf(g, mu, L, Sp, a_, exc, sa >= 0 and with_adot, ftn, sf >= 0,
+                                     Lo.tau_act, Lo.tau_deact, dft)
+        if sa >= 0 and with_adot:
+            zdot_sink(sa, adot)
+        if sf >= 0:
+            zdot_sink(sf, ftdot)
+        if resid is not None and resid_sink is not None:
+            resid_sink(idv - Lo.NACC, resid)
+        return T
+
+    def path_wraps(self, im):
+        """Muscle im's PathWrap entries [(entry, wrap object, wrap body)]:
+        structure (their count, objects and bodies are match() conditions;
+        the cylinders' geometry and the ranges are read at run time)."""
+        out = []
+        for k, pw in enumerate(self.M.pathwraps):
+            if pw.muscle != im:
+                continue
+            w = pw.wrap
+            out.append((k, w, self.M.wraps[w].body))
+        return out
+
+    def muscle_bodies(self, im):
+        """Bodies whose pose muscle im's path reads: its path points' and
+        its wrap surfaces' (ground excluded)."""
+        mu = self.M.muscles[im]
+        bs = {self.M.points[i].body for i in range(mu.point_begin, mu.point_begin + mu.point_count)}
+        bs |= {wb for (_, _, wb) in self.path_wraps(im)}
+        return sorted(b for b in bs if b >= 0)
+
+    def wrapped_muscle(self, im, mu, pts, pos, vel, act, dl_funcs, pws, R, P, V, Facc, tau, zdot_sink,
+                       with_adot, resid_sink):
+        """A muscle whose path wraps over cylinders (GeometryPath::
+        applyWrapObjects): the path is data-dependent (tangent points come
+        and go with the pose), so it is built at run time -- the active path
+        points from the generated positions and velocities, then the
+        interpreter's own wrapping (dae_device.hpp dev_apply_wraps), path
+        length and speed (mh::gen_wrap_path) -- and the tension's point
+        forces come back per original path point and per wrap surface
+        (mh::gen_wrap_forces), to be applied to the bodies known here."""
+        g = self.g
+        npt, nw = len(pts), len(pws)
+        MP = npt + 2 * nw
+        g.k += 1
+        k = g.k
+        C = f"cp{k}"
+        g.raw(f"mh::CPath<{MP}> {C}; {C}.n = 0;")
+        for kk, pt in enumerate(pts):
+            st = " ".join(f"{C}.P[{C}.n][{d}] = {pos[kk][d]}; {C}.V[{C}.n][{d}] = {vel[kk][d]};"
+                          for d in range(3))
+            st += (f" {C}.pt[{C}.n] = {mu.point_begin + kk}; {C}.pwi[{C}.n] = -1; "
+                   f"{C}.body[{C}.n] = {pt.body}; {C}.wlen[{C}.n] = 0.0; ++{C}.n;")
+            g.raw(f"if ({act[kk]}) {{ {st} }}" if act[kk] else f"{{ {st} }}")
+        wbs = sorted({wb for (_, _, wb) in pws})
+        poses = ", ".join("{{" + ", ".join(str(x) for x in R[b]) + "}, {" + ", ".join(str(x) for x in P[b]) + "}}"
+                          for b in wbs)
+        vels = ", ".join("{" + ", ".join(str(x) for x in list(V[b][0]) + list(V[b][1])) + "}" for b in wbs)
+        nb = len(wbs)
+        g.raw(f"const mh::Pose xp{k}[{nb}] = {{{poses}}};")
+        g.raw(f"const mh::SV xv{k}[{nb}] = {{{vels}}};")
+        g.raw(f"const int xb{k}[{nb}] = {{{', '.join(str(b + 1) for b in wbs)}}};")
+        g.raw(f"double L{k}, S{k}; mh::gen_wrap_path<{MP}, {nb}>(M, {im}, xp{k}, xv{k}, xb{k}, {C}, L{k}, S{k});")
+        g.flops["fn"] += 40 * nw + 12 * npt
+        T = self.muscle_force(im, mu, S(n=f"L{k}"), S(n=f"S{k}"), zdot_sink, with_adot, resid_sink)
+        g.raw(f"double fp{k}[{npt}][3], np{k}[{npt}][3], fw{k}[{nw}][3], nw{k}[{nw}][3];")
+        g.raw(f"mh::gen_wrap_forces<{MP}, {npt}, {nw}>(M, {im}, {C}, {T}, fp{k}, np{k}, fw{k}, nw{k});")
+        g.flops["add"] += 12 * (npt + 2 * nw)
+        g.flops["mul"] += 12 * (npt + 2 * nw)
+
+        def apply(b, f, n):
+            fa = Facc[b]
+            for c in range(3):
+                self.acc(fa[c], n[c], -1.0)
+                self.acc(fa[3 + c], f[c], -1.0)
+        for kk, pt in enumerate(pts):
+            if pt.body < 0:
+                continue
+            f = [S(n=f"fp{k}[{kk}][{c}]") for c in range(3)]
+            apply(pt.body, f, [S(n=f"np{k}[{kk}][{c}]") for c in range(3)])
+            for (dd, coord, d1) in dl_funcs[kk]:
+                Rb = R[pt.body]
+                self.acc(tau[coord], g.mul(g.dot([Rb[dd], Rb[3 + dd], Rb[6 + dd]], f), d1))
+        for s, (_, _, wb) in enumerate(pws):
+            if wb >= 0:
+                apply(wb, [S(n=f"fw{k}[{s}][{c}]") for c in range(3)],
+                      [S(n=f"nw{k}[{s}][{c}]") for c in range(3)])
 
     def body_force_vars(self, bodies, init):
         out = {}
@@ -1253,9 +1343,7 @@ def _emit_groups(M: ModelView, Lo: _Layout) -> List[_Group]:
     # muscles
     for im, mu in enumerate(M.muscles):
         E = _Emitter(M, Lo)
-        bodies = sorted({M.points[i].body for i in range(mu.point_begin, mu.point_begin + mu.point_count)
-                         if M.points[i].body >= 0})
-        cl = E.closure(bodies)
+        cl = E.closure(E.muscle_bodies(im))
         R, P, V, _, Sj, cb = E.kinematics(cl, accel=False)
         Facc = E.body_force_vars(cl, None)
         tv = [E.g.var(_c(0.0)) for _ in range(NQ)]

@@ -43,8 +43,8 @@ class MocoHipSolver:
     optim_sparsity_detection: str = "none"
     optim_sparsity_detection_random_count: int = 3
     # how a detection probe decides a coupling (include/mocohip.h
-    # mh_sparsity_rule): "robust" (default; changes below 1e-10 of the
-    # output's magnitude are rounding noise -- the pattern is the model's,
+    # mh_sparsity_rule): "robust" (default; changes below 1e-12 of the
+    # callback's output magnitude are rounding noise -- the pattern is the model's,
     # the same in every implementation) or "any-change" (the reference's
     # rule, CasOCFunction.cpp:44-61, which makes couplings that cancel to
     # rounding level depend on the order of floating-point operations)

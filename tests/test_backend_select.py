@@ -32,6 +32,20 @@ def test_bundled_models_select_their_generated_back_end():
     assert _backend(configs.double_pendulum_coupled(4)) == "generated:coupled_pendulum"
     assert _backend(configs.rajagopal80(4)) == "generated:rajagopal80"
     assert _backend(configs.rajagopal18_inverse(4)) == "generated:rajagopal18_inverse"
+    # muscle wrapping over cylinders (PathWraps kept)
+    assert _backend(configs.wrapped_pendulum(4)) == "generated:wrapped_pendulum"
+    assert _backend(configs.rajagopal80(4, keep_path_wraps=True)) == "generated:rajagopal80_wrapped"
+    assert _backend(configs.rajagopal18_inverse(4, keep_path_wraps=True)) == \
+        "generated:rajagopal18_inverse_wrapped"
+    # the wrap geometry is run-time data: another quadrant / radius / offset
+    # keeps the code
+    for quad in ("+x", "-y"):
+        assert _backend(configs.wrapped_pendulum(4, quadrant=quad)) == "generated:wrapped_pendulum"
+    st = configs.rajagopal80(4, keep_path_wraps=True)
+    for w in st.problem.model.wraps.values():
+        w.radius *= 1.05
+        w.translation = tuple(x + 0.001 for x in w.translation)
+    assert _backend(st) == "generated:rajagopal80_wrapped"
     # other constraint-derivative settings than generated: the interpreter
     assert _backend(configs.double_pendulum_coupled(4, enforce_constraint_derivatives=False)).startswith(
         "generic")

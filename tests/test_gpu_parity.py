@@ -186,6 +186,9 @@ CASES = {
     "gait_rigid_scaled_subject": lambda: _scaled(configs.gait10dof18musc(6)),
     "gait_inverse_scaled_subject": lambda: _scaled(configs.gait10dof18musc_inverse(4, sparsity="none")),
     "rajagopal80_wrapped_trap": lambda: _trap(configs.rajagopal80(2, keep_path_wraps=True)),
+    # the wrapped Rajagopal 80 in the generated back end's configuration (HS,
+    # velocity-correction slacks)
+    "rajagopal80_wrapped": lambda: configs.rajagopal80(2, keep_path_wraps=True),
 }
 
 
@@ -636,7 +639,10 @@ def test_generated_backends_are_selected_for_bundled_models():
     for name in ["sliding_mass", "double_pendulum_hs", "gait_rigid_forward",
                  "gait_compliant_central", "gait_torque_driven", "sliding_mass_implicit",
                  "double_pendulum_implicit_hs", "gait_rigid_implicit", "gait_rigid_pathcon",
-                 "gait_implicit_tendon", "gait_implicit_both_central", "gait_inverse"]:
+                 "gait_implicit_tendon", "gait_implicit_both_central", "gait_inverse",
+                 "coupled_pendulum", "rajagopal18_inverse", "rajagopal80", "wrapped_pendulum",
+                 "rajagopal18_inverse_wrapped", "rajagopal80_wrapped",
+                 "gait_rigid_heavy_femur", "gait_rigid_scaled_subject"]:
         gpu, _, _ = _pair(name)
         be, flops, _ = gpu.backend()
         assert be.startswith("generated:"), (name, be)
@@ -654,7 +660,8 @@ def test_fused_g_jac_identical_to_separate_calls(name):
 
 @pytest.mark.parametrize("name", ["double_pendulum_hs", "gait_rigid_forward", "gait_rigid_central",
                                   "gait_compliant_central", "gait_torque_driven", "gait_rigid_implicit",
-                                  "gait_implicit_tendon", "gait_inverse"])
+                                  "gait_implicit_tendon", "gait_inverse", "coupled_pendulum",
+                                  "wrapped_pendulum", "rajagopal18_inverse_wrapped"])
 def test_pruned_tasks_bit_identical(name):
     """Re-evaluating only the groups a direction perturbs gives exactly the
     Jacobian of re-evaluating every group for every direction: the reused
@@ -677,7 +684,7 @@ def test_pruned_tasks_bit_identical(name):
                                   "pendulum_bound_equality_trap", "pendulum_bound_both_implicit",
                                   "gait_rigid_sparse_random", "gait_implicit_pathcon_sparse",
                                   "gait_inverse_random", "double_pendulum_nointerp",
-                                  "gait_rigid_nointerp_trap"])
+                                  "gait_rigid_nointerp_trap", "wrapped_pendulum", "coupled_pendulum"])
 @pytest.mark.parametrize("variant", [{"MOCOHIP_INTERVAL": "0"},
                                      {"MOCOHIP_INTERVAL": "0", "MOCOHIP_ASM": "gs"},
                                      {"MOCOHIP_INTERVAL": "0", "MOCOHIP_QUOT": "1"},
@@ -754,7 +761,8 @@ SPARSE = [n for n in CASES if "sparse" in n]
 def test_sparsity_detection_agrees(name):
     """Detected sparsity is bit-reproducible: with the default rule
     (include/mocohip.h MH_SPARSITY_RULE_ROBUST: a probe counts as a coupling
-    when its change exceeds 1e-10 of the output's magnitude, or is NaN) the
+    when its change exceeds 1e-12 of the callback's output magnitude at that
+    detection point, or is NaN) the
     device's detection (mh_create, on its own kernels) and the oracle's (the
     CPU restatement) give the SAME pattern, coupling for coupling, and so
     the same NLP structure (every sparse parity case builds the oracle from
@@ -1072,7 +1080,7 @@ def test_batch_rejects_other_shapes():
     b = HipNLP(configs.gait10dof18musc(8).problem.create_rep(), configs.gait10dof18musc(8).solver.options())
     with pytest.raises(RuntimeError, match="shape differs"):
         HipBatch([a, b])
-    st = configs.wrapped_pendulum(6)    # generic interpreter: no task back end
+    st = configs.wrapped_pendulum(6, tendon_compliance=True)    # generic interpreter: no task back end
     c = HipNLP(st.problem.create_rep(), st.solver.options())
     with pytest.raises(RuntimeError, match="error 3"):
         HipBatch([c])
