@@ -68,9 +68,15 @@ struct GenericDae {
     static constexpr int MI = Z::MI, MO = Z::MO;
     static constexpr bool SPLIT = false;
     static constexpr bool EXC_LANES = true;   // k_exc_lanes reproduces its excitation lanes
+    using W = Work<Z::MB, Z::MQ, Z::MP>;      // per-lane multibody workspace
     __device__ __forceinline__ static void eval(const DevModel& M, double t, const double* in,
             double* out) {
-        Work<Z::MB, Z::MQ, Z::MP> w;
+        W w;
+        eval_w(M, t, in, out, w);
+    }
+    // the same with the workspace where the caller puts it (k_eval_lds: LDS)
+    __device__ __forceinline__ static void eval_w(const DevModel& M, double t, const double* in,
+            double* out, W& w) {
         if (M.presc) {
             // prescribed kinematics: [q, u] and udot from the motion, the
             // NLP states are the auxiliary states
@@ -190,6 +196,34 @@ __global__ void __launch_bounds__(64) k_eval(DevModel M, Layout L, Lanes Ln,
         double* __restrict__ times, double* __restrict__ Y, const int* __restrict__ map = nullptr,
         int nmap = 0) {
     eval_lane<D>(M, L, Ln, x, grid, times, Y, map, nmap);
+}
+// The generic interpreter's lanes with their multibody workspace (D::W:
+// poses, velocities, body forces, motion subspaces, tau, mass matrix) in LDS
+// instead of scratch: one slot per thread of the workgroup (blockDim.x <=
+// 16 lanes, launched with blockDim.x * sizeof(W) bytes of dynamic LDS).  A
+// thread past the last lane returns before it touches LDS, so every slot
+// address stays inside the allocation.  Same arithmetic as k_eval, bit for
+// bit (tests/test_gpu_parity.py::test_eval_g_lds_workspace_bit_identical).
+template <class D>
+__global__ void __launch_bounds__(16) k_eval_lds(DevModel M, Layout L, Lanes Ln,
+        const double* __restrict__ x, const double* __restrict__ grid,
+        double* __restrict__ times, double* __restrict__ Y) {
+    extern __shared__ double smem[];
+    typename D::W* ws = reinterpret_cast<typename D::W*>(smem);
+    const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= (long)L.nk * Ln.stride) return;
+    const int kl = (int)(gid / Ln.stride);
+    const int r = (int)(gid - (long)kl * Ln.stride);
+    const int k = L.k0 + kl;
+    double in[D::MI];
+    double out[D::MO];
+    const double t = lane_inputs<D>(L, Ln, x, grid[k], k, r, in);
+    if (r == Ln.base) times[kl] = t;
+    D::eval_w(M, t, in, out, ws[threadIdx.x]);
+    double* Yk = Y + (long)kl * L.NO * Ln.stride + r;
+#pragma unroll
+    for (int o = 0; o < D::MO; ++o)
+        if (o < L.NO) Yk[(long)o * Ln.stride] = out[o];
 }
 // Excitation lanes of the generic interpreter.  A lane that perturbs the
 // excitation of a muscle with activation dynamics changes one DAE output,
@@ -1199,8 +1233,10 @@ __global__ void __launch_bounds__(1024) k_interval(DevModel M, Src S, Lanes Ln, 
         Interval I, const TplEntry* __restrict__ tpl, const uint32_t* __restrict__ ctpl,
         const int* __restrict__ ctgen, int nctgen,
         const double* __restrict__ T, const double* __restrict__ H, double* __restrict__ g,
-        double* __restrict__ values) {
-    interval_body<D, false>(M, S, Ln, TK, L, I, tpl, ctpl, ctgen, nctgen, T, H, g, values, blockIdx.x);
+        double* __restrict__ values, int il0) {
+    // il0: the first interval of this launch within the shard (a chunked
+    // assembly, whose chunks are copied to the host while the next runs)
+    interval_body<D, false>(M, S, Ln, TK, L, I, tpl, ctpl, ctgen, nctgen, T, H, g, values, il0 + (int)blockIdx.x);
 }
 
 // ------------------------------------------------------------------------
@@ -1820,6 +1856,13 @@ struct mh_ctx {
     int iv_pf = 1;                     // MOCOHIP_IV_PF=0: no assembly-word prefetch (A/B)
     int iv_qfuse = 1;                  // MOCOHIP_IV_QFUSE=0: in-place quotient pass (A/B)
     hipEvent_t ev[5] = {};         // stage boundaries (+ ev[4] after k_groups)
+    // host entries: the Jacobian values go to the host in interval chunks on
+    // copy_stream while the next chunk's k_interval runs (MOCOHIP_D2H_CHUNKS)
+    static constexpr int kMaxD2hChunks = 16;
+    int d2h_chunks = 4;
+    hipStream_t copy_stream = nullptr;
+    hipEvent_t ev_chunk[kMaxD2hChunks] = {};
+    hipEvent_t ev_copied = nullptr;
     char* dmem = nullptr;
     DevModel M{};
     GoalSet GS{};
@@ -1834,6 +1877,7 @@ struct mh_ctx {
     int* d_lane_map = nullptr;     // the other lanes, in order (k_eval's lane map)
     int n_exc_lanes = 0;
     int g_block = 4;               // generic interpreter, eval_g: k_eval workgroup size (A/B: profiles/r02_l)
+    bool g_lds = false;            // generic interpreter, eval_g: workspace in LDS (k_eval_lds)
     uint32_t* d_ctpl = nullptr;    // compiled template of the Jacobian lanes (k_interval)
     std::vector<uint32_t> ctpl;
     int* d_ctgen = nullptr;        // the entries it leaves to jac_entry (t0 / tf of defect rows)
@@ -1942,7 +1986,8 @@ struct Backend {
     const TaskInfo* tasks;   // task-decomposed back ends (else one lane per DAE)
     // task back ends: fused combine + transcription (k_interval) for lanes
     // of mode 0/1 writing g and/or values; null for one-lane back ends
-    void (*interval)(mh_ctx*, const double* x, int mode, double* g, double* v);
+    // (intervals [i0, i1) of the shard; i1 < 0: all)
+    void (*interval)(mh_ctx*, const double* x, int mode, double* g, double* v, int i0, int i1);
     size_t (*interval_bytes)(const mh_ctx*, int mode);   // its LDS need
     // raw outputs of every Jacobian lane into Y ([point][output][lane]) and
     // the base-lane times into d_times, whatever path eval_jac_g takes
@@ -1964,6 +2009,16 @@ static void be_eval_lane(mh_ctx* c, const double* x, int mode, double* Y) {
         // wave each) keep a wave's scratch within its CU's L1
         // (MOCOHIP_G_BLOCK; k_eval indexes by blockDim, any size <= 64 works)
         const int tb = (mode == 0 && D::EXC_LANES) ? c->g_block : 64;
+        if constexpr (D::EXC_LANES) {   // the generic interpreter (GenericDae)
+            if (mode == 0 && c->g_lds) {
+                // MOCOHIP_G_LDS: the workspace in LDS, tb <= 16 slots per workgroup
+                const int tl = std::max(1, std::min({tb, 16, (int)(65536 / sizeof(typename D::W))}));
+                const size_t lds = sizeof(typename D::W) * (size_t)tl;
+                hipLaunchKernelGGL(k_eval_lds<D>, dim3((unsigned)((lanes + tl - 1) / tl)), dim3(tl), lds,
+                        c->stream, c->M, L, ln, x, c->d_grid, c->d_times, Y);
+                return;
+            }
+        }
         hipLaunchKernelGGL(k_eval<D>, dim3((unsigned)((lanes + tb - 1) / tb)), dim3(tb), 0, c->stream, c->M, L,
                 ln, x, c->d_grid, c->d_times, Y, nullptr, 0);
         return;
@@ -2064,7 +2119,7 @@ static void be_batch(mh_batch* bt, int mode, const BatchPtrs& BP, int with_g, in
             (int)c->ctgen.size(), with_g, with_v, c->nep, c->nnz_ep);
 }
 template <class D>
-static void be_interval(mh_ctx* c, const double* x, int mode, double* g, double* v) {
+static void be_interval(mh_ctx* c, const double* x, int mode, double* g, double* v, int i0, int i1) {
     const Src S = src_of(c, x);
     const Lanes& ln = mode ? c->lanes_jac : c->lanes_g;
     const TaskSet& ts = mode ? c->ts_jac : c->ts_g;
@@ -2093,9 +2148,11 @@ static void be_interval(mh_ctx* c, const double* x, int mode, double* g, double*
     if (lds > 65536)
         (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     const unsigned threads = v ? (unsigned)c->iv_threads : 256u;
-    hipLaunchKernelGGL(kern, dim3((unsigned)(c->ie - c->ib)), dim3(threads), lds, c->stream, c->M,
+    if (i1 < 0) { i0 = 0; i1 = c->ie - c->ib; }
+    if (i1 <= i0) return;
+    hipLaunchKernelGGL(kern, dim3((unsigned)(i1 - i0)), dim3(threads), lds, c->stream, c->M,
             S, ln, ts.dev, L, I, c->d_tpl, (mode == 1 && c->use_ctpl) ? c->d_ctpl : nullptr, c->d_ctgen,
-            (int)c->ctgen.size(), c->d_T, c->d_H, g, v);
+            (int)c->ctgen.size(), c->d_T, c->d_H, g, v, i0);
 }
 template <class D>
 static void be_integrand(mh_ctx* c, const double* x) {

@@ -1403,6 +1403,7 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     c->GS.gw = (const double*)(b + o_gw);
     if (c->n_exc_lanes) { c->d_exc = (int*)(b + o_exc); c->d_lane_map = (int*)(b + o_lmap); }
     if (const char* eb = std::getenv("MOCOHIP_G_BLOCK")) c->g_block = std::min(64, std::max(1, std::atoi(eb)));
+    if (const char* el = std::getenv("MOCOHIP_G_LDS")) c->g_lds = std::atoi(el) != 0;
     c->d_grid = (double*)(b + o_grid); c->d_quad = (double*)(b + o_quad);
     c->d_tpl = (TplEntry*)(b + o_tpl);
     c->d_ctpl = (uint32_t*)(b + o_ctpl);
@@ -1510,6 +1511,11 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
             c->use_interval[mode] = allow && interval_fits(c.get(), mode);
     }
     for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
+    if (const char* ek = std::getenv("MOCOHIP_D2H_CHUNKS"))
+        c->d2h_chunks = std::min(mh_ctx::kMaxD2hChunks, std::max(1, std::atoi(ek)));
+    HIPCHK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+    for (auto& e : c->ev_chunk) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&c->ev_copied, hipEventDisableTiming));
     *out = c.release();
     return MH_OK;
 }
@@ -1520,6 +1526,13 @@ extern "C" void mh_destroy(mh_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);
+    for (auto& e : c->ev_chunk)
+        if (e) (void)hipEventDestroy(e);
+    if (c->ev_copied) (void)hipEventDestroy(c->ev_copied);
+    if (c->copy_stream) {
+        (void)hipStreamSynchronize(c->copy_stream);
+        (void)hipStreamDestroy(c->copy_stream);
+    }
     if (c->own_stream) {
         (void)hipStreamSynchronize(c->own_stream);
         (void)hipStreamDestroy(c->own_stream);
@@ -1702,7 +1715,7 @@ static int launch_stage(mh_ctx* c, int stage, int kind, const double* x, double*
     double* g = kind == 1 ? nullptr : a;
     double* v = kind == 0 ? nullptr : (kind == 1 ? a : b);
     if (c->use_interval[kind == 0 ? 0 : 1] && !glane) {
-        c->be->interval(c, x, kind == 0 ? 0 : 1, g, v);
+        c->be->interval(c, x, kind == 0 ? 0 : 1, g, v, 0, -1);
         HIPCHK(hipGetLastError());
         return MH_OK;
     }
@@ -1978,14 +1991,59 @@ extern "C" int mh_eval_g(mh_ctx* c, const double* x, int, double* g) {
     return finish(c);
 }
 
+// The host entries' Jacobian: eval_jac_g's k_interval launched in interval
+// chunks, each chunk's values (a contiguous slice: the head with the first,
+// the tail with the last) copied to the host on copy_stream as soon as that
+// chunk's launch completes, while the next chunk assembles -- the PCIe
+// transfer, which bounds a host-buffer call (15.4 MB at N = 200), overlaps the
+// assembly instead of following it.  Same kernels, same values.  Paths
+// without a per-interval task launch copy the whole block after the call.
+static int jac_to_host(mh_ctx* c, int kind, double* g_host, double* v_host) {
+    const int nint = c->ie - c->ib;
+    const int nch = std::min(c->d2h_chunks, nint);
+    const size_t nnz = shard_nnz(c), rows = shard_rows(c);
+    double* gd = kind == 2 ? c->d_g : nullptr;
+    if (nch <= 1 || c->use_graphs || c->jac_seeds || c->timing || !c->be->tasks || !c->be->interval ||
+            !c->use_interval[1] || c->use_roles || c->iv_dbg_stop) {
+        int rc = run_cached(c, kind, c->d_x, kind == 2 ? c->d_g : c->d_vals, kind == 2 ? c->d_vals : nullptr);
+        if (rc) return rc;
+        if (kind == 2)
+            HIPCHK(hipMemcpyAsync(g_host, c->d_g, sizeof(double) * rows, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(v_host, c->d_vals, sizeof(double) * nnz, hipMemcpyDeviceToHost, c->stream));
+        return MH_OK;
+    }
+    int rc = run_stage(c, 0, kind, c->d_x, kind == 2 ? c->d_g : c->d_vals, kind == 2 ? c->d_vals : nullptr);
+    if (rc) return rc;
+    const size_t head = c->ib == 0 ? (size_t)c->nnz_ep : 0;
+    // every chunk's launch first (a copy into pageable memory can block the
+    // host until it completes; the kernels are queued by then), then the copies
+    for (int k = 0; k < nch; ++k) {
+        const int i0 = (int)((long)nint * k / nch), i1 = (int)((long)nint * (k + 1) / nch);
+        c->be->interval(c, c->d_x, 1, gd, c->d_vals, i0, i1);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(c->ev_chunk[k], c->stream));
+    }
+    for (int k = 0; k < nch; ++k) {
+        const int i0 = (int)((long)nint * k / nch), i1 = (int)((long)nint * (k + 1) / nch);
+        HIPCHK(hipStreamWaitEvent(c->copy_stream, c->ev_chunk[k], 0));
+        const size_t from = k == 0 ? 0 : head + (size_t)i0 * c->nnz_int;
+        const size_t to = k == nch - 1 ? nnz : head + (size_t)i1 * c->nnz_int;
+        HIPCHK(hipMemcpyAsync(v_host + from, c->d_vals + from, sizeof(double) * (to - from),
+                hipMemcpyDeviceToHost, c->copy_stream));
+    }
+    if (kind == 2)
+        HIPCHK(hipMemcpyAsync(g_host, c->d_g, sizeof(double) * rows, hipMemcpyDeviceToHost, c->copy_stream));
+    HIPCHK(hipEventRecord(c->ev_copied, c->copy_stream));
+    HIPCHK(hipStreamWaitEvent(c->stream, c->ev_copied, 0));
+    return MH_OK;
+}
+
 extern "C" int mh_eval_jac_g(mh_ctx* c, const double* x, int, double* values) {
     if (!c || !x || !values) return set_err(MH_ERR_INVALID, "null argument");
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipMemcpyAsync(c->d_x, x, sizeof(double) * c->n, hipMemcpyHostToDevice, c->stream));
-    int rc = run_cached(c, 1, c->d_x, c->d_vals, nullptr);
+    const int rc = jac_to_host(c, 1, nullptr, values);
     if (rc) return rc;
-    HIPCHK(hipMemcpyAsync(values, c->d_vals, sizeof(double) * shard_nnz(c),
-            hipMemcpyDeviceToHost, c->stream));
     return finish(c);
 }
 
@@ -2114,12 +2172,8 @@ extern "C" int mh_eval_g_jac_g(mh_ctx* c, const double* x, double* g, double* va
     if (!c || !x || !g || !values) return set_err(MH_ERR_INVALID, "null argument");
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipMemcpyAsync(c->d_x, x, sizeof(double) * c->n, hipMemcpyHostToDevice, c->stream));
-    int rc = run_cached(c, 2, c->d_x, c->d_g, c->d_vals);
+    const int rc = jac_to_host(c, 2, g, values);
     if (rc) return rc;
-    HIPCHK(hipMemcpyAsync(g, c->d_g, sizeof(double) * shard_rows(c),
-            hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipMemcpyAsync(values, c->d_vals, sizeof(double) * shard_nnz(c),
-            hipMemcpyDeviceToHost, c->stream));
     return finish(c);
 }
 
@@ -2499,6 +2553,7 @@ extern "C" int mh_get_backend_flags(const mh_ctx* c, char* flags, int32_t len) {
     if (c->quot) f += " quot";
     if (c->asm_grid_stride) f += " asm-gs";
     if (c->d_exc) f += " exc-lanes";
+    if (c->g_lds && !c->be->tasks && std::strncmp(c->be->name, "generic", 7) == 0) f += " g-lds";
     std::strncpy(flags, f.c_str(), (size_t)len - 1);
     flags[len - 1] = 0;
     return MH_OK;

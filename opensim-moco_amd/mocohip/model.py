@@ -82,9 +82,25 @@ def rot_z(a):
     return np.array([[c, -s, 0], [s, c, 0], [0, 0, 1]], float)
 
 
+def _mm3(A, B):
+    """3x3 product with each entry summed left to right (no BLAS): the same
+    IEEE operations as the C++ builder (csrc/host/mh_builder.cpp mm3)."""
+    return [[(A[i][0] * B[0][j] + A[i][1] * B[1][j]) + A[i][2] * B[2][j] for j in range(3)]
+            for i in range(3)]
+
+
 def body_fixed_xyz(angles) -> np.ndarray:
-    """OpenSim frame orientation: Euler XYZ body-fixed angles."""
-    return rot_x(angles[0]) @ rot_y(angles[1]) @ rot_z(angles[2])
+    """OpenSim frame orientation: Euler XYZ body-fixed angles,
+    rot_x(a0) rot_y(a1) rot_z(a2)."""
+    X, Y, Z = (r(float(a)).tolist() for r, a in zip((rot_x, rot_y, rot_z), angles))
+    return np.array(_mm3(_mm3(X, Y), Z), float)
+
+
+def unit3(d) -> List[float]:
+    """d / |d| with |d| = sqrt((d0 d0 + d1 d1) + d2 d2) (as the C++ builder)."""
+    d0, d1, d2 = (float(v) for v in d)
+    n = math.sqrt(d0 * d0 + d1 * d1 + d2 * d2)
+    return [d0 / n, d1 / n, d2 / n]
 
 
 @dataclass
@@ -468,9 +484,7 @@ class CompiledModel:
             for ax in j.axes:
                 a = abi.mh_axis()
                 a.type = ax.type
-                d = np.asarray(ax.dir, float)
-                d = d / np.linalg.norm(d)
-                a.dir[:] = d.tolist()
+                a.dir[:] = unit3(ax.dir)
                 a.func = add_function(ax.func)
                 axes.append(a)
             b.axis_count = len(axes) - b.axis_begin

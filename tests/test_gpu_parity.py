@@ -308,7 +308,7 @@ def _pair(name, backend="auto", tasks=None, env=None):
                                                   "MOCOHIP_ASM", "MOCOHIP_QUOT", "MOCOHIP_CTPL",
                                                   "MOCOHIP_ROLES", "MOCOHIP_ROLE_COUPLE",
                                                   "MOCOHIP_IV_QFUSE", "MOCOHIP_IV_THREADS",
-                                                  "MOCOHIP_EXC_LANES", "MOCOHIP_G_BLOCK")}
+                                                  "MOCOHIP_EXC_LANES", "MOCOHIP_G_BLOCK", "MOCOHIP_G_LDS")}
     if backend != "auto":
         os.environ["MOCOHIP_BACKEND"] = backend
     if tasks:
@@ -598,6 +598,42 @@ def test_device_pointer_entry_points():
     assert np.array_equal(vd.cpu().numpy(), gpu.eval_jac_g(x))
 
 
+@pytest.mark.parametrize("chunks", ["1", "3", "16"])
+@pytest.mark.parametrize("name", ["gait_rigid_forward", "gait_inverse", "gait_rigid_pathcon", "coupled_pendulum",
+                                  "double_pendulum_N1"])
+def test_chunked_host_copy_bit_identical(name, chunks):
+    """The host entries' Jacobian goes to the host in interval chunks on a
+    copy stream overlapping the rest of the assembly (MOCOHIP_D2H_CHUNKS):
+    the host vectors equal the device entries' values bit for bit, for whole
+    NLPs and for shards (endpoint head on the first, tail on the last)."""
+    import torch
+    st = CASES[name]()
+    rep = st.problem.create_rep()
+    N = st.solver.num_mesh_intervals
+    for a, b in ((0, 0), (0, max(1, N // 2)), (N // 2, N)):
+        if b and a >= b:
+            continue
+        ref = HipNLP(rep, st.solver.options(a, b))
+        import os
+        os.environ["MOCOHIP_D2H_CHUNKS"] = chunks
+        try:
+            nlp = HipNLP(rep, st.solver.options(a, b))
+        finally:
+            os.environ.pop("MOCOHIP_D2H_CHUNKS", None)
+        x = nlp.random_iterate(np.random.default_rng(12).uniform(-1, 1, nlp.n))
+        xd = torch.tensor(x, dtype=torch.float64, device="cuda")
+        gd = torch.empty(max(1, nlp.row_end - nlp.row_begin), dtype=torch.float64, device="cuda")
+        vd = torch.empty(max(1, nlp.nnz_end - nlp.nnz_begin), dtype=torch.float64, device="cuda")
+        ref.eval_g_jac_g_device(xd.data_ptr(), gd.data_ptr(), vd.data_ptr())
+        ref.synchronize()
+        g_ref, J_ref = gd.cpu().numpy()[:nlp.row_end - nlp.row_begin], vd.cpu().numpy()[:nlp.nnz_end - nlp.nnz_begin]
+        assert np.array_equal(nlp.eval_jac_g(x), J_ref, equal_nan=True)
+        g, J = nlp.eval_g_jac_g(x)
+        assert np.array_equal(g, g_ref, equal_nan=True) and np.array_equal(J, J_ref, equal_nan=True)
+        ref.close()
+        nlp.close()
+
+
 def test_async_calls_on_a_caller_stream():
     """mh_set_stream + mh_set_async: device calls enqueue on the caller's
     (torch) stream after its producer of x, return before completion, and
@@ -744,6 +780,23 @@ def test_eval_g_block_bit_identical(name, tb):
     for _, x in _iterates(gpu):
         assert np.array_equal(gpu.eval_g(x), small.eval_g(x), equal_nan=True)
         assert np.array_equal(gpu.eval_jac_g(x), small.eval_jac_g(x), equal_nan=True)
+
+
+@pytest.mark.parametrize("tb", ["1", "4", "8", "16"])
+@pytest.mark.parametrize("name", ["gait_rigid_forward", "wrapped_pendulum", "rajagopal18_inverse_wrapped",
+                                  "coupled_pendulum_implicit", "rajagopal80_wrapped_trap"])
+def test_eval_g_lds_workspace_bit_identical(name, tb):
+    """Generic interpreter: eval_g's DAE lanes with their multibody workspace
+    (Work: poses, velocities, forces, motion subspaces, mass matrix) in LDS
+    instead of scratch (MOCOHIP_G_LDS=1, TB lanes per workgroup, one
+    workspace slot per lane: k_eval_lds) write what the scratch workspace
+    writes, g and Jacobian."""
+    gpu, _, _ = _pair(name, "generic")
+    lds, _, _ = _pair(name, "generic", env={"MOCOHIP_G_LDS": "1", "MOCOHIP_G_BLOCK": tb})
+    assert "g-lds" in lds.backend_flags() and "g-lds" not in gpu.backend_flags()
+    for _, x in _iterates(gpu):
+        assert np.array_equal(gpu.eval_g(x), lds.eval_g(x), equal_nan=True)
+        assert np.array_equal(gpu.eval_jac_g(x), lds.eval_jac_g(x), equal_nan=True)
 
 
 def test_work_accounting():
