@@ -77,17 +77,22 @@ struct GenericDae {
     // the same with the workspace where the caller puts it (k_eval_lds: LDS)
     __device__ __forceinline__ static void eval_w(const DevModel& M, double t, const double* in,
             double* out, W& w) {
+        // one dae_eval call site, so that it can be inlined where w lives in
+        // LDS (k_eval_lds): the workspace accesses then compile to ds_*
+        // instructions instead of flat accesses through a generic pointer
+        double xf[2 * Z::MQ + Z::MI], ud[Z::MQ];
+        const double* xs = in;
+        const double* wp = nullptr;
         if (M.presc) {
             // prescribed kinematics: [q, u] and udot from the motion, the
             // NLP states are the auxiliary states
-            double xf[2 * Z::MQ + Z::MI], ud[Z::MQ];
             for (int j = 0; j < M.nq; ++j)
                 table_eval_d(M, M.kin_table, M.kin_col[j], t, xf[j], xf[M.nq + j], ud[j]);
             for (int k = 0; k < M.nz; ++k) xf[2 * M.nq + k] = in[k];
-            dae_eval<Z::MB, Z::MQ, Z::MP>(M, w, t, xf, in + M.ns, out, ud);
-            return;
+            xs = xf;
+            wp = ud;
         }
-        dae_eval<Z::MB, Z::MQ, Z::MP>(M, w, t, in, in + M.ns, out);
+        dae_eval<Z::MB, Z::MQ, Z::MP>(M, w, t, xs, in + M.ns, out, wp);
     }
 };
 
@@ -391,12 +396,19 @@ struct Tasks {
 
 #define MH_IV_STAMP(i)
 
-template <class D>
+// CLS: 0 = every group; 1 = the two heavy groups only (mass matrix and bias,
+// groups 0 and 1 of every generated model); 2 = the others.  A kernel
+// compiled for one class allocates registers for that class's code alone
+// (k_groups_part: a large model's heavy groups no longer set the register
+// budget, hence the occupancy, of its many light ones).
+template <class D, int CLS = 0>
 __device__ __forceinline__ void groups_body(const DevModel& M, const Src& S, const Lanes& Ln, const Tasks& TK,
         double* __restrict__ T, double* __restrict__ H, int blk) {
     const int lane = threadIdx.x;
     const int4 rec = TK.blk[blk];   // one scalar load: no dependent table chain
     const int g = __builtin_amdgcn_readfirstlane(rec.x);
+    if constexpr (CLS == 1) __builtin_assume(g < 2);
+    if constexpr (CLS == 2) __builtin_assume(g >= 2);
     const int first = __builtin_amdgcn_readfirstlane(rec.y);
     const int n = __builtin_amdgcn_readfirstlane(rec.z);
     const float inv = __int_as_float(__builtin_amdgcn_readfirstlane(rec.w));
@@ -436,6 +448,12 @@ template <class D>
 __global__ void __launch_bounds__(64) k_groups(DevModel M, Src S, Lanes Ln, Tasks TK,
         double* __restrict__ T, double* __restrict__ H) {
     groups_body<D>(M, S, Ln, TK, T, H, blockIdx.x);
+}
+// One class of groups (groups_body CLS), blocks blk0.. of the task table.
+template <class D, int CLS>
+__global__ void __launch_bounds__(64) k_groups_part(DevModel M, Src S, Lanes Ln, Tasks TK,
+        double* __restrict__ T, double* __restrict__ H, int blk0) {
+    groups_body<D, CLS>(M, S, Ln, TK, T, H, blk0 + (int)blockIdx.x);
 }
 
 // Combine: one workgroup per grid point.  The grid point's group results
@@ -1785,6 +1803,7 @@ struct TaskInfo {
 struct TaskSet {
     Tasks dev{};
     int nblocks = 0;
+    int nheavy = -1;        // leading blocks of the heavy groups (0, 1); -1: not contiguous
     double flops = 0.0;     // FP64 ops per launch (groups + combine)
     double ntasks = 0.0;    // group evaluations per launch
     std::vector<int> dlen, off, roles, jd, blk;
@@ -1878,6 +1897,7 @@ struct mh_ctx {
     int n_exc_lanes = 0;
     int g_block = 4;               // generic interpreter, eval_g: k_eval workgroup size (A/B: profiles/r02_l)
     bool g_lds = false;            // generic interpreter, eval_g: workspace in LDS (k_eval_lds)
+    int groups_split = -1;         // task back ends: heavy / light group kernels (-1: by occupancy)
     uint32_t* d_ctpl = nullptr;    // compiled template of the Jacobian lanes (k_interval)
     std::vector<uint32_t> ctpl;
     int* d_ctgen = nullptr;        // the entries it leaves to jac_entry (t0 / tf of defect rows)
@@ -2030,13 +2050,47 @@ static void be_eval_lane(mh_ctx* c, const double* x, int mode, double* Y) {
     hipLaunchKernelGGL(k_exc_lanes<D>, dim3((unsigned)((lanes + 63) / 64)), dim3(64), 0, c->stream, c->M,
             L, ln, x, Y, c->d_exc);
 }
+// The group tasks of a task set: one k_groups launch, or -- when the model's
+// group code needs so many registers that k_groups runs fewer waves per SIMD
+// than the light groups' own kernel would (large models: Rajagopal) -- the
+// heavy groups' blocks and then the light groups' blocks as two launches of
+// k_groups_part, each with its own register budget (MOCOHIP_GROUPS_SPLIT=0/1
+// overrides; same arithmetic, bit for bit).
+template <class D>
+static bool split_groups(const mh_ctx* c) {
+    static int decided = -1;   // per model struct: the kernels' occupancy is a property of the code
+    if (c->groups_split >= 0) return c->groups_split != 0;
+    if (decided < 0) {
+        int whole = 0, light = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&whole, k_groups<D>, 64, 0) != hipSuccess ||
+                hipOccupancyMaxActiveBlocksPerMultiprocessor(&light, k_groups_part<D, 2>, 64, 0) != hipSuccess)
+            whole = light = 0;
+        // only where the whole kernel is down to one wave per SIMD: otherwise
+        // the heavy groups' latency hides behind the light ones in one launch
+        // (gait: 11.2 us as one launch vs 8.3 + 6.9 us for the two classes
+        // alone, tools/group_timing.py)
+        decided = (whole > 0 && whole <= 4 && light > whole) ? 1 : 0;
+    }
+    return decided != 0;
+}
+template <class D>
+static void launch_groups(mh_ctx* c, const Src& S, const Lanes& ln, const TaskSet& ts, double* T, double* H) {
+    if (ts.nheavy > 0 && ts.nheavy < ts.nblocks && split_groups<D>(c)) {
+        hipLaunchKernelGGL((k_groups_part<D, 1>), dim3((unsigned)ts.nheavy), dim3(64), 0, c->stream, c->M, S, ln,
+                ts.dev, T, H, 0);
+        hipLaunchKernelGGL((k_groups_part<D, 2>), dim3((unsigned)(ts.nblocks - ts.nheavy)), dim3(64), 0,
+                c->stream, c->M, S, ln, ts.dev, T, H, ts.nheavy);
+        return;
+    }
+    hipLaunchKernelGGL(k_groups<D>, dim3((unsigned)ts.nblocks), dim3(64), 0, c->stream, c->M, S, ln, ts.dev, T, H);
+}
+
 template <class D>
 // Returns 1 when Y holds finite-difference quotients (k_combine quot mode,
 // Jacobian lanes staged in LDS), 0 when it holds raw lane values.
 static int launch_tasks(mh_ctx* c, const Src& S, const Lanes& ln, const TaskSet& ts, double* T,
         double* H, double* times, double* Y, bool quot) {
-    hipLaunchKernelGGL(k_groups<D>, dim3((unsigned)ts.nblocks), dim3(64), 0, c->stream, c->M, S, ln,
-            ts.dev, T, H);
+    launch_groups<D>(c, S, ln, ts, T, H);
     if (c->timing && times) (void)hipEventRecord(c->ev[4], c->stream);
     const unsigned threads = (unsigned)((ln.stride + 63) / 64 * 64);
     quot = quot && ln.stride > 1;
@@ -2062,8 +2116,7 @@ static void be_eval_tasks(mh_ctx* c, const double* x, int mode, double* Y) {
     const Lanes& ln = mode ? c->lanes_jac : c->lanes_g;
     const TaskSet& ts = mode ? c->ts_jac : c->ts_g;
     if (c->use_interval[mode]) {   // combine happens inside k_interval
-        hipLaunchKernelGGL(k_groups<D>, dim3((unsigned)ts.nblocks), dim3(64), 0, c->stream, c->M, S, ln,
-                ts.dev, c->d_T, c->d_H);
+        launch_groups<D>(c, S, ln, ts, c->d_T, c->d_H);
         return;
     }
     c->yq[mode] = launch_tasks<D>(c, S, ln, ts, c->d_T, c->d_H, c->d_times, Y, mode == 1 && c->quot);

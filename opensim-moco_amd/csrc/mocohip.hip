@@ -435,6 +435,11 @@ static void build_taskset(const TaskInfo& ti, const Lanes& ln, int nk, int nsimd
         for (int a = nsimd, b = ts.nblocks - 1; a < b; ++a, --b)
             for (int w = 0; w < 4; ++w) std::swap(ts.blk[4 * (size_t)a + w], ts.blk[4 * (size_t)b + w]);
     }
+    // the heavy groups' blocks (groups 0, 1) as one leading run (k_groups_part)
+    ts.nheavy = 0;
+    while (ts.nheavy < ts.nblocks && ts.blk[4 * (size_t)ts.nheavy] < 2) ++ts.nheavy;
+    for (int b = ts.nheavy; b < ts.nblocks; ++b)
+        if (ts.blk[4 * (size_t)b] < 2) { ts.nheavy = -1; break; }
     ts.dev.ng = ng;
     ts.dev.stride = S;
     ts.dev.tdoubles = tdoubles;
@@ -1404,6 +1409,7 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     if (c->n_exc_lanes) { c->d_exc = (int*)(b + o_exc); c->d_lane_map = (int*)(b + o_lmap); }
     if (const char* eb = std::getenv("MOCOHIP_G_BLOCK")) c->g_block = std::min(64, std::max(1, std::atoi(eb)));
     if (const char* el = std::getenv("MOCOHIP_G_LDS")) c->g_lds = std::atoi(el) != 0;
+    if (const char* es = std::getenv("MOCOHIP_GROUPS_SPLIT")) c->groups_split = std::atoi(es) != 0 ? 1 : 0;
     c->d_grid = (double*)(b + o_grid); c->d_quad = (double*)(b + o_quad);
     c->d_tpl = (TplEntry*)(b + o_tpl);
     c->d_ctpl = (uint32_t*)(b + o_ctpl);

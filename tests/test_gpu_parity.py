@@ -308,7 +308,8 @@ def _pair(name, backend="auto", tasks=None, env=None):
                                                   "MOCOHIP_ASM", "MOCOHIP_QUOT", "MOCOHIP_CTPL",
                                                   "MOCOHIP_ROLES", "MOCOHIP_ROLE_COUPLE",
                                                   "MOCOHIP_IV_QFUSE", "MOCOHIP_IV_THREADS",
-                                                  "MOCOHIP_EXC_LANES", "MOCOHIP_G_BLOCK", "MOCOHIP_G_LDS")}
+                                                  "MOCOHIP_EXC_LANES", "MOCOHIP_G_BLOCK", "MOCOHIP_G_LDS",
+                                                  "MOCOHIP_GROUPS_SPLIT")}
     if backend != "auto":
         os.environ["MOCOHIP_BACKEND"] = backend
     if tasks:
@@ -797,6 +798,20 @@ def test_eval_g_lds_workspace_bit_identical(name, tb):
     for _, x in _iterates(gpu):
         assert np.array_equal(gpu.eval_g(x), lds.eval_g(x), equal_nan=True)
         assert np.array_equal(gpu.eval_jac_g(x), lds.eval_jac_g(x), equal_nan=True)
+
+
+@pytest.mark.parametrize("name", ["gait_rigid_forward", "gait_inverse_random", "rajagopal18_inverse",
+                                  "rajagopal80", "rajagopal80_wrapped", "coupled_pendulum"])
+def test_group_kernel_split_bit_identical(name):
+    """The group tasks as one k_groups launch, or as the heavy groups' and
+    then the light groups' k_groups_part launches (each compiled with its own
+    register budget; the default where the whole kernel would run one wave
+    per SIMD): identical g and Jacobian."""
+    one, _, _ = _pair(name, env={"MOCOHIP_GROUPS_SPLIT": "0"})
+    two, _, _ = _pair(name, env={"MOCOHIP_GROUPS_SPLIT": "1"})
+    for _, x in _iterates(one):
+        assert np.array_equal(one.eval_g(x), two.eval_g(x), equal_nan=True)
+        assert np.array_equal(one.eval_jac_g(x), two.eval_jac_g(x), equal_nan=True)
 
 
 def test_work_accounting():

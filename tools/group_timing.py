@@ -2,7 +2,8 @@
 workload (gait N=200 forward, generated rigid back end) with only group G's
 blocks launched (MOCOHIP_DEBUG_GROUP, read at mh_create; results invalid),
 DAE-stage device time per eval_jac_g from mh_debug_time_stages.
-usage: python tools/group_timing.py [N] [G ...]"""
+usage: python tools/group_timing.py [N] [G ...]
+       python tools/group_timing.py rajagopal80 [N] [G ...]   (configs[3])"""
 import os
 import sys
 
@@ -16,9 +17,13 @@ def main():
     import torch
     from mocohip import configs
     from mocohip.solver import HipNLP
-    N = int(sys.argv[1]) if len(sys.argv) > 1 else 200
-    groups = [int(a) for a in sys.argv[2:]] or [-1, 0, 1, 2, 4, 22, 27, 39]
-    st = configs.gait10dof18musc(N, fd_scheme="forward")
+    args = sys.argv[1:]
+    raja = bool(args) and args[0] == "rajagopal80"
+    if raja:
+        args = args[1:]
+    N = int(args[0]) if args else 200
+    groups = [int(a) for a in args[1:]] or [-1, 0, 1, 2, 4, 22, 27, 39]
+    st = configs.rajagopal80(N, fd_scheme="forward") if raja else configs.gait10dof18musc(N, fd_scheme="forward")
     rep = st.problem.create_rep()
     for g in groups:
         os.environ["MOCOHIP_DEBUG_GROUP"] = str(g)
