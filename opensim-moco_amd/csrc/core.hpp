@@ -456,6 +456,20 @@ __global__ void __launch_bounds__(64) k_groups_part(DevModel M, Src S, Lanes Ln,
     groups_body<D, CLS>(M, S, Ln, TK, T, H, blk0 + (int)blockIdx.x);
 }
 
+// Output writers of a lane's combine: output o goes straight to its Y / LDS
+// slot when the generated code produces it (no NO-long array held in
+// registers until the end; the large models' combine spilled on it).
+struct StridedOut {
+    double* p;
+    long s;
+    __device__ __forceinline__ double& operator[](int o) const { return p[(long)o * s]; }
+};
+struct LdsOut {
+    lds_double* p;
+    int s;
+    __device__ __forceinline__ lds_double& operator[](int o) const { return p[o * s]; }
+};
+
 // Combine: one workgroup per grid point.  The grid point's group results
 // (contiguous in T and H) are staged in LDS with coalesced loads; each lane
 // (one lane role) then reads the slots it needs from LDS.
@@ -503,11 +517,7 @@ __global__ void __launch_bounds__(64) k_combine_global(DevModel M, Src S, Lanes 
     if (r == Ln.base && times) times[kl] = t;
     const TaskLoadGlobal<D> TL{T + (long)kl * TK.tdoubles, H + (long)kl * TK.nmass * D::NST,
                                TK.jd, r};
-    double out[D::NO];
-    D::combine(M, t, in, TL, out);
-    double* Yk = Y + (long)kl * ystride_pt + r;
-#pragma unroll
-    for (int o = 0; o < D::NO; ++o) Yk[(long)o * Ln.stride] = out[o];
+    D::combine(M, t, in, TL, StridedOut{Y + (long)kl * ystride_pt + r, (long)Ln.stride});
 }
 
 // Copy n doubles to LDS with U loads in flight per thread before the first
@@ -536,8 +546,13 @@ __device__ __forceinline__ void stage_lds(double* __restrict__ dst, const double
 // (f0 - f-)/h; the base slot keeps the raw base value): one division per
 // (grid point, output, direction) instead of one per Jacobian nonzero that
 // reads it.  The lanes exchange their raw values through LDS.
-template <class D>
-__global__ void __launch_bounds__(1024) k_combine(DevModel M, Src S, Lanes Ln, Tasks TK,
+// MAXT: the launch bound.  A grid point of up to 256 lane roles launches the
+// 256-thread instantiation, whose lanes may keep up to 512 VGPRs: a large
+// model's combine (Rajagopal 80: ~120 outputs, an 18-coordinate L^T L solve)
+// then runs without the scratch spills the 1024-thread bound (128 VGPRs)
+// forces on it.
+template <class D, int MAXT = 1024>
+__global__ void __launch_bounds__(MAXT) k_combine(DevModel M, Src S, Lanes Ln, Tasks TK,
         const double* __restrict__ T, const double* __restrict__ H, double* __restrict__ times,
         double* __restrict__ Y, long ystride_pt, int quot) {
     extern __shared__ double smem[];
@@ -552,6 +567,19 @@ __global__ void __launch_bounds__(1024) k_combine(DevModel M, Src S, Lanes Ln, T
     __syncthreads();
     const int r = threadIdx.x;
     const bool act = r < Ln.stride;
+    // Y[(kl*NO + o)*stride + r]  (ystride_pt = NO*stride; explicit points:
+    // stride 1 -> out[p*NO + o])
+    double* Yk = Y + (long)kl * ystride_pt + r;
+    if (!quot) {   // raw lane values: each output straight to Y
+        if (act) {
+            double t;
+            const LaneIn<D> in = lane_input<D>(S, Ln, kl, r, t);
+            if (r == Ln.base && times) times[kl] = t;
+            const TaskLoadLds<D> TL{lds(sT), lds(sH), TK.jd, r};
+            D::combine(M, t, in, TL, StridedOut{Yk, (long)Ln.stride});
+        }
+        return;
+    }
     double out[D::NO];
     if (act) {
         double t;
@@ -559,16 +587,6 @@ __global__ void __launch_bounds__(1024) k_combine(DevModel M, Src S, Lanes Ln, T
         if (r == Ln.base && times) times[kl] = t;
         const TaskLoadLds<D> TL{lds(sT), lds(sH), TK.jd, r};
         D::combine(M, t, in, TL, out);
-    }
-    // Y[(kl*NO + o)*stride + r]  (ystride_pt = NO*stride; explicit points:
-    // stride 1 -> out[p*NO + o])
-    double* Yk = Y + (long)kl * ystride_pt + r;
-    if (!quot) {
-        if (act) {
-#pragma unroll
-            for (int o = 0; o < D::NO; ++o) Yk[(long)o * Ln.stride] = out[o];
-        }
-        return;
     }
     __syncthreads();                 // every lane is done reading sT / sH
     double* sY = smem;               // [NO][stride] raw lane values
@@ -1075,7 +1093,7 @@ __device__ __forceinline__ void interval_body(const DevModel& M, const Src& S, c
                       lds(sXm + p * L.NM), L.vc(k_first + p) ? lds(sXl) : nullptr};
         const double t = lane_time(Ln, S.grid[k_first + p], t0, tf, r, in.pi, in.step);
         if (r == Ln.base) sTimes[p] = t;
-        double out[D::NO];
+        const LdsOut out{lds(sY + p * ny + r), Ln.stride};
         if constexpr (GM) {
             const TaskLoadGlobal<D> TL{T + (long)(kl0 + p) * nt, H + (long)(kl0 + p) * nh, TK.jd, r};
             D::combine(M, t, in, TL, out);
@@ -1083,9 +1101,6 @@ __device__ __forceinline__ void interval_body(const DevModel& M, const Src& S, c
             const TaskLoadLds<D> TL{lds(sT + p * nt), lds(sH + p * nh), TK.jd, r};
             D::combine(M, t, in, TL, out);
         }
-        lds_double* Yp = lds(sY + p * ny + r);
-#pragma unroll
-        for (int o = 0; o < D::NO; ++o) Yp[o * Ln.stride] = out[o];
     }
     // the compiled words of this thread's first IV_PF assembly entries,
     // loaded now: their latency hides behind the quotients and the g rows
@@ -1878,7 +1893,13 @@ struct mh_ctx {
     // host entries: the Jacobian values go to the host in interval chunks on
     // copy_stream while the next chunk's k_interval runs (MOCOHIP_D2H_CHUNKS)
     static constexpr int kMaxD2hChunks = 16;
-    int d2h_chunks = 4;
+    // default 1 (one copy after the call): measured on MI355X, every chunked
+    // variant was slower (gait N=200, page-locked buffers: 2,561 calls/s with
+    // one copy, 2,244 / 2,097 / 1,942 with 2 / 4 / 8 chunks;
+    // profiles/r03_h/d2h.txt) -- the PCIe transfer, not the assembly, is
+    // the call, and each extra copy + cross-stream event costs more than the
+    // ~18 us of k_interval it hides
+    int d2h_chunks = 1;
     hipStream_t copy_stream = nullptr;
     hipEvent_t ev_chunk[kMaxD2hChunks] = {};
     hipEvent_t ev_copied = nullptr;
@@ -1898,6 +1919,7 @@ struct mh_ctx {
     int g_block = 4;               // generic interpreter, eval_g: k_eval workgroup size (A/B: profiles/r02_l)
     bool g_lds = false;            // generic interpreter, eval_g: workspace in LDS (k_eval_lds)
     int groups_split = -1;         // task back ends: heavy / light group kernels (-1: by occupancy)
+    int combine_mode = -1;         // split path combine: 0 LDS-staged, 1 global memory (-1: by spills)
     uint32_t* d_ctpl = nullptr;    // compiled template of the Jacobian lanes (k_interval)
     std::vector<uint32_t> ctpl;
     int* d_ctgen = nullptr;        // the entries it leaves to jac_entry (t0 / tf of defect rows)
@@ -2085,6 +2107,26 @@ static void launch_groups(mh_ctx* c, const Src& S, const Lanes& ln, const TaskSe
     hipLaunchKernelGGL(k_groups<D>, dim3((unsigned)ts.nblocks), dim3(64), 0, c->stream, c->M, S, ln, ts.dev, T, H);
 }
 
+// Raw-value combine of a large model: k_combine_global (64-thread blocks,
+// group results read from global memory) when the LDS-staged k_combine would
+// keep its lanes' loads in scratch -- measured on the compiled kernels
+// (Rajagopal 80: 8.2 KB of scratch per lane for the LDS-staged kernel at 512
+// VGPRs, 56 B for the global-memory one; gait: neither spills, LDS staging
+// stays).  MOCOHIP_COMBINE=lds / global overrides.
+template <class D>
+static bool combine_from_global(const mh_ctx* c, unsigned threads) {
+    if (c->combine_mode >= 0) return c->combine_mode == 1;
+    static int decided = -1;
+    if (decided < 0) {
+        hipFuncAttributes a{}, b{};
+        const void* kl = threads <= 256 ? (const void*)k_combine<D, 256> : (const void*)k_combine<D, 1024>;
+        decided = (hipFuncGetAttributes(&a, kl) == hipSuccess &&
+                   hipFuncGetAttributes(&b, (const void*)k_combine_global<D>) == hipSuccess &&
+                   a.localSizeBytes > 1024 && b.localSizeBytes < a.localSizeBytes / 4) ? 1 : 0;
+    }
+    return decided != 0;
+}
+
 template <class D>
 // Returns 1 when Y holds finite-difference quotients (k_combine quot mode,
 // Jacobian lanes staged in LDS), 0 when it holds raw lane values.
@@ -2096,11 +2138,11 @@ static int launch_tasks(mh_ctx* c, const Src& S, const Lanes& ln, const TaskSet&
     quot = quot && ln.stride > 1;
     size_t lds = sizeof(double) * ((size_t)ts.dev.tdoubles + (size_t)ts.dev.nmass * D::NST);
     if (quot) lds = std::max(lds, sizeof(double) * (size_t)D::NO * ln.stride);
-    if (threads <= 1024 && lds <= kMaxLds) {
+    if (threads <= 1024 && lds <= kMaxLds && !(!quot && combine_from_global<D>(c, threads))) {
+        auto kern = threads <= 256 ? k_combine<D, 256> : k_combine<D, 1024>;
         if (lds > 65536)
-            (void)hipFuncSetAttribute((const void*)k_combine<D>,
-                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL(k_combine<D>, dim3((unsigned)ts.dev.nk), dim3(threads), lds, c->stream, c->M,
+            (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL(kern, dim3((unsigned)ts.dev.nk), dim3(threads), lds, c->stream, c->M,
                 S, ln, ts.dev, T, H, times, Y, (long)D::NO * ln.stride, quot ? 1 : 0);
         return quot ? 1 : 0;
     } else {

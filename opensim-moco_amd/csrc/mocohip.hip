@@ -1410,6 +1410,8 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     if (const char* eb = std::getenv("MOCOHIP_G_BLOCK")) c->g_block = std::min(64, std::max(1, std::atoi(eb)));
     if (const char* el = std::getenv("MOCOHIP_G_LDS")) c->g_lds = std::atoi(el) != 0;
     if (const char* es = std::getenv("MOCOHIP_GROUPS_SPLIT")) c->groups_split = std::atoi(es) != 0 ? 1 : 0;
+    if (const char* ec = std::getenv("MOCOHIP_COMBINE"))
+        c->combine_mode = std::strcmp(ec, "global") == 0 ? 1 : std::strcmp(ec, "lds") == 0 ? 0 : -1;
     c->d_grid = (double*)(b + o_grid); c->d_quad = (double*)(b + o_quad);
     c->d_tpl = (TplEntry*)(b + o_tpl);
     c->d_ctpl = (uint32_t*)(b + o_ctpl);

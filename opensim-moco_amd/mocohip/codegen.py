@@ -1160,14 +1160,17 @@ def generate(cm, struct_name: str, implicit: bool = False, prescribed: bool = Fa
     parts.append(("group", "const int g, const mh::DevModel& M, const double t, "
                            "const double* __restrict__ in, double* __restrict__ out", body))
     parts.append(("combine", "const mh::DevModel& M, const double t, const double* __restrict__ in, "
-                             "const TL& T, double* __restrict__ out", comb))
+                             "const TL& T, OUT out", comb))
 
     fns = []
     for name, args, lines in parts:
         tpl = ""
         if name in ("group", "combine"):
             # inputs through an accessor (loaded where used, not held in VGPRs)
-            tpl = "template <class IN> " if name == "group" else "template <class IN, class TL> "
+            # combine: outputs through a writer (OUT: a pointer, or a strided
+            # Y / LDS writer -- each output is stored as it is produced
+            # instead of living in registers until the end)
+            tpl = "template <class IN> " if name == "group" else "template <class IN, class TL, class OUT> "
             args = args.replace("const double* __restrict__ in", "const IN& in")
         pre = ["    const double* __restrict__ K = M.pool;", "    (void)K;"]
         fns.append(f"    {tpl}__device__ __forceinline__ static void {name}({args}) {{\n"

@@ -309,7 +309,7 @@ def _pair(name, backend="auto", tasks=None, env=None):
                                                   "MOCOHIP_ROLES", "MOCOHIP_ROLE_COUPLE",
                                                   "MOCOHIP_IV_QFUSE", "MOCOHIP_IV_THREADS",
                                                   "MOCOHIP_EXC_LANES", "MOCOHIP_G_BLOCK", "MOCOHIP_G_LDS",
-                                                  "MOCOHIP_GROUPS_SPLIT")}
+                                                  "MOCOHIP_GROUPS_SPLIT", "MOCOHIP_COMBINE")}
     if backend != "auto":
         os.environ["MOCOHIP_BACKEND"] = backend
     if tasks:
@@ -812,6 +812,20 @@ def test_group_kernel_split_bit_identical(name):
     for _, x in _iterates(one):
         assert np.array_equal(one.eval_g(x), two.eval_g(x), equal_nan=True)
         assert np.array_equal(one.eval_jac_g(x), two.eval_jac_g(x), equal_nan=True)
+
+
+@pytest.mark.parametrize("name", ["gait_rigid_central", "gait_compliant_central", "rajagopal80",
+                                  "rajagopal80_wrapped", "gait_inverse_central_trap"])
+def test_combine_variants_bit_identical(name):
+    """Split path (k_combine + k_transcribe): the combine with the group
+    results staged in LDS (k_combine) or read from global memory
+    (k_combine_global; chosen where the LDS-staged kernel spills) write
+    identical lanes, g and Jacobian."""
+    a, _, _ = _pair(name, env={"MOCOHIP_COMBINE": "lds", "MOCOHIP_INTERVAL": "0"})
+    b, _, _ = _pair(name, env={"MOCOHIP_COMBINE": "global", "MOCOHIP_INTERVAL": "0"})
+    for _, x in _iterates(a):
+        assert np.array_equal(a.eval_g(x), b.eval_g(x), equal_nan=True)
+        assert np.array_equal(a.eval_jac_g(x), b.eval_jac_g(x), equal_nan=True)
 
 
 def test_work_accounting():
