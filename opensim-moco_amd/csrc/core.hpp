@@ -396,8 +396,9 @@ struct Tasks {
 
 #define MH_IV_STAMP(i)
 
-// CLS: 0 = every group; 1 = the two heavy groups only (mass matrix and bias,
-// groups 0 and 1 of every generated model); 2 = the others.  A kernel
+// CLS: 0 = every group; 1 = the heavy groups only (mass matrix and bias, or
+// their parts: groups 0 .. D::NHEAVY - 1 of every generated model); 2 = the
+// others.  A kernel
 // compiled for one class allocates registers for that class's code alone
 // (k_groups_part: a large model's heavy groups no longer set the register
 // budget, hence the occupancy, of its many light ones).
@@ -407,8 +408,8 @@ __device__ __forceinline__ void groups_body(const DevModel& M, const Src& S, con
     const int lane = threadIdx.x;
     const int4 rec = TK.blk[blk];   // one scalar load: no dependent table chain
     const int g = __builtin_amdgcn_readfirstlane(rec.x);
-    if constexpr (CLS == 1) __builtin_assume(g < 2);
-    if constexpr (CLS == 2) __builtin_assume(g >= 2);
+    if constexpr (CLS == 1) __builtin_assume(g < D::NHEAVY);
+    if constexpr (CLS == 2) __builtin_assume(g >= D::NHEAVY);
     const int first = __builtin_amdgcn_readfirstlane(rec.y);
     const int n = __builtin_amdgcn_readfirstlane(rec.z);
     const float inv = __int_as_float(__builtin_amdgcn_readfirstlane(rec.w));
@@ -427,7 +428,7 @@ __device__ __forceinline__ void groups_body(const DevModel& M, const Src& S, con
     double out[NOUT];
     // the mass-matrix and bias groups are the longest tasks: give them issue
     // priority over the short muscle tasks sharing their SIMD
-    if (g < 2) __builtin_amdgcn_s_setprio(2);
+    if (g < D::NHEAVY) __builtin_amdgcn_s_setprio(2);
     D::group(g, M, t, in, out);
     if (!live) return;
     if (g == 0) {
@@ -1806,7 +1807,7 @@ __global__ void __launch_bounds__(64) k_dae_probe(DevModel M, Layout L, int npts
 // ------------------------------------------------------------------------
 // Static description of a task-decomposed generated model (codegen.py).
 struct TaskInfo {
-    int ng, nst, nf, rw;
+    int ng, nst, nf, rw, nheavy;
     const int* group_nf;
     const unsigned long long* reads;   // [ng][rw] bit i = group reads point input i
     const unsigned char* time;         // [ng] group reads the time
@@ -1818,7 +1819,7 @@ struct TaskInfo {
 struct TaskSet {
     Tasks dev{};
     int nblocks = 0;
-    int nheavy = -1;        // leading blocks of the heavy groups (0, 1); -1: not contiguous
+    int nheavy = -1;        // leading blocks of the heavy groups (< NHEAVY); -1: not contiguous
     double flops = 0.0;     // FP64 ops per launch (groups + combine)
     double ntasks = 0.0;    // group evaluations per launch
     std::vector<int> dlen, off, roles, jd, blk;
@@ -1942,7 +1943,18 @@ struct mh_ctx {
     float timings[4] = {0, 0, 0, 0};
     // task-decomposed back ends
     TaskSet ts_jac, ts_g, ts_probe;
-    double *d_T = nullptr, *d_H = nullptr;
+    double *d_T = nullptr, *d_H = nullptr;     // group results of the Jacobian lanes
+    double *d_Tg = nullptr, *d_Hg = nullptr;   // of the eval_g lanes (their own: the two
+                                               // evaluations may run concurrently)
+    // IPOPT's new_x on the device entries (mh_tnlp_eval_*_device): ev_x is
+    // recorded on the caller's stream where an evaluation at a new iterate
+    // x_last starts; an eval_jac_g with new_x = 0 at the same x then runs on
+    // aux_stream from that point -- concurrently with what the caller queued
+    // since (its eval_g) -- and the caller's stream waits for it (ev_aux)
+    hipStream_t aux_stream = nullptr;
+    hipEvent_t ev_x = nullptr, ev_aux = nullptr;
+    const double* x_last = nullptr;
+    bool overlap = true;           // MOCOHIP_OVERLAP=0: new_x = 0 runs on the caller's stream
     char* probe_mem = nullptr;     // tables + T/H of the last mh_eval_dae size
     double *d_pT = nullptr, *d_pH = nullptr;
     int probe_np = -1;
@@ -2157,11 +2169,13 @@ static void be_eval_tasks(mh_ctx* c, const double* x, int mode, double* Y) {
     const Src S = src_of(c, x);
     const Lanes& ln = mode ? c->lanes_jac : c->lanes_g;
     const TaskSet& ts = mode ? c->ts_jac : c->ts_g;
+    double* T = mode ? c->d_T : c->d_Tg;
+    double* H = mode ? c->d_H : c->d_Hg;
     if (c->use_interval[mode]) {   // combine happens inside k_interval
-        launch_groups<D>(c, S, ln, ts, c->d_T, c->d_H);
+        launch_groups<D>(c, S, ln, ts, T, H);
         return;
     }
-    c->yq[mode] = launch_tasks<D>(c, S, ln, ts, c->d_T, c->d_H, c->d_times, Y, mode == 1 && c->quot);
+    c->yq[mode] = launch_tasks<D>(c, S, ln, ts, T, H, c->d_times, Y, mode == 1 && c->quot);
 }
 // LDS bytes of k_interval for one lane configuration (0: does not apply).
 template <class D>
@@ -2247,7 +2261,7 @@ static void be_interval(mh_ctx* c, const double* x, int mode, double* g, double*
     if (i1 <= i0) return;
     hipLaunchKernelGGL(kern, dim3((unsigned)(i1 - i0)), dim3(threads), lds, c->stream, c->M,
             S, ln, ts.dev, L, I, c->d_tpl, (mode == 1 && c->use_ctpl) ? c->d_ctpl : nullptr, c->d_ctgen,
-            (int)c->ctgen.size(), c->d_T, c->d_H, g, v, i0);
+            (int)c->ctgen.size(), mode ? c->d_T : c->d_Tg, mode ? c->d_H : c->d_Hg, g, v, i0);
 }
 template <class D>
 static void be_integrand(mh_ctx* c, const double* x) {
@@ -2290,7 +2304,7 @@ static constexpr Backend make_backend_lane(const char* name, double flops) {
 }
 template <class D>
 struct TaskInfoOf {
-    static constexpr TaskInfo value{D::NG, D::NST, D::NF, D::RW, D::GROUP_NF, &D::GROUP_READS[0][0],
+    static constexpr TaskInfo value{D::NG, D::NST, D::NF, D::RW, D::NHEAVY, D::GROUP_NF, &D::GROUP_READS[0][0],
                                     D::GROUP_TIME, D::GROUP_FLOPS, D::COMBINE_FLOPS};
 };
 template <class D>

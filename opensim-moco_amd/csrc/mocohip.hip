@@ -435,11 +435,11 @@ static void build_taskset(const TaskInfo& ti, const Lanes& ln, int nk, int nsimd
         for (int a = nsimd, b = ts.nblocks - 1; a < b; ++a, --b)
             for (int w = 0; w < 4; ++w) std::swap(ts.blk[4 * (size_t)a + w], ts.blk[4 * (size_t)b + w]);
     }
-    // the heavy groups' blocks (groups 0, 1) as one leading run (k_groups_part)
+    // the heavy groups' blocks (groups < NHEAVY) as one leading run (k_groups_part)
     ts.nheavy = 0;
-    while (ts.nheavy < ts.nblocks && ts.blk[4 * (size_t)ts.nheavy] < 2) ++ts.nheavy;
+    while (ts.nheavy < ts.nblocks && ts.blk[4 * (size_t)ts.nheavy] < ti.nheavy) ++ts.nheavy;
     for (int b = ts.nheavy; b < ts.nblocks; ++b)
-        if (ts.blk[4 * (size_t)b] < 2) { ts.nheavy = -1; break; }
+        if (ts.blk[4 * (size_t)b] < ti.nheavy) { ts.nheavy = -1; break; }
     ts.dev.ng = ng;
     ts.dev.stride = S;
     ts.dev.tdoubles = tdoubles;
@@ -1350,7 +1350,7 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     }
 
     TaskOffsets to_jac{}, to_g{};
-    size_t o_T = 0, o_H = 0;
+    size_t o_T = 0, o_H = 0, o_Tg = 0, o_Hg = 0;
     const TaskInfo* ti = backend_tasks(c->be);
     if (ti) {
         build_taskset(*ti, c->lanes_jac, c->nk, c->nsimd, c->ts_jac);
@@ -1359,6 +1359,8 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
         to_g = put_taskset(A, c->ts_g);
         o_T = A.reserve(sizeof(double) * std::max(c->ts_jac.t_doubles, c->ts_g.t_doubles));
         o_H = A.reserve(sizeof(double) * std::max(c->ts_jac.h_doubles, c->ts_g.h_doubles));
+        o_Tg = A.reserve(sizeof(double) * c->ts_g.t_doubles);
+        o_Hg = A.reserve(sizeof(double) * c->ts_g.h_doubles);
     }
     A.size = A.used;
     HIPCHK(hipMalloc(&c->dmem, A.size));
@@ -1442,6 +1444,8 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
         bind_taskset(b, to_g, c->ts_g);
         c->d_T = (double*)(b + o_T);
         c->d_H = (double*)(b + o_H);
+        c->d_Tg = (double*)(b + o_Tg);
+        c->d_Hg = (double*)(b + o_Hg);
     }
     HIPCHK(hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
     c->stream = c->own_stream;
@@ -1521,6 +1525,10 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
     if (const char* ek = std::getenv("MOCOHIP_D2H_CHUNKS"))
         c->d2h_chunks = std::min(mh_ctx::kMaxD2hChunks, std::max(1, std::atoi(ek)));
+    HIPCHK(hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&c->ev_x, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&c->ev_aux, hipEventDisableTiming));
+    if (const char* eov = std::getenv("MOCOHIP_OVERLAP")) c->overlap = std::strcmp(eov, "0") != 0;
     HIPCHK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
     for (auto& e : c->ev_chunk) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->ev_copied, hipEventDisableTiming));
@@ -1537,6 +1545,12 @@ extern "C" void mh_destroy(mh_ctx* c) {
     for (auto& e : c->ev_chunk)
         if (e) (void)hipEventDestroy(e);
     if (c->ev_copied) (void)hipEventDestroy(c->ev_copied);
+    if (c->aux_stream) {
+        (void)hipStreamSynchronize(c->aux_stream);
+        (void)hipStreamDestroy(c->aux_stream);
+    }
+    if (c->ev_x) (void)hipEventDestroy(c->ev_x);
+    if (c->ev_aux) (void)hipEventDestroy(c->ev_aux);
     if (c->copy_stream) {
         (void)hipStreamSynchronize(c->copy_stream);
         (void)hipStreamDestroy(c->copy_stream);
@@ -1924,6 +1938,7 @@ static int run_seeds(mh_ctx* c, const double* x, double* values) {
 }
 
 static int run_cached(mh_ctx* c, int kind, const double* x, double* a, double* b) {
+    if (kind != 0) c->x_last = nullptr;   // the Jacobian slabs are in use from here on
     if (c->jac_seeds && kind != 0) {   // tropter's global-seed Jacobian
         if (kind == 2) {
             int rc = run_stage(c, 0, 0, x, a, nullptr);
@@ -2071,6 +2086,52 @@ extern "C" int mh_eval_jac_g_device(mh_ctx* c, const double* x_dev, double* v_de
     return finish(c, true);
 }
 
+// mh_tnlp_eval_*_device: an eval_jac_g with new_x = 0 at the iterate of the
+// last mh_tnlp_eval_g_device runs on aux_stream from that eval_g's start
+// (ev_x), concurrently with the eval_g kernels the caller's stream holds.
+// Only the default task path qualifies (k_groups + k_interval, reading x and
+// the Jacobian lanes' own slabs d_T / d_H; eval_g uses d_Tg / d_Hg); any
+// other evaluation in between invalidates the point (run_cached clears
+// x_last for every Jacobian evaluation), so the Jacobian never runs beside
+// work that shares its buffers.
+static bool can_overlap(const mh_ctx* c) {
+    return c->overlap && !c->timing && !c->use_graphs && !c->jac_seeds && c->be->tasks && c->be->interval &&
+           c->use_interval[1] && !c->use_roles && !c->iv_dbg_stop && c->aux_stream;
+}
+
+extern "C" int mh_tnlp_eval_g_device(mh_ctx* c, const double* x_dev, int new_x, double* g_dev) {
+    (void)new_x;   // x's state at this call is what the eval_g kernels read either way
+    if (!c || !x_dev || !g_dev) return set_err(MH_ERR_INVALID, "null argument");
+    HIPCHK(hipSetDevice(c->device));
+    c->x_last = nullptr;
+    if (can_overlap(c)) {
+        HIPCHK(hipEventRecord(c->ev_x, c->stream));
+        c->x_last = x_dev;
+    }
+    int rc = run_cached(c, 0, x_dev, g_dev, nullptr);
+    if (rc) return rc;
+    return finish(c, true);
+}
+
+extern "C" int mh_tnlp_eval_jac_g_device(mh_ctx* c, const double* x_dev, int new_x, double* v_dev) {
+    if (!c || !x_dev || !v_dev) return set_err(MH_ERR_INVALID, "null argument");
+    HIPCHK(hipSetDevice(c->device));
+    if (new_x || x_dev != c->x_last || !can_overlap(c)) {
+        int rc = run_cached(c, 1, x_dev, v_dev, nullptr);
+        if (rc) return rc;
+        return finish(c, true);
+    }
+    hipStream_t caller = c->stream;
+    HIPCHK(hipStreamWaitEvent(c->aux_stream, c->ev_x, 0));
+    c->stream = c->aux_stream;
+    const int rc = run_cached(c, 1, x_dev, v_dev, nullptr);
+    c->stream = caller;
+    if (rc) return rc;
+    HIPCHK(hipEventRecord(c->ev_aux, c->aux_stream));
+    HIPCHK(hipStreamWaitEvent(caller, c->ev_aux, 0));
+    return finish(c, true);
+}
+
 extern "C" int mh_eval_g_jac_g_device(mh_ctx* c, const double* x_dev, double* g_dev, double* v_dev) {
     if (!c || !x_dev || !g_dev || !v_dev) return set_err(MH_ERR_INVALID, "null argument");
     HIPCHK(hipSetDevice(c->device));
@@ -2150,6 +2211,7 @@ extern "C" int mh_batch_set_group_results_global(mh_batch* bt, int on) {
 static int batch_run(mh_batch* bt, int kind, const double* const* x, double* const* g, double* const* v) {
     if (!bt || !x || (kind != 1 && !g) || (kind != 0 && !v)) return set_err(MH_ERR_INVALID, "null argument");
     BatchPtrs P{};
+    for (int b = 0; b < bt->B; ++b) bt->ctx[b]->x_last = nullptr;   // writes every slab (d_T)
     for (int b = 0; b < bt->B; ++b) {
         if (!x[b] || (kind != 1 && !g[b]) || (kind != 0 && !v[b]))
             return set_err(MH_ERR_INVALID, "null pointer for batch item %d", b);

@@ -218,6 +218,8 @@ MOCOHIP_SYMBOLS = {
     "mh_eval_jac_g_device": (i32, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "mh_eval_g_jac_g": (i32, [C.c_void_p, P(f64), P(f64), P(f64)]),
     "mh_eval_g_jac_g_device": (i32, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "mh_tnlp_eval_g_device": (i32, [C.c_void_p, C.c_void_p, i32, C.c_void_p]),
+    "mh_tnlp_eval_jac_g_device": (i32, [C.c_void_p, C.c_void_p, i32, C.c_void_p]),
     "mh_eval_dae": (i32, [C.c_void_p, i32, P(f64), P(f64)]),
     "mh_set_timing": (i32, [C.c_void_p, i32]),
     "mh_get_backend_flags": (i32, [C.c_void_p, C.c_char_p, i32]),

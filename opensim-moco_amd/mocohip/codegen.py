@@ -666,11 +666,16 @@ class _Emitter:
         self.g.raw(f"{name} {'+=' if sign > 0 else '-='} {val};")
         self.g.flops["add"] += 1
 
-    def muscle(self, im, R, P, V, Facc, tau, zdot_sink, with_adot: bool = True, resid_sink=None):
+    def muscle(self, im, R, P, V, Facc, tau, zdot_sink, with_adot: bool = True, resid_sink=None,
+               part: Optional[str] = None):
         """Path geometry, DGF and tension point forces of muscle im.  Point
         forces are subtracted into the body accumulators Facc (RNEA sign
         convention), MovingPathPoint terms added into tau; zdot values are
-        handed to zdot_sink(state_index, S)."""
+        handed to zdot_sink(state_index, S).
+        part "force": the path length and lengthening speed and the DGF
+        tension only (returned; no point forces -- V is needed, Facc / tau
+        are not); part "arm": the point forces of a unit tension (the
+        generalized forces per unit tension; no DGF, V not needed)."""
         g, M, Lo, u, q = self.g, self.M, self.Lo, self.u, self.q
         Z3 = _vec([0, 0, 0])
         mu = M.muscles[im]
@@ -696,16 +701,18 @@ class _Emitter:
                     loc[d] = fv[0]
                     F = M.funcs[fi]
                     if F.kind != abi.MH_FN_CONSTANT:
-                        dloc[d] = g.mul(fv[1], u[F.coord])
+                        if part != "arm":   # (the arms read q only)
+                            dloc[d] = g.mul(fv[1], u[F.coord])
                         mov.append((d, F.coord, fv[1]))
             b = pt.body
             Pw = g.vadd(P[b], g.mv(R[b], loc))
-            Vw = g.vadd(g.vadd(V[b][1], g.cross(V[b][0], Pw)), g.mv(R[b], dloc))
+            Vw = None if part == "arm" else g.vadd(g.vadd(V[b][1], g.cross(V[b][0], Pw)), g.mv(R[b], dloc))
             pos.append(Pw)
             vel.append(Vw)
             dl_funcs.append(mov)
         pws = self.path_wraps(im)
         if pws:
+            assert part is None, "wrapped muscles are not split"
             self.wrapped_muscle(im, mu, pts, pos, vel, act, dl_funcs, pws, R, P, V, Facc, tau, zdot_sink,
                                 with_adot, resid_sink)
             return
@@ -722,12 +729,18 @@ class _Emitter:
         for (j, i, cond) in segs:
             d = g.vsub(pos[i], pos[j])
             l = g.fn("sqrt", g.dot(d, d))
-            sp = g.div(g.dot(d, g.vsub(vel[i], vel[j])), l)
             ind = g.sel(cond, _c(1.0), _c(0.0)) if cond else None
-            L = g.add(L, l if ind is None else g.mul(ind, l))
-            Sp = g.add(Sp, sp if ind is None else g.mul(ind, sp))
+            if part != "arm":
+                sp = g.div(g.dot(d, g.vsub(vel[i], vel[j])), l)
+                L = g.add(L, l if ind is None else g.mul(ind, l))
+                Sp = g.add(Sp, sp if ind is None else g.mul(ind, sp))
             seginfo.append((j, i, d, l, ind))
-        T = self.muscle_force(im, mu, L, Sp, zdot_sink, with_adot, resid_sink)
+        if part == "arm":
+            T = _c(1.0)
+        else:
+            T = self.muscle_force(im, mu, L, Sp, zdot_sink, with_adot, resid_sink)
+            if part == "force":
+                return T
         for (j, i, d, l, ind) in seginfo:
             Tl = g.div(T, l) if ind is None else g.mul(ind, g.div(T, l))
             Fv = g.vscale(d, Tl)
@@ -876,55 +889,36 @@ class _Emitter:
     def mass_matrix_factor(self, Ibody, Sj, coord_body):
         """CRBA composite inertias + Featherstone L^T L on the coordinate
         tree.  Returns (lam, H) with H the factor entries."""
-        g, M, NQ = self.g, self.M, self.Lo.NQ
+        NQ = self.Lo.NQ
+        lam, H = self.crba(Ibody, Sj, {j: coord_body[j] for j in range(NQ)})
+        factor_columns(self.g, H, lam, range(NQ))
+        return lam, H
+
+    def crba(self, Ibody, Sj, coord_body):
+        """Mass-matrix entries H[(i, j)] = S_j . (Ic_body(i) S_i) for every
+        coordinate i of `coord_body` and its ancestor coordinates j, with the
+        composite inertias Ic built from the bodies of `Ibody` only (the
+        mass matrix is linear in the bodies' inertias: a subset gives that
+        subset's share).  coord_body must be ancestor-closed."""
+        g, M = self.g, self.M
         Ic = dict(Ibody)
         for b in range(M.nb - 1, -1, -1):
             p = M.bodies[b].parent
-            if p >= 0:
-                mp, hp, Ip = Ic[p]
-                mb, hb, Ibb = Ic[b]
-                Ic[p] = (g.add(mp, mb), g.vadd(hp, hb), [g.add(x, y) for x, y in zip(Ip, Ibb)])
-        body_coords: Dict[int, List[int]] = {}
-        for j in range(NQ):
-            body_coords.setdefault(coord_body[j], []).append(j)
-
-        def anc_coord(b):
-            p = M.bodies[b].parent
-            while p >= 0:
-                if p in body_coords:
-                    return body_coords[p][-1]
-                p = M.bodies[p].parent
-            return -1
-        lam = [-1] * NQ
-        for b, cs in body_coords.items():
-            for idx, j in enumerate(cs):
-                lam[j] = cs[idx - 1] if idx > 0 else anc_coord(b)
-        for j in range(NQ):
-            if lam[j] >= j:
-                raise ValueError("coordinates must be ordered parents-first")
+            if p >= 0 and b in Ic:
+                if p in Ic:
+                    mp, hp, Ip = Ic[p]
+                    mb, hb, Ibb = Ic[b]
+                    Ic[p] = (g.add(mp, mb), g.vadd(hp, hb), [g.add(x, y) for x, y in zip(Ip, Ibb)])
+                else:
+                    Ic[p] = Ic[b]
+        lam = coordinate_tree(M, coord_body, self.Lo.NQ)
         H: Dict[Tuple[int, int], S] = {}
-        for i in range(NQ):
+        for i in sorted(coord_body):
             Fi = g.rbi_mul(Ic[coord_body[i]], Sj[i])
             j = i
             while j >= 0:
                 H[(i, j)] = g.svdot(Sj[j], Fi)
                 j = lam[j]
-        for k in range(NQ - 1, -1, -1):
-            # the factor keeps 1/L_kk on the diagonal: one division per
-            # column here, multiplications in the factorization and solves
-            a = g.div(_c(1.0), g.fn("sqrt", H[(k, k)]))
-            H[(k, k)] = a
-            i = lam[k]
-            while i >= 0:
-                H[(k, i)] = g.mul(H[(k, i)], a)
-                i = lam[i]
-            i = lam[k]
-            while i >= 0:
-                j = i
-                while j >= 0:
-                    H[(i, j)] = g.sub(H[(i, j)], g.mul(H[(k, i)], H[(k, j)]))
-                    j = lam[j]
-                i = lam[i]
         return lam, H
 
     def solve(self, lam, H, bvec):
@@ -1048,6 +1042,82 @@ class _Emitter:
                 self.acc(tau[a.target], self.g.mul(self.ctrl[ia], _c(a.optimal_force)))
 
 
+def coordinate_tree(M: ModelView, coord_body: Dict[int, int], NQ: int) -> List[int]:
+    """lam[j]: the parent coordinate of coordinate j on the coordinate tree
+    (the previous coordinate of the same body, else the last coordinate of
+    the nearest ancestor body that has one; -1 at the root); -1 for the
+    coordinates absent from coord_body."""
+    body_coords: Dict[int, List[int]] = {}
+    for j in sorted(coord_body):
+        body_coords.setdefault(coord_body[j], []).append(j)
+
+    def anc_coord(b):
+        p = M.bodies[b].parent
+        while p >= 0:
+            if p in body_coords:
+                return body_coords[p][-1]
+            p = M.bodies[p].parent
+        return -1
+    lam = [-1] * NQ
+    for b, cs in body_coords.items():
+        for idx, j in enumerate(cs):
+            lam[j] = cs[idx - 1] if idx > 0 else anc_coord(b)
+    for j in coord_body:
+        if lam[j] >= j:
+            raise ValueError("coordinates must be ordered parents-first")
+    return lam
+
+
+def factor_columns(g: Gen, H: Dict[Tuple[int, int], S], lam: List[int], cols) -> None:
+    """Featherstone's fill-free L^T L factorization of the columns `cols`
+    (processed from the last coordinate down), in place on H: column k
+    scales its row by 1/L_kk (kept on the diagonal: one division per column
+    here, multiplications in the solves) and updates the entries (i, j) of
+    k's ancestor coordinates.  Columns of disjoint subtrees touch disjoint
+    entries except their common ancestors'."""
+    for k in sorted(cols, reverse=True):
+        a = g.div(_c(1.0), g.fn("sqrt", H[(k, k)]))
+        H[(k, k)] = a
+        i = lam[k]
+        while i >= 0:
+            H[(k, i)] = g.mul(H[(k, i)], a)
+            i = lam[i]
+        i = lam[k]
+        while i >= 0:
+            j = i
+            while j >= 0:
+                H[(i, j)] = g.sub(H[(i, j)], g.mul(H[(k, i)], H[(k, j)]))
+                j = lam[j]
+            i = lam[i]
+
+
+def branch_parts(M: ModelView) -> Optional[Tuple[List[int], List[List[int]]]]:
+    """The tree split of the heavy multibody groups: (root chain, parts).
+    The root chain is the bodies from the ground down to the first body
+    with more than one child (gait models: the pelvis); the parts are the
+    subtrees below it (legs, torso), the root chain's bodies added to the
+    smallest.  None when the tree does not branch (chains: no split)."""
+    children: Dict[int, List[int]] = {b: [] for b in range(-1, M.nb)}
+    for b in range(M.nb):
+        children[M.bodies[b].parent].append(b)
+    root, cur = [], -1
+    while len(children[cur]) == 1:
+        cur = children[cur][0]
+        root.append(cur)
+    if len(children[cur]) < 2:
+        return None
+
+    def subtree(b):
+        out = [b]
+        for c in children[b]:
+            out += subtree(c)
+        return out
+    parts = [sorted(subtree(c)) for c in children[cur]]
+    small = min(range(len(parts)), key=lambda i: (len(parts[i]), i))
+    parts[small] = sorted(parts[small] + root)
+    return root, parts
+
+
 def _multibody_front(E: _Emitter, with_muscles: bool):
     """Kinematics, RNEA (bias + external + coordinate actuators [+ muscles]),
     CRBA and the L^T L factor.  Returns (tau vars, lam, H)."""
@@ -1144,6 +1214,9 @@ def generate(cm, struct_name: str, implicit: bool = False, prescribed: bool = Fa
     NG = len(groups)
     NF = max([gr.nf for gr in groups[1:]] + [1])
     NST = max(groups[0].nf, 1)
+    # the leading heavy groups: mass (or its placeholder), its parts and the
+    # bias parts (k_groups gives them issue priority; k_groups_part CLS 1)
+    NHEAVY = 1 + sum(1 for gr in groups[1:] if gr.name.startswith(("mass", "bias")))
     RW = (Lo.NI + 63) // 64
     reads = []
     for gr in groups:
@@ -1185,9 +1258,11 @@ def generate(cm, struct_name: str, implicit: bool = False, prescribed: bool = Fa
     static constexpr bool EXC_LANES = false;   // k_exc_lanes is the generic interpreter's
     static constexpr int MI = NI, MO = NO;
     static constexpr double FLOPS_PER_EVAL = {float(fl['total'])};
-    // task decomposition: group 0 = mass matrix factor (NST values), groups
-    // 1.. = force groups (NF values: nonzero generalized forces, z output)
-    static constexpr int NG = {NG}, NST = {NST}, NF = {NF}, RW = {RW};
+    // task decomposition: group 0 = mass matrix factor (NST values; a
+    // placeholder where the mass matrix is split into parts), groups 1.. =
+    // mass-matrix parts and force groups (NF values: factor entries and
+    // root-chain shares, nonzero generalized forces, z output)
+    static constexpr int NG = {NG}, NST = {NST}, NF = {NF}, RW = {RW}, NHEAVY = {NHEAVY};
     static constexpr int GROUP_NF[NG] = {lst([gr.nf for gr in groups])};
     static constexpr unsigned long long GROUP_READS[NG][RW] = {{{", ".join(reads)}}};
     static constexpr unsigned char GROUP_TIME[NG] = {lst([int(gr.time) for gr in groups])};
@@ -1249,11 +1324,13 @@ def _emit_groups(M: ModelView, Lo: _Layout) -> List[_Group]:
     NQ = Lo.NQ
     allb = list(range(M.nb))
     out = []
+    split = branch_parts(M)
 
     # mass (implicit mode: the residual needs no mass matrix -- the group is
-    # an empty placeholder so group 0 keeps its role in the task tables)
+    # an empty placeholder so group 0 keeps its role in the task tables; the
+    # same where the tree splits: the mass-matrix parts below carry it)
     E = _Emitter(M, Lo)
-    if Lo.implicit:
+    if Lo.implicit or split:
         E.g.raw("out[0] = 0.0;")
         g0 = _Group("mass", E.g.lines, [("H", (0, 0))], set(), False, 0)
         g0.lam = None
@@ -1289,20 +1366,55 @@ def _emit_groups(M: ModelView, Lo: _Layout) -> List[_Group]:
         r, t = _reads_of(lines)
         out.append(_Group(name, lines, fields, r, t, sum(Eg.g.flops.values())))
 
-    # bias
-    E = _Emitter(M, Lo)
-    R, P, V, A, Sj, cb = E.kinematics(allb, accel=True)
-    Ib = {b: E.inertia(b, R, P) for b in allb}
+    # Where the tree branches, the two heavy groups are split by subtree so
+    # that no single task carries the whole multibody system (a task is one
+    # wave's instruction stream: its length is the stage's critical path),
+    # and a perturbed coordinate re-evaluates only its own subtree's part.
+    # Mass-matrix part p: the CRBA entries of its bodies' inertias (the mass
+    # matrix is linear in them), its own coordinates' columns factored
+    # (they touch only its own entries and the root chain's), and its share
+    # of the root-chain block after those columns' updates ("HR"); the
+    # combine sums the shares and factors the root columns.
+    if split and not Lo.implicit:
+        root, parts = split
+        for ip, bodies in enumerate(parts):
+            E = _Emitter(M, Lo)
+            cl = E.closure(bodies)
+            R, P, _, _, Sj, cb = E.kinematics(cl, accel=False, vel=False)
+            Ib = {b: E.inertia(b, R, P) for b in bodies}
+            lam, H = E.crba(Ib, Sj, cb)
+            own = [j for j in cb if cb[j] not in root]
+            factor_columns(E.g, H, lam, own)
+            fields = []
+            for k in sorted(H):
+                kind = "HR" if cb[k[0]] in root else "H"
+                E.g.raw(f"out[{len(fields)}] = {H[k]};")
+                fields.append((kind, k))
+            r, t = _reads_of(E.g.lines)
+            out.append(_Group(f"mass_{ip}", E.g.lines, fields, r, t, sum(E.g.flops.values())))
 
-    def init(b):
-        Ia = E.g.rbi_mul(Ib[b], A[b])
-        hV = E.g.rbi_mul(Ib[b], V[b])
-        w, v = E.g.svadd(Ia, E.g.crf(V[b], hV))
-        return list(w) + list(v)
-    Facc = E.body_force_vars(allb, init)
-    tv = [E.g.var(_c(0.0)) for _ in range(NQ)]
-    E.backward(allb, Facc, Sj, cb, tv)
-    finish(E, "bias", tv)
+    # bias (RNEA inertial + gravity forces); split: part p applies its own
+    # bodies' forces only and runs the backward pass over their closure --
+    # the generalized forces are linear in the body forces, and the combine
+    # sums the parts' tau like any other force group
+    bias_parts = split[1] if split else [allb]
+    for ip, bodies in enumerate(bias_parts):
+        E = _Emitter(M, Lo)
+        cl = E.closure(bodies) if split else allb
+        R, P, V, A, Sj, cb = E.kinematics(cl, accel=True)
+        Ib = {b: E.inertia(b, R, P) for b in bodies}
+
+        def init(b):
+            if b not in Ib:
+                return [_c(0.0)] * 6
+            Ia = E.g.rbi_mul(Ib[b], A[b])
+            hV = E.g.rbi_mul(Ib[b], V[b])
+            w, v = E.g.svadd(Ia, E.g.crf(V[b], hV))
+            return list(w) + list(v)
+        Facc = E.body_force_vars(cl, init)
+        tv = [E.g.var(_c(0.0)) for _ in range(NQ)]
+        E.backward(cl, Facc, Sj, cb, tv)
+        finish(E, f"bias_{ip}" if split else "bias", tv)
 
     # external loads
     for ie, e in enumerate(M.ext):
@@ -1343,8 +1455,38 @@ def _emit_groups(M: ModelView, Lo: _Layout) -> List[_Group]:
         out.append(_Group(f"activation_{im}", E.g.lines, [("z", sa - 2 * NQ)], r, t,
                           sum(E.g.flops.values())))
 
-    # muscles
+    # muscles.  A muscle without wrapping is two groups: its tension (path
+    # length and lengthening speed, DeGroote-Fregly force; reads q, u and its
+    # activation / excitation / tendon state) and its moment arms (the
+    # generalized forces of a unit tension; reads q only) -- the combine
+    # multiplies them.  Each is a shorter task than the whole muscle, and a
+    # speed, activation or excitation direction re-evaluates the tension only.
     for im, mu in enumerate(M.muscles):
+        if not _Emitter(M, Lo).path_wraps(im):
+            E = _Emitter(M, Lo)
+            cl = E.closure(E.muscle_bodies(im))
+            R, P, V, _, Sj, cb = E.kinematics(cl, accel=False)
+            zs, rs = {}, {}
+            T = E.muscle(im, R, P, V, None, None, lambda si, v: zs.__setitem__(si, v), with_adot=False,
+                         resid_sink=lambda k, v: rs.__setitem__(k, v), part="force")
+            zf = (Lo.ftn_state[im] - 2 * NQ, zs[Lo.ftn_state[im]]) if Lo.ftn_state[im] >= 0 else None
+            finish(E, f"muscle_{im}", [None] * NQ, zf, next(iter(rs.items()), None),
+                   extra=[("tension", im, T)])
+            E = _Emitter(M, Lo)
+            R, P, _, _, Sj, cb = E.kinematics(cl, accel=False, vel=False)
+            Facc = E.body_force_vars(cl, None)
+            tv = [E.g.var(_c(0.0)) for _ in range(NQ)]
+            E.muscle(im, R, P, None, Facc, tv, None, part="arm")
+            E.backward(cl, Facc, Sj, cb, tv)
+            fields = []
+            for j in range(NQ):
+                if tv[j] in E.touched:
+                    E.g.raw(f"out[{len(fields)}] = {tv[j]};")
+                    fields.append(("arm", (im, j)))
+            lines = _presc_prelude(E.g.lines) + E.g.lines
+            r, t = _reads_of(lines)
+            out.append(_Group(f"marm_{im}", lines, fields, r, t, sum(E.g.flops.values())))
+            continue
         E = _Emitter(M, Lo)
         cl = E.closure(E.muscle_bodies(im))
         R, P, V, _, Sj, cb = E.kinematics(cl, accel=False)
@@ -1371,10 +1513,15 @@ def _emit_combine(M: ModelView, Lo: _Layout, groups: List[_Group]):
     E = _Emitter(M, Lo)
     g = E.g
     terms = [[] for _ in range(NQ)]
+    tension = {}
     for gi, gr in enumerate(groups[1:], start=1):
         for f, (kind, j) in enumerate(gr.fields):
             if kind == "tau":
                 terms[j].append(S(n=f"T({gi}, {f})"))
+            elif kind == "tension":
+                tension[j] = S(n=f"T({gi}, {f})")
+            elif kind == "arm":     # muscle j[0]'s tension times its moment arm
+                terms[j[1]].append(g.mul(tension[j[0]], S(n=f"T({gi}, {f})")))
     for ia, a in enumerate(M.acts):
         if a.kind == abi.MH_ACT_COORDINATE:
             terms[a.target].append(g.mul(E.ctrl[ia], _c(a.optimal_force)))
@@ -1388,10 +1535,27 @@ def _emit_combine(M: ModelView, Lo: _Layout, groups: List[_Group]):
     bvec = [tree(t) for t in terms]
     if Lo.implicit:
         xs = [g.neg(b) for b in bvec]     # residual = -(applied - bias with udot = w)
-    else:
+    elif groups[0].lam is not None:
         keys = [k for _, k in groups[0].fields]
         Hs = {k: S(n=f"T.h({f})") for f, k in enumerate(keys)}
         xs = E.solve(groups[0].lam, Hs, bvec)
+    else:
+        # the mass matrix in parts (_emit_groups): the parts' factored
+        # columns as they are, the root-chain block summed over the parts
+        # (fixed order) and factored here
+        Hs, shares = {}, {}
+        for gi, gr in enumerate(groups):
+            for f, (kind, k) in enumerate(gr.fields):
+                if kind == "H" and gi > 0:
+                    Hs[k] = S(n=f"T({gi}, {f})")
+                elif kind == "HR":
+                    shares.setdefault(k, []).append(S(n=f"T({gi}, {f})"))
+        for k in sorted(shares):
+            Hs[k] = tree(shares[k])
+        R0, _, _, _, _, cb = _Emitter(M, Lo).kinematics(list(range(M.nb)), accel=False, vel=False)
+        lam = coordinate_tree(M, cb, NQ)
+        factor_columns(g, Hs, lam, sorted({k[0] for k in shares}))
+        xs = E.solve(lam, Hs, bvec)
     for i in range(NQ):
         g.raw(f"out[{i}] = {xs[i]};")
     kcf = {}

@@ -502,6 +502,18 @@ class HipNLP(_NLPBase):
     def eval_jac_g_device(self, x_ptr: int, v_ptr: int):
         self._check(self.lib.mh_eval_jac_g_device(self.ctx, C.c_void_p(x_ptr), C.c_void_p(v_ptr)))
 
+    def tnlp_eval_g_device(self, x_ptr: int, new_x: bool, g_ptr: int):
+        """TNLP::eval_g on device pointers with IPOPT's new_x."""
+        self._check(self.lib.mh_tnlp_eval_g_device(self.ctx, C.c_void_p(x_ptr), int(bool(new_x)),
+                                                   C.c_void_p(g_ptr)))
+
+    def tnlp_eval_jac_g_device(self, x_ptr: int, new_x: bool, v_ptr: int):
+        """TNLP::eval_jac_g on device pointers with IPOPT's new_x: new_x =
+        False (x unchanged since the last tnlp_eval_g_device) lets the
+        Jacobian run beside that eval_g on the context's auxiliary stream."""
+        self._check(self.lib.mh_tnlp_eval_jac_g_device(self.ctx, C.c_void_p(x_ptr), int(bool(new_x)),
+                                                       C.c_void_p(v_ptr)))
+
     def lane_stride(self) -> int:
         """Finite-difference lanes per grid point (mh_debug_jacobian_lanes)."""
         ND = 2 + self.NI

@@ -664,6 +664,50 @@ def test_async_calls_on_a_caller_stream():
     assert np.array_equal(gpu.eval_jac_g(x), J_ref)
 
 
+@pytest.mark.parametrize("name", ["gait_rigid_forward", "gait_rigid_central", "gait_inverse",
+                                  "gait_rigid_implicit", "coupled_pendulum", "double_pendulum_hs",
+                                  "gait_rigid_pathcon"])
+def test_tnlp_new_x_overlap(name):
+    """mh_tnlp_eval_*_device with IPOPT's new_x: eval_g(new_x=1) then
+    eval_jac_g(new_x=0) -- the Jacobian runs on the auxiliary stream beside
+    that eval_g -- over a queue of iterates written by the caller's stream
+    between the pairs (x rewritten in place, asynchronous calls): every pair's
+    g and J equal the plain entries' at its iterate bit for bit.  Also the
+    cases that must not overlap: new_x=1 on the Jacobian, another x pointer,
+    and a fused call between the pair."""
+    import torch
+    gpu, _, _ = _pair(name)
+    xs = [physiological_iterate(gpu, 20 + i) for i in range(4)]
+    want = [(gpu.eval_g(x), gpu.eval_jac_g(x)) for x in xs]
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        xd = torch.zeros(gpu.n, dtype=torch.float64, device="cuda")
+        x2 = torch.zeros(gpu.n, dtype=torch.float64, device="cuda")
+        gd = [torch.full((gpu.m,), np.nan, dtype=torch.float64, device="cuda") for _ in xs]
+        vd = [torch.full((gpu.nnz,), np.nan, dtype=torch.float64, device="cuda") for _ in xs]
+        hx = [torch.from_numpy(x).pin_memory() for x in xs]
+        gpu.set_stream(s.cuda_stream)
+        gpu.set_async(True)
+        for rep in range(2):
+            for i in range(len(xs)):
+                xd.copy_(hx[i], non_blocking=True)          # the caller's producer of x on s
+                gpu.tnlp_eval_g_device(xd.data_ptr(), True, gd[i].data_ptr())
+                if rep == 1 and i == 1:
+                    x2.copy_(xd)
+                    gpu.tnlp_eval_jac_g_device(x2.data_ptr(), False, vd[i].data_ptr())   # other pointer
+                elif rep == 1 and i == 2:
+                    gpu.eval_g_jac_g_device(xd.data_ptr(), gd[i].data_ptr(), vd[i].data_ptr())
+                    gpu.tnlp_eval_jac_g_device(xd.data_ptr(), False, vd[i].data_ptr())
+                else:
+                    gpu.tnlp_eval_jac_g_device(xd.data_ptr(), rep == 1 and i == 3, vd[i].data_ptr())
+            s.synchronize()
+            for i, (g, J) in enumerate(want):
+                assert np.array_equal(gd[i].cpu().numpy(), g, equal_nan=True), (rep, i)
+                assert np.array_equal(vd[i].cpu().numpy(), J, equal_nan=True), (rep, i)
+    gpu.set_async(False)
+    gpu.set_stream(None)
+
+
 def test_repeatable_bitwise():
     gpu, _, _ = _pair("gait_rigid_forward")
     x = gpu.random_iterate(np.random.default_rng(3).uniform(-1, 1, gpu.n))
