@@ -180,12 +180,8 @@ def make_nlp(cx, st, ib=0, ie=0, blocking=False):
     return nlp
 
 
-def device_steps(cx, nlp, x, plain=False):
-    """(step_separate, step_fused) on device buffers.  step_separate is
-    IPOPT's pair at a new iterate through the TNLP-shaped device entries:
-    eval_g(new_x=true), then eval_jac_g(new_x=false) -- which the library
-    runs beside that eval_g on its auxiliary stream; plain=True: the entries
-    without new_x (every call ordered after the previous one)."""
+def device_steps(cx, nlp, x):
+    """(step_separate, step_fused) on device buffers."""
     torch = cx.torch
     xd = torch.tensor(x, dtype=torch.float64, device=cx.dev)
     gd = torch.zeros(max(nlp.row_end - nlp.row_begin, 1), dtype=torch.float64, device=cx.dev)
@@ -193,16 +189,12 @@ def device_steps(cx, nlp, x, plain=False):
     xp, gp, vp = xd.data_ptr(), gd.data_ptr(), vd.data_ptr()
 
     def separate():
-        nlp.tnlp_eval_g_device(xp, True, gp)
-        nlp.tnlp_eval_jac_g_device(xp, False, vp)
-
-    def separate_plain():
         nlp.eval_g_device(xp, gp)
         nlp.eval_jac_g_device(xp, vp)
 
     def fused():
         nlp.eval_g_jac_g_device(xp, gp, vp)
-    return (separate_plain if plain else separate), fused, (xd, gd, vd)
+    return separate, fused, (xd, gd, vd)
 
 
 def measure(cx, step, args, k=None, w=None):
@@ -611,11 +603,6 @@ def main():
         other = sep if args.mode == "fused" else fused
         _, el = measure(cx, other, args)
         extra["value_fused" if args.mode == "separate" else "value_separate"] = round(k * cx.world / el, 3)
-        # the same separate calls without IPOPT's new_x (no overlap of the
-        # Jacobian with eval_g)
-        plain, _, _ = device_steps(cx, nlp, x, plain=True)
-        _, el = measure(cx, plain, args)
-        extra["value_separate_without_new_x"] = round(k * cx.world / el, 3)
         nlp.set_async(False)
         _, el = measure(cx, head, args)
         extra["value_blocking"] = round(k * cx.world / el, 3)
@@ -704,8 +691,7 @@ def main():
                        "mesh_intervals": N, "grid_points": nlp.G, "n": nlp.n, "m": nlp.m,
                        "nnz_jac": nlp.nnz, "transcription": "hermite-simpson",
                        "fd": args.fd, "mode": args.mode,
-                       "calls": ("blocking" if args.blocking else "asynchronous (device pointers, torch stream)")
-                        + "; eval_g(new_x=true) + eval_jac_g(new_x=false) through mh_tnlp_eval_*_device",
+                       "calls": "blocking" if args.blocking else "asynchronous (device pointers, torch stream)",
                        "parallelism": f"replicas{cx.world}" if cx.world > 1 else "single",
                        "iterate": "bounds-midpoint states, uniform random controls"},
             "roofline": roof,

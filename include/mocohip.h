@@ -578,11 +578,13 @@ int mh_eval_jac_g_device(mh_ctx* ctx, const double* x_dev,
  * tropter/tropter/optimization/IPOPTSolver.cpp:383-447): new_x = 0 promises
  * that x_dev is the iterate of this context's previous mh_tnlp_eval_g_device
  * call, unchanged since (IPOPT's eval_g(new_x=true) -> eval_jac_g(new_x=false)
- * pair).  The Jacobian then depends on nothing queued after that call, so it
- * runs on the context's auxiliary stream from that point, concurrently with
- * the eval_g kernels, and the context's stream waits for it before anything
- * queued after this call (MOCOHIP_OVERLAP=0: on the context's stream).
- * Results are identical to mh_eval_g_device / mh_eval_jac_g_device. */
+ * pair).  The Jacobian then depends on nothing queued after that call; with
+ * MOCOHIP_OVERLAP=1 it runs on the context's auxiliary stream from that
+ * point, concurrently with the eval_g kernels, and the context's stream
+ * waits for it before anything queued after this call (off by default: on
+ * MI355X the two cross-queue waits cost more than the overlap gains, see
+ * DESIGN.md).  Results are identical to mh_eval_g_device /
+ * mh_eval_jac_g_device. */
 int mh_tnlp_eval_g_device(mh_ctx* ctx, const double* x_dev, int new_x, double* g_dev);
 int mh_tnlp_eval_jac_g_device(mh_ctx* ctx, const double* x_dev, int new_x,
         double* values_dev);

@@ -1954,7 +1954,7 @@ struct mh_ctx {
     hipStream_t aux_stream = nullptr;
     hipEvent_t ev_x = nullptr, ev_aux = nullptr;
     const double* x_last = nullptr;
-    bool overlap = true;           // MOCOHIP_OVERLAP=0: new_x = 0 runs on the caller's stream
+    bool overlap = false;          // MOCOHIP_OVERLAP=1 (measured slower: DESIGN.md section 4)
     char* probe_mem = nullptr;     // tables + T/H of the last mh_eval_dae size
     double *d_pT = nullptr, *d_pH = nullptr;
     int probe_np = -1;

@@ -1528,7 +1528,7 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     HIPCHK(hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&c->ev_x, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->ev_aux, hipEventDisableTiming));
-    if (const char* eov = std::getenv("MOCOHIP_OVERLAP")) c->overlap = std::strcmp(eov, "0") != 0;
+    if (const char* eov = std::getenv("MOCOHIP_OVERLAP")) c->overlap = std::strcmp(eov, "1") == 0;
     HIPCHK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
     for (auto& e : c->ev_chunk) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->ev_copied, hipEventDisableTiming));

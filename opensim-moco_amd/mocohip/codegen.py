@@ -666,16 +666,11 @@ class _Emitter:
         self.g.raw(f"{name} {'+=' if sign > 0 else '-='} {val};")
         self.g.flops["add"] += 1
 
-    def muscle(self, im, R, P, V, Facc, tau, zdot_sink, with_adot: bool = True, resid_sink=None,
-               part: Optional[str] = None):
+    def muscle(self, im, R, P, V, Facc, tau, zdot_sink, with_adot: bool = True, resid_sink=None):
         """Path geometry, DGF and tension point forces of muscle im.  Point
         forces are subtracted into the body accumulators Facc (RNEA sign
         convention), MovingPathPoint terms added into tau; zdot values are
-        handed to zdot_sink(state_index, S).
-        part "force": the path length and lengthening speed and the DGF
-        tension only (returned; no point forces -- V is needed, Facc / tau
-        are not); part "arm": the point forces of a unit tension (the
-        generalized forces per unit tension; no DGF, V not needed)."""
+        handed to zdot_sink(state_index, S)."""
         g, M, Lo, u, q = self.g, self.M, self.Lo, self.u, self.q
         Z3 = _vec([0, 0, 0])
         mu = M.muscles[im]
@@ -701,18 +696,16 @@ class _Emitter:
                     loc[d] = fv[0]
                     F = M.funcs[fi]
                     if F.kind != abi.MH_FN_CONSTANT:
-                        if part != "arm":   # (the arms read q only)
-                            dloc[d] = g.mul(fv[1], u[F.coord])
+                        dloc[d] = g.mul(fv[1], u[F.coord])
                         mov.append((d, F.coord, fv[1]))
             b = pt.body
             Pw = g.vadd(P[b], g.mv(R[b], loc))
-            Vw = None if part == "arm" else g.vadd(g.vadd(V[b][1], g.cross(V[b][0], Pw)), g.mv(R[b], dloc))
+            Vw = g.vadd(g.vadd(V[b][1], g.cross(V[b][0], Pw)), g.mv(R[b], dloc))
             pos.append(Pw)
             vel.append(Vw)
             dl_funcs.append(mov)
         pws = self.path_wraps(im)
         if pws:
-            assert part is None, "wrapped muscles are not split"
             self.wrapped_muscle(im, mu, pts, pos, vel, act, dl_funcs, pws, R, P, V, Facc, tau, zdot_sink,
                                 with_adot, resid_sink)
             return
@@ -729,18 +722,12 @@ class _Emitter:
         for (j, i, cond) in segs:
             d = g.vsub(pos[i], pos[j])
             l = g.fn("sqrt", g.dot(d, d))
+            sp = g.div(g.dot(d, g.vsub(vel[i], vel[j])), l)
             ind = g.sel(cond, _c(1.0), _c(0.0)) if cond else None
-            if part != "arm":
-                sp = g.div(g.dot(d, g.vsub(vel[i], vel[j])), l)
-                L = g.add(L, l if ind is None else g.mul(ind, l))
-                Sp = g.add(Sp, sp if ind is None else g.mul(ind, sp))
+            L = g.add(L, l if ind is None else g.mul(ind, l))
+            Sp = g.add(Sp, sp if ind is None else g.mul(ind, sp))
             seginfo.append((j, i, d, l, ind))
-        if part == "arm":
-            T = _c(1.0)
-        else:
-            T = self.muscle_force(im, mu, L, Sp, zdot_sink, with_adot, resid_sink)
-            if part == "force":
-                return T
+        T = self.muscle_force(im, mu, L, Sp, zdot_sink, with_adot, resid_sink)
         for (j, i, d, l, ind) in seginfo:
             Tl = g.div(T, l) if ind is None else g.mul(ind, g.div(T, l))
             Fv = g.vscale(d, Tl)
@@ -1455,38 +1442,8 @@ def _emit_groups(M: ModelView, Lo: _Layout) -> List[_Group]:
         out.append(_Group(f"activation_{im}", E.g.lines, [("z", sa - 2 * NQ)], r, t,
                           sum(E.g.flops.values())))
 
-    # muscles.  A muscle without wrapping is two groups: its tension (path
-    # length and lengthening speed, DeGroote-Fregly force; reads q, u and its
-    # activation / excitation / tendon state) and its moment arms (the
-    # generalized forces of a unit tension; reads q only) -- the combine
-    # multiplies them.  Each is a shorter task than the whole muscle, and a
-    # speed, activation or excitation direction re-evaluates the tension only.
+    # muscles
     for im, mu in enumerate(M.muscles):
-        if not _Emitter(M, Lo).path_wraps(im):
-            E = _Emitter(M, Lo)
-            cl = E.closure(E.muscle_bodies(im))
-            R, P, V, _, Sj, cb = E.kinematics(cl, accel=False)
-            zs, rs = {}, {}
-            T = E.muscle(im, R, P, V, None, None, lambda si, v: zs.__setitem__(si, v), with_adot=False,
-                         resid_sink=lambda k, v: rs.__setitem__(k, v), part="force")
-            zf = (Lo.ftn_state[im] - 2 * NQ, zs[Lo.ftn_state[im]]) if Lo.ftn_state[im] >= 0 else None
-            finish(E, f"muscle_{im}", [None] * NQ, zf, next(iter(rs.items()), None),
-                   extra=[("tension", im, T)])
-            E = _Emitter(M, Lo)
-            R, P, _, _, Sj, cb = E.kinematics(cl, accel=False, vel=False)
-            Facc = E.body_force_vars(cl, None)
-            tv = [E.g.var(_c(0.0)) for _ in range(NQ)]
-            E.muscle(im, R, P, None, Facc, tv, None, part="arm")
-            E.backward(cl, Facc, Sj, cb, tv)
-            fields = []
-            for j in range(NQ):
-                if tv[j] in E.touched:
-                    E.g.raw(f"out[{len(fields)}] = {tv[j]};")
-                    fields.append(("arm", (im, j)))
-            lines = _presc_prelude(E.g.lines) + E.g.lines
-            r, t = _reads_of(lines)
-            out.append(_Group(f"marm_{im}", lines, fields, r, t, sum(E.g.flops.values())))
-            continue
         E = _Emitter(M, Lo)
         cl = E.closure(E.muscle_bodies(im))
         R, P, V, _, Sj, cb = E.kinematics(cl, accel=False)
@@ -1513,15 +1470,10 @@ def _emit_combine(M: ModelView, Lo: _Layout, groups: List[_Group]):
     E = _Emitter(M, Lo)
     g = E.g
     terms = [[] for _ in range(NQ)]
-    tension = {}
     for gi, gr in enumerate(groups[1:], start=1):
         for f, (kind, j) in enumerate(gr.fields):
             if kind == "tau":
                 terms[j].append(S(n=f"T({gi}, {f})"))
-            elif kind == "tension":
-                tension[j] = S(n=f"T({gi}, {f})")
-            elif kind == "arm":     # muscle j[0]'s tension times its moment arm
-                terms[j[1]].append(g.mul(tension[j[0]], S(n=f"T({gi}, {f})")))
     for ia, a in enumerate(M.acts):
         if a.kind == abi.MH_ACT_COORDINATE:
             terms[a.target].append(g.mul(E.ctrl[ia], _c(a.optimal_force)))

@@ -1,9 +1,8 @@
 """Host-side checks of the model-specialized code generator's task
 decomposition (codegen.py): the subtree split of the mass-matrix and RNEA
-groups and the tension / moment-arm split of the muscles.  The numerics of
-the emitted code are checked on the GPU against the oracle
-(tests/test_gpu_parity.py); here: that every quantity the single-lane DAE
-computes has exactly one producer among the groups."""
+groups.  The numerics of the emitted code are checked on the GPU against
+the oracle (tests/test_gpu_parity.py); here: that every quantity the
+single-lane DAE computes has exactly one producer among the groups."""
 import pytest
 
 from mocohip import codegen, configs
@@ -74,20 +73,15 @@ def test_split_groups_cover_the_dae_once(mk, implicit, prescribed):
         assert sorted(H) == sorted(own)                  # each factor entry once
         shared = sorted(k for k in want if k[0] in root_coords)
         assert sorted(HR) == sorted(shared * nparts)     # each part's share of the root block
-        # muscle fields: one tension per muscle, arms only on coordinates
-        tens = [k for g in gs for kind, k in g.fields if kind == "tension"]
-        assert sorted(tens) == list(range(len(M.muscles)))
+        # a part reads its own subtree's and the root chain's coordinates only
         for g in gs:
-            if g.name.startswith("marm_"):
-                assert g.fields and all(kind == "arm" for kind, _ in g.fields)
-                assert not (set(g.reads) - set(range(M.nq)))   # moment arms read q only
+            if g.name.startswith("mass_"):
+                own_q = {k[0] for kind, k in g.fields if kind == "H"} | root_coords
+                assert set(g.reads) <= own_q
     assert sum(1 for n in names if n.startswith("bias_")) == len(parts)
     assert f"NHEAVY = {1 + sum(1 for n in names if n.startswith(('mass_', 'bias_')))}" in src
-    # every muscle without wrapping: one tension group and one moment-arm group
     for im in range(len(M.muscles)):
-        assert f"muscle_{im}" in names and f"marm_{im}" in names
-    # the combine multiplies tension and arms: the muscle groups write no tau
-    assert "T(" in src.split("static void combine")[1]
+        assert f"muscle_{im}" in names
 
 
 def _ancestors(lam, i):
@@ -96,11 +90,3 @@ def _ancestors(lam, i):
         out.append(j)
         j = lam[j]
     return out
-
-
-def test_wrapped_muscles_stay_whole():
-    rep, M = _model(configs.wrapped_pendulum(4))
-    codegen._CTX = None
-    src, info = generate(rep.compiled, "X")
-    names = [g[0] for g in info["groups"]]
-    assert "muscle_0" in names and "marm_0" not in names
