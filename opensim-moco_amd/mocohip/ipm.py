@@ -335,15 +335,17 @@ class _KKT:
         keep = np.ones(self.nx, bool)
         keep[dense] = False
         Jb = Jx[:, np.where(keep)[0]]
-        S = (Jb @ sp.diags(1.0 / Dx[keep]) @ Jb.T + sp.diags(dc)).tocoo()
+        S = (Jb @ sp.diags(1.0 / Dx[keep]) @ Jb.T + sp.diags(dc)).tocsr().tocoo()   # canonical
         band = int(np.abs(S.row - S.col).max(initial=0))
         self.band = None
         if m and band * 4 < m:
             # banded Cholesky (LAPACK pbtrf): S is symmetric positive
-            # definite unless J is rank deficient (then delta_c > 0 is retried)
+            # definite unless J is rank deficient (then delta_c > 0 is retried);
+            # S is canonical (no duplicate entries), so its lower band is
+            # scattered by plain assignment
             low = S.row >= S.col
             ab = np.zeros((band + 1, m))
-            np.add.at(ab, (S.row[low] - S.col[low], S.col[low]), S.data[low])
+            ab[S.row[low] - S.col[low], S.col[low]] = S.data[low]
             try:
                 self.band = sla.cholesky_banded(ab, lower=True, check_finite=False)
             except np.linalg.LinAlgError as e:
@@ -416,7 +418,22 @@ class _KKT:
 
 
 def solve_ipm(nlp, x0: np.ndarray, options: Optional[IpmOptions] = None) -> IpmResult:
-    """Minimize nlp.eval_f subject to nlp's bounds and g bounds from x0."""
+    """Minimize nlp.eval_f subject to nlp's bounds and g bounds from x0.
+
+    The host linear algebra runs with single-threaded BLAS: the banded
+    Cholesky (LAPACK pbtrf) of a transcription's Schur complement is a chain
+    of small blocks, on which OpenBLAS's threads cost ~100x (gait MocoInverse
+    N=125: m = 16,046, band 164: 4.8 s threaded against 0.057 s on one
+    thread, measured on this repository's host)."""
+    try:
+        from threadpoolctl import threadpool_limits
+    except ImportError:   # pragma: no cover - threadpoolctl ships with scikit-learn
+        return _solve_ipm(nlp, x0, options)
+    with threadpool_limits(1, user_api="blas"):
+        return _solve_ipm(nlp, x0, options)
+
+
+def _solve_ipm(nlp, x0: np.ndarray, options: Optional[IpmOptions] = None) -> IpmResult:
     opt = options or IpmOptions()
     t_start = time.perf_counter()
     P = _Scaled(nlp, x0, opt)
