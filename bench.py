@@ -28,12 +28,14 @@ kernels are enqueued and the timed region ends with torch.cuda.synchronize()
   --multi mesh (default for N > 1): the north star's layout -- ONE NLP (the
       headline's, so the driver's per-N values form a strong-scaling curve)
       for one host IPOPT, its mesh intervals sharded over the ranks.  value =
-      device-resident calls/s: x broadcast over RCCL, every rank evaluates its
-      shard into HBM; "host_inclusive": the same plus each rank's DMA of its
-      contiguous g / Jacobian slice into its offset of one page-locked host
-      buffer shared by the node's ranks over its own PCIe link
-      (mocohip.distributed.HostGather); "scaling": "strong".  The replicas
-      layout is reported beside it ("replicas").
+      device-resident calls/s: x resident in every rank's HBM, every rank
+      evaluates its shard into HBM (no collective); "x_broadcast": the same
+      with an RCCL broadcast of x from rank 0 per call; "host_inclusive": the
+      host IPOPT's round trip -- x from page-locked host memory, the shard's
+      evaluation, each rank's DMA of its contiguous g / Jacobian slice into its
+      offset of one page-locked host buffer shared by the node's ranks over
+      its own PCIe link (mocohip.distributed.HostGather); "scaling": "strong".
+      The replicas layout is reported beside it ("replicas").
   --multi replicas: every rank evaluates its own NLP (independent trials,
       the configs[4] batch layout), no collective on the data path
       -> "scaling": "weak".
@@ -81,6 +83,8 @@ def parse():
     ap.add_argument("--config", choices=["gait", "rajagopal80"], default="gait",
                     help="--multi mesh workload: configs[2] gait10dof18musc or configs[3] Rajagopal")
     ap.add_argument("--inverse-batch", type=int, default=8)
+    ap.add_argument("--solve-batch", type=int, default=8,
+                    help="configs[4] MocoInverse solves run together on this GPU (0: skip)")
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--batch-only", action="store_true",
                     help="print only the batch line (A/B of queue / launch settings)")
@@ -514,18 +518,25 @@ def mesh_main(cx, args):
     stream = cx.stream()
     evaluate = fused if args.mode == "fused" else sep
 
+    xh = torch.from_numpy(np.ascontiguousarray(x)).pin_memory()   # IPOPT's iterate on the host
+
     def step_device():
+        evaluate()                             # x resident in every rank's HBM
+
+    def step_bcast():
         if cx.world > 1:
-            dist.broadcast(xd, src=0)          # IPOPT's iterate to every rank (RCCL)
+            dist.broadcast(xd, src=0)          # the iterate from rank 0 to every rank (RCCL)
         evaluate()
 
     def step_host():
-        step_device()
+        xd.copy_(xh, non_blocking=True)        # the iterate from host memory over the rank's PCIe link
+        evaluate()
         hg.copy_from_device_async(gd.data_ptr(), vd.data_ptr(), stream)
         torch.cuda.current_stream().synchronize()
         if cx.world > 1:
             dist.barrier()                     # every slice has landed on the IPOPT host
     k, el = measure(cx, step_device, args)
+    kb, elb = measure(cx, step_bcast, args, k=max(50, args.steps // 4), w=max(10, args.warmup // 10))
     kh, elh = measure(cx, step_host, args, k=max(50, args.steps // 4), w=max(10, args.warmup // 10))
     ok = None
     if cx.rank == 0:
@@ -553,12 +564,17 @@ def mesh_main(cx, args):
                 "config": {"workload": wl + ", one NLP sharded by mesh interval for one host IPOPT",
                            "mesh_intervals": N, "n": nlp.n, "m": nlp.m, "nnz_jac": nlp.nnz,
                            "fd": args.fd, "mode": args.mode,
-                           "parallelism": f"mesh-shard{cx.world}: RCCL broadcast of x, each rank its "
-                                          "contiguous intervals, g / J slices in its HBM",
+                           "parallelism": f"mesh-shard{cx.world}: x resident on every rank, each rank "
+                                          "its contiguous intervals, g / J slices in its HBM",
                            "calls": "asynchronous (device pointers, torch stream)"},
+                "x_broadcast": {"value": round(kb / elb, 3), "unit": "calls/s", "steps": kb,
+                                "ms_per_step": round(1e3 * elb / kb, 5),
+                                "note": "+ an RCCL broadcast of x from rank 0 before every evaluation"},
                 "host_inclusive": {"value": round(kh / elh, 3), "unit": "calls/s", "steps": kh,
                                    "ms_per_step": round(1e3 * elh / kh, 5),
-                                   "note": "+ each rank's slice DMA into one page-locked host buffer "
+                                   "note": "the host IPOPT's round trip: x from page-locked host memory "
+                                           "over each rank's PCIe link, the shard's evaluation, each "
+                                           "rank's g / J slice DMA into one page-locked host buffer "
                                            "shared by the node's ranks (HostGather), barrier",
                                    "reassembly_bit_exact": ok},
                 "replicas": {"value": round(kr * cx.world / elr, 3), "unit": "calls/s", "steps": kr,
@@ -659,6 +675,14 @@ def main():
             extra["config3"] = config3_line(cx, args)
         if cx.world == 1:
             extra["solve"] = solve_lines()
+            if args.solve_batch > 0:
+                # configs[4]: the GPU's share of the 64-solve MocoInverse sweep,
+                # one solver (process, HIP context + stream, host IPM) each
+                from mocohip import batchsolve
+                sb = batchsolve.solve_batch(batchsolve.sweep(args.solve_batch), 125, device=cx.local)
+                sb["workload"] = ("configs[4]: MocoInverse gait10dof18musc N=125 for scaled subjects "
+                                  "(length 0.97-1.03, mass 0.90-1.10), all started together on one GPU")
+                extra["inverse_solve_batch"] = sb
         if args.inverse_batch > 0:
             # MocoTool mesh_interval 0.02 s: ceil((2.499 - 0.001) / 0.02) = 125
             # intervals (MocoTool.cpp:27,68-69)

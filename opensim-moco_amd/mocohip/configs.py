@@ -333,7 +333,7 @@ def gait10dof18musc_track(num_mesh_intervals: int = 65) -> MocoStudy:
 
 
 def gait10dof18musc_inverse(num_mesh_intervals: int = 25, fd_scheme: str = "forward",
-                            sparsity: str = "random") -> MocoStudy:
+                            sparsity: str = "random", subject=None) -> MocoStudy:
     """MocoInverse on gait10dof18musc (configs[4], one solve of the batch):
     kinematics prescribed by a PositionMotion of the coordinate trajectories
     (MocoInverse.cpp:46-66; GCVSpline degree 5, PositionMotion.cpp:121-155),
@@ -344,8 +344,12 @@ def gait10dof18musc_inverse(num_mesh_intervals: int = 25, fd_scheme: str = "forw
     no control-midpoint interpolation, forward differences and "random"
     sparsity detection (MocoInverse.cpp:104-114).  The kinematics are the
     bundled walking coordinate trajectories, clipped by 1e-3 at both ends
-    (clip_time_range, MocoInverse.cpp:82-86)."""
+    (clip_time_range, MocoInverse.cpp:82-86).  ``subject`` = (length,
+    mass) scales the model (scale_subject: one subject of a configs[4]
+    sweep; the same kinematics)."""
     m = gait10dof18musc_model(tendon_compliance=True, tendon_dynamics="implicit")
+    if subject is not None:
+        m = scale_subject(m, *subject)
     ref = _load("walk_gait1018_state_reference.json")
     t = np.asarray(ref["time"])
     kin = DataTable("kinematics", t, {k: np.asarray(v) for k, v in ref["columns"].items()

@@ -151,3 +151,16 @@ def test_moco_inverse_gait_n125_converges():
     assert sol.metadata["success"] == "true", sol.metadata
     # (measured 7.762 through the oracle and on the GPU path)
     assert 7.5 < float(sol.metadata["objective"]) < 8.1
+
+
+def test_inverse_solve_batch():
+    """configs[4] layout: MocoInverse solves of scaled subjects started
+    together, one process (HIP context, stream, host IPM) each, on one GPU:
+    every solve converges on the generated back end (structure-only
+    specialization keeps the scaled subjects on it)."""
+    from mocohip import batchsolve
+    out = batchsolve.solve_batch(batchsolve.sweep(3), num_mesh_intervals=10)
+    assert out["succeeded"] == 3, out
+    for r in out["results"]:
+        assert r["backend"].startswith("generated:"), r
+        assert r["iterations"] > 0
