@@ -639,6 +639,14 @@ def main():
                          "value_fused": round(k4 * cx.world / ef4, 3),
                          "n": n4.n, "m": n4.m, "nnz_jac": n4.nnz, "host_inclusive": hi4,
                          "workload": "configs[2] workload at N=400 (north_star target size)"}
+        if cx.world == 1 and not args.no_cpu_baseline:
+            # the north star's target ratio is quoted at N=400 (>= 10x the
+            # CPU eval_jac_g throughput): the oracle on the same N=400 NLP
+            box = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+            cb4 = cpu_baseline(n4.rep, st4.solver.options(), x4, max(3.0, args.cpu_baseline_seconds / 2),
+                               max(1, min(box, os.cpu_count() or 1)))
+            extra["n400"]["cpu_baseline"] = cb4
+            extra["n400"]["speedup_vs_cpu_baseline"] = round(extra["n400"]["value"] / cb4["value"], 1)
         n4.close()
         extra["host_inclusive"] = host_inclusive(cx, nlp, x, args)
         # optim_sparsity_detection "random" (MocoInverse's setting,
