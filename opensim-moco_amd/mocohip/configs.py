@@ -72,12 +72,13 @@ def sliding_mass_interface(num_mesh_intervals: int = 19, scheme: str = "trapezoi
     return MocoStudy(p, s)
 
 
-def n_link_pendulum(num_links: int) -> Model:
-    """ModelFactory::createNLinkPendulum."""
+def n_link_pendulum(num_links: int, inertia=(1, 1, 1, 0, 0, 0)) -> Model:
+    """ModelFactory::createNLinkPendulum (inertia=(0,)*6: point masses at
+    the link tips, tropter's double pendulum, test_double_pendulum.cpp:45-74)."""
     m = Model({1: "pendulum", 2: "double_pendulum"}.get(num_links, f"{num_links}_link_pendulum"))
     prev = "ground"
     for i in range(num_links):
-        m.add_body(Body(f"b{i}", 1.0, (0, 0, 0), (1, 1, 1, 0, 0, 0)))
+        m.add_body(Body(f"b{i}", 1.0, (0, 0, 0), tuple(inertia)))
         q = Coordinate(f"q{i}", (-math.pi / 2, math.pi / 2))
         m.add_joint(Joint.pin(f"j{i}", prev, f"b{i}", q, loc_in_child=(-1, 0, 0)))
         prev = f"b{i}"
@@ -143,11 +144,12 @@ def double_pendulum_coupled(num_mesh_intervals: int = 20, scheme: str = "hermite
 
 
 def double_pendulum_swingup(num_mesh_intervals: int = 29, scheme: str = "trapezoidal",
-                            dynamics: str = "explicit") -> MocoStudy:
+                            dynamics: str = "explicit", point_masses: bool = False) -> MocoStudy:
     """testImplicit.cpp:30-100 (solveDoublePendulumSwingup): final-time goal
     (weight 0.001) + MocoMarkerFinalGoal on /markerset/marker1 to (0, 2, 0)
-    (weight 1000), trapezoidal, N=29, both dynamics modes."""
-    m = n_link_pendulum(2)
+    (weight 1000), trapezoidal, N=29, both dynamics modes.  point_masses:
+    tropter's pendulum (no link inertia; test_double_pendulum.cpp:80-150)."""
+    m = n_link_pendulum(2, inertia=(0, 0, 0, 0, 0, 0) if point_masses else (1, 1, 1, 0, 0, 0))
     p = MocoProblem(m)
     p.set_time_bounds(0.0, (0.0, 5.0))
     p.set_state_info("/jointset/j0/q0/value", (-10, 10), 0)

