@@ -1041,7 +1041,9 @@ __device__ __host__ __forceinline__ uint32_t ct_word(uint32_t off, uint32_t coef
 }
 // LDS constants after the times: [0] 0.0, [1] 1.0, [2..7] the interval's
 // coefficients {0, -h/8, h/8, -h/6, (-h/6) 4, -h/2}, [8..11] the bases {0,
-// -1/2, 1, -1}.
+// -1/2, 1, -1} (a word's coefficient / base selectors index them).  After
+// the words (entries(N - 1) of them) the compiled template holds one more
+// word per entry: the LDS offset of the entry's row's base lane.
 constexpr int CT_CONST = 4;      // offset of the constants after sTimes
 constexpr int CT_NCONST = 12;
 
@@ -1114,6 +1116,13 @@ __device__ __forceinline__ void interval_body(const DevModel& M, const Src& S, c
         const int e = threadIdx.x + u * blockDim.x;
         pw[u] = I.pf && ctpl && e < ne_iv ? ctpl[e] : CT_GEN;
     }
+    const uint32_t* __restrict__ cbase = ctpl ? ctpl + I.nnz_int + I.nnz_tail : nullptr;
+    uint32_t pb[IV_PF];
+#pragma unroll
+    for (int u = 0; u < IV_PF; ++u) {
+        const int e = threadIdx.x + u * blockDim.x;
+        pb[u] = I.pf && ctpl && e < ne_iv ? cbase[e] : 0u;
+    }
     // likewise the template entry of this thread's first t0 / tf entry
     int eg0 = -1;
     TplEntry tg0{};
@@ -1122,6 +1131,13 @@ __device__ __forceinline__ void interval_body(const DevModel& M, const Src& S, c
         tg0 = tpl[eg0];
     }
     __syncthreads();
+    if (values && ctpl && threadIdx.x == 0) {
+        // the coefficient / base tables the words select from (the same
+        // doubles the general path computes)
+        const IvC C0 = iv_const(sTimes[npts - 1] - sTimes[0], S.grid[k_last] - S.grid[k_first]);
+        sK[2] = 0.0; sK[3] = -C0.h8; sK[4] = C0.h8; sK[5] = -C0.h6; sK[6] = -C0.h6 * 4.0; sK[7] = -C0.hh;
+        sK[8] = 0.0; sK[9] = -0.5; sK[10] = 1.0; sK[11] = -1.0;
+    }
     // finite-difference quotients in place (CasADi FiniteDiff formulas), once
     // per (point, output, direction) instead of once per Jacobian entry that
     // reads them; the base slot keeps the raw value for the defect rows
@@ -1169,6 +1185,7 @@ __device__ __forceinline__ void interval_body(const DevModel& M, const Src& S, c
         for (int r = threadIdx.x; r < I.rows(i); r += blockDim.x) gi[r] = defect_row(L, I, Ln, S.x, YV, i, r);
     }
     if (I.dbg_stop == 4) return;
+    if (values && ctpl) __syncthreads();   // the coefficient / base tables in sK
     if (values) {
         const IvC C = iv_const(YV.t(k_last) - YV.t(k_first), S.grid[k_last] - S.grid[k_first]);
         double* vi = values + (long)il * I.nnz_int;
@@ -1180,30 +1197,26 @@ __device__ __forceinline__ void interval_body(const DevModel& M, const Src& S, c
         if (ctpl) {
 #pragma clang fp contract(off)
             const lds_double* q0 = lds(sY);
-            // coefficient / base of a word, selected in registers
-            const double c1 = -C.h8, c2 = C.h8, c3 = -C.h6, c4 = -C.h6 * 4.0, c5 = -C.hh;
+            // coefficient / base of a word: LDS tables (sK, filled above)
+            const lds_double* kc = lds(sK + 2);
+            const lds_double* kb = lds(sK + 8);
             // I.qfuse: the word's LDS offset names the raw value of the
             // perturbed lane; the quotient (CasADi FiniteDiff) is formed here
-            // from it and its row's base (forward / backward) or mirror
-            // (central) lane -- the quotient pass's arithmetic, bit for bit
+            // from it and its row's base (forward / backward: the base-lane
+            // offset stored after the words) or mirror (central) lane -- the
+            // quotient pass's arithmetic, bit for bit
             const int nyall = npts * ny;
             const int fuse = values && Ln.stride > 1 && I.qfuse;
-            const float inv_stride = 1.0f / (float)Ln.stride;
             const double h1 = Ln.h, h2 = 2.0 * Ln.h;
-            auto qat = [&](uint32_t off) -> double {
+            auto qat = [&](uint32_t off, uint32_t boff) -> double {
                 const double y = q0[off];
                 if (!fuse || (int)off >= nyall) return y;
                 if (Ln.fd == MH_FD_CENTRAL) return (y - q0[off + Ln.ND]) / h2;
-                int row = (int)((float)off * inv_stride);
-                row += (row + 1) * Ln.stride <= (int)off ? 1 : 0;
-                row -= row * Ln.stride > (int)off ? 1 : 0;
-                const double yb = q0[row * Ln.stride + Ln.base];
+                const double yb = q0[boff];
                 return Ln.fd == MH_FD_FORWARD ? (y - yb) / h1 : (yb - y) / h1;
             };
             auto value = [&](uint32_t wu, double q) {
-                const uint32_t ks = (wu >> 20) & 7, bs = (wu >> 23) & 7;
-                const double coef = ks == 1 ? c1 : ks == 2 ? c2 : ks == 3 ? c3 : ks == 4 ? c4 : ks == 5 ? c5 : 0.0;
-                const double base = bs == 1 ? -0.5 : bs == 2 ? 1.0 : bs == 3 ? -1.0 : 0.0;
+                const double coef = kc[(wu >> 20) & 7], base = kb[(wu >> 23) & 7];
                 return (wu & CT_RAW) ? q : base + coef * q;
             };
             // the bulk: one LDS value, a product and a sum per entry; the
@@ -1211,22 +1224,25 @@ __device__ __forceinline__ void interval_body(const DevModel& M, const Src& S, c
             // entries are written by the loops below
 #pragma unroll
             for (int u = 0; u < IV_PF; ++u)
-                if (!(pw[u] & (CT_GEN | CT_PATH))) vi[e + u * B] = value(pw[u], qat(pw[u] & CT_OFF));
+                if (!(pw[u] & (CT_GEN | CT_PATH))) vi[e + u * B] = value(pw[u], qat(pw[u] & CT_OFF, pb[u]));
             if (I.pf) e += IV_PF * B;
             for (; e + (IV_UNROLL - 1) * B < ne; e += IV_UNROLL * B) {
-                uint32_t w[IV_UNROLL];
+                uint32_t w[IV_UNROLL], wb[IV_UNROLL];
                 double q[IV_UNROLL];
 #pragma unroll
-                for (int u = 0; u < IV_UNROLL; ++u) w[u] = ctpl[e + u * B];
+                for (int u = 0; u < IV_UNROLL; ++u) {
+                    w[u] = ctpl[e + u * B];
+                    wb[u] = cbase[e + u * B];
+                }
 #pragma unroll
-                for (int u = 0; u < IV_UNROLL; ++u) q[u] = qat(w[u] & CT_OFF);
+                for (int u = 0; u < IV_UNROLL; ++u) q[u] = qat(w[u] & CT_OFF, wb[u]);
 #pragma unroll
                 for (int u = 0; u < IV_UNROLL; ++u)
                     if (!(w[u] & (CT_GEN | CT_PATH))) vi[e + u * B] = value(w[u], q[u]);
             }
             for (; e < ne; e += B) {
                 const uint32_t wu = ctpl[e];
-                if (!(wu & (CT_GEN | CT_PATH))) vi[e] = value(wu, qat(wu & CT_OFF));
+                if (!(wu & (CT_GEN | CT_PATH))) vi[e] = value(wu, qat(wu & CT_OFF, cbase[e]));
             }
             if (eg0 >= 0) vi[eg0] = jac_entry<false>(L, Ln, I.P, S.x, YV, tg0, k_first, C);
             for (int j = threadIdx.x + (I.pf ? B : 0); j < nctgen; j += B) {

@@ -781,6 +781,19 @@ static bool compile_template(mh_ctx* c) {
     c->ctgen.clear();
     for (int e = 0; e < c->nnz_int + c->nnz_tail; ++e)
         if (c->ctpl[e] & CT_GEN) c->ctgen.push_back(e);
+    // after the words, per entry the LDS offset of its row's base lane (the
+    // forward / backward quotient's y(x) in the assembly; 0 where unused):
+    // read with the word instead of dividing the offset by the stride
+    const size_t nw = c->ctpl.size();
+    if (nw != (size_t)c->nnz_int + (size_t)c->nnz_tail) return false;
+    const uint32_t nyall = (uint32_t)(npts * NO * stride);
+    const int base = stride - 1;   // the base lane closes a point's lanes (Lanes, mh_create)
+    for (size_t e = 0; e < nw; ++e) {
+        const uint32_t w = c->ctpl[e];
+        const uint32_t off = w & CT_OFF;
+        const bool lane = !(w & (CT_GEN | CT_PATH)) && off < nyall;
+        c->ctpl.push_back(lane ? off / (uint32_t)stride * (uint32_t)stride + (uint32_t)base : 0u);
+    }
     // k_role lists: entry e goes to the role of its point, its word against
     // that role's own-point layout (q at o * stride + dir)
     const int R = npts;
