@@ -250,10 +250,10 @@ def roofline(cx, nlp, steps, args, mode):
     nlp.set_timing(False)
     J = np.array(rec["jac"])          # [whole, DAE stage, transcription stage, k_groups] ms
     ev_dae_ms, ev_tr_ms = float(np.median(J[:, 1])), float(np.median(J[:, 2]))
-    # per-launch kernel durations: each stage of eval_jac_g alone, launched
-    # back to back (the queue ahead of the GPU), between HIP events on the
-    # context stream (mh_debug_time_stages) -- the figure a rocprofv3 kernel
-    # trace of the same launches gives, plus the inter-kernel gap
+    # per-launch kernel durations: the stages of eval_jac_g in call order,
+    # a HIP event after each on the context stream (the queue ahead of the
+    # GPU; mh_debug_time_stages) -- the figure a rocprofv3 kernel trace of
+    # the same launches gives, plus the inter-kernel gap
     dae_ms, tr_ms = nlp.time_stages(steps[3][0], kind=1, reps=max(50, args.steps))
     G, ND = nlp.G, nlp.NS + nlp.NC + 2
     n_dae = G * (ND + 1) if args.fd != "central" else G * (2 * ND + 1)
@@ -293,7 +293,7 @@ def roofline(cx, nlp, steps, args, mode):
     roof["other_kernel"] = other
     roof.update({"backend": be_name, "model_hash": f"0x{mhash:016x}",
                  "backend_flags": nlp.backend_flags(),
-                 "timing": "mh_debug_time_stages: back-to-back launches of one stage between HIP events",
+                 "timing": "mh_debug_time_stages: both stages in call order, a HIP event after each",
                  "instrumented_ms_per_step": round(1e3 * el / args.steps, 4),
                  "in_call_stage_ms": [round(ev_dae_ms, 5), round(ev_tr_ms, 5)]})
     if rec["g"]:

@@ -706,11 +706,12 @@ int mh_debug_jacobian_lanes(mh_ctx* ctx, const double* x, double* times,
 
 /* Benchmark entry: average device duration of each stage of eval_jac_g
  * (kind 1) or eval_g (kind 0) at the device iterate x_dev, over reps
- * back-to-back launches of that stage alone (HIP events around the run on
- * the context stream; the queue stays ahead of the GPU, so the figure is
- * the kernels' own duration plus the inter-kernel gap, comparable with a
- * rocprofv3 kernel trace).  ms2[0]: DAE stage, ms2[1]: transcription stage.
- * Results land in the context's internal buffers. */
+ * (at most 500) evaluations of both stages in their call order with a HIP
+ * event after each stage on the context stream (the queue stays ahead of
+ * the GPU, so each figure is that kernel's own duration plus the launch gap
+ * in the sequence a call runs, comparable with a rocprofv3 kernel trace).
+ * ms2[0]: DAE stage, ms2[1]: transcription stage.  Results land in the
+ * context's internal buffers. */
 int mh_debug_time_stages(mh_ctx* ctx, const double* x_dev, int kind, int reps, double* ms2);
 
 /* Stage timing: when on, every evaluation records HIP events between its

@@ -2561,16 +2561,32 @@ extern "C" int mh_debug_time_stages(mh_ctx* c, const double* x, int kind, int re
     int rc = launch_stage(c, 0, kind, x, a, nullptr);   // warm: the transcription reads its results
     if (!rc) rc = launch_stage(c, 1, kind, x, a, nullptr);
     if (rc) return rc;
-    HIPCHK(hipEventRecord(c->ev[0], c->stream));
-    for (int r = 0; r < reps && !rc; ++r) rc = launch_stage(c, 0, kind, x, a, nullptr);
-    HIPCHK(hipEventRecord(c->ev[1], c->stream));
-    for (int r = 0; r < reps && !rc; ++r) rc = launch_stage(c, 1, kind, x, a, nullptr);
-    HIPCHK(hipEventRecord(c->ev[2], c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    // the two stages in their real order (the DAE stage, then the
+    // transcription reading what it just wrote), an event after each: every
+    // launch is timed in the sequence a call runs, as a kernel trace sees it
+    // (back-to-back launches of one stage alone read up to ~10 % faster)
+    reps = std::min(reps, 500);
+    std::vector<hipEvent_t> ev((size_t)2 * reps + 1, nullptr);
+    for (auto& e : ev) HIPCHK(hipEventCreate(&e));
+    HIPCHK(hipEventRecord(ev[0], c->stream));
+    for (int r = 0; r < reps && !rc; ++r) {
+        rc = launch_stage(c, 0, kind, x, a, nullptr);
+        if (!rc) (void)hipEventRecord(ev[2 * r + 1], c->stream);
+        if (!rc) rc = launch_stage(c, 1, kind, x, a, nullptr);
+        if (!rc) (void)hipEventRecord(ev[2 * r + 2], c->stream);
+    }
+    const hipError_t es = hipStreamSynchronize(c->stream);
+    double t0 = 0.0, t1 = 0.0;
+    for (int r = 0; r < reps && !rc && es == hipSuccess; ++r) {
+        float a0 = 0, a1 = 0;
+        (void)hipEventElapsedTime(&a0, ev[2 * r], ev[2 * r + 1]);
+        (void)hipEventElapsedTime(&a1, ev[2 * r + 1], ev[2 * r + 2]);
+        t0 += a0;
+        t1 += a1;
+    }
+    for (auto& e : ev) (void)hipEventDestroy(e);
+    HIPCHK(es);
     if (rc) return rc;
-    float t0 = 0, t1 = 0;
-    HIPCHK(hipEventElapsedTime(&t0, c->ev[0], c->ev[1]));
-    HIPCHK(hipEventElapsedTime(&t1, c->ev[1], c->ev[2]));
     ms2[0] = t0 / reps;
     ms2[1] = t1 / reps;
     return MH_OK;
