@@ -1954,6 +1954,7 @@ struct mh_ctx {
     bool use_roles = false;        // MOCOHIP_ROLES=1: k_role (+ k_couple) for the Jacobian lanes
     int role_threads = 256;        // k_role workgroup size (MOCOHIP_ROLE_THREADS: 64..512)
     int iv_threads = 1024;         // k_interval workgroup size, Jacobian lanes (MOCOHIP_IV_THREADS: 256..1024)
+    int ivg_threads = 256;         // k_interval workgroup size, eval_g lanes (MOCOHIP_IVG_THREADS: 64..1024)
     bool role_couple = true;       // coupling in k_role's time role (MOCOHIP_ROLE_COUPLE=0: k_couple)
     bool use_ctpl = true;          // MOCOHIP_CTPL=0: k_interval assembles through jac_entry
     float timings[4] = {0, 0, 0, 0};
@@ -2272,7 +2273,7 @@ static void be_interval(mh_ctx* c, const double* x, int mode, double* g, double*
     auto kern = k_interval<D>;
     if (lds > 65536)
         (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    const unsigned threads = v ? (unsigned)c->iv_threads : 256u;
+    const unsigned threads = v ? (unsigned)c->iv_threads : (unsigned)c->ivg_threads;
     if (i1 < 0) { i0 = 0; i1 = c->ie - c->ib; }
     if (i1 <= i0) return;
     hipLaunchKernelGGL(kern, dim3((unsigned)(i1 - i0)), dim3(threads), lds, c->stream, c->M,

@@ -1492,6 +1492,8 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
         c->iv_qfuse = !(eqf && std::strcmp(eqf, "0") == 0);   // default: measured faster
         const char* eth = std::getenv("MOCOHIP_IV_THREADS");
         if (eth) c->iv_threads = std::min(1024, std::max(256, std::atoi(eth) / 64 * 64));
+        const char* egt = std::getenv("MOCOHIP_IVG_THREADS");
+        if (egt) c->ivg_threads = std::min(1024, std::max(64, std::atoi(egt) / 64 * 64));
         const char* eo = std::getenv("MOCOHIP_ROLE_COUPLE");
         c->role_couple = !(eo && std::strcmp(eo, "0") == 0);
         const char* ea = std::getenv("MOCOHIP_ASM");
