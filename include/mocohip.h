@@ -489,7 +489,10 @@ typedef struct mh_options {
     int32_t jacobian_mode;
     int32_t reserved_jm;
     /* (ABI v6) How detection decides a coupling (mh_sparsity_rule).
-     * ROBUST (0, default): output k depends on input j iff its change under
+     * The plugin surface (MocoHipSolver optim_sparsity_detection_rule, the
+     * C++ builder's MocoHipSolver) defaults to ANY_CHANGE, the reference's
+     * rule; a zero-initialized mh_options means ROBUST.
+     * ROBUST (0): output k depends on input j iff its change under
      * the +1e-5 perturbation is NaN or exceeds 1e-12 * the callback's
      * magnitude at the detection iterate (max(1, max over its outputs of
      * |output|)) -- a true dependency changes an output by ~1e-5 *

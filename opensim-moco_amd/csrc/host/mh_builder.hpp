@@ -300,7 +300,7 @@ struct SolverSettings {
     double velocity_correction_bounds[2] = {-0.1, 0.1};
     std::string optim_sparsity_detection = "none";
     int optim_sparsity_detection_random_count = 3;
-    std::string optim_sparsity_detection_rule = "robust";
+    std::string optim_sparsity_detection_rule = "any-change";   // the reference's rule (CasOCFunction.cpp:44-61)
 };
 mh_options make_options(const SolverSettings& s, int interval_begin = 0, int interval_end = 0);
 

@@ -72,6 +72,13 @@ class IpmOptions:
     max_iter: int = 3000
     mu_init: float = 0.1
     mu_min: float = 1e-11
+    # the tol-derived floor of Ipopt 3.12's monotone barrier update
+    # (MonotoneMuUpdate::CalcNewMuAndTau: mu >= min(tol, compl_inf_tol) /
+    # (barrier_tol_factor + 1)).  Off by default: measured on the two
+    # reference golden solves ("Solves"), the floor
+    # stops MocoInverse Rajagopal-18 at objective 1.1259 (controls RMS 0.025
+    # against its golden file) where mu_min alone reaches 1.08769 (RMS 0.0018)
+    mu_floor_from_tol: bool = False
     kappa_eps: float = 10.0
     kappa_mu: float = 0.2
     theta_mu: float = 1.5
@@ -87,6 +94,13 @@ class IpmOptions:
     limited_memory_init_val: float = 1.0
     max_soc: int = 4
     kappa_soc: float = 0.99
+    # after the restoration phase (Ipopt 3.12 IpRestoMinC_1Nrm): the least-
+    # squares constraint multipliers are kept only when their max-norm is at
+    # most constr_mult_reset_threshold (default 0: they are set to zero), and
+    # the bound multipliers are reset to 1 when their max-norm exceeds
+    # bound_mult_reset_threshold
+    constr_mult_reset_threshold: float = 0.0
+    bound_mult_reset_threshold: float = 1000.0
     print_level: int = 0
     # filter line search constants (Waechter & Biegler 2006, Table 1)
     gamma_theta: float = 1e-5
@@ -174,12 +188,19 @@ class _Scaled:
 
     def __init__(self, nlp, x0: np.ndarray, opt: IpmOptions):
         self.nlp = nlp
-        self.n_full, self.m = int(nlp.n), int(nlp.m)
+        self.n_full, self.m_full = int(nlp.n), int(nlp.m)
         xl, xu, gl, gu = nlp.bounds()
         xl = np.asarray(xl[:self.n_full], float).copy()
         xu = np.asarray(xu[:self.n_full], float).copy()
-        gl = np.asarray(gl[:self.m], float).copy()
-        gu = np.asarray(gu[:self.m], float).copy()
+        gl = np.asarray(gl[:self.m_full], float).copy()
+        gu = np.asarray(gu[:self.m_full], float).copy()
+        # rows with both bounds infinite constrain nothing (their slack would
+        # have no barrier term): left out of the problem the method sees
+        self.rows = np.where(~(np.isneginf(gl) & np.isposinf(gu)))[0]
+        self.m = len(self.rows)
+        row_map = -np.ones(self.m_full, np.int64)
+        row_map[self.rows] = np.arange(self.m)
+        gl, gu = gl[self.rows], gu[self.rows]
         self.xl_full, self.xu_full = xl, xu
         self.gl, self.gu = gl, gu
         self.fixed = np.isfinite(xl) & (xl == xu)
@@ -195,9 +216,9 @@ class _Scaled:
         jc = np.asarray(jc[:nlp.nnz], np.int64)
         col_map = -np.ones(self.n_full, np.int64)
         col_map[self.free] = np.arange(self.nx)
-        keep = col_map[jc] >= 0
+        keep = (col_map[jc] >= 0) & (row_map[ir] >= 0)
         self.keep = np.where(keep)[0]
-        self.ir, self.jc = ir[keep], col_map[jc[keep]]
+        self.ir, self.jc = row_map[ir[keep]], col_map[jc[keep]]
         # CSR pattern of J_x and the permutation of the kept values into it
         order = np.lexsort((self.jc, self.ir))
         self.order = order
@@ -245,7 +266,7 @@ class _Scaled:
         return self.obj_scale * np.concatenate([g[self.free], np.zeros(self.ns)])
 
     def g_raw(self, v):
-        return np.asarray(self._timed("g", self.nlp.eval_g, self._x(v)), float)[:self.m]
+        return np.asarray(self._timed("g", self.nlp.eval_g, self._x(v)), float)[self.rows]
 
     def C(self, v, graw=None):
         g = self.g_raw(v) if graw is None else graw
@@ -501,7 +522,7 @@ def _solve_ipm(nlp, x0: np.ndarray, options: Optional[IpmOptions] = None) -> Ipm
             _, _, y = kk.solve(-(gf[:nx] - zl[:nx] + zu[:nx]), -(gf[nx:] - zl[nx:] + zu[nx:]), np.zeros(m))
             if not np.all(np.isfinite(y)) or np.abs(y).max(initial=0) > opt.constr_mult_init_max:
                 y = np.zeros(m)
-        except RuntimeError:
+        except (RuntimeError, np.linalg.LinAlgError):
             y = np.zeros(m)
 
     theta = float(np.abs(c).sum())
@@ -560,11 +581,13 @@ def _solve_ipm(nlp, x0: np.ndarray, options: Optional[IpmOptions] = None) -> Ipm
             Emu = max(d_ / sd_, p_, cm / sc_)
             if Emu > opt.kappa_eps * mu:
                 break
-            # Ipopt's monotone strategy bounds mu by mu_min only (the
-            # tol/10 floor of the paper's (7) belongs to its adaptive
-            # strategy); MocoInverse's golden solution sits within 5e-6 of
-            # its 0.01 control bounds, which mu >= tol / 11 cannot reach
-            mu_new = max(opt.mu_min, min(opt.kappa_mu * mu, mu ** opt.theta_mu))
+            # Ipopt's MonotoneMuUpdate::CalcNewMuAndTau: the superlinear
+            # decrease, bounded below by min(tol, compl_inf_tol) /
+            # (barrier_tol_factor + 1) and by mu_min
+            mu_new = min(opt.kappa_mu * mu, mu ** opt.theta_mu)
+            if opt.mu_floor_from_tol:
+                mu_new = max(mu_new, min(opt.tol, opt.compl_inf_tol) / (opt.kappa_eps + 1.0))
+            mu_new = max(opt.mu_min, mu_new)
             if mu_new >= mu:
                 break
             mu = mu_new
@@ -588,7 +611,7 @@ def _solve_ipm(nlp, x0: np.ndarray, options: Optional[IpmOptions] = None) -> Ipm
                 dx, ds, dy = kkt.solve(rhs_v[:nx], rhs_v[nx:], -c)
                 if np.all(np.isfinite(dx)) and np.all(np.isfinite(dy)):
                     break
-            except RuntimeError:
+            except (RuntimeError, np.linalg.LinAlgError):
                 pass
             delta_c = 1e-8 * mu ** 0.25 if delta_c == 0.0 else delta_c * 100.0
             kkt = None
@@ -692,14 +715,20 @@ def _solve_ipm(nlp, x0: np.ndarray, options: Optional[IpmOptions] = None) -> Ipm
             gf = P.grad_f(v)
             vals = P.jac_vals(v)
             Jx = P.Jx(vals)
-            try:
-                kk = _KKT(Jx, P.ineq, np.ones(nx), np.ones(ns), 0.0, None, m)
-                _, _, y = kk.solve(-(gf[:nx] - zl[:nx] + zu[:nx]), -(gf[nx:] - zl[nx:] + zu[nx:]),
-                                   np.zeros(m))
-                if np.abs(y).max(initial=0) > opt.constr_mult_init_max:
+            if max(float(np.abs(zl).max(initial=0.0)), float(np.abs(zu).max(initial=0.0))) \
+                    > opt.bound_mult_reset_threshold:
+                zl = np.where(hl, 1.0, 0.0)
+                zu = np.where(hu, 1.0, 0.0)
+            y = np.zeros(m)
+            if opt.constr_mult_reset_threshold > 0:
+                try:
+                    kk = _KKT(Jx, P.ineq, np.ones(nx), np.ones(ns), 0.0, None, m)
+                    _, _, y = kk.solve(-(gf[:nx] - zl[:nx] + zu[:nx]), -(gf[nx:] - zl[nx:] + zu[nx:]),
+                                       np.zeros(m))
+                    if not np.all(np.isfinite(y)) or np.abs(y).max(initial=0) > opt.constr_mult_reset_threshold:
+                        y = np.zeros(m)
+                except (RuntimeError, np.linalg.LinAlgError):
                     y = np.zeros(m)
-            except RuntimeError:
-                y = np.zeros(m)
             lb = _LBFGS(nx, opt.limited_memory_max_history, opt.limited_memory_init_val)
             prev = None
             it += 1
@@ -733,7 +762,9 @@ def _solve_ipm(nlp, x0: np.ndarray, options: Optional[IpmOptions] = None) -> Ipm
     x_full = P._x(v)
     viol = P.unscaled_violation(v, graw)
     # multipliers of the original NLP (unscaled, Ipopt's lambda = y * row scale / obj scale)
-    lam = y * P.row_scale / P.obj_scale if m else np.zeros(0)
+    lam = np.zeros(P.m_full)
+    if m:
+        lam[P.rows] = y * P.row_scale / P.obj_scale
     z_l = np.zeros(P.n_full)
     z_u = np.zeros(P.n_full)
     z_l[P.free] = zl[:nx] / P.obj_scale
@@ -761,7 +792,7 @@ def _restore(P, v, c, Jx, lo, hi, hl, hu, Sig, tau, filt, theta, phi, barrier, o
         try:
             kk = _KKT(Jr, P.ineq, Dx, Ds, 1e-10, None, m)
             dx, ds, _ = kk.solve(np.zeros(nx), np.zeros(len(Ds)), -cr)
-        except RuntimeError:
+        except (RuntimeError, np.linalg.LinAlgError):
             return None
         d = np.concatenate([dx, ds])
         a = _ftb(vr, d, lo, hi, tau)
@@ -785,3 +816,35 @@ def _restore(P, v, c, Jx, lo, hi, hl, hu, Sig, tau, filt, theta, phi, barrier, o
         vals = P.jac_vals(vr)
         Jr = P.Jx(vals)
     return None
+
+
+def kkt_residuals(nlp, x: np.ndarray, options: Optional[IpmOptions] = None,
+                  x_scaling: Optional[np.ndarray] = None) -> dict:
+    """Ipopt's termination quantities at a given iterate x, with least-squares
+    constraint multipliers (no active variable bounds assumed beyond the
+    fixed ones): the unscaled constraint violation, the unscaled dual
+    infeasibility ||grad f + J^T lambda||_inf over the free variables, and
+    the scaled optimality error E0 = max(dual / s_d, primal) that Ipopt's
+    ``tol`` tests, under the gradient-based scaling computed at
+    ``x_scaling`` (Ipopt's starting point; default x).  Used to check a
+    reference solution file against this NLP's own termination test."""
+    from scipy.sparse.linalg import lsqr
+    opt = options or IpmOptions()
+    P = _Scaled(nlp, x if x_scaling is None else x_scaling, opt)
+    x = np.asarray(x, float)
+    g = np.asarray(nlp.eval_g(x), float)[P.rows]
+    gf = np.asarray(nlp.eval_grad_f(x), float)
+    vals = np.asarray(nlp.eval_jac_g(x), float)[:nlp.nnz][P.keep]
+    J = P.Jx(vals)                                   # row-scaled, free columns
+    b = -P.obj_scale * gf[P.free]
+    y = lsqr(J.T.tocsr(), b, atol=1e-14, btol=1e-14, iter_lim=50000)[0]
+    r = J.T @ y - b
+    viol = float(np.max(np.concatenate([[0.0], P.gl - g, g - P.gu]))) if P.m else 0.0
+    primal = float(np.abs(np.where(P.gl == P.gu, P.row_scale * (g - P.gl),
+                                   P.row_scale * np.maximum(0.0, np.maximum(P.gl - g, g - P.gu))))
+                   .max(initial=0.0))
+    sd = max(opt.s_max, float(np.abs(y).sum()) / max(1, P.m)) / opt.s_max
+    dual = float(np.abs(r).max(initial=0.0))
+    return {"objective": float(nlp.eval_f(x)), "constraint_violation": viol,
+            "dual_infeasibility": dual / P.obj_scale, "scaled_primal": primal, "s_d": sd,
+            "E0": max(dual / sd, primal), "lambda_max": float(np.abs(y).max(initial=0.0))}

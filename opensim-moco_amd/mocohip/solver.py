@@ -43,12 +43,16 @@ class MocoHipSolver:
     optim_sparsity_detection: str = "none"
     optim_sparsity_detection_random_count: int = 3
     # how a detection probe decides a coupling (include/mocohip.h
-    # mh_sparsity_rule): "robust" (default; changes below 1e-12 of the
-    # callback's output magnitude are rounding noise -- the pattern is the model's,
-    # the same in every implementation) or "any-change" (the reference's
-    # rule, CasOCFunction.cpp:44-61, which makes couplings that cancel to
-    # rounding level depend on the order of floating-point operations)
-    optim_sparsity_detection_rule: str = "robust"
+    # mh_sparsity_rule): "any-change" (default: the reference's rule,
+    # CasOCFunction.cpp:44-61 -- any nonzero change or NaN; couplings that
+    # cancel to rounding level are then detected or not depending on the
+    # order of floating-point operations, so the device's pattern can be a
+    # strict superset or subset of another implementation's on those
+    # entries, whose values are rounding noise) or "robust" (opt-in: changes
+    # below 1e-12 of the callback's output magnitude count as noise -- the
+    # pattern is then the model's, the same in every implementation, at the
+    # price of dropping real couplings smaller than that)
+    optim_sparsity_detection_rule: str = "any-change"
     sparsity_guess: Optional[np.ndarray] = None
     # "given": the callback sparsity itself (HipNLP.callback_sparsity()),
     # e.g. detected once and shared by every shard / replica

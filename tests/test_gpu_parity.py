@@ -323,9 +323,15 @@ def _pair(name, backend="auto", tasks=None, env=None):
             if v is not None:
                 os.environ[k] = v
     name_ = gpu.backend()[0]
-    # with sparsity detection the oracle detects its own pattern (the robust
-    # rule makes it the device's, test_sparsity_detection_agrees), so the
-    # structures compared below are independent
+    # with sparsity detection under the robust rule the oracle detects its
+    # own pattern (equal to the device's, test_sparsity_detection_agrees), so
+    # the structures compared below are independent; under the reference's
+    # rule (any-change, the default) the rounding-level couplings differ
+    # between implementations, so the oracle takes the device's pattern
+    from mocohip import abi
+    if (opts.sparsity_detection not in (abi.MH_SPARSITY_NONE, abi.MH_SPARSITY_GIVEN)
+            and opts.sparsity_rule == abi.MH_SPARSITY_RULE_ANY_CHANGE):
+        opts = _given(st, gpu.callback_sparsity())
     if backend == "generic":
         assert name_.startswith("generic"), name_
     elif backend == "lane":
@@ -886,8 +892,8 @@ SPARSE = [n for n in CASES if "sparse" in n]
 
 @pytest.mark.parametrize("name", SPARSE)
 def test_sparsity_detection_agrees(name):
-    """Detected sparsity is bit-reproducible: with the default rule
-    (include/mocohip.h MH_SPARSITY_RULE_ROBUST: a probe counts as a coupling
+    """Detected sparsity is bit-reproducible: with the robust rule
+    (opt-in; include/mocohip.h MH_SPARSITY_RULE_ROBUST: a probe counts as a coupling
     when its change exceeds 1e-12 of the callback's output magnitude at that
     detection point, or is NaN) the
     device's detection (mh_create, on its own kernels) and the oracle's (the
@@ -896,9 +902,11 @@ def test_sparsity_detection_agrees(name):
     its own detection).  Under the reference's rule (any nonzero change,
     CasOCFunction.cpp:44-61) the two differ exactly on rounding-level
     couplings -- changes within 64 eps of the DAE's magnitude, numerical
-    noise of couplings that cancel mathematically -- which is why that rule
-    is implementation-dependent and not the default."""
+    noise of couplings that cancel mathematically -- that rule (the
+    default, the reference's) is implementation-dependent, and it only adds
+    couplings to the robust pattern."""
     st = CASES[name]()
+    st.solver.optim_sparsity_detection_rule = "robust"
     rep = st.problem.create_rep()
     gpu = HipNLP(rep, st.solver.options())
     ref = OracleNLP(rep, st.solver.options())
