@@ -1,0 +1,743 @@
+// kkt.hip — the host optimizer's Newton-system linear algebra on the device
+// (include/mocohip.h mh_kkt_*), next to the Jacobian it factors.
+//
+// Ipopt (MocoCasADiSolver -> Ipopt 3.12.8) factors each Newton system with
+// MUMPS on the host.  The interior-point restatement here (mocohip/ipm.py)
+// solves through the Schur complement S = R J W J^T R + diag(dc) of the
+// bound-multiplier-eliminated system.  A collocation Jacobian's rows are
+// contiguous per mesh interval and read only their interval's grid points
+// (CasOCTranscription.h:219-313), so with the host's symbolic block map
+// (mocohip/kkt.py block_map: one block per interval, a head block for the
+// endpoint rows, a tail block for the final point's rows, dense columns t0 /
+// tf kept out) S is block tridiagonal:
+//
+//   D_b = A_b W_b A_b^T + diag(dc_b),  E_b = A_{b+1}[:, shared] W A_b[:, shared]^T
+//
+// with A_b the block's rows over its local columns (a small dense matrix).
+// Everything below is batched over blocks, one workgroup (or a few) per
+// block, FP64:
+//   k_kkt_gather   J's values (the context's own eval_jac_g kernels wrote
+//                  them into this module's buffer) -> A_b, row-scaled, and
+//                  the dense columns Jd;
+//   k_kkt_gemm     C = alpha P diag(w) Q^T + beta C over strided operands,
+//                  64 x 64 output tiles staged through LDS: forms D_b and E_b
+//                  and every update of the cyclic reduction;
+//   k_kkt_potrf    in-place Cholesky of one block per workgroup (in LDS when
+//                  it fits: r <= 143);
+//   k_kkt_trsm     L^-1 B / L^-T B, one column per lane;
+// and block cyclic reduction over them: at level l the active blocks are
+// every 2^l-th, the odd ones are eliminated in parallel (L_i L_i^T = D_i,
+// U_i = L_i^-1 S[i, left], V_i = L_i^-1 S[i, right]) and the even ones
+// updated (D_j -= V^T V + U^T U, new coupling -V^T U): ceil(log2 blocks)
+// levels of a handful of launches each instead of a sequential banded
+// factorization.  tests/_kkt_ref.py restates the same algorithm in numpy.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/mocohip_kkt.h"
+
+// the context interface of mocohip.hip this module uses
+struct mh_ctx;
+int mh_internal_error(int code, const char* msg);
+hipStream_t mh_internal_stream(const mh_ctx* c);
+int mh_internal_device(const mh_ctx* c);
+int mh_internal_shape(const mh_ctx* c, int64_t* n, int64_t* m, int64_t* nnz, int* unsharded);
+int mh_internal_jac_device(mh_ctx* c, const double* x_dev, double* v_dev);
+
+#define KCHK(expr)                                                                       \
+    do {                                                                                 \
+        hipError_t e_ = (expr);                                                          \
+        if (e_ != hipSuccess)                                                            \
+            return mh_internal_error(MH_ERR_HIP, (std::string(#expr " failed: ") +       \
+                                                  hipGetErrorString(e_)).c_str());       \
+    } while (0)
+
+namespace {
+
+constexpr int KMAX = 32;              // right-hand sides per solve pass
+constexpr int LDS_MAX = 160 * 1024;   // gfx950 LDS per workgroup
+
+struct KTask { const double* P; const double* Q; const double* w; double* C; };
+struct KTri { const double* L; const double* B; double* X; };
+
+// ------------------------------------------------------------------------
+// kernels
+// ------------------------------------------------------------------------
+__global__ void k_kkt_gather(int64_t na, int c, const int32_t* __restrict__ src, const int32_t* __restrict__ rowmap,
+                             const double* __restrict__ vals, const double* __restrict__ rs,
+                             double* __restrict__ A) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= na) return;
+    const int s = src[e];
+    double v = 0.0;
+    if (s >= 0) {
+        const int row = rowmap[e / c];
+        v = vals[s] * rs[row];
+    }
+    A[e] = v;
+}
+
+__global__ void k_kkt_gather_dense(int64_t nj, int nd, const int32_t* __restrict__ src,
+                                   const double* __restrict__ vals, const double* __restrict__ rs,
+                                   double* __restrict__ Jd) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= nj) return;
+    const int s = src[e];
+    Jd[e] = s >= 0 ? vals[s] * rs[e / nd] : 0.0;
+}
+
+// local weights wl[b][j] = w[colmap] (0 on padding), local diagonal shifts
+// dcl[b][i] = dc[rowmap] (1 on padding rows: S stays positive definite and
+// their unknowns stay 0)
+__global__ void k_kkt_local(int nbc, int nbr, const int32_t* __restrict__ colmap, const int32_t* __restrict__ rowmap,
+                            const double* __restrict__ w, const double* __restrict__ dc,
+                            double* __restrict__ wl, double* __restrict__ dcl) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < nbc) {
+        const int j = colmap[e];
+        wl[e] = j >= 0 ? w[j] : 0.0;
+    }
+    if (e < nbr) {
+        const int i = rowmap[e];
+        dcl[e] = i >= 0 ? dc[i] : 1.0;
+    }
+}
+
+__global__ void k_kkt_add_diag(int r, const double* __restrict__ dcl, double* __restrict__ D) {
+    const int b = blockIdx.x;
+    for (int i = threadIdx.x; i < r; i += blockDim.x) D[((int64_t)b * r + i) * r + i] += dcl[(int64_t)b * r + i];
+}
+
+// C = alpha * P diag(w) Q^T + beta * C for one task per blockIdx.z, one 64 x
+// 64 output tile per workgroup; P(i, k) = P[i psi + k psk], Q(j, k) =
+// Q[j qsi + k qsk], C(i, j) = C[i ldc + j].  Thread (ty, tx) owns rows ty +
+// 16 a and columns tx + 16 b (a, b < 4): conflict-free LDS reads.  Each
+// output is one thread's fixed-order sum: deterministic.
+__global__ __launch_bounds__(256) void k_kkt_gemm(const KTask* __restrict__ tasks, int M, int N, int K,
+                                                  int psi, int psk, int qsi, int qsk, int ldc,
+                                                  double alpha, double beta) {
+    constexpr int TM = 64, TN = 64, TK = 16;
+    __shared__ double Ps[TK][TM + 1];
+    __shared__ double Qs[TK][TN + 1];
+    const KTask t = tasks[blockIdx.z];
+    const int i0 = blockIdx.y * TM, j0 = blockIdx.x * TN;
+    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+    double acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = 0.0;
+    for (int k0 = 0; k0 < K; k0 += TK) {
+        for (int e = tid; e < TM * TK; e += 256) {
+            int ii, kk;
+            if (psk == 1) { ii = e / TK; kk = e % TK; } else { kk = e / TM; ii = e % TM; }
+            const int gi = i0 + ii, gk = k0 + kk;
+            double v = 0.0;
+            if (gi < M && gk < K) {
+                v = t.P[(int64_t)gi * psi + (int64_t)gk * psk];
+                if (t.w) v *= t.w[gk];
+            }
+            Ps[kk][ii] = v;
+        }
+        for (int e = tid; e < TN * TK; e += 256) {
+            int jj, kk;
+            if (qsk == 1) { jj = e / TK; kk = e % TK; } else { kk = e / TN; jj = e % TN; }
+            const int gj = j0 + jj, gk = k0 + kk;
+            Qs[kk][jj] = (gj < N && gk < K) ? t.Q[(int64_t)gj * qsi + (int64_t)gk * qsk] : 0.0;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int kk = 0; kk < TK; ++kk) {
+            double p[4], q[4];
+#pragma unroll
+            for (int a = 0; a < 4; ++a) p[a] = Ps[kk][ty + 16 * a];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) q[b] = Qs[kk][tx + 16 * b];
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int b = 0; b < 4; ++b) acc[a][b] = fma(p[a], q[b], acc[a][b]);
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+        const int gi = i0 + ty + 16 * a;
+        if (gi >= M) continue;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int gj = j0 + tx + 16 * b;
+            if (gj >= N) continue;
+            double* cp = t.C + (int64_t)gi * ldc + gj;
+            *cp = beta == 0.0 ? alpha * acc[a][b] : alpha * acc[a][b] + beta * *cp;
+        }
+    }
+}
+
+// In-place lower Cholesky of one r x r block per workgroup (right-looking:
+// pivot, column scale, trailing update, one barrier each), in dynamic LDS
+// when use_lds.  A non-positive or non-finite pivot sets *status (the caller
+// regularizes and refactors, as Ipopt does on a wrong inertia).
+__global__ __launch_bounds__(256) void k_kkt_potrf(double* const* __restrict__ mats, int r, int use_lds,
+                                                   int* __restrict__ status) {
+    extern __shared__ double lds[];
+    __shared__ int bad;
+    double* a = mats[blockIdx.x];
+    double* s = use_lds ? lds : a;
+    const int tid = threadIdx.x, nt = blockDim.x;
+    if (use_lds)
+        for (int e = tid; e < r * r; e += nt) s[e] = a[e];
+    if (tid == 0) bad = 0;
+    for (int j = 0; j < r; ++j) {
+        __syncthreads();
+        if (tid == 0) {
+            double d = s[j * r + j];
+            if (!(d > 0.0) || !isfinite(d)) {
+                bad = 1;
+                d = 1.0;
+            }
+            s[j * r + j] = sqrt(d);
+        }
+        __syncthreads();
+        const double djj = s[j * r + j];
+        for (int i = j + 1 + tid; i < r; i += nt) s[i * r + j] /= djj;
+        __syncthreads();
+        const int m = r - j - 1;
+        for (int e = tid; e < m * m; e += nt) {
+            const int i = j + 1 + e / m, k = j + 1 + e % m;
+            if (k <= i) s[i * r + k] -= s[i * r + j] * s[k * r + j];
+        }
+    }
+    __syncthreads();
+    if (use_lds)
+        for (int e = tid; e < r * r; e += nt) a[e] = s[e];
+    if (tid == 0 && bad) *status = 1;
+}
+
+// X = L^-1 B (trans = 0) or L^-T B (trans = 1), one column of B per lane,
+// B(i, j) = B[i bsi + j bsj], X(i, j) = X[i ldx + j] (in place when B == X
+// with the same strides); L staged in dynamic LDS when use_lds.
+__global__ __launch_bounds__(64) void k_kkt_trsm(const KTri* __restrict__ tasks, int r, int ncols, int bsi, int bsj,
+                                                 int ldx, int trans, int use_lds) {
+    extern __shared__ double Ls[];
+    const KTri t = tasks[blockIdx.y];
+    const double* L = t.L;
+    if (use_lds) {
+        for (int e = threadIdx.x; e < r * r; e += blockDim.x) Ls[e] = t.L[e];
+        __syncthreads();
+        L = Ls;
+    }
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= ncols) return;
+    double* x = t.X + j;
+    const double* B = t.B + (int64_t)j * bsj;
+    if (!trans) {
+        for (int i = 0; i < r; ++i) {
+            double s = B[(int64_t)i * bsi];
+            const double* Li = L + (int64_t)i * r;
+            for (int k = 0; k < i; ++k) s -= Li[k] * x[(int64_t)k * ldx];
+            x[(int64_t)i * ldx] = s / Li[i];
+        }
+    } else {
+        for (int i = r - 1; i >= 0; --i) {
+            double s = B[(int64_t)i * bsi];
+            for (int k = i + 1; k < r; ++k) s -= L[(int64_t)k * r + i] * x[(int64_t)k * ldx];
+            x[(int64_t)i * ldx] = s / L[(int64_t)i * r + i];
+        }
+    }
+}
+
+// [m, kc] (row-major) -> X [nb][r][KMAX] (padding rows 0), and back
+__global__ void k_kkt_to_blocks(int64_t nbr, int kc, const int32_t* __restrict__ rowmap,
+                                const double* __restrict__ b, double* __restrict__ X) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= nbr * kc) return;
+    const int64_t bi = e / kc;
+    const int k = (int)(e % kc);
+    const int row = rowmap[bi];
+    X[bi * KMAX + k] = row >= 0 ? b[(int64_t)row * kc + k] : 0.0;
+}
+__global__ void k_kkt_from_blocks(int64_t nbr, int kc, const int32_t* __restrict__ rowmap,
+                                  const double* __restrict__ X, double* __restrict__ b) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= nbr * kc) return;
+    const int64_t bi = e / kc;
+    const int k = (int)(e % kc);
+    const int row = rowmap[bi];
+    if (row >= 0) b[(int64_t)row * kc + k] = X[bi * KMAX + k];
+}
+
+// y = R J v: per block y_b = A_b v_loc, plus the dense columns
+__global__ __launch_bounds__(256) void k_kkt_jmul(int r, int c, int nd, int kc, const double* __restrict__ A,
+                                                  const int32_t* __restrict__ rowmap,
+                                                  const int32_t* __restrict__ colmap,
+                                                  const double* __restrict__ Jd,
+                                                  const int32_t* __restrict__ dcols,
+                                                  const double* __restrict__ v, double* __restrict__ y) {
+    const int b = blockIdx.x;
+    for (int e = threadIdx.x; e < r * kc; e += blockDim.x) {
+        const int i = e / kc, k = e % kc;
+        const int row = rowmap[(int64_t)b * r + i];
+        if (row < 0) continue;
+        const double* Ai = A + ((int64_t)b * r + i) * c;
+        const int32_t* cm = colmap + (int64_t)b * c;
+        double s = 0.0;
+        for (int j = 0; j < c; ++j) {
+            const int col = cm[j];
+            if (col >= 0) s += Ai[j] * v[(int64_t)col * kc + k];
+        }
+        for (int d = 0; d < nd; ++d) s += Jd[(int64_t)row * nd + d] * v[(int64_t)dcols[d] * kc + k];
+        y[(int64_t)row * kc + k] = s;
+    }
+}
+
+// z_b = A_b^T y_b (local columns), then per global column the (up to two)
+// block contributions in block order, and the dense columns' reductions
+__global__ __launch_bounds__(256) void k_kkt_jtmul_blocks(int r, int c, int kc, const double* __restrict__ A,
+                                                          const int32_t* __restrict__ rowmap,
+                                                          const double* __restrict__ y, double* __restrict__ z) {
+    const int b = blockIdx.x;
+    for (int e = threadIdx.x; e < c * kc; e += blockDim.x) {
+        const int j = e / kc, k = e % kc;
+        double s = 0.0;
+        for (int i = 0; i < r; ++i) {
+            const int row = rowmap[(int64_t)b * r + i];
+            if (row >= 0) s += A[((int64_t)b * r + i) * c + j] * y[(int64_t)row * kc + k];
+        }
+        z[((int64_t)b * c + j) * kc + k] = s;
+    }
+}
+__global__ void k_kkt_jtmul_collect(int64_t n, int kc, const int32_t* __restrict__ col2,
+                                    const double* __restrict__ z, double* __restrict__ out) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n * kc) return;
+    const int64_t j = e / kc;
+    const int k = (int)(e % kc);
+    const int p0 = col2[2 * j], p1 = col2[2 * j + 1];
+    double s = 0.0;
+    if (p0 >= 0) s += z[(int64_t)p0 * kc + k];
+    if (p1 >= 0) s += z[(int64_t)p1 * kc + k];
+    out[e] = s;
+}
+__global__ __launch_bounds__(256) void k_kkt_jtmul_dense(int64_t m, int nd, int kc, const double* __restrict__ Jd,
+                                                         const int32_t* __restrict__ dcols,
+                                                         const double* __restrict__ y, double* __restrict__ out) {
+    __shared__ double red[256];
+    const int d = blockIdx.x, k = blockIdx.y;
+    double s = 0.0;
+    for (int64_t i = threadIdx.x; i < m; i += blockDim.x) s += Jd[i * nd + d] * y[i * kc + k];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int h = 128; h > 0; h >>= 1) {
+        if ((int)threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[(int64_t)dcols[d] * kc + k] = red[0];
+}
+
+inline unsigned nblk(int64_t n, int t) { return (unsigned)((n + t - 1) / t); }
+
+}  // namespace
+
+// ------------------------------------------------------------------------
+// the module object
+// ------------------------------------------------------------------------
+struct KLevel {
+    // factor
+    KTask* gemm_vv = nullptr;  int n_vv = 0;   // D[right] -= V^T V
+    KTask* gemm_uu = nullptr;  int n_uu = 0;   // D[left]  -= U^T U
+    KTask* gemm_e = nullptr;   int n_e = 0;    // E[left]   = -V^T U
+    double** potrf = nullptr;  int n_odd = 0;
+    KTri* tri_u = nullptr;     int n_u = 0;    // U = L^-1 E[left] (every odd block but the last level's)
+    KTri* tri_v = nullptr;     int n_v = 0;    // V = L^-1 E[i]^T
+    // solve
+    KTri* sol = nullptr;                       // X_i in place
+    KTask* fwd_v = nullptr;                    // X[right] -= V^T X_i   (n_v)
+    KTask* fwd_u = nullptr;                    // X[left]  -= U^T X_i   (n_u)
+    KTask* bwd_u = nullptr;                    // X_i -= U X[left]      (n_u)
+    KTask* bwd_v = nullptr;                    // X_i -= V X[right]     (n_v)
+};
+
+struct mh_kkt {
+    mh_ctx* ctx = nullptr;
+    int device = 0;
+    int nb = 0, r = 0, c = 0, nd = 0, P = 0;
+    int64_t m = 0, n = 0, nnz = 0;
+    std::vector<int32_t> lshare, rshare;
+    // device
+    int32_t *a_src = nullptr, *rowmap = nullptr, *colmap = nullptr, *d_src = nullptr, *col2 = nullptr,
+            *dcols = nullptr;
+    double *vals = nullptr, *A = nullptr, *Jd = nullptr, *rs = nullptr, *w = nullptr, *dc = nullptr,
+           *wl = nullptr, *dcl = nullptr, *D = nullptr, *E = nullptr, *U = nullptr, *V = nullptr,
+           *x = nullptr, *X = nullptr, *bm = nullptr, *bn = nullptr, *z = nullptr;
+    int* status = nullptr;
+    KTask *t_schur = nullptr, *t_e = nullptr;
+    std::vector<KLevel> levels;      // the last level holds the single remaining block
+    std::vector<void*> allocs;
+    bool factored = false;
+};
+
+template <typename T>
+static int kalloc(mh_kkt* h, T** p, size_t count) {
+    void* q = nullptr;
+    KCHK(hipMalloc(&q, std::max<size_t>(count, 1) * sizeof(T)));
+    h->allocs.push_back(q);
+    *p = (T*)q;
+    return MH_OK;
+}
+template <typename T>
+static int kupload(mh_kkt* h, T** p, const std::vector<T>& v) {
+    int rc = kalloc(h, p, v.size());
+    if (rc) return rc;
+    if (!v.empty()) KCHK(hipMemcpy(*p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    return MH_OK;
+}
+template <typename T>
+static int kupload(mh_kkt* h, T** p, const T* src, size_t count) {
+    int rc = kalloc(h, p, count);
+    if (rc) return rc;
+    if (count) KCHK(hipMemcpy(*p, src, count * sizeof(T), hipMemcpyHostToDevice));
+    return MH_OK;
+}
+
+extern "C" void mh_kkt_destroy(mh_kkt* h) {
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    for (void* p : h->allocs) (void)hipFree(p);
+    delete h;
+}
+
+static int build_levels(mh_kkt* h) {
+    const int r = h->r;
+    const size_t rr = (size_t)r * r;
+    std::vector<int> active(h->nb);
+    for (int i = 0; i < h->nb; ++i) active[i] = i;
+    auto Dp = [&](int i) { return h->D + rr * i; };
+    auto Ep = [&](int i) { return h->E + rr * i; };
+    auto Up = [&](int i) { return h->U + rr * i; };
+    auto Vp = [&](int i) { return h->V + rr * i; };
+    auto Xp = [&](int i) { return h->X + (size_t)r * KMAX * i; };
+    while (true) {
+        KLevel L;
+        std::vector<double*> potrf;
+        std::vector<KTri> tu, tv, sol;
+        std::vector<KTask> vv, uu, ee, fv, fu, bu, bv;
+        if (active.size() == 1) {
+            const int i = active[0];
+            potrf.push_back(Dp(i));
+            sol.push_back({Dp(i), Xp(i), Xp(i)});
+        } else {
+            for (size_t k = 1; k < active.size(); k += 2) {
+                const int i = active[k], left = active[k - 1];
+                const int right = k + 1 < active.size() ? active[k + 1] : -1;
+                potrf.push_back(Dp(i));
+                sol.push_back({Dp(i), Xp(i), Xp(i)});
+                tu.push_back({Dp(i), Ep(left), Up(i)});
+                uu.push_back({Up(i), Up(i), nullptr, Dp(left)});
+                fu.push_back({Up(i), Xp(i), nullptr, Xp(left)});
+                bu.push_back({Up(i), Xp(left), nullptr, Xp(i)});
+                if (right >= 0) {
+                    tv.push_back({Dp(i), Ep(i), Vp(i)});
+                    vv.push_back({Vp(i), Vp(i), nullptr, Dp(right)});
+                    ee.push_back({Vp(i), Up(i), nullptr, Ep(left)});
+                    fv.push_back({Vp(i), Xp(i), nullptr, Xp(right)});
+                    bv.push_back({Vp(i), Xp(right), nullptr, Xp(i)});
+                }
+            }
+        }
+        int rc = 0;
+        L.n_odd = (int)potrf.size();
+        L.n_u = (int)tu.size();
+        L.n_v = (int)tv.size();
+        L.n_vv = (int)vv.size();
+        L.n_uu = (int)uu.size();
+        L.n_e = (int)ee.size();
+        if ((rc = kupload(h, &L.potrf, potrf)) || (rc = kupload(h, &L.sol, sol)) ||
+            (rc = kupload(h, &L.tri_u, tu)) || (rc = kupload(h, &L.tri_v, tv)) ||
+            (rc = kupload(h, &L.gemm_vv, vv)) || (rc = kupload(h, &L.gemm_uu, uu)) ||
+            (rc = kupload(h, &L.gemm_e, ee)) || (rc = kupload(h, &L.fwd_v, fv)) ||
+            (rc = kupload(h, &L.fwd_u, fu)) || (rc = kupload(h, &L.bwd_u, bu)) || (rc = kupload(h, &L.bwd_v, bv)))
+            return rc;
+        h->levels.push_back(L);
+        if (active.size() == 1) break;
+        std::vector<int> next;
+        for (size_t k = 0; k < active.size(); k += 2) next.push_back(active[k]);
+        active.swap(next);
+    }
+    return MH_OK;
+}
+
+extern "C" int mh_kkt_create(mh_ctx* ctx, const mh_kkt_layout* L, mh_kkt** out) {
+    if (!ctx || !L || !out) return mh_internal_error(MH_ERR_INVALID, "null argument");
+    *out = nullptr;
+    int64_t n = 0, m = 0, nnz = 0;
+    int unsharded = 0;
+    int rc = mh_internal_shape(ctx, &n, &m, &nnz, &unsharded);
+    if (rc) return rc;
+    if (!unsharded) return mh_internal_error(MH_ERR_UNSUPPORTED, "mh_kkt needs an unsharded context");
+    if (L->n != n || L->m != m || L->nnz != nnz)
+        return mh_internal_error(MH_ERR_INVALID, "mh_kkt_layout does not match the context (n, m, nnz)");
+    if (L->nblocks < 1 || L->r < 1 || L->c < 1 || L->nd < 0 || L->nshare < 0 || L->nshare > L->c || !L->a_src ||
+            !L->rowmap || !L->colmap || !L->lshare || !L->rshare || !L->col2 || (L->nd > 0 && (!L->dcols || !L->d_src)))
+        return mh_internal_error(MH_ERR_INVALID, "bad mh_kkt_layout");
+    // host-side checks of every index the kernels follow
+    const int64_t na = (int64_t)L->nblocks * L->r * L->c;
+    for (int64_t e = 0; e < na; ++e)
+        if (L->a_src[e] < -1 || L->a_src[e] >= nnz) return mh_internal_error(MH_ERR_INVALID, "a_src out of range");
+    for (int64_t e = 0; e < (int64_t)L->nblocks * L->r; ++e)
+        if (L->rowmap[e] < -1 || L->rowmap[e] >= m) return mh_internal_error(MH_ERR_INVALID, "rowmap out of range");
+    for (int64_t e = 0; e < (int64_t)L->nblocks * L->c; ++e)
+        if (L->colmap[e] < -1 || L->colmap[e] >= n) return mh_internal_error(MH_ERR_INVALID, "colmap out of range");
+    for (int64_t e = 0; e < 2 * n; ++e)
+        if (L->col2[e] < -1 || L->col2[e] >= L->nblocks * L->c)
+            return mh_internal_error(MH_ERR_INVALID, "col2 out of range");
+    for (int b = 0; b < L->nblocks; ++b)
+        if (L->lshare[b] < 0 || L->rshare[b] < 0 || L->lshare[b] + L->nshare > L->c || L->rshare[b] + L->nshare > L->c)
+            return mh_internal_error(MH_ERR_INVALID, "shared column range out of the block");
+    for (int d = 0; d < L->nd; ++d)
+        if (L->dcols[d] < 0 || L->dcols[d] >= n) return mh_internal_error(MH_ERR_INVALID, "dcols out of range");
+    for (int64_t e = 0; e < m * L->nd; ++e)
+        if (L->d_src[e] < -1 || L->d_src[e] >= nnz) return mh_internal_error(MH_ERR_INVALID, "d_src out of range");
+    auto* h = new mh_kkt;
+    h->ctx = ctx;
+    h->device = mh_internal_device(ctx);
+    h->nb = L->nblocks; h->r = L->r; h->c = L->c; h->nd = L->nd; h->P = L->nshare;
+    h->m = m; h->n = n; h->nnz = nnz;
+    h->lshare.assign(L->lshare, L->lshare + h->nb);
+    h->rshare.assign(L->rshare, L->rshare + h->nb);
+    auto fail = [&](int code) { mh_kkt_destroy(h); return code; };
+    if (hipSetDevice(h->device) != hipSuccess) return fail(mh_internal_error(MH_ERR_HIP, "hipSetDevice failed"));
+    const size_t rr = (size_t)h->r * h->r;
+    if ((rc = kupload(h, &h->a_src, L->a_src, (size_t)na)) ||
+        (rc = kupload(h, &h->rowmap, L->rowmap, (size_t)h->nb * h->r)) ||
+        (rc = kupload(h, &h->colmap, L->colmap, (size_t)h->nb * h->c)) ||
+        (rc = kupload(h, &h->col2, L->col2, (size_t)2 * n)) ||
+        (rc = kupload(h, &h->dcols, L->dcols, (size_t)h->nd)) ||
+        (rc = kupload(h, &h->d_src, L->d_src, (size_t)(m * h->nd))) ||
+        (rc = kalloc(h, &h->vals, (size_t)nnz)) || (rc = kalloc(h, &h->A, (size_t)na)) ||
+        (rc = kalloc(h, &h->Jd, (size_t)(m * h->nd))) || (rc = kalloc(h, &h->rs, (size_t)m)) ||
+        (rc = kalloc(h, &h->w, (size_t)n)) || (rc = kalloc(h, &h->dc, (size_t)m)) ||
+        (rc = kalloc(h, &h->wl, (size_t)h->nb * h->c)) || (rc = kalloc(h, &h->dcl, (size_t)h->nb * h->r)) ||
+        (rc = kalloc(h, &h->D, rr * h->nb)) || (rc = kalloc(h, &h->E, rr * h->nb)) ||
+        (rc = kalloc(h, &h->U, rr * h->nb)) || (rc = kalloc(h, &h->V, rr * h->nb)) ||
+        (rc = kalloc(h, &h->x, (size_t)n)) || (rc = kalloc(h, &h->X, (size_t)h->nb * h->r * KMAX)) ||
+        (rc = kalloc(h, &h->bm, (size_t)m * KMAX)) || (rc = kalloc(h, &h->bn, (size_t)n * KMAX)) ||
+        (rc = kalloc(h, &h->z, (size_t)h->nb * h->c * KMAX)) || (rc = kalloc(h, &h->status, 1)))
+        return fail(rc);
+    std::vector<double> ones((size_t)m, 1.0);
+    if (hipMemcpy(h->rs, ones.data(), sizeof(double) * m, hipMemcpyHostToDevice) != hipSuccess)
+        return fail(mh_internal_error(MH_ERR_HIP, "upload failed"));
+    std::vector<KTask> ts, te;
+    for (int b = 0; b < h->nb; ++b) ts.push_back({h->A + (size_t)b * h->r * h->c, h->A + (size_t)b * h->r * h->c,
+                                                 h->wl + (size_t)b * h->c, h->D + rr * b});
+    for (int b = 0; b + 1 < h->nb; ++b)
+        te.push_back({h->A + (size_t)(b + 1) * h->r * h->c + h->lshare[b + 1],
+                      h->A + (size_t)b * h->r * h->c + h->rshare[b], h->wl + (size_t)b * h->c + h->rshare[b],
+                      h->E + rr * b});
+    if ((rc = kupload(h, &h->t_schur, ts)) || (rc = kupload(h, &h->t_e, te)) || (rc = build_levels(h)))
+        return fail(rc);
+    *out = h;
+    return MH_OK;
+}
+
+extern "C" int mh_kkt_set_row_scale(mh_kkt* h, const double* rs) {
+    if (!h || !rs) return mh_internal_error(MH_ERR_INVALID, "null argument");
+    KCHK(hipSetDevice(h->device));
+    hipStream_t s = mh_internal_stream(h->ctx);
+    KCHK(hipMemcpyAsync(h->rs, rs, sizeof(double) * h->m, hipMemcpyHostToDevice, s));
+    KCHK(hipStreamSynchronize(s));
+    return MH_OK;
+}
+
+static int gather(mh_kkt* h, hipStream_t s) {
+    const int64_t na = (int64_t)h->nb * h->r * h->c;
+    hipLaunchKernelGGL(k_kkt_gather, dim3(nblk(na, 256)), dim3(256), 0, s, na, h->c, h->a_src, h->rowmap, h->vals,
+                       h->rs, h->A);
+    if (h->nd) {
+        const int64_t nj = h->m * h->nd;
+        hipLaunchKernelGGL(k_kkt_gather_dense, dim3(nblk(nj, 256)), dim3(256), 0, s, nj, h->nd, h->d_src, h->vals,
+                           h->rs, h->Jd);
+    }
+    KCHK(hipGetLastError());
+    return MH_OK;
+}
+
+extern "C" int mh_kkt_eval_jacobian(mh_kkt* h, const double* x) {
+    if (!h || !x) return mh_internal_error(MH_ERR_INVALID, "null argument");
+    KCHK(hipSetDevice(h->device));
+    hipStream_t s = mh_internal_stream(h->ctx);
+    KCHK(hipMemcpyAsync(h->x, x, sizeof(double) * h->n, hipMemcpyHostToDevice, s));
+    int rc = mh_internal_jac_device(h->ctx, h->x, h->vals);
+    if (rc) return rc;
+    if ((rc = gather(h, s))) return rc;
+    h->factored = false;
+    KCHK(hipStreamSynchronize(s));
+    return MH_OK;
+}
+
+extern "C" int mh_kkt_get_values(mh_kkt* h, double* v) {
+    if (!h || !v) return mh_internal_error(MH_ERR_INVALID, "null argument");
+    KCHK(hipSetDevice(h->device));
+    hipStream_t s = mh_internal_stream(h->ctx);
+    KCHK(hipMemcpyAsync(v, h->vals, sizeof(double) * h->nnz, hipMemcpyDeviceToHost, s));
+    KCHK(hipStreamSynchronize(s));
+    return MH_OK;
+}
+
+extern "C" int mh_kkt_get_dense(mh_kkt* h, double* Jd) {
+    if (!h || !Jd) return mh_internal_error(MH_ERR_INVALID, "null argument");
+    if (!h->nd) return MH_OK;
+    KCHK(hipSetDevice(h->device));
+    hipStream_t s = mh_internal_stream(h->ctx);
+    KCHK(hipMemcpyAsync(Jd, h->Jd, sizeof(double) * h->m * h->nd, hipMemcpyDeviceToHost, s));
+    KCHK(hipStreamSynchronize(s));
+    return MH_OK;
+}
+
+static void launch_gemm(hipStream_t s, const KTask* tasks, int ntasks, int M, int N, int K, int psi, int psk,
+                        int qsi, int qsk, int ldc, double alpha, double beta) {
+    if (ntasks <= 0) return;
+    hipLaunchKernelGGL(k_kkt_gemm, dim3(nblk(N, 64), nblk(M, 64), (unsigned)ntasks), dim3(256), 0, s, tasks, M, N,
+                       K, psi, psk, qsi, qsk, ldc, alpha, beta);
+}
+
+static void launch_trsm(hipStream_t s, const KTri* tasks, int ntasks, int r, int ncols, int bsi, int bsj, int ldx,
+                        int trans) {
+    if (ntasks <= 0) return;
+    const size_t lds = sizeof(double) * r * r;
+    const int use = lds + 64 <= (size_t)LDS_MAX ? 1 : 0;
+    hipLaunchKernelGGL(k_kkt_trsm, dim3(nblk(ncols, 64), (unsigned)ntasks), dim3(64), use ? lds : 0, s, tasks, r,
+                       ncols, bsi, bsj, ldx, trans, use);
+}
+
+extern "C" int mh_kkt_factor(mh_kkt* h, const double* w, const double* dc, int32_t* ok) {
+    if (!h || !w || !dc || !ok) return mh_internal_error(MH_ERR_INVALID, "null argument");
+    KCHK(hipSetDevice(h->device));
+    hipStream_t s = mh_internal_stream(h->ctx);
+    const int r = h->r;
+    KCHK(hipMemcpyAsync(h->w, w, sizeof(double) * h->n, hipMemcpyHostToDevice, s));
+    KCHK(hipMemcpyAsync(h->dc, dc, sizeof(double) * h->m, hipMemcpyHostToDevice, s));
+    KCHK(hipMemsetAsync(h->status, 0, sizeof(int), s));
+    const int nbc = h->nb * h->c, nbr = h->nb * r;
+    hipLaunchKernelGGL(k_kkt_local, dim3(nblk(std::max(nbc, nbr), 256)), dim3(256), 0, s, nbc, nbr, h->colmap,
+                       h->rowmap, h->w, h->dc, h->wl, h->dcl);
+    // D_b = A_b W_b A_b^T + diag(dc_b); E_b = A_{b+1}[:, shared] W A_b[:, shared]^T
+    launch_gemm(s, h->t_schur, h->nb, r, r, h->c, h->c, 1, h->c, 1, r, 1.0, 0.0);
+    hipLaunchKernelGGL(k_kkt_add_diag, dim3(h->nb), dim3(256), 0, s, r, h->dcl, h->D);
+    launch_gemm(s, h->t_e, h->nb - 1, r, r, h->P, h->c, 1, h->c, 1, r, 1.0, 0.0);
+    KCHK(hipGetLastError());
+    const size_t lds = sizeof(double) * r * r;
+    const int use_lds = lds + 64 <= (size_t)LDS_MAX ? 1 : 0;
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)k_kkt_potrf, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+        (void)hipFuncSetAttribute((const void*)k_kkt_trsm, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+        attr_set = true;
+    }
+    for (const KLevel& L : h->levels) {
+        hipLaunchKernelGGL(k_kkt_potrf, dim3((unsigned)L.n_odd), dim3(256), use_lds ? lds : 0, s, L.potrf, r,
+                           use_lds, h->status);
+        // U = L^-1 E[left] (row-major B), V = L^-1 E[i]^T (transposed B)
+        launch_trsm(s, L.tri_u, L.n_u, r, r, r, 1, r, 0);
+        launch_trsm(s, L.tri_v, L.n_v, r, r, 1, r, r, 0);
+        // D[right] -= V^T V, D[left] -= U^T U, E[left] = -V^T U
+        launch_gemm(s, L.gemm_vv, L.n_vv, r, r, r, 1, r, 1, r, r, -1.0, 1.0);
+        launch_gemm(s, L.gemm_uu, L.n_uu, r, r, r, 1, r, 1, r, r, -1.0, 1.0);
+        launch_gemm(s, L.gemm_e, L.n_e, r, r, r, 1, r, 1, r, r, -1.0, 0.0);
+        KCHK(hipGetLastError());
+    }
+    int st = 0;
+    KCHK(hipMemcpyAsync(&st, h->status, sizeof(int), hipMemcpyDeviceToHost, s));
+    KCHK(hipStreamSynchronize(s));
+    *ok = st ? 0 : 1;
+    h->factored = st == 0;
+    return MH_OK;
+}
+
+extern "C" int mh_kkt_solve(mh_kkt* h, int32_t k, const double* b, double* xout) {
+    if (!h || !b || !xout || k < 1) return mh_internal_error(MH_ERR_INVALID, "bad argument");
+    if (!h->factored) return mh_internal_error(MH_ERR_INVALID, "mh_kkt_solve before a successful mh_kkt_factor");
+    KCHK(hipSetDevice(h->device));
+    hipStream_t s = mh_internal_stream(h->ctx);
+    const int r = h->r;
+    const int64_t nbr = (int64_t)h->nb * r;
+    for (int k0 = 0; k0 < k; k0 += KMAX) {
+        const int kc = std::min(KMAX, k - k0);
+        // the chunk's columns, row-major [m][kc]
+        std::vector<double> in((size_t)h->m * kc);
+        for (int64_t i = 0; i < h->m; ++i)
+            std::memcpy(&in[(size_t)i * kc], b + (size_t)i * k + k0, sizeof(double) * kc);
+        KCHK(hipMemcpyAsync(h->bm, in.data(), sizeof(double) * in.size(), hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(k_kkt_to_blocks, dim3(nblk(nbr * kc, 256)), dim3(256), 0, s, nbr, kc, h->rowmap, h->bm,
+                           h->X);
+        for (size_t l = 0; l < h->levels.size(); ++l) {                 // forward
+            const KLevel& L = h->levels[l];
+            launch_trsm(s, L.sol, L.n_odd, r, kc, KMAX, 1, KMAX, 0);
+            launch_gemm(s, L.fwd_v, L.n_v, r, kc, r, 1, r, 1, KMAX, KMAX, -1.0, 1.0);
+            launch_gemm(s, L.fwd_u, L.n_u, r, kc, r, 1, r, 1, KMAX, KMAX, -1.0, 1.0);
+        }
+        for (size_t l = h->levels.size(); l-- > 0;) {                   // backward
+            const KLevel& L = h->levels[l];
+            launch_gemm(s, L.bwd_u, L.n_u, r, kc, r, r, 1, 1, KMAX, KMAX, -1.0, 1.0);
+            launch_gemm(s, L.bwd_v, L.n_v, r, kc, r, r, 1, 1, KMAX, KMAX, -1.0, 1.0);
+            launch_trsm(s, L.sol, L.n_odd, r, kc, KMAX, 1, KMAX, 1);
+        }
+        hipLaunchKernelGGL(k_kkt_from_blocks, dim3(nblk(nbr * kc, 256)), dim3(256), 0, s, nbr, kc, h->rowmap, h->X,
+                           h->bm);
+        KCHK(hipGetLastError());
+        KCHK(hipMemcpyAsync(in.data(), h->bm, sizeof(double) * in.size(), hipMemcpyDeviceToHost, s));
+        KCHK(hipStreamSynchronize(s));
+        for (int64_t i = 0; i < h->m; ++i)
+            std::memcpy(xout + (size_t)i * k + k0, &in[(size_t)i * kc], sizeof(double) * kc);
+    }
+    return MH_OK;
+}
+
+extern "C" int mh_kkt_jmul(mh_kkt* h, int32_t k, const double* v, double* y) {
+    if (!h || !v || !y || k < 1) return mh_internal_error(MH_ERR_INVALID, "bad argument");
+    KCHK(hipSetDevice(h->device));
+    hipStream_t s = mh_internal_stream(h->ctx);
+    for (int k0 = 0; k0 < k; k0 += KMAX) {
+        const int kc = std::min(KMAX, k - k0);
+        std::vector<double> in((size_t)h->n * kc), o((size_t)h->m * kc);
+        for (int64_t j = 0; j < h->n; ++j) std::memcpy(&in[(size_t)j * kc], v + (size_t)j * k + k0, sizeof(double) * kc);
+        KCHK(hipMemcpyAsync(h->bn, in.data(), sizeof(double) * in.size(), hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(k_kkt_jmul, dim3(h->nb), dim3(256), 0, s, h->r, h->c, h->nd, kc, h->A, h->rowmap,
+                           h->colmap, h->Jd, h->dcols, h->bn, h->bm);
+        KCHK(hipGetLastError());
+        KCHK(hipMemcpyAsync(o.data(), h->bm, sizeof(double) * o.size(), hipMemcpyDeviceToHost, s));
+        KCHK(hipStreamSynchronize(s));
+        for (int64_t i = 0; i < h->m; ++i) std::memcpy(y + (size_t)i * k + k0, &o[(size_t)i * kc], sizeof(double) * kc);
+    }
+    return MH_OK;
+}
+
+extern "C" int mh_kkt_jtmul(mh_kkt* h, int32_t k, const double* y, double* v) {
+    if (!h || !v || !y || k < 1) return mh_internal_error(MH_ERR_INVALID, "bad argument");
+    KCHK(hipSetDevice(h->device));
+    hipStream_t s = mh_internal_stream(h->ctx);
+    for (int k0 = 0; k0 < k; k0 += KMAX) {
+        const int kc = std::min(KMAX, k - k0);
+        std::vector<double> in((size_t)h->m * kc), o((size_t)h->n * kc);
+        for (int64_t i = 0; i < h->m; ++i) std::memcpy(&in[(size_t)i * kc], y + (size_t)i * k + k0, sizeof(double) * kc);
+        KCHK(hipMemcpyAsync(h->bm, in.data(), sizeof(double) * in.size(), hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(k_kkt_jtmul_blocks, dim3(h->nb), dim3(256), 0, s, h->r, h->c, kc, h->A, h->rowmap, h->bm,
+                           h->z);
+        hipLaunchKernelGGL(k_kkt_jtmul_collect, dim3(nblk(h->n * kc, 256)), dim3(256), 0, s, h->n, kc, h->col2, h->z,
+                           h->bn);
+        if (h->nd)
+            hipLaunchKernelGGL(k_kkt_jtmul_dense, dim3(h->nd, kc), dim3(256), 0, s, h->m, h->nd, kc, h->Jd, h->dcols,
+                               h->bm, h->bn);
+        KCHK(hipGetLastError());
+        KCHK(hipMemcpyAsync(o.data(), h->bn, sizeof(double) * o.size(), hipMemcpyDeviceToHost, s));
+        KCHK(hipStreamSynchronize(s));
+        for (int64_t j = 0; j < h->n; ++j) std::memcpy(v + (size_t)j * k + k0, &o[(size_t)j * kc], sizeof(double) * kc);
+    }
+    return MH_OK;
+}

@@ -2037,6 +2037,7 @@ extern "C" int mh_eval_g(mh_ctx* c, const double* x, int, double* g) {
 // assembly instead of following it.  Same kernels, same values.  Paths
 // without a per-interval task launch copy the whole block after the call.
 static int jac_to_host(mh_ctx* c, int kind, double* g_host, double* v_host) {
+    c->x_last = nullptr;   // every Jacobian evaluation invalidates the overlap point (run_cached's rule)
     const int nint = c->ie - c->ib;
     const int nch = std::min(c->d2h_chunks, nint);
     const size_t nnz = shard_nnz(c), rows = shard_rows(c);
@@ -2153,6 +2154,26 @@ extern "C" int mh_eval_g_jac_g_device(mh_ctx* c, const double* x_dev, double* g_
     int rc = run_cached(c, 2, x_dev, g_dev, v_dev);
     if (rc) return rc;
     return finish(c, true);
+}
+
+// ---- the context interface of the device KKT module (csrc/kkt.hip) -------
+int mh_internal_error(int code, const char* msg) { return set_err(code, "%s", msg); }
+hipStream_t mh_internal_stream(const mh_ctx* c) { return c->stream; }
+int mh_internal_device(const mh_ctx* c) { return c->device; }
+int mh_internal_shape(const mh_ctx* c, int64_t* n, int64_t* m, int64_t* nnz, int* unsharded) {
+    if (!c) return set_err(MH_ERR_INVALID, "null context");
+    *n = c->n;
+    *m = (int64_t)shard_rows(c);
+    *nnz = (int64_t)shard_nnz(c);
+    *unsharded = c->ib == 0 && c->ie == c->N;
+    return MH_OK;
+}
+// eval_jac_g at a device iterate into a device buffer, enqueued on the
+// context stream (no synchronization: the KKT module's kernels follow)
+int mh_internal_jac_device(mh_ctx* c, const double* x_dev, double* v_dev) {
+    HIPCHK(hipSetDevice(c->device));
+    (void)hipGetLastError();
+    return run_cached(c, 1, x_dev, v_dev, nullptr);
 }
 
 // ---- batches (include/mocohip.h mh_batch_*) -------------------------------

@@ -284,6 +284,21 @@ def _bind(lib, table):
 _libs: dict = {}
 
 
+# include/mocohip_kkt.h: the device KKT module (mocohip/kkt.py)
+MOCOHIP_KKT_SYMBOLS = {
+    "mh_kkt_create": (i32, [C.c_void_p, C.c_void_p, P(C.c_void_p)]),
+    "mh_kkt_destroy": (None, [C.c_void_p]),
+    "mh_kkt_set_row_scale": (i32, [C.c_void_p, P(f64)]),
+    "mh_kkt_eval_jacobian": (i32, [C.c_void_p, P(f64)]),
+    "mh_kkt_get_values": (i32, [C.c_void_p, P(f64)]),
+    "mh_kkt_get_dense": (i32, [C.c_void_p, P(f64)]),
+    "mh_kkt_factor": (i32, [C.c_void_p, P(f64), P(f64), P(i32)]),
+    "mh_kkt_solve": (i32, [C.c_void_p, i32, P(f64), P(f64)]),
+    "mh_kkt_jmul": (i32, [C.c_void_p, i32, P(f64), P(f64)]),
+    "mh_kkt_jtmul": (i32, [C.c_void_p, i32, P(f64), P(f64)]),
+}
+
+
 def load_mocohip(path: str | None = None):
     """Load the product library.  Raises if it is missing: there is no CPU
     fallback for the hot path."""
@@ -300,7 +315,7 @@ def load_mocohip(path: str | None = None):
             raise RuntimeError(
                 f"libmocohip.so not built at {path}; run "
                 "`python -c 'import __graft_entry__ as g; g.build()'`")
-        lib = _bind(C.CDLL(path), MOCOHIP_SYMBOLS)
+        lib = _bind(C.CDLL(path), {**MOCOHIP_SYMBOLS, **MOCOHIP_KKT_SYMBOLS})
         if lib.mh_abi_version() != MH_ABI_VERSION:
             raise RuntimeError(f"{path}: ABI version {lib.mh_abi_version()}, "
                                f"this binding expects {MH_ABI_VERSION}; rebuild")

@@ -311,7 +311,7 @@ def scale_subject(m: Model, length: float = 1.03, mass: float = 1.05) -> Model:
     return m
 
 
-def gait10dof18musc_track(num_mesh_intervals: int = 65) -> MocoStudy:
+def gait10dof18musc_track(num_mesh_intervals: int = 65, muscles: bool = False) -> MocoStudy:
     """The reference's MocoTrack golden-solution problem (testMocoTrack.cpp:
     46-68): gait10dof18musc | ModOpRemoveMuscles | ModOpAddReserves(100) |
     ModOpAddExternalLoads; states reference walk_gait1018_state_reference.mot
@@ -319,9 +319,15 @@ def gait10dof18musc_track(num_mesh_intervals: int = 65) -> MocoStudy:
     control effort 0.001, time [0.01, 1.3], mesh_interval 0.02 (N = 65),
     explicit dynamics, forward differences, convergence and constraint
     tolerances 1e-2, bounds guess (MocoTrack.cpp:54-132).  Its converged
-    solution is std_testMocoTrackGait10dof18musc_solution.sto."""
+    solution is std_testMocoTrackGait10dof18musc_solution.sto.
+
+    muscles=True: BASELINE configs[2], the same MocoTrack with the 18
+    muscles replaced by DeGrooteFregly2016Muscle (rigid tendons,
+    ModOpReplaceMusclesWithDeGrooteFregly2016) instead of removed -- the
+    muscle-driven workload the headline throughput is measured on, solved
+    with MocoTrack's settings."""
     from .splines import filter_lowpass_table
-    m = gait10dof18musc_model(muscles=False)
+    m = gait10dof18musc_model(muscles=muscles)
     ref = _load("walk_gait1018_state_reference.json")
     tp, cols = filter_lowpass_table(ref["time"], {k: np.asarray(v) for k, v in ref["columns"].items()}, 6.0)
     m.add_table(DataTable("state_reference", tp, cols, degree=5))

@@ -93,6 +93,12 @@ class IpmOptions:
     limited_memory_max_history: int = 6
     limited_memory_init_val: float = 1.0
     max_soc: int = 4
+    # the Newton systems' linear algebra: "host" (scipy / LAPACK over J
+    # copied to the host), "device" (include/mocohip_kkt.h: J stays in HBM,
+    # the Schur complement is factored on the GPU), "auto" (device when the
+    # NLP offers a device KKT module -- HipNLP -- and its Jacobian has the
+    # per-interval block structure, else host)
+    linear_solver: str = "auto"
     kappa_soc: float = 0.99
     # after the restoration phase (Ipopt 3.12 IpRestoMinC_1Nrm): the least-
     # squares constraint multipliers are kept only when their max-norm is at
@@ -306,6 +312,25 @@ class _Scaled:
         return float(np.max(np.concatenate([[0.0], self.gl - g, g - self.gu]))) if self.m else 0.0
 
 
+def _linear_algebra(nlp, P, opt):
+    """The Newton systems' back end (IpmOptions.linear_solver)."""
+    want = opt.linear_solver
+    if want not in ("auto", "host", "device"):
+        raise ValueError("linear_solver must be 'auto', 'host' or 'device'")
+    if want != "host" and P.m and hasattr(nlp, "device_kkt"):
+        try:
+            dk = nlp.device_kkt()
+        except (ValueError, RuntimeError):
+            if want == "device":
+                raise
+            dk = None
+        if dk is not None:
+            return _DevLA(P, dk)
+    if want == "device":
+        raise ValueError("linear_solver='device' needs an NLP with a device KKT module (HipNLP)")
+    return _HostLA(P)
+
+
 def _ftb(v, dv, lo, hi, tau):
     """Largest alpha in (0, 1] with v + alpha dv >= v - tau (v - lo) (and
     the same for the upper bounds): the fraction-to-the-boundary rule."""
@@ -327,17 +352,80 @@ def _ftb_pos(z, dz, tau):
     return max(a, 0.0)
 
 
-class _KKT:
-    """Solves with K = [[D_x + B, J^T], [J, -Dc]] (slacks eliminated).
+class _KKTBase:
+    """Solves with K = [[D_x + B, J^T], [J, -Dc]] (slacks eliminated) through
+    the Schur complement S = J D_x^-1 J^T + Dc of K0 (B = 0); the dense
+    columns (free initial / final time) are taken out of S and put back with
+    Sherman-Morrison-Woodbury, as is the limited-memory term B = -W M W^T.
+    Subclasses provide S0^-1 (_s0) and the products with J (_mv, _rmv)."""
 
-    K0 (B = 0) is solved through its Schur complement S = J D_x^-1 J^T + Dc,
-    which is banded for a transcription (rows and columns are ordered by mesh
-    interval) and is factored by SuperLU in its natural order (MMD when the
-    band is wide); the few dense columns (free initial / final time) are
-    taken out of S and put back with Sherman-Morrison-Woodbury, as is the
-    limited-memory term B = -W M W^T."""
+    def _lowrank(self, Dx, dense, Jd, lbfgs_compact):
+        self.Sd = None
+        if len(dense):
+            Zd = self._s0(Jd)
+            Td = np.diag(Dx[dense]) + Jd.T @ Zd
+            self.Sd = (Jd, Zd, np.linalg.inv(Td))
+        self.low = None
+        if lbfgs_compact is not None:
+            W, Minv = lbfgs_compact
+            P = np.zeros((self.nx + self.m, W.shape[1]))
+            P[:self.nx] = W
+            Z = self._solve0_once(P)
+            T = Minv - P.T @ Z
+            self.low = (P, Z, np.linalg.inv(T))
+
+    def _ssolve(self, t):
+        u = self._s0(t)
+        if self.Sd is not None:
+            Jd, Zd, Tinv = self.Sd
+            u = u - Zd @ (Tinv @ (Jd.T @ u))
+        return u
+
+    def _solve0_once(self, b):
+        nx = self.nx
+        rx, rc = b[:nx], b[nx:]
+        Dx = self.Dx if b.ndim == 1 else self.Dx[:, None]
+        dy = self._ssolve(self._mv(rx / Dx) - rc)
+        dx = (rx - self._rmv(dy)) / Dx
+        return np.concatenate([dx, dy]) if b.ndim == 1 else np.vstack([dx, dy])
+
+    def _K0(self, u):
+        nx = self.nx
+        ux, uy = u[:nx], u[nx:]
+        Dx = self.Dx if u.ndim == 1 else self.Dx[:, None]
+        dc = self.dc if u.ndim == 1 else self.dc[:, None]
+        top = Dx * ux + self._rmv(uy)
+        bot = self._mv(ux) - dc * uy
+        return np.concatenate([top, bot]) if u.ndim == 1 else np.vstack([top, bot])
+
+    def _solve0(self, b):
+        u = self._solve0_once(b)
+        return u + self._solve0_once(b - self._K0(u))   # one step of iterative refinement
+
+    def solve(self, rx, rs, rc):
+        """Solve [[B + D_x, 0, J_x^T], [0, D_s, -E^T], [J_x, -E, -delta_c]]
+        [dx; ds; dy] = [rx; rs; rc]; E selects the inequality rows."""
+        rc2 = rc.copy()
+        # ds = (rs + dy_in) / Ds  ->  row block: J dx - (1/Ds) dy_in - dc dy = rc + rs / Ds
+        rc2[self.Js_idx] += rs / self.Ds
+        b = np.concatenate([rx, rc2])
+        u = self._solve0(b)
+        if self.low is not None:
+            P, Z, Tinv = self.low
+            u = u + Z @ (Tinv @ (P.T @ u))
+        dx, dy = u[:self.nx], u[self.nx:]
+        ds = (rs + dy[self.Js_idx]) / self.Ds
+        return dx, ds, dy
+
+
+class _KKT(_KKTBase):
+    """Host linear algebra: S is banded for a transcription (rows and
+    columns ordered by mesh interval) and is factored by LAPACK's banded
+    Cholesky, or by SuperLU in its natural order (MMD) when the band is
+    wide."""
 
     def __init__(self, Jx, Js_idx, Dx, Ds, delta_c, lbfgs_compact, m):
+        Jx = Jx.csr if isinstance(Jx, _HostJ) else Jx
         self.nx = Jx.shape[1]
         self.m = m
         self.J = Jx
@@ -374,68 +462,141 @@ class _KKT:
         else:
             self.lu = splu(S.tocsc(), permc_spec="MMD_AT_PLUS_A", diag_pivot_thresh=0.1,
                            options={"SymmetricMode": True})
-        self.Sd = None
-        if len(dense):
-            Jd = Jx[:, dense].toarray()
-            Zd = self._s0(Jd)
-            Td = np.diag(Dx[dense]) + Jd.T @ Zd
-            self.Sd = (Jd, Zd, np.linalg.inv(Td))
-        self.low = None
-        if lbfgs_compact is not None:
-            W, Minv = lbfgs_compact
-            P = np.zeros((self.nx + m, W.shape[1]))
-            P[:self.nx] = W
-            Z = self._solve0_once(P)
-            T = Minv - P.T @ Z
-            self.low = (P, Z, np.linalg.inv(T))
+        self._lowrank(Dx, dense, Jx[:, dense].toarray() if len(dense) else None, lbfgs_compact)
+
+    def _mv(self, d):
+        return self.J @ d
+
+    def _rmv(self, y):
+        return self.JT @ y
 
     def _s0(self, t):
         if self.band is not None:
             return sla.cho_solve_banded((self.band, True), t, check_finite=False)
         return self.lu.solve(t)
 
-    def _ssolve(self, t):
-        u = self._s0(t)
-        if self.Sd is not None:
-            Jd, Zd, Tinv = self.Sd
-            u = u - Zd @ (Tinv @ (Jd.T @ u))
-        return u
 
-    def _solve0_once(self, b):
-        nx = self.nx
-        rx, rc = b[:nx], b[nx:]
-        Dx = self.Dx if b.ndim == 1 else self.Dx[:, None]
-        dy = self._ssolve(self.J @ (rx / Dx) - rc)
-        dx = (rx - self.JT @ dy) / Dx
-        return np.concatenate([dx, dy]) if b.ndim == 1 else np.vstack([dx, dy])
+class _HostJ:
+    """J_x (scaled, free columns) as a host CSR matrix."""
 
-    def _K0(self, u):
-        nx = self.nx
-        ux, uy = u[:nx], u[nx:]
-        Dx = self.Dx if u.ndim == 1 else self.Dx[:, None]
-        dc = self.dc if u.ndim == 1 else self.dc[:, None]
-        top = Dx * ux + self.JT @ uy
-        bot = self.J @ ux - dc * uy
-        return np.concatenate([top, bot]) if u.ndim == 1 else np.vstack([top, bot])
+    def __init__(self, csr):
+        self.csr = csr
+        self._t = None
 
-    def _solve0(self, b):
-        u = self._solve0_once(b)
-        return u + self._solve0_once(b - self._K0(u))   # one step of iterative refinement
+    def mv(self, d):
+        return self.csr @ d
 
-    def solve(self, rx, rs, rc):
-        """Solve [[B + D_x, 0, J_x^T], [0, D_s, -E^T], [J_x, -E, -delta_c]]
-        [dx; ds; dy] = [rx; rs; rc]; E selects the inequality rows."""
-        rc2 = rc.copy()
-        # ds = (rs + dy_in) / Ds  ->  row block: J dx - (1/Ds) dy_in - dc dy = rc + rs / Ds
-        rc2[self.Js_idx] += rs / self.Ds
-        b = np.concatenate([rx, rc2])
-        u = self._solve0(b)
-        if self.low is not None:
-            P, Z, Tinv = self.low
-            u = u + Z @ (Tinv @ (P.T @ u))
-        dx, dy = u[:self.nx], u[self.nx:]
-        ds = (rs + dy[self.Js_idx]) / self.Ds
-        return dx, ds, dy
+    def rmv(self, y):
+        if self._t is None:
+            self._t = self.csr.T.tocsr()
+        return self._t @ y
+
+
+class _HostLA:
+    """The host linear algebra: J's values copied to the host every
+    iteration, scipy / LAPACK factorizations."""
+    name = "host (scipy: banded LAPACK Cholesky / SuperLU)"
+
+    def __init__(self, P):
+        self.P = P
+
+    def jac(self, v):
+        P = self.P
+        if not P.m:
+            return _HostJ(sp.csr_matrix((0, P.nx)))
+        return _HostJ(P.Jx(P.jac_vals(v)))
+
+    def kkt(self, J, Js_idx, Dx, Ds, delta_c, lbfgs_compact, m):
+        return _KKT(J, Js_idx, Dx, Ds, delta_c, lbfgs_compact, m)
+
+
+class _DevJ:
+    """J_x (scaled, free columns) resident on the device (mocohip.kkt
+    DeviceKKT's blocks): products cross the bus as vectors."""
+
+    def __init__(self, la):
+        self.la = la
+
+    def mv(self, d):
+        P, dk = self.la.P, self.la.dk
+        full = np.zeros((P.n_full,) + d.shape[1:])
+        full[P.free] = d
+        return dk.jmul(full)[P.rows]
+
+    def rmv(self, y):
+        P, dk = self.la.P, self.la.dk
+        full = np.zeros((P.m_full,) + y.shape[1:])
+        full[P.rows] = y
+        return dk.jtmul(full)[P.free]
+
+
+class _DevLA:
+    """The device linear algebra (include/mocohip_kkt.h): J evaluated into
+    device memory by the context's own kernels and never copied back; the
+    Schur complement over the block columns formed and factored on the
+    device by block cyclic reduction (csrc/kkt.hip); the dense columns (t0,
+    tf) and the limited-memory term through Sherman-Morrison-Woodbury on the
+    host, as in the host path."""
+    name = "device (mh_kkt: block cyclic reduction of the Schur complement on the GPU)"
+
+    def __init__(self, P, dk):
+        self.P, self.dk = P, dk
+        rs = np.zeros(P.m_full)
+        rs[P.rows] = P.row_scale
+        dk.set_row_scale(rs)
+        col_map = -np.ones(P.n_full, np.int64)
+        col_map[P.free] = np.arange(P.nx)
+        d = col_map[dk.bm.dcols]
+        self.dense_nx = d[d >= 0]                 # dense free columns, in the free-column index
+        self.dense_sel = np.where(d >= 0)[0]      # their position among the dense columns
+        self.dense_free = dk.bm.dcols[d >= 0]     # their global index
+
+    def jac(self, v):
+        P = self.P
+        t = time.perf_counter()
+        self.dk.eval_jacobian(P._x(v))
+        P.eval_time += time.perf_counter() - t
+        P.counts["jac_g"] += 1
+        return _DevJ(self)
+
+    def kkt(self, J, Js_idx, Dx, Ds, delta_c, lbfgs_compact, m):
+        return _DevKKT(self, Js_idx, Dx, Ds, delta_c, lbfgs_compact, m)
+
+
+class _DevKKT(_KKTBase):
+    def __init__(self, la, Js_idx, Dx, Ds, delta_c, lbfgs_compact, m):
+        P, dk = la.P, la.dk
+        self.la, self.P, self.dk = la, P, dk
+        self.nx, self.m = P.nx, m
+        self.Js_idx, self.Ds, self.Dx = Js_idx, Ds, Dx
+        dc = np.full(m, float(delta_c))
+        dc[Js_idx] += 1.0 / Ds
+        self.dc = dc
+        w = np.zeros(P.n_full)
+        w[P.free] = 1.0 / Dx
+        w[dk.bm.dcols] = 0.0
+        dcf = np.ones(P.m_full)              # rows the method leaves out: unit pivots, zero rows of J
+        dcf[P.rows] = dc
+        if not dk.factor(w, dcf):
+            raise RuntimeError("device KKT factorization: non-positive pivot")
+        self._J = _DevJ(la)
+        Jd = None
+        if len(la.dense_nx):
+            _, Jd_all = dk.dense_columns()
+            Jd = Jd_all[P.rows][:, la.dense_sel]
+        self._lowrank(Dx, la.dense_nx, Jd, lbfgs_compact)
+
+    def _mv(self, d):
+        return self._J.mv(d)
+
+    def _rmv(self, y):
+        return self._J.rmv(y)
+
+    def _s0(self, t):
+        P = self.P
+        full = np.zeros((P.m_full,) + t.shape[1:])
+        full[P.rows] = t
+        return self.dk.solve(full)[P.rows]
 
 
 def solve_ipm(nlp, x0: np.ndarray, options: Optional[IpmOptions] = None) -> IpmResult:
@@ -500,25 +661,20 @@ def _solve_ipm(nlp, x0: np.ndarray, options: Optional[IpmOptions] = None) -> Ipm
 
     def JT(Jx, y):
         r = np.empty(nv)
-        r[:nx] = Jx.T @ y
+        r[:nx] = Jx.rmv(y)
         r[nx:] = -y[P.ineq]
         return r
 
-    def Jmul(Jx, d):
-        r = Jx @ d[:nx]
-        r[P.ineq] -= d[nx:]
-        return r
-
+    la = _linear_algebra(nlp, P, opt)
     f = P.f(v)
     c = P.C(v, graw)
     gf = P.grad_f(v)
-    vals = P.jac_vals(v) if m else np.zeros(0)
-    Jx = P.Jx(vals) if m else sp.csr_matrix((0, nx))
+    Jx = la.jac(v)
     # least-squares constraint multipliers (constr_mult_init_max)
     y = np.zeros(m)
     if m:
         try:
-            kk = _KKT(Jx, P.ineq, np.ones(nx), np.ones(ns), 0.0, None, m)
+            kk = la.kkt(Jx, P.ineq, np.ones(nx), np.ones(ns), 0.0, None, m)
             _, _, y = kk.solve(-(gf[:nx] - zl[:nx] + zu[:nx]), -(gf[nx:] - zl[nx:] + zu[nx:]), np.zeros(m))
             if not np.all(np.isfinite(y)) or np.abs(y).max(initial=0) > opt.constr_mult_init_max:
                 y = np.zeros(m)
@@ -607,7 +763,7 @@ def _solve_ipm(nlp, x0: np.ndarray, options: Optional[IpmOptions] = None) -> Ipm
         delta_c = 0.0
         for attempt in range(6):
             try:
-                kkt = _KKT(Jx, P.ineq, Dx, Ds, delta_c, comp, m)
+                kkt = la.kkt(Jx, P.ineq, Dx, Ds, delta_c, comp, m)
                 dx, ds, dy = kkt.solve(rhs_v[:nx], rhs_v[nx:], -c)
                 if np.all(np.isfinite(dx)) and np.all(np.isfinite(dy)):
                     break
@@ -702,7 +858,7 @@ def _solve_ipm(nlp, x0: np.ndarray, options: Optional[IpmOptions] = None) -> Ipm
             alpha *= 0.5
         if not accepted:
             # ---- feasibility restoration --------------------------------
-            r = _restore(P, v, c, Jx, lo, hi, hl, hu, Sig, tau, filt, theta, phi, barrier, opt, m, nx)
+            r = _restore(P, la, v, c, Jx, lo, hi, hl, hu, Sig, tau, filt, theta, phi, barrier, opt, m, nx)
             if r is None:
                 status = "Restoration_Failed"
                 break
@@ -713,8 +869,7 @@ def _solve_ipm(nlp, x0: np.ndarray, options: Optional[IpmOptions] = None) -> Ipm
             v = vt
             f, graw, c = ft, gt, ct
             gf = P.grad_f(v)
-            vals = P.jac_vals(v)
-            Jx = P.Jx(vals)
+            Jx = la.jac(v)
             if max(float(np.abs(zl).max(initial=0.0)), float(np.abs(zu).max(initial=0.0))) \
                     > opt.bound_mult_reset_threshold:
                 zl = np.where(hl, 1.0, 0.0)
@@ -722,7 +877,7 @@ def _solve_ipm(nlp, x0: np.ndarray, options: Optional[IpmOptions] = None) -> Ipm
             y = np.zeros(m)
             if opt.constr_mult_reset_threshold > 0:
                 try:
-                    kk = _KKT(Jx, P.ineq, np.ones(nx), np.ones(ns), 0.0, None, m)
+                    kk = la.kkt(Jx, P.ineq, np.ones(nx), np.ones(ns), 0.0, None, m)
                     _, _, y = kk.solve(-(gf[:nx] - zl[:nx] + zu[:nx]), -(gf[nx:] - zl[nx:] + zu[nx:]),
                                        np.zeros(m))
                     if not np.all(np.isfinite(y)) or np.abs(y).max(initial=0) > opt.constr_mult_reset_threshold:
@@ -737,9 +892,12 @@ def _solve_ipm(nlp, x0: np.ndarray, options: Optional[IpmOptions] = None) -> Ipm
             filt.append(((1 - opt.gamma_theta) * theta, phi - opt.gamma_phi * theta))
         # ---- accept -----------------------------------------------------
         x_old = v[:nx].copy()
-        gLx_old_parts = (gf[:nx].copy(), Jx)
+        gf_old = gf[:nx].copy()
         v = vt
         y = y + alpha * dy
+        # grad_x L(x, y+) with the Jacobian at x, before J moves to x+ (the
+        # device keeps one Jacobian)
+        gL_old = gf_old + Jx.rmv(y)
         zl = zl + a_z * dzl
         zu = zu + a_z * dzu
         # kappa_Sigma safeguard of the bound multipliers
@@ -750,12 +908,10 @@ def _solve_ipm(nlp, x0: np.ndarray, options: Optional[IpmOptions] = None) -> Ipm
             zu = np.where(hu, np.clip(zu, mu / (opt.kappa_sigma * du), opt.kappa_sigma * mu / du), 0.0)
         f, graw, c = ft, gt, ct
         gf = P.grad_f(v)
-        vals = P.jac_vals(v)
-        Jx = P.Jx(vals)
+        Jx = la.jac(v)
         # BFGS pair: s = dx, y = grad_x L(x+, y+) - grad_x L(x, y+)
         s_k = v[:nx] - x_old
-        gf_old, Jx_old = gLx_old_parts
-        y_k = (gf[:nx] + Jx.T @ y) - (gf_old + Jx_old.T @ y)
+        y_k = (gf[:nx] + Jx.rmv(y)) - gL_old
         lb.update(s_k, y_k)
         it += 1
 
@@ -773,10 +929,10 @@ def _solve_ipm(nlp, x0: np.ndarray, options: Optional[IpmOptions] = None) -> Ipm
     return IpmResult(x_full, success, status, f / P.obj_scale, it, dur, viol, dict(P.counts),
                      lam, z_l, z_u, history,
                      {"evaluations_s": P.eval_time, "linear_algebra_s": t_lin,
-                      "delta_c": delta_c_last})
+                      "delta_c": delta_c_last, "linear_solver": la.name})
 
 
-def _restore(P, v, c, Jx, lo, hi, hl, hu, Sig, tau, filt, theta, phi, barrier, opt, m, nx, iters=30):
+def _restore(P, la, v, c, Jx, lo, hi, hl, hu, Sig, tau, filt, theta, phi, barrier, opt, m, nx, iters=30):
     """Feasibility restoration: Gauss-Newton steps on the constraint
     violation (minimum-norm in the barrier metric), each kept inside the
     bounds by the fraction-to-the-boundary rule and backtracked until
@@ -790,7 +946,7 @@ def _restore(P, v, c, Jx, lo, hi, hl, hu, Sig, tau, filt, theta, phi, barrier, o
         Dx = Sig[:nx] + zeta
         Ds = Sig[nx:] + zeta
         try:
-            kk = _KKT(Jr, P.ineq, Dx, Ds, 1e-10, None, m)
+            kk = la.kkt(Jr, P.ineq, Dx, Ds, 1e-10, None, m)
             dx, ds, _ = kk.solve(np.zeros(nx), np.zeros(len(Ds)), -cr)
         except (RuntimeError, np.linalg.LinAlgError):
             return None
@@ -813,8 +969,7 @@ def _restore(P, v, c, Jx, lo, hi, hl, hu, Sig, tau, filt, theta, phi, barrier, o
         ph = barrier(vr, fr)
         if all(th <= tj or ph <= pj for (tj, pj) in filt2) and th <= (1 - opt.gamma_theta) * theta:
             return vr, fr, gt, cr
-        vals = P.jac_vals(vr)
-        Jr = P.Jx(vals)
+        Jr = la.jac(vr)
     return None
 
 

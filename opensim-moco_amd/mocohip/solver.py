@@ -465,6 +465,24 @@ class HipNLP(_NLPBase):
         self.lib = lib or abi.load_mocohip()
         super().__init__(rep, opts)
 
+    def device_kkt(self):
+        """The device KKT module over this context (include/mocohip_kkt.h,
+        mocohip.kkt.DeviceKKT; created once): the host optimizer's Newton
+        systems factored next to the Jacobian.  Raises ValueError when the
+        Jacobian lacks the per-interval block structure, RuntimeError on a
+        sharded context."""
+        if getattr(self, "_dkkt", None) is None:
+            from .kkt import DeviceKKT
+            self._dkkt = DeviceKKT(self)
+        return self._dkkt
+
+    def close(self):
+        k = getattr(self, "_dkkt", None)
+        if k is not None:
+            k.close()
+            self._dkkt = None
+        super().close()
+
     def eval_f(self, x, new_x=True):
         x = np.ascontiguousarray(x, float)
         f = np.zeros(1)

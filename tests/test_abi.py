@@ -13,6 +13,7 @@ from mocohip import abi
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "mocohip.h")
+KKT_HEADER = os.path.join(ROOT, "include", "mocohip_kkt.h")
 
 STRUCTS = ["mh_function", "mh_axis", "mh_body", "mh_path_point", "mh_muscle",
            "mh_actuator", "mh_table", "mh_external_force", "mh_constraint", "mh_wrap_object",
@@ -22,24 +23,25 @@ STRUCTS = ["mh_function", "mh_axis", "mh_body", "mh_path_point", "mh_muscle",
            "mh_options", "mh_nlp_info"]
 
 
-def header_functions():
-    src = open(HEADER).read()
+def header_functions(path=HEADER):
+    src = open(path).read()
     return sorted(set(re.findall(r"\b(mh_[a-z_]+)\s*\(", src)) - set(STRUCTS))
 
 
 def test_header_declares_exactly_the_bound_symbols():
     assert header_functions() == sorted(abi.MOCOHIP_SYMBOLS)
+    assert header_functions(KKT_HEADER) == sorted(abi.MOCOHIP_KKT_SYMBOLS)
 
 
 def test_library_loads_and_exports_every_symbol():
     lib = abi.load_mocohip()
-    for name in abi.MOCOHIP_SYMBOLS:
+    for name in list(abi.MOCOHIP_SYMBOLS) + list(abi.MOCOHIP_KKT_SYMBOLS):
         assert hasattr(lib, name), name
     assert lib.mh_abi_version() == abi.MH_ABI_VERSION == 6
     out = subprocess.run(["nm", "-D", "--defined-only", abi.LIBMOCOHIP_PATH],
                          capture_output=True, text=True, check=True).stdout
     exported = set(re.findall(r" T (mh_\w+)", out))
-    assert set(abi.MOCOHIP_SYMBOLS) <= exported
+    assert set(abi.MOCOHIP_SYMBOLS) | set(abi.MOCOHIP_KKT_SYMBOLS) <= exported
 
 
 @pytest.mark.parametrize("name", ["sliding_mass", "double_pendulum", "gait10dof18musc"])

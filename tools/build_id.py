@@ -16,7 +16,7 @@ CSRC = os.path.join(ROOT, "opensim-moco_amd", "csrc")
 def source_files():
     pats = ["*.hip", "*.hpp", "generated/*.hip", "generated/models_table.inc", "Makefile"]
     files = [f for p in pats for f in glob.glob(os.path.join(CSRC, p))]
-    files.append(os.path.join(ROOT, "include", "mocohip.h"))
+    files += glob.glob(os.path.join(ROOT, "include", "*.h"))
     return sorted(set(files), key=lambda f: os.path.relpath(f, ROOT))
 
 
