@@ -25,20 +25,19 @@ kernels are enqueued and the timed region ends with torch.cuda.synchronize()
                   cores, on a bounded sample of the same workload.
 
 --gpus N > 1 (one process per GPU, torch.distributed.run):
-  --multi mesh (default for N > 1): the north star's layout -- ONE NLP (the
-      headline's, so the driver's per-N values form a strong-scaling curve)
-      for one host IPOPT, its mesh intervals sharded over the ranks.  value =
-      device-resident calls/s: x resident in every rank's HBM, every rank
-      evaluates its shard into HBM (no collective); "x_broadcast": the same
-      with an RCCL broadcast of x from rank 0 per call; "host_inclusive": the
-      host IPOPT's round trip -- x from page-locked host memory, the shard's
-      evaluation, each rank's DMA of its contiguous g / Jacobian slice into its
-      offset of one page-locked host buffer shared by the node's ranks over
-      its own PCIe link (mocohip.distributed.HostGather); "scaling": "strong".
-      The replicas layout is reported beside it ("replicas").
-  --multi replicas: every rank evaluates its own NLP (independent trials,
-      the configs[4] batch layout), no collective on the data path
-      -> "scaling": "weak".
+  --multi replicas (default): every rank evaluates its own NLP (independent
+      trials, the configs[4] batch layout), no collective on the data path
+      -> "scaling": "weak"; the mesh layout's measurements ride along under
+      "mesh" (below).
+  --multi mesh: the north star's layout -- ONE NLP for one host IPOPT, its
+      mesh intervals sharded over the ranks; value = the host-inclusive rate:
+      x from page-locked host memory over each rank's PCIe link, the shard's
+      evaluation, each rank's DMA of its contiguous g / Jacobian slice into
+      its offset of one page-locked host buffer shared by the node's ranks
+      (mocohip.distributed.HostGather), a barrier; "scaling": "strong".
+      Beside it, labelled: "device_resident" (x already in HBM, results left
+      there -- an upper bound with no data movement) and "x_broadcast" (+ an
+      RCCL broadcast of x per call).
 
 Prints one JSON line on rank 0.
 """
@@ -469,6 +468,14 @@ def solve_lines():
                 round(g.compare_continuous_variables_rms(m, controls=["none"]), 5))
     out = {}
     problems = (
+        # BASELINE configs[2] itself: the muscle-driven MocoTrack the headline
+        # throughput is quoted on, solved with MocoTrack's settings
+        # (MocoTrack.cpp:105-121: tolerances 1e-2, forward FD, bounds guess)
+        ("gait10dof18musc_track_N200", lambda: configs.gait10dof18musc_track(200, muscles=True), None,
+         "configs[2]: MocoTrack gait10dof18musc, 18 DGF muscles + reserves, N=200 (testMocoTrack.cpp:46-68 "
+         "with ModOpReplaceMusclesWithDeGrooteFregly2016)"),
+        ("gait10dof18musc_track_N400", lambda: configs.gait10dof18musc_track(400, muscles=True), None,
+         "configs[2] at the north-star size N=400"),
         ("moco_inverse_rajagopal18_N11", lambda: configs.rajagopal18_inverse(),
          "std_testMocoInverse_subject_18musc_solution.npz",
          "testMocoInverse.cpp:118-147; reference file: objective 1.087741, 52 Ipopt iterations, 54.5 s"),
@@ -484,22 +491,31 @@ def solve_lines():
         rep = st.problem.create_rep()
         sol = st.solve()
         r = sol.stats
+        ev, la = r.timings.get("evaluations_s", 0.0), r.timings.get("linear_algebra_s", 0.0)
         line = {"success": r.success, "wall_clock_s": round(r.duration, 3), "iterations": r.iterations,
                 "objective": r.objective, "status": r.status, "evaluations": r.evaluations,
-                "seconds_in_evaluations": round(r.timings.get("evaluations_s", 0.0), 3),
-                "seconds_in_kkt": round(r.timings.get("linear_algebra_s", 0.0), 3),
-                "optimizer": r.optimizer, "reference": ref}
+                "seconds_in_evaluations": round(ev, 3), "seconds_in_kkt": round(la, 3),
+                "seconds_other_host": round(r.duration - ev - la, 3),
+                "evaluation_share": round(ev / r.duration, 4) if r.duration > 0 else None,
+                "linear_solver": r.timings.get("linear_solver"),
+                "n": int(len(r.x)), "optimizer": r.optimizer, "reference": ref,
+                "note": "evaluations are the host-pointer C-ABI calls (x in, f / grad f / g out over PCIe); "
+                        "with the device linear solver the Jacobian is evaluated into HBM and never copied"}
         if gold:
             line["rms_controls_states_vs_golden"] = rms_vs(sol, rep, gold)
         out[name] = line
     return out
 
 
-def mesh_main(cx, args):
-    """--multi mesh: one NLP sharded by mesh interval (strong scaling).
-    value = device-resident (x broadcast + shard evaluation into HBM);
-    host_inclusive adds each rank's slice DMA into the shared page-locked
-    host buffer; replicas = every rank its own whole NLP."""
+def mesh_measure(cx, args):
+    """--multi mesh measurements: one NLP sharded by mesh interval over the
+    ranks (strong scaling of the north star's layout).  Returns (on rank 0)
+    the host-inclusive rate -- the host IPOPT's round trip: x from page-locked
+    host memory over each rank's PCIe link, the shard's evaluation, each
+    rank's g / J slice DMA into one page-locked host buffer shared by the
+    node's ranks (HostGather), a barrier -- and, labelled, the device-resident
+    rate (x already in every rank's HBM, results left there: no data moves,
+    an upper bound) and the same with an RCCL broadcast of x per call."""
     from mocohip import configs
     from mocohip.distributed import HostGather, interval_shard
     torch, dist = cx.torch, cx.dist
@@ -514,7 +530,7 @@ def mesh_main(cx, args):
     tag = os.environ.get("MOCOHIP_BENCH_TAG") or f"mocohip_bench_{os.getppid()}"
     barrier = dist.barrier if cx.world > 1 else (lambda: None)
     hg = HostGather(tag, nlp.m, nlp.nnz, (nlp.row_begin, nlp.row_end), (nlp.nnz_begin, nlp.nnz_end),
-                    cx.rank, barrier, pin=True)
+                    cx.rank, barrier, pin=True, device=cx.local)
     stream = cx.stream()
     evaluate = fused if args.mode == "fused" else sep
 
@@ -535,9 +551,9 @@ def mesh_main(cx, args):
         torch.cuda.current_stream().synchronize()
         if cx.world > 1:
             dist.barrier()                     # every slice has landed on the IPOPT host
+    kh, elh = measure(cx, step_host, args, k=max(50, args.steps // 4), w=max(10, args.warmup // 10))
     k, el = measure(cx, step_device, args)
     kb, elb = measure(cx, step_bcast, args, k=max(50, args.steps // 4), w=max(10, args.warmup // 10))
-    kh, elh = measure(cx, step_host, args, k=max(50, args.steps // 4), w=max(10, args.warmup // 10))
     ok = None
     if cx.rank == 0:
         # the reassembled host vectors against one unsharded evaluation
@@ -547,8 +563,30 @@ def mesh_main(cx, args):
         full.close()
     barrier()
     hg.close(unlink=cx.rank == 0)
-    # replicas: every rank evaluates the whole NLP (independent trials)
+    out = {"value": round(kh / elh, 3), "unit": "calls/s", "steps": kh, "ms_per_step": round(1e3 * elh / kh, 5),
+           "scaling": "strong", "mesh_intervals": N, "n": nlp.n, "m": nlp.m, "nnz_jac": nlp.nnz,
+           "reassembly_bit_exact": ok,
+           "parallelism": f"mesh-shard{cx.world}: each rank its contiguous intervals, its g / J slice DMA'd "
+                          "over its own PCIe link into one page-locked host buffer (HostGather)",
+           "device_resident": {"value": round(k / el, 3), "unit": "calls/s", "steps": k,
+                               "ms_per_step": round(1e3 * el / k, 5),
+                               "note": "upper bound, not a deliverable rate: x already in every rank's HBM, "
+                                       "g / J left there (no data moves)"},
+           "x_broadcast": {"value": round(kb / elb, 3), "unit": "calls/s", "steps": kb,
+                           "ms_per_step": round(1e3 * elb / kb, 5),
+                           "note": "device-resident + an RCCL broadcast of x from rank 0 before every call"}}
     nlp.close()
+    return out
+
+
+def mesh_main(cx, args):
+    """--multi mesh: the headline is the host-inclusive rate of one NLP
+    sharded over the ranks (mesh_measure); replicas beside it."""
+    from mocohip import configs
+    m = mesh_measure(cx, args)
+    N = args.intervals
+    build = ((lambda: configs.rajagopal80(N, fd_scheme=args.fd)) if args.config == "rajagopal80"
+             else (lambda: configs.gait10dof18musc(N, fd_scheme=args.fd)))
     rnlp = make_nlp(cx, build(), blocking=False)
     rsep, rfused, _ = device_steps(cx, rnlp, track_iterate(rnlp, cx.rank))
     kr, elr = measure(cx, rfused if args.mode == "fused" else rsep, args)
@@ -558,25 +596,15 @@ def mesh_main(cx, args):
               else "MocoTrack gait10dof18musc DGF rigid tendon (configs[2])")
         line = {"metric": "NLP eval_g+eval_jac_g calls/sec (gait10dof18musc)" if args.config == "gait"
                           else "NLP eval_g+eval_jac_g calls/sec (Rajagopal 80-muscle)",
-                "value": round(k / el, 3), "unit": "calls/s", "n_gpus": cx.world, "steps": k,
-                "warmup": args.warmup, "ms_per_step": round(1e3 * el / k, 5), "higher_is_better": True,
+                "value": m["value"], "unit": "calls/s", "n_gpus": cx.world, "steps": m["steps"],
+                "warmup": args.warmup, "ms_per_step": m["ms_per_step"], "higher_is_better": True,
                 "scaling": "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-                "config": {"workload": wl + ", one NLP sharded by mesh interval for one host IPOPT",
-                           "mesh_intervals": N, "n": nlp.n, "m": nlp.m, "nnz_jac": nlp.nnz,
-                           "fd": args.fd, "mode": args.mode,
-                           "parallelism": f"mesh-shard{cx.world}: x resident on every rank, each rank "
-                                          "its contiguous intervals, g / J slices in its HBM",
-                           "calls": "asynchronous (device pointers, torch stream)"},
-                "x_broadcast": {"value": round(kb / elb, 3), "unit": "calls/s", "steps": kb,
-                                "ms_per_step": round(1e3 * elb / kb, 5),
-                                "note": "+ an RCCL broadcast of x from rank 0 before every evaluation"},
-                "host_inclusive": {"value": round(kh / elh, 3), "unit": "calls/s", "steps": kh,
-                                   "ms_per_step": round(1e3 * elh / kh, 5),
-                                   "note": "the host IPOPT's round trip: x from page-locked host memory "
-                                           "over each rank's PCIe link, the shard's evaluation, each "
-                                           "rank's g / J slice DMA into one page-locked host buffer "
-                                           "shared by the node's ranks (HostGather), barrier",
-                                   "reassembly_bit_exact": ok},
+                "config": {"workload": wl + ", one NLP sharded by mesh interval for one host IPOPT "
+                                            "(host-inclusive: x in and g / J out over PCIe every call)",
+                           "mesh_intervals": N, "n": m["n"], "m": m["m"], "nnz_jac": m["nnz_jac"],
+                           "fd": args.fd, "mode": args.mode, "parallelism": m["parallelism"]},
+                "device_resident": m["device_resident"], "x_broadcast": m["x_broadcast"],
+                "reassembly_bit_exact": m["reassembly_bit_exact"],
                 "replicas": {"value": round(kr * cx.world / elr, 3), "unit": "calls/s", "steps": kr,
                              "scaling": "weak", "note": "every rank its own whole NLP, no collective"}}
         print(json.dumps(line), flush=True)
@@ -586,7 +614,10 @@ def main():
     args = parse()
     cx = Ctx(args)
     if args.multi is None:
-        args.multi = "mesh" if cx.world > 1 else "replicas"
+        # independent NLPs per GPU (the configs[4] layout; weak scaling) is
+        # the default at every N; the mesh layout's strong scaling of one NLP
+        # is reported beside it (its host-inclusive rate) when N > 1
+        args.multi = "replicas"
     if args.multi == "mesh":
         mesh_main(cx, args)
         if cx.world > 1:
@@ -704,6 +735,9 @@ def main():
                                       args, args.inverse_batch)
             invb["workload"] = inv["workload"]
             extra["inverse_batched"] = invb
+    mesh = None
+    if cx.world > 1 and not args.single_mode:
+        mesh = mesh_measure(cx, args)
     if cx.rank == 0:
         cpu = cpu1 = None
         if cx.world == 1 and not args.no_cpu_baseline:
@@ -730,6 +764,8 @@ def main():
             "cpu_baseline": cpu,
         }
         line.update(extra)
+        if mesh is not None:
+            line["mesh"] = mesh
         if cpu1:
             line["cpu_baseline_1thread"] = cpu1
         if cpu and cpu.get("value"):

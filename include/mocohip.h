@@ -565,6 +565,18 @@ int mh_get_jac_structure(const mh_ctx* ctx, int32_t* iRow, int32_t* jCol);
  * context is unsharded, otherwise this shard's rows / nonzeros only. */
 int mh_eval_f(mh_ctx* ctx, const double* x, int new_x, double* f);
 int mh_eval_grad_f(mh_ctx* ctx, const double* x, int new_x, double* grad_f);
+/* The objective's partial over this context's shard (SURVEY §8(e) E2-E3:
+ * the integral goals summed over the shard's own mesh intervals only --
+ * CasOCTranscription.cpp:489-493 assembles the integral from the per-interval
+ * quadrature -- and the endpoint goals (final time, final marker) on the
+ * shard that owns the final grid point): the partials of all shards sum to
+ * mh_eval_f, one all-reduce of a double.  On an unsharded context it equals
+ * mh_eval_f bit for bit. */
+int mh_eval_f_partial(mh_ctx* ctx, const double* x, double* f);
+/* Its gradient (n doubles): nonzero at t0 / tf and the shard's grid points
+ * (the boundary point a shard shares with its neighbour carries each side's
+ * share); the sum over the shards is mh_eval_grad_f (an all-reduce). */
+int mh_eval_grad_f_partial(mh_ctx* ctx, const double* x, double* grad_f);
 int mh_eval_g(mh_ctx* ctx, const double* x, int new_x, double* g);
 int mh_eval_jac_g(mh_ctx* ctx, const double* x, int new_x, double* values);
 

@@ -205,18 +205,37 @@ __global__ void __launch_bounds__(64) k_eval(DevModel M, Layout L, Lanes Ln,
 // The generic interpreter's lanes with their multibody workspace (D::W:
 // poses, velocities, body forces, motion subspaces, tau, mass matrix) in LDS
 // instead of scratch: one slot per thread of the workgroup (blockDim.x <=
-// 16 lanes, launched with blockDim.x * sizeof(W) bytes of dynamic LDS).  A
-// thread past the last lane returns before it touches LDS, so every slot
-// address stays inside the allocation.  Same arithmetic as k_eval, bit for
-// bit (tests/test_gpu_parity.py::test_eval_g_lds_workspace_bit_identical).
+// 16 lanes, launched with blockDim.x * (sizeof(W) + 16 guard_words) bytes of
+// dynamic LDS).  A thread past the last lane returns before it touches LDS,
+// so every slot address stays inside the allocation.  Same arithmetic as
+// k_eval, bit for bit (tests/test_gpu_parity.py::
+// test_eval_g_lds_workspace_bit_identical).
+// guard_words > 0 (MOCOHIP_G_LDS_GUARD, a check of the workspace's own
+// indexing): each slot sits between two guard bands of guard_words doubles
+// filled with a canary bit pattern, the slot itself is filled with NaN
+// before the evaluation (a read of a word the evaluation did not write
+// first then poisons the outputs, which the bit-identity test sees), and
+// after it each thread compares its two bands and sets *status on any
+// change (a workspace store outside its slot).
+constexpr unsigned long long kLdsCanary = 0x7ff4deadbeefcafeull;
 template <class D>
 __global__ void __launch_bounds__(16) k_eval_lds(DevModel M, Layout L, Lanes Ln,
         const double* __restrict__ x, const double* __restrict__ grid,
-        double* __restrict__ times, double* __restrict__ Y) {
+        double* __restrict__ times, double* __restrict__ Y, int guard_words, int* __restrict__ status) {
+    static_assert(sizeof(typename D::W) % sizeof(double) == 0, "workspace slots are whole doubles");
+    constexpr int WW = (int)(sizeof(typename D::W) / sizeof(double));
     extern __shared__ double smem[];
-    typename D::W* ws = reinterpret_cast<typename D::W*>(smem);
     const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= (long)L.nk * Ln.stride) return;
+    double* band = smem + (long)threadIdx.x * (WW + 2 * guard_words);
+    typename D::W* ws = reinterpret_cast<typename D::W*>(band + guard_words);
+    if (guard_words) {
+        for (int i = 0; i < guard_words; ++i) {
+            band[i] = __longlong_as_double((long long)kLdsCanary);
+            band[guard_words + WW + i] = __longlong_as_double((long long)kLdsCanary);
+        }
+        for (int i = 0; i < WW; ++i) band[guard_words + i] = __longlong_as_double(0x7ff8000000000badll);
+    }
     const int kl = (int)(gid / Ln.stride);
     const int r = (int)(gid - (long)kl * Ln.stride);
     const int k = L.k0 + kl;
@@ -224,7 +243,14 @@ __global__ void __launch_bounds__(16) k_eval_lds(DevModel M, Layout L, Lanes Ln,
     double out[D::MO];
     const double t = lane_inputs<D>(L, Ln, x, grid[k], k, r, in);
     if (r == Ln.base) times[kl] = t;
-    D::eval_w(M, t, in, out, ws[threadIdx.x]);
+    D::eval_w(M, t, in, out, *ws);
+    if (guard_words) {
+        bool ok = true;
+        for (int i = 0; i < guard_words; ++i)
+            ok = ok && (unsigned long long)__double_as_longlong(band[i]) == kLdsCanary &&
+                 (unsigned long long)__double_as_longlong(band[guard_words + WW + i]) == kLdsCanary;
+        if (!ok) status[0] = 1;
+    }
     double* Yk = Y + (long)kl * L.NO * Ln.stride + r;
 #pragma unroll
     for (int o = 0; o < D::MO; ++o)
@@ -1923,6 +1949,10 @@ struct mh_ctx {
     char* dmem = nullptr;
     DevModel M{};
     GoalSet GS{};
+    // d_quadp: the quadrature of this shard's own mesh intervals only (its
+    // objective partial: the partials of the shards sum to the objective)
+    double* d_quadp = nullptr;
+    std::vector<double> quadp;
     double *d_x = nullptr, *d_grid = nullptr, *d_quad = nullptr, *d_times = nullptr, *d_Y = nullptr,
            *d_Yg = nullptr, *d_g = nullptr, *d_vals = nullptr, *d_C = nullptr, *d_grad = nullptr,
            *d_tpart = nullptr, *d_f = nullptr;
@@ -1935,6 +1965,8 @@ struct mh_ctx {
     int n_exc_lanes = 0;
     int g_block = 4;               // generic interpreter, eval_g: k_eval workgroup size (A/B: profiles/r02_l)
     bool g_lds = false;            // generic interpreter, eval_g: workspace in LDS (k_eval_lds)
+    int g_lds_guard = 0;           // k_eval_lds guard band per slot side, doubles (MOCOHIP_G_LDS_GUARD)
+    int* d_lds_status = nullptr;   // set by k_eval_lds when a guard band changed
     int groups_split = -1;         // task back ends: heavy / light group kernels (-1: by occupancy)
     int combine_mode = -1;         // split path combine: 0 LDS-staged, 1 global memory (-1: by spills)
     uint32_t* d_ctpl = nullptr;    // compiled template of the Jacobian lanes (k_interval)
@@ -2083,10 +2115,11 @@ static void be_eval_lane(mh_ctx* c, const double* x, int mode, double* Y) {
         if constexpr (D::EXC_LANES) {   // the generic interpreter (GenericDae)
             if (mode == 0 && c->g_lds) {
                 // MOCOHIP_G_LDS: the workspace in LDS, tb <= 16 slots per workgroup
-                const int tl = std::max(1, std::min({tb, 16, (int)(65536 / sizeof(typename D::W))}));
-                const size_t lds = sizeof(typename D::W) * (size_t)tl;
+                const size_t slot = sizeof(typename D::W) + 2 * sizeof(double) * (size_t)c->g_lds_guard;
+                const int tl = std::max(1, std::min({tb, 16, (int)(65536 / slot)}));
+                const size_t lds = slot * (size_t)tl;
                 hipLaunchKernelGGL(k_eval_lds<D>, dim3((unsigned)((lanes + tl - 1) / tl)), dim3(tl), lds,
-                        c->stream, c->M, L, ln, x, c->d_grid, c->d_times, Y);
+                        c->stream, c->M, L, ln, x, c->d_grid, c->d_times, Y, c->g_lds_guard, c->d_lds_status);
                 return;
             }
         }

@@ -143,7 +143,7 @@ __global__ void __launch_bounds__(256) k_transcribe_gs(Layout L, Interval I, Lan
 
 // Single-workgroup deterministic reduction of the objective (mode 0) or of
 // the t0/tf gradient entries (mode 1).
-__global__ void __launch_bounds__(256) k_reduce_obj(Layout L, GoalSet GS, int mode,
+__global__ void __launch_bounds__(256) k_reduce_obj(Layout L, GoalSet GS, int mode, int endpoint,
         const double* __restrict__ x, const double* __restrict__ C,
         const double* __restrict__ tpart, const double* __restrict__ ep, double* __restrict__ out) {
     __shared__ double red[256];
@@ -162,10 +162,12 @@ __global__ void __launch_bounds__(256) k_reduce_obj(Layout L, GoalSet GS, int mo
         __syncthreads();
         const mh_goal G = GS.goals[gi];
         if (G.kind == MH_GOAL_FINAL_TIME) {
-            total += G.weight * x[1];
-            g1 += G.weight;
+            if (endpoint) {
+                total += G.weight * x[1];
+                g1 += G.weight;
+            }
         } else if (G.kind == MH_GOAL_MARKER_FINAL) {
-            total += G.weight * ep[gi];   // its gradient: k_marker_final
+            if (endpoint) total += G.weight * ep[gi];   // its gradient: k_marker_final
         } else {
             total += G.weight * ((x[1] - x[0]) * acc);
             g0 += -G.weight * acc;
@@ -848,6 +850,28 @@ static bool compile_template(mh_ctx* c) {
     return true;
 }
 
+static const int kZeroInt = 0;
+
+// The objective partial of a shard (mh_eval_f_partial): the quadrature
+// weights of the shard's own mesh intervals, accumulated exactly as the
+// whole problem's are (CasOCHermiteSimpson.cpp:36-43, CasOCTrapezoidal.cpp:
+// 26-37), so an unsharded context's partial IS its objective, bit for bit,
+// and the shards' partials sum to it.
+static void shard_quadrature(mh_ctx* c) {
+    c->quadp.assign(c->G, 0.0);
+    for (int i = c->ib; i < c->ie; ++i) {
+        const double dm = (i + 1) / (double)c->N - i / (double)c->N;
+        if (c->scheme == MH_HERMITE_SIMPSON) {
+            c->quadp[2 * i] += (1.0 / 6.0) * dm;
+            c->quadp[2 * i + 1] += (2.0 / 3.0) * dm;
+            c->quadp[2 * i + 2] += (1.0 / 6.0) * dm;
+        } else {
+            c->quadp[i] += 0.5 * dm;
+            c->quadp[i + 1] += 0.5 * dm;
+        }
+    }
+}
+
 static int validate_and_layout(mh_ctx* c, const mh_problem* p, const mh_options* o,
         std::vector<int>& coord_body, std::vector<int>& act_state, std::vector<int>& ftn_state,
         std::vector<int>& mus_control, double& tau_act, double& tau_deact) {
@@ -1133,6 +1157,7 @@ static int validate_and_layout(mh_ctx* c, const mh_problem* p, const mh_options*
     c->nnz = c->nnz_ep + (int64_t)c->nnz_int * c->N + c->nnz_tail;
     c->ib = std::max(0, o->interval_begin);
     c->ie = o->interval_end > 0 ? std::min(o->interval_end, c->N) : c->N;
+    shard_quadrature(c);
     if (c->ib >= c->ie) return set_err(MH_ERR_INVALID, "empty interval shard [%d, %d)", c->ib, c->ie);
     c->k0 = c->scheme == MH_HERMITE_SIMPSON ? 2 * c->ib : c->ib;
     const int klast = c->scheme == MH_HERMITE_SIMPSON ? 2 * c->ie : c->ie;
@@ -1280,6 +1305,8 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
                  o_gcol = A.put(c->gcol.data(), c->gcol.size()), o_gw = A.put(c->gw.data(), c->gw.size()),
                  o_grid = A.put(c->grid.data(), c->grid.size()),
                  o_quad = A.put(c->quad.data(), c->quad.size()),
+                 o_quadp = A.put(c->quadp.data(), c->quadp.size()),
+                 o_ldss = A.put(&kZeroInt, 1),
                  o_tpl = A.put(c->tpl.data(), c->tpl.size()),
                  o_pc = A.put(c->pc.data(), c->pc.size()),
                  o_ep = A.put(c->ep.data(), c->ep.size()),
@@ -1424,10 +1451,13 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     if (c->n_exc_lanes) { c->d_exc = (int*)(b + o_exc); c->d_lane_map = (int*)(b + o_lmap); }
     if (const char* eb = std::getenv("MOCOHIP_G_BLOCK")) c->g_block = std::min(64, std::max(1, std::atoi(eb)));
     if (const char* el = std::getenv("MOCOHIP_G_LDS")) c->g_lds = std::atoi(el) != 0;
+    if (const char* eg = std::getenv("MOCOHIP_G_LDS_GUARD")) c->g_lds_guard = std::min(64, std::max(0, std::atoi(eg)));
     if (const char* es = std::getenv("MOCOHIP_GROUPS_SPLIT")) c->groups_split = std::atoi(es) != 0 ? 1 : 0;
     if (const char* ec = std::getenv("MOCOHIP_COMBINE"))
         c->combine_mode = std::strcmp(ec, "global") == 0 ? 1 : std::strcmp(ec, "lds") == 0 ? 0 : -1;
     c->d_grid = (double*)(b + o_grid); c->d_quad = (double*)(b + o_quad);
+    c->d_quadp = (double*)(b + o_quadp);
+    c->d_lds_status = (int*)(b + o_ldss);
     c->d_tpl = (TplEntry*)(b + o_tpl);
     c->d_ctpl = (uint32_t*)(b + o_ctpl);
     c->d_ctgen = (int*)(b + o_ctgen);
@@ -2283,55 +2313,75 @@ extern "C" int mh_eval_g_jac_g(mh_ctx* c, const double* x, double* g, double* va
     return finish(c);
 }
 
-extern "C" int mh_eval_f(mh_ctx* c, const double* x, int, double* f) {
+// The objective (partial = false) or this shard's partial of it (partial =
+// true: the integrals over the shard's own mesh intervals, d_quadp, and the
+// endpoint goals -- final time, final marker -- on the shard that owns the
+// final grid point only).  Swapping d_quad lets the back ends' integrand /
+// gradient launches read the shard's weights unchanged.
+static int eval_f_impl(mh_ctx* c, const double* x, double* f, bool partial) {
     if (!c || !x || !f) return set_err(MH_ERR_INVALID, "null argument");
     HIPCHK(hipSetDevice(c->device));
     (void)hipGetLastError();   // report only this call's launch errors
     HIPCHK(hipMemcpyAsync(c->d_x, x, sizeof(double) * c->n, hipMemcpyHostToDevice, c->stream));
     if (c->timing) HIPCHK(hipEventRecord(c->ev[0], c->stream));
+    const bool endpoint = !partial || c->ie == c->N;
+    double* quad = c->d_quad;
+    if (partial) c->d_quad = c->d_quadp;
     Layout L = make_layout(c, 0, c->G);
-    if (c->ngoals > 0) {
-        c->be->integrand(c, c->d_x);
-        HIPCHK(hipGetLastError());
-    }
-    if (c->has_marker)
+    if (c->ngoals > 0) c->be->integrand(c, c->d_x);
+    c->d_quad = quad;
+    HIPCHK(hipGetLastError());
+    if (c->has_marker && endpoint)
         hipLaunchKernelGGL(k_marker_final, dim3((unsigned)c->ngoals), dim3(128), 0, c->stream, c->M, L, c->GS,
                 c->fd, c->h, 0, c->d_x, c->d_ep, c->d_grad);
     if (c->timing) HIPCHK(hipEventRecord(c->ev[1], c->stream));
-    hipLaunchKernelGGL(k_reduce_obj, dim3(1), dim3(256), 0, c->stream, L, c->GS, 0, c->d_x, c->d_C,
-            c->d_tpart, c->d_ep, c->d_f);
+    hipLaunchKernelGGL(k_reduce_obj, dim3(1), dim3(256), 0, c->stream, L, c->GS, 0, endpoint ? 1 : 0, c->d_x,
+            c->d_C, c->d_tpart, c->d_ep, c->d_f);
     HIPCHK(hipGetLastError());
     if (c->timing) HIPCHK(hipEventRecord(c->ev[2], c->stream));
     HIPCHK(hipMemcpyAsync(f, c->d_f, sizeof(double), hipMemcpyDeviceToHost, c->stream));
     return finish(c);
 }
 
-extern "C" int mh_eval_grad_f(mh_ctx* c, const double* x, int, double* grad) {
+static int eval_grad_f_impl(mh_ctx* c, const double* x, double* grad, bool partial) {
     if (!c || !x || !grad) return set_err(MH_ERR_INVALID, "null argument");
     HIPCHK(hipSetDevice(c->device));
     (void)hipGetLastError();   // report only this call's launch errors
     HIPCHK(hipMemcpyAsync(c->d_x, x, sizeof(double) * c->n, hipMemcpyHostToDevice, c->stream));
     if (c->timing) HIPCHK(hipEventRecord(c->ev[0], c->stream));
+    const bool endpoint = !partial || c->ie == c->N;
     Layout L = make_layout(c, 0, c->G);
     HIPCHK(hipMemsetAsync(c->d_grad, 0, sizeof(double) * c->n, c->stream));
     HIPCHK(hipMemsetAsync(c->d_tpart, 0, sizeof(double) * 2 * c->G, c->stream));
     HIPCHK(hipMemsetAsync(c->d_C, 0, sizeof(double) * c->G * std::max(1, c->ngoals), c->stream));
+    double* quad = c->d_quad;
+    if (partial) c->d_quad = c->d_quadp;
     if (c->ngoals > 0) {
         c->be->integrand(c, c->d_x);
         c->be->grad(c, c->d_x);
-        HIPCHK(hipGetLastError());
     }
-    if (c->has_marker)   // after k_grad: adds to the final coordinates' entries
+    c->d_quad = quad;
+    HIPCHK(hipGetLastError());
+    if (c->has_marker && endpoint)   // after k_grad: adds to the final coordinates' entries
         hipLaunchKernelGGL(k_marker_final, dim3((unsigned)c->ngoals), dim3(128), 0, c->stream, c->M, L, c->GS,
                 c->fd, c->h, 1, c->d_x, c->d_ep, c->d_grad);
     if (c->timing) HIPCHK(hipEventRecord(c->ev[1], c->stream));
-    hipLaunchKernelGGL(k_reduce_obj, dim3(1), dim3(256), 0, c->stream, L, c->GS, 1, c->d_x, c->d_C,
-            c->d_tpart, c->d_ep, c->d_f);
+    hipLaunchKernelGGL(k_reduce_obj, dim3(1), dim3(256), 0, c->stream, L, c->GS, 1, endpoint ? 1 : 0, c->d_x,
+            c->d_C, c->d_tpart, c->d_ep, c->d_f);
     HIPCHK(hipGetLastError());
     if (c->timing) HIPCHK(hipEventRecord(c->ev[2], c->stream));
     HIPCHK(hipMemcpyAsync(c->d_grad, c->d_f, sizeof(double) * 2, hipMemcpyDeviceToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(grad, c->d_grad, sizeof(double) * c->n, hipMemcpyDeviceToHost, c->stream));
     return finish(c);
+}
+
+extern "C" int mh_eval_f(mh_ctx* c, const double* x, int, double* f) { return eval_f_impl(c, x, f, false); }
+extern "C" int mh_eval_grad_f(mh_ctx* c, const double* x, int, double* grad) {
+    return eval_grad_f_impl(c, x, grad, false);
+}
+extern "C" int mh_eval_f_partial(mh_ctx* c, const double* x, double* f) { return eval_f_impl(c, x, f, true); }
+extern "C" int mh_eval_grad_f_partial(mh_ctx* c, const double* x, double* grad) {
+    return eval_grad_f_impl(c, x, grad, true);
 }
 
 extern "C" int mh_eval_dae(mh_ctx* c, int32_t np, const double* inputs, double* outputs) {
@@ -2690,7 +2740,16 @@ extern "C" int mh_get_backend_flags(const mh_ctx* c, char* flags, int32_t len) {
     if (c->quot) f += " quot";
     if (c->asm_grid_stride) f += " asm-gs";
     if (c->d_exc) f += " exc-lanes";
-    if (c->g_lds && !c->be->tasks && std::strncmp(c->be->name, "generic", 7) == 0) f += " g-lds";
+    if (c->g_lds && !c->be->tasks && std::strncmp(c->be->name, "generic", 7) == 0) {
+        f += " g-lds";
+        if (c->g_lds_guard) {
+            // the guard bands' verdict over every k_eval_lds launch so far
+            int st = 0;
+            if (hipMemcpy(&st, c->d_lds_status, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
+                return set_err(MH_ERR_HIP, "reading the LDS guard status failed");
+            f += st ? " g-lds-guard-violated" : " g-lds-guard-intact";
+        }
+    }
     std::strncpy(flags, f.c_str(), (size_t)len - 1);
     flags[len - 1] = 0;
     return MH_OK;

@@ -212,6 +212,8 @@ MOCOHIP_SYMBOLS = {
     "mh_get_jac_structure": (i32, [C.c_void_p, P(i32), P(i32)]),
     "mh_eval_f": (i32, [C.c_void_p, P(f64), C.c_int, P(f64)]),
     "mh_eval_grad_f": (i32, [C.c_void_p, P(f64), C.c_int, P(f64)]),
+    "mh_eval_f_partial": (i32, [C.c_void_p, P(f64), P(f64)]),
+    "mh_eval_grad_f_partial": (i32, [C.c_void_p, P(f64), P(f64)]),
     "mh_eval_g": (i32, [C.c_void_p, P(f64), C.c_int, P(f64)]),
     "mh_eval_jac_g": (i32, [C.c_void_p, P(f64), C.c_int, P(f64)]),
     "mh_eval_g_device": (i32, [C.c_void_p, C.c_void_p, C.c_void_p]),
@@ -256,6 +258,8 @@ ORACLE_SYMBOLS = {
     "orc_get_jac_structure": (i32, [C.c_void_p, P(i32), P(i32)]),
     "orc_eval_f": (i32, [C.c_void_p, P(f64), P(f64)]),
     "orc_eval_grad_f": (i32, [C.c_void_p, P(f64), P(f64)]),
+    "orc_eval_f_partial": (i32, [C.c_void_p, P(f64), P(f64)]),
+    "orc_eval_grad_f_partial": (i32, [C.c_void_p, P(f64), P(f64)]),
     "orc_eval_g": (i32, [C.c_void_p, P(f64), P(f64)]),
     "orc_eval_jac_g": (i32, [C.c_void_p, P(f64), P(f64)]),
     "orc_eval_dae": (i32, [C.c_void_p, i32, P(f64), P(f64)]),

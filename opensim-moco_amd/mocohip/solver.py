@@ -400,6 +400,22 @@ class _NLPBase:
         self._check(self._fn("get_jacobian_seeds")(self.ctx, abi.iptr(color), C.byref(k)))
         return color, int(k.value)
 
+    def eval_f_partial(self, x) -> float:
+        """This shard's objective partial (mh_eval_f_partial): the partials
+        of all shards sum to eval_f."""
+        x = np.ascontiguousarray(x, float)
+        f = np.zeros(1)
+        self._check(self._fn("eval_f_partial")(self.ctx, abi.dptr(x), abi.dptr(f)))
+        return float(f[0])
+
+    def eval_grad_f_partial(self, x) -> np.ndarray:
+        """This shard's gradient partial (n doubles; the sum over the shards
+        is eval_grad_f)."""
+        x = np.ascontiguousarray(x, float)
+        g = np.empty(self.n)
+        self._check(self._fn("eval_grad_f_partial")(self.ctx, abi.dptr(x), abi.dptr(g)))
+        return g
+
     def eval_dae(self, inputs: np.ndarray) -> np.ndarray:
         """Per-point DAE: rows [t, states, controls, derivatives] ->
         [udot or multibody residual, zdot, auxiliary residuals]."""

@@ -2948,7 +2948,46 @@ static double marker_cost(const orc_ctx* c, const mh_goal* G, const double* st, 
     return s;
 }
 
-int orc_eval_f(orc_ctx* c, const double* x, double* f) {
+/* The shard's own quadrature (mh_eval_f_partial): the intervals [ib, ie)
+ * accumulated as c->quad is, so an unsharded context's partial is its
+ * objective bit for bit. */
+static double* shard_quad(const orc_ctx* c) {
+    double* q = (double*)calloc((size_t)c->G, sizeof(double));
+    for (int i = c->ib; i < c->ie; ++i) {
+        double dm = (i + 1) / (double)c->N - i / (double)c->N;
+        if (c->scheme == MH_HERMITE_SIMPSON) {
+            q[2 * i] += (1.0 / 6.0) * dm;
+            q[2 * i + 1] += (2.0 / 3.0) * dm;
+            q[2 * i + 2] += (1.0 / 6.0) * dm;
+        } else {
+            q[i] += 0.5 * dm;
+            q[i + 1] += 0.5 * dm;
+        }
+    }
+    return q;
+}
+
+static int eval_f_impl(orc_ctx* c, const double* x, double* f, const double* quad, int endpoint);
+static int eval_grad_f_impl(orc_ctx* c, const double* x, double* grad, const double* quad, int endpoint);
+
+int orc_eval_f(orc_ctx* c, const double* x, double* f) { return eval_f_impl(c, x, f, c->quad, 1); }
+int orc_eval_grad_f(orc_ctx* c, const double* x, double* grad) {
+    return eval_grad_f_impl(c, x, grad, c->quad, 1);
+}
+int orc_eval_f_partial(orc_ctx* c, const double* x, double* f) {
+    double* q = shard_quad(c);
+    int rc = eval_f_impl(c, x, f, q, c->ie == c->N);
+    free(q);
+    return rc;
+}
+int orc_eval_grad_f_partial(orc_ctx* c, const double* x, double* grad) {
+    double* q = shard_quad(c);
+    int rc = eval_grad_f_impl(c, x, grad, q, c->ie == c->N);
+    free(q);
+    return rc;
+}
+
+static int eval_f_impl(orc_ctx* c, const double* x, double* f, const double* quad, int endpoint) {
     double* times = (double*)malloc(sizeof(double) * (size_t)c->G);
     double* st = (double*)malloc(sizeof(double) * (size_t)(c->NP + 1));
     double* ct = st + c->NS;
@@ -2959,6 +2998,7 @@ int orc_eval_f(orc_ctx* c, const double* x, double* f) {
         const mh_goal* G = &c->goals[g];
         double cost;
         if (G->kind == MH_GOAL_MARKER_FINAL) {
+            if (!endpoint) continue;
             dae_ws w;
             ws_alloc(c, &w);
             gather_point(c, x, c->G - 1, st, ct);
@@ -2968,11 +3008,12 @@ int orc_eval_f(orc_ctx* c, const double* x, double* f) {
             double acc = 0.0;
             for (int k = 0; k < c->G; ++k) {
                 gather_point(c, x, k, st, ct);
-                acc += c->quad[k] * goal_integrand(c, G, times[k], st, ct);
+                acc += quad[k] * goal_integrand(c, G, times[k], st, ct);
             }
             double integral = (x[1] - x[0]) * acc;
             cost = G->weight * integral;
         } else {
+            if (!endpoint) continue;
             cost = G->weight * x[1];
         }
         total += cost;
@@ -2983,7 +3024,7 @@ int orc_eval_f(orc_ctx* c, const double* x, double* f) {
     return MH_OK;
 }
 
-int orc_eval_grad_f(orc_ctx* c, const double* x, double* grad) {
+static int eval_grad_f_impl(orc_ctx* c, const double* x, double* grad, const double* quad, int endpoint) {
     int NS = c->NS, NP = c->NP;
     double h = c->h;
     double* times = (double*)malloc(sizeof(double) * (size_t)c->G);
@@ -2994,6 +3035,7 @@ int orc_eval_grad_f(orc_ctx* c, const double* x, double* grad) {
     for (int g = 0; g < c->P.ngoals; ++g) {
         const mh_goal* G = &c->goals[g];
         if (G->kind == MH_GOAL_MARKER_FINAL) {
+            if (!endpoint) continue;
             /* FD of the cost over the final coordinates (the other final
              * states do not change a Position-stage cost: exactly 0) */
             dae_ws w;
@@ -3012,14 +3054,14 @@ int orc_eval_grad_f(orc_ctx* c, const double* x, double* grad) {
             ws_free(&w);
             continue;
         }
-        if (!goal_has_integral(G)) { grad[1] += G->weight; continue; }
+        if (!goal_has_integral(G)) { if (endpoint) grad[1] += G->weight; continue; }
         double acc = 0.0;
         for (int k = 0; k < c->G; ++k) {
             gather_point(c, x, k, in, in + NS);
             double t = times[k];
             double L0 = goal_integrand(c, G, t, in, in + NS);
-            acc += c->quad[k] * L0;
-            double wq = G->weight * dur * c->quad[k];
+            acc += quad[k] * L0;
+            double wq = G->weight * dur * quad[k];
             for (int d = 0; d < c->NPD + 2; ++d) {   /* the goal callback's inputs */
                 double seed = d == 0 ? 1.0 - c->grid[k] : (d == 1 ? c->grid[k] : 1.0);
                 double lp = 0, lm = 0;

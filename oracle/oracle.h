@@ -46,6 +46,10 @@ int orc_get_jac_structure(const orc_ctx* ctx, int32_t* iRow, int32_t* jCol);
 
 int orc_eval_f(orc_ctx* ctx, const double* x, double* f);
 int orc_eval_grad_f(orc_ctx* ctx, const double* x, double* grad_f);
+/* mh_eval_f_partial / mh_eval_grad_f_partial: the shard's own mesh
+ * intervals' quadrature, endpoint goals on the shard owning the final point. */
+int orc_eval_f_partial(orc_ctx* ctx, const double* x, double* f);
+int orc_eval_grad_f_partial(orc_ctx* ctx, const double* x, double* grad_f);
 int orc_eval_g(orc_ctx* ctx, const double* x, double* g);
 int orc_eval_jac_g(orc_ctx* ctx, const double* x, double* values);
 

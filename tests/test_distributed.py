@@ -7,7 +7,10 @@ its own rows / nonzeros), receives IPOPT's iterate x by broadcast from rank 0
 (the one collective on the data path), and copies its slices into its offset
 of the node-wide HostGather buffer.  Rank 0 -- the IPOPT rank -- then holds g
 and the Jacobian values of the whole NLP; they must equal an unsharded
-evaluation bit for bit.  The device shard contexts' slices are checked
+evaluation bit for bit.  The objective is sharded too: each rank's partial
+(mh_eval_f_partial: its own intervals' quadrature, endpoint goals on the last
+rank) and gradient partial, all-reduced, give f and grad f of the whole NLP.
+The device shard contexts' slices are checked
 against the unsharded device evaluation in
 tests/test_gpu_parity.py::test_shards_reassemble_bit_exact; bench.py
 --multi mesh runs the same HostGather with hipMemcpyAsync over each GPU's
@@ -24,7 +27,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from mocohip import configs
-from mocohip.distributed import HostGather, interval_shard, shard_counts
+from mocohip.distributed import HostGather, interval_shard, shard_counts, sharded_gradient, sharded_objective
 from mocohip.solver import OracleNLP
 
 
@@ -51,7 +54,8 @@ CASES = {"pendulum": lambda N: configs.double_pendulum(N),
          "pendulum_implicit": lambda N: configs.double_pendulum(N, dynamics="implicit"),
          "gait_pathcon": lambda N: configs.gait10dof18musc(N, control_bounds=True),
          "bound_implicit": lambda N: configs.pendulum_control_bound(N, "both", dynamics="implicit"),
-         "inverse": lambda N: configs.gait10dof18musc_inverse(N, sparsity="none")}
+         "inverse": lambda N: configs.gait10dof18musc_inverse(N, sparsity="none"),
+         "swingup": lambda N: configs.double_pendulum_swingup(N)}
 
 
 def _worker(rank, world, port, case, N, tag, out):
@@ -75,11 +79,25 @@ def _worker(rank, world, port, case, N, tag, out):
         assert len(g) == shard.row_end - shard.row_begin and len(J) == shard.nnz_end - shard.nnz_begin
         hg.copy_from_host(g, J)
         dist.barrier()
+
+        # the sharded objective: each rank's partial, one all-reduce
+        def allreduce(a):
+            t = torch.from_numpy(np.ascontiguousarray(a, np.float64))
+            dist.all_reduce(t)
+            return t.numpy()
+        f = sharded_objective(shard, xn, allreduce)
+        gf = sharded_gradient(shard, xn, allreduce)
         ok = True
         if rank == 0:
             full = OracleNLP(rep, st.solver.options(), threads=1)
             ok = (np.array_equal(hg.full_g(), full.eval_g(xn))
                   and np.array_equal(hg.full_values(), full.eval_jac_g(xn)))
+            f0, g0 = full.eval_f(xn), full.eval_grad_f(xn)
+            # (the partial sums add the integral's terms in another order)
+            ok = ok and abs(f - f0) <= 1e-12 * max(1.0, abs(f0))
+            ok = ok and float(np.abs(gf - g0).max()) <= 1e-12 * max(1.0, float(np.abs(g0).max()))
+            # an unsharded context's partial is its objective, bit for bit
+            ok = ok and full.eval_f_partial(xn) == f0 and np.array_equal(full.eval_grad_f_partial(xn), g0)
         out[rank] = int(ok)
         dist.barrier()
     finally:
@@ -90,7 +108,8 @@ def _worker(rank, world, port, case, N, tag, out):
 
 @pytest.mark.parametrize("case,N,world", [("pendulum", 7, 2), ("pendulum", 10, 3), ("gait", 5, 2),
                                           ("pendulum_implicit", 7, 3), ("gait_pathcon", 4, 2),
-                                          ("bound_implicit", 9, 3), ("inverse", 4, 2), ("inverse", 5, 3)])
+                                          ("bound_implicit", 9, 3), ("inverse", 4, 2), ("inverse", 5, 3),
+                                          ("swingup", 6, 2), ("swingup", 7, 3)])
 def test_shard_contexts_reassemble_on_the_ipopt_host(case, N, world):
     ctx = mp.get_context("spawn")
     out = ctx.Array("i", [0] * world)
