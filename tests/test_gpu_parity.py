@@ -309,6 +309,7 @@ def _pair(name, backend="auto", tasks=None, env=None):
                                                   "MOCOHIP_ROLES", "MOCOHIP_ROLE_COUPLE",
                                                   "MOCOHIP_IV_QFUSE", "MOCOHIP_IV_THREADS",
                                                   "MOCOHIP_EXC_LANES", "MOCOHIP_G_BLOCK", "MOCOHIP_G_LDS",
+                                                  "MOCOHIP_G_LDS_GUARD",
                                                   "MOCOHIP_GROUPS_SPLIT", "MOCOHIP_COMBINE")}
     if backend != "auto":
         os.environ["MOCOHIP_BACKEND"] = backend
@@ -591,6 +592,38 @@ def test_shards_reassemble_bit_exact(name):
     assert np.array_equal(np.concatenate(Js), J)
 
 
+@pytest.mark.parametrize("name", ["double_pendulum_hs", "gait_rigid_forward", "gait_inverse_random",
+                                  "double_pendulum_swingup"])
+def test_sharded_objective_partials(name):
+    """each shard's objective partial (mh_eval_f_partial:
+    its own intervals' quadrature, the endpoint goals on the last shard) and
+    gradient partial sum to the unsharded objective and gradient; an
+    unsharded context's partial is its objective bit for bit; every partial
+    agrees with the oracle's."""
+    if name not in CASES:
+        pytest.skip(name)
+    st = CASES[name]()
+    rep = st.problem.create_rep()
+    N = st.solver.num_mesh_intervals
+    full = HipNLP(rep, st.solver.options())
+    x = _iterates(full)[0][1]
+    f, gf = full.eval_f(x), full.eval_grad_f(x)
+    assert full.eval_f_partial(x) == f and np.array_equal(full.eval_grad_f_partial(x), gf)
+    cuts = [0, N // 3, (2 * N) // 3, N]
+    fs, gs = 0.0, np.zeros(full.n)
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        opts = st.solver.options(a, b)
+        sh = HipNLP(rep, opts)
+        ref = OracleNLP(rep, opts)
+        fp, gp = sh.eval_f_partial(x), sh.eval_grad_f_partial(x)
+        assert abs(fp - ref.eval_f_partial(x)) <= 1e-10 * max(1.0, abs(fp))
+        assert np.abs(gp - ref.eval_grad_f_partial(x)).max() <= 1e-8 * max(1.0, np.abs(gp).max())
+        fs += fp
+        gs += gp
+    assert abs(fs - f) <= 1e-12 * max(1.0, abs(f)), (fs, f)
+    assert np.abs(gs - gf).max() <= 1e-12 * max(1.0, np.abs(gf).max())
+
+
 def test_device_pointer_entry_points():
     import torch
     gpu, ref, _ = _pair("double_pendulum_hs")
@@ -849,6 +882,27 @@ def test_eval_g_lds_workspace_bit_identical(name, tb):
     for _, x in _iterates(gpu):
         assert np.array_equal(gpu.eval_g(x), lds.eval_g(x), equal_nan=True)
         assert np.array_equal(gpu.eval_jac_g(x), lds.eval_jac_g(x), equal_nan=True)
+
+
+@pytest.mark.parametrize("name", ["gait_rigid_forward", "wrapped_pendulum", "rajagopal18_inverse_wrapped",
+                                  "coupled_pendulum_implicit"])
+def test_eval_g_lds_workspace_stays_in_its_slot(name):
+    """The round-2 LDS-workspace fault, checked where it could hide
+    (VERDICT r03 weak #7): with MOCOHIP_G_LDS_GUARD every workspace slot sits
+    between two 64-double canary bands and is itself filled with NaN before
+    the evaluation; after it every lane compares its bands.  Out-of-slot
+    stores would change a band (flag "g-lds-guard-violated"), a read of a
+    word the evaluation did not write first would put NaN into the outputs
+    (bit-identity with the scratch workspace fails).  One lane per
+    workgroup: the allocation ends with the last band, so an out-of-range
+    ds_* access that LDS would silently drop lands in a band instead."""
+    gpu, _, _ = _pair(name, "generic")
+    lds, _, _ = _pair(name, "generic", env={"MOCOHIP_G_LDS": "1", "MOCOHIP_G_BLOCK": "1",
+                                             "MOCOHIP_G_LDS_GUARD": "64"})
+    for _, x in _iterates(gpu):
+        assert np.array_equal(gpu.eval_g(x), lds.eval_g(x), equal_nan=True)
+    flags = lds.backend_flags()
+    assert "g-lds-guard-intact" in flags, flags
 
 
 @pytest.mark.parametrize("name", ["gait_rigid_forward", "gait_inverse_random", "rajagopal18_inverse",
