@@ -16,6 +16,7 @@
 #pragma once
 
 #include <IpIpoptApplication.hpp>
+#include <IpIpoptData.hpp>
 #include <IpTNLP.hpp>
 
 #include <stdexcept>
@@ -111,15 +112,17 @@ public:
         return mh_eval_jac_g(m_ctx, x, new_x, values) == MH_OK;
     }
     void finalize_solution(Ipopt::SolverReturn status, Index n, const Number* x, const Number*,
-            const Number*, Index, const Number*, const Number*, Number obj, const Ipopt::IpoptData*,
+            const Number*, Index, const Number*, const Number*, Number obj, const Ipopt::IpoptData* ip_data,
             Ipopt::IpoptCalculatedQuantities*) override {
         m_status = status;
         m_objective = obj;
         m_solution.assign(x, x + n);
+        m_iterations = ip_data ? ip_data->iter_count() : -1;
     }
 
     const std::vector<double>& solution() const { return m_solution; }
     double objective() const { return m_objective; }
+    int iterations() const { return m_iterations; }
     Ipopt::SolverReturn status() const { return m_status; }
 
 private:
@@ -128,6 +131,7 @@ private:
     std::vector<double> m_guess;
     std::vector<double> m_solution;
     double m_objective = 0.0;
+    int m_iterations = -1;
     Ipopt::SolverReturn m_status = Ipopt::UNASSIGNED;
 };
 
