@@ -634,11 +634,12 @@ extern "C" int mh_kkt_factor(mh_kkt* h, const double* w, const double* dc, int32
     KCHK(hipGetLastError());
     const size_t lds = sizeof(double) * r * r;
     const int use_lds = lds + 64 <= (size_t)LDS_MAX ? 1 : 0;
-    static bool attr_set = false;
-    if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)k_kkt_potrf, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
-        (void)hipFuncSetAttribute((const void*)k_kkt_trsm, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
-        attr_set = true;
+    if (use_lds && lds > 65536) {
+        // the block's own size (the attribute's maximum is the device's LDS
+        // minus the kernel's static LDS); a refused request would resurface
+        // as the next launch check's error, so it is checked here
+        KCHK(hipFuncSetAttribute((const void*)k_kkt_potrf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        KCHK(hipFuncSetAttribute((const void*)k_kkt_trsm, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     }
     for (const KLevel& L : h->levels) {
         hipLaunchKernelGGL(k_kkt_potrf, dim3((unsigned)L.n_odd), dim3(256), use_lds ? lds : 0, s, L.potrf, r,

@@ -70,19 +70,26 @@ def test_device_kkt_matches_restatement(name):
         A, _ = K.gather(bm, vals, rs)
         D, E = K.schur_blocks(bm, A, w, dc)
         Lf, U, Vf, levels = K.cr_factor(D, E)
+        # (S's condition number reaches ~1e8 here -- J's entries span
+        # orders of magnitude, dc ~ 1e-8 -- so two stable orderings of the
+        # same factorization agree to ~cond * eps, and the residual below
+        # is the sharp check)
         for k in (1, 5, 40):                                     # 40: two passes of 32 columns
             B = rng.standard_normal((nlp.m, k))
             Xr = K.from_blocks(bm, K.cr_solve(Lf, U, Vf, levels, K.to_blocks(bm, B)))
             Xg = dk.solve(B)
-            assert np.abs(Xg - Xr).max() <= 1e-9 * np.abs(Xr).max(), k
+            assert np.abs(Xg - Xr).max() <= 1e-6 * np.abs(Xr).max(), k
         # and the Schur complement itself: S X = B
         B = rng.standard_normal(nlp.m)
         X = dk.solve(B)
         Jb = J.tolil()
         Jb[:, bm.dcols] = 0.0
         Jb = Jb.tocsr()
-        resid = Jb @ (w * (Jb.T @ X)) + dc * X - B
-        assert np.abs(resid).max() <= 1e-8 * np.abs(B).max()
+        SX = Jb @ (w * (Jb.T @ X)) + dc * X
+        resid = SX - B
+        # backward error: the residual against |S| |X| (componentwise scale)
+        absS_absX = abs(Jb) @ (w * (abs(Jb).T @ np.abs(X))) + dc * np.abs(X) + np.abs(B)
+        assert (np.abs(resid) / absS_absX).max() <= 1e-12
     finally:
         nlp.close()
 

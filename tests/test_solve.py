@@ -250,9 +250,11 @@ def test_iterate_sequence_gpu_vs_oracle(linear_solver):
         assert len(hg) == len(ho) == k + 1
         worst = 0.0
         for a, b in zip(hg, ho):
+            dev = [abs(a[q] - b[q]) / max(1.0, abs(b[q])) for q in (1, 2, 3)]
+            print(f"  iter {a[0]:3d} mu {a[4]:.1e} f {a[1]: .10e} / {b[1]: .10e}  inf_pr {a[2]:.6e} / {b[2]:.6e}"
+                  f"  inf_du {a[3]:.6e} / {b[3]:.6e}  rel dev {max(dev):.1e}")
             assert a[0] == b[0] and a[4] == b[4], (a, b)          # iteration, mu
-            for q in (1, 2, 3):                                   # f, inf_pr, inf_du
-                worst = max(worst, abs(a[q] - b[q]) / max(1.0, abs(b[q])))
+            worst = max(worst, *dev)                              # f, inf_pr, inf_du
         dx = np.abs(out["gpu"].x - out["oracle"].x).max() / max(1.0, np.abs(out["oracle"].x).max())
         print(f"iterate sequence ({linear_solver}): max rel deviation of (f, inf_pr, inf_du) {worst:.2e}, "
               f"x after {k} iterations {dx:.2e}")

@@ -1,0 +1,28 @@
+"""Wall-clock of the configs[2] solve (muscle-driven MocoTrack
+gait10dof18musc, MocoTrack's settings) on the GPU path with the device or
+host linear algebra: one JSON line per run."""
+import json
+import sys
+import time
+
+sys.path.insert(0, "opensim-moco_amd")
+from mocohip import configs  # noqa: E402
+from mocohip.ipm import IpmOptions, solve_ipm  # noqa: E402
+
+N = int(sys.argv[1]) if len(sys.argv) > 1 else 200
+ls = sys.argv[2] if len(sys.argv) > 2 else "device"
+verbose = len(sys.argv) > 3
+st = configs.gait10dof18musc_track(N, muscles=True)
+t0 = time.perf_counter()
+nlp = st.create_nlp()
+setup = time.perf_counter() - t0
+x0 = st.solver.starting_point(nlp)
+o = IpmOptions.from_ipopt(st.solver.ipopt_options())
+o.linear_solver = ls
+o.print_level = 1 if verbose else 0
+r = solve_ipm(nlp, x0, o)
+print(json.dumps({"N": N, "linear_solver": r.timings.get("linear_solver"), "status": r.status,
+                  "iterations": r.iterations, "objective": r.objective, "wall_clock_s": round(r.duration, 3),
+                  "evaluations_s": round(r.timings["evaluations_s"], 3),
+                  "linear_algebra_s": round(r.timings["linear_algebra_s"], 3), "setup_s": round(setup, 2),
+                  "evaluations": r.evaluations, "n": nlp.n, "m": nlp.m, "nnz": nlp.nnz}), flush=True)
