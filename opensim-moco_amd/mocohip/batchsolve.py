@@ -4,10 +4,16 @@ interior-point solver (mocohip.ipm, the Ipopt restatement) -- all on one
 device, started together.  MocoInverse's setup: MocoInverse.cpp:46-120
 (configs.gait10dof18musc_inverse); subjects are the generic model scaled by
 (length, mass) factors (configs.scale_subject), which keep the generated
-back end (structure-only specialization)."""
+back end (structure-only specialization).
+
+Failures are reported, not raised: a worker whose setup fails still reaches
+the start barrier and posts its error, and the parent watches the workers
+while it waits, so a worker that dies (a crash, a GPU fault) becomes a
+failed entry of the batch instead of a hang."""
 from __future__ import annotations
 
 import multiprocessing as mp
+import queue
 import time
 from typing import List, Sequence, Tuple
 
@@ -20,52 +26,85 @@ def sweep(count: int) -> List[Tuple[float, float]]:
             for i in range(count)]
 
 
-def _worker(subject, num_mesh_intervals, device, start, out):
-    from . import configs
-    st = configs.gait10dof18musc_inverse(num_mesh_intervals, subject=subject)
-    st.solver.device = device
-    nlp = st.create_nlp()
-    start.wait()                                  # every solver built: go
+def _worker(index, subject, num_mesh_intervals, device, start, out, linear_solver):
+    nlp = None
+    res = {"subject": list(subject), "success": False}
+    try:
+        from . import configs
+        st = configs.gait10dof18musc_inverse(num_mesh_intervals, subject=subject)
+        st.solver.device = device
+        nlp = st.create_nlp()
+        if linear_solver == "device":
+            nlp.device_kkt()                  # the device KKT module built before the start
+    except Exception as e:   # setup failed: still meet the others at the barrier
+        res["error"] = "setup: " + repr(e)[:200]
+    try:
+        start.wait()                          # every solver built: go
+    except Exception:
+        pass
     t0 = time.perf_counter()
     try:
-        sol = st.solve(nlp=nlp)
-        r = sol.stats
-        res = {"subject": list(subject), "success": bool(r.success), "iterations": int(r.iterations),
-               "objective": float(r.objective), "wall_clock_s": round(time.perf_counter() - t0, 3),
-               "backend": nlp.backend()[0]}
+        if nlp is not None:
+            sol = st.solve(nlp=nlp, linear_solver=linear_solver)
+            r = sol.stats
+            res = {"subject": list(subject), "success": bool(r.success), "iterations": int(r.iterations),
+                   "objective": float(r.objective), "wall_clock_s": round(time.perf_counter() - t0, 3),
+                   "seconds_in_evaluations": round((r.timings or {}).get("evaluations_s", 0.0), 3),
+                   "seconds_in_kkt": round((r.timings or {}).get("linear_algebra_s", 0.0), 3),
+                   "linear_solver": (r.timings or {}).get("linear_solver"),
+                   "backend": nlp.backend()[0]}
     except Exception as e:   # reported, not raised: the batch line says which solve failed
         res = {"subject": list(subject), "success": False, "error": repr(e)[:200]}
     finally:
-        nlp.close()
-    out.put((time.perf_counter(), res))
+        if nlp is not None:
+            nlp.close()
+    out.put((index, time.perf_counter(), res))
 
 
 def solve_batch(subjects: Sequence[Tuple[float, float]], num_mesh_intervals: int = 125,
-                device: int = 0, timeout: float = 600.0) -> dict:
+                device: int = 0, timeout: float = 600.0, linear_solver: str = "auto") -> dict:
     """Solve every subject's MocoInverse at once, one process each; wall
     clock from the common start to the last solution."""
     ctx = mp.get_context("spawn")
     start = ctx.Barrier(len(subjects) + 1)
     out = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(s, num_mesh_intervals, device, start, out), daemon=True)
-             for s in subjects]
+    procs = [ctx.Process(target=_worker, args=(i, s, num_mesh_intervals, device, start, out, linear_solver),
+                         daemon=True)
+             for i, s in enumerate(subjects)]
     for p in procs:
         p.start()
-    start.wait(timeout=timeout)
+    try:
+        start.wait(timeout=timeout)
+    except Exception:      # a worker died before the barrier: the rest still run
+        start.abort()
     t0 = time.perf_counter()
-    results = []
+    results = {}
     t_last = t0
-    for _ in procs:
-        t, r = out.get(timeout=timeout)
-        t_last = max(t_last, t)
-        results.append(r)
+    deadline = t0 + timeout
+    while len(results) < len(procs) and time.perf_counter() < deadline:
+        try:
+            i, t, r = out.get(timeout=1.0)
+            results[i] = r
+            t_last = max(t_last, t)
+        except queue.Empty:
+            # a worker that exited without posting crashed: record it
+            for i, p in enumerate(procs):
+                if i not in results and not p.is_alive() and p.exitcode not in (0, None):
+                    results[i] = {"subject": list(subjects[i]), "success": False,
+                                  "error": f"worker exited with code {p.exitcode}"}
+    for i in range(len(procs)):
+        results.setdefault(i, {"subject": list(subjects[i]), "success": False, "error": "timeout"})
     for p in procs:
         p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
     wall = t_last - t0
-    ok = [r for r in results if r.get("success")]
+    res = [results[i] for i in range(len(procs))]
+    ok = [r for r in res if r.get("success")]
     return {"solves": len(subjects), "processes": len(procs), "succeeded": len(ok),
             "wall_clock_s": round(wall, 3),
             "solves_per_minute": round(60.0 * len(subjects) / wall, 2) if wall > 0 else None,
             "mean_iterations": round(sum(r["iterations"] for r in ok) / len(ok), 1) if ok else None,
             "mean_solve_s": round(sum(r["wall_clock_s"] for r in ok) / len(ok), 3) if ok else None,
-            "results": sorted(results, key=lambda r: r["subject"])}
+            "linear_solver": ok[0].get("linear_solver") if ok else None,
+            "results": sorted(res, key=lambda r: r["subject"])}

@@ -126,7 +126,7 @@ class IpmOptions:
         max_iter, print_level ...); unknown keys are ignored."""
         o = cls()
         for k, v in opts.items():
-            if hasattr(o, k) and not isinstance(v, str):
+            if hasattr(o, k) and (not isinstance(v, str) or isinstance(getattr(o, k), str)):
                 setattr(o, k, type(getattr(o, k))(v))
         return o
 

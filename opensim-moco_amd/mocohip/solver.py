@@ -695,7 +695,7 @@ class MocoStudy:
         rep = self.problem.create_rep()
         return HipNLP(rep, self.solver.options(interval_begin, interval_end))
 
-    def solve(self, guess=None, nlp=None, method: str = "ipm"):
+    def solve(self, guess=None, nlp=None, method: str = "ipm", linear_solver: str = "auto"):
         """MocoStudy::solve (MocoStudy.cpp:79-101): transcribe on the HIP
         path, optimize from the solver's starting point, return the
         solution as a MocoTrajectory with the solve statistics in its
@@ -705,7 +705,10 @@ class MocoStudy:
         interior-point restatement mocohip.ipm) with the Ipopt options
         MocoCasADiSolver sets from optim_convergence_tolerance /
         optim_constraint_tolerance / optim_max_iterations
-        (MocoHipSolver.ipopt_options; Ipopt's defaults where unset)."""
+        (MocoHipSolver.ipopt_options; Ipopt's defaults where unset).
+        linear_solver: the Newton systems' back end (mocohip.ipm
+        IpmOptions.linear_solver: "auto" = on the device next to the
+        Jacobian when the NLP offers it)."""
         from .nlpsolve import solve_nlp
         from .trajectory import MocoTrajectory
         own = nlp is None
@@ -716,8 +719,10 @@ class MocoStudy:
             tol = s.optim_convergence_tolerance if s.optim_convergence_tolerance > 0 else 1e-8
             ctol = s.optim_constraint_tolerance if s.optim_constraint_tolerance > 0 else 1e-8
             it = s.optim_max_iterations if s.optim_max_iterations > 0 else 5000
-            r = solve_nlp(nlp, x0, tol, ctol, it, method=method,
-                          ipopt_options=s.ipopt_options() if method == "ipm" else None)
+            opts = s.ipopt_options() if method == "ipm" else None
+            if opts is not None:
+                opts["linear_solver"] = linear_solver
+            r = solve_nlp(nlp, x0, tol, ctol, it, method=method, ipopt_options=opts)
             sol = MocoTrajectory.from_iterate(nlp, r.x)
         finally:
             if own:
