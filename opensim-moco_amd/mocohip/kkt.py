@@ -37,6 +37,7 @@ logic and its vectors; J never leaves the device.
 from __future__ import annotations
 
 import ctypes as C
+import time
 from dataclasses import dataclass
 
 import numpy as np
@@ -228,6 +229,13 @@ class DeviceKKT:
         self.h = C.c_void_p()
         self._check(self.lib.mh_kkt_create(nlp.ctx, C.byref(L), C.byref(self.h)))
         self.m, self.n, self.nd = b.m, b.n, b.nd
+        self.stats = {}          # op -> [calls, seconds, columns] (host wall clock per C-ABI call)
+
+    def _tick(self, op, t0, k=1):
+        s = self.stats.setdefault(op, [0, 0.0, 0])
+        s[0] += 1
+        s[1] += time.perf_counter() - t0
+        s[2] += k
 
     def _check(self, rc):
         if rc:
@@ -242,7 +250,9 @@ class DeviceKKT:
         """J(x) evaluated on the device (the context's eval_jac_g kernels)
         into the module's own buffer and gathered into the blocks."""
         x = np.ascontiguousarray(x, float)
+        t0 = time.perf_counter()
         self._check(self.lib.mh_kkt_eval_jacobian(self.h, _dp(x)))
+        self._tick("eval_jacobian", t0)
 
     def dense_columns(self):
         """(global column indices, row-scaled values m x nd)."""
@@ -263,7 +273,9 @@ class DeviceKKT:
         w = np.ascontiguousarray(w, float)
         dc = np.ascontiguousarray(dc, float)
         ok = C.c_int32()
+        t0 = time.perf_counter()
         self._check(self.lib.mh_kkt_factor(self.h, _dp(w), _dp(dc), C.byref(ok)))
+        self._tick("factor", t0)
         return bool(ok.value)
 
     def _k(self, a, rows):
@@ -276,21 +288,27 @@ class DeviceKKT:
         """S^-1 b (b: m or m x k)."""
         b, k = self._k(b, self.m)
         out = np.empty_like(b)
+        t0 = time.perf_counter()
         self._check(self.lib.mh_kkt_solve(self.h, k, _dp(b), _dp(out)))
+        self._tick("solve", t0, k)
         return out
 
     def jmul(self, v):
         """R J v (v: n or n x k; every column, dense ones included)."""
         v, k = self._k(v, self.n)
         out = np.empty((self.m,) + v.shape[1:])
+        t0 = time.perf_counter()
         self._check(self.lib.mh_kkt_jmul(self.h, k, _dp(v), _dp(out)))
+        self._tick("jmul", t0, k)
         return out
 
     def jtmul(self, y):
         """J^T R y (y: m or m x k)."""
         y, k = self._k(y, self.m)
         out = np.empty((self.n,) + y.shape[1:])
+        t0 = time.perf_counter()
         self._check(self.lib.mh_kkt_jtmul(self.h, k, _dp(y), _dp(out)))
+        self._tick("jtmul", t0, k)
         return out
 
     def close(self):

@@ -25,4 +25,6 @@ print(json.dumps({"N": N, "linear_solver": r.timings.get("linear_solver"), "stat
                   "iterations": r.iterations, "objective": r.objective, "wall_clock_s": round(r.duration, 3),
                   "evaluations_s": round(r.timings["evaluations_s"], 3),
                   "linear_algebra_s": round(r.timings["linear_algebra_s"], 3), "setup_s": round(setup, 2),
-                  "evaluations": r.evaluations, "n": nlp.n, "m": nlp.m, "nnz": nlp.nnz}), flush=True)
+                  "evaluations": r.evaluations, "n": nlp.n, "m": nlp.m, "nnz": nlp.nnz,
+                  "kkt_ops": {k: [v[0], round(v[1], 4), v[2]] for k, v in
+                              (getattr(getattr(nlp, "_dkkt", None), "stats", {}) or {}).items()}}), flush=True)
