@@ -24,7 +24,7 @@
 //                  and every update of the cyclic reduction;
 //   k_kkt_potrf    in-place Cholesky of one block per workgroup (in LDS when
 //                  it fits: r <= 143);
-//   k_kkt_trsm     L^-1 B / L^-T B, one column per lane;
+//   k_kkt_trsm     L^-1 B / L^-T B, blocked by 16 rows in LDS (diagonal blocks one lane per column, the rest by the workgroup);
 // and block cyclic reduction over them: at level l the active blocks are
 // every 2^l-th, the odd ones are eliminated in parallel (L_i L_i^T = D_i,
 // U_i = L_i^-1 S[i, left], V_i = L_i^-1 S[i, right]) and the even ones
@@ -208,10 +208,11 @@ __global__ __launch_bounds__(256) void k_kkt_potrf(double* const* __restrict__ m
         const double djj = s[j * r + j];
         for (int i = j + 1 + tid; i < r; i += nt) s[i * r + j] /= djj;
         __syncthreads();
-        const int m = r - j - 1;
-        for (int e = tid; e < m * m; e += nt) {
-            const int i = j + 1 + e / m, k = j + 1 + e % m;
-            if (k <= i) s[i * r + k] -= s[i * r + j] * s[k * r + j];
+        // trailing update of the lower triangle, threads as a 16 x (nt/16) grid
+        const int tx = tid & 15, ty = tid >> 4, ny = nt >> 4;
+        for (int i = j + 1 + ty; i < r; i += ny) {
+            const double lij = s[i * r + j];
+            for (int k = j + 1 + tx; k <= i; k += 16) s[i * r + k] -= lij * s[k * r + j];
         }
     }
     __syncthreads();
@@ -220,36 +221,73 @@ __global__ __launch_bounds__(256) void k_kkt_potrf(double* const* __restrict__ m
     if (tid == 0 && bad) *status = 1;
 }
 
-// X = L^-1 B (trans = 0) or L^-T B (trans = 1), one column of B per lane,
+// X = L^-1 B (trans = 0) or L^-T B (trans = 1) for the JW columns j0.. of
+// one task per workgroup (blockIdx.x: column chunk, blockIdx.y: task);
 // B(i, j) = B[i bsi + j bsj], X(i, j) = X[i ldx + j] (in place when B == X
-// with the same strides); L staged in dynamic LDS when use_lds.
-__global__ __launch_bounds__(64) void k_kkt_trsm(const KTri* __restrict__ tasks, int r, int ncols, int bsi, int bsj,
-                                                 int ldx, int trans, int use_lds) {
-    extern __shared__ double Ls[];
+// with the same strides).  Blocked by TB rows: the chunk of X is staged in
+// LDS, each diagonal TB x TB block is solved by one lane per column, and the
+// rows below (above, for L^T) are updated by the whole workgroup with the
+// block's TB columns of L -- r / TB barriers instead of a sequential
+// r^2 / 2 chain per lane.  L is staged in LDS as well when use_lds.
+constexpr int TRSM_TB = 16;
+__global__ __launch_bounds__(256) void k_kkt_trsm(const KTri* __restrict__ tasks, int r, int ncols, int bsi, int bsj,
+                                                  int ldx, int trans, int use_lds, int JW) {
+    extern __shared__ double lds[];
     const KTri t = tasks[blockIdx.y];
+    const int tid = threadIdx.x, nt = blockDim.x;
+    const int j0 = blockIdx.x * JW;
+    const int jw = min(JW, ncols - j0);
+    double* Xs = lds;                                   // [r][JW]
     const double* L = t.L;
     if (use_lds) {
-        for (int e = threadIdx.x; e < r * r; e += blockDim.x) Ls[e] = t.L[e];
-        __syncthreads();
+        double* Ls = lds + (size_t)r * JW;
+        for (int e = tid; e < r * r; e += nt) Ls[e] = t.L[e];
         L = Ls;
     }
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= ncols) return;
-    double* x = t.X + j;
-    const double* B = t.B + (int64_t)j * bsj;
-    if (!trans) {
-        for (int i = 0; i < r; ++i) {
-            double s = B[(int64_t)i * bsi];
-            const double* Li = L + (int64_t)i * r;
-            for (int k = 0; k < i; ++k) s -= Li[k] * x[(int64_t)k * ldx];
-            x[(int64_t)i * ldx] = s / Li[i];
+    for (int e = tid; e < r * jw; e += nt) {
+        const int i = e / jw, j = e - i * jw;
+        Xs[i * JW + j] = t.B[(int64_t)i * bsi + (int64_t)(j0 + j) * bsj];
+    }
+    __syncthreads();
+    const int ntile = (r + TRSM_TB - 1) / TRSM_TB;
+    for (int q = 0; q < ntile; ++q) {
+        const int tt = trans ? ntile - 1 - q : q;
+        const int a = tt * TRSM_TB, b = min(r, a + TRSM_TB);
+        // the diagonal block, one lane per column
+        if (tid < jw) {
+            double* x = Xs + tid;
+            if (!trans) {
+                for (int i = a; i < b; ++i) {
+                    double s = x[i * JW];
+                    for (int k = a; k < i; ++k) s -= L[(int64_t)i * r + k] * x[k * JW];
+                    x[i * JW] = s / L[(int64_t)i * r + i];
+                }
+            } else {
+                for (int i = b - 1; i >= a; --i) {
+                    double s = x[i * JW];
+                    for (int k = i + 1; k < b; ++k) s -= L[(int64_t)k * r + i] * x[k * JW];
+                    x[i * JW] = s / L[(int64_t)i * r + i];
+                }
+            }
         }
-    } else {
-        for (int i = r - 1; i >= 0; --i) {
-            double s = B[(int64_t)i * bsi];
-            for (int k = i + 1; k < r; ++k) s -= L[(int64_t)k * r + i] * x[(int64_t)k * ldx];
-            x[(int64_t)i * ldx] = s / L[(int64_t)i * r + i];
+        __syncthreads();
+        // the remaining rows: below the block (L), above it (L^T)
+        const int lo = trans ? 0 : b, hi = trans ? a : r;
+        const int nrow = hi - lo;
+        for (int e = tid; e < nrow * jw; e += nt) {
+            const int i = lo + e / jw, j = e % jw;
+            double s = Xs[i * JW + j];
+            if (!trans)
+                for (int k = a; k < b; ++k) s -= L[(int64_t)i * r + k] * Xs[k * JW + j];
+            else
+                for (int k = a; k < b; ++k) s -= L[(int64_t)k * r + i] * Xs[k * JW + j];
+            Xs[i * JW + j] = s;
         }
+        __syncthreads();
+    }
+    for (int e = tid; e < r * jw; e += nt) {
+        const int i = e / jw, j = e - i * jw;
+        t.X[(int64_t)i * ldx + j0 + j] = Xs[i * JW + j];
     }
 }
 
@@ -607,13 +645,29 @@ static void launch_gemm(hipStream_t s, const KTask* tasks, int ntasks, int M, in
                        K, psi, psk, qsi, qsk, ldc, alpha, beta);
 }
 
+// LDS plan of k_kkt_trsm for blocks of r rows: (use_lds, JW, bytes)
+static void trsm_plan(int r, int& use_lds, int& JW, size_t& bytes) {
+    const size_t cap = (size_t)LDS_MAX - 1024;
+    for (int jw : {64, 32, 16, 8}) {
+        if (sizeof(double) * ((size_t)r * r + (size_t)r * jw) <= cap) {
+            use_lds = 1; JW = jw; bytes = sizeof(double) * ((size_t)r * r + (size_t)r * jw);
+            return;
+        }
+    }
+    use_lds = 0;
+    JW = 64;
+    while (JW > 8 && sizeof(double) * (size_t)r * JW > cap) JW /= 2;
+    bytes = sizeof(double) * (size_t)r * JW;
+}
+
 static void launch_trsm(hipStream_t s, const KTri* tasks, int ntasks, int r, int ncols, int bsi, int bsj, int ldx,
                         int trans) {
     if (ntasks <= 0) return;
-    const size_t lds = sizeof(double) * r * r;
-    const int use = lds + 64 <= (size_t)LDS_MAX ? 1 : 0;
-    hipLaunchKernelGGL(k_kkt_trsm, dim3(nblk(ncols, 64), (unsigned)ntasks), dim3(64), use ? lds : 0, s, tasks, r,
-                       ncols, bsi, bsj, ldx, trans, use);
+    int use, JW;
+    size_t lds;
+    trsm_plan(r, use, JW, lds);
+    hipLaunchKernelGGL(k_kkt_trsm, dim3(nblk(ncols, JW), (unsigned)ntasks), dim3(256), lds, s, tasks, r, ncols,
+                       bsi, bsj, ldx, trans, use, JW);
 }
 
 extern "C" int mh_kkt_factor(mh_kkt* h, const double* w, const double* dc, int32_t* ok) {
@@ -634,12 +688,17 @@ extern "C" int mh_kkt_factor(mh_kkt* h, const double* w, const double* dc, int32
     KCHK(hipGetLastError());
     const size_t lds = sizeof(double) * r * r;
     const int use_lds = lds + 64 <= (size_t)LDS_MAX ? 1 : 0;
-    if (use_lds && lds > 65536) {
-        // the block's own size (the attribute's maximum is the device's LDS
-        // minus the kernel's static LDS); a refused request would resurface
-        // as the next launch check's error, so it is checked here
+    // the blocks' own LDS sizes (the attribute's maximum is the device's LDS
+    // minus the kernel's static LDS); a refused request would resurface as
+    // the next launch check's error, so it is checked here
+    if (use_lds && lds > 65536)
         KCHK(hipFuncSetAttribute((const void*)k_kkt_potrf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        KCHK(hipFuncSetAttribute((const void*)k_kkt_trsm, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    {
+        int tu, tj;
+        size_t tl;
+        trsm_plan(r, tu, tj, tl);
+        if (tl > 65536)
+            KCHK(hipFuncSetAttribute((const void*)k_kkt_trsm, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tl));
     }
     for (const KLevel& L : h->levels) {
         hipLaunchKernelGGL(k_kkt_potrf, dim3((unsigned)L.n_odd), dim3(256), use_lds ? lds : 0, s, L.potrf, r,
