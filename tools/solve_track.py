@@ -2,10 +2,11 @@
 gait10dof18musc, MocoTrack's settings) on the GPU path with the device or
 host linear algebra: one JSON line per run."""
 import json
+import os
 import sys
 import time
 
-sys.path.insert(0, "opensim-moco_amd")
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "opensim-moco_amd"))
 from mocohip import configs  # noqa: E402
 from mocohip.ipm import IpmOptions, solve_ipm  # noqa: E402
 
