@@ -34,6 +34,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
+#include <functional>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -63,12 +65,32 @@ namespace {
 constexpr int KMAX = 32;              // right-hand sides per solve pass
 constexpr int LDS_MAX = 160 * 1024;   // gfx950 LDS per workgroup
 
-struct KTask { const double* P; const double* Q; const double* w; double* C; };
+// C = alpha (P diag(w) Q^T + P2 Q2^T) + beta C (P2 null: the first product only)
+struct KTask { const double* P; const double* Q; const double* w; double* C; const double* P2; const double* Q2; };
 struct KTri { const double* L; const double* B; double* X; };
 
 // ------------------------------------------------------------------------
 // kernels
 // ------------------------------------------------------------------------
+// n doubles global -> LDS with U loads in flight per thread before the
+// first store (a plain loop waits for each load's round trip in turn)
+template <int U>
+__device__ __forceinline__ void stage(double* __restrict__ dst, const double* __restrict__ src, int n) {
+    for (int b = 0; b < n; b += U * (int)blockDim.x) {
+        double v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = b + u * (int)blockDim.x + (int)threadIdx.x;
+            v[u] = src[i < n ? i : n - 1];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = b + u * (int)blockDim.x + (int)threadIdx.x;
+            if (i < n) dst[i] = v[u];
+        }
+    }
+}
+
 __global__ void k_kkt_gather(int64_t na, int c, const int32_t* __restrict__ src, const int32_t* __restrict__ rowmap,
                              const double* __restrict__ vals, const double* __restrict__ rs,
                              double* __restrict__ A) {
@@ -133,6 +155,11 @@ __global__ __launch_bounds__(256) void k_kkt_gemm(const KTask* __restrict__ task
     for (int a = 0; a < 4; ++a)
 #pragma unroll
         for (int b = 0; b < 4; ++b) acc[a][b] = 0.0;
+    const int npair = t.P2 ? 2 : 1;
+    for (int pr = 0; pr < npair; ++pr) {
+    const double* __restrict__ Pp = pr ? t.P2 : t.P;
+    const double* __restrict__ Qp = pr ? t.Q2 : t.Q;
+    const double* __restrict__ wp = pr ? nullptr : t.w;
     for (int k0 = 0; k0 < K; k0 += TK) {
         for (int e = tid; e < TM * TK; e += 256) {
             int ii, kk;
@@ -140,8 +167,8 @@ __global__ __launch_bounds__(256) void k_kkt_gemm(const KTask* __restrict__ task
             const int gi = i0 + ii, gk = k0 + kk;
             double v = 0.0;
             if (gi < M && gk < K) {
-                v = t.P[(int64_t)gi * psi + (int64_t)gk * psk];
-                if (t.w) v *= t.w[gk];
+                v = Pp[(int64_t)gi * psi + (int64_t)gk * psk];
+                if (wp) v *= wp[gk];
             }
             Ps[kk][ii] = v;
         }
@@ -149,7 +176,7 @@ __global__ __launch_bounds__(256) void k_kkt_gemm(const KTask* __restrict__ task
             int jj, kk;
             if (qsk == 1) { jj = e / TK; kk = e % TK; } else { kk = e / TN; jj = e % TN; }
             const int gj = j0 + jj, gk = k0 + kk;
-            Qs[kk][jj] = (gj < N && gk < K) ? t.Q[(int64_t)gj * qsi + (int64_t)gk * qsk] : 0.0;
+            Qs[kk][jj] = (gj < N && gk < K) ? Qp[(int64_t)gj * qsi + (int64_t)gk * qsk] : 0.0;
         }
         __syncthreads();
 #pragma unroll
@@ -165,6 +192,7 @@ __global__ __launch_bounds__(256) void k_kkt_gemm(const KTask* __restrict__ task
                 for (int b = 0; b < 4; ++b) acc[a][b] = fma(p[a], q[b], acc[a][b]);
         }
         __syncthreads();
+    }
     }
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
@@ -191,8 +219,7 @@ __global__ __launch_bounds__(256) void k_kkt_potrf(double* const* __restrict__ m
     double* a = mats[blockIdx.x];
     double* s = use_lds ? lds : a;
     const int tid = threadIdx.x, nt = blockDim.x;
-    if (use_lds)
-        for (int e = tid; e < r * r; e += nt) s[e] = a[e];
+    if (use_lds) stage<8>(s, a, r * r);
     if (tid == 0) bad = 0;
     for (int j = 0; j < r; ++j) {
         __syncthreads();
@@ -241,12 +268,25 @@ __global__ __launch_bounds__(256) void k_kkt_trsm(const KTri* __restrict__ tasks
     const double* L = t.L;
     if (use_lds) {
         double* Ls = lds + (size_t)r * JW;
-        for (int e = tid; e < r * r; e += nt) Ls[e] = t.L[e];
+        stage<8>(Ls, t.L, r * r);
         L = Ls;
     }
-    for (int e = tid; e < r * jw; e += nt) {
-        const int i = e / jw, j = e - i * jw;
-        Xs[i * JW + j] = t.B[(int64_t)i * bsi + (int64_t)(j0 + j) * bsj];
+    for (int e0 = 0; e0 < r * jw; e0 += 4 * nt) {
+        double v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int e = min(e0 + u * nt + tid, r * jw - 1);
+            const int i = e / jw, j = e - i * jw;
+            v[u] = t.B[(int64_t)i * bsi + (int64_t)(j0 + j) * bsj];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int e = e0 + u * nt + tid;
+            if (e < r * jw) {
+                const int i = e / jw, j = e - i * jw;
+                Xs[i * JW + j] = v[u];
+            }
+        }
     }
     __syncthreads();
     const int ntile = (r + TRSM_TB - 1) / TRSM_TB;
@@ -388,18 +428,15 @@ inline unsigned nblk(int64_t n, int t) { return (unsigned)((n + t - 1) / t); }
 // ------------------------------------------------------------------------
 struct KLevel {
     // factor
-    KTask* gemm_vv = nullptr;  int n_vv = 0;   // D[right] -= V^T V
-    KTask* gemm_uu = nullptr;  int n_uu = 0;   // D[left]  -= U^T U
-    KTask* gemm_e = nullptr;   int n_e = 0;    // E[left]   = -V^T U
+    KTask* gemm_d = nullptr;   int n_d = 0;    // even j: D_j -= V_{j-1}^T V_{j-1} + U_{j+1}^T U_{j+1}
+    KTask* gemm_e = nullptr;   int n_e = 0;    // even j: E_j = -V_{j+1}^T U_{j+1} (the new coupling j+2 -> j)
     double** potrf = nullptr;  int n_odd = 0;
     KTri* tri_u = nullptr;     int n_u = 0;    // U = L^-1 E[left] (every odd block but the last level's)
     KTri* tri_v = nullptr;     int n_v = 0;    // V = L^-1 E[i]^T
     // solve
     KTri* sol = nullptr;                       // X_i in place
-    KTask* fwd_v = nullptr;                    // X[right] -= V^T X_i   (n_v)
-    KTask* fwd_u = nullptr;                    // X[left]  -= U^T X_i   (n_u)
-    KTask* bwd_u = nullptr;                    // X_i -= U X[left]      (n_u)
-    KTask* bwd_v = nullptr;                    // X_i -= V X[right]     (n_v)
+    KTask* fwd = nullptr;                      // even j: X_j -= V_{j-1}^T X_{j-1} + U_{j+1}^T X_{j+1}  (n_d)
+    KTask* bwd = nullptr;                      // odd i: X_i -= U_i X[left] + V_i X[right]            (n_u)
 };
 
 struct mh_kkt {
@@ -419,6 +456,12 @@ struct mh_kkt {
     std::vector<KLevel> levels;      // the last level holds the single remaining block
     std::vector<void*> allocs;
     bool factored = false;
+    // the factorization's and each solve width's kernel sequences as HIP
+    // graphs (captured on first use; every pointer they take is fixed at
+    // create): one launch per call instead of ~50 (MOCOHIP_KKT_GRAPHS=0: off)
+    bool graphs = true;
+    hipGraphExec_t g_factor = nullptr;
+    hipGraphExec_t g_solve[KMAX + 1] = {};
 };
 
 template <typename T>
@@ -447,6 +490,9 @@ static int kupload(mh_kkt* h, T** p, const T* src, size_t count) {
 extern "C" void mh_kkt_destroy(mh_kkt* h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
+    if (h->g_factor) (void)hipGraphExecDestroy(h->g_factor);
+    for (auto& g : h->g_solve)
+        if (g) (void)hipGraphExecDestroy(g);
     for (void* p : h->allocs) (void)hipFree(p);
     delete h;
 }
@@ -465,47 +511,61 @@ static int build_levels(mh_kkt* h) {
         KLevel L;
         std::vector<double*> potrf;
         std::vector<KTri> tu, tv, sol;
-        std::vector<KTask> vv, uu, ee, fv, fu, bu, bv;
-        if (active.size() == 1) {
+        std::vector<KTask> dd, ee, fw, bw;
+        const int na = (int)active.size();
+        if (na == 1) {
             const int i = active[0];
             potrf.push_back(Dp(i));
             sol.push_back({Dp(i), Xp(i), Xp(i)});
         } else {
-            for (size_t k = 1; k < active.size(); k += 2) {
+            // odd positions: eliminated (their factors, U, V)
+            for (int k = 1; k < na; k += 2) {
                 const int i = active[k], left = active[k - 1];
-                const int right = k + 1 < active.size() ? active[k + 1] : -1;
+                const int right = k + 1 < na ? active[k + 1] : -1;
                 potrf.push_back(Dp(i));
                 sol.push_back({Dp(i), Xp(i), Xp(i)});
                 tu.push_back({Dp(i), Ep(left), Up(i)});
-                uu.push_back({Up(i), Up(i), nullptr, Dp(left)});
-                fu.push_back({Up(i), Xp(i), nullptr, Xp(left)});
-                bu.push_back({Up(i), Xp(left), nullptr, Xp(i)});
                 if (right >= 0) {
                     tv.push_back({Dp(i), Ep(i), Vp(i)});
-                    vv.push_back({Vp(i), Vp(i), nullptr, Dp(right)});
-                    ee.push_back({Vp(i), Up(i), nullptr, Ep(left)});
-                    fv.push_back({Vp(i), Xp(i), nullptr, Xp(right)});
-                    bv.push_back({Vp(i), Xp(right), nullptr, Xp(i)});
+                    bw.push_back({Up(i), Xp(left), nullptr, Xp(i), Vp(i), Xp(right)});
+                } else {
+                    bw.push_back({Up(i), Xp(left), nullptr, Xp(i), nullptr, nullptr});
                 }
+            }
+            // even positions: updated from the odd neighbours, the left one's
+            // V first, then the right one's U (one output tile per thread,
+            // fixed order: deterministic)
+            for (int k = 0; k < na; k += 2) {
+                const int j = active[k];
+                const int il = k - 1 >= 0 ? active[k - 1] : -1, ir = k + 1 < na ? active[k + 1] : -1;
+                if (il >= 0 && ir >= 0) {
+                    dd.push_back({Vp(il), Vp(il), nullptr, Dp(j), Up(ir), Up(ir)});
+                    fw.push_back({Vp(il), Xp(il), nullptr, Xp(j), Up(ir), Xp(ir)});
+                } else if (il >= 0) {
+                    dd.push_back({Vp(il), Vp(il), nullptr, Dp(j), nullptr, nullptr});
+                    fw.push_back({Vp(il), Xp(il), nullptr, Xp(j), nullptr, nullptr});
+                } else if (ir >= 0) {
+                    dd.push_back({Up(ir), Up(ir), nullptr, Dp(j), nullptr, nullptr});
+                    fw.push_back({Up(ir), Xp(ir), nullptr, Xp(j), nullptr, nullptr});
+                }
+                if (ir >= 0 && k + 2 < na) ee.push_back({Vp(ir), Up(ir), nullptr, Ep(j), nullptr, nullptr});
             }
         }
         int rc = 0;
         L.n_odd = (int)potrf.size();
         L.n_u = (int)tu.size();
         L.n_v = (int)tv.size();
-        L.n_vv = (int)vv.size();
-        L.n_uu = (int)uu.size();
+        L.n_d = (int)dd.size();
         L.n_e = (int)ee.size();
         if ((rc = kupload(h, &L.potrf, potrf)) || (rc = kupload(h, &L.sol, sol)) ||
             (rc = kupload(h, &L.tri_u, tu)) || (rc = kupload(h, &L.tri_v, tv)) ||
-            (rc = kupload(h, &L.gemm_vv, vv)) || (rc = kupload(h, &L.gemm_uu, uu)) ||
-            (rc = kupload(h, &L.gemm_e, ee)) || (rc = kupload(h, &L.fwd_v, fv)) ||
-            (rc = kupload(h, &L.fwd_u, fu)) || (rc = kupload(h, &L.bwd_u, bu)) || (rc = kupload(h, &L.bwd_v, bv)))
+            (rc = kupload(h, &L.gemm_d, dd)) || (rc = kupload(h, &L.gemm_e, ee)) ||
+            (rc = kupload(h, &L.fwd, fw)) || (rc = kupload(h, &L.bwd, bw)))
             return rc;
         h->levels.push_back(L);
-        if (active.size() == 1) break;
+        if (na == 1) break;
         std::vector<int> next;
-        for (size_t k = 0; k < active.size(); k += 2) next.push_back(active[k]);
+        for (int k = 0; k < na; k += 2) next.push_back(active[k]);
         active.swap(next);
     }
     return MH_OK;
@@ -548,6 +608,7 @@ extern "C" int mh_kkt_create(mh_ctx* ctx, const mh_kkt_layout* L, mh_kkt** out) 
     h->nb = L->nblocks; h->r = L->r; h->c = L->c; h->nd = L->nd; h->P = L->nshare;
     h->m = m; h->n = n; h->nnz = nnz;
     h->lshare.assign(L->lshare, L->lshare + h->nb);
+    if (const char* eg = std::getenv("MOCOHIP_KKT_GRAPHS")) h->graphs = std::atoi(eg) != 0;
     h->rshare.assign(L->rshare, L->rshare + h->nb);
     auto fail = [&](int code) { mh_kkt_destroy(h); return code; };
     if (hipSetDevice(h->device) != hipSuccess) return fail(mh_internal_error(MH_ERR_HIP, "hipSetDevice failed"));
@@ -573,11 +634,11 @@ extern "C" int mh_kkt_create(mh_ctx* ctx, const mh_kkt_layout* L, mh_kkt** out) 
         return fail(mh_internal_error(MH_ERR_HIP, "upload failed"));
     std::vector<KTask> ts, te;
     for (int b = 0; b < h->nb; ++b) ts.push_back({h->A + (size_t)b * h->r * h->c, h->A + (size_t)b * h->r * h->c,
-                                                 h->wl + (size_t)b * h->c, h->D + rr * b});
+                                                 h->wl + (size_t)b * h->c, h->D + rr * b, nullptr, nullptr});
     for (int b = 0; b + 1 < h->nb; ++b)
         te.push_back({h->A + (size_t)(b + 1) * h->r * h->c + h->lshare[b + 1],
                       h->A + (size_t)b * h->r * h->c + h->rshare[b], h->wl + (size_t)b * h->c + h->rshare[b],
-                      h->E + rr * b});
+                      h->E + rr * b, nullptr, nullptr});
     if ((rc = kupload(h, &h->t_schur, ts)) || (rc = kupload(h, &h->t_e, te)) || (rc = build_levels(h)))
         return fail(rc);
     *out = h;
@@ -670,6 +731,30 @@ static void launch_trsm(hipStream_t s, const KTri* tasks, int ntasks, int r, int
                        bsi, bsj, ldx, trans, use, JW);
 }
 
+// Run a fixed kernel sequence on s: replayed from its HIP graph, captured
+// from the sequence itself on first use.
+static int run_sequence(mh_kkt* h, hipStream_t s, hipGraphExec_t& exec, const std::function<void()>& enqueue) {
+    if (!h->graphs) {
+        enqueue();
+        KCHK(hipGetLastError());
+        return MH_OK;
+    }
+    if (!exec) {
+        (void)hipGetLastError();
+        KCHK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+        enqueue();
+        hipGraph_t g = nullptr;
+        const hipError_t le = hipGetLastError();
+        KCHK(hipStreamEndCapture(s, &g));
+        KCHK(le);
+        const hipError_t ei = hipGraphInstantiate(&exec, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        KCHK(ei);
+    }
+    KCHK(hipGraphLaunch(exec, s));
+    return MH_OK;
+}
+
 extern "C" int mh_kkt_factor(mh_kkt* h, const double* w, const double* dc, int32_t* ok) {
     if (!h || !w || !dc || !ok) return mh_internal_error(MH_ERR_INVALID, "null argument");
     KCHK(hipSetDevice(h->device));
@@ -678,14 +763,6 @@ extern "C" int mh_kkt_factor(mh_kkt* h, const double* w, const double* dc, int32
     KCHK(hipMemcpyAsync(h->w, w, sizeof(double) * h->n, hipMemcpyHostToDevice, s));
     KCHK(hipMemcpyAsync(h->dc, dc, sizeof(double) * h->m, hipMemcpyHostToDevice, s));
     KCHK(hipMemsetAsync(h->status, 0, sizeof(int), s));
-    const int nbc = h->nb * h->c, nbr = h->nb * r;
-    hipLaunchKernelGGL(k_kkt_local, dim3(nblk(std::max(nbc, nbr), 256)), dim3(256), 0, s, nbc, nbr, h->colmap,
-                       h->rowmap, h->w, h->dc, h->wl, h->dcl);
-    // D_b = A_b W_b A_b^T + diag(dc_b); E_b = A_{b+1}[:, shared] W A_b[:, shared]^T
-    launch_gemm(s, h->t_schur, h->nb, r, r, h->c, h->c, 1, h->c, 1, r, 1.0, 0.0);
-    hipLaunchKernelGGL(k_kkt_add_diag, dim3(h->nb), dim3(256), 0, s, r, h->dcl, h->D);
-    launch_gemm(s, h->t_e, h->nb - 1, r, r, h->P, h->c, 1, h->c, 1, r, 1.0, 0.0);
-    KCHK(hipGetLastError());
     const size_t lds = sizeof(double) * r * r;
     const int use_lds = lds + 64 <= (size_t)LDS_MAX ? 1 : 0;
     // the blocks' own LDS sizes (the attribute's maximum is the device's LDS
@@ -700,18 +777,26 @@ extern "C" int mh_kkt_factor(mh_kkt* h, const double* w, const double* dc, int32
         if (tl > 65536)
             KCHK(hipFuncSetAttribute((const void*)k_kkt_trsm, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tl));
     }
-    for (const KLevel& L : h->levels) {
-        hipLaunchKernelGGL(k_kkt_potrf, dim3((unsigned)L.n_odd), dim3(256), use_lds ? lds : 0, s, L.potrf, r,
-                           use_lds, h->status);
-        // U = L^-1 E[left] (row-major B), V = L^-1 E[i]^T (transposed B)
-        launch_trsm(s, L.tri_u, L.n_u, r, r, r, 1, r, 0);
-        launch_trsm(s, L.tri_v, L.n_v, r, r, 1, r, r, 0);
-        // D[right] -= V^T V, D[left] -= U^T U, E[left] = -V^T U
-        launch_gemm(s, L.gemm_vv, L.n_vv, r, r, r, 1, r, 1, r, r, -1.0, 1.0);
-        launch_gemm(s, L.gemm_uu, L.n_uu, r, r, r, 1, r, 1, r, r, -1.0, 1.0);
-        launch_gemm(s, L.gemm_e, L.n_e, r, r, r, 1, r, 1, r, r, -1.0, 0.0);
-        KCHK(hipGetLastError());
-    }
+    const int nbc = h->nb * h->c, nbr = h->nb * r;
+    int rc = run_sequence(h, s, h->g_factor, [&]() {
+        hipLaunchKernelGGL(k_kkt_local, dim3(nblk(std::max(nbc, nbr), 256)), dim3(256), 0, s, nbc, nbr, h->colmap,
+                           h->rowmap, h->w, h->dc, h->wl, h->dcl);
+        // D_b = A_b W_b A_b^T + diag(dc_b); E_b = A_{b+1}[:, shared] W A_b[:, shared]^T
+        launch_gemm(s, h->t_schur, h->nb, r, r, h->c, h->c, 1, h->c, 1, r, 1.0, 0.0);
+        hipLaunchKernelGGL(k_kkt_add_diag, dim3(h->nb), dim3(256), 0, s, r, h->dcl, h->D);
+        launch_gemm(s, h->t_e, h->nb - 1, r, r, h->P, h->c, 1, h->c, 1, r, 1.0, 0.0);
+        for (const KLevel& L : h->levels) {
+            hipLaunchKernelGGL(k_kkt_potrf, dim3((unsigned)L.n_odd), dim3(256), use_lds ? lds : 0, s, L.potrf, r,
+                               use_lds, h->status);
+            // U = L^-1 E[left] (row-major B), V = L^-1 E[i]^T (transposed B)
+            launch_trsm(s, L.tri_u, L.n_u, r, r, r, 1, r, 0);
+            launch_trsm(s, L.tri_v, L.n_v, r, r, 1, r, r, 0);
+            // even j: D_j -= V_{j-1}^T V_{j-1} + U_{j+1}^T U_{j+1}; E_j = -V_{j+1}^T U_{j+1}
+            launch_gemm(s, L.gemm_d, L.n_d, r, r, r, 1, r, 1, r, r, -1.0, 1.0);
+            launch_gemm(s, L.gemm_e, L.n_e, r, r, r, 1, r, 1, r, r, -1.0, 0.0);
+        }
+    });
+    if (rc) return rc;
     int st = 0;
     KCHK(hipMemcpyAsync(&st, h->status, sizeof(int), hipMemcpyDeviceToHost, s));
     KCHK(hipStreamSynchronize(s));
@@ -734,23 +819,23 @@ extern "C" int mh_kkt_solve(mh_kkt* h, int32_t k, const double* b, double* xout)
         for (int64_t i = 0; i < h->m; ++i)
             std::memcpy(&in[(size_t)i * kc], b + (size_t)i * k + k0, sizeof(double) * kc);
         KCHK(hipMemcpyAsync(h->bm, in.data(), sizeof(double) * in.size(), hipMemcpyHostToDevice, s));
-        hipLaunchKernelGGL(k_kkt_to_blocks, dim3(nblk(nbr * kc, 256)), dim3(256), 0, s, nbr, kc, h->rowmap, h->bm,
-                           h->X);
-        for (size_t l = 0; l < h->levels.size(); ++l) {                 // forward
-            const KLevel& L = h->levels[l];
-            launch_trsm(s, L.sol, L.n_odd, r, kc, KMAX, 1, KMAX, 0);
-            launch_gemm(s, L.fwd_v, L.n_v, r, kc, r, 1, r, 1, KMAX, KMAX, -1.0, 1.0);
-            launch_gemm(s, L.fwd_u, L.n_u, r, kc, r, 1, r, 1, KMAX, KMAX, -1.0, 1.0);
-        }
-        for (size_t l = h->levels.size(); l-- > 0;) {                   // backward
-            const KLevel& L = h->levels[l];
-            launch_gemm(s, L.bwd_u, L.n_u, r, kc, r, r, 1, 1, KMAX, KMAX, -1.0, 1.0);
-            launch_gemm(s, L.bwd_v, L.n_v, r, kc, r, r, 1, 1, KMAX, KMAX, -1.0, 1.0);
-            launch_trsm(s, L.sol, L.n_odd, r, kc, KMAX, 1, KMAX, 1);
-        }
-        hipLaunchKernelGGL(k_kkt_from_blocks, dim3(nblk(nbr * kc, 256)), dim3(256), 0, s, nbr, kc, h->rowmap, h->X,
-                           h->bm);
-        KCHK(hipGetLastError());
+        int rc = run_sequence(h, s, h->g_solve[kc], [&]() {
+            hipLaunchKernelGGL(k_kkt_to_blocks, dim3(nblk(nbr * kc, 256)), dim3(256), 0, s, nbr, kc, h->rowmap,
+                               h->bm, h->X);
+            for (size_t l = 0; l < h->levels.size(); ++l) {                 // forward
+                const KLevel& L = h->levels[l];
+                launch_trsm(s, L.sol, L.n_odd, r, kc, KMAX, 1, KMAX, 0);
+                launch_gemm(s, L.fwd, L.n_d, r, kc, r, 1, r, 1, KMAX, KMAX, -1.0, 1.0);
+            }
+            for (size_t l = h->levels.size(); l-- > 0;) {                   // backward
+                const KLevel& L = h->levels[l];
+                launch_gemm(s, L.bwd, L.n_u, r, kc, r, r, 1, 1, KMAX, KMAX, -1.0, 1.0);
+                launch_trsm(s, L.sol, L.n_odd, r, kc, KMAX, 1, KMAX, 1);
+            }
+            hipLaunchKernelGGL(k_kkt_from_blocks, dim3(nblk(nbr * kc, 256)), dim3(256), 0, s, nbr, kc, h->rowmap,
+                               h->X, h->bm);
+        });
+        if (rc) return rc;
         KCHK(hipMemcpyAsync(in.data(), h->bm, sizeof(double) * in.size(), hipMemcpyDeviceToHost, s));
         KCHK(hipStreamSynchronize(s));
         for (int64_t i = 0; i < h->m; ++i)
