@@ -4,7 +4,7 @@
 # solve.  Output: gpurun_out/<tag>/...
 set -e
 TAG=${1:-solve}
-N=${2:-200}
+N=${2:-200}   # or inverse125
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
