@@ -145,6 +145,7 @@ __global__ __launch_bounds__(256) void k_kkt_gemm(const KTask* __restrict__ task
                                                   int psi, int psk, int qsi, int qsk, int ldc,
                                                   double alpha, double beta) {
     constexpr int TM = 64, TN = 64, TK = 16;
+    constexpr int PL = TM * TK / 256, QL = TN * TK / 256;   // elements per thread per tile
     __shared__ double Ps[TK][TM + 1];
     __shared__ double Qs[TK][TN + 1];
     const KTask t = tasks[blockIdx.z];
@@ -155,30 +156,51 @@ __global__ __launch_bounds__(256) void k_kkt_gemm(const KTask* __restrict__ task
     for (int a = 0; a < 4; ++a)
 #pragma unroll
         for (int b = 0; b < 4; ++b) acc[a][b] = 0.0;
+    // thread -> tile element maps (coalesced along the operand's contiguous dimension)
+    int pii[PL], pkk[PL], qjj[QL], qkk[QL];
+#pragma unroll
+    for (int u = 0; u < PL; ++u) {
+        const int e = tid + u * 256;
+        if (psk == 1) { pii[u] = e / TK; pkk[u] = e % TK; } else { pkk[u] = e / TM; pii[u] = e % TM; }
+    }
+#pragma unroll
+    for (int u = 0; u < QL; ++u) {
+        const int e = tid + u * 256;
+        if (qsk == 1) { qjj[u] = e / TK; qkk[u] = e % TK; } else { qkk[u] = e / TN; qjj[u] = e % TN; }
+    }
     const int npair = t.P2 ? 2 : 1;
-    for (int pr = 0; pr < npair; ++pr) {
-    const double* __restrict__ Pp = pr ? t.P2 : t.P;
-    const double* __restrict__ Qp = pr ? t.Q2 : t.Q;
-    const double* __restrict__ wp = pr ? nullptr : t.w;
-    for (int k0 = 0; k0 < K; k0 += TK) {
-        for (int e = tid; e < TM * TK; e += 256) {
-            int ii, kk;
-            if (psk == 1) { ii = e / TK; kk = e % TK; } else { kk = e / TM; ii = e % TM; }
-            const int gi = i0 + ii, gk = k0 + kk;
+    const int nk = (K + TK - 1) / TK;
+    const int nsteps = npair * nk;
+    auto load = [&](int step, double* pv, double* qv) {
+        const int pr = step / nk, k0 = (step % nk) * TK;
+        const double* __restrict__ Pp = pr ? t.P2 : t.P;
+        const double* __restrict__ Qp = pr ? t.Q2 : t.Q;
+        const double* __restrict__ wp = pr ? nullptr : t.w;
+#pragma unroll
+        for (int u = 0; u < PL; ++u) {
+            const int gi = i0 + pii[u], gk = k0 + pkk[u];
             double v = 0.0;
             if (gi < M && gk < K) {
                 v = Pp[(int64_t)gi * psi + (int64_t)gk * psk];
                 if (wp) v *= wp[gk];
             }
-            Ps[kk][ii] = v;
+            pv[u] = v;
         }
-        for (int e = tid; e < TN * TK; e += 256) {
-            int jj, kk;
-            if (qsk == 1) { jj = e / TK; kk = e % TK; } else { kk = e / TN; jj = e % TN; }
-            const int gj = j0 + jj, gk = k0 + kk;
-            Qs[kk][jj] = (gj < N && gk < K) ? Qp[(int64_t)gj * qsi + (int64_t)gk * qsk] : 0.0;
+#pragma unroll
+        for (int u = 0; u < QL; ++u) {
+            const int gj = j0 + qjj[u], gk = k0 + qkk[u];
+            qv[u] = (gj < N && gk < K) ? Qp[(int64_t)gj * qsi + (int64_t)gk * qsk] : 0.0;
         }
+    };
+    double pv[PL], qv[QL];
+    load(0, pv, qv);
+    for (int step = 0; step < nsteps; ++step) {
+#pragma unroll
+        for (int u = 0; u < PL; ++u) Ps[pkk[u]][pii[u]] = pv[u];
+#pragma unroll
+        for (int u = 0; u < QL; ++u) Qs[qkk[u]][qjj[u]] = qv[u];
         __syncthreads();
+        if (step + 1 < nsteps) load(step + 1, pv, qv);     // in flight while this tile is multiplied
 #pragma unroll
         for (int kk = 0; kk < TK; ++kk) {
             double p[4], q[4];
@@ -192,7 +214,6 @@ __global__ __launch_bounds__(256) void k_kkt_gemm(const KTask* __restrict__ task
                 for (int b = 0; b < 4; ++b) acc[a][b] = fma(p[a], q[b], acc[a][b]);
         }
         __syncthreads();
-    }
     }
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
@@ -331,6 +352,128 @@ __global__ __launch_bounds__(256) void k_kkt_trsm(const KTri* __restrict__ tasks
     }
 }
 
+// D_i -> L_i^-1, one block per workgroup, entirely in LDS (the inverse
+// path: r <= INV_RMAX).  Blocked right-looking Cholesky by 16-column panels
+// -- the panel's diagonal block factored by one lane, its 16 x 16 inverse by
+// 16 lanes (one column each), the rows below it as row x inverse products,
+// the trailing lower triangle updated by the workgroup -- then the blocked
+// triangular inverse in place (LAPACK dtrtri's column-block recursion from
+// the last panel: inv(L)[below, j] = -inv(L)[below, below] L[below, j]
+// inv(L_jj)).  Every later product of the reduction and of its solves is then
+// a GEMM with inv(L) (k_kkt_gemm) instead of a substitution chain: the
+// batched-inverse form GPU solvers use for small blocks; the solves'
+// rounding is that of a product with the inverse (~cond(L) eps), which the
+// optimizer's iterative refinement absorbs.
+constexpr int INV_TB = 16;
+constexpr int INV_RMAX = 134;    // r^2 + 16 r + 256 doubles <= 159 KB
+__device__ __forceinline__ void tri_inverse16(const double* A, int lda, int pb, double* Ainv, int tid) {
+    // Ainv (pb x pb, ld INV_TB) = inverse of the lower-triangular pb x pb block of A; lanes = columns
+    if (tid < pb) {
+        const int c = tid;
+        for (int i = 0; i < pb; ++i) {
+            double sacc = i == c ? 1.0 : 0.0;
+            if (i >= c) {
+                for (int k = c; k < i; ++k) sacc -= A[i * lda + k] * Ainv[k * INV_TB + c];
+                Ainv[i * INV_TB + c] = sacc / A[i * lda + i];
+            } else {
+                Ainv[i * INV_TB + c] = 0.0;
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_kkt_potri(double* const* __restrict__ mats, int r, int* __restrict__ status) {
+    extern __shared__ double lds[];
+    __shared__ int bad;
+    double* a = mats[blockIdx.x];
+    double* Ls = lds;                                   // r x r
+    double* Tmp = lds + (size_t)r * r;                  // r x INV_TB
+    double* Inv = Tmp + (size_t)r * INV_TB;             // INV_TB x INV_TB
+    const int tid = threadIdx.x, nt = blockDim.x;
+    stage<8>(Ls, a, r * r);
+    if (tid == 0) bad = 0;
+    __syncthreads();
+    // ---- Cholesky
+    for (int p0 = 0; p0 < r; p0 += INV_TB) {
+        const int pb = min(INV_TB, r - p0);
+        if (tid == 0) {
+            for (int j = p0; j < p0 + pb; ++j) {
+                double d = Ls[j * r + j];
+                if (!(d > 0.0) || !isfinite(d)) {
+                    bad = 1;
+                    d = 1.0;
+                }
+                d = sqrt(d);
+                Ls[j * r + j] = d;
+                for (int i = j + 1; i < p0 + pb; ++i) Ls[i * r + j] /= d;
+                for (int i = j + 1; i < p0 + pb; ++i) {
+                    const double lij = Ls[i * r + j];
+                    for (int k = j + 1; k <= i; ++k) Ls[i * r + k] -= lij * Ls[k * r + j];
+                }
+            }
+        }
+        __syncthreads();
+        tri_inverse16(Ls + (size_t)p0 * r + p0, r, pb, Inv, tid);
+        __syncthreads();
+        // rows below: L[i, p0:p0+pb] = A[i, p0:p0+pb] inv(L_pp)^T
+        for (int i = p0 + pb + tid; i < r; i += nt) {
+            double arow[INV_TB];
+#pragma unroll
+            for (int k = 0; k < INV_TB; ++k) arow[k] = k < pb ? Ls[i * r + p0 + k] : 0.0;
+#pragma unroll
+            for (int c = 0; c < INV_TB; ++c) {
+                if (c >= pb) break;
+                double sacc = 0.0;
+                for (int k = 0; k <= c; ++k) sacc += arow[k] * Inv[c * INV_TB + k];
+                Ls[i * r + p0 + c] = sacc;
+            }
+        }
+        __syncthreads();
+        // trailing lower triangle
+        const int tx = tid & 15, ty = tid >> 4, ny = nt >> 4;
+        for (int i = p0 + pb + ty; i < r; i += ny)
+            for (int k = p0 + pb + tx; k <= i; k += 16) {
+                double sacc = Ls[i * r + k];
+                for (int c = 0; c < pb; ++c) sacc -= Ls[i * r + p0 + c] * Ls[k * r + p0 + c];
+                Ls[i * r + k] = sacc;
+            }
+        __syncthreads();
+    }
+    // ---- inverse in place, column blocks from the last
+    const int np = (r + INV_TB - 1) / INV_TB;
+    for (int q = np - 1; q >= 0; --q) {
+        const int j0 = q * INV_TB, jb = min(INV_TB, r - j0), b0 = j0 + jb;
+        tri_inverse16(Ls + (size_t)j0 * r + j0, r, jb, Inv, tid);
+        __syncthreads();
+        // Tmp = inv(L)[below, below] L[below, j]   ((r - b0) x jb)
+        for (int e = tid; e < (r - b0) * jb; e += nt) {
+            const int i = b0 + e / jb, c = e % jb;
+            double sacc = 0.0;
+            for (int k = b0; k <= i; ++k) sacc += Ls[i * r + k] * Ls[k * r + j0 + c];
+            Tmp[(i - b0) * INV_TB + c] = sacc;
+        }
+        __syncthreads();
+        // inv(L)[below, j] = -Tmp inv(L_jj); inv(L)[j, j] = inv(L_jj)
+        for (int e = tid; e < (r - b0) * jb; e += nt) {
+            const int i = e / jb, c = e % jb;
+            double sacc = 0.0;
+            for (int k = c; k < jb; ++k) sacc += Tmp[i * INV_TB + k] * Inv[k * INV_TB + c];
+            Ls[(b0 + i) * r + j0 + c] = -sacc;
+        }
+        for (int e = tid; e < jb * jb; e += nt) {
+            const int i = e / jb, c = e % jb;
+            Ls[(j0 + i) * r + j0 + c] = i >= c ? Inv[i * INV_TB + c] : 0.0;
+        }
+        __syncthreads();
+    }
+    // the upper triangle as zeros: the GEMMs read the full block
+    for (int e = tid; e < r * r; e += nt) {
+        const int i = e / r, k = e - i * r;
+        a[e] = k <= i ? Ls[e] : 0.0;
+    }
+    if (tid == 0 && bad) *status = 1;
+}
+
 // [m, kc] (row-major) -> X [nb][r][KMAX] (padding rows 0), and back
 __global__ void k_kkt_to_blocks(int64_t nbr, int kc, const int32_t* __restrict__ rowmap,
                                 const double* __restrict__ b, double* __restrict__ X) {
@@ -437,6 +580,13 @@ struct KLevel {
     KTri* sol = nullptr;                       // X_i in place
     KTask* fwd = nullptr;                      // even j: X_j -= V_{j-1}^T X_{j-1} + U_{j+1}^T X_{j+1}  (n_d)
     KTask* bwd = nullptr;                      // odd i: X_i -= U_i X[left] + V_i X[right]            (n_u)
+    // the inverse path (D_i -> inv(L_i) by k_kkt_potri; every step a GEMM)
+    KTask* inv_u = nullptr;                    // U_i = inv(L_i) E[left]        (n_u)
+    KTask* inv_v = nullptr;                    // V_i = inv(L_i) E[i]^T         (n_v)
+    KTask* inv_y = nullptr;                    // Y_i = inv(L_i) X_i            (n_odd)
+    KTask* inv_fwd = nullptr;                  // even j: X_j -= V^T Y_{j-1} + U^T Y_{j+1}  (n_d)
+    KTask* inv_bwd = nullptr;                  // odd i: Y_i -= U_i X[left] + V_i X[right]  (n_u)
+    KTask* inv_x = nullptr;                    // X_i = inv(L_i)^T Y_i          (n_odd)
 };
 
 struct mh_kkt {
@@ -450,7 +600,7 @@ struct mh_kkt {
             *dcols = nullptr;
     double *vals = nullptr, *A = nullptr, *Jd = nullptr, *rs = nullptr, *w = nullptr, *dc = nullptr,
            *wl = nullptr, *dcl = nullptr, *D = nullptr, *E = nullptr, *U = nullptr, *V = nullptr,
-           *x = nullptr, *X = nullptr, *bm = nullptr, *bn = nullptr, *z = nullptr;
+           *x = nullptr, *X = nullptr, *Y = nullptr, *bm = nullptr, *bn = nullptr, *z = nullptr;
     int* status = nullptr;
     KTask *t_schur = nullptr, *t_e = nullptr;
     std::vector<KLevel> levels;      // the last level holds the single remaining block
@@ -460,6 +610,7 @@ struct mh_kkt {
     // graphs (captured on first use; every pointer they take is fixed at
     // create): one launch per call instead of ~50 (MOCOHIP_KKT_GRAPHS=0: off)
     bool graphs = true;
+    bool inv_path = true;            // r <= INV_RMAX and not MOCOHIP_KKT_INV=0
     hipGraphExec_t g_factor = nullptr;
     hipGraphExec_t g_solve[KMAX + 1] = {};
 };
@@ -507,16 +658,19 @@ static int build_levels(mh_kkt* h) {
     auto Up = [&](int i) { return h->U + rr * i; };
     auto Vp = [&](int i) { return h->V + rr * i; };
     auto Xp = [&](int i) { return h->X + (size_t)r * KMAX * i; };
+    auto Yp = [&](int i) { return h->Y + (size_t)r * KMAX * i; };
     while (true) {
         KLevel L;
         std::vector<double*> potrf;
         std::vector<KTri> tu, tv, sol;
-        std::vector<KTask> dd, ee, fw, bw;
+        std::vector<KTask> dd, ee, fw, bw, iu, iv, iy, ifw, ibw, ix;
         const int na = (int)active.size();
         if (na == 1) {
             const int i = active[0];
             potrf.push_back(Dp(i));
             sol.push_back({Dp(i), Xp(i), Xp(i)});
+            iy.push_back({Dp(i), Xp(i), nullptr, Yp(i), nullptr, nullptr});
+            ix.push_back({Dp(i), Yp(i), nullptr, Xp(i), nullptr, nullptr});
         } else {
             // odd positions: eliminated (their factors, U, V)
             for (int k = 1; k < na; k += 2) {
@@ -525,11 +679,17 @@ static int build_levels(mh_kkt* h) {
                 potrf.push_back(Dp(i));
                 sol.push_back({Dp(i), Xp(i), Xp(i)});
                 tu.push_back({Dp(i), Ep(left), Up(i)});
+                iu.push_back({Dp(i), Ep(left), nullptr, Up(i), nullptr, nullptr});
+                iy.push_back({Dp(i), Xp(i), nullptr, Yp(i), nullptr, nullptr});
+                ix.push_back({Dp(i), Yp(i), nullptr, Xp(i), nullptr, nullptr});
                 if (right >= 0) {
                     tv.push_back({Dp(i), Ep(i), Vp(i)});
+                    iv.push_back({Dp(i), Ep(i), nullptr, Vp(i), nullptr, nullptr});
                     bw.push_back({Up(i), Xp(left), nullptr, Xp(i), Vp(i), Xp(right)});
+                    ibw.push_back({Up(i), Xp(left), nullptr, Yp(i), Vp(i), Xp(right)});
                 } else {
                     bw.push_back({Up(i), Xp(left), nullptr, Xp(i), nullptr, nullptr});
+                    ibw.push_back({Up(i), Xp(left), nullptr, Yp(i), nullptr, nullptr});
                 }
             }
             // even positions: updated from the odd neighbours, the left one's
@@ -541,12 +701,15 @@ static int build_levels(mh_kkt* h) {
                 if (il >= 0 && ir >= 0) {
                     dd.push_back({Vp(il), Vp(il), nullptr, Dp(j), Up(ir), Up(ir)});
                     fw.push_back({Vp(il), Xp(il), nullptr, Xp(j), Up(ir), Xp(ir)});
+                    ifw.push_back({Vp(il), Yp(il), nullptr, Xp(j), Up(ir), Yp(ir)});
                 } else if (il >= 0) {
                     dd.push_back({Vp(il), Vp(il), nullptr, Dp(j), nullptr, nullptr});
                     fw.push_back({Vp(il), Xp(il), nullptr, Xp(j), nullptr, nullptr});
+                    ifw.push_back({Vp(il), Yp(il), nullptr, Xp(j), nullptr, nullptr});
                 } else if (ir >= 0) {
                     dd.push_back({Up(ir), Up(ir), nullptr, Dp(j), nullptr, nullptr});
                     fw.push_back({Up(ir), Xp(ir), nullptr, Xp(j), nullptr, nullptr});
+                    ifw.push_back({Up(ir), Yp(ir), nullptr, Xp(j), nullptr, nullptr});
                 }
                 if (ir >= 0 && k + 2 < na) ee.push_back({Vp(ir), Up(ir), nullptr, Ep(j), nullptr, nullptr});
             }
@@ -560,7 +723,10 @@ static int build_levels(mh_kkt* h) {
         if ((rc = kupload(h, &L.potrf, potrf)) || (rc = kupload(h, &L.sol, sol)) ||
             (rc = kupload(h, &L.tri_u, tu)) || (rc = kupload(h, &L.tri_v, tv)) ||
             (rc = kupload(h, &L.gemm_d, dd)) || (rc = kupload(h, &L.gemm_e, ee)) ||
-            (rc = kupload(h, &L.fwd, fw)) || (rc = kupload(h, &L.bwd, bw)))
+            (rc = kupload(h, &L.fwd, fw)) || (rc = kupload(h, &L.bwd, bw)) ||
+            (rc = kupload(h, &L.inv_u, iu)) || (rc = kupload(h, &L.inv_v, iv)) ||
+            (rc = kupload(h, &L.inv_y, iy)) || (rc = kupload(h, &L.inv_fwd, ifw)) ||
+            (rc = kupload(h, &L.inv_bwd, ibw)) || (rc = kupload(h, &L.inv_x, ix)))
             return rc;
         h->levels.push_back(L);
         if (na == 1) break;
@@ -609,6 +775,8 @@ extern "C" int mh_kkt_create(mh_ctx* ctx, const mh_kkt_layout* L, mh_kkt** out) 
     h->m = m; h->n = n; h->nnz = nnz;
     h->lshare.assign(L->lshare, L->lshare + h->nb);
     if (const char* eg = std::getenv("MOCOHIP_KKT_GRAPHS")) h->graphs = std::atoi(eg) != 0;
+    h->inv_path = L->r <= INV_RMAX;
+    if (const char* ei = std::getenv("MOCOHIP_KKT_INV")) h->inv_path = h->inv_path && std::atoi(ei) != 0;
     h->rshare.assign(L->rshare, L->rshare + h->nb);
     auto fail = [&](int code) { mh_kkt_destroy(h); return code; };
     if (hipSetDevice(h->device) != hipSuccess) return fail(mh_internal_error(MH_ERR_HIP, "hipSetDevice failed"));
@@ -626,6 +794,7 @@ extern "C" int mh_kkt_create(mh_ctx* ctx, const mh_kkt_layout* L, mh_kkt** out) 
         (rc = kalloc(h, &h->D, rr * h->nb)) || (rc = kalloc(h, &h->E, rr * h->nb)) ||
         (rc = kalloc(h, &h->U, rr * h->nb)) || (rc = kalloc(h, &h->V, rr * h->nb)) ||
         (rc = kalloc(h, &h->x, (size_t)n)) || (rc = kalloc(h, &h->X, (size_t)h->nb * h->r * KMAX)) ||
+        (rc = kalloc(h, &h->Y, (size_t)h->nb * h->r * KMAX)) ||
         (rc = kalloc(h, &h->bm, (size_t)m * KMAX)) || (rc = kalloc(h, &h->bn, (size_t)n * KMAX)) ||
         (rc = kalloc(h, &h->z, (size_t)h->nb * h->c * KMAX)) || (rc = kalloc(h, &h->status, 1)))
         return fail(rc);
@@ -777,6 +946,9 @@ extern "C" int mh_kkt_factor(mh_kkt* h, const double* w, const double* dc, int32
         if (tl > 65536)
             KCHK(hipFuncSetAttribute((const void*)k_kkt_trsm, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tl));
     }
+    const size_t plds = sizeof(double) * ((size_t)r * r + (size_t)r * INV_TB + INV_TB * INV_TB);
+    if (h->inv_path && plds > 65536)
+        KCHK(hipFuncSetAttribute((const void*)k_kkt_potri, hipFuncAttributeMaxDynamicSharedMemorySize, (int)plds));
     const int nbc = h->nb * h->c, nbr = h->nb * r;
     int rc = run_sequence(h, s, h->g_factor, [&]() {
         hipLaunchKernelGGL(k_kkt_local, dim3(nblk(std::max(nbc, nbr), 256)), dim3(256), 0, s, nbc, nbr, h->colmap,
@@ -786,6 +958,15 @@ extern "C" int mh_kkt_factor(mh_kkt* h, const double* w, const double* dc, int32
         hipLaunchKernelGGL(k_kkt_add_diag, dim3(h->nb), dim3(256), 0, s, r, h->dcl, h->D);
         launch_gemm(s, h->t_e, h->nb - 1, r, r, h->P, h->c, 1, h->c, 1, r, 1.0, 0.0);
         for (const KLevel& L : h->levels) {
+            if (h->inv_path) {
+                // D_i -> inv(L_i); U, V, the even updates: GEMMs
+                hipLaunchKernelGGL(k_kkt_potri, dim3((unsigned)L.n_odd), dim3(256), plds, s, L.potrf, r, h->status);
+                launch_gemm(s, L.inv_u, L.n_u, r, r, r, r, 1, 1, r, r, 1.0, 0.0);
+                launch_gemm(s, L.inv_v, L.n_v, r, r, r, r, 1, r, 1, r, 1.0, 0.0);
+                launch_gemm(s, L.gemm_d, L.n_d, r, r, r, 1, r, 1, r, r, -1.0, 1.0);
+                launch_gemm(s, L.gemm_e, L.n_e, r, r, r, 1, r, 1, r, r, -1.0, 0.0);
+                continue;
+            }
             hipLaunchKernelGGL(k_kkt_potrf, dim3((unsigned)L.n_odd), dim3(256), use_lds ? lds : 0, s, L.potrf, r,
                                use_lds, h->status);
             // U = L^-1 E[left] (row-major B), V = L^-1 E[i]^T (transposed B)
@@ -822,15 +1003,28 @@ extern "C" int mh_kkt_solve(mh_kkt* h, int32_t k, const double* b, double* xout)
         int rc = run_sequence(h, s, h->g_solve[kc], [&]() {
             hipLaunchKernelGGL(k_kkt_to_blocks, dim3(nblk(nbr * kc, 256)), dim3(256), 0, s, nbr, kc, h->rowmap,
                                h->bm, h->X);
-            for (size_t l = 0; l < h->levels.size(); ++l) {                 // forward
-                const KLevel& L = h->levels[l];
-                launch_trsm(s, L.sol, L.n_odd, r, kc, KMAX, 1, KMAX, 0);
-                launch_gemm(s, L.fwd, L.n_d, r, kc, r, 1, r, 1, KMAX, KMAX, -1.0, 1.0);
-            }
-            for (size_t l = h->levels.size(); l-- > 0;) {                   // backward
-                const KLevel& L = h->levels[l];
-                launch_gemm(s, L.bwd, L.n_u, r, kc, r, r, 1, 1, KMAX, KMAX, -1.0, 1.0);
-                launch_trsm(s, L.sol, L.n_odd, r, kc, KMAX, 1, KMAX, 1);
+            if (h->inv_path) {
+                for (size_t l = 0; l < h->levels.size(); ++l) {             // forward: Y = inv(L) X, updates
+                    const KLevel& L = h->levels[l];
+                    launch_gemm(s, L.inv_y, L.n_odd, r, kc, r, r, 1, 1, KMAX, KMAX, 1.0, 0.0);
+                    launch_gemm(s, L.inv_fwd, L.n_d, r, kc, r, 1, r, 1, KMAX, KMAX, -1.0, 1.0);
+                }
+                for (size_t l = h->levels.size(); l-- > 0;) {               // backward: X = inv(L)^T (Y - U X_l - V X_r)
+                    const KLevel& L = h->levels[l];
+                    launch_gemm(s, L.inv_bwd, L.n_u, r, kc, r, r, 1, 1, KMAX, KMAX, -1.0, 1.0);
+                    launch_gemm(s, L.inv_x, L.n_odd, r, kc, r, 1, r, 1, KMAX, KMAX, 1.0, 0.0);
+                }
+            } else {
+                for (size_t l = 0; l < h->levels.size(); ++l) {             // forward
+                    const KLevel& L = h->levels[l];
+                    launch_trsm(s, L.sol, L.n_odd, r, kc, KMAX, 1, KMAX, 0);
+                    launch_gemm(s, L.fwd, L.n_d, r, kc, r, 1, r, 1, KMAX, KMAX, -1.0, 1.0);
+                }
+                for (size_t l = h->levels.size(); l-- > 0;) {               // backward
+                    const KLevel& L = h->levels[l];
+                    launch_gemm(s, L.bwd, L.n_u, r, kc, r, r, 1, 1, KMAX, KMAX, -1.0, 1.0);
+                    launch_trsm(s, L.sol, L.n_odd, r, kc, KMAX, 1, KMAX, 1);
+                }
             }
             hipLaunchKernelGGL(k_kkt_from_blocks, dim3(nblk(nbr * kc, 256)), dim3(256), 0, s, nbr, kc, h->rowmap,
                                h->X, h->bm);

@@ -39,8 +39,13 @@ def _setup(name, seed=0):
     return nlp, x, rng
 
 
+@pytest.mark.parametrize("path", ["inverse", "substitution"])
 @pytest.mark.parametrize("name", sorted(CASES))
-def test_device_kkt_matches_restatement(name):
+def test_device_kkt_matches_restatement(name, path, monkeypatch):
+    """Both factorization paths of csrc/kkt.hip: blocks inverted in LDS and
+    every step a GEMM (default for r <= 134), or substitution
+    (MOCOHIP_KKT_INV=0; the path large blocks take)."""
+    monkeypatch.setenv("MOCOHIP_KKT_INV", "1" if path == "inverse" else "0")
     nlp, x, rng = _setup(name)
     try:
         dk = nlp.device_kkt()
@@ -78,7 +83,7 @@ def test_device_kkt_matches_restatement(name):
             B = rng.standard_normal((nlp.m, k))
             Xr = K.from_blocks(bm, K.cr_solve(Lf, U, Vf, levels, K.to_blocks(bm, B)))
             Xg = dk.solve(B)
-            assert np.abs(Xg - Xr).max() <= 1e-6 * np.abs(Xr).max(), k
+            assert np.abs(Xg - Xr).max() <= 1e-5 * np.abs(Xr).max(), k
         # and the Schur complement itself: S X = B
         B = rng.standard_normal(nlp.m)
         X = dk.solve(B)
@@ -89,7 +94,9 @@ def test_device_kkt_matches_restatement(name):
         resid = SX - B
         # backward error: the residual against |S| |X| (componentwise scale)
         absS_absX = abs(Jb) @ (w * (abs(Jb).T @ np.abs(X))) + dc * np.abs(X) + np.abs(B)
-        assert (np.abs(resid) / absS_absX).max() <= 1e-12
+        # (the inverse path multiplies by inv(L_i): its backward error is
+        # ~cond(L_i) eps rather than substitution's ~eps)
+        assert (np.abs(resid) / absS_absX).max() <= 1e-10
     finally:
         nlp.close()
 
