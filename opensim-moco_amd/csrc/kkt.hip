@@ -365,111 +365,133 @@ __global__ __launch_bounds__(256) void k_kkt_trsm(const KTri* __restrict__ tasks
 // rounding is that of a product with the inverse (~cond(L) eps), which the
 // optimizer's iterative refinement absorbs.
 constexpr int INV_TB = 16;
-constexpr int INV_RMAX = 134;    // r^2 + 16 r + 256 doubles <= 159 KB
+constexpr int INV_RMAX = 132;    // r (r + 1) + 17 (r + 16) doubles <= 159 KB
+// inverse of a pb x pb (pb <= 16) lower-triangular block A (ld lda) into
+// Ainv (ld INV_TB + 1): lane c < pb forward-substitutes column c of the
+// identity with the column held in registers (only L's loads, independent of
+// the chain, touch LDS)
 __device__ __forceinline__ void tri_inverse16(const double* A, int lda, int pb, double* Ainv, int tid) {
-    // Ainv (pb x pb, ld INV_TB) = inverse of the lower-triangular pb x pb block of A; lanes = columns
-    if (tid < pb) {
-        const int c = tid;
-        for (int i = 0; i < pb; ++i) {
-            double sacc = i == c ? 1.0 : 0.0;
-            if (i >= c) {
-                for (int k = c; k < i; ++k) sacc -= A[i * lda + k] * Ainv[k * INV_TB + c];
-                Ainv[i * INV_TB + c] = sacc / A[i * lda + i];
-            } else {
-                Ainv[i * INV_TB + c] = 0.0;
-            }
-        }
+    if (tid >= pb) return;
+    const int c = tid;
+    double x[INV_TB];
+#pragma unroll
+    for (int i = 0; i < INV_TB; ++i) {
+        double sacc = i == c ? 1.0 : 0.0;
+#pragma unroll
+        for (int k = 0; k < INV_TB; ++k)
+            if (k < i && k >= c && i < pb) sacc -= A[i * lda + k] * x[k];
+        x[i] = (i >= c && i < pb) ? sacc / A[i * lda + i] : 0.0;
     }
+#pragma unroll
+    for (int i = 0; i < INV_TB; ++i)
+        if (i < pb) Ainv[i * (INV_TB + 1) + c] = x[i];
 }
 
 __global__ __launch_bounds__(256) void k_kkt_potri(double* const* __restrict__ mats, int r, int* __restrict__ status) {
     extern __shared__ double lds[];
     __shared__ int bad;
     double* a = mats[blockIdx.x];
-    double* Ls = lds;                                   // r x r
-    double* Tmp = lds + (size_t)r * r;                  // r x INV_TB
-    double* Inv = Tmp + (size_t)r * INV_TB;             // INV_TB x INV_TB
+    const int ld = r + 1;                               // padded rows: column walks are bank-conflict free
+    constexpr int IL = INV_TB + 1;
+    double* Ls = lds;                                   // r x ld
+    double* Tmp = lds + (size_t)r * ld;                 // r x IL
+    double* Inv = Tmp + (size_t)r * IL;                 // INV_TB x IL
     const int tid = threadIdx.x, nt = blockDim.x;
-    stage<8>(Ls, a, r * r);
+    for (int e0 = 0; e0 < r * r; e0 += 8 * nt) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = a[min(e0 + u * nt + tid, r * r - 1)];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int e = e0 + u * nt + tid;
+            if (e < r * r) Ls[(e / r) * ld + e % r] = v[u];
+        }
+    }
     if (tid == 0) bad = 0;
     __syncthreads();
-    // ---- Cholesky
+    // ---- Cholesky by 16-column panels
     for (int p0 = 0; p0 < r; p0 += INV_TB) {
-        const int pb = min(INV_TB, r - p0);
-        if (tid == 0) {
-            for (int j = p0; j < p0 + pb; ++j) {
-                double d = Ls[j * r + j];
-                if (!(d > 0.0) || !isfinite(d)) {
-                    bad = 1;
-                    d = 1.0;
-                }
-                d = sqrt(d);
-                Ls[j * r + j] = d;
-                for (int i = j + 1; i < p0 + pb; ++i) Ls[i * r + j] /= d;
-                for (int i = j + 1; i < p0 + pb; ++i) {
-                    const double lij = Ls[i * r + j];
-                    for (int k = j + 1; k <= i; ++k) Ls[i * r + k] -= lij * Ls[k * r + j];
-                }
+        const int pb = min(INV_TB, r - p0), pe = p0 + pb;
+        // the diagonal block, unblocked: step j updates the block's trailing
+        // triangle from the unscaled column j (A_ik -= A_ij A_kj / A_jj), and
+        // scales column j after the barrier, beside step j + 1's update
+        for (int j = p0; j < pe; ++j) {
+            const double d2 = Ls[j * ld + j];
+            for (int e = tid; e < (pe - j - 1) * (pe - j - 1); e += nt) {
+                const int i = j + 1 + e / (pe - j - 1), k = j + 1 + e % (pe - j - 1);
+                if (k <= i) Ls[i * ld + k] -= Ls[i * ld + j] * Ls[k * ld + j] / d2;
             }
+            __syncthreads();
+            if (tid == 0 && (!(d2 > 0.0) || !isfinite(d2))) bad = 1;
+            const double d = sqrt(d2 > 0.0 ? d2 : 1.0);
+            for (int i = j + 1 + tid; i < pe; i += nt) Ls[i * ld + j] /= d;
+            if (tid == 0) Ls[j * ld + j] = d;
         }
         __syncthreads();
-        tri_inverse16(Ls + (size_t)p0 * r + p0, r, pb, Inv, tid);
+        tri_inverse16(Ls + (size_t)p0 * ld + p0, ld, pb, Inv, tid);
         __syncthreads();
-        // rows below: L[i, p0:p0+pb] = A[i, p0:p0+pb] inv(L_pp)^T
-        for (int i = p0 + pb + tid; i < r; i += nt) {
+        // rows below: L[i, p0:pe] = A[i, p0:pe] inv(L_pp)^T
+        for (int i = pe + tid; i < r; i += nt) {
             double arow[INV_TB];
 #pragma unroll
-            for (int k = 0; k < INV_TB; ++k) arow[k] = k < pb ? Ls[i * r + p0 + k] : 0.0;
+            for (int k = 0; k < INV_TB; ++k) arow[k] = k < pb ? Ls[i * ld + p0 + k] : 0.0;
 #pragma unroll
             for (int c = 0; c < INV_TB; ++c) {
                 if (c >= pb) break;
                 double sacc = 0.0;
-                for (int k = 0; k <= c; ++k) sacc += arow[k] * Inv[c * INV_TB + k];
-                Ls[i * r + p0 + c] = sacc;
+#pragma unroll
+                for (int k = 0; k < INV_TB; ++k)
+                    if (k <= c) sacc += arow[k] * Inv[c * IL + k];
+                Ls[i * ld + p0 + c] = sacc;
             }
         }
         __syncthreads();
-        // trailing lower triangle
+        // the trailing lower triangle
         const int tx = tid & 15, ty = tid >> 4, ny = nt >> 4;
-        for (int i = p0 + pb + ty; i < r; i += ny)
-            for (int k = p0 + pb + tx; k <= i; k += 16) {
-                double sacc = Ls[i * r + k];
-                for (int c = 0; c < pb; ++c) sacc -= Ls[i * r + p0 + c] * Ls[k * r + p0 + c];
-                Ls[i * r + k] = sacc;
+        for (int i = pe + ty; i < r; i += ny) {
+            double li[INV_TB];
+#pragma unroll
+            for (int c = 0; c < INV_TB; ++c) li[c] = c < pb ? Ls[i * ld + p0 + c] : 0.0;
+            for (int k = pe + tx; k <= i; k += 16) {
+                double sacc = Ls[i * ld + k];
+#pragma unroll
+                for (int c = 0; c < INV_TB; ++c)
+                    if (c < pb) sacc -= li[c] * Ls[k * ld + p0 + c];
+                Ls[i * ld + k] = sacc;
             }
+        }
         __syncthreads();
     }
-    // ---- inverse in place, column blocks from the last
+    // ---- inverse in place, column blocks from the last (dtrtri's recursion)
     const int np = (r + INV_TB - 1) / INV_TB;
     for (int q = np - 1; q >= 0; --q) {
         const int j0 = q * INV_TB, jb = min(INV_TB, r - j0), b0 = j0 + jb;
-        tri_inverse16(Ls + (size_t)j0 * r + j0, r, jb, Inv, tid);
-        __syncthreads();
+        tri_inverse16(Ls + (size_t)j0 * ld + j0, ld, jb, Inv, tid);
         // Tmp = inv(L)[below, below] L[below, j]   ((r - b0) x jb)
         for (int e = tid; e < (r - b0) * jb; e += nt) {
             const int i = b0 + e / jb, c = e % jb;
             double sacc = 0.0;
-            for (int k = b0; k <= i; ++k) sacc += Ls[i * r + k] * Ls[k * r + j0 + c];
-            Tmp[(i - b0) * INV_TB + c] = sacc;
+            for (int k = b0; k <= i; ++k) sacc += Ls[i * ld + k] * Ls[k * ld + j0 + c];
+            Tmp[(i - b0) * IL + c] = sacc;
         }
         __syncthreads();
         // inv(L)[below, j] = -Tmp inv(L_jj); inv(L)[j, j] = inv(L_jj)
         for (int e = tid; e < (r - b0) * jb; e += nt) {
             const int i = e / jb, c = e % jb;
             double sacc = 0.0;
-            for (int k = c; k < jb; ++k) sacc += Tmp[i * INV_TB + k] * Inv[k * INV_TB + c];
-            Ls[(b0 + i) * r + j0 + c] = -sacc;
+            for (int k = c; k < jb; ++k) sacc += Tmp[i * IL + k] * Inv[k * IL + c];
+            Ls[(b0 + i) * ld + j0 + c] = -sacc;
         }
         for (int e = tid; e < jb * jb; e += nt) {
             const int i = e / jb, c = e % jb;
-            Ls[(j0 + i) * r + j0 + c] = i >= c ? Inv[i * INV_TB + c] : 0.0;
+            Ls[(j0 + i) * ld + j0 + c] = i >= c ? Inv[i * IL + c] : 0.0;
         }
         __syncthreads();
     }
-    // the upper triangle as zeros: the GEMMs read the full block
+    // out, the upper triangle as zeros: the GEMMs read the full block
     for (int e = tid; e < r * r; e += nt) {
         const int i = e / r, k = e - i * r;
-        a[e] = k <= i ? Ls[e] : 0.0;
+        a[e] = k <= i ? Ls[i * ld + k] : 0.0;
     }
     if (tid == 0 && bad) *status = 1;
 }
@@ -610,7 +632,7 @@ struct mh_kkt {
     // graphs (captured on first use; every pointer they take is fixed at
     // create): one launch per call instead of ~50 (MOCOHIP_KKT_GRAPHS=0: off)
     bool graphs = true;
-    bool inv_path = true;            // r <= INV_RMAX and not MOCOHIP_KKT_INV=0
+    bool inv_path = true;            // r <= INV_RMAX (132) and not MOCOHIP_KKT_INV=0
     hipGraphExec_t g_factor = nullptr;
     hipGraphExec_t g_solve[KMAX + 1] = {};
 };
@@ -946,7 +968,7 @@ extern "C" int mh_kkt_factor(mh_kkt* h, const double* w, const double* dc, int32
         if (tl > 65536)
             KCHK(hipFuncSetAttribute((const void*)k_kkt_trsm, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tl));
     }
-    const size_t plds = sizeof(double) * ((size_t)r * r + (size_t)r * INV_TB + INV_TB * INV_TB);
+    const size_t plds = sizeof(double) * ((size_t)r * (r + 1) + (size_t)(r + INV_TB) * (INV_TB + 1));
     if (h->inv_path && plds > 65536)
         KCHK(hipFuncSetAttribute((const void*)k_kkt_potri, hipFuncAttributeMaxDynamicSharedMemorySize, (int)plds));
     const int nbc = h->nb * h->c, nbr = h->nb * r;

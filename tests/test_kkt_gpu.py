@@ -43,7 +43,7 @@ def _setup(name, seed=0):
 @pytest.mark.parametrize("name", sorted(CASES))
 def test_device_kkt_matches_restatement(name, path, monkeypatch):
     """Both factorization paths of csrc/kkt.hip: blocks inverted in LDS and
-    every step a GEMM (default for r <= 134), or substitution
+    every step a GEMM (default for r <= 132), or substitution
     (MOCOHIP_KKT_INV=0; the path large blocks take)."""
     monkeypatch.setenv("MOCOHIP_KKT_INV", "1" if path == "inverse" else "0")
     nlp, x, rng = _setup(name)
