@@ -352,148 +352,126 @@ __global__ __launch_bounds__(256) void k_kkt_trsm(const KTri* __restrict__ tasks
     }
 }
 
-// D_i -> L_i^-1, one block per workgroup, entirely in LDS (the inverse
-// path: r <= INV_RMAX).  Blocked right-looking Cholesky by 16-column panels
-// -- the panel's diagonal block factored by one lane, its 16 x 16 inverse by
-// 16 lanes (one column each), the rows below it as row x inverse products,
-// the trailing lower triangle updated by the workgroup -- then the blocked
-// triangular inverse in place (LAPACK dtrtri's column-block recursion from
-// the last panel: inv(L)[below, j] = -inv(L)[below, below] L[below, j]
-// inv(L_jj)).  Every later product of the reduction and of its solves is then
-// a GEMM with inv(L) (k_kkt_gemm) instead of a substitution chain: the
+// D_i -> L_i^-1, one block per workgroup, in registers (the inverse path:
+// r <= INV_RMAX).  Every later product of the reduction and of its solves is
+// then a GEMM with inv(L) (k_kkt_gemm) instead of a substitution chain: the
 // batched-inverse form GPU solvers use for small blocks; the solves'
 // rounding is that of a product with the inverse (~cond(L) eps), which the
 // optimizer's iterative refinement absorbs.
-constexpr int INV_TB = 16;
-constexpr int INV_RMAX = 132;    // r (r + 1) + 17 (r + 16) doubles <= 159 KB
-// inverse of a pb x pb (pb <= 16) lower-triangular block A (ld lda) into
-// Ainv (ld INV_TB + 1): lane c < pb forward-substitutes column c of the
-// identity with the column held in registers (only L's loads, independent of
-// the chain, touch LDS)
-__device__ __forceinline__ void tri_inverse16(const double* A, int lda, int pb, double* Ainv, int tid) {
-    if (tid >= pb) return;
-    const int c = tid;
-    double x[INV_TB];
-#pragma unroll
-    for (int i = 0; i < INV_TB; ++i) {
-        double sacc = i == c ? 1.0 : 0.0;
-#pragma unroll
-        for (int k = 0; k < INV_TB; ++k)
-            if (k < i && k >= c && i < pb) sacc -= A[i * lda + k] * x[k];
-        x[i] = (i >= c && i < pb) ? sacc / A[i * lda + i] : 0.0;
-    }
-#pragma unroll
-    for (int i = 0; i < INV_TB; ++i)
-        if (i < pb) Ainv[i * (INV_TB + 1) + c] = x[i];
-}
-
+constexpr int INV_T = 10;                 // register tile edge: r <= 16 INV_T
+constexpr int INV_RMAX = 16 * INV_T;
+// In-place inverse Cholesky in registers.  Z starts as A; step k reads row k
+// of Z (w) and, for every row i > k,
+//     Z[i, c] <- (c == k ? 0 : Z[i, c]) - w[i] (c == k ? 1 : w[c]) / w[k],
+// and row k becomes w[c] / sqrt(w[k]) (c < k) and 1 / sqrt(w[k]) (c = k) --
+// applied once after the last step, since no later step reads row k.
+// Columns c > k of rows > k carry the trailing Schur complement (right-looking
+// Cholesky, kept symmetric, so row k also holds column k); columns c <= k
+// accumulate inv(L) (the identity eliminated by the same row operations).
+// After step r - 1 the lower triangle of Z is inv(L).  Thread (ty, tx) of a
+// 16 x 16 grid holds rows ty T + a (blocked: a thread whose rows are all done
+// skips its update) and columns tx + 16 b (interleaved: row k's broadcast is
+// one contiguous, conflict-free LDS line).  One barrier per step (w double
+// buffered); LDS holds 2 rows.
+template <int T>
 __global__ __launch_bounds__(256) void k_kkt_potri(double* const* __restrict__ mats, int r, int* __restrict__ status) {
-    extern __shared__ double lds[];
+    __shared__ double wbuf[2][16 * INV_T];
+    __shared__ double piv[16 * INV_T];
     __shared__ int bad;
     double* a = mats[blockIdx.x];
-    const int ld = r + 1;                               // padded rows: column walks are bank-conflict free
-    constexpr int IL = INV_TB + 1;
-    double* Ls = lds;                                   // r x ld
-    double* Tmp = lds + (size_t)r * ld;                 // r x IL
-    double* Inv = Tmp + (size_t)r * IL;                 // INV_TB x IL
-    const int tid = threadIdx.x, nt = blockDim.x;
-    for (int e0 = 0; e0 < r * r; e0 += 8 * nt) {
-        double v[8];
+    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+    const int row0 = ty * T;
+    double z[T][T];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = a[min(e0 + u * nt + tid, r * r - 1)];
+    for (int i = 0; i < T; ++i)
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int e = e0 + u * nt + tid;
-            if (e < r * r) Ls[(e / r) * ld + e % r] = v[u];
+        for (int j = 0; j < T; ++j) {
+            const int row = row0 + i, col = tx + 16 * j;
+            const double v = a[(size_t)min(row, r - 1) * r + min(col, r - 1)];
+            z[i][j] = (row < r && col < r) ? v : 0.0;
         }
-    }
+    // entries >= r of w stay 0 (rows and columns past r then never change);
+    // every LDS read below is unconditional, so none waits inside a branch
+    for (int e = tid; e < 2 * 16 * INV_T; e += 256) (&wbuf[0][0])[e] = 0.0;
     if (tid == 0) bad = 0;
-    __syncthreads();
-    // ---- Cholesky by 16-column panels
-    for (int p0 = 0; p0 < r; p0 += INV_TB) {
-        const int pb = min(INV_TB, r - p0), pe = p0 + pb;
-        // the diagonal block, unblocked: step j updates the block's trailing
-        // triangle from the unscaled column j (A_ik -= A_ij A_kj / A_jj), and
-        // scales column j after the barrier, beside step j + 1's update
-        for (int j = p0; j < pe; ++j) {
-            const double d2 = Ls[j * ld + j];
-            for (int e = tid; e < (pe - j - 1) * (pe - j - 1); e += nt) {
-                const int i = j + 1 + e / (pe - j - 1), k = j + 1 + e % (pe - j - 1);
-                if (k <= i) Ls[i * ld + k] -= Ls[i * ld + j] * Ls[k * ld + j] / d2;
-            }
-            __syncthreads();
-            if (tid == 0 && (!(d2 > 0.0) || !isfinite(d2))) bad = 1;
-            const double d = sqrt(d2 > 0.0 ? d2 : 1.0);
-            for (int i = j + 1 + tid; i < pe; i += nt) Ls[i * ld + j] /= d;
-            if (tid == 0) Ls[j * ld + j] = d;
+    // k's owner coordinates are uniform (scalar branches); the per-lane work
+    // is branch-free: rows <= k get f = 0
+    for (int k = 0; k < r; ++k) {
+        double* w = wbuf[k & 1];
+        const int tyk = k / T, ik = k - tyk * T, jk = k >> 4, txk = k & 15;
+        if (ty == tyk) {
+#pragma unroll
+            for (int i = 0; i < T; ++i)
+                if (i == ik) {
+#pragma unroll
+                    for (int j = 0; j < T; ++j) w[tx + 16 * j] = z[i][j];   // 0 past r
+                }
         }
         __syncthreads();
-        tri_inverse16(Ls + (size_t)p0 * ld + p0, ld, pb, Inv, tid);
-        __syncthreads();
-        // rows below: L[i, p0:pe] = A[i, p0:pe] inv(L_pp)^T
-        for (int i = pe + tid; i < r; i += nt) {
-            double arow[INV_TB];
-#pragma unroll
-            for (int k = 0; k < INV_TB; ++k) arow[k] = k < pb ? Ls[i * ld + p0 + k] : 0.0;
-#pragma unroll
-            for (int c = 0; c < INV_TB; ++c) {
-                if (c >= pb) break;
-                double sacc = 0.0;
-#pragma unroll
-                for (int k = 0; k < INV_TB; ++k)
-                    if (k <= c) sacc += arow[k] * Inv[c * IL + k];
-                Ls[i * ld + p0 + c] = sacc;
-            }
+        const double p = w[k];
+        const double pp = (p > 0.0 && isfinite(p)) ? p : 1.0;
+        if (tid == 0) {
+            if (pp != p) bad = 1;
+            piv[k] = pp;
         }
-        __syncthreads();
-        // the trailing lower triangle
-        const int tx = tid & 15, ty = tid >> 4, ny = nt >> 4;
-        for (int i = pe + ty; i < r; i += ny) {
-            double li[INV_TB];
+        if (row0 + T - 1 < k) continue;              // every row of this thread done
+        const double pinv = 1.0 / pp;
+        double wc[T], f[T];
 #pragma unroll
-            for (int c = 0; c < INV_TB; ++c) li[c] = c < pb ? Ls[i * ld + p0 + c] : 0.0;
-            for (int k = pe + tx; k <= i; k += 16) {
-                double sacc = Ls[i * ld + k];
+        for (int j = 0; j < T; ++j) wc[j] = w[tx + 16 * j];
 #pragma unroll
-                for (int c = 0; c < INV_TB; ++c)
-                    if (c < pb) sacc -= li[c] * Ls[k * ld + p0 + c];
-                Ls[i * ld + k] = sacc;
+        for (int i = 0; i < T; ++i) f[i] = w[row0 + i] * (row0 + i > k ? pinv : 0.0);
+#pragma unroll
+        for (int j = 0; j < T; ++j)
+            if (j == jk && tx == txk) {              // column k of rows > k: restart at 0, w = 1
+                wc[j] = 1.0;
+#pragma unroll
+                for (int i = 0; i < T; ++i) z[i][j] = row0 + i > k ? 0.0 : z[i][j];
             }
-        }
-        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < T; ++i)
+#pragma unroll
+            for (int j = 0; j < T; ++j) z[i][j] = fma(-f[i], wc[j], z[i][j]);
     }
-    // ---- inverse in place, column blocks from the last (dtrtri's recursion)
-    const int np = (r + INV_TB - 1) / INV_TB;
-    for (int q = np - 1; q >= 0; --q) {
-        const int j0 = q * INV_TB, jb = min(INV_TB, r - j0), b0 = j0 + jb;
-        tri_inverse16(Ls + (size_t)j0 * ld + j0, ld, jb, Inv, tid);
-        // Tmp = inv(L)[below, below] L[below, j]   ((r - b0) x jb)
-        for (int e = tid; e < (r - b0) * jb; e += nt) {
-            const int i = b0 + e / jb, c = e % jb;
-            double sacc = 0.0;
-            for (int k = b0; k <= i; ++k) sacc += Ls[i * ld + k] * Ls[k * ld + j0 + c];
-            Tmp[(i - b0) * IL + c] = sacc;
+    __syncthreads();
+    // row i of inv(L): its unscaled row over columns < i, times 1 / sqrt(p_i),
+    // and 1 / sqrt(p_i) on the diagonal (row i is never read after step i,
+    // so the scaling waits until here)
+#pragma unroll
+    for (int i = 0; i < T; ++i) {
+        const int row = row0 + i;
+        const double dinv = 1.0 / sqrt(row < r ? piv[row] : 1.0);
+#pragma unroll
+        for (int j = 0; j < T; ++j) {
+            const int col = tx + 16 * j;
+            z[i][j] = col < row ? z[i][j] * dinv : (col == row ? dinv : z[i][j]);
         }
-        __syncthreads();
-        // inv(L)[below, j] = -Tmp inv(L_jj); inv(L)[j, j] = inv(L_jj)
-        for (int e = tid; e < (r - b0) * jb; e += nt) {
-            const int i = e / jb, c = e % jb;
-            double sacc = 0.0;
-            for (int k = c; k < jb; ++k) sacc += Tmp[i * IL + k] * Inv[k * IL + c];
-            Ls[(b0 + i) * ld + j0 + c] = -sacc;
-        }
-        for (int e = tid; e < jb * jb; e += nt) {
-            const int i = e / jb, c = e % jb;
-            Ls[(j0 + i) * ld + j0 + c] = i >= c ? Inv[i * IL + c] : 0.0;
-        }
-        __syncthreads();
     }
     // out, the upper triangle as zeros: the GEMMs read the full block
-    for (int e = tid; e < r * r; e += nt) {
-        const int i = e / r, k = e - i * r;
-        a[e] = k <= i ? Ls[i * ld + k] : 0.0;
-    }
+#pragma unroll
+    for (int i = 0; i < T; ++i)
+#pragma unroll
+        for (int j = 0; j < T; ++j) {
+            const int row = row0 + i, col = tx + 16 * j;
+            if (row < r && col < r) a[(size_t)row * r + col] = col <= row ? z[i][j] : 0.0;
+        }
     if (tid == 0 && bad) *status = 1;
+}
+
+using potri_fn = void (*)(double* const*, int, int*);
+static potri_fn potri_kernel(int r) {
+    switch ((r + 15) / 16) {
+        case 1: return k_kkt_potri<1>;
+        case 2: return k_kkt_potri<2>;
+        case 3: return k_kkt_potri<3>;
+        case 4: return k_kkt_potri<4>;
+        case 5: return k_kkt_potri<5>;
+        case 6: return k_kkt_potri<6>;
+        case 7: return k_kkt_potri<7>;
+        case 8: return k_kkt_potri<8>;
+        case 9: return k_kkt_potri<9>;
+        default: return k_kkt_potri<10>;
+    }
 }
 
 // [m, kc] (row-major) -> X [nb][r][KMAX] (padding rows 0), and back
@@ -516,58 +494,41 @@ __global__ void k_kkt_from_blocks(int64_t nbr, int kc, const int32_t* __restrict
     if (row >= 0) b[(int64_t)row * kc + k] = X[bi * KMAX + k];
 }
 
-// y = R J v: per block y_b = A_b v_loc, plus the dense columns
-__global__ __launch_bounds__(256) void k_kkt_jmul(int r, int c, int nd, int kc, const double* __restrict__ A,
-                                                  const int32_t* __restrict__ rowmap,
-                                                  const int32_t* __restrict__ colmap,
-                                                  const double* __restrict__ Jd,
-                                                  const int32_t* __restrict__ dcols,
-                                                  const double* __restrict__ v, double* __restrict__ y) {
-    const int b = blockIdx.x;
-    for (int e = threadIdx.x; e < r * kc; e += blockDim.x) {
-        const int i = e / kc, k = e % kc;
-        const int row = rowmap[(int64_t)b * r + i];
-        if (row < 0) continue;
-        const double* Ai = A + ((int64_t)b * r + i) * c;
-        const int32_t* cm = colmap + (int64_t)b * c;
-        double s = 0.0;
-        for (int j = 0; j < c; ++j) {
-            const int col = cm[j];
-            if (col >= 0) s += Ai[j] * v[(int64_t)col * kc + k];
-        }
-        for (int d = 0; d < nd; ++d) s += Jd[(int64_t)row * nd + d] * v[(int64_t)dcols[d] * kc + k];
-        y[(int64_t)row * kc + k] = s;
-    }
+// R J's values in CSR order (cv[p] = vals[src[p]] rs[row[p]]): the
+// products with J and J^T read them from here
+__global__ void k_kkt_csr_vals(int64_t nnz, const int32_t* __restrict__ src, const int32_t* __restrict__ row,
+                               const double* __restrict__ vals, const double* __restrict__ rs,
+                               double* __restrict__ cv) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < nnz) cv[p] = vals[src[p]] * rs[row[p]];
 }
 
-// z_b = A_b^T y_b (local columns), then per global column the (up to two)
-// block contributions in block order, and the dense columns' reductions
-__global__ __launch_bounds__(256) void k_kkt_jtmul_blocks(int r, int c, int kc, const double* __restrict__ A,
-                                                          const int32_t* __restrict__ rowmap,
-                                                          const double* __restrict__ y, double* __restrict__ z) {
-    const int b = blockIdx.x;
-    for (int e = threadIdx.x; e < c * kc; e += blockDim.x) {
-        const int j = e / kc, k = e % kc;
-        double s = 0.0;
-        for (int i = 0; i < r; ++i) {
-            const int row = rowmap[(int64_t)b * r + i];
-            if (row >= 0) s += A[((int64_t)b * r + i) * c + j] * y[(int64_t)row * kc + k];
-        }
-        z[((int64_t)b * c + j) * kc + k] = s;
+// out[i][k] = sum_p val[pos ? pos[p] : p] x[idx[p]][k] over p in
+// [ptr[i], ptr[i + 1]): y = R J v over the CSR rows, or (pos the CSC -> CSR
+// permutation) v = J^T R y over the CSC columns.  G lanes per (i, k), summed
+// by a fixed butterfly: deterministic.
+template <int G>
+__global__ __launch_bounds__(256) void k_kkt_spmv(int64_t nout, int kc, const int32_t* __restrict__ ptr,
+                                                  const int32_t* __restrict__ idx, const int32_t* __restrict__ pos,
+                                                  const double* __restrict__ val, const double* __restrict__ x,
+                                                  double* __restrict__ out) {
+    const int64_t item = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / G;
+    const int lane = (int)(threadIdx.x % G);
+    double acc = 0.0;
+    if (item < nout * kc) {
+        const int64_t i = item / kc;
+        const int k = (int)(item - i * kc);
+        const int p1 = ptr[i + 1];
+        for (int p = ptr[i] + lane; p < p1; p += G)
+            acc += val[pos ? pos[p] : p] * x[(int64_t)idx[p] * kc + k];
     }
+#pragma unroll
+    for (int o = G / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o, G);
+    if (item < nout * kc && lane == 0) out[item] = acc;
 }
-__global__ void k_kkt_jtmul_collect(int64_t n, int kc, const int32_t* __restrict__ col2,
-                                    const double* __restrict__ z, double* __restrict__ out) {
-    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= n * kc) return;
-    const int64_t j = e / kc;
-    const int k = (int)(e % kc);
-    const int p0 = col2[2 * j], p1 = col2[2 * j + 1];
-    double s = 0.0;
-    if (p0 >= 0) s += z[(int64_t)p0 * kc + k];
-    if (p1 >= 0) s += z[(int64_t)p1 * kc + k];
-    out[e] = s;
-}
+
+// the dense columns of J^T R y (their CSC ranges are empty): one workgroup
+// per (column, right-hand side)
 __global__ __launch_bounds__(256) void k_kkt_jtmul_dense(int64_t m, int nd, int kc, const double* __restrict__ Jd,
                                                          const int32_t* __restrict__ dcols,
                                                          const double* __restrict__ y, double* __restrict__ out) {
@@ -618,12 +579,19 @@ struct mh_kkt {
     int64_t m = 0, n = 0, nnz = 0;
     std::vector<int32_t> lshare, rshare;
     // device
-    int32_t *a_src = nullptr, *rowmap = nullptr, *colmap = nullptr, *d_src = nullptr, *col2 = nullptr,
+    int32_t *a_src = nullptr, *rowmap = nullptr, *colmap = nullptr, *d_src = nullptr,
             *dcols = nullptr;
     double *vals = nullptr, *A = nullptr, *Jd = nullptr, *rs = nullptr, *w = nullptr, *dc = nullptr,
            *wl = nullptr, *dcl = nullptr, *D = nullptr, *E = nullptr, *U = nullptr, *V = nullptr,
-           *x = nullptr, *X = nullptr, *Y = nullptr, *bm = nullptr, *bn = nullptr, *z = nullptr;
+           *x = nullptr, *X = nullptr, *Y = nullptr, *bm = nullptr, *bn = nullptr;
     int* status = nullptr;
+    // J in CSR (every nonzero) and CSC (the block columns; the dense columns'
+    // products are k_kkt_jtmul_dense's)
+    int32_t *csr_ptr = nullptr, *csr_col = nullptr, *csr_src = nullptr, *csr_row = nullptr, *csc_ptr = nullptr,
+            *csc_row = nullptr, *csc_pos = nullptr;
+    double* cv = nullptr;
+    // pinned staging for the host vectors each call exchanges
+    double *hm = nullptr, *hn = nullptr;
     KTask *t_schur = nullptr, *t_e = nullptr;
     std::vector<KLevel> levels;      // the last level holds the single remaining block
     std::vector<void*> allocs;
@@ -632,7 +600,7 @@ struct mh_kkt {
     // graphs (captured on first use; every pointer they take is fixed at
     // create): one launch per call instead of ~50 (MOCOHIP_KKT_GRAPHS=0: off)
     bool graphs = true;
-    bool inv_path = true;            // r <= INV_RMAX (132) and not MOCOHIP_KKT_INV=0
+    bool inv_path = true;            // r <= INV_RMAX (160) and not MOCOHIP_KKT_INV=0
     hipGraphExec_t g_factor = nullptr;
     hipGraphExec_t g_solve[KMAX + 1] = {};
 };
@@ -667,6 +635,8 @@ extern "C" void mh_kkt_destroy(mh_kkt* h) {
     for (auto& g : h->g_solve)
         if (g) (void)hipGraphExecDestroy(g);
     for (void* p : h->allocs) (void)hipFree(p);
+    if (h->hm) (void)hipHostFree(h->hm);
+    if (h->hn) (void)hipHostFree(h->hn);
     delete h;
 }
 
@@ -806,7 +776,6 @@ extern "C" int mh_kkt_create(mh_ctx* ctx, const mh_kkt_layout* L, mh_kkt** out) 
     if ((rc = kupload(h, &h->a_src, L->a_src, (size_t)na)) ||
         (rc = kupload(h, &h->rowmap, L->rowmap, (size_t)h->nb * h->r)) ||
         (rc = kupload(h, &h->colmap, L->colmap, (size_t)h->nb * h->c)) ||
-        (rc = kupload(h, &h->col2, L->col2, (size_t)2 * n)) ||
         (rc = kupload(h, &h->dcols, L->dcols, (size_t)h->nd)) ||
         (rc = kupload(h, &h->d_src, L->d_src, (size_t)(m * h->nd))) ||
         (rc = kalloc(h, &h->vals, (size_t)nnz)) || (rc = kalloc(h, &h->A, (size_t)na)) ||
@@ -818,8 +787,61 @@ extern "C" int mh_kkt_create(mh_ctx* ctx, const mh_kkt_layout* L, mh_kkt** out) 
         (rc = kalloc(h, &h->x, (size_t)n)) || (rc = kalloc(h, &h->X, (size_t)h->nb * h->r * KMAX)) ||
         (rc = kalloc(h, &h->Y, (size_t)h->nb * h->r * KMAX)) ||
         (rc = kalloc(h, &h->bm, (size_t)m * KMAX)) || (rc = kalloc(h, &h->bn, (size_t)n * KMAX)) ||
-        (rc = kalloc(h, &h->z, (size_t)h->nb * h->c * KMAX)) || (rc = kalloc(h, &h->status, 1)))
+        (rc = kalloc(h, &h->status, 1)))
         return fail(rc);
+    {
+        // every nonzero sits in exactly one block entry or dense-column slot
+        std::vector<int32_t> row_of((size_t)nnz, -1), col_of((size_t)nnz, -1);
+        auto place = [&](int32_t sidx, int64_t row, int64_t col) {
+            if (sidx < 0) return true;
+            if (row < 0 || col < 0 || row_of[sidx] >= 0) return false;
+            row_of[sidx] = (int32_t)row;
+            col_of[sidx] = (int32_t)col;
+            return true;
+        };
+        for (int bb = 0; bb < h->nb; ++bb)
+            for (int i = 0; i < h->r; ++i)
+                for (int j = 0; j < h->c; ++j)
+                    if (!place(L->a_src[((int64_t)bb * h->r + i) * h->c + j], L->rowmap[(int64_t)bb * h->r + i],
+                               L->colmap[(int64_t)bb * h->c + j]))
+                        return fail(mh_internal_error(MH_ERR_INVALID, "a_src places a nonzero twice or off the map"));
+        for (int64_t i = 0; i < m; ++i)
+            for (int d = 0; d < h->nd; ++d)
+                if (!place(L->d_src[i * h->nd + d], i, L->dcols[d]))
+                    return fail(mh_internal_error(MH_ERR_INVALID, "d_src places a nonzero twice"));
+        std::vector<char> dense((size_t)n, 0);
+        for (int d = 0; d < h->nd; ++d) dense[L->dcols[d]] = 1;
+        std::vector<int32_t> rptr((size_t)m + 1, 0), cptr((size_t)n + 1, 0);
+        for (int64_t sidx = 0; sidx < nnz; ++sidx) {
+            if (row_of[sidx] < 0) return fail(mh_internal_error(MH_ERR_INVALID, "a nonzero outside the block map"));
+            ++rptr[row_of[sidx] + 1];
+            if (!dense[col_of[sidx]]) ++cptr[col_of[sidx] + 1];
+        }
+        for (int64_t i = 0; i < m; ++i) rptr[i + 1] += rptr[i];
+        for (int64_t j = 0; j < n; ++j) cptr[j + 1] += cptr[j];
+        std::vector<int32_t> ccol((size_t)nnz), csrc((size_t)nnz), crow((size_t)nnz), fill(rptr.begin(), rptr.end() - 1);
+        for (int64_t sidx = 0; sidx < nnz; ++sidx) {   // rows in nonzero order: columns ascending within a row
+            const int32_t p = fill[row_of[sidx]]++;
+            ccol[p] = col_of[sidx];
+            csrc[p] = (int32_t)sidx;
+            crow[p] = row_of[sidx];
+        }
+        std::vector<int32_t> kr((size_t)cptr[n]), kp((size_t)cptr[n]), cfill(cptr.begin(), cptr.end() - 1);
+        for (int64_t p = 0; p < nnz; ++p)              // CSR order: rows ascending within a column
+            if (!dense[ccol[p]]) {
+                const int32_t q = cfill[ccol[p]]++;
+                kr[q] = crow[p];
+                kp[q] = (int32_t)p;
+            }
+        if ((rc = kupload(h, &h->csr_ptr, rptr)) || (rc = kupload(h, &h->csr_col, ccol)) ||
+            (rc = kupload(h, &h->csr_src, csrc)) || (rc = kupload(h, &h->csr_row, crow)) ||
+            (rc = kupload(h, &h->csc_ptr, cptr)) || (rc = kupload(h, &h->csc_row, kr)) ||
+            (rc = kupload(h, &h->csc_pos, kp)) || (rc = kalloc(h, &h->cv, (size_t)nnz)))
+            return fail(rc);
+    }
+    if (hipHostMalloc((void**)&h->hm, sizeof(double) * std::max<int64_t>(m, 1) * KMAX) != hipSuccess ||
+        hipHostMalloc((void**)&h->hn, sizeof(double) * std::max<int64_t>(n, 1) * KMAX) != hipSuccess)
+        return fail(mh_internal_error(MH_ERR_HIP, "pinned staging allocation failed"));
     std::vector<double> ones((size_t)m, 1.0);
     if (hipMemcpy(h->rs, ones.data(), sizeof(double) * m, hipMemcpyHostToDevice) != hipSuccess)
         return fail(mh_internal_error(MH_ERR_HIP, "upload failed"));
@@ -854,6 +876,8 @@ static int gather(mh_kkt* h, hipStream_t s) {
         hipLaunchKernelGGL(k_kkt_gather_dense, dim3(nblk(nj, 256)), dim3(256), 0, s, nj, h->nd, h->d_src, h->vals,
                            h->rs, h->Jd);
     }
+    hipLaunchKernelGGL(k_kkt_csr_vals, dim3(nblk(h->nnz, 256)), dim3(256), 0, s, h->nnz, h->csr_src, h->csr_row,
+                       h->vals, h->rs, h->cv);
     KCHK(hipGetLastError());
     return MH_OK;
 }
@@ -951,8 +975,10 @@ extern "C" int mh_kkt_factor(mh_kkt* h, const double* w, const double* dc, int32
     KCHK(hipSetDevice(h->device));
     hipStream_t s = mh_internal_stream(h->ctx);
     const int r = h->r;
-    KCHK(hipMemcpyAsync(h->w, w, sizeof(double) * h->n, hipMemcpyHostToDevice, s));
-    KCHK(hipMemcpyAsync(h->dc, dc, sizeof(double) * h->m, hipMemcpyHostToDevice, s));
+    std::memcpy(h->hn, w, sizeof(double) * h->n);
+    std::memcpy(h->hm, dc, sizeof(double) * h->m);
+    KCHK(hipMemcpyAsync(h->w, h->hn, sizeof(double) * h->n, hipMemcpyHostToDevice, s));
+    KCHK(hipMemcpyAsync(h->dc, h->hm, sizeof(double) * h->m, hipMemcpyHostToDevice, s));
     KCHK(hipMemsetAsync(h->status, 0, sizeof(int), s));
     const size_t lds = sizeof(double) * r * r;
     const int use_lds = lds + 64 <= (size_t)LDS_MAX ? 1 : 0;
@@ -968,9 +994,7 @@ extern "C" int mh_kkt_factor(mh_kkt* h, const double* w, const double* dc, int32
         if (tl > 65536)
             KCHK(hipFuncSetAttribute((const void*)k_kkt_trsm, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tl));
     }
-    const size_t plds = sizeof(double) * ((size_t)r * (r + 1) + (size_t)(r + INV_TB) * (INV_TB + 1));
-    if (h->inv_path && plds > 65536)
-        KCHK(hipFuncSetAttribute((const void*)k_kkt_potri, hipFuncAttributeMaxDynamicSharedMemorySize, (int)plds));
+    const potri_fn potri = potri_kernel(r);
     const int nbc = h->nb * h->c, nbr = h->nb * r;
     int rc = run_sequence(h, s, h->g_factor, [&]() {
         hipLaunchKernelGGL(k_kkt_local, dim3(nblk(std::max(nbc, nbr), 256)), dim3(256), 0, s, nbc, nbr, h->colmap,
@@ -982,7 +1006,7 @@ extern "C" int mh_kkt_factor(mh_kkt* h, const double* w, const double* dc, int32
         for (const KLevel& L : h->levels) {
             if (h->inv_path) {
                 // D_i -> inv(L_i); U, V, the even updates: GEMMs
-                hipLaunchKernelGGL(k_kkt_potri, dim3((unsigned)L.n_odd), dim3(256), plds, s, L.potrf, r, h->status);
+                hipLaunchKernelGGL(potri, dim3((unsigned)L.n_odd), dim3(256), 0, s, L.potrf, r, h->status);
                 launch_gemm(s, L.inv_u, L.n_u, r, r, r, r, 1, 1, r, r, 1.0, 0.0);
                 launch_gemm(s, L.inv_v, L.n_v, r, r, r, r, 1, r, 1, r, 1.0, 0.0);
                 launch_gemm(s, L.gemm_d, L.n_d, r, r, r, 1, r, 1, r, r, -1.0, 1.0);
@@ -1018,10 +1042,12 @@ extern "C" int mh_kkt_solve(mh_kkt* h, int32_t k, const double* b, double* xout)
     for (int k0 = 0; k0 < k; k0 += KMAX) {
         const int kc = std::min(KMAX, k - k0);
         // the chunk's columns, row-major [m][kc]
-        std::vector<double> in((size_t)h->m * kc);
-        for (int64_t i = 0; i < h->m; ++i)
-            std::memcpy(&in[(size_t)i * kc], b + (size_t)i * k + k0, sizeof(double) * kc);
-        KCHK(hipMemcpyAsync(h->bm, in.data(), sizeof(double) * in.size(), hipMemcpyHostToDevice, s));
+        double* in = h->hm;
+        if (kc == k) std::memcpy(in, b, sizeof(double) * h->m * kc);
+        else
+            for (int64_t i = 0; i < h->m; ++i)
+                std::memcpy(in + (size_t)i * kc, b + (size_t)i * k + k0, sizeof(double) * kc);
+        KCHK(hipMemcpyAsync(h->bm, in, sizeof(double) * h->m * kc, hipMemcpyHostToDevice, s));
         int rc = run_sequence(h, s, h->g_solve[kc], [&]() {
             hipLaunchKernelGGL(k_kkt_to_blocks, dim3(nblk(nbr * kc, 256)), dim3(256), 0, s, nbr, kc, h->rowmap,
                                h->bm, h->X);
@@ -1052,13 +1078,28 @@ extern "C" int mh_kkt_solve(mh_kkt* h, int32_t k, const double* b, double* xout)
                                h->X, h->bm);
         });
         if (rc) return rc;
-        KCHK(hipMemcpyAsync(in.data(), h->bm, sizeof(double) * in.size(), hipMemcpyDeviceToHost, s));
+        KCHK(hipMemcpyAsync(in, h->bm, sizeof(double) * h->m * kc, hipMemcpyDeviceToHost, s));
         KCHK(hipStreamSynchronize(s));
-        for (int64_t i = 0; i < h->m; ++i)
-            std::memcpy(xout + (size_t)i * k + k0, &in[(size_t)i * kc], sizeof(double) * kc);
+        if (kc == k) std::memcpy(xout, in, sizeof(double) * h->m * kc);
+        else
+            for (int64_t i = 0; i < h->m; ++i)
+                std::memcpy(xout + (size_t)i * k + k0, in + (size_t)i * kc, sizeof(double) * kc);
     }
     return MH_OK;
 }
+
+// a host [rows][k] matrix's columns k0 .. k0 + kc -> pinned [rows][kc], and back
+static void pack(double* dst, const double* src, int64_t rows, int k, int k0, int kc) {
+    if (kc == k) std::memcpy(dst, src, sizeof(double) * rows * kc);
+    else
+        for (int64_t i = 0; i < rows; ++i) std::memcpy(dst + (size_t)i * kc, src + (size_t)i * k + k0, sizeof(double) * kc);
+}
+static void unpack(double* dst, const double* src, int64_t rows, int k, int k0, int kc) {
+    if (kc == k) std::memcpy(dst, src, sizeof(double) * rows * kc);
+    else
+        for (int64_t i = 0; i < rows; ++i) std::memcpy(dst + (size_t)i * k + k0, src + (size_t)i * kc, sizeof(double) * kc);
+}
+constexpr int SPMV_G = 8;
 
 extern "C" int mh_kkt_jmul(mh_kkt* h, int32_t k, const double* v, double* y) {
     if (!h || !v || !y || k < 1) return mh_internal_error(MH_ERR_INVALID, "bad argument");
@@ -1066,15 +1107,14 @@ extern "C" int mh_kkt_jmul(mh_kkt* h, int32_t k, const double* v, double* y) {
     hipStream_t s = mh_internal_stream(h->ctx);
     for (int k0 = 0; k0 < k; k0 += KMAX) {
         const int kc = std::min(KMAX, k - k0);
-        std::vector<double> in((size_t)h->n * kc), o((size_t)h->m * kc);
-        for (int64_t j = 0; j < h->n; ++j) std::memcpy(&in[(size_t)j * kc], v + (size_t)j * k + k0, sizeof(double) * kc);
-        KCHK(hipMemcpyAsync(h->bn, in.data(), sizeof(double) * in.size(), hipMemcpyHostToDevice, s));
-        hipLaunchKernelGGL(k_kkt_jmul, dim3(h->nb), dim3(256), 0, s, h->r, h->c, h->nd, kc, h->A, h->rowmap,
-                           h->colmap, h->Jd, h->dcols, h->bn, h->bm);
+        pack(h->hn, v, h->n, k, k0, kc);
+        KCHK(hipMemcpyAsync(h->bn, h->hn, sizeof(double) * h->n * kc, hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(k_kkt_spmv<SPMV_G>, dim3(nblk(h->m * kc * SPMV_G, 256)), dim3(256), 0, s, h->m, kc,
+                           h->csr_ptr, h->csr_col, (const int32_t*)nullptr, h->cv, h->bn, h->bm);
         KCHK(hipGetLastError());
-        KCHK(hipMemcpyAsync(o.data(), h->bm, sizeof(double) * o.size(), hipMemcpyDeviceToHost, s));
+        KCHK(hipMemcpyAsync(h->hm, h->bm, sizeof(double) * h->m * kc, hipMemcpyDeviceToHost, s));
         KCHK(hipStreamSynchronize(s));
-        for (int64_t i = 0; i < h->m; ++i) std::memcpy(y + (size_t)i * k + k0, &o[(size_t)i * kc], sizeof(double) * kc);
+        unpack(y, h->hm, h->m, k, k0, kc);
     }
     return MH_OK;
 }
@@ -1085,20 +1125,17 @@ extern "C" int mh_kkt_jtmul(mh_kkt* h, int32_t k, const double* y, double* v) {
     hipStream_t s = mh_internal_stream(h->ctx);
     for (int k0 = 0; k0 < k; k0 += KMAX) {
         const int kc = std::min(KMAX, k - k0);
-        std::vector<double> in((size_t)h->m * kc), o((size_t)h->n * kc);
-        for (int64_t i = 0; i < h->m; ++i) std::memcpy(&in[(size_t)i * kc], y + (size_t)i * k + k0, sizeof(double) * kc);
-        KCHK(hipMemcpyAsync(h->bm, in.data(), sizeof(double) * in.size(), hipMemcpyHostToDevice, s));
-        hipLaunchKernelGGL(k_kkt_jtmul_blocks, dim3(h->nb), dim3(256), 0, s, h->r, h->c, kc, h->A, h->rowmap, h->bm,
-                           h->z);
-        hipLaunchKernelGGL(k_kkt_jtmul_collect, dim3(nblk(h->n * kc, 256)), dim3(256), 0, s, h->n, kc, h->col2, h->z,
-                           h->bn);
+        pack(h->hm, y, h->m, k, k0, kc);
+        KCHK(hipMemcpyAsync(h->bm, h->hm, sizeof(double) * h->m * kc, hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(k_kkt_spmv<SPMV_G>, dim3(nblk(h->n * kc * SPMV_G, 256)), dim3(256), 0, s, h->n, kc,
+                           h->csc_ptr, h->csc_row, h->csc_pos, h->cv, h->bm, h->bn);
         if (h->nd)
             hipLaunchKernelGGL(k_kkt_jtmul_dense, dim3(h->nd, kc), dim3(256), 0, s, h->m, h->nd, kc, h->Jd, h->dcols,
                                h->bm, h->bn);
         KCHK(hipGetLastError());
-        KCHK(hipMemcpyAsync(o.data(), h->bn, sizeof(double) * o.size(), hipMemcpyDeviceToHost, s));
+        KCHK(hipMemcpyAsync(h->hn, h->bn, sizeof(double) * h->n * kc, hipMemcpyDeviceToHost, s));
         KCHK(hipStreamSynchronize(s));
-        for (int64_t j = 0; j < h->n; ++j) std::memcpy(v + (size_t)j * k + k0, &o[(size_t)j * kc], sizeof(double) * kc);
+        unpack(v, h->hn, h->n, k, k0, kc);
     }
     return MH_OK;
 }

@@ -96,9 +96,15 @@ class IpmOptions:
     # the Newton systems' linear algebra: "host" (scipy / LAPACK over J
     # copied to the host), "device" (include/mocohip_kkt.h: J stays in HBM,
     # the Schur complement is factored on the GPU), "auto" (device when the
-    # NLP offers a device KKT module -- HipNLP -- and its Jacobian has the
-    # per-interval block structure, else host)
+    # NLP offers a device KKT module -- HipNLP --, its Jacobian has the
+    # per-interval block structure and it has at least
+    # device_kkt_min_constraints rows, else host: below that a banded host
+    # factorization costs less than the device's per-call latency chain --
+    # Rajagopal-18's MocoInverse, m = 1347, solves in 0.25 s on the host and
+    # 0.65 s on the device; the gait MocoInverse at N = 125, m = 16046, in
+    # 1.27 s and 0.57 s)
     linear_solver: str = "auto"
+    device_kkt_min_constraints: int = 5000
     kappa_soc: float = 0.99
     # after the restoration phase (Ipopt 3.12 IpRestoMinC_1Nrm): the least-
     # squares constraint multipliers are kept only when their max-norm is at
@@ -317,7 +323,8 @@ def _linear_algebra(nlp, P, opt):
     want = opt.linear_solver
     if want not in ("auto", "host", "device"):
         raise ValueError("linear_solver must be 'auto', 'host' or 'device'")
-    if want != "host" and P.m and hasattr(nlp, "device_kkt"):
+    big = P.m >= opt.device_kkt_min_constraints
+    if (want == "device" or (want == "auto" and big)) and P.m and hasattr(nlp, "device_kkt"):
         try:
             dk = nlp.device_kkt()
         except (ValueError, RuntimeError):

@@ -43,7 +43,7 @@ def _setup(name, seed=0):
 @pytest.mark.parametrize("name", sorted(CASES))
 def test_device_kkt_matches_restatement(name, path, monkeypatch):
     """Both factorization paths of csrc/kkt.hip: blocks inverted in LDS and
-    every step a GEMM (default for r <= 132), or substitution
+    every step a GEMM (default for r <= 160), or substitution
     (MOCOHIP_KKT_INV=0; the path large blocks take)."""
     monkeypatch.setenv("MOCOHIP_KKT_INV", "1" if path == "inverse" else "0")
     nlp, x, rng = _setup(name)
@@ -62,7 +62,10 @@ def test_device_kkt_matches_restatement(name, path, monkeypatch):
         J = sp.csr_matrix((vals * rs[ir], (ir, jc)), shape=(nlp.m, nlp.n))
         V = rng.standard_normal((nlp.n, 3))
         Y = rng.standard_normal((nlp.m, 3))
-        for got, want in ((dk.jmul(V), J @ V), (dk.jtmul(Y), J.T @ Y), (dk.jmul(V[:, 0]), J @ V[:, 0])):
+        V40 = rng.standard_normal((nlp.n, 40))                 # two passes of 32 and 8 columns
+        Y40 = rng.standard_normal((nlp.m, 40))
+        for got, want in ((dk.jmul(V), J @ V), (dk.jtmul(Y), J.T @ Y), (dk.jmul(V[:, 0]), J @ V[:, 0]),
+                          (dk.jmul(V40), J @ V40), (dk.jtmul(Y40), J.T @ Y40)):
             assert np.abs(got - want).max() <= 1e-12 * (np.abs(want).max() + 1.0)
         cols, Jd = dk.dense_columns()
         assert np.array_equal(cols, bm.dcols)
