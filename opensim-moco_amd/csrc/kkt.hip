@@ -63,6 +63,7 @@ int mh_internal_jac_device(mh_ctx* c, const double* x_dev, double* v_dev);
 namespace {
 
 constexpr int KMAX = 32;              // right-hand sides per solve pass
+constexpr int INV_RMAX_SK = 160;      // the skinny products' largest K (= INV_RMAX)
 constexpr int LDS_MAX = 160 * 1024;   // gfx950 LDS per workgroup
 
 // C = alpha (P diag(w) Q^T + P2 Q2^T) + beta C (P2 null: the first product only)
@@ -144,7 +145,7 @@ __global__ void k_kkt_add_diag(int r, const double* __restrict__ dcl, double* __
 __global__ __launch_bounds__(256) void k_kkt_gemm(const KTask* __restrict__ tasks, int M, int N, int K,
                                                   int psi, int psk, int qsi, int qsk, int ldc,
                                                   double alpha, double beta) {
-    constexpr int TM = 64, TN = 64, TK = 16;
+    constexpr int TM = 64, TN = 64, TK = 32;    // K = 128: 4 load rounds per product
     constexpr int PL = TM * TK / 256, QL = TN * TK / 256;   // elements per thread per tile
     __shared__ double Ps[TK][TM + 1];
     __shared__ double Qs[TK][TN + 1];
@@ -226,6 +227,77 @@ __global__ __launch_bounds__(256) void k_kkt_gemm(const KTask* __restrict__ task
             double* cp = t.C + (int64_t)gi * ldc + gj;
             *cp = beta == 0.0 ? alpha * acc[a][b] : alpha * acc[a][b] + beta * *cp;
         }
+    }
+}
+
+// The solves' products, C = alpha (P diag(w) Q^T + P2 Q2^T) + beta C with few
+// columns (N <= NT <= KMAX right-hand sides): one workgroup per (task, 32
+// rows).  Q (and Q2) are staged whole in LDS in one round of loads; each row
+// is 8 threads' fixed-stride partial sums (k = s, s + 8, ...), their P loads
+// all in flight at once, combined by a fixed butterfly: deterministic.  In
+// place of k_kkt_gemm's 64 x 64 tiles, whose K loop of dependent load rounds
+// set the latency of every solve step.
+constexpr int SK_ROWS = 32;
+constexpr int SK_KPT = INV_RMAX_SK / 8;               // P values per thread and product
+template <int NT>
+__global__ __launch_bounds__(256) void k_kkt_gemm_skinny(const KTask* __restrict__ tasks, int M, int N, int K,
+                                                         int psi, int psk, int qsi, int qsk, int ldc,
+                                                         double alpha, double beta) {
+    extern __shared__ double qs[];                    // [npair][K][NP]
+    constexpr int NP = NT == 1 ? 1 : NT + 1;          // padded rows: the 8 sub-lanes' k rows hit distinct banks
+    const KTask t = tasks[blockIdx.y];
+    const int npair = t.P2 ? 2 : 1;
+    const int tid = threadIdx.x;
+    const int i = blockIdx.x * SK_ROWS + (tid >> 3), sl = tid & 7;
+    const int ic = min(i, M - 1);
+    // this thread's P values first (independent of the staging: in flight
+    // beside it), k = sl, sl + 8, ...
+    double pv[2][SK_KPT];
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+        const double* __restrict__ Pp = pr ? t.P2 : t.P;
+        const double* __restrict__ wp = pr ? nullptr : t.w;
+#pragma unroll
+        for (int u = 0; u < SK_KPT; ++u) {
+            const int k = 8 * u + sl;
+            pv[pr][u] = (pr < npair && k < K) ? Pp[(int64_t)ic * psi + (int64_t)k * psk] * (wp ? wp[k] : 1.0) : 0.0;
+        }
+    }
+    for (int e = tid; e < npair * K * NT; e += 256) {
+        const int pr = e / (K * NT), rem = e - pr * K * NT, k = rem / NT, j = rem - k * NT;
+        const double* __restrict__ Qp = pr ? t.Q2 : t.Q;
+        qs[(pr * K + k) * NP + j] = j < N ? Qp[(int64_t)j * qsi + (int64_t)k * qsk] : 0.0;
+    }
+    double acc[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[j] = 0.0;
+    __syncthreads();
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+        if (pr >= npair) break;
+        const double* qp = qs + (size_t)pr * K * NP;
+#pragma unroll
+        for (int u = 0; u < SK_KPT; ++u) {
+            const int k = 8 * u + sl;
+            if (k < K) {
+#pragma unroll
+                for (int j = 0; j < NT; ++j) acc[j] = fma(pv[pr][u], qp[k * NP + j], acc[j]);
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        acc[j] += __shfl_xor(acc[j], 4, 8);
+        acc[j] += __shfl_xor(acc[j], 2, 8);
+        acc[j] += __shfl_xor(acc[j], 1, 8);
+    }
+    if (i < M) {
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+            if (j % 8 == sl && j < N) {
+                double* cp = t.C + (int64_t)i * ldc + j;
+                *cp = beta == 0.0 ? alpha * acc[j] : alpha * acc[j] + beta * *cp;
+            }
     }
 }
 
@@ -360,6 +432,7 @@ __global__ __launch_bounds__(256) void k_kkt_trsm(const KTri* __restrict__ tasks
 // optimizer's iterative refinement absorbs.
 constexpr int INV_T = 10;                 // register tile edge: r <= 16 INV_T
 constexpr int INV_RMAX = 16 * INV_T;
+static_assert(INV_RMAX == INV_RMAX_SK, "skinny product K bound");
 // In-place inverse Cholesky in registers.  Z starts as A; step k reads row k
 // of Z (w) and, for every row i > k,
 //     Z[i, c] <- (c == k ? 0 : Z[i, c]) - w[i] (c == k ? 1 : w[c]) / w[k],
@@ -369,9 +442,11 @@ constexpr int INV_RMAX = 16 * INV_T;
 // Cholesky, kept symmetric, so row k also holds column k); columns c <= k
 // accumulate inv(L) (the identity eliminated by the same row operations).
 // After step r - 1 the lower triangle of Z is inv(L).  Thread (ty, tx) of a
-// 16 x 16 grid holds rows ty T + a (blocked: a thread whose rows are all done
-// skips its update) and columns tx + 16 b (interleaved: row k's broadcast is
-// one contiguous, conflict-free LDS line).  One barrier per step (w double
+// 16 x 16 grid holds the T x T tile of rows ty T + a and columns tx T + b;
+// the steps run in unrolled runs of T, so step k = k0 + ii's row and column
+// are register (.., ii) of the threads with ty (tx) = k0 / T -- no dynamic
+// register index, no selects over the tile -- and a thread whose rows are
+// all done (ty < k0 / T) skips its update.  One barrier per step (w double
 // buffered); LDS holds 2 rows.
 template <int T>
 __global__ __launch_bounds__(256) void k_kkt_potri(double* const* __restrict__ mats, int r, int* __restrict__ status) {
@@ -380,13 +455,13 @@ __global__ __launch_bounds__(256) void k_kkt_potri(double* const* __restrict__ m
     __shared__ int bad;
     double* a = mats[blockIdx.x];
     const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
-    const int row0 = ty * T;
+    const int row0 = ty * T, col0 = tx * T;
     double z[T][T];
 #pragma unroll
     for (int i = 0; i < T; ++i)
 #pragma unroll
         for (int j = 0; j < T; ++j) {
-            const int row = row0 + i, col = tx + 16 * j;
+            const int row = row0 + i, col = col0 + j;
             const double v = a[(size_t)min(row, r - 1) * r + min(col, r - 1)];
             z[i][j] = (row < r && col < r) ? v : 0.0;
         }
@@ -394,44 +469,42 @@ __global__ __launch_bounds__(256) void k_kkt_potri(double* const* __restrict__ m
     // every LDS read below is unconditional, so none waits inside a branch
     for (int e = tid; e < 2 * 16 * INV_T; e += 256) (&wbuf[0][0])[e] = 0.0;
     if (tid == 0) bad = 0;
-    // k's owner coordinates are uniform (scalar branches); the per-lane work
-    // is branch-free: rows <= k get f = 0
-    for (int k = 0; k < r; ++k) {
-        double* w = wbuf[k & 1];
-        const int tyk = k / T, ik = k - tyk * T, jk = k >> 4, txk = k & 15;
-        if (ty == tyk) {
+    __syncthreads();                                 // zeros in before step 0's row
+    for (int k0 = 0; k0 < r; k0 += T) {
+        const int tk = k0 / T;                       // the owners' ty (row) and tx (column)
 #pragma unroll
-            for (int i = 0; i < T; ++i)
-                if (i == ik) {
+        for (int ii = 0; ii < T; ++ii) {
+            const int k = k0 + ii;
+            if (k >= r) break;                       // uniform
+            double* w = wbuf[k & 1];
+            if (ty == tk) {
 #pragma unroll
-                    for (int j = 0; j < T; ++j) w[tx + 16 * j] = z[i][j];   // 0 past r
-                }
-        }
-        __syncthreads();
-        const double p = w[k];
-        const double pp = (p > 0.0 && isfinite(p)) ? p : 1.0;
-        if (tid == 0) {
-            if (pp != p) bad = 1;
-            piv[k] = pp;
-        }
-        if (row0 + T - 1 < k) continue;              // every row of this thread done
-        const double pinv = 1.0 / pp;
-        double wc[T], f[T];
+                for (int j = 0; j < T; ++j) w[col0 + j] = z[ii][j];   // 0 past r
+            }
+            __syncthreads();
+            const double p = w[k];
+            const double pp = (p > 0.0 && isfinite(p)) ? p : 1.0;
+            if (tid == 0) {
+                if (pp != p) bad = 1;
+                piv[k] = pp;
+            }
+            if (ty < tk) continue;                   // every row of this thread done
+            const double pinv = 1.0 / pp;
+            double wc[T], f[T];
 #pragma unroll
-        for (int j = 0; j < T; ++j) wc[j] = w[tx + 16 * j];
+            for (int j = 0; j < T; ++j) wc[j] = w[col0 + j];
 #pragma unroll
-        for (int i = 0; i < T; ++i) f[i] = w[row0 + i] * (row0 + i > k ? pinv : 0.0);
+            for (int i = 0; i < T; ++i) f[i] = w[row0 + i] * (row0 + i > k ? pinv : 0.0);
+            if (tx == tk) {                          // column k of rows > k: restart at 0, w = 1
+                wc[ii] = 1.0;
 #pragma unroll
-        for (int j = 0; j < T; ++j)
-            if (j == jk && tx == txk) {              // column k of rows > k: restart at 0, w = 1
-                wc[j] = 1.0;
-#pragma unroll
-                for (int i = 0; i < T; ++i) z[i][j] = row0 + i > k ? 0.0 : z[i][j];
+                for (int i = 0; i < T; ++i) z[i][ii] = row0 + i > k ? 0.0 : z[i][ii];
             }
 #pragma unroll
-        for (int i = 0; i < T; ++i)
+            for (int i = 0; i < T; ++i)
 #pragma unroll
-            for (int j = 0; j < T; ++j) z[i][j] = fma(-f[i], wc[j], z[i][j]);
+                for (int j = 0; j < T; ++j) z[i][j] = fma(-f[i], wc[j], z[i][j]);
+        }
     }
     __syncthreads();
     // row i of inv(L): its unscaled row over columns < i, times 1 / sqrt(p_i),
@@ -443,7 +516,7 @@ __global__ __launch_bounds__(256) void k_kkt_potri(double* const* __restrict__ m
         const double dinv = 1.0 / sqrt(row < r ? piv[row] : 1.0);
 #pragma unroll
         for (int j = 0; j < T; ++j) {
-            const int col = tx + 16 * j;
+            const int col = col0 + j;
             z[i][j] = col < row ? z[i][j] * dinv : (col == row ? dinv : z[i][j]);
         }
     }
@@ -452,7 +525,7 @@ __global__ __launch_bounds__(256) void k_kkt_potri(double* const* __restrict__ m
     for (int i = 0; i < T; ++i)
 #pragma unroll
         for (int j = 0; j < T; ++j) {
-            const int row = row0 + i, col = tx + 16 * j;
+            const int row = row0 + i, col = col0 + j;
             if (row < r && col < r) a[(size_t)row * r + col] = col <= row ? z[i][j] : 0.0;
         }
     if (tid == 0 && bad) *status = 1;
@@ -839,6 +912,11 @@ extern "C" int mh_kkt_create(mh_ctx* ctx, const mh_kkt_layout* L, mh_kkt** out) 
             (rc = kupload(h, &h->csc_pos, kp)) || (rc = kalloc(h, &h->cv, (size_t)nnz)))
             return fail(rc);
     }
+    // the 32-column skinny product's pair of staged operands exceeds the
+    // default 64 KB of dynamic LDS at K = INV_RMAX
+    if (hipFuncSetAttribute((const void*)k_kkt_gemm_skinny<32>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)(sizeof(double) * 2 * INV_RMAX * 33)) != hipSuccess)
+        return fail(mh_internal_error(MH_ERR_HIP, "hipFuncSetAttribute (skinny product LDS) failed"));
     if (hipHostMalloc((void**)&h->hm, sizeof(double) * std::max<int64_t>(m, 1) * KMAX) != hipSuccess ||
         hipHostMalloc((void**)&h->hn, sizeof(double) * std::max<int64_t>(n, 1) * KMAX) != hipSuccess)
         return fail(mh_internal_error(MH_ERR_HIP, "pinned staging allocation failed"));
@@ -914,9 +992,26 @@ extern "C" int mh_kkt_get_dense(mh_kkt* h, double* Jd) {
     return MH_OK;
 }
 
+template <int NT>
+static void launch_skinny(hipStream_t s, const KTask* tasks, int ntasks, int M, int N, int K, int psi, int psk,
+                          int qsi, int qsk, int ldc, double alpha, double beta) {
+    // LDS for a pair of operands (the tasks of one launch share their shape;
+    // single-product tasks use half)
+    const size_t lds = sizeof(double) * 2 * (size_t)K * (NT == 1 ? 1 : NT + 1);
+    hipLaunchKernelGGL(k_kkt_gemm_skinny<NT>, dim3(nblk(M, SK_ROWS), (unsigned)ntasks), dim3(256), lds, s, tasks, M,
+                       N, K, psi, psk, qsi, qsk, ldc, alpha, beta);
+}
 static void launch_gemm(hipStream_t s, const KTask* tasks, int ntasks, int M, int N, int K, int psi, int psk,
                         int qsi, int qsk, int ldc, double alpha, double beta) {
     if (ntasks <= 0) return;
+    if (N <= KMAX && K <= INV_RMAX) {           // the solves: a few right-hand sides
+        if (N <= 1) return launch_skinny<1>(s, tasks, ntasks, M, N, K, psi, psk, qsi, qsk, ldc, alpha, beta);
+        if (N <= 2) return launch_skinny<2>(s, tasks, ntasks, M, N, K, psi, psk, qsi, qsk, ldc, alpha, beta);
+        if (N <= 4) return launch_skinny<4>(s, tasks, ntasks, M, N, K, psi, psk, qsi, qsk, ldc, alpha, beta);
+        if (N <= 8) return launch_skinny<8>(s, tasks, ntasks, M, N, K, psi, psk, qsi, qsk, ldc, alpha, beta);
+        if (N <= 16) return launch_skinny<16>(s, tasks, ntasks, M, N, K, psi, psk, qsi, qsk, ldc, alpha, beta);
+        return launch_skinny<32>(s, tasks, ntasks, M, N, K, psi, psk, qsi, qsk, ldc, alpha, beta);
+    }
     hipLaunchKernelGGL(k_kkt_gemm, dim3(nblk(N, 64), nblk(M, 64), (unsigned)ntasks), dim3(256), 0, s, tasks, M, N,
                        K, psi, psk, qsi, qsk, ldc, alpha, beta);
 }
