@@ -59,11 +59,23 @@ extern "C" const char* mh_last_error(void) { return g_err.c_str(); }
 // interval; blockIdx.x < nchunks streams Jacobian nonzeros (values != null),
 // the last x-block (when g != null) writes the interval's defect /
 // interpolation rows.
+//
+// ctpl (the compiled template of k_interval, core.hpp CT_*): a nonzero is
+// base + coef q with q one quotient of the interval's Y run -- the interval's
+// grid points are consecutive, so their Y rows form the [point][NO][stride]
+// run the words' offsets index -- read with one 4-byte word (and its row's
+// base-lane offset) instead of a TplEntry and the formula's branches; t0 / tf
+// (CT_GEN) and path (CT_PATH) entries take jac_entry.  The same operations in
+// the same order as jac_entry: bit-identical (MOCOHIP_CTPL=0 compares).
+constexpr int ASM_CHUNK_CT = 8192;   // nonzeros per compiled-template assembly workgroup
+__device__ __forceinline__ double ct_select(uint32_t k, double a1, double a2, double a3, double a4, double a5) {
+    return k == 1 ? a1 : k == 2 ? a2 : k == 3 ? a3 : k == 4 ? a4 : k == 5 ? a5 : 0.0;
+}
 __global__ void __launch_bounds__(256) k_transcribe(Layout L, Interval I, Lanes Ln,
-        const TplEntry* __restrict__ tpl, const double* __restrict__ x,
+        const TplEntry* __restrict__ tpl, const uint32_t* __restrict__ ctpl, const double* __restrict__ x,
         const double* __restrict__ grid, const double* __restrict__ times,
         const double* __restrict__ Y, double* __restrict__ g, double* __restrict__ values,
-        int nchunks, int yq) {
+        int nchunks, int yq, int chunk) {
     const int il = blockIdx.y;
     const int i = I.ib + il;
     const YG YV{Y, times, L.NO, Ln.stride, L.k0, yq, x, L.NS, L.NC, L.G, L.NDV, L.DB};
@@ -72,9 +84,65 @@ __global__ void __launch_bounds__(256) k_transcribe(Layout L, Interval I, Lanes 
         interval_span(I, i, k_first, k_last);
         const IvC C = iv_const(YV.t(k_last) - YV.t(k_first), grid[k_last] - grid[k_first]);
         double* vi = values + (long)il * I.nnz_int;
-        const int e_end = min(I.entries(i), ((int)blockIdx.x + 1) * ASM_CHUNK);
-        for (int e = (int)blockIdx.x * ASM_CHUNK + threadIdx.x; e < e_end; e += blockDim.x)
-            vi[e] = jac_entry(L, Ln, I.P, x, YV, tpl[e], k_first, C);
+        const int e_end = min(I.entries(i), ((int)blockIdx.x + 1) * chunk);
+        if (ctpl) {   // chunks of ASM_CHUNK_CT entries
+#pragma clang fp contract(off)
+            const int npts = k_last - k_first + 1;
+            const uint32_t nyall = (uint32_t)(npts * L.NO * Ln.stride);
+            const uint32_t kconst = nyall + CT_CONST;
+            const double* __restrict__ Yi = Y + (long)(k_first - L.k0) * L.NO * Ln.stride;
+            const uint32_t* __restrict__ cbase = ctpl + I.nnz_int + I.nnz_tail;
+            const double h1 = Ln.h, h2 = 2.0 * Ln.h;
+            const double c4 = -C.h6 * 4.0;
+            const int eb = (int)blockIdx.x * chunk, ee = min(I.entries(i), eb + chunk);
+            // CT_U entries per thread per pass: their words, then their Y
+            // values, then their stores (independent loads in flight together)
+            constexpr int CT_U = 4;
+            for (int e0 = eb + (int)threadIdx.x; e0 < ee; e0 += CT_U * (int)blockDim.x) {
+                uint32_t w[CT_U], wb[CT_U];
+#pragma unroll
+                for (int u = 0; u < CT_U; ++u) {
+                    const int e = e0 + u * (int)blockDim.x;
+                    w[u] = e < ee ? ctpl[e] : CT_PATH;
+                    wb[u] = e < ee ? cbase[e] : 0u;
+                }
+                double ya[CT_U], yb[CT_U];
+#pragma unroll
+                for (int u = 0; u < CT_U; ++u) {
+                    const uint32_t off = w[u] & CT_OFF;
+                    const bool lane = !(w[u] & (CT_GEN | CT_PATH)) && off < nyall;
+                    ya[u] = lane ? Yi[off] : 0.0;
+                    yb[u] = 0.0;
+                    if (lane && !yq) yb[u] = Ln.fd == MH_FD_CENTRAL ? Yi[off + Ln.ND] : Yi[wb[u]];
+                }
+#pragma unroll
+                for (int u = 0; u < CT_U; ++u) {
+                    const int e = e0 + u * (int)blockDim.x;
+                    if (e >= ee) break;
+                    if (w[u] & (CT_GEN | CT_PATH)) {
+                        vi[e] = jac_entry(L, Ln, I.P, x, YV, tpl[e], k_first, C);
+                        continue;
+                    }
+                    const uint32_t off = w[u] & CT_OFF;
+                    double q;
+                    if (off >= nyall) q = off == kconst + 1 ? 1.0 : 0.0;
+                    else if (yq) q = ya[u];
+                    else if (Ln.fd == MH_FD_CENTRAL) q = (ya[u] - yb[u]) / h2;
+                    else if (Ln.fd == MH_FD_FORWARD) q = (ya[u] - yb[u]) / h1;
+                    else q = (yb[u] - ya[u]) / h1;
+                    if (w[u] & CT_RAW) {
+                        vi[e] = q;
+                    } else {
+                        const double coef = ct_select((w[u] >> 20) & 7, -C.h8, C.h8, -C.h6, c4, -C.hh);
+                        const double base = ct_select((w[u] >> 23) & 7, -0.5, 1.0, -1.0, 0.0, 0.0);
+                        vi[e] = base + coef * q;
+                    }
+                }
+            }
+        } else {
+            for (int e = (int)blockIdx.x * chunk + threadIdx.x; e < e_end; e += blockDim.x)
+                vi[e] = jac_entry(L, Ln, I.P, x, YV, tpl[e], k_first, C);
+        }
     } else {
         double* gi = g + (long)il * I.rpi;
         for (int r = threadIdx.x; r < I.rows(i); r += blockDim.x) gi[r] = defect_row(L, I, Ln, x, YV, i, r);
@@ -1778,7 +1846,11 @@ static int launch_stage(mh_ctx* c, int stage, int kind, const double* x, double*
     Layout L = make_layout(c, c->k0, c->nk);
     const Lanes& ln = kind == 0 ? c->lanes_g : c->lanes_jac;
     const double* Y = kind == 0 ? c->d_Yg : c->d_Y;
-    const int nchunks = kind == 0 ? 0 : (c->nnz_int + (c->ie == c->N ? c->nnz_tail : 0) + ASM_CHUNK - 1) / ASM_CHUNK;
+    // the compiled-template assembly's workgroups take ASM_CHUNK_CT nonzeros
+    // each (a few per thread and pass: per-workgroup setup, not the stores,
+    // bounded ASM_CHUNK-sized ones); jac_entry's ASM_CHUNK
+    const int chunk = c->use_ctpl ? ASM_CHUNK_CT : ASM_CHUNK;
+    const int nchunks = kind == 0 ? 0 : (c->nnz_int + (c->ie == c->N ? c->nnz_tail : 0) + chunk - 1) / chunk;
     double* g = kind == 1 ? nullptr : a;
     double* v = kind == 0 ? nullptr : (kind == 1 ? a : b);
     if (c->use_interval[kind == 0 ? 0 : 1] && !glane) {
@@ -1795,8 +1867,8 @@ static int launch_stage(mh_ctx* c, int stage, int kind, const double* x, double*
                 c->d_grid, c->d_times, Y, g, v, nint, c->yq[kind == 0 ? 0 : 1]);
     } else {
         hipLaunchKernelGGL(k_transcribe, dim3((unsigned)(nchunks + (g ? 1 : 0)), (unsigned)nint), dim3(256), 0,
-                c->stream, L, I, ln, c->d_tpl, x, c->d_grid, c->d_times, Y, g, v, nchunks,
-                c->yq[kind == 0 ? 0 : 1]);
+                c->stream, L, I, ln, c->d_tpl, c->use_ctpl ? c->d_ctpl : nullptr, x, c->d_grid, c->d_times, Y, g,
+                v, nchunks, c->yq[kind == 0 ? 0 : 1], chunk);
     }
     HIPCHK(hipGetLastError());
     return MH_OK;

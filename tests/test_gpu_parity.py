@@ -809,6 +809,8 @@ def test_pruned_tasks_bit_identical(name):
 @pytest.mark.parametrize("variant", [{"MOCOHIP_INTERVAL": "0"},
                                      {"MOCOHIP_INTERVAL": "0", "MOCOHIP_ASM": "gs"},
                                      {"MOCOHIP_INTERVAL": "0", "MOCOHIP_QUOT": "1"},
+                                     {"MOCOHIP_INTERVAL": "0", "MOCOHIP_CTPL": "0"},
+                                     {"MOCOHIP_INTERVAL": "0", "MOCOHIP_QUOT": "1", "MOCOHIP_CTPL": "0"},
                                      {"MOCOHIP_CTPL": "0"},
                                      {"MOCOHIP_ROLES": "1"},
                                      {"MOCOHIP_ROLES": "1", "MOCOHIP_ROLE_COUPLE": "0"},
@@ -821,8 +823,9 @@ def test_kernel_variants_bit_identical(name, variant):
     jac_entry (MOCOHIP_CTPL=0), what k_role writes (one workgroup per mesh
     interval and grid point, the coupling entries in the time role or in
     k_couple) and what the split path writes through HBM: k_combine +
-    k_transcribe (chunked or grid-stride), with raw lane values or with
-    finite-difference quotients in Y."""
+    k_transcribe (chunked -- compiled-template words or jac_entry -- or
+    grid-stride), with raw lane values or with finite-difference quotients in
+    Y."""
     gpu, _, _ = _pair(name)
     split, _, _ = _pair(name, env=variant)
     for _, x in _iterates(gpu):
