@@ -531,20 +531,44 @@ struct TaskLoadGlobal {
     }
 };
 
+// cmap (nmap roles per grid point): the lanes to combine, the others being
+// excitation lanes k_exc_fill writes (null: every lane).
 template <class D>
 __global__ void __launch_bounds__(64) k_combine_global(DevModel M, Src S, Lanes Ln, Tasks TK,
         const double* __restrict__ T, const double* __restrict__ H, double* __restrict__ times,
-        double* __restrict__ Y, long ystride_pt) {
+        double* __restrict__ Y, long ystride_pt, const int* __restrict__ cmap, int nmap) {
     const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (gid >= (long)TK.nk * Ln.stride) return;
-    const int kl = (int)(gid / Ln.stride);
-    const int r = (int)(gid - (long)kl * Ln.stride);
+    const int per = cmap ? nmap : Ln.stride;
+    if (gid >= (long)TK.nk * per) return;
+    const int kl = (int)(gid / per);
+    const int j = (int)(gid - (long)kl * per);
+    const int r = cmap ? cmap[j] : j;
     double t;
     const LaneIn<D> in = lane_input<D>(S, Ln, kl, r, t);
     if (r == Ln.base && times) times[kl] = t;
     const TaskLoadGlobal<D> TL{T + (long)kl * TK.tdoubles, H + (long)kl * TK.nmass * D::NST,
                                TK.jd, r};
     D::combine(M, t, in, TL, StridedOut{Y + (long)kl * ystride_pt + r, (long)Ln.stride});
+}
+
+// Excitation lanes of a generated back end: a direction that perturbs the
+// excitation of one muscle with activation dynamics re-evaluates only that
+// muscle's activation group, whose one field is the activation derivative
+// output; every other output of its combine reads base-lane slots only, so
+// it equals the base lane's.  xs[2 r] = the group's slot for role r (-1: not
+// such a lane), xs[2 r + 1] = the output.  Bit-identical to combining the
+// lane (test_excitation_lanes_bit_identical, MOCOHIP_EXC_LANES=0).
+static __global__ void __launch_bounds__(256) k_exc_fill(int nk, int NO, int stride, int base, int tdoubles,
+        const int* __restrict__ xs, const double* __restrict__ T, double* __restrict__ Y) {
+    const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= (long)nk * stride) return;
+    const int kl = (int)(gid / stride);
+    const int r = (int)(gid - (long)kl * stride);
+    const int slot = xs[2 * r];
+    if (slot < 0) return;
+    double* Yk = Y + (long)kl * NO * stride;
+    for (int o = 0; o < NO; ++o) Yk[(long)o * stride + r] = Yk[(long)o * stride + base];
+    Yk[(long)xs[2 * r + 1] * stride + r] = T[(long)kl * tdoubles + slot];
 }
 
 // Copy n doubles to LDS with U loads in flight per thread before the first
@@ -1963,6 +1987,12 @@ struct mh_ctx {
     int* d_exc = nullptr;
     int* d_lane_map = nullptr;     // the other lanes, in order (k_eval's lane map)
     int n_exc_lanes = 0;
+    // generated back ends: per Jacobian lane (slot, output) of an excitation
+    // lane k_exc_fill writes instead of k_combine_global, and the lanes left
+    // to combine (null / 0: none qualifies, or MOCOHIP_EXC_LANES=0)
+    int* d_exc_slot = nullptr;
+    int* d_cmb_map = nullptr;
+    int n_exc_gen = 0;
     int g_block = 4;               // generic interpreter, eval_g: k_eval workgroup size (A/B: profiles/r02_l)
     bool g_lds = false;            // generic interpreter, eval_g: workspace in LDS (k_eval_lds)
     int g_lds_guard = 0;           // k_eval_lds guard band per slot side, doubles (MOCOHIP_G_LDS_GUARD)
@@ -2208,9 +2238,19 @@ static int launch_tasks(mh_ctx* c, const Src& S, const Lanes& ln, const TaskSet&
                 S, ln, ts.dev, T, H, times, Y, (long)D::NO * ln.stride, quot ? 1 : 0);
         return quot ? 1 : 0;
     } else {
-        const long lanes = (long)ts.dev.nk * ln.stride;
+        // excitation lanes (Jacobian lanes, raw values): filled after the
+        // other lanes' combine instead of combined
+        const bool xs = c->d_exc_slot && &ts == &c->ts_jac;
+        const int per = xs ? ln.stride - c->n_exc_gen : ln.stride;
+        const long lanes = (long)ts.dev.nk * per;
         hipLaunchKernelGGL(k_combine_global<D>, dim3((unsigned)((lanes + 63) / 64)), dim3(64), 0,
-                c->stream, c->M, S, ln, ts.dev, T, H, times, Y, (long)D::NO * ln.stride);
+                c->stream, c->M, S, ln, ts.dev, T, H, times, Y, (long)D::NO * ln.stride,
+                xs ? (const int*)c->d_cmb_map : nullptr, per);
+        if (xs) {
+            const long all = (long)ts.dev.nk * ln.stride;
+            hipLaunchKernelGGL(k_exc_fill, dim3((unsigned)((all + 255) / 256)), dim3(256), 0, c->stream,
+                    ts.dev.nk, D::NO, ln.stride, ln.base, ts.dev.tdoubles, (const int*)c->d_exc_slot, T, Y);
+        }
     }
     return 0;
 }

@@ -1405,9 +1405,8 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     // excitation lanes (k_exc_lanes): a direction that perturbs the control
     // of exactly one muscle with activation dynamics, read by nothing else
     // in the DAE (coordinate actuators read their own controls only)
-    std::vector<int> exc_lane(stride, -1);
-    if (!backend_tasks(c->be) && std::strncmp(c->be->name, "generic", 7) == 0 &&
-            !(std::getenv("MOCOHIP_EXC_LANES") && std::strcmp(std::getenv("MOCOHIP_EXC_LANES"), "0") == 0)) {
+    std::vector<int> exc_lane(stride, -1), exc_mus(stride, -1);
+    if (!(std::getenv("MOCOHIP_EXC_LANES") && std::strcmp(std::getenv("MOCOHIP_EXC_LANES"), "0") == 0)) {
         for (int dir = 2; dir < ND; ++dir) {
             const int ci = dir - 2 - c->NS;
             if (ci < 0 || ci >= c->NC || ci >= M.nactuators || M.actuators[ci].kind != MH_ACT_MUSCLE) continue;
@@ -1415,10 +1414,13 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
             for (int im = 0; im < M.nmuscles; ++im)
                 if (mus_control[im] == ci) { mus = im; ++users; }
             if (users != 1 || act_state[mus] < 0) continue;
-            exc_lane[dir] = mus;
-            if (c->fd == MH_FD_CENTRAL) exc_lane[dir + ND] = mus;
+            exc_mus[dir] = mus;
+            if (c->fd == MH_FD_CENTRAL) exc_mus[dir + ND] = mus;
         }
-        for (int v : exc_lane) c->n_exc_lanes += v >= 0;
+        if (!backend_tasks(c->be) && std::strncmp(c->be->name, "generic", 7) == 0) {
+            exc_lane = exc_mus;
+            for (int v : exc_lane) c->n_exc_lanes += v >= 0;
+        }
     }
     std::vector<int> lane_map;
     for (int r = 0; r < stride; ++r)
@@ -1458,13 +1460,36 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     }
 
     TaskOffsets to_jac{}, to_g{};
-    size_t o_T = 0, o_H = 0, o_Tg = 0, o_Hg = 0;
+    size_t o_T = 0, o_H = 0, o_Tg = 0, o_Hg = 0, o_xsl = 0, o_cmap = 0;
     const TaskInfo* ti = backend_tasks(c->be);
     if (ti) {
         build_taskset(*ti, c->lanes_jac, c->nk, c->nsimd, c->ts_jac);
         build_taskset(*ti, c->lanes_g, c->nk, c->nsimd, c->ts_g);
         to_jac = put_taskset(A, c->ts_jac);
         to_g = put_taskset(A, c->ts_g);
+        // excitation lanes of the generated back end (k_exc_fill): the lane
+        // re-evaluates exactly one group besides none of the mass factor's,
+        // of one field (the activation derivative)
+        if (!c->presc) {
+            const int ng = ti->ng;
+            std::vector<int> xs(2 * (size_t)stride, -1), cmap;
+            for (int r = 0; r < stride; ++r) {
+                if (exc_mus[r] < 0 || c->ts_jac.jd[(size_t)r * ng] != 0) continue;
+                int gx = -1, nre = 0;
+                for (int gg = 1; gg < ng; ++gg)
+                    if (c->ts_jac.jd[(size_t)r * ng + gg] != c->ts_jac.off[gg]) { gx = gg; ++nre; }
+                if (nre != 1 || ti->group_nf[gx] != 1) continue;
+                xs[2 * (size_t)r] = c->ts_jac.jd[(size_t)r * ng + gx];
+                xs[2 * (size_t)r + 1] = c->NQ + act_state[exc_mus[r]] - 2 * M.nq;
+                ++c->n_exc_gen;
+            }
+            for (int r = 0; r < stride; ++r)
+                if (xs[2 * (size_t)r] < 0) cmap.push_back(r);
+            if (c->n_exc_gen) {
+                o_xsl = A.put(xs.data(), xs.size());
+                o_cmap = A.put(cmap.data(), cmap.size());
+            }
+        }
         o_T = A.reserve(sizeof(double) * std::max(c->ts_jac.t_doubles, c->ts_g.t_doubles));
         o_H = A.reserve(sizeof(double) * std::max(c->ts_jac.h_doubles, c->ts_g.h_doubles));
         o_Tg = A.reserve(sizeof(double) * c->ts_g.t_doubles);
@@ -1517,6 +1542,7 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     c->GS.gcol = (const int*)(b + o_gcol);
     c->GS.gw = (const double*)(b + o_gw);
     if (c->n_exc_lanes) { c->d_exc = (int*)(b + o_exc); c->d_lane_map = (int*)(b + o_lmap); }
+    if (c->n_exc_gen) { c->d_exc_slot = (int*)(b + o_xsl); c->d_cmb_map = (int*)(b + o_cmap); }
     if (const char* eb = std::getenv("MOCOHIP_G_BLOCK")) c->g_block = std::min(64, std::max(1, std::atoi(eb)));
     if (const char* el = std::getenv("MOCOHIP_G_LDS")) c->g_lds = std::atoi(el) != 0;
     if (const char* eg = std::getenv("MOCOHIP_G_LDS_GUARD")) c->g_lds_guard = std::min(64, std::max(0, std::atoi(eg)));
@@ -2812,6 +2838,7 @@ extern "C" int mh_get_backend_flags(const mh_ctx* c, char* flags, int32_t len) {
     if (c->quot) f += " quot";
     if (c->asm_grid_stride) f += " asm-gs";
     if (c->d_exc) f += " exc-lanes";
+    if (c->d_exc_slot) f += " exc-fill";
     if (c->g_lds && !c->be->tasks && std::strncmp(c->be->name, "generic", 7) == 0) {
         f += " g-lds";
         if (c->g_lds_guard) {

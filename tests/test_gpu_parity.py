@@ -857,6 +857,28 @@ def test_excitation_lanes_bit_identical(name):
         assert np.array_equal(gpu.eval_g(x), full.eval_g(x), equal_nan=True)
 
 
+@pytest.mark.parametrize("name", ["gait_rigid_forward", "gait_rigid_central", "gait_rigid_backward",
+                                  "gait_compliant_central", "gait_rigid_implicit", "wrapped_pendulum",
+                                  "rajagopal80_wrapped_trap"])
+def test_generated_excitation_fill_bit_identical(name):
+    """Generated back ends, split path with the global-memory combine (the
+    large models' path): the lanes that perturb a muscle excitation are
+    written by k_exc_fill (the base lane's outputs + the activation group's
+    one field) instead of k_combine_global; raw lanes, g and the Jacobian
+    equal combining every lane (MOCOHIP_EXC_LANES=0) bit for bit."""
+    env = {"MOCOHIP_INTERVAL": "0", "MOCOHIP_COMBINE": "global"}
+    gpu, _, _ = _pair(name, env=env)
+    full, _, _ = _pair(name, env={**env, "MOCOHIP_EXC_LANES": "0"})
+    assert gpu.backend()[0].startswith("generated")
+    assert "exc-fill" in gpu.backend_flags() and "exc-fill" not in full.backend_flags()
+    for _, x in _iterates(gpu):
+        ta, Ya = gpu.jacobian_lanes(x)
+        tb, Yb = full.jacobian_lanes(x)
+        assert np.array_equal(ta, tb) and np.array_equal(Ya, Yb, equal_nan=True)
+        assert np.array_equal(gpu.eval_jac_g(x), full.eval_jac_g(x), equal_nan=True)
+        assert np.array_equal(gpu.eval_g(x), full.eval_g(x), equal_nan=True)
+
+
 @pytest.mark.parametrize("tb", ["1", "8", "64"])
 @pytest.mark.parametrize("name", ["gait_rigid_forward", "gait_inverse_random", "wrapped_pendulum",
                                   "rajagopal18_inverse", "coupled_pendulum_implicit"])
