@@ -551,25 +551,10 @@ __global__ void __launch_bounds__(64) k_combine_global(DevModel M, Src S, Lanes 
     D::combine(M, t, in, TL, StridedOut{Y + (long)kl * ystride_pt + r, (long)Ln.stride});
 }
 
-// Excitation lanes of a generated back end: a direction that perturbs the
-// excitation of one muscle with activation dynamics re-evaluates only that
-// muscle's activation group, whose one field is the activation derivative
-// output; every other output of its combine reads base-lane slots only, so
-// it equals the base lane's.  xs[2 r] = the group's slot for role r (-1: not
-// such a lane), xs[2 r + 1] = the output.  Bit-identical to combining the
-// lane (test_excitation_lanes_bit_identical, MOCOHIP_EXC_LANES=0).
-static __global__ void __launch_bounds__(256) k_exc_fill(int nk, int NO, int stride, int base, int tdoubles,
-        const int* __restrict__ xs, const double* __restrict__ T, double* __restrict__ Y) {
-    const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (gid >= (long)nk * stride) return;
-    const int kl = (int)(gid / stride);
-    const int r = (int)(gid - (long)kl * stride);
-    const int slot = xs[2 * r];
-    if (slot < 0) return;
-    double* Yk = Y + (long)kl * NO * stride;
-    for (int o = 0; o < NO; ++o) Yk[(long)o * stride + r] = Yk[(long)o * stride + base];
-    Yk[(long)xs[2 * r + 1] * stride + r] = T[(long)kl * tdoubles + slot];
-}
+// Excitation lanes of a generated back end (mocohip.hip k_exc_fill, launched
+// through this host entry so that the fill kernel lives in one unit).
+int mh_launch_exc_fill(const mh_ctx* c, int nk, int NO, int stride, int base, int tdoubles, const double* T,
+                       double* Y);
 
 // Copy n doubles to LDS with U loads in flight per thread before the first
 // store (a plain strided loop serializes one memory round trip per pass).
@@ -1987,9 +1972,9 @@ struct mh_ctx {
     int* d_exc = nullptr;
     int* d_lane_map = nullptr;     // the other lanes, in order (k_eval's lane map)
     int n_exc_lanes = 0;
-    // generated back ends: per Jacobian lane (slot, output) of an excitation
-    // lane k_exc_fill writes instead of k_combine_global, and the lanes left
-    // to combine (null / 0: none qualifies, or MOCOHIP_EXC_LANES=0)
+    // generated back ends: per excitation lane (role, slot, output) that
+    // k_exc_fill writes instead of k_combine_global, and the lanes left to
+    // combine (null / 0: none qualifies, or MOCOHIP_EXC_LANES=0)
     int* d_exc_slot = nullptr;
     int* d_cmb_map = nullptr;
     int n_exc_gen = 0;
@@ -2047,6 +2032,8 @@ struct mh_ctx {
     bool use_interval[2] = {false, false};
     int nsimd = 1024;              // SIMDs of the device (4 per CU)
     bool asm_grid_stride = false;  // k_transcribe_gs (MOCOHIP_ASM=gs) instead of k_transcribe
+    bool asm_ctpl = true;          // k_transcribe on the compiled template (MOCOHIP_ASM_CTPL=0: jac_entry)
+    int asm_chunk_ct = 8192;       // ... its nonzeros per workgroup (MOCOHIP_ASM_CHUNK)
     bool quot = false;             // k_combine writes FD quotients (MOCOHIP_QUOT=1)
     const Backend* be_lane = nullptr;   // the generated model's one-lane back end (if any)
     bool g_lane = false;           // eval_g alone through be_lane + the split transcription
@@ -2246,11 +2233,7 @@ static int launch_tasks(mh_ctx* c, const Src& S, const Lanes& ln, const TaskSet&
         hipLaunchKernelGGL(k_combine_global<D>, dim3((unsigned)((lanes + 63) / 64)), dim3(64), 0,
                 c->stream, c->M, S, ln, ts.dev, T, H, times, Y, (long)D::NO * ln.stride,
                 xs ? (const int*)c->d_cmb_map : nullptr, per);
-        if (xs) {
-            const long all = (long)ts.dev.nk * ln.stride;
-            hipLaunchKernelGGL(k_exc_fill, dim3((unsigned)((all + 255) / 256)), dim3(256), 0, c->stream,
-                    ts.dev.nk, D::NO, ln.stride, ln.base, ts.dev.tdoubles, (const int*)c->d_exc_slot, T, Y);
-        }
+        if (xs) (void)mh_launch_exc_fill(c, ts.dev.nk, D::NO, ln.stride, ln.base, ts.dev.tdoubles, T, Y);
     }
     return 0;
 }

@@ -446,11 +446,11 @@ static_assert(INV_RMAX == INV_RMAX_SK, "skinny product K bound");
 // the steps run in unrolled runs of T, so step k = k0 + ii's row and column
 // are register (.., ii) of the threads with ty (tx) = k0 / T -- no dynamic
 // register index, no selects over the tile -- and a thread whose rows are
-// all done (ty < k0 / T) skips its update.  One barrier per step (w double
-// buffered); LDS holds 2 rows.
+// all done (ty < k0 / T) skips its update.  One barrier per two steps;
+// LDS holds 4 rows.
 template <int T>
 __global__ __launch_bounds__(256) void k_kkt_potri(double* const* __restrict__ mats, int r, int* __restrict__ status) {
-    __shared__ double wbuf[2][16 * INV_T];
+    __shared__ double wbuf[4][16 * INV_T];
     __shared__ double piv[16 * INV_T];
     __shared__ int bad;
     double* a = mats[blockIdx.x];
@@ -467,43 +467,70 @@ __global__ __launch_bounds__(256) void k_kkt_potri(double* const* __restrict__ m
         }
     // entries >= r of w stay 0 (rows and columns past r then never change);
     // every LDS read below is unconditional, so none waits inside a branch
-    for (int e = tid; e < 2 * 16 * INV_T; e += 256) (&wbuf[0][0])[e] = 0.0;
+    for (int e = tid; e < 4 * 16 * INV_T; e += 256) (&wbuf[0][0])[e] = 0.0;
     if (tid == 0) bad = 0;
     __syncthreads();                                 // zeros in before step 0's row
+    // step kk with row kk of Z in w (its owners' tile row / column ii_)
+    auto step = [&](int ii_, int kk, int tk, const double* w) {
+        const double p = w[kk];
+        const double pp = (p > 0.0 && isfinite(p)) ? p : 1.0;
+        if (tid == 0) {
+            if (pp != p) bad = 1;
+            piv[kk] = pp;
+        }
+        if (ty < tk) return;                         // every row of this thread done
+        const int ic = ii_ < T ? ii_ : T - 1;
+        const double pinv = 1.0 / pp;
+        double wc[T], f[T];
+#pragma unroll
+        for (int j = 0; j < T; ++j) wc[j] = w[col0 + j];
+#pragma unroll
+        for (int i = 0; i < T; ++i) f[i] = w[row0 + i] * (row0 + i > kk ? pinv : 0.0);
+        if (tx == tk) {                              // column kk of rows > kk: restart at 0, w = 1
+            wc[ic] = 1.0;
+#pragma unroll
+            for (int i = 0; i < T; ++i) z[i][ic] = row0 + i > kk ? 0.0 : z[i][ic];
+        }
+#pragma unroll
+        for (int i = 0; i < T; ++i)
+#pragma unroll
+            for (int j = 0; j < T; ++j) z[i][j] = fma(-f[i], wc[j], z[i][j]);
+    };
+    // steps in pairs per barrier: the owners (one 16-lane segment of a wave)
+    // also broadcast row k + 1 as step k leaves it, formed privately by the
+    // same operations every thread then applies (pivot and coupling from the
+    // column owner's lane), so step k + 1 needs no barrier of its own;
+    // buffers alternate by pair (a fast owner never overwrites a row being read)
+    int bs = 0;
     for (int k0 = 0; k0 < r; k0 += T) {
         const int tk = k0 / T;                       // the owners' ty (row) and tx (column)
 #pragma unroll
-        for (int ii = 0; ii < T; ++ii) {
+        for (int ii = 0; ii < T; ii += 2) {
             const int k = k0 + ii;
             if (k >= r) break;                       // uniform
-            double* w = wbuf[k & 1];
+            const int i1 = ii + 1 < T ? ii + 1 : T - 1;
+            const bool two = ii + 1 < T && k + 1 < r;
+            double* w0 = wbuf[(bs & 1) * 2];
+            double* w1 = wbuf[(bs & 1) * 2 + 1];
+            ++bs;
             if (ty == tk) {
 #pragma unroll
-                for (int j = 0; j < T; ++j) w[col0 + j] = z[ii][j];   // 0 past r
+                for (int j = 0; j < T; ++j) w0[col0 + j] = z[ii][j];   // 0 past r
+                if (two) {
+                    const double pk = __shfl(z[ii][ii], tk, 16);
+                    const double ak = __shfl(z[ii][i1], tk, 16);
+                    const double ppk = (pk > 0.0 && isfinite(pk)) ? pk : 1.0;
+                    const double fk = ak * (1.0 / ppk);
+#pragma unroll
+                    for (int j = 0; j < T; ++j) {
+                        const bool ck = tx == tk && j == ii;
+                        w1[col0 + j] = fma(-fk, ck ? 1.0 : z[ii][j], ck ? 0.0 : z[i1][j]);
+                    }
+                }
             }
             __syncthreads();
-            const double p = w[k];
-            const double pp = (p > 0.0 && isfinite(p)) ? p : 1.0;
-            if (tid == 0) {
-                if (pp != p) bad = 1;
-                piv[k] = pp;
-            }
-            if (ty < tk) continue;                   // every row of this thread done
-            const double pinv = 1.0 / pp;
-            double wc[T], f[T];
-#pragma unroll
-            for (int j = 0; j < T; ++j) wc[j] = w[col0 + j];
-#pragma unroll
-            for (int i = 0; i < T; ++i) f[i] = w[row0 + i] * (row0 + i > k ? pinv : 0.0);
-            if (tx == tk) {                          // column k of rows > k: restart at 0, w = 1
-                wc[ii] = 1.0;
-#pragma unroll
-                for (int i = 0; i < T; ++i) z[i][ii] = row0 + i > k ? 0.0 : z[i][ii];
-            }
-#pragma unroll
-            for (int i = 0; i < T; ++i)
-#pragma unroll
-                for (int j = 0; j < T; ++j) z[i][j] = fma(-f[i], wc[j], z[i][j]);
+            step(ii, k, tk, w0);
+            if (two) step(ii + 1, k + 1, tk, w1);
         }
     }
     __syncthreads();

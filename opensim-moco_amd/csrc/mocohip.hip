@@ -55,6 +55,33 @@ extern "C" int mh_abi_version(void) { return MH_ABI_VERSION; }
 extern "C" const char* mh_build_id(void) { return MH_BUILD_ID; }
 extern "C" const char* mh_last_error(void) { return g_err.c_str(); }
 
+// Excitation lanes of a generated back end: a direction that perturbs the
+// excitation of one muscle with activation dynamics re-evaluates only that
+// muscle's activation group, whose one field is the activation derivative
+// output; every other output of its combine reads base-lane slots only, so
+// it equals the base lane's.  One thread per (grid point, output, such lane):
+// xs[3 e] = the lane, xs[3 e + 1] = the group's slot, xs[3 e + 2] = the
+// output.  Bit-identical to combining the lane
+// (test_generated_excitation_fill_bit_identical, MOCOHIP_EXC_LANES=0).
+__global__ void __launch_bounds__(256) k_exc_fill(int nk, int NO, int stride, int base, int tdoubles, int nx,
+        const int* __restrict__ xs, const double* __restrict__ T, double* __restrict__ Y) {
+    const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= (long)nk * NO * nx) return;
+    const int e = (int)(gid % nx);
+    const long ko = gid / nx;
+    const int o = (int)(ko % NO);
+    const int kl = (int)(ko / NO);
+    double* Yo = Y + ((long)kl * NO + o) * stride;
+    Yo[xs[3 * e]] = o == xs[3 * e + 2] ? T[(long)kl * tdoubles + xs[3 * e + 1]] : Yo[base];
+}
+int mh_launch_exc_fill(const mh_ctx* c, int nk, int NO, int stride, int base, int tdoubles, const double* T,
+                       double* Y) {
+    const long all = (long)nk * NO * c->n_exc_gen;
+    hipLaunchKernelGGL(k_exc_fill, dim3((unsigned)((all + 255) / 256)), dim3(256), 0, c->stream, nk, NO, stride,
+                       base, tdoubles, c->n_exc_gen, (const int*)c->d_exc_slot, T, Y);
+    return MH_OK;
+}
+
 // Transcription stage of the split path, one launch: blockIdx.y = mesh
 // interval; blockIdx.x < nchunks streams Jacobian nonzeros (values != null),
 // the last x-block (when g != null) writes the interval's defect /
@@ -67,7 +94,6 @@ extern "C" const char* mh_last_error(void) { return g_err.c_str(); }
 // base-lane offset) instead of a TplEntry and the formula's branches; t0 / tf
 // (CT_GEN) and path (CT_PATH) entries take jac_entry.  The same operations in
 // the same order as jac_entry: bit-identical (MOCOHIP_CTPL=0 compares).
-constexpr int ASM_CHUNK_CT = 8192;   // nonzeros per compiled-template assembly workgroup
 __device__ __forceinline__ double ct_select(uint32_t k, double a1, double a2, double a3, double a4, double a5) {
     return k == 1 ? a1 : k == 2 ? a2 : k == 3 ? a3 : k == 4 ? a4 : k == 5 ? a5 : 0.0;
 }
@@ -85,7 +111,7 @@ __global__ void __launch_bounds__(256) k_transcribe(Layout L, Interval I, Lanes 
         const IvC C = iv_const(YV.t(k_last) - YV.t(k_first), grid[k_last] - grid[k_first]);
         double* vi = values + (long)il * I.nnz_int;
         const int e_end = min(I.entries(i), ((int)blockIdx.x + 1) * chunk);
-        if (ctpl) {   // chunks of ASM_CHUNK_CT entries
+        if (ctpl) {   // chunks of asm_chunk_ct entries
 #pragma clang fp contract(off)
             const int npts = k_last - k_first + 1;
             const uint32_t nyall = (uint32_t)(npts * L.NO * Ln.stride);
@@ -1472,19 +1498,23 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
         // of one field (the activation derivative)
         if (!c->presc) {
             const int ng = ti->ng;
-            std::vector<int> xs(2 * (size_t)stride, -1), cmap;
+            std::vector<int> xs, cmap;   // xs: [lane][role, slot, output]
             for (int r = 0; r < stride; ++r) {
-                if (exc_mus[r] < 0 || c->ts_jac.jd[(size_t)r * ng] != 0) continue;
-                int gx = -1, nre = 0;
-                for (int gg = 1; gg < ng; ++gg)
-                    if (c->ts_jac.jd[(size_t)r * ng + gg] != c->ts_jac.off[gg]) { gx = gg; ++nre; }
-                if (nre != 1 || ti->group_nf[gx] != 1) continue;
-                xs[2 * (size_t)r] = c->ts_jac.jd[(size_t)r * ng + gx];
-                xs[2 * (size_t)r + 1] = c->NQ + act_state[exc_mus[r]] - 2 * M.nq;
-                ++c->n_exc_gen;
+                bool fill = false;
+                if (exc_mus[r] >= 0 && c->ts_jac.jd[(size_t)r * ng] == 0) {
+                    int gx = -1, nre = 0;
+                    for (int gg = 1; gg < ng; ++gg)
+                        if (c->ts_jac.jd[(size_t)r * ng + gg] != c->ts_jac.off[gg]) { gx = gg; ++nre; }
+                    if (nre == 1 && ti->group_nf[gx] == 1) {
+                        xs.push_back(r);
+                        xs.push_back(c->ts_jac.jd[(size_t)r * ng + gx]);
+                        xs.push_back(c->NQ + act_state[exc_mus[r]] - 2 * M.nq);
+                        ++c->n_exc_gen;
+                        fill = true;
+                    }
+                }
+                if (!fill) cmap.push_back(r);
             }
-            for (int r = 0; r < stride; ++r)
-                if (xs[2 * (size_t)r] < 0) cmap.push_back(r);
             if (c->n_exc_gen) {
                 o_xsl = A.put(xs.data(), xs.size());
                 o_cmap = A.put(cmap.data(), cmap.size());
@@ -1622,6 +1652,10 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
         c->role_couple = !(eo && std::strcmp(eo, "0") == 0);
         const char* ea = std::getenv("MOCOHIP_ASM");
         c->asm_grid_stride = ea && std::strcmp(ea, "gs") == 0;
+        const char* eac = std::getenv("MOCOHIP_ASM_CTPL");
+        c->asm_ctpl = !(eac && std::strcmp(eac, "0") == 0);
+        if (const char* ech = std::getenv("MOCOHIP_ASM_CHUNK"))
+            c->asm_chunk_ct = std::min(1 << 20, std::max(256, std::atoi(ech)));
         const char* ee = std::getenv("MOCOHIP_EVENTS");
         c->timing = ee && std::strcmp(ee, "1") == 0;
         const char* egl = std::getenv("MOCOHIP_G_LANE");
@@ -1872,10 +1906,10 @@ static int launch_stage(mh_ctx* c, int stage, int kind, const double* x, double*
     Layout L = make_layout(c, c->k0, c->nk);
     const Lanes& ln = kind == 0 ? c->lanes_g : c->lanes_jac;
     const double* Y = kind == 0 ? c->d_Yg : c->d_Y;
-    // the compiled-template assembly's workgroups take ASM_CHUNK_CT nonzeros
-    // each (a few per thread and pass: per-workgroup setup, not the stores,
-    // bounded ASM_CHUNK-sized ones); jac_entry's ASM_CHUNK
-    const int chunk = c->use_ctpl ? ASM_CHUNK_CT : ASM_CHUNK;
+    // the compiled-template assembly's workgroups take asm_chunk_ct nonzeros
+    // each (a few per thread and pass); jac_entry's ASM_CHUNK
+    const bool ctw = c->use_ctpl && c->asm_ctpl;
+    const int chunk = ctw ? c->asm_chunk_ct : ASM_CHUNK;
     const int nchunks = kind == 0 ? 0 : (c->nnz_int + (c->ie == c->N ? c->nnz_tail : 0) + chunk - 1) / chunk;
     double* g = kind == 1 ? nullptr : a;
     double* v = kind == 0 ? nullptr : (kind == 1 ? a : b);
@@ -1893,7 +1927,7 @@ static int launch_stage(mh_ctx* c, int stage, int kind, const double* x, double*
                 c->d_grid, c->d_times, Y, g, v, nint, c->yq[kind == 0 ? 0 : 1]);
     } else {
         hipLaunchKernelGGL(k_transcribe, dim3((unsigned)(nchunks + (g ? 1 : 0)), (unsigned)nint), dim3(256), 0,
-                c->stream, L, I, ln, c->d_tpl, c->use_ctpl ? c->d_ctpl : nullptr, x, c->d_grid, c->d_times, Y, g,
+                c->stream, L, I, ln, c->d_tpl, ctw ? c->d_ctpl : nullptr, x, c->d_grid, c->d_times, Y, g,
                 v, nchunks, c->yq[kind == 0 ? 0 : 1], chunk);
     }
     HIPCHK(hipGetLastError());

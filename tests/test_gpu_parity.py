@@ -310,7 +310,8 @@ def _pair(name, backend="auto", tasks=None, env=None):
                                                   "MOCOHIP_IV_QFUSE", "MOCOHIP_IV_THREADS",
                                                   "MOCOHIP_EXC_LANES", "MOCOHIP_G_BLOCK", "MOCOHIP_G_LDS",
                                                   "MOCOHIP_G_LDS_GUARD",
-                                                  "MOCOHIP_GROUPS_SPLIT", "MOCOHIP_COMBINE")}
+                                                  "MOCOHIP_GROUPS_SPLIT", "MOCOHIP_COMBINE",
+                                                  "MOCOHIP_ASM_CHUNK", "MOCOHIP_ASM_CTPL")}
     if backend != "auto":
         os.environ["MOCOHIP_BACKEND"] = backend
     if tasks:
@@ -810,6 +811,7 @@ def test_pruned_tasks_bit_identical(name):
                                      {"MOCOHIP_INTERVAL": "0", "MOCOHIP_ASM": "gs"},
                                      {"MOCOHIP_INTERVAL": "0", "MOCOHIP_QUOT": "1"},
                                      {"MOCOHIP_INTERVAL": "0", "MOCOHIP_CTPL": "0"},
+                                     {"MOCOHIP_INTERVAL": "0", "MOCOHIP_ASM_CHUNK": "1000"},
                                      {"MOCOHIP_INTERVAL": "0", "MOCOHIP_QUOT": "1", "MOCOHIP_CTPL": "0"},
                                      {"MOCOHIP_CTPL": "0"},
                                      {"MOCOHIP_ROLES": "1"},
@@ -859,7 +861,7 @@ def test_excitation_lanes_bit_identical(name):
 
 @pytest.mark.parametrize("name", ["gait_rigid_forward", "gait_rigid_central", "gait_rigid_backward",
                                   "gait_compliant_central", "gait_rigid_implicit", "wrapped_pendulum",
-                                  "rajagopal80_wrapped_trap"])
+                                  "rajagopal80", "rajagopal80_wrapped"])
 def test_generated_excitation_fill_bit_identical(name):
     """Generated back ends, split path with the global-memory combine (the
     large models' path): the lanes that perturb a muscle excitation are
