@@ -1125,8 +1125,10 @@ __device__ __forceinline__ void interval_body(const DevModel& M, const Src& S, c
     if (threadIdx.x < 2) sK[threadIdx.x] = threadIdx.x ? 1.0 : 0.0;
     __syncthreads();
     if (I.dbg_stop == 1) return;
-    for (int w = threadIdx.x; w < npts * Ln.stride; w += blockDim.x) {
-        const int p = w / Ln.stride, r = w - p * Ln.stride;
+    // eval_g's lanes (stride 1: every lane is the base role 0, written as a
+    // constant so that the role -> slot reads have uniform addresses and
+    // compile to scalar loads off the combine's critical path)
+    auto combine_lane = [&](int p, int r) {
         LaneInL<D> in{lds(sXs + p * L.NS), lds(sXc + p * L.NC), lds(sXd + p * L.NDV), -1, 0.0,
                       lds(sXm + p * L.NM), L.vc(k_first + p) ? lds(sXl) : nullptr};
         const double t = lane_time(Ln, S.grid[k_first + p], t0, tf, r, in.pi, in.step);
@@ -1138,6 +1140,14 @@ __device__ __forceinline__ void interval_body(const DevModel& M, const Src& S, c
         } else {
             const TaskLoadLds<D> TL{lds(sT + p * nt), lds(sH + p * nh), TK.jd, r};
             D::combine(M, t, in, TL, out);
+        }
+    };
+    if (Ln.stride == 1) {
+        if ((int)threadIdx.x < npts) combine_lane((int)threadIdx.x, 0);
+    } else {
+        for (int w = threadIdx.x; w < npts * Ln.stride; w += blockDim.x) {
+            const int p = w / Ln.stride, r = w - p * Ln.stride;
+            combine_lane(p, r);
         }
     }
     // the compiled words of this thread's first IV_PF assembly entries,

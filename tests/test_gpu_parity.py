@@ -346,6 +346,18 @@ def _pair(name, backend="auto", tasks=None, env=None):
 _KEEP = []   # solvers owning the pattern buffers mh_options points at
 
 
+def _oracle_for(st, gpu, rep, threads=8):
+    """The oracle NLP of ``st`` checking ``gpu``: under the reference's
+    sparsity rule (any-change) with detection on, it takes the device's
+    detected pattern (see _pair)."""
+    from mocohip import abi
+    opts = st.solver.options()
+    if (opts.sparsity_detection not in (abi.MH_SPARSITY_NONE, abi.MH_SPARSITY_GIVEN)
+            and opts.sparsity_rule == abi.MH_SPARSITY_RULE_ANY_CHANGE):
+        opts = _given(st, gpu.callback_sparsity())
+    return OracleNLP(rep, opts, threads=threads)
+
+
 def _given(st, pattern):
     import copy
     s2 = copy.copy(st.solver)
@@ -1104,7 +1116,7 @@ def test_jacobian_tight_bound(name):
     st.solver.fd_step = 1e-4
     rep = st.problem.create_rep()
     gpu = HipNLP(rep, st.solver.options())
-    ref = OracleNLP(rep, st.solver.options(), threads=8)
+    ref = _oracle_for(st, gpu, rep)
     for _, x in _iterates(gpu):
         J, J0 = gpu.eval_jac_g(x), ref.eval_jac_g(x)
         _, Y, Y0 = _device_lanes_check(gpu, ref, x)
@@ -1166,7 +1178,7 @@ def test_config_at_full_size(name):
     st = SIZES[name]()
     rep = st.problem.create_rep()
     gpu = HipNLP(rep, st.solver.options())
-    ref = OracleNLP(rep, st.solver.options(), threads=16)   # its own detection (inverse_N125)
+    ref = _oracle_for(st, gpu, rep, threads=16)   # the device's pattern under any-change (inverse_N125)
     assert (gpu.n, gpu.m, gpu.nnz) == (ref.n, ref.m, ref.nnz)
     ir, jc = gpu.jac_structure()
     ir0, jc0 = ref.jac_structure()
@@ -1209,7 +1221,7 @@ def test_global_seed_jacobian(name):
     st.solver.jacobian_mode = "global-seeds"
     rep = st.problem.create_rep()
     gpu = HipNLP(rep, st.solver.options())
-    ref = OracleNLP(rep, st.solver.options(), threads=8)
+    ref = _oracle_for(st, gpu, rep)
     ir, jc = gpu.jac_structure()
     cg, kg = gpu.jacobian_seeds()
     co, ko = ref.jacobian_seeds()
