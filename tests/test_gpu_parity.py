@@ -1274,7 +1274,14 @@ def test_batch_bit_identical(name, gm):
             configs.scale_subject(st.problem.model, 1.03, 1.05)
             t = st.problem.model.tables["grf"]
             t.columns = {k: np.asarray(v) * 1.01 for k, v in t.columns.items()}
-        nlps.append(HipNLP(st.problem.create_rep(), st.solver.options()))
+        opts = st.solver.options()
+        from mocohip import abi
+        if b > 0 and opts.sparsity_detection not in (abi.MH_SPARSITY_NONE, abi.MH_SPARSITY_GIVEN):
+            # one batch, one structure: the subjects share the first one's
+            # detected pattern (under the reference's any-change rule a
+            # scaled subject's rounding-level couplings differ)
+            opts = _given(st, nlps[0].callback_sparsity())
+        nlps.append(HipNLP(st.problem.create_rep(), opts))
     bt = HipBatch(nlps, group_results_global=gm)
     dev = torch.device("cuda", 0)
     xs = [torch.tensor(physiological_iterate(n, 20 + b), dtype=torch.float64, device=dev)
