@@ -1323,8 +1323,12 @@ __device__ __forceinline__ void interval_body(const DevModel& M, const Src& S, c
         endpoint_head(L, Ln, I.E, S.x, g ? I.gh : nullptr, values ? I.vh : nullptr, threadIdx.x, blockDim.x);
 }
 
-template <class D>
-__global__ void __launch_bounds__(1024) k_interval(DevModel M, Src S, Lanes Ln, Tasks TK, Layout L,
+// MAXT: the launch bound.  eval_g's launches (stride-1 lanes, c->ivg_threads
+// = 256) take the 256-thread instantiation: its combine lanes may keep up to
+// 512 VGPRs, where the 1024-thread bound (128) made a large model's combine
+// spill (Rajagopal 80: 2.9 KB of scratch per lane, ~150 us per eval_g).
+template <class D, int MAXT = 1024>
+__global__ void __launch_bounds__(MAXT) k_interval(DevModel M, Src S, Lanes Ln, Tasks TK, Layout L,
         Interval I, const TplEntry* __restrict__ tpl, const uint32_t* __restrict__ ctpl,
         const int* __restrict__ ctgen, int nctgen,
         const double* __restrict__ T, const double* __restrict__ H, double* __restrict__ g,
@@ -2336,10 +2340,10 @@ static void be_interval(mh_ctx* c, const double* x, int mode, double* g, double*
         return;
     }
     const size_t lds = interval_lds<D>(c, ln, ts);
-    auto kern = k_interval<D>;
+    const unsigned threads = v ? (unsigned)c->iv_threads : (unsigned)c->ivg_threads;
+    auto kern = threads <= 256 ? k_interval<D, 256> : k_interval<D, 1024>;
     if (lds > 65536)
         (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    const unsigned threads = v ? (unsigned)c->iv_threads : (unsigned)c->ivg_threads;
     if (i1 < 0) { i0 = 0; i1 = c->ie - c->ib; }
     if (i1 <= i0) return;
     hipLaunchKernelGGL(kern, dim3((unsigned)(i1 - i0)), dim3(threads), lds, c->stream, c->M,
