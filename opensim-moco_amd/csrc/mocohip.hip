@@ -94,11 +94,9 @@ int mh_launch_exc_fill(const mh_ctx* c, int nk, int NO, int stride, int base, in
 // base-lane offset) instead of a TplEntry and the formula's branches; t0 / tf
 // (CT_GEN) and path (CT_PATH) entries take jac_entry.  The same operations in
 // the same order as jac_entry: bit-identical (MOCOHIP_CTPL=0 compares).
-__device__ __forceinline__ double ct_select(uint32_t k, double a1, double a2, double a3, double a4, double a5) {
-    return k == 1 ? a1 : k == 2 ? a2 : k == 3 ? a3 : k == 4 ? a4 : k == 5 ? a5 : 0.0;
-}
 __global__ void __launch_bounds__(256) k_transcribe(Layout L, Interval I, Lanes Ln,
-        const TplEntry* __restrict__ tpl, const uint32_t* __restrict__ ctpl, const double* __restrict__ x,
+        const TplEntry* __restrict__ tpl, const uint32_t* __restrict__ ctpl, const int* __restrict__ ctgen,
+        int nctgen, const double* __restrict__ x,
         const double* __restrict__ grid, const double* __restrict__ times,
         const double* __restrict__ Y, double* __restrict__ g, double* __restrict__ values,
         int nchunks, int yq, int chunk) {
@@ -113,57 +111,70 @@ __global__ void __launch_bounds__(256) k_transcribe(Layout L, Interval I, Lanes 
         const int e_end = min(I.entries(i), ((int)blockIdx.x + 1) * chunk);
         if (ctpl) {   // chunks of asm_chunk_ct entries
 #pragma clang fp contract(off)
+            // the coefficient / base tables the words select from (the same
+            // doubles jac_entry forms)
+            __shared__ double kc[8], kb[8];
+            if (threadIdx.x < 8) {
+                const int t = threadIdx.x;
+                kc[t] = t == 1 ? -C.h8 : t == 2 ? C.h8 : t == 3 ? -C.h6 : t == 4 ? -C.h6 * 4.0 : t == 5 ? -C.hh : 0.0;
+                kb[t] = t == 1 ? -0.5 : t == 2 ? 1.0 : t == 3 ? -1.0 : 0.0;
+            }
+            __syncthreads();
             const int npts = k_last - k_first + 1;
             const uint32_t nyall = (uint32_t)(npts * L.NO * Ln.stride);
-            const uint32_t kconst = nyall + CT_CONST;
+            const uint32_t kone = nyall + CT_CONST + 1;
             const double* __restrict__ Yi = Y + (long)(k_first - L.k0) * L.NO * Ln.stride;
             const uint32_t* __restrict__ cbase = ctpl + I.nnz_int + I.nnz_tail;
-            const double h1 = Ln.h, h2 = 2.0 * Ln.h;
-            const double c4 = -C.h6 * 4.0;
             const int eb = (int)blockIdx.x * chunk, ee = min(I.entries(i), eb + chunk);
-            // CT_U entries per thread per pass: their words, then their Y
-            // values, then their stores (independent loads in flight together)
-            constexpr int CT_U = 4;
-            for (int e0 = eb + (int)threadIdx.x; e0 < ee; e0 += CT_U * (int)blockDim.x) {
-                uint32_t w[CT_U], wb[CT_U];
+            // the bulk, branch-free per entry: CT_U entries per thread and
+            // pass (their words, then their Y values, then their stores);
+            // t0 / tf (CT_GEN) and path (CT_PATH) entries are skipped here and
+            // written by the two loops below.  One instantiation per
+            // finite-difference formula (no per-entry scalar branches).
+            auto bulk = [&](auto fdc) {
+                constexpr int FD = decltype(fdc)::value;
+                const double hq = FD == MH_FD_CENTRAL ? 2.0 * Ln.h : Ln.h;
+                constexpr int CT_U = 4;
+                for (int e0 = eb + (int)threadIdx.x; e0 < ee; e0 += CT_U * (int)blockDim.x) {
+                    uint32_t w[CT_U], wb[CT_U];
 #pragma unroll
-                for (int u = 0; u < CT_U; ++u) {
-                    const int e = e0 + u * (int)blockDim.x;
-                    w[u] = e < ee ? ctpl[e] : CT_PATH;
-                    wb[u] = e < ee ? cbase[e] : 0u;
-                }
-                double ya[CT_U], yb[CT_U];
-#pragma unroll
-                for (int u = 0; u < CT_U; ++u) {
-                    const uint32_t off = w[u] & CT_OFF;
-                    const bool lane = !(w[u] & (CT_GEN | CT_PATH)) && off < nyall;
-                    ya[u] = lane ? Yi[off] : 0.0;
-                    yb[u] = 0.0;
-                    if (lane && !yq) yb[u] = Ln.fd == MH_FD_CENTRAL ? Yi[off + Ln.ND] : Yi[wb[u]];
-                }
-#pragma unroll
-                for (int u = 0; u < CT_U; ++u) {
-                    const int e = e0 + u * (int)blockDim.x;
-                    if (e >= ee) break;
-                    if (w[u] & (CT_GEN | CT_PATH)) {
-                        vi[e] = jac_entry(L, Ln, I.P, x, YV, tpl[e], k_first, C);
-                        continue;
+                    for (int u = 0; u < CT_U; ++u) {
+                        const int e = min(e0 + u * (int)blockDim.x, ee - 1);
+                        w[u] = ctpl[e];
+                        wb[u] = FD == MH_FD_CENTRAL ? 0u : cbase[e];
                     }
-                    const uint32_t off = w[u] & CT_OFF;
-                    double q;
-                    if (off >= nyall) q = off == kconst + 1 ? 1.0 : 0.0;
-                    else if (yq) q = ya[u];
-                    else if (Ln.fd == MH_FD_CENTRAL) q = (ya[u] - yb[u]) / h2;
-                    else if (Ln.fd == MH_FD_FORWARD) q = (ya[u] - yb[u]) / h1;
-                    else q = (yb[u] - ya[u]) / h1;
-                    if (w[u] & CT_RAW) {
-                        vi[e] = q;
-                    } else {
-                        const double coef = ct_select((w[u] >> 20) & 7, -C.h8, C.h8, -C.h6, c4, -C.hh);
-                        const double base = ct_select((w[u] >> 23) & 7, -0.5, 1.0, -1.0, 0.0, 0.0);
-                        vi[e] = base + coef * q;
+                    double ya[CT_U], yb[CT_U];
+#pragma unroll
+                    for (int u = 0; u < CT_U; ++u) {
+                        const uint32_t off = w[u] & CT_OFF;
+                        const uint32_t oy = off < nyall ? off : 0u;
+                        ya[u] = Yi[oy];
+                        yb[u] = FD == MH_FD_CENTRAL ? Yi[off < nyall ? off + Ln.ND : 0u] : Yi[wb[u] < nyall ? wb[u] : 0u];
+                    }
+#pragma unroll
+                    for (int u = 0; u < CT_U; ++u) {
+                        const int e = e0 + u * (int)blockDim.x;
+                        const uint32_t off = w[u] & CT_OFF;
+                        const double qd = FD == MH_FD_BACKWARD ? (yb[u] - ya[u]) / hq : (ya[u] - yb[u]) / hq;
+                        const double q = off >= nyall ? (off == kone ? 1.0 : 0.0) : (yq ? ya[u] : qd);
+                        const double v = (w[u] & CT_RAW) ? q : kb[(w[u] >> 23) & 7] + kc[(w[u] >> 20) & 7] * q;
+                        if (e < ee && !(w[u] & (CT_GEN | CT_PATH))) vi[e] = v;
                     }
                 }
+            };
+            if (Ln.fd == MH_FD_FORWARD) bulk(std::integral_constant<int, MH_FD_FORWARD>{});
+            else if (Ln.fd == MH_FD_BACKWARD) bulk(std::integral_constant<int, MH_FD_BACKWARD>{});
+            else bulk(std::integral_constant<int, MH_FD_CENTRAL>{});
+            // t0 / tf entries of this chunk
+            for (int j = threadIdx.x; j < nctgen; j += blockDim.x) {
+                const int e = ctgen[j];
+                if (e >= eb && e < ee) vi[e] = jac_entry<false>(L, Ln, I.P, x, YV, tpl[e], k_first, C);
+            }
+            // path entries (the first npe of the interval and of the tail)
+            const int nw = i == I.N - 1 ? 2 * I.npe : I.npe;
+            for (int w = threadIdx.x; w < nw; w += blockDim.x) {
+                const int ep = w < I.npe ? w : I.nnz_int + (w - I.npe);
+                if (ep >= eb && ep < ee) vi[ep] = jac_entry<true>(L, Ln, I.P, x, YV, tpl[ep], k_first, C);
             }
         } else {
             for (int e = (int)blockIdx.x * chunk + threadIdx.x; e < e_end; e += blockDim.x)
@@ -1927,7 +1938,8 @@ static int launch_stage(mh_ctx* c, int stage, int kind, const double* x, double*
                 c->d_grid, c->d_times, Y, g, v, nint, c->yq[kind == 0 ? 0 : 1]);
     } else {
         hipLaunchKernelGGL(k_transcribe, dim3((unsigned)(nchunks + (g ? 1 : 0)), (unsigned)nint), dim3(256), 0,
-                c->stream, L, I, ln, c->d_tpl, ctw ? c->d_ctpl : nullptr, x, c->d_grid, c->d_times, Y, g,
+                c->stream, L, I, ln, c->d_tpl, ctw ? c->d_ctpl : nullptr, c->d_ctgen, (int)c->ctgen.size(), x,
+                c->d_grid, c->d_times, Y, g,
                 v, nchunks, c->yq[kind == 0 ? 0 : 1], chunk);
     }
     HIPCHK(hipGetLastError());
