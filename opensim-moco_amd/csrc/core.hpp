@@ -15,6 +15,7 @@
 #include <cstring>
 #include <memory>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/mocohip.h"
@@ -1253,42 +1254,63 @@ __device__ __forceinline__ void interval_body(const DevModel& M, const Src& S, c
             const int nyall = npts * ny;
             const int fuse = values && Ln.stride > 1 && I.qfuse;
             const double h1 = Ln.h, h2 = 2.0 * Ln.h;
-            auto qat = [&](uint32_t off, uint32_t boff) -> double {
-                const double y = q0[off];
-                if (!fuse || (int)off >= nyall) return y;
-                if (Ln.fd == MH_FD_CENTRAL) return (y - q0[off + Ln.ND]) / h2;
-                const double yb = q0[boff];
-                return Ln.fd == MH_FD_FORWARD ? (y - yb) / h1 : (yb - y) / h1;
-            };
             auto value = [&](uint32_t wu, double q) {
                 const double coef = kc[(wu >> 20) & 7], base = kb[(wu >> 23) & 7];
                 return (wu & CT_RAW) ? q : base + coef * q;
             };
-            // the bulk: one LDS value, a product and a sum per entry; the
-            // t0 / tf columns of the defect rows (CT_GEN) and the path
-            // entries are written by the loops below
+            // one instantiation per (finite-difference formula, fused
+            // quotient): the per-entry quotient is branch-free (its other
+            // operand is read unconditionally -- the mirror lane, or the
+            // row's base lane, 0 where unused -- and selected away for the
+            // LDS constants past the lanes)
+            auto bulk = [&](auto fdc, auto fusec) {
+                constexpr int FD = decltype(fdc)::value;
+                constexpr bool FUSE = decltype(fusec)::value;
+                auto qat = [&](uint32_t off, uint32_t boff) -> double {
+                    const double y = q0[off];
+                    if constexpr (!FUSE) {
+                        return y;
+                    } else {
+                        const bool lane = (int)off < nyall;
+                        const double ym = FD == MH_FD_CENTRAL ? q0[lane ? off + Ln.ND : off] : q0[boff];
+                        const double qd = FD == MH_FD_CENTRAL ? (y - ym) / h2
+                                        : FD == MH_FD_FORWARD ? (y - ym) / h1 : (ym - y) / h1;
+                        return lane ? qd : y;
+                    }
+                };
+                // the bulk: one LDS value, a product and a sum per entry; the
+                // t0 / tf columns of the defect rows (CT_GEN) and the path
+                // entries are written by the loops below
 #pragma unroll
-            for (int u = 0; u < IV_PF; ++u)
-                if (!(pw[u] & (CT_GEN | CT_PATH))) vi[e + u * B] = value(pw[u], qat(pw[u] & CT_OFF, pb[u]));
-            if (I.pf) e += IV_PF * B;
-            for (; e + (IV_UNROLL - 1) * B < ne; e += IV_UNROLL * B) {
-                uint32_t w[IV_UNROLL], wb[IV_UNROLL];
-                double q[IV_UNROLL];
+                for (int u = 0; u < IV_PF; ++u)
+                    if (!(pw[u] & (CT_GEN | CT_PATH))) vi[e + u * B] = value(pw[u], qat(pw[u] & CT_OFF, pb[u]));
+                if (I.pf) e += IV_PF * B;
+                for (; e + (IV_UNROLL - 1) * B < ne; e += IV_UNROLL * B) {
+                    uint32_t w[IV_UNROLL], wb[IV_UNROLL];
+                    double q[IV_UNROLL];
 #pragma unroll
-                for (int u = 0; u < IV_UNROLL; ++u) {
-                    w[u] = ctpl[e + u * B];
-                    wb[u] = cbase[e + u * B];
+                    for (int u = 0; u < IV_UNROLL; ++u) {
+                        w[u] = ctpl[e + u * B];
+                        wb[u] = cbase[e + u * B];
+                    }
+#pragma unroll
+                    for (int u = 0; u < IV_UNROLL; ++u) q[u] = qat(w[u] & CT_OFF, wb[u]);
+#pragma unroll
+                    for (int u = 0; u < IV_UNROLL; ++u)
+                        if (!(w[u] & (CT_GEN | CT_PATH))) vi[e + u * B] = value(w[u], q[u]);
                 }
-#pragma unroll
-                for (int u = 0; u < IV_UNROLL; ++u) q[u] = qat(w[u] & CT_OFF, wb[u]);
-#pragma unroll
-                for (int u = 0; u < IV_UNROLL; ++u)
-                    if (!(w[u] & (CT_GEN | CT_PATH))) vi[e + u * B] = value(w[u], q[u]);
-            }
-            for (; e < ne; e += B) {
-                const uint32_t wu = ctpl[e];
-                if (!(wu & (CT_GEN | CT_PATH))) vi[e] = value(wu, qat(wu & CT_OFF, cbase[e]));
-            }
+                for (; e < ne; e += B) {
+                    const uint32_t wu = ctpl[e];
+                    if (!(wu & (CT_GEN | CT_PATH))) vi[e] = value(wu, qat(wu & CT_OFF, cbase[e]));
+                }
+            };
+            using FF = std::integral_constant<int, MH_FD_FORWARD>;
+            using FB = std::integral_constant<int, MH_FD_BACKWARD>;
+            using FC = std::integral_constant<int, MH_FD_CENTRAL>;
+            if (!fuse) bulk(FF{}, std::false_type{});
+            else if (Ln.fd == MH_FD_FORWARD) bulk(FF{}, std::true_type{});
+            else if (Ln.fd == MH_FD_BACKWARD) bulk(FB{}, std::true_type{});
+            else bulk(FC{}, std::true_type{});
             if (eg0 >= 0) vi[eg0] = jac_entry<false>(L, Ln, I.P, S.x, YV, tg0, k_first, C);
             for (int j = threadIdx.x + (I.pf ? B : 0); j < nctgen; j += B) {
                 const int eg = ctgen[j];
