@@ -139,9 +139,9 @@ __global__ void k_kkt_add_diag(int r, const double* __restrict__ dcl, double* __
 
 // C = alpha * P diag(w) Q^T + beta * C for one task per blockIdx.z, one 64 x
 // 64 output tile per workgroup; P(i, k) = P[i psi + k psk], Q(j, k) =
-// Q[j qsi + k qsk], C(i, j) = C[i ldc + j].  Thread (ty, tx) owns rows ty +
-// 16 a and columns tx + 16 b (a, b < 4): conflict-free LDS reads.  Each
-// output is one thread's fixed-order sum: deterministic.
+// Q[j qsi + k qsk], C(i, j) = C[i ldc + j].  The tile's products run on the
+// FP64 matrix cores (a fixed k order per output: deterministic); the
+// operands stream through LDS in 32-deep K tiles.
 __global__ __launch_bounds__(256) void k_kkt_gemm(const KTask* __restrict__ tasks, int M, int N, int K,
                                                   int psi, int psk, int qsi, int qsk, int ldc,
                                                   double alpha, double beta) {
@@ -151,12 +151,18 @@ __global__ __launch_bounds__(256) void k_kkt_gemm(const KTask* __restrict__ task
     __shared__ double Qs[TK][TN + 1];
     const KTask t = tasks[blockIdx.z];
     const int i0 = blockIdx.y * TM, j0 = blockIdx.x * TN;
-    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
-    double acc[4][4];
+    const int tid = threadIdx.x;
+    // four waves, each a 32 x 32 quarter of the tile as 2 x 2 FP64 MFMA
+    // tiles (v_mfma_f64_16x16x4_f64: A[i][k] from lane (i + 16 k), B[k][j]
+    // from lane (j + 16 k); D element (row (lane >> 4) + 4 reg, col lane & 15))
+    const int wave = tid >> 6, lane = tid & 63;
+    const int wr = (wave >> 1) * 32, wcol = (wave & 1) * 32;
+    typedef double f64x4 __attribute__((ext_vector_type(4)));
+    f64x4 acc[2][2];
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+    for (int a = 0; a < 2; ++a)
 #pragma unroll
-        for (int b = 0; b < 4; ++b) acc[a][b] = 0.0;
+        for (int b = 0; b < 2; ++b) acc[a][b] = f64x4{0.0, 0.0, 0.0, 0.0};
     // thread -> tile element maps (coalesced along the operand's contiguous dimension)
     int pii[PL], pkk[PL], qjj[QL], qkk[QL];
 #pragma unroll
@@ -203,31 +209,32 @@ __global__ __launch_bounds__(256) void k_kkt_gemm(const KTask* __restrict__ task
         __syncthreads();
         if (step + 1 < nsteps) load(step + 1, pv, qv);     // in flight while this tile is multiplied
 #pragma unroll
-        for (int kk = 0; kk < TK; ++kk) {
-            double p[4], q[4];
+        for (int kk = 0; kk < TK; kk += 4) {
+            const int kr = kk + (lane >> 4), lc = lane & 15;
+            double pa[2], qb[2];
 #pragma unroll
-            for (int a = 0; a < 4; ++a) p[a] = Ps[kk][ty + 16 * a];
+            for (int t = 0; t < 2; ++t) pa[t] = Ps[kr][wr + 16 * t + lc];
 #pragma unroll
-            for (int b = 0; b < 4; ++b) q[b] = Qs[kk][tx + 16 * b];
+            for (int t = 0; t < 2; ++t) qb[t] = Qs[kr][wcol + 16 * t + lc];
 #pragma unroll
-            for (int a = 0; a < 4; ++a)
+            for (int a = 0; a < 2; ++a)
 #pragma unroll
-                for (int b = 0; b < 4; ++b) acc[a][b] = fma(p[a], q[b], acc[a][b]);
+                for (int b = 0; b < 2; ++b) acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(pa[a], qb[b], acc[a][b], 0, 0, 0);
         }
         __syncthreads();
     }
 #pragma unroll
-    for (int a = 0; a < 4; ++a) {
-        const int gi = i0 + ty + 16 * a;
-        if (gi >= M) continue;
+    for (int a = 0; a < 2; ++a)
 #pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            const int gj = j0 + tx + 16 * b;
-            if (gj >= N) continue;
-            double* cp = t.C + (int64_t)gi * ldc + gj;
-            *cp = beta == 0.0 ? alpha * acc[a][b] : alpha * acc[a][b] + beta * *cp;
-        }
-    }
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int gi = i0 + wr + 16 * a + (lane >> 4) + 4 * g, gj = j0 + wcol + 16 * b + (lane & 15);
+                if (gi < M && gj < N) {
+                    double* cp = t.C + (int64_t)gi * ldc + gj;
+                    *cp = beta == 0.0 ? alpha * acc[a][b][g] : alpha * acc[a][b][g] + beta * *cp;
+                }
+            }
 }
 
 // The solves' products, C = alpha (P diag(w) Q^T + P2 Q2^T) + beta C with few
