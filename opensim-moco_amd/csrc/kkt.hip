@@ -641,8 +641,20 @@ __global__ __launch_bounds__(256) void k_kkt_jtmul_dense(int64_t m, int nd, int 
                                                          const double* __restrict__ y, double* __restrict__ out) {
     __shared__ double red[256];
     const int d = blockIdx.x, k = blockIdx.y;
-    double s = 0.0;
-    for (int64_t i = threadIdx.x; i < m; i += blockDim.x) s += Jd[i * nd + d] * y[i * kc + k];
+    // 8 independent partial sums per thread (8 loads in flight), combined in
+    // a fixed order: deterministic
+    double p[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) p[u] = 0.0;
+    for (int64_t i0 = threadIdx.x; i0 < m; i0 += 8 * (int64_t)blockDim.x) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int64_t i = i0 + u * (int64_t)blockDim.x;
+            const int64_t ic = i < m ? i : m - 1;
+            p[u] = fma(i < m ? Jd[ic * nd + d] : 0.0, y[ic * kc + k], p[u]);
+        }
+    }
+    const double s = ((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7]));
     red[threadIdx.x] = s;
     __syncthreads();
     for (int h = 128; h > 0; h >>= 1) {
