@@ -6,6 +6,11 @@ device, started together.  MocoInverse's setup: MocoInverse.cpp:46-120
 (length, mass) factors (configs.scale_subject), which keep the generated
 back end (structure-only specialization).
 
+Set-up before the common start, per worker: the NLP (HIP context, device
+buffers, generated back end) and, where the solve will factor on the
+device, the device KKT module with its first kernel launches and graph
+captures (mocohip.kkt.DeviceKKT.warm); the timed region holds the solves.
+
 Failures are reported, not raised: a worker whose setup fails still reaches
 the start barrier and posts its error, and the parent watches the workers
 while it waits, so a worker that dies (a crash, a GPU fault) becomes a
@@ -34,8 +39,10 @@ def _worker(index, subject, num_mesh_intervals, device, start, out, linear_solve
         st = configs.gait10dof18musc_inverse(num_mesh_intervals, subject=subject)
         st.solver.device = device
         nlp = st.create_nlp()
-        if linear_solver == "device":
-            nlp.device_kkt()                  # the device KKT module built before the start
+        from .ipm import IpmOptions
+        if linear_solver == "device" or (linear_solver == "auto" and
+                                         nlp.m >= IpmOptions().device_kkt_min_constraints):
+            nlp.device_kkt()                  # the device KKT module (and its first launches) set up before the start
     except Exception as e:   # setup failed: still meet the others at the barrier
         res["error"] = "setup: " + repr(e)[:200]
     try:

@@ -311,6 +311,23 @@ class DeviceKKT:
         self._tick("jtmul", t0, k)
         return out
 
+    def warm(self, x, widths=tuple(range(1, 13))):
+        """One-time setup of the module's device work at iterate ``x``: the
+        first launch of each kernel (code objects load then) and the HIP
+        graphs of the factorization and of each solve width (captured on
+        first use) -- a Jacobian, a factorization of J J^T + I and solves of
+        ``widths`` (plus the dense columns' width) right-hand sides, results
+        discarded; the per-op statistics are reset afterwards."""
+        self.eval_jacobian(x)
+        w = np.ones(self.n)
+        w[self.bm.dcols] = 0.0
+        if self.factor(w, np.ones(self.m)):
+            for k in sorted(set(widths) | ({self.nd} if self.nd else set())):
+                self.solve(np.ones(self.m) if k == 1 else np.ones((self.m, k)))
+        self.jmul(np.zeros(self.n))
+        self.jtmul(np.zeros(self.m))
+        self.stats.clear()
+
     def close(self):
         if self.h:
             self.lib.mh_kkt_destroy(self.h)

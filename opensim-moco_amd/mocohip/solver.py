@@ -486,10 +486,17 @@ class HipNLP(_NLPBase):
         mocohip.kkt.DeviceKKT; created once): the host optimizer's Newton
         systems factored next to the Jacobian.  Raises ValueError when the
         Jacobian lacks the per-interval block structure, RuntimeError on a
-        sharded context."""
+        sharded context.  Creation includes DeviceKKT.warm (first kernel
+        launches and graph captures at the bounds-midpoint guess)."""
         if getattr(self, "_dkkt", None) is None:
             from .kkt import DeviceKKT
-            self._dkkt = DeviceKKT(self)
+            dk = DeviceKKT(self)
+            try:
+                dk.warm(self.initial_guess_from_bounds())
+            except Exception:
+                dk.close()
+                raise
+            self._dkkt = dk
         return self._dkkt
 
     def close(self):
