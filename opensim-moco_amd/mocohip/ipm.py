@@ -231,13 +231,7 @@ class _Scaled:
         keep = (col_map[jc] >= 0) & (row_map[ir] >= 0)
         self.keep = np.where(keep)[0]
         self.ir, self.jc = row_map[ir[keep]], col_map[jc[keep]]
-        # CSR pattern of J_x and the permutation of the kept values into it
-        order = np.lexsort((self.jc, self.ir))
-        self.order = order
-        self.indptr = np.zeros(self.m + 1, np.int64)
-        np.add.at(self.indptr, self.ir + 1, 1)
-        self.indptr = np.cumsum(self.indptr)
-        self.indices = self.jc[order]
+        self._csr = None          # host CSR pattern of J_x, built on first use (host linear algebra)
         self.counts = {"f": 0, "grad_f": 0, "g": 0, "jac_g": 0}
         self.eval_time = 0.0
         # bounds of v = [x, s] (relaxed, bound_relax_factor)
@@ -295,6 +289,28 @@ class _Scaled:
         """Scaled J_x (m x nx, CSR) from the kept Jacobian values."""
         data = (vals * self.row_scale[self.ir])[self.order]
         return sp.csr_matrix((data, self.indices, self.indptr), shape=(self.m, self.nx))
+
+    def _csr_pattern(self):
+        """(order, indptr, indices): the CSR pattern of J_x and the
+        permutation of the kept values into it (the host linear algebra's;
+        the device path never builds it)."""
+        if self._csr is None:
+            order = np.lexsort((self.jc, self.ir))
+            indptr = np.concatenate([[0], np.cumsum(np.bincount(self.ir, minlength=self.m))]).astype(np.int64)
+            self._csr = (order, indptr, self.jc[order])
+        return self._csr
+
+    @property
+    def order(self):
+        return self._csr_pattern()[0]
+
+    @property
+    def indptr(self):
+        return self._csr_pattern()[1]
+
+    @property
+    def indices(self):
+        return self._csr_pattern()[2]
 
     def _set_scaling(self, opt: IpmOptions):
         """Gradient-based scaling at the starting point (Ipopt
