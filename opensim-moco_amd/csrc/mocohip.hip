@@ -134,7 +134,7 @@ __global__ void __launch_bounds__(256) k_transcribe(Layout L, Interval I, Lanes 
             auto bulk = [&](auto fdc) {
                 constexpr int FD = decltype(fdc)::value;
                 const double hq = FD == MH_FD_CENTRAL ? 2.0 * Ln.h : Ln.h;
-                constexpr int CT_U = 4;
+                constexpr int CT_U = 8;
                 for (int e0 = eb + (int)threadIdx.x; e0 < ee; e0 += CT_U * (int)blockDim.x) {
                     uint32_t w[CT_U], wb[CT_U];
 #pragma unroll
