@@ -42,7 +42,7 @@ def _worker(index, subject, num_mesh_intervals, device, start, out, linear_solve
         from .ipm import IpmOptions
         if linear_solver == "device" or (linear_solver == "auto" and
                                          nlp.m >= IpmOptions().device_kkt_min_constraints):
-            nlp.device_kkt()                  # the device KKT module (and its first launches) set up before the start
+            nlp.device_kkt(warm=True)         # the device KKT module (and its first launches) set up before the start
     except Exception as e:   # setup failed: still meet the others at the barrier
         res["error"] = "setup: " + repr(e)[:200]
     try:

@@ -481,21 +481,24 @@ class HipNLP(_NLPBase):
         self.lib = lib or abi.load_mocohip()
         super().__init__(rep, opts)
 
-    def device_kkt(self):
+    def device_kkt(self, warm: bool = False):
         """The device KKT module over this context (include/mocohip_kkt.h,
         mocohip.kkt.DeviceKKT; created once): the host optimizer's Newton
         systems factored next to the Jacobian.  Raises ValueError when the
         Jacobian lacks the per-interval block structure, RuntimeError on a
-        sharded context.  Creation includes DeviceKKT.warm (first kernel
-        launches and graph captures at the bounds-midpoint guess)."""
+        sharded context.  warm=True (set-up ahead of a timed region, e.g. a
+        sweep's workers) also runs DeviceKKT.warm at creation: the first
+        kernel launches and graph captures, at the bounds-midpoint guess;
+        otherwise they happen in the first solve."""
         if getattr(self, "_dkkt", None) is None:
             from .kkt import DeviceKKT
             dk = DeviceKKT(self)
-            try:
-                dk.warm(self.initial_guess_from_bounds())
-            except Exception:
-                dk.close()
-                raise
+            if warm:
+                try:
+                    dk.warm(self.initial_guess_from_bounds())
+                except Exception:
+                    dk.close()
+                    raise
             self._dkkt = dk
         return self._dkkt
 
