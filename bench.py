@@ -53,6 +53,17 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "opensim-moco_amd"))
 
+# One GPU (no torch.distributed launcher): this process and the configs[4]
+# sweep's eight solver processes it starts run with 2 HIP hardware queues
+# each, read by the HIP runtime at its start (before anything below touches
+# the GPU).  The sweep's small, latency-bound kernels overlap on the GPU only
+# while every process's queues are mapped together (0.72 -> 0.69 s for the
+# sweep with this process at 2 instead of 4; the workers' own setting:
+# mocohip.batchsolve); the single-stream lines are unaffected (21.3 k vs
+# 21.5 k calls/s).  The multi-GPU runs keep the environment's setting.
+if int(os.environ.get("WORLD_SIZE", "1")) == 1:
+    os.environ["GPU_MAX_HW_QUEUES"] = "2"
+
 FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector (= FP64 matrix) dense peak, spec
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md (spec; 6.29 TB/s measured copy)
 
