@@ -695,6 +695,7 @@ struct Interval {
     int pf;          // k_interval prefetches its first IV_PF assembly words per thread
     int qfuse;       // k_interval forms each finite-difference quotient in the assembly
                      // (no in-place quotient pass)
+    int xcd;         // k_interval: contiguous interval runs per XCD (xcd_interval)
     // Every interval opens with its mesh point's path rows.  The interval
     // N-1 also owns the tail (flattenConstraints, CasOCTranscription.h:
     // 286-308): the final mesh point's path rows, then the final grid
@@ -1345,6 +1346,18 @@ __device__ __forceinline__ void interval_body(const DevModel& M, const Src& S, c
         endpoint_head(L, Ln, I.E, S.x, g ? I.gh : nullptr, values ? I.vh : nullptr, threadIdx.x, blockDim.x);
 }
 
+// The hardware dispatches a launch's workgroups to the 8 XCDs round-robin
+// (workgroup b -> XCD b % 8), each XCD with its own L2.  Hermite-Simpson
+// neighbours share a grid point, whose group results both intervals stage,
+// so with I.xcd workgroup b takes interval c * q + min(c, rem) + b / 8
+// (c = b % 8, q / rem = nb / 8, nb % 8): XCD c gets one contiguous run of
+// intervals and the shared point's second read can hit that XCD's L2.  A
+// bijection of 0 .. nb - 1 for every nb.
+__device__ __forceinline__ int xcd_interval(int b, int nb) {
+    const int c = b & 7, s = b >> 3, q = nb >> 3, rem = nb & 7;
+    return c * q + (c < rem ? c : rem) + s;
+}
+
 // MAXT: the launch bound.  eval_g's launches (stride-1 lanes, c->ivg_threads
 // = 256) take the 256-thread instantiation: its combine lanes may keep up to
 // 512 VGPRs, where the 1024-thread bound (128) made a large model's combine
@@ -1357,7 +1370,9 @@ __global__ void __launch_bounds__(MAXT) k_interval(DevModel M, Src S, Lanes Ln, 
         double* __restrict__ values, int il0) {
     // il0: the first interval of this launch within the shard (a chunked
     // assembly, whose chunks are copied to the host while the next runs)
-    interval_body<D, false>(M, S, Ln, TK, L, I, tpl, ctpl, ctgen, nctgen, T, H, g, values, il0 + (int)blockIdx.x);
+    const int b = (int)blockIdx.x;
+    interval_body<D, false>(M, S, Ln, TK, L, I, tpl, ctpl, ctgen, nctgen, T, H, g, values,
+                            il0 + (I.xcd ? xcd_interval(b, (int)gridDim.x) : b));
 }
 
 // ------------------------------------------------------------------------
@@ -1398,7 +1413,15 @@ template <class D, bool GM>
 __global__ void __launch_bounds__(1024) kb_interval(const BatchItem* __restrict__ items, BatchPtrs BP, Lanes Ln,
         Tasks TK, Layout L, Interval I0, const TplEntry* __restrict__ tpl, const uint32_t* __restrict__ ctpl,
         const int* __restrict__ ctgen, int nctgen, int with_g, int with_v, int nep, int nnz_ep) {
-    const int b = blockIdx.y;
+    // XCD-contiguous order over the whole (interval, NLP) grid (xcd_interval
+    // on the linear workgroup id, x fastest)
+    int b = (int)blockIdx.y, il = (int)blockIdx.x;
+    if (I0.xcd) {
+        const int nb = (int)gridDim.x;
+        const int lin = xcd_interval(b * nb + il, nb * (int)gridDim.y);
+        b = lin / nb;
+        il = lin - b * nb;
+    }
     const BatchItem& it = items[b];
     const Src S{BP.x[b], it.grid, nullptr, L.G, L.k0, L.XM, L.XL, L.DB};
     Interval I = I0;
@@ -1414,7 +1437,7 @@ __global__ void __launch_bounds__(1024) kb_interval(const BatchItem* __restrict_
         if (g) g += nep;
         if (v) v += nnz_ep;
     }
-    interval_body<D, GM>(it.M, S, Ln, TK, L, I, tpl, ctpl, ctgen, nctgen, it.T, it.H, g, v, blockIdx.x);
+    interval_body<D, GM>(it.M, S, Ln, TK, L, I, tpl, ctpl, ctgen, nctgen, it.T, it.H, g, v, il);
 }
 
 // ------------------------------------------------------------------------
@@ -1976,6 +1999,7 @@ struct mh_ctx {
     bool async = false;                // *_device entries return once enqueued
     int iv_dbg_stop = 0;               // diagnostic: k_interval stops after phase n
     int iv_pf = 1;                     // MOCOHIP_IV_PF=0: no assembly-word prefetch (A/B)
+    int iv_xcd = 1;                    // XCD-contiguous interval order (MOCOHIP_IV_XCD=0: off, A/B)
     int iv_qfuse = 1;                  // MOCOHIP_IV_QFUSE=0: in-place quotient pass (A/B)
     hipEvent_t ev[5] = {};         // stage boundaries (+ ev[4] after k_groups)
     // host entries: the Jacobian values go to the host in interval chunks on
@@ -2100,7 +2124,8 @@ inline Layout make_layout(const mh_ctx* c, int k0, int nk) {
 // block writes through I.gh / I.vh when this shard owns it.
 inline Interval make_interval(const mh_ctx* c, double*& g, double*& v) {
     Interval I{c->scheme, c->interp, c->ib, c->rpi, c->nnz_int, c->NMB + c->NAR, c->NMB, c->NQ + c->NZ,
-               c->N, c->nnz_tail, c->ntail, c->npe, c->NK, c->OKC, c->P, c->E, nullptr, nullptr, c->iv_dbg_stop, c->iv_pf, c->iv_qfuse};
+               c->N, c->nnz_tail, c->ntail, c->npe, c->NK, c->OKC, c->P, c->E, nullptr, nullptr, c->iv_dbg_stop, c->iv_pf, c->iv_qfuse,
+               c->iv_xcd};
     if (c->ib == 0 && c->nep > 0) {
         I.gh = g;
         I.vh = v;

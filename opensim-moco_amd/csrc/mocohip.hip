@@ -1635,6 +1635,11 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
         c->iv_dbg_stop = ed ? std::atoi(ed) : 0;
         const char* ef = std::getenv("MOCOHIP_IV_PF");
         c->iv_pf = ef && std::strcmp(ef, "0") == 0 ? 0 : 1;
+        // XCD-contiguous interval order in k_interval / kb_interval
+        // (xcd_interval, core.hpp; gait N=200: k_interval's HBM reads 10.4 ->
+        // 7.5 MB per launch, profiles/r04_xcd); MOCOHIP_IV_XCD=0: plain order
+        const char* ex = std::getenv("MOCOHIP_IV_XCD");
+        c->iv_xcd = ex && std::strcmp(ex, "0") == 0 ? 0 : 1;
         // hipGraph replay of the stages: measured slower than direct launches
         // on ROCm 7.2 for this sequence (opt-in, MOCOHIP_GRAPHS=1)
         const char* eg = std::getenv("MOCOHIP_GRAPHS");

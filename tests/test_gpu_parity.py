@@ -307,7 +307,7 @@ def _pair(name, backend="auto", tasks=None, env=None):
     saved = {k: os.environ.pop(k, None) for k in ("MOCOHIP_BACKEND", "MOCOHIP_TASKS", "MOCOHIP_INTERVAL",
                                                   "MOCOHIP_ASM", "MOCOHIP_QUOT", "MOCOHIP_CTPL",
                                                   "MOCOHIP_ROLES", "MOCOHIP_ROLE_COUPLE",
-                                                  "MOCOHIP_IV_QFUSE", "MOCOHIP_IV_THREADS",
+                                                  "MOCOHIP_IV_QFUSE", "MOCOHIP_IV_THREADS", "MOCOHIP_IV_XCD",
                                                   "MOCOHIP_EXC_LANES", "MOCOHIP_G_BLOCK", "MOCOHIP_G_LDS",
                                                   "MOCOHIP_G_LDS_GUARD",
                                                   "MOCOHIP_GROUPS_SPLIT", "MOCOHIP_COMBINE",
@@ -830,7 +830,8 @@ def test_pruned_tasks_bit_identical(name):
                                      {"MOCOHIP_ROLES": "1", "MOCOHIP_ROLE_COUPLE": "0"},
                                      {"MOCOHIP_IV_THREADS": "512"},
                                      {"MOCOHIP_IV_QFUSE": "0"},
-                                     {"MOCOHIP_IV_QFUSE": "0", "MOCOHIP_CTPL": "0"}])
+                                     {"MOCOHIP_IV_QFUSE": "0", "MOCOHIP_CTPL": "0"},
+                                     {"MOCOHIP_IV_XCD": "0"}])
 def test_kernel_variants_bit_identical(name, variant):
     """The default k_interval (combine + transcription per mesh interval,
     raw outputs in LDS) writes exactly what k_interval writes through
