@@ -52,8 +52,14 @@ typedef struct {
     const int32_t* col2;
 } mh_kkt_layout;
 
-/* A KKT module over an unsharded context (its n, m, nnz must match the
- * layout's).  The context must outlive it. */
+/* A KKT module over a context; the context must outlive it.  The layout is
+ * the whole NLP's (n, m, nnz of mh_get_nlp_info).  Over a SHARD context
+ * (mh_options interval_begin / interval_end: one rank of an NLP sharded by
+ * mesh interval) the module still factors the whole
+ * Jacobian on this GPU: mh_kkt_eval_jacobian writes only the shard's slice
+ * [nnz_begin, nnz_end) of the values buffer, the caller receives the other
+ * ranks' slices into their offsets (e.g. RCCL over xGMI into a buffer bound
+ * with mh_kkt_bind_values), then calls mh_kkt_assemble. */
 int mh_kkt_create(mh_ctx* ctx, const mh_kkt_layout* layout, mh_kkt** out);
 void mh_kkt_destroy(mh_kkt* kkt);
 /* R (m doubles, default 1): the optimizer's constraint row scaling. */
@@ -62,6 +68,17 @@ int mh_kkt_set_row_scale(mh_kkt* kkt, const double* row_scale);
  * buffer, gathered into the blocks A_b and the dense columns (row-scaled).
  * Replaces the eval_jac_g a host Ipopt would make at this iterate. */
 int mh_kkt_eval_jacobian(mh_kkt* kkt, const double* x);
+/* Sharded module: the blocks and dense columns from the whole values buffer
+ * once every slice is in it (the gather mh_kkt_eval_jacobian does itself on
+ * an unsharded context); synchronous. */
+int mh_kkt_assemble(mh_kkt* kkt);
+/* The Jacobian values buffer: nnz doubles of device memory on the module's
+ * GPU owned by the caller, used from now on instead of the module's own
+ * (which stays allocated); the caller keeps it alive. */
+int mh_kkt_bind_values(mh_kkt* kkt, double* values_device);
+/* This module's own slice [*nnz_begin, *nnz_end) of the values (the whole
+ * range on an unsharded context). */
+int mh_kkt_shard_range(const mh_kkt* kkt, int64_t* nnz_begin, int64_t* nnz_end);
 /* The raw values of the last mh_kkt_eval_jacobian (nnz doubles). */
 int mh_kkt_get_values(mh_kkt* kkt, double* values);
 /* The row-scaled dense columns, [m][nd]. */

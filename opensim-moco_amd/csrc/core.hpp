@@ -434,14 +434,17 @@ __device__ __forceinline__ void groups_body(const DevModel& M, const Src& S, con
         double* __restrict__ T, double* __restrict__ H, int blk) {
     const int lane = threadIdx.x;
     const int4 rec = TK.blk[blk];   // one scalar load: no dependent table chain
-    const int g = __builtin_amdgcn_readfirstlane(rec.x);
+    // (group | live tasks << 16, first task, tasks per grid point, 1 / that)
+    const int gx = __builtin_amdgcn_readfirstlane(rec.x);
+    const int g = gx & 0xffff, cnt = gx >> 16;
+    if (cnt == 0) return;           // a padding block of the XCD arrangement
     if constexpr (CLS == 1) __builtin_assume(g < D::NHEAVY);
     if constexpr (CLS == 2) __builtin_assume(g >= D::NHEAVY);
     const int first = __builtin_amdgcn_readfirstlane(rec.y);
     const int n = __builtin_amdgcn_readfirstlane(rec.z);
     const float inv = __int_as_float(__builtin_amdgcn_readfirstlane(rec.w));
     const int task = first + lane;
-    const bool live = task < TK.nk * n;
+    const bool live = lane < cnt;
     const int tc = live ? task : 0;
     // tc / n through the float reciprocal, corrected to the exact quotient
     int kl = (int)((float)tc * inv);
@@ -496,6 +499,13 @@ struct LdsOut {
     lds_double* p;
     int s;
     __device__ __forceinline__ lds_double& operator[](int o) const { return p[o * s]; }
+};
+// A lane role's combine sums (D::combine_sum) as D::combine_finish reads
+// them: sum q at p[q * s] (LDS, [q][role]).
+struct SumsLds {
+    const lds_double* p;
+    int s;
+    __device__ __forceinline__ double operator()(int q) const { return p[q * s]; }
 };
 
 // Combine: one workgroup per grid point.  The grid point's group results
@@ -1127,29 +1137,55 @@ __device__ __forceinline__ void interval_body(const DevModel& M, const Src& S, c
     if (threadIdx.x < 2) sK[threadIdx.x] = threadIdx.x ? 1.0 : 0.0;
     __syncthreads();
     if (I.dbg_stop == 1) return;
-    // eval_g's lanes (stride 1: every lane is the base role 0, written as a
-    // constant so that the role -> slot reads have uniform addresses and
-    // compile to scalar loads off the combine's critical path)
-    auto combine_lane = [&](int p, int r) {
-        LaneInL<D> in{lds(sXs + p * L.NS), lds(sXc + p * L.NC), lds(sXd + p * L.NDV), -1, 0.0,
-                      lds(sXm + p * L.NM), L.vc(k_first + p) ? lds(sXl) : nullptr};
-        const double t = lane_time(Ln, S.grid[k_first + p], t0, tf, r, in.pi, in.step);
-        if (r == Ln.base) sTimes[p] = t;
-        const LdsOut out{lds(sY + p * ny + r), Ln.stride};
-        if constexpr (GM) {
-            const TaskLoadGlobal<D> TL{T + (long)(kl0 + p) * nt, H + (long)(kl0 + p) * nh, TK.jd, r};
-            D::combine(M, t, in, TL, out);
-        } else {
-            const TaskLoadLds<D> TL{lds(sT + p * nt), lds(sH + p * nh), TK.jd, r};
-            D::combine(M, t, in, TL, out);
+    {
+        // the combine in two steps (D::combine_sum / D::combine_finish, the
+        // same arithmetic as D::combine, bit for bit): first its NSUM
+        // independent sums (each coordinate's generalized force, each
+        // root-chain mass-matrix entry) of every lane role, one sum per
+        // wave task -- q uniform over the wave, lanes over the roles -- into
+        // LDS [q][role]; then per role the factorization and solves from
+        // those sums.  A role's ~NSUM chains of LDS reads and adds run on
+        // NSUM waves instead of one thread (eval_g: 3 threads did all of it)
+        const int R = npts * Ln.stride;
+        lds_double* sS = lds(sXl + L.NSL);
+        const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+        const int ln = (int)threadIdx.x & 63, nw = (int)blockDim.x >> 6;
+        const int nch = (R + 63) >> 6;
+        for (int v = wv; v < D::NSUM * nch; v += nw) {
+            const int q = v % D::NSUM;
+            const int pr = (v / D::NSUM) * 64 + ln;
+            if (pr < R) {
+                const int p = pr / Ln.stride, r = pr - p * Ln.stride;
+                LaneInL<D> in{lds(sXs + p * L.NS), lds(sXc + p * L.NC), lds(sXd + p * L.NDV), -1, 0.0,
+                              lds(sXm + p * L.NM), L.vc(k_first + p) ? lds(sXl) : nullptr};
+                const double t = lane_time(Ln, S.grid[k_first + p], t0, tf, r, in.pi, in.step);
+                double sv;
+                if constexpr (GM) {
+                    const TaskLoadGlobal<D> TL{T + (long)(kl0 + p) * nt, H + (long)(kl0 + p) * nh, TK.jd, r};
+                    sv = D::combine_sum(q, M, t, in, TL);
+                } else {
+                    const TaskLoadLds<D> TL{lds(sT + p * nt), lds(sH + p * nh), TK.jd, r};
+                    sv = D::combine_sum(q, M, t, in, TL);
+                }
+                sS[q * R + pr] = sv;
+            }
         }
-    };
-    if (Ln.stride == 1) {
-        if ((int)threadIdx.x < npts) combine_lane((int)threadIdx.x, 0);
-    } else {
-        for (int w = threadIdx.x; w < npts * Ln.stride; w += blockDim.x) {
+        __syncthreads();
+        for (int w = threadIdx.x; w < R; w += blockDim.x) {
             const int p = w / Ln.stride, r = w - p * Ln.stride;
-            combine_lane(p, r);
+            LaneInL<D> in{lds(sXs + p * L.NS), lds(sXc + p * L.NC), lds(sXd + p * L.NDV), -1, 0.0,
+                          lds(sXm + p * L.NM), L.vc(k_first + p) ? lds(sXl) : nullptr};
+            const double t = lane_time(Ln, S.grid[k_first + p], t0, tf, r, in.pi, in.step);
+            if (r == Ln.base) sTimes[p] = t;
+            const LdsOut out{lds(sY + p * ny + r), Ln.stride};
+            const SumsLds SV{sS + w, R};
+            if constexpr (GM) {
+                const TaskLoadGlobal<D> TL{T + (long)(kl0 + p) * nt, H + (long)(kl0 + p) * nh, TK.jd, r};
+                D::combine_finish(M, t, in, TL, SV, out);
+            } else {
+                const TaskLoadLds<D> TL{lds(sT + p * nt), lds(sH + p * nh), TK.jd, r};
+                D::combine_finish(M, t, in, TL, SV, out);
+            }
         }
     }
     // the compiled words of this thread's first IV_PF assembly entries,
@@ -2062,6 +2098,7 @@ struct mh_ctx {
     int role_threads = 256;        // k_role workgroup size (MOCOHIP_ROLE_THREADS: 64..512)
     int iv_threads = 1024;         // k_interval workgroup size, Jacobian lanes (MOCOHIP_IV_THREADS: 256..1024)
     int ivg_threads = 256;         // k_interval workgroup size, eval_g lanes (MOCOHIP_IVG_THREADS: 64..1024)
+    int csplit = 1;                // MOCOHIP_CSPLIT=0: no k_interval (its combine is the split one)
     bool role_couple = true;       // coupling in k_role's time role (MOCOHIP_ROLE_COUPLE=0: k_couple)
     bool use_ctpl = true;          // MOCOHIP_CTPL=0: k_interval assembles through jac_entry
     float timings[4] = {0, 0, 0, 0};
@@ -2311,13 +2348,24 @@ static void be_eval_tasks(mh_ctx* c, const double* x, int mode, double* Y) {
     }
     c->yq[mode] = launch_tasks<D>(c, S, ln, ts, T, H, c->d_times, Y, mode == 1 && c->quot);
 }
+// LDS bytes of k_interval's combine sums (interval_body: [NSUM][npts x
+// lanes] doubles).  MOCOHIP_CSPLIT=0 reports "does not fit": the evaluation
+// then takes the split path (k_combine's one-thread-per-lane combine + the
+// transcription), the A/B reference of the split combine.
+template <class D>
+static size_t interval_sums_lds(const mh_ctx* c, const Lanes& ln) {
+    if (!c->csplit) return kMaxLds + 1;
+    const size_t npts = c->scheme == MH_HERMITE_SIMPSON ? 3 : 2;
+    return sizeof(double) * npts * (size_t)ln.stride * (size_t)(D::NSUM > 0 ? D::NSUM : 1);
+}
 // LDS bytes of k_interval for one lane configuration (0: does not apply).
 template <class D>
 static size_t interval_lds(const mh_ctx* c, const Lanes& ln, const TaskSet& ts) {
     const size_t npts = c->scheme == MH_HERMITE_SIMPSON ? 3 : 2;
     return sizeof(double) * (npts * D::NO * ln.stride + CT_CONST + CT_NCONST +
                              npts * (size_t)(c->NS + c->NC + c->NDV + c->NM) + (size_t)c->NSL +
-                             npts * ((size_t)ts.dev.tdoubles + (size_t)ts.dev.nmass * D::NST));
+                             npts * ((size_t)ts.dev.tdoubles + (size_t)ts.dev.nmass * D::NST)) +
+           interval_sums_lds<D>(c, ln);
 }
 // LDS bytes of k_role (Jacobian lanes).
 template <class D>
@@ -2338,7 +2386,8 @@ template <class D>
 static size_t interval_lds_gm(const mh_ctx* c, const Lanes& ln) {
     const size_t npts = c->scheme == MH_HERMITE_SIMPSON ? 3 : 2;
     return sizeof(double) * (npts * D::NO * ln.stride + CT_CONST + CT_NCONST +
-                             npts * (size_t)(c->NS + c->NC + c->NDV + c->NM) + (size_t)c->NSL);
+                             npts * (size_t)(c->NS + c->NC + c->NDV + c->NM) + (size_t)c->NSL) +
+           interval_sums_lds<D>(c, ln);
 }
 template <class D>
 static void be_batch(mh_batch* bt, int mode, const BatchPtrs& BP, int with_g, int with_v) {

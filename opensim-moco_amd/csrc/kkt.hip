@@ -51,6 +51,7 @@ hipStream_t mh_internal_stream(const mh_ctx* c);
 int mh_internal_device(const mh_ctx* c);
 int mh_internal_shape(const mh_ctx* c, int64_t* n, int64_t* m, int64_t* nnz, int* unsharded);
 int mh_internal_jac_device(mh_ctx* c, const double* x_dev, double* v_dev);
+int mh_internal_shard(const mh_ctx* c, int64_t* m_full, int64_t* nnz_full, int64_t* nnz_begin, int64_t* nnz_end);
 
 #define KCHK(expr)                                                                       \
     do {                                                                                 \
@@ -715,6 +716,11 @@ struct mh_kkt {
     std::vector<KLevel> levels;      // the last level holds the single remaining block
     std::vector<void*> allocs;
     bool factored = false;
+    // a module over a SHARD context (the whole NLP's Jacobian on this GPU,
+    // mh_kkt_eval_jacobian writing only the shard's slice [nz0, nz1), the
+    // caller filling the rest of the bound buffer, then mh_kkt_assemble)
+    bool sharded = false;
+    int64_t nz0 = 0, nz1 = 0;
     // the factorization's and each solve width's kernel sequences as HIP
     // graphs (captured on first use; every pointer they take is fixed at
     // create): one launch per call instead of ~50 (MOCOHIP_KKT_GRAPHS=0: off)
@@ -855,9 +861,12 @@ extern "C" int mh_kkt_create(mh_ctx* ctx, const mh_kkt_layout* L, mh_kkt** out) 
     int unsharded = 0;
     int rc = mh_internal_shape(ctx, &n, &m, &nnz, &unsharded);
     if (rc) return rc;
-    if (!unsharded) return mh_internal_error(MH_ERR_UNSUPPORTED, "mh_kkt needs an unsharded context");
+    // a shard context: the layout is the WHOLE NLP's (the module factors the
+    // whole Jacobian; the context evaluates its own slice of it)
+    int64_t nz0 = 0, nz1 = nnz;
+    if (!unsharded && (rc = mh_internal_shard(ctx, &m, &nnz, &nz0, &nz1))) return rc;
     if (L->n != n || L->m != m || L->nnz != nnz)
-        return mh_internal_error(MH_ERR_INVALID, "mh_kkt_layout does not match the context (n, m, nnz)");
+        return mh_internal_error(MH_ERR_INVALID, "mh_kkt_layout does not match the context's NLP (n, m, nnz)");
     if (L->nblocks < 1 || L->r < 1 || L->c < 1 || L->nd < 0 || L->nshare < 0 || L->nshare > L->c || !L->a_src ||
             !L->rowmap || !L->colmap || !L->lshare || !L->rshare || !L->col2 || (L->nd > 0 && (!L->dcols || !L->d_src)))
         return mh_internal_error(MH_ERR_INVALID, "bad mh_kkt_layout");
@@ -884,6 +893,8 @@ extern "C" int mh_kkt_create(mh_ctx* ctx, const mh_kkt_layout* L, mh_kkt** out) 
     h->device = mh_internal_device(ctx);
     h->nb = L->nblocks; h->r = L->r; h->c = L->c; h->nd = L->nd; h->P = L->nshare;
     h->m = m; h->n = n; h->nnz = nnz;
+    h->sharded = !unsharded;
+    h->nz0 = nz0; h->nz1 = nz1;
     h->lshare.assign(L->lshare, L->lshare + h->nb);
     if (const char* eg = std::getenv("MOCOHIP_KKT_GRAPHS")) h->graphs = std::atoi(eg) != 0;
     h->inv_path = L->r <= INV_RMAX;
@@ -1011,11 +1022,40 @@ extern "C" int mh_kkt_eval_jacobian(mh_kkt* h, const double* x) {
     KCHK(hipSetDevice(h->device));
     hipStream_t s = mh_internal_stream(h->ctx);
     KCHK(hipMemcpyAsync(h->x, x, sizeof(double) * h->n, hipMemcpyHostToDevice, s));
-    int rc = mh_internal_jac_device(h->ctx, h->x, h->vals);
+    int rc = mh_internal_jac_device(h->ctx, h->x, h->vals + h->nz0);
     if (rc) return rc;
+    h->factored = false;
+    if (h->sharded) {   // the other slices come from the other ranks, then mh_kkt_assemble
+        KCHK(hipStreamSynchronize(s));
+        return MH_OK;
+    }
     if ((rc = gather(h, s))) return rc;
+    KCHK(hipStreamSynchronize(s));
+    return MH_OK;
+}
+
+extern "C" int mh_kkt_assemble(mh_kkt* h) {
+    if (!h) return mh_internal_error(MH_ERR_INVALID, "null argument");
+    KCHK(hipSetDevice(h->device));
+    hipStream_t s = mh_internal_stream(h->ctx);
+    int rc = gather(h, s);
+    if (rc) return rc;
     h->factored = false;
     KCHK(hipStreamSynchronize(s));
+    return MH_OK;
+}
+
+extern "C" int mh_kkt_bind_values(mh_kkt* h, double* values_dev) {
+    if (!h || !values_dev) return mh_internal_error(MH_ERR_INVALID, "null argument");
+    h->vals = values_dev;   // the module's own buffer stays allocated (freed with it)
+    h->factored = false;
+    return MH_OK;
+}
+
+extern "C" int mh_kkt_shard_range(const mh_kkt* h, int64_t* nnz_begin, int64_t* nnz_end) {
+    if (!h || !nnz_begin || !nnz_end) return mh_internal_error(MH_ERR_INVALID, "null argument");
+    *nnz_begin = h->nz0;
+    *nnz_end = h->nz1;
     return MH_OK;
 }
 

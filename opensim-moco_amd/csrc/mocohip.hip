@@ -470,7 +470,12 @@ struct Arena {
 // perturbed lane those that read its perturbed input (or the time, for the
 // t0/tf directions).  MOCOHIP_TASKS=all disables the pruning (every group
 // for every lane; the reference for the bit-identity test).
-static void build_taskset(const TaskInfo& ti, const Lanes& ln, int nk, int nsimd, TaskSet& ts) {
+// nint > 0: the k_groups blocks are arranged for the XCDs (groups_xcd below):
+// the tasks of the grid points whose intervals k_interval hands to XCD c
+// (xcd_interval: one contiguous run of nint intervals per XCD; pts_per = 2
+// Hermite-Simpson, 1 trapezoidal) run in blocks b with b % 8 = c.
+static void build_taskset(const TaskInfo& ti, const Lanes& ln, int nk, int nsimd, TaskSet& ts,
+        int nint = 0, int pts_per = 2) {
     const char* env = std::getenv("MOCOHIP_TASKS");
     const bool all = env && std::strcmp(env, "all") == 0;
     const int ng = ti.ng, S = ln.stride;
@@ -517,18 +522,61 @@ static void build_taskset(const TaskInfo& ti, const Lanes& ln, int nk, int nsimd
     // timing diagnostic only (results invalid): launch group G's blocks alone
     const char* dg = std::getenv("MOCOHIP_DEBUG_GROUP");
     const int only = dg ? std::atoi(dg) : -1;
-    for (int g : order) {
-        if (only >= 0 && g != only) continue;
-        const long n = (long)nk * ts.dlen[g];
+    // A block record is (group | live tasks << 16, first task, tasks per
+    // grid point, 1 / tasks per grid point as float bits); its live tasks
+    // are first .. first + live - 1 (live = 0: an empty padding block).
+    auto push = [&](std::vector<int>& v, int g, long f, long cnt) {
         const float inv = 1.0f / (float)ts.dlen[g];
         int inv_bits;
         std::memcpy(&inv_bits, &inv, sizeof inv);
-        for (long f = 0; f < n; f += 64) {
-            ts.blk.push_back(g); ts.blk.push_back((int)f);
-            ts.blk.push_back(ts.dlen[g]); ts.blk.push_back(inv_bits);
+        v.push_back(g | (int)(cnt << 16)); v.push_back((int)f);
+        v.push_back(ts.dlen[g]); v.push_back(inv_bits);
+    };
+    // groups_xcd: XCD c's grid points are [P[c], P[c + 1]) -- the points of
+    // the intervals xcd_interval gives XCD c, a shared mesh point going to
+    // the later run -- so the group results k_interval stages on XCD c were
+    // written by blocks of that XCD and can still sit in its L2 (plain stores
+    // keep their lines in the writing XCD's L2; the next kernel's acquire
+    // invalidates L1 only).  Per XCD the heavy groups' blocks lead, in the
+    // same heaviest-first order; the lists are padded to equal heavy and
+    // light lengths and interleaved (block b -> XCD b % 8 under the
+    // hardware's round-robin dispatch; placement is speed only).
+    const char* ex = std::getenv("MOCOHIP_GROUPS_XCD");
+    const bool xcd = nint > 0 && only < 0 && !(ex && std::atoi(ex) == 0);
+    std::vector<long> P(9, 0);
+    if (xcd) {
+        const int q = nint / 8, rem = nint % 8;
+        for (int c = 0; c < 8; ++c) P[c] = (long)pts_per * (c * q + std::min(c, rem));
+        P[8] = nk;
+    }
+    std::vector<int> lists[2][8];   // [heavy / light][XCD]
+    for (int g : order) {
+        if (only >= 0 && g != only) continue;
+        const long n = (long)nk * ts.dlen[g];
+        if (!xcd) {
+            for (long f = 0; f < n; f += 64) push(ts.blk, g, f, std::min(64L, n - f));
+        } else {
+            for (int c = 0; c < 8; ++c) {
+                const long a = P[c] * ts.dlen[g], e = P[c + 1] * ts.dlen[g];
+                for (long f = a; f < e; f += 64) push(lists[g < ti.nheavy ? 0 : 1][c], g, f, std::min(64L, e - f));
+            }
         }
         ts.flops += (double)n * ti.gflops[g];
         ts.ntasks += (double)n;
+    }
+    if (xcd) {
+        for (int h = 0; h < 2; ++h) {
+            size_t len = 0;
+            for (int c = 0; c < 8; ++c) len = std::max(len, lists[h][c].size() / 4);
+            const int gpad = h == 0 ? 0 : ti.ng - 1;   // a group of the class (heavy: 0)
+            for (size_t s = 0; s < len; ++s)
+                for (int c = 0; c < 8; ++c) {
+                    if (s < lists[h][c].size() / 4)
+                        ts.blk.insert(ts.blk.end(), lists[h][c].begin() + 4 * s, lists[h][c].begin() + 4 * s + 4);
+                    else
+                        push(ts.blk, gpad, 0, 0);
+                }
+        }
     }
     ts.flops += (double)nk * S * ti.combine_flops;
     ts.nblocks = (int)(ts.blk.size() / 4);
@@ -537,16 +585,16 @@ static void build_taskset(const TaskInfo& ti, const Lanes& ln, int nk, int nsimd
     // shares its SIMD with the lightest (MOCOHIP_ORDER=desc keeps plain
     // longest-first order).
     const char* eo = std::getenv("MOCOHIP_ORDER");
-    const bool pair = !(eo && std::strcmp(eo, "desc") == 0);
+    const bool pair = !(eo && std::strcmp(eo, "desc") == 0) && !xcd;
     if (pair && ts.nblocks > nsimd && ts.nblocks <= 2 * nsimd) {
         for (int a = nsimd, b = ts.nblocks - 1; a < b; ++a, --b)
             for (int w = 0; w < 4; ++w) std::swap(ts.blk[4 * (size_t)a + w], ts.blk[4 * (size_t)b + w]);
     }
     // the heavy groups' blocks (groups < NHEAVY) as one leading run (k_groups_part)
     ts.nheavy = 0;
-    while (ts.nheavy < ts.nblocks && ts.blk[4 * (size_t)ts.nheavy] < ti.nheavy) ++ts.nheavy;
+    while (ts.nheavy < ts.nblocks && (ts.blk[4 * (size_t)ts.nheavy] & 0xffff) < ti.nheavy) ++ts.nheavy;
     for (int b = ts.nheavy; b < ts.nblocks; ++b)
-        if (ts.blk[4 * (size_t)b] < ti.nheavy) { ts.nheavy = -1; break; }
+        if ((ts.blk[4 * (size_t)b] & 0xffff) < ti.nheavy) { ts.nheavy = -1; break; }
     ts.dev.ng = ng;
     ts.dev.stride = S;
     ts.dev.tdoubles = tdoubles;
@@ -1500,8 +1548,13 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     size_t o_T = 0, o_H = 0, o_Tg = 0, o_Hg = 0, o_xsl = 0, o_cmap = 0;
     const TaskInfo* ti = backend_tasks(c->be);
     if (ti) {
-        build_taskset(*ti, c->lanes_jac, c->nk, c->nsimd, c->ts_jac);
-        build_taskset(*ti, c->lanes_g, c->nk, c->nsimd, c->ts_g);
+        // the blocks of both task sets in k_interval's XCD order (groups_xcd)
+        // (MOCOHIP_IV_XCD=0, the plain interval order, keeps the plain block order too)
+        const char* eiv = std::getenv("MOCOHIP_IV_XCD");
+        const bool ivx = !(eiv && std::strcmp(eiv, "0") == 0);
+        const int nint = ivx ? c->ie - c->ib : 0, ppi = c->scheme == MH_HERMITE_SIMPSON ? 2 : 1;
+        build_taskset(*ti, c->lanes_jac, c->nk, c->nsimd, c->ts_jac, nint, ppi);
+        build_taskset(*ti, c->lanes_g, c->nk, c->nsimd, c->ts_g, nint, ppi);
         to_jac = put_taskset(A, c->ts_jac);
         to_g = put_taskset(A, c->ts_g);
         // excitation lanes of the generated back end (k_exc_fill): the lane
@@ -1640,6 +1693,13 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
         // 7.5 MB per launch, profiles/r04_xcd); MOCOHIP_IV_XCD=0: plain order
         const char* ex = std::getenv("MOCOHIP_IV_XCD");
         c->iv_xcd = ex && std::strcmp(ex, "0") == 0 ? 0 : 1;
+        // k_interval's combine is its independent sums spread over the
+        // workgroup's waves, then the factorization and solves per lane role
+        // (D::combine_sum / combine_finish; interval_body); MOCOHIP_CSPLIT=0
+        // takes the split path instead (k_combine: one thread per lane role
+        // does all of it, D::combine) -- the A/B reference
+        const char* ecs = std::getenv("MOCOHIP_CSPLIT");
+        c->csplit = ecs && std::strcmp(ecs, "0") == 0 ? 0 : 1;
         // hipGraph replay of the stages: measured slower than direct launches
         // on ROCm 7.2 for this sequence (opt-in, MOCOHIP_GRAPHS=1)
         const char* eg = std::getenv("MOCOHIP_GRAPHS");
@@ -2345,6 +2405,18 @@ int mh_internal_shape(const mh_ctx* c, int64_t* n, int64_t* m, int64_t* nnz, int
     *m = (int64_t)shard_rows(c);
     *nnz = (int64_t)shard_nnz(c);
     *unsharded = c->ib == 0 && c->ie == c->N;
+    return MH_OK;
+}
+// The whole NLP's m and nnz and this shard's nonzero range (mh_nlp_info).
+int mh_internal_shard(const mh_ctx* c, int64_t* m_full, int64_t* nnz_full, int64_t* nnz_begin, int64_t* nnz_end) {
+    if (!c) return set_err(MH_ERR_INVALID, "null context");
+    mh_nlp_info info;
+    const int rc = mh_get_nlp_info(c, &info);
+    if (rc) return rc;
+    *m_full = info.m;
+    *nnz_full = info.nnz_jac_g;
+    *nnz_begin = info.nnz_begin;
+    *nnz_end = info.nnz_end;
     return MH_OK;
 }
 // eval_jac_g at a device iterate into a device buffer, enqueued on the

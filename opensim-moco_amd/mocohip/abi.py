@@ -300,6 +300,9 @@ MOCOHIP_KKT_SYMBOLS = {
     "mh_kkt_solve": (i32, [C.c_void_p, i32, P(f64), P(f64)]),
     "mh_kkt_jmul": (i32, [C.c_void_p, i32, P(f64), P(f64)]),
     "mh_kkt_jtmul": (i32, [C.c_void_p, i32, P(f64), P(f64)]),
+    "mh_kkt_assemble": (i32, [C.c_void_p]),
+    "mh_kkt_bind_values": (i32, [C.c_void_p, C.c_void_p]),
+    "mh_kkt_shard_range": (i32, [C.c_void_p, P(C.c_int64), P(C.c_int64)]),
 }
 
 

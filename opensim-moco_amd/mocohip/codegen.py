@@ -1221,19 +1221,32 @@ def generate(cm, struct_name: str, implicit: bool = False, prescribed: bool = Fa
                            "const double* __restrict__ in, double* __restrict__ out", body))
     parts.append(("combine", "const mh::DevModel& M, const double t, const double* __restrict__ in, "
                              "const TL& T, OUT out", comb))
+    # the same combine in two steps (core.hpp interval_body's split combine):
+    # its independent sums one at a time, then the rest from the sums
+    nsum, sums_body, consts, sum_flops = _emit_combine_sums(M, Lo, groups)
+    fin, fin_flops = _emit_combine_finish(M, Lo, groups, consts)
+    parts.append(("combine_sum", "const int q, const mh::DevModel& M, const double t, "
+                                 "const double* __restrict__ in, const TL& T", sums_body))
+    parts.append(("combine_finish", "const mh::DevModel& M, const double t, const double* __restrict__ in, "
+                                    "const TL& T, const SUMS& S, OUT out", fin))
+    info["nsum"] = nsum
+    info["combine_split_flops"] = (sum_flops, fin_flops)
 
     fns = []
     for name, args, lines in parts:
         tpl = ""
-        if name in ("group", "combine"):
+        if name in ("group", "combine", "combine_sum", "combine_finish"):
             # inputs through an accessor (loaded where used, not held in VGPRs)
             # combine: outputs through a writer (OUT: a pointer, or a strided
             # Y / LDS writer -- each output is stored as it is produced
             # instead of living in registers until the end)
-            tpl = "template <class IN> " if name == "group" else "template <class IN, class TL, class OUT> "
+            tpl = {"group": "template <class IN> ", "combine": "template <class IN, class TL, class OUT> ",
+                   "combine_sum": "template <class IN, class TL> ",
+                   "combine_finish": "template <class IN, class TL, class SUMS, class OUT> "}[name]
             args = args.replace("const double* __restrict__ in", "const IN& in")
         pre = ["    const double* __restrict__ K = M.pool;", "    (void)K;"]
-        fns.append(f"    {tpl}__device__ __forceinline__ static void {name}({args}) {{\n"
+        ret = "double" if name == "combine_sum" else "void"
+        fns.append(f"    {tpl}__device__ __forceinline__ static {ret} {name}({args}) {{\n"
                    + "\n".join(pre + lines) + "\n    }")
     lst = lambda v: "{" + ", ".join(str(x) for x in v) + "}"
     src = f"""struct {struct_name} {{
@@ -1255,6 +1268,8 @@ def generate(cm, struct_name: str, implicit: bool = False, prescribed: bool = Fa
     static constexpr unsigned char GROUP_TIME[NG] = {lst([int(gr.time) for gr in groups])};
     static constexpr double GROUP_FLOPS[NG] = {lst([float(gr.flops) for gr in groups])};
     static constexpr double COMBINE_FLOPS = {float(comb_flops)};
+    // the combine's independent sums (combine_sum / combine_finish)
+    static constexpr int NSUM = {nsum};
     // the model's constant pool (DevModel::pool, filled by fill())
     static constexpr int NPOOL = {max(1, len(_CTX.pool))};
 {chr(10).join(fns)}
@@ -1507,6 +1522,120 @@ def _emit_combine(M: ModelView, Lo: _Layout, groups: List[_Group]):
         R0, _, _, _, _, cb = _Emitter(M, Lo).kinematics(list(range(M.nb)), accel=False, vel=False)
         lam = coordinate_tree(M, cb, NQ)
         factor_columns(g, Hs, lam, sorted({k[0] for k in shares}))
+        xs = E.solve(lam, Hs, bvec)
+    for i in range(NQ):
+        g.raw(f"out[{i}] = {xs[i]};")
+    kcf = {}
+    for gi, gr in enumerate(groups[1:], start=1):
+        for f, (kind, zi) in enumerate(gr.fields):
+            if kind == "z":
+                g.raw(f"out[{NQ + zi}] = T({gi}, {f});")
+            elif kind == "r":
+                g.raw(f"out[{NQ + Lo.NZ + zi}] = T({gi}, {f});")
+            elif kind in ("kpos", "kvel", "kg", "kc2"):
+                kcf[(kind, zi)] = S(n=f"T({gi}, {f})")
+    if Lo.NK:
+        info = []
+        for i, K in enumerate(M.kcs):
+            F = M.funcs[K.func]
+            info.append((i, F.coord, K.dependent, kcf[("kpos", i)], kcf.get(("kvel", i)),
+                         kcf.get(("kg", i)), kcf.get(("kc2", i))))
+        udot = [E.inp[Lo.NS + Lo.NC + j] for j in range(NQ)] if Lo.implicit else xs
+        E.kc_outputs(info, udot)
+    return g.lines, sum(g.flops.values())
+
+
+def _tree(g: Gen, ts):
+    """The combine's fixed-order pairwise sum of a term list."""
+    if not ts:
+        return _c(0.0)
+    while len(ts) > 1:
+        ts = [g.add(ts[i], ts[i + 1]) if i + 1 < len(ts) else ts[i] for i in range(0, len(ts), 2)]
+    return ts[0]
+
+
+def _sum_terms(M: ModelView, Lo: _Layout, groups: List[_Group]):
+    """The combine's independent sums, in _emit_combine's order: sum j < NQ
+    is coordinate j's generalized force (the groups' tau fields in group
+    order, then the coordinate actuators' control x optimal force), sum NQ +
+    i the i-th root-chain mass-matrix entry (sorted keys) summed over the
+    mass-matrix parts.  Returns (number of sums, terms(q, g, E) -> the term
+    list of sum q built in Gen g, the share keys)."""
+    NQ = Lo.NQ
+    taus = [[] for _ in range(NQ)]
+    for gi, gr in enumerate(groups[1:], start=1):
+        for f, (kind, j) in enumerate(gr.fields):
+            if kind == "tau":
+                taus[j].append((gi, f))
+    acts = [[] for _ in range(NQ)]
+    for ia, a in enumerate(M.acts):
+        if a.kind == abi.MH_ACT_COORDINATE:
+            acts[a.target].append((ia, a.optimal_force))
+    shares: Dict = {}
+    if not Lo.implicit and groups[0].lam is None:
+        for gi, gr in enumerate(groups):
+            for f, (kind, k) in enumerate(gr.fields):
+                if kind == "HR":
+                    shares.setdefault(k, []).append((gi, f))
+    keys = sorted(shares)
+
+    def terms(q, g, E):
+        if q < NQ:
+            return ([S(n=f"T({gi}, {f})") for gi, f in taus[q]] +
+                    [g.mul(E.ctrl[ia], _c(of)) for ia, of in acts[q]])
+        return [S(n=f"T({gi}, {f})") for gi, f in shares[keys[q - NQ]]]
+    return NQ + len(keys), terms, keys
+
+
+def _emit_combine_sums(M: ModelView, Lo: _Layout, groups: List[_Group]):
+    """combine_sum(q): sum q of _sum_terms alone (the same tree, so the same
+    value bit for bit as inside combine()), so that a lane role's sums can
+    be spread over the threads of a workgroup.  Returns (NSUM, switch body,
+    per sum its constant value when it has no terms, else None)."""
+    nsum, terms_of, _ = _sum_terms(M, Lo, groups)
+    body = ["        switch (q) {"]
+    consts = []
+    flops = 0
+    for q in range(nsum):
+        E = _Emitter(M, Lo)
+        v = _tree(E.g, terms_of(q, E.g, E))
+        consts.append(v if v.is_k() else None)
+        flops += sum(E.g.flops.values())
+        body.append(f"        case {q}: {{")
+        body.extend("    " + l for l in E.g.lines)
+        body.append(f"            return {v};")
+        body.append("        }")
+    body += ["        default: return 0.0;", "        }"]
+    return nsum, body, consts, flops
+
+
+def _emit_combine_finish(M: ModelView, Lo: _Layout, groups: List[_Group], consts):
+    """combine_finish(): _emit_combine's arithmetic after the sums, which it
+    reads through the accessor S (S(q) = combine_sum(q) of the same lane
+    role; a sum without terms stays the literal it folds to)."""
+    NQ = Lo.NQ
+    nsum, _, keys = _sum_terms(M, Lo, groups)
+    E = _Emitter(M, Lo)
+    g = E.g
+    vals = [consts[q] if consts[q] is not None else S(n=f"S({q})") for q in range(nsum)]
+    bvec = vals[:NQ]
+    if Lo.implicit:
+        xs = [g.neg(b) for b in bvec]
+    elif groups[0].lam is not None:
+        fkeys = [k for _, k in groups[0].fields]
+        Hs = {k: S(n=f"T.h({f})") for f, k in enumerate(fkeys)}
+        xs = E.solve(groups[0].lam, Hs, bvec)
+    else:
+        Hs = {}
+        for gi, gr in enumerate(groups):
+            for f, (kind, k) in enumerate(gr.fields):
+                if kind == "H" and gi > 0:
+                    Hs[k] = S(n=f"T({gi}, {f})")
+        for i, k in enumerate(keys):
+            Hs[k] = vals[NQ + i]
+        R0, _, _, _, _, cb = _Emitter(M, Lo).kinematics(list(range(M.nb)), accel=False, vel=False)
+        lam = coordinate_tree(M, cb, NQ)
+        factor_columns(g, Hs, lam, sorted({k[0] for k in keys}))
         xs = E.solve(lam, Hs, bvec)
     for i in range(NQ):
         g.raw(f"out[{i}] = {xs[i]};")

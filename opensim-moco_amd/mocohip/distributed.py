@@ -226,3 +226,192 @@ class HostGather:
             pass
         if unlink and os.path.exists(self.path):
             os.unlink(self.path)
+
+
+# ---------------------------------------------------------------------------
+# One solve spanning several GPUs: the optimizer on rank 0, the evaluation
+# sharded by mesh interval.
+# ---------------------------------------------------------------------------
+OP_STOP, OP_F, OP_GRAD, OP_G, OP_JAC, OP_JAC_DEV = range(6)
+
+
+class ShardedNLP:
+    """ONE NLP whose mesh intervals are sharded over the ranks of a
+    torch.distributed group, seen from rank 0 as the whole NLP -- the
+    interface mocohip.ipm / mocohip.nlpsolve drive (n, m, nnz, bounds,
+    jac_structure, eval_f / eval_grad_f / eval_g / eval_jac_g, device_kkt).
+
+    ``shard``: this rank's shard context (HipNLP, or OracleNLP on the CPU),
+    created with mh_options interval_begin / interval_end = interval_shard().
+    Rank 0 runs the optimizer through this object; every other rank calls
+    ``serve()``, which answers rank 0's requests until ``close()``.  Per
+    request rank 0 broadcasts an op code and the iterate x (the one
+    collective every evaluation needs); then
+      f, grad f   each rank's partial (mh_eval_f_partial / _grad_f_partial),
+                  summed onto rank 0 by a reduce;
+      g, J        each rank's contiguous slice (CasOCTranscription.h:
+                  219-313: rows and nonzeros are contiguous per interval)
+                  sent to rank 0 point to point;
+      J on the device (device_kkt; the optimizer's Newton systems factored
+                  on rank 0's GPU, include/mocohip_kkt.h): rank 0's own slice
+                  is written by its kernels straight into the KKT module's
+                  Jacobian buffer, the other ranks' slices are received into
+                  their offsets of that buffer -- over RCCL / xGMI GPU to GPU
+                  (``transport="device"``, backend nccl) or staged through
+                  host memory (``transport="host"``, backend gloo) -- and the
+                  module then gathers its blocks from the whole buffer.
+    g and J reach rank 0 bit-identical to an unsharded evaluation; f and
+    grad f are sums of partials (another order of the same terms)."""
+
+    def __init__(self, shard, dist, transport: str = "host", device=None):
+        if transport not in ("host", "device"):
+            raise ValueError("transport must be 'host' or 'device'")
+        self.shard, self.dist, self.transport = shard, dist, transport
+        self.rank, self.world = dist.get_rank(), dist.get_world_size()
+        self.n, self.m, self.nnz = int(shard.n), int(shard.m), int(shard.nnz)
+        import torch
+        self.torch = torch
+        self.device = torch.device("cuda", int(device)) if transport == "device" else torch.device("cpu")
+        mine = torch.tensor([shard.row_begin, shard.row_end, shard.nnz_begin, shard.nnz_end],
+                            dtype=torch.int64, device=self.device)
+        got = [torch.zeros_like(mine) for _ in range(self.world)]
+        dist.all_gather(got, mine)
+        self.ranges = [tuple(int(v) for v in t.cpu()) for t in got]
+        # the whole NLP's view (rank 0 holds every row and nonzero)
+        self.row_begin, self.row_end, self.nnz_begin, self.nnz_end = 0, self.m, 0, self.nnz
+        self._dkkt = None
+        self._vbuf = None      # this rank's device slice buffer (transport "device")
+        self.closed = False
+
+    def __getattr__(self, name):
+        # problem attributes (opts, G, NS, NC, rep, NSL, NEP, tail_rows, ...)
+        # are the shard context's: the same problem, whole
+        if name.startswith("__") or name == "shard":
+            raise AttributeError(name)
+        return getattr(self.shard, name)
+
+    # -- the protocol ----------------------------------------------------------
+    def _tensor(self, a, dtype=None):
+        t = self.torch
+        return t.as_tensor(np.ascontiguousarray(a), dtype=dtype or t.float64).to(self.device)
+
+    def _request(self, op: int, x):
+        """Rank 0: op code and iterate to every rank."""
+        t = self.torch
+        self.dist.broadcast(t.tensor([op], dtype=t.int64, device=self.device), 0)
+        if op != OP_STOP:
+            xt = self._tensor(x)
+            self.dist.broadcast(xt, 0)
+            return xt
+        return None
+
+    def _receive(self):
+        """Ranks > 0: the next (op, x as a tensor on self.device)."""
+        t = self.torch
+        hdr = t.zeros(1, dtype=t.int64, device=self.device)
+        self.dist.broadcast(hdr, 0)
+        op = int(hdr.item())
+        if op == OP_STOP:
+            return op, None
+        xt = t.zeros(self.n, dtype=t.float64, device=self.device)
+        self.dist.broadcast(xt, 0)
+        return op, xt
+
+    def _sum_to_root(self, a) -> np.ndarray:
+        t = self._tensor(a)
+        self.dist.reduce(t, 0, op=self.dist.ReduceOp.SUM)
+        return t.cpu().numpy()
+
+    def _gather_slices(self, own, which: int, out):
+        """Rank 0: its own slice into ``out`` (a float64 tensor of the whole
+        vector), the other ranks' slices received into their offsets."""
+        b0, e0 = self.ranges[0][which], self.ranges[0][which + 1]
+        out[b0:e0] = self._tensor(own) if not isinstance(own, self.torch.Tensor) else own
+        for r in range(1, self.world):
+            b, e = self.ranges[r][which], self.ranges[r][which + 1]
+            if e > b:
+                self.dist.recv(out[b:e], src=r)
+        return out
+
+    def _send_slice(self, v):
+        if len(v):
+            self.dist.send(v if isinstance(v, self.torch.Tensor) else self._tensor(v), dst=0)
+
+    # -- rank 0: the NLP the optimizer sees -------------------------------------
+    def eval_f(self, x, new_x=True):
+        self._request(OP_F, x)
+        return float(self._sum_to_root([self.shard.eval_f_partial(x)])[0])
+
+    def eval_grad_f(self, x, new_x=True):
+        self._request(OP_GRAD, x)
+        return self._sum_to_root(self.shard.eval_grad_f_partial(x))
+
+    def eval_g(self, x, new_x=True):
+        self._request(OP_G, x)
+        out = self.torch.zeros(self.m, dtype=self.torch.float64, device=self.device)
+        return self._gather_slices(self.shard.eval_g(x), 0, out).cpu().numpy()
+
+    def eval_jac_g(self, x, new_x=True):
+        self._request(OP_JAC, x)
+        out = self.torch.zeros(self.nnz, dtype=self.torch.float64, device=self.device)
+        return self._gather_slices(self.shard.eval_jac_g(x), 2, out).cpu().numpy()
+
+    def device_kkt(self, warm: bool = False):
+        """The device KKT module on rank 0's GPU over the WHOLE Jacobian
+        (mocohip.kkt.ShardedDeviceKKT).  ValueError where the shards are not
+        device contexts (the optimizer then takes its host linear algebra)."""
+        if not hasattr(self.shard, "eval_jac_g_device"):
+            raise ValueError("device_kkt needs HipNLP shards")
+        if self._dkkt is None:
+            from .kkt import ShardedDeviceKKT
+            dk = ShardedDeviceKKT(self)
+            if warm:
+                dk.warm(self.initial_guess_from_bounds())
+            self._dkkt = dk
+        return self._dkkt
+
+    def close(self):
+        """Rank 0: release the other ranks from serve()."""
+        if self.rank == 0 and not self.closed:
+            self._request(OP_STOP, None)
+        self.closed = True
+        if self._dkkt is not None:
+            self._dkkt.close()
+            self._dkkt = None
+
+    # -- ranks > 0 -----------------------------------------------------------------
+    def serve(self) -> int:
+        """Answer rank 0's requests until it closes; returns the number of
+        requests served."""
+        t = self.torch
+        served = 0
+        while True:
+            op, xt = self._receive()
+            if op == OP_STOP:
+                self.closed = True
+                return served
+            served += 1
+            if op == OP_JAC_DEV and self.transport == "device":
+                # the slice stays on the GPU: evaluated into a device buffer
+                # on a dedicated stream, sent GPU to GPU from that stream
+                if self._vbuf is None:
+                    self._vbuf = t.zeros(max(1, self.shard.nnz_end - self.shard.nnz_begin),
+                                         dtype=t.float64, device=self.device)
+                    self._stream = t.cuda.Stream(device=self.device)
+                    self.shard.set_stream(self._stream.cuda_stream)
+                self._stream.wait_stream(t.cuda.current_stream(self.device))   # x has arrived
+                with t.cuda.stream(self._stream):
+                    self.shard.eval_jac_g_device(xt.data_ptr(), self._vbuf.data_ptr())
+                    self._send_slice(self._vbuf[:self.shard.nnz_end - self.shard.nnz_begin])
+                continue
+            x = xt.cpu().numpy()
+            if op == OP_F:
+                self._sum_to_root([self.shard.eval_f_partial(x)])
+            elif op == OP_GRAD:
+                self._sum_to_root(self.shard.eval_grad_f_partial(x))
+            elif op == OP_G:
+                self._send_slice(self.shard.eval_g(x))
+            elif op in (OP_JAC, OP_JAC_DEV):
+                self._send_slice(self.shard.eval_jac_g(x))
+            else:
+                raise RuntimeError(f"unknown request {op}")

@@ -338,3 +338,59 @@ class DeviceKKT:
             self.close()
         except Exception:
             pass
+
+
+class ShardedDeviceKKT(DeviceKKT):
+    """DeviceKKT on rank 0 of a mocohip.distributed.ShardedNLP: ONE NLP
+    sharded by mesh interval over the ranks, its Newton systems factored on
+    rank 0's GPU over the WHOLE Jacobian (the slices
+    reassembled on the GPU that feeds the optimizer).  The module is created
+    over rank 0's shard context with the whole NLP's block map; its Jacobian
+    buffer is a torch tensor bound to it (mh_kkt_bind_values), so that the
+    other ranks' slices can be received straight into their offsets -- RCCL
+    point to point over xGMI (transport "device") or through host memory
+    (transport "host", gloo) -- and mh_kkt_assemble then gathers the blocks.
+    Everything else (factor, solve, products with J) is the module's own
+    work on rank 0's GPU, as for an unsharded context."""
+
+    def __init__(self, snlp):
+        torch = snlp.torch
+        self.snlp = snlp
+        shard = snlp.shard
+        dev = snlp.device if snlp.transport == "device" else torch.device("cuda", torch.cuda.current_device())
+        self.dev = dev
+        # the shard context's kernels, the received slices and the module's
+        # kernels ordered on one dedicated stream (not torch's default one,
+        # handle 0, which mh_set_stream reads as the context's own stream)
+        self.stream = torch.cuda.Stream(device=dev)
+        shard.set_stream(self.stream.cuda_stream)
+        super().__init__(shard, block_map(snlp))
+        self.vals = torch.zeros(max(1, self.bm.nnz), dtype=torch.float64, device=dev)
+        self._check(self.lib.mh_kkt_bind_values(self.h, C.c_void_p(self.vals.data_ptr())))
+        b, e = C.c_int64(), C.c_int64()
+        self._check(self.lib.mh_kkt_shard_range(self.h, C.byref(b), C.byref(e)))
+        assert (b.value, e.value) == snlp.ranges[0][2:4]
+
+    def eval_jacobian(self, x):
+        """J(x) of the whole NLP in rank 0's HBM: the request to every rank,
+        rank 0's slice by its own kernels, the others' slices received into
+        their offsets of the bound buffer, then the blocks gathered."""
+        from .distributed import OP_JAC_DEV
+        snlp, torch = self.snlp, self.snlp.torch
+        x = np.ascontiguousarray(x, float)
+        t0 = time.perf_counter()
+        snlp._request(OP_JAC_DEV, x)
+        with torch.cuda.stream(self.stream):
+            self._check(self.lib.mh_kkt_eval_jacobian(self.h, _dp(x)))
+            for r in range(1, snlp.world):
+                b, e = snlp.ranges[r][2], snlp.ranges[r][3]
+                if e <= b:
+                    continue
+                if snlp.transport == "device":
+                    snlp.dist.recv(self.vals[b:e], src=r)
+                else:
+                    buf = torch.empty(e - b, dtype=torch.float64)
+                    snlp.dist.recv(buf, src=r)
+                    self.vals[b:e].copy_(buf)
+            self._check(self.lib.mh_kkt_assemble(self.h))
+        self._tick("eval_jacobian", t0)

@@ -123,3 +123,75 @@ def test_shard_contexts_reassemble_on_the_ipopt_host(case, N, world):
         p.join(120)
         assert p.exitcode == 0
     assert list(out) == [1] * world
+
+
+# ---------------------------------------------------------------------------
+# One solve spanning the ranks (mocohip.distributed.ShardedNLP): the
+# optimizer on rank 0, the evaluation sharded, g / J reassembled on rank 0.
+# ---------------------------------------------------------------------------
+SOLVE_CASES = {"pendulum": lambda N: configs.double_pendulum(N),
+               "gait_inverse": lambda N: configs.gait10dof18musc_inverse(N, sparsity="none"),
+               "gait_track": lambda N: configs.gait10dof18musc_track(N, muscles=True)}
+
+
+def _ipm_opts(iters):
+    from mocohip.ipm import IpmOptions
+    o = IpmOptions.from_ipopt({"tol": 1e-8, "constr_viol_tol": 1e-8, "max_iter": iters})
+    o.linear_solver = "host"
+    return o
+
+
+def _sharded_worker(rank, world, port, case, N, iters, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mocohip.distributed import ShardedNLP
+        from mocohip.ipm import solve_ipm
+        st = SOLVE_CASES[case](N)
+        rep = st.problem.create_rep()
+        ib, ie = interval_shard(N, rank, world)
+        snlp = ShardedNLP(OracleNLP(rep, st.solver.options(ib, ie), threads=1), dist)
+        if rank > 0:
+            snlp.serve()
+            out[rank] = 1
+            return
+        full = OracleNLP(rep, st.solver.options(), threads=1)
+        ok = (snlp.n, snlp.m, snlp.nnz) == (full.n, full.m, full.nnz)
+        x = full.random_iterate(np.random.default_rng(5).uniform(-1, 1, full.n))
+        # g and J reassembled on rank 0: bit for bit the unsharded evaluation
+        ok = ok and np.array_equal(snlp.eval_g(x), full.eval_g(x))
+        ok = ok and np.array_equal(snlp.eval_jac_g(x), full.eval_jac_g(x))
+        f0 = full.eval_f(x)
+        ok = ok and abs(snlp.eval_f(x) - f0) <= 1e-12 * max(1.0, abs(f0))
+        # the optimizer driven through the shards takes the unsharded run's
+        # Newton steps: the same iterates (to the rounding of the objective's
+        # partial sums) after `iters` iterations
+        x0 = st.solver.starting_point(full, None)
+        a = solve_ipm(snlp, x0, _ipm_opts(iters))
+        b = solve_ipm(full, x0, _ipm_opts(iters))
+        ok = ok and a.iterations == b.iterations
+        ok = ok and float(np.abs(a.x - b.x).max()) <= 1e-9 * max(1.0, float(np.abs(b.x).max()))
+        out[0] = int(bool(ok))
+        snlp.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case,N,world,iters", [("pendulum", 8, 2, 1), ("pendulum", 9, 3, 4),
+                                                ("gait_inverse", 4, 2, 2), ("gait_track", 4, 2, 1)])
+def test_sharded_solve_takes_the_unsharded_steps(case, N, world, iters):
+    """ShardedNLP (world 2 / 3 over gloo, oracle shard contexts): rank 0's
+    reassembled g and J equal the unsharded evaluation bit for bit, and the
+    interior-point method driven through the shards takes the same Newton
+    steps as on the unsharded NLP."""
+    ctx = mp.get_context("spawn")
+    out = ctx.Array("i", [0] * world)
+    port = _free_port()
+    procs = [ctx.Process(target=_sharded_worker, args=(r, world, port, case, N, iters, out))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(300)
+        assert p.exitcode == 0
+    assert list(out) == [1] * world
