@@ -25,19 +25,24 @@ kernels are enqueued and the timed region ends with torch.cuda.synchronize()
                   cores, on a bounded sample of the same workload.
 
 --gpus N > 1 (one process per GPU, torch.distributed.run):
-  --multi replicas (default): every rank evaluates its own NLP (independent
-      trials, the configs[4] batch layout), no collective on the data path
-      -> "scaling": "weak"; the mesh layout's measurements ride along under
-      "mesh" (below).
-  --multi mesh: the north star's layout -- ONE NLP for one host IPOPT, its
-      mesh intervals sharded over the ranks; value = the host-inclusive rate:
-      x from page-locked host memory over each rank's PCIe link, the shard's
-      evaluation, each rank's DMA of its contiguous g / Jacobian slice into
-      its offset of one page-locked host buffer shared by the node's ranks
-      (mocohip.distributed.HostGather), a barrier; "scaling": "strong".
+  --multi mesh (default): the north star's layout -- ONE NLP for one host
+      optimizer, its mesh intervals sharded over the ranks; value = the
+      host-inclusive rate: x from page-locked host memory over each rank's
+      PCIe link, the shard's evaluation, each rank's DMA of its contiguous g /
+      Jacobian slice into its offset of one page-locked host buffer shared by
+      the node's ranks (mocohip.distributed.HostGather), a barrier;
+      "scaling": "strong", with "one_gpu_host_inclusive" (rank 0 alone, the
+      whole NLP, the same round trip) and their ratio "strong_scaling".
       Beside it, labelled: "device_resident" (x already in HBM, results left
-      there -- an upper bound with no data movement) and "x_broadcast" (+ an
-      RCCL broadcast of x per call).
+      there -- an upper bound with no data movement), "x_broadcast" (+ an
+      RCCL broadcast of x per call), "replicas" (every rank its own NLP, weak
+      scaling), "inverse_solve_sweep" (configs[4]: 64 MocoInverse solves
+      distributed over the ranks) and "sharded_solve" (configs[2] solved by
+      one optimizer over all ranks, Jacobian slices to rank 0's HBM over
+      RCCL).
+  --multi replicas: every rank evaluates its own NLP (independent trials,
+      the configs[4] batch layout), no collective on the data path ->
+      "scaling": "weak"; the mesh measurements ride along under "mesh".
 
 Prints one JSON line on rank 0.
 """
@@ -84,7 +89,7 @@ def parse():
                     help="every C-ABI call synchronizes before returning (default: asynchronous "
                          "device calls, synchronized at the end of the timed region)")
     ap.add_argument("--multi", choices=["replicas", "mesh"], default=None,
-                    help="default: mesh when WORLD_SIZE > 1")
+                    help="default: mesh when WORLD_SIZE > 1 (strong scaling of one NLP)")
     ap.add_argument("--single-mode", action="store_true",
                     help="measure only the headline (no secondary lines): for profiler runs, so "
                          "that every launch of a kernel has the same shape")
@@ -96,6 +101,11 @@ def parse():
     ap.add_argument("--solve-batch", type=int, default=8,
                     help="configs[4] MocoInverse solves run together on this GPU (0: skip)")
     ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--sweep", type=int, default=64,
+                    help="--multi mesh: configs[4]'s MocoInverse solves distributed over the ranks (0: skip)")
+    ap.add_argument("--solve-intervals", type=int, default=200,
+                    help="--multi mesh, N > 1: mesh intervals of the configs[2] solve sharded over the ranks "
+                         "(0: skip)")
     ap.add_argument("--batch-only", action="store_true",
                     help="print only the batch line (A/B of queue / launch settings)")
     return ap.parse_args()
@@ -308,7 +318,14 @@ def roofline(cx, nlp, steps, args, mode):
                  "in_call_stage_ms": [round(ev_dae_ms, 5), round(ev_tr_ms, 5)]})
     if rec["g"]:
         Gt = np.array(rec["g"])
+        # [whole call, DAE stage, transcription stage, k_groups] as recorded by
+        # events INSIDE each eval_g call (host launch latency included)
         roof["eval_g_stage_ms"] = [round(float(np.median(Gt[:, i])), 5) for i in range(4)]
+        # eval_g's two kernels timed the way the roofline's are (in call
+        # order, an event after each; the kernel-trace figures)
+        gd_ms, gi_ms = nlp.time_stages(steps[2][0], kind=0, reps=max(50, args.steps))
+        roof["eval_g_kernels_ms"] = {"k_groups": round(gd_ms, 5), "k_interval_256": round(gi_ms, 5),
+                                     "sum": round(gd_ms + gi_ms, 5)}
     return roof
 
 
@@ -590,6 +607,109 @@ def mesh_measure(cx, args):
     return out
 
 
+def one_gpu_host_inclusive(cx, args, build):
+    """The strong-scaling reference inside a multi-rank run: rank 0 alone
+    evaluates the WHOLE NLP host-inclusively (x in, g and J out over its
+    PCIe link every call) while the other ranks wait; None on other ranks."""
+    torch = cx.torch
+    out = None
+    if cx.rank == 0:
+        nlp = make_nlp(cx, build(), blocking=False)
+        x = track_iterate(nlp, 0)
+        xh = torch.from_numpy(np.ascontiguousarray(x)).pin_memory()
+        gh = torch.empty(nlp.m, dtype=torch.float64).pin_memory()
+        vh = torch.empty(nlp.nnz, dtype=torch.float64).pin_memory()
+        xp, gp, vp = (t.numpy().ctypes.data for t in (xh, gh, vh))
+        import ctypes as C
+
+        def step():
+            nlp.lib.mh_eval_g(nlp.ctx, C.c_void_p(xp), 1, C.c_void_p(gp))
+            nlp.lib.mh_eval_jac_g(nlp.ctx, C.c_void_p(xp), 0, C.c_void_p(vp))
+        for _ in range(max(10, args.warmup // 10)):
+            step()
+        k = max(50, args.steps // 4)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(k):
+            step()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        out = {"value": round(k / el, 3), "unit": "calls/s", "steps": k, "ms_per_step": round(1e3 * el / k, 5),
+               "note": "rank 0 alone, the whole NLP, host-inclusive (the same round trip as the headline "
+                       "on one GPU): the denominator of strong_scaling"}
+        nlp.close()
+    if cx.world > 1:
+        cx.dist.barrier()
+    return out
+
+
+def sweep_distributed(cx, args):
+    """configs[4] as BASELINE names it: 64 MocoInverse solves over the
+    node's ranks -- rank r solves every W-th subject on its own GPU
+    (mocohip.batchsolve.solve_sweep, rounds of <= 8 solver processes per
+    GPU), no collective on the data path; the counts and the wall clock
+    (max over ranks) reduced at the end."""
+    from mocohip import batchsolve
+    torch, dist = cx.torch, cx.dist
+    if cx.world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    r = batchsolve.solve_sweep(args.sweep, 125, rank=cx.rank, world=cx.world, device=cx.local)
+    el = time.perf_counter() - t0
+    t = torch.tensor([r["solves"], r["succeeded"]], dtype=torch.float64, device=cx.dev)
+    w = torch.tensor([el, r["wall_clock_s"]], dtype=torch.float64, device=cx.dev)
+    if cx.world > 1:
+        dist.all_reduce(t)
+        dist.all_reduce(w, op=dist.ReduceOp.MAX)
+    solves, ok = int(t[0].item()), int(t[1].item())
+    wall = float(w[1].item())
+    return {"solves": solves, "succeeded": ok, "ranks": cx.world, "solves_per_rank": r["solves"],
+            "rounds_per_rank": r["rounds"], "wall_clock_s": round(wall, 3),
+            "wall_clock_incl_setup_s": round(float(w[0].item()), 3),
+            "solves_per_minute": round(60.0 * solves / wall, 2) if wall > 0 else None,
+            "mean_iterations_rank0": r["mean_iterations"],
+            "workload": "configs[4]: 64 MocoInverse gait10dof18musc N=125 solves (scaled subjects), "
+                        "rank r solves subjects r, r+W, ... on its own GPU, <= 8 solver processes at once"}
+
+
+def sharded_solve(cx, args):
+    """configs[2] solved by ONE optimizer whose NLP spans the ranks
+    (mocohip.distributed.ShardedNLP): rank 0 runs the interior-point method
+    with its Newton systems on its GPU over the whole Jacobian
+    (ShardedDeviceKKT), every rank evaluates its mesh intervals, the other
+    ranks' Jacobian slices arrive in rank 0's HBM over RCCL (send / recv,
+    xGMI).  Beside it the same solve on rank 0's GPU alone."""
+    from mocohip import configs
+    from mocohip.distributed import ShardedNLP, interval_shard
+    from mocohip.solver import HipNLP
+    N = args.solve_intervals
+    st = configs.gait10dof18musc_track(N, muscles=True)
+    st.solver.device = cx.local
+    rep = st.problem.create_rep()
+    ib, ie = interval_shard(N, cx.rank, cx.world)
+    snlp = ShardedNLP(HipNLP(rep, st.solver.options(ib, ie)), cx.dist, transport="device", device=cx.local)
+    out = None
+    if cx.rank == 0:
+        sol = st.solve(nlp=snlp, linear_solver="device")
+        r = sol.stats
+        snlp.close()
+        full = HipNLP(rep, st.solver.options())
+        ref = st.solve(nlp=full, linear_solver="device").stats
+        full.close()
+        out = {"success": bool(r.success), "wall_clock_s": round(r.duration, 3), "iterations": r.iterations,
+               "objective": r.objective, "ranks": cx.world,
+               "seconds_in_kkt": round(r.timings.get("linear_algebra_s", 0.0), 3),
+               "one_gpu": {"success": bool(ref.success), "wall_clock_s": round(ref.duration, 3),
+                           "iterations": ref.iterations, "objective": ref.objective},
+               "workload": f"configs[2] MocoTrack gait10dof18musc, 18 DGF muscles, N={N}, one solve whose "
+                           f"mesh intervals are sharded over {cx.world} GPUs (Jacobian slices to rank 0's "
+                           "HBM over RCCL, Newton systems on rank 0's GPU)"}
+    else:
+        snlp.serve()
+    cx.dist.barrier()
+    return out
+
+
 def mesh_main(cx, args):
     """--multi mesh: the headline is the host-inclusive rate of one NLP
     sharded over the ranks (mesh_measure); replicas beside it."""
@@ -602,6 +722,13 @@ def mesh_main(cx, args):
     rsep, rfused, _ = device_steps(cx, rnlp, track_iterate(rnlp, cx.rank))
     kr, elr = measure(cx, rfused if args.mode == "fused" else rsep, args)
     rnlp.close()
+    one = sweep = solve = None
+    if not args.single_mode:
+        one = one_gpu_host_inclusive(cx, args, build)
+        if args.sweep > 0:
+            sweep = sweep_distributed(cx, args)
+        if cx.world > 1 and args.solve_intervals > 0:
+            solve = sharded_solve(cx, args)
     if cx.rank == 0:
         wl = ("Rajagopal 80-muscle gait NLP (configs[3])" if args.config == "rajagopal80"
               else "MocoTrack gait10dof18musc DGF rigid tendon (configs[2])")
@@ -618,6 +745,13 @@ def mesh_main(cx, args):
                 "reassembly_bit_exact": m["reassembly_bit_exact"],
                 "replicas": {"value": round(kr * cx.world / elr, 3), "unit": "calls/s", "steps": kr,
                              "scaling": "weak", "note": "every rank its own whole NLP, no collective"}}
+        if one is not None:
+            line["one_gpu_host_inclusive"] = one
+            line["strong_scaling"] = round(m["value"] / one["value"], 3)
+        if sweep is not None:
+            line["inverse_solve_sweep"] = sweep
+        if solve is not None:
+            line["sharded_solve"] = solve
         print(json.dumps(line), flush=True)
 
 
@@ -625,10 +759,12 @@ def main():
     args = parse()
     cx = Ctx(args)
     if args.multi is None:
-        # independent NLPs per GPU (the configs[4] layout; weak scaling) is
-        # the default at every N; the mesh layout's strong scaling of one NLP
-        # is reported beside it (its host-inclusive rate) when N > 1
-        args.multi = "replicas"
+        # N > 1: the north star's layout -- ONE NLP sharded by mesh interval
+        # for one host optimizer, strong scaling, the host-inclusive rate as
+        # the headline (mesh_main); the replicas layout (independent NLPs per
+        # GPU, weak scaling) rides along in its line.  N = 1: the single-GPU
+        # headline below.
+        args.multi = "mesh" if cx.world > 1 else "replicas"
     if args.multi == "mesh":
         mesh_main(cx, args)
         if cx.world > 1:

@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define MH_ABI_VERSION 6
+#define MH_ABI_VERSION 7
 
 enum mh_status {
     MH_OK = 0,
@@ -488,27 +488,26 @@ typedef struct mh_options {
      * contexts only. */
     int32_t jacobian_mode;
     int32_t reserved_jm;
-    /* (ABI v6) How detection decides a coupling (mh_sparsity_rule).
-     * The plugin surface (MocoHipSolver optim_sparsity_detection_rule, the
-     * C++ builder's MocoHipSolver) defaults to ANY_CHANGE, the reference's
-     * rule; a zero-initialized mh_options means ROBUST.
-     * ROBUST (0): output k depends on input j iff its change under
+    /* (ABI v6; v7: the values swapped) How detection decides a coupling
+     * (mh_sparsity_rule).  ANY_CHANGE (0, the default of a zero-initialized
+     * mh_options and of every surface above it): the reference's rule
+     * (CasOCFunction.cpp:44-61: any nonzero change or NaN), under which
+     * couplings that cancel to rounding level (a muscle on a coordinate it
+     * does not cross) are detected or not depending on the order of the
+     * floating-point operations: implementation-dependent.
+     * ROBUST (1): output k depends on input j iff its change under
      * the +1e-5 perturbation is NaN or exceeds 1e-12 * the callback's
      * magnitude at the detection iterate (max(1, max over its outputs of
      * |output|)) -- a true dependency changes an output by ~1e-5 *
      * d(output) / d(input), the rounding noise of a coupling that cancels
      * stays within ~64 eps of the callback's magnitude (1.4e-14), so the
      * pattern is a property of the model: the same on the device and in any
-     * other implementation.  ANY_CHANGE (1): the reference's rule
-     * (CasOCFunction.cpp:44-61: any nonzero change or NaN), under which
-     * couplings that cancel to rounding level (a muscle on a coordinate it
-     * does not cross) are detected or not depending on the order of the
-     * floating-point operations: implementation-dependent. */
+     * other implementation. */
     int32_t sparsity_rule;
     int32_t reserved_sr;
 } mh_options;
 
-enum mh_sparsity_rule { MH_SPARSITY_RULE_ROBUST = 0, MH_SPARSITY_RULE_ANY_CHANGE = 1 };
+enum mh_sparsity_rule { MH_SPARSITY_RULE_ANY_CHANGE = 0, MH_SPARSITY_RULE_ROBUST = 1 };
 /* ROBUST: the change, relative to the callback's magnitude, below which a
  * detection probe counts as rounding noise. */
 #define MH_SPARSITY_ROBUST_TOL 1e-12
@@ -573,6 +572,12 @@ int mh_eval_grad_f(mh_ctx* ctx, const double* x, int new_x, double* grad_f);
  * mh_eval_f, one all-reduce of a double.  On an unsharded context it equals
  * mh_eval_f bit for bit. */
 int mh_eval_f_partial(mh_ctx* ctx, const double* x, double* f);
+/* The objective's terms at x, one per goal (mh_problem.goals order: the
+ * weighted value each contributes to mh_eval_f; the solution's objective
+ * breakdown, MocoSolver::setSolutionStats / MocoCasADiSolver.cpp:395-402).
+ * *nterms: in, the doubles terms holds; out, the number of goals (also when
+ * too small: MH_ERR_INVALID).  Whole-NLP contexts; synchronous. */
+int mh_eval_objective_terms(mh_ctx* ctx, const double* x, double* terms, int32_t* nterms);
 /* Its gradient (n doubles): nonzero at t0 / tf and the shard's grid points
  * (the boundary point a shard shares with its neighbour carries each side's
  * share); the sum over the shards is mh_eval_grad_f (an all-reduce). */

@@ -35,6 +35,7 @@
 #include <OpenSim/Moco/MocoGoal/MocoGoal.h>
 #include <OpenSim/Moco/MocoControlBoundConstraint.h>
 #include <OpenSim/Moco/MocoProblemRep.h>
+#include <OpenSim/Moco/MocoUtilities.h>
 #include <OpenSim/Simulation/Model/ExternalForce.h>
 #include <OpenSim/Simulation/Model/Model.h>
 #include <OpenSim/Simulation/Model/PhysicalOffsetFrame.h>
@@ -49,6 +50,7 @@
 #include <OpenSim/Simulation/Model/MovingPathPoint.h>
 
 #include "mh_ipopt_tnlp.hpp"
+#include "mh_trajectory.hpp"
 
 using namespace OpenSim;
 
@@ -563,62 +565,99 @@ const MocoTrajectory& MocoHipSolver::getGuess() const {
 
 namespace {
 
-// The grid times of the NLP at iterate x (CasOCTranscription.cpp:126-127:
-// times = (tf - t0) grid + t0; mesh uniform, HS midpoints in between).
-std::vector<double> gridTimes(const mh_options& o, double t0, double tf) {
-    const int N = o.num_mesh_intervals;
-    const bool hs = o.transcription == MH_HERMITE_SIMPSON;
-    std::vector<double> t;
-    for (int k = 0; k < (hs ? 2 * N + 1 : N + 1); ++k) {
-        const double g = hs ? ((k % 2 == 0) ? (k / 2) / (double)N
-                                            : 0.5 * ((k / 2) / (double)N + (k / 2 + 1) / (double)N))
-                            : k / (double)N;
-        t.push_back((tf - t0) * g + t0);
-    }
-    return t;
+// The trajectory conversions of the reference (MocoCasOCProblem.h:70-187:
+// convertToCasOCIterate / convertToMocoTrajectory) over every variable block
+// by name -- states, controls, multipliers, derivatives, slacks -- shared
+// with the command-line path (csrc/host/mh_trajectory.hpp; mh_build
+// --solution writes the same MocoSolution as a .sto, tests/
+// test_trajectory_cpp.py checks it against the Python conversion and the
+// reference's MocoInverse solution file).
+mhb::TrajectoryTable toTable(const MocoTrajectory& t) {
+    mhb::TrajectoryTable T;
+    const SimTK::Vector time = t.getTime();
+    for (int k = 0; k < time.size(); ++k) T.time.push_back(time[k]);
+    auto take = [&](const std::vector<std::string>& names, const SimTK::Matrix& M, std::vector<std::string>& tn,
+                    std::vector<double>& td) {
+        tn = names;
+        td.assign((size_t)M.nrow() * M.ncol(), 0.0);
+        for (int k = 0; k < M.nrow(); ++k)
+            for (int j = 0; j < M.ncol(); ++j) td[(size_t)k * M.ncol() + j] = M(k, j);
+    };
+    take(t.getStateNames(), t.getStatesTrajectory(), T.state_names, T.states);
+    take(t.getControlNames(), t.getControlsTrajectory(), T.control_names, T.controls);
+    take(t.getMultiplierNames(), t.getMultipliersTrajectory(), T.multiplier_names, T.multipliers);
+    take(t.getDerivativeNames(), t.getDerivativesTrajectory(), T.derivative_names, T.derivatives);
+    take(t.getSlackNames(), t.getSlacksTrajectory(), T.slack_names, T.slacks);
+    return T;
 }
 
-// x layout (CasOCIterate.h:27-44, include/mocohip.h): t0, tf, states NS x G
-// grid-major, controls NC x G, multipliers NM x G, slacks NSL x N,
-// derivatives NDV x G.  The guess path fills the states and controls (and
-// multipliers / derivatives when the guess carries them) of the grid from
-// the MocoTrajectory resampled at the grid times (CasOCTranscription.cpp:
-// 593-597 resamples the guess the same way).
-std::vector<double> toIterate(MocoTrajectory guess, const mhb::ProblemRep& hrep, const mh_options& o,
-        const mh_nlp_info& info) {
+// The guess resampled at the grid times (CasOCTranscription.cpp:593-597),
+// then every block it names into the iterate; unnamed blocks stay 0.
+std::vector<double> toIterate(MocoTrajectory guess, const mhb::ProblemRep& hrep, const mh_options& o) {
     const auto t = guess.getTime();
-    const double t0 = t[0], tf = t[t.size() - 1];
-    const auto times = gridTimes(o, t0, tf);
+    const auto times = mhb::grid_times(o, t[0], t[t.size() - 1]);
     guess.resample(SimTK::Vector((int)times.size(), times.data()));
-    const int G = (int)times.size(), NS = (int)info.num_states, NC = (int)info.num_controls;
-    std::vector<double> x((size_t)info.n, 0.0);
-    x[0] = t0;
-    x[1] = tf;
-    for (int s = 0; s < NS; ++s) {
-        const SimTK::Vector col = guess.getState(hrep.state_names[s]);
-        for (int k = 0; k < G; ++k) x[2 + (size_t)k * NS + s] = col[k];
-    }
-    for (int j = 0; j < NC; ++j) {
-        const SimTK::Vector col = guess.getControl(hrep.control_names[j]);
-        for (int k = 0; k < G; ++k) x[2 + (size_t)G * NS + (size_t)k * NC + j] = col[k];
-    }
-    return x;
+    return mhb::trajectory_to_iterate(toTable(guess), hrep, o);
 }
 
-// The solution iterate -> MocoSolution at the grid times (the reference's
-// convertToMocoTrajectory over CasOC's expandVariables).
-MocoSolution toSolution(const std::vector<double>& x, const mhb::ProblemRep& hrep, const mh_options& o,
-        const mh_nlp_info& info) {
-    const auto times = gridTimes(o, x[0], x[1]);
-    const int G = (int)times.size(), NS = (int)info.num_states, NC = (int)info.num_controls;
-    SimTK::Matrix S(G, NS), U(G, NC);
-    for (int k = 0; k < G; ++k) {
-        for (int s = 0; s < NS; ++s) S(k, s) = x[2 + (size_t)k * NS + s];
-        for (int j = 0; j < NC; ++j) U(k, j) = x[2 + (size_t)G * NS + (size_t)k * NC + j];
+// The solution iterate as a MocoSolution at the grid times, every block by
+// name; the slacks appended the reference's way (convertToMocoTrajectory:
+// the N interval values placed uniformly over [t0, tf] and interpolated
+// onto the grid).
+MocoSolution toSolution(const std::vector<double>& x, const mhb::ProblemRep& hrep, const mh_options& o) {
+    const mhb::TrajectoryTable T = mhb::iterate_to_trajectory(x, hrep, o);
+    const int G = (int)T.time.size();
+    auto matrix = [&](const std::vector<double>& d, size_t nv) {
+        SimTK::Matrix M(G, (int)nv);
+        for (int k = 0; k < G; ++k)
+            for (size_t j = 0; j < nv; ++j) M(k, (int)j) = d[(size_t)k * nv + j];
+        return M;
+    };
+    MocoSolution sol(SimTK::Vector(G, T.time.data()), T.state_names, T.control_names, T.multiplier_names,
+            T.derivative_names, {}, matrix(T.states, T.state_names.size()),
+            matrix(T.controls, T.control_names.size()), matrix(T.multipliers, T.multiplier_names.size()),
+            matrix(T.derivatives, T.derivative_names.size()), SimTK::RowVector());
+    const int N = o.num_mesh_intervals;
+    const int nsl = (int)T.slack_names.size();
+    if (nsl) {
+        const SimTK::Vector slackTime = createVectorLinspace(N, T.time.front(), T.time.back());
+        for (int l = 0; l < nsl; ++l) {
+            SimTK::Vector v(N);
+            for (int i = 0; i < N; ++i) v[i] = T.slacks[(size_t)(2 * i + 1) * nsl + l];   // the midpoints
+            sol.appendSlack(T.slack_names[l], interpolate(slackTime, v, sol.getTime()));
+        }
     }
-    return MocoSolution(SimTK::Vector(G, times.data()), hrep.state_names, hrep.control_names, {}, {},
-            S, U, SimTK::Matrix(), SimTK::RowVector());
+    return sol;
 }
+
+// Ipopt's return status by name (IpReturnCodes_inc.h), as MocoCasADiSolver
+// reports CasADi's "return_status".
+std::string ipoptStatusName(Ipopt::ApplicationReturnStatus s) {
+    switch (s) {
+    case Ipopt::Solve_Succeeded: return "Solve_Succeeded";
+    case Ipopt::Solved_To_Acceptable_Level: return "Solved_To_Acceptable_Level";
+    case Ipopt::Infeasible_Problem_Detected: return "Infeasible_Problem_Detected";
+    case Ipopt::Search_Direction_Becomes_Too_Small: return "Search_Direction_Becomes_Too_Small";
+    case Ipopt::Diverging_Iterates: return "Diverging_Iterates";
+    case Ipopt::User_Requested_Stop: return "User_Requested_Stop";
+    case Ipopt::Feasible_Point_Found: return "Feasible_Point_Found";
+    case Ipopt::Maximum_Iterations_Exceeded: return "Maximum_Iterations_Exceeded";
+    case Ipopt::Restoration_Failed: return "Restoration_Failed";
+    case Ipopt::Error_In_Step_Computation: return "Error_In_Step_Computation";
+    case Ipopt::Maximum_CpuTime_Exceeded: return "Maximum_CpuTime_Exceeded";
+    case Ipopt::Not_Enough_Degrees_Of_Freedom: return "Not_Enough_Degrees_Of_Freedom";
+    case Ipopt::Invalid_Problem_Definition: return "Invalid_Problem_Definition";
+    case Ipopt::Invalid_Option: return "Invalid_Option";
+    case Ipopt::Invalid_Number_Detected: return "Invalid_Number_Detected";
+    default: return "Ipopt status " + std::to_string((int)s);
+    }
+}
+
+// The context owned for the solve: destroyed on every exit path.
+struct CtxGuard {
+    mh_ctx* ctx = nullptr;
+    ~CtxGuard() { mh_destroy(ctx); }
+};
 
 }  // namespace
 
@@ -634,18 +673,19 @@ MocoSolution MocoHipSolver::solveImpl() const {
     const mhb::Problem prob = compileProblemRep(rep);
     mhb::ProblemRep hrep;
     mhb::make_rep(prob, hrep);
-    const mh_options opt = mhb::make_options(settings());
-    mh_ctx* ctx = nullptr;
-    OPENSIM_THROW_IF(mh_create(&hrep.problem, &opt, &ctx) != MH_OK, Exception,
-            "MocoHipSolver: mh_create failed: {}", mh_last_error());
-    mh_nlp_info info{};
-    mh_get_nlp_info(ctx, &info);
-    // the starting point: the user's guess resampled on the grid, else the
-    // bounds-midpoint guess (MocoCasADiSolver.cpp:326-332)
+    mh_options opt = mhb::make_options(settings());
+    // the starting point: the user's guess resampled on the grid, every
+    // block by name, else the bounds-midpoint guess (MocoCasADiSolver.cpp:
+    // 326-332); "initial-guess" sparsity detection probes at it
+    // (CasOCSolver.cpp:74-76; null: the bounds midpoint, the same guess)
     std::vector<double> x0;
     const MocoTrajectory& guess = getGuess();
-    if (!guess.empty()) x0 = toIterate(guess, hrep, opt, info);
-    Ipopt::SmartPtr<mocohip::MocoHipTNLP> tnlp = new mocohip::MocoHipTNLP(ctx, x0);
+    if (!guess.empty()) x0 = toIterate(guess, hrep, opt);
+    if (opt.sparsity_detection == MH_SPARSITY_INITIAL_GUESS) opt.sparsity_guess = x0.empty() ? nullptr : x0.data();
+    CtxGuard ctx;
+    OPENSIM_THROW_IF(mh_create(&hrep.problem, &opt, &ctx.ctx) != MH_OK, Exception,
+            "MocoHipSolver: mh_create failed: {}", mh_last_error());
+    Ipopt::SmartPtr<mocohip::MocoHipTNLP> tnlp = new mocohip::MocoHipTNLP(ctx.ctx, x0);
     mocohip::IpoptSettings ips;
     ips.verbosity = get_verbosity();
     ips.optim_max_iterations = get_optim_max_iterations();
@@ -654,13 +694,19 @@ MocoSolution MocoHipSolver::solveImpl() const {
     ips.optim_hessian_approximation = get_optim_hessian_approximation();
     ips.optim_ipopt_print_level = get_optim_ipopt_print_level();
     const Ipopt::ApplicationReturnStatus status = mocohip::solve(tnlp, ips);
-    MocoSolution solution = toSolution(tnlp->solution(), hrep, opt, info);
-    mh_destroy(ctx);
+    MocoSolution solution = toSolution(tnlp->solution(), hrep, opt);
+    // the objective's terms at the solution, one per cost goal
+    // (MocoCasADiSolver.cpp:395-402: the solution's objective breakdown)
+    std::vector<std::pair<std::string, double>> breakdown;
+    const std::vector<std::string> costs = rep.createCostNames();
+    std::vector<double> terms(costs.size() + 1, 0.0);
+    int32_t nterms = (int32_t)terms.size();
+    if (mh_eval_objective_terms(ctx.ctx, tnlp->solution().data(), terms.data(), &nterms) == MH_OK)
+        for (int i = 0; i < (int)costs.size() && i < nterms; ++i) breakdown.emplace_back(costs[i], terms[i]);
     const long long elapsed = stopwatch.getElapsedTimeInNs();
     const bool success = status == Ipopt::Solve_Succeeded || status == Ipopt::Solved_To_Acceptable_Level;
-    setSolutionStats(solution, success, tnlp->objective(),
-            success ? "Solve_Succeeded" : "Ipopt status " + std::to_string((int)status), tnlp->iterations(),
-            SimTK::nsToSec(elapsed));
+    setSolutionStats(solution, success, tnlp->objective(), ipoptStatusName(status), tnlp->iterations(),
+            SimTK::nsToSec(elapsed), breakdown);
     if (get_verbosity()) {
         log_info("Elapsed real time: {}.", stopwatch.formatNs(elapsed));
         log_info(std::string(72, '='));

@@ -562,6 +562,43 @@ __global__ void __launch_bounds__(64) k_combine_global(DevModel M, Src S, Lanes 
     D::combine(M, t, in, TL, StridedOut{Y + (long)kl * ystride_pt + r, (long)Ln.stride});
 }
 
+// k_combine_global with the combine in two steps (D::combine_sum /
+// D::combine_finish, the arithmetic of D::combine bit for bit): a
+// 256-thread workgroup takes 64 lane roles; its 4 waves compute the roles'
+// NSUM independent sums -- wave w the sums w, w + 4, ... (q uniform over the
+// wave), lanes over the roles -- into LDS [q][lane], then the first wave
+// runs each role's factorization, solves and outputs from those sums.  A
+// large model's sums are long chains of dependent group-result loads (each
+// coordinate's generalized force over 80 muscles: Rajagopal 80), which one
+// thread per role walked one after the other.
+template <class D>
+__global__ void __launch_bounds__(256) k_combine_split(DevModel M, Src S, Lanes Ln, Tasks TK,
+        const double* __restrict__ T, const double* __restrict__ H, double* __restrict__ times,
+        double* __restrict__ Y, long ystride_pt, const int* __restrict__ cmap, int nmap) {
+    __shared__ double sS[(D::NSUM > 0 ? D::NSUM : 1) * 64];
+    const int per = cmap ? nmap : Ln.stride;
+    const int ln = (int)threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    const long gid = (long)blockIdx.x * 64 + ln;
+    const bool live = gid < (long)TK.nk * per;
+    const long g = live ? gid : 0;
+    const int kl = (int)(g / per);
+    const int j = (int)(g - (long)kl * per);
+    const int r = cmap ? cmap[j] : j;
+    double t;
+    const LaneIn<D> in = lane_input<D>(S, Ln, kl, r, t);
+    const TaskLoadGlobal<D> TL{T + (long)kl * TK.tdoubles, H + (long)kl * TK.nmass * D::NST, TK.jd, r};
+    for (int q = wv; q < D::NSUM; q += 4) {
+        const double v = D::combine_sum(q, M, t, in, TL);
+        if (live) sS[q * 64 + ln] = v;
+    }
+    __syncthreads();
+    if (wv != 0 || !live) return;
+    if (r == Ln.base && times) times[kl] = t;
+    D::combine_finish(M, t, in, TL, SumsLds{lds(sS + ln), 64},
+                      StridedOut{Y + (long)kl * ystride_pt + r, (long)Ln.stride});
+}
+
 // Excitation lanes of a generated back end (mocohip.hip k_exc_fill, launched
 // through this host entry so that the fill kernel lives in one unit).
 int mh_launch_exc_fill(const mh_ctx* c, int nk, int NO, int stride, int base, int tdoubles, const double* T,
@@ -1137,55 +1174,33 @@ __device__ __forceinline__ void interval_body(const DevModel& M, const Src& S, c
     if (threadIdx.x < 2) sK[threadIdx.x] = threadIdx.x ? 1.0 : 0.0;
     __syncthreads();
     if (I.dbg_stop == 1) return;
-    {
-        // the combine in two steps (D::combine_sum / D::combine_finish, the
-        // same arithmetic as D::combine, bit for bit): first its NSUM
-        // independent sums (each coordinate's generalized force, each
-        // root-chain mass-matrix entry) of every lane role, one sum per
-        // wave task -- q uniform over the wave, lanes over the roles -- into
-        // LDS [q][role]; then per role the factorization and solves from
-        // those sums.  A role's ~NSUM chains of LDS reads and adds run on
-        // NSUM waves instead of one thread (eval_g: 3 threads did all of it)
-        const int R = npts * Ln.stride;
-        lds_double* sS = lds(sXl + L.NSL);
-        const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-        const int ln = (int)threadIdx.x & 63, nw = (int)blockDim.x >> 6;
-        const int nch = (R + 63) >> 6;
-        for (int v = wv; v < D::NSUM * nch; v += nw) {
-            const int q = v % D::NSUM;
-            const int pr = (v / D::NSUM) * 64 + ln;
-            if (pr < R) {
-                const int p = pr / Ln.stride, r = pr - p * Ln.stride;
-                LaneInL<D> in{lds(sXs + p * L.NS), lds(sXc + p * L.NC), lds(sXd + p * L.NDV), -1, 0.0,
-                              lds(sXm + p * L.NM), L.vc(k_first + p) ? lds(sXl) : nullptr};
-                const double t = lane_time(Ln, S.grid[k_first + p], t0, tf, r, in.pi, in.step);
-                double sv;
-                if constexpr (GM) {
-                    const TaskLoadGlobal<D> TL{T + (long)(kl0 + p) * nt, H + (long)(kl0 + p) * nh, TK.jd, r};
-                    sv = D::combine_sum(q, M, t, in, TL);
-                } else {
-                    const TaskLoadLds<D> TL{lds(sT + p * nt), lds(sH + p * nh), TK.jd, r};
-                    sv = D::combine_sum(q, M, t, in, TL);
-                }
-                sS[q * R + pr] = sv;
-            }
+    // eval_g's lanes (stride 1: every lane is the base role 0, written as a
+    // constant so that the role -> slot reads have uniform addresses and
+    // compile to scalar loads off the combine's critical path)
+    auto combine_lane = [&](int p, int r) {
+        LaneInL<D> in{lds(sXs + p * L.NS), lds(sXc + p * L.NC), lds(sXd + p * L.NDV), -1, 0.0,
+                      lds(sXm + p * L.NM), L.vc(k_first + p) ? lds(sXl) : nullptr};
+        const double t = lane_time(Ln, S.grid[k_first + p], t0, tf, r, in.pi, in.step);
+        if (r == Ln.base) sTimes[p] = t;
+        const LdsOut out{lds(sY + p * ny + r), Ln.stride};
+        if constexpr (GM) {
+            const TaskLoadGlobal<D> TL{T + (long)(kl0 + p) * nt, H + (long)(kl0 + p) * nh, TK.jd, r};
+            D::combine(M, t, in, TL, out);
+        } else {
+            const TaskLoadLds<D> TL{lds(sT + p * nt), lds(sH + p * nh), TK.jd, r};
+            D::combine(M, t, in, TL, out);
         }
-        __syncthreads();
-        for (int w = threadIdx.x; w < R; w += blockDim.x) {
+    };
+    // (one thread per lane role: the combine split over the waves --
+    // D::combine_sum into LDS, then D::combine_finish -- measured slower:
+    // k_interval 17.6 -> 19.7 us, eval_g's 9.9 -> 10.6 us, profiles/r05_b;
+    // the combine is not bound by its sums' load-and-add chains)
+    if (Ln.stride == 1) {
+        if ((int)threadIdx.x < npts) combine_lane((int)threadIdx.x, 0);
+    } else {
+        for (int w = threadIdx.x; w < npts * Ln.stride; w += blockDim.x) {
             const int p = w / Ln.stride, r = w - p * Ln.stride;
-            LaneInL<D> in{lds(sXs + p * L.NS), lds(sXc + p * L.NC), lds(sXd + p * L.NDV), -1, 0.0,
-                          lds(sXm + p * L.NM), L.vc(k_first + p) ? lds(sXl) : nullptr};
-            const double t = lane_time(Ln, S.grid[k_first + p], t0, tf, r, in.pi, in.step);
-            if (r == Ln.base) sTimes[p] = t;
-            const LdsOut out{lds(sY + p * ny + r), Ln.stride};
-            const SumsLds SV{sS + w, R};
-            if constexpr (GM) {
-                const TaskLoadGlobal<D> TL{T + (long)(kl0 + p) * nt, H + (long)(kl0 + p) * nh, TK.jd, r};
-                D::combine_finish(M, t, in, TL, SV, out);
-            } else {
-                const TaskLoadLds<D> TL{lds(sT + p * nt), lds(sH + p * nh), TK.jd, r};
-                D::combine_finish(M, t, in, TL, SV, out);
-            }
+            combine_lane(p, r);
         }
     }
     // the compiled words of this thread's first IV_PF assembly entries,
@@ -2098,7 +2113,7 @@ struct mh_ctx {
     int role_threads = 256;        // k_role workgroup size (MOCOHIP_ROLE_THREADS: 64..512)
     int iv_threads = 1024;         // k_interval workgroup size, Jacobian lanes (MOCOHIP_IV_THREADS: 256..1024)
     int ivg_threads = 256;         // k_interval workgroup size, eval_g lanes (MOCOHIP_IVG_THREADS: 64..1024)
-    int csplit = 1;                // MOCOHIP_CSPLIT=0: no k_interval (its combine is the split one)
+    int csplit = 1;                // large models' combine: k_combine_split (MOCOHIP_CSPLIT=0: k_combine_global)
     bool role_couple = true;       // coupling in k_role's time role (MOCOHIP_ROLE_COUPLE=0: k_couple)
     bool use_ctpl = true;          // MOCOHIP_CTPL=0: k_interval assembles through jac_entry
     float timings[4] = {0, 0, 0, 0};
@@ -2328,9 +2343,15 @@ static int launch_tasks(mh_ctx* c, const Src& S, const Lanes& ln, const TaskSet&
         const bool xs = c->d_exc_slot && &ts == &c->ts_jac;
         const int per = xs ? ln.stride - c->n_exc_gen : ln.stride;
         const long lanes = (long)ts.dev.nk * per;
-        hipLaunchKernelGGL(k_combine_global<D>, dim3((unsigned)((lanes + 63) / 64)), dim3(64), 0,
-                c->stream, c->M, S, ln, ts.dev, T, H, times, Y, (long)D::NO * ln.stride,
-                xs ? (const int*)c->d_cmb_map : nullptr, per);
+        // the sums over the waves (k_combine_split) unless MOCOHIP_CSPLIT=0
+        if (c->csplit && D::NSUM > 0)
+            hipLaunchKernelGGL(k_combine_split<D>, dim3((unsigned)((lanes + 63) / 64)), dim3(256), 0,
+                    c->stream, c->M, S, ln, ts.dev, T, H, times, Y, (long)D::NO * ln.stride,
+                    xs ? (const int*)c->d_cmb_map : nullptr, per);
+        else
+            hipLaunchKernelGGL(k_combine_global<D>, dim3((unsigned)((lanes + 63) / 64)), dim3(64), 0,
+                    c->stream, c->M, S, ln, ts.dev, T, H, times, Y, (long)D::NO * ln.stride,
+                    xs ? (const int*)c->d_cmb_map : nullptr, per);
         if (xs) (void)mh_launch_exc_fill(c, ts.dev.nk, D::NO, ln.stride, ln.base, ts.dev.tdoubles, T, Y);
     }
     return 0;
@@ -2348,24 +2369,13 @@ static void be_eval_tasks(mh_ctx* c, const double* x, int mode, double* Y) {
     }
     c->yq[mode] = launch_tasks<D>(c, S, ln, ts, T, H, c->d_times, Y, mode == 1 && c->quot);
 }
-// LDS bytes of k_interval's combine sums (interval_body: [NSUM][npts x
-// lanes] doubles).  MOCOHIP_CSPLIT=0 reports "does not fit": the evaluation
-// then takes the split path (k_combine's one-thread-per-lane combine + the
-// transcription), the A/B reference of the split combine.
-template <class D>
-static size_t interval_sums_lds(const mh_ctx* c, const Lanes& ln) {
-    if (!c->csplit) return kMaxLds + 1;
-    const size_t npts = c->scheme == MH_HERMITE_SIMPSON ? 3 : 2;
-    return sizeof(double) * npts * (size_t)ln.stride * (size_t)(D::NSUM > 0 ? D::NSUM : 1);
-}
 // LDS bytes of k_interval for one lane configuration (0: does not apply).
 template <class D>
 static size_t interval_lds(const mh_ctx* c, const Lanes& ln, const TaskSet& ts) {
     const size_t npts = c->scheme == MH_HERMITE_SIMPSON ? 3 : 2;
     return sizeof(double) * (npts * D::NO * ln.stride + CT_CONST + CT_NCONST +
                              npts * (size_t)(c->NS + c->NC + c->NDV + c->NM) + (size_t)c->NSL +
-                             npts * ((size_t)ts.dev.tdoubles + (size_t)ts.dev.nmass * D::NST)) +
-           interval_sums_lds<D>(c, ln);
+                             npts * ((size_t)ts.dev.tdoubles + (size_t)ts.dev.nmass * D::NST));
 }
 // LDS bytes of k_role (Jacobian lanes).
 template <class D>
@@ -2386,8 +2396,7 @@ template <class D>
 static size_t interval_lds_gm(const mh_ctx* c, const Lanes& ln) {
     const size_t npts = c->scheme == MH_HERMITE_SIMPSON ? 3 : 2;
     return sizeof(double) * (npts * D::NO * ln.stride + CT_CONST + CT_NCONST +
-                             npts * (size_t)(c->NS + c->NC + c->NDV + c->NM) + (size_t)c->NSL) +
-           interval_sums_lds<D>(c, ln);
+                             npts * (size_t)(c->NS + c->NC + c->NDV + c->NM) + (size_t)c->NSL);
 }
 template <class D>
 static void be_batch(mh_batch* bt, int mode, const BatchPtrs& BP, int with_g, int with_v) {

@@ -689,6 +689,29 @@ void make_rep(const Problem& P, ProblemRep& R) {
     p.kinematic_constraint_bounds.upper = P.kinematic_constraint_bounds.upper;
     for (auto& m : model.muscles)
         R.num_aux_residuals += !m.ignore_tendon_compliance && m.tendon_compliance_dynamics_mode == "implicit";
+    // the reference's names of the other variable blocks (problem.py
+    // ProblemRep): multipliers lambda_cid<c>_p0 after the Simbody
+    // ConstraintIndex c -- every Coordinate owns a (disabled) lock constraint
+    // ahead of the ConstraintSet, so the enabled couplers are c = ncoord + i
+    // (MocoProblemRep.cpp:202-230) --, slacks gamma_cid<c>_p0
+    // (MocoCasOCProblem.cpp:186-201), accelerations <coordinate>/accel
+    // (CasOCProblem.h:363-377), implicit auxiliary derivatives
+    // <muscle>/implicitderiv_normalized_tendon_force (MocoProblemRep.cpp:445-460)
+    const int ncoord = (int)model.coordinates().size();
+    R.multiplier_names.clear();
+    R.slack_names.clear();
+    for (size_t i = 0; i < model.constraints.size(); ++i) {
+        R.multiplier_names.push_back("lambda_cid" + std::to_string(ncoord + (int)i) + "_p0");
+        R.slack_names.push_back("gamma_cid" + std::to_string(ncoord + (int)i) + "_p0");
+    }
+    R.accel_names.clear();
+    for (auto& n : R.state_names)
+        if (n.size() >= 6 && n.compare(n.size() - 6, 6, "/speed") == 0)
+            R.accel_names.push_back(n.substr(0, n.size() - 5) + "accel");
+    R.aux_derivative_names.clear();
+    for (auto& m : model.muscles)
+        if (!m.ignore_tendon_compliance && m.tendon_compliance_dynamics_mode == "implicit")
+            R.aux_derivative_names.push_back(m.path + "/implicitderiv_normalized_tendon_force");
     R.bind();
 }
 
@@ -708,7 +731,10 @@ mh_options make_options(const SolverSettings& s, int interval_begin, int interva
     else fail("multibody_dynamics_mode must be 'explicit' or 'implicit'");
     if (s.optim_sparsity_detection == "none") o.sparsity_detection = MH_SPARSITY_NONE;
     else if (s.optim_sparsity_detection == "random") o.sparsity_detection = MH_SPARSITY_RANDOM;
-    else fail("optim_sparsity_detection must be 'none' or 'random' in a description");
+    // "initial-guess" (CasOCSolver.cpp:74-76): the caller points
+    // o.sparsity_guess at the guess iterate (null: the bounds midpoint)
+    else if (s.optim_sparsity_detection == "initial-guess") o.sparsity_detection = MH_SPARSITY_INITIAL_GUESS;
+    else fail("optim_sparsity_detection must be 'none', 'random' or 'initial-guess'");
     o.num_mesh_intervals = s.num_mesh_intervals;
     o.interpolate_control_midpoints = s.interpolate_control_midpoints;
     o.fd_step = s.fd_step;
@@ -734,7 +760,7 @@ mh_options make_options(const SolverSettings& s, int interval_begin, int interva
     return o;
 }
 
-// ---- the tape (mocohip/tape.py write_tape, version 6) -----------------------
+// ---- the tape (mocohip/tape.py write_tape, version 7) -----------------------
 namespace {
 struct Out {
     std::string b;
@@ -760,7 +786,7 @@ void write_tape(const ProblemRep& R, const mh_options& o0, const std::string& pa
     o.sparsity_pattern = nullptr;
     Out w;
     w.bytes("MHTAPE01", 8);
-    const int32_t head[3] = {6, ns, nc};
+    const int32_t head[3] = {7, ns, nc};
     w.bytes(head, sizeof head);
     w.pod(o);
     const int32_t counts[12] = {m.nq, m.nbodies, m.naxes, m.nfunctions, m.nknots, m.nmuscles,

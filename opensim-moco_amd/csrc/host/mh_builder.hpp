@@ -275,6 +275,9 @@ struct ProblemRep {
     std::vector<mh_endpoint_equation> endpoint;
     std::vector<int32_t> kin_cols;
     int num_aux_residuals = 0;
+    // the reference's names of the multipliers, slacks, accelerations (implicit
+    // multibody dynamics) and implicit auxiliary derivatives (make_rep)
+    std::vector<std::string> multiplier_names, slack_names, accel_names, aux_derivative_names;
     mh_problem problem{};
     void bind();
 };

@@ -112,15 +112,19 @@ bool read_tape(const char* path, Tape& t, std::string& err) {
     t.nc = r.pod<int32_t>();
     // version 4 = ABI v4's mh_options (unchanged in v5); earlier tapes carry a
     // shorter one; version 5 appends the wrap surfaces; version 6 carries ABI
-    // v6's mh_options (+ sparsity_rule: 8 bytes; older tapes leave it 0)
-    if (version < 4 || version > 6) {
-        err = "unsupported tape version (this build reads versions 4 to 6)";
+    // v6's mh_options (+ sparsity_rule: 8 bytes; older tapes leave it 0, the
+    // reference's rule since v7); version 7: ABI v7 (the rule's values
+    // swapped: a v6 tape's 0 / 1 was robust / any-change)
+    if (version < 4 || version > 7) {
+        err = "unsupported tape version (this build reads versions 4 to 7)";
         return false;
     }
     {
         const size_t nopt = version >= 6 ? sizeof(mh_options) : sizeof(mh_options) - 2 * sizeof(int32_t);
         t.opts = mh_options{};
         std::memcpy(&t.opts, r.take(nopt), nopt);
+        if (version == 6)
+            t.opts.sparsity_rule = t.opts.sparsity_rule == 0 ? MH_SPARSITY_RULE_ROBUST : MH_SPARSITY_RULE_ANY_CHANGE;
     }
     mh_model& m = t.prob.model;
     int32_t* counts[] = {&m.nq, &m.nbodies, &m.naxes, &m.nfunctions, &m.nknots, &m.nmuscles,

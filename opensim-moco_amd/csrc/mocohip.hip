@@ -266,19 +266,28 @@ __global__ void __launch_bounds__(256) k_reduce_obj(Layout L, GoalSet GS, int mo
         const double acc = red[0];
         __syncthreads();
         const mh_goal G = GS.goals[gi];
+        double term = 0.0;
         if (G.kind == MH_GOAL_FINAL_TIME) {
             if (endpoint) {
-                total += G.weight * x[1];
+                term = G.weight * x[1];
+                total += term;
                 g1 += G.weight;
             }
         } else if (G.kind == MH_GOAL_MARKER_FINAL) {
-            if (endpoint) total += G.weight * ep[gi];   // its gradient: k_marker_final
+            if (endpoint) {
+                term = G.weight * ep[gi];   // its gradient: k_marker_final
+                total += term;
+            }
         } else {
-            total += G.weight * ((x[1] - x[0]) * acc);
+            term = G.weight * ((x[1] - x[0]) * acc);
+            total += term;
             g0 += -G.weight * acc;
             g1 += G.weight * acc;
         }
+        // mode 2: the objective's terms, one per goal (mh_eval_objective_terms)
+        if (mode == 2 && threadIdx.x == 0) out[gi] = term;
     }
+    if (mode == 2) return;
     if (mode == 0) {
         if (threadIdx.x == 0) out[0] = total;
         return;
@@ -1693,11 +1702,11 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
         // 7.5 MB per launch, profiles/r04_xcd); MOCOHIP_IV_XCD=0: plain order
         const char* ex = std::getenv("MOCOHIP_IV_XCD");
         c->iv_xcd = ex && std::strcmp(ex, "0") == 0 ? 0 : 1;
-        // k_interval's combine is its independent sums spread over the
-        // workgroup's waves, then the factorization and solves per lane role
-        // (D::combine_sum / combine_finish; interval_body); MOCOHIP_CSPLIT=0
-        // takes the split path instead (k_combine: one thread per lane role
-        // does all of it, D::combine) -- the A/B reference
+        // the combine of a large model's lanes (k_combine_global's case):
+        // its independent sums spread over a workgroup's waves, then the
+        // factorization and solves per lane role (k_combine_split: D::
+        // combine_sum / combine_finish); MOCOHIP_CSPLIT=0: k_combine_global
+        // (one thread per lane role does all of it, D::combine)
         const char* ecs = std::getenv("MOCOHIP_CSPLIT");
         c->csplit = ecs && std::strcmp(ecs, "0") == 0 ? 0 : 1;
         // hipGraph replay of the stages: measured slower than direct launches
@@ -2597,6 +2606,37 @@ static int eval_grad_f_impl(mh_ctx* c, const double* x, double* grad, bool parti
 }
 
 extern "C" int mh_eval_f(mh_ctx* c, const double* x, int, double* f) { return eval_f_impl(c, x, f, false); }
+
+// The objective's terms, one per goal (the solution's objective breakdown,
+// MocoCasADiSolver.cpp:395-402; CasOCTranscription.cpp:699-702 evaluates the
+// objective terms at the solution): eval_f's arithmetic, each goal's weighted
+// value kept apart instead of summed.
+extern "C" int mh_eval_objective_terms(mh_ctx* c, const double* x, double* terms, int32_t* nterms) {
+    if (!c || !x || !terms || !nterms) return set_err(MH_ERR_INVALID, "null argument");
+    if (*nterms < c->ngoals) {
+        const int have = *nterms;
+        *nterms = c->ngoals;
+        return set_err(MH_ERR_INVALID, "terms holds %d doubles, the problem has %d goals", have, c->ngoals);
+    }
+    *nterms = c->ngoals;
+    if (c->ngoals == 0) return MH_OK;
+    HIPCHK(hipSetDevice(c->device));
+    (void)hipGetLastError();
+    HIPCHK(hipMemcpyAsync(c->d_x, x, sizeof(double) * c->n, hipMemcpyHostToDevice, c->stream));
+    Layout L = make_layout(c, 0, c->G);
+    c->be->integrand(c, c->d_x);
+    HIPCHK(hipGetLastError());
+    if (c->has_marker)
+        hipLaunchKernelGGL(k_marker_final, dim3((unsigned)c->ngoals), dim3(128), 0, c->stream, c->M, L, c->GS,
+                c->fd, c->h, 0, c->d_x, c->d_ep, c->d_grad);
+    // the per-goal terms into the gradient's buffer (n >= goals; scratch here)
+    hipLaunchKernelGGL(k_reduce_obj, dim3(1), dim3(256), 0, c->stream, L, c->GS, 2, 1, c->d_x, c->d_C, c->d_tpart,
+            c->d_ep, c->d_grad);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(terms, c->d_grad, sizeof(double) * c->ngoals, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return MH_OK;
+}
 extern "C" int mh_eval_grad_f(mh_ctx* c, const double* x, int, double* grad) {
     return eval_grad_f_impl(c, x, grad, false);
 }
@@ -2966,8 +3006,11 @@ extern "C" int mh_get_backend_flags(const mh_ctx* c, char* flags, int32_t len) {
         f += " g-lds";
         if (c->g_lds_guard) {
             // the guard bands' verdict over every k_eval_lds launch so far
+            // ordered after every k_eval_lds launch still in flight on the
+            // context's (non-blocking) stream
             int st = 0;
-            if (hipMemcpy(&st, c->d_lds_status, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
+            if (hipMemcpyAsync(&st, c->d_lds_status, sizeof(int), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+                    hipStreamSynchronize(c->stream) != hipSuccess)
                 return set_err(MH_ERR_HIP, "reading the LDS guard status failed");
             f += st ? " g-lds-guard-violated" : " g-lds-guard-intact";
         }

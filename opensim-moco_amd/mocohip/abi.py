@@ -137,7 +137,7 @@ class mh_goal(C.Structure):
                 ("weight", f64)]
 
 
-MH_ABI_VERSION = 6     # include/mocohip.h
+MH_ABI_VERSION = 7     # include/mocohip.h
 MH_PATH_CONTROL_BOUND = 0
 MH_ENDPOINT_INITIAL_ACTIVATION = 0
 
@@ -184,7 +184,7 @@ class mh_options(C.Structure):
 
 
 MH_SPARSITY_NONE, MH_SPARSITY_RANDOM, MH_SPARSITY_INITIAL_GUESS, MH_SPARSITY_GIVEN = 0, 1, 2, 3
-MH_SPARSITY_RULE_ROBUST, MH_SPARSITY_RULE_ANY_CHANGE = 0, 1
+MH_SPARSITY_RULE_ANY_CHANGE, MH_SPARSITY_RULE_ROBUST = 0, 1   # ABI v7: the reference's rule is 0
 MH_SPARSITY_ROBUST_TOL = 1e-12
 
 
@@ -200,6 +200,7 @@ class mh_nlp_info(C.Structure):
 # C-ABI test checks every one is exported (and matches include/mocohip.h).
 MOCOHIP_SYMBOLS = {
     "mh_abi_version": (i32, []),
+    "mh_eval_objective_terms": (i32, [C.c_void_p, P(f64), P(f64), P(i32)]),
     "mh_build_id": (C.c_char_p, []),
     "mh_backend_for": (i32, [P(mh_problem), P(mh_options), C.c_char_p, i32]),
     "mh_last_error": (C.c_char_p, []),

@@ -135,3 +135,35 @@ def solve_batch(subjects: Sequence[Tuple[float, float]], num_mesh_intervals: int
             "mean_solve_s": round(sum(r["wall_clock_s"] for r in ok) / len(ok), 3) if ok else None,
             "linear_solver": ok[0].get("linear_solver") if ok else None,
             "results": sorted(res, key=lambda r: r["subject"])}
+
+
+def rank_share(subjects: Sequence[Tuple[float, float]], rank: int, world: int) -> List[Tuple[float, float]]:
+    """The subjects rank ``rank`` of ``world`` solves: every world-th one
+    starting at its rank (independent solves: no data-path collective)."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError(f"bad rank {rank} of {world}")
+    return list(subjects[rank::world])
+
+
+def solve_sweep(count: int, num_mesh_intervals: int = 125, rank: int = 0, world: int = 1, device: int = 0,
+                max_concurrent: int = 8, linear_solver: str = "auto", hw_queues: int | None = 2,
+                timeout: float = 600.0) -> dict:
+    """configs[4] over the ranks of a node: rank r solves rank_share(
+    sweep(count), r, world) on its own GPU ``device``, in rounds of at most
+    ``max_concurrent`` solver processes started together (solve_batch).
+    Returns this rank's record; the caller reduces the ranks' counts and wall
+    clocks (bench.py: an all-reduce of [solves, succeeded] and of the max
+    wall clock)."""
+    mine = rank_share(sweep(count), rank, world)
+    rounds, wall, results = [], 0.0, []
+    for i in range(0, len(mine), max(1, int(max_concurrent))):
+        r = solve_batch(mine[i:i + max_concurrent], num_mesh_intervals, device=device, timeout=timeout,
+                        linear_solver=linear_solver, hw_queues=hw_queues)
+        rounds.append(r["wall_clock_s"])
+        wall += r["wall_clock_s"]
+        results += r["results"]
+    ok = [r for r in results if r.get("success")]
+    return {"rank": rank, "world": world, "solves": len(mine), "succeeded": len(ok),
+            "rounds": len(rounds), "round_wall_clock_s": rounds, "wall_clock_s": round(wall, 3),
+            "mean_iterations": round(sum(r["iterations"] for r in ok) / len(ok), 1) if ok else None,
+            "results": results}

@@ -133,6 +133,11 @@ class IpmOptions:
         o = cls()
         for k, v in opts.items():
             if hasattr(o, k) and (not isinstance(v, str) or isinstance(getattr(o, k), str)):
+                # Ipopt's own linear_solver names its sparse factorization
+                # ('mumps', 'ma27', ... as MocoCasADiSolver / tropter pass it):
+                # not this option's values (the Newton systems' back end here)
+                if k == "linear_solver" and v not in ("auto", "host", "device"):
+                    continue
                 setattr(o, k, type(getattr(o, k))(v))
         return o
 

@@ -315,6 +315,7 @@ class ProblemRep:
         # goals (endpoint-constraint mode goals become endpoint equations,
         # in goal order: MocoProblemRep::createEndpointConstraintNames)
         goals, gidx, gcol, gw = [], [], [], []
+        goal_names: List[str] = []   # the mh_goal entries' goal names (objective breakdown)
         endpoint: List[abi.mh_endpoint_equation] = []
         sidx = {n: i for i, n in enumerate(self.state_names)}
         cidx = {n: i for i, n in enumerate(self.control_names)}
@@ -391,12 +392,14 @@ class ProblemRep:
                 raise TypeError(f"unsupported goal {type(g).__name__}")
             gs.term_count = len(gidx) - gs.term_begin
             goals.append(gs)
+            goal_names.append(getattr(g, "name", "") or type(g).__name__)
 
         self._sinfo = (abi.mh_variable_info * max(1, len(self.state_infos)))(
             *[_vi(i) for i in self.state_infos])
         self._cinfo = (abi.mh_variable_info * max(1, len(self.control_infos)))(
             *[_vi(i) for i in self.control_infos])
         self._goals = (abi.mh_goal * max(1, len(goals)))(*goals)
+        self.goal_names = goal_names
         self._gidx = np.ascontiguousarray(gidx + [0], np.int32)
         self._gcol = np.ascontiguousarray(gcol + [0], np.int32)
         self._gw = np.ascontiguousarray(gw + [0.0], float)
@@ -444,6 +447,25 @@ class ProblemRep:
         self.num_aux_residuals = sum(
             1 for m in model.muscles
             if not m.ignore_tendon_compliance and m.tendon_compliance_dynamics_mode == "implicit")
+        # the reference's names of the other variable blocks (MocoTrajectory
+        # columns).  Multipliers: MocoProblemRep.cpp:202-230 names them
+        # lambda_cid<c>_p<i> after the Simbody ConstraintIndex c, and OpenSim
+        # gives every Coordinate a (disabled) lock constraint of its own
+        # before the model's ConstraintSet, so the enabled couplers are
+        # ConstraintIndex ncoord, ncoord + 1, ... (Rajagopal 18: 21 coordinates
+        # -> lambda_cid21_p0, lambda_cid22_p0 in std_testMocoInverse_subject_
+        # 18musc_solution.sto).  Slacks: the same with gamma
+        # (MocoCasOCProblem.cpp:186-201).  Implicit auxiliary derivatives:
+        # <component>/implicitderiv_<state> (MocoProblemRep.cpp:445-460,
+        # MocoCasOCProblem.cpp:92-97), after the accelerations <coordinate>/accel
+        # of implicit multibody dynamics (CasOCProblem.h:363-377).
+        ncoord = len(model.coordinates())
+        self.multiplier_names = [f"lambda_cid{ncoord + i}_p0" for i in range(len(model.constraints))]
+        self.slack_names_all = [f"gamma_cid{ncoord + i}_p0" for i in range(len(model.constraints))]
+        self.aux_derivative_names = [
+            m.path + "/implicitderiv_normalized_tendon_force" for m in model.muscles
+            if not m.ignore_tendon_compliance and m.tendon_compliance_dynamics_mode == "implicit"]
+        self.accel_names_all = [n[:-len("speed")] + "accel" for n in self.state_names if n.endswith("/speed")]
 
     @staticmethod
     def _path_equations(problem: MocoProblem):

@@ -521,6 +521,17 @@ class HipNLP(_NLPBase):
         self._check(self.lib.mh_eval_grad_f(self.ctx, abi.dptr(x), int(new_x), abi.dptr(g)))
         return g
 
+    def objective_terms(self, x) -> np.ndarray:
+        """The objective's weighted terms at x, one per goal of the problem
+        (mh_eval_objective_terms; their sum in goal order is eval_f)."""
+        x = np.ascontiguousarray(x, float)
+        k = C.c_int32(0)
+        self.lib.mh_eval_objective_terms(self.ctx, abi.dptr(x), abi.dptr(np.zeros(1)), C.byref(k))
+        out = np.zeros(max(int(k.value), 1))
+        k = C.c_int32(len(out))
+        self._check(self.lib.mh_eval_objective_terms(self.ctx, abi.dptr(x), abi.dptr(out), C.byref(k)))
+        return out[:int(k.value)]
+
     def eval_g(self, x, new_x=True):
         x = np.ascontiguousarray(x, float)
         g = np.empty(max(self.row_end - self.row_begin, 1))
@@ -734,6 +745,14 @@ class MocoStudy:
                 opts["linear_solver"] = linear_solver
             r = solve_nlp(nlp, x0, tol, ctol, it, method=method, ipopt_options=opts)
             sol = MocoTrajectory.from_iterate(nlp, r.x)
+            # the objective's breakdown at the solution (setSolutionStats'
+            # objectiveBreakdown, MocoSolver.h:97-102): one term per goal
+            r.objective_breakdown = None
+            if hasattr(nlp, "objective_terms"):
+                terms = nlp.objective_terms(r.x)
+                names = list(getattr(nlp.rep, "goal_names", []))
+                r.objective_breakdown = [(names[i] if i < len(names) else f"goal_{i}", float(v))
+                                         for i, v in enumerate(terms)]
         finally:
             if own:
                 nlp.close()

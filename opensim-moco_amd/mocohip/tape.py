@@ -16,8 +16,9 @@ Layout (little endian, x86-64 struct layout of include/mocohip.h):
   (mh_model.nconstraints/constraints) and the multiplier and
   kinematic-constraint bounds; version 5 (ABI v5) appends the wrap surfaces
   and PathWraps (mh_model.nwraps/wraps, npathwraps/pathwraps); version 6
-  carries ABI v6's mh_options (+ sparsity_rule).  Readers accept versions 4
-  to 6."""
+  carries ABI v6's mh_options (+ sparsity_rule); version 7 ABI v7's (the
+  rule's values swapped: the reference's any-change rule is 0).  Readers
+  accept versions 4 to 7 (a version-6 tape's rule is mapped to v7's value)."""
 from __future__ import annotations
 
 import ctypes as C
@@ -26,8 +27,8 @@ import struct
 from . import abi
 
 MAGIC = b"MHTAPE01"
-VERSION = 6   # 2: + path constraints; 3: + endpoint constraints; 4: + kinematic constraints; 5: + wraps;
-#               6: ABI v6 mh_options
+VERSION = 7   # 2: + path constraints; 3: + endpoint constraints; 4: + kinematic constraints; 5: + wraps;
+#               6: ABI v6 mh_options; 7: ABI v7 (sparsity_rule values swapped)
 
 # (field, element type, count attribute of mh_model / None for problem arrays)
 _MODEL_ARRAYS = [

@@ -36,6 +36,26 @@ from .splines import gcv_interpolating_ppoly, ppoly_eval
 _BLOCKS = ("states", "controls", "multipliers", "derivatives", "slacks", "parameters")
 
 
+def variable_names(nlp):
+    """(derivative, multiplier, slack) names of ``nlp``'s iterate in the
+    reference's convention (problem.ProblemRep: accelerations <coordinate>/
+    accel then <muscle>/implicitderiv_normalized_tendon_force, CasOCProblem.h:
+    363-377; lambda_cid<c>_p0 / gamma_cid<c>_p0, MocoProblemRep.cpp:202-230);
+    generic names where the rep does not carry them."""
+    rep = nlp.rep
+    ndv, nm, nsl = nlp.NDV, getattr(nlp, "NM", 0), getattr(nlp, "NSL", 0)
+    nacc = getattr(nlp, "NACC", 0)
+    acc = list(getattr(rep, "accel_names_all", []))
+    aux = list(getattr(rep, "aux_derivative_names", []))
+    dn = (acc[:nacc] if len(acc) >= nacc else [f"accel_{j}" for j in range(nacc)]) + \
+         (aux if len(aux) == ndv - nacc else [f"derivative_{j}" for j in range(nacc, ndv)])
+    mult = list(getattr(rep, "multiplier_names", []))
+    mn = mult if len(mult) == nm else [f"lambda_{j}" for j in range(nm)]
+    slk = list(getattr(rep, "slack_names_all", []))
+    sn = slk[:nsl] if len(slk) >= nsl else [f"gamma_{j}" for j in range(nsl)]
+    return dn, mn, sn
+
+
 @dataclass
 class MocoTrajectory:
     time: np.ndarray
@@ -236,10 +256,26 @@ class MocoTrajectory:
             if n not in self.control_names:
                 raise ValueError(f"guess has no control '{n}'")
             Cm[:, j] = r.controls[:, self.control_names.index(n)]
-        D = np.zeros((G, ndv))
-        for j in range(min(ndv, r.derivatives.shape[1])):
-            D[:, j] = r.derivatives[:, j]
-        return np.concatenate([[t0, tf], S.ravel(), Cm.ravel(), D.ravel()])
+        dn, mn, sn = variable_names(nlp)
+        nm, nsl = len(mn), len(sn)
+        N = nlp.opts.num_mesh_intervals
+
+        def by_name(want, have, data):
+            # columns matched by name (convertToCasOCIterate); where the guess
+            # names none of them, its columns are taken in order; missing: 0
+            out = np.zeros((G, len(want)))
+            named = [n for n in want if n in have]
+            for j, n in enumerate(want):
+                if n in have:
+                    out[:, j] = data[:, have.index(n)]
+                elif not named and j < data.shape[1]:
+                    out[:, j] = data[:, j]
+            return out
+        D = by_name(dn, list(self.derivative_names), r.derivatives)
+        Mu = by_name(mn, list(self.multiplier_names), r.multipliers)
+        Lg = by_name(sn, list(self.slack_names), r.slacks)
+        L = Lg[1::2][:N] if nsl else np.zeros((N, 0))   # the slacks at the mesh-interval midpoints
+        return np.concatenate([[t0, tf], S.ravel(), Cm.ravel(), Mu.ravel(), L.ravel(), D.ravel()])
 
     @staticmethod
     def from_iterate(nlp, x: np.ndarray) -> "MocoTrajectory":
@@ -265,9 +301,7 @@ class MocoTrajectory:
         Lg = np.full((G, nsl), np.nan)
         if nsl:
             Lg[1::2] = L
-        dn = [f"derivative_{j}" for j in range(ndv)]
-        mn = [f"lambda_{j}" for j in range(nm)]
-        sn = [f"gamma_{j}" for j in range(nsl)]
+        dn, mn, sn = variable_names(nlp)
         return MocoTrajectory((tf - t0) * grid + t0, list(rep.state_names), list(rep.control_names),
                               mn, dn, sn, [], S, Cm, Mu, D, Lg)
 

@@ -195,3 +195,19 @@ def test_sharded_solve_takes_the_unsharded_steps(case, N, world, iters):
         p.join(300)
         assert p.exitcode == 0
     assert list(out) == [1] * world
+
+
+def test_sweep_rank_partition():
+    """configs[4] over W ranks (mocohip.batchsolve.rank_share): every one
+    of the 64 subjects is solved by exactly one rank, the shares differ by at
+    most one solve, and W = 1 keeps the sweep's order."""
+    from mocohip.batchsolve import rank_share, sweep
+    s = sweep(64)
+    assert len(set(s)) == 64
+    for W in (1, 2, 3, 4, 8):
+        parts = [rank_share(s, r, W) for r in range(W)]
+        assert sorted(sum(parts, [])) == sorted(s)
+        assert max(map(len, parts)) - min(map(len, parts)) <= 1
+    assert rank_share(s, 0, 1) == s
+    with pytest.raises(ValueError):
+        rank_share(s, 8, 8)

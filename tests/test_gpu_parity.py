@@ -834,8 +834,7 @@ def test_pruned_tasks_bit_identical(name):
                                      {"MOCOHIP_IV_QFUSE": "0", "MOCOHIP_CTPL": "0"},
                                      {"MOCOHIP_IV_XCD": "0"},
                                      {"MOCOHIP_GROUPS_XCD": "0"},
-                                     {"MOCOHIP_CSPLIT": "0"},
-                                     {"MOCOHIP_CSPLIT": "0", "MOCOHIP_IVG_THREADS": "1024"}])
+                                     {"MOCOHIP_IVG_THREADS": "1024"}])
 def test_kernel_variants_bit_identical(name, variant):
     """The default k_interval (combine + transcription per mesh interval,
     raw outputs in LDS) writes exactly what k_interval writes through
@@ -968,13 +967,19 @@ def test_group_kernel_split_bit_identical(name):
 def test_combine_variants_bit_identical(name):
     """Split path (k_combine + k_transcribe): the combine with the group
     results staged in LDS (k_combine) or read from global memory
-    (k_combine_global; chosen where the LDS-staged kernel spills) write
-    identical lanes, g and Jacobian."""
+    (k_combine_split, its sums over a workgroup's waves, and
+    k_combine_global, one thread per lane role; chosen where the LDS-staged
+    kernel spills) write identical lanes, g and Jacobian."""
     a, _, _ = _pair(name, env={"MOCOHIP_COMBINE": "lds", "MOCOHIP_INTERVAL": "0"})
     b, _, _ = _pair(name, env={"MOCOHIP_COMBINE": "global", "MOCOHIP_INTERVAL": "0"})
+    # the global-memory combine as one thread per lane role (k_combine_global)
+    # and with its sums over a workgroup's waves (k_combine_split, default)
+    c, _, _ = _pair(name, env={"MOCOHIP_COMBINE": "global", "MOCOHIP_INTERVAL": "0", "MOCOHIP_CSPLIT": "0"})
     for _, x in _iterates(a):
         assert np.array_equal(a.eval_g(x), b.eval_g(x), equal_nan=True)
         assert np.array_equal(a.eval_jac_g(x), b.eval_jac_g(x), equal_nan=True)
+        assert np.array_equal(c.eval_g(x), b.eval_g(x), equal_nan=True)
+        assert np.array_equal(c.eval_jac_g(x), b.eval_jac_g(x), equal_nan=True)
 
 
 def test_work_accounting():

@@ -126,3 +126,15 @@ def test_gait_track_problem_layout():
                                            "std_testMocoTrackGait10dof18musc_solution.npz"))
     assert [str(l) for l in d["labels"]][1:] == rep.state_names + rep.control_names
     assert d["data"].shape[0] == nlp.G
+
+
+def test_ipopt_linear_solver_option_ignored():
+    """An Ipopt option dictionary's linear_solver ('mumps', the value
+    MocoCasADiSolver / tropter hand Ipopt) names Ipopt's sparse
+    factorization, not the Newton systems' back end here: it is ignored, and
+    this option's own values still apply."""
+    from mocohip.ipm import IpmOptions
+    assert IpmOptions.from_ipopt({"linear_solver": "mumps", "tol": 1e-6}).linear_solver == "auto"
+    assert IpmOptions.from_ipopt({"linear_solver": "ma27"}).linear_solver == "auto"
+    assert IpmOptions.from_ipopt({"linear_solver": "host"}).linear_solver == "host"
+    assert IpmOptions.from_ipopt({"linear_solver": "mumps", "tol": 1e-6}).tol == 1e-6

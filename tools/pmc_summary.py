@@ -17,7 +17,19 @@ import os
 import sys
 
 KERNELS = {"k_groups": "k_groups<", "k_combine": "k_combine<", "k_transcribe": "k_transcribe(",
-           "k_transcribe_gs": "k_transcribe_gs(", "k_interval": "k_interval<", "k_eval": "k_eval<"}
+           "k_transcribe_gs": "k_transcribe_gs(", "k_interval": "k_interval<", "k_eval": "k_eval<",
+           "k_combine_split": "k_combine_split<"}
+
+
+def _short(name):
+    """The table key of a kernel: k_interval's 256-thread instantiation (the
+    eval_g launches of the separate step) as k_interval_256."""
+    for short, pat in KERNELS.items():
+        if pat in name:
+            if short == "k_interval" and ", 256>" in name:
+                return "k_interval_256"
+            return short
+    return None
 
 
 def means(path, counter):
@@ -26,15 +38,24 @@ def means(path, counter):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] != counter:
                 continue
-            for short, pat in KERNELS.items():
-                if pat in r["Kernel_Name"]:
-                    acc[short].append(float(r["Counter_Value"]))
+            short = _short(r["Kernel_Name"])
+            if short:
+                acc[short].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in acc.items()}
 
 
 def main(d, workload, out):
     fetch = means(os.path.join(d, "pmc_fetch"), "FETCH_SIZE")
     write = means(os.path.join(d, "pmc_write"), "WRITE_SIZE")
+    # the separate step's passes (eval_g's own launches: k_interval_256 and
+    # its k_groups, which the fused step does not run)
+    fs = means(os.path.join(d, "pmc_fetch_sep"), "FETCH_SIZE")
+    ws = means(os.path.join(d, "pmc_write_sep"), "WRITE_SIZE")
+    for k in ("k_interval_256",):
+        if k in fs:
+            fetch[k] = fs[k]
+        if k in ws:
+            write[k] = ws[k]
     ks = {}
     for k in sorted(set(fetch) | set(write)):
         f, w = fetch.get(k), write.get(k)

@@ -22,5 +22,13 @@ timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_wr
     -- python3 $B --mode fused > "$OUT/pmc_write.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU --output-format csv -d "$OUT/pmc_sq" -o run \
     -- python3 $B --mode fused > "$OUT/pmc_sq.log" 2>&1
+# the separate step: eval_g's own launches (k_interval<D, 256> and its
+# k_groups) beside eval_jac_g's
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_sep" -o run \
+    -- python3 $B --mode separate > "$OUT/pmc_fetch_sep.log" 2>&1
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_sep" -o run \
+    -- python3 $B --mode separate > "$OUT/pmc_write_sep.log" 2>&1
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU --output-format csv -d "$OUT/pmc_sq_sep" -o run \
+    -- python3 $B --mode separate > "$OUT/pmc_sq_sep.log" 2>&1
 python3 "$ROOT/tools/pmc_summary.py" "$OUT" "N=200,fd=forward" "$OUT/pmc.json" > "$OUT/pmc_summary.log" 2>&1
 echo "profile done: $OUT"
