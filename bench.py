@@ -616,15 +616,16 @@ def one_gpu_host_inclusive(cx, args, build):
     if cx.rank == 0:
         nlp = make_nlp(cx, build(), blocking=False)
         x = track_iterate(nlp, 0)
+        from mocohip import abi
         xh = torch.from_numpy(np.ascontiguousarray(x)).pin_memory()
         gh = torch.empty(nlp.m, dtype=torch.float64).pin_memory()
         vh = torch.empty(nlp.nnz, dtype=torch.float64).pin_memory()
-        xp, gp, vp = (t.numpy().ctypes.data for t in (xh, gh, vh))
-        import ctypes as C
+        xn, gn, vn = xh.numpy(), gh.numpy(), vh.numpy()
+        xp, gp, vp = abi.dptr(xn), abi.dptr(gn), abi.dptr(vn)
 
         def step():
-            nlp.lib.mh_eval_g(nlp.ctx, C.c_void_p(xp), 1, C.c_void_p(gp))
-            nlp.lib.mh_eval_jac_g(nlp.ctx, C.c_void_p(xp), 0, C.c_void_p(vp))
+            nlp.lib.mh_eval_g(nlp.ctx, xp, 1, gp)
+            nlp.lib.mh_eval_jac_g(nlp.ctx, xp, 0, vp)
         for _ in range(max(10, args.warmup // 10)):
             step()
         k = max(50, args.steps // 4)

@@ -2113,7 +2113,7 @@ struct mh_ctx {
     int role_threads = 256;        // k_role workgroup size (MOCOHIP_ROLE_THREADS: 64..512)
     int iv_threads = 1024;         // k_interval workgroup size, Jacobian lanes (MOCOHIP_IV_THREADS: 256..1024)
     int ivg_threads = 256;         // k_interval workgroup size, eval_g lanes (MOCOHIP_IVG_THREADS: 64..1024)
-    int csplit = 1;                // large models' combine: k_combine_split (MOCOHIP_CSPLIT=0: k_combine_global)
+    int csplit = 0;                // large models' combine as k_combine_split (opt-in, MOCOHIP_CSPLIT=1)
     bool role_couple = true;       // coupling in k_role's time role (MOCOHIP_ROLE_COUPLE=0: k_couple)
     bool use_ctpl = true;          // MOCOHIP_CTPL=0: k_interval assembles through jac_entry
     float timings[4] = {0, 0, 0, 0};
@@ -2343,7 +2343,7 @@ static int launch_tasks(mh_ctx* c, const Src& S, const Lanes& ln, const TaskSet&
         const bool xs = c->d_exc_slot && &ts == &c->ts_jac;
         const int per = xs ? ln.stride - c->n_exc_gen : ln.stride;
         const long lanes = (long)ts.dev.nk * per;
-        // the sums over the waves (k_combine_split) unless MOCOHIP_CSPLIT=0
+        // the sums over the waves (k_combine_split, MOCOHIP_CSPLIT=1; slower)
         if (c->csplit && D::NSUM > 0)
             hipLaunchKernelGGL(k_combine_split<D>, dim3((unsigned)((lanes + 63) / 64)), dim3(256), 0,
                     c->stream, c->M, S, ln, ts.dev, T, H, times, Y, (long)D::NO * ln.stride,

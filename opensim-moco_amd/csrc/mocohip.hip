@@ -1702,13 +1702,15 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
         // 7.5 MB per launch, profiles/r04_xcd); MOCOHIP_IV_XCD=0: plain order
         const char* ex = std::getenv("MOCOHIP_IV_XCD");
         c->iv_xcd = ex && std::strcmp(ex, "0") == 0 ? 0 : 1;
-        // the combine of a large model's lanes (k_combine_global's case):
+        // the combine of a large model's lanes (k_combine_global's case) with
         // its independent sums spread over a workgroup's waves, then the
         // factorization and solves per lane role (k_combine_split: D::
-        // combine_sum / combine_finish); MOCOHIP_CSPLIT=0: k_combine_global
-        // (one thread per lane role does all of it, D::combine)
+        // combine_sum / combine_finish): opt-in, MOCOHIP_CSPLIT=1 -- measured
+        // slower (configs[3]: DAE stage 0.39 -> 0.47 ms, 1,585 -> 1,380
+        // calls/s, profiles/r05_c; so was the same split inside k_interval,
+        // profiles/r05_b): the combine is not bound by its sums' chains
         const char* ecs = std::getenv("MOCOHIP_CSPLIT");
-        c->csplit = ecs && std::strcmp(ecs, "0") == 0 ? 0 : 1;
+        c->csplit = ecs && std::strcmp(ecs, "1") == 0 ? 1 : 0;
         // hipGraph replay of the stages: measured slower than direct launches
         // on ROCm 7.2 for this sequence (opt-in, MOCOHIP_GRAPHS=1)
         const char* eg = std::getenv("MOCOHIP_GRAPHS");

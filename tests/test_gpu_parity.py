@@ -972,9 +972,9 @@ def test_combine_variants_bit_identical(name):
     kernel spills) write identical lanes, g and Jacobian."""
     a, _, _ = _pair(name, env={"MOCOHIP_COMBINE": "lds", "MOCOHIP_INTERVAL": "0"})
     b, _, _ = _pair(name, env={"MOCOHIP_COMBINE": "global", "MOCOHIP_INTERVAL": "0"})
-    # the global-memory combine as one thread per lane role (k_combine_global)
-    # and with its sums over a workgroup's waves (k_combine_split, default)
-    c, _, _ = _pair(name, env={"MOCOHIP_COMBINE": "global", "MOCOHIP_INTERVAL": "0", "MOCOHIP_CSPLIT": "0"})
+    # the global-memory combine as one thread per lane role (k_combine_global,
+    # default) and with its sums over a workgroup's waves (k_combine_split)
+    c, _, _ = _pair(name, env={"MOCOHIP_COMBINE": "global", "MOCOHIP_INTERVAL": "0", "MOCOHIP_CSPLIT": "1"})
     for _, x in _iterates(a):
         assert np.array_equal(a.eval_g(x), b.eval_g(x), equal_nan=True)
         assert np.array_equal(a.eval_jac_g(x), b.eval_jac_g(x), equal_nan=True)
