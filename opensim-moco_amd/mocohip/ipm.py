@@ -74,10 +74,14 @@ class IpmOptions:
     mu_min: float = 1e-11
     # the tol-derived floor of Ipopt 3.12's monotone barrier update
     # (MonotoneMuUpdate::CalcNewMuAndTau: mu >= min(tol, compl_inf_tol) /
-    # (barrier_tol_factor + 1)).  Off by default: measured on the two
-    # reference golden solves ("Solves"), the floor
-    # stops MocoInverse Rajagopal-18 at objective 1.1259 (controls RMS 0.025
-    # against its golden file) where mu_min alone reaches 1.08769 (RMS 0.0018)
+    # (barrier_tol_factor + 1)).  Off by default: the reference's golden
+    # MocoInverse solution sits at a barrier parameter ~1e-6 (its
+    # activations' distances to their bounds times this solve's bound
+    # multipliers), the unfloored sequence's last mu (1.8e-6), where the
+    # floor would hold mu at 9.1e-5 -- and the floored solve is exactly the
+    # barrier problem's solution there (objective 1.1260, controls RMS 0.026
+    # against the file, over testMocoInverse's 1e-2), not an early stop:
+    # tests/test_mu_floor.py, tools/mu_floor_probe.py
     mu_floor_from_tol: bool = False
     kappa_eps: float = 10.0
     kappa_mu: float = 0.2
