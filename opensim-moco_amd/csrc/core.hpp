@@ -542,6 +542,35 @@ struct TaskLoadGlobal {
     }
 };
 
+// eval_g's lanes (stride 1: the base role only).  Every group then has one
+// slot, so build_taskset puts group g (g > 0) at the prefix sum of GROUP_NF
+// over groups 1 .. g - 1 and the mass factor at 0 -- offsets known at
+// compile time.  Reading them as constants makes the combine's group-result
+// reads plain loads at immediate offsets instead of each waiting on a scalar
+// load of the slot table (the same values, bit for bit; the table path is
+// MOCOHIP_IVG_BASE=0).
+template <class D>
+struct BaseSlots {
+    int off[D::NG];
+    constexpr BaseSlots() : off{} {
+        int s = 0;
+        for (int g = 0; g < D::NG; ++g) {
+            off[g] = g > 0 ? s : 0;
+            if (g > 0) s += D::GROUP_NF[g];
+        }
+    }
+};
+template <class D, class P>
+struct TaskLoadBase {
+    P sT;
+    P sH;
+    __device__ __forceinline__ double operator()(int g, int f) const {
+        constexpr BaseSlots<D> B{};
+        return sT[B.off[g] + f];
+    }
+    __device__ __forceinline__ double h(int f) const { return sH[f]; }
+};
+
 // cmap (nmap roles per grid point): the lanes to combine, the others being
 // excitation lanes k_exc_fill writes (null: every lane).
 template <class D>
@@ -1135,13 +1164,17 @@ constexpr int CT_NCONST = 12;
 // H) instead of staging them in LDS -- a third of the LDS, so that several
 // interval blocks share a CU (the batched launches, where many blocks queue);
 // the same arithmetic in the same order, bit for bit.
-template <class D, bool GM>
+// BASE: eval_g's kernel (stride-1 lanes, no Jacobian values): the combine
+// reads the group results at their compile-time base slots (TaskLoadBase)
+// and the assembly is compiled out.
+template <class D, bool GM, bool BASE = false>
 __device__ __forceinline__ void interval_body(const DevModel& M, const Src& S, const Lanes& Ln, const Tasks& TK,
         const Layout& L, const Interval& I, const TplEntry* __restrict__ tpl, const uint32_t* __restrict__ ctpl,
         const int* __restrict__ ctgen, int nctgen,
         const double* __restrict__ T, const double* __restrict__ H, double* __restrict__ g,
         double* __restrict__ values, int il) {
     extern __shared__ double smem[];
+    if constexpr (BASE) values = nullptr;
     const int i = I.ib + il;
     int k_first, k_last;
     interval_span(I, i, k_first, k_last);
@@ -1183,7 +1216,13 @@ __device__ __forceinline__ void interval_body(const DevModel& M, const Src& S, c
         const double t = lane_time(Ln, S.grid[k_first + p], t0, tf, r, in.pi, in.step);
         if (r == Ln.base) sTimes[p] = t;
         const LdsOut out{lds(sY + p * ny + r), Ln.stride};
-        if constexpr (GM) {
+        if constexpr (BASE && GM) {
+            const TaskLoadBase<D, const double*> TL{T + (long)(kl0 + p) * nt, H + (long)(kl0 + p) * nh};
+            D::combine(M, t, in, TL, out);
+        } else if constexpr (BASE) {
+            const TaskLoadBase<D, const lds_double*> TL{lds(sT + p * nt), lds(sH + p * nh)};
+            D::combine(M, t, in, TL, out);
+        } else if constexpr (GM) {
             const TaskLoadGlobal<D> TL{T + (long)(kl0 + p) * nt, H + (long)(kl0 + p) * nh, TK.jd, r};
             D::combine(M, t, in, TL, out);
         } else {
@@ -1195,7 +1234,7 @@ __device__ __forceinline__ void interval_body(const DevModel& M, const Src& S, c
     // D::combine_sum into LDS, then D::combine_finish -- measured slower:
     // k_interval 17.6 -> 19.7 us, eval_g's 9.9 -> 10.6 us, profiles/r05_b;
     // the combine is not bound by its sums' load-and-add chains)
-    if (Ln.stride == 1) {
+    if (BASE || Ln.stride == 1) {
         if ((int)threadIdx.x < npts) combine_lane((int)threadIdx.x, 0);
     } else {
         for (int w = threadIdx.x; w < npts * Ln.stride; w += blockDim.x) {
@@ -1413,7 +1452,7 @@ __device__ __forceinline__ int xcd_interval(int b, int nb) {
 // = 256) take the 256-thread instantiation: its combine lanes may keep up to
 // 512 VGPRs, where the 1024-thread bound (128) made a large model's combine
 // spill (Rajagopal 80: 2.9 KB of scratch per lane, ~150 us per eval_g).
-template <class D, int MAXT = 1024>
+template <class D, int MAXT = 1024, bool BASE = false>
 __global__ void __launch_bounds__(MAXT) k_interval(DevModel M, Src S, Lanes Ln, Tasks TK, Layout L,
         Interval I, const TplEntry* __restrict__ tpl, const uint32_t* __restrict__ ctpl,
         const int* __restrict__ ctgen, int nctgen,
@@ -1422,8 +1461,8 @@ __global__ void __launch_bounds__(MAXT) k_interval(DevModel M, Src S, Lanes Ln, 
     // il0: the first interval of this launch within the shard (a chunked
     // assembly, whose chunks are copied to the host while the next runs)
     const int b = (int)blockIdx.x;
-    interval_body<D, false>(M, S, Ln, TK, L, I, tpl, ctpl, ctgen, nctgen, T, H, g, values,
-                            il0 + (I.xcd ? xcd_interval(b, (int)gridDim.x) : b));
+    interval_body<D, false, BASE>(M, S, Ln, TK, L, I, tpl, ctpl, ctgen, nctgen, T, H, g, values,
+                                  il0 + (I.xcd ? xcd_interval(b, (int)gridDim.x) : b));
 }
 
 // ------------------------------------------------------------------------
@@ -1460,8 +1499,8 @@ kb_groups(const BatchItem* __restrict__ items, BatchPtrs BP, Lanes Ln, Tasks TK,
     groups_body<D>(it.M, S, Ln, TK, it.T, it.H, blockIdx.x);
 }
 
-template <class D, bool GM>
-__global__ void __launch_bounds__(1024) kb_interval(const BatchItem* __restrict__ items, BatchPtrs BP, Lanes Ln,
+template <class D, bool GM, bool BASE = false>
+__global__ void __launch_bounds__(BASE ? 256 : 1024) kb_interval(const BatchItem* __restrict__ items, BatchPtrs BP, Lanes Ln,
         Tasks TK, Layout L, Interval I0, const TplEntry* __restrict__ tpl, const uint32_t* __restrict__ ctpl,
         const int* __restrict__ ctgen, int nctgen, int with_g, int with_v, int nep, int nnz_ep) {
     // XCD-contiguous order over the whole (interval, NLP) grid (xcd_interval
@@ -1488,7 +1527,7 @@ __global__ void __launch_bounds__(1024) kb_interval(const BatchItem* __restrict_
         if (g) g += nep;
         if (v) v += nnz_ep;
     }
-    interval_body<D, GM>(it.M, S, Ln, TK, L, I, tpl, ctpl, ctgen, nctgen, it.T, it.H, g, v, il);
+    interval_body<D, GM, BASE>(it.M, S, Ln, TK, L, I, tpl, ctpl, ctgen, nctgen, it.T, it.H, g, v, il);
 }
 
 // ------------------------------------------------------------------------
@@ -2113,7 +2152,10 @@ struct mh_ctx {
     int role_threads = 256;        // k_role workgroup size (MOCOHIP_ROLE_THREADS: 64..512)
     int iv_threads = 1024;         // k_interval workgroup size, Jacobian lanes (MOCOHIP_IV_THREADS: 256..1024)
     int ivg_threads = 256;         // k_interval workgroup size, eval_g lanes (MOCOHIP_IVG_THREADS: 64..1024)
-    int csplit = 0;                // large models' combine as k_combine_split (opt-in, MOCOHIP_CSPLIT=1)
+    int csplit = 0;
+    // eval_g's k_interval reads group results at compile-time base slots
+    // (MOCOHIP_IVG_BASE, default 1)
+    int ivg_base = 1;                // large models' combine as k_combine_split (opt-in, MOCOHIP_CSPLIT=1)
     bool role_couple = true;       // coupling in k_role's time role (MOCOHIP_ROLE_COUPLE=0: k_couple)
     bool use_ctpl = true;          // MOCOHIP_CTPL=0: k_interval assembles through jac_entry
     float timings[4] = {0, 0, 0, 0};
@@ -2411,7 +2453,10 @@ static void be_batch(mh_batch* bt, int mode, const BatchPtrs& BP, int with_g, in
     double *g0 = nullptr, *v0 = nullptr;
     const Interval I = make_interval(c, g0, v0);
     const size_t lds = bt->gm ? interval_lds_gm<D>(c, ln) : interval_lds<D>(c, ln, ts);
-    auto kern = bt->gm ? kb_interval<D, true> : kb_interval<D, false>;
+    // eval_g (stride-1 lanes, no values, 256 threads): the base-slot kernel
+    const bool base = !with_v && ln.stride == 1 && c->ivg_base;
+    auto kern = bt->gm ? (base ? kb_interval<D, true, true> : kb_interval<D, true>)
+                       : (base ? kb_interval<D, false, true> : kb_interval<D, false>);
     if (lds > 65536)
         (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     const unsigned threads = with_v ? (unsigned)bt->threads : 256u;
@@ -2447,6 +2492,9 @@ static void be_interval(mh_ctx* c, const double* x, int mode, double* g, double*
     const size_t lds = interval_lds<D>(c, ln, ts);
     const unsigned threads = v ? (unsigned)c->iv_threads : (unsigned)c->ivg_threads;
     auto kern = threads <= 256 ? k_interval<D, 256> : k_interval<D, 1024>;
+    // eval_g's launches: the base-slot kernel (MOCOHIP_IVG_BASE=0: the
+    // slot-table path, bit-identical)
+    if (!v && ln.stride == 1 && threads <= 256 && c->ivg_base) kern = k_interval<D, 256, true>;
     if (lds > 65536)
         (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (i1 < 0) { i0 = 0; i1 = c->ie - c->ib; }

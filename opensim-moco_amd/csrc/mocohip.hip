@@ -483,6 +483,17 @@ struct Arena {
 // the tasks of the grid points whose intervals k_interval hands to XCD c
 // (xcd_interval: one contiguous run of nint intervals per XCD; pts_per = 2
 // Hermite-Simpson, 1 trapezoidal) run in blocks b with b % 8 = c.
+// Stride-1 task sets put every group at its base slot, the prefix sum of
+// GROUP_NF (the mass factor at 0): what eval_g's base-slot kernel
+// (core.hpp TaskLoadBase) assumes at compile time.  Checked once per context.
+static bool base_slots_match(const TaskInfo& ti, const TaskSet& ts) {
+    int s = 0;
+    for (int g = 0; g < ti.ng; ++g) {
+        if (ts.jd[(size_t)g] != (g > 0 ? s : 0)) return false;
+        if (g > 0) s += ti.group_nf[g];
+    }
+    return true;
+}
 static void build_taskset(const TaskInfo& ti, const Lanes& ln, int nk, int nsimd, TaskSet& ts,
         int nint = 0, int pts_per = 2) {
     const char* env = std::getenv("MOCOHIP_TASKS");
@@ -1711,6 +1722,14 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
         // profiles/r05_b): the combine is not bound by its sums' chains
         const char* ecs = std::getenv("MOCOHIP_CSPLIT");
         c->csplit = ecs && std::strcmp(ecs, "1") == 0 ? 1 : 0;
+        // eval_g's k_interval with the group results at compile-time base
+        // slots (core.hpp TaskLoadBase; MOCOHIP_IVG_BASE=0: the slot table)
+        const char* eb = std::getenv("MOCOHIP_IVG_BASE");
+        c->ivg_base = eb && std::strcmp(eb, "0") == 0 ? 0 : 1;
+        const TaskInfo* tib = backend_tasks(c->be);
+        if (c->ivg_base && (c->lanes_g.stride != 1 || !tib || c->ts_g.jd.size() < (size_t)tib->ng ||
+                            !base_slots_match(*tib, c->ts_g)))
+            c->ivg_base = 0;
         // hipGraph replay of the stages: measured slower than direct launches
         // on ROCm 7.2 for this sequence (opt-in, MOCOHIP_GRAPHS=1)
         const char* eg = std::getenv("MOCOHIP_GRAPHS");
@@ -2997,7 +3016,7 @@ extern "C" int mh_get_backend_flags(const mh_ctx* c, char* flags, int32_t len) {
     if (!c || !flags || len <= 0) return set_err(MH_ERR_INVALID, "bad argument");
     std::string f = c->be->tasks ? "tasks" : (std::strncmp(c->be->name, "generic", 7) == 0 ? "generic" : "lane");
     f += c->use_interval[1] ? " interval" : " split";
-    if (c->use_interval[0]) f += " interval-g";
+    if (c->use_interval[0]) f += c->ivg_base ? " interval-g base-slots" : " interval-g";
     if (!c->use_ctpl) f += " no-ctpl";
     if (c->use_roles && c->use_interval[1]) f += " roles";
     if (c->quot) f += " quot";
