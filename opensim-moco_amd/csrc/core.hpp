@@ -451,7 +451,9 @@ __device__ __forceinline__ void groups_body(const DevModel& M, const Src& S, con
     kl += (kl + 1) * n <= tc ? 1 : 0;
     kl -= kl * n > tc ? 1 : 0;
     const int j = tc - kl * n;
-    const int r = TK.roles[g * TK.stride + j];
+    // stride-1 lanes (eval_g): every task is the base role -- no dependent
+    // load of the role table in front of the group's input loads
+    const int r = TK.stride == 1 ? Ln.base : TK.roles[g * TK.stride + j];
     double t;
     const LaneIn<D> in = lane_input<D>(S, Ln, kl, r, t);
     constexpr int NOUT = D::NST > D::NF ? D::NST : D::NF;
@@ -1452,7 +1454,7 @@ __device__ __forceinline__ int xcd_interval(int b, int nb) {
 // = 256) take the 256-thread instantiation: its combine lanes may keep up to
 // 512 VGPRs, where the 1024-thread bound (128) made a large model's combine
 // spill (Rajagopal 80: 2.9 KB of scratch per lane, ~150 us per eval_g).
-template <class D, int MAXT = 1024, bool BASE = false>
+template <class D, int MAXT = 1024, bool BASE = false, bool GM = false>
 __global__ void __launch_bounds__(MAXT) k_interval(DevModel M, Src S, Lanes Ln, Tasks TK, Layout L,
         Interval I, const TplEntry* __restrict__ tpl, const uint32_t* __restrict__ ctpl,
         const int* __restrict__ ctgen, int nctgen,
@@ -1461,8 +1463,8 @@ __global__ void __launch_bounds__(MAXT) k_interval(DevModel M, Src S, Lanes Ln, 
     // il0: the first interval of this launch within the shard (a chunked
     // assembly, whose chunks are copied to the host while the next runs)
     const int b = (int)blockIdx.x;
-    interval_body<D, false, BASE>(M, S, Ln, TK, L, I, tpl, ctpl, ctgen, nctgen, T, H, g, values,
-                                  il0 + (I.xcd ? xcd_interval(b, (int)gridDim.x) : b));
+    interval_body<D, GM, BASE>(M, S, Ln, TK, L, I, tpl, ctpl, ctgen, nctgen, T, H, g, values,
+                               il0 + (I.xcd ? xcd_interval(b, (int)gridDim.x) : b));
 }
 
 // ------------------------------------------------------------------------
@@ -2155,7 +2157,8 @@ struct mh_ctx {
     int csplit = 0;
     // eval_g's k_interval reads group results at compile-time base slots
     // (MOCOHIP_IVG_BASE, default 1)
-    int ivg_base = 1;                // large models' combine as k_combine_split (opt-in, MOCOHIP_CSPLIT=1)
+    int ivg_base = 1;
+    int ivg_gm = 0;                // large models' combine as k_combine_split (opt-in, MOCOHIP_CSPLIT=1)
     bool role_couple = true;       // coupling in k_role's time role (MOCOHIP_ROLE_COUPLE=0: k_couple)
     bool use_ctpl = true;          // MOCOHIP_CTPL=0: k_interval assembles through jac_entry
     float timings[4] = {0, 0, 0, 0};
@@ -2489,12 +2492,17 @@ static void be_interval(mh_ctx* c, const double* x, int mode, double* g, double*
                 c->d_ctgen, (int)c->ctgen.size(), c->d_xch, g, v);
         return;
     }
-    const size_t lds = interval_lds<D>(c, ln, ts);
+    size_t lds = interval_lds<D>(c, ln, ts);
     const unsigned threads = v ? (unsigned)c->iv_threads : (unsigned)c->ivg_threads;
     auto kern = threads <= 256 ? k_interval<D, 256> : k_interval<D, 1024>;
     // eval_g's launches: the base-slot kernel (MOCOHIP_IVG_BASE=0: the
-    // slot-table path, bit-identical)
-    if (!v && ln.stride == 1 && threads <= 256 && c->ivg_base) kern = k_interval<D, 256, true>;
+    // slot-table path, bit-identical); MOCOHIP_IVG_GM=1: its three combine
+    // lanes read the group results from global memory at their constant
+    // offsets instead of a staging pass through LDS
+    if (!v && ln.stride == 1 && threads <= 256 && c->ivg_base) {
+        kern = c->ivg_gm ? k_interval<D, 256, true, true> : k_interval<D, 256, true>;
+        if (c->ivg_gm) lds = interval_lds_gm<D>(c, ln);
+    }
     if (lds > 65536)
         (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (i1 < 0) { i0 = 0; i1 = c->ie - c->ib; }

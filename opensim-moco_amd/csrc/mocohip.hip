@@ -1726,6 +1726,8 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
         // slots (core.hpp TaskLoadBase; MOCOHIP_IVG_BASE=0: the slot table)
         const char* eb = std::getenv("MOCOHIP_IVG_BASE");
         c->ivg_base = eb && std::strcmp(eb, "0") == 0 ? 0 : 1;
+        const char* egm = std::getenv("MOCOHIP_IVG_GM");
+        c->ivg_gm = egm && std::strcmp(egm, "1") == 0 ? 1 : 0;
         const TaskInfo* tib = backend_tasks(c->be);
         if (c->ivg_base && (c->lanes_g.stride != 1 || !tib || c->ts_g.jd.size() < (size_t)tib->ng ||
                             !base_slots_match(*tib, c->ts_g)))
