@@ -573,86 +573,9 @@ struct TaskLoadBase {
     __device__ __forceinline__ double h(int f) const { return sH[f]; }
 };
 
-// The Jacobian lanes' slots, computed instead of loaded from the slot table.
-// build_taskset gives group g its base slot, then one slot per lane role that
-// perturbs it, in role order: the directions whose input g reads
-// (GROUP_READS) or, for the t0 / tf directions, whose time it reads
-// (GROUP_TIME); with central differences the second half's roles follow the
-// first half's.  So role r's slot j in group g is 0 when r is the base or
-// does not perturb g, else 1 + (second half: the group's perturbing
-// directions) + the perturbing directions before r's; its offset is
-// off[g] + j nf[g], off[g] the prefix sum of (1 + perturbing roles) nf over
-// the groups 1 .. g - 1 -- all compile-time per finite-difference kind but
-// the lane's direction.  The host checks the formula against the table once
-// per context (mh_ctx::jslot; MOCOHIP_JSLOT=0: the table).
-constexpr int cpop64(unsigned long long v) {
-    int n = 0;
-    while (v) { v &= v - 1; ++n; }
-    return n;
-}
-template <class D>
-struct JacSlots {
-    int nhit[D::NG];
-    int offf[D::NG];   // one perturbed lane per direction (forward / backward)
-    int offc[D::NG];   // two (central)
-    constexpr JacSlots() : nhit{}, offf{}, offc{} {
-        int sf = 0, sc = 0;
-        for (int g = 0; g < D::NG; ++g) {
-            int n = D::GROUP_TIME[g] ? 2 : 0;
-            for (int w = 0; w < D::RW; ++w) n += cpop64(D::GROUP_READS[g][w]);
-            nhit[g] = n;
-            offf[g] = g > 0 ? sf : 0;
-            offc[g] = g > 0 ? sc : 0;
-            if (g > 0) {
-                sf += (1 + n) * D::GROUP_NF[g];
-                sc += (1 + 2 * n) * D::GROUP_NF[g];
-            }
-        }
-    }
-};
-template <class D, class P>
-struct TaskLoadArith {
-    P sT;
-    P sH;
-    int dir;       // the lane's direction (-1: the base lane)
-    int second;    // central differences, second half
-    int central;
-    __device__ __forceinline__ int slot(int g) const {
-        constexpr JacSlots<D> J{};
-        if (dir < 0) return 0;
-        const bool tm = D::GROUP_TIME[g] != 0;
-        bool hit;
-        int before;
-        if (dir < 2) {
-            hit = tm;
-            before = (dir == 1 && tm) ? 1 : 0;
-        } else {
-            const int i = dir - 2, iw = i >> 6, ib = i & 63;
-            unsigned long long word = 0;
-            int cnt = tm ? 2 : 0;
-#pragma unroll
-            for (int w = 0; w < D::RW; ++w) {
-                if (w == iw) word = D::GROUP_READS[g][w];
-                if (w < iw) cnt += cpop64(D::GROUP_READS[g][w]);
-            }
-            hit = (word >> ib) & 1ULL;
-            before = cnt + __builtin_popcountll(word & ((1ULL << ib) - 1ULL));
-        }
-        return hit ? 1 + (second ? J.nhit[g] : 0) + before : 0;
-    }
-    __device__ __forceinline__ double operator()(int g, int f) const {
-        constexpr JacSlots<D> J{};
-        const int off = central ? J.offc[g] : J.offf[g];
-        return sT[off + slot(g) * D::GROUP_NF[g] + f];
-    }
-    __device__ __forceinline__ double h(int f) const { return sH[slot(0) * D::NST + f]; }
-};
-
 // cmap (nmap roles per grid point): the lanes to combine, the others being
 // excitation lanes k_exc_fill writes (null: every lane).
-// SL: the slots -- 0 the table, 1 eval_g's compile-time base slots
-// (TaskLoadBase), 2 the Jacobian lanes' computed slots (TaskLoadArith).
-template <class D, int SL = 0>
+template <class D>
 __global__ void __launch_bounds__(64) k_combine_global(DevModel M, Src S, Lanes Ln, Tasks TK,
         const double* __restrict__ T, const double* __restrict__ H, double* __restrict__ times,
         double* __restrict__ Y, long ystride_pt, const int* __restrict__ cmap, int nmap) {
@@ -665,19 +588,9 @@ __global__ void __launch_bounds__(64) k_combine_global(DevModel M, Src S, Lanes 
     double t;
     const LaneIn<D> in = lane_input<D>(S, Ln, kl, r, t);
     if (r == Ln.base && times) times[kl] = t;
-    const double* Tk = T + (long)kl * TK.tdoubles;
-    const double* Hk = H + (long)kl * TK.nmass * D::NST;
-    const StridedOut out{Y + (long)kl * ystride_pt + r, (long)Ln.stride};
-    if constexpr (SL == 1) {
-        D::combine(M, t, in, TaskLoadBase<D, const double*>{Tk, Hk}, out);
-    } else if constexpr (SL == 2) {
-        const bool cen = Ln.fd == MH_FD_CENTRAL;
-        const int dir = r == Ln.base ? -1 : (cen && r >= Ln.ND ? r - Ln.ND : r);
-        D::combine(M, t, in, TaskLoadArith<D, const double*>{Tk, Hk, dir, cen && r >= Ln.ND && r != Ln.base, cen},
-                   out);
-    } else {
-        D::combine(M, t, in, TaskLoadGlobal<D>{Tk, Hk, TK.jd, r}, out);
-    }
+    const TaskLoadGlobal<D> TL{T + (long)kl * TK.tdoubles, H + (long)kl * TK.nmass * D::NST,
+                               TK.jd, r};
+    D::combine(M, t, in, TL, StridedOut{Y + (long)kl * ystride_pt + r, (long)Ln.stride});
 }
 
 // k_combine_global with the combine in two steps (D::combine_sum /
@@ -1256,7 +1169,7 @@ constexpr int CT_NCONST = 12;
 // BASE: eval_g's kernel (stride-1 lanes, no Jacobian values): the combine
 // reads the group results at their compile-time base slots (TaskLoadBase)
 // and the assembly is compiled out.
-template <class D, bool GM, bool BASE = false, bool JS = false>
+template <class D, bool GM, bool BASE = false>
 __device__ __forceinline__ void interval_body(const DevModel& M, const Src& S, const Lanes& Ln, const Tasks& TK,
         const Layout& L, const Interval& I, const TplEntry* __restrict__ tpl, const uint32_t* __restrict__ ctpl,
         const int* __restrict__ ctgen, int nctgen,
@@ -1313,12 +1226,6 @@ __device__ __forceinline__ void interval_body(const DevModel& M, const Src& S, c
             D::combine(M, t, in, TL, out);
         } else if constexpr (GM) {
             const TaskLoadGlobal<D> TL{T + (long)(kl0 + p) * nt, H + (long)(kl0 + p) * nh, TK.jd, r};
-            D::combine(M, t, in, TL, out);
-        } else if constexpr (JS) {
-            const bool cen = Ln.fd == MH_FD_CENTRAL;
-            const int dir = r == Ln.base ? -1 : (cen && r >= Ln.ND ? r - Ln.ND : r);
-            const TaskLoadArith<D, const lds_double*> TL{lds(sT + p * nt), lds(sH + p * nh), dir,
-                                                         cen && r >= Ln.ND && r != Ln.base, cen};
             D::combine(M, t, in, TL, out);
         } else {
             const TaskLoadLds<D> TL{lds(sT + p * nt), lds(sH + p * nh), TK.jd, r};
@@ -1547,7 +1454,7 @@ __device__ __forceinline__ int xcd_interval(int b, int nb) {
 // = 256) take the 256-thread instantiation: its combine lanes may keep up to
 // 512 VGPRs, where the 1024-thread bound (128) made a large model's combine
 // spill (Rajagopal 80: 2.9 KB of scratch per lane, ~150 us per eval_g).
-template <class D, int MAXT = 1024, bool BASE = false, bool GM = false, bool JS = false>
+template <class D, int MAXT = 1024, bool BASE = false, bool GM = false>
 __global__ void __launch_bounds__(MAXT) k_interval(DevModel M, Src S, Lanes Ln, Tasks TK, Layout L,
         Interval I, const TplEntry* __restrict__ tpl, const uint32_t* __restrict__ ctpl,
         const int* __restrict__ ctgen, int nctgen,
@@ -1556,8 +1463,8 @@ __global__ void __launch_bounds__(MAXT) k_interval(DevModel M, Src S, Lanes Ln, 
     // il0: the first interval of this launch within the shard (a chunked
     // assembly, whose chunks are copied to the host while the next runs)
     const int b = (int)blockIdx.x;
-    interval_body<D, GM, BASE, JS>(M, S, Ln, TK, L, I, tpl, ctpl, ctgen, nctgen, T, H, g, values,
-                                   il0 + (I.xcd ? xcd_interval(b, (int)gridDim.x) : b));
+    interval_body<D, GM, BASE>(M, S, Ln, TK, L, I, tpl, ctpl, ctgen, nctgen, T, H, g, values,
+                               il0 + (I.xcd ? xcd_interval(b, (int)gridDim.x) : b));
 }
 
 // ------------------------------------------------------------------------
@@ -2247,13 +2154,12 @@ struct mh_ctx {
     int role_threads = 256;        // k_role workgroup size (MOCOHIP_ROLE_THREADS: 64..512)
     int iv_threads = 1024;         // k_interval workgroup size, Jacobian lanes (MOCOHIP_IV_THREADS: 256..1024)
     int ivg_threads = 256;         // k_interval workgroup size, eval_g lanes (MOCOHIP_IVG_THREADS: 64..1024)
-    int csplit = 0;
+    int csplit = 0;                // large models' combine as k_combine_split (opt-in, MOCOHIP_CSPLIT=1)
     // eval_g's k_interval reads group results at compile-time base slots
-    // (MOCOHIP_IVG_BASE, default 1)
+    // (MOCOHIP_IVG_BASE, default 1), from global memory (MOCOHIP_IVG_GM;
+    // -1: by the grid point's result count, kIvgGmMaxDoubles)
     int ivg_base = 1;
-    int ivg_gm = 1;
-    // eval_jac_g's k_interval computes its lanes' slots (MOCOHIP_JSLOT)
-    int jslot = 1;                // large models' combine as k_combine_split (opt-in, MOCOHIP_CSPLIT=1)
+    int ivg_gm = -1;
     bool role_couple = true;       // coupling in k_role's time role (MOCOHIP_ROLE_COUPLE=0: k_couple)
     bool use_ctpl = true;          // MOCOHIP_CTPL=0: k_interval assembles through jac_entry
     float timings[4] = {0, 0, 0, 0};
@@ -2488,16 +2394,10 @@ static int launch_tasks(mh_ctx* c, const Src& S, const Lanes& ln, const TaskSet&
             hipLaunchKernelGGL(k_combine_split<D>, dim3((unsigned)((lanes + 63) / 64)), dim3(256), 0,
                     c->stream, c->M, S, ln, ts.dev, T, H, times, Y, (long)D::NO * ln.stride,
                     xs ? (const int*)c->d_cmb_map : nullptr, per);
-        else {
-            // the computed slots where the host found them equal to the table
-            // (the Jacobian set: c->jslot; eval_g's stride-1 set: c->ivg_base)
-            const bool jac = &ts == &c->ts_jac;
-            auto kern = jac ? (c->jslot ? k_combine_global<D, 2> : k_combine_global<D, 0>)
-                            : (c->ivg_base && ln.stride == 1 ? k_combine_global<D, 1> : k_combine_global<D, 0>);
-            hipLaunchKernelGGL(kern, dim3((unsigned)((lanes + 63) / 64)), dim3(64), 0,
+        else
+            hipLaunchKernelGGL(k_combine_global<D>, dim3((unsigned)((lanes + 63) / 64)), dim3(64), 0,
                     c->stream, c->M, S, ln, ts.dev, T, H, times, Y, (long)D::NO * ln.stride,
                     xs ? (const int*)c->d_cmb_map : nullptr, per);
-        }
         if (xs) (void)mh_launch_exc_fill(c, ts.dev.nk, D::NO, ln.stride, ln.base, ts.dev.tdoubles, T, Y);
     }
     return 0;
@@ -2538,6 +2438,9 @@ static size_t be_interval_bytes(const mh_ctx* c, int mode) {
     return interval_lds<D>(c, mode ? c->lanes_jac : c->lanes_g, mode ? c->ts_jac : c->ts_g);
 }
 // LDS bytes of k_interval reading the group results from global memory.
+// eval_g's base-slot kernel reads the group results from global memory up
+// to this many doubles per grid point, stages them in LDS above
+constexpr int kIvgGmMaxDoubles = 512;
 template <class D>
 static size_t interval_lds_gm(const mh_ctx* c, const Lanes& ln) {
     const size_t npts = c->scheme == MH_HERMITE_SIMPSON ? 3 : 2;
@@ -2598,15 +2501,16 @@ static void be_interval(mh_ctx* c, const double* x, int mode, double* g, double*
     auto kern = threads <= 256 ? k_interval<D, 256> : k_interval<D, 1024>;
     // eval_g's launches: the base-slot kernel (MOCOHIP_IVG_BASE=0: the
     // slot-table path, bit-identical), its three combine lanes reading the
-    // group results from global memory at their constant offsets: k_interval
-    // 8.2 -> 5.7 us against a staging pass through LDS first (MOCOHIP_IVG_GM=0;
-    // profiles/r05_e/ab_ivg_gm.txt)
-    // eval_jac_g's launches (1024 threads): the computed slots (core.hpp
-    // TaskLoadArith) when the host found them equal to the table
-    if (v && threads > 256 && c->jslot) kern = k_interval<D, 1024, false, false, true>;
+    // group results from global memory at their constant offsets when a grid
+    // point's results are few (gait: 190 doubles; k_interval 8.2 -> 5.7 us
+    // against a staging pass through LDS first, profiles/r05_e/ab_ivg_gm.txt),
+    // staged in LDS when they are many (Rajagopal 80: 1,111 doubles, where the
+    // global-memory reads made eval_g slower, profiles/r05_f); MOCOHIP_IVG_GM
+    // = 0 / 1 forces either
     if (!v && ln.stride == 1 && threads <= 256 && c->ivg_base) {
-        kern = c->ivg_gm ? k_interval<D, 256, true, true> : k_interval<D, 256, true>;
-        if (c->ivg_gm) lds = interval_lds_gm<D>(c, ln);
+        const bool gm = c->ivg_gm < 0 ? ts.dev.tdoubles <= kIvgGmMaxDoubles : c->ivg_gm != 0;
+        kern = gm ? k_interval<D, 256, true, true> : k_interval<D, 256, true>;
+        if (gm) lds = interval_lds_gm<D>(c, ln);
     }
     if (lds > 65536)
         (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

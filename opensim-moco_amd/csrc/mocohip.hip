@@ -494,46 +494,6 @@ static bool base_slots_match(const TaskInfo& ti, const TaskSet& ts) {
     }
     return true;
 }
-// The Jacobian task set's slots as k_interval computes them (core.hpp
-// TaskLoadArith): checked against the table once per context.
-static bool jac_slots_match(const TaskInfo& ti, const Lanes& ln, const TaskSet& ts) {
-    const bool central = ln.fd == MH_FD_CENTRAL;
-    const int ng = ti.ng, S = ln.stride, ND = ln.ND;
-    if (S != (central ? 2 * ND + 1 : ND + 1) || ln.base != S - 1) return false;
-    if (ts.jd.size() < (size_t)ng * S) return false;
-    std::vector<int> nhit(ng);
-    for (int g = 0; g < ng; ++g) {
-        int n = ti.time[g] ? 2 : 0;
-        for (int w = 0; w < ti.rw; ++w) n += __builtin_popcountll(ti.reads[(size_t)g * ti.rw + w]);
-        nhit[g] = n;
-    }
-    int off = 0;
-    for (int g = 0; g < ng; ++g) {
-        const int offg = g > 0 ? off : 0, nf = g > 0 ? ti.group_nf[g] : 1;
-        for (int r = 0; r < S; ++r) {
-            int j = 0;
-            if (r != ln.base) {
-                const bool second = central && r >= ND;
-                const int dir = second ? r - ND : r;
-                bool hit;
-                int before;
-                if (dir < 2) {
-                    hit = ti.time[g] != 0;
-                    before = (dir == 1 && ti.time[g]) ? 1 : 0;
-                } else {
-                    const int i = dir - 2;
-                    hit = (ti.reads[(size_t)g * ti.rw + i / 64] >> (i % 64)) & 1ULL;
-                    before = ti.time[g] ? 2 : 0;
-                    for (int k = 0; k < i; ++k) before += (ti.reads[(size_t)g * ti.rw + k / 64] >> (k % 64)) & 1ULL;
-                }
-                j = hit ? 1 + (second ? nhit[g] : 0) + before : 0;
-            }
-            if (ts.jd[(size_t)r * ng + g] != offg + j * nf) return false;
-        }
-        if (g > 0) off += (1 + (central ? 2 : 1) * nhit[g]) * ti.group_nf[g];
-    }
-    return true;
-}
 static void build_taskset(const TaskInfo& ti, const Lanes& ln, int nk, int nsimd, TaskSet& ts,
         int nint = 0, int pts_per = 2) {
     const char* env = std::getenv("MOCOHIP_TASKS");
@@ -1767,11 +1727,8 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
         const char* eb = std::getenv("MOCOHIP_IVG_BASE");
         c->ivg_base = eb && std::strcmp(eb, "0") == 0 ? 0 : 1;
         const char* egm = std::getenv("MOCOHIP_IVG_GM");
-        c->ivg_gm = egm && std::strcmp(egm, "0") == 0 ? 0 : 1;
+        c->ivg_gm = !egm ? -1 : std::strcmp(egm, "0") == 0 ? 0 : 1;
         const TaskInfo* tib = backend_tasks(c->be);
-        const char* ejs = std::getenv("MOCOHIP_JSLOT");
-        c->jslot = ejs && std::strcmp(ejs, "0") == 0 ? 0 : 1;
-        if (c->jslot && (!tib || !jac_slots_match(*tib, c->lanes_jac, c->ts_jac))) c->jslot = 0;
         if (c->ivg_base && (c->lanes_g.stride != 1 || !tib || c->ts_g.jd.size() < (size_t)tib->ng ||
                             !base_slots_match(*tib, c->ts_g)))
             c->ivg_base = 0;
@@ -3063,7 +3020,6 @@ extern "C" int mh_get_backend_flags(const mh_ctx* c, char* flags, int32_t len) {
     f += c->use_interval[1] ? " interval" : " split";
     if (c->use_interval[0]) f += c->ivg_base ? " interval-g base-slots" : " interval-g";
     if (!c->use_ctpl) f += " no-ctpl";
-    if (c->jslot && c->use_interval[1]) f += " computed-slots";
     if (c->use_roles && c->use_interval[1]) f += " roles";
     if (c->quot) f += " quot";
     if (c->asm_grid_stride) f += " asm-gs";

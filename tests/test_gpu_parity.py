@@ -20,7 +20,6 @@ range, everything else random within bounds): at least 99 % of every
 compared array must be regular (finite, below REGULAR), and the compared
 fraction and the largest relative error are reported on failure.
 """
-import os
 import numpy as np
 import pytest
 
@@ -310,7 +309,7 @@ def _pair(name, backend="auto", tasks=None, env=None):
                                                   "MOCOHIP_ROLES", "MOCOHIP_ROLE_COUPLE",
                                                   "MOCOHIP_IV_QFUSE", "MOCOHIP_IV_THREADS", "MOCOHIP_IV_XCD",
                                                   "MOCOHIP_GROUPS_XCD", "MOCOHIP_CSPLIT", "MOCOHIP_IVG_THREADS",
-                                                  "MOCOHIP_IVG_BASE", "MOCOHIP_IVG_GM", "MOCOHIP_JSLOT",
+                                                  "MOCOHIP_IVG_BASE", "MOCOHIP_IVG_GM",
                                                   "MOCOHIP_EXC_LANES", "MOCOHIP_G_BLOCK", "MOCOHIP_G_LDS",
                                                   "MOCOHIP_G_LDS_GUARD",
                                                   "MOCOHIP_GROUPS_SPLIT", "MOCOHIP_COMBINE",
@@ -838,8 +837,7 @@ def test_pruned_tasks_bit_identical(name):
                                      {"MOCOHIP_GROUPS_XCD": "0"},
                                      {"MOCOHIP_IVG_THREADS": "1024"},
                                      {"MOCOHIP_IVG_BASE": "0"},
-                                     {"MOCOHIP_IVG_GM": "0"},
-                                     {"MOCOHIP_JSLOT": "0"}])
+                                     {"MOCOHIP_IVG_GM": "0"}])
 def test_kernel_variants_bit_identical(name, variant):
     """The default k_interval (combine + transcription per mesh interval,
     raw outputs in LDS) writes exactly what k_interval writes through
@@ -856,12 +854,6 @@ def test_kernel_variants_bit_identical(name, variant):
         fa, fb = gpu.backend_flags().split(), split.backend_flags().split()
         assert "base-slots" not in fb
         assert ("base-slots" in fa) == ("tasks" in fa and "interval-g" in fa), fa
-    if variant == {"MOCOHIP_JSLOT": "0"}:
-        # the Jacobian lanes' computed slots against the slot table
-        fa, fb = gpu.backend_flags().split(), split.backend_flags().split()
-        assert "computed-slots" not in fb
-        if "tasks" in fa and "interval" in fa and "all" not in os.environ.get("MOCOHIP_TASKS", ""):
-            assert "computed-slots" in fa, fa
     for _, x in _iterates(gpu):
         assert np.array_equal(gpu.eval_g(x), split.eval_g(x), equal_nan=True)
         assert np.array_equal(gpu.eval_jac_g(x), split.eval_jac_g(x), equal_nan=True)
