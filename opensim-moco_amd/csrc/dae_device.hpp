@@ -68,6 +68,12 @@ struct DevModel {
     // "Structure-only specialization"; <Name>_fill at mh_create), else null
     const double* pool;
 };
+// The generated code reads the constant pool through the constant address
+// space: the pool does not change during a launch, so its wave-uniform reads
+// compile to scalar loads (SMEM through the scalar cache, into SGPRs) instead
+// of vector loads that share the lanes' input loads' queue and wait counter.
+typedef __attribute__((address_space(4))) const double kconst;
+__device__ __forceinline__ const kconst* kpool(const DevModel& M) { return (const kconst*)M.pool; }
 constexpr int MUS_DERIVED = 6;
 
 struct SV { double w0, w1, w2, v0, v1, v2; };

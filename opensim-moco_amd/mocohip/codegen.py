@@ -1244,7 +1244,9 @@ def generate(cm, struct_name: str, implicit: bool = False, prescribed: bool = Fa
                    "combine_sum": "template <class IN, class TL> ",
                    "combine_finish": "template <class IN, class TL, class SUMS, class OUT> "}[name]
             args = args.replace("const double* __restrict__ in", "const IN& in")
-        pre = ["    const double* __restrict__ K = M.pool;", "    (void)K;"]
+        # the pool through the constant address space (dae_device.hpp kpool:
+        # scalar loads)
+        pre = ["    const mh::kconst* __restrict__ K = mh::kpool(M);", "    (void)K;"]
         ret = "double" if name == "combine_sum" else "void"
         fns.append(f"    {tpl}__device__ __forceinline__ static {ret} {name}({args}) {{\n"
                    + "\n".join(pre + lines) + "\n    }")
