@@ -834,6 +834,7 @@ def test_pruned_tasks_bit_identical(name):
                                      {"MOCOHIP_IV_QFUSE": "0"},
                                      {"MOCOHIP_IV_QFUSE": "0", "MOCOHIP_CTPL": "0"},
                                      {"MOCOHIP_IV_XCD": "0"},
+                                     {"MOCOHIP_INTERVAL": "0", "MOCOHIP_IV_XCD": "0"},
                                      {"MOCOHIP_GROUPS_XCD": "0"},
                                      {"MOCOHIP_IVG_THREADS": "1024"},
                                      {"MOCOHIP_IVG_BASE": "0"},
