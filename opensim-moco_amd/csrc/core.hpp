@@ -573,13 +573,29 @@ struct TaskLoadBase {
     __device__ __forceinline__ double h(int f) const { return sH[f]; }
 };
 
+// The hardware dispatches a launch's workgroups to the 8 XCDs round-robin
+// (workgroup b -> XCD b % 8), each XCD with its own L2.  Hermite-Simpson
+// neighbours share a grid point, whose group results both intervals stage,
+// so with I.xcd workgroup b takes interval c * q + min(c, rem) + b / 8
+// (c = b % 8, q / rem = nb / 8, nb % 8): XCD c gets one contiguous run of
+// intervals and the shared point's second read can hit that XCD's L2.  A
+// bijection of 0 .. nb - 1 for every nb.
+__device__ __forceinline__ int xcd_interval(int b, int nb) {
+    const int c = b & 7, s = b >> 3, q = nb >> 3, rem = nb & 7;
+    return c * q + (c < rem ? c : rem) + s;
+}
+
 // cmap (nmap roles per grid point): the lanes to combine, the others being
 // excitation lanes k_exc_fill writes (null: every lane).
 template <class D>
 __global__ void __launch_bounds__(64) k_combine_global(DevModel M, Src S, Lanes Ln, Tasks TK,
         const double* __restrict__ T, const double* __restrict__ H, double* __restrict__ times,
-        double* __restrict__ Y, long ystride_pt, const int* __restrict__ cmap, int nmap) {
-    const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+        double* __restrict__ Y, long ystride_pt, const int* __restrict__ cmap, int nmap, int xcd) {
+    // xcd: the blocks of one grid point's lanes on one XCD (xcd_interval over
+    // the lane blocks): the lanes of a point gather from the same group
+    // results, which then cross the XCD's L2 once instead of once per XCD
+    const int blk = xcd ? xcd_interval((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+    const long gid = (long)blk * blockDim.x + threadIdx.x;
     const int per = cmap ? nmap : Ln.stride;
     if (gid >= (long)TK.nk * per) return;
     const int kl = (int)(gid / per);
@@ -1438,17 +1454,6 @@ __device__ __forceinline__ void interval_body(const DevModel& M, const Src& S, c
         endpoint_head(L, Ln, I.E, S.x, g ? I.gh : nullptr, values ? I.vh : nullptr, threadIdx.x, blockDim.x);
 }
 
-// The hardware dispatches a launch's workgroups to the 8 XCDs round-robin
-// (workgroup b -> XCD b % 8), each XCD with its own L2.  Hermite-Simpson
-// neighbours share a grid point, whose group results both intervals stage,
-// so with I.xcd workgroup b takes interval c * q + min(c, rem) + b / 8
-// (c = b % 8, q / rem = nb / 8, nb % 8): XCD c gets one contiguous run of
-// intervals and the shared point's second read can hit that XCD's L2.  A
-// bijection of 0 .. nb - 1 for every nb.
-__device__ __forceinline__ int xcd_interval(int b, int nb) {
-    const int c = b & 7, s = b >> 3, q = nb >> 3, rem = nb & 7;
-    return c * q + (c < rem ? c : rem) + s;
-}
 
 // MAXT: the launch bound.  eval_g's launches (stride-1 lanes, c->ivg_threads
 // = 256) take the 256-thread instantiation: its combine lanes may keep up to
@@ -2397,7 +2402,7 @@ static int launch_tasks(mh_ctx* c, const Src& S, const Lanes& ln, const TaskSet&
         else
             hipLaunchKernelGGL(k_combine_global<D>, dim3((unsigned)((lanes + 63) / 64)), dim3(64), 0,
                     c->stream, c->M, S, ln, ts.dev, T, H, times, Y, (long)D::NO * ln.stride,
-                    xs ? (const int*)c->d_cmb_map : nullptr, per);
+                    xs ? (const int*)c->d_cmb_map : nullptr, per, c->iv_xcd);
         if (xs) (void)mh_launch_exc_fill(c, ts.dev.nk, D::NO, ln.stride, ln.base, ts.dev.tdoubles, T, Y);
     }
     return 0;

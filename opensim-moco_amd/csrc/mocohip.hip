@@ -100,15 +100,24 @@ __global__ void __launch_bounds__(256) k_transcribe(Layout L, Interval I, Lanes 
         const double* __restrict__ grid, const double* __restrict__ times,
         const double* __restrict__ Y, double* __restrict__ g, double* __restrict__ values,
         int nchunks, int yq, int chunk) {
-    const int il = blockIdx.y;
+    // I.xcd: the chunks of one interval on one XCD (xcd_interval over the
+    // linear block id): an interval's chunks gather from the same Y run,
+    // which then crosses the XCD's L2 once instead of once per XCD
+    int il = (int)blockIdx.y, bx = (int)blockIdx.x;
+    if (I.xcd) {
+        const int gx = (int)gridDim.x;
+        const int lin = xcd_interval(il * gx + bx, gx * (int)gridDim.y);
+        il = lin / gx;
+        bx = lin - il * gx;
+    }
     const int i = I.ib + il;
     const YG YV{Y, times, L.NO, Ln.stride, L.k0, yq, x, L.NS, L.NC, L.G, L.NDV, L.DB};
-    if ((int)blockIdx.x < nchunks) {
+    if (bx < nchunks) {
         int k_first, k_last;
         interval_span(I, i, k_first, k_last);
         const IvC C = iv_const(YV.t(k_last) - YV.t(k_first), grid[k_last] - grid[k_first]);
         double* vi = values + (long)il * I.nnz_int;
-        const int e_end = min(I.entries(i), ((int)blockIdx.x + 1) * chunk);
+        const int e_end = min(I.entries(i), (bx + 1) * chunk);
         if (ctpl) {   // chunks of asm_chunk_ct entries
 #pragma clang fp contract(off)
             // the coefficient / base tables the words select from (the same
@@ -125,7 +134,7 @@ __global__ void __launch_bounds__(256) k_transcribe(Layout L, Interval I, Lanes 
             const uint32_t kone = nyall + CT_CONST + 1;
             const double* __restrict__ Yi = Y + (long)(k_first - L.k0) * L.NO * Ln.stride;
             const uint32_t* __restrict__ cbase = ctpl + I.nnz_int + I.nnz_tail;
-            const int eb = (int)blockIdx.x * chunk, ee = min(I.entries(i), eb + chunk);
+            const int eb = bx * chunk, ee = min(I.entries(i), eb + chunk);
             // the bulk, branch-free per entry: CT_U entries per thread and
             // pass (their words, then their Y values, then their stores);
             // t0 / tf (CT_GEN) and path (CT_PATH) entries are skipped here and
@@ -177,14 +186,14 @@ __global__ void __launch_bounds__(256) k_transcribe(Layout L, Interval I, Lanes 
                 if (ep >= eb && ep < ee) vi[ep] = jac_entry<true>(L, Ln, I.P, x, YV, tpl[ep], k_first, C);
             }
         } else {
-            for (int e = (int)blockIdx.x * chunk + threadIdx.x; e < e_end; e += blockDim.x)
+            for (int e = bx * chunk + threadIdx.x; e < e_end; e += blockDim.x)
                 vi[e] = jac_entry(L, Ln, I.P, x, YV, tpl[e], k_first, C);
         }
     } else {
         double* gi = g + (long)il * I.rpi;
         for (int r = threadIdx.x; r < I.rows(i); r += blockDim.x) gi[r] = defect_row(L, I, Ln, x, YV, i, r);
     }
-    if (i == 0 && blockIdx.x == 0 && (I.gh || I.vh))
+    if (i == 0 && bx == 0 && (I.gh || I.vh))
         endpoint_head(L, Ln, I.E, x, g ? I.gh : nullptr, values ? I.vh : nullptr, threadIdx.x, blockDim.x);
 }
 
