@@ -682,7 +682,11 @@ __device__ __forceinline__ void stage_lds(double* __restrict__ dst, const double
 // model's combine (Rajagopal 80: ~120 outputs, an 18-coordinate L^T L solve)
 // then runs without the scratch spills the 1024-thread bound (128 VGPRs)
 // forces on it.
-template <class D, int MAXT = 1024>
+// QUOT: the quotient mode compiled in (its per-lane out[NO] array sets the
+// register budget; raw-value launches take the instantiation without it, so
+// that a large model's combine does not spill for the quotient path it does
+// not run: Rajagopal 80's 256-thread kernel carried 8.6 KB of scratch).
+template <class D, int MAXT = 1024, bool QUOT = false>
 __global__ void __launch_bounds__(MAXT) k_combine(DevModel M, Src S, Lanes Ln, Tasks TK,
         const double* __restrict__ T, const double* __restrict__ H, double* __restrict__ times,
         double* __restrict__ Y, long ystride_pt, int quot) {
@@ -701,7 +705,8 @@ __global__ void __launch_bounds__(MAXT) k_combine(DevModel M, Src S, Lanes Ln, T
     // Y[(kl*NO + o)*stride + r]  (ystride_pt = NO*stride; explicit points:
     // stride 1 -> out[p*NO + o])
     double* Yk = Y + (long)kl * ystride_pt + r;
-    if (!quot) {   // raw lane values: each output straight to Y
+    if constexpr (!QUOT) {   // raw lane values: each output straight to Y
+        (void)quot;
         if (act) {
             double t;
             const LaneIn<D> in = lane_input<D>(S, Ln, kl, r, t);
@@ -710,7 +715,7 @@ __global__ void __launch_bounds__(MAXT) k_combine(DevModel M, Src S, Lanes Ln, T
             D::combine(M, t, in, TL, StridedOut{Yk, (long)Ln.stride});
         }
         return;
-    }
+    } else {
     double out[D::NO];
     if (act) {
         double t;
@@ -736,6 +741,7 @@ __global__ void __launch_bounds__(MAXT) k_combine(DevModel M, Src S, Lanes Ln, T
         else if (Ln.fd == MH_FD_FORWARD) v = (out[o] - y[Ln.base]) / Ln.h;
         else v = (y[Ln.base] - out[o]) / Ln.h;
         Yk[(long)o * Ln.stride] = v;
+    }
     }
 }
 
@@ -2382,7 +2388,8 @@ static int launch_tasks(mh_ctx* c, const Src& S, const Lanes& ln, const TaskSet&
     size_t lds = sizeof(double) * ((size_t)ts.dev.tdoubles + (size_t)ts.dev.nmass * D::NST);
     if (quot) lds = std::max(lds, sizeof(double) * (size_t)D::NO * ln.stride);
     if (threads <= 1024 && lds <= kMaxLds && !(!quot && combine_from_global<D>(c, threads))) {
-        auto kern = threads <= 256 ? k_combine<D, 256> : k_combine<D, 1024>;
+        auto kern = quot ? (threads <= 256 ? k_combine<D, 256, true> : k_combine<D, 1024, true>)
+                         : (threads <= 256 ? k_combine<D, 256> : k_combine<D, 1024>);
         if (lds > 65536)
             (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         hipLaunchKernelGGL(kern, dim3((unsigned)ts.dev.nk), dim3(threads), lds, c->stream, c->M,
