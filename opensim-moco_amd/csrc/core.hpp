@@ -430,10 +430,9 @@ struct Tasks {
 // (k_groups_part: a large model's heavy groups no longer set the register
 // budget, hence the occupancy, of its many light ones).
 template <class D, int CLS = 0>
-__device__ __forceinline__ void groups_body(const DevModel& M, const Src& S, const Lanes& Ln, const Tasks& TK,
-        double* __restrict__ T, double* __restrict__ H, int blk) {
+__device__ __forceinline__ void groups_body_rec(const DevModel& M, const Src& S, const Lanes& Ln, const Tasks& TK,
+        double* __restrict__ T, double* __restrict__ H, const int4 rec) {
     const int lane = threadIdx.x;
-    const int4 rec = TK.blk[blk];   // one scalar load: no dependent table chain
     // (group | live tasks << 16, first task, tasks per grid point, 1 / that)
     const int gx = __builtin_amdgcn_readfirstlane(rec.x);
     const int g = gx & 0xffff, cnt = gx >> 16;
@@ -477,10 +476,33 @@ __device__ __forceinline__ void groups_body(const DevModel& M, const Src& S, con
     }
 }
 
+template <class D, int CLS = 0>
+__device__ __forceinline__ void groups_body(const DevModel& M, const Src& S, const Lanes& Ln, const Tasks& TK,
+        double* __restrict__ T, double* __restrict__ H, int blk) {
+    groups_body_rec<D, CLS>(M, S, Ln, TK, T, H, TK.blk[blk]);   // one scalar load of the block's record
+}
+
 template <class D>
 __global__ void __launch_bounds__(64) k_groups(DevModel M, Src S, Lanes Ln, Tasks TK,
         double* __restrict__ T, double* __restrict__ H) {
     groups_body<D>(M, S, Ln, TK, T, H, blockIdx.x);
+}
+
+// eval_g's task records in the kernel arguments.  With stride-1 lanes a
+// block's record is (group | live tasks << 16, first task) -- one task per
+// grid point and group -- and up to KR_MAX of them fit beside the other
+// arguments: the record then arrives with the launch's arguments instead of
+// one load of the task table after them (a dependent round trip at the head
+// of every task wave's chain).  MOCOHIP_GROUPS_KR=0: the table.
+constexpr int KR_MAX = 384;
+struct KRecs {
+    int2 r[KR_MAX];
+};
+template <class D>
+__global__ void __launch_bounds__(64) k_groups_kr(DevModel M, Src S, Lanes Ln, Tasks TK,
+        double* __restrict__ T, double* __restrict__ H, KRecs KR) {
+    const int2 rr = KR.r[blockIdx.x];
+    groups_body_rec<D>(M, S, Ln, TK, T, H, make_int4(rr.x, rr.y, 1, __float_as_int(1.0f)));
 }
 // One class of groups (groups_body CLS), blocks blk0.. of the task table.
 template <class D, int CLS>
@@ -2176,6 +2198,9 @@ struct mh_ctx {
     float timings[4] = {0, 0, 0, 0};
     // task-decomposed back ends
     TaskSet ts_jac, ts_g, ts_probe;
+    // eval_g's task records as kernel arguments (k_groups_kr; MOCOHIP_GROUPS_KR)
+    bool krec_ok = false;
+    KRecs krec_g{};
     double *d_T = nullptr, *d_H = nullptr;     // group results of the Jacobian lanes
     double *d_Tg = nullptr, *d_Hg = nullptr;   // of the eval_g lanes (their own: the two
                                                // evaluations may run concurrently)
@@ -2351,6 +2376,13 @@ static void launch_groups(mh_ctx* c, const Src& S, const Lanes& ln, const TaskSe
                 ts.dev, T, H, 0);
         hipLaunchKernelGGL((k_groups_part<D, 2>), dim3((unsigned)(ts.nblocks - ts.nheavy)), dim3(64), 0,
                 c->stream, c->M, S, ln, ts.dev, T, H, ts.nheavy);
+        return;
+    }
+    if (&ts == &c->ts_g && c->krec_ok) {
+        static_assert(sizeof(DevModel) + sizeof(Src) + sizeof(Lanes) + sizeof(Tasks) + 2 * sizeof(double*) +
+                      sizeof(KRecs) <= 4096, "k_groups_kr: kernel arguments over 4 KB");
+        hipLaunchKernelGGL(k_groups_kr<D>, dim3((unsigned)ts.nblocks), dim3(64), 0, c->stream, c->M, S, ln, ts.dev,
+                T, H, c->krec_g);
         return;
     }
     hipLaunchKernelGGL(k_groups<D>, dim3((unsigned)ts.nblocks), dim3(64), 0, c->stream, c->M, S, ln, ts.dev, T, H);

@@ -1586,6 +1586,23 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
         build_taskset(*ti, c->lanes_g, c->nk, c->nsimd, c->ts_g, nint, ppi);
         to_jac = put_taskset(A, c->ts_jac);
         to_g = put_taskset(A, c->ts_g);
+        // eval_g's task records as kernel arguments (core.hpp k_groups_kr):
+        // stride-1 lanes, one task per grid point and group, <= KR_MAX blocks
+        {
+            const char* ekr = std::getenv("MOCOHIP_GROUPS_KR");
+            bool ok = !(ekr && std::strcmp(ekr, "0") == 0) && c->lanes_g.stride == 1 &&
+                      c->ts_g.nblocks > 0 && c->ts_g.nblocks <= KR_MAX &&
+                      c->ts_g.blk.size() >= 4 * (size_t)c->ts_g.nblocks;
+            const float one = 1.0f;
+            int one_bits;
+            std::memcpy(&one_bits, &one, sizeof one_bits);
+            for (int b = 0; ok && b < c->ts_g.nblocks; ++b) {
+                const int* r = &c->ts_g.blk[4 * (size_t)b];
+                if (r[2] != 1 || r[3] != one_bits) ok = false;
+                else c->krec_g.r[b] = make_int2(r[0], r[1]);
+            }
+            c->krec_ok = ok;
+        }
         // excitation lanes of the generated back end (k_exc_fill): the lane
         // re-evaluates exactly one group besides none of the mass factor's,
         // of one field (the activation derivative)
@@ -3028,6 +3045,7 @@ extern "C" int mh_get_backend_flags(const mh_ctx* c, char* flags, int32_t len) {
     std::string f = c->be->tasks ? "tasks" : (std::strncmp(c->be->name, "generic", 7) == 0 ? "generic" : "lane");
     f += c->use_interval[1] ? " interval" : " split";
     if (c->use_interval[0]) f += c->ivg_base ? " interval-g base-slots" : " interval-g";
+    if (c->krec_ok) f += " groups-kernarg";
     if (!c->use_ctpl) f += " no-ctpl";
     if (c->use_roles && c->use_interval[1]) f += " roles";
     if (c->quot) f += " quot";
