@@ -535,11 +535,11 @@ struct SumsLds {
 // Combine: one workgroup per grid point.  The grid point's group results
 // (contiguous in T and H) are staged in LDS with coalesced loads; each lane
 // (one lane role) then reads the slots it needs from LDS.
-template <class D>
+template <class D, class SP = const int* __restrict__>
 struct TaskLoadLds {
     const lds_double* sT;
     const lds_double* sH;
-    const int* __restrict__ slot;   // [stride][ng]: slot of group g for this role
+    SP slot;                        // [stride][ng]: slot of group g for this role
     int r;
     __device__ __forceinline__ double operator()(int g, int f) const {
         return sT[slot[r * D::NG + g] + f];
@@ -1213,7 +1213,10 @@ constexpr int CT_NCONST = 12;
 // BASE: eval_g's kernel (stride-1 lanes, no Jacobian values): the combine
 // reads the group results at their compile-time base slots (TaskLoadBase)
 // and the assembly is compiled out.
-template <class D, bool GM, bool BASE = false>
+// SLDS: the role -> slot table staged in LDS with the group results (the
+// Jacobian lanes' combine then reads its slots from LDS instead of global
+// memory after the barrier; MOCOHIP_IV_SLOTS_LDS=1).
+template <class D, bool GM, bool BASE = false, bool SLDS = false>
 __device__ __forceinline__ void interval_body(const DevModel& M, const Src& S, const Lanes& Ln, const Tasks& TK,
         const Layout& L, const Interval& I, const TplEntry* __restrict__ tpl, const uint32_t* __restrict__ ctpl,
         const int* __restrict__ ctgen, int nctgen,
@@ -1237,10 +1240,27 @@ __device__ __forceinline__ void interval_body(const DevModel& M, const Src& S, c
     double* sXd = sXc + npts * L.NC;         // [npts][NM] multipliers, [NSL] the
     double* sXm = sXd + npts * L.NDV;        // interval's slacks (HS midpoint)
     double* sXl = sXm + npts * L.NM;
+    int* sSl = (int*)(sXl + L.NSL);          // SLDS: [stride][NG] slots
     // the interval's points are consecutive local grid points: their T (and
     // H) slabs are one contiguous run each
     const int kl0 = k_first - S.k0;
     if (I.dbg_stop == 7) return;   // diagnostic: the launch floor
+    if constexpr (BASE && GM) {
+        // eval_g's combine lanes (one per grid point, the base role) start at
+        // once: their inputs from global memory, the group results at their
+        // base slots, while the other threads stage the states the g rows
+        // read -- one memory round trip after the arguments instead of the
+        // staging's round trip and barrier first (the same values: the LDS
+        // path, MOCOHIP_IVG_GM=0, compares bit for bit)
+        if ((int)threadIdx.x < npts) {
+            const int p = threadIdx.x;
+            double t;
+            const LaneIn<D> in = lane_input<D>(S, Ln, kl0 + p, Ln.base, t);
+            sTimes[p] = t;
+            const TaskLoadBase<D, const double*> TL{T + (long)(kl0 + p) * nt, H + (long)(kl0 + p) * nh};
+            D::combine(M, t, in, TL, LdsOut{lds(sY + p * ny + Ln.base), Ln.stride});
+        }
+    }
     if (!GM && nt > 0) stage_lds<16>(sT, T + (long)kl0 * nt, npts * nt);
     if (!GM && nh > 0) stage_lds<8>(sH, H + (long)kl0 * nh, npts * nh);
     stage_lds<1>(sXs, S.x + 2 + (long)k_first * L.NS, npts * L.NS);
@@ -1249,6 +1269,8 @@ __device__ __forceinline__ void interval_body(const DevModel& M, const Src& S, c
         stage_lds<1>(sXd, S.x + L.DB + (long)k_first * L.NDV, npts * L.NDV);
     if (L.NM > 0) stage_lds<1>(sXm, S.x + L.XM + (long)k_first * L.NM, npts * L.NM);
     if (L.NSL > 0) stage_lds<1>(sXl, S.x + L.XL + (long)i * L.NSL, L.NSL);
+    if constexpr (SLDS)
+        for (int q = threadIdx.x; q < Ln.stride * D::NG; q += blockDim.x) sSl[q] = TK.jd[q];
     const double t0 = S.x[0], tf = S.x[1];
     if (threadIdx.x < 2) sK[threadIdx.x] = threadIdx.x ? 1.0 : 0.0;
     __syncthreads();
@@ -1262,14 +1284,14 @@ __device__ __forceinline__ void interval_body(const DevModel& M, const Src& S, c
         const double t = lane_time(Ln, S.grid[k_first + p], t0, tf, r, in.pi, in.step);
         if (r == Ln.base) sTimes[p] = t;
         const LdsOut out{lds(sY + p * ny + r), Ln.stride};
-        if constexpr (BASE && GM) {
-            const TaskLoadBase<D, const double*> TL{T + (long)(kl0 + p) * nt, H + (long)(kl0 + p) * nh};
-            D::combine(M, t, in, TL, out);
-        } else if constexpr (BASE) {
+        if constexpr (BASE) {   // (BASE && GM combined before the staging, above)
             const TaskLoadBase<D, const lds_double*> TL{lds(sT + p * nt), lds(sH + p * nh)};
             D::combine(M, t, in, TL, out);
         } else if constexpr (GM) {
             const TaskLoadGlobal<D> TL{T + (long)(kl0 + p) * nt, H + (long)(kl0 + p) * nh, TK.jd, r};
+            D::combine(M, t, in, TL, out);
+        } else if constexpr (SLDS) {
+            const TaskLoadLds<D, const lds_int*> TL{lds(sT + p * nt), lds(sH + p * nh), (const lds_int*)sSl, r};
             D::combine(M, t, in, TL, out);
         } else {
             const TaskLoadLds<D> TL{lds(sT + p * nt), lds(sH + p * nh), TK.jd, r};
@@ -1280,7 +1302,8 @@ __device__ __forceinline__ void interval_body(const DevModel& M, const Src& S, c
     // D::combine_sum into LDS, then D::combine_finish -- measured slower:
     // k_interval 17.6 -> 19.7 us, eval_g's 9.9 -> 10.6 us, profiles/r05_b;
     // the combine is not bound by its sums' load-and-add chains)
-    if (BASE || Ln.stride == 1) {
+    if constexpr (BASE && GM) {
+    } else if (BASE || Ln.stride == 1) {
         if ((int)threadIdx.x < npts) combine_lane((int)threadIdx.x, 0);
     } else {
         for (int w = threadIdx.x; w < npts * Ln.stride; w += blockDim.x) {
@@ -1487,7 +1510,7 @@ __device__ __forceinline__ void interval_body(const DevModel& M, const Src& S, c
 // = 256) take the 256-thread instantiation: its combine lanes may keep up to
 // 512 VGPRs, where the 1024-thread bound (128) made a large model's combine
 // spill (Rajagopal 80: 2.9 KB of scratch per lane, ~150 us per eval_g).
-template <class D, int MAXT = 1024, bool BASE = false, bool GM = false>
+template <class D, int MAXT = 1024, bool BASE = false, bool GM = false, bool SLDS = false>
 __global__ void __launch_bounds__(MAXT) k_interval(DevModel M, Src S, Lanes Ln, Tasks TK, Layout L,
         Interval I, const TplEntry* __restrict__ tpl, const uint32_t* __restrict__ ctpl,
         const int* __restrict__ ctgen, int nctgen,
@@ -1496,8 +1519,8 @@ __global__ void __launch_bounds__(MAXT) k_interval(DevModel M, Src S, Lanes Ln, 
     // il0: the first interval of this launch within the shard (a chunked
     // assembly, whose chunks are copied to the host while the next runs)
     const int b = (int)blockIdx.x;
-    interval_body<D, GM, BASE>(M, S, Ln, TK, L, I, tpl, ctpl, ctgen, nctgen, T, H, g, values,
-                               il0 + (I.xcd ? xcd_interval(b, (int)gridDim.x) : b));
+    interval_body<D, GM, BASE, SLDS>(M, S, Ln, TK, L, I, tpl, ctpl, ctgen, nctgen, T, H, g, values,
+                                     il0 + (I.xcd ? xcd_interval(b, (int)gridDim.x) : b));
 }
 
 // ------------------------------------------------------------------------
@@ -2193,6 +2216,7 @@ struct mh_ctx {
     // -1: by the grid point's result count, kIvgGmMaxDoubles)
     int ivg_base = 1;
     int ivg_gm = -1;
+    int iv_slots_lds = 0;          // k_interval stages the slot table in LDS (MOCOHIP_IV_SLOTS_LDS=1)
     bool role_couple = true;       // coupling in k_role's time role (MOCOHIP_ROLE_COUPLE=0: k_couple)
     bool use_ctpl = true;          // MOCOHIP_CTPL=0: k_interval assembles through jac_entry
     float timings[4] = {0, 0, 0, 0};
@@ -2465,7 +2489,8 @@ static size_t interval_lds(const mh_ctx* c, const Lanes& ln, const TaskSet& ts) 
     const size_t npts = c->scheme == MH_HERMITE_SIMPSON ? 3 : 2;
     return sizeof(double) * (npts * D::NO * ln.stride + CT_CONST + CT_NCONST +
                              npts * (size_t)(c->NS + c->NC + c->NDV + c->NM) + (size_t)c->NSL +
-                             npts * ((size_t)ts.dev.tdoubles + (size_t)ts.dev.nmass * D::NST));
+                             npts * ((size_t)ts.dev.tdoubles + (size_t)ts.dev.nmass * D::NST)) +
+           (c->iv_slots_lds && ln.stride > 1 ? sizeof(int) * (size_t)ln.stride * D::NG : 0);
 }
 // LDS bytes of k_role (Jacobian lanes).
 template <class D>
@@ -2551,6 +2576,7 @@ static void be_interval(mh_ctx* c, const double* x, int mode, double* g, double*
     // staged in LDS when they are many (Rajagopal 80: 1,111 doubles, where the
     // global-memory reads made eval_g slower, profiles/r05_f); MOCOHIP_IVG_GM
     // = 0 / 1 forces either
+    if (v && threads > 256 && c->iv_slots_lds && ln.stride > 1) kern = k_interval<D, 1024, false, false, true>;
     if (!v && ln.stride == 1 && threads <= 256 && c->ivg_base) {
         const bool gm = c->ivg_gm < 0 ? ts.dev.tdoubles <= kIvgGmMaxDoubles : c->ivg_gm != 0;
         kern = gm ? k_interval<D, 256, true, true> : k_interval<D, 256, true>;

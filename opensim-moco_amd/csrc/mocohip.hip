@@ -1752,6 +1752,8 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
         // slots (core.hpp TaskLoadBase; MOCOHIP_IVG_BASE=0: the slot table)
         const char* eb = std::getenv("MOCOHIP_IVG_BASE");
         c->ivg_base = eb && std::strcmp(eb, "0") == 0 ? 0 : 1;
+        const char* esl = std::getenv("MOCOHIP_IV_SLOTS_LDS");
+        c->iv_slots_lds = esl && std::strcmp(esl, "1") == 0 ? 1 : 0;
         const char* egm = std::getenv("MOCOHIP_IVG_GM");
         c->ivg_gm = !egm ? -1 : std::strcmp(egm, "0") == 0 ? 0 : 1;
         const TaskInfo* tib = backend_tasks(c->be);

@@ -309,7 +309,7 @@ def _pair(name, backend="auto", tasks=None, env=None):
                                                   "MOCOHIP_ROLES", "MOCOHIP_ROLE_COUPLE",
                                                   "MOCOHIP_IV_QFUSE", "MOCOHIP_IV_THREADS", "MOCOHIP_IV_XCD",
                                                   "MOCOHIP_GROUPS_XCD", "MOCOHIP_CSPLIT", "MOCOHIP_IVG_THREADS",
-                                                  "MOCOHIP_IVG_BASE", "MOCOHIP_IVG_GM", "MOCOHIP_GROUPS_KR",
+                                                  "MOCOHIP_IVG_BASE", "MOCOHIP_IVG_GM", "MOCOHIP_GROUPS_KR", "MOCOHIP_IV_SLOTS_LDS",
                                                   "MOCOHIP_EXC_LANES", "MOCOHIP_G_BLOCK", "MOCOHIP_G_LDS",
                                                   "MOCOHIP_G_LDS_GUARD",
                                                   "MOCOHIP_GROUPS_SPLIT", "MOCOHIP_COMBINE",
@@ -839,7 +839,8 @@ def test_pruned_tasks_bit_identical(name):
                                      {"MOCOHIP_IVG_THREADS": "1024"},
                                      {"MOCOHIP_IVG_BASE": "0"},
                                      {"MOCOHIP_IVG_GM": "0"},
-                                     {"MOCOHIP_GROUPS_KR": "0"}])
+                                     {"MOCOHIP_GROUPS_KR": "0"},
+                                     {"MOCOHIP_IV_SLOTS_LDS": "1"}])
 def test_kernel_variants_bit_identical(name, variant):
     """The default k_interval (combine + transcription per mesh interval,
     raw outputs in LDS) writes exactly what k_interval writes through
