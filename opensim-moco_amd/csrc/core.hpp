@@ -493,7 +493,8 @@ __global__ void __launch_bounds__(64) k_groups(DevModel M, Src S, Lanes Ln, Task
 // grid point and group -- and up to KR_MAX of them fit beside the other
 // arguments: the record then arrives with the launch's arguments instead of
 // one load of the task table after them (a dependent round trip at the head
-// of every task wave's chain).  MOCOHIP_GROUPS_KR=0: the table.
+// of every task wave's chain).  Opt-in (MOCOHIP_GROUPS_KR=1): measured no
+// faster than the table's one scalar load (profiles/r05_n).
 constexpr int KR_MAX = 384;
 struct KRecs {
     int2 r[KR_MAX];

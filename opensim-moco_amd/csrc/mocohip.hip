@@ -1587,10 +1587,12 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
         to_jac = put_taskset(A, c->ts_jac);
         to_g = put_taskset(A, c->ts_g);
         // eval_g's task records as kernel arguments (core.hpp k_groups_kr):
-        // stride-1 lanes, one task per grid point and group, <= KR_MAX blocks
+        // stride-1 lanes, one task per grid point and group, <= KR_MAX blocks;
+        // opt-in (MOCOHIP_GROUPS_KR=1): measured no faster than the table
+        // (eval_g's k_groups 7.12 vs 7.05 us, profiles/r05_n)
         {
             const char* ekr = std::getenv("MOCOHIP_GROUPS_KR");
-            bool ok = !(ekr && std::strcmp(ekr, "0") == 0) && c->lanes_g.stride == 1 &&
+            bool ok = ekr && std::strcmp(ekr, "1") == 0 && c->lanes_g.stride == 1 &&
                       c->ts_g.nblocks > 0 && c->ts_g.nblocks <= KR_MAX &&
                       c->ts_g.blk.size() >= 4 * (size_t)c->ts_g.nblocks;
             const float one = 1.0f;

@@ -839,7 +839,7 @@ def test_pruned_tasks_bit_identical(name):
                                      {"MOCOHIP_IVG_THREADS": "1024"},
                                      {"MOCOHIP_IVG_BASE": "0"},
                                      {"MOCOHIP_IVG_GM": "0"},
-                                     {"MOCOHIP_GROUPS_KR": "0"},
+                                     {"MOCOHIP_GROUPS_KR": "1"},
                                      {"MOCOHIP_IV_SLOTS_LDS": "1"}])
 def test_kernel_variants_bit_identical(name, variant):
     """The default k_interval (combine + transcription per mesh interval,
@@ -852,9 +852,9 @@ def test_kernel_variants_bit_identical(name, variant):
     Y."""
     gpu, _, _ = _pair(name)
     split, _, _ = _pair(name, env=variant)
-    if variant == {"MOCOHIP_GROUPS_KR": "0"}:
+    if variant == {"MOCOHIP_GROUPS_KR": "1"}:
         # eval_g's task records as kernel arguments against the task table
-        assert "groups-kernarg" not in split.backend_flags().split()
+        assert "groups-kernarg" not in gpu.backend_flags().split()
     if variant == {"MOCOHIP_IVG_BASE": "0"}:
         # eval_g's base-slot kernel against the slot-table path
         fa, fb = gpu.backend_flags().split(), split.backend_flags().split()
