@@ -563,10 +563,11 @@ static void build_taskset(const TaskInfo& ti, const Lanes& ln, int nk, int nsimd
     };
     // groups_xcd: XCD c's grid points are [P[c], P[c + 1]) -- the points of
     // the intervals xcd_interval gives XCD c, a shared mesh point going to
-    // the later run -- so the group results k_interval stages on XCD c were
-    // written by blocks of that XCD and can still sit in its L2 (plain stores
-    // keep their lines in the writing XCD's L2; the next kernel's acquire
-    // invalidates L1 only).  Per XCD the heavy groups' blocks lead, in the
+    // the later run -- so XCD c's task waves read one contiguous run of x
+    // (k_groups FETCH 6.55 -> 5.14 MB per launch, profiles/r05_ab).  The
+    // group results do not stay in the writing XCD's L2 for k_interval:
+    // its FETCH is the same in either order (7.48 MB), each launch starts
+    // cold.  Per XCD the heavy groups' blocks lead, in the
     // same heaviest-first order; the lists are padded to equal heavy and
     // light lengths and interleaved (block b -> XCD b % 8 under the
     // hardware's round-robin dispatch; placement is speed only).

@@ -1212,9 +1212,15 @@ def generate(cm, struct_name: str, implicit: bool = False, prescribed: bool = Fa
             words[i // 64] |= 1 << (i % 64)
         reads.append("{" + ", ".join(f"0x{w:x}ULL" for w in words) + "}")
     body = ["        switch (g) {"]
+    rin = re.compile(r"\bin\[(\d+)\]")
     for gi, gr in enumerate(groups):
         body.append(f"        case {gi}: {{  // {gr.name}")
-        body.extend("    " + l for l in gr.lines)
+        # the group's inputs loaded at its top, all at once (one memory round
+        # trip before the arithmetic instead of loads spread through it, each
+        # waited on where first used)
+        used = sorted({int(m) for l in gr.lines for m in rin.findall(l)})
+        body.extend(f"            const double in_{i} = in[{i}];" for i in used)
+        body.extend("    " + rin.sub(lambda m: f"in_{m.group(1)}", l) for l in gr.lines)
         body.append("        } break;")
     body += ["        default: break;", "        }"]
     parts.append(("group", "const int g, const mh::DevModel& M, const double t, "
