@@ -30,6 +30,11 @@ import numpy as np
 
 from . import abi
 
+# generated task decompositions of at most this many groups load each
+# group's inputs at the top of the group (see generate(): gait 42-45 groups
+# yes, Rajagopal 80's 170 no)
+HOIST_MAX_GROUPS = 64
+
 
 def lit(v: float) -> str:
     """Exact C++ literal of a double (Python repr round-trips exactly)."""
@@ -1213,14 +1218,22 @@ def generate(cm, struct_name: str, implicit: bool = False, prescribed: bool = Fa
         reads.append("{" + ", ".join(f"0x{w:x}ULL" for w in words) + "}")
     body = ["        switch (g) {"]
     rin = re.compile(r"\bin\[(\d+)\]")
+    # the group's inputs loaded at its top, all at once (one memory round trip
+    # before the arithmetic instead of loads spread through it, each waited
+    # on where first used): gait's task kernels 7.15 -> 6.76 us (eval_g) and
+    # ~9.2 -> 8.5 us (Jacobian), headline 24.6 k -> 25.3 k calls/s
+    # (profiles/r05_p).  Not for the large models, whose group kernels run at
+    # the register cap (Rajagopal 80: 254 VGPRs; its DAE stage 0.38 -> 0.46 ms
+    # with the inputs hoisted).
+    hoist = len(groups) <= HOIST_MAX_GROUPS
     for gi, gr in enumerate(groups):
         body.append(f"        case {gi}: {{  // {gr.name}")
-        # the group's inputs loaded at its top, all at once (one memory round
-        # trip before the arithmetic instead of loads spread through it, each
-        # waited on where first used)
-        used = sorted({int(m) for l in gr.lines for m in rin.findall(l)})
-        body.extend(f"            const double in_{i} = in[{i}];" for i in used)
-        body.extend("    " + rin.sub(lambda m: f"in_{m.group(1)}", l) for l in gr.lines)
+        if hoist:
+            used = sorted({int(m) for l in gr.lines for m in rin.findall(l)})
+            body.extend(f"            const double in_{i} = in[{i}];" for i in used)
+            body.extend("    " + rin.sub(lambda m: f"in_{m.group(1)}", l) for l in gr.lines)
+        else:
+            body.extend("    " + l for l in gr.lines)
         body.append("        } break;")
     body += ["        default: break;", "        }"]
     parts.append(("group", "const int g, const mh::DevModel& M, const double t, "
