@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define MH_ABI_VERSION 7
+#define MH_ABI_VERSION 8
 
 enum mh_status {
     MH_OK = 0,
@@ -487,7 +487,11 @@ typedef struct mh_options {
      * 91-94), step sqrt(DBL_EPSILON), recovered per nonzero.  Unsharded
      * contexts only. */
     int32_t jacobian_mode;
-    int32_t reserved_jm;
+    /* (ABI v8) The column order of that coloring (mh_coloring_order):
+     * SMALLEST_LAST (0, the zero value) is ColPack's ordering as tropter
+     * requests it (GraphColoring.cpp:91-94), NATURAL (1) the columns in
+     * index order (ABI <= 7).  Only the seed count depends on it. */
+    int32_t coloring_order;
     /* (ABI v6; v7: the values swapped) How detection decides a coupling
      * (mh_sparsity_rule).  ANY_CHANGE (0, the default of a zero-initialized
      * mh_options and of every surface above it): the reference's rule
@@ -513,6 +517,7 @@ enum mh_sparsity_rule { MH_SPARSITY_RULE_ANY_CHANGE = 0, MH_SPARSITY_RULE_ROBUST
 #define MH_SPARSITY_ROBUST_TOL 1e-12
 
 enum mh_jacobian_mode { MH_JACOBIAN_CALLBACK_FD = 0, MH_JACOBIAN_GLOBAL_SEEDS = 1 };
+enum mh_coloring_order { MH_COLORING_SMALLEST_LAST = 0, MH_COLORING_NATURAL = 1 };
 
 enum mh_sparsity {
     MH_SPARSITY_NONE = 0, MH_SPARSITY_RANDOM = 1, MH_SPARSITY_INITIAL_GUESS = 2, MH_SPARSITY_GIVEN = 3
@@ -694,12 +699,28 @@ int mh_model_hash(const mh_model* model, uint64_t* hash);
 /* Column partial distance-2 coloring of a sparsity pattern (the seeds of
  * tropter's JacobianColoring, GraphColoring.cpp:71-120; ColPack
  * COLUMN_PARTIAL_DISTANCE_TWO): two columns share a color only if no row has
- * both.  Greedy over columns in natural order (ColPack orders them
- * SMALLEST_LAST: the seed count may differ, the recovered values do not).
+ * both.  Greedy over columns in natural order (MH_COLORING_NATURAL; see
+ * mh_color_jacobian_ordered for ColPack's SMALLEST_LAST).
  * color[ncols] receives each column's seed, *ncolors the seed count.  Host
  * only (no device, no context). */
 int mh_color_jacobian(int64_t nrows, int64_t ncols, int64_t nnz, const int32_t* iRow,
                       const int32_t* jCol, int32_t* color, int32_t* ncolors);
+/* The same with the column order chosen (mh_coloring_order).
+ * MH_COLORING_SMALLEST_LAST restates ColPack's SMALLEST_LAST ordering
+ * (tropter requests it, GraphColoring.cpp:91-94; Matula & Beck's
+ * smallest-last order of the column intersection graph: two columns are
+ * adjacent iff a row has both).  Columns sit in buckets by their number of
+ * distinct adjacent columns, inserted in index order; n times the LAST column
+ * of the lowest non-empty bucket is removed and placed at the end of the
+ * order still free, and each of its adjacent columns not yet removed --
+ * visited row by row, rows and each row's columns in the input's nonzero
+ * order -- leaves its bucket (the bucket's last column takes its place) and is
+ * appended to the bucket one lower.  The columns are then colored first-fit
+ * in that order.  ColPack's own tie-breaking is not in the reference tree:
+ * the order is this restatement's, the seed count may differ from ColPack's,
+ * the recovered values cannot. */
+int mh_color_jacobian_ordered(int64_t nrows, int64_t ncols, int64_t nnz, const int32_t* iRow,
+                              const int32_t* jCol, int32_t order, int32_t* color, int32_t* ncolors);
 /* The seed of every x column (n entries) that eval_jac_g uses in
  * MH_JACOBIAN_GLOBAL_SEEDS mode (the coloring of mh_get_jac_structure). */
 int mh_get_jacobian_seeds(const mh_ctx* ctx, int32_t* color, int32_t* nseeds);

@@ -2262,6 +2262,7 @@ struct mh_ctx {
     // MH_JACOBIAN_GLOBAL_SEEDS (tropter): column coloring, per seed its
     // columns and its (nonzero, row) pairs, perturbed iterates and g's
     int jac_seeds = 0, nseeds = 0;
+    int coloring_order = MH_COLORING_SMALLEST_LAST;   // mh_options.coloring_order
     std::vector<int32_t> seed_color;           // [n]
     std::vector<int32_t> seed_col_off, seed_cols, seed_ent_off, seed_ents, seed_rows;
     int32_t *d_seed_cols = nullptr, *d_seed_ents = nullptr, *d_seed_rows = nullptr;

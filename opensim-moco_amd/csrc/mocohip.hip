@@ -1561,6 +1561,9 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     if (c->jac_seeds && (c->ib != 0 || c->ie != c->N || o->sparsity_detection != MH_SPARSITY_NONE))
         return set_err(MH_ERR_UNSUPPORTED, "MH_JACOBIAN_GLOBAL_SEEDS needs an unsharded context and "
                        "the block-dense structure");
+    if (o->coloring_order != MH_COLORING_SMALLEST_LAST && o->coloring_order != MH_COLORING_NATURAL)
+        return set_err(MH_ERR_INVALID, "unknown coloring_order %d", o->coloring_order);
+    c->coloring_order = o->coloring_order;
     size_t o_scol = 0, o_sent = 0, o_srow = 0, o_xp = 0, o_xm = 0, o_gp = 0, o_gm = 0;
     if (c->jac_seeds) {
         int rc2 = build_seeds(c.get());
@@ -2118,9 +2121,69 @@ static int run_stage(mh_ctx* c, int stage, int kind, const double* x, double* a,
 // nonzeros of the seed's columns (each row meets at most one of them, so
 // the quotient is that column's derivative).
 // ------------------------------------------------------------------------
-// Greedy column partial distance-2 coloring over CSR rows / CSC columns.
+// Greedy column partial distance-2 coloring over CSR rows / CSC columns,
+// the columns visited in natural order (order = MH_COLORING_NATURAL) or in
+// the smallest-last order of the column intersection graph
+// (MH_COLORING_SMALLEST_LAST, ColPack's ordering in tropter,
+// GraphColoring.cpp:91-94; Matula & Beck 1983).  Smallest-last as restated
+// here (oracle/oracle.c restates it independently; both follow this text):
+// two columns are adjacent iff they share a row; deg(v) = the number of
+// distinct adjacent columns.  Columns sit in buckets by current degree,
+// inserted in natural order.  n times: take the LAST column of the lowest
+// non-empty bucket, place it at the end of the order still free (the first
+// removed is colored last), and for each of its distinct adjacent columns
+// not yet removed -- visited row by row in ascending row order, each row's
+// columns ascending -- remove it from its bucket (the bucket's last column
+// takes its place) and append it to the bucket one degree lower.
+static void smallest_last_order(int64_t ncols, const std::vector<int64_t>& roff,
+        const std::vector<int64_t>& coff, const std::vector<int32_t>& rcol, const std::vector<int32_t>& crow,
+        std::vector<int32_t>& order) {
+    std::vector<int64_t> deg(ncols, 0), stamp(ncols, -1);
+    for (int64_t v = 0; v < ncols; ++v) {
+        stamp[v] = v;
+        for (int64_t q = coff[v]; q < coff[v + 1]; ++q)
+            for (int64_t t = roff[crow[q]]; t < roff[crow[q] + 1]; ++t)
+                if (stamp[rcol[t]] != v) { stamp[rcol[t]] = v; ++deg[v]; }
+    }
+    int64_t maxdeg = 0;
+    for (int64_t v = 0; v < ncols; ++v) maxdeg = std::max(maxdeg, deg[v]);
+    std::vector<std::vector<int32_t>> bucket((size_t)maxdeg + 1);
+    std::vector<int64_t> pos(ncols);
+    for (int64_t v = 0; v < ncols; ++v) {
+        pos[v] = (int64_t)bucket[deg[v]].size();
+        bucket[deg[v]].push_back((int32_t)v);
+    }
+    std::vector<char> removed(ncols, 0);
+    std::fill(stamp.begin(), stamp.end(), -1);
+    order.assign(ncols, -1);
+    int64_t lo = 0;
+    for (int64_t i = 0; i < ncols; ++i) {
+        while (bucket[lo].empty()) ++lo;
+        const int32_t u = bucket[lo].back();
+        bucket[lo].pop_back();
+        removed[u] = 1;
+        order[ncols - 1 - i] = u;
+        stamp[u] = u;
+        for (int64_t q = coff[u]; q < coff[u + 1]; ++q)
+            for (int64_t t = roff[crow[q]]; t < roff[crow[q] + 1]; ++t) {
+                const int32_t x = rcol[t];
+                if (stamp[x] == u || removed[x]) continue;
+                stamp[x] = u;
+                std::vector<int32_t>& b = bucket[deg[x]];
+                const int32_t last = b.back();
+                b[pos[x]] = last;
+                pos[last] = pos[x];
+                b.pop_back();
+                --deg[x];
+                pos[x] = (int64_t)bucket[deg[x]].size();
+                bucket[deg[x]].push_back(x);
+            }
+        if (lo > 0) --lo;   // a neighbour may now sit one bucket lower
+    }
+}
+
 static int color_columns(int64_t nrows, int64_t ncols, int64_t nnz, const int32_t* iRow,
-        const int32_t* jCol, int32_t* color) {
+        const int32_t* jCol, int32_t* color, int order_kind = MH_COLORING_NATURAL) {
     std::vector<int64_t> roff(nrows + 1, 0), coff(ncols + 1, 0);
     for (int64_t e = 0; e < nnz; ++e) {
         if (iRow[e] < 0 || iRow[e] >= nrows || jCol[e] < 0 || jCol[e] >= ncols) return -1;
@@ -2137,10 +2200,13 @@ static int color_columns(int64_t nrows, int64_t ncols, int64_t nnz, const int32_
             crow[cp[jCol[e]]++] = iRow[e];
         }
     }
+    std::vector<int32_t> order;
+    if (order_kind == MH_COLORING_SMALLEST_LAST) smallest_last_order(ncols, roff, coff, rcol, crow, order);
     std::vector<int64_t> stamp;   // stamp[color] == column: color forbidden for it
     int32_t ncolors = 0;
     for (int64_t j = 0; j < ncols; ++j) color[j] = -1;
-    for (int64_t j = 0; j < ncols; ++j) {
+    for (int64_t jj = 0; jj < ncols; ++jj) {
+        const int64_t j = order.empty() ? jj : order[jj];
         for (int64_t q = coff[j]; q < coff[j + 1]; ++q) {
             const int32_t r = crow[q];
             for (int64_t t = roff[r]; t < roff[r + 1]; ++t) {
@@ -2166,6 +2232,18 @@ extern "C" int mh_color_jacobian(int64_t nrows, int64_t ncols, int64_t nnz, cons
     return MH_OK;
 }
 
+extern "C" int mh_color_jacobian_ordered(int64_t nrows, int64_t ncols, int64_t nnz, const int32_t* iRow,
+        const int32_t* jCol, int32_t order, int32_t* color, int32_t* ncolors) {
+    if (nrows < 0 || ncols < 0 || nnz < 0 || (nnz && (!iRow || !jCol)) || (ncols && !color) || !ncolors)
+        return set_err(MH_ERR_INVALID, "bad argument");
+    if (order != MH_COLORING_SMALLEST_LAST && order != MH_COLORING_NATURAL)
+        return set_err(MH_ERR_INVALID, "unknown coloring order %d", order);
+    const int k = color_columns(nrows, ncols, nnz, iRow, jCol, color, order);
+    if (k < 0) return set_err(MH_ERR_INVALID, "index out of range");
+    *ncolors = k;
+    return MH_OK;
+}
+
 extern "C" int mh_get_jacobian_seeds(const mh_ctx* c, int32_t* color, int32_t* nseeds) {
     if (!c || !color || !nseeds) return set_err(MH_ERR_INVALID, "null argument");
     if (!c->jac_seeds) return set_err(MH_ERR_INVALID, "context not in MH_JACOBIAN_GLOBAL_SEEDS mode");
@@ -2180,7 +2258,7 @@ static int build_seeds(mh_ctx* c) {
     int rc = mh_get_jac_structure(c, ir.data(), jc.data());
     if (rc) return rc;
     c->seed_color.assign(c->n, -1);
-    c->nseeds = color_columns(c->m, c->n, c->nnz, ir.data(), jc.data(), c->seed_color.data());
+    c->nseeds = color_columns(c->m, c->n, c->nnz, ir.data(), jc.data(), c->seed_color.data(), c->coloring_order);
     if (c->nseeds < 0) return set_err(MH_ERR_INVALID, "internal: Jacobian structure out of range");
     const int S = c->nseeds;
     c->seed_col_off.assign(S + 1, 0);

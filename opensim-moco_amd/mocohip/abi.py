@@ -85,6 +85,7 @@ class mh_external_force(C.Structure):
 
 MH_KC_COORDINATE_COUPLER = 0
 MH_JACOBIAN_CALLBACK_FD, MH_JACOBIAN_GLOBAL_SEEDS = 0, 1
+MH_COLORING_SMALLEST_LAST, MH_COLORING_NATURAL = 0, 1
 
 
 class mh_constraint(C.Structure):
@@ -137,7 +138,7 @@ class mh_goal(C.Structure):
                 ("weight", f64)]
 
 
-MH_ABI_VERSION = 7     # include/mocohip.h
+MH_ABI_VERSION = 8     # include/mocohip.h
 MH_PATH_CONTROL_BOUND = 0
 MH_ENDPOINT_INITIAL_ACTIVATION = 0
 
@@ -179,7 +180,7 @@ class mh_options(C.Structure):
                 ("implicit_aux_bounds", f64 * 2),
                 ("ignore_constraint_derivatives", i32), ("minimize_lagrange_multipliers", i32),
                 ("velocity_correction_bounds", f64 * 2), ("lagrange_multiplier_weight", f64),
-                ("jacobian_mode", i32), ("reserved_jm", i32),
+                ("jacobian_mode", i32), ("coloring_order", i32),
                 ("sparsity_rule", i32), ("reserved_sr", i32)]
 
 
@@ -232,6 +233,8 @@ MOCOHIP_SYMBOLS = {
     "mh_get_callback_sparsity": (i32, [C.c_void_p, P(C.c_uint8), C.c_int64]),
     "mh_get_work": (i32, [C.c_void_p, P(f64)]),
     "mh_color_jacobian": (i32, [C.c_int64, C.c_int64, C.c_int64, P(i32), P(i32), P(i32), P(i32)]),
+    "mh_color_jacobian_ordered": (i32, [C.c_int64, C.c_int64, C.c_int64, P(i32), P(i32), i32, P(i32),
+                                        P(i32)]),
     "mh_get_jacobian_seeds": (i32, [C.c_void_p, P(i32), P(i32)]),
     "mh_debug_jacobian_lanes": (i32, [C.c_void_p, P(f64), P(f64), P(f64)]),
     "mh_debug_time_stages": (i32, [C.c_void_p, C.c_void_p, i32, i32, P(f64)]),
@@ -271,6 +274,7 @@ ORACLE_SYMBOLS = {
     "orc_eval_function": (i32, [C.c_void_p, C.c_int, f64, P(f64)]),
     "orc_get_callback_sparsity": (i32, [C.c_void_p, P(C.c_uint8), C.c_int64]),
     "orc_get_jacobian_seeds": (i32, [C.c_void_p, P(i32), P(i32)]),
+    "orc_color_jacobian": (i32, [C.c_int64, C.c_int64, C.c_int64, P(i32), P(i32), i32, P(i32), P(i32)]),
     "orc_assemble_from_lanes": (i32, [C.c_void_p, P(f64), P(f64), P(f64), P(f64), P(f64)]),
 }
 

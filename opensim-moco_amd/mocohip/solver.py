@@ -73,6 +73,10 @@ class MocoHipSolver:
     # "global-seeds" (tropter: central FD of g along colored seed columns,
     # ProblemDecorator_double.cpp:261-291)
     jacobian_mode: str = "callback-fd"
+    # the column order of the global-seed coloring: "smallest-last" (ColPack's
+    # SMALLEST_LAST, as tropter requests it, GraphColoring.cpp:91-94) or
+    # "natural" (index order; ABI <= 7)
+    coloring_order: str = "smallest-last"
     # the optimizer settings (MocoDirectCollocationSolver.cpp:23-42), mapped
     # to Ipopt options by ipopt_options()
     verbosity: int = 2
@@ -169,6 +173,10 @@ class MocoHipSolver:
         if self.jacobian_mode not in modes:
             raise ValueError("jacobian_mode must be 'callback-fd' or 'global-seeds'")
         o.jacobian_mode = modes[self.jacobian_mode]
+        orders = {"smallest-last": abi.MH_COLORING_SMALLEST_LAST, "natural": abi.MH_COLORING_NATURAL}
+        if self.coloring_order not in orders:
+            raise ValueError("coloring_order must be 'smallest-last' or 'natural'")
+        o.coloring_order = orders[self.coloring_order]
         lo, hi = self.velocity_correction_bounds
         o.velocity_correction_bounds[0] = float(lo)
         o.velocity_correction_bounds[1] = float(hi)

@@ -619,13 +619,83 @@ static int detect_sparsity(orc_ctx* c, const mh_options* o);
 #endif
 static int sharded(const orc_ctx* c);
 
-/* Column partial distance-2 coloring, greedy in natural column order: the
- * smallest color no column sharing a row already has (ColPack's
- * COLUMN_PARTIAL_DISTANCE_TWO, GraphColoring.cpp:91-94; ColPack orders the
- * columns SMALLEST_LAST -- only the seed count depends on the order).
- * Returns the color count. */
+/* ColPack's SMALLEST_LAST column ordering as tropter requests it
+ * (GraphColoring.cpp:91-94: GenerateSeedJacobian_unmanaged(..., "SMALLEST_LAST",
+ * "COLUMN_PARTIAL_DISTANCE_TWO")), restated from Matula & Beck's published
+ * smallest-last algorithm on the column intersection graph (ColPack itself is
+ * not in the reference tree; its tie-breaking is this restatement's, the rule
+ * include/mocohip.h gives for mh_color_jacobian_ordered):
+ *   adjacency  columns a != b sharing a row; deg = distinct adjacent columns;
+ *   buckets    one list per degree, columns appended in index order;
+ *   step       the last column of the lowest non-empty bucket is removed and
+ *              written at the last free slot of the order; every adjacent
+ *              column still present (rows of the removed column in nonzero
+ *              order, each row's columns in nonzero order, each column once)
+ *              leaves its bucket -- the bucket's last column moves into its
+ *              slot -- and is appended to the bucket one degree lower.
+ * ord[n] receives the coloring order. */
+static void smallest_last(int64_t ncols, const int64_t* roff, const int64_t* coff, const int32_t* rcol,
+        const int32_t* crow, int32_t* ord) {
+    int64_t* deg = (int64_t*)calloc((size_t)ncols + 1, sizeof(int64_t));
+    int64_t* seen = (int64_t*)malloc(sizeof(int64_t) * ((size_t)ncols + 1));
+    int64_t* slot = (int64_t*)malloc(sizeof(int64_t) * ((size_t)ncols + 1));
+    char* gone = (char*)calloc((size_t)ncols + 1, 1);
+    int64_t maxd = 0;
+    for (int64_t v = 0; v < ncols; ++v) seen[v] = -1;
+    for (int64_t v = 0; v < ncols; ++v) {
+        seen[v] = v;
+        for (int64_t q = coff[v]; q < coff[v + 1]; ++q) {
+            const int32_t r = crow[q];
+            for (int64_t t = roff[r]; t < roff[r + 1]; ++t)
+                if (seen[rcol[t]] != v) { seen[rcol[t]] = v; deg[v]++; }
+        }
+        if (deg[v] > maxd) maxd = deg[v];
+    }
+    /* bucket d: the columns of current degree d, list[bstart[d] .. + bsize[d]) of a
+     * per-degree array sized by how many columns start at or above d */
+    int64_t** list = (int64_t**)calloc((size_t)maxd + 1, sizeof(int64_t*));
+    int64_t* bsize = (int64_t*)calloc((size_t)maxd + 1, sizeof(int64_t));
+    int64_t* cap = (int64_t*)calloc((size_t)maxd + 2, sizeof(int64_t));
+    for (int64_t v = 0; v < ncols; ++v) cap[deg[v]]++;
+    for (int64_t d = maxd; d > 0; --d) cap[d - 1] += cap[d];   /* a column only moves down */
+    for (int64_t d = 0; d <= maxd; ++d) list[d] = (int64_t*)malloc(sizeof(int64_t) * (size_t)(cap[d] + 1));
+    for (int64_t v = 0; v < ncols; ++v) { slot[v] = bsize[deg[v]]; list[deg[v]][bsize[deg[v]]++] = v; }
+    for (int64_t v = 0; v < ncols; ++v) seen[v] = -1;
+    int64_t low = 0;
+    for (int64_t i = 0; i < ncols; ++i) {
+        while (bsize[low] == 0) ++low;
+        const int64_t u = list[low][--bsize[low]];
+        gone[u] = 1;
+        ord[ncols - 1 - i] = (int32_t)u;
+        seen[u] = u;
+        for (int64_t q = coff[u]; q < coff[u + 1]; ++q) {
+            const int32_t r = crow[q];
+            for (int64_t t = roff[r]; t < roff[r + 1]; ++t) {
+                const int64_t w = rcol[t];
+                if (gone[w] || seen[w] == u) continue;
+                seen[w] = u;
+                const int64_t d = deg[w];
+                const int64_t moved = list[d][bsize[d] - 1];
+                list[d][slot[w]] = moved;
+                slot[moved] = slot[w];
+                bsize[d]--;
+                deg[w] = d - 1;
+                slot[w] = bsize[d - 1];
+                list[d - 1][bsize[d - 1]++] = w;
+            }
+        }
+        if (low > 0) low--;
+    }
+    for (int64_t d = 0; d <= maxd; ++d) free(list[d]);
+    free(list); free(bsize); free(cap); free(deg); free(seen); free(slot); free(gone);
+}
+
+/* Column partial distance-2 coloring: the smallest color no column sharing
+ * a row already has (ColPack's COLUMN_PARTIAL_DISTANCE_TWO, GraphColoring.cpp:
+ * 91-94), the columns visited in natural order (MH_COLORING_NATURAL) or in
+ * the SMALLEST_LAST order above.  Returns the color count. */
 static int color_columns(int64_t nrows, int64_t ncols, int64_t nnz, const int32_t* iRow,
-        const int32_t* jCol, int32_t* color) {
+        const int32_t* jCol, int32_t* color, int order) {
     int64_t* roff = (int64_t*)calloc((size_t)nrows + 1, sizeof(int64_t));
     int64_t* coff = (int64_t*)calloc((size_t)ncols + 1, sizeof(int64_t));
     int32_t* rcol = (int32_t*)malloc(sizeof(int32_t) * (size_t)(nnz + 1));
@@ -639,9 +709,13 @@ static int color_columns(int64_t nrows, int64_t ncols, int64_t nnz, const int32_
     memcpy(rp, roff, sizeof(int64_t) * (size_t)nrows);
     memcpy(cp, coff, sizeof(int64_t) * (size_t)ncols);
     for (int64_t e = 0; e < nnz; ++e) { rcol[rp[iRow[e]]++] = jCol[e]; crow[cp[jCol[e]]++] = iRow[e]; }
+    int32_t* ord = (int32_t*)malloc(sizeof(int32_t) * (size_t)(ncols + 1));
+    for (int64_t j = 0; j < ncols; ++j) ord[j] = (int32_t)j;
+    if (order == MH_COLORING_SMALLEST_LAST) smallest_last(ncols, roff, coff, rcol, crow, ord);
     int ncolors = 0;
     for (int64_t j = 0; j < ncols; ++j) color[j] = -1;
-    for (int64_t j = 0; j < ncols; ++j) {
+    for (int64_t jj = 0; jj < ncols; ++jj) {
+        const int64_t j = ord[jj];
         for (int64_t q = coff[j]; q < coff[j + 1]; ++q)
             for (int64_t t = roff[crow[q]]; t < roff[crow[q] + 1]; ++t)
                 if (color[rcol[t]] >= 0) stamp[color[rcol[t]]] = j;
@@ -650,8 +724,19 @@ static int color_columns(int64_t nrows, int64_t ncols, int64_t nnz, const int32_
         if (k == ncolors) stamp[ncolors++] = -1;
         color[j] = k;
     }
-    free(roff); free(coff); free(rcol); free(crow); free(rp); free(cp); free(stamp);
+    free(roff); free(coff); free(rcol); free(crow); free(rp); free(cp); free(stamp); free(ord);
     return ncolors;
+}
+
+int orc_color_jacobian(int64_t nrows, int64_t ncols, int64_t nnz, const int32_t* iRow, const int32_t* jCol,
+        int32_t order, int32_t* color, int32_t* ncolors) {
+    for (int64_t e = 0; e < nnz; ++e)
+        if (iRow[e] < 0 || iRow[e] >= nrows || jCol[e] < 0 || jCol[e] >= ncols)
+            return fail(MH_ERR_INVALID, "index out of range");
+    if (order != MH_COLORING_SMALLEST_LAST && order != MH_COLORING_NATURAL)
+        return fail(MH_ERR_INVALID, "unknown coloring order %d", order);
+    *ncolors = color_columns(nrows, ncols, nnz, iRow, jCol, color, order);
+    return MH_OK;
 }
 
 int orc_create(const mh_problem* p, const mh_options* o, orc_ctx** out) {
@@ -1048,7 +1133,8 @@ int orc_create(const mh_problem* p, const mh_options* o, orc_ctx** out) {
     c->nnz_end = c->nnz_begin;
     while (c->nnz_end < c->nnz && c->iRow[c->nnz_end] < c->row_end) ++c->nnz_end;
     /* tropter's global-seed Jacobian (ProblemDecorator_double.cpp:261-291):
-     * greedy column partial distance-2 coloring of the structure */
+     * column partial distance-2 coloring of the structure (ColPack's
+     * SMALLEST_LAST order unless mh_options.coloring_order says natural) */
     c->jac_seeds = o->jacobian_mode == MH_JACOBIAN_GLOBAL_SEEDS;
     if (o->jacobian_mode != MH_JACOBIAN_CALLBACK_FD && !c->jac_seeds) {
         orc_destroy(c);
@@ -1061,7 +1147,11 @@ int orc_create(const mh_problem* p, const mh_options* o, orc_ctx** out) {
                         "block-dense structure");
         }
         c->seed_color = (int32_t*)malloc(sizeof(int32_t) * (size_t)(c->n + 1));
-        c->nseeds = color_columns(c->m, c->n, c->nnz, c->iRow, c->jCol, c->seed_color);
+        if (o->coloring_order != MH_COLORING_SMALLEST_LAST && o->coloring_order != MH_COLORING_NATURAL) {
+            orc_destroy(c);
+            return fail(MH_ERR_INVALID, "unknown coloring_order %d", o->coloring_order);
+        }
+        c->nseeds = color_columns(c->m, c->n, c->nnz, c->iRow, c->jCol, c->seed_color, o->coloring_order);
     }
     *out = c;
     return MH_OK;

@@ -86,6 +86,9 @@ int orc_eval_function(orc_ctx* ctx, int ifn, double q, double* out3);
 /* The callback sparsity behind the structure (mh_get_callback_sparsity). */
 int orc_get_callback_sparsity(const orc_ctx* ctx, uint8_t* pattern, int64_t len);
 int orc_get_jacobian_seeds(const orc_ctx* c, int32_t* color, int32_t* nseeds);
+/* mh_color_jacobian_ordered restated (host, no context). */
+int orc_color_jacobian(int64_t nrows, int64_t ncols, int64_t nnz, const int32_t* iRow, const int32_t* jCol,
+        int32_t order, int32_t* color, int32_t* ncolors);
 
 #ifdef __cplusplus
 }

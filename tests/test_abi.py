@@ -37,7 +37,7 @@ def test_library_loads_and_exports_every_symbol():
     lib = abi.load_mocohip()
     for name in list(abi.MOCOHIP_SYMBOLS) + list(abi.MOCOHIP_KKT_SYMBOLS):
         assert hasattr(lib, name), name
-    assert lib.mh_abi_version() == abi.MH_ABI_VERSION == 7
+    assert lib.mh_abi_version() == abi.MH_ABI_VERSION == 8
     out = subprocess.run(["nm", "-D", "--defined-only", abi.LIBMOCOHIP_PATH],
                          capture_output=True, text=True, check=True).stdout
     exported = set(re.findall(r" T (mh_\w+)", out))

@@ -1216,6 +1216,21 @@ def _color(ir, jc, m, n):
     return color, k.value
 
 
+def _color_ordered(ir, jc, m, n, order, lib="hip"):
+    """mh_color_jacobian_ordered (the library) or orc_color_jacobian (the
+    oracle's independent restatement); host only."""
+    ir = np.ascontiguousarray(ir, np.int32)
+    jc = np.ascontiguousarray(jc, np.int32)
+    color = np.empty(n, np.int32)
+    k = C.c_int32()
+    if lib == "hip":
+        fn = abi.load_mocohip().mh_color_jacobian_ordered
+    else:
+        fn = abi.load_oracle().orc_color_jacobian
+    assert fn(m, n, len(ir), abi.iptr(ir), abi.iptr(jc), order, abi.iptr(color), C.byref(k)) == 0
+    return color, k.value
+
+
 def _valid_coloring(ir, jc, color):
     seen = {}
     for r, c in zip(ir, jc):
@@ -1270,7 +1285,8 @@ def test_global_seed_jacobian_is_columnwise_fd_of_g(case):
     ir, jc = gs.jac_structure()
     color, k = gs.jacobian_seeds()
     _valid_coloring(ir, jc, color)
-    assert np.array_equal(color, _color(ir, jc, gs.m, gs.n)[0]) and k < gs.n
+    assert np.array_equal(color, _color_ordered(ir, jc, gs.m, gs.n, abi.MH_COLORING_SMALLEST_LAST)[0])
+    assert k < gs.n
     x = gs.random_iterate(np.random.default_rng(1).uniform(-1, 1, gs.n))
     J = gs.eval_jac_g(x)
     eps = math.sqrt(np.finfo(float).eps)
@@ -1444,3 +1460,65 @@ def test_wrap_cylinder_geometry():
             lib.orc_muscle_length_speed(nlp.ctx, 0, abi.dptr(q - h), abi.dptr(u), abi.dptr(Lm))
             assert out[1] == pytest.approx((Lp[0] - Lm[0]) / (2 * h) * u[0], rel=1e-6, abs=1e-9)
         assert nwrap >= 6
+
+
+def _structures():
+    """Jacobian structures to color: tropter's sparse-Jacobian test, the
+    transcriptions of a few problems, a random sparse pattern."""
+    out = {}
+    ir = [i for i in range(5) for j in range(max(i - 1, 0), min(i + 1, 4))]
+    jc = [j for i in range(5) for j in range(max(i - 1, 0), min(i + 1, 4))]
+    out["tropter_sparse"] = (np.array(ir), np.array(jc), 5, 4)
+    for name, mk in (("hs", lambda: configs.double_pendulum(5)),
+                     ("trap", lambda: configs.double_pendulum(5, "trapezoidal", dynamics="implicit")),
+                     ("coupled", lambda: configs.double_pendulum_coupled(4)),
+                     ("gait", lambda: configs.gait10dof18musc(3))):
+        st = mk()
+        o = OracleNLP(st.problem.create_rep(), st.solver.options())
+        i, j = o.jac_structure()
+        out[name] = (i, j, o.m, o.n)
+        o.close()
+    r = np.random.default_rng(7)
+    m, n = 300, 200
+    dense = r.random((m, n)) < 0.03
+    i, j = np.nonzero(dense)
+    out["random"] = (i, j, m, n)
+    return out
+
+
+def test_smallest_last_coloring_library_equals_oracle():
+    """ColPack's SMALLEST_LAST column order (GraphColoring.cpp:91-94), restated
+    in the library (mocohip.hip smallest_last_order) and independently in the
+    oracle (oracle.c smallest_last): the same colors column for column on every
+    structure, a valid partial distance-2 coloring, and -- on the
+    transcriptions, whose t0 / tf columns meet every defect row -- no more seeds
+    than the natural order; tropter's sparse-Jacobian test keeps its 2 seeds."""
+    for name, (ir, jc, m, n) in _structures().items():
+        for order in (abi.MH_COLORING_SMALLEST_LAST, abi.MH_COLORING_NATURAL):
+            ch, kh = _color_ordered(ir, jc, m, n, order, "hip")
+            co, ko = _color_ordered(ir, jc, m, n, order, "oracle")
+            assert kh == ko and np.array_equal(ch, co), (name, order)
+            _valid_coloring(ir, jc, ch)
+        sl = _color_ordered(ir, jc, m, n, abi.MH_COLORING_SMALLEST_LAST)[1]
+        nat = _color_ordered(ir, jc, m, n, abi.MH_COLORING_NATURAL)[1]
+        assert np.array_equal(_color_ordered(ir, jc, m, n, abi.MH_COLORING_NATURAL)[0], _color(ir, jc, m, n)[0])
+        if name == "tropter_sparse":
+            assert sl == 2
+        if name != "random":
+            assert sl <= nat, (name, sl, nat)
+
+
+def test_smallest_last_order_is_smallest_last():
+    """The order itself on a graph small enough to follow by hand: a star
+    (column 0 shares a row with each of columns 1..4) plus an isolated
+    column 5.  Degrees: 0 -> 4, 1..4 -> 1, 5 -> 0.  Smallest-last removes 5
+    (degree 0), then 4, 3, 2 (the last of bucket 1 each time; 0 drops to
+    degree 1 after three removals and is appended behind 1), then 0, then 1;
+    coloring in reverse removal order (1, 0, 2, 3, 4, 5) gives 1 -> 0, 0 -> 1,
+    2, 3, 4 -> 0, 5 -> 0: two seeds."""
+    ir = np.array([0, 0, 1, 1, 2, 2, 3, 3])
+    jc = np.array([0, 1, 0, 2, 0, 3, 0, 4])
+    for lib in ("hip", "oracle"):
+        color, k = _color_ordered(ir, jc, 4, 6, abi.MH_COLORING_SMALLEST_LAST, lib)
+        assert k == 2
+        assert color.tolist() == [1, 0, 0, 0, 0, 0]
