@@ -25,24 +25,29 @@ kernels are enqueued and the timed region ends with torch.cuda.synchronize()
                   cores, on a bounded sample of the same workload.
 
 --gpus N > 1 (one process per GPU, torch.distributed.run):
-  --multi mesh (default): the north star's layout -- ONE NLP for one host
-      optimizer, its mesh intervals sharded over the ranks; value = the
-      host-inclusive rate: x from page-locked host memory over each rank's
-      PCIe link, the shard's evaluation, each rank's DMA of its contiguous g /
-      Jacobian slice into its offset of one page-locked host buffer shared by
-      the node's ranks (mocohip.distributed.HostGather), a barrier;
-      "scaling": "strong", with "one_gpu_host_inclusive" (rank 0 alone, the
-      whole NLP, the same round trip) and their ratio "strong_scaling".
-      Beside it, labelled: "device_resident" (x already in HBM, results left
-      there -- an upper bound with no data movement), "x_broadcast" (+ an
-      RCCL broadcast of x per call), "replicas" (every rank its own NLP, weak
-      scaling), "inverse_solve_sweep" (configs[4]: 64 MocoInverse solves
-      distributed over the ranks) and "sharded_solve" (configs[2] solved by
-      one optimizer over all ranks, Jacobian slices to rank 0's HBM over
-      RCCL).
+  --multi mesh (default): the north star's layout -- ONE NLP (the N = 1
+      workload) for one optimizer, its mesh intervals sharded over the
+      ranks; value = calls/s of the whole data path per call: x broadcast
+      from rank 0 over RCCL, every rank's shard evaluation, the other ranks'
+      g / Jacobian slices received into rank 0's HBM over xGMI
+      (mocohip.distributed.SliceGather), so g and J are complete in rank 0's
+      HBM after every call -- the same quantity as the N = 1 headline (where
+      nothing moves); "scaling": "strong", with "one_gpu" (rank 0 alone on
+      the whole NLP, the N = 1 quantity) and their ratio "strong_scaling".
+      Labelled beside it: "device_resident" (each rank only evaluates its
+      shard, no broadcast / gather: an upper bound), "host_inclusive"
+      (HostGather: x from and g / J into page-locked host memory over each
+      rank's PCIe link), "replicas" (every rank its own NLP, weak scaling),
+      "inverse_solve_sweep" (configs[4]: 64 MocoInverse solves distributed
+      over the ranks) and "sharded_solve" (configs[2] solved by one
+      optimizer over all ranks).  The secondary legs run after the headline
+      under try/except and a watchdog (--leg-timeout): a failure lands in
+      "errors", never loses the line.
   --multi replicas: every rank evaluates its own NLP (independent trials,
       the configs[4] batch layout), no collective on the data path ->
       "scaling": "weak"; the mesh measurements ride along under "mesh".
+--shard-model (one GPU): the per-shard times and gather volumes of
+  DESIGN.md's multi-GPU model.
 
 Prints one JSON line on rank 0.
 """
@@ -106,6 +111,12 @@ def parse():
     ap.add_argument("--solve-intervals", type=int, default=200,
                     help="--multi mesh, N > 1: mesh intervals of the configs[2] solve sharded over the ranks "
                          "(0: skip)")
+    ap.add_argument("--leg-timeout", type=float, default=300.0,
+                    help="--gpus N > 1: seconds the secondary legs (replicas, sweep, sharded solve) may take "
+                         "after the headline before the line is printed without them")
+    ap.add_argument("--shard-model", action="store_true",
+                    help="one GPU: time rank 0's and the last rank's mesh shard of the headline NLP for "
+                         "W = 1, 2, 4, 8 (device-resident), the inputs of DESIGN.md's multi-GPU model")
     ap.add_argument("--batch-only", action="store_true",
                     help="print only the batch line (A/B of queue / launch settings)")
     return ap.parse_args()
@@ -161,7 +172,8 @@ class Ctx:
         torch.cuda.set_device(self.local)
         self.dev = torch.device("cuda", self.local)
         if self.world > 1:
-            dist.init_process_group("nccl", device_id=self.dev)
+            import datetime
+            dist.init_process_group("nccl", device_id=self.dev, timeout=datetime.timedelta(seconds=600))
         # a dedicated (non-null) stream made current: the contexts, torch's
         # tensors and the host copies all order on it (torch's default stream
         # has handle 0, which mh_set_stream reads as "the context's own
@@ -545,109 +557,136 @@ def solve_lines():
     return out
 
 
-def mesh_measure(cx, args):
-    """--multi mesh measurements: one NLP sharded by mesh interval over the
-    ranks (strong scaling of the north star's layout).  Returns (on rank 0)
-    the host-inclusive rate -- the host IPOPT's round trip: x from page-locked
-    host memory over each rank's PCIe link, the shard's evaluation, each
-    rank's g / J slice DMA into one page-locked host buffer shared by the
-    node's ranks (HostGather), a barrier -- and, labelled, the device-resident
-    rate (x already in every rank's HBM, results left there: no data moves,
-    an upper bound) and the same with an RCCL broadcast of x per call."""
+def _mesh_build(args):
     from mocohip import configs
-    from mocohip.distributed import HostGather, interval_shard
+    N = args.intervals
+    return ((lambda: configs.rajagopal80(N, fd_scheme=args.fd)) if args.config == "rajagopal80"
+            else (lambda: configs.gait10dof18musc(N, fd_scheme=args.fd)))
+
+
+def mesh_measure(cx, args):
+    """--gpus N > 1, the headline: ONE NLP (the N = 1 headline's workload)
+    sharded by mesh interval over the ranks, and per call the north star's
+    data path for a single optimizer -- x broadcast from rank 0 over RCCL,
+    each rank's shard evaluation, g and the Jacobian values reassembled in
+    rank 0's HBM (mocohip.distributed.SliceGather: the other ranks' slices
+    received point to point over xGMI into their offsets, rank 0's own
+    written in place).  At N = 1 there is nothing to broadcast or gather and
+    this is the single-GPU headline (g / J complete in the one GPU's HBM).
+    Rank 0 checks the reassembled vectors against one unsharded evaluation
+    (bit for bit).  Labelled beside it: "device_resident" (each rank only
+    evaluates its shard: no x broadcast, no gather -- an upper bound) and
+    "host_inclusive" (x from page-locked host memory over each rank's PCIe
+    link, each slice DMA'd into one page-locked host buffer shared by the
+    node's ranks, mocohip.distributed.HostGather)."""
+    from mocohip.distributed import HostGather, SliceGather, interval_shard
     torch, dist = cx.torch, cx.dist
     N = args.intervals
     ib, ie = interval_shard(N, cx.rank, cx.world)
-    build = ((lambda: configs.rajagopal80(N, fd_scheme=args.fd)) if args.config == "rajagopal80"
-             else (lambda: configs.gait10dof18musc(N, fd_scheme=args.fd)))
-    st = build()
-    nlp = make_nlp(cx, st, ib, ie, blocking=False)
+    build = _mesh_build(args)
+    nlp = make_nlp(cx, build(), ib, ie, blocking=False)
     x = track_iterate(nlp, 0)
-    sep, fused, (xd, gd, vd) = device_steps(cx, nlp, x)
+    xd = torch.tensor(x, dtype=torch.float64, device=cx.dev)
+    sg = SliceGather(nlp.m, nlp.nnz, (nlp.row_begin, nlp.row_end, nlp.nnz_begin, nlp.nnz_end), dist, cx.dev)
+    xp, gp, vp = xd.data_ptr(), sg.own_g.data_ptr(), sg.own_values.data_ptr()
+    fused_mode = args.mode == "fused"
+
+    def evaluate():
+        if fused_mode:
+            nlp.eval_g_jac_g_device(xp, gp, vp)
+            return sg.post("g") + sg.post("values")
+        nlp.eval_g_device(xp, gp)
+        rg = sg.post("g")                      # g's fan-in overlaps the Jacobian's kernels
+        nlp.eval_jac_g_device(xp, vp)
+        return rg + sg.post("values")
+
+    def step_reassembled():
+        if cx.world > 1:
+            dist.broadcast(xd, src=0)          # the iterate from rank 0 to every rank (RCCL)
+        sg.wait(evaluate())                    # the current stream waits for the fan-in
+
+    def step_device():                         # x resident in every rank's HBM, results left there
+        if fused_mode:
+            nlp.eval_g_jac_g_device(xp, gp, vp)
+        else:
+            nlp.eval_g_device(xp, gp)
+            nlp.eval_jac_g_device(xp, vp)
+    k, el = measure(cx, step_reassembled, args)
+    ok = None
+    if cx.rank == 0:
+        # the reassembled vectors against one unsharded evaluation
+        torch.cuda.synchronize()
+        full = make_nlp(cx, build(), blocking=True)
+        ok = bool(np.array_equal(sg.g[:nlp.m].cpu().numpy(), full.eval_g(x))
+                  and np.array_equal(sg.values[:nlp.nnz].cpu().numpy(), full.eval_jac_g(x)))
+        full.close()
+    if cx.world > 1:
+        dist.barrier()
+    kd, eld = measure(cx, step_device, args)
+    # host-inclusive: HostGather over each rank's PCIe link
     tag = os.environ.get("MOCOHIP_BENCH_TAG") or f"mocohip_bench_{os.getppid()}"
     barrier = dist.barrier if cx.world > 1 else (lambda: None)
     hg = HostGather(tag, nlp.m, nlp.nnz, (nlp.row_begin, nlp.row_end), (nlp.nnz_begin, nlp.nnz_end),
                     cx.rank, barrier, pin=True, device=cx.local)
     stream = cx.stream()
-    evaluate = fused if args.mode == "fused" else sep
-
     xh = torch.from_numpy(np.ascontiguousarray(x)).pin_memory()   # IPOPT's iterate on the host
-
-    def step_device():
-        evaluate()                             # x resident in every rank's HBM
-
-    def step_bcast():
-        if cx.world > 1:
-            dist.broadcast(xd, src=0)          # the iterate from rank 0 to every rank (RCCL)
-        evaluate()
 
     def step_host():
         xd.copy_(xh, non_blocking=True)        # the iterate from host memory over the rank's PCIe link
-        evaluate()
-        hg.copy_from_device_async(gd.data_ptr(), vd.data_ptr(), stream)
+        step_device()
+        hg.copy_from_device_async(gp, vp, stream)
         torch.cuda.current_stream().synchronize()
         if cx.world > 1:
             dist.barrier()                     # every slice has landed on the IPOPT host
     kh, elh = measure(cx, step_host, args, k=max(50, args.steps // 4), w=max(10, args.warmup // 10))
-    k, el = measure(cx, step_device, args)
-    kb, elb = measure(cx, step_bcast, args, k=max(50, args.steps // 4), w=max(10, args.warmup // 10))
-    ok = None
+    hok = None
     if cx.rank == 0:
-        # the reassembled host vectors against one unsharded evaluation
         full = make_nlp(cx, build(), blocking=True)
-        ok = bool(np.array_equal(hg.full_g(), full.eval_g(x))
-                  and np.array_equal(hg.full_values(), full.eval_jac_g(x)))
+        hok = bool(np.array_equal(hg.full_g(), full.eval_g(x)) and np.array_equal(hg.full_values(), full.eval_jac_g(x)))
         full.close()
     barrier()
     hg.close(unlink=cx.rank == 0)
-    out = {"value": round(kh / elh, 3), "unit": "calls/s", "steps": kh, "ms_per_step": round(1e3 * elh / kh, 5),
+    out = {"value": round(k / el, 3), "unit": "calls/s", "steps": k, "ms_per_step": round(1e3 * el / k, 5),
            "scaling": "strong", "mesh_intervals": N, "n": nlp.n, "m": nlp.m, "nnz_jac": nlp.nnz,
            "reassembly_bit_exact": ok,
-           "parallelism": f"mesh-shard{cx.world}: each rank its contiguous intervals, its g / J slice DMA'd "
-                          "over its own PCIe link into one page-locked host buffer (HostGather)",
-           "device_resident": {"value": round(k / el, 3), "unit": "calls/s", "steps": k,
-                               "ms_per_step": round(1e3 * el / k, 5),
-                               "note": "upper bound, not a deliverable rate: x already in every rank's HBM, "
-                                       "g / J left there (no data moves)"},
-           "x_broadcast": {"value": round(kb / elb, 3), "unit": "calls/s", "steps": kb,
-                           "ms_per_step": round(1e3 * elb / kb, 5),
-                           "note": "device-resident + an RCCL broadcast of x from rank 0 before every call"}}
+           "bytes_gathered_per_call": sg.bytes_received(),
+           "parallelism": f"mesh-shard{cx.world}: rank r evaluates intervals [N r / W, N (r + 1) / W); x broadcast "
+                          "from rank 0 (RCCL), every other rank's g / J slice received point to point (RCCL over "
+                          "xGMI, one grouped batch per vector) into rank 0's HBM",
+           "device_resident": {"value": round(kd / eld, 3), "unit": "calls/s", "steps": kd,
+                               "ms_per_step": round(1e3 * eld / kd, 5),
+                               "note": "upper bound, not a deliverable rate: x already in every rank's HBM, each "
+                                       "rank's g / J slice left in its own HBM (no broadcast, no gather)"},
+           "host_inclusive": {"value": round(kh / elh, 3), "unit": "calls/s", "steps": kh,
+                              "ms_per_step": round(1e3 * elh / kh, 5), "reassembly_bit_exact": hok,
+                              "note": "x from page-locked host memory over each rank's PCIe link, each rank's g / J "
+                                      "slice DMA'd into one page-locked host buffer shared by the node's ranks "
+                                      "(HostGather), a barrier"}}
     nlp.close()
     return out
 
 
-def one_gpu_host_inclusive(cx, args, build):
-    """The strong-scaling reference inside a multi-rank run: rank 0 alone
-    evaluates the WHOLE NLP host-inclusively (x in, g and J out over its
-    PCIe link every call) while the other ranks wait; None on other ranks."""
-    torch = cx.torch
+def one_gpu_reference(cx, args, build):
+    """The strong-scaling denominator inside a multi-rank run: rank 0 alone
+    evaluates the WHOLE NLP with x resident and g / J left in its HBM (the
+    N = 1 headline's quantity) while the other ranks wait; None elsewhere."""
     out = None
     if cx.rank == 0:
         nlp = make_nlp(cx, build(), blocking=False)
-        x = track_iterate(nlp, 0)
-        from mocohip import abi
-        xh = torch.from_numpy(np.ascontiguousarray(x)).pin_memory()
-        gh = torch.empty(nlp.m, dtype=torch.float64).pin_memory()
-        vh = torch.empty(nlp.nnz, dtype=torch.float64).pin_memory()
-        xn, gn, vn = xh.numpy(), gh.numpy(), vh.numpy()
-        xp, gp, vp = abi.dptr(xn), abi.dptr(gn), abi.dptr(vn)
-
-        def step():
-            nlp.lib.mh_eval_g(nlp.ctx, xp, 1, gp)
-            nlp.lib.mh_eval_jac_g(nlp.ctx, xp, 0, vp)
-        for _ in range(max(10, args.warmup // 10)):
+        sep, fused, _ = device_steps(cx, nlp, track_iterate(nlp, 0))
+        step = fused if args.mode == "fused" else sep
+        for _ in range(args.warmup):
             step()
-        k = max(50, args.steps // 4)
-        torch.cuda.synchronize()
+        cx.torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(k):
+        for _ in range(args.steps):
             step()
-        torch.cuda.synchronize()
+        cx.torch.cuda.synchronize()
         el = time.perf_counter() - t0
-        out = {"value": round(k / el, 3), "unit": "calls/s", "steps": k, "ms_per_step": round(1e3 * el / k, 5),
-               "note": "rank 0 alone, the whole NLP, host-inclusive (the same round trip as the headline "
-                       "on one GPU): the denominator of strong_scaling"}
+        out = {"value": round(args.steps / el, 3), "unit": "calls/s", "steps": args.steps,
+               "ms_per_step": round(1e3 * el / args.steps, 5),
+               "note": "rank 0 alone, the whole NLP, x resident and g / J left in its HBM (the N = 1 "
+                       "headline's quantity): the denominator of strong_scaling"}
         nlp.close()
     if cx.world > 1:
         cx.dist.barrier()
@@ -659,28 +698,39 @@ def sweep_distributed(cx, args):
     node's ranks -- rank r solves every W-th subject on its own GPU
     (mocohip.batchsolve.solve_sweep, rounds of <= 8 solver processes per
     GPU), no collective on the data path; the counts and the wall clock
-    (max over ranks) reduced at the end."""
+    (max over ranks) reduced at the end.  A rank whose share fails reports
+    zero solves and its error; every rank still reaches the reductions."""
     from mocohip import batchsolve
     torch, dist = cx.torch, cx.dist
     if cx.world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    r = batchsolve.solve_sweep(args.sweep, 125, rank=cx.rank, world=cx.world, device=cx.local)
+    err = None
+    try:
+        r = batchsolve.solve_sweep(args.sweep, 125, rank=cx.rank, world=cx.world, device=cx.local)
+    except Exception as e:   # noqa: BLE001 -- reported in the line, never fatal to it
+        r = {"solves": 0, "succeeded": 0, "wall_clock_s": 0.0, "rounds": 0, "mean_iterations": None}
+        err = f"rank {cx.rank}: {type(e).__name__}: {e}"
     el = time.perf_counter() - t0
-    t = torch.tensor([r["solves"], r["succeeded"]], dtype=torch.float64, device=cx.dev)
+    t = torch.tensor([r["solves"], r["succeeded"], 1.0 if err else 0.0], dtype=torch.float64, device=cx.dev)
     w = torch.tensor([el, r["wall_clock_s"]], dtype=torch.float64, device=cx.dev)
     if cx.world > 1:
         dist.all_reduce(t)
         dist.all_reduce(w, op=dist.ReduceOp.MAX)
-    solves, ok = int(t[0].item()), int(t[1].item())
+    solves, ok, failed = int(t[0].item()), int(t[1].item()), int(t[2].item())
     wall = float(w[1].item())
-    return {"solves": solves, "succeeded": ok, "ranks": cx.world, "solves_per_rank": r["solves"],
-            "rounds_per_rank": r["rounds"], "wall_clock_s": round(wall, 3),
-            "wall_clock_incl_setup_s": round(float(w[0].item()), 3),
-            "solves_per_minute": round(60.0 * solves / wall, 2) if wall > 0 else None,
-            "mean_iterations_rank0": r["mean_iterations"],
-            "workload": "configs[4]: 64 MocoInverse gait10dof18musc N=125 solves (scaled subjects), "
-                        "rank r solves subjects r, r+W, ... on its own GPU, <= 8 solver processes at once"}
+    out = {"solves": solves, "succeeded": ok, "ranks": cx.world, "solves_per_rank": r["solves"],
+           "rounds_per_rank": r["rounds"], "wall_clock_s": round(wall, 3),
+           "wall_clock_incl_setup_s": round(float(w[0].item()), 3),
+           "solves_per_minute": round(60.0 * solves / wall, 2) if wall > 0 else None,
+           "mean_iterations_rank0": r["mean_iterations"],
+           "workload": "configs[4]: 64 MocoInverse gait10dof18musc N=125 solves (scaled subjects), "
+                       "rank r solves subjects r, r+W, ... on its own GPU, <= 8 solver processes at once"}
+    if failed:
+        out["ranks_failed"] = failed
+    if err:
+        out["error"] = err
+    return out
 
 
 def sharded_solve(cx, args):
@@ -689,7 +739,10 @@ def sharded_solve(cx, args):
     with its Newton systems on its GPU over the whole Jacobian
     (ShardedDeviceKKT), every rank evaluates its mesh intervals, the other
     ranks' Jacobian slices arrive in rank 0's HBM over RCCL (send / recv,
-    xGMI).  Beside it the same solve on rank 0's GPU alone."""
+    xGMI).  Beside it the same solve on rank 0's GPU alone.  Rank 0 releases
+    the serving ranks whatever happens to its solve (close() in finally);
+    a serving rank whose evaluation fails answers with NaN so that the
+    protocol -- and the job -- keeps going, and the failure is reported."""
     from mocohip import configs
     from mocohip.distributed import ShardedNLP, interval_shard
     from mocohip.solver import HipNLP
@@ -701,9 +754,11 @@ def sharded_solve(cx, args):
     snlp = ShardedNLP(HipNLP(rep, st.solver.options(ib, ie)), cx.dist, transport="device", device=cx.local)
     out = None
     if cx.rank == 0:
-        sol = st.solve(nlp=snlp, linear_solver="device")
+        try:
+            sol = st.solve(nlp=snlp, linear_solver="device")
+        finally:
+            snlp.close()
         r = sol.stats
-        snlp.close()
         full = HipNLP(rep, st.solver.options())
         ref = st.solve(nlp=full, linear_solver="device").stats
         full.close()
@@ -717,29 +772,80 @@ def sharded_solve(cx, args):
                            "HBM over RCCL, Newton systems on rank 0's GPU)"}
     else:
         snlp.serve()
-    cx.dist.barrier()
+        if snlp.error:
+            out = {"error": snlp.error}
     return out
 
 
-def mesh_main(cx, args):
-    """--multi mesh: the headline is the host-inclusive rate of one NLP
-    sharded over the ranks (mesh_measure); replicas beside it."""
-    from mocohip import configs
-    m = mesh_measure(cx, args)
+def shard_model(cx, args):
+    """The inputs of DESIGN.md's multi-GPU model, measured on ONE GPU: for
+    W = 1, 2, 4, 8 the mesh shards of the headline NLP that rank 0 (the
+    endpoint head) and rank W - 1 (the tail) would own, each timed alone,
+    device-resident (K separate eval_g + eval_jac_g steps), and the bytes
+    rank 0 receives per call when the other W - 1 slices are gathered into its
+    HBM.  Predicted per-call time at W GPUs: max over the two shards + the
+    x broadcast + the slowest peer's slice over one xGMI link (each peer
+    sends over its own link), printed for two link rates (the 153 GB/s per
+    link figure of the task statement, and a 50 GB/s achieved P2P rate)."""
+    from mocohip.distributed import interval_shard
     N = args.intervals
-    build = ((lambda: configs.rajagopal80(N, fd_scheme=args.fd)) if args.config == "rajagopal80"
-             else (lambda: configs.gait10dof18musc(N, fd_scheme=args.fd)))
-    rnlp = make_nlp(cx, build(), blocking=False)
-    rsep, rfused, _ = device_steps(cx, rnlp, track_iterate(rnlp, cx.rank))
-    kr, elr = measure(cx, rfused if args.mode == "fused" else rsep, args)
-    rnlp.close()
-    one = sweep = solve = None
-    if not args.single_mode:
-        one = one_gpu_host_inclusive(cx, args, build)
-        if args.sweep > 0:
-            sweep = sweep_distributed(cx, args)
-        if cx.world > 1 and args.solve_intervals > 0:
-            solve = sharded_solve(cx, args)
+    build = _mesh_build(args)
+    full = make_nlp(cx, build(), blocking=False)
+    m, nnz, n = full.m, full.nnz, full.n
+    full.close()
+    out = {"mesh_intervals": N, "n": n, "m": m, "nnz_jac": nnz, "mode": "separate", "steps": args.steps, "W": {}}
+    for W in (1, 2, 4, 8):
+        row = {}
+        for r in sorted({0, W - 1}):
+            ib, ie = interval_shard(N, r, W)
+            nlp = make_nlp(cx, build(), ib, ie, blocking=False)
+            sep, _, bufs = device_steps(cx, nlp, track_iterate(nlp, 0))
+            k, el = measure(cx, sep, args)
+            row[f"rank{r}"] = {"intervals": [ib, ie], "ms_per_step": round(1e3 * el / k, 5),
+                               "rows": nlp.row_end - nlp.row_begin, "nnz": nlp.nnz_end - nlp.nnz_begin}
+            nlp.close()
+        r0 = row["rank0"]
+        slice_bytes = [8 * ((r["rows"]) + r["nnz"]) for key, r in row.items() if key != "rank0"]
+        peer = max(slice_bytes) if slice_bytes else 0
+        row["bytes_to_rank0"] = 8 * ((m - r0["rows"]) + (nnz - r0["nnz"])) if W > 1 else 0
+        row["largest_peer_slice_bytes"] = peer
+        t_eval = max(v["ms_per_step"] for k2, v in row.items() if k2.startswith("rank"))
+        xb = 8 * n
+        for name, bw in (("link153", 153e9), ("link50", 50e9)):
+            t = t_eval + (1e3 * (xb + peer) / bw if W > 1 else 0.0)
+            row[f"predicted_ms_{name}"] = round(t, 5)
+            row[f"predicted_calls_per_s_{name}"] = round(1e3 / t, 1)
+        out["W"][str(W)] = row
+    return out
+
+
+def guarded(cx, name, fn, errors):
+    """Run a secondary leg of the multi-GPU line; an exception is reported
+    under errors[name] instead of ending the job (the headline is already
+    measured).  Every rank then meets at a barrier."""
+    res = None
+    try:
+        res = fn()
+    except Exception as e:   # noqa: BLE001
+        errors[name] = f"rank {cx.rank}: {type(e).__name__}: {e}"
+    if cx.world > 1:
+        cx.dist.barrier()
+    return res
+
+
+def mesh_main(cx, args):
+    """--multi mesh (the default at N > 1): the headline is one NLP sharded
+    over the ranks with g / J reassembled in rank 0's HBM (mesh_measure),
+    against rank 0 alone on the whole NLP; the secondary legs follow under a
+    watchdog: if they do not finish within --leg-timeout seconds, rank 0
+    prints the line with the headline and what finished, and every rank
+    exits (a hung collective cannot lose the measured headline)."""
+    import threading
+    N = args.intervals
+    build = _mesh_build(args)
+    m = mesh_measure(cx, args)
+    one = one_gpu_reference(cx, args, build)
+    line = None
     if cx.rank == 0:
         wl = ("Rajagopal 80-muscle gait NLP (configs[3])" if args.config == "rajagopal80"
               else "MocoTrack gait10dof18musc DGF rigid tendon (configs[2])")
@@ -748,21 +854,57 @@ def mesh_main(cx, args):
                 "value": m["value"], "unit": "calls/s", "n_gpus": cx.world, "steps": m["steps"],
                 "warmup": args.warmup, "ms_per_step": m["ms_per_step"], "higher_is_better": True,
                 "scaling": "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-                "config": {"workload": wl + ", one NLP sharded by mesh interval for one host IPOPT "
-                                            "(host-inclusive: x in and g / J out over PCIe every call)",
+                "config": {"workload": wl + ", one NLP sharded by mesh interval for one optimizer: x broadcast "
+                                            "over RCCL, g / J reassembled in rank 0's HBM every call",
                            "mesh_intervals": N, "n": m["n"], "m": m["m"], "nnz_jac": m["nnz_jac"],
                            "fd": args.fd, "mode": args.mode, "parallelism": m["parallelism"]},
-                "device_resident": m["device_resident"], "x_broadcast": m["x_broadcast"],
                 "reassembly_bit_exact": m["reassembly_bit_exact"],
-                "replicas": {"value": round(kr * cx.world / elr, 3), "unit": "calls/s", "steps": kr,
-                             "scaling": "weak", "note": "every rank its own whole NLP, no collective"}}
+                "bytes_gathered_per_call": m["bytes_gathered_per_call"],
+                "device_resident": m["device_resident"], "host_inclusive": m["host_inclusive"]}
         if one is not None:
-            line["one_gpu_host_inclusive"] = one
-            line["strong_scaling"] = round(m["value"] / one["value"], 3)
+            line["one_gpu"] = one
+            line["strong_scaling"] = round(m["value"] / one["value"], 4)
+    if args.single_mode:
+        if cx.rank == 0:
+            print(json.dumps(line), flush=True)
+        return
+    errors = {}
+    done = threading.Event()
+
+    def fire():   # the watchdog: the measured headline survives a hung secondary leg
+        if done.is_set():
+            return
+        if cx.rank == 0:
+            line["errors"] = dict(errors, watchdog=f"secondary legs unfinished after {args.leg_timeout} s")
+            print(json.dumps(line), flush=True)
+        os._exit(0)
+    timer = threading.Timer(args.leg_timeout, fire)
+    timer.daemon = True
+    timer.start()
+
+    def replicas():
+        rnlp = make_nlp(cx, build(), blocking=False)
+        rsep, rfused, _ = device_steps(cx, rnlp, track_iterate(rnlp, cx.rank))
+        kr, elr = measure(cx, rfused if args.mode == "fused" else rsep, args)
+        rnlp.close()
+        return {"value": round(kr * cx.world / elr, 3), "unit": "calls/s", "steps": kr, "scaling": "weak",
+                "note": "every rank its own whole NLP, no collective"}
+    rep_line = guarded(cx, "replicas", replicas, errors)
+    sweep = solve = None
+    if args.sweep > 0:
+        sweep = guarded(cx, "inverse_solve_sweep", lambda: sweep_distributed(cx, args), errors)
+    if cx.world > 1 and args.solve_intervals > 0:
+        solve = guarded(cx, "sharded_solve", lambda: sharded_solve(cx, args), errors)
+    done.set()
+    timer.cancel()
+    if cx.rank == 0:
+        line["replicas"] = rep_line
         if sweep is not None:
             line["inverse_solve_sweep"] = sweep
         if solve is not None:
             line["sharded_solve"] = solve
+        if errors:
+            line["errors"] = errors
         print(json.dumps(line), flush=True)
 
 
@@ -776,6 +918,11 @@ def main():
         # GPU, weak scaling) rides along in its line.  N = 1: the single-GPU
         # headline below.
         args.multi = "mesh" if cx.world > 1 else "replicas"
+    if args.shard_model:
+        res = shard_model(cx, args)
+        if cx.rank == 0:
+            print(json.dumps(res), flush=True)
+        return
     if args.multi == "mesh":
         mesh_main(cx, args)
         if cx.world > 1:

@@ -228,6 +228,90 @@ class HostGather:
             os.unlink(self.path)
 
 
+class SliceGather:
+    """g and the Jacobian values of ONE NLP reassembled in rank 0's device
+    memory from the ranks' mesh shards (the north star's
+    "RCCL all-gather over xGMI to reassemble g and the CSR Jacobian" --
+    only rank 0, where the optimizer's Newton systems are factored, needs the
+    whole vectors, so it is a fan-in, not an all-gather: every other rank sends
+    its contiguous slice (CasOCTranscription.h:219-313) point to point and
+    rank 0 receives them straight into their offsets, one grouped
+    batch_isend_irecv per vector, so the W - 1 transfers run concurrently, each
+    on its own xGMI link).
+
+    Rank 0 allocates the whole-NLP buffers ``g`` (m) and ``values`` (nnz);
+    its own context writes its slice in place through the views ``own_g`` /
+    ``own_values`` (no copy); the other ranks' ``own_*`` are buffers of their
+    slice length.  ``ranges[r]`` = rank r's (row_begin, row_end, nnz_begin,
+    nnz_end), all-gathered at construction.  Tensors live on ``device`` (a
+    CUDA device: RCCL P2P over xGMI with backend nccl; the CPU: gloo, as in
+    tests/test_distributed.py)."""
+
+    def __init__(self, m: int, nnz: int, mine, dist, device):
+        import torch
+        self.torch, self.dist = torch, dist
+        single = not dist.is_initialized()    # one process: nothing to gather
+        self.rank, self.world = (0, 1) if single else (dist.get_rank(), dist.get_world_size())
+        self.m, self.nnz = int(m), int(nnz)
+        self.device = torch.device(device)
+        t = torch.tensor([int(v) for v in mine], dtype=torch.int64, device=self.device)
+        got = [torch.zeros_like(t) for _ in range(self.world)]
+        if single:
+            got[0] = t
+        else:
+            dist.all_gather(got, t)
+        self.ranges = [tuple(int(v) for v in a.cpu()) for a in got]
+        rb, re, nb, ne = self.ranges[self.rank]
+        # the slices must tile [0, m) and [0, nnz) in rank order
+        for which, total in ((0, self.m), (2, self.nnz)):
+            pos = 0
+            for r in range(self.world):
+                b, e = self.ranges[r][which], self.ranges[r][which + 1]
+                if b != pos or e < b:
+                    raise ValueError(f"rank {r}'s slice [{b}, {e}) does not continue at {pos}")
+                pos = e
+            if pos != total:
+                raise ValueError(f"the slices end at {pos}, not {total}")
+        f64 = torch.float64
+        if self.rank == 0:
+            self.g = torch.zeros(max(1, self.m), dtype=f64, device=self.device)
+            self.values = torch.zeros(max(1, self.nnz), dtype=f64, device=self.device)
+            self.own_g, self.own_values = self.g[rb:re], self.values[nb:ne]
+        else:
+            self.g = self.values = None
+            self.own_g = torch.zeros(max(1, re - rb), dtype=f64, device=self.device)[:re - rb]
+            self.own_values = torch.zeros(max(1, ne - nb), dtype=f64, device=self.device)[:ne - nb]
+
+    def post(self, which: str):
+        """Start the fan-in of ``which`` ("g" or "values") after the shard's
+        evaluation was enqueued on the current stream; returns the requests
+        (``wait`` them before reading rank 0's buffer)."""
+        dist = self.dist
+        k = 0 if which == "g" else 2
+        ops = []
+        if self.rank == 0:
+            whole = self.g if which == "g" else self.values
+            for r in range(1, self.world):
+                b, e = self.ranges[r][k], self.ranges[r][k + 1]
+                if e > b:
+                    ops.append(dist.P2POp(dist.irecv, whole[b:e], r))
+        else:
+            own = self.own_g if which == "g" else self.own_values
+            if own.numel():
+                ops.append(dist.P2POp(dist.isend, own, 0))
+        return dist.batch_isend_irecv(ops) if ops else []
+
+    @staticmethod
+    def wait(reqs):
+        for q in reqs:
+            q.wait()
+
+    def bytes_received(self) -> int:
+        """Bytes rank 0 receives per g + Jacobian reassembly."""
+        rb, re, nb, ne = self.ranges[0]
+        return 8 * ((self.m - (re - rb)) + (self.nnz - (ne - nb)))
+
+
 # ---------------------------------------------------------------------------
 # One solve spanning several GPUs: the optimizer on rank 0, the evaluation
 # sharded by mesh interval (SURVEY.md §8 E2-E3).
@@ -282,6 +366,7 @@ class ShardedNLP:
         self._dkkt = None
         self._vbuf = None      # this rank's device slice buffer (transport "device")
         self.closed = False
+        self.error = None      # serving ranks: the first evaluation failure (answered with NaN)
 
     def __getattr__(self, name):
         # problem attributes (opts, G, NS, NC, rep, NSL, NEP, tail_rows, ...)
@@ -327,10 +412,15 @@ class ShardedNLP:
         vector), the other ranks' slices received into their offsets."""
         b0, e0 = self.ranges[0][which], self.ranges[0][which + 1]
         out[b0:e0] = self._tensor(own) if not isinstance(own, self.torch.Tensor) else own
+        # the other ranks' slices as one grouped batch of receives (they run
+        # concurrently, each from its own peer)
+        ops = []
         for r in range(1, self.world):
             b, e = self.ranges[r][which], self.ranges[r][which + 1]
             if e > b:
-                self.dist.recv(out[b:e], src=r)
+                ops.append(self.dist.P2POp(self.dist.irecv, out[b:e], r))
+        for q in (self.dist.batch_isend_irecv(ops) if ops else []):
+            q.wait()
         return out
 
     def _send_slice(self, v):
@@ -391,27 +481,46 @@ class ShardedNLP:
                 self.closed = True
                 return served
             served += 1
-            if op == OP_JAC_DEV and self.transport == "device":
-                # the slice stays on the GPU: evaluated into a device buffer
-                # on a dedicated stream, sent GPU to GPU from that stream
-                if self._vbuf is None:
-                    self._vbuf = t.zeros(max(1, self.shard.nnz_end - self.shard.nnz_begin),
-                                         dtype=t.float64, device=self.device)
-                    self._stream = t.cuda.Stream(device=self.device)
-                    self.shard.set_stream(self._stream.cuda_stream)
-                self._stream.wait_stream(t.cuda.current_stream(self.device))   # x has arrived
-                with t.cuda.stream(self._stream):
-                    self.shard.eval_jac_g_device(xt.data_ptr(), self._vbuf.data_ptr())
-                    self._send_slice(self._vbuf[:self.shard.nnz_end - self.shard.nnz_begin])
-                continue
-            x = xt.cpu().numpy()
-            if op == OP_F:
-                self._sum_to_root([self.shard.eval_f_partial(x)])
-            elif op == OP_GRAD:
-                self._sum_to_root(self.shard.eval_grad_f_partial(x))
-            elif op == OP_G:
-                self._send_slice(self.shard.eval_g(x))
-            elif op in (OP_JAC, OP_JAC_DEV):
-                self._send_slice(self.shard.eval_jac_g(x))
-            else:
-                raise RuntimeError(f"unknown request {op}")
+            try:
+                self._answer(op, xt)
+            except Exception as e:   # noqa: BLE001 -- keep the protocol (and rank 0) going
+                if self.error is None:
+                    self.error = f"rank {self.rank}, request {op}: {type(e).__name__}: {e}"
+                self._answer_nan(op)
+
+    def _answer_nan(self, op):
+        """The reply to a request whose evaluation failed: NaN of the reply's
+        shape (the optimizer sees a non-finite value and stops)."""
+        if op in (OP_F, OP_GRAD):
+            self._sum_to_root(np.full(1 if op == OP_F else self.n, np.nan))
+        elif op == OP_G:
+            self._send_slice(np.full(self.shard.row_end - self.shard.row_begin, np.nan))
+        elif op in (OP_JAC, OP_JAC_DEV):
+            self._send_slice(np.full(self.shard.nnz_end - self.shard.nnz_begin, np.nan))
+
+    def _answer(self, op, xt):
+        t = self.torch
+        if op == OP_JAC_DEV and self.transport == "device":
+            # the slice stays on the GPU: evaluated into a device buffer
+            # on a dedicated stream, sent GPU to GPU from that stream
+            if self._vbuf is None:
+                self._vbuf = t.zeros(max(1, self.shard.nnz_end - self.shard.nnz_begin),
+                                     dtype=t.float64, device=self.device)
+                self._stream = t.cuda.Stream(device=self.device)
+                self.shard.set_stream(self._stream.cuda_stream)
+            self._stream.wait_stream(t.cuda.current_stream(self.device))   # x has arrived
+            with t.cuda.stream(self._stream):
+                self.shard.eval_jac_g_device(xt.data_ptr(), self._vbuf.data_ptr())
+                self._send_slice(self._vbuf[:self.shard.nnz_end - self.shard.nnz_begin])
+            return
+        x = xt.cpu().numpy()
+        if op == OP_F:
+            self._sum_to_root([self.shard.eval_f_partial(x)])
+        elif op == OP_GRAD:
+            self._sum_to_root(self.shard.eval_grad_f_partial(x))
+        elif op == OP_G:
+            self._send_slice(self.shard.eval_g(x))
+        elif op in (OP_JAC, OP_JAC_DEV):
+            self._send_slice(self.shard.eval_jac_g(x))
+        else:
+            raise RuntimeError(f"unknown request {op}")

@@ -357,7 +357,11 @@ class ShardedDeviceKKT(DeviceKKT):
         torch = snlp.torch
         self.snlp = snlp
         shard = snlp.shard
-        dev = snlp.device if snlp.transport == "device" else torch.device("cuda", torch.cuda.current_device())
+        # the shard context's own GPU (mh_options.device), which its kernels
+        # write the Jacobian slice on, for both transports
+        dev = torch.device("cuda", int(shard.opts.device))
+        if snlp.transport == "device" and snlp.device != dev:
+            raise ValueError(f"ShardedNLP device {snlp.device} is not the shard context's {dev}")
         self.dev = dev
         # the shard context's kernels, the received slices and the module's
         # kernels ordered on one dedicated stream (not torch's default one,
@@ -382,15 +386,22 @@ class ShardedDeviceKKT(DeviceKKT):
         snlp._request(OP_JAC_DEV, x)
         with torch.cuda.stream(self.stream):
             self._check(self.lib.mh_kkt_eval_jacobian(self.h, _dp(x)))
+            # the other ranks' slices: one grouped batch of receives (the
+            # peers' transfers run concurrently, each over its own link)
+            ops, staged = [], []
             for r in range(1, snlp.world):
                 b, e = snlp.ranges[r][2], snlp.ranges[r][3]
                 if e <= b:
                     continue
                 if snlp.transport == "device":
-                    snlp.dist.recv(self.vals[b:e], src=r)
+                    ops.append(snlp.dist.P2POp(snlp.dist.irecv, self.vals[b:e], r))
                 else:
                     buf = torch.empty(e - b, dtype=torch.float64)
-                    snlp.dist.recv(buf, src=r)
-                    self.vals[b:e].copy_(buf)
+                    ops.append(snlp.dist.P2POp(snlp.dist.irecv, buf, r))
+                    staged.append((b, e, buf))
+            for q in (snlp.dist.batch_isend_irecv(ops) if ops else []):
+                q.wait()
+            for b, e, buf in staged:
+                self.vals[b:e].copy_(buf)
             self._check(self.lib.mh_kkt_assemble(self.h))
         self._tick("eval_jacobian", t0)

@@ -211,3 +211,70 @@ def test_sweep_rank_partition():
     assert rank_share(s, 0, 1) == s
     with pytest.raises(ValueError):
         rank_share(s, 8, 8)
+
+
+# ---------------------------------------------------------------------------
+# The multi-GPU headline's reassembly (bench.py --gpus N > 1): every rank's
+# g / Jacobian slice into its offset of rank 0's whole-NLP buffers
+# (mocohip.distributed.SliceGather; RCCL P2P over xGMI on the GPUs, gloo here).
+# ---------------------------------------------------------------------------
+def _gather_worker(rank, world, port, case, N, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mocohip.distributed import SliceGather
+        st = CASES[case](N)
+        rep = st.problem.create_rep()
+        ib, ie = interval_shard(N, rank, world)
+        shard = OracleNLP(rep, st.solver.options(ib, ie), threads=1)
+        sg = SliceGather(shard.m, shard.nnz, (shard.row_begin, shard.row_end, shard.nnz_begin, shard.nnz_end),
+                         dist, "cpu")
+        ok = True
+        for it in range(2):   # two calls through the same buffers
+            x = torch.zeros(shard.n, dtype=torch.float64)
+            if rank == 0:
+                x[:] = torch.from_numpy(shard.random_iterate(np.random.default_rng(11 + it).uniform(-1, 1, shard.n)))
+            dist.broadcast(x, src=0)
+            xn = x.numpy()
+            # the shard's results land in its own slice buffers (rank 0: views
+            # of the whole vectors), then the fan-in
+            sg.own_g.copy_(torch.from_numpy(shard.eval_g(xn)))
+            rg = sg.post("g")
+            sg.own_values.copy_(torch.from_numpy(shard.eval_jac_g(xn)))
+            rv = sg.post("values")
+            sg.wait(rg)
+            sg.wait(rv)
+            if rank == 0:
+                full = OracleNLP(rep, st.solver.options(), threads=1)
+                ok = ok and np.array_equal(sg.g.numpy()[:full.m], full.eval_g(xn))
+                ok = ok and np.array_equal(sg.values.numpy()[:full.nnz], full.eval_jac_g(xn))
+                rb, re, nb, ne = sg.ranges[0]
+                ok = ok and sg.bytes_received() == 8 * ((full.m - (re - rb)) + (full.nnz - (ne - nb)))
+                full.close()
+        # the ranges tile the whole vectors in rank order
+        if rank == 0:
+            ok = ok and sg.ranges[0][0] == 0 and sg.ranges[-1][1] == shard.m
+            ok = ok and sg.ranges[0][2] == 0 and sg.ranges[-1][3] == shard.nnz
+        out[rank] = int(bool(ok))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case,N,world", [("pendulum", 7, 2), ("gait", 6, 3), ("pendulum_implicit", 16, 8),
+                                          ("inverse", 9, 8), ("gait_pathcon", 5, 3)])
+def test_slice_gather_reassembles_on_rank0(case, N, world):
+    """SliceGather (world 2 / 3 / 8 over gloo, oracle shard contexts): rank
+    0's whole-NLP g and Jacobian buffers, filled by its own shard in place and
+    by the other ranks' slices at their offsets, equal the unsharded
+    evaluation bit for bit, call after call."""
+    ctx = mp.get_context("spawn")
+    out = ctx.Array("i", [0] * world)
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, case, N, out)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(300)
+        assert p.exitcode == 0
+    assert list(out) == [1] * world
