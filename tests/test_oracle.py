@@ -279,16 +279,22 @@ def test_muscle_geometry_matches_reference_gso_fiber_lengths():
     from InverseMuscleSolverMotionData.cpp:49-114 (_gso_preprocess).
     Residual: the fiber velocity of the two muscles with MovingPathPoints
     (rect_fem_r, vasti_r) is off by up to 3.8e-5 within 0.03 s of the final
-    time, where the knee angle crosses the three knots their SimmSplines put
-    within 3.5e-4 rad of zero and the differentiated length spline amplifies
-    rounding-level length differences; every other velocity and every length
-    is within 1e-5."""
+    time; every other velocity is within 5e-7 and every length within 2.7e-6.
+    tools/gso_bisect.py (profiles/r06_gso) localizes it: at the golden times
+    that coincide with samples (every 0.05 s) our lengths equal the golden
+    ones up to a constant per-muscle offset to 1e-9 m, and per-sample length
+    perturbations ONLY at the samples from t = 1.833 s on (the last two data
+    rows and the padded rows after the data end) reproduce the window's
+    errors to 6e-10 m -- the residual comes from how the end of the data
+    enters the length spline, not from the path geometry at the golden times;
+    no restated stage variant (pad, time pad, filter step / start, spline
+    degree / end conditions / smoothing, selection) reproduces it."""
     nfl_err, nfv_err, t = _gso_errors(configs.gait10dof18musc_model())
     assert nfl_err.max() <= 1e-5, nfl_err.max(0)
     z = np.load(os.path.join(os.path.dirname(__file__), "golden", "gso_norm_fiber_length.npz"))
     moving = [i for i, l in enumerate(z["nfl_labels"][1:]) if l.split("/")[-1] in ("rect_fem_r", "vasti_r")]
     other = np.setdiff1d(np.arange(nfv_err.shape[1]), moving)
-    assert nfv_err[:, other].max() <= 1e-5, nfv_err.max(0)
+    assert nfv_err[:, other].max() <= 5e-7, nfv_err.max(0)
     assert nfv_err[t < 1.77][:, moving].max() <= 1e-5, nfv_err.max(0)
     assert nfv_err.max() <= 5e-5, nfv_err.max(0)
     # sensitivity: one vasti_r path point moved by 1 mm is far outside this
@@ -330,7 +336,8 @@ def _gso_errors(m):
     """|normalized fiber length / velocity - GSO golden| per (time,
     right-leg muscle), and the golden times.  InverseMuscleSolverMotionData:
     rows within [0.58 - 0.05, 1.8 + 0.05] s (:49-59), Storage::pad(size/2) and
-    lowpassIIR at 6 Hz (:62-71), muscle-tendon lengths at every padded row
+    lowpassIIR at 6 Hz (:62-71; on the .mot's non-uniform 8-decimal times
+    after resampling to the smallest step), muscle-tendon lengths at every padded row
     (:91-111), GCVSplineSet (degree 5, zero error variance: the interpolating
     natural quintic, mocohip.splines) evaluated and differentiated at the
     solution times (:249-290), then calcRigidTendonFiberKinematics
@@ -349,7 +356,21 @@ def _gso_errors(m):
                   else kin[sel, kl.index(q)] for q in qnames], 1)
     p = len(t) // 2
     tp = _gso_pad(t, p)
-    Q = np.stack([_gso_lowpass(t[1] - t[0], 6.0, _gso_pad(Q[:, j], p)) for j in range(Q.shape[1])], 1)
+    Q = np.stack([_gso_pad(Q[:, j], p) for j in range(Q.shape[1])], 1)
+    # the .mot's times are printed to 8 decimals, so its steps alternate
+    # between 0.01666667 and 0.01666666: Storage::lowpassIIR on non-uniform
+    # times resamples onto the uniform grid of the smallest step (degree-5 GCV
+    # spline, Storage::resample) and filters with that step.  Restated so
+    # (opensim-core is absent: inferred, tools/gso_bisect.py): it takes every
+    # velocity but the two knee-crossing muscles' end window from 2.3e-6 to
+    # 1.9e-7 of the golden file.
+    dtmin = float(np.diff(tp).min())
+    tn = tp[0] + np.arange(len(tp)) * dtmin
+    brk, co = gcv_interpolating_ppoly(tp, Q, 5)
+    seg = np.clip(np.searchsorted(brk, tn, side="right") - 1, 0, len(brk) - 2)
+    Q = sum(co[seg, :, k] * (tn - brk[seg])[:, None] ** k for k in range(co.shape[2]))
+    tp = tn
+    Q = np.stack([_gso_lowpass(dtmin, 6.0, Q[:, j]) for j in range(Q.shape[1])], 1)
     names = [mu.name for mu in m.muscles]
     cols = [names.index(l.split("/")[-1]) for l in gl[1:]]
     L = np.zeros((len(tp), len(cols)))
