@@ -235,6 +235,18 @@ typedef struct mh_path_wrap {
     int32_t range_end;   /*                                       < 1 = last  */
 } mh_path_wrap;
 
+/* OpenSim SpringGeneralizedForce (ABI v8; Simulation/Model, opensim-core,
+ * third-party): the generalized force  -stiffness (q - rest_length) -
+ * viscosity u  on coordinate `coord`, added to the applied forces like a
+ * coordinate actuator's (testMocoParameters.cpp:52-57). */
+typedef struct mh_spring {
+    int32_t coord;
+    int32_t reserved;
+    double stiffness;
+    double rest_length;
+    double viscosity;
+} mh_spring;
+
 typedef struct mh_model {
     int32_t nq;          /* coordinates (= speeds)                          */
     int32_t nbodies;
@@ -268,6 +280,9 @@ typedef struct mh_model {
     int32_t npathwraps;     /* PathWrap entries over all muscles               */
     const mh_wrap_object* wraps;
     const mh_path_wrap* pathwraps;
+    int32_t nsprings;       /* SpringGeneralizedForce elements (ABI v8)        */
+    int32_t reserved_sp;
+    const mh_spring* springs;
 } mh_model;
 
 /* ------------------------------------------------------------------------ */
@@ -369,6 +384,31 @@ typedef struct mh_endpoint_equation {
     mh_bounds g;         /* bounds on the row                              */
 } mh_endpoint_equation;
 
+/* MocoParameter (ABI v8; Moco/Moco/MocoParameter.h:31-170): a scalar NLP
+ * variable written into model properties before every evaluation
+ * (MocoCasOCProblem.h:508-515, applyParametersToModelProperties).  The
+ * parameters are the LAST block of x ("parameters", CasOCIterate.h:27-44
+ * key order, CasOCTranscription.cpp:141), bounded by the MocoParameter's
+ * bounds, their guess the bounds' midpoint.  One parameter may write several
+ * properties (a MocoParameter over several components); each written
+ * property is one target: */
+enum mh_parameter_kind {
+    MH_PARAM_BODY_MASS = 0,            /* Body mass                           */
+    MH_PARAM_BODY_MASS_CENTER = 1,     /* Body mass_center[element]           */
+    MH_PARAM_BODY_INERTIA = 2,         /* Body inertia[element], xx yy zz xy xz yz */
+    MH_PARAM_SPRING_STIFFNESS = 3,     /* SpringGeneralizedForce stiffness    */
+    MH_PARAM_SPRING_REST_LENGTH = 4,   /* SpringGeneralizedForce rest_length  */
+    MH_PARAM_SPRING_VISCOSITY = 5,     /* SpringGeneralizedForce viscosity    */
+    MH_PARAM_ACTUATOR_OPTIMAL_FORCE = 6,   /* CoordinateActuator optimal_force */
+    MH_PARAM_MUSCLE_MAX_ISOMETRIC_FORCE = 7 /* DGF max_isometric_force         */
+};
+typedef struct mh_parameter_target {
+    int32_t parameter;   /* index of the NLP parameter                          */
+    int32_t kind;        /* mh_parameter_kind                                   */
+    int32_t index;       /* body / spring / actuator / muscle index             */
+    int32_t element;     /* vector element (mass_center, inertia); else 0      */
+} mh_parameter_target;
+
 typedef struct mh_problem {
     mh_model model;
     mh_bounds time_initial;      /* bounds on initial_time                  */
@@ -408,6 +448,21 @@ typedef struct mh_problem {
      * NaN/NaN = the default [0, 0], MocoProblem.cpp:42). */
     mh_bounds multiplier_bounds;
     mh_bounds kinematic_constraint_bounds;
+    /* MocoParameters (ABI v8, see mh_parameter_target): NP NLP variables
+     * after the derivatives; every per-point callback (DAE, path
+     * constraints) and the endpoint equations take them as inputs, so each
+     * of those rows carries NP dense parameter columns (the last columns of
+     * x), whose values are the finite-difference quotients of the callback
+     * along the parameter (the property perturbed by the FD step) chained
+     * through the transcription like the t0 / tf columns.  The goals of
+     * mh_goal_kind do not read the model's parameterized properties: their
+     * gradient along a parameter is 0.  Generic device interpreter only (a
+     * generated back end folds the properties into its constant pool); no
+     * sparsity detection, no batches. */
+    int32_t nparameters;
+    int32_t nparameter_targets;
+    const mh_bounds* parameter_bounds;            /* [nparameters]             */
+    const mh_parameter_target* parameter_targets; /* [nparameter_targets]      */
 } mh_problem;
 
 enum mh_scheme { MH_HERMITE_SIMPSON = 0, MH_TRAPEZOIDAL = 1 };
@@ -553,6 +608,13 @@ const char* mh_build_id(void);
 
 int mh_create(const mh_problem* problem, const mh_options* options,
         mh_ctx** ctx);
+/* The sizes mh_create would give this problem and options, host only (no
+ * device, no context): n, m, the grid, states / controls, the shard's rows;
+ * nnz_jac_g and the shard's nonzeros of the block-dense structure (sparsity
+ * detection, which needs the device, can only remove nonzeros).  Lets a
+ * host size an initial-guess iterate (mh_options.sparsity_guess: n doubles)
+ * before mh_create reads it. */
+int mh_get_nlp_info_for(const mh_problem* problem, const mh_options* options, mh_nlp_info* info);
 void mh_destroy(mh_ctx* ctx);
 
 int mh_get_nlp_info(const mh_ctx* ctx, mh_nlp_info* info);

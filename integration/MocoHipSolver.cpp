@@ -17,6 +17,7 @@
 #include "MocoHipSolver.h"
 
 #include <OpenSim/Actuators/CoordinateActuator.h>
+#include <OpenSim/Actuators/SpringGeneralizedForce.h>
 #include <OpenSim/Common/Constant.h>
 #include <OpenSim/Common/GCVSpline.h>
 #include <OpenSim/Common/GCVSplineSet.h>
@@ -326,6 +327,19 @@ void compileModel(const Model& model, mhb::Problem& prob) {
                     a.getName(), a.getConcreteClassName());
         }
     }
+    // SpringGeneralizedForces (-stiffness (q - rest_length) - viscosity u on
+    // their coordinate; testMocoParameters.cpp:50-55)
+    for (const SpringGeneralizedForce& f : model.getComponentList<SpringGeneralizedForce>()) {
+        if (!f.get_appliesForce()) continue;
+        mhb::SpringGeneralizedForce hs;
+        hs.name = f.getName();
+        hs.path = f.getAbsolutePathString();
+        hs.coordinate = f.get_coordinate();
+        hs.stiffness = f.getStiffness();
+        hs.rest_length = f.getRestLength();
+        hs.viscosity = f.getViscosity();
+        m.add_spring(hs);
+    }
     // ExternalForces on ground-expressed data (ModOpAddExternalLoads): one
     // table per data source, cubic GCV splines as ExternalForce builds them
     int ntab = 0;
@@ -499,6 +513,21 @@ mhb::Problem OpenSim::compileProblemRep(const MocoProblemRep& rep) {
         hc.equality_with_lower = cb->getEqualityWithLower();
         prob.path_constraints.push_back(hc);
     }
+    // MocoParameters in createParameterNames order (the x layout's last
+    // block); mhb::make_rep resolves the component paths and properties and
+    // throws MocoParameter::initializeOnModel's errors for the rest (a
+    // property this build does not parameterize, e.g. optimal_fiber_length,
+    // is refused there by name)
+    for (const std::string& name : rep.createParameterNames()) {
+        const MocoParameter& par = rep.getParameter(name);
+        mhb::Parameter hp;
+        hp.name = name;
+        hp.component_paths = par.getComponentPaths();
+        hp.property_name = par.getPropertyName();
+        hp.bounds = toBounds(par.getBounds());
+        hp.property_element = par.getProperty_property_element().size() ? par.get_property_element() : -1;
+        prob.parameters.push_back(hp);
+    }
     return prob;
 }
 
@@ -588,6 +617,9 @@ mhb::TrajectoryTable toTable(const MocoTrajectory& t) {
     take(t.getMultiplierNames(), t.getMultipliersTrajectory(), T.multiplier_names, T.multipliers);
     take(t.getDerivativeNames(), t.getDerivativesTrajectory(), T.derivative_names, T.derivatives);
     take(t.getSlackNames(), t.getSlacksTrajectory(), T.slack_names, T.slacks);
+    T.parameter_names = t.getParameterNames();
+    const SimTK::RowVector& pv = t.getParameters();
+    for (int j = 0; j < pv.size(); ++j) T.parameters.push_back(pv[j]);
     return T;
 }
 
@@ -613,10 +645,12 @@ MocoSolution toSolution(const std::vector<double>& x, const mhb::ProblemRep& hre
             for (size_t j = 0; j < nv; ++j) M(k, (int)j) = d[(size_t)k * nv + j];
         return M;
     };
+    SimTK::RowVector parameters((int)T.parameters.size());
+    for (int j = 0; j < parameters.size(); ++j) parameters[j] = T.parameters[(size_t)j];
     MocoSolution sol(SimTK::Vector(G, T.time.data()), T.state_names, T.control_names, T.multiplier_names,
-            T.derivative_names, {}, matrix(T.states, T.state_names.size()),
+            T.derivative_names, T.parameter_names, matrix(T.states, T.state_names.size()),
             matrix(T.controls, T.control_names.size()), matrix(T.multipliers, T.multiplier_names.size()),
-            matrix(T.derivatives, T.derivative_names.size()), SimTK::RowVector());
+            matrix(T.derivatives, T.derivative_names.size()), parameters);
     const int N = o.num_mesh_intervals;
     const int nsl = (int)T.slack_names.size();
     if (nsl) {
@@ -681,6 +715,14 @@ MocoSolution MocoHipSolver::solveImpl() const {
     std::vector<double> x0;
     const MocoTrajectory& guess = getGuess();
     if (!guess.empty()) x0 = toIterate(guess, hrep, opt);
+    // the library's n before mh_create reads the guess (n doubles): the
+    // host-only layout query, so a layout mismatch is an error, not a read
+    // past the iterate
+    mh_nlp_info layout{};
+    OPENSIM_THROW_IF(mh_get_nlp_info_for(&hrep.problem, &opt, &layout) != MH_OK, Exception,
+            "MocoHipSolver: {}", mh_last_error());
+    OPENSIM_THROW_IF(!x0.empty() && (int64_t)x0.size() != layout.n, Exception,
+            "MocoHipSolver: the guess iterate has {} values, the problem has n = {}", x0.size(), layout.n);
     if (opt.sparsity_detection == MH_SPARSITY_INITIAL_GUESS) opt.sparsity_guess = x0.empty() ? nullptr : x0.data();
     CtxGuard ctx;
     OPENSIM_THROW_IF(mh_create(&hrep.problem, &opt, &ctx.ctx) != MH_OK, Exception,

@@ -1102,8 +1102,14 @@ __device__ __forceinline__ double jac_entry(const Layout& L, const Lanes& Ln, co
     const int s = T.s, dir = T.dir;
     double v = 0.0;
     switch (T.kind) {
+    // t0 / tf columns, and (dir >= 2) the parameter columns of a row: a
+    // parameter moves no time, so only the callbacks' quotients remain
     case T_HERM_T: {
         const int ki = k_first, kp = k_first + 2;
+        if (dir >= 2) {
+            v = 0.0 - C.h8 * (dxdot(L, Ln, Y, ki, s, dir) - dxdot(L, Ln, Y, kp, s, dir));
+            break;
+        }
         const double fi = xdot_at(L, Ln, x, Y, ki, s), fp = xdot_at(L, Ln, x, Y, kp, s);
         v = (dir == 0 ? C.g8 : -C.g8) * (fi - fp) -
             C.h8 * (dxdot(L, Ln, Y, ki, s, dir) - dxdot(L, Ln, Y, kp, s, dir));
@@ -1111,6 +1117,11 @@ __device__ __forceinline__ double jac_entry(const Layout& L, const Lanes& Ln, co
     }
     case T_SIMP_T: {
         const int ki = k_first, km = k_first + 1, kp = k_first + 2;
+        if (dir >= 2) {
+            v = 0.0 - C.h6 * (dxdot(L, Ln, Y, kp, s, dir) + 4.0 * dxdot(L, Ln, Y, km, s, dir) +
+                              dxdot(L, Ln, Y, ki, s, dir));
+            break;
+        }
         const double fi = xdot_at(L, Ln, x, Y, ki, s), fm = xdot_at(L, Ln, x, Y, km, s),
                      fp = xdot_at(L, Ln, x, Y, kp, s);
         v = (dir == 0 ? C.g6 : -C.g6) * (fp + 4.0 * fm + fi) -
@@ -1150,6 +1161,10 @@ __device__ __forceinline__ double jac_entry(const Layout& L, const Lanes& Ln, co
         break;
     case T_TRAP_T: {
         const int ki = k_first, kp = k_first + 1;
+        if (dir >= 2) {
+            v = 0.0 - C.hh * (dxdot(L, Ln, Y, kp, s, dir) + dxdot(L, Ln, Y, ki, s, dir));
+            break;
+        }
         const double fi = xdot_at(L, Ln, x, Y, ki, s), fp = xdot_at(L, Ln, x, Y, kp, s);
         v = (dir == 0 ? C.gh : -C.gh) * (fp + fi) -
             C.hh * (dxdot(L, Ln, Y, kp, s, dir) + dxdot(L, Ln, Y, ki, s, dir));
@@ -2120,6 +2135,24 @@ struct mh_ctx {
     // endpoint constraints: the head of g (rows 0..nep) and of the Jacobian
     // (entries 0..nnz_ep), owned by the shard with interval 0
     int nep = 0, nnz_ep = 0;
+    // MocoParameters (mh_problem.parameter_*): NPAR NLP variables at x[XP..];
+    // the device model's parameterized arrays (bodies, actuators, muscles,
+    // springs) exist in NCOPY copies: copy 0 with the iterate's parameter
+    // values, copy 1 + p (and 1 + NPAR + p for central differences) with
+    // parameter p moved by the finite-difference step; k_apply_params writes
+    // them from the pristine arrays before every evaluation.  Each parameter
+    // direction's lanes run as their own k_eval launch over its copy (Mp).
+    int NPAR = 0, NCOPY = 1;
+    int64_t XP = 0;
+    std::vector<mh_bounds> par_bounds;
+    std::vector<mh_parameter_target> par_targets;
+    mh_parameter_target* d_par_targets = nullptr;
+    std::vector<DevModel> Mp;          // [NCOPY]: Mp[0] = M
+    DevModel M0{};                     // the pristine model (mh_eval_dae)
+    int* d_lane_main = nullptr;        // Jacobian lanes that are not parameter lanes
+    int n_lane_main = 0;
+    int* d_par_lanes = nullptr;        // the lane of copy cp (cp >= 1) at [cp - 1]
+    int nsprings = 0;
     std::vector<mh_endpoint_equation> ep;
     std::vector<TplEntry> eptpl;       // row = equation, dir = endpoint input index
     std::vector<uint8_t> sp_ep;        // detected [equation][2 (1 + NI)] (empty: dense)
@@ -2345,6 +2378,21 @@ static void be_eval_lane(mh_ctx* c, const double* x, int mode, double* Y) {
     const Lanes& ln = mode ? c->lanes_jac : c->lanes_g;
     const long lanes = (long)c->nk * ln.stride;
     const bool exc = mode && c->d_exc && D::EXC_LANES;
+    if (mode && c->NPAR > 0) {
+        // MocoParameters: the lanes that perturb no parameter over the
+        // iterate's model copy (c->M), then each parameter lane over its own
+        // copy (Mp[cp]), one lane per grid point -- the kernels as they are
+        const long nm = (long)c->nk * c->n_lane_main;
+        hipLaunchKernelGGL(k_eval<D>, dim3((unsigned)((nm + 63) / 64)), dim3(64), 0, c->stream, c->M, L, ln, x,
+                c->d_grid, c->d_times, Y, c->d_lane_main, c->n_lane_main);
+        if (exc)
+            hipLaunchKernelGGL(k_exc_lanes<D>, dim3((unsigned)((lanes + 63) / 64)), dim3(64), 0, c->stream, c->M,
+                    L, ln, x, Y, c->d_exc);
+        for (int cp = 1; cp < c->NCOPY; ++cp)
+            hipLaunchKernelGGL(k_eval<D>, dim3((unsigned)((c->nk + 63) / 64)), dim3(64), 0, c->stream, c->Mp[cp],
+                    L, ln, x, c->d_grid, c->d_times, Y, c->d_par_lanes + (cp - 1), 1);
+        return;
+    }
     if (!exc) {
         // eval_g of the generic interpreter: fewer lanes per workgroup (one
         // wave each) keep a wave's scratch within its CU's L1
@@ -2608,7 +2656,8 @@ static void be_grad(mh_ctx* c, const double* x) {
 template <class D>
 static void be_probe_lane(mh_ctx* c, int np, const double* in, double* out) {
     Layout L = make_layout(c, 0, 0);
-    hipLaunchKernelGGL(k_dae_probe<D>, dim3((np + 63) / 64), dim3(64), 0, c->stream, c->M, L, np, in,
+    // the pristine model: a probe point carries no parameter values
+    hipLaunchKernelGGL(k_dae_probe<D>, dim3((np + 63) / 64), dim3(64), 0, c->stream, c->M0, L, np, in,
             out);
 }
 // mh_eval_dae through the task kernels: explicit points, base lanes only.

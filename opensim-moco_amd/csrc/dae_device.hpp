@@ -67,6 +67,9 @@ struct DevModel {
     // generated back ends: the model's constant pool (codegen.py
     // "Structure-only specialization"; <Name>_fill at mh_create), else null
     const double* pool;
+    // SpringGeneralizedForce elements (ABI v8)
+    int nsp;
+    const mh_spring* sp;
 };
 // The generated code reads the constant pool through the constant address
 // space: the pool does not change during a launch, so its wave-uniform reads
@@ -834,6 +837,12 @@ __device__ void dae_eval(const DevModel& M, Work<MB, MQ, MP>& w, double time, co
     for (int ia = 0; ia < M.nact; ++ia) {
         const mh_actuator A = M.acts[ia];
         if (A.kind == MH_ACT_COORDINATE) w.tau[A.target] += c[ia] * A.optimal_force;
+    }
+    // ---- SpringGeneralizedForce: -stiffness (q - rest_length) - viscosity u
+    for (int is = 0; is < M.nsp; ++is) {
+        const mh_spring S = M.sp[is];
+        const double f = -S.stiffness * (q[S.coord] - S.rest_length) - S.viscosity * u[S.coord];
+        w.tau[S.coord] += f;
     }
     // ---- kinematic constraint forces -G^T lambda (MocoCasOCProblem.h:643-662)
     for (int i = 0; i < M.nkc; ++i) {

@@ -76,6 +76,10 @@ void Model::add_coordinate_actuator(CoordinateActuator a) {
     coordinate_actuators.push_back(std::move(a));
     actuators.emplace_back(false, (int)coordinate_actuators.size() - 1);
 }
+void Model::add_spring(SpringGeneralizedForce f) {
+    if (f.path.empty()) f.path = "/forceset/" + f.name;
+    springs.push_back(std::move(f));
+}
 void Model::add_marker(Marker m) {
     if (m.path.empty()) m.path = "/markerset/" + m.name;
     for (auto& x : markers)
@@ -168,6 +172,7 @@ void CompiledModel::bind() {
     model.constraints = ptr(constraints);
     model.wraps = ptr(wraps);
     model.pathwraps = ptr(pathwraps);
+    model.springs = ptr(springs);
 }
 
 void compile_model(const Model& M, const std::vector<Table>& extra_tables, CompiledModel& C) {
@@ -360,6 +365,14 @@ void compile_model(const Model& M, const std::vector<Table>& extra_tables, Compi
         ks.scale = k.scale_factor;
         C.constraints.push_back(ks);
     }
+    for (auto& f : M.springs) {
+        mh_spring ss{};
+        ss.coord = C.index_of_coord(f.coordinate);
+        ss.stiffness = f.stiffness;
+        ss.rest_length = f.rest_length;
+        ss.viscosity = f.viscosity;
+        C.springs.push_back(ss);
+    }
 
     mh_model& mm = C.model;
     mm = mh_model{};
@@ -379,6 +392,7 @@ void compile_model(const Model& M, const std::vector<Table>& extra_tables, Compi
     for (int k = 0; k < 3; ++k) mm.gravity[k] = M.gravity[k];
     mm.nwraps = (int)C.wraps.size();
     mm.npathwraps = (int)C.pathwraps.size();
+    mm.nsprings = (int)C.springs.size();
     C.state_names = M.state_names();
     C.control_names = M.control_names();
     C.bind();
@@ -397,6 +411,8 @@ void ProblemRep::bind() {
     problem.path = ptr(path);
     problem.kinematics_column = ptr(kin_cols);
     problem.endpoint = ptr(endpoint);
+    problem.parameter_bounds = ptr(parameter_bounds);
+    problem.parameter_targets = ptr(parameter_targets);
 }
 
 namespace {
@@ -496,6 +512,91 @@ void path_equations(const Problem& P, std::vector<mh_path_equation>& eqs, std::v
     }
 }
 }  // namespace
+
+// MocoParameter::initializeOnModel (problem.py ProblemRep._parameter_targets):
+// every component path names a component owning the property; vector
+// properties need an element in range, scalar ones none.
+static void parameter_targets(const Problem& P, const CompiledModel& C, ProblemRep& R) {
+    const Model& model = P.model;
+    struct Prop { const char* name; int kind; int nel; const char* owner; };
+    static const Prop props[] = {
+        {"mass", MH_PARAM_BODY_MASS, 0, "body"},
+        {"mass_center", MH_PARAM_BODY_MASS_CENTER, 3, "body"},
+        {"inertia", MH_PARAM_BODY_INERTIA, 6, "body"},
+        {"stiffness", MH_PARAM_SPRING_STIFFNESS, 0, "spring"},
+        {"rest_length", MH_PARAM_SPRING_REST_LENGTH, 0, "spring"},
+        {"viscosity", MH_PARAM_SPRING_VISCOSITY, 0, "spring"},
+        {"optimal_force", MH_PARAM_ACTUATOR_OPTIMAL_FORCE, 0, "actuator"},
+        {"max_isometric_force", MH_PARAM_MUSCLE_MAX_ISOMETRIC_FORCE, 0, "muscle"},
+    };
+    auto find = [&](const std::string& path, int& idx) -> std::string {
+        std::string key = path;
+        while (!key.empty() && key.back() == '/') key.pop_back();
+        key = key.substr(key.find_last_of('/') == std::string::npos ? 0 : key.find_last_of('/') + 1);
+        for (auto& b : model.bodies)
+            if (path == b.name || path == "/bodyset/" + b.name || path == "/" + b.name) {
+                idx = C.index_of_body(b.name);
+                return "body";
+            }
+        for (size_t i = 0; i < model.springs.size(); ++i) {
+            const auto& f = model.springs[i];
+            if (path == f.name || path == f.path || key == f.name) { idx = (int)i; return "spring"; }
+        }
+        for (size_t i = 0; i < model.actuators.size(); ++i) {
+            const auto& a = model.actuators[i];
+            const std::string& n = a.first ? model.muscles[a.second].name : model.coordinate_actuators[a.second].name;
+            const std::string& pth = a.first ? model.muscles[a.second].path : model.coordinate_actuators[a.second].path;
+            if (path == n || path == pth) {
+                idx = a.first ? a.second : (int)i;
+                return a.first ? "muscle" : "actuator";
+            }
+        }
+        fail("MocoParameter: no component '" + path + "' in the model");
+        return "";
+    };
+    std::vector<std::string> names;
+    for (size_t ip = 0; ip < P.parameters.size(); ++ip) {
+        const Parameter& par = P.parameters[ip];
+        if (std::find(names.begin(), names.end(), par.name) != names.end())
+            fail("MocoParameter '" + par.name + "': duplicate name");
+        names.push_back(par.name);
+        if (par.component_paths.empty()) fail("MocoParameter '" + par.name + "': no component paths");
+        const Prop* pr = nullptr;
+        for (auto& x : props)
+            if (par.property_name == x.name) pr = &x;
+        if (!pr)
+            fail("MocoParameter '" + par.name + "': property '" + par.property_name +
+                 "' is not a parameterizable property of this build");
+        int elem = 0;
+        if (pr->nel) {
+            if (par.property_element < 0 || par.property_element >= pr->nel)
+                fail("MocoParameter '" + par.name + "': property '" + par.property_name +
+                     "' needs an element in [0, " + std::to_string(pr->nel) + ")");
+            elem = par.property_element;
+        } else if (par.property_element >= 0) {
+            fail("MocoParameter '" + par.name + "': a property element was given for the scalar property '" +
+                 par.property_name + "'");
+        }
+        for (auto& path : par.component_paths) {
+            int idx = -1;
+            const std::string what = find(path, idx);
+            if (what != pr->owner)
+                fail("MocoParameter '" + par.name + "': component '" + path + "' (" + what +
+                     ") has no property '" + par.property_name + "'");
+            mh_parameter_target t{};
+            t.parameter = (int32_t)ip;
+            t.kind = pr->kind;
+            t.index = idx;
+            t.element = elem;
+            R.parameter_targets.push_back(t);
+        }
+        mh_bounds b{};
+        b.lower = par.bounds.lower;
+        b.upper = par.bounds.upper;
+        R.parameter_bounds.push_back(b);
+        R.parameter_names.push_back(par.name);
+    }
+}
 
 void make_rep(const Problem& P, ProblemRep& R) {
     R = ProblemRep();
@@ -683,6 +784,9 @@ void make_rep(const Problem& P, ProblemRep& R) {
     }
     p.npath = (int)R.path.size();
     p.nendpoint = (int)R.endpoint.size();
+    parameter_targets(P, R.cm, R);
+    p.nparameters = (int)R.parameter_bounds.size();
+    p.nparameter_targets = (int)R.parameter_targets.size();
     p.multiplier_bounds.lower = P.multiplier_bounds.lower;
     p.multiplier_bounds.upper = P.multiplier_bounds.upper;
     p.kinematic_constraint_bounds.lower = P.kinematic_constraint_bounds.lower;
@@ -760,7 +864,7 @@ mh_options make_options(const SolverSettings& s, int interval_begin, int interva
     return o;
 }
 
-// ---- the tape (mocohip/tape.py write_tape, version 7) -----------------------
+// ---- the tape (mocohip/tape.py write_tape, version 8) -----------------------
 namespace {
 struct Out {
     std::string b;
@@ -786,7 +890,7 @@ void write_tape(const ProblemRep& R, const mh_options& o0, const std::string& pa
     o.sparsity_pattern = nullptr;
     Out w;
     w.bytes("MHTAPE01", 8);
-    const int32_t head[3] = {7, ns, nc};
+    const int32_t head[3] = {8, ns, nc};
     w.bytes(head, sizeof head);
     w.pod(o);
     const int32_t counts[12] = {m.nq, m.nbodies, m.naxes, m.nfunctions, m.nknots, m.nmuscles,
@@ -832,6 +936,12 @@ void write_tape(const ProblemRep& R, const mh_options& o0, const std::string& pa
     w.blob(m.wraps, m.nwraps);
     w.pod(m.npathwraps);
     w.blob(m.pathwraps, m.npathwraps);
+    w.pod(m.nsprings);
+    w.blob(m.springs, m.nsprings);
+    w.pod(p.nparameters);
+    w.blob(p.parameter_bounds, p.nparameters);
+    w.pod(p.nparameter_targets);
+    w.blob(p.parameter_targets, p.nparameter_targets);
     std::ofstream f(path, std::ios::binary);
     if (!f) fail("cannot write " + path);
     f.write(w.b.data(), (std::streamsize)w.b.size());
@@ -1056,6 +1166,15 @@ void read_description(const std::string& path, Problem& P, SolverSettings& S) {
             a.max_control = t.d();
             a.path = t.s();
             M.add_coordinate_actuator(a);
+        } else if (rec == "spring") {
+            SpringGeneralizedForce f;
+            f.name = t.s();
+            f.coordinate = t.s();
+            f.stiffness = t.d();
+            f.rest_length = t.d();
+            f.viscosity = t.d();
+            f.path = t.s();
+            M.add_spring(f);
         } else if (rec == "marker") {
             Marker mk;
             mk.name = t.s();
@@ -1134,6 +1253,15 @@ void read_description(const std::string& path, Problem& P, SolverSettings& S) {
             pc.upper = read_bound_fn(t);
             pc.equality_with_lower = t.i() != 0;
             P.path_constraints.push_back(pc);
+        } else if (rec == "parameter") {
+            Parameter par;
+            par.name = t.s();
+            par.property_name = t.s();
+            par.property_element = (int)t.i();
+            par.bounds = read_bounds(t);
+            const long n = t.i();
+            for (long k = 0; k < n; ++k) par.component_paths.push_back(t.s());
+            P.parameters.push_back(par);
         } else if (rec == "position_motion") {
             if (t.word() != "table") fail("description: position_motion needs a table");
             P.position_motion = read_table(t);

@@ -122,6 +122,13 @@ struct CoordinateActuator {
     std::string path;
 };
 
+// SpringGeneralizedForce (model.py SpringGeneralizedForce; mh_spring)
+struct SpringGeneralizedForce {
+    std::string name, coordinate;
+    double stiffness = 0.0, rest_length = 0.0, viscosity = 0.0;
+    std::string path;   // "/forceset/<name>" unless given
+};
+
 struct Marker {
     std::string name, body;
     double location[3] = {0, 0, 0};
@@ -164,6 +171,7 @@ public:
     std::vector<Marker> markers;
     std::vector<CoordinateCoupler> constraints;
     std::vector<WrapCylinder> wraps;
+    std::vector<SpringGeneralizedForce> springs;
 
     void add_body(const Body& b) { bodies.push_back(b); }
     void add_joint(Joint j);
@@ -174,6 +182,7 @@ public:
     void add_marker(Marker m);
     void add_constraint(const CoordinateCoupler& k) { constraints.push_back(k); }
     void add_wrap(const WrapCylinder& w) { wraps.push_back(w); }
+    void add_spring(SpringGeneralizedForce f);
 
     std::vector<const Joint*> tree_order() const;
     std::vector<const Coordinate*> coordinates() const;
@@ -197,6 +206,7 @@ struct CompiledModel {
     std::vector<mh_constraint> constraints;
     std::vector<mh_wrap_object> wraps;
     std::vector<mh_path_wrap> pathwraps;
+    std::vector<mh_spring> springs;
     std::vector<std::string> state_names, control_names;
     std::vector<std::pair<std::string, int>> body_index, qidx, table_index;
     std::vector<std::pair<std::string, std::vector<std::string>>> table_columns;
@@ -251,8 +261,19 @@ struct ControlBoundConstraint {
     bool equality_with_lower = false;
 };
 
+// MocoParameter (problem.py MocoParameter; MocoParameter.h:91-170):
+// property_element -1 for a scalar property
+struct Parameter {
+    std::string name;
+    std::vector<std::string> component_paths;
+    std::string property_name;
+    Bounds bounds;
+    int property_element = -1;
+};
+
 struct Problem {
     Model model;
+    std::vector<Parameter> parameters;
     Bounds time_initial, time_final;
     std::vector<std::pair<std::string, VariableInfo>> state_infos, control_infos;
     std::vector<Goal> goals;
@@ -274,6 +295,9 @@ struct ProblemRep {
     std::vector<mh_path_equation> path;
     std::vector<mh_endpoint_equation> endpoint;
     std::vector<int32_t> kin_cols;
+    std::vector<mh_bounds> parameter_bounds;
+    std::vector<mh_parameter_target> parameter_targets;
+    std::vector<std::string> parameter_names;
     int num_aux_residuals = 0;
     // the reference's names of the multipliers, slacks, accelerations (implicit
     // multibody dynamics) and implicit auxiliary derivatives (make_rep)
@@ -307,7 +331,7 @@ struct SolverSettings {
 };
 mh_options make_options(const SolverSettings& s, int interval_begin = 0, int interval_end = 0);
 
-// The problem tape of mocohip/tape.py (version 6), byte for byte.
+// The problem tape of mocohip/tape.py (version 8), byte for byte.
 void write_tape(const ProblemRep& rep, const mh_options& o, const std::string& path);
 
 // The text description written by mocohip/describe.py.

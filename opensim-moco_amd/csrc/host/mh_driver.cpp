@@ -86,6 +86,9 @@ struct Tape {
     std::vector<mh_constraint> constraints;
     std::vector<mh_wrap_object> wraps;
     std::vector<mh_path_wrap> pathwraps;
+    std::vector<mh_spring> springs;
+    std::vector<mh_bounds> par_bounds;
+    std::vector<mh_parameter_target> par_targets;
     std::vector<double> guess;
     std::vector<uint8_t> pattern;
     std::vector<int32_t> kin_col;
@@ -114,9 +117,12 @@ bool read_tape(const char* path, Tape& t, std::string& err) {
     // shorter one; version 5 appends the wrap surfaces; version 6 carries ABI
     // v6's mh_options (+ sparsity_rule: 8 bytes; older tapes leave it 0, the
     // reference's rule since v7); version 7: ABI v7 (the rule's values
-    // swapped: a v6 tape's 0 / 1 was robust / any-change)
-    if (version < 4 || version > 7) {
-        err = "unsupported tape version (this build reads versions 4 to 7)";
+    // swapped: a v6 tape's 0 / 1 was robust / any-change); version 8: ABI v8
+    // (coloring_order in mh_options' former reserved word; the springs and
+    // the MocoParameters appended; the initial-guess blob is the whole
+    // iterate, n doubles)
+    if (version < 4 || version > 8) {
+        err = "unsupported tape version (this build reads versions 4 to 8)";
         return false;
     }
     {
@@ -191,6 +197,14 @@ bool read_tape(const char* path, Tape& t, std::string& err) {
         m.npathwraps = r.pod<int32_t>();
         t.pathwraps = r.array<mh_path_wrap>(m.npathwraps);
     }
+    if (version >= 8) {   // springs, MocoParameters
+        m.nsprings = r.pod<int32_t>();
+        t.springs = r.array<mh_spring>(m.nsprings);
+        t.prob.nparameters = r.pod<int32_t>();
+        t.par_bounds = r.array<mh_bounds>(t.prob.nparameters);
+        t.prob.nparameter_targets = r.pod<int32_t>();
+        t.par_targets = r.array<mh_parameter_target>(t.prob.nparameter_targets);
+    }
     if (!r.ok || r.pos != r.buf.size()) { err = "truncated or malformed tape"; return false; }
     m.bodies = t.bodies.data(); m.axes = t.axes.data(); m.functions = t.functions.data();
     m.knot_x = t.knot_x.data(); m.knot_y = t.knot_y.data(); m.muscles = t.muscles.data();
@@ -210,6 +224,23 @@ bool read_tape(const char* path, Tape& t, std::string& err) {
     m.constraints = t.constraints.empty() ? nullptr : t.constraints.data();
     m.wraps = t.wraps.empty() ? nullptr : t.wraps.data();
     m.pathwraps = t.pathwraps.empty() ? nullptr : t.pathwraps.data();
+    m.springs = t.springs.empty() ? nullptr : t.springs.data();
+    t.prob.parameter_bounds = t.par_bounds.empty() ? nullptr : t.par_bounds.data();
+    t.prob.parameter_targets = t.par_targets.empty() ? nullptr : t.par_targets.data();
+    // the initial-guess iterate must be the whole x (mh_options.sparsity_guess:
+    // n doubles, read by mh_create): sized against the host-only layout query
+    if (!t.guess.empty()) {
+        mh_nlp_info info{};
+        if (mh_get_nlp_info_for(&t.prob, &t.opts, &info) != MH_OK) {
+            err = std::string("tape problem rejected: ") + mh_last_error();
+            return false;
+        }
+        if ((int64_t)t.guess.size() != info.n) {
+            err = "the tape's initial-guess iterate has " + std::to_string(t.guess.size()) + " doubles, the "
+                  "problem has n = " + std::to_string(info.n);
+            return false;
+        }
+    }
     return true;
 }
 

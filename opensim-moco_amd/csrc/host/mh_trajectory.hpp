@@ -10,7 +10,8 @@
 // include/mocohip.h): t0, tf, states NS x G grid-major, controls NC x G,
 // multipliers NM x G, slacks NSL x N (one per mesh interval, at the
 // Hermite-Simpson midpoints), derivatives NDV x G (accelerations of implicit
-// multibody dynamics, then implicit auxiliary derivatives).
+// multibody dynamics, then implicit auxiliary derivatives), parameters NPAR
+// (MocoParameters, CasOCIterate.h: Var::parameters).
 #ifndef MOCOHIP_HOST_MH_TRAJECTORY_HPP
 #define MOCOHIP_HOST_MH_TRAJECTORY_HPP
 
@@ -27,14 +28,15 @@ namespace mhb {
 // The block sizes of one transcription (what mh_get_nlp_info reports,
 // computed from the rep and options without a context).
 struct IterateLayout {
-    int N = 0, G = 0, NS = 0, NC = 0, NM = 0, NSL = 0, NACC = 0, NAR = 0;
+    int N = 0, G = 0, NS = 0, NC = 0, NM = 0, NSL = 0, NACC = 0, NAR = 0, NPAR = 0;
     bool hs = true;
     int NDV() const { return NACC + NAR; }
-    long n() const { return 2 + (long)(NS + NC + NM + NDV()) * G + (long)NSL * N; }
+    long n() const { return 2 + (long)(NS + NC + NM + NDV()) * G + (long)NSL * N + NPAR; }
     long off_controls() const { return 2 + (long)NS * G; }
     long off_multipliers() const { return off_controls() + (long)NC * G; }
     long off_slacks() const { return off_multipliers() + (long)NM * G; }
     long off_derivatives() const { return off_slacks() + (long)NSL * N; }
+    long off_parameters() const { return off_derivatives() + (long)NDV() * G; }
 };
 
 inline IterateLayout iterate_layout(const ProblemRep& R, const mh_options& o) {
@@ -52,6 +54,7 @@ inline IterateLayout iterate_layout(const ProblemRep& R, const mh_options& o) {
     L.NSL = (L.hs && !o.ignore_constraint_derivatives && !presc) ? L.NM : 0;
     L.NACC = (o.multibody_dynamics_mode == MH_DYNAMICS_IMPLICIT && !presc) ? R.cm.model.nq : 0;
     L.NAR = R.num_aux_residuals;
+    L.NPAR = (int)R.parameter_bounds.size();
     return L;
 }
 
@@ -103,6 +106,8 @@ inline TrajectoryTable iterate_to_trajectory(const std::vector<double>& x, const
     T.multiplier_names = R.multiplier_names;
     T.derivative_names = derivative_names(R, L);
     T.slack_names.assign(R.slack_names.begin(), R.slack_names.begin() + L.NSL);
+    T.parameter_names = R.parameter_names;
+    T.parameters.assign(x.begin() + L.off_parameters(), x.begin() + L.off_parameters() + L.NPAR);
     auto block = [&](long off, int nv, std::vector<double>& out) {
         out.assign((size_t)G * nv, 0.0);
         for (int k = 0; k < G; ++k)
@@ -121,7 +126,9 @@ inline TrajectoryTable iterate_to_trajectory(const std::vector<double>& x, const
 
 // The trajectory (already resampled onto the grid times, e.g. by OpenSim's
 // MocoTrajectory::resample) -> x; blocks the guess does not name stay 0, its
-// slacks are read at the midpoints (convertToCasOCIterate).
+// slacks are read at the midpoints (convertToCasOCIterate); parameters by
+// name, a missing one at its bounds' midpoint (the bounds guess,
+// CasOCTranscription.cpp:1124-1139; mocohip/trajectory.py to_iterate).
 inline std::vector<double> trajectory_to_iterate(const TrajectoryTable& T, const ProblemRep& R,
         const mh_options& o) {
     const IterateLayout L = iterate_layout(R, o);
@@ -151,23 +158,33 @@ inline std::vector<double> trajectory_to_iterate(const TrajectoryTable& T, const
         const std::vector<std::string> sn(R.slack_names.begin(), R.slack_names.begin() + L.NSL);
         fill(sn, T.slack_names, T.slacks, L.off_slacks(), true);
     }
+    for (int q = 0; q < L.NPAR; ++q) {
+        const mh_bounds& b = R.parameter_bounds[q];
+        const bool set = !std::isnan(b.lower) && !std::isnan(b.upper);
+        const double l = set ? b.lower : -INFINITY, u = set ? b.upper : INFINITY;
+        double v = !std::isinf(l) && !std::isinf(u) ? 0.5 * (u + l) : !std::isinf(l) ? l : !std::isinf(u) ? u : 0.0;
+        for (size_t h = 0; h < T.parameter_names.size(); ++h)
+            if (T.parameter_names[h] == R.parameter_names[q] && h < T.parameters.size()) { v = T.parameters[h]; break; }
+        x[(size_t)(L.off_parameters() + q)] = v;
+    }
     return x;
 }
 
 // MocoTrajectory::write's .sto (MocoTrajectory.cpp: the block counts as
 // header metadata, sorted, then DataType / version, endheader, a time column
-// and the states, controls, multipliers, derivatives, slacks; NaN where a
-// slack has no value).
+// and the states, controls, multipliers, derivatives, slacks, parameters; NaN
+// where a slack has no value; the parameters in the first row, NaN below,
+// convertToTable).
 inline void write_sto(const TrajectoryTable& T, const std::string& path) {
     FILE* f = std::fopen(path.c_str(), "w");
     if (!f) throw std::runtime_error("cannot write " + path);
     const size_t G = T.time.size();
     std::fprintf(f, "MocoHipSolution\nnum_controls=%zu\nnum_derivatives=%zu\nnum_multipliers=%zu\n"
-                    "num_parameters=0\nnum_slacks=%zu\nnum_states=%zu\nDataType=double\nversion=3\nendheader\ntime",
+                    "num_parameters=%zu\nnum_slacks=%zu\nnum_states=%zu\nDataType=double\nversion=3\nendheader\ntime",
                  T.control_names.size(), T.derivative_names.size(), T.multiplier_names.size(),
-                 T.slack_names.size(), T.state_names.size());
+                 T.parameter_names.size(), T.slack_names.size(), T.state_names.size());
     for (auto* names : {&T.state_names, &T.control_names, &T.multiplier_names, &T.derivative_names,
-                        &T.slack_names})
+                        &T.slack_names, &T.parameter_names})
         for (auto& n : *names) std::fprintf(f, "\t%s", n.c_str());
     std::fprintf(f, "\n");
     for (size_t k = 0; k < G; ++k) {
@@ -184,6 +201,10 @@ inline void write_sto(const TrajectoryTable& T, const std::string& path) {
         row(T.multipliers, T.multiplier_names.size());
         row(T.derivatives, T.derivative_names.size());
         row(T.slacks, T.slack_names.size());
+        for (size_t j = 0; j < T.parameter_names.size(); ++j) {
+            if (k == 0 && j < T.parameters.size()) std::fprintf(f, "\t%.17g", T.parameters[j]);
+            else std::fprintf(f, "\tNaN");
+        }
         std::fprintf(f, "\n");
     }
     std::fclose(f);

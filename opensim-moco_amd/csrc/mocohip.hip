@@ -82,6 +82,65 @@ int mh_launch_exc_fill(const mh_ctx* c, int nk, int NO, int stride, int base, in
     return MH_OK;
 }
 
+// MocoParameters (applyParametersToModelProperties before every
+// evaluation, MocoCasOCProblem.h:309,508-515): every model copy starts as
+// the pristine arrays (copied as 8-byte words), then each target property
+// gets its parameter's value -- copy 0 the iterate's, copy cp >= 1 the
+// iterate's moved by the finite-difference step along parameter (cp - 1) mod
+// NPAR (+h; -h for backward differences and for central's second half).
+// One workgroup: a few KB per copy.
+struct ParamCopies {
+    const mh_body* b0; const mh_actuator* a0; const mh_muscle* m0; const mh_spring* s0;
+    mh_body* b; mh_actuator* a; mh_muscle* m; mh_spring* s;
+    int nb, na, nm, ns, ncopy, npar;
+};
+__global__ void __launch_bounds__(256) k_apply_params(ParamCopies P, const mh_parameter_target* __restrict__ tg,
+        int nt, const double* __restrict__ xp, double h, int fd) {
+#pragma clang fp contract(off)
+    const int tid = threadIdx.x, nthr = blockDim.x;
+    auto copy = [&](const void* src, void* dst, size_t bytes) {
+        const long words = (long)(bytes / 8);
+        const unsigned long long* s = (const unsigned long long*)src;
+        unsigned long long* d = (unsigned long long*)dst;
+        for (long w = tid; w < words * P.ncopy; w += nthr) d[w] = s[w % words];
+    };
+    copy(P.b0, P.b, sizeof(mh_body) * (size_t)P.nb);
+    copy(P.a0, P.a, sizeof(mh_actuator) * (size_t)P.na);
+    copy(P.m0, P.m, sizeof(mh_muscle) * (size_t)P.nm);
+    copy(P.s0, P.s, sizeof(mh_spring) * (size_t)P.ns);
+    __syncthreads();
+    for (int k = tid; k < nt * P.ncopy; k += nthr) {
+        const int t = k / P.ncopy, cp = k - t * P.ncopy;
+        const mh_parameter_target T = tg[t];
+        double v = xp[T.parameter];
+        if (cp >= 1 && (cp - 1) % P.npar == T.parameter) {
+            const bool minus = fd == MH_FD_BACKWARD || (fd == MH_FD_CENTRAL && cp > P.npar);
+            v = minus ? v - h : v + h;
+        }
+        switch (T.kind) {
+        case MH_PARAM_BODY_MASS: P.b[(size_t)cp * P.nb + T.index].mass = v; break;
+        case MH_PARAM_BODY_MASS_CENTER: P.b[(size_t)cp * P.nb + T.index].com[T.element] = v; break;
+        case MH_PARAM_BODY_INERTIA: P.b[(size_t)cp * P.nb + T.index].inertia[T.element] = v; break;
+        case MH_PARAM_SPRING_STIFFNESS: P.s[(size_t)cp * P.ns + T.index].stiffness = v; break;
+        case MH_PARAM_SPRING_REST_LENGTH: P.s[(size_t)cp * P.ns + T.index].rest_length = v; break;
+        case MH_PARAM_SPRING_VISCOSITY: P.s[(size_t)cp * P.ns + T.index].viscosity = v; break;
+        case MH_PARAM_ACTUATOR_OPTIMAL_FORCE: P.a[(size_t)cp * P.na + T.index].optimal_force = v; break;
+        case MH_PARAM_MUSCLE_MAX_ISOMETRIC_FORCE: P.m[(size_t)cp * P.nm + T.index].max_isometric_force = v; break;
+        default: break;
+        }
+    }
+}
+// Writes the model copies for iterate x (device pointer) on the context stream.
+static void apply_params(mh_ctx* c, const double* x) {
+    if (c->NPAR <= 0) return;
+    const DevModel& B = c->M0;
+    const DevModel& Q = c->Mp[0];
+    ParamCopies P{B.bodies, B.acts, B.mus, B.sp, (mh_body*)Q.bodies, (mh_actuator*)Q.acts, (mh_muscle*)Q.mus,
+                  (mh_spring*)Q.sp, B.nb, B.nact, B.nmus, B.nsp, c->NCOPY, c->NPAR};
+    hipLaunchKernelGGL(k_apply_params, dim3(1), dim3(256), 0, c->stream, P, c->d_par_targets,
+            (int)c->par_targets.size(), x + c->XP, c->h, c->fd);
+}
+
 // Transcription stage of the split path, one launch: blockIdx.y = mesh
 // interval; blockIdx.x < nchunks streams Jacobian nonzeros (values != null),
 // the last x-block (when g != null) writes the interval's defect /
@@ -709,6 +768,7 @@ static int64_t col_input(const mh_ctx* c, int64_t k, int j) {
 // x column of endpoint input si: [initial_time, initial point inputs,
 // final_time, final point inputs] (EndpointEqs, CasOCFunction.h:167-240).
 static int64_t ep_col(const mh_ctx* c, int si) {
+    if (si >= 2 * (1 + c->NI)) return c->XP + (si - 2 * (1 + c->NI));   // parameter
     const int W = 1 + c->NI, pt = si / W, j = si % W - 1;
     if (j < 0) return pt;
     const int64_t k = pt ? c->G - 1 : 0;
@@ -725,26 +785,36 @@ static int64_t ep_col(const mh_ctx* c, int si) {
 static void build_template(mh_ctx* c) {
     const int NS = c->NS, NQ = c->TQ, NC = c->NC, NDV = c->NDV;   // NQ: coordinates among the states
     const bool implicit = c->NACC > 0;
-    struct Col { int pt; int dir; };  // dir: 0/1 time, 2+input
+    struct Col { int pt; int dir; };  // dir: 0/1 time, 2+input, 2+NI+p parameter p
+    const int pdir = 2 + c->NI;       // direction of parameter 0
     auto key = [&](const Col& col) -> int64_t {
         // column index for interval 0
         if (col.dir < 2) return col.dir;
+        if (col.dir >= pdir) return c->XP + (col.dir - pdir);
         return col_input(c, col.pt, col.dir - 2);
     };
-    // time columns carry pt_time (the residual rows' grid point; 0 otherwise)
+    // time and parameter columns carry pt_time (the residual rows' grid
+    // point; 0 otherwise) and the row's general (t0 / tf) kind: like a time
+    // column, a parameter column reads the callbacks of every point of the row
     auto emit_row = [&](int row, uint8_t kind_t, uint8_t kind_x, int s, std::vector<Col> cols,
             int pt_time = 0) {
         std::sort(cols.begin(), cols.end(), [&](const Col& a, const Col& b) { return key(a) < key(b); });
         for (const auto& col : cols) {
             TplEntry e{};
+            const bool gen = col.dir < 2 || col.dir >= pdir;
             e.row = (int16_t)row;
-            e.kind = col.dir < 2 ? kind_t : kind_x;
-            e.pt = (uint8_t)(col.dir < 2 ? pt_time : col.pt);
+            e.kind = gen ? kind_t : kind_x;
+            e.pt = (uint8_t)(gen ? pt_time : col.pt);
             e.dir = (int16_t)col.dir;
             e.s = (int16_t)s;
             c->tpl.push_back(e);
-            c->tpl_col_pt.push_back(col.dir < 2 ? -1 : col.pt);
+            c->tpl_col_pt.push_back(gen ? -1 : col.pt);
         }
+    };
+    // the parameters are inputs of every callback (ContinuousInput.parameters,
+    // CasOCProblem.h:132-165): dense columns of each row that reads one
+    auto param_dep = [&](std::vector<Col>& v) {
+        for (int q = 0; q < c->NPAR; ++q) v.push_back({0, pdir + q});
     };
     // Inputs of point pt that callback output o reads: all of them without
     // sparsity detection (block-dense, CasOCFunction.cpp:25-105 "none"),
@@ -766,6 +836,7 @@ static void build_template(mh_ctx* c) {
             std::vector<Col> v;
             if (time_dep(c->sp, o)) { v.push_back({pt, 0}); v.push_back({pt, 1}); }
             point_dep(c->sp, o, pt, -1, v);
+            param_dep(v);
             emit_row(row++, T_RES, T_RES, o, v, pt);
         }
     };
@@ -776,6 +847,7 @@ static void build_template(mh_ctx* c) {
             std::vector<Col> v;
             if (time_dep(c->sp_pc, e)) { v.push_back({pt, 0}); v.push_back({pt, 1}); }
             point_dep(c->sp_pc, e, pt, -1, v);
+            param_dep(v);
             emit_row(row++, T_PATH, T_PATH, e, v, pt);
         }
     };
@@ -786,6 +858,7 @@ static void build_template(mh_ctx* c) {
         for (int r = 0; r < c->NK; ++r) {
             std::vector<Col> v{{pt, 0}, {pt, 1}};
             point_dep({}, 0, pt, -1, v);
+            param_dep(v);
             emit_row(row++, T_RES, T_RES, c->OKC + r, v, pt);
         }
     };
@@ -812,6 +885,7 @@ static void build_template(mh_ctx* c) {
                 // prescribed: zdot after the NQ residuals)
                 v.push_back({1, 2 + s});
                 point_dep(c->sp, s + c->SO, 0, s, v); point_dep(c->sp, s + c->SO, 2, s, v);
+                param_dep(v);
             }
             emit_row(row++, T_HERM_T, T_HERM_X, s, v);
         }
@@ -825,6 +899,7 @@ static void build_template(mh_ctx* c) {
                 v.push_back({0, 2 + NQ + s}); v.push_back({2, 2 + NQ + s});
                 for (int j = 0; j < 2 * NQ; ++j) v.push_back({1, 2 + j});
                 for (int l = 0; l < c->NSL; ++l) v.push_back({1, 2 + NPD + l});
+                param_dep(v);
             } else if (s < NQ) {
                 v.push_back({0, 2 + s}); v.push_back({2, 2 + s});
                 v.push_back({0, 2 + NQ + s}); v.push_back({1, 2 + NQ + s}); v.push_back({2, 2 + NQ + s});
@@ -834,6 +909,7 @@ static void build_template(mh_ctx* c) {
             } else {
                 point_dep(c->sp, s + c->SO, 0, s, v); point_dep(c->sp, s + c->SO, 1, -1, v);
                 point_dep(c->sp, s + c->SO, 2, s, v);
+                param_dep(v);
             }
             emit_row(row++, T_SIMP_T, T_SIMP_X, s, v);
         }
@@ -857,6 +933,7 @@ static void build_template(mh_ctx* c) {
                 v.push_back({0, adir + s - NQ}); v.push_back({1, adir + s - NQ});
             } else {
                 point_dep(c->sp, s + c->SO, 0, s, v); point_dep(c->sp, s + c->SO, 1, s, v);
+                param_dep(v);
             }
             emit_row(row++, T_TRAP_T, T_TRAP_X, s, v);
         }
@@ -883,6 +960,7 @@ static void build_template(mh_ctx* c) {
         std::vector<std::pair<int64_t, int>> cols;
         for (int si = 0; si < WE; ++si)
             if (c->sp_ep.empty() || c->sp_ep[(size_t)e * WE + si]) cols.push_back({ep_col(c, si), si});
+        for (int q = 0; q < c->NPAR; ++q) cols.push_back({ep_col(c, WE + q), WE + q});   // the parameters
         std::sort(cols.begin(), cols.end());
         for (const auto& cs : cols) {
             TplEntry t{};
@@ -913,7 +991,8 @@ static bool path_entries_lead(const mh_ctx* c) {
 // its coefficient and base -- the operations jac_entry performs for it.
 static bool compile_template(mh_ctx* c) {
     const int NS = c->NS, NQ = c->TQ, NC = c->NC, NO = c->NO;
-    const int stride = c->fd == MH_FD_CENTRAL ? 2 * (c->NI + 2) + 1 : (c->NI + 2) + 1;
+    const int ND = c->NI + 2 + c->NPAR;   // directions: t0, tf, point inputs, parameters
+    const int stride = c->fd == MH_FD_CENTRAL ? 2 * ND + 1 : ND + 1;
     const int npts = c->scheme == MH_HERMITE_SIMPSON ? 3 : 2;
     const uint32_t kconst = (uint32_t)(npts * NO * stride + CT_CONST);   // sK relative to sY
     if ((size_t)kconst + CT_NCONST > CT_OFF) return false;
@@ -1303,6 +1382,43 @@ static int validate_and_layout(mh_ctx* c, const mh_problem* p, const mh_options*
         if (E.body < 0 || E.body >= M.nbodies || E.table < 0 || E.table >= M.ntables)
             return set_err(MH_ERR_INVALID, "external force %d: bad body/table", e);
     }
+    // SpringGeneralizedForce elements (ABI v8)
+    if (M.nsprings < 0 || (M.nsprings > 0 && !M.springs)) return set_err(MH_ERR_INVALID, "bad springs");
+    for (int i = 0; i < M.nsprings; ++i)
+        if (M.springs[i].coord < 0 || M.springs[i].coord >= M.nq)
+            return set_err(MH_ERR_INVALID, "spring %d: bad coordinate", i);
+    c->nsprings = M.nsprings;
+    // MocoParameters (ABI v8): bounds per parameter, the properties each writes
+    if (p->nparameters < 0 || p->nparameter_targets < 0 || (p->nparameters > 0 && !p->parameter_bounds) ||
+            (p->nparameter_targets > 0 && !p->parameter_targets))
+        return set_err(MH_ERR_INVALID, "bad parameters");
+    c->NPAR = p->nparameters;
+    c->par_bounds.assign(p->parameter_bounds, p->parameter_bounds + c->NPAR);
+    c->par_targets.assign(p->parameter_targets, p->parameter_targets + p->nparameter_targets);
+    std::vector<int> written(c->NPAR, 0);
+    for (int t = 0; t < p->nparameter_targets; ++t) {
+        const mh_parameter_target& T = c->par_targets[t];
+        if (T.parameter < 0 || T.parameter >= c->NPAR)
+            return set_err(MH_ERR_INVALID, "parameter target %d: bad parameter %d", t, T.parameter);
+        int count = 0, elems = 1;
+        switch (T.kind) {
+        case MH_PARAM_BODY_MASS: count = M.nbodies; break;
+        case MH_PARAM_BODY_MASS_CENTER: count = M.nbodies; elems = 3; break;
+        case MH_PARAM_BODY_INERTIA: count = M.nbodies; elems = 6; break;
+        case MH_PARAM_SPRING_STIFFNESS: case MH_PARAM_SPRING_REST_LENGTH: case MH_PARAM_SPRING_VISCOSITY:
+            count = M.nsprings; break;
+        case MH_PARAM_ACTUATOR_OPTIMAL_FORCE: count = M.nactuators; break;
+        case MH_PARAM_MUSCLE_MAX_ISOMETRIC_FORCE: count = M.nmuscles; break;
+        default: return set_err(MH_ERR_UNSUPPORTED, "parameter target %d: kind %d", t, T.kind);
+        }
+        if (T.index < 0 || T.index >= count || T.element < 0 || T.element >= elems)
+            return set_err(MH_ERR_INVALID, "parameter target %d: bad index / element", t);
+        if (T.kind == MH_PARAM_ACTUATOR_OPTIMAL_FORCE && M.actuators[T.index].kind != MH_ACT_COORDINATE)
+            return set_err(MH_ERR_INVALID, "parameter target %d: optimal_force of a non-coordinate actuator", t);
+        written[T.parameter] = 1;
+    }
+    for (int q = 0; q < c->NPAR; ++q)
+        if (!written[q]) return set_err(MH_ERR_INVALID, "parameter %d writes no model property", q);
     // transcription
     c->scheme = o->transcription;
     c->N = o->num_mesh_intervals;
@@ -1330,6 +1446,8 @@ static int validate_and_layout(mh_ctx* c, const mh_problem* p, const mh_options*
         }
     }
     c->n = 2 + (int64_t)(c->NS + c->NC + c->NDV + c->NM) * c->G + (int64_t)c->NSL * c->N;
+    c->XP = c->n;   // the parameters: the last block of x (CasOCIterate.h:27-44)
+    c->n += c->NPAR;
     build_template(c);
     // (kinematic rows precede the path rows: such contexts never run
     // k_interval, whose path loop needs the path entries first)
@@ -1434,6 +1552,8 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
         return set_err(MH_ERR_HIP, "no HIP device available (the hot path has no CPU fallback)");
     if (o->device < 0 || o->device >= ndev) return set_err(MH_ERR_HIP, "device %d out of range", o->device);
     c->device = o->device;
+    if (c->NPAR > 0 && o->sparsity_detection != MH_SPARSITY_NONE)
+        return set_err(MH_ERR_UNSUPPORTED, "MocoParameters with sparsity detection");
     c->be = select_backend(c.get(), p);
     HIPCHK(hipSetDevice(c->device));
     hipDeviceProp_t prop;
@@ -1494,7 +1614,18 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
                  o_pc = A.put(c->pc.data(), c->pc.size()),
                  o_ep = A.put(c->ep.data(), c->ep.size()),
                  o_eptpl = A.put(c->eptpl.data(), c->eptpl.size()),
-                 o_kcs = A.put(c->kcs.data(), c->kcs.size());
+                 o_kcs = A.put(c->kcs.data(), c->kcs.size()),
+                 o_sp = A.put(M.springs, M.nsprings);
+    // MocoParameters: NCOPY copies of the parameterized arrays (ParamCopies)
+    c->NCOPY = c->NPAR > 0 ? 1 + c->NPAR * (o->finite_difference_scheme == MH_FD_CENTRAL ? 2 : 1) : 1;
+    size_t o_cb2 = 0, o_ca2 = 0, o_cm2 = 0, o_cs2 = 0, o_ptg = 0;
+    if (c->NPAR > 0) {
+        o_cb2 = A.reserve(sizeof(mh_body) * (size_t)c->NCOPY * std::max(1, M.nbodies));
+        o_ca2 = A.reserve(sizeof(mh_actuator) * (size_t)c->NCOPY * std::max(1, M.nactuators));
+        o_cm2 = A.reserve(sizeof(mh_muscle) * (size_t)c->NCOPY * std::max(1, M.nmuscles));
+        o_cs2 = A.reserve(sizeof(mh_spring) * (size_t)c->NCOPY * std::max(1, M.nsprings));
+        o_ptg = A.put(c->par_targets.data(), c->par_targets.size());
+    }
     // a generated back end's constant pool for this model
     std::vector<double> pool;
     if (c->gen) {
@@ -1511,7 +1642,7 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     const size_t o_rl_w = A.put(c->rl_w.data(), c->rl_w.size());
 
     const int nint = c->ie - c->ib;
-    const int ND = c->NI + 2;
+    const int ND = c->NI + 2 + c->NPAR;   // t0, tf, the point inputs, the parameters
     const size_t o_x = A.reserve(sizeof(double) * c->n);
     const size_t o_times = A.reserve(sizeof(double) * c->nk);
     const int stride = c->fd == MH_FD_CENTRAL ? 2 * ND + 1 : ND + 1;
@@ -1542,6 +1673,21 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
         if (exc_lane[r] < 0) lane_map.push_back(r);
     const size_t o_exc = c->n_exc_lanes ? A.put(exc_lane.data(), exc_lane.size()) : 0;
     const size_t o_lmap = c->n_exc_lanes ? A.put(lane_map.data(), lane_map.size()) : 0;
+    // parameter lanes: the lane of model copy cp (1 + p: +h, or -h for
+    // backward differences; central: 1 + NPAR + p at -h), evaluated by a
+    // launch of their own over that copy; the other lanes by the main launch
+    size_t o_lmain = 0, o_plan = 0;
+    if (c->NPAR > 0) {
+        const int pd = 2 + c->NI;
+        std::vector<int> plan, lmain;
+        for (int cp = 1; cp < c->NCOPY; ++cp)
+            plan.push_back(cp <= c->NPAR ? pd + (cp - 1) : ND + pd + (cp - 1 - c->NPAR));
+        for (int r = 0; r < stride; ++r)
+            if (exc_lane[r] < 0 && std::find(plan.begin(), plan.end(), r) == plan.end()) lmain.push_back(r);
+        c->n_lane_main = (int)lmain.size();
+        o_lmain = A.put(lmain.data(), lmain.size());
+        o_plan = A.put(plan.data(), plan.size());
+    }
     const size_t o_Y = A.reserve(sizeof(double) * (size_t)c->nk * std::max(1, c->NO) * stride);
     const size_t o_Yg = A.reserve(sizeof(double) * (size_t)c->nk * std::max(1, c->NO));
     const size_t o_g = A.reserve(sizeof(double) * ((size_t)c->nep + (size_t)nint * c->rpi + c->ntail));
@@ -1679,6 +1825,25 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
     D.mus_pw_begin = (const int*)(b + o_pwb);
     D.mus_pw_count = (const int*)(b + o_pwc);
     D.pool = c->gen ? (const double*)(b + o_pool) : nullptr;
+    D.nsp = M.nsprings;
+    D.sp = (const mh_spring*)(b + o_sp);
+    c->M0 = D;   // the pristine model (mh_eval_dae)
+    if (c->NPAR > 0) {
+        // the copies: every DevModel reads its own parameterized arrays;
+        // copy 0 (the iterate's values) is the context's model
+        c->Mp.assign(c->NCOPY, D);
+        for (int cp = 0; cp < c->NCOPY; ++cp) {
+            DevModel& Q = c->Mp[cp];
+            Q.bodies = (const mh_body*)(b + o_cb2) + (size_t)cp * M.nbodies;
+            Q.acts = (const mh_actuator*)(b + o_ca2) + (size_t)cp * M.nactuators;
+            Q.mus = (const mh_muscle*)(b + o_cm2) + (size_t)cp * M.nmuscles;
+            Q.sp = (const mh_spring*)(b + o_cs2) + (size_t)cp * M.nsprings;
+        }
+        D = c->Mp[0];
+        c->d_par_targets = (mh_parameter_target*)(b + o_ptg);
+        c->d_lane_main = (int*)(b + o_lmain);
+        c->d_par_lanes = (int*)(b + o_plan);
+    }
     c->GS.ngoals = c->ngoals;
     c->GS.ndv = c->NDV;
     c->GS.nc = c->NC;
@@ -1937,6 +2102,8 @@ extern "C" int mh_get_bounds(const mh_ctx* c, double* xl, double* xu, double* gl
         for (int k = 0; k < c->G; ++k) { xl[col_mult(c, k, j)] = c->mult_lo; xu[col_mult(c, k, j)] = c->mult_hi; }
     for (int l = 0; l < c->NSL; ++l)
         for (int i = 0; i < c->N; ++i) { xl[col_slack(c, i, l)] = c->vc_lo; xu[col_slack(c, i, l)] = c->vc_hi; }
+    // parameters: the MocoParameter's bounds (CasOCTranscription.cpp:243-248)
+    for (int q = 0; q < c->NPAR; ++q) put_bounds(c->par_bounds[q], xl[c->XP + q], xu[c->XP + q]);
     if (gl && gu) {
         for (int64_t r = 0; r < c->m; ++r) { gl[r] = 0.0; gu[r] = 0.0; }
         // kinematic rows: kinematic_constraint_bounds (CasOCTranscription.cpp:303-309)
@@ -2002,6 +2169,7 @@ extern "C" int mh_get_jac_structure(const mh_ctx* c, int32_t* iRow, int32_t* jCo
             iRow[e] = (int32_t)(c->nep + (int64_t)i * c->rpi + T.row);
             int64_t col;
             if (T.dir < 2) col = T.dir;
+            else if (T.dir >= 2 + c->NI) col = c->XP + (T.dir - 2 - c->NI);   // parameter
             else col = col_input(c, (int64_t)i * step + T.pt, T.dir - 2);
             jCol[e] = (int32_t)col;
             ++e;
@@ -2041,6 +2209,7 @@ static int launch_stage(mh_ctx* c, int stage, int kind, const double* x, double*
     // grid point) and the split transcription (MOCOHIP_G_LANE=1)
     const bool glane = kind == 0 && c->g_lane && c->be_lane;
     if (stage == 0) {
+        apply_params(c, x);   // MocoParameters: the model copies for this iterate
         (glane ? c->be_lane : c->be)->eval(c, x, kind == 0 ? 0 : 1, kind == 0 ? c->d_Yg : c->d_Y);
         HIPCHK(hipGetLastError());
         return MH_OK;
@@ -2983,6 +3152,7 @@ extern "C" int mh_debug_jacobian_lanes(mh_ctx* c, const double* x, double* times
     HIPCHK(hipSetDevice(c->device));
     (void)hipGetLastError();
     HIPCHK(hipMemcpyAsync(c->d_x, x, sizeof(double) * c->n, hipMemcpyHostToDevice, c->stream));
+    apply_params(c, c->d_x);
     c->be->lanes(c, c->d_x, c->d_Y);
     HIPCHK(hipGetLastError());
     const size_t ny = (size_t)c->nk * c->NO * c->lanes_jac.stride;
@@ -3097,6 +3267,17 @@ extern "C" int mh_get_backend(const mh_ctx* c, char* name, int32_t name_len, dou
     return MH_OK;
 }
 
+extern "C" int mh_get_nlp_info_for(const mh_problem* p, const mh_options* o, mh_nlp_info* info) {
+    if (!p || !o || !info) return set_err(MH_ERR_INVALID, "null argument");
+    std::unique_ptr<mh_ctx> c(new mh_ctx());
+    std::vector<int> coord_body, act_state, ftn_state, mus_control;
+    double tau_act, tau_deact;
+    int rc = validate_and_layout(c.get(), p, o, coord_body, act_state, ftn_state, mus_control, tau_act,
+            tau_deact);
+    if (rc) return rc;
+    return mh_get_nlp_info(c.get(), info);
+}
+
 extern "C" int mh_backend_for(const mh_problem* p, const mh_options* o, char* name, int32_t name_len) {
     if (!p || !o || !name || name_len <= 0) return set_err(MH_ERR_INVALID, "bad argument");
     std::unique_ptr<mh_ctx> c(new mh_ctx());
@@ -3178,7 +3359,10 @@ static const Backend* select_backend(mh_ctx* c, const mh_problem* p) {
     // for (match: topology, joint / path / wrap / constraint wiring, zero
     // pattern); its numbers come from the model's constant pool (fill, in
     // mh_create)
-    if (!generic) {
+    // MocoParameters write model properties a generated back end folds into
+    // its constant pool, and SpringGeneralizedForce is not in the generated
+    // code: both run on the generic interpreter
+    if (!generic && c->NPAR == 0 && c->nsprings == 0) {
         for (auto entry : kGeneratedModels) {
             const GenEntry& e = entry();
             if (e.implicit != (c->NMB > 0) || e.prescribed != (c->presc != 0)) continue;

@@ -105,6 +105,20 @@ class mh_path_wrap(C.Structure):
     _fields_ = [("muscle", i32), ("wrap", i32), ("range_begin", i32), ("range_end", i32)]
 
 
+class mh_spring(C.Structure):
+    _fields_ = [("coord", i32), ("reserved", i32), ("stiffness", f64), ("rest_length", f64),
+                ("viscosity", f64)]
+
+
+MH_PARAM_BODY_MASS, MH_PARAM_BODY_MASS_CENTER, MH_PARAM_BODY_INERTIA, MH_PARAM_SPRING_STIFFNESS, \
+    MH_PARAM_SPRING_REST_LENGTH, MH_PARAM_SPRING_VISCOSITY, MH_PARAM_ACTUATOR_OPTIMAL_FORCE, \
+    MH_PARAM_MUSCLE_MAX_ISOMETRIC_FORCE = range(8)
+
+
+class mh_parameter_target(C.Structure):
+    _fields_ = [("parameter", i32), ("kind", i32), ("index", i32), ("element", i32)]
+
+
 class mh_model(C.Structure):
     _fields_ = [("nq", i32), ("nbodies", i32), ("naxes", i32),
                 ("nfunctions", i32), ("nknots", i32), ("nmuscles", i32),
@@ -120,7 +134,8 @@ class mh_model(C.Structure):
                 ("external", P(mh_external_force)),
                 ("nconstraints", i32), ("reserved_kc", i32), ("constraints", P(mh_constraint)),
                 ("nwraps", i32), ("npathwraps", i32), ("wraps", P(mh_wrap_object)),
-                ("pathwraps", P(mh_path_wrap))]
+                ("pathwraps", P(mh_path_wrap)),
+                ("nsprings", i32), ("reserved_sp", i32), ("springs", P(mh_spring))]
 
 
 class mh_bounds(C.Structure):
@@ -165,7 +180,9 @@ class mh_problem(C.Structure):
                 ("prescribed_kinematics", i32), ("kinematics_table", i32),
                 ("kinematics_column", P(i32)),
                 ("nendpoint", i32), ("reserved2", i32), ("endpoint", P(mh_endpoint_equation)),
-                ("multiplier_bounds", mh_bounds), ("kinematic_constraint_bounds", mh_bounds)]
+                ("multiplier_bounds", mh_bounds), ("kinematic_constraint_bounds", mh_bounds),
+                ("nparameters", i32), ("nparameter_targets", i32),
+                ("parameter_bounds", P(mh_bounds)), ("parameter_targets", P(mh_parameter_target))]
 
 
 class mh_options(C.Structure):
@@ -206,6 +223,7 @@ MOCOHIP_SYMBOLS = {
     "mh_backend_for": (i32, [P(mh_problem), P(mh_options), C.c_char_p, i32]),
     "mh_last_error": (C.c_char_p, []),
     "mh_create": (i32, [P(mh_problem), P(mh_options), P(C.c_void_p)]),
+    "mh_get_nlp_info_for": (i32, [P(mh_problem), P(mh_options), P(mh_nlp_info)]),
     "mh_destroy": (None, [C.c_void_p]),
     "mh_get_nlp_info": (i32, [C.c_void_p, P(mh_nlp_info)]),
     "mh_get_bounds": (i32, [C.c_void_p, P(f64), P(f64), P(f64), P(f64)]),

@@ -22,7 +22,7 @@ from typing import Optional
 import numpy as np
 
 from .model import (Body, Coordinate, CoordinateActuator, DataTable,
-                    ExternalForce, Joint, Marker, Model, model_from_dict)
+                    ExternalForce, Joint, Marker, Model, SpringGeneralizedForce, model_from_dict)
 from . import abi
 from .osim import add_reserves
 from .problem import (Constant, GCVSpline, ImplicitAuxiliaryDerivativesTerm,
@@ -48,6 +48,82 @@ def sliding_mass(num_mesh_intervals: int = 50, dynamics: str = "explicit") -> Mo
     p.add_goal(MocoFinalTimeGoal())
     s = MocoHipSolver(num_mesh_intervals=num_mesh_intervals, multibody_dynamics_mode=dynamics)
     return MocoStudy(p, s)
+
+
+# testMocoParameters.cpp:34-37: the oscillator's true mass and stiffness
+OSCILLATOR_STIFFNESS = 100.0
+OSCILLATOR_MASS = 5.0
+OSCILLATOR_FINAL_TIME = math.pi * math.sqrt(OSCILLATOR_MASS / OSCILLATOR_STIFFNESS)
+
+
+def _oscillator(body_mass: float, springs) -> Model:
+    """createOscillatorModel / createOscillatorTwoSpringsModel
+    (testMocoParameters.cpp:38-58,103-133): a body on a SliderJoint
+    ("slider", coordinate "position"), no gravity, SpringGeneralizedForce(s)
+    on the coordinate, rest length 0, no viscosity; a marker at the body's
+    origin stands for the test's FinalPositionGoal (below)."""
+    m = Model("oscillator", gravity=(0, 0, 0))
+    m.add_body(Body("body", body_mass, (0, 0, 0), (0, 0, 0, 0, 0, 0)))
+    pos = Coordinate("position", (-math.inf, math.inf), "translational", path="/slider/position")
+    m.add_joint(Joint.slider("slider", "ground", "body", pos))
+    for name, k in springs:
+        m.add_spring(SpringGeneralizedForce(name, "position", stiffness=k, rest_length=0.0, viscosity=0.0))
+    m.add_marker(Marker("body_origin", "body", (0.0, 0.0, 0.0)))
+    return m
+
+
+def _oscillator_study(m: Model, num_mesh_intervals: int) -> MocoStudy:
+    """The test's problem (testMocoParameters.cpp:81-94,141-156): time in [0,
+    pi sqrt(MASS / STIFFNESS)], position starting at -0.5 and ending in [0.25,
+    0.75], speed 0 at both ends, and FinalPositionGoal -- (final position -
+    0.5)^2 (:60-72), here MocoMarkerFinalGoal of the body origin against (0.5,
+    0, 0): the same cost, since the origin is at (q, 0, 0)."""
+    p = MocoProblem(m)
+    p.set_time_bounds(0, OSCILLATOR_FINAL_TIME)
+    p.set_state_info("/slider/position/value", (-5.0, 5.0), -0.5, (0.25, 0.75))
+    p.set_state_info("/slider/position/speed", (-20, 20), 0, 0)
+    p.add_goal(MocoMarkerFinalGoal(name="final_position", point_name="/markerset/body_origin",
+                                   reference_location=(0.5, 0.0, 0.0)))
+    return MocoStudy(p, MocoHipSolver(num_mesh_intervals=num_mesh_intervals))
+
+
+def oscillator_mass(num_mesh_intervals: int = 25) -> MocoStudy:
+    """testMocoParameters.cpp:78-99 ("Oscillator mass"): the body starts at
+    half the true mass; MocoParameter "oscillator_mass" writes the body's
+    mass, bounds [0, 10]; the solve must recover MASS within 0.3 %."""
+    st = _oscillator_study(_oscillator(0.5 * OSCILLATOR_MASS, [("spring", OSCILLATOR_STIFFNESS)]),
+                           num_mesh_intervals)
+    st.problem.add_parameter("oscillator_mass", "body", "mass", (0, 10))
+    return st
+
+
+def oscillator_two_springs(num_mesh_intervals: int = 25) -> MocoStudy:
+    """testMocoParameters.cpp:135-166 ("One parameter two springs"): two
+    springs of a quarter of the stiffness each, ONE MocoParameter
+    "spring_stiffness" writing both (bounds [0, 100]); the solve must find
+    half the stiffness within 0.3 %."""
+    st = _oscillator_study(_oscillator(OSCILLATOR_MASS, [("spring1", 0.25 * OSCILLATOR_STIFFNESS),
+                                                         ("spring2", 0.25 * OSCILLATOR_STIFFNESS)]),
+                           num_mesh_intervals)
+    st.problem.add_parameter("spring_stiffness", ["spring1", "spring2"], "stiffness", (0, 100))
+    return st
+
+
+def gait10dof18musc_parameters(num_mesh_intervals: int = 6, **kw) -> MocoStudy:
+    """gait10dof18musc with MocoParameters over every property kind a
+    muscle-driven gait model offers (MocoParameter.h:91-170; test case, no
+    reference counterpart on this model): one parameter on both femurs'
+    mass, both soleus' max_isometric_force, the torso's mass-center y (a
+    vector-property element), a reserve actuator's optimal_force."""
+    st = gait10dof18musc(num_mesh_intervals, **kw)
+    p = st.problem
+    p.add_parameter("femur_mass", ["/bodyset/femur_r", "/bodyset/femur_l"], "mass", (5.0, 12.0))
+    p.add_parameter("soleus_fmax", ["/forceset/soleus_r", "/forceset/soleus_l"], "max_isometric_force",
+                    (2000.0, 5000.0))
+    p.add_parameter("torso_com_y", "/bodyset/torso", "mass_center", (0.25, 0.45), property_element=1)
+    p.add_parameter("pelvis_tilt_reserve", "/forceset/reserve_jointset_ground_pelvis_pelvis_tilt",
+                    "optimal_force", (1.0, 50.0))
+    return st
 
 
 def sliding_mass_interface(num_mesh_intervals: int = 19, scheme: str = "trapezoidal",

@@ -117,6 +117,9 @@ def describe(study) -> str:
                                  _d(a.min_control), _d(a.max_control), _s(a.path)]))
         else:
             raise TypeError(f"unsupported actuator {type(a).__name__}")
+    for f in m.springs:
+        out.append(" ".join(["spring", _s(f.name), _s(f.coordinate), _d(f.stiffness), _d(f.rest_length),
+                             _d(f.viscosity), _s(f.path)]))
     for mk in m.markers.values():
         out.append(f"marker {_s(mk.name)} {_s(mk.body)} {_ds(mk.location)} {_s(mk.path)}")
     for k in m.constraints:
@@ -165,6 +168,10 @@ def describe(study) -> str:
                             + [_s(c) for c in pc.control_paths]
                             + [_bound_fn(pc.lower_bound), _bound_fn(pc.upper_bound),
                                str(int(bool(pc.equality_with_lower)))]))
+    for par in p.parameters:
+        out.append(" ".join(["parameter", _s(par.name), _s(par.property_name), str(int(par.property_element)),
+                             _bounds(par.bounds), str(len(par.component_paths))]
+                            + [_s(c) for c in par.component_paths]))
     if p.position_motion is not None:
         kin = p.position_motion
         qpaths = [c.path + "/value" for c in m.coordinates()]

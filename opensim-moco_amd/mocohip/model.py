@@ -254,6 +254,20 @@ class CoordinateActuator:
 
 
 @dataclass
+class SpringGeneralizedForce:
+    """OpenSim SpringGeneralizedForce (opensim-core, third-party): the
+    generalized force -stiffness (q - rest_length) - viscosity u on one
+    coordinate (include/mocohip.h mh_spring; testMocoParameters.cpp:52-57);
+    path /forceset/<name>."""
+    name: str
+    coordinate: str
+    stiffness: float = 0.0
+    rest_length: float = 0.0
+    viscosity: float = 0.0
+    path: str = ""
+
+
+@dataclass
 class Marker:
     """OpenSim::Marker: a point fixed on a body (``location`` in the body
     frame); path /markerset/<name>."""
@@ -310,6 +324,7 @@ class Model:
         self.markers: Dict[str, Marker] = {}    # by path
         self.constraints: List[CoordinateCouplerConstraint] = []   # enabled ones
         self.wraps: Dict[str, WrapCylinder] = {}
+        self.springs: List[SpringGeneralizedForce] = []
 
     # building ---------------------------------------------------------------
     def add_body(self, body: Body):
@@ -335,6 +350,12 @@ class Model:
             a.path = f"/forceset/{a.name}"
         self.actuators.append(a)
         return a
+
+    def add_spring(self, f: SpringGeneralizedForce):
+        if not f.path:
+            f.path = f"/forceset/{f.name}"
+        self.springs.append(f)
+        return f
 
     def add_table(self, t: DataTable):
         self.tables[t.name] = t
@@ -636,6 +657,13 @@ class CompiledModel:
         self._kx = np.ascontiguousarray(knot_x + [0.0], float)
         self._ky = np.ascontiguousarray(knot_y + [0.0], float)
         self._kcs = _arr(abi.mh_constraint, kcs)
+        springs = []
+        for f in model.springs:
+            ss = abi.mh_spring()
+            ss.coord = qidx[f.coordinate]
+            ss.stiffness, ss.rest_length, ss.viscosity = float(f.stiffness), float(f.rest_length), float(f.viscosity)
+            springs.append(ss)
+        self._springs = _arr(abi.mh_spring, springs)
 
         mm = abi.mh_model()
         mm.nq = len(qidx)
@@ -669,6 +697,8 @@ class CompiledModel:
         mm.npathwraps = len(pathwraps)
         mm.wraps = self._wraps
         mm.pathwraps = self._pathwraps
+        mm.nsprings = len(springs)
+        mm.springs = self._springs
         self.struct = mm
         self.nq = mm.nq
         self.state_names = model.state_names()
@@ -730,6 +760,9 @@ def model_to_dict(m: Model) -> dict:
                    "active": w.active} for w in m.wraps.values()],
         "constraints": [{"name": k.name, "dependent": k.dependent, "function": _fn_to(k.function),
                          "scale_factor": k.scale_factor} for k in m.constraints],
+        "springs": [{"name": f.name, "coordinate": f.coordinate, "stiffness": f.stiffness,
+                     "rest_length": f.rest_length, "viscosity": f.viscosity, "path": f.path}
+                    for f in m.springs],
     }
 
 
@@ -765,4 +798,7 @@ def model_from_dict(d: dict) -> Model:
     for k in d.get("constraints", []):
         m.add_constraint(CoordinateCouplerConstraint(k["name"], k["dependent"],
                                                      _fn_from(k["function"]), k["scale_factor"]))
+    for f in d.get("springs", []):
+        m.add_spring(SpringGeneralizedForce(f["name"], f["coordinate"], f["stiffness"], f["rest_length"],
+                                            f["viscosity"], f.get("path", "")))
     return m

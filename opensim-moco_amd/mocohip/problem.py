@@ -16,7 +16,7 @@ import numpy as np
 
 from . import abi
 from .model import CompiledModel, CoordinateActuator, DataTable, \
-    DeGrooteFregly2016Muscle, Model
+    DeGrooteFregly2016Muscle, Model, SpringGeneralizedForce
 from .splines import gcv_interpolating_ppoly
 
 NAN = float("nan")
@@ -182,6 +182,25 @@ class ImplicitAuxiliaryDerivativesTerm:
     weight: float = 1.0
 
 
+@dataclass
+class MocoParameter:
+    """MocoParameter (Moco/Moco/MocoParameter.h:91-170): an NLP variable
+    written into the property ``property_name`` of every component in
+    ``component_paths`` before each evaluation; ``property_element`` picks
+    the element of a vector property (mass_center: 0-2, inertia: 0-5 = xx yy
+    zz xy xz yz), -1 for a scalar one.  Components are named by name or path
+    (a Body, SpringGeneralizedForce, CoordinateActuator or DGF muscle);
+    supported properties: Body mass / mass_center / inertia,
+    SpringGeneralizedForce stiffness / rest_length / viscosity,
+    CoordinateActuator optimal_force, muscle max_isometric_force
+    (include/mocohip.h mh_parameter_kind)."""
+    name: str
+    component_paths: Sequence[str]
+    property_name: str
+    bounds: MocoBounds = field(default_factory=MocoBounds)
+    property_element: int = -1
+
+
 class MocoProblem:
     """Single-phase MocoProblem (MocoProblem.h)."""
 
@@ -200,6 +219,7 @@ class MocoProblem:
         # (MocoProblem.cpp:42-43)
         self.kinematic_constraint_bounds = MocoBounds(0.0, 0.0)
         self.multiplier_bounds = MocoBounds(-1000.0, 1000.0)
+        self.parameters: List[MocoParameter] = []
 
     def set_model(self, model: Model):
         self.model = model
@@ -221,6 +241,15 @@ class MocoProblem:
     def set_control_info(self, name, bounds=None, initial=None, final=None):
         self.control_infos[name] = MocoVariableInfo(
             MocoBounds.of(bounds), MocoBounds.of(initial), MocoBounds.of(final))
+
+    def add_parameter(self, name: str, component_paths, property_name: str, bounds=None,
+                      property_element: int = -1) -> MocoParameter:
+        """MocoProblem::addParameter (MocoProblem.h: the MocoParameter
+        constructors, MocoParameter.h:100-112)."""
+        paths = [component_paths] if isinstance(component_paths, str) else list(component_paths)
+        par = MocoParameter(name, paths, property_name, MocoBounds.of(bounds), int(property_element))
+        self.parameters.append(par)
+        return par
 
     def add_goal(self, goal):
         self.goals.append(goal)
@@ -434,6 +463,15 @@ class ProblemRep:
         p.multiplier_bounds.upper = problem.multiplier_bounds.upper
         p.kinematic_constraint_bounds.lower = problem.kinematic_constraint_bounds.lower
         p.kinematic_constraint_bounds.upper = problem.kinematic_constraint_bounds.upper
+        # MocoParameters: bounds per parameter, one target per written property
+        targets, pbounds = self._parameter_targets(problem, self.compiled)
+        self.parameter_names = [par.name for par in problem.parameters]
+        self._pbounds = (abi.mh_bounds * max(1, len(pbounds)))(*pbounds)
+        self._ptargets = (abi.mh_parameter_target * max(1, len(targets)))(*targets)
+        p.nparameters = len(pbounds)
+        p.nparameter_targets = len(targets)
+        p.parameter_bounds = self._pbounds
+        p.parameter_targets = self._ptargets
         self.num_kinematic_constraints = len(model.constraints)
         self.num_endpoint_equations = len(endpoint)
         self.num_path_equations = len(path_eqs)
@@ -466,6 +504,71 @@ class ProblemRep:
             m.path + "/implicitderiv_normalized_tendon_force" for m in model.muscles
             if not m.ignore_tendon_compliance and m.tendon_compliance_dynamics_mode == "implicit"]
         self.accel_names_all = [n[:-len("speed")] + "accel" for n in self.state_names if n.endswith("/speed")]
+
+    @staticmethod
+    def _parameter_targets(problem: MocoProblem, compiled: CompiledModel):
+        """MocoParameter::initializeOnModel (MocoParameter.cpp): each
+        component path must name a component with the property; vector
+        properties need an element in range, scalar ones none."""
+        model = problem.model
+        scalar = {"mass": abi.MH_PARAM_BODY_MASS, "stiffness": abi.MH_PARAM_SPRING_STIFFNESS,
+                  "rest_length": abi.MH_PARAM_SPRING_REST_LENGTH, "viscosity": abi.MH_PARAM_SPRING_VISCOSITY,
+                  "optimal_force": abi.MH_PARAM_ACTUATOR_OPTIMAL_FORCE,
+                  "max_isometric_force": abi.MH_PARAM_MUSCLE_MAX_ISOMETRIC_FORCE}
+        vector = {"mass_center": (abi.MH_PARAM_BODY_MASS_CENTER, 3), "inertia": (abi.MH_PARAM_BODY_INERTIA, 6)}
+
+        def find(path):
+            key = path.rstrip("/").split("/")[-1]
+            for b in model.bodies.values():
+                if path in (b.name, "/bodyset/" + b.name, "/" + b.name):
+                    return "body", compiled.body_index[b.name]
+            for i, f in enumerate(model.springs):
+                if path in (f.name, f.path) or key == f.name:
+                    return "spring", i
+            for i, a in enumerate(model.actuators):
+                if path in (a.name, a.path):
+                    return ("muscle", model.muscles.index(a)) if isinstance(a, DeGrooteFregly2016Muscle) \
+                        else ("actuator", i)
+            raise ValueError(f"MocoParameter: no component '{path}' in the model")
+        owner = {abi.MH_PARAM_BODY_MASS: "body", abi.MH_PARAM_BODY_MASS_CENTER: "body",
+                 abi.MH_PARAM_BODY_INERTIA: "body", abi.MH_PARAM_SPRING_STIFFNESS: "spring",
+                 abi.MH_PARAM_SPRING_REST_LENGTH: "spring", abi.MH_PARAM_SPRING_VISCOSITY: "spring",
+                 abi.MH_PARAM_ACTUATOR_OPTIMAL_FORCE: "actuator",
+                 abi.MH_PARAM_MUSCLE_MAX_ISOMETRIC_FORCE: "muscle"}
+        targets, bounds = [], []
+        names = set()
+        for ip, par in enumerate(problem.parameters):
+            if par.name in names:
+                raise ValueError(f"MocoParameter '{par.name}': duplicate name")
+            names.add(par.name)
+            if not par.component_paths:
+                raise ValueError(f"MocoParameter '{par.name}': no component paths")
+            if par.property_name in vector:
+                kind, nel = vector[par.property_name]
+                if not 0 <= par.property_element < nel:
+                    raise ValueError(f"MocoParameter '{par.name}': property '{par.property_name}' needs an "
+                                     f"element in [0, {nel})")
+                elem = par.property_element
+            elif par.property_name in scalar:
+                if par.property_element >= 0:
+                    raise ValueError(f"MocoParameter '{par.name}': a property element was given for the "
+                                     f"scalar property '{par.property_name}'")
+                kind, elem = scalar[par.property_name], 0
+            else:
+                raise NotImplementedError(f"MocoParameter '{par.name}': property '{par.property_name}' is "
+                                          "not a parameterizable property of this build")
+            for path in par.component_paths:
+                what, idx = find(path)
+                if what != owner[kind]:
+                    raise ValueError(f"MocoParameter '{par.name}': component '{path}' ({what}) has no "
+                                     f"property '{par.property_name}'")
+                t = abi.mh_parameter_target()
+                t.parameter, t.kind, t.index, t.element = ip, kind, idx, elem
+                targets.append(t)
+            b = abi.mh_bounds()
+            b.lower, b.upper = par.bounds.lower, par.bounds.upper
+            bounds.append(b)
+        return targets, bounds
 
     @staticmethod
     def _path_equations(problem: MocoProblem):

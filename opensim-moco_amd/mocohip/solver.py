@@ -189,8 +189,9 @@ class MocoHipSolver:
         if self.sparsity_guess is not None:
             if self.optim_sparsity_detection != "initial-guess":
                 raise ValueError("sparsity_guess needs optim_sparsity_detection='initial-guess'")
-            self._guess = np.ascontiguousarray(self.sparsity_guess, float)
+            self._guess = np.ascontiguousarray(self.sparsity_guess, float).reshape(-1)
             o.sparsity_guess = abi.dptr(self._guess)
+            o._guess_size = self._guess.size   # checked against n by check_guess_size
         if (self.sparsity_pattern is not None) != (self.optim_sparsity_detection == "given"):
             raise ValueError("optim_sparsity_detection='given' goes with sparsity_pattern")
         if self.sparsity_pattern is not None:
@@ -346,6 +347,11 @@ class _NLPBase:
         return self.NS + self.NC + self.NDV + self.NM + self.NSL
 
     @property
+    def NPAR(self) -> int:
+        """MocoParameters: the last NPAR variables of x."""
+        return int(self.rep.struct.nparameters)
+
+    @property
     def NO(self) -> int:
         """DAE callback outputs: udot or multibody residual, zdot, auxiliary
         residuals, kinematic errors, velocity correction (with slacks)."""
@@ -481,12 +487,28 @@ class HipBatch:
             pass
 
 
+def check_guess_size(rep: ProblemRep, opts: abi.mh_options, lib=None) -> None:
+    """mh_create reads n doubles from mh_options.sparsity_guess: refuse a
+    guess of another size before it does (n from mh_get_nlp_info_for, the
+    host-only layout query)."""
+    size = getattr(opts, "_guess_size", None)
+    if not opts.sparsity_guess or size is None:
+        return
+    lib = lib or abi.load_mocohip()
+    info = abi.mh_nlp_info()
+    if lib.mh_get_nlp_info_for(C.byref(rep.struct), C.byref(opts), C.byref(info)) != 0:
+        raise ValueError(lib.mh_last_error().decode())
+    if size != int(info.n):
+        raise ValueError(f"sparsity_guess has {size} values, the problem has n = {int(info.n)}")
+
+
 class HipNLP(_NLPBase):
     """NLP backed by libmocohip.so (the product path)."""
     prefix = "mh_"
 
     def __init__(self, rep: ProblemRep, opts: abi.mh_options, lib=None):
         self.lib = lib or abi.load_mocohip()
+        check_guess_size(rep, opts, self.lib)
         super().__init__(rep, opts)
 
     def device_kkt(self, warm: bool = False):
@@ -583,7 +605,7 @@ class HipNLP(_NLPBase):
 
     def lane_stride(self) -> int:
         """Finite-difference lanes per grid point (mh_debug_jacobian_lanes)."""
-        ND = 2 + self.NI
+        ND = 2 + self.NI + self.NPAR   # t0, tf, the point inputs, the parameters
         return 2 * ND + 1 if self.opts.finite_difference_scheme == abi.MH_FD_CENTRAL else ND + 1
 
     def jacobian_lanes(self, x):

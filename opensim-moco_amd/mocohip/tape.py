@@ -17,8 +17,13 @@ Layout (little endian, x86-64 struct layout of include/mocohip.h):
   kinematic-constraint bounds; version 5 (ABI v5) appends the wrap surfaces
   and PathWraps (mh_model.nwraps/wraps, npathwraps/pathwraps); version 6
   carries ABI v6's mh_options (+ sparsity_rule); version 7 ABI v7's (the
-  rule's values swapped: the reference's any-change rule is 0).  Readers
-  accept versions 4 to 7 (a version-6 tape's rule is mapped to v7's value)."""
+  rule's values swapped: the reference's any-change rule is 0); version 8
+  ABI v8's (coloring_order) and appends the springs (mh_model.nsprings /
+  springs) and the MocoParameters (nparameters + bounds, nparameter_targets
+  + targets); from version 8 the initial-guess blob is the whole iterate (n
+  doubles, what mh_create reads; mh_driver checks it against
+  mh_get_nlp_info_for).  Readers accept versions 4 to 8 (a version-6 tape's
+  rule is mapped to v7's value)."""
 from __future__ import annotations
 
 import ctypes as C
@@ -27,8 +32,9 @@ import struct
 from . import abi
 
 MAGIC = b"MHTAPE01"
-VERSION = 7   # 2: + path constraints; 3: + endpoint constraints; 4: + kinematic constraints; 5: + wraps;
-#               6: ABI v6 mh_options; 7: ABI v7 (sparsity_rule values swapped)
+VERSION = 8   # 2: + path constraints; 3: + endpoint constraints; 4: + kinematic constraints; 5: + wraps;
+#               6: ABI v6 mh_options; 7: ABI v7 (sparsity_rule values swapped); 8: ABI v8 (springs,
+#               parameters, the guess blob = n doubles)
 
 # (field, element type, count attribute of mh_model / None for problem arrays)
 _MODEL_ARRAYS = [
@@ -61,9 +67,15 @@ def write_tape(rep, opts: abi.mh_options, path: str) -> None:
     nar = getattr(rep, "num_aux_residuals", 0)
     ndv = (m.nq if implicit and not presc else 0) + nar
     if opts.sparsity_guess:
-        G = (2 * opts.num_mesh_intervals + 1 if opts.transcription == abi.MH_HERMITE_SIMPSON
-             else opts.num_mesh_intervals + 1)
-        guess = C.string_at(opts.sparsity_guess, 8 * (2 + (ns + nc + ndv) * G))
+        # the whole iterate: n doubles (mh_options.sparsity_guess)
+        info = abi.mh_nlp_info()
+        lib = abi.load_mocohip()
+        if lib.mh_get_nlp_info_for(C.byref(p), C.byref(opts), C.byref(info)) != 0:
+            raise RuntimeError(lib.mh_last_error().decode())
+        size = getattr(opts, "_guess_size", None)
+        if size is not None and size != int(info.n):
+            raise ValueError(f"sparsity_guess has {size} values, the problem has n = {int(info.n)}")
+        guess = C.string_at(opts.sparsity_guess, 8 * int(info.n))
     pattern = b""
     if opts.sparsity_pattern:
         # mh_get_callback_sparsity layout: NO DAE outputs and the path
@@ -104,5 +116,11 @@ def write_tape(rep, opts: abi.mh_options, path: str) -> None:
     pw = _blob(m.pathwraps, abi.mh_path_wrap, m.npathwraps)
     out += [struct.pack("<i", m.nwraps), struct.pack("<q", len(wb)), wb,
             struct.pack("<i", m.npathwraps), struct.pack("<q", len(pw)), pw]
+    sb = _blob(m.springs, abi.mh_spring, m.nsprings)
+    pbnd = _blob(p.parameter_bounds, abi.mh_bounds, p.nparameters)
+    ptg = _blob(p.parameter_targets, abi.mh_parameter_target, p.nparameter_targets)
+    out += [struct.pack("<i", m.nsprings), struct.pack("<q", len(sb)), sb,
+            struct.pack("<i", p.nparameters), struct.pack("<q", len(pbnd)), pbnd,
+            struct.pack("<i", p.nparameter_targets), struct.pack("<q", len(ptg)), ptg]
     with open(path, "wb") as fh:
         fh.write(b"".join(out))

@@ -96,6 +96,10 @@ class MocoTrajectory:
     def get_state(self, name: str) -> np.ndarray:
         return self.states[:, self.state_names.index(name)]
 
+    def get_parameter(self, name: str) -> float:
+        """MocoTrajectory::getParameter."""
+        return float(self.parameters[self.parameter_names.index(name)])
+
     def get_control(self, name: str) -> np.ndarray:
         return self.controls[:, self.control_names.index(name)]
 
@@ -275,7 +279,13 @@ class MocoTrajectory:
         Mu = by_name(mn, list(self.multiplier_names), r.multipliers)
         Lg = by_name(sn, list(self.slack_names), r.slacks)
         L = Lg[1::2][:N] if nsl else np.zeros((N, 0))   # the slacks at the mesh-interval midpoints
-        return np.concatenate([[t0, tf], S.ravel(), Cm.ravel(), Mu.ravel(), L.ravel(), D.ravel()])
+        # parameters by name (the guess's value; missing: the bounds midpoint)
+        pn = list(getattr(rep, "parameter_names", []))
+        P = nlp.initial_guess_from_bounds()[nlp.n - len(pn):] if pn else np.zeros(0)
+        for q, n in enumerate(pn):
+            if n in self.parameter_names:
+                P[q] = self.parameters[self.parameter_names.index(n)]
+        return np.concatenate([[t0, tf], S.ravel(), Cm.ravel(), Mu.ravel(), L.ravel(), D.ravel(), P])
 
     @staticmethod
     def from_iterate(nlp, x: np.ndarray) -> "MocoTrajectory":
@@ -287,7 +297,8 @@ class MocoTrajectory:
         nm, nsl = getattr(nlp, "NM", 0), getattr(nlp, "NSL", 0)
         N = nlp.opts.num_mesh_intervals
         x = np.asarray(x, float)
-        if len(x) != 2 + (ns + nc + nm + ndv) * G + nsl * N:
+        pn = list(getattr(rep, "parameter_names", []))
+        if len(x) != 2 + (ns + nc + nm + ndv) * G + nsl * N + len(pn):
             raise ValueError("iterate size does not match the problem and grid")
         t0, tf = x[0], x[1]
         o = 2
@@ -302,8 +313,9 @@ class MocoTrajectory:
         if nsl:
             Lg[1::2] = L
         dn, mn, sn = variable_names(nlp)
+        P = x[len(x) - len(pn):] if pn else np.zeros(0)
         return MocoTrajectory((tf - t0) * grid + t0, list(rep.state_names), list(rep.control_names),
-                              mn, dn, sn, [], S, Cm, Mu, D, Lg)
+                              mn, dn, sn, pn, S, Cm, Mu, D, Lg, P.copy())
 
     # -------------------------------------------------------------- comparison
     def compare_continuous_variables_rms(self, other: "MocoTrajectory", states=None, controls=None,

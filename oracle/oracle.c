@@ -299,6 +299,17 @@ struct orc_ctx {
     mh_path_wrap* pw;
     int *mus_pw_begin, *mus_pw_count;
     int maxcp;
+    /* SpringGeneralizedForce elements (ABI v8) */
+    int NSPR;
+    mh_spring* spr;
+    /* MocoParameters (ABI v8): NPAR variables at x[XP..] (the last block,
+     * CasOCIterate.h:27-44), bounds, the properties they write
+     * (applyParametersToModelProperties, MocoCasOCProblem.h:309,508-515) */
+    int NPAR, NPT;
+    int64_t XP;
+    mh_bounds* par_bounds;
+    mh_parameter_target* par_targets;
+    int owns_model;   /* 0 for the parameter copies (param_ctx): arrays shared but the parameterized ones */
 };
 
 static double* dup_d(const double* p, size_t n) {
@@ -315,6 +326,48 @@ void orc_set_threads(orc_ctx* c, int nthreads) { c->nthreads = nthreads < 1 ? 1 
 /* Jacobian structure (block-dense CasOC rule).         */
 /* Columns of x: [t0, tf, states(NS x G grid-major), controls(NC x G)].      */
 /* ------------------------------------------------------------------------ */
+/* MocoParameters applied (applyParametersToModelProperties,
+ * MocoCasOCProblem.h:309,508-515): a shallow copy of the context whose
+ * parameterized arrays (bodies, actuators, muscles, springs) are its own,
+ * every target property set to its parameter's value in x -- parameter
+ * `moved` (>= 0) moved by `step` (the finite-difference lanes along a
+ * parameter).  Without parameters: the context itself. */
+static orc_ctx* param_ctx(const orc_ctx* c, const double* x, int moved, double step) {
+    if (c->NPAR <= 0) return (orc_ctx*)c;
+    const mh_model* M = &c->P.model;
+    orc_ctx* q = (orc_ctx*)malloc(sizeof(orc_ctx));
+    *q = *c;
+    q->owns_model = 0;
+    q->bodies = DUP(mh_body, c->bodies, M->nbodies);
+    q->acts = DUP(mh_actuator, c->acts, M->nactuators);
+    q->mus = DUP(mh_muscle, c->mus, M->nmuscles);
+    q->spr = DUP(mh_spring, c->spr, c->NSPR);
+    for (int t = 0; t < c->NPT; ++t) {
+        const mh_parameter_target* T = &c->par_targets[t];
+        double v = x[c->XP + T->parameter];
+        if (T->parameter == moved) v = v + step;
+        switch (T->kind) {
+        case MH_PARAM_BODY_MASS: q->bodies[T->index].mass = v; break;
+        case MH_PARAM_BODY_MASS_CENTER: q->bodies[T->index].com[T->element] = v; break;
+        case MH_PARAM_BODY_INERTIA: q->bodies[T->index].inertia[T->element] = v; break;
+        case MH_PARAM_SPRING_STIFFNESS: q->spr[T->index].stiffness = v; break;
+        case MH_PARAM_SPRING_REST_LENGTH: q->spr[T->index].rest_length = v; break;
+        case MH_PARAM_SPRING_VISCOSITY: q->spr[T->index].viscosity = v; break;
+        case MH_PARAM_ACTUATOR_OPTIMAL_FORCE: q->acts[T->index].optimal_force = v; break;
+        case MH_PARAM_MUSCLE_MAX_ISOMETRIC_FORCE: q->mus[T->index].max_isometric_force = v; break;
+        default: break;
+        }
+    }
+    return q;
+}
+static void param_ctx_free(const orc_ctx* c, orc_ctx* q) {
+    if (q == c || !q) return;
+    free(q->bodies); free(q->acts); free(q->mus); free(q->spr);
+    free(q);
+}
+/* finite-difference directions: t0, tf, the NP point inputs, the parameters */
+static int ndir(const orc_ctx* c) { return c->NP + 2 + c->NPAR; }
+
 static int64_t col_state(const orc_ctx* c, int k, int s) { return 2 + (int64_t)k * c->NS + s; }
 static int64_t col_control(const orc_ctx* c, int k, int j) {
     return 2 + (int64_t)c->NS * c->G + (int64_t)k * c->NC + j;
@@ -384,6 +437,13 @@ static int point_cols_dep(const orc_ctx* c, const uint8_t* sp, int o, int k, int
 /* Emits the sorted column set of every row of interval i, in row order.
  * emit(row_local, cols, ncols). Returns rows per interval. */
 typedef void (*row_fn)(void* ud, int64_t row, const int64_t* cols, int ncols);
+/* The parameters are inputs of every callback (ContinuousInput.parameters,
+ * CasOCProblem.h:132-165): a row that reads a callback output gets the NPAR
+ * parameter columns, the last of x, after its sorted columns. */
+static int add_param_cols(const orc_ctx* c, int64_t* cols, int n) {
+    for (int q = 0; q < c->NPAR; ++q) cols[n++] = c->XP + q;
+    return n;
+}
 /* Multibody residual rows of grid point k (implicit mode): the callback
  * output depends on every input of the point and on the time. */
 static int64_t residual_rows(const orc_ctx* c, int k, int64_t row, row_fn emit, void* ud,
@@ -393,6 +453,7 @@ static int64_t residual_rows(const orc_ctx* c, int k, int64_t row, row_fn emit, 
         if (dep(c->sp, c->NP, o, -1)) { cols[n++] = 0; cols[n++] = 1; }
         n += point_cols_dep(c, c->sp, o, k, -1, cols + n);
         qsort(cols, (size_t)n, sizeof(int64_t), cmp64);   /* multipliers precede derivatives in x */
+        n = add_param_cols(c, cols, n);
         emit(ud, row++, cols, n);
     }
     return row;
@@ -408,6 +469,7 @@ static int64_t path_rows(const orc_ctx* c, int k, int64_t row, row_fn emit, void
         if (dep(c->sp_pc, c->NP, e, -1)) { cols[n++] = 0; cols[n++] = 1; }
         n += point_cols_dep(c, c->sp_pc, e, k, -1, cols + n);
         qsort(cols, (size_t)n, sizeof(int64_t), cmp64);
+        n = add_param_cols(c, cols, n);
         emit(ud, row++, cols, n);
     }
     return row;
@@ -423,6 +485,7 @@ static int64_t kc_rows(const orc_ctx* c, int k, int64_t row, row_fn emit, void* 
         cols[n++] = 0; cols[n++] = 1;
         n += point_cols_dep(c, NULL, 0, k, -1, cols + n);
         qsort(cols, (size_t)n, sizeof(int64_t), cmp64);
+        n = add_param_cols(c, cols, n);
         emit(ud, row++, cols, n);
     }
     return row;
@@ -434,7 +497,7 @@ static int speed_row_sparse(const orc_ctx* c, int s) { return c->NACC && s >= c-
 
 static void interval_rows(const orc_ctx* c, int i, int64_t row0, row_fn emit, void* ud) {
     int NQ = c->TQ, NS = c->NS, NC = c->NC;   /* NQ: coordinates among the states */
-    int64_t* cols = (int64_t*)malloc(sizeof(int64_t) * (size_t)(3 * c->NP + 8));
+    int64_t* cols = (int64_t*)malloc(sizeof(int64_t) * (size_t)(3 * c->NP + 8 + c->NPAR));
     int64_t row = row0;
     if (c->scheme == MH_HERMITE_SIMPSON) {
         int ki = 2 * i, km = 2 * i + 1, kp = 2 * i + 2;
@@ -458,13 +521,17 @@ static void interval_rows(const orc_ctx* c, int i, int64_t row0, row_fn emit, vo
                         cols[n++] = col_state(c, ki, NQ + s); cols[n++] = col_state(c, kp, NQ + s);
                     } else if (c->NSL) {
                         /* qdot at the midpoint = u + G^T gamma: the velocity
-                         * correction function reads the midpoint's q, u and
-                         * the interval's slacks (block-dense,
+                         * correction function reads the midpoint's q, u, the
+                         * interval's slacks and the parameters (block-dense,
                          * CasOCTranscription.cpp:316-333) */
                         cols[n++] = col_state(c, ki, s); cols[n++] = col_state(c, kp, s);
                         cols[n++] = col_state(c, ki, NQ + s); cols[n++] = col_state(c, kp, NQ + s);
                         for (int j = 0; j < 2 * NQ; ++j) cols[n++] = col_state(c, km, j);
                         for (int l = 0; l < c->NSL; ++l) cols[n++] = col_slack(c, i, l);
+                        qsort(cols, (size_t)n, sizeof(int64_t), cmp64);
+                        n = add_param_cols(c, cols, n);
+                        emit(ud, row++, cols, n);
+                        continue;
                     } else {
                         cols[n++] = col_state(c, ki, s); cols[n++] = col_state(c, kp, s);
                         cols[n++] = col_state(c, ki, NQ + s); cols[n++] = col_state(c, km, NQ + s);
@@ -494,6 +561,10 @@ static void interval_rows(const orc_ctx* c, int i, int64_t row0, row_fn emit, vo
                         n += point_cols_dep(c, c->sp, o, km, -1, cols + n);
                         n += point_cols_dep(c, c->sp, o, kp, s, cols + n);
                     }
+                    qsort(cols, (size_t)n, sizeof(int64_t), cmp64);
+                    n = add_param_cols(c, cols, n);
+                    emit(ud, row++, cols, n);
+                    continue;
                 }
                 qsort(cols, (size_t)n, sizeof(int64_t), cmp64);
                 emit(ud, row++, cols, n);
@@ -523,6 +594,10 @@ static void interval_rows(const orc_ctx* c, int i, int64_t row0, row_fn emit, vo
             } else {
                 n += point_cols_dep(c, c->sp, s + c->SO, ki, s, cols + n);
                 n += point_cols_dep(c, c->sp, s + c->SO, kp, s, cols + n);
+                qsort(cols, (size_t)n, sizeof(int64_t), cmp64);
+                n = add_param_cols(c, cols, n);
+                emit(ud, row++, cols, n);
+                continue;
             }
             qsort(cols, (size_t)n, sizeof(int64_t), cmp64);
             emit(ud, row++, cols, n);
@@ -554,7 +629,7 @@ static int rows_per_interval(const orc_ctx* c) {
  * (CasOCTranscription.h:286-308) */
 static int ntail(const orc_ctx* c) { return c->NK + c->NPC + nres(c); }
 static void tail_rows(const orc_ctx* c, int64_t row0, row_fn emit, void* ud) {
-    int64_t* cols = (int64_t*)malloc(sizeof(int64_t) * (size_t)(c->NP + 4));
+    int64_t* cols = (int64_t*)malloc(sizeof(int64_t) * (size_t)(c->NP + 4 + c->NPAR));
     row0 = kc_rows(c, c->G - 1, row0, emit, ud, cols);
     row0 = path_rows(c, c->G - 1, row0, emit, ud, cols);
     residual_rows(c, c->G - 1, row0, emit, ud, cols);
@@ -569,7 +644,10 @@ static void tail_rows(const orc_ctx* c, int64_t row0, row_fn emit, void* ud) {
  * no integrand, CasOCTranscription.cpp:562-564).  Subset index si of that
  * vector -> NLP column. */
 static int ep_width(const orc_ctx* c) { return 2 * (1 + c->NP); }
+/* ... and then the parameters (inputs 2 W + q; the Endpoint callback's
+ * `parameters` input, CasOCTranscription.cpp:574-580) */
 static int64_t ep_col(const orc_ctx* c, int si) {
+    if (si >= ep_width(c)) return c->XP + (si - ep_width(c));
     int W = 1 + c->NP;
     int pt = si / W, j = si % W - 1;
     if (j < 0) return pt;                 /* initial_time: 0, final_time: 1 */
@@ -585,6 +663,7 @@ static int ep_row_cols(const orc_ctx* c, int e, int64_t* cols, int* si) {
     int WE = ep_width(c), n = 0;
     for (int i = 0; i < WE; ++i)
         if (!c->sp_ep || c->sp_ep[(int64_t)e * WE + i]) { cols[n] = ep_col(c, i); si[n] = i; ++n; }
+    for (int q = 0; q < c->NPAR; ++q) { cols[n] = ep_col(c, WE + q); si[n] = WE + q; ++n; }
     /* insertion sort by column (the initial point's block and the final
      * point's interleave per variable kind) */
     for (int a = 1; a < n; ++a) {
@@ -595,8 +674,8 @@ static int ep_row_cols(const orc_ctx* c, int e, int64_t* cols, int* si) {
     return n;
 }
 static void endpoint_rows(const orc_ctx* c, row_fn emit, void* ud) {
-    int64_t* cols = (int64_t*)malloc(sizeof(int64_t) * (size_t)(ep_width(c) + 1));
-    int* si = (int*)malloc(sizeof(int) * (size_t)(ep_width(c) + 1));
+    int64_t* cols = (int64_t*)malloc(sizeof(int64_t) * (size_t)(ep_width(c) + 1 + c->NPAR));
+    int* si = (int*)malloc(sizeof(int) * (size_t)(ep_width(c) + 1 + c->NPAR));
     for (int e = 0; e < c->NEP; ++e) emit(ud, e, cols, ep_row_cols(c, e, cols, si));
     free(cols); free(si);
 }
@@ -605,6 +684,7 @@ static void ep_gather(const orc_ctx* c, const double* x, double* in) {
     int W = 1 + c->NP;
     for (int pt = 0; pt < 2; ++pt)
         for (int i = 0; i < W; ++i) in[pt * W + i] = x[ep_col(c, pt * W + i)];
+    for (int q = 0; q < c->NPAR; ++q) in[2 * W + q] = x[c->XP + q];   /* the parameters */
 }
 /* MocoInitialActivationGoal::calcGoalImpl in endpoint-constraint mode
  * (MocoInitialActivationGoal.cpp:41-58): initial excitation - initial
@@ -760,6 +840,44 @@ int orc_create(const mh_problem* p, const mh_options* o, orc_ctx** out) {
     c->brk = dup_d(M->table_breaks, (size_t)M->nbreaks);
     c->coef = dup_d(M->table_coefs, (size_t)M->ncoefs);
     c->ext = DUP(mh_external_force, M->external, M->nexternal);
+    /* SpringGeneralizedForce elements and MocoParameters (ABI v8) */
+    c->NSPR = M->nsprings;
+    c->spr = DUP(mh_spring, M->springs, M->nsprings);
+    c->NPAR = p->nparameters;
+    c->NPT = p->nparameter_targets;
+    c->par_bounds = DUP(mh_bounds, p->parameter_bounds, p->nparameters);
+    c->par_targets = DUP(mh_parameter_target, p->parameter_targets, p->nparameter_targets);
+    c->owns_model = 1;
+    if (c->NSPR < 0 || (c->NSPR > 0 && !M->springs) || c->NPAR < 0 || c->NPT < 0 ||
+            (c->NPAR > 0 && !p->parameter_bounds) || (c->NPT > 0 && !p->parameter_targets)) {
+        orc_destroy(c);
+        return fail(MH_ERR_INVALID, "bad springs / parameters");
+    }
+    for (int i = 0; i < c->NSPR; ++i)
+        if (c->spr[i].coord < 0 || c->spr[i].coord >= M->nq) {
+            orc_destroy(c);
+            return fail(MH_ERR_INVALID, "spring %d: bad coordinate", i);
+        }
+    for (int t = 0; t < c->NPT; ++t) {
+        const mh_parameter_target* T = &c->par_targets[t];
+        int count = 0, elems = 1;
+        switch (T->kind) {
+        case MH_PARAM_BODY_MASS: count = M->nbodies; break;
+        case MH_PARAM_BODY_MASS_CENTER: count = M->nbodies; elems = 3; break;
+        case MH_PARAM_BODY_INERTIA: count = M->nbodies; elems = 6; break;
+        case MH_PARAM_SPRING_STIFFNESS: case MH_PARAM_SPRING_REST_LENGTH: case MH_PARAM_SPRING_VISCOSITY:
+            count = M->nsprings; break;
+        case MH_PARAM_ACTUATOR_OPTIMAL_FORCE: count = M->nactuators; break;
+        case MH_PARAM_MUSCLE_MAX_ISOMETRIC_FORCE: count = M->nmuscles; break;
+        default: orc_destroy(c); return fail(MH_ERR_UNSUPPORTED, "parameter target %d: kind %d", t, T->kind);
+        }
+        if (T->parameter < 0 || T->parameter >= c->NPAR || T->index < 0 || T->index >= count ||
+                T->element < 0 || T->element >= elems ||
+                (T->kind == MH_PARAM_ACTUATOR_OPTIMAL_FORCE && M->actuators[T->index].kind != MH_ACT_COORDINATE)) {
+            orc_destroy(c);
+            return fail(MH_ERR_INVALID, "parameter target %d: bad parameter / index / element", t);
+        }
+    }
     c->goals = DUP(mh_goal, p->goals, p->ngoals);
     c->gidx = DUP(int32_t, p->goal_index, p->nterms);
     c->gcol = DUP(int32_t, p->goal_column, p->nterms);
@@ -1095,9 +1213,15 @@ int orc_create(const mh_problem* p, const mh_options* o, orc_ctx** out) {
     }
     free(mesh);
     c->n = 2 + (int64_t)(c->NS + c->NC + c->NDV + c->NM) * c->G + (int64_t)c->NSL * c->N;
+    c->XP = c->n;             /* the parameters: the last block of x */
+    c->n += c->NPAR;
     c->m = c->NEP + (int64_t)rows_per_interval(c) * c->N + ntail(c);
     c->fd = o->finite_difference_scheme;
     c->h = o->fd_step > 0 ? o->fd_step : 1e-8;
+    if (o->sparsity_detection != MH_SPARSITY_NONE && c->NPAR > 0) {
+        orc_destroy(c);
+        return fail(MH_ERR_UNSUPPORTED, "MocoParameters with sparsity detection");
+    }
     if (o->sparsity_detection != MH_SPARSITY_NONE) {
 #ifndef ORACLE_COUNTING
         int rc = detect_sparsity(c, o);
@@ -1171,7 +1295,8 @@ void orc_destroy(orc_ctx* c) {
             c->goals, c->gidx, c->gcol, c->gw, c->pc, c->sp, c->sp_pc, c->mus_ider, c->kin_col,
             c->ep, c->sp_ep, c->kcs, c->seed_color, c->wr, c->pw, c->mus_pw_begin, c->mus_pw_count,
             c->mus_act_state, c->mus_ftn_state,
-            c->mus_control, c->coord_body, c->grid, c->quad, c->iRow, c->jCol};
+            c->mus_control, c->coord_body, c->grid, c->quad, c->iRow, c->jCol,
+            c->spr, c->par_bounds, c->par_targets};
     for (size_t i = 0; i < sizeof ptrs / sizeof ptrs[0]; ++i) free(ptrs[i]);
     free(c);
 }
@@ -1241,6 +1366,8 @@ int orc_get_bounds(const orc_ctx* c, double* xl, double* xu, double* gl, double*
         for (int i = 0; i < c->N; ++i) { xl[col_slack(c, i, l)] = c->vc_lo; xu[col_slack(c, i, l)] = c->vc_hi; }
     /* defects, residuals and interpolating-control rows: equality to 0
      * (CasOCTranscription.cpp:275-278, 440-443) */
+    /* parameters: the MocoParameter's bounds (CasOCTranscription.cpp:243-248) */
+    for (int q = 0; q < c->NPAR; ++q) set_bounds(c->par_bounds[q], &xl[c->XP + q], &xu[c->XP + q]);
     if (gl) for (int64_t r = 0; r < c->m; ++r) { gl[r] = 0.0; gu[r] = 0.0; }
     /* kinematic rows: kinematic_constraint_bounds at every mesh point
      * (CasOCTranscription.cpp:303-309) */
@@ -2115,6 +2242,13 @@ static void eval_dae_full(const orc_ctx* c, dae_ws* w, real time, const real* x,
             w->tau[A->target] += ctrl[ia] * A->optimal_force;
         }
     }
+    /* SpringGeneralizedForce (OpenSim, third-party): the generalized force
+     * -stiffness (q - rest_length) - viscosity u on its coordinate */
+    for (int is = 0; is < c->NSPR; ++is) {
+        const mh_spring* S = &c->spr[is];
+        real f = -S->stiffness * (q[S->coord] - S->rest_length) - S->viscosity * u[S->coord];
+        w->tau[S->coord] += f;
+    }
     /* Kinematic constraint forces from the multipliers, applied like applied
      * forces: -G^T lambda (MocoCasOCProblem.h:643-662) */
     const real* lam = ctrl + c->NC + c->NDV;
@@ -2500,7 +2634,7 @@ static void g_assemble(const orc_ctx* c, const double* x, const double* times, c
     int rpi = rows_per_interval(c);
     /* endpoint rows first */
     if (c->NEP) {
-        double* ein = (double*)malloc(sizeof(double) * (size_t)ep_width(c));
+        double* ein = (double*)malloc(sizeof(double) * (size_t)(ep_width(c) + c->NPAR));
         ep_gather(c, x, ein);
         for (int e = 0; e < c->NEP; ++e) g[e] = endpoint_value(c, e, ein);
         free(ein);
@@ -2559,7 +2693,8 @@ static void g_assemble(const orc_ctx* c, const double* x, const double* times, c
  * nonzeros: the full-layout assembly goes through a scratch vector. */
 static int sharded(const orc_ctx* c) { return c->ib != 0 || c->ie != c->N; }
 
-int orc_eval_g(orc_ctx* c, const double* x, double* g) {
+int orc_eval_g(orc_ctx* c0, const double* x, double* g) {
+    orc_ctx* c = param_ctx(c0, x, -1, 0.0);   /* the iterate's parameters applied */
     int NS = c->NS, NR = nres(c);
     double* times = (double*)malloc(sizeof(double) * (size_t)c->G);
     double* xd = (double*)calloc((size_t)c->G * (size_t)NS + 1, sizeof(double));
@@ -2579,6 +2714,7 @@ int orc_eval_g(orc_ctx* c, const double* x, double* g) {
     free(xd);
     free(res);
     free(kce);
+    param_ctx_free(c0, c);
     return MH_OK;
 }
 
@@ -2589,8 +2725,16 @@ int orc_eval_g(orc_ctx* c, const double* x, double* g) {
  * d(time_k)/d(tf) = grid_k (CasOCTranscription.cpp:126-127,1189). */
 static void fd_blocks(orc_ctx* c, const double* x, const double* times, double* D) {
     int NS = c->NS, NP = c->NP, NO = nout(c);
-    int ND = NP + 2;
+    int ND = ndir(c);
     double h = c->h;
+    /* c: the iterate's parameters applied; along parameter p the callbacks
+     * run over the model with that parameter moved by +h / -h */
+    orc_ctx** pplus = (orc_ctx**)calloc((size_t)c->NPAR + 1, sizeof(orc_ctx*));
+    orc_ctx** pminus = (orc_ctx**)calloc((size_t)c->NPAR + 1, sizeof(orc_ctx*));
+    for (int q = 0; q < c->NPAR; ++q) {
+        if (c->fd != MH_FD_BACKWARD) pplus[q] = param_ctx(c, x, q, h);
+        if (c->fd != MH_FD_FORWARD) pminus[q] = param_ctx(c, x, q, -h);
+    }
 #pragma omp parallel num_threads(c->nthreads)
     {
         dae_ws w;
@@ -2607,10 +2751,21 @@ static void fd_blocks(orc_ctx* c, const double* x, const double* times, double* 
             for (int d = 0; d < ND; ++d) {
                 double seed;
                 int idx = -1;
+                double* Dk = D + ((int64_t)k * ND + d) * NO;
+                if (d >= 2 + NP) {   /* parameter d - 2 - NP */
+                    int q = d - 2 - NP;
+                    if (c->fd != MH_FD_BACKWARD) eval_dae_point(pplus[q], &w, t, in, in + NS, yp);
+                    if (c->fd != MH_FD_FORWARD) eval_dae_point(pminus[q], &w, t, in, in + NS, ym);
+                    for (int o = 0; o < NO; ++o) {
+                        if (c->fd == MH_FD_CENTRAL) Dk[o] = (yp[o] - ym[o]) / (2.0 * h);
+                        else if (c->fd == MH_FD_FORWARD) Dk[o] = (yp[o] - y0[o]) / h;
+                        else Dk[o] = (y0[o] - ym[o]) / h;
+                    }
+                    continue;
+                }
                 if (d == 0) seed = 1.0 - c->grid[k];
                 else if (d == 1) seed = c->grid[k];
                 else { seed = 1.0; idx = d - 2; }
-                double* Dk = D + ((int64_t)k * ND + d) * NO;
                 if (c->fd != MH_FD_BACKWARD) {
                     if (idx < 0) eval_dae_point(c, &w, t + h * seed, in, in + NS, yp);
                     else {
@@ -2640,13 +2795,15 @@ static void fd_blocks(orc_ctx* c, const double* x, const double* times, double* 
         free(yp);
         ws_free(&w);
     }
+    for (int q = 0; q < c->NPAR; ++q) { param_ctx_free(c, pplus[q]); param_ctx_free(c, pminus[q]); }
+    free(pplus); free(pminus);
 }
 
 /* FD blocks of the path-constraint equations at every mesh point:
  * Dp[(i * ND + d) * NPC + e], directions and seeds as in fd_blocks (the
  * path function has its own FiniteDiff, CasOCTranscription.cpp:424-428). */
 static void path_blocks(const orc_ctx* c, const double* x, const double* times, double* Dp) {
-    int NS = c->NS, NP = c->NP, NPC = c->NPC, ND = NP + 2;
+    int NS = c->NS, NP = c->NP, NPC = c->NPC, ND = ndir(c);
     double h = c->h;
     double* in = (double*)malloc(sizeof(double) * (size_t)(NP + 1));
     for (int i = c->ib; i <= c->ie; ++i) {
@@ -2656,6 +2813,10 @@ static void path_blocks(const orc_ctx* c, const double* x, const double* times, 
         for (int d = 0; d < ND; ++d) {
             double seed;
             int idx = -1;
+            if (d >= 2 + NP) {   /* a parameter: the control bound reads no model property */
+                for (int e = 0; e < NPC; ++e) Dp[((int64_t)i * ND + d) * NPC + e] = 0.0;
+                continue;
+            }
             if (d == 0) seed = 1.0 - c->grid[k];
             else if (d == 1) seed = c->grid[k];
             else { seed = 1.0; idx = d - 2; }
@@ -2694,7 +2855,7 @@ static void path_blocks(const orc_ctx* c, const double* x, const double* times, 
 /* Derivative of xdot[s] at grid point k along direction d (0=t0, 1=tf,
  * 2+j = input j).  For s < NQ, qdot = u exactly. */
 static double xdot_deriv(const orc_ctx* c, const double* D, int k, int s, int d) {
-    int NQ = c->TQ, NO = nout(c), ND = c->NP + 2;
+    int NQ = c->TQ, NO = nout(c), ND = ndir(c);
     if (s < NQ) {
         double v = (d == 2 + NQ + s) ? 1.0 : 0.0;
         /* midpoint: + the velocity correction's FD quotient */
@@ -2708,6 +2869,7 @@ static double xdot_deriv(const orc_ctx* c, const double* D, int k, int s, int d)
 /* Map a Jacobian column to (grid point, direction) for an interval row. */
 static int col_to_dir(const orc_ctx* c, int64_t col, int* k) {
     if (col < 2) { *k = -1; return (int)col; }
+    if (col >= c->XP) { *k = -1; return 2 + c->NP + (int)(col - c->XP); }   /* parameter */
     int64_t sblock = (int64_t)c->NS * c->G;
     if (col < 2 + sblock) {
         int64_t r = col - 2;
@@ -2746,8 +2908,9 @@ static int col_to_dir(const orc_ctx* c, int64_t col, int* k) {
 static void jac_assemble(const orc_ctx* c, const double* x, const double* times, const double* xd,
         const double* D, const double* Dp, double* values) {
     int NS = c->NS, NQ = c->NQ;
-    int NO = nout(c), ND = c->NP + 2;
+    int NO = nout(c), ND = ndir(c);
     int NR = nres(c);
+    int PD = 2 + c->NP;   /* direction of parameter 0 */
     int NPC = c->NPC;
     int rpi = rows_per_interval(c);
     int npts_res = c->scheme == MH_HERMITE_SIMPSON ? 2 : 1;
@@ -2756,9 +2919,9 @@ static void jac_assemble(const orc_ctx* c, const double* x, const double* times,
     int64_t e0 = 0;
     if (c->NEP) {
         int WE = ep_width(c);
-        double* ein = (double*)malloc(sizeof(double) * (size_t)WE);
-        int64_t* cols = (int64_t*)malloc(sizeof(int64_t) * (size_t)(WE + 1));
-        int* si = (int*)malloc(sizeof(int) * (size_t)(WE + 1));
+        double* ein = (double*)malloc(sizeof(double) * (size_t)(WE + c->NPAR));
+        int64_t* cols = (int64_t*)malloc(sizeof(int64_t) * (size_t)(WE + 1 + c->NPAR));
+        int* si = (int*)malloc(sizeof(int) * (size_t)(WE + 1 + c->NPAR));
         ep_gather(c, x, ein);
         for (int r = 0; r < c->NEP; ++r) {
             int nc = ep_row_cols(c, r, cols, si);
@@ -2815,7 +2978,9 @@ static void jac_assemble(const orc_ctx* c, const double* x, const double* times,
                 int s = rl;
                 const double* fi = xd + (int64_t)ki * NS;
                 const double* fp = xd + (int64_t)kp * NS;
-                if (dir < 2) {
+                if (dir >= PD) {   /* a parameter moves no time: the callbacks' quotients */
+                    v = 0.0 - (h / 8.0) * (xdot_deriv(c, D, ki, s, dir) - xdot_deriv(c, D, kp, s, dir));
+                } else if (dir < 2) {
                     double dh = dir == 0 ? dh0 : dhf;
                     v = -(dh / 8.0) * (fi[s] - fp[s]) -
                         (h / 8.0) * (xdot_deriv(c, D, ki, s, dir) - xdot_deriv(c, D, kp, s, dir));
@@ -2835,7 +3000,10 @@ static void jac_assemble(const orc_ctx* c, const double* x, const double* times,
                 const double* fi = xd + (int64_t)ki * NS;
                 const double* fm = xd + (int64_t)km * NS;
                 const double* fp = xd + (int64_t)kp * NS;
-                if (dir < 2) {
+                if (dir >= PD) {
+                    v = 0.0 - (h / 6.0) * (xdot_deriv(c, D, kp, s, dir) + 4.0 * xdot_deriv(c, D, km, s, dir) +
+                                           xdot_deriv(c, D, ki, s, dir));
+                } else if (dir < 2) {
                     double dh = dir == 0 ? dh0 : dhf;
                     v = -(dh / 6.0) * (fp[s] + 4.0 * fm[s] + fi[s]) -
                         (h / 6.0) * (xdot_deriv(c, D, kp, s, dir) + 4.0 * xdot_deriv(c, D, km, s, dir) +
@@ -2862,7 +3030,9 @@ static void jac_assemble(const orc_ctx* c, const double* x, const double* times,
             int s = rl;
             const double* fi = xd + (int64_t)ki * NS;
             const double* fp = xd + (int64_t)kp * NS;
-            if (dir < 2) {
+            if (dir >= PD) {
+                v = 0.0 - (0.5 * h) * (xdot_deriv(c, D, kp, s, dir) + xdot_deriv(c, D, ki, s, dir));
+            } else if (dir < 2) {
                 double dh = dir == 0 ? dh0 : dhf;
                 v = -0.5 * dh * (fp[s] + fi[s]) -
                     0.5 * h * (xdot_deriv(c, D, kp, s, dir) + xdot_deriv(c, D, ki, s, dir));
@@ -2905,9 +3075,10 @@ static int jac_global_seeds(orc_ctx* c, const double* x, double* values) {
     return MH_OK;
 }
 
-int orc_eval_jac_g(orc_ctx* c, const double* x, double* values) {
-    if (c->jac_seeds) return jac_global_seeds(c, x, values);
-    int NS = c->NS, NO = nout(c), ND = c->NP + 2, NR = nres(c), NPC = c->NPC;
+int orc_eval_jac_g(orc_ctx* c0, const double* x, double* values) {
+    if (c0->jac_seeds) return jac_global_seeds(c0, x, values);
+    orc_ctx* c = param_ctx(c0, x, -1, 0.0);   /* the iterate's parameters applied */
+    int NS = c->NS, NO = nout(c), ND = ndir(c), NR = nres(c), NPC = c->NPC;
     double* times = (double*)malloc(sizeof(double) * (size_t)c->G);
     double* xd = (double*)calloc((size_t)c->G * (size_t)NS + 1, sizeof(double));
     double* D = (double*)calloc((size_t)c->G * (size_t)ND * (size_t)NO + 1, sizeof(double));
@@ -2932,6 +3103,7 @@ int orc_eval_jac_g(orc_ctx* c, const double* x, double* values) {
     free(xd);
     free(D);
     free(res);
+    param_ctx_free(c0, c);
     return MH_OK;
 }
 
@@ -2941,7 +3113,7 @@ int orc_eval_jac_g(orc_ctx* c, const double* x, double* values) {
  * the device's quotient + assembly arithmetic. */
 int orc_assemble_from_lanes(orc_ctx* c, const double* x, const double* times, const double* Y,
         double* g, double* values) {
-    int NS = c->NS, NO = nout(c), ND = c->NP + 2, NR = nres(c), NPC = c->NPC, TQ = c->TQ;
+    int NS = c->NS, NO = nout(c), ND = ndir(c), NR = nres(c), NPC = c->NPC, TQ = c->TQ;
     int S = c->fd == MH_FD_CENTRAL ? 2 * ND + 1 : ND + 1, base = S - 1;
     double h = c->h;
     double* xd = (double*)malloc(sizeof(double) * (size_t)c->G * (size_t)NS);

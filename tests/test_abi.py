@@ -15,7 +15,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "mocohip.h")
 KKT_HEADER = os.path.join(ROOT, "include", "mocohip_kkt.h")
 
-STRUCTS = ["mh_function", "mh_axis", "mh_body", "mh_path_point", "mh_muscle",
+STRUCTS = ["mh_function", "mh_axis", "mh_body", "mh_path_point", "mh_muscle", "mh_spring",
+           "mh_parameter_target",
            "mh_actuator", "mh_table", "mh_external_force", "mh_constraint", "mh_wrap_object",
            "mh_path_wrap", "mh_model",
            "mh_bounds", "mh_variable_info", "mh_goal", "mh_path_equation", "mh_endpoint_equation",

@@ -66,6 +66,9 @@ STUDIES = {
     "pendulum_bound_spline_eq": lambda: _bounded_pendulum("spline"),
     "pendulum_control_bound_both_implicit": lambda: configs.pendulum_control_bound(6, "both",
                                                                                    dynamics="implicit"),
+    # tape v8: MocoParameters on a body mass / two springs' stiffness
+    "oscillator_mass": lambda: configs.oscillator_mass(6),
+    "oscillator_two_springs": lambda: configs.oscillator_two_springs(6),
 }
 
 
@@ -116,6 +119,15 @@ def test_cpp_builder_reports_the_reference_errors(tmp_path):
     st = configs.double_pendulum(4)
     next(g for g in st.problem.goals if hasattr(g, "control_weights")).exponent = 1
     cases.append((st, "Exponent must be 2 or greater"))
+    st = configs.oscillator_mass(4)
+    st.problem.parameters[0].property_name = "mass_center"
+    cases.append((st, "needs an element in [0, 3)"))
+    st = configs.oscillator_two_springs(4)
+    st.problem.parameters[0].component_paths.append("/forceset/nosuchspring")
+    cases.append((st, "no component '/forceset/nosuchspring'"))
+    st = configs.oscillator_mass(4)
+    st.problem.parameters[0].property_name = "stiffness"
+    cases.append((st, "has no property 'stiffness'"))
     for i, (st, msg) in enumerate(cases):
         desc = tmp_path / f"e{i}.mhdesc"
         write_description(st, str(desc))
@@ -124,7 +136,8 @@ def test_cpp_builder_reports_the_reference_errors(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["gait10dof18musc", "rajagopal18_inverse_wrapped", "pendulum_bound_pwl"])
+@pytest.mark.parametrize("name", ["gait10dof18musc", "rajagopal18_inverse_wrapped", "pendulum_bound_pwl",
+                                  "oscillator_two_springs"])
 def test_cpp_built_tape_drives_the_library_like_python(tmp_path, name):
     """g and the Jacobian values the C ABI computes from the C++-built tape
     (mh_driver) equal the Python binding's on the Python-lowered problem."""

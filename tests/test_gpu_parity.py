@@ -189,6 +189,15 @@ CASES = {
     # the wrapped Rajagopal 80 in the generated back end's configuration (HS,
     # velocity-correction slacks)
     "rajagopal80_wrapped": lambda: configs.rajagopal80(2, keep_path_wraps=True),
+    # MocoParameters (testMocoParameters.cpp): the oscillator's body mass, one
+    # parameter on two springs' stiffness, and every property kind of a
+    # muscle-driven model (body mass / mass-center element, muscle max force,
+    # actuator optimal force) in both dynamics modes
+    "oscillator_mass": lambda: configs.oscillator_mass(10),
+    "oscillator_two_springs_central": lambda: _central(configs.oscillator_two_springs(8)),
+    "gait_parameters": lambda: configs.gait10dof18musc_parameters(6),
+    "gait_parameters_implicit_trap_central": lambda: _central(_trap(configs.gait10dof18musc_parameters(
+        5, dynamics="implicit"))),
 }
 
 
@@ -1279,6 +1288,8 @@ SEED_CASES = {
     "coupled_pendulum": lambda: configs.double_pendulum_coupled(6),
     "gait_rigid": lambda: configs.gait10dof18musc(2),
     "gait_inverse": lambda: configs.gait10dof18musc_inverse(2, sparsity="none"),
+    "oscillator_two_springs": lambda: configs.oscillator_two_springs(6),
+    "gait_parameters": lambda: configs.gait10dof18musc_parameters(2),
 }
 
 

@@ -46,10 +46,52 @@ def test_driver_loads_tape_and_fails_loudly_without_gpu(tmp_path):
     write_tape(st5.problem.create_rep(), st5.solver.options(), str(p5))
     r = _run(p5)
     assert r.returncode == 2 and "no CPU fallback" in r.stderr, r.stderr
+    # version 8: springs + MocoParameters
+    st8 = configs.oscillator_two_springs(5)
+    p8 = tmp_path / "osc.tape"
+    write_tape(st8.problem.create_rep(), st8.solver.options(), str(p8))
+    r = _run(p8)
+    assert r.returncode == 2 and "no CPU fallback" in r.stderr, r.stderr
     data = path.read_bytes()
     (tmp_path / "cut.tape").write_bytes(data[:-8])
     r = _run(tmp_path / "cut.tape")
     assert r.returncode == 1 and "malformed" in r.stderr
+
+
+def test_driver_checks_the_guess_size(tmp_path):
+    """The initial-guess iterate on a tape (tape v8) is the whole x: n
+    doubles (mh_options.sparsity_guess), sized with mh_get_nlp_info_for
+    before any device call; the driver rejects a guess blob of another size,
+    and the Python side refuses a guess array of the wrong size."""
+    import ctypes as C
+    import struct
+    from mocohip import abi
+    from mocohip.solver import check_guess_size
+    st = configs.double_pendulum(5)
+    rep = st.problem.create_rep()
+    st.solver.optim_sparsity_detection = "initial-guess"
+    info = abi.mh_nlp_info()
+    opts = st.solver.options()
+    assert abi.load_mocohip().mh_get_nlp_info_for(C.byref(rep.struct), C.byref(opts), C.byref(info)) == 0
+    n = int(info.n)
+    st.solver.sparsity_guess = np.linspace(-0.5, 0.5, n + 1)
+    with pytest.raises(ValueError, match="sparsity_guess has"):
+        check_guess_size(rep, st.solver.options())
+    st.solver.sparsity_guess = np.linspace(-0.5, 0.5, n)
+    opts = st.solver.options()
+    check_guess_size(rep, opts)
+    path = tmp_path / "g.tape"
+    write_tape(rep, opts, str(path))
+    data = path.read_bytes()
+    key = struct.pack("<q", 8 * n) + np.linspace(-0.5, 0.5, n).tobytes()
+    at = data.find(key)
+    assert at > 0
+    r = _run(path)
+    assert "initial-guess iterate" not in r.stderr, r.stderr
+    bad = data[:at] + struct.pack("<q", 8 * (n - 1)) + data[at + 8:at + 8 * n] + data[at + 8 + 8 * n:]
+    (tmp_path / "bad.tape").write_bytes(bad)
+    r = _run(tmp_path / "bad.tape")
+    assert r.returncode == 1 and "initial-guess iterate has" in r.stderr, r.stderr
 
 
 @pytest.mark.gpu
@@ -62,6 +104,9 @@ def test_driver_loads_tape_and_fails_loudly_without_gpu(tmp_path):
     # multipliers, endpoint rows and detected sparsity
     ("wrapped_pendulum", lambda: configs.wrapped_pendulum(12, quadrant="-y")),
     ("rajagopal18_inverse_wrapped", lambda: configs.rajagopal18_inverse(3, keep_path_wraps=True)),
+    # tape v8: springs and MocoParameters
+    ("oscillator_two_springs", lambda: configs.oscillator_two_springs(12)),
+    ("oscillator_mass", lambda: configs.oscillator_mass(12)),
 ])
 def test_driver_matches_python_binding_bit_exact(tmp_path, name, mk):
     """The C++ host and the ctypes binding drive the same library: same g and

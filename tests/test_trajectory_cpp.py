@@ -4,7 +4,7 @@ integration/MocoHipSolver.cpp; driven here through ``mh_build --solution``)
 carries EVERY variable block by the reference's names -- states, controls,
 multipliers (lambda_cid<c>_p0), derivatives (<coordinate>/accel,
 <muscle>/implicitderiv_normalized_tendon_force), slacks (gamma_cid<c>_p0)
--- as MocoCasOCProblem.h:70-187 converts CasOC iterates, and converts back
+-- and parameters (MocoParameter names) as MocoCasOCProblem.h:70-187 converts CasOC iterates, and converts back
 to the same iterate bit for bit.
 
 Checked against the Python conversion (mocohip.trajectory.MocoTrajectory.
@@ -52,6 +52,9 @@ STUDIES = {
     "gait_implicit_both": lambda: configs.gait10dof18musc(3, tendon_compliance=True, tendon_dynamics="implicit",
                                                           dynamics="implicit"),
     "gait_inverse": lambda: configs.gait10dof18musc_inverse(3, sparsity="none"),
+    # MocoParameters: the last block, one value each (the .sto's first row)
+    "oscillator_mass": lambda: configs.oscillator_mass(4),
+    "gait_parameters_implicit": lambda: configs.gait10dof18musc_parameters(3, dynamics="implicit"),
 }
 
 
@@ -63,9 +66,10 @@ def test_cpp_solution_matches_python_conversion(tmp_path, name):
     cpp, info = _cpp_solution(tmp_path, st, x)
     assert info["n"] == nlp.n
     py = MocoTrajectory.from_iterate(nlp, x)
-    for b in ("state", "control", "multiplier", "derivative", "slack"):
+    for b in ("state", "control", "multiplier", "derivative", "slack", "parameter"):
         assert getattr(cpp, b + "_names") == getattr(py, b + "_names"), b
         assert np.array_equal(getattr(cpp, b + "s"), getattr(py, b + "s"), equal_nan=True), b
+    assert len(cpp.parameter_names) == nlp.NPAR
     assert np.array_equal(cpp.time, py.time)
     # every block named the reference's way
     if nlp.NM:
