@@ -1843,6 +1843,16 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
         c->d_par_targets = (mh_parameter_target*)(b + o_ptg);
         c->d_lane_main = (int*)(b + o_lmain);
         c->d_par_lanes = (int*)(b + o_plan);
+        // every copy starts as the pristine model (no targets written): a
+        // copy is a valid model before the first iterate's values arrive
+        const DevModel& B0 = c->M0;
+        const DevModel& Q0 = c->Mp[0];
+        ParamCopies P{B0.bodies, B0.acts, B0.mus, B0.sp, (mh_body*)Q0.bodies, (mh_actuator*)Q0.acts,
+                      (mh_muscle*)Q0.mus, (mh_spring*)Q0.sp, B0.nb, B0.nact, B0.nmus, B0.nsp, c->NCOPY, c->NPAR};
+        hipLaunchKernelGGL(k_apply_params, dim3(1), dim3(256), 0, 0, P, c->d_par_targets, 0,
+                (const double*)(b + o_x), c->h, c->fd);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipStreamSynchronize(0));
     }
     c->GS.ngoals = c->ngoals;
     c->GS.ndv = c->NDV;
@@ -2856,6 +2866,7 @@ static int eval_f_impl(mh_ctx* c, const double* x, double* f, bool partial) {
     HIPCHK(hipMemcpyAsync(c->d_x, x, sizeof(double) * c->n, hipMemcpyHostToDevice, c->stream));
     if (c->timing) HIPCHK(hipEventRecord(c->ev[0], c->stream));
     const bool endpoint = !partial || c->ie == c->N;
+    apply_params(c, c->d_x);   // the goals read the context's model, copy 0
     double* quad = c->d_quad;
     if (partial) c->d_quad = c->d_quadp;
     Layout L = make_layout(c, 0, c->G);
@@ -2881,6 +2892,7 @@ static int eval_grad_f_impl(mh_ctx* c, const double* x, double* grad, bool parti
     HIPCHK(hipMemcpyAsync(c->d_x, x, sizeof(double) * c->n, hipMemcpyHostToDevice, c->stream));
     if (c->timing) HIPCHK(hipEventRecord(c->ev[0], c->stream));
     const bool endpoint = !partial || c->ie == c->N;
+    apply_params(c, c->d_x);   // the goals read the context's model, copy 0
     Layout L = make_layout(c, 0, c->G);
     HIPCHK(hipMemsetAsync(c->d_grad, 0, sizeof(double) * c->n, c->stream));
     HIPCHK(hipMemsetAsync(c->d_tpart, 0, sizeof(double) * 2 * c->G, c->stream));
@@ -2924,6 +2936,7 @@ extern "C" int mh_eval_objective_terms(mh_ctx* c, const double* x, double* terms
     HIPCHK(hipSetDevice(c->device));
     (void)hipGetLastError();
     HIPCHK(hipMemcpyAsync(c->d_x, x, sizeof(double) * c->n, hipMemcpyHostToDevice, c->stream));
+    apply_params(c, c->d_x);   // the goals read the context's model, copy 0
     Layout L = make_layout(c, 0, c->G);
     c->be->integrand(c, c->d_x);
     HIPCHK(hipGetLastError());

@@ -285,6 +285,7 @@ ORACLE_SYMBOLS = {
     "orc_eval_g": (i32, [C.c_void_p, P(f64), P(f64)]),
     "orc_eval_jac_g": (i32, [C.c_void_p, P(f64), P(f64)]),
     "orc_eval_dae": (i32, [C.c_void_p, i32, P(f64), P(f64)]),
+    "orc_eval_dae_params": (i32, [C.c_void_p, P(f64), i32, f64, i32, P(f64), P(f64)]),
     "orc_dgf_curve": (f64, [P(mh_muscle), C.c_int, f64]),
     "orc_muscle_length_speed": (i32, [C.c_void_p, C.c_int, P(f64), P(f64),
                                       P(f64)]),

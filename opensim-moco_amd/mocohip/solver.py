@@ -440,7 +440,6 @@ class _NLPBase:
         self._check(self._fn("eval_dae")(self.ctx, npts, abi.dptr(inputs), abi.dptr(out)))
         return out
 
-
 class HipBatch:
     """mh_batch: structurally identical HipNLPs evaluated by one launch per
     kernel (include/mocohip.h mh_batch_*).  Calls take one device pointer
@@ -684,6 +683,19 @@ class OracleNLP(_NLPBase):
         self.lib = abi.load_oracle()
         super().__init__(rep, opts)
         self.lib.orc_set_threads(self.ctx, int(threads))
+
+    def eval_dae_params(self, inputs: np.ndarray, x: np.ndarray, moved: int = -1,
+                        step: float = 0.0) -> np.ndarray:
+        """eval_dae on the model with iterate x's MocoParameters applied,
+        parameter ``moved`` (-1: none) moved by ``step``."""
+        inputs = np.ascontiguousarray(inputs, float)
+        x = np.ascontiguousarray(x, float)
+        npts = inputs.shape[0]
+        assert inputs.shape[1] == 1 + self.NI and x.size == self.n
+        out = np.empty((npts, self.NO))
+        self._check(self.lib.orc_eval_dae_params(self.ctx, abi.dptr(x), int(moved), float(step), npts,
+                                                 abi.dptr(inputs), abi.dptr(out)))
+        return out
 
     def eval_f(self, x, new_x=True):
         x = np.ascontiguousarray(x, float)

@@ -2425,6 +2425,18 @@ int orc_eval_dae(orc_ctx* c, int32_t np, const double* in, double* out) {
     return MH_OK;
 }
 
+/* The DAE on the model with the iterate x's parameters applied, parameter
+ * `moved` (>= 0) moved by `step`: the device's parameter lanes (test use:
+ * tests/_lanes.py checks every lane output, parameter lanes included). */
+int orc_eval_dae_params(orc_ctx* c0, const double* x, int32_t moved, double step, int32_t np,
+        const double* in, double* out) {
+    if (moved >= c0->NPAR) return MH_ERR_INVALID;
+    orc_ctx* c = param_ctx(c0, x, moved, step);
+    int rc = orc_eval_dae(c, np, in, out);
+    param_ctx_free(c0, c);
+    return rc;
+}
+
 /* ======================================================================== */
 /* Transcription evaluation.                                                 */
 /* ======================================================================== */

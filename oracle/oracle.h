@@ -64,6 +64,10 @@ int orc_assemble_from_lanes(orc_ctx* ctx, const double* x, const double* times,
  * outputs per point: [udot(NQ), zdot(NZ)]. */
 int orc_eval_dae(orc_ctx* ctx, int32_t npoints, const double* inputs,
         double* outputs);
+/* the same on the model with iterate x's MocoParameters applied, parameter
+ * `moved` (-1: none) moved by `step` */
+int orc_eval_dae_params(orc_ctx* ctx, const double* x, int32_t moved, double step, int32_t npoints,
+        const double* inputs, double* outputs);
 
 /* Muscle-level probes for the DGF known-answer tests
  * (Moco/Tests/testMocoActuators.cpp:199-220,1026-1039). which:

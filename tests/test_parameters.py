@@ -234,6 +234,36 @@ def test_device_parameter_jacobian_matches_the_oracle(name):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("name", ["oscillator_two_springs", "gait_parameters"])
+def test_device_objective_first_call(name):
+    """The objective and its gradient as a fresh context's FIRST calls (the
+    optimizer's scaling pass, before any constraint evaluation): the goals
+    read the model copy the iterate's parameters were applied to -- created
+    as the pristine model and rewritten by every objective call -- and agree
+    with the oracle."""
+    from mocohip.solver import HipNLP
+    st = STUDIES[name]()
+    rep = st.problem.create_rep()
+    ref = OracleNLP(rep, st.solver.options(), threads=8)
+    for trial in range(2):
+        gpu = HipNLP(rep, st.solver.options())
+        try:
+            x = ref.initial_guess_from_bounds()
+            x[gpu.n - gpu.NPAR:] *= 0.8 + 0.1 * trial
+            if trial == 0:
+                gf, f = gpu.eval_grad_f(x), gpu.eval_f(x)
+            else:
+                f, gf = gpu.eval_f(x), gpu.eval_grad_f(x)
+            f0, gf0 = ref.eval_f(x), ref.eval_grad_f(x)
+            assert f == pytest.approx(f0, rel=1e-12, abs=1e-12)
+            tol = 1e-8 * np.abs(gf0) + 1e3 * np.finfo(float).eps * max(abs(f0), 1.0) / st.solver.fd_step
+            assert np.all(np.abs(gf - gf0) <= tol)
+        finally:
+            gpu.close()
+    ref.close()
+
+
+@pytest.mark.gpu
 def test_device_parameter_shards_reassemble_bit_exact():
     """Mesh-interval shards with parameters (every shard holds the parameter
     columns of its rows) concatenate to the unsharded g and Jacobian."""
@@ -264,3 +294,25 @@ def test_device_solve_recovers_the_parameter(name, true):
     sol = st.solve()
     assert sol.metadata["success"] == "true", sol.metadata
     assert sol.get_parameter(st.problem.parameters[0].name) == pytest.approx(true, rel=0.003)
+
+
+def test_oracle_dae_with_parameters_applied():
+    """orc_eval_dae_params (the oracle side of the device's parameter lanes):
+    at the model's own property value it is the pristine DAE bit for bit;
+    the oscillator's acceleration -k q / m scales with 1 / mass."""
+    st = configs.oscillator_mass(4)
+    rep = st.problem.create_rep()
+    nlp = OracleNLP(rep, st.solver.options())
+    try:
+        x = nlp.initial_guess_from_bounds()
+        rows = np.array([[0.1, 0.3, -0.2, 0.0], [0.2, -0.4, 0.5, 0.0]])[:, :1 + nlp.NI]
+        x[-1] = 0.5 * configs.OSCILLATOR_MASS   # the model's body mass
+        assert np.array_equal(nlp.eval_dae_params(rows, x), nlp.eval_dae(rows))
+        x[-1] = configs.OSCILLATOR_MASS
+        a = nlp.eval_dae_params(rows, x)[:, 0]
+        assert a == pytest.approx(-configs.OSCILLATOR_STIFFNESS * rows[:, 1] / configs.OSCILLATOR_MASS, rel=1e-14)
+        b = nlp.eval_dae_params(rows, x, 0, 1.0)[:, 0]
+        assert b == pytest.approx(-configs.OSCILLATOR_STIFFNESS * rows[:, 1] / (configs.OSCILLATOR_MASS + 1.0),
+                                  rel=1e-14)
+    finally:
+        nlp.close()
