@@ -117,7 +117,40 @@ def spline_eval(tp, L, te, kind):
             s = make_interp_spline(tp, L[:, c], k=deg)
             Lg[:, c], Vg[:, c] = s(te), s.derivative()(te)
         return Lg, Vg
+    if kind.startswith("smooth5:"):
+        return smoothing_eval(tp, L, te, float(kind.split(":")[1]))
     raise ValueError(kind)
+
+
+def smoothing_eval(tp, L, te, prel, m=3):
+    """The natural smoothing spline of degree 2m - 1 (GCVSPL's model:
+    minimize sum (y_i - s(x_i))^2 + p int (s^(m))^2, unit weights), in the
+    B-spline basis of degree 2m - 1 with knots at the data sites (which holds
+    the natural spline, the minimizer); p = prel * trace(B^T B) / trace(P).
+    prel -> 0 is the interpolating natural spline of the restatement; GCVSPL
+    with a prescribed error variance of 0 (GCVSpline's default) searches p
+    down to its lower bound, which a positive prel stands for."""
+    from scipy.interpolate import BSpline
+    k = 2 * m - 1
+    x = np.asarray(tp, float)
+    kn = np.concatenate([[x[0]] * (k + 1), x[1:-1], [x[-1]] * (k + 1)])
+    nb = len(kn) - k - 1
+    B = BSpline.design_matrix(x, kn, k).toarray()
+    # penalty: int B_i^(m) B_j^(m) over each interval, Gauss-Legendre exact
+    gx, gw = np.polynomial.legendre.leggauss(k)
+    P = np.zeros((nb, nb))
+    eye = np.eye(nb)
+    ders = [BSpline(kn, eye[i], k).derivative(m) for i in range(nb)]
+    for a, b in zip(x[:-1], x[1:]):
+        xs = 0.5 * (b - a) * gx + 0.5 * (a + b)
+        D = np.stack([d(xs) for d in ders])          # nb x q
+        P += (D * (0.5 * (b - a) * gw)) @ D.T
+    BtB = B.T @ B
+    lam = prel * np.trace(BtB) / np.trace(P)
+    C = np.linalg.solve(BtB + lam * P, B.T @ L)
+    Lg = np.stack([BSpline(kn, C[:, c], k)(te) for c in range(L.shape[1])], 1)
+    Vg = np.stack([BSpline(kn, C[:, c], k).derivative()(te) for c in range(L.shape[1])], 1)
+    return Lg, Vg
 
 
 def fiber(paths, Lg, Vg):
@@ -183,7 +216,8 @@ VARIANTS = [
     ("selection slop 0 (rows within [t0, tf] only)", {"slop": 0.0}),
     ("padded rows resampled onto the uniform min-step grid (quintic) and filtered with that step",
      {"resampled": True}),
-]
+] + [(f"resampled, quintic SMOOTHING spline p = {pr:.0e} trace(B^T B) / trace(P) (GCVSPL's residual smoothing)",
+      {"resampled": True, "spline": f"smooth5:{pr}"}) for pr in (1e-8, 1e-6, 1e-4, 1e-3, 1e-2)]
 
 
 def report(name, r, labels):
