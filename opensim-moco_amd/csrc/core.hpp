@@ -488,6 +488,15 @@ __global__ void __launch_bounds__(64) k_groups(DevModel M, Src S, Lanes Ln, Task
     groups_body<D>(M, S, Ln, TK, T, H, blockIdx.x);
 }
 
+// Variants measured no faster than the default path (round 5: k_groups_kr,
+// k_combine_split, the slot table staged in LDS by k_interval) are compiled
+// only with MOCOHIP_AB_VARIANTS=1 (make AB_VARIANTS=1), for A/B runs; the
+// default build instantiates none of them and ignores their environment
+// switches (profiles/r05_b, r05_n keep the measurements).
+#ifndef MOCOHIP_AB_VARIANTS
+#define MOCOHIP_AB_VARIANTS 0
+#endif
+
 // eval_g's task records in the kernel arguments.  With stride-1 lanes a
 // block's record is (group | live tasks << 16, first task) -- one task per
 // grid point and group -- and up to KR_MAX of them fit beside the other
@@ -499,12 +508,14 @@ constexpr int KR_MAX = 384;
 struct KRecs {
     int2 r[KR_MAX];
 };
+#if MOCOHIP_AB_VARIANTS
 template <class D>
 __global__ void __launch_bounds__(64) k_groups_kr(DevModel M, Src S, Lanes Ln, Tasks TK,
         double* __restrict__ T, double* __restrict__ H, KRecs KR) {
     const int2 rr = KR.r[blockIdx.x];
     groups_body_rec<D>(M, S, Ln, TK, T, H, make_int4(rr.x, rr.y, 1, __float_as_int(1.0f)));
 }
+#endif
 // One class of groups (groups_body CLS), blocks blk0.. of the task table.
 template <class D, int CLS>
 __global__ void __launch_bounds__(64) k_groups_part(DevModel M, Src S, Lanes Ln, Tasks TK,
@@ -632,6 +643,7 @@ __global__ void __launch_bounds__(64) k_combine_global(DevModel M, Src S, Lanes 
     D::combine(M, t, in, TL, StridedOut{Y + (long)kl * ystride_pt + r, (long)Ln.stride});
 }
 
+#if MOCOHIP_AB_VARIANTS
 // k_combine_global with the combine in two steps (D::combine_sum /
 // D::combine_finish, the arithmetic of D::combine bit for bit): a
 // 256-thread workgroup takes 64 lane roles; its 4 waves compute the roles'
@@ -668,6 +680,7 @@ __global__ void __launch_bounds__(256) k_combine_split(DevModel M, Src S, Lanes 
     D::combine_finish(M, t, in, TL, SumsLds{lds(sS + ln), 64},
                       StridedOut{Y + (long)kl * ystride_pt + r, (long)Ln.stride});
 }
+#endif
 
 // Excitation lanes of a generated back end (mocohip.hip k_exc_fill, launched
 // through this host entry so that the fill kernel lives in one unit).
@@ -791,6 +804,31 @@ struct EndpointEqs {
     const TplEntry* __restrict__ tpl;
 };
 
+// Compiled Jacobian template (k_interval's assembly): one word per template
+// entry of the Jacobian lane layout.  A value is base + coef * q, with q one
+// double in the interval's LDS (a finite-difference quotient of sY, or the
+// constant 0 / 1 of dxdot's exact qdot = u rows), or q itself (raw: residual
+// rows); entries along t0 / tf (several f and dxdot terms) take the general
+// jac_entry path, path-constraint entries their own loop.  Same operations in
+// the same order as jac_entry, so the two agree bit for bit
+// (test_kernel_variants_bit_identical, MOCOHIP_CTPL=0).
+enum : uint32_t {
+    CT_OFF = 0xFFFFFu,          // bits 0-19: LDS offset of q relative to sY
+    CT_RAW = 1u << 26,
+    CT_GEN = 1u << 27,
+    CT_PATH = 1u << 28
+};
+__device__ __host__ __forceinline__ uint32_t ct_word(uint32_t off, uint32_t coef, uint32_t base) {
+    return off | (coef << 20) | (base << 23);
+}
+
+// A Jacobian value's store: plain, or non-temporal (nt = 1: the values are
+// written once and read by the host / the optimizer, not by this kernel)
+__device__ __forceinline__ void vstore(double* p, double v, int nt) {
+    if (nt) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
 struct Interval {
     int scheme;      // MH_HERMITE_SIMPSON / MH_TRAPEZOIDAL
     int interp;
@@ -819,6 +857,18 @@ struct Interval {
     int qfuse;       // k_interval forms each finite-difference quotient in the assembly
                      // (no in-place quotient pass)
     int xcd;         // k_interval: contiguous interval runs per XCD (xcd_interval)
+    // the assembly's base-lane offsets: read from the table after the words
+    // (0) or derived from the word's offset (1: off / stride * stride + base,
+    // the division as a multiply-high by smagic, exact below 2^20 / stride;
+    // the host checks it against the table once)
+    int dbase;
+    uint32_t smagic, sstride, sbase;
+    int nts;         // the Jacobian values stored non-temporally (streamed past L2)
+    __device__ __forceinline__ uint32_t base_of(uint32_t w, uint32_t nyall) const {
+        const uint32_t off = w & CT_OFF;
+        const bool lane = !(w & (CT_GEN | CT_PATH)) && off < nyall;
+        return lane ? __umulhi(off, smagic) * sstride + sbase : 0u;
+    }
     // Every interval opens with its mesh point's path rows.  The interval
     // N-1 also owns the tail (flattenConstraints, CasOCTranscription.h:
     // 286-308): the final mesh point's path rows, then the final grid
@@ -1197,23 +1247,6 @@ __device__ __forceinline__ void interval_span(const Interval& I, int i, int& k_f
 // allows (interval_lds), otherwise the split path runs.
 constexpr int IV_UNROLL = 4;
 constexpr int IV_PF = 12;   // k_interval: assembly words per thread prefetched before the quotients
-// Compiled Jacobian template (k_interval's assembly): one word per template
-// entry of the Jacobian lane layout.  A value is base + coef * q, with q one
-// double in the interval's LDS (a finite-difference quotient of sY, or the
-// constant 0 / 1 of dxdot's exact qdot = u rows), or q itself (raw: residual
-// rows); entries along t0 / tf (several f and dxdot terms) take the general
-// jac_entry path, path-constraint entries their own loop.  Same operations in
-// the same order as jac_entry, so the two agree bit for bit
-// (test_kernel_variants_bit_identical, MOCOHIP_CTPL=0).
-enum : uint32_t {
-    CT_OFF = 0xFFFFFu,          // bits 0-19: LDS offset of q relative to sY
-    CT_RAW = 1u << 26,
-    CT_GEN = 1u << 27,
-    CT_PATH = 1u << 28
-};
-__device__ __host__ __forceinline__ uint32_t ct_word(uint32_t off, uint32_t coef, uint32_t base) {
-    return off | (coef << 20) | (base << 23);
-}
 // LDS constants after the times: [0] 0.0, [1] 1.0, [2..7] the interval's
 // coefficients {0, -h/8, h/8, -h/6, (-h/6) 4, -h/2}, [8..11] the bases {0,
 // -1/2, 1, -1} (a word's coefficient / base selectors index them).  After
@@ -1343,7 +1376,7 @@ __device__ __forceinline__ void interval_body(const DevModel& M, const Src& S, c
 #pragma unroll
     for (int u = 0; u < IV_PF; ++u) {
         const int e = threadIdx.x + u * blockDim.x;
-        pb[u] = I.pf && ctpl && e < ne_iv ? cbase[e] : 0u;
+        pb[u] = I.pf && ctpl && e < ne_iv ? (I.dbase ? I.base_of(pw[u], (uint32_t)(npts * ny)) : cbase[e]) : 0u;
     }
     // likewise the template entry of this thread's first t0 / tf entry
     int eg0 = -1;
@@ -1459,7 +1492,7 @@ __device__ __forceinline__ void interval_body(const DevModel& M, const Src& S, c
                 // entries are written by the loops below
 #pragma unroll
                 for (int u = 0; u < IV_PF; ++u)
-                    if (!(pw[u] & (CT_GEN | CT_PATH))) vi[e + u * B] = value(pw[u], qat(pw[u] & CT_OFF, pb[u]));
+                    if (!(pw[u] & (CT_GEN | CT_PATH))) vstore(vi + e + u * B, value(pw[u], qat(pw[u] & CT_OFF, pb[u])), I.nts);
                 if (I.pf) e += IV_PF * B;
                 for (; e + (IV_UNROLL - 1) * B < ne; e += IV_UNROLL * B) {
                     uint32_t w[IV_UNROLL], wb[IV_UNROLL];
@@ -1467,17 +1500,22 @@ __device__ __forceinline__ void interval_body(const DevModel& M, const Src& S, c
 #pragma unroll
                     for (int u = 0; u < IV_UNROLL; ++u) {
                         w[u] = ctpl[e + u * B];
-                        wb[u] = cbase[e + u * B];
+                        if (!I.dbase) wb[u] = cbase[e + u * B];
+                    }
+                    if (I.dbase) {
+#pragma unroll
+                        for (int u = 0; u < IV_UNROLL; ++u) wb[u] = I.base_of(w[u], (uint32_t)nyall);
                     }
 #pragma unroll
                     for (int u = 0; u < IV_UNROLL; ++u) q[u] = qat(w[u] & CT_OFF, wb[u]);
 #pragma unroll
                     for (int u = 0; u < IV_UNROLL; ++u)
-                        if (!(w[u] & (CT_GEN | CT_PATH))) vi[e + u * B] = value(w[u], q[u]);
+                        if (!(w[u] & (CT_GEN | CT_PATH))) vstore(vi + e + u * B, value(w[u], q[u]), I.nts);
                 }
                 for (; e < ne; e += B) {
                     const uint32_t wu = ctpl[e];
-                    if (!(wu & (CT_GEN | CT_PATH))) vi[e] = value(wu, qat(wu & CT_OFF, cbase[e]));
+                    const uint32_t bu = I.dbase ? I.base_of(wu, (uint32_t)nyall) : cbase[e];
+                    if (!(wu & (CT_GEN | CT_PATH))) vstore(vi + e, value(wu, qat(wu & CT_OFF, bu)), I.nts);
                 }
             };
             using FF = std::integral_constant<int, MH_FD_FORWARD>;
@@ -2181,6 +2219,9 @@ struct mh_ctx {
     bool async = false;                // *_device entries return once enqueued
     int iv_dbg_stop = 0;               // diagnostic: k_interval stops after phase n
     int iv_pf = 1;                     // MOCOHIP_IV_PF=0: no assembly-word prefetch (A/B)
+    int iv_dbase = 0;                  // base-lane offsets derived from the words (MOCOHIP_DBASE)
+    uint32_t iv_smagic = 0, iv_sstride = 1, iv_sbase = 0;
+    int iv_nts = 0;                    // non-temporal Jacobian value stores (MOCOHIP_NT_STORES)
     int iv_xcd = 1;                    // XCD-contiguous interval order (MOCOHIP_IV_XCD=0: off, A/B)
     int iv_qfuse = 1;                  // MOCOHIP_IV_QFUSE=0: in-place quotient pass (A/B)
     hipEvent_t ev[5] = {};         // stage boundaries (+ ev[4] after k_groups)
@@ -2318,7 +2359,7 @@ inline Layout make_layout(const mh_ctx* c, int k0, int nk) {
 inline Interval make_interval(const mh_ctx* c, double*& g, double*& v) {
     Interval I{c->scheme, c->interp, c->ib, c->rpi, c->nnz_int, c->NMB + c->NAR, c->NMB, c->NQ + c->NZ,
                c->N, c->nnz_tail, c->ntail, c->npe, c->NK, c->OKC, c->P, c->E, nullptr, nullptr, c->iv_dbg_stop, c->iv_pf, c->iv_qfuse,
-               c->iv_xcd};
+               c->iv_xcd, c->iv_dbase, c->iv_smagic, c->iv_sstride, c->iv_sbase, c->iv_nts};
     if (c->ib == 0 && c->nep > 0) {
         I.gh = g;
         I.vh = v;
@@ -2452,6 +2493,7 @@ static void launch_groups(mh_ctx* c, const Src& S, const Lanes& ln, const TaskSe
                 c->stream, c->M, S, ln, ts.dev, T, H, ts.nheavy);
         return;
     }
+#if MOCOHIP_AB_VARIANTS
     if (&ts == &c->ts_g && c->krec_ok) {
         static_assert(sizeof(DevModel) + sizeof(Src) + sizeof(Lanes) + sizeof(Tasks) + 2 * sizeof(double*) +
                       sizeof(KRecs) <= 4096, "k_groups_kr: kernel arguments over 4 KB");
@@ -2459,6 +2501,7 @@ static void launch_groups(mh_ctx* c, const Src& S, const Lanes& ln, const TaskSe
                 T, H, c->krec_g);
         return;
     }
+#endif
     hipLaunchKernelGGL(k_groups<D>, dim3((unsigned)ts.nblocks), dim3(64), 0, c->stream, c->M, S, ln, ts.dev, T, H);
 }
 
@@ -2507,12 +2550,14 @@ static int launch_tasks(mh_ctx* c, const Src& S, const Lanes& ln, const TaskSet&
         const bool xs = c->d_exc_slot && &ts == &c->ts_jac;
         const int per = xs ? ln.stride - c->n_exc_gen : ln.stride;
         const long lanes = (long)ts.dev.nk * per;
+#if MOCOHIP_AB_VARIANTS
         // the sums over the waves (k_combine_split, MOCOHIP_CSPLIT=1; slower)
         if (c->csplit && D::NSUM > 0)
             hipLaunchKernelGGL(k_combine_split<D>, dim3((unsigned)((lanes + 63) / 64)), dim3(256), 0,
                     c->stream, c->M, S, ln, ts.dev, T, H, times, Y, (long)D::NO * ln.stride,
                     xs ? (const int*)c->d_cmb_map : nullptr, per);
         else
+#endif
             hipLaunchKernelGGL(k_combine_global<D>, dim3((unsigned)((lanes + 63) / 64)), dim3(64), 0,
                     c->stream, c->M, S, ln, ts.dev, T, H, times, Y, (long)D::NO * ln.stride,
                     xs ? (const int*)c->d_cmb_map : nullptr, per, c->iv_xcd);
@@ -2626,7 +2671,9 @@ static void be_interval(mh_ctx* c, const double* x, int mode, double* g, double*
     // staged in LDS when they are many (Rajagopal 80: 1,111 doubles, where the
     // global-memory reads made eval_g slower, profiles/r05_f); MOCOHIP_IVG_GM
     // = 0 / 1 forces either
+#if MOCOHIP_AB_VARIANTS
     if (v && threads > 256 && c->iv_slots_lds && ln.stride > 1) kern = k_interval<D, 1024, false, false, true>;
+#endif
     if (!v && ln.stride == 1 && threads <= 256 && c->ivg_base) {
         const bool gm = c->ivg_gm < 0 ? ts.dev.tdoubles <= kIvgGmMaxDoubles : c->ivg_gm != 0;
         kern = gm ? k_interval<D, 256, true, true> : k_interval<D, 256, true>;

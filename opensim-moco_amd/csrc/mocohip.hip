@@ -209,7 +209,11 @@ __global__ void __launch_bounds__(256) k_transcribe(Layout L, Interval I, Lanes 
                     for (int u = 0; u < CT_U; ++u) {
                         const int e = min(e0 + u * (int)blockDim.x, ee - 1);
                         w[u] = ctpl[e];
-                        wb[u] = FD == MH_FD_CENTRAL ? 0u : cbase[e];
+                        if (!I.dbase) wb[u] = FD == MH_FD_CENTRAL ? 0u : cbase[e];
+                    }
+                    if (I.dbase) {
+#pragma unroll
+                        for (int u = 0; u < CT_U; ++u) wb[u] = FD == MH_FD_CENTRAL ? 0u : I.base_of(w[u], nyall);
                     }
                     double ya[CT_U], yb[CT_U];
 #pragma unroll
@@ -226,7 +230,7 @@ __global__ void __launch_bounds__(256) k_transcribe(Layout L, Interval I, Lanes 
                         const double qd = FD == MH_FD_BACKWARD ? (yb[u] - ya[u]) / hq : (ya[u] - yb[u]) / hq;
                         const double q = off >= nyall ? (off == kone ? 1.0 : 0.0) : (yq ? ya[u] : qd);
                         const double v = (w[u] & CT_RAW) ? q : kb[(w[u] >> 23) & 7] + kc[(w[u] >> 20) & 7] * q;
-                        if (e < ee && !(w[u] & (CT_GEN | CT_PATH))) vi[e] = v;
+                        if (e < ee && !(w[u] & (CT_GEN | CT_PATH))) vstore(vi + e, v, I.nts);
                     }
                 }
             };
@@ -986,6 +990,35 @@ static bool path_entries_lead(const mh_ctx* c) {
     return true;
 }
 
+// The assembly's base-lane offsets derived from the words instead of read
+// from the table (MOCOHIP_DBASE=1; enabled only where the derivation equals
+// the table entry for entry) and the Jacobian values stored non-temporally
+// (MOCOHIP_NT_STORES=1).  Called again after a detected template replaces
+// the block-dense one.
+static void setup_assembly_variants(mh_ctx* c) {
+    const char* ed = std::getenv("MOCOHIP_DBASE");
+    const char* en = std::getenv("MOCOHIP_NT_STORES");
+    c->iv_nts = en && std::strcmp(en, "1") == 0 ? 1 : 0;
+    const uint32_t stride = (uint32_t)c->lanes_jac.stride;
+    c->iv_sstride = stride;
+    c->iv_sbase = (uint32_t)c->lanes_jac.base;
+    c->iv_smagic = (uint32_t)(0xFFFFFFFFull / stride + 1);
+    c->iv_dbase = 0;
+    if (ed && std::strcmp(ed, "1") == 0 && !c->ctpl.empty() && c->lanes_jac.fd != MH_FD_CENTRAL) {
+        const size_t nw = (size_t)c->nnz_int + (size_t)c->nnz_tail;
+        const int npts = c->scheme == MH_HERMITE_SIMPSON ? 3 : 2;
+        const uint32_t nyall = (uint32_t)(npts * c->NO) * stride;
+        bool ok = c->ctpl.size() >= 2 * nw && nyall < (1u << 20);
+        for (size_t e = 0; ok && e < nw; ++e) {
+            const uint32_t w = c->ctpl[e], off = w & CT_OFF;
+            const bool lane = !(w & (CT_GEN | CT_PATH)) && off < nyall;
+            const uint32_t d = lane ? (uint32_t)(((uint64_t)off * c->iv_smagic) >> 32) * stride + c->iv_sbase : 0u;
+            ok = d == c->ctpl[nw + e];
+        }
+        c->iv_dbase = ok ? 1 : 0;
+    }
+}
+
 // The compiled template (core.hpp CT_*) of c->tpl for the Jacobian lane
 // layout: per entry the LDS offset of the quotient (or constant) it scales,
 // its coefficient and base -- the operations jac_entry performs for it.
@@ -1742,7 +1775,7 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
         // (eval_g's k_groups 7.12 vs 7.05 us, profiles/r05_n)
         {
             const char* ekr = std::getenv("MOCOHIP_GROUPS_KR");
-            bool ok = ekr && std::strcmp(ekr, "1") == 0 && c->lanes_g.stride == 1 &&
+            bool ok = MOCOHIP_AB_VARIANTS && ekr && std::strcmp(ekr, "1") == 0 && c->lanes_g.stride == 1 &&
                       c->ts_g.nblocks > 0 && c->ts_g.nblocks <= KR_MAX &&
                       c->ts_g.blk.size() >= 4 * (size_t)c->ts_g.nblocks;
             const float one = 1.0f;
@@ -1928,13 +1961,13 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
         // calls/s, profiles/r05_c; so was the same split inside k_interval,
         // profiles/r05_b): the combine is not bound by its sums' chains
         const char* ecs = std::getenv("MOCOHIP_CSPLIT");
-        c->csplit = ecs && std::strcmp(ecs, "1") == 0 ? 1 : 0;
+        c->csplit = MOCOHIP_AB_VARIANTS && ecs && std::strcmp(ecs, "1") == 0 ? 1 : 0;   // AB build only
         // eval_g's k_interval with the group results at compile-time base
         // slots (core.hpp TaskLoadBase; MOCOHIP_IVG_BASE=0: the slot table)
         const char* eb = std::getenv("MOCOHIP_IVG_BASE");
         c->ivg_base = eb && std::strcmp(eb, "0") == 0 ? 0 : 1;
         const char* esl = std::getenv("MOCOHIP_IV_SLOTS_LDS");
-        c->iv_slots_lds = esl && std::strcmp(esl, "1") == 0 ? 1 : 0;
+        c->iv_slots_lds = MOCOHIP_AB_VARIANTS && esl && std::strcmp(esl, "1") == 0 ? 1 : 0;   // AB build only
         const char* egm = std::getenv("MOCOHIP_IVG_GM");
         c->ivg_gm = !egm ? -1 : std::strcmp(egm, "0") == 0 ? 0 : 1;
         const TaskInfo* tib = backend_tasks(c->be);
@@ -1955,6 +1988,7 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
         const bool allow = !(ei && std::strcmp(ei, "0") == 0);
         const char* ec = std::getenv("MOCOHIP_CTPL");
         c->use_ctpl = !(ec && std::strcmp(ec, "0") == 0);
+        setup_assembly_variants(c.get());
         const char* er = std::getenv("MOCOHIP_ROLES");
         c->use_roles = er && std::strcmp(er, "1") == 0 && c->NM == 0;   // measured slower
         const char* et = std::getenv("MOCOHIP_ROLE_THREADS");
@@ -1996,6 +2030,7 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
             c->E.nnz = c->nnz_ep;
             c->nnz = c->nnz_ep + (int64_t)c->nnz_int * c->N + c->nnz_tail;
             if (!compile_template(c.get())) return set_err(MH_ERR_UNSUPPORTED, "Jacobian template does not compile");
+            setup_assembly_variants(c.get());
             HIPCHK(hipMemcpy(c->d_tpl, c->tpl.data(), sizeof(TplEntry) * c->tpl.size(), hipMemcpyHostToDevice));
             HIPCHK(hipMemcpy(c->d_ctpl, c->ctpl.data(), sizeof(uint32_t) * c->ctpl.size(),
                     hipMemcpyHostToDevice));
@@ -3324,6 +3359,8 @@ extern "C" int mh_get_backend_flags(const mh_ctx* c, char* flags, int32_t len) {
     if (c->use_interval[0]) f += c->ivg_base ? " interval-g base-slots" : " interval-g";
     if (c->krec_ok) f += " groups-kernarg";
     if (!c->use_ctpl) f += " no-ctpl";
+    if (c->iv_dbase) f += " dbase";
+    if (c->iv_nts) f += " nt-stores";
     if (c->use_roles && c->use_interval[1]) f += " roles";
     if (c->quot) f += " quot";
     if (c->asm_grid_stride) f += " asm-gs";

@@ -24,7 +24,7 @@ import numpy as np
 import pytest
 
 import _lanes
-from mocohip import configs
+from mocohip import abi, configs
 from mocohip.solver import HipNLP, OracleNLP
 
 pytestmark = pytest.mark.gpu
@@ -322,7 +322,8 @@ def _pair(name, backend="auto", tasks=None, env=None):
                                                   "MOCOHIP_EXC_LANES", "MOCOHIP_G_BLOCK", "MOCOHIP_G_LDS",
                                                   "MOCOHIP_G_LDS_GUARD",
                                                   "MOCOHIP_GROUPS_SPLIT", "MOCOHIP_COMBINE",
-                                                  "MOCOHIP_ASM_CHUNK", "MOCOHIP_ASM_CTPL")}
+                                                  "MOCOHIP_ASM_CHUNK", "MOCOHIP_ASM_CTPL", "MOCOHIP_DBASE",
+                                                  "MOCOHIP_NT_STORES")}
     if backend != "auto":
         os.environ["MOCOHIP_BACKEND"] = backend
     if tasks:
@@ -848,8 +849,9 @@ def test_pruned_tasks_bit_identical(name):
                                      {"MOCOHIP_IVG_THREADS": "1024"},
                                      {"MOCOHIP_IVG_BASE": "0"},
                                      {"MOCOHIP_IVG_GM": "0"},
-                                     {"MOCOHIP_GROUPS_KR": "1"},
-                                     {"MOCOHIP_IV_SLOTS_LDS": "1"}])
+                                     {"MOCOHIP_DBASE": "1"},
+                                     {"MOCOHIP_NT_STORES": "1"},
+                                     {"MOCOHIP_INTERVAL": "0", "MOCOHIP_DBASE": "1", "MOCOHIP_NT_STORES": "1"}])
 def test_kernel_variants_bit_identical(name, variant):
     """The default k_interval (combine + transcription per mesh interval,
     raw outputs in LDS) writes exactly what k_interval writes through
@@ -861,9 +863,9 @@ def test_kernel_variants_bit_identical(name, variant):
     Y."""
     gpu, _, _ = _pair(name)
     split, _, _ = _pair(name, env=variant)
-    if variant == {"MOCOHIP_GROUPS_KR": "1"}:
-        # eval_g's task records as kernel arguments against the task table
-        assert "groups-kernarg" not in gpu.backend_flags().split()
+    if variant.get("MOCOHIP_DBASE") == "1" and split.opts.finite_difference_scheme != abi.MH_FD_CENTRAL:
+        # forward / backward differences: the derived offsets equal the table
+        assert "dbase" in split.backend_flags().split(), split.backend_flags()
     if variant == {"MOCOHIP_IVG_BASE": "0"}:
         # eval_g's base-slot kernel against the slot-table path
         fa, fb = gpu.backend_flags().split(), split.backend_flags().split()
@@ -990,19 +992,13 @@ def test_group_kernel_split_bit_identical(name):
 def test_combine_variants_bit_identical(name):
     """Split path (k_combine + k_transcribe): the combine with the group
     results staged in LDS (k_combine) or read from global memory
-    (k_combine_split, its sums over a workgroup's waves, and
-    k_combine_global, one thread per lane role; chosen where the LDS-staged
+    (k_combine_global, one thread per lane role; chosen where the LDS-staged
     kernel spills) write identical lanes, g and Jacobian."""
     a, _, _ = _pair(name, env={"MOCOHIP_COMBINE": "lds", "MOCOHIP_INTERVAL": "0"})
     b, _, _ = _pair(name, env={"MOCOHIP_COMBINE": "global", "MOCOHIP_INTERVAL": "0"})
-    # the global-memory combine as one thread per lane role (k_combine_global,
-    # default) and with its sums over a workgroup's waves (k_combine_split)
-    c, _, _ = _pair(name, env={"MOCOHIP_COMBINE": "global", "MOCOHIP_INTERVAL": "0", "MOCOHIP_CSPLIT": "1"})
     for _, x in _iterates(a):
         assert np.array_equal(a.eval_g(x), b.eval_g(x), equal_nan=True)
         assert np.array_equal(a.eval_jac_g(x), b.eval_jac_g(x), equal_nan=True)
-        assert np.array_equal(c.eval_g(x), b.eval_g(x), equal_nan=True)
-        assert np.array_equal(c.eval_jac_g(x), b.eval_jac_g(x), equal_nan=True)
 
 
 def test_work_accounting():
