@@ -822,13 +822,6 @@ __device__ __host__ __forceinline__ uint32_t ct_word(uint32_t off, uint32_t coef
     return off | (coef << 20) | (base << 23);
 }
 
-// A Jacobian value's store: plain, or non-temporal (nt = 1: the values are
-// written once and read by the host / the optimizer, not by this kernel)
-__device__ __forceinline__ void vstore(double* p, double v, int nt) {
-    if (nt) __builtin_nontemporal_store(v, p);
-    else *p = v;
-}
-
 struct Interval {
     int scheme;      // MH_HERMITE_SIMPSON / MH_TRAPEZOIDAL
     int interp;
@@ -857,13 +850,14 @@ struct Interval {
     int qfuse;       // k_interval forms each finite-difference quotient in the assembly
                      // (no in-place quotient pass)
     int xcd;         // k_interval: contiguous interval runs per XCD (xcd_interval)
-    // the assembly's base-lane offsets: read from the table after the words
+    // k_transcribe's base-lane offsets: read from the table after the words
     // (0) or derived from the word's offset (1: off / stride * stride + base,
     // the division as a multiply-high by smagic, exact below 2^20 / stride;
-    // the host checks it against the table once)
+    // the host checks it against the table once).  k_interval reads the
+    // table: its words are prefetched with their offsets, and the derivation
+    // measured slower there (17.7 -> 19.8 us, profiles/r06_c)
     int dbase;
     uint32_t smagic, sstride, sbase;
-    int nts;         // the Jacobian values stored non-temporally (streamed past L2)
     __device__ __forceinline__ uint32_t base_of(uint32_t w, uint32_t nyall) const {
         const uint32_t off = w & CT_OFF;
         const bool lane = !(w & (CT_GEN | CT_PATH)) && off < nyall;
@@ -1376,7 +1370,7 @@ __device__ __forceinline__ void interval_body(const DevModel& M, const Src& S, c
 #pragma unroll
     for (int u = 0; u < IV_PF; ++u) {
         const int e = threadIdx.x + u * blockDim.x;
-        pb[u] = I.pf && ctpl && e < ne_iv ? (I.dbase ? I.base_of(pw[u], (uint32_t)(npts * ny)) : cbase[e]) : 0u;
+        pb[u] = I.pf && ctpl && e < ne_iv ? cbase[e] : 0u;
     }
     // likewise the template entry of this thread's first t0 / tf entry
     int eg0 = -1;
@@ -1492,7 +1486,7 @@ __device__ __forceinline__ void interval_body(const DevModel& M, const Src& S, c
                 // entries are written by the loops below
 #pragma unroll
                 for (int u = 0; u < IV_PF; ++u)
-                    if (!(pw[u] & (CT_GEN | CT_PATH))) vstore(vi + e + u * B, value(pw[u], qat(pw[u] & CT_OFF, pb[u])), I.nts);
+                    if (!(pw[u] & (CT_GEN | CT_PATH))) vi[e + u * B] = value(pw[u], qat(pw[u] & CT_OFF, pb[u]));
                 if (I.pf) e += IV_PF * B;
                 for (; e + (IV_UNROLL - 1) * B < ne; e += IV_UNROLL * B) {
                     uint32_t w[IV_UNROLL], wb[IV_UNROLL];
@@ -1500,22 +1494,17 @@ __device__ __forceinline__ void interval_body(const DevModel& M, const Src& S, c
 #pragma unroll
                     for (int u = 0; u < IV_UNROLL; ++u) {
                         w[u] = ctpl[e + u * B];
-                        if (!I.dbase) wb[u] = cbase[e + u * B];
-                    }
-                    if (I.dbase) {
-#pragma unroll
-                        for (int u = 0; u < IV_UNROLL; ++u) wb[u] = I.base_of(w[u], (uint32_t)nyall);
+                        wb[u] = cbase[e + u * B];
                     }
 #pragma unroll
                     for (int u = 0; u < IV_UNROLL; ++u) q[u] = qat(w[u] & CT_OFF, wb[u]);
 #pragma unroll
                     for (int u = 0; u < IV_UNROLL; ++u)
-                        if (!(w[u] & (CT_GEN | CT_PATH))) vstore(vi + e + u * B, value(w[u], q[u]), I.nts);
+                        if (!(w[u] & (CT_GEN | CT_PATH))) vi[e + u * B] = value(w[u], q[u]);
                 }
                 for (; e < ne; e += B) {
                     const uint32_t wu = ctpl[e];
-                    const uint32_t bu = I.dbase ? I.base_of(wu, (uint32_t)nyall) : cbase[e];
-                    if (!(wu & (CT_GEN | CT_PATH))) vstore(vi + e, value(wu, qat(wu & CT_OFF, bu)), I.nts);
+                    if (!(wu & (CT_GEN | CT_PATH))) vi[e] = value(wu, qat(wu & CT_OFF, cbase[e]));
                 }
             };
             using FF = std::integral_constant<int, MH_FD_FORWARD>;
@@ -2219,9 +2208,8 @@ struct mh_ctx {
     bool async = false;                // *_device entries return once enqueued
     int iv_dbg_stop = 0;               // diagnostic: k_interval stops after phase n
     int iv_pf = 1;                     // MOCOHIP_IV_PF=0: no assembly-word prefetch (A/B)
-    int iv_dbase = 0;                  // base-lane offsets derived from the words (MOCOHIP_DBASE)
+    int iv_dbase = 0;                  // k_transcribe derives base-lane offsets (MOCOHIP_DBASE=0: the table)
     uint32_t iv_smagic = 0, iv_sstride = 1, iv_sbase = 0;
-    int iv_nts = 0;                    // non-temporal Jacobian value stores (MOCOHIP_NT_STORES)
     int iv_xcd = 1;                    // XCD-contiguous interval order (MOCOHIP_IV_XCD=0: off, A/B)
     int iv_qfuse = 1;                  // MOCOHIP_IV_QFUSE=0: in-place quotient pass (A/B)
     hipEvent_t ev[5] = {};         // stage boundaries (+ ev[4] after k_groups)
@@ -2359,7 +2347,7 @@ inline Layout make_layout(const mh_ctx* c, int k0, int nk) {
 inline Interval make_interval(const mh_ctx* c, double*& g, double*& v) {
     Interval I{c->scheme, c->interp, c->ib, c->rpi, c->nnz_int, c->NMB + c->NAR, c->NMB, c->NQ + c->NZ,
                c->N, c->nnz_tail, c->ntail, c->npe, c->NK, c->OKC, c->P, c->E, nullptr, nullptr, c->iv_dbg_stop, c->iv_pf, c->iv_qfuse,
-               c->iv_xcd, c->iv_dbase, c->iv_smagic, c->iv_sstride, c->iv_sbase, c->iv_nts};
+               c->iv_xcd, c->iv_dbase, c->iv_smagic, c->iv_sstride, c->iv_sbase};
     if (c->ib == 0 && c->nep > 0) {
         I.gh = g;
         I.vh = v;

@@ -230,7 +230,7 @@ __global__ void __launch_bounds__(256) k_transcribe(Layout L, Interval I, Lanes 
                         const double qd = FD == MH_FD_BACKWARD ? (yb[u] - ya[u]) / hq : (ya[u] - yb[u]) / hq;
                         const double q = off >= nyall ? (off == kone ? 1.0 : 0.0) : (yq ? ya[u] : qd);
                         const double v = (w[u] & CT_RAW) ? q : kb[(w[u] >> 23) & 7] + kc[(w[u] >> 20) & 7] * q;
-                        if (e < ee && !(w[u] & (CT_GEN | CT_PATH))) vstore(vi + e, v, I.nts);
+                        if (e < ee && !(w[u] & (CT_GEN | CT_PATH))) vi[e] = v;
                     }
                 }
             };
@@ -990,21 +990,21 @@ static bool path_entries_lead(const mh_ctx* c) {
     return true;
 }
 
-// The assembly's base-lane offsets derived from the words instead of read
-// from the table (MOCOHIP_DBASE=1; enabled only where the derivation equals
-// the table entry for entry) and the Jacobian values stored non-temporally
-// (MOCOHIP_NT_STORES=1).  Called again after a detected template replaces
-// the block-dense one.
+// k_transcribe's base-lane offsets derived from the words instead of read
+// from the table after them (default; MOCOHIP_DBASE=0 reads the table),
+// enabled only where the derivation equals the table entry for entry:
+// configs[3] 1,605 -> 1,628 calls/s (profiles/r06_c; the table read shares
+// the word's dependency chain).  (Non-temporal value stores were measured
+// too: no difference.)  Called again after a detected template replaces the
+// block-dense one.
 static void setup_assembly_variants(mh_ctx* c) {
     const char* ed = std::getenv("MOCOHIP_DBASE");
-    const char* en = std::getenv("MOCOHIP_NT_STORES");
-    c->iv_nts = en && std::strcmp(en, "1") == 0 ? 1 : 0;
     const uint32_t stride = (uint32_t)c->lanes_jac.stride;
     c->iv_sstride = stride;
     c->iv_sbase = (uint32_t)c->lanes_jac.base;
     c->iv_smagic = (uint32_t)(0xFFFFFFFFull / stride + 1);
     c->iv_dbase = 0;
-    if (ed && std::strcmp(ed, "1") == 0 && !c->ctpl.empty() && c->lanes_jac.fd != MH_FD_CENTRAL) {
+    if (!(ed && std::strcmp(ed, "0") == 0) && !c->ctpl.empty() && c->lanes_jac.fd != MH_FD_CENTRAL) {
         const size_t nw = (size_t)c->nnz_int + (size_t)c->nnz_tail;
         const int npts = c->scheme == MH_HERMITE_SIMPSON ? 3 : 2;
         const uint32_t nyall = (uint32_t)(npts * c->NO) * stride;
@@ -3360,7 +3360,6 @@ extern "C" int mh_get_backend_flags(const mh_ctx* c, char* flags, int32_t len) {
     if (c->krec_ok) f += " groups-kernarg";
     if (!c->use_ctpl) f += " no-ctpl";
     if (c->iv_dbase) f += " dbase";
-    if (c->iv_nts) f += " nt-stores";
     if (c->use_roles && c->use_interval[1]) f += " roles";
     if (c->quot) f += " quot";
     if (c->asm_grid_stride) f += " asm-gs";

@@ -1544,17 +1544,17 @@ def _emit_combine(M: ModelView, Lo: _Layout, groups: List[_Group]):
         lam = coordinate_tree(M, cb, NQ)
         factor_columns(g, Hs, lam, sorted({k[0] for k in shares}))
         xs = E.solve(lam, Hs, bvec)
-    for i in range(NQ):
-        g.raw(f"out[{i}] = {xs[i]};")
     kcf = {}
+    copies = []
     for gi, gr in enumerate(groups[1:], start=1):
         for f, (kind, zi) in enumerate(gr.fields):
             if kind == "z":
-                g.raw(f"out[{NQ + zi}] = T({gi}, {f});")
+                copies.append((NQ + zi, gi, f))
             elif kind == "r":
-                g.raw(f"out[{NQ + Lo.NZ + zi}] = T({gi}, {f});")
+                copies.append((NQ + Lo.NZ + zi, gi, f))
             elif kind in ("kpos", "kvel", "kg", "kc2"):
                 kcf[(kind, zi)] = S(n=f"T({gi}, {f})")
+    _emit_outputs(g, xs, copies)
     if Lo.NK:
         info = []
         for i, K in enumerate(M.kcs):
@@ -1564,6 +1564,39 @@ def _emit_combine(M: ModelView, Lo: _Layout, groups: List[_Group]):
         udot = [E.inp[Lo.NS + Lo.NC + j] for j in range(NQ)] if Lo.implicit else xs
         E.kc_outputs(info, udot)
     return g.lines, sum(g.flops.values())
+
+
+OUT_BATCH = 24   # group-result copies loaded together before their stores
+
+
+def _emit_outputs(g: Gen, xs, copies):
+    """The combine's outputs: the NQ solved values, then the outputs that
+    copy a group result (z, auxiliary residuals).  A copy is a load of T and
+    a store to out; emitted one after the other, every load waited for the
+    store before it (one counter covers a wave's loads and stores on CDNA,
+    and the compiler cannot move a T load above an out store), one memory
+    round trip per output -- for Rajagopal 80's 86 copies the combine's
+    longest chain.  So the copies are loaded in batches of OUT_BATCH, the
+    first before the solved values are stored, each batch's stores after
+    its loads: a round trip per batch.  The same values (copies), bit for
+    bit."""
+    batches = [copies[i:i + OUT_BATCH] for i in range(0, len(copies), OUT_BATCH)]
+
+    def load(b):
+        for o, gi, f in b:
+            g.raw(f"const double zo_{o} = T({gi}, {f});")
+
+    def store(b):
+        for o, _, _ in b:
+            g.raw(f"out[{o}] = zo_{o};")
+    if batches:
+        load(batches[0])
+    for i in range(len(xs)):
+        g.raw(f"out[{i}] = {xs[i]};")
+    for k, b in enumerate(batches):
+        if k:
+            load(b)
+        store(b)
 
 
 def _tree(g: Gen, ts):
@@ -1658,17 +1691,17 @@ def _emit_combine_finish(M: ModelView, Lo: _Layout, groups: List[_Group], consts
         lam = coordinate_tree(M, cb, NQ)
         factor_columns(g, Hs, lam, sorted({k[0] for k in keys}))
         xs = E.solve(lam, Hs, bvec)
-    for i in range(NQ):
-        g.raw(f"out[{i}] = {xs[i]};")
     kcf = {}
+    copies = []
     for gi, gr in enumerate(groups[1:], start=1):
         for f, (kind, zi) in enumerate(gr.fields):
             if kind == "z":
-                g.raw(f"out[{NQ + zi}] = T({gi}, {f});")
+                copies.append((NQ + zi, gi, f))
             elif kind == "r":
-                g.raw(f"out[{NQ + Lo.NZ + zi}] = T({gi}, {f});")
+                copies.append((NQ + Lo.NZ + zi, gi, f))
             elif kind in ("kpos", "kvel", "kg", "kc2"):
                 kcf[(kind, zi)] = S(n=f"T({gi}, {f})")
+    _emit_outputs(g, xs, copies)
     if Lo.NK:
         info = []
         for i, K in enumerate(M.kcs):

@@ -849,9 +849,7 @@ def test_pruned_tasks_bit_identical(name):
                                      {"MOCOHIP_IVG_THREADS": "1024"},
                                      {"MOCOHIP_IVG_BASE": "0"},
                                      {"MOCOHIP_IVG_GM": "0"},
-                                     {"MOCOHIP_DBASE": "1"},
-                                     {"MOCOHIP_NT_STORES": "1"},
-                                     {"MOCOHIP_INTERVAL": "0", "MOCOHIP_DBASE": "1", "MOCOHIP_NT_STORES": "1"}])
+                                     {"MOCOHIP_INTERVAL": "0", "MOCOHIP_DBASE": "0"}])
 def test_kernel_variants_bit_identical(name, variant):
     """The default k_interval (combine + transcription per mesh interval,
     raw outputs in LDS) writes exactly what k_interval writes through
@@ -863,8 +861,9 @@ def test_kernel_variants_bit_identical(name, variant):
     Y."""
     gpu, _, _ = _pair(name)
     split, _, _ = _pair(name, env=variant)
-    if variant.get("MOCOHIP_DBASE") == "1" and split.opts.finite_difference_scheme != abi.MH_FD_CENTRAL:
-        # forward / backward differences: the derived offsets equal the table
+    if variant == {"MOCOHIP_INTERVAL": "0"} and split.opts.finite_difference_scheme != abi.MH_FD_CENTRAL:
+        # k_transcribe's base-lane offsets derived from the words (against
+        # the table's, MOCOHIP_DBASE=0): forward / backward differences
         assert "dbase" in split.backend_flags().split(), split.backend_flags()
     if variant == {"MOCOHIP_IVG_BASE": "0"}:
         # eval_g's base-slot kernel against the slot-table path
