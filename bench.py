@@ -242,11 +242,23 @@ def settle(cx, step, seconds):
     not cover.  Reported in the line as "settle_s"; nothing of it is timed."""
     if seconds <= 0:
         return 0.0
+    torch = cx.torch
+    sync = getattr(cx, "sync", None) or torch.cuda.synchronize
     t0 = time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
+    # with several ranks the steps hold collectives: every rank runs the same
+    # number of chunks, rank 0's clock deciding (one broadcast per chunk)
+    flag = torch.ones(1, dtype=torch.int32, device=cx.dev) if cx.world > 1 else None
+    while True:
         for _ in range(50):
             step()
-        cx.torch.cuda.synchronize()
+        sync()
+        more = time.perf_counter() - t0 < seconds
+        if flag is not None:
+            flag.fill_(1 if more else 0)
+            cx.dist.broadcast(flag, src=0)
+            more = bool(flag.item())
+        if not more:
+            break
     return round(time.perf_counter() - t0, 3)
 
 

@@ -278,3 +278,49 @@ def test_slice_gather_reassembles_on_rank0(case, N, world):
         p.join(300)
         assert p.exitcode == 0
     assert list(out) == [1] * world
+
+
+def _settle_worker(rank, world, port, q):
+    import os
+    import time
+    import types
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    calls = [0]
+    buf = torch.zeros(4)
+
+    def step():                      # a collective per step, like the mesh step
+        calls[0] += 1
+        dist.broadcast(buf, src=0)
+        if rank == 1:
+            time.sleep(0.0005)       # the ranks' clocks disagree
+    cx = types.SimpleNamespace(torch=torch, dist=dist, world=world, dev="cpu", sync=lambda: None)
+    bench.settle(cx, step, 0.05 if rank == 0 else 0.5)
+    dist.barrier()
+    q.put((rank, calls[0]))
+    dist.destroy_process_group()
+
+
+def test_bench_settle_runs_the_same_steps_on_every_rank():
+    """bench.settle's untimed calls hold collectives at N > 1: every rank
+    must run the same number of them whatever its own clock says (rank 0
+    decides per chunk), or the next collective deadlocks."""
+    import multiprocessing as mp
+    import socket
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_settle_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(120)
+    got = dict(q.get(timeout=5) for _ in range(2))
+    assert got[0] == got[1] and got[0] % 50 == 0, got
