@@ -728,7 +728,7 @@ def sweep_distributed(cx, args):
     """configs[4] as BASELINE names it: 64 MocoInverse solves over the
     node's ranks -- rank r solves every W-th subject on its own GPU
     (mocohip.batchsolve.solve_sweep, rounds of <= 8 solver processes per
-    GPU), no collective on the data path; the counts and the wall clock
+    GPU, at most 16 GPU processes on the node), no collective on the data path; the counts and the wall clock
     (max over ranks) reduced at the end.  A rank whose share fails reports
     zero solves and its error; every rank still reaches the reductions."""
     from mocohip import batchsolve
@@ -738,7 +738,11 @@ def sweep_distributed(cx, args):
     t0 = time.perf_counter()
     err = None
     try:
-        r = batchsolve.solve_sweep(args.sweep, 125, rank=cx.rank, world=cx.world, device=cx.local)
+        # at most 16 processes on the node's GPUs at once (the ranks and their
+        # solver processes): 7 / 3 / 1 solvers per rank at W = 2 / 4 / 8
+        conc = max(1, min(8, 16 // cx.world - 1))
+        r = batchsolve.solve_sweep(args.sweep, 125, rank=cx.rank, world=cx.world, device=cx.local,
+                                   max_concurrent=conc)
     except Exception as e:   # noqa: BLE001 -- reported in the line, never fatal to it
         r = {"solves": 0, "succeeded": 0, "wall_clock_s": 0.0, "rounds": 0, "mean_iterations": None}
         err = f"rank {cx.rank}: {type(e).__name__}: {e}"
@@ -756,7 +760,8 @@ def sweep_distributed(cx, args):
            "solves_per_minute": round(60.0 * solves / wall, 2) if wall > 0 else None,
            "mean_iterations_rank0": r["mean_iterations"],
            "workload": "configs[4]: 64 MocoInverse gait10dof18musc N=125 solves (scaled subjects), "
-                       "rank r solves subjects r, r+W, ... on its own GPU, <= 8 solver processes at once"}
+                       "rank r solves subjects r, r+W, ... on its own GPU, <= 8 solver processes at once "
+                       "(<= 16 GPU processes on the node: ranks + solvers)"}
     if failed:
         out["ranks_failed"] = failed
     if err:
