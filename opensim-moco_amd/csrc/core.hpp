@@ -2209,6 +2209,9 @@ struct mh_ctx {
     int iv_dbg_stop = 0;               // diagnostic: k_interval stops after phase n
     int iv_pf = 1;                     // MOCOHIP_IV_PF=0: no assembly-word prefetch (A/B)
     int iv_dbase = 0;                  // k_transcribe derives base-lane offsets (MOCOHIP_DBASE=0: the table)
+    std::vector<int> exc_xs;           // excitation lanes of k_exc_fill: [lane, slot, output] per lane
+    bool exc_redirected = false;       // the template reads their copied outputs at the base lane
+    bool exc_full = false;             // mh_debug_jacobian_lanes: fill every output
     uint32_t iv_smagic = 0, iv_sstride = 1, iv_sbase = 0;
     int iv_xcd = 1;                    // XCD-contiguous interval order (MOCOHIP_IV_XCD=0: off, A/B)
     int iv_qfuse = 1;                  // MOCOHIP_IV_QFUSE=0: in-place quotient pass (A/B)

@@ -74,8 +74,29 @@ __global__ void __launch_bounds__(256) k_exc_fill(int nk, int NO, int stride, in
     double* Yo = Y + ((long)kl * NO + o) * stride;
     Yo[xs[3 * e]] = o == xs[3 * e + 2] ? T[(long)kl * tdoubles + xs[3 * e + 1]] : Yo[base];
 }
+// The activation-derivative output of each excitation lane only (one thread
+// per (grid point, lane)): when the compiled template reads every other
+// output of those lanes at the base lane (redirect_exc_words), the copies
+// k_exc_fill writes are never read
+__global__ void __launch_bounds__(256) k_exc_fill_adot(int nk, int NO, int stride, int tdoubles, int nx,
+        const int* __restrict__ xs, const double* __restrict__ T, double* __restrict__ Y) {
+    const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= (long)nk * nx) return;
+    const int e = (int)(gid % nx);
+    const int kl = (int)(gid / nx);
+    Y[((long)kl * NO + xs[3 * e + 2]) * stride + xs[3 * e]] = T[(long)kl * tdoubles + xs[3 * e + 1]];
+}
 int mh_launch_exc_fill(const mh_ctx* c, int nk, int NO, int stride, int base, int tdoubles, const double* T,
                        double* Y) {
+    // (the redirected words are the compiled template's: the TplEntry
+    // assembly, MOCOHIP_CTPL=0 / MOCOHIP_ASM_CTPL=0 / MOCOHIP_ASM=gs, reads
+    // every copy)
+    if (c->exc_redirected && !c->exc_full && c->use_ctpl && c->asm_ctpl && !c->asm_grid_stride) {
+        const long all = (long)nk * c->n_exc_gen;
+        hipLaunchKernelGGL(k_exc_fill_adot, dim3((unsigned)((all + 255) / 256)), dim3(256), 0, c->stream, nk, NO,
+                           stride, tdoubles, c->n_exc_gen, (const int*)c->d_exc_slot, T, Y);
+        return MH_OK;
+    }
     const long all = (long)nk * NO * c->n_exc_gen;
     hipLaunchKernelGGL(k_exc_fill, dim3((unsigned)((all + 255) / 256)), dim3(256), 0, c->stream, nk, NO, stride,
                        base, tdoubles, c->n_exc_gen, (const int*)c->d_exc_slot, T, Y);
@@ -1019,6 +1040,39 @@ static void setup_assembly_variants(mh_ctx* c) {
     }
 }
 
+// Excitation lanes filled by k_exc_fill (c->exc_xs: [lane, slot, output]
+// triplets): every output of such a lane but its activation derivative is a
+// copy of the base lane's, so a template word that reads one of them reads
+// the base lane instead -- the quotient (y_base - y_base) / h is the same
+// bits (+0, or NaN where y_base is not finite) -- and the fill then writes
+// the activation derivatives only (k_exc_fill_adot).  Forward / backward
+// differences (a central word also reads its mirror lane at off + ND);
+// MOCOHIP_EXC_REDIRECT=0 turns it off.  Returns the words changed.
+static long redirect_exc_words(mh_ctx* c) {
+    c->exc_redirected = false;
+    const char* e = std::getenv("MOCOHIP_EXC_REDIRECT");
+    if (c->exc_xs.empty() || c->lanes_jac.fd == MH_FD_CENTRAL || (e && std::strcmp(e, "0") == 0)) return 0;
+    const uint32_t stride = (uint32_t)c->lanes_jac.stride, base = (uint32_t)c->lanes_jac.base;
+    const int npts = c->scheme == MH_HERMITE_SIMPSON ? 3 : 2;
+    const uint32_t nyall = (uint32_t)(npts * c->NO) * stride;
+    std::vector<int> adot(stride, -2);   // lane -> its filled output (-2: not an excitation lane)
+    for (size_t k = 0; k + 2 < c->exc_xs.size(); k += 3) adot[c->exc_xs[k]] = c->exc_xs[k + 2];
+    const size_t nw = (size_t)c->nnz_int + (size_t)c->nnz_tail;
+    long changed = 0;
+    for (size_t i = 0; i < nw && i < c->ctpl.size(); ++i) {
+        uint32_t& w = c->ctpl[i];
+        const uint32_t off = w & CT_OFF;
+        if ((w & (CT_GEN | CT_PATH)) || off >= nyall) continue;
+        const uint32_t lane = off % stride;
+        const int o = (int)((off / stride) % (uint32_t)c->NO);
+        if (adot[lane] == -2 || adot[lane] == o) continue;
+        w = (w & ~(uint32_t)CT_OFF) | (off - lane + base);
+        ++changed;
+    }
+    c->exc_redirected = true;
+    return changed;
+}
+
 // The compiled template (core.hpp CT_*) of c->tpl for the Jacobian lane
 // layout: per entry the LDS offset of the quotient (or constant) it scales,
 // its coefficient and base -- the operations jac_entry performs for it.
@@ -1813,6 +1867,13 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
             if (c->n_exc_gen) {
                 o_xsl = A.put(xs.data(), xs.size());
                 o_cmap = A.put(cmap.data(), cmap.size());
+                c->exc_xs = xs;
+                // the words read the base lane for the copies (the upload
+                // of the compiled template, made above, is patched)
+                if (redirect_exc_words(c.get()) > 0)
+                    for (auto& up : A.uploads)
+                        if (up.first == o_ctpl)
+                            std::memcpy(up.second.data(), c->ctpl.data(), sizeof(uint32_t) * c->ctpl.size());
             }
         }
         o_T = A.reserve(sizeof(double) * std::max(c->ts_jac.t_doubles, c->ts_g.t_doubles));
@@ -2030,6 +2091,7 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
             c->E.nnz = c->nnz_ep;
             c->nnz = c->nnz_ep + (int64_t)c->nnz_int * c->N + c->nnz_tail;
             if (!compile_template(c.get())) return set_err(MH_ERR_UNSUPPORTED, "Jacobian template does not compile");
+            (void)redirect_exc_words(c.get());
             setup_assembly_variants(c.get());
             HIPCHK(hipMemcpy(c->d_tpl, c->tpl.data(), sizeof(TplEntry) * c->tpl.size(), hipMemcpyHostToDevice));
             HIPCHK(hipMemcpy(c->d_ctpl, c->ctpl.data(), sizeof(uint32_t) * c->ctpl.size(),
@@ -3201,7 +3263,9 @@ extern "C" int mh_debug_jacobian_lanes(mh_ctx* c, const double* x, double* times
     (void)hipGetLastError();
     HIPCHK(hipMemcpyAsync(c->d_x, x, sizeof(double) * c->n, hipMemcpyHostToDevice, c->stream));
     apply_params(c, c->d_x);
+    c->exc_full = true;   // every lane complete (the eval path fills the read outputs only)
     c->be->lanes(c, c->d_x, c->d_Y);
+    c->exc_full = false;
     HIPCHK(hipGetLastError());
     const size_t ny = (size_t)c->nk * c->NO * c->lanes_jac.stride;
     HIPCHK(hipMemcpyAsync(times, c->d_times, sizeof(double) * c->nk, hipMemcpyDeviceToHost, c->stream));
@@ -3364,7 +3428,9 @@ extern "C" int mh_get_backend_flags(const mh_ctx* c, char* flags, int32_t len) {
     if (c->quot) f += " quot";
     if (c->asm_grid_stride) f += " asm-gs";
     if (c->d_exc) f += " exc-lanes";
-    if (c->d_exc_slot) f += " exc-fill";
+    if (c->d_exc_slot)
+        f += c->exc_redirected && c->use_ctpl && c->asm_ctpl && !c->asm_grid_stride ? " exc-fill adot-only"
+                                                                                     : " exc-fill";
     if (c->g_lds && !c->be->tasks && std::strncmp(c->be->name, "generic", 7) == 0) {
         f += " g-lds";
         if (c->g_lds_guard) {

@@ -323,7 +323,7 @@ def _pair(name, backend="auto", tasks=None, env=None):
                                                   "MOCOHIP_G_LDS_GUARD",
                                                   "MOCOHIP_GROUPS_SPLIT", "MOCOHIP_COMBINE",
                                                   "MOCOHIP_ASM_CHUNK", "MOCOHIP_ASM_CTPL", "MOCOHIP_DBASE",
-                                                  "MOCOHIP_NT_STORES")}
+                                                  "MOCOHIP_NT_STORES", "MOCOHIP_EXC_REDIRECT")}
     if backend != "auto":
         os.environ["MOCOHIP_BACKEND"] = backend
     if tasks:
@@ -919,6 +919,33 @@ def test_generated_excitation_fill_bit_identical(name):
         assert np.array_equal(ta, tb) and np.array_equal(Ya, Yb, equal_nan=True)
         assert np.array_equal(gpu.eval_jac_g(x), full.eval_jac_g(x), equal_nan=True)
         assert np.array_equal(gpu.eval_g(x), full.eval_g(x), equal_nan=True)
+
+
+@pytest.mark.parametrize("env", [{"MOCOHIP_INTERVAL": "0", "MOCOHIP_COMBINE": "global"}, {}],
+                         ids=["split", "default"])
+@pytest.mark.parametrize("name", ["gait_rigid_forward", "gait_rigid_backward", "gait_rigid_implicit",
+                                  "gait_compliant_central", "wrapped_pendulum", "rajagopal80",
+                                  "rajagopal80_wrapped"])
+def test_excitation_words_read_the_base_lane(name, env):
+    """Generated back ends, forward / backward differences: the compiled
+    template's words that read an excitation lane's copied outputs read the
+    base lane instead, and k_exc_fill writes the activation derivatives only
+    ("adot-only"); the Jacobian and g equal combining every lane
+    (MOCOHIP_EXC_LANES=0) bit for bit.  eval_jac_g runs first on each fresh
+    context, so no full fill (jacobian_lanes) can leave the copies behind."""
+    gpu, _, st = _pair(name, env=env)
+    full, _, _ = _pair(name, env={**env, "MOCOHIP_EXC_LANES": "0"})
+    flags = gpu.backend_flags()
+    if "exc-fill" in flags:
+        central = st.solver.optim_finite_difference_scheme == "central"
+        assert ("adot-only" in flags) != central
+    for _, x in _iterates(gpu):
+        assert np.array_equal(gpu.eval_jac_g(x), full.eval_jac_g(x), equal_nan=True)
+        assert np.array_equal(gpu.eval_g(x), full.eval_g(x), equal_nan=True)
+    ta, Ya = gpu.jacobian_lanes(x)
+    tb, Yb = full.jacobian_lanes(x)
+    assert np.array_equal(ta, tb) and np.array_equal(Ya, Yb, equal_nan=True)
+    assert np.array_equal(gpu.eval_jac_g(x), full.eval_jac_g(x), equal_nan=True)
 
 
 @pytest.mark.parametrize("tb", ["1", "8", "64"])
