@@ -822,6 +822,26 @@ __device__ __host__ __forceinline__ uint32_t ct_word(uint32_t off, uint32_t coef
     return off | (coef << 20) | (base << 23);
 }
 
+// a / b rounded to nearest from y = 1 / b (itself rounded to nearest, formed
+// once by the division): q = a y, then two residual corrections q += (a - b q)
+// y with the residual exact in one fma.  A faithful q and y = RN(1/b) make
+// q + (a - b q) y round to RN(a / b) (Markstein's theorem), and the first
+// correction makes a y (within 1.5 ulp) faithful; tests/test_div_rn.py.  Valid while no product
+// over- or underflows: |a| in [2^-900, 2^900] for b, y in [2^-60, 2^60];
+// outside it (and for infinities) the division itself; a zero keeps its sign
+// (a y).  The same bits as a / b at about half its instructions (no
+// div_scale / rcp / div_fmas / div_fixup chain).
+__device__ __forceinline__ double div_rn(double a, double b, double y) {
+    double q = a * y;
+    double r = __builtin_fma(-q, b, a);
+    q = __builtin_fma(r, y, q);
+    r = __builtin_fma(-q, b, a);
+    q = __builtin_fma(r, y, q);
+    const double m = __builtin_fabs(a);
+    if (!(m >= 0x1p-900 && m <= 0x1p+900) && m != 0.0 && m == m) q = a / b;
+    return m == 0.0 ? a * y : q;
+}
+
 struct Interval {
     int scheme;      // MH_HERMITE_SIMPSON / MH_TRAPEZOIDAL
     int interp;
@@ -858,6 +878,7 @@ struct Interval {
     // measured slower there (17.7 -> 19.8 us, profiles/r06_c)
     int dbase;
     uint32_t smagic, sstride, sbase;
+    int qdiv;        // k_transcribe's quotients by div_rn (1, MOCOHIP_QDIV=1) or the division (0)
     __device__ __forceinline__ uint32_t base_of(uint32_t w, uint32_t nyall) const {
         const uint32_t off = w & CT_OFF;
         const bool lane = !(w & (CT_GEN | CT_PATH)) && off < nyall;
@@ -2213,6 +2234,7 @@ struct mh_ctx {
     bool exc_redirected = false;       // the template reads their copied outputs at the base lane
     bool exc_full = false;             // mh_debug_jacobian_lanes: fill every output
     uint32_t iv_smagic = 0, iv_sstride = 1, iv_sbase = 0;
+    int iv_qdiv = 0;                   // k_transcribe: quotients by div_rn (MOCOHIP_QDIV=1; no faster)
     int iv_xcd = 1;                    // XCD-contiguous interval order (MOCOHIP_IV_XCD=0: off, A/B)
     int iv_qfuse = 1;                  // MOCOHIP_IV_QFUSE=0: in-place quotient pass (A/B)
     hipEvent_t ev[5] = {};         // stage boundaries (+ ev[4] after k_groups)
@@ -2350,7 +2372,8 @@ inline Layout make_layout(const mh_ctx* c, int k0, int nk) {
 inline Interval make_interval(const mh_ctx* c, double*& g, double*& v) {
     Interval I{c->scheme, c->interp, c->ib, c->rpi, c->nnz_int, c->NMB + c->NAR, c->NMB, c->NQ + c->NZ,
                c->N, c->nnz_tail, c->ntail, c->npe, c->NK, c->OKC, c->P, c->E, nullptr, nullptr, c->iv_dbg_stop, c->iv_pf, c->iv_qfuse,
-               c->iv_xcd, c->iv_dbase, c->iv_smagic, c->iv_sstride, c->iv_sbase};
+               c->iv_xcd, c->iv_dbase, c->iv_smagic, c->iv_sstride, c->iv_sbase,
+               c->iv_qdiv};
     if (c->ib == 0 && c->nep > 0) {
         I.gh = g;
         I.vh = v;

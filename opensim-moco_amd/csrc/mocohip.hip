@@ -220,9 +220,11 @@ __global__ void __launch_bounds__(256) k_transcribe(Layout L, Interval I, Lanes 
             // t0 / tf (CT_GEN) and path (CT_PATH) entries are skipped here and
             // written by the two loops below.  One instantiation per
             // finite-difference formula (no per-entry scalar branches).
-            auto bulk = [&](auto fdc) {
+            auto bulk = [&](auto fdc, auto qdc) {
                 constexpr int FD = decltype(fdc)::value;
+                constexpr bool QD = decltype(qdc)::value;
                 const double hq = FD == MH_FD_CENTRAL ? 2.0 * Ln.h : Ln.h;
+                const double rq = 1.0 / hq;
                 constexpr int CT_U = 8;
                 for (int e0 = eb + (int)threadIdx.x; e0 < ee; e0 += CT_U * (int)blockDim.x) {
                     uint32_t w[CT_U], wb[CT_U];
@@ -248,16 +250,22 @@ __global__ void __launch_bounds__(256) k_transcribe(Layout L, Interval I, Lanes 
                     for (int u = 0; u < CT_U; ++u) {
                         const int e = e0 + u * (int)blockDim.x;
                         const uint32_t off = w[u] & CT_OFF;
-                        const double qd = FD == MH_FD_BACKWARD ? (yb[u] - ya[u]) / hq : (ya[u] - yb[u]) / hq;
+                        const double dy = FD == MH_FD_BACKWARD ? yb[u] - ya[u] : ya[u] - yb[u];
+                        const double qd = QD ? div_rn(dy, hq, rq) : dy / hq;
                         const double q = off >= nyall ? (off == kone ? 1.0 : 0.0) : (yq ? ya[u] : qd);
                         const double v = (w[u] & CT_RAW) ? q : kb[(w[u] >> 23) & 7] + kc[(w[u] >> 20) & 7] * q;
                         if (e < ee && !(w[u] & (CT_GEN | CT_PATH))) vi[e] = v;
                     }
                 }
             };
-            if (Ln.fd == MH_FD_FORWARD) bulk(std::integral_constant<int, MH_FD_FORWARD>{});
-            else if (Ln.fd == MH_FD_BACKWARD) bulk(std::integral_constant<int, MH_FD_BACKWARD>{});
-            else bulk(std::integral_constant<int, MH_FD_CENTRAL>{});
+            // (div_rn: the step within [2^-60, 2^60], checked on the host)
+            auto bulk_fd = [&](auto qdc) {
+                if (Ln.fd == MH_FD_FORWARD) bulk(std::integral_constant<int, MH_FD_FORWARD>{}, qdc);
+                else if (Ln.fd == MH_FD_BACKWARD) bulk(std::integral_constant<int, MH_FD_BACKWARD>{}, qdc);
+                else bulk(std::integral_constant<int, MH_FD_CENTRAL>{}, qdc);
+            };
+            if (I.qdiv) bulk_fd(std::true_type{});
+            else bulk_fd(std::false_type{});
             // t0 / tf entries of this chunk
             for (int j = threadIdx.x; j < nctgen; j += blockDim.x) {
                 const int e = ctgen[j];
@@ -1025,6 +1033,13 @@ static void setup_assembly_variants(mh_ctx* c) {
     c->iv_sbase = (uint32_t)c->lanes_jac.base;
     c->iv_smagic = (uint32_t)(0xFFFFFFFFull / stride + 1);
     c->iv_dbase = 0;
+    // k_transcribe's quotients by div_rn, opt-in (MOCOHIP_QDIV=1): the same
+    // bits as the division, measured no faster (configs[3] 1,720 vs 1,729
+    // calls/s, profiles/r06_n -- the kernel waits on memory, not on the
+    // division); its range: the step (and twice it) within [2^-60, 2^60]
+    const char* eq = std::getenv("MOCOHIP_QDIV");
+    const double hs = c->lanes_jac.h;
+    c->iv_qdiv = eq && std::strcmp(eq, "1") == 0 && hs >= 0x1p-60 && hs <= 0x1p+59;
     if (!(ed && std::strcmp(ed, "0") == 0) && !c->ctpl.empty() && c->lanes_jac.fd != MH_FD_CENTRAL) {
         const size_t nw = (size_t)c->nnz_int + (size_t)c->nnz_tail;
         const int npts = c->scheme == MH_HERMITE_SIMPSON ? 3 : 2;
@@ -1047,11 +1062,15 @@ static void setup_assembly_variants(mh_ctx* c) {
 // bits (+0, or NaN where y_base is not finite) -- and the fill then writes
 // the activation derivatives only (k_exc_fill_adot).  Forward / backward
 // differences (a central word also reads its mirror lane at off + ND);
-// MOCOHIP_EXC_REDIRECT=0 turns it off.  Returns the words changed.
+// MOCOHIP_EXC_REDIRECT=0 turns it off.  Returns the words changed (the
+// caller uploads them).
 static long redirect_exc_words(mh_ctx* c) {
     c->exc_redirected = false;
     const char* e = std::getenv("MOCOHIP_EXC_REDIRECT");
     if (c->exc_xs.empty() || c->lanes_jac.fd == MH_FD_CENTRAL || (e && std::strcmp(e, "0") == 0)) return 0;
+    // quotients formed in place (k_combine's MOCOHIP_QUOT=1, k_interval's
+    // MOCOHIP_IV_QFUSE=0) leave the base lane raw: its slot is no quotient
+    if (c->quot || !c->iv_qfuse) return 0;
     const uint32_t stride = (uint32_t)c->lanes_jac.stride, base = (uint32_t)c->lanes_jac.base;
     const int npts = c->scheme == MH_HERMITE_SIMPSON ? 3 : 2;
     const uint32_t nyall = (uint32_t)(npts * c->NO) * stride;
@@ -1867,13 +1886,7 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
             if (c->n_exc_gen) {
                 o_xsl = A.put(xs.data(), xs.size());
                 o_cmap = A.put(cmap.data(), cmap.size());
-                c->exc_xs = xs;
-                // the words read the base lane for the copies (the upload
-                // of the compiled template, made above, is patched)
-                if (redirect_exc_words(c.get()) > 0)
-                    for (auto& up : A.uploads)
-                        if (up.first == o_ctpl)
-                            std::memcpy(up.second.data(), c->ctpl.data(), sizeof(uint32_t) * c->ctpl.size());
+                c->exc_xs = xs;   // redirect_exc_words, once the quotient modes are known
             }
         }
         o_T = A.reserve(sizeof(double) * std::max(c->ts_jac.t_doubles, c->ts_g.t_doubles));
@@ -2074,6 +2087,12 @@ extern "C" int mh_create(const mh_problem* p, const mh_options* o, mh_ctx** out)
         c->g_lane = egl && std::strcmp(egl, "1") == 0;
         const char* eq = std::getenv("MOCOHIP_QUOT");
         c->quot = eq && std::strcmp(eq, "1") == 0;   // opt-in: measured slower
+        // the words read the base lane for an excitation lane's copies
+        if (redirect_exc_words(c.get()) > 0) {
+            setup_assembly_variants(c.get());
+            HIPCHK(hipMemcpy(c->d_ctpl, c->ctpl.data(), sizeof(uint32_t) * c->ctpl.size(),
+                    hipMemcpyHostToDevice));
+        }
         if (o->sparsity_detection != MH_SPARSITY_NONE) {
             // detect on the device, then rebuild the (smaller) template in
             // place of the block-dense one
@@ -3424,6 +3443,7 @@ extern "C" int mh_get_backend_flags(const mh_ctx* c, char* flags, int32_t len) {
     if (c->krec_ok) f += " groups-kernarg";
     if (!c->use_ctpl) f += " no-ctpl";
     if (c->iv_dbase) f += " dbase";
+    if (c->iv_qdiv) f += " qdiv";
     if (c->use_roles && c->use_interval[1]) f += " roles";
     if (c->quot) f += " quot";
     if (c->asm_grid_stride) f += " asm-gs";

@@ -323,7 +323,7 @@ def _pair(name, backend="auto", tasks=None, env=None):
                                                   "MOCOHIP_G_LDS_GUARD",
                                                   "MOCOHIP_GROUPS_SPLIT", "MOCOHIP_COMBINE",
                                                   "MOCOHIP_ASM_CHUNK", "MOCOHIP_ASM_CTPL", "MOCOHIP_DBASE",
-                                                  "MOCOHIP_NT_STORES", "MOCOHIP_EXC_REDIRECT")}
+                                                  "MOCOHIP_NT_STORES", "MOCOHIP_EXC_REDIRECT", "MOCOHIP_QDIV")}
     if backend != "auto":
         os.environ["MOCOHIP_BACKEND"] = backend
     if tasks:
@@ -849,7 +849,8 @@ def test_pruned_tasks_bit_identical(name):
                                      {"MOCOHIP_IVG_THREADS": "1024"},
                                      {"MOCOHIP_IVG_BASE": "0"},
                                      {"MOCOHIP_IVG_GM": "0"},
-                                     {"MOCOHIP_INTERVAL": "0", "MOCOHIP_DBASE": "0"}])
+                                     {"MOCOHIP_INTERVAL": "0", "MOCOHIP_DBASE": "0"},
+                                     {"MOCOHIP_INTERVAL": "0", "MOCOHIP_QDIV": "1"}])
 def test_kernel_variants_bit_identical(name, variant):
     """The default k_interval (combine + transcription per mesh interval,
     raw outputs in LDS) writes exactly what k_interval writes through
@@ -865,6 +866,10 @@ def test_kernel_variants_bit_identical(name, variant):
         # k_transcribe's base-lane offsets derived from the words (against
         # the table's, MOCOHIP_DBASE=0): forward / backward differences
         assert "dbase" in split.backend_flags().split(), split.backend_flags()
+    if variant.get("MOCOHIP_INTERVAL") == "0":
+        # k_transcribe's quotients by div_rn (MOCOHIP_QDIV=1) against
+        # k_interval's division
+        assert ("qdiv" in split.backend_flags().split()) == ("MOCOHIP_QDIV" in variant)
     if variant == {"MOCOHIP_IVG_BASE": "0"}:
         # eval_g's base-slot kernel against the slot-table path
         fa, fb = gpu.backend_flags().split(), split.backend_flags().split()
